@@ -1,0 +1,173 @@
+"""Reference byte layouts of the map keys/values on the classification path.
+
+These are the exact layouts the reference datapath and its Go map wrappers
+exchange through bpf(2); the C ABI (include/cgpu.h) takes the same bytes so a
+cgo caller can pass ``unsafe.Pointer`` straight through.
+
+* ``policy_key`` 8 B / ``policy_entry`` 24 B — bpf/lib/common.h:180-193,
+  Go mirror pkg/maps/policymap/policymap.go:63-80.  ``egress`` is the byte
+  holding the ``egress:1, pad:7`` bitfield (bit 0 = egress on little endian).
+* ``ipcache_key`` 24 B / ``remote_endpoint_info`` 8 B — bpf/lib/maps.h:135-148,
+  bpf/lib/common.h:175-178, Go pkg/maps/ipcache/ipcache.go:54-61,132-135.
+  ``prefixlen`` counts the 32 static bits (pad[3] + family) plus the IP bits
+  (bpf/lib/eps.h:48-52, ipcache.go:72-98).
+* ``lpm_v4_key`` 8 B / ``lpm_v6_key`` 20 B — bpf/lib/xdp.h:23-31, Go
+  pkg/maps/cidrmap/cidrmap.go:49-52 (``cidrKey`` truncated to 4 + AddrSize).
+* ``endpoint_key`` 20 B — bpf/lib/common.h:147-160.
+* ``metrics`` {reason, dir} -> {count, bytes} — bpf/lib/common.h:195-206.
+"""
+from __future__ import annotations
+
+import ipaddress
+import socket
+import struct
+
+import numpy as np
+
+POLICY_KEY = np.dtype([("sec_label", "<u4"), ("dport", "<u2"), ("protocol", "u1"),
+                       ("egress", "u1")])
+POLICY_ENTRY = np.dtype([("proxy_port", "<u2"), ("pad", "<u2", (3,)), ("packets", "<u8"),
+                         ("bytes", "<u8")])
+IPCACHE_KEY = np.dtype([("prefixlen", "<u4"), ("pad", "u1", (3,)), ("family", "u1"),
+                        ("ip", "u1", (16,))])
+REMOTE_ENDPOINT_INFO = np.dtype([("sec_label", "<u4"), ("tunnel_endpoint", "<u4")])
+LPM_V4_KEY = np.dtype([("prefixlen", "<u4"), ("addr", "u1", (4,))])
+LPM_V6_KEY = np.dtype([("prefixlen", "<u4"), ("addr", "u1", (16,))])
+ENDPOINT_KEY = np.dtype([("ip", "u1", (16,)), ("family", "u1"), ("pad4", "u1"),
+                         ("pad5", "<u2")])
+
+assert POLICY_KEY.itemsize == 8 and POLICY_ENTRY.itemsize == 24
+assert IPCACHE_KEY.itemsize == 24 and REMOTE_ENDPOINT_INFO.itemsize == 8
+assert LPM_V4_KEY.itemsize == 8 and LPM_V6_KEY.itemsize == 20
+assert ENDPOINT_KEY.itemsize == 20
+
+# bpf/lib/common.h:139-140
+ENDPOINT_KEY_IPV4 = 1
+ENDPOINT_KEY_IPV6 = 2
+# bpf/lib/eps.h:48-52: 8 * (sizeof(ipcache_key) - sizeof(bpf_lpm_trie_key) - 16)
+IPCACHE_STATIC_PREFIX = 32
+
+# reserved identities, bpf/node_config.h:34-38 / pkg/identity
+HOST_ID, WORLD_ID, CLUSTER_ID, HEALTH_ID, INIT_ID = 1, 2, 3, 4, 5
+# drop reasons, bpf/lib/common.h:237-269
+DROP_POLICY = -133
+DROP_CT_UNKNOWN_PROTO = -137
+DROP_FRAG_NOSUPPORT = -157
+XDP_DROP, XDP_PASS = 1, 2
+METRIC_INGRESS, METRIC_EGRESS = 1, 2
+# CT direction (bpf/lib/common.h:327-328); policy_key.egress = !dir
+CT_EGRESS, CT_INGRESS = 0, 1
+
+PROTO_ICMP, PROTO_TCP, PROTO_UDP = 1, 6, 17
+
+# tuple flag bits of the classify SoA
+F_EGRESS = 1
+F_FRAGMENT = 2
+# prefilter packet flags
+PKT_OK, PKT_TRUNCATED, PKT_NOT_IP = 0, 1, 2
+
+
+def htons(x: int) -> int:
+    return socket.htons(x)
+
+
+def ntohs(x: int) -> int:
+    return socket.ntohs(x)
+
+
+def ip4_be(addr: str | int) -> int:
+    """IPv4 address -> u32 whose little-endian memory bytes are network order."""
+    if isinstance(addr, str):
+        b = socket.inet_aton(addr)
+    else:
+        b = struct.pack(">I", addr)
+    return struct.unpack("<I", b)[0]
+
+
+def be_to_host4(x):
+    """network-order u32 (as stored) -> host integer; works on numpy arrays."""
+    if isinstance(x, np.ndarray):
+        return x.byteswap()
+    return struct.unpack(">I", struct.pack("<I", x))[0]
+
+
+def policy_key(sec_label: int, dport_host: int, proto: int, egress: int,
+               pad_bits: int = 0) -> np.ndarray:
+    k = np.zeros((), POLICY_KEY)
+    k["sec_label"] = sec_label
+    k["dport"] = htons(dport_host)
+    k["protocol"] = proto
+    k["egress"] = (egress & 1) | (pad_bits << 1)
+    return k
+
+
+def policy_entry(proxy_port_host: int = 0, packets: int = 0, nbytes: int = 0) -> np.ndarray:
+    e = np.zeros((), POLICY_ENTRY)
+    e["proxy_port"] = htons(proxy_port_host)
+    e["packets"] = packets
+    e["bytes"] = nbytes
+    return e
+
+
+def ipcache_key(cidr: str, prefixlen_override: int | None = None) -> np.ndarray:
+    """pkg/maps/ipcache/ipcache.go:102-123 NewKey."""
+    net = ipaddress.ip_network(cidr, strict=False)
+    k = np.zeros((), IPCACHE_KEY)
+    raw = ipaddress.ip_address(cidr.split("/")[0]).packed
+    if net.version == 4:
+        k["family"] = ENDPOINT_KEY_IPV4
+        k["ip"][:4] = np.frombuffer(raw, np.uint8)
+    else:
+        k["family"] = ENDPOINT_KEY_IPV6
+        k["ip"][:] = np.frombuffer(raw, np.uint8)
+    k["prefixlen"] = IPCACHE_STATIC_PREFIX + net.prefixlen if prefixlen_override is None \
+        else prefixlen_override
+    return k
+
+
+def remote_info(sec_label: int, tunnel: int = 0) -> np.ndarray:
+    v = np.zeros((), REMOTE_ENDPOINT_INFO)
+    v["sec_label"] = sec_label
+    v["tunnel_endpoint"] = tunnel
+    return v
+
+
+def lpm_key(cidr: str) -> np.ndarray:
+    net = ipaddress.ip_network(cidr, strict=False)
+    raw = ipaddress.ip_address(cidr.split("/")[0]).packed
+    k = np.zeros((), LPM_V4_KEY if net.version == 4 else LPM_V6_KEY)
+    k["prefixlen"] = net.prefixlen
+    k["addr"][:] = np.frombuffer(raw, np.uint8)
+    return k
+
+
+def endpoint_key(ip: str) -> np.ndarray:
+    a = ipaddress.ip_address(ip)
+    k = np.zeros((), ENDPOINT_KEY)
+    if a.version == 4:
+        k["ip"][:4] = np.frombuffer(a.packed, np.uint8)
+        k["family"] = ENDPOINT_KEY_IPV4
+    else:
+        k["ip"][:] = np.frombuffer(a.packed, np.uint8)
+        k["family"] = ENDPOINT_KEY_IPV6
+    return k
+
+
+def get_prefix_mask_be(prefix: int) -> int:
+    """GET_PREFIX (bpf/lib/ipv6.h:136-138): network-order mask of `prefix` bits."""
+    if prefix <= 0:
+        h = 0
+    elif prefix < 32:
+        h = ((1 << prefix) - 1) << (32 - prefix)
+    else:
+        h = 0xFFFFFFFF
+    return ip4_be(h & 0xFFFFFFFF)
+
+
+def ipv6_addr_clear_suffix(addr16: bytes, prefix: int) -> bytes:
+    """ipv6_addr_clear_suffix (bpf/lib/ipv6.h:140-150)."""
+    words = list(struct.unpack("<4I", addr16))
+    for i in range(4):
+        words[i] &= get_prefix_mask_be(prefix)
+        prefix -= 32
+    return struct.pack("<4I", *words)

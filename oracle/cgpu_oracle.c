@@ -1,0 +1,850 @@
+/*
+ * TEST INFRASTRUCTURE — CPU restatement of the reference semantics.
+ * See cgpu_oracle.h for what this is (and is not) allowed to be used for.
+ */
+#define _GNU_SOURCE
+#include "cgpu_oracle.h"
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- reference constants (bpf/node_config.h:34-43, bpf/lib/common.h:237-269) ---- */
+#define DROP_POLICY (-133)
+#define DROP_FRAG_NOSUPPORT (-157)
+#define DROP_CT_UNKNOWN_PROTO (-137)
+#define XDP_DROP 1
+#define XDP_PASS 2
+#define METRIC_INGRESS 1 /* bpf/lib/common.h METRIC_INGRESS */
+#define METRIC_EGRESS 2
+#define PROTO_ICMP 1
+#define PROTO_TCP 6
+#define PROTO_UDP 17
+
+/* ====================================================================== */
+/* Path-compressed binary LPM trie, restating kernel/bpf/lpm_trie.c:       */
+/* trie_lookup_elem / trie_update_elem / trie_delete_elem (Linux >= 4.11). */
+/* Key = {u32 prefixlen; u8 data[data_size]}, bits MSB first per byte.     */
+/* ====================================================================== */
+#define LPM_IM 1u
+
+struct lpm_node {
+	struct lpm_node *child[2];
+	uint32_t prefixlen;
+	uint32_t flags;
+	uint8_t *val;
+	uint8_t data[];
+};
+
+struct lpm_trie {
+	struct lpm_node *root;
+	size_t data_size, vsz, n;
+	uint32_t max_prefixlen;
+};
+
+static void lpm_init(struct lpm_trie *t, size_t data_size, size_t vsz)
+{
+	memset(t, 0, sizeof(*t));
+	t->data_size = data_size;
+	t->vsz = vsz;
+	t->max_prefixlen = (uint32_t)data_size * 8;
+}
+
+static void lpm_free_node(struct lpm_node *n)
+{
+	if (!n)
+		return;
+	lpm_free_node(n->child[0]);
+	lpm_free_node(n->child[1]);
+	free(n->val);
+	free(n);
+}
+
+static void lpm_destroy(struct lpm_trie *t)
+{
+	lpm_free_node(t->root);
+	t->root = NULL;
+	t->n = 0;
+}
+
+static inline int lpm_bit(const uint8_t *data, uint32_t i)
+{
+	return (data[i >> 3] >> (7 - (i & 7))) & 1;
+}
+
+/* longest_prefix_match(): matching leading bits, capped at both lengths */
+static uint32_t lpm_match(const struct lpm_node *n, uint32_t kplen, const uint8_t *kdata)
+{
+	uint32_t limit = n->prefixlen < kplen ? n->prefixlen : kplen, i = 0;
+	while (i + 8 <= limit && n->data[i >> 3] == kdata[i >> 3])
+		i += 8;
+	while (i < limit && lpm_bit(n->data, i) == lpm_bit(kdata, i))
+		i++;
+	return i;
+}
+
+static const uint8_t *lpm_lookup(const struct lpm_trie *t, const uint8_t *key)
+{
+	uint32_t kplen;
+	const uint8_t *kdata = key + 4;
+	const struct lpm_node *n, *found = NULL;
+	memcpy(&kplen, key, 4);
+	for (n = t->root; n;) {
+		uint32_t m = lpm_match(n, kplen, kdata);
+		if (m == t->max_prefixlen) {
+			found = n;
+			break;
+		}
+		if (m < n->prefixlen)
+			break;
+		if (!(n->flags & LPM_IM))
+			found = n;
+		n = n->child[lpm_bit(kdata, n->prefixlen)];
+	}
+	return found ? found->val : NULL;
+}
+
+static struct lpm_node *lpm_new(const struct lpm_trie *t, uint32_t plen, const uint8_t *data,
+				const void *val)
+{
+	struct lpm_node *n = calloc(1, sizeof(*n) + t->data_size);
+	n->prefixlen = plen;
+	memcpy(n->data, data, t->data_size);
+	if (val) {
+		n->val = malloc(t->vsz ? t->vsz : 1);
+		memcpy(n->val, val, t->vsz);
+	} else {
+		n->flags = LPM_IM;
+	}
+	return n;
+}
+
+static int lpm_update(struct lpm_trie *t, const uint8_t *key, const void *val)
+{
+	uint32_t kplen, m = 0;
+	const uint8_t *kdata = key + 4;
+	struct lpm_node **slot = &t->root, *n, *nn, *im;
+	memcpy(&kplen, key, 4);
+	if (kplen > t->max_prefixlen)
+		return -EINVAL;
+	nn = lpm_new(t, kplen, kdata, val);
+	while ((n = *slot)) {
+		m = lpm_match(n, kplen, kdata);
+		if (n->prefixlen != m || n->prefixlen == kplen || n->prefixlen == t->max_prefixlen)
+			break;
+		slot = &n->child[lpm_bit(kdata, n->prefixlen)];
+	}
+	if (!n) {
+		*slot = nn;
+		t->n++;
+		return 0;
+	}
+	if (n->prefixlen == m) { /* same prefix: replace the node */
+		nn->child[0] = n->child[0];
+		nn->child[1] = n->child[1];
+		if (n->flags & LPM_IM)
+			t->n++;
+		*slot = nn;
+		free(n->val);
+		free(n);
+		return 0;
+	}
+	if (m == kplen) { /* new node is a prefix of n */
+		nn->child[lpm_bit(n->data, m)] = n;
+		*slot = nn;
+		t->n++;
+		return 0;
+	}
+	im = lpm_new(t, m, n->data, NULL);
+	if (lpm_bit(kdata, m)) {
+		im->child[0] = n;
+		im->child[1] = nn;
+	} else {
+		im->child[0] = nn;
+		im->child[1] = n;
+	}
+	*slot = im;
+	t->n++;
+	return 0;
+}
+
+static int lpm_delete(struct lpm_trie *t, const uint8_t *key)
+{
+	uint32_t kplen, m = 0;
+	const uint8_t *kdata = key + 4;
+	struct lpm_node **trim = &t->root, **trim2 = trim, *n, *parent = NULL;
+	memcpy(&kplen, key, 4);
+	if (kplen > t->max_prefixlen)
+		return -EINVAL;
+	while ((n = *trim)) {
+		m = lpm_match(n, kplen, kdata);
+		if (n->prefixlen != m || n->prefixlen == kplen)
+			break;
+		parent = n;
+		trim2 = trim;
+		trim = &n->child[lpm_bit(kdata, n->prefixlen)];
+	}
+	if (!n || n->prefixlen != kplen || n->prefixlen != m || (n->flags & LPM_IM))
+		return -ENOENT;
+	t->n--;
+	if (n->child[0] && n->child[1]) {
+		n->flags |= LPM_IM;
+		free(n->val);
+		n->val = NULL;
+		return 0;
+	}
+	if (parent && (parent->flags & LPM_IM) && !n->child[0] && !n->child[1]) {
+		*trim2 = (n == parent->child[0]) ? parent->child[1] : parent->child[0];
+		free(parent);
+		free(n->val);
+		free(n);
+		return 0;
+	}
+	*trim = n->child[0] ? n->child[0] : n->child[1];
+	free(n->val);
+	free(n);
+	return 0;
+}
+
+/* ====================================================================== */
+/* Exact-match open hash, whole-key memcmp (kernel/bpf/hashtab.c).         */
+/* Linear probing with backward-shift delete.                              */
+/* ====================================================================== */
+struct ohash {
+	size_t ksz, vsz, cap, n;
+	uint8_t *used;
+	uint8_t *keys;
+	uint8_t *vals;
+};
+
+static uint64_t hash_bytes(const uint8_t *p, size_t n)
+{
+	uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+	while (n >= 8) {
+		uint64_t w;
+		memcpy(&w, p, 8);
+		h = (h ^ w) * 0xff51afd7ed558ccdull;
+		h ^= h >> 32;
+		p += 8;
+		n -= 8;
+	}
+	while (n--) {
+		h = (h ^ *p++) * 0x100000001b3ull;
+	}
+	h ^= h >> 33;
+	h *= 0xc4ceb9fe1a85ec53ull;
+	h ^= h >> 33;
+	return h;
+}
+
+static void oh_init(struct ohash *h, size_t ksz, size_t vsz)
+{
+	memset(h, 0, sizeof(*h));
+	h->ksz = ksz;
+	h->vsz = vsz;
+}
+
+static void oh_destroy(struct ohash *h)
+{
+	free(h->used);
+	free(h->keys);
+	free(h->vals);
+	h->used = h->keys = h->vals = NULL;
+	h->cap = h->n = 0;
+}
+
+static long oh_find(const struct ohash *h, const void *key)
+{
+	size_t mask, i;
+	if (!h->cap)
+		return -1;
+	mask = h->cap - 1;
+	for (i = hash_bytes(key, h->ksz) & mask; h->used[i]; i = (i + 1) & mask)
+		if (!memcmp(h->keys + i * h->ksz, key, h->ksz))
+			return (long)i;
+	return -1;
+}
+
+static void oh_put_new(struct ohash *h, const void *key, const void *val)
+{
+	size_t mask = h->cap - 1, i;
+	for (i = hash_bytes(key, h->ksz) & mask; h->used[i]; i = (i + 1) & mask)
+		;
+	h->used[i] = 1;
+	memcpy(h->keys + i * h->ksz, key, h->ksz);
+	memcpy(h->vals + i * h->vsz, val, h->vsz);
+	h->n++;
+}
+
+static void oh_grow(struct ohash *h)
+{
+	struct ohash o = *h;
+	size_t ncap = o.cap ? o.cap * 2 : 64;
+	h->cap = ncap;
+	h->n = 0;
+	h->used = calloc(ncap, 1);
+	h->keys = malloc(ncap * h->ksz);
+	h->vals = malloc(ncap * (h->vsz ? h->vsz : 1));
+	for (size_t i = 0; i < o.cap; i++)
+		if (o.used[i])
+			oh_put_new(h, o.keys + i * o.ksz, o.vals + i * o.vsz);
+	oh_destroy(&o);
+}
+
+static int oh_update(struct ohash *h, const void *key, const void *val)
+{
+	long i = oh_find(h, key);
+	if (i >= 0) {
+		memcpy(h->vals + i * h->vsz, val, h->vsz);
+		return 0;
+	}
+	if ((h->n + 1) * 2 > h->cap)
+		oh_grow(h);
+	oh_put_new(h, key, val);
+	return 0;
+}
+
+static int oh_delete(struct ohash *h, const void *key)
+{
+	long f = oh_find(h, key);
+	size_t mask, i, j;
+	if (f < 0)
+		return -ENOENT;
+	mask = h->cap - 1;
+	i = (size_t)f;
+	h->used[i] = 0;
+	h->n--;
+	for (j = (i + 1) & mask; h->used[j]; j = (j + 1) & mask) {
+		size_t home = hash_bytes(h->keys + j * h->ksz, h->ksz) & mask;
+		/* move j back to i if i lies cyclically in [home, j) */
+		if ((j > i && (home <= i || home > j)) || (j < i && (home <= i && home > j))) {
+			memcpy(h->keys + i * h->ksz, h->keys + j * h->ksz, h->ksz);
+			memcpy(h->vals + i * h->vsz, h->vals + j * h->vsz, h->vsz);
+			h->used[i] = 1;
+			h->used[j] = 0;
+			i = j;
+		}
+	}
+	return 0;
+}
+
+static inline uint8_t *oh_get(const struct ohash *h, const void *key)
+{
+	long i = oh_find(h, key);
+	return i < 0 ? NULL : h->vals + i * h->vsz;
+}
+
+/* ====================================================================== */
+/* Context                                                                 */
+/* ====================================================================== */
+#define N_METRICS (256 * 4 * 2)
+
+struct or_ctx {
+	or_config cfg;
+	struct lpm_trie ipcache;  /* ipcache_key data = {pad[3], family, ip[16]} */
+	struct ohash *policy;     /* per endpoint: policy_key -> policy_entry */
+	size_t n_ep;
+	struct lpm_trie dyn4, dyn6; /* lpm_v{4,6}_key -> lpm_val */
+	struct ohash fix4, fix6;
+	struct ohash lxc;           /* endpoint_key -> present */
+	uint64_t metrics[N_METRICS];
+};
+
+void or_default_config(or_config *cfg)
+{
+	memset(cfg, 0, sizeof(*cfg));
+	cfg->host_id = 1;
+	cfg->world_id = 2;
+	cfg->cluster_id = 3;
+	cfg->health_id = 4;
+	cfg->ipv4_cluster_mask = 0xff0000;  /* node_config.h:42 */
+	cfg->ipv4_cluster_range = 0x100000; /* node_config.h:43 */
+	cfg->ct_proto_gate = 1;
+	cfg->ingress_src_identity = 0; /* from_netdev: identity = 0 (bpf_netdev.c:487) */
+	cfg->ingress_secctx_world = 0;
+	cfg->dyn4 = cfg->fix4 = cfg->dyn6 = cfg->fix6 = 1; /* bpf/filter_config.h */
+}
+
+or_ctx *or_create(void)
+{
+	or_ctx *c = calloc(1, sizeof(*c));
+	or_default_config(&c->cfg);
+	lpm_init(&c->ipcache, 20, 8);
+	lpm_init(&c->dyn4, 4, 1);
+	lpm_init(&c->dyn6, 16, 1);
+	oh_init(&c->fix4, 8, 1);
+	oh_init(&c->fix6, 20, 1);
+	oh_init(&c->lxc, 20, 1);
+	return c;
+}
+
+void or_destroy(or_ctx *c)
+{
+	if (!c)
+		return;
+	lpm_destroy(&c->ipcache);
+	lpm_destroy(&c->dyn4);
+	lpm_destroy(&c->dyn6);
+	oh_destroy(&c->fix4);
+	oh_destroy(&c->fix6);
+	oh_destroy(&c->lxc);
+	for (size_t i = 0; i < c->n_ep; i++)
+		oh_destroy(&c->policy[i]);
+	free(c->policy);
+	free(c);
+}
+
+void or_set_config(or_ctx *c, const or_config *cfg)
+{
+	c->cfg = *cfg;
+}
+
+int or_ipcache_update(or_ctx *c, const void *key24, const void *val8)
+{
+	return lpm_update(&c->ipcache, key24, val8);
+}
+
+int or_ipcache_delete(or_ctx *c, const void *key24)
+{
+	return lpm_delete(&c->ipcache, key24);
+}
+
+int or_ipcache_lookup(or_ctx *c, const void *key24, void *val8_out)
+{
+	const uint8_t *v = lpm_lookup(&c->ipcache, key24);
+	if (!v)
+		return -ENOENT;
+	memcpy(val8_out, v, 8);
+	return 0;
+}
+
+size_t or_ipcache_count(or_ctx *c)
+{
+	return c->ipcache.n;
+}
+
+static struct ohash *policy_map(or_ctx *c, uint32_t ep, int create)
+{
+	if (ep >= c->n_ep) {
+		size_t nn;
+		if (!create)
+			return NULL;
+		nn = ep + 1;
+		c->policy = realloc(c->policy, nn * sizeof(*c->policy));
+		for (size_t i = c->n_ep; i < nn; i++)
+			oh_init(&c->policy[i], 8, 24);
+		c->n_ep = nn;
+	}
+	return &c->policy[ep];
+}
+
+int or_policy_update(or_ctx *c, uint32_t ep, const void *key8, const void *entry24)
+{
+	return oh_update(policy_map(c, ep, 1), key8, entry24);
+}
+
+int or_policy_delete(or_ctx *c, uint32_t ep, const void *key8)
+{
+	struct ohash *h = policy_map(c, ep, 0);
+	return h ? oh_delete(h, key8) : -ENOENT;
+}
+
+int or_policy_lookup(or_ctx *c, uint32_t ep, const void *key8, void *entry24_out)
+{
+	struct ohash *h = policy_map(c, ep, 0);
+	const uint8_t *v = h ? oh_get(h, key8) : NULL;
+	if (!v)
+		return -ENOENT;
+	memcpy(entry24_out, v, 24);
+	return 0;
+}
+
+int or_cidr_update(or_ctx *c, int which, const void *key)
+{
+	uint8_t one = 0;
+	switch (which) {
+	case 0: return lpm_update(&c->dyn4, key, &one);
+	case 1: return oh_update(&c->fix4, key, &one);
+	case 2: return lpm_update(&c->dyn6, key, &one);
+	case 3: return oh_update(&c->fix6, key, &one);
+	}
+	return -EINVAL;
+}
+
+int or_cidr_delete(or_ctx *c, int which, const void *key)
+{
+	switch (which) {
+	case 0: return lpm_delete(&c->dyn4, key);
+	case 1: return oh_delete(&c->fix4, key);
+	case 2: return lpm_delete(&c->dyn6, key);
+	case 3: return oh_delete(&c->fix6, key);
+	}
+	return -EINVAL;
+}
+
+int or_endpoint_update(or_ctx *c, const void *key20)
+{
+	uint8_t one = 1;
+	return oh_update(&c->lxc, key20, &one);
+}
+
+int or_endpoint_delete(or_ctx *c, const void *key20)
+{
+	return oh_delete(&c->lxc, key20);
+}
+
+/* ====================================================================== */
+/* Per-tuple semantics                                                     */
+/* ====================================================================== */
+
+/* ipcache_lookup4 (bpf/lib/eps.h:70-80, HAVE_LPM_MAP_TYPE form eps.h:113):
+ * key {prefixlen = 32 static + 32, pad = 0, family = ENDPOINT_KEY_IPV4, ip4}. */
+static const uint8_t *ipcache4(const or_ctx *c, uint32_t addr_be)
+{
+	uint8_t key[24];
+	uint32_t plen = 64;
+	memset(key, 0, sizeof(key));
+	memcpy(key, &plen, 4);
+	key[7] = 1; /* ENDPOINT_KEY_IPV4, bpf/lib/common.h:139 */
+	memcpy(key + 8, &addr_be, 4);
+	return lpm_lookup(&c->ipcache, key);
+}
+
+struct pol_res {
+	int ret;
+	int probes;
+	int stage;
+};
+
+/* __policy_can_access (bpf/lib/policy.h:46-110) with cb[CB_POLICY] == 0.
+ * key = {sec_label, dport, protocol, egress = !dir, pad = 0} (policy.h:53-59);
+ * on this little-endian layout the egress:1 bitfield is bit 0 of byte 7. */
+static struct pol_res policy_access(struct ohash *h, uint32_t identity, uint16_t dport,
+				    uint8_t proto, int egress, int frag, uint32_t len)
+{
+	struct pol_res r = { 0, 0, 0 };
+	uint8_t key[8];
+	uint8_t *e;
+	uint16_t pp;
+
+	memcpy(key, &identity, 4);
+	memcpy(key + 4, &dport, 2);
+	key[6] = proto;
+	key[7] = egress ? 1 : 0;
+
+	if (!frag) { /* policy.h:61-72, exact L4 */
+		r.probes++;
+		if (h && (e = oh_get(h, key))) {
+			__atomic_fetch_add((uint64_t *)(e + 8), 1, __ATOMIC_RELAXED);
+			__atomic_fetch_add((uint64_t *)(e + 16), (uint64_t)len, __ATOMIC_RELAXED);
+			memcpy(&pp, e, 2);
+			r.ret = pp; /* get_proxy_port: raw __be16 as int, policy.h:104-107 */
+			r.stage = 1;
+			return r;
+		}
+	}
+	/* policy.h:74-83, L3-only {id, 0, 0, dir} */
+	memset(key + 4, 0, 3);
+	r.probes++;
+	if (h && (e = oh_get(h, key))) {
+		__atomic_fetch_add((uint64_t *)(e + 8), 1, __ATOMIC_RELAXED);
+		__atomic_fetch_add((uint64_t *)(e + 16), (uint64_t)len, __ATOMIC_RELAXED);
+		r.ret = 0; /* TC_ACT_OK */
+		r.stage = 2;
+		return r;
+	}
+	if (!frag) { /* policy.h:85-96, identity-wildcard L4 {0, dport, proto, dir} */
+		memset(key, 0, 4);
+		memcpy(key + 4, &dport, 2);
+		key[6] = proto;
+		r.probes++;
+		if (h && (e = oh_get(h, key))) {
+			__atomic_fetch_add((uint64_t *)(e + 8), 1, __ATOMIC_RELAXED);
+			__atomic_fetch_add((uint64_t *)(e + 16), (uint64_t)len, __ATOMIC_RELAXED);
+			memcpy(&pp, e, 2);
+			r.ret = pp;
+			r.stage = 3;
+			return r;
+		}
+	}
+	r.ret = frag ? DROP_FRAG_NOSUPPORT : DROP_POLICY; /* policy.h:101-103 */
+	return r;
+}
+
+struct cls_job {
+	or_ctx *c;
+	size_t lo, hi;
+	const uint32_t *saddr, *daddr, *len;
+	const uint16_t *dport, *ep;
+	const uint8_t *proto, *flags;
+	int32_t *verdict;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t probes;
+	uint64_t metrics[N_METRICS];
+};
+
+static void *cls_worker(void *arg)
+{
+	struct cls_job *j = arg;
+	const or_ctx *c = j->c;
+	const or_config *cfg = &c->cfg;
+	for (size_t i = j->lo; i < j->hi; i++) {
+		int egress = j->flags[i] & 1, frag = (j->flags[i] >> 1) & 1;
+		uint8_t proto = j->proto[i];
+		uint32_t id;
+		int32_t v;
+		int st, dir = egress ? METRIC_EGRESS : METRIC_INGRESS;
+		uint32_t ep = j->ep[i];
+		struct ohash *h = ep < c->n_ep ? &c->policy[ep] : NULL;
+
+		if (cfg->ct_proto_gate && proto != PROTO_ICMP && proto != PROTO_TCP &&
+		    proto != PROTO_UDP) {
+			/* ct_lookup4 default case, bpf/lib/conntrack.h:526-528 */
+			v = DROP_CT_UNKNOWN_PROTO;
+			id = 0;
+			st = 4;
+		} else if (egress) {
+			/* bpf_lxc.c:484-505 */
+			const uint8_t *info = ipcache4(c, j->daddr[i]);
+			uint32_t label = 0;
+			struct pol_res r;
+			if (info)
+				memcpy(&label, info, 4);
+			if (info && label)
+				id = label;
+			else if ((j->daddr[i] & cfg->ipv4_cluster_mask) == cfg->ipv4_cluster_range)
+				id = cfg->cluster_id;
+			else
+				id = cfg->world_id;
+			j->probes += 1;
+			/* policy_can_egress (policy.h:150-163): is_fragment = false,
+			 * negative collapsed to DROP_POLICY */
+			r = policy_access(h, id, j->dport[i], proto, 1, 0, j->len[i]);
+			v = r.ret >= 0 ? r.ret : DROP_POLICY;
+			st = r.stage;
+			j->probes += r.probes;
+		} else {
+			/* bpf_netdev.c:374-398 (identity_is_reserved: policy.h:41-44) */
+			uint32_t src = cfg->ingress_src_identity, secctx;
+			struct pol_res r;
+			if (src < cfg->health_id) {
+				const uint8_t *info = ipcache4(c, j->saddr[i]);
+				j->probes += 1;
+				if (info) {
+					uint32_t label;
+					memcpy(&label, info, 4);
+					if (label && label != cfg->cluster_id && label != cfg->host_id)
+						src = label;
+				}
+			}
+			secctx = cfg->ingress_secctx_world ? cfg->world_id : src;
+			/* policy_can_access_ingress (policy.h:126-146) */
+			r = policy_access(h, secctx, j->dport[i], proto, 0, frag, j->len[i]);
+			v = r.ret >= 0 ? r.ret : DROP_POLICY;
+			id = secctx;
+			st = r.stage;
+			j->probes += r.probes;
+		}
+		j->verdict[i] = v;
+		if (j->identity)
+			j->identity[i] = id;
+		if (j->stage)
+			j->stage[i] = (uint8_t)st;
+		/* drop: send_drop_notify -> update_metrics(len, dir, -reason)
+		 * (bpf/lib/drop.h:104); forward: REASON_FORWARDED (0) at the verdict */
+		{
+			uint32_t reason = v < 0 ? (uint32_t)(-v) & 0xff : 0;
+			uint64_t *m = &j->metrics[(reason * 4 + dir) * 2];
+			m[0] += 1;
+			m[1] += j->len[i];
+		}
+	}
+	return NULL;
+}
+
+int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
+{
+	struct cls_job *jobs;
+	pthread_t *th;
+	uint64_t probes = 0;
+	if (nthreads <= 0)
+		nthreads = 1;
+	if ((size_t)nthreads > n && n > 0)
+		nthreads = (int)n;
+	jobs = calloc((size_t)nthreads, sizeof(*jobs));
+	th = calloc((size_t)nthreads, sizeof(*th));
+	for (int t = 0; t < nthreads; t++) {
+		struct cls_job *j = &jobs[t];
+		j->c = c;
+		j->lo = n * (size_t)t / (size_t)nthreads;
+		j->hi = n * (size_t)(t + 1) / (size_t)nthreads;
+		j->saddr = saddr;
+		j->daddr = daddr;
+		j->len = len;
+		j->dport = dport;
+		j->ep = ep;
+		j->proto = proto;
+		j->flags = flags;
+		j->verdict = verdict;
+		j->identity = identity;
+		j->stage = stage;
+		if (nthreads == 1)
+			cls_worker(j);
+		else
+			pthread_create(&th[t], NULL, cls_worker, j);
+	}
+	for (int t = 0; t < nthreads; t++) {
+		if (nthreads > 1)
+			pthread_join(th[t], NULL);
+		probes += jobs[t].probes;
+		for (int k = 0; k < N_METRICS; k++)
+			c->metrics[k] += jobs[t].metrics[k];
+	}
+	if (probe_sum)
+		*probe_sum = probes;
+	free(jobs);
+	free(th);
+	return 0;
+}
+
+/* ---- XDP prefilter (bpf/bpf_xdp.c:88-184) ---- */
+
+struct pf_job {
+	or_ctx *c;
+	int v6;
+	size_t lo, hi;
+	const uint32_t *s4, *d4;
+	const uint8_t *s6, *d6, *flags;
+	uint8_t *verdict;
+	uint64_t probes;
+};
+
+static void *pf_worker(void *arg)
+{
+	struct pf_job *j = arg;
+	const or_ctx *c = j->c;
+	const or_config *cfg = &c->cfg;
+	for (size_t i = j->lo; i < j->hi; i++) {
+		uint8_t f = j->flags[i], v;
+		uint8_t pfx[20], ek[20];
+		int fix = j->v6 ? cfg->fix6 : cfg->fix4, dyn = j->v6 ? cfg->dyn6 : cfg->dyn4;
+		if (f == 2) { /* check_filters: other ethertypes pass (bpf_xdp.c:173-177) */
+			j->verdict[i] = XDP_PASS;
+			continue;
+		}
+		if (f == 1) { /* xdp_no_room (bpf_xdp.c:104-105, :139-140, :165-166) */
+			j->verdict[i] = XDP_DROP;
+			continue;
+		}
+		memset(pfx, 0, sizeof(pfx));
+		memset(ek, 0, sizeof(ek));
+		if (!j->v6) {
+			uint32_t plen = 32;
+			memcpy(pfx, &plen, 4);
+			memcpy(pfx + 4, &j->s4[i], 4);
+			memcpy(ek, &j->d4[i], 4);
+			ek[16] = 1; /* ENDPOINT_KEY_IPV4 */
+		} else {
+			uint32_t plen = 128;
+			memcpy(pfx, &plen, 4);
+			memcpy(pfx + 4, j->s6 + 16 * i, 16);
+			memcpy(ek, j->d6 + 16 * i, 16);
+			ek[16] = 2; /* ENDPOINT_KEY_IPV6 */
+		}
+		v = 0;
+		if (fix) { /* CIDR{4,6}_FILTER */
+			if (dyn) { /* CIDR{4,6}_LPM_PREFILTER */
+				j->probes++;
+				if (lpm_lookup(j->v6 ? &c->dyn6 : &c->dyn4, pfx))
+					v = XDP_DROP;
+			}
+			if (!v) {
+				j->probes++;
+				if (oh_get(j->v6 ? &c->fix6 : &c->fix4, pfx))
+					v = XDP_DROP;
+			}
+		}
+		if (!v) { /* check_v{4,6}_endpoint (bpf_xdp.c:88-95, :123-130) */
+			j->probes++;
+			v = oh_get(&c->lxc, ek) ? XDP_PASS : XDP_DROP;
+		}
+		j->verdict[i] = v;
+	}
+	return NULL;
+}
+
+static int prefilter(or_ctx *c, int v6, size_t n, const uint32_t *s4, const uint32_t *d4,
+		     const uint8_t *s6, const uint8_t *d6, const uint8_t *flags,
+		     uint8_t *verdict, int nthreads, uint64_t *probe_sum)
+{
+	struct pf_job *jobs;
+	pthread_t *th;
+	uint64_t probes = 0;
+	if (nthreads <= 0)
+		nthreads = 1;
+	if ((size_t)nthreads > n && n > 0)
+		nthreads = (int)n;
+	jobs = calloc((size_t)nthreads, sizeof(*jobs));
+	th = calloc((size_t)nthreads, sizeof(*th));
+	for (int t = 0; t < nthreads; t++) {
+		struct pf_job *j = &jobs[t];
+		j->c = c;
+		j->v6 = v6;
+		j->lo = n * (size_t)t / (size_t)nthreads;
+		j->hi = n * (size_t)(t + 1) / (size_t)nthreads;
+		j->s4 = s4;
+		j->d4 = d4;
+		j->s6 = s6;
+		j->d6 = d6;
+		j->flags = flags;
+		j->verdict = verdict;
+		if (nthreads == 1)
+			pf_worker(j);
+		else
+			pthread_create(&th[t], NULL, pf_worker, j);
+	}
+	for (int t = 0; t < nthreads; t++) {
+		if (nthreads > 1)
+			pthread_join(th[t], NULL);
+		probes += jobs[t].probes;
+	}
+	if (probe_sum)
+		*probe_sum = probes;
+	free(jobs);
+	free(th);
+	return 0;
+}
+
+int or_prefilter_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		    const uint8_t *flags, uint8_t *verdict, int nthreads, uint64_t *probe_sum)
+{
+	return prefilter(c, 0, n, saddr, daddr, NULL, NULL, flags, verdict, nthreads, probe_sum);
+}
+
+int or_prefilter_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		    const uint8_t *flags, uint8_t *verdict, int nthreads, uint64_t *probe_sum)
+{
+	return prefilter(c, 1, n, NULL, NULL, saddr16, daddr16, flags, verdict, nthreads,
+			 probe_sum);
+}
+
+void or_metrics_read(or_ctx *c, uint64_t *out)
+{
+	memcpy(out, c->metrics, sizeof(c->metrics));
+}
+
+void or_counters_reset(or_ctx *c)
+{
+	memset(c->metrics, 0, sizeof(c->metrics));
+	for (size_t e = 0; e < c->n_ep; e++) {
+		struct ohash *h = &c->policy[e];
+		for (size_t i = 0; i < h->cap; i++)
+			if (h->used[i])
+				memset(h->vals + i * h->vsz + 8, 0, 16);
+	}
+}

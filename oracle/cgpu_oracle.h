@@ -1,0 +1,87 @@
+/*
+ * TEST INFRASTRUCTURE — CPU restatement ("port") of the reference's
+ * classification semantics.  NOT part of the product.  Loaded only by
+ * tests/, bench.py's cpu_baseline leg and __graft_entry__.smoke(), always as
+ * the checker or the timed CPU baseline, never on the product path.
+ *
+ * Parity pinning: every function here is checked against golden vectors the
+ * reference's own BPF C produced (oracle/ref/, tests/golden/).
+ *
+ * Structures are deliberately kernel-like (the "reference CPU path" of
+ * BASELINE.md §2): a path-compressed binary LPM trie walked bit by bit as
+ * kernel/bpf/lpm_trie.c does, and an open hash with whole-key compare as
+ * kernel/bpf/hashtab.c does.  Keys/values use the reference byte layouts:
+ *   policy_key 8 B / policy_entry 24 B       bpf/lib/common.h:180-193
+ *   ipcache_key 24 B / remote_endpoint_info   bpf/lib/maps.h:135-148, common.h:175-178
+ *   lpm_v4_key 8 B / lpm_v6_key 20 B          bpf/lib/xdp.h:23-31
+ *   endpoint_key 20 B                         bpf/lib/common.h:147-160
+ */
+#ifndef CGPU_ORACLE_H
+#define CGPU_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+typedef struct or_ctx or_ctx;
+
+typedef struct or_config {
+	uint32_t host_id, world_id, cluster_id, health_id; /* node_config.h:34-37 */
+	uint32_t ipv4_cluster_mask, ipv4_cluster_range;    /* network-order u32 */
+	int ct_proto_gate;      /* CONNTRACK: DROP_CT_UNKNOWN_PROTO before policy */
+	uint32_t ingress_src_identity; /* identity handed to handle_ipv4 */
+	int ingress_secctx_world;      /* non-FROM_HOST netdev: label = WORLD_ID */
+	int dyn4, fix4, dyn6, fix6;    /* CIDR{4,6}_LPM_PREFILTER / CIDR{4,6}_FILTER */
+} or_config;
+
+or_ctx *or_create(void);
+void or_destroy(or_ctx *c);
+void or_set_config(or_ctx *c, const or_config *cfg);
+void or_default_config(or_config *cfg);
+
+/* table ops: 0 on success, -errno (bpf(2) convention) on failure */
+int or_ipcache_update(or_ctx *c, const void *key24, const void *val8);
+int or_ipcache_delete(or_ctx *c, const void *key24);
+int or_ipcache_lookup(or_ctx *c, const void *key24, void *val8_out); /* LPM */
+size_t or_ipcache_count(or_ctx *c);
+
+int or_policy_update(or_ctx *c, uint32_t ep, const void *key8, const void *entry24);
+int or_policy_delete(or_ctx *c, uint32_t ep, const void *key8);
+int or_policy_lookup(or_ctx *c, uint32_t ep, const void *key8, void *entry24_out);
+
+/* which: 0 v4 dyn (LPM), 1 v4 fix (hash), 2 v6 dyn (LPM), 3 v6 fix (hash) */
+int or_cidr_update(or_ctx *c, int which, const void *key);
+int or_cidr_delete(or_ctx *c, int which, const void *key);
+int or_endpoint_update(or_ctx *c, const void *key20);
+int or_endpoint_delete(or_ctx *c, const void *key20);
+
+/*
+ * Stateless IPv4 classification of n tuples (SoA, network byte order for
+ * addresses and dport).  flags bit0 = egress, bit1 = is_fragment.
+ * verdict: proxy port (raw be16 as int) / 0 allow / negative DROP_*.
+ * identity: label given to policy.  stage: 1 exact, 2 L3, 3 wildcard L4,
+ * 0 miss, 4 protocol-gated.  Per-entry packets/bytes and the metrics table
+ * are accumulated.  *probe_sum receives sum(N_addr + N_pol).
+ * stage / identity may be NULL.  nthreads <= 0 means 1.
+ */
+int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum);
+
+/*
+ * XDP prefilter (bpf/bpf_xdp.c:88-184) over pre-parsed packets.
+ * flags: 0 = IP packet of this family, 1 = truncated (xdp_no_room -> DROP),
+ *        2 = not IPv4/IPv6 ethertype (-> PASS).
+ * v4: addresses are network-order u32; v6: 16 bytes per packet.
+ * verdict: XDP_DROP (1) / XDP_PASS (2).
+ */
+int or_prefilter_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		    const uint8_t *flags, uint8_t *verdict, int nthreads, uint64_t *probe_sum);
+int or_prefilter_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		    const uint8_t *flags, uint8_t *verdict, int nthreads, uint64_t *probe_sum);
+
+/* metrics {reason, dir} -> {count, bytes}; out is [256][4][2] u64 */
+void or_metrics_read(or_ctx *c, uint64_t *out);
+void or_counters_reset(or_ctx *c);
+
+#endif

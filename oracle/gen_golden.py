@@ -1,0 +1,484 @@
+"""TEST INFRASTRUCTURE — emit golden fixtures from the reference's own BPF C.
+
+Run in the development container only (needs /root/reference):
+
+    make -C oracle ref && python oracle/gen_golden.py
+
+It loads oracle/_ref/libref_{policy,xdp}.so — the reference's
+bpf/lib/policy.h, bpf/lib/eps.h and bpf/bpf_xdp.c compiled as host C with
+mocked kernel maps (oracle/ref/) — feeds them seeded scenarios, and writes
+inputs + reference outputs as small .npz files (plain arrays, no pickles)
+under tests/golden/, plus tests/golden/MANIFEST.json.  The fixtures are data;
+nothing from the reference's sources is stored.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+from cilium_amd import layouts as L  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+SEED = 0xC1110000
+
+
+def load_ref():
+    subprocess.run(["make", "-s", "-C", HERE, "ref", "_ref/unit-test"], check=True)
+    pol = C.CDLL(os.path.join(HERE, "_ref", "libref_policy.so"))
+    xdp = C.CDLL(os.path.join(HERE, "_ref", "libref_xdp.so"))
+    u32p = C.POINTER(C.c_uint32)
+    ip = C.POINTER(C.c_int)
+    pol.ref_reset.restype = None
+    pol.ref_policy_update.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+    pol.ref_policy_read.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+    pol.ref_ipcache_update.argtypes = [C.c_void_p, C.c_void_p]
+    pol.ref_ipcache_lookup4.argtypes = [C.c_uint32, u32p, u32p]
+    pol.ref_ipcache_lookup6.argtypes = [C.c_void_p, u32p, u32p]
+    pol.ref_policy_ingress.argtypes = [C.c_int, C.c_uint32, C.c_uint16, C.c_uint8, C.c_int,
+                                       C.c_uint32, ip, ip]
+    pol.ref_policy_egress.argtypes = [C.c_int, C.c_uint32, C.c_uint16, C.c_uint8, C.c_uint32,
+                                      ip, ip]
+    pol.ref_policy_raw.argtypes = [C.c_int, C.c_uint32, C.c_uint16, C.c_uint8, C.c_int, C.c_int,
+                                   C.c_uint32, ip, ip]
+    pol.ref_classify_v4.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint8, C.c_uint8,
+                                    C.c_uint32, C.c_int, C.c_int, C.c_uint32, C.c_int, u32p, ip,
+                                    ip, ip]
+    pol.ref_constants.argtypes = [u32p, C.c_int]
+    xdp.ref_xdp_reset.restype = None
+    xdp.ref_xdp_cidr_update.argtypes = [C.c_int, C.c_void_p]
+    xdp.ref_xdp_endpoint_update.argtypes = [C.c_void_p]
+    xdp.ref_xdp_run.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+    return pol, xdp
+
+
+def b(x):
+    return np.ascontiguousarray(x).tobytes()
+
+
+# ------------------------------------------------------------------ policy
+IDENTS = np.array([0, 1, 2, 3, 4, 5, 256, 257, 300, 1000, 65535, 70000, 0xFFFFFFFF], np.uint32)
+PORTS = np.array([0, 22, 53, 80, 443, 8080, 65535, 4000, 8, 0x0800], np.uint16)
+PROTOS = np.array([0, 1, 6, 17, 132], np.uint8)
+
+
+def gen_policy_keys(rng, n_ep, per_ep):
+    keys, entries, eps = [], [], []
+    for ep in range(n_ep):
+        seen = set()
+        while len([e for e in eps if e == ep]) < per_ep:
+            kind = rng.integers(0, 3)
+            ident = int(rng.choice(IDENTS))
+            port = int(rng.choice(PORTS))
+            proto = int(rng.choice(PROTOS))
+            egress = int(rng.integers(0, 2))
+            if kind == 1:
+                port, proto = 0, 0
+            elif kind == 2:
+                ident = 0
+            pad = int(rng.integers(1, 128)) if rng.random() < 0.05 else 0
+            k = L.policy_key(ident, port, proto, egress, pad)
+            kb = b(k)
+            if kb in seen:
+                continue
+            seen.add(kb)
+            proxy = int(rng.integers(1, 65536)) if rng.random() < 0.15 else 0
+            keys.append(k)
+            entries.append(L.policy_entry(proxy))
+            eps.append(ep)
+    return (np.array(keys, L.POLICY_KEY), np.array(entries, L.POLICY_ENTRY),
+            np.array(eps, np.uint16))
+
+
+def gen_policy_fixture(pol, rng):
+    pol.ref_reset()
+    keys, entries, eps = gen_policy_keys(rng, 4, 60)
+    for k, e, ep in zip(keys, entries, eps):
+        pol.ref_policy_update(int(ep), b(k), b(e))
+    n = 4000
+    q = {
+        "ep": rng.integers(0, 5, n).astype(np.uint16),  # ep 4 has an empty map
+        "identity": np.where(rng.random(n) < 0.8, rng.choice(IDENTS, n),
+                             rng.integers(0, 2**32, n, dtype=np.uint64)).astype(np.uint32),
+        "dport": np.array([L.htons(int(p)) for p in
+                           np.where(rng.random(n) < 0.85, rng.choice(PORTS, n),
+                                    rng.integers(0, 65536, n))], np.uint16),
+        "proto": np.where(rng.random(n) < 0.9, rng.choice(PROTOS, n),
+                          rng.integers(0, 256, n)).astype(np.uint8),
+        "kind": rng.integers(0, 3, n).astype(np.uint8),  # 0 ingress, 1 egress, 2 raw
+        "dir": rng.integers(0, 2, n).astype(np.uint8),   # CT_EGRESS 0 / CT_INGRESS 1 (raw)
+        "frag": (rng.random(n) < 0.15).astype(np.uint8),
+        "len": rng.integers(0, 70000, n).astype(np.uint32),
+    }
+    ret = np.empty(n, np.int32)
+    nprobes = np.empty(n, np.int32)
+    hit = np.empty(n, np.int32)
+    a, h = C.c_int(), C.c_int()
+    for i in range(n):
+        ep, ident, dp, pr = int(q["ep"][i]), int(q["identity"][i]), int(q["dport"][i]), int(q["proto"][i])
+        ln, fr = int(q["len"][i]), int(q["frag"][i])
+        if q["kind"][i] == 0:
+            r = pol.ref_policy_ingress(ep, ident, dp, pr, fr, ln, C.byref(a), C.byref(h))
+        elif q["kind"][i] == 1:
+            r = pol.ref_policy_egress(ep, ident, dp, pr, ln, C.byref(a), C.byref(h))
+        else:
+            r = pol.ref_policy_raw(ep, ident, dp, pr, int(q["dir"][i]), fr, ln, C.byref(a),
+                                   C.byref(h))
+        ret[i], nprobes[i], hit[i] = r, a.value, h.value
+    final = np.zeros(len(keys), L.POLICY_ENTRY)
+    for i, (k, ep) in enumerate(zip(keys, eps)):
+        buf = C.create_string_buffer(24)
+        assert pol.ref_policy_read(int(ep), b(k), buf) == 0
+        final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+    return dict(keys=keys, entries=entries, key_ep=eps, **{"q_" + k: v for k, v in q.items()},
+                ret=ret, nprobes=nprobes, hit_probe=hit, final_entries=final)
+
+
+# ----------------------------------------------------------------- ipcache
+def rand_v4_prefixes(rng, n, lens, weights):
+    lens = rng.choice(lens, n, p=np.array(weights) / np.sum(weights))
+    addrs = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    # cluster prefixes in a few /8s so they overlap
+    top = rng.choice(np.array([10, 172, 192, 100, 16], np.uint32), n)
+    addrs = np.where(rng.random(n) < 0.7, (addrs & 0x00FFFFFF) | (top << 24), addrs)
+    return addrs.astype(np.uint32), lens.astype(np.int64)
+
+
+def v4_str(h):
+    h = int(h)
+    return f"{h >> 24}.{(h >> 16) & 255}.{(h >> 8) & 255}.{h & 255}"
+
+
+def gen_ipcache_entries(rng, n4, n6, static=True):
+    keys, vals = [], []
+    addrs, lens = rand_v4_prefixes(rng, n4, [1, 2, 7, 8, 12, 16, 20, 23, 24, 25, 28, 31, 32],
+                                   [1, 1, 2, 5, 5, 10, 10, 5, 30, 5, 10, 3, 15])
+    for a, ln in zip(addrs, lens):
+        k = L.ipcache_key(f"{v4_str(a)}/{ln}")
+        if rng.random() < 0.3:  # keep host bits beyond the prefix (kernel ignores them)
+            k["ip"][:4] = np.frombuffer(int(a).to_bytes(4, "big"), np.uint8)
+        label = 0 if rng.random() < 0.05 else int(rng.choice(
+            [1, 2, 3, 4, 5, int(rng.integers(256, 70000)), int(rng.integers(0, 2**32))]))
+        keys.append(k)
+        vals.append(L.remote_info(label, int(rng.integers(0, 2**32))))
+    for _ in range(n6):
+        ln = int(rng.choice([3, 8, 16, 32, 48, 56, 64, 65, 96, 112, 127, 128]))
+        raw = bytearray(rng.integers(0, 256, 16, dtype=np.uint8).tobytes())
+        if rng.random() < 0.7:
+            raw[0:4] = bytes([0xf0, 0x0d, 0, int(rng.integers(0, 4))])
+        k = np.zeros((), L.IPCACHE_KEY)
+        k["family"] = L.ENDPOINT_KEY_IPV6
+        k["prefixlen"] = 32 + ln
+        k["ip"][:] = np.frombuffer(bytes(raw), np.uint8)
+        label = 0 if rng.random() < 0.05 else int(rng.integers(1, 2**32))
+        keys.append(k)
+        vals.append(L.remote_info(label, int(rng.integers(0, 2**32))))
+    # entries whose prefixlen stops inside the static {pad, family} part
+    for plen, fam, pad in () if not static else ((0, 0, 0), (20, 0, 0), (30, 1, 0), (31, 2, 0), (31, 1, 0),
+                           (24, 0, 5), (32, 1, 7)):
+        k = np.zeros((), L.IPCACHE_KEY)
+        k["prefixlen"] = plen
+        k["family"] = fam
+        k["pad"][2] = pad
+        keys.append(k)
+        vals.append(L.remote_info(0xABC00000 + plen, plen))
+    return np.array(keys, L.IPCACHE_KEY), np.array(vals, L.REMOTE_ENDPOINT_INFO)
+
+
+def v4_queries_near(rng, keys, n):
+    v4 = keys[keys["family"] == L.ENDPOINT_KEY_IPV4]
+    base = v4["ip"][:, :4].copy().view(">u4").ravel().astype(np.uint64)
+    pick = base[rng.integers(0, len(base), n)]
+    noise = rng.integers(0, 2**32, n, dtype=np.uint64) & rng.choice(
+        np.array([0, 0xFF, 0xFFFF, 0xFFFFFF, 0xFFFFFFFF], np.uint64), n)
+    h = np.where(rng.random(n) < 0.8, pick ^ noise, rng.integers(0, 2**32, n, dtype=np.uint64))
+    return np.array([L.ip4_be(int(x)) for x in h.astype(np.uint32)], np.uint32)
+
+
+def v6_queries_near(rng, keys, n):
+    v6 = keys[keys["family"] == L.ENDPOINT_KEY_IPV6]["ip"]
+    out = np.empty((n, 16), np.uint8)
+    for i in range(n):
+        if rng.random() < 0.8 and len(v6):
+            a = v6[rng.integers(0, len(v6))].copy()
+            cut = int(rng.integers(0, 17))
+            a[cut:] = rng.integers(0, 256, 16 - cut, dtype=np.uint8)
+        else:
+            a = rng.integers(0, 256, 16, dtype=np.uint8)
+        out[i] = a
+    return out
+
+
+def gen_ipcache_fixture(pol, rng):
+    pol.ref_reset()
+    keys, vals = gen_ipcache_entries(rng, 400, 300, static=True)
+    n_static = 7  # the last 7 entries stop inside the static {pad, family} bits
+    q4 = v4_queries_near(rng, keys, 4000)
+    q6 = v6_queries_near(rng, keys, 3000)
+    lab, tun = C.c_uint32(), C.c_uint32()
+    out = dict(keys=keys, vals=vals, n_static=np.array(n_static), q4=q4, q6=q6)
+    # phase a: without the static-part entries (misses occur); phase b: all
+    for phase, upto in (("a", len(keys) - n_static), ("b", len(keys))):
+        pol.ref_reset()
+        for k, v in zip(keys[:upto], vals[:upto]):
+            pol.ref_ipcache_update(b(k), b(v))
+        r4 = np.zeros((len(q4), 3), np.uint32)
+        for i, a in enumerate(q4):
+            f = pol.ref_ipcache_lookup4(int(a), C.byref(lab), C.byref(tun))
+            r4[i] = (f, lab.value if f else 0, tun.value if f else 0)
+        r6 = np.zeros((len(q6), 3), np.uint32)
+        for i, a in enumerate(q6):
+            f = pol.ref_ipcache_lookup6(a.tobytes(), C.byref(lab), C.byref(tun))
+            r6[i] = (f, lab.value if f else 0, tun.value if f else 0)
+        out["r4" + phase], out["r6" + phase] = r4, r6
+    return out
+
+
+# ---------------------------------------------------------------- classify
+CONFIGS = [  # (ct_proto_gate, ingress_src_identity, ingress_secctx_world)
+    (1, 0, 0), (0, 2, 0), (1, 0, 1), (1, 256, 0), (1, 3, 0)]
+
+
+def gen_classify_fixture(pol, rng):
+    ikeys, ivals = gen_ipcache_entries(rng, 500, 0, static=False)
+    keep = ikeys["prefixlen"] > 32 + 4  # no catch-all: exercise the cluster/world fallback
+    ikeys, ivals = ikeys[keep], ivals[keep]
+    # the agent's reserved entries (daemon/daemon.go:957-1013), minus 0.0.0.0/0
+    extra = [("0.0.16.0/24", 3), ("10.0.0.1/32", 1), ("10.0.0.2/32", 1), ("172.16.0.0/12", 0)]
+    ek = np.array([L.ipcache_key(c) for c, _ in extra], L.IPCACHE_KEY)
+    ev = np.array([L.remote_info(i) for _, i in extra], L.REMOTE_ENDPOINT_INFO)
+    ikeys = np.concatenate([ek, ikeys])
+    ivals = np.concatenate([ev, ivals])
+    hot = rng.choice(len(ikeys), 40, replace=False)
+    labels = np.unique(ivals["sec_label"][hot])
+    # policy keys drawn from the identities the ipcache resolves to
+    pk, pe, pep = [], [], []
+    for ep in range(4):
+        seen = set()
+        for _ in range(120):
+            kind = rng.integers(0, 3)
+            ident = int(rng.choice(labels)) if rng.random() < 0.8 else int(rng.choice(IDENTS))
+            port = int(rng.choice(PORTS))
+            proto = int(rng.choice(np.array([6, 17, 1, 6, 6, 132], np.uint8)))
+            port = int(rng.choice(PORTS[1:6])) if kind != 1 and rng.random() < 0.7 else port
+            egress = int(rng.integers(0, 2))
+            if kind == 1:
+                port, proto = 0, 0
+            elif kind == 2:
+                ident = 0
+            k = L.policy_key(ident, port, proto, egress)
+            if b(k) in seen:
+                continue
+            seen.add(b(k))
+            pk.append(k)
+            pe.append(L.policy_entry(int(rng.integers(1, 65536)) if rng.random() < 0.1 else 0))
+            pep.append(ep)
+    pk = np.array(pk, L.POLICY_KEY)
+    pe = np.array(pe, L.POLICY_ENTRY)
+    pep = np.array(pep, np.uint16)
+
+    n = 6000
+    hk = ikeys[hot]
+    q4s = np.where(rng.random(n) < 0.5, v4_queries_near(rng, hk, n), v4_queries_near(rng, ikeys, n))
+    q4d = np.where(rng.random(n) < 0.5, v4_queries_near(rng, hk, n), v4_queries_near(rng, ikeys, n))
+    t = {
+        "saddr": q4s, "daddr": q4d,
+        "dport": np.array([L.htons(int(p)) for p in np.where(
+            rng.random(n) < 0.9, rng.choice(PORTS[:6], n), rng.integers(0, 65536, n))], np.uint16),
+        "proto": rng.choice(np.array([6, 6, 6, 6, 17, 17, 17, 1, 1, 47, 132, 0], np.uint8), n),
+        "flags": ((rng.random(n) < 0.5).astype(np.uint8) |
+                  ((rng.random(n) < 0.08).astype(np.uint8) << 1)),
+        "len": rng.integers(0, 70000, n).astype(np.uint32),
+        "ep": rng.integers(0, 5, n).astype(np.uint16),
+    }
+    out = {}
+    for ci, (gate, src, sw) in enumerate(CONFIGS):
+        pol.ref_reset()
+        for k, v in zip(ikeys, ivals):
+            pol.ref_ipcache_update(b(k), b(v))
+        for k, e, ep in zip(pk, pe, pep):
+            pol.ref_policy_update(int(ep), b(k), b(e))
+        verdict = np.empty(n, np.int32)
+        ident = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        nprobes = np.empty(n, np.int32)
+        naddr = np.empty(n, np.int32)
+        idv, st, npb, na = C.c_uint32(), C.c_int(), C.c_int(), C.c_int()
+        for i in range(n):
+            verdict[i] = pol.ref_classify_v4(
+                int(t["saddr"][i]), int(t["daddr"][i]), int(t["dport"][i]), int(t["proto"][i]),
+                int(t["flags"][i]), int(t["len"][i]), int(t["ep"][i]), gate, src, sw,
+                C.byref(idv), C.byref(st), C.byref(npb), C.byref(na))
+            ident[i], stage[i], nprobes[i], naddr[i] = idv.value, st.value, npb.value, na.value
+        final = np.zeros(len(pk), L.POLICY_ENTRY)
+        for i, (k, ep) in enumerate(zip(pk, pep)):
+            buf = C.create_string_buffer(24)
+            assert pol.ref_policy_read(int(ep), b(k), buf) == 0
+            final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+        out[f"c{ci}_verdict"] = verdict
+        out[f"c{ci}_identity"] = ident
+        out[f"c{ci}_stage"] = stage
+        out[f"c{ci}_nprobes"] = nprobes
+        out[f"c{ci}_naddr"] = naddr
+        out[f"c{ci}_final_entries"] = final
+    return dict(ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe, pol_ep=pep,
+                configs=np.array(CONFIGS, np.int64), **{"t_" + k: v for k, v in t.items()}, **out)
+
+
+# --------------------------------------------------------------------- xdp
+def eth(ethertype, payload):
+    return bytes(6) + bytes([2, 0, 0, 0, 0, 1]) + ethertype.to_bytes(2, "big") + payload
+
+
+def ip4hdr(saddr_be, daddr_be):
+    h = bytearray(20)
+    h[0] = 0x45
+    h[9] = 6
+    h[12:16] = int(saddr_be).to_bytes(4, "little")
+    h[16:20] = int(daddr_be).to_bytes(4, "little")
+    return bytes(h)
+
+
+def ip6hdr(s16, d16):
+    h = bytearray(40)
+    h[0] = 0x60
+    h[6] = 17
+    h[8:24] = bytes(s16)
+    h[24:40] = bytes(d16)
+    return bytes(h)
+
+
+def gen_xdp_fixture(xdp, rng):
+    xdp.ref_xdp_reset()
+    dyn4, fix4, dyn6, fix6, eps = [], [], [], [], []
+    a4, l4 = rand_v4_prefixes(rng, 150, [4, 8, 12, 16, 20, 24, 28, 31, 32], [1, 3, 3, 5, 5, 10, 3, 1, 2])
+    for a, ln in zip(a4, l4):
+        k = np.zeros((), L.LPM_V4_KEY)
+        k["prefixlen"] = ln
+        k["addr"][:] = np.frombuffer(int(a).to_bytes(4, "big"), np.uint8)
+        dyn4.append(k)
+    a4f, _ = rand_v4_prefixes(rng, 150, [32], [1])
+    for i, a in enumerate(a4f):
+        k = np.zeros((), L.LPM_V4_KEY)
+        k["prefixlen"] = 32 if i % 25 else 24  # a hash key with prefixlen != 32 never matches
+        k["addr"][:] = np.frombuffer(int(a).to_bytes(4, "big"), np.uint8)
+        fix4.append(k)
+    for i in range(150):
+        k = np.zeros((), L.LPM_V6_KEY)
+        k["prefixlen"] = int(rng.choice([16, 32, 48, 56, 64, 100, 128]))
+        raw = bytearray(rng.integers(0, 256, 16, dtype=np.uint8).tobytes())
+        raw[0:3] = bytes([0x20, 0x01, int(rng.integers(0, 4))])
+        k["addr"][:] = np.frombuffer(bytes(raw), np.uint8)
+        dyn6.append(k)
+    for i in range(150):
+        k = np.zeros((), L.LPM_V6_KEY)
+        k["prefixlen"] = 128 if i % 25 else 64
+        raw = bytearray(rng.integers(0, 256, 16, dtype=np.uint8).tobytes())
+        raw[0:3] = bytes([0x20, 0x01, int(rng.integers(0, 4))])
+        k["addr"][:] = np.frombuffer(bytes(raw), np.uint8)
+        fix6.append(k)
+    ep4 = rng.integers(0, 2**32, 60, dtype=np.uint64).astype(np.uint32)
+    ep6 = rng.integers(0, 256, (60, 16), dtype=np.uint8)
+    for i in range(60):
+        k = np.zeros((), L.ENDPOINT_KEY)
+        k["ip"][:4] = np.frombuffer(int(ep4[i]).to_bytes(4, "little"), np.uint8)
+        k["family"] = 1
+        if i % 20 == 19:
+            k["pad4"] = 1  # never matches a lookup key
+        eps.append(k)
+        k6 = np.zeros((), L.ENDPOINT_KEY)
+        k6["ip"][:] = ep6[i]
+        k6["family"] = 2
+        eps.append(k6)
+    dyn4, fix4 = np.array(dyn4, L.LPM_V4_KEY), np.array(fix4, L.LPM_V4_KEY)
+    dyn6, fix6 = np.array(dyn6, L.LPM_V6_KEY), np.array(fix6, L.LPM_V6_KEY)
+    eps = np.array(eps, L.ENDPOINT_KEY)
+    for w, arr in enumerate((dyn4, fix4, dyn6, fix6)):
+        for k in arr:
+            xdp.ref_xdp_cidr_update(w, b(k))
+    for k in eps:
+        xdp.ref_xdp_endpoint_update(b(k))
+
+    def pick4(src):
+        r = rng.random()
+        if r < 0.35:
+            base = int.from_bytes(bytes(src[rng.integers(0, len(src))]["addr"]), "big")
+            return L.ip4_be(base ^ int(rng.integers(0, 256)) if rng.random() < 0.5 else base)
+        return int(rng.integers(0, 2**32))
+
+    frames, s4l, d4l, f4l, s6l, d6l, f6l, fam = [], [], [], [], [], [], [], []
+    n = 2500
+    for i in range(n):
+        s = pick4(dyn4 if rng.random() < 0.5 else fix4)
+        d = int(ep4[rng.integers(0, 60)]) if rng.random() < 0.6 else int(rng.integers(0, 2**32))
+        fr = eth(0x0800, ip4hdr(s, d))
+        if rng.random() < 0.03:
+            fr = fr[: int(rng.integers(0, 34))]
+        frames.append(fr)
+    for i in range(n):
+        src = dyn6 if rng.random() < 0.5 else fix6
+        a = bytearray(bytes(src[rng.integers(0, len(src))]["addr"]))
+        if rng.random() < 0.6:
+            cut = int(rng.integers(2, 17))
+            a[cut:] = rng.integers(0, 256, 16 - cut, dtype=np.uint8).tobytes()
+        if rng.random() < 0.3:
+            a = bytearray(rng.integers(0, 256, 16, dtype=np.uint8).tobytes())
+        d = ep6[rng.integers(0, 60)].tobytes() if rng.random() < 0.6 else \
+            rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        fr = eth(0x86DD, ip6hdr(a, d))
+        if rng.random() < 0.03:
+            fr = fr[: int(rng.integers(0, 54))]
+        frames.append(fr)
+    for i in range(100):  # other ethertypes and runts
+        et = int(rng.choice([0x0806, 0x8100, 0x88CC, 0x0000, 0xFFFF]))
+        frames.append(eth(et, bytes(40))[: int(rng.integers(0, 60))])
+    verdict = np.empty(len(frames), np.uint8)
+    probes = np.empty(len(frames), np.uint64)
+    pc = C.c_uint64()
+    for i, fr in enumerate(frames):
+        verdict[i] = xdp.ref_xdp_run(fr, len(fr), C.byref(pc))
+        probes[i] = pc.value
+    lens = np.array([len(f) for f in frames], np.uint32)
+    blob = np.frombuffer(b"".join(frames), np.uint8)
+    return dict(dyn4=dyn4, fix4=fix4, dyn6=dyn6, fix6=fix6, endpoints=eps,
+                frame_bytes=blob, frame_len=lens, verdict=verdict, probes=probes)
+
+
+def save(name, d):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **d)
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    pol, xdp = load_ref()
+    # the reference's own host unit test (test/bpf/unit-test.c) must pass as built
+    subprocess.run([os.path.join(HERE, "_ref", "unit-test")], check=True)
+    consts = (C.c_uint32 * 16)()
+    k = pol.ref_constants(consts, 16)
+    manifest = {"generator": "oracle/gen_golden.py", "seed": SEED,
+                "reference": "sunxiaojun2014/cilium @ VERSION 1.2.90 (bpf/ compiled as host C)",
+                "constants": [int(consts[i]) for i in range(k)], "files": {}}
+    rng = np.random.Generator(np.random.PCG64(SEED))
+    manifest["files"]["policy_cascade.npz"] = save("policy_cascade.npz", gen_policy_fixture(pol, rng))
+    manifest["files"]["ipcache_lpm.npz"] = save("ipcache_lpm.npz", gen_ipcache_fixture(pol, rng))
+    manifest["files"]["classify_v4.npz"] = save("classify_v4.npz", gen_classify_fixture(pol, rng))
+    manifest["files"]["xdp_prefilter.npz"] = save("xdp_prefilter.npz", gen_xdp_fixture(xdp, rng))
+    with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print(json.dumps(manifest, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+"""TEST INFRASTRUCTURE — ctypes wrapper of the CPU restatement (liboracle.so).
+
+Only tests/, bench.py's ``cpu_baseline`` leg and ``__graft_entry__.smoke()``
+may import this module, and only as the checker / the timed CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+
+class OrConfig(C.Structure):
+    _fields_ = [
+        ("host_id", C.c_uint32), ("world_id", C.c_uint32), ("cluster_id", C.c_uint32),
+        ("health_id", C.c_uint32), ("ipv4_cluster_mask", C.c_uint32),
+        ("ipv4_cluster_range", C.c_uint32), ("ct_proto_gate", C.c_int),
+        ("ingress_src_identity", C.c_uint32), ("ingress_secctx_world", C.c_int),
+        ("dyn4", C.c_int), ("fix4", C.c_int), ("dyn6", C.c_int), ("fix6", C.c_int),
+    ]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, sz = C.c_void_p, C.c_size_t
+        L.or_create.restype = vp
+        L.or_destroy.argtypes = [vp]
+        L.or_set_config.argtypes = [vp, C.POINTER(OrConfig)]
+        L.or_default_config.argtypes = [C.POINTER(OrConfig)]
+        for f in ("or_ipcache_update", "or_ipcache_lookup"):
+            getattr(L, f).argtypes = [vp, vp, vp]
+        L.or_ipcache_delete.argtypes = [vp, vp]
+        L.or_ipcache_count.argtypes = [vp]
+        L.or_ipcache_count.restype = sz
+        L.or_policy_update.argtypes = [vp, C.c_uint32, vp, vp]
+        L.or_policy_lookup.argtypes = [vp, C.c_uint32, vp, vp]
+        L.or_policy_delete.argtypes = [vp, C.c_uint32, vp]
+        L.or_cidr_update.argtypes = [vp, C.c_int, vp]
+        L.or_cidr_delete.argtypes = [vp, C.c_int, vp]
+        L.or_endpoint_update.argtypes = [vp, vp]
+        L.or_endpoint_delete.argtypes = [vp, vp]
+        L.or_classify_v4.argtypes = [vp, sz] + [vp] * 10 + [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_prefilter_v4.argtypes = [vp, sz, vp, vp, vp, vp, C.c_int, C.POINTER(C.c_uint64)]
+        L.or_prefilter_v6.argtypes = [vp, sz, vp, vp, vp, vp, C.c_int, C.POINTER(C.c_uint64)]
+        L.or_metrics_read.argtypes = [vp, vp]
+        L.or_counters_reset.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _b(x):
+    """numpy scalar/record -> bytes buffer kept alive by caller."""
+    return np.ascontiguousarray(x).tobytes()
+
+
+class Oracle:
+    def __init__(self, **cfg):
+        self.L = lib()
+        self.h = self.L.or_create()
+        self.cfg = OrConfig()
+        self.L.or_default_config(C.byref(self.cfg))
+        self.configure(**cfg)
+
+    def configure(self, **kw):
+        for k, v in kw.items():
+            setattr(self.cfg, k, v)
+        self.L.or_set_config(self.h, C.byref(self.cfg))
+
+    def close(self):
+        if self.h:
+            self.L.or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- tables ---
+    def ipcache_update(self, key, val):
+        return self.L.or_ipcache_update(self.h, _b(key), _b(val))
+
+    def ipcache_delete(self, key):
+        return self.L.or_ipcache_delete(self.h, _b(key))
+
+    def ipcache_lookup(self, key):
+        out = C.create_string_buffer(8)
+        r = self.L.or_ipcache_lookup(self.h, _b(key), out)
+        return r, out.raw
+
+    def policy_update(self, ep, key, entry):
+        return self.L.or_policy_update(self.h, ep, _b(key), _b(entry))
+
+    def policy_delete(self, ep, key):
+        return self.L.or_policy_delete(self.h, ep, _b(key))
+
+    def policy_lookup(self, ep, key):
+        out = C.create_string_buffer(24)
+        r = self.L.or_policy_lookup(self.h, ep, _b(key), out)
+        return r, out.raw
+
+    def cidr_update(self, which, key):
+        return self.L.or_cidr_update(self.h, which, _b(key))
+
+    def cidr_delete(self, which, key):
+        return self.L.or_cidr_delete(self.h, which, _b(key))
+
+    def endpoint_update(self, key):
+        return self.L.or_endpoint_update(self.h, _b(key))
+
+    def endpoint_delete(self, key):
+        return self.L.or_endpoint_delete(self.h, _b(key))
+
+    # --- batch ---
+    def classify_v4(self, t, nthreads=1):
+        n = len(t["saddr"])
+        verdict = np.empty(n, np.int32)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint32), ("daddr", np.uint32), ("dport", np.uint16),
+            ("proto", np.uint8), ("flags", np.uint8), ("len", np.uint32), ("ep", np.uint16))]
+        self.L.or_classify_v4(self.h, n, *[_p(a) for a in arrs], _p(verdict), _p(identity),
+                              _p(stage), nthreads, C.byref(probes))
+        return verdict, identity, stage, probes.value
+
+    def prefilter_v4(self, saddr, daddr, flags, nthreads=1):
+        n = len(flags)
+        out = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        s, d, f = (np.ascontiguousarray(saddr, np.uint32), np.ascontiguousarray(daddr, np.uint32),
+                   np.ascontiguousarray(flags, np.uint8))
+        self.L.or_prefilter_v4(self.h, n, _p(s), _p(d), _p(f), _p(out), nthreads, C.byref(probes))
+        return out, probes.value
+
+    def prefilter_v6(self, saddr16, daddr16, flags, nthreads=1):
+        n = len(flags)
+        out = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        s, d, f = (np.ascontiguousarray(saddr16, np.uint8), np.ascontiguousarray(daddr16, np.uint8),
+                   np.ascontiguousarray(flags, np.uint8))
+        self.L.or_prefilter_v6(self.h, n, _p(s), _p(d), _p(f), _p(out), nthreads, C.byref(probes))
+        return out, probes.value
+
+    def metrics(self):
+        out = np.zeros((256, 4, 2), np.uint64)
+        self.L.or_metrics_read(self.h, _p(out))
+        return out
+
+    def counters_reset(self):
+        self.L.or_counters_reset(self.h)

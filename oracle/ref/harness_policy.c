@@ -1,0 +1,285 @@
+/*
+ * TEST INFRASTRUCTURE — the reference oracle.  Built ONLY in the development
+ * container (it #includes /root/reference/bpf, which never travels to the
+ * GPU box) into oracle/_ref/libref_policy.so by oracle/Makefile.  It is run
+ * solely by oracle/gen_golden.py to emit tests/golden/* fixtures.
+ *
+ * It compiles the reference's own datapath C as host C, unmodified:
+ *   - __policy_can_access / policy_can_access_ingress / policy_can_egress
+ *     (bpf/lib/policy.h:46-177)
+ *   - ipcache_lookup4 / ipcache_lookup6 (bpf/lib/eps.h:56-80)
+ *   - identity_is_reserved (bpf/lib/policy.h:41-44)
+ * with map_lookup_elem pointed at the mock map store (mockmap.c), because
+ * the map implementations live in the Linux kernel, not in the reference.
+ *
+ * The per-tuple composition (which address feeds ipcache, the identity
+ * fallback, the protocol gate) is glue restated from the reference's
+ * callers, each line citing the caller it follows.
+ */
+#include <stdio.h>
+#include <string.h>
+#include <stdint.h>
+
+#include "lib/utils.h"
+#include "node_config.h"
+#include "lxc_config.h"
+/* Notification/debug paths emit perf events through helpers the harness
+ * does not mock; they do not influence verdicts or map contents. */
+#undef DROP_NOTIFY
+#undef TRACE_NOTIFY
+#undef DEBUG
+#include "lib/common.h"
+#include "lib/policy.h"
+#include "lib/eps.h"
+
+#include "mockmap.h"
+
+#define REF_MAX_EP 64
+
+static struct mockmap policy_maps[REF_MAX_EP];
+static struct mockmap ipcache;
+static int cur_ep;
+static int inited;
+/* probe accounting: index (1-based) of the policy probe that hit, and count */
+static int pol_probes, pol_hit_probe;
+
+static void *mock_lookup(void *map, const void *key)
+{
+	if (map == &POLICY_MAP) {
+		void *v;
+		pol_probes++;
+		v = mockmap_lookup(&policy_maps[cur_ep], key);
+		if (v)
+			pol_hit_probe = pol_probes;
+		return v;
+	}
+	if (map == &cilium_ipcache)
+		return mockmap_lookup(&ipcache, key);
+	fprintf(stderr, "ref harness: lookup on unexpected map %p\n", map);
+	return NULL;
+}
+
+static void ensure_init(void)
+{
+	if (inited)
+		return;
+	for (int i = 0; i < REF_MAX_EP; i++)
+		mockmap_init(&policy_maps[i], MOCK_HASH, sizeof(struct policy_key),
+			     sizeof(struct policy_entry));
+	mockmap_init(&ipcache, MOCK_LPM, sizeof(struct ipcache_key),
+		     sizeof(struct remote_endpoint_info));
+	map_lookup_elem = mock_lookup;
+	inited = 1;
+}
+
+void ref_reset(void)
+{
+	ensure_init();
+	for (int i = 0; i < REF_MAX_EP; i++)
+		mockmap_clear(&policy_maps[i]);
+	mockmap_clear(&ipcache);
+}
+
+int ref_sizes(int *policy_key_sz, int *policy_entry_sz, int *ipcache_key_sz,
+	      int *remote_info_sz)
+{
+	*policy_key_sz = sizeof(struct policy_key);
+	*policy_entry_sz = sizeof(struct policy_entry);
+	*ipcache_key_sz = sizeof(struct ipcache_key);
+	*remote_info_sz = sizeof(struct remote_endpoint_info);
+	return 0;
+}
+
+/* Raw 8-byte policy_key / 24-byte policy_entry, as bpf(2) would copy them. */
+int ref_policy_update(int ep, const void *key, const void *entry)
+{
+	ensure_init();
+	if (ep < 0 || ep >= REF_MAX_EP)
+		return -1;
+	return mockmap_update(&policy_maps[ep], key, entry);
+}
+
+int ref_policy_read(int ep, const void *key, void *entry_out)
+{
+	void *v;
+	ensure_init();
+	v = mockmap_lookup(&policy_maps[ep], key);
+	if (!v)
+		return -1;
+	memcpy(entry_out, v, sizeof(struct policy_entry));
+	return 0;
+}
+
+/* Raw 24-byte ipcache_key / 8-byte remote_endpoint_info. */
+int ref_ipcache_update(const void *key, const void *info)
+{
+	ensure_init();
+	return mockmap_update(&ipcache, key, info);
+}
+
+/* ipcache_lookup4 (bpf/lib/eps.h:70-80) at V4_CACHE_KEY_LEN, the
+ * HAVE_LPM_MAP_TYPE form used by the datapath (eps.h:111-114). */
+int ref_ipcache_lookup4(uint32_t addr_be, uint32_t *sec_label, uint32_t *tunnel)
+{
+	struct remote_endpoint_info *info;
+	ensure_init();
+	info = ipcache_lookup4(&cilium_ipcache, addr_be, V4_CACHE_KEY_LEN);
+	if (!info)
+		return 0;
+	*sec_label = info->sec_label;
+	*tunnel = info->tunnel_endpoint;
+	return 1;
+}
+
+/* ipcache_lookup6 (bpf/lib/eps.h:56-66) at V6_CACHE_KEY_LEN. */
+int ref_ipcache_lookup6(const uint8_t *addr16, uint32_t *sec_label, uint32_t *tunnel)
+{
+	struct remote_endpoint_info *info;
+	union v6addr a;
+	ensure_init();
+	memcpy(&a, addr16, 16);
+	info = ipcache_lookup6(&cilium_ipcache, &a, V6_CACHE_KEY_LEN);
+	if (!info)
+		return 0;
+	*sec_label = info->sec_label;
+	*tunnel = info->tunnel_endpoint;
+	return 1;
+}
+
+static void fresh_skb(struct __sk_buff *skb, uint32_t len)
+{
+	memset(skb, 0, sizeof(*skb));
+	skb->len = len; /* cb[CB_POLICY] == 0: no CT reply/proxy skip mark */
+}
+
+/* policy_can_access_ingress (bpf/lib/policy.h:126-146). */
+int ref_policy_ingress(int ep, uint32_t identity, uint16_t dport_be, uint8_t proto,
+		       int is_fragment, uint32_t len, int *nprobes, int *hit_probe)
+{
+	struct __sk_buff skb;
+	int ret;
+	ensure_init();
+	fresh_skb(&skb, len);
+	cur_ep = ep;
+	pol_probes = pol_hit_probe = 0;
+	ret = policy_can_access_ingress(&skb, identity, dport_be, proto, 0, NULL,
+					is_fragment ? true : false);
+	*nprobes = pol_probes;
+	*hit_probe = pol_hit_probe;
+	return ret;
+}
+
+/* policy_can_egress (bpf/lib/policy.h:150-163). */
+int ref_policy_egress(int ep, uint32_t identity, uint16_t dport_be, uint8_t proto,
+		      uint32_t len, int *nprobes, int *hit_probe)
+{
+	struct __sk_buff skb;
+	int ret;
+	ensure_init();
+	fresh_skb(&skb, len);
+	cur_ep = ep;
+	pol_probes = pol_hit_probe = 0;
+	ret = policy_can_egress(&skb, identity, dport_be, proto);
+	*nprobes = pol_probes;
+	*hit_probe = pol_hit_probe;
+	return ret;
+}
+
+/* Raw __policy_can_access (bpf/lib/policy.h:46-110), to pin the
+ * un-collapsed DROP_FRAG_NOSUPPORT (-157) path. */
+int ref_policy_raw(int ep, uint32_t identity, uint16_t dport_be, uint8_t proto,
+		   int dir, int is_fragment, uint32_t len, int *nprobes, int *hit_probe)
+{
+	struct __sk_buff skb;
+	int ret;
+	ensure_init();
+	fresh_skb(&skb, len);
+	cur_ep = ep;
+	pol_probes = pol_hit_probe = 0;
+	ret = __policy_can_access(&POLICY_MAP, &skb, identity, dport_be, proto, 0,
+				  NULL, dir, is_fragment ? true : false);
+	*nprobes = pol_probes;
+	*hit_probe = pol_hit_probe;
+	return ret;
+}
+
+/*
+ * One stateless IPv4 tuple through the reference's decision (CT_NEW, no
+ * CB_POLICY mark).  Glue, each step restated from the caller it follows:
+ *
+ *  flags bit0 = egress (from-container), bit1 = is_fragment.
+ *  cfg_gate: CONNTRACK's protocol gate — ct_lookup4 returns
+ *    DROP_CT_UNKNOWN_PROTO for anything but ICMP/TCP/UDP before any policy
+ *    (bpf/lib/conntrack.h:470-528; callers bpf_lxc.c:477-481, :895-897).
+ *  Egress (bpf_lxc.c:484-505): dstID = ipcache(daddr) sec_label if nonzero,
+ *    else CLUSTER_ID if (daddr & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE,
+ *    else WORLD_ID; verdict = policy_can_egress4(dstID, dport, proto).
+ *  Ingress (bpf_netdev.c:374-398 then bpf_lxc.c:893-926): src starts at
+ *    cfg_src_identity; if identity_is_reserved(src), ipcache(saddr) replaces
+ *    it when sec_label is nonzero and not CLUSTER_ID/HOST_ID.  The policy
+ *    label is secctx: src (FROM_HOST form, :403) or, with cfg_secctx_world,
+ *    derive_ipv4_sec_ctx() == WORLD_ID (non-FROM_HOST form, :278-290,371).
+ *    verdict = policy_can_access_ingress(label, dport, proto, is_fragment).
+ *
+ * Outputs: verdict, identity (label given to policy), stage (1 exact,
+ * 2 L3-only, 3 identity-wildcard L4, 0 miss, 4 protocol-gated), probes.
+ */
+int ref_classify_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t dport_be,
+		    uint8_t proto, uint8_t flags, uint32_t len, int ep,
+		    int cfg_gate, uint32_t cfg_src_identity, int cfg_secctx_world,
+		    uint32_t *identity_out, int *stage_out, int *nprobes_out,
+		    int *naddr_out)
+{
+	int egress = flags & 1, frag = (flags >> 1) & 1;
+	int ret, probes = 0, hit = 0;
+	uint32_t label, tun;
+
+	*naddr_out = 0;
+	if (cfg_gate && proto != IPPROTO_ICMP && proto != IPPROTO_TCP &&
+	    proto != IPPROTO_UDP) {
+		*identity_out = 0;
+		*stage_out = 4;
+		*nprobes_out = 0;
+		return DROP_CT_UNKNOWN_PROTO;
+	}
+	if (egress) {
+		uint32_t dst_id;
+		*naddr_out = 1;
+		if (ref_ipcache_lookup4(daddr_be, &label, &tun) && label)
+			dst_id = label;
+		else if ((daddr_be & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE)
+			dst_id = CLUSTER_ID;
+		else
+			dst_id = WORLD_ID;
+		ret = ref_policy_egress(ep, dst_id, dport_be, proto, len, &probes, &hit);
+		*identity_out = dst_id;
+	} else {
+		uint32_t src = cfg_src_identity, secctx;
+		if (identity_is_reserved(src)) {
+			*naddr_out = 1;
+			if (ref_ipcache_lookup4(saddr_be, &label, &tun) && label &&
+			    label != CLUSTER_ID && label != HOST_ID)
+				src = label;
+		}
+		secctx = cfg_secctx_world ? WORLD_ID : src;
+		ret = ref_policy_ingress(ep, secctx, dport_be, proto, frag, len,
+					 &probes, &hit);
+		*identity_out = secctx;
+	}
+	*nprobes_out = probes;
+	*stage_out = hit ? (frag && !egress ? 2 : hit) : 0;
+	return ret;
+}
+
+/* Constants the restatement must agree with (node_config.h, common.h). */
+int ref_constants(uint32_t *out, int n)
+{
+	uint32_t c[] = { HOST_ID, WORLD_ID, CLUSTER_ID, HEALTH_ID, INIT_ID,
+			 IPV4_CLUSTER_MASK, IPV4_CLUSTER_RANGE,
+			 (uint32_t)DROP_POLICY, (uint32_t)DROP_FRAG_NOSUPPORT,
+			 (uint32_t)DROP_CT_UNKNOWN_PROTO, CT_EGRESS, CT_INGRESS };
+	int k = (int)(sizeof(c) / sizeof(c[0]));
+	for (int i = 0; i < n && i < k; i++)
+		out[i] = c[i];
+	return k;
+}
