@@ -1,0 +1,112 @@
+"""ctypes prototypes of include/cgpu.h (the product's C ABI).
+
+Loading fails loudly: there is no Python or CPU fallback for any entry point.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcgpu.so")
+
+CGPU_ABI_VERSION = 1
+
+
+class CgpuConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32),
+        ("ipcache_max", C.c_uint32), ("policy_max_per_ep", C.c_uint32),
+        ("policy_max_total", C.c_uint32), ("max_endpoints", C.c_uint32),
+        ("cidr_dyn_max", C.c_uint32), ("cidr_fix_max", C.c_uint32),
+        ("endpoints_max", C.c_uint32),
+        ("host_id", C.c_uint32), ("world_id", C.c_uint32), ("cluster_id", C.c_uint32),
+        ("health_id", C.c_uint32),
+        ("ipv4_cluster_mask", C.c_uint32), ("ipv4_cluster_range", C.c_uint32),
+        ("ipv6_router_ip", C.c_uint8 * 16),
+        ("ct_proto_gate", C.c_uint8), ("ingress_secctx_world", C.c_uint8),
+        ("prefilter_fix4", C.c_uint8), ("prefilter_dyn4", C.c_uint8),
+        ("prefilter_fix6", C.c_uint8), ("prefilter_dyn6", C.c_uint8),
+        ("reserved0", C.c_uint8 * 2),
+        ("ingress_src_identity", C.c_uint32),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
+class TuplesV4(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")]
+
+
+vp, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
+
+# name -> (restype, argtypes)
+PROTOS = {
+    "cgpu_config_default": (None, [C.POINTER(CgpuConfig)]),
+    "cgpu_ctx_create": (i32, [C.POINTER(CgpuConfig), i32, C.POINTER(vp)]),
+    "cgpu_ctx_destroy": (None, [vp]),
+    "cgpu_last_error": (C.c_char_p, []),
+    "cgpu_version": (C.c_char_p, []),
+    "cgpu_ipcache_update": (i32, [vp, vp, vp, u64]),
+    "cgpu_ipcache_delete": (i32, [vp, vp]),
+    "cgpu_ipcache_lookup": (i32, [vp, vp, vp]),
+    "cgpu_ipcache_get_next_key": (i32, [vp, vp, vp]),
+    "cgpu_ipcache_count": (sz, [vp]),
+    "cgpu_policy_update": (i32, [vp, u32, vp, vp, u64]),
+    "cgpu_policy_delete": (i32, [vp, u32, vp]),
+    "cgpu_policy_lookup": (i32, [vp, u32, vp, vp]),
+    "cgpu_policy_get_next_key": (i32, [vp, u32, vp, vp]),
+    "cgpu_policy_flush": (i32, [vp, u32]),
+    "cgpu_policy_count": (sz, [vp, u32]),
+    "cgpu_cidr_update": (i32, [vp, i32, vp, u64]),
+    "cgpu_cidr_delete": (i32, [vp, i32, vp]),
+    "cgpu_cidr_lookup": (i32, [vp, i32, vp]),
+    "cgpu_cidr_get_next_key": (i32, [vp, i32, vp, vp]),
+    "cgpu_endpoint_update": (i32, [vp, vp, u64]),
+    "cgpu_endpoint_delete": (i32, [vp, vp]),
+    "cgpu_endpoint_lookup": (i32, [vp, vp]),
+    "cgpu_commit": (i32, [vp, C.POINTER(u64)]),
+    "cgpu_table_checksum": (i32, [vp, C.POINTER(u64)]),
+    "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
+    "cgpu_prefilter_v4": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+    "cgpu_prefilter_v6": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+    "cgpu_counter_delta_bytes": (sz, [vp]),
+    "cgpu_counter_bind": (i32, [vp, vp, sz]),
+    "cgpu_counter_fold": (i32, [vp, vp]),
+    "cgpu_metrics_read": (i32, [vp, vp]),
+    "cgpu_counters_reset": (i32, [vp]),
+}
+
+_lib = None
+
+
+class CgpuLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libcgpu.so (built by cilium_amd.build / __graft_entry__.build)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CgpuLibraryMissing(
+                f"{LIB_PATH} is missing: build it with `python -m cilium_amd.build` "
+                "(there is no CPU fallback for the classification path)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class CgpuError(OSError):
+    pass
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        msg = lib().cgpu_last_error().decode(errors="replace")
+        raise CgpuError(-rc, f"{what}: {os.strerror(-rc)} ({msg})")
+    return rc

@@ -1,0 +1,1287 @@
+/*
+ * host.cpp — C ABI (include/cgpu.h): host mirror of the reference maps,
+ * table compiler (mirror -> HBM snapshot), counters, batch launch wrappers.
+ *
+ * The host mirror is the authoritative copy of every table (SURVEY §5:
+ * "the host keeps the authoritative table mirror, so the device can be
+ * rebuilt from it at any time"); cgpu_commit() compiles it into the device
+ * layouts of tables.h and publishes the result as an immutable snapshot.
+ * Map semantics follow the kernel maps the reference programs:
+ *   BPF_MAP_TYPE_LPM_TRIE  kernel/bpf/lpm_trie.c (ipcache, prefilter dyn)
+ *   BPF_MAP_TYPE_HASH      kernel/bpf/hashtab.c  (policy, prefilter fix, lxc)
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/cgpu.h"
+#include "launch.h"
+#include "tables.h"
+
+#define CGPU_EXPORT extern "C" __attribute__((visibility("default")))
+
+static_assert(sizeof(cgpu_policy_key) == 8, "policy_key layout");
+static_assert(sizeof(cgpu_policy_entry) == 24, "policy_entry layout");
+static_assert(sizeof(cgpu_ipcache_key) == 24, "ipcache_key layout");
+static_assert(sizeof(cgpu_remote_endpoint_info) == 8, "remote_endpoint_info layout");
+static_assert(sizeof(cgpu_endpoint_key) == 20, "endpoint_key layout");
+static_assert(sizeof(pol_slot) == 16, "policy slot");
+static_assert(sizeof(set16_slot) == 32, "set16 slot");
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int err, const char *fmt, ...)
+{
+	char buf[512];
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(buf, sizeof(buf), fmt, ap);
+	va_end(ap);
+	g_last_error = buf;
+	return err;
+}
+
+#define HIP_OR_EIO(expr)                                                                  \
+	do {                                                                              \
+		hipError_t e_ = (expr);                                                   \
+		if (e_ != hipSuccess)                                                     \
+			return fail(-EIO, "%s: %s", #expr, hipGetErrorString(e_));        \
+	} while (0)
+
+/* ---------------- LPM canonical keys (kernel lpm_trie identity) ---------- */
+template <size_t N> struct LpmKey {
+	uint32_t plen;
+	std::array<uint8_t, N> data;
+	bool operator<(const LpmKey &o) const
+	{
+		if (data != o.data)
+			return data < o.data;
+		return plen < o.plen;
+	}
+	bool operator==(const LpmKey &o) const { return plen == o.plen && data == o.data; }
+};
+
+template <size_t N> LpmKey<N> lpm_canon(uint32_t plen, const uint8_t *data)
+{
+	LpmKey<N> k;
+	k.plen = plen;
+	for (size_t i = 0; i < N; i++) {
+		uint32_t bit0 = (uint32_t)i * 8;
+		uint8_t b = data[i];
+		if (plen <= bit0)
+			b = 0;
+		else if (plen < bit0 + 8)
+			b &= (uint8_t)(0xFFu << (8 - (plen - bit0)));
+		k.data[i] = b;
+	}
+	return k;
+}
+
+/* does the first `bits` bits of a and b agree (MSB first per byte) */
+static bool prefix_eq(const uint8_t *a, const uint8_t *b, uint32_t bits)
+{
+	uint32_t i = 0;
+	for (; i + 8 <= bits; i += 8)
+		if (a[i / 8] != b[i / 8])
+			return false;
+	if (i < bits) {
+		uint8_t m = (uint8_t)(0xFFu << (8 - (bits - i)));
+		if ((a[i / 8] ^ b[i / 8]) & m)
+			return false;
+	}
+	return true;
+}
+
+static uint32_t next_pow2(uint64_t x)
+{
+	uint32_t p = 1;
+	while (p < x)
+		p <<= 1;
+	return p;
+}
+
+static inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+struct IpcEntry {
+	cgpu_ipcache_key raw;
+	cgpu_remote_endpoint_info val;
+};
+struct PolEntry {
+	uint16_t proxy_port;
+	uint32_t slot;
+};
+struct SlotInit {
+	uint32_t slot;
+	uint64_t packets, bytes;
+};
+
+/* ---------------- DIR-24-8 builder ---------------- */
+struct Dir248 {
+	std::vector<uint32_t> tbl24, tbl8, vals;
+	void init() { tbl24.assign(DIR_TBL24_ENTRIES, 0u); tbl8.clear(); vals.clear(); }
+	uint32_t encode(uint32_t label)
+	{
+		if (label < (1u << DIR_TAG_SHIFT))
+			return DIR_TAG_DIRECT | label;
+		vals.push_back(label);
+		return DIR_TAG_INDIRECT | (uint32_t)(vals.size() - 1);
+	}
+	/* apply in ascending rank order; len in [0, 32], addr host order */
+	void apply(uint32_t addr, uint32_t len, uint32_t enc)
+	{
+		if (len <= 24) {
+			uint32_t cnt = 1u << (24 - len);
+			uint32_t base = len == 0 ? 0 : ((addr >> 8) & ~(cnt - 1));
+			std::fill(tbl24.begin() + base, tbl24.begin() + base + cnt, enc);
+			return;
+		}
+		uint32_t idx = addr >> 8, e = tbl24[idx];
+		if ((e & DIR_TAG_MASK) != DIR_TAG_GROUP) {
+			uint32_t g = (uint32_t)(tbl8.size() / 256);
+			tbl8.resize(tbl8.size() + 256, e);
+			tbl24[idx] = DIR_TAG_GROUP | g;
+		}
+		uint32_t g = tbl24[idx] & DIR_PAYLOAD_MASK;
+		uint32_t cnt = 1u << (32 - len);
+		uint32_t lo = (addr & 255u) & ~(cnt - 1);
+		std::fill(tbl8.begin() + g * 256 + lo, tbl8.begin() + g * 256 + lo + cnt, enc);
+	}
+};
+
+struct Rank4 {
+	uint32_t rank; /* < 32: static-part entry (acts as /0 below every IP prefix) */
+	uint32_t addr; /* host order */
+	uint32_t len;
+	uint32_t label;
+};
+
+/* ---------------- device arena ---------------- */
+struct Arena {
+	std::vector<std::pair<const void *, size_t>> parts; /* host src, bytes */
+	std::vector<size_t> offs;
+	size_t total = 0;
+	size_t add(const void *src, size_t bytes)
+	{
+		size_t off = (total + 255) & ~(size_t)255;
+		parts.push_back({src, bytes});
+		offs.push_back(off);
+		total = off + bytes;
+		return off;
+	}
+};
+
+} // namespace
+
+struct cgpu_ctx {
+	cgpu_config cfg;
+	int device = -1;
+	std::mutex mu;
+
+	/* ---- host mirror ---- */
+	std::map<LpmKey<20>, IpcEntry> ipc;
+	std::vector<std::map<uint64_t, PolEntry>> pol;
+	size_t pol_total = 0;
+	std::vector<uint32_t> free_slots;
+	uint32_t next_slot = 0;
+	std::vector<SlotInit> slot_inits;
+	std::map<LpmKey<4>, cgpu_cidr_key> dyn4;
+	std::map<LpmKey<16>, cgpu_cidr_key> dyn6;
+	std::set<std::array<uint8_t, 8>> fix4;
+	std::set<std::array<uint8_t, 20>> fix6;
+	std::set<std::array<uint8_t, 20>> lxc;
+
+	/* ---- device ---- */
+	void *arena = nullptr;
+	cgpu_snapshot snap{};
+	bool committed = false;
+	uint64_t epoch = 0;
+	uint64_t checksum = 0;
+	uint32_t n_ctr_slots = 0;
+	uint64_t *d_totals = nullptr; /* [2*slots + METRICS] */
+	uint64_t *d_delta_own = nullptr;
+	uint64_t *d_delta = nullptr;  /* own or bound */
+};
+
+/* ======================================================================= */
+/* config / context                                                          */
+/* ======================================================================= */
+CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
+{
+	memset(c, 0, sizeof(*c));
+	c->abi_version = CGPU_ABI_VERSION;
+	c->ipcache_max = 512000;      /* pkg/maps/ipcache/ipcache.go:36 */
+	c->policy_max_per_ep = 16384; /* pkg/maps/policymap/policymap.go:37 */
+	c->policy_max_total = 1u << 20;
+	c->max_endpoints = 65536;     /* ENDPOINTS_MAP_SIZE */
+	c->cidr_dyn_max = 1u << 20;   /* > maxLKeys: device capacity, configurable */
+	c->cidr_fix_max = 20u << 20;  /* maxHKeys (pkg/policy/prefilter.go:44) */
+	c->endpoints_max = 65536;
+	c->host_id = 1;
+	c->world_id = 2;
+	c->cluster_id = 3;
+	c->health_id = 4;
+	c->ipv4_cluster_mask = 0xff0000;  /* bpf/node_config.h:42 */
+	c->ipv4_cluster_range = 0x100000; /* bpf/node_config.h:43 */
+	c->ct_proto_gate = 1;             /* CONNTRACK (bpf/lxc_config.h:46) */
+	c->ingress_secctx_world = 0;
+	c->prefilter_fix4 = c->prefilter_dyn4 = 1; /* bpf/filter_config.h */
+	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
+	c->ingress_src_identity = 0;
+}
+
+CGPU_EXPORT const char *cgpu_last_error(void) { return g_last_error.c_str(); }
+CGPU_EXPORT const char *cgpu_version(void) { return "cgpu 0.1 gfx950 abi1"; }
+
+CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **out)
+{
+	if (!cfg || !out)
+		return fail(-EINVAL, "null argument");
+	if (cfg->abi_version != CGPU_ABI_VERSION)
+		return fail(-EINVAL, "abi_version %u != %u", cfg->abi_version, CGPU_ABI_VERSION);
+	if (!cfg->max_endpoints || !cfg->policy_max_total)
+		return fail(-EINVAL, "zero capacity");
+	cgpu_ctx *c = new cgpu_ctx();
+	c->cfg = *cfg;
+	c->pol.resize(cfg->max_endpoints);
+	c->n_ctr_slots = cfg->policy_max_total;
+	if (device >= 0) {
+		int ndev = 0;
+		if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+			delete c;
+			return fail(-ENODEV, "HIP device %d not present", device);
+		}
+		c->device = device;
+		size_t words = (size_t)2 * c->n_ctr_slots + CGPU_METRICS_WORDS;
+		if (hipSetDevice(device) != hipSuccess ||
+		    hipMalloc((void **)&c->d_totals, words * 8) != hipSuccess ||
+		    hipMalloc((void **)&c->d_delta_own, words * 8) != hipSuccess ||
+		    hipMemset(c->d_totals, 0, words * 8) != hipSuccess ||
+		    hipMemset(c->d_delta_own, 0, words * 8) != hipSuccess) {
+			(void)hipFree(c->d_totals);
+			(void)hipFree(c->d_delta_own);
+			delete c;
+			return fail(-EIO, "device counter allocation failed");
+		}
+		c->d_delta = c->d_delta_own;
+	}
+	*out = c;
+	return 0;
+}
+
+CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
+{
+	if (!c)
+		return;
+	if (c->device >= 0) {
+		(void)hipSetDevice(c->device);
+		(void)hipDeviceSynchronize();
+		(void)hipFree(c->arena);
+		(void)hipFree(c->d_totals);
+		(void)hipFree(c->d_delta_own);
+	}
+	delete c;
+}
+
+static int check_flags(uint64_t flags)
+{
+	return flags > CGPU_EXIST ? fail(-EINVAL, "bad update flags %llu", (unsigned long long)flags) : 0;
+}
+
+/* ======================================================================= */
+/* ipcache                                                                   */
+/* ======================================================================= */
+CGPU_EXPORT int cgpu_ipcache_update(cgpu_ctx *c, const cgpu_ipcache_key *key,
+				    const cgpu_remote_endpoint_info *val, uint64_t flags)
+{
+	if (!c || !key || !val)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	if (key->prefixlen > 160) /* data is 20 bytes: lpm_trie max_prefixlen */
+		return fail(-EINVAL, "ipcache prefixlen %u > 160", key->prefixlen);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto k = lpm_canon<20>(key->prefixlen, (const uint8_t *)key + 4);
+	auto it = c->ipc.find(k);
+	if (it == c->ipc.end()) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "ipcache key not present");
+		if (c->ipc.size() >= c->cfg.ipcache_max)
+			return fail(-ENOSPC, "ipcache full (%u)", c->cfg.ipcache_max);
+		c->ipc.emplace(k, IpcEntry{*key, *val});
+	} else {
+		if (flags == CGPU_NOEXIST)
+			return fail(-EEXIST, "ipcache key exists");
+		it->second = IpcEntry{*key, *val};
+	}
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_ipcache_delete(cgpu_ctx *c, const cgpu_ipcache_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (key->prefixlen > 160)
+		return fail(-EINVAL, "ipcache prefixlen %u > 160", key->prefixlen);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto n = c->ipc.erase(lpm_canon<20>(key->prefixlen, (const uint8_t *)key + 4));
+	return n ? 0 : fail(-ENOENT, "ipcache key not present");
+}
+
+/* bpf(2) lookup on an LPM trie = longest prefix match of the given key */
+CGPU_EXPORT int cgpu_ipcache_lookup(cgpu_ctx *c, const cgpu_ipcache_key *key,
+				    cgpu_remote_endpoint_info *out)
+{
+	if (!c || !key || !out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	const uint8_t *q = (const uint8_t *)key + 4;
+	uint32_t qlen = std::min<uint32_t>(key->prefixlen, 160);
+	/* probe each shorter-or-equal prefix length, longest first */
+	for (int64_t p = qlen; p >= 0; p--) {
+		auto it = c->ipc.find(lpm_canon<20>((uint32_t)p, q));
+		if (it != c->ipc.end()) {
+			*out = it->second.val;
+			return 0;
+		}
+	}
+	return -ENOENT;
+}
+
+CGPU_EXPORT int cgpu_ipcache_get_next_key(cgpu_ctx *c, const cgpu_ipcache_key *key,
+					  cgpu_ipcache_key *next)
+{
+	if (!c || !next)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = c->ipc.begin();
+	if (key) {
+		auto k = lpm_canon<20>(std::min<uint32_t>(key->prefixlen, 160), (const uint8_t *)key + 4);
+		it = c->ipc.upper_bound(k);
+	}
+	if (it == c->ipc.end())
+		return -ENOENT;
+	*next = it->second.raw;
+	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_ipcache_count(cgpu_ctx *c)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->ipc.size();
+}
+
+/* ======================================================================= */
+/* policy                                                                    */
+/* ======================================================================= */
+static inline uint64_t pol_key64(const cgpu_policy_key *k)
+{
+	uint64_t x;
+	memcpy(&x, k, 8);
+	return x;
+}
+
+CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+				   const cgpu_policy_entry *e, uint64_t flags)
+{
+	if (!c || !key || !e)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	if (ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "endpoint %u >= max_endpoints %u", ep, c->cfg.max_endpoints);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	uint64_t k = pol_key64(key);
+	auto it = m.find(k);
+	uint32_t slot;
+	if (it == m.end()) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "policy key not present");
+		if (m.size() >= c->cfg.policy_max_per_ep)
+			return fail(-E2BIG, "policy map of ep %u full (%u)", ep, c->cfg.policy_max_per_ep);
+		if (c->free_slots.empty() && c->next_slot >= c->n_ctr_slots)
+			return fail(-E2BIG, "policy device slots exhausted (%u)", c->n_ctr_slots);
+		if (!c->free_slots.empty()) {
+			slot = c->free_slots.back();
+			c->free_slots.pop_back();
+		} else {
+			slot = c->next_slot++;
+		}
+		m.emplace(k, PolEntry{e->proxy_port, slot});
+		c->pol_total++;
+	} else {
+		if (flags == CGPU_NOEXIST)
+			return fail(-EEXIST, "policy key exists");
+		it->second.proxy_port = e->proxy_port;
+		slot = it->second.slot;
+	}
+	/* kernel htab replaces the whole value: counters restart from it */
+	c->slot_inits.push_back(SlotInit{slot, e->packets, e->bytes});
+	return 0;
+}
+
+static void pol_erase(cgpu_ctx *c, std::map<uint64_t, PolEntry> &m,
+		      std::map<uint64_t, PolEntry>::iterator it)
+{
+	c->free_slots.push_back(it->second.slot);
+	m.erase(it);
+	c->pol_total--;
+}
+
+CGPU_EXPORT int cgpu_policy_delete(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "endpoint %u out of range", ep);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	auto it = m.find(pol_key64(key));
+	if (it == m.end())
+		return fail(-ENOENT, "policy key not present");
+	pol_erase(c, m, it);
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_flush(cgpu_ctx *c, uint32_t ep)
+{
+	if (!c || ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "bad argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	while (!m.empty())
+		pol_erase(c, m, m.begin());
+	return 0;
+}
+
+static int read_counter_words(cgpu_ctx *c, size_t word, size_t nwords, uint64_t *out)
+{
+	/* totals + delta; pending launches complete first */
+	std::vector<uint64_t> a(nwords), b(nwords);
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipDeviceSynchronize());
+	HIP_OR_EIO(hipMemcpy(a.data(), c->d_totals + word, nwords * 8, hipMemcpyDeviceToHost));
+	HIP_OR_EIO(hipMemcpy(b.data(), c->d_delta + word, nwords * 8, hipMemcpyDeviceToHost));
+	for (size_t i = 0; i < nwords; i++)
+		out[i] = a[i] + b[i];
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_lookup(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+				   cgpu_policy_entry *out)
+{
+	if (!c || !key || !out)
+		return fail(-EINVAL, "null argument");
+	if (ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "endpoint %u out of range", ep);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	auto it = m.find(pol_key64(key));
+	if (it == m.end())
+		return -ENOENT;
+	memset(out, 0, sizeof(*out));
+	out->proxy_port = it->second.proxy_port;
+	/* the most recent update's counter values until the next commit */
+	uint64_t pk = 0, by = 0;
+	bool pending = false;
+	for (auto s = c->slot_inits.rbegin(); s != c->slot_inits.rend(); ++s)
+		if (s->slot == it->second.slot) {
+			pk = s->packets;
+			by = s->bytes;
+			pending = true;
+			break;
+		}
+	if (!pending && c->device >= 0 && c->committed) {
+		uint64_t w[2];
+		if (int r = read_counter_words(c, (size_t)2 * it->second.slot, 2, w))
+			return r;
+		pk = w[0];
+		by = w[1];
+	}
+	out->packets = pk;
+	out->bytes = by;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_get_next_key(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+					 cgpu_policy_key *next)
+{
+	if (!c || !next || ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "bad argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	auto it = key ? m.upper_bound(pol_key64(key)) : m.begin();
+	if (it == m.end())
+		return -ENOENT;
+	memcpy(next, &it->first, 8);
+	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_policy_count(cgpu_ctx *c, uint32_t ep)
+{
+	if (!c || ep >= c->cfg.max_endpoints)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->pol[ep].size();
+}
+
+/* ======================================================================= */
+/* prefilter CIDR maps + endpoint map                                        */
+/* ======================================================================= */
+CGPU_EXPORT int cgpu_cidr_update(cgpu_ctx *c, int which, const cgpu_cidr_key *key, uint64_t flags)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	bool exists;
+	switch (which) {
+	case CGPU_CIDR_V4_DYN:
+	case CGPU_CIDR_V6_DYN: {
+		uint32_t maxp = which == CGPU_CIDR_V4_DYN ? 32 : 128;
+		if (key->prefixlen > maxp)
+			return fail(-EINVAL, "prefixlen %u > %u", key->prefixlen, maxp);
+		if (which == CGPU_CIDR_V4_DYN) {
+			auto k = lpm_canon<4>(key->prefixlen, key->addr);
+			exists = c->dyn4.count(k);
+			if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+			if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+			if (!exists && c->dyn4.size() >= c->cfg.cidr_dyn_max) return fail(-ENOSPC, "dyn4 full");
+			c->dyn4[k] = *key;
+		} else {
+			auto k = lpm_canon<16>(key->prefixlen, key->addr);
+			exists = c->dyn6.count(k);
+			if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+			if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+			if (!exists && c->dyn6.size() >= c->cfg.cidr_dyn_max) return fail(-ENOSPC, "dyn6 full");
+			c->dyn6[k] = *key;
+		}
+		return 0;
+	}
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k;
+		memcpy(k.data(), key, 8);
+		exists = c->fix4.count(k);
+		if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+		if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+		if (!exists && c->fix4.size() >= c->cfg.cidr_fix_max) return fail(-E2BIG, "fix4 full");
+		c->fix4.insert(k);
+		return 0;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k;
+		memcpy(k.data(), key, 20);
+		exists = c->fix6.count(k);
+		if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+		if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+		if (!exists && c->fix6.size() >= c->cfg.cidr_fix_max) return fail(-E2BIG, "fix6 full");
+		c->fix6.insert(k);
+		return 0;
+	}
+	}
+	return fail(-EINVAL, "bad cidr map %d", which);
+}
+
+CGPU_EXPORT int cgpu_cidr_delete(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	size_t n = 0;
+	switch (which) {
+	case CGPU_CIDR_V4_DYN:
+		if (key->prefixlen > 32) return fail(-EINVAL, "prefixlen");
+		n = c->dyn4.erase(lpm_canon<4>(key->prefixlen, key->addr));
+		break;
+	case CGPU_CIDR_V6_DYN:
+		if (key->prefixlen > 128) return fail(-EINVAL, "prefixlen");
+		n = c->dyn6.erase(lpm_canon<16>(key->prefixlen, key->addr));
+		break;
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k;
+		memcpy(k.data(), key, 8);
+		n = c->fix4.erase(k);
+		break;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k;
+		memcpy(k.data(), key, 20);
+		n = c->fix6.erase(k);
+		break;
+	}
+	default:
+		return fail(-EINVAL, "bad cidr map %d", which);
+	}
+	return n ? 0 : -ENOENT;
+}
+
+CGPU_EXPORT int cgpu_cidr_lookup(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	switch (which) {
+	case CGPU_CIDR_V4_DYN:
+		for (int64_t p = std::min<uint32_t>(key->prefixlen, 32); p >= 0; p--)
+			if (c->dyn4.count(lpm_canon<4>((uint32_t)p, key->addr)))
+				return 0;
+		return -ENOENT;
+	case CGPU_CIDR_V6_DYN:
+		for (int64_t p = std::min<uint32_t>(key->prefixlen, 128); p >= 0; p--)
+			if (c->dyn6.count(lpm_canon<16>((uint32_t)p, key->addr)))
+				return 0;
+		return -ENOENT;
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k;
+		memcpy(k.data(), key, 8);
+		return c->fix4.count(k) ? 0 : -ENOENT;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k;
+		memcpy(k.data(), key, 20);
+		return c->fix6.count(k) ? 0 : -ENOENT;
+	}
+	}
+	return fail(-EINVAL, "bad cidr map %d", which);
+}
+
+CGPU_EXPORT int cgpu_cidr_get_next_key(cgpu_ctx *c, int which, const cgpu_cidr_key *key,
+				       cgpu_cidr_key *next)
+{
+	if (!c || !next)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	memset(next, 0, sizeof(*next));
+	switch (which) {
+	case CGPU_CIDR_V4_DYN: {
+		auto it = key ? c->dyn4.upper_bound(lpm_canon<4>(std::min<uint32_t>(key->prefixlen, 32), key->addr))
+			      : c->dyn4.begin();
+		if (it == c->dyn4.end()) return -ENOENT;
+		*next = it->second;
+		return 0;
+	}
+	case CGPU_CIDR_V6_DYN: {
+		auto it = key ? c->dyn6.upper_bound(lpm_canon<16>(std::min<uint32_t>(key->prefixlen, 128), key->addr))
+			      : c->dyn6.begin();
+		if (it == c->dyn6.end()) return -ENOENT;
+		*next = it->second;
+		return 0;
+	}
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k{};
+		if (key) memcpy(k.data(), key, 8);
+		auto it = key ? c->fix4.upper_bound(k) : c->fix4.begin();
+		if (it == c->fix4.end()) return -ENOENT;
+		memcpy(next, it->data(), 8);
+		return 0;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k{};
+		if (key) memcpy(k.data(), key, 20);
+		auto it = key ? c->fix6.upper_bound(k) : c->fix6.begin();
+		if (it == c->fix6.end()) return -ENOENT;
+		memcpy(next, it->data(), 20);
+		return 0;
+	}
+	}
+	return fail(-EINVAL, "bad cidr map %d", which);
+}
+
+CGPU_EXPORT int cgpu_endpoint_update(cgpu_ctx *c, const cgpu_endpoint_key *key, uint64_t flags)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::array<uint8_t, 20> k;
+	memcpy(k.data(), key, 20);
+	std::lock_guard<std::mutex> g(c->mu);
+	bool exists = c->lxc.count(k);
+	if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+	if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+	if (!exists && c->lxc.size() >= c->cfg.endpoints_max) return fail(-E2BIG, "endpoint map full");
+	c->lxc.insert(k);
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_endpoint_delete(cgpu_ctx *c, const cgpu_endpoint_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::array<uint8_t, 20> k;
+	memcpy(k.data(), key, 20);
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lxc.erase(k) ? 0 : -ENOENT;
+}
+
+CGPU_EXPORT int cgpu_endpoint_lookup(cgpu_ctx *c, const cgpu_endpoint_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::array<uint8_t, 20> k;
+	memcpy(k.data(), key, 20);
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lxc.count(k) ? 0 : -ENOENT;
+}
+
+/* ======================================================================= */
+/* compiler: mirror -> device layouts                                        */
+/* ======================================================================= */
+namespace {
+
+uint64_t fnv(uint64_t h, const void *p, size_t n)
+{
+	const uint8_t *b = (const uint8_t *)p;
+	for (size_t i = 0; i < n; i++)
+		h = (h ^ b[i]) * 0x100000001b3ull;
+	return h;
+}
+
+/* ipcache -> DIR-24-8 for IPv4 lookups (ipcache_lookup4, eps.h:70-80):
+ * a lookup key is {prefixlen 64, pad 0, family 1, ip4, zero pad words}.
+ * An entry is a candidate iff its prefixlen <= 64 and its first prefixlen
+ * bits equal the lookup key's.  Entries with prefixlen < 32 end inside the
+ * static {pad, family} part: they match every IPv4 address and rank below
+ * any entry that reaches the address bits. */
+void build_ipc4(const cgpu_ctx *c, Dir248 &d)
+{
+	static const uint8_t static_v4[4] = {0, 0, 0, 1};
+	std::vector<Rank4> cand;
+	for (auto &kv : c->ipc) {
+		const IpcEntry &e = kv.second;
+		uint32_t p = e.raw.prefixlen;
+		const uint8_t *data = (const uint8_t *)&e.raw + 4;
+		if (p > 64)
+			continue;
+		if (!prefix_eq(data, static_v4, std::min<uint32_t>(p, 32)))
+			continue;
+		Rank4 r;
+		r.label = e.val.sec_label;
+		if (p < 32) {
+			r.rank = p;
+			r.addr = 0;
+			r.len = 0;
+		} else {
+			r.rank = p;
+			r.len = p - 32;
+			uint32_t a;
+			memcpy(&a, data + 4, 4);
+			r.addr = bswap32(a);
+		}
+		cand.push_back(r);
+	}
+	std::stable_sort(cand.begin(), cand.end(),
+			 [](const Rank4 &a, const Rank4 &b) { return a.rank < b.rank; });
+	d.init();
+	for (auto &r : cand)
+		d.apply(r.addr, r.len, d.encode(r.label));
+}
+
+/* prefilter v4 any-match: dyn4 (if CIDR4_LPM_PREFILTER) + fix4 keys with
+ * prefixlen 32 (a hash key with another prefixlen never equals the lookup
+ * key {32, saddr}); both lead to XDP_DROP (bpf_xdp.c:107-117). */
+bool build_pf4(const cgpu_ctx *c, Dir248 &d)
+{
+	std::vector<Rank4> cand;
+	if (!c->cfg.prefilter_fix4)
+		return false;
+	if (c->cfg.prefilter_dyn4)
+		for (auto &kv : c->dyn4) {
+			uint32_t a;
+			memcpy(&a, kv.first.data.data(), 4);
+			cand.push_back(Rank4{kv.first.plen, bswap32(a), kv.first.plen, 1});
+		}
+	for (auto &k : c->fix4) {
+		uint32_t plen, a;
+		memcpy(&plen, k.data(), 4);
+		if (plen != 32)
+			continue;
+		memcpy(&a, k.data() + 4, 4);
+		cand.push_back(Rank4{32, bswap32(a), 32, 1});
+	}
+	if (cand.empty())
+		return false;
+	std::stable_sort(cand.begin(), cand.end(),
+			 [](const Rank4 &a, const Rank4 &b) { return a.rank < b.rank; });
+	d.init();
+	for (auto &r : cand)
+		d.apply(r.addr, r.len, DIR_TAG_DIRECT | 1u);
+	return true;
+}
+
+struct PolBuild {
+	std::vector<pol_slot> slots;
+	uint32_t mask = 0, max_probe = 1;
+};
+
+void build_pol(const cgpu_ctx *c, PolBuild &b)
+{
+	uint32_t nb = next_pow2(std::max<uint64_t>(64, (c->pol_total + 1) / 2 + 1));
+	b.slots.assign((size_t)nb * POL_SLOTS_PER_BUCKET, pol_slot{0, 0, 0, POL_EMPTY});
+	b.mask = nb - 1;
+	b.max_probe = 1;
+	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+		for (auto &kv : c->pol[ep]) {
+			uint32_t lo = (uint32_t)kv.first, hi = (uint32_t)(kv.first >> 32);
+			uint32_t bk = pol_hash(lo, hi, ep) & b.mask, probe = 1;
+			for (;;) {
+				pol_slot *s = &b.slots[(size_t)bk * POL_SLOTS_PER_BUCKET];
+				int k = 0;
+				while (k < (int)POL_SLOTS_PER_BUCKET && s[k].ctr != POL_EMPTY)
+					k++;
+				if (k < (int)POL_SLOTS_PER_BUCKET) {
+					s[k] = pol_slot{lo, hi, ep | (uint32_t)kv.second.proxy_port << 16,
+							kv.second.slot};
+					break;
+				}
+				bk = (bk + 1) & b.mask;
+				probe++;
+			}
+			b.max_probe = std::max(b.max_probe, probe);
+		}
+}
+
+struct Set4Build {
+	std::vector<set4_slot> slots;
+	uint32_t mask = 0, max_probe = 1;
+};
+struct Set16Build {
+	std::vector<set16_slot> slots;
+	uint32_t mask = 0, max_probe = 1;
+};
+
+void build_set4(const std::vector<uint32_t> &keys, Set4Build &b)
+{
+	uint32_t nb = next_pow2(std::max<uint64_t>(8, keys.size() / 4 + 1));
+	b.slots.assign((size_t)nb * 8, set4_slot{0, 0});
+	b.mask = nb - 1;
+	b.max_probe = 1;
+	for (uint32_t a : keys) {
+		uint32_t bk = mix32(a, 0x5e7) & b.mask, probe = 1;
+		for (;;) {
+			set4_slot *s = &b.slots[(size_t)bk * 8];
+			int k = 0;
+			while (k < 8 && s[k].used)
+				k++;
+			if (k < 8) {
+				s[k] = set4_slot{a, 1};
+				break;
+			}
+			bk = (bk + 1) & b.mask;
+			probe++;
+		}
+		b.max_probe = std::max(b.max_probe, probe);
+	}
+}
+
+/* keys: 4 u32 words + tag (tag goes to `used` bits 8..15; hashed as salt) */
+void build_set16(const std::vector<std::array<uint32_t, 5>> &keys, Set16Build &b)
+{
+	uint32_t nb = next_pow2(std::max<uint64_t>(8, keys.size() + 1));
+	b.slots.assign((size_t)nb * 2, set16_slot{});
+	b.mask = nb - 1;
+	b.max_probe = 1;
+	for (auto &k : keys) {
+		uint32_t bk = hash16(k[0], k[1], k[2], k[3], k[4]) & b.mask, probe = 1;
+		for (;;) {
+			set16_slot *s = &b.slots[(size_t)bk * 2];
+			int j = 0;
+			while (j < 2 && (s[j].used & 1))
+				j++;
+			if (j < 2) {
+				set16_slot v{};
+				memcpy(v.a, k.data(), 16);
+				v.used = 1u | (k[4] << 8);
+				s[j] = v;
+				break;
+			}
+			bk = (bk + 1) & b.mask;
+			probe++;
+		}
+		b.max_probe = std::max(b.max_probe, probe);
+	}
+}
+
+/* IPv6 address words as stored (network byte order in memory, u32 LE view) */
+void mask_v6(const uint8_t *addr, uint32_t len, uint32_t out[4])
+{
+	uint8_t m[16];
+	for (int i = 0; i < 16; i++) {
+		uint32_t bit0 = (uint32_t)i * 8;
+		uint8_t b = addr[i];
+		if (len <= bit0)
+			b = 0;
+		else if (len < bit0 + 8)
+			b &= (uint8_t)(0xFFu << (8 - (len - bit0)));
+		m[i] = b;
+	}
+	memcpy(out, m, 16);
+}
+
+struct Pf6Build {
+	std::vector<uint16_t> root;
+	std::vector<uint32_t> masks;
+	Set16Build set;
+	bool any = false;
+};
+
+/* prefilter v6 any-match set (bpf_xdp.c:132-156): dyn6 (if
+ * CIDR6_LPM_PREFILTER) + fix6 keys with prefixlen 128. */
+void build_pf6(const cgpu_ctx *c, Pf6Build &b)
+{
+	b.any = false;
+	if (!c->cfg.prefilter_fix6)
+		return;
+	std::set<std::pair<uint32_t, std::array<uint8_t, 16>>> pfx; /* (len, masked) */
+	if (c->cfg.prefilter_dyn6)
+		for (auto &kv : c->dyn6)
+			pfx.insert({kv.first.plen, kv.first.data});
+	for (auto &k : c->fix6) {
+		uint32_t plen;
+		memcpy(&plen, k.data(), 4);
+		if (plen != 128)
+			continue;
+		std::array<uint8_t, 16> a;
+		memcpy(a.data(), k.data() + 4, 16);
+		pfx.insert({128, a});
+	}
+	if (pfx.empty())
+		return;
+	b.any = true;
+	std::vector<std::array<uint32_t, 4>> rootmask(65536, std::array<uint32_t, 4>{0, 0, 0, 0});
+	std::vector<uint8_t> covered(65536, 0);
+	std::vector<std::array<uint32_t, 5>> keys;
+	for (auto &p : pfx) {
+		uint32_t len = p.first;
+		uint32_t top = (uint32_t)p.second[0] << 8 | p.second[1];
+		if (len <= 16) {
+			uint32_t cnt = 1u << (16 - len);
+			uint32_t base = len == 0 ? 0 : (top & ~(cnt - 1));
+			for (uint32_t r = base; r < base + cnt; r++)
+				covered[r] = 1;
+			continue;
+		}
+		uint32_t bit = len - 17;
+		rootmask[top][bit / 32] |= 1u << (bit % 32);
+		std::array<uint32_t, 5> k;
+		uint32_t w[4];
+		mask_v6(p.second.data(), len, w);
+		memcpy(k.data(), w, 16);
+		k[4] = len;
+		keys.push_back(k);
+	}
+	std::map<std::array<uint32_t, 4>, uint16_t> ids;
+	b.masks.assign(4, 0); /* row 0: nothing */
+	ids[{0, 0, 0, 0}] = 0;
+	b.root.assign(65536, 0);
+	for (uint32_t r = 0; r < 65536; r++) {
+		if (covered[r]) {
+			b.root[r] = V6_ROOT_COVERED;
+			continue;
+		}
+		auto it = ids.find(rootmask[r]);
+		if (it == ids.end()) {
+			uint16_t id = (uint16_t)(b.masks.size() / 4);
+			ids[rootmask[r]] = id;
+			b.masks.insert(b.masks.end(), rootmask[r].begin(), rootmask[r].end());
+			b.root[r] = id;
+		} else {
+			b.root[r] = it->second;
+		}
+	}
+	build_set16(keys, b.set);
+}
+
+} // namespace
+
+CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
+{
+	if (!c)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+
+	Dir248 ipc4, pf4;
+	PolBuild pol;
+	Set4Build ep4;
+	Set16Build ep6;
+	Pf6Build pf6;
+	build_ipc4(c, ipc4);
+	bool have_pf4 = build_pf4(c, pf4);
+	build_pol(c, pol);
+	std::vector<uint32_t> e4;
+	std::vector<std::array<uint32_t, 5>> e6;
+	for (auto &k : c->lxc) {
+		const cgpu_endpoint_key *ek = (const cgpu_endpoint_key *)k.data();
+		if (ek->pad4 || ek->pad5)
+			continue; /* lookup keys have zero padding: never matches */
+		uint32_t w[4];
+		memcpy(w, ek->ip, 16);
+		if (ek->family == 1 && !w[1] && !w[2] && !w[3])
+			e4.push_back(w[0]);
+		else if (ek->family == 2)
+			e6.push_back({w[0], w[1], w[2], w[3], 0});
+	}
+	build_set4(e4, ep4);
+	build_set16(e6, ep6);
+	build_pf6(c, pf6);
+
+	Arena ar;
+	size_t o_t24 = ar.add(ipc4.tbl24.data(), ipc4.tbl24.size() * 4);
+	size_t o_t8 = ar.add(ipc4.tbl8.data(), ipc4.tbl8.size() * 4);
+	size_t o_v = ar.add(ipc4.vals.data(), ipc4.vals.size() * 4);
+	size_t o_pol = ar.add(pol.slots.data(), pol.slots.size() * sizeof(pol_slot));
+	size_t o_p24 = 0, o_p8 = 0;
+	if (have_pf4) {
+		o_p24 = ar.add(pf4.tbl24.data(), pf4.tbl24.size() * 4);
+		o_p8 = ar.add(pf4.tbl8.data(), pf4.tbl8.size() * 4);
+	}
+	size_t o_e4 = ar.add(ep4.slots.data(), ep4.slots.size() * sizeof(set4_slot));
+	size_t o_e6 = ar.add(ep6.slots.data(), ep6.slots.size() * sizeof(set16_slot));
+	size_t o_r6 = 0, o_m6 = 0, o_s6 = 0;
+	if (pf6.any) {
+		o_r6 = ar.add(pf6.root.data(), pf6.root.size() * 2);
+		o_m6 = ar.add(pf6.masks.data(), pf6.masks.size() * 4);
+		o_s6 = ar.add(pf6.set.slots.data(), pf6.set.slots.size() * sizeof(set16_slot));
+	}
+	std::vector<uint32_t> init_slot;
+	std::vector<uint64_t> init_pk, init_by;
+	for (auto &s : c->slot_inits) {
+		init_slot.push_back(s.slot);
+		init_pk.push_back(s.packets);
+		init_by.push_back(s.bytes);
+	}
+	size_t o_is = ar.add(init_slot.data(), init_slot.size() * 4);
+	size_t o_ip = ar.add(init_pk.data(), init_pk.size() * 8);
+	size_t o_ib = ar.add(init_by.data(), init_by.size() * 8);
+
+	HIP_OR_EIO(hipSetDevice(c->device));
+	/* launches on the previous snapshot must drain before it is freed */
+	HIP_OR_EIO(hipDeviceSynchronize());
+	char *arena = nullptr;
+	HIP_OR_EIO(hipMalloc((void **)&arena, ar.total ? ar.total : 256));
+	for (size_t i = 0; i < ar.parts.size(); i++)
+		if (ar.parts[i].second)
+			HIP_OR_EIO(hipMemcpy(arena + ar.offs[i], ar.parts[i].first, ar.parts[i].second,
+					     hipMemcpyHostToDevice));
+	if (!init_slot.empty()) {
+		HIP_OR_EIO(launch_slot_init(c->d_totals, c->d_delta, (const uint32_t *)(arena + o_is),
+					    (const uint64_t *)(arena + o_ip),
+					    (const uint64_t *)(arena + o_ib), (uint32_t)init_slot.size(),
+					    nullptr));
+	}
+	HIP_OR_EIO(hipDeviceSynchronize());
+	(void)hipFree(c->arena);
+	c->arena = arena;
+	c->slot_inits.clear();
+
+	cgpu_snapshot s{};
+	s.ipc4 = dir248{(const uint32_t *)(arena + o_t24), (const uint32_t *)(arena + o_t8),
+			(const uint32_t *)(arena + o_v), (uint32_t)(ipc4.tbl8.size() / 256),
+			(uint32_t)ipc4.vals.size()};
+	s.pol = pol_table{(const pol_slot *)(arena + o_pol), pol.mask, pol.max_probe};
+	if (have_pf4)
+		s.pf4 = dir248{(const uint32_t *)(arena + o_p24), (const uint32_t *)(arena + o_p8),
+			       nullptr, (uint32_t)(pf4.tbl8.size() / 256), 0};
+	s.ep4 = addr_set4{(const set4_slot *)(arena + o_e4), ep4.mask, ep4.max_probe};
+	s.ep6 = addr_set16{(const set16_slot *)(arena + o_e6), ep6.mask, ep6.max_probe};
+	if (pf6.any)
+		s.pf6 = v6_anyset{(const uint16_t *)(arena + o_r6), (const uint32_t *)(arena + o_m6),
+				  addr_set16{(const set16_slot *)(arena + o_s6), pf6.set.mask,
+					     pf6.set.max_probe},
+				  (uint32_t)(pf6.masks.size() / 4)};
+	s.pf4_enabled = c->cfg.prefilter_fix4;
+	s.pf6_enabled = c->cfg.prefilter_fix6;
+	s.world_id = c->cfg.world_id;
+	s.cluster_id = c->cfg.cluster_id;
+	s.host_id = c->cfg.host_id;
+	s.health_id = c->cfg.health_id;
+	s.ipv4_cluster_mask = c->cfg.ipv4_cluster_mask;
+	s.ipv4_cluster_range = c->cfg.ipv4_cluster_range;
+	s.ct_proto_gate = c->cfg.ct_proto_gate;
+	s.ingress_secctx_world = c->cfg.ingress_secctx_world;
+	s.ingress_src_identity = c->cfg.ingress_src_identity;
+	s.n_ctr_slots = c->n_ctr_slots;
+	s.epoch = ++c->epoch;
+	c->snap = s;
+	c->committed = true;
+
+	/* content checksum: order-independent over the mirror */
+	uint64_t sum = 0;
+	for (auto &kv : c->ipc)
+		sum += fnv(fnv(1469598103934665603ull, &kv.first, sizeof(kv.first)), &kv.second.val, 8);
+	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+		for (auto &kv : c->pol[ep]) {
+			uint64_t h = fnv(1469598103934665603ull ^ ep, &kv.first, 8);
+			sum += fnv(h, &kv.second.proxy_port, 2) ^ ((uint64_t)kv.second.slot << 1);
+		}
+	for (auto &kv : c->dyn4) sum += fnv(7, &kv.first, sizeof(kv.first));
+	for (auto &kv : c->dyn6) sum += fnv(11, &kv.first, sizeof(kv.first));
+	for (auto &k : c->fix4) sum += fnv(13, k.data(), k.size());
+	for (auto &k : c->fix6) sum += fnv(17, k.data(), k.size());
+	for (auto &k : c->lxc) sum += fnv(19, k.data(), k.size());
+	c->checksum = sum;
+	if (epoch_out)
+		*epoch_out = s.epoch;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
+{
+	if (!c || !sum)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (!c->committed)
+		return fail(-ENOENT, "nothing committed");
+	*sum = c->checksum;
+	return 0;
+}
+
+/* ======================================================================= */
+/* batch entry points                                                        */
+/* ======================================================================= */
+static int snapshot_for_launch(cgpu_ctx *c, cgpu_snapshot &s, uint64_t *&delta)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device (host-only); no CPU classification path");
+	if (!c->committed)
+		return fail(-ENOENT, "no committed snapshot (call cgpu_commit)");
+	s = c->snap;
+	delta = c->d_delta;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
+				 uint32_t *identity, uint8_t *stage, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
+			 !t->ep || !verdict || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (!n)
+		return 0;
+	classify_v4_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
+			   verdict, identity, stage, delta, (uint64_t)n};
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_classify_v4(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_prefilter_v4(cgpu_ctx *c, const uint32_t *saddr, const uint32_t *daddr,
+				  const uint8_t *flags, size_t n, uint8_t *verdict, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (n && (!saddr || !daddr || !flags || !verdict))
+		return fail(-EINVAL, "null column");
+	if (!n)
+		return 0;
+	prefilter_args a{saddr, daddr, nullptr, nullptr, flags, verdict, (uint64_t)n};
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_prefilter_v4(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_prefilter_v6(cgpu_ctx *c, const uint8_t *saddr, const uint8_t *daddr,
+				  const uint8_t *flags, size_t n, uint8_t *verdict, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (n && (!saddr || !daddr || !flags || !verdict))
+		return fail(-EINVAL, "null column");
+	if (!n)
+		return 0;
+	prefilter_args a{nullptr, nullptr, saddr, daddr, flags, verdict, (uint64_t)n};
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_prefilter_v6(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+/* ======================================================================= */
+/* counters                                                                  */
+/* ======================================================================= */
+CGPU_EXPORT size_t cgpu_counter_delta_bytes(cgpu_ctx *c)
+{
+	return c ? ((size_t)2 * c->n_ctr_slots + CGPU_METRICS_WORDS) * 8 : 0;
+}
+
+CGPU_EXPORT int cgpu_counter_bind(cgpu_ctx *c, void *buf, size_t bytes)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (!buf) {
+		c->d_delta = c->d_delta_own;
+		return 0;
+	}
+	if (bytes < cgpu_counter_delta_bytes(c))
+		return fail(-EINVAL, "counter buffer %zu < %zu bytes", bytes, cgpu_counter_delta_bytes(c));
+	if ((uintptr_t)buf & 7)
+		return fail(-EINVAL, "counter buffer not 8-byte aligned");
+	c->d_delta = (uint64_t *)buf;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_counter_fold(cgpu_ctx *c, void *stream)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_fold(c->d_totals, c->d_delta,
+			       (uint64_t)2 * c->n_ctr_slots + CGPU_METRICS_WORDS, (hipStream_t)stream));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_metrics_read(cgpu_ctx *c, uint64_t *out)
+{
+	if (!c || !out)
+		return fail(-EINVAL, "null argument");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	std::lock_guard<std::mutex> g(c->mu);
+	return read_counter_words(c, (size_t)2 * c->n_ctr_slots, CGPU_METRICS_WORDS, out);
+}
+
+CGPU_EXPORT int cgpu_counters_reset(cgpu_ctx *c)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (c->device < 0)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	size_t bytes = cgpu_counter_delta_bytes(c);
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipDeviceSynchronize());
+	HIP_OR_EIO(hipMemset(c->d_totals, 0, bytes));
+	HIP_OR_EIO(hipMemset(c->d_delta, 0, bytes));
+	HIP_OR_EIO(hipDeviceSynchronize());
+	return 0;
+}

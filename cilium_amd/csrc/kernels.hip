@@ -1,0 +1,369 @@
+/*
+ * kernels.hip — gfx950 kernels of the classification path.
+ *
+ * One lane per tuple, grid-stride over SoA columns (coalesced 1/2/4-byte
+ * loads of every column, both addresses loaded and selected per lane).
+ * The path is memory-latency bound (dependent gathers into HBM/L2-resident
+ * tables, no arithmetic to speak of), so there is no MFMA: the levers are
+ * waves in flight, independent loads issued together, and 64-byte-aligned
+ * table buckets (one cache-line sector per probe).  See DESIGN.md §4.
+ */
+#include "launch.h"
+
+#define DROP_POLICY (-133)           /* bpf/lib/common.h:240 */
+#define DROP_CT_UNKNOWN_PROTO (-137) /* bpf/lib/common.h:244 */
+#define XDP_DROP 1
+#define XDP_PASS 2
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+/* DIR-24-8 longest-prefix lookup of a network-order address.
+ * Returns the entry (0 = no match); *label receives sec_label. */
+__device__ __forceinline__ uint32_t dir_lookup(const dir248 &d, uint32_t addr_be, uint32_t *label)
+{
+	uint32_t h = bswap32(addr_be);
+	uint32_t e = d.tbl24[h >> 8];
+	if ((e & DIR_TAG_MASK) == DIR_TAG_GROUP)
+		e = d.tbl8[(size_t)(e & DIR_PAYLOAD_MASK) * 256u + (h & 255u)];
+	uint32_t p = e & DIR_PAYLOAD_MASK;
+	*label = (e & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? d.vals[p] : p;
+	return e;
+}
+
+/* Policy hash probe: exact 8-byte policy_key + endpoint.  Returns the
+ * counter slot, or -1 (map_lookup_elem NULL); *z receives ep|proxy<<16. */
+__device__ __forceinline__ int pol_lookup(const pol_table &t, uint32_t lo, uint32_t hi, uint32_t ep,
+					  uint32_t *z)
+{
+	uint32_t b = pol_hash(lo, hi, ep) & t.bucket_mask;
+	for (uint32_t p = 0; p < t.max_probe; p++) {
+		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
+		uint4 s[4];
+#pragma unroll
+		for (int k = 0; k < 4; k++)
+			s[k] = bk[k];
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			if (s[k].w == POL_EMPTY)
+				return -1;
+			if (s[k].x == lo && s[k].y == hi && (s[k].z & 0xFFFFu) == ep) {
+				*z = s[k].z;
+				return (int)s[k].w;
+			}
+		}
+		b = (b + 1) & t.bucket_mask;
+	}
+	return -1;
+}
+
+__device__ __forceinline__ bool set4_has(const addr_set4 &t, uint32_t a)
+{
+	uint32_t b = mix32(a, 0x5e7) & t.bucket_mask;
+	for (uint32_t p = 0; p < t.max_probe; p++) {
+		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
+		uint4 s[4];
+#pragma unroll
+		for (int k = 0; k < 4; k++)
+			s[k] = bk[k];
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			if (!s[k].y)
+				return false;
+			if (s[k].x == a)
+				return true;
+			if (!s[k].w)
+				return false;
+			if (s[k].z == a)
+				return true;
+		}
+		b = (b + 1) & t.bucket_mask;
+	}
+	return false;
+}
+
+/* 16-byte key set probe; tag in used bits 8..15 (prefix length or 0) */
+__device__ __forceinline__ bool set16_has(const addr_set16 &t, uint4 a, uint32_t tag)
+{
+	uint32_t b = hash16(a.x, a.y, a.z, a.w, tag) & t.bucket_mask;
+	uint32_t want = 1u | (tag << 8);
+	for (uint32_t p = 0; p < t.max_probe; p++) {
+		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
+		uint4 k0 = bk[0], m0 = bk[1], k1 = bk[2], m1 = bk[3];
+		if (!(m0.x & 1u))
+			return false;
+		if (m0.x == want && k0.x == a.x && k0.y == a.y && k0.z == a.z && k0.w == a.w)
+			return true;
+		if (!(m1.x & 1u))
+			return false;
+		if (m1.x == want && k1.x == a.x && k1.y == a.y && k1.z == a.z && k1.w == a.w)
+			return true;
+		b = (b + 1) & t.bucket_mask;
+	}
+	return false;
+}
+
+template <typename T> __device__ __forceinline__ T wave_sum(T v)
+{
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1)
+		v += __shfl_xor(v, off, 64);
+	return v;
+}
+
+/*
+ * Stateless IPv4 classification (see cgpu.h cgpu_classify_v4).
+ *   egress : bpf_lxc.c:484-505   dstID = ipcache(daddr) | CLUSTER | WORLD
+ *   ingress: bpf_netdev.c:374-404 src identity from ipcache(saddr)
+ *   policy : bpf/lib/policy.h:46-110 (3 probes), collapsed to DROP_POLICY by
+ *            policy_can_access_ingress / policy_can_egress (:126-163)
+ *   gate   : bpf/lib/conntrack.h:526-528 DROP_CT_UNKNOWN_PROTO
+ *   metrics: bpf/lib/drop.h:104 update_metrics(len, dir, -reason); forwarded
+ *            at the verdict with reason 0
+ */
+__global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify_v4_args a)
+{
+	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
+	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+	uint64_t *pctr = a.delta;
+
+	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t fl = a.flags[i];
+		const uint32_t proto = a.proto[i];
+		const uint32_t len = a.len[i];
+		const uint32_t dport = a.dport[i];
+		const uint32_t ep = a.ep[i];
+		const uint32_t sa = a.saddr[i];
+		const uint32_t da = a.daddr[i];
+		const bool egress = fl & 1u;
+		int32_t v;
+		uint32_t id;
+		uint32_t st = 0;
+
+		if (s.ct_proto_gate && proto != 1u && proto != 6u && proto != 17u) {
+			v = DROP_CT_UNKNOWN_PROTO;
+			id = 0;
+			st = 4;
+		} else {
+			bool frag = false;
+			if (egress) {
+				uint32_t label;
+				uint32_t e = dir_lookup(s.ipc4, da, &label);
+				if (e && label)
+					id = label;
+				else if ((da & s.ipv4_cluster_mask) == s.ipv4_cluster_range)
+					id = s.cluster_id;
+				else
+					id = s.world_id;
+			} else {
+				uint32_t src = s.ingress_src_identity;
+				frag = (fl >> 1) & 1u;
+				if (src < s.health_id) {
+					uint32_t label;
+					uint32_t e = dir_lookup(s.ipc4, sa, &label);
+					if (e && label && label != s.cluster_id && label != s.host_id)
+						src = label;
+				}
+				id = s.ingress_secctx_world ? s.world_id : src;
+			}
+			const uint32_t eg = egress ? (1u << 24) : 0u;
+			const uint32_t hi4 = dport | (proto << 16) | eg;
+			uint32_t z = 0;
+			int ctr = -1;
+			if (!frag) {
+				ctr = pol_lookup(s.pol, id, hi4, ep, &z);
+				st = 1;
+			}
+			if (ctr < 0) {
+				ctr = pol_lookup(s.pol, id, eg, ep, &z);
+				st = 2;
+			}
+			if (ctr < 0 && !frag) {
+				ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
+				st = 3;
+			}
+			if (ctr >= 0) {
+				atomicAdd((unsigned long long *)&pctr[2u * (uint32_t)ctr], 1ull);
+				atomicAdd((unsigned long long *)&pctr[2u * (uint32_t)ctr + 1u],
+					  (unsigned long long)len);
+				v = st == 2 ? 0 : (int32_t)(z >> 16);
+			} else {
+				st = 0;
+				v = DROP_POLICY;
+			}
+		}
+		a.verdict[i] = v;
+		a.identity[i] = id;
+		if (a.stage)
+			a.stage[i] = (uint8_t)st;
+		const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : 2u);
+		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
+#pragma unroll
+		for (int k = 0; k < 6; k++) {
+			mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
+			mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
+		}
+	}
+
+	/* metrics: wave-reduce, one atomic per nonzero {reason, dir} per wave */
+	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
+	const uint32_t reasons[3] = {0u, 133u, 137u};
+#pragma unroll
+	for (int k = 0; k < 6; k++) {
+		uint64_t c = wave_sum(mcnt[k]);
+		uint64_t b = wave_sum(mbyt[k]);
+		if ((threadIdx.x & 63) == 0 && c) {
+			uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
+			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
+			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
+		}
+	}
+}
+
+/* XDP prefilter IPv4 (bpf/bpf_xdp.c:97-121, :158-178) */
+__global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilter_args a)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t f = a.flags[i];
+		const uint32_t sa = a.saddr4[i], da = a.daddr4[i];
+		uint8_t v;
+		if (f == 2u) {
+			v = XDP_PASS;
+		} else if (f != 0u) {
+			v = XDP_DROP;
+		} else {
+			bool drop = false;
+			if (s.pf4_enabled && s.pf4.tbl24) {
+				uint32_t label;
+				drop = dir_lookup(s.pf4, sa, &label) != 0;
+			}
+			v = drop ? XDP_DROP : (set4_has(s.ep4, da) ? XDP_PASS : XDP_DROP);
+		}
+		a.verdict[i] = v;
+	}
+}
+
+__device__ __forceinline__ uint4 mask6(uint4 w, uint32_t len)
+{
+	uint32_t m[4];
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		int bits = (int)len - 32 * k;
+		uint32_t mh = bits <= 0 ? 0u : (bits >= 32 ? 0xFFFFFFFFu : (0xFFFFFFFFu << (32 - bits)));
+		m[k] = bswap32(mh);
+	}
+	return make_uint4(w.x & m[0], w.y & m[1], w.z & m[2], w.w & m[3]);
+}
+
+/* XDP prefilter IPv6 (bpf/bpf_xdp.c:132-156): any-match over dyn6 + fix6 */
+__global__ __launch_bounds__(BLOCK) void k_prefilter_v6(cgpu_snapshot s, prefilter_args a)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
+	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
+	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t f = a.flags[i];
+		const uint4 sa = sa16[i], da = da16[i];
+		uint8_t v;
+		if (f == 2u) {
+			v = XDP_PASS;
+		} else if (f != 0u) {
+			v = XDP_DROP;
+		} else {
+			bool drop = false;
+			if (s.pf6_enabled && s.pf6.root) {
+				const uint32_t top = ((sa.x & 0xFFu) << 8) | ((sa.x >> 8) & 0xFFu);
+				const uint32_t r = s.pf6.root[top];
+				if (r == V6_ROOT_COVERED) {
+					drop = true;
+				} else if (r) {
+					const uint4 m = reinterpret_cast<const uint4 *>(s.pf6.masks)[r];
+					uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						while (mw[k] && !drop) {
+							uint32_t bit = __builtin_ctz(mw[k]);
+							mw[k] &= mw[k] - 1u;
+							uint32_t len = 17u + 32u * (uint32_t)k + bit;
+							drop = set16_has(s.pf6.set, mask6(sa, len), len);
+						}
+					}
+				}
+			}
+			v = drop ? XDP_DROP : (set16_has(s.ep6, da, 0u) ? XDP_PASS : XDP_DROP);
+		}
+		a.verdict[i] = v;
+	}
+}
+
+__global__ void k_fold(uint64_t *totals, uint64_t *delta, uint64_t n)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+	     i += (uint64_t)gridDim.x * blockDim.x) {
+		uint64_t d = delta[i];
+		if (d) {
+			totals[i] += d;
+			delta[i] = 0;
+		}
+	}
+}
+
+__global__ void k_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *slot,
+			    const uint64_t *pk, const uint64_t *by, uint32_t n)
+{
+	uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) {
+		uint32_t sl = slot[i];
+		totals[2u * sl] = pk[i];
+		totals[2u * sl + 1u] = by[i];
+		delta[2u * sl] = 0;
+		delta[2u * sl + 1u] = 0;
+	}
+}
+
+unsigned grid_for(uint64_t n)
+{
+	uint64_t blocks = (n + BLOCK - 1) / BLOCK;
+	/* 256 CUs x 8 resident 256-thread blocks; grid-stride beyond that */
+	const uint64_t cap = 256ull * 8ull;
+	return (unsigned)(blocks < cap ? (blocks ? blocks : 1) : cap);
+}
+
+} // namespace
+
+hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_classify_v4, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_prefilter_v4, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_prefilter_v6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st)
+{
+	unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
+	hipLaunchKernelGGL(k_fold, dim3(g ? g : 1), dim3(256), 0, st, totals, delta, n);
+	return hipGetLastError();
+}
+
+hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *slot,
+			    const uint64_t *pk, const uint64_t *by, uint32_t n, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_slot_init, dim3((n + 255) / 256), dim3(256), 0, st, totals, delta, slot,
+			   pk, by, n);
+	return hipGetLastError();
+}

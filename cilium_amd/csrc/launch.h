@@ -1,0 +1,44 @@
+/* Internal interface between host.cpp (C ABI, table compiler) and
+ * kernels.hip (gfx950 kernels).  Not exported. */
+#ifndef CGPU_LAUNCH_H
+#define CGPU_LAUNCH_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "tables.h"
+
+struct classify_v4_args {
+	const uint32_t *saddr, *daddr;
+	const uint16_t *dport;
+	const uint8_t *proto, *flags;
+	const uint32_t *len;
+	const uint16_t *ep;
+	int32_t *verdict;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t *delta; /* [2 * n_ctr_slots] policy + [CGPU_METRICS_WORDS] metrics */
+	uint64_t n;
+};
+
+hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st);
+
+struct prefilter_args {
+	const uint32_t *saddr4, *daddr4;
+	const uint8_t *saddr16, *daddr16;
+	const uint8_t *flags;
+	uint8_t *verdict;
+	uint64_t n;
+};
+
+hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st);
+hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st);
+
+/* totals[i] += delta[i]; delta[i] = 0 over n u64 words */
+hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st);
+/* totals[2*slot[i]] = pk[i]; totals[2*slot[i]+1] = by[i]; delta[..] = 0 */
+hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *slot,
+			    const uint64_t *pk, const uint64_t *by, uint32_t n, hipStream_t st);
+
+#endif

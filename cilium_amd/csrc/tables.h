@@ -1,0 +1,153 @@
+/*
+ * Device-resident table layouts (HBM) shared by the host compiler
+ * (host.cpp) and the gfx950 kernels (kernels.hip).  See DESIGN.md §3.
+ *
+ * All tables of one committed snapshot live in ONE hipMalloc'd arena; the
+ * snapshot descriptor below holds device pointers into it and is passed to
+ * kernels by value (kernarg), so a launch never dereferences host memory.
+ */
+#ifndef CGPU_TABLES_H
+#define CGPU_TABLES_H
+
+#include <stdint.h>
+
+/* ---- DIR-24-8 longest-prefix table (ipcache v4, prefilter v4) ----
+ * tbl24[addr >> 8] (2^24 u32 = 64 MiB) and 256-entry tbl8 groups for
+ * prefixes longer than /24.  Entry encoding (u32):
+ *   0                      no match (NULL from map_lookup_elem)
+ *   0b01 << 30 | label     match, sec_label < 2^30 stored inline
+ *   0b10 << 30 | group     descend into tbl8[group * 256 + (addr & 255)]
+ *   0b11 << 30 | idx       match, sec_label = vals[idx] (labels >= 2^30)
+ * tbl8 entries never hold the group form.  A tombstone (sec_label 0) is a
+ * match (0x40000000): it shadows shorter prefixes exactly as the kernel LPM
+ * trie does (pkg/maps/ipcache/ipcache.go:182-194). */
+#define DIR_TAG_SHIFT 30u
+#define DIR_TAG_MASK (3u << DIR_TAG_SHIFT)
+#define DIR_TAG_DIRECT (1u << DIR_TAG_SHIFT)
+#define DIR_TAG_GROUP (2u << DIR_TAG_SHIFT)
+#define DIR_TAG_INDIRECT (3u << DIR_TAG_SHIFT)
+#define DIR_PAYLOAD_MASK ((1u << DIR_TAG_SHIFT) - 1u)
+#define DIR_TBL24_ENTRIES (1u << 24)
+
+typedef struct dir248 {
+	const uint32_t *tbl24;
+	const uint32_t *tbl8;
+	const uint32_t *vals;
+	uint32_t n_groups;
+	uint32_t n_vals;
+} dir248;
+
+/* ---- policy hash: one open-addressing table for all endpoints ----
+ * 64-byte buckets (one cache-line sector) of 4 x 16-byte slots:
+ *   x = sec_label, y = dport | proto << 16 | egress_pad << 24,
+ *   z = ep | proxy_port << 16, w = counter slot (0xFFFFFFFF = empty).
+ * (x, y) is the raw 8-byte policy_key, compared whole like the kernel htab
+ * memcmp (pad bits included).  Bucket index = mix(key, ep) & mask, linear
+ * probing over buckets; a bucket with an empty slot ends the probe. */
+#define POL_SLOTS_PER_BUCKET 4u
+#define POL_EMPTY 0xFFFFFFFFu
+
+typedef struct pol_slot {
+	uint32_t key_lo;  /* sec_label */
+	uint32_t key_hi;  /* dport | protocol << 16 | egress_pad << 24 */
+	uint32_t ep_proxy;/* ep | proxy_port << 16 */
+	uint32_t ctr;     /* counter slot or POL_EMPTY */
+} pol_slot;
+
+typedef struct pol_table {
+	const pol_slot *slots; /* n_buckets * 4 */
+	uint32_t bucket_mask;
+	uint32_t max_probe;    /* longest probe sequence in buckets (>= 1) */
+} pol_table;
+
+static inline __host__ __device__ uint32_t pol_hash(uint32_t key_lo, uint32_t key_hi, uint32_t ep)
+{
+	uint64_t h = ((uint64_t)key_hi << 32 | key_lo) ^ ((uint64_t)ep * 0x9E3779B97F4A7C15ull);
+	h ^= h >> 33;
+	h *= 0xff51afd7ed558ccdull;
+	h ^= h >> 33;
+	h *= 0xc4ceb9fe1a85ec53ull;
+	h ^= h >> 33;
+	return (uint32_t)h;
+}
+
+/* ---- exact address sets (cilium_lxc endpoints) ----
+ * v4: 64-byte buckets of 8 x {addr_be, used}; v6: 64-byte buckets of
+ * 2 x {addr[16], used, pad[3]} (32-byte slots). */
+typedef struct set4_slot {
+	uint32_t addr;
+	uint32_t used;
+} set4_slot;
+
+typedef struct set16_slot {
+	uint32_t a[4];
+	uint32_t used; /* bit0 used; bits 8..15 = prefix length for prefix sets */
+	uint32_t pad[3];
+} set16_slot;
+
+typedef struct addr_set4 {
+	const set4_slot *slots; /* n_buckets * 8 */
+	uint32_t bucket_mask;
+	uint32_t max_probe;
+} addr_set4;
+
+typedef struct addr_set16 {
+	const set16_slot *slots; /* n_buckets * 2 */
+	uint32_t bucket_mask;
+	uint32_t max_probe;
+} addr_set16;
+
+static inline __host__ __device__ uint32_t mix32(uint32_t a, uint32_t b)
+{
+	uint64_t h = ((uint64_t)b << 32 | a) * 0x9E3779B97F4A7C15ull;
+	h ^= h >> 29;
+	h *= 0xbf58476d1ce4e5b9ull;
+	h ^= h >> 32;
+	return (uint32_t)h;
+}
+
+static inline __host__ __device__ uint32_t hash16(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+						  uint32_t salt)
+{
+	return mix32(mix32(a0, a1) ^ salt, mix32(a2, a3));
+}
+
+/* ---- IPv6 any-match prefix set (prefilter dyn6 + fix6) ----
+ * root[addr >> 112] (65536 x u16) selects a row of `masks`: the set of
+ * prefix lengths 17..128 present under that /16 (bit L-17 of 128 bits);
+ * row 0 = none, ROOT_COVERED = a prefix of length <= 16 covers the root.
+ * Each present length L is then ONE independent probe of `set`, keyed by
+ * (addr masked to L, L): the probes of one packet have no dependence on
+ * each other, so they are issued together (memory-level parallelism
+ * instead of a pointer chase down a trie). */
+#define V6_ROOT_COVERED 0xFFFFu
+
+typedef struct v6_anyset {
+	const uint16_t *root;  /* 65536 */
+	const uint32_t *masks; /* n_masks x 4 u32 */
+	addr_set16 set;        /* used word: bit0 used, bits 8..15 length */
+	uint32_t n_masks;
+} v6_anyset;
+
+/* ---- one committed snapshot ---- */
+typedef struct cgpu_snapshot {
+	dir248 ipc4;
+	pol_table pol;
+	dir248 pf4;      /* any-match: dyn4 (if enabled) + fix4 /32 */
+	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
+	addr_set16 ep6;  /* cilium_lxc IPv6 keys */
+	v6_anyset pf6;   /* any-match: dyn6 (if enabled) + fix6 /128 */
+	uint32_t pf4_enabled; /* CIDR4_FILTER */
+	uint32_t pf6_enabled; /* CIDR6_FILTER */
+	/* config */
+	uint32_t world_id, cluster_id, host_id, health_id;
+	uint32_t ipv4_cluster_mask, ipv4_cluster_range;
+	uint32_t ct_proto_gate, ingress_secctx_world, ingress_src_identity;
+	uint32_t n_ctr_slots;
+	uint64_t epoch;
+} cgpu_snapshot;
+
+/* counters: u64 {packets, bytes} per policy slot, then metrics */
+#define CGPU_METRICS_WORDS (256u * 4u * 2u)
+
+#endif

@@ -1,0 +1,330 @@
+"""Python face of the engine: a thin wrapper over the C ABI (include/cgpu.h).
+
+The map objects mirror the method sets of the reference's Go map wrappers so
+that tests read like the reference's own callers:
+
+* :class:`PolicyMap`  — pkg/maps/policymap/policymap.go (Allow/AllowKey/Exists/
+  Delete/DeleteKey/DumpToSlice/Flush)
+* :class:`IPCacheMap` — pkg/maps/ipcache/ipcache.go (Update/Delete with the
+  tombstone-on-ENOSYS variant, NewKey) and the IPIdentityMappingListener hook
+  (pkg/ipcache/listener.go:36-48, pkg/datapath/ipcache/listener.go:78-127)
+* :class:`CIDRMap`    — pkg/maps/cidrmap/cidrmap.go (InsertCIDR/DeleteCIDR/
+  CIDRExists/CIDRDump, checkPrefixlen)
+
+Batch entry points take torch CUDA tensors (device memory) and launch on the
+caller's current HIP stream.  Nothing here computes a verdict on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import ipaddress
+
+import numpy as np
+
+from . import layouts as L
+from ._abi import CgpuConfig, CgpuError, TuplesV4, check, lib
+
+CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX = 0, 1, 2, 3
+BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
+
+
+def _buf(x) -> bytes:
+    return np.ascontiguousarray(x).tobytes()
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+class Engine:
+    """One cgpu context bound to one GPU (device=-1: host-only, table ops)."""
+
+    def __init__(self, device: int = 0, **cfg):
+        self.L = lib()
+        self.cfg = CgpuConfig()
+        self.L.cgpu_config_default(C.byref(self.cfg))
+        for k, v in cfg.items():
+            if not hasattr(self.cfg, k):
+                raise TypeError(f"unknown config field {k}")
+            setattr(self.cfg, k, v)
+        h = C.c_void_p()
+        check(self.L.cgpu_ctx_create(C.byref(self.cfg), device, C.byref(h)), "cgpu_ctx_create")
+        self.h = h
+        self.device = device
+        self._bound = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.cgpu_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------- raw map ops
+    def ipcache_update(self, key, val, flags=BPF_ANY) -> int:
+        return self.L.cgpu_ipcache_update(self.h, _buf(key), _buf(val), flags)
+
+    def ipcache_delete(self, key) -> int:
+        return self.L.cgpu_ipcache_delete(self.h, _buf(key))
+
+    def ipcache_lookup(self, key):
+        out = C.create_string_buffer(8)
+        rc = self.L.cgpu_ipcache_lookup(self.h, _buf(key), out)
+        return rc, (np.frombuffer(out.raw, L.REMOTE_ENDPOINT_INFO)[0] if rc == 0 else None)
+
+    def ipcache_keys(self):
+        keys, prev = [], None
+        out = C.create_string_buffer(24)
+        while self.L.cgpu_ipcache_get_next_key(self.h, prev, out) == 0:
+            prev = out.raw
+            keys.append(np.frombuffer(prev, L.IPCACHE_KEY)[0])
+        return keys
+
+    def policy_update(self, ep, key, entry, flags=BPF_ANY) -> int:
+        return self.L.cgpu_policy_update(self.h, ep, _buf(key), _buf(entry), flags)
+
+    def policy_delete(self, ep, key) -> int:
+        return self.L.cgpu_policy_delete(self.h, ep, _buf(key))
+
+    def policy_lookup(self, ep, key):
+        out = C.create_string_buffer(24)
+        rc = self.L.cgpu_policy_lookup(self.h, ep, _buf(key), out)
+        return rc, (np.frombuffer(out.raw, L.POLICY_ENTRY)[0] if rc == 0 else None)
+
+    def policy_keys(self, ep):
+        keys, prev = [], None
+        out = C.create_string_buffer(8)
+        while self.L.cgpu_policy_get_next_key(self.h, ep, prev, out) == 0:
+            prev = out.raw
+            keys.append(np.frombuffer(prev, L.POLICY_KEY)[0])
+        return keys
+
+    def policy_flush(self, ep) -> int:
+        return self.L.cgpu_policy_flush(self.h, ep)
+
+    @staticmethod
+    def _cidr_buf(key) -> bytes:
+        raw = _buf(key)
+        return raw + bytes(20 - len(raw))
+
+    def cidr_update(self, which, key, flags=BPF_ANY) -> int:
+        return self.L.cgpu_cidr_update(self.h, which, self._cidr_buf(key), flags)
+
+    def cidr_delete(self, which, key) -> int:
+        return self.L.cgpu_cidr_delete(self.h, which, self._cidr_buf(key))
+
+    def cidr_lookup(self, which, key) -> int:
+        return self.L.cgpu_cidr_lookup(self.h, which, self._cidr_buf(key))
+
+    def cidr_keys(self, which):
+        keys, prev = [], None
+        out = C.create_string_buffer(20)
+        dt = L.LPM_V4_KEY if which in (CIDR_V4_DYN, CIDR_V4_FIX) else L.LPM_V6_KEY
+        while self.L.cgpu_cidr_get_next_key(self.h, which, prev, out) == 0:
+            prev = out.raw
+            keys.append(np.frombuffer(prev[:dt.itemsize], dt)[0])
+        return keys
+
+    def endpoint_update(self, key, flags=BPF_ANY) -> int:
+        return self.L.cgpu_endpoint_update(self.h, _buf(key), flags)
+
+    def endpoint_delete(self, key) -> int:
+        return self.L.cgpu_endpoint_delete(self.h, _buf(key))
+
+    def endpoint_lookup(self, key) -> int:
+        return self.L.cgpu_endpoint_lookup(self.h, _buf(key))
+
+    def commit(self) -> int:
+        ep = C.c_uint64()
+        check(self.L.cgpu_commit(self.h, C.byref(ep)), "cgpu_commit")
+        return ep.value
+
+    def checksum(self) -> int:
+        s = C.c_uint64()
+        check(self.L.cgpu_table_checksum(self.h, C.byref(s)), "cgpu_table_checksum")
+        return s.value
+
+    # -------------------------------------------------------------- batches
+    def classify_v4(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """t: dict of CUDA tensors saddr/daddr (int32 view of network-order
+        u32), dport (int16), proto/flags (uint8), len (int32), ep (int16)."""
+        import torch
+        n = t["saddr"].numel()
+        dev = t["saddr"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
+        tv = TuplesV4(*[t[k].data_ptr() for k in
+                        ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")])
+        check(self.L.cgpu_classify_v4(self.h, C.byref(tv), n, _ptr(out["verdict"]),
+                                      _ptr(out["identity"]), _ptr(out.get("stage")),
+                                      _stream(stream)), "cgpu_classify_v4")
+        return out
+
+    def prefilter_v4(self, saddr, daddr, flags, out=None, stream=None):
+        import torch
+        n = flags.numel()
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint8, device=flags.device)
+        check(self.L.cgpu_prefilter_v4(self.h, _ptr(saddr), _ptr(daddr), _ptr(flags), n,
+                                       _ptr(out), _stream(stream)), "cgpu_prefilter_v4")
+        return out
+
+    def prefilter_v6(self, saddr16, daddr16, flags, out=None, stream=None):
+        import torch
+        n = flags.numel()
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint8, device=flags.device)
+        check(self.L.cgpu_prefilter_v6(self.h, _ptr(saddr16), _ptr(daddr16), _ptr(flags), n,
+                                       _ptr(out), _stream(stream)), "cgpu_prefilter_v6")
+        return out
+
+    # ------------------------------------------------------------- counters
+    def counter_delta_bytes(self) -> int:
+        return self.L.cgpu_counter_delta_bytes(self.h)
+
+    def counter_bind(self, tensor) -> None:
+        """Accumulate launches into `tensor` (CUDA int64, >= delta bytes)."""
+        if tensor is None:
+            check(self.L.cgpu_counter_bind(self.h, None, 0), "cgpu_counter_bind")
+        else:
+            check(self.L.cgpu_counter_bind(self.h, _ptr(tensor),
+                                           tensor.numel() * tensor.element_size()),
+                  "cgpu_counter_bind")
+        self._bound = tensor
+
+    def counter_fold(self, stream=None) -> None:
+        check(self.L.cgpu_counter_fold(self.h, _stream(stream)), "cgpu_counter_fold")
+
+    def metrics(self) -> np.ndarray:
+        out = np.zeros((256, 4, 2), np.uint64)
+        check(self.L.cgpu_metrics_read(self.h, out.ctypes.data_as(C.c_void_p)),
+              "cgpu_metrics_read")
+        return out
+
+    def counters_reset(self) -> None:
+        check(self.L.cgpu_counters_reset(self.h), "cgpu_counters_reset")
+
+
+# ---------------------------------------------------------------------------
+# Go-API mirrors
+# ---------------------------------------------------------------------------
+class PolicyMap:
+    """pkg/maps/policymap.PolicyMap over one endpoint's map (ports host order)."""
+
+    def __init__(self, engine: Engine, ep: int):
+        self.e, self.ep = engine, ep
+
+    def Allow(self, identity, dport, proto, direction, proxy_port=0):  # noqa: N802
+        rc = self.e.policy_update(self.ep, L.policy_key(identity, dport, proto, direction),
+                                  L.policy_entry(proxy_port))
+        check(rc, "PolicyMap.Allow")
+
+    def AllowKey(self, key, proxy_port=0):  # noqa: N802 (key: host-order fields)
+        self.Allow(int(key["sec_label"]), int(key["dport"]), int(key["protocol"]),
+                   int(key["egress"]) & 1, proxy_port)
+
+    def Exists(self, identity, dport, proto, direction) -> bool:  # noqa: N802
+        rc, _ = self.e.policy_lookup(self.ep, L.policy_key(identity, dport, proto, direction))
+        return rc == 0
+
+    def Delete(self, identity, dport, proto, direction):  # noqa: N802
+        check(self.e.policy_delete(self.ep, L.policy_key(identity, dport, proto, direction)),
+              "PolicyMap.Delete")
+
+    def DeleteKey(self, key):  # noqa: N802
+        self.Delete(int(key["sec_label"]), int(key["dport"]), int(key["protocol"]),
+                    int(key["egress"]) & 1)
+
+    def DumpToSlice(self):  # noqa: N802
+        out = []
+        for k in self.e.policy_keys(self.ep):
+            rc, ent = self.e.policy_lookup(self.ep, k)
+            if rc == 0:
+                out.append((k, ent))
+        return out
+
+    def Flush(self):  # noqa: N802
+        check(self.e.policy_flush(self.ep), "PolicyMap.Flush")
+
+
+class IPCacheMap:
+    """pkg/maps/ipcache.Map + the ipcache listener hook."""
+
+    def __init__(self, engine: Engine, supports_delete: bool = True):
+        self.e = engine
+        self.supports_delete = supports_delete
+
+    def Update(self, cidr: str, identity: int, tunnel: int = 0):  # noqa: N802
+        check(self.e.ipcache_update(L.ipcache_key(cidr), L.remote_info(identity, tunnel)),
+              "ipcache.Update")
+
+    def Delete(self, cidr: str):  # noqa: N802
+        # pkg/maps/ipcache/ipcache.go:182-200: without delete support the
+        # entry is overwritten with zeroes (a tombstone that still matches)
+        if not self.supports_delete:
+            return self.Update(cidr, 0, 0)
+        check(self.e.ipcache_delete(L.ipcache_key(cidr)), "ipcache.Delete")
+
+    # IPIdentityMappingListener.OnIPIdentityCacheChange (listener.go:78-127)
+    def OnIPIdentityCacheChange(self, modType: str, cidr: str, identity: int,  # noqa: N802
+                                hostIP: int = 0):
+        if modType == "upsert":
+            self.Update(cidr, identity, hostIP)
+        elif modType == "delete":
+            try:
+                self.Delete(cidr)
+            except CgpuError as ex:
+                if ex.errno != errno.ENOENT:
+                    raise
+
+
+class CIDRMap:
+    """pkg/maps/cidrmap.CIDRMap (prefilter maps)."""
+
+    def __init__(self, engine: Engine, which: int):
+        self.e, self.which = engine, which
+        self.v6 = which in (CIDR_V6_DYN, CIDR_V6_FIX)
+        self.prefixlen = 0 if which in (CIDR_V4_DYN, CIDR_V6_DYN) else (128 if self.v6 else 32)
+        self.dynamic = which in (CIDR_V4_DYN, CIDR_V6_DYN)
+
+    def _check(self, plen, op):
+        # checkPrefixlen (cidrmap.go:75-83)
+        if self.prefixlen != 0 and ((self.dynamic and self.prefixlen < plen) or
+                                    (not self.dynamic and self.prefixlen != plen)):
+            raise ValueError(f"Unable to {op} element with dynamic prefix length "
+                             f"cm.Prefixlen={self.prefixlen} key.Prefixlen={plen}")
+
+    def InsertCIDR(self, cidr: str):  # noqa: N802
+        k = L.lpm_key(cidr)
+        self._check(int(k["prefixlen"]), "update")
+        check(self.e.cidr_update(self.which, k), "InsertCIDR")
+
+    def DeleteCIDR(self, cidr: str):  # noqa: N802
+        k = L.lpm_key(cidr)
+        self._check(int(k["prefixlen"]), "delete")
+        check(self.e.cidr_delete(self.which, k), "DeleteCIDR")
+
+    def CIDRExists(self, cidr: str) -> bool:  # noqa: N802
+        return self.e.cidr_lookup(self.which, L.lpm_key(cidr)) == 0
+
+    def CIDRDump(self):  # noqa: N802
+        out = []
+        for k in self.e.cidr_keys(self.which):
+            raw = bytes(k["addr"])
+            addr = ipaddress.ip_address(raw)
+            out.append(f"{addr}/{int(k['prefixlen'])}")
+        return out

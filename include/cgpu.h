@@ -1,0 +1,273 @@
+/*
+ * cgpu.h — C ABI of the MI355X flow-classification engine.
+ *
+ * Drop-in for the kernel-map boundary the reference's Go agent programs
+ * through bpf(2) (pkg/bpf/bpf.go:153-245 UpdateElement / LookupElement /
+ * DeleteElement / GetNextKey) and for the per-packet BPF datapath functions
+ * that read those maps (bpf/lib/policy.h, bpf/lib/eps.h, bpf/bpf_xdp.c).
+ * A Go package pkg/datapath/gpu binds this header through cgo (see
+ * INTEGRATION.md); keys and values are the reference byte layouts so the Go
+ * side passes unsafe.Pointer through unchanged, exactly as it does today.
+ *
+ * Conventions (mirroring bpf(2) as wrapped by pkg/bpf):
+ *   - every function returns 0 or a negative errno:
+ *       -ENOENT missing key, -EEXIST / -ENOENT for BPF_NOEXIST / BPF_EXIST,
+ *       -E2BIG hash map full, -ENOSPC LPM map full, -EINVAL bad argument
+ *       (prefixlen, family, flags), -ENODEV no GPU bound to the context,
+ *       -EIO device error (details: cgpu_last_error()).
+ *   - the caller owns every key/value/tuple buffer; the library copies.
+ *   - table updates are thread-safe (one mutex on the host mirror) and become
+ *     visible to classification only at cgpu_commit(), which publishes a new
+ *     immutable device snapshot (epoch).  Classification launches read the
+ *     latest committed snapshot and may run concurrently with updates.
+ *     Like the reference (pkg/endpoint/bpf.go:459-465), a set of updates is
+ *     not atomic unless it is committed at once.
+ *   - batch entry points take DEVICE pointers (HBM-resident SoA columns) and
+ *     a hipStream_t (passed as void*; NULL = the null stream).  They enqueue
+ *     and return; results are ready when the stream reaches that point.
+ *     There is no CPU execution path: without a device they fail -ENODEV.
+ */
+#ifndef CGPU_H
+#define CGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGPU_ABI_VERSION 1u
+
+/* bpf(2) update flags (include/uapi/linux/bpf.h) */
+#define CGPU_ANY 0u
+#define CGPU_NOEXIST 1u
+#define CGPU_EXIST 2u
+
+/* ------------------------------------------------------------------ */
+/* Reference byte layouts                                              */
+/* ------------------------------------------------------------------ */
+
+/* struct policy_key, bpf/lib/common.h:180-186; Go PolicyKey
+ * (pkg/maps/policymap/policymap.go:63-68).  dport in network order.
+ * egress_pad holds the bitfield byte {egress:1, pad:7}: bit 0 = egress. */
+typedef struct cgpu_policy_key {
+	uint32_t sec_label;
+	uint16_t dport;
+	uint8_t protocol;
+	uint8_t egress_pad;
+} cgpu_policy_key;
+
+/* struct policy_entry, bpf/lib/common.h:188-193 (proxy_port network order) */
+typedef struct cgpu_policy_entry {
+	uint16_t proxy_port;
+	uint16_t pad[3];
+	uint64_t packets;
+	uint64_t bytes;
+} cgpu_policy_entry;
+
+/* struct ipcache_key, bpf/lib/maps.h:135-148 (24 B, packed).  prefixlen
+ * counts the 32 static bits {pad[3], family} plus the IP bits
+ * (bpf/lib/eps.h:48-52; Go pkg/maps/ipcache/ipcache.go:72-98). */
+typedef struct cgpu_ipcache_key {
+	uint32_t prefixlen;
+	uint8_t pad[3];
+	uint8_t family; /* ENDPOINT_KEY_IPV4 = 1, ENDPOINT_KEY_IPV6 = 2 */
+	uint8_t ip[16];
+} cgpu_ipcache_key;
+
+/* struct remote_endpoint_info, bpf/lib/common.h:175-178 */
+typedef struct cgpu_remote_endpoint_info {
+	uint32_t sec_label;
+	uint32_t tunnel_endpoint;
+} cgpu_remote_endpoint_info;
+
+/* struct lpm_v4_key / lpm_v6_key, bpf/lib/xdp.h:23-31 (Go cidrKey,
+ * pkg/maps/cidrmap/cidrmap.go:49-52, truncated to 4 + AddrSize bytes).
+ * Only the first 4 (v4) or 16 (v6) bytes of addr are used. */
+typedef struct cgpu_cidr_key {
+	uint32_t prefixlen;
+	uint8_t addr[16];
+} cgpu_cidr_key;
+
+/* struct endpoint_key, bpf/lib/common.h:147-160 (20 B, packed) */
+typedef struct cgpu_endpoint_key {
+	uint8_t ip[16];
+	uint8_t family;
+	uint8_t pad4;
+	uint16_t pad5;
+} cgpu_endpoint_key;
+
+/* prefilter maps: pkg/policy/prefilter.go:33-39 preFilterMapType */
+enum cgpu_cidr_map {
+	CGPU_CIDR_V4_DYN = 0, /* LPM, bpf_xdp.c CIDR4_LMAP_NAME */
+	CGPU_CIDR_V4_FIX = 1, /* exact hash, CIDR4_HMAP_NAME */
+	CGPU_CIDR_V6_DYN = 2,
+	CGPU_CIDR_V6_FIX = 3,
+};
+
+/* ------------------------------------------------------------------ */
+/* Configuration: the compile-time #defines the agent writes into      */
+/* node_config.h / lxc_config.h / filter_config.h become runtime fields */
+/* ------------------------------------------------------------------ */
+typedef struct cgpu_config {
+	uint32_t abi_version;       /* = CGPU_ABI_VERSION */
+	/* capacities (max_elem of the reference maps; device sizing) */
+	uint32_t ipcache_max;       /* IPCACHE_MAP_SIZE 512000 (node_config.h:63) */
+	uint32_t policy_max_per_ep; /* POLICY_MAP_SIZE 16384 (policymap.go:37) */
+	uint32_t policy_max_total;  /* device slots across all endpoints */
+	uint32_t max_endpoints;     /* policy maps = endpoint ids [0, max) */
+	uint32_t cidr_dyn_max;      /* maxLKeys 64k (prefilter.go:43) */
+	uint32_t cidr_fix_max;      /* maxHKeys 20M (prefilter.go:44) */
+	uint32_t endpoints_max;     /* ENDPOINTS_MAP_SIZE 65536 */
+	/* reserved identities (node_config.h:34-37) */
+	uint32_t host_id, world_id, cluster_id, health_id;
+	/* IPV4_CLUSTER_MASK / IPV4_CLUSTER_RANGE, network-order u32 as the
+	 * agent writes them (daemon/daemon.go:919-920) */
+	uint32_t ipv4_cluster_mask, ipv4_cluster_range;
+	uint8_t ipv6_router_ip[16]; /* ROUTER_IP, ipv6_match_prefix_64 */
+	/* CONNTRACK protocol gate: non ICMP/TCP/UDP -> DROP_CT_UNKNOWN_PROTO
+	 * before policy (bpf/lib/conntrack.h:526-528) */
+	uint8_t ct_proto_gate;
+	/* ingress label: 0 -> secctx = resolved source identity (FROM_HOST
+	 * form, bpf_netdev.c:403); 1 -> WORLD_ID (derive_ipv4_sec_ctx,
+	 * bpf_netdev.c:278-290) */
+	uint8_t ingress_secctx_world;
+	/* prefilter: CIDR4_FILTER/CIDR4_LPM_PREFILTER/... (prefilter.go:65-89) */
+	uint8_t prefilter_fix4, prefilter_dyn4, prefilter_fix6, prefilter_dyn6;
+	uint8_t reserved0[2];
+	/* identity handed to handle_ipv4 on ingress (from_netdev: 0) */
+	uint32_t ingress_src_identity;
+	uint32_t reserved[8];
+} cgpu_config;
+
+typedef struct cgpu_ctx cgpu_ctx;
+
+void cgpu_config_default(cgpu_config *cfg);
+/* device: HIP device ordinal, or -1 for a host-only context (table
+ * management and dumps work; batch entry points return -ENODEV). */
+int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **out);
+void cgpu_ctx_destroy(cgpu_ctx *ctx);
+const char *cgpu_last_error(void);
+const char *cgpu_version(void);
+
+/* ------------------------------------------------------------------ */
+/* ipcache: pkg/maps/ipcache (Map.Update/Delete, LPM semantics of       */
+/* kernel/bpf/lpm_trie.c; lookup is longest-prefix like bpf(2) lookup)  */
+/* ------------------------------------------------------------------ */
+int cgpu_ipcache_update(cgpu_ctx *ctx, const cgpu_ipcache_key *key,
+			const cgpu_remote_endpoint_info *val, uint64_t flags);
+int cgpu_ipcache_delete(cgpu_ctx *ctx, const cgpu_ipcache_key *key);
+int cgpu_ipcache_lookup(cgpu_ctx *ctx, const cgpu_ipcache_key *key,
+			cgpu_remote_endpoint_info *val_out);
+/* GetNextKey: key == NULL returns the first key; -ENOENT after the last */
+int cgpu_ipcache_get_next_key(cgpu_ctx *ctx, const cgpu_ipcache_key *key,
+			      cgpu_ipcache_key *next_out);
+size_t cgpu_ipcache_count(cgpu_ctx *ctx);
+
+/* ------------------------------------------------------------------ */
+/* policy maps: pkg/maps/policymap (AllowKey/DeleteKey/DumpToSlice/     */
+/* Flush), one map per endpoint id                                      */
+/* ------------------------------------------------------------------ */
+int cgpu_policy_update(cgpu_ctx *ctx, uint32_t ep, const cgpu_policy_key *key,
+		       const cgpu_policy_entry *entry, uint64_t flags);
+int cgpu_policy_delete(cgpu_ctx *ctx, uint32_t ep, const cgpu_policy_key *key);
+/* entry_out.packets/bytes include every committed-and-classified batch */
+int cgpu_policy_lookup(cgpu_ctx *ctx, uint32_t ep, const cgpu_policy_key *key,
+		       cgpu_policy_entry *entry_out);
+int cgpu_policy_get_next_key(cgpu_ctx *ctx, uint32_t ep, const cgpu_policy_key *key,
+			     cgpu_policy_key *next_out);
+int cgpu_policy_flush(cgpu_ctx *ctx, uint32_t ep);
+size_t cgpu_policy_count(cgpu_ctx *ctx, uint32_t ep);
+
+/* ------------------------------------------------------------------ */
+/* prefilter CIDR maps: pkg/maps/cidrmap (InsertCIDR/DeleteCIDR/        */
+/* CIDRExists/CIDRDump) and the endpoint map cilium_lxc (lxcmap)        */
+/* ------------------------------------------------------------------ */
+int cgpu_cidr_update(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key, uint64_t flags);
+int cgpu_cidr_delete(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key);
+/* exact key presence (CIDRExists semantics for fix; LPM lookup for dyn) */
+int cgpu_cidr_lookup(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key);
+int cgpu_cidr_get_next_key(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key,
+			   cgpu_cidr_key *next_out);
+int cgpu_endpoint_update(cgpu_ctx *ctx, const cgpu_endpoint_key *key, uint64_t flags);
+int cgpu_endpoint_delete(cgpu_ctx *ctx, const cgpu_endpoint_key *key);
+int cgpu_endpoint_lookup(cgpu_ctx *ctx, const cgpu_endpoint_key *key);
+
+/* ------------------------------------------------------------------ */
+/* publication                                                          */
+/* ------------------------------------------------------------------ */
+/* Compile the host mirror into device tables and publish them as the new
+ * snapshot read by later batch launches.  *epoch_out (optional) receives
+ * the snapshot number.  Blocks until the upload completes. */
+int cgpu_commit(cgpu_ctx *ctx, uint64_t *epoch_out);
+/* order-independent checksum of the committed table contents; replicas on
+ * different GPUs/ranks holding the same tables report the same value */
+int cgpu_table_checksum(cgpu_ctx *ctx, uint64_t *sum_out);
+
+/* ------------------------------------------------------------------ */
+/* batch classification (device pointers)                              */
+/* ------------------------------------------------------------------ */
+/* Tuple flag bits */
+#define CGPU_F_EGRESS 1u   /* from-container (bpf_lxc.c handle_ipv4_from_lxc) */
+#define CGPU_F_FRAGMENT 2u /* ipv4_is_fragment (bpf/lib/ipv4.h:50-61) */
+
+typedef struct cgpu_tuples_v4 {
+	const uint32_t *saddr; /* network order */
+	const uint32_t *daddr; /* network order */
+	const uint16_t *dport; /* network order (policy port, conntrack.h:471-524) */
+	const uint8_t *proto;
+	const uint8_t *flags;  /* CGPU_F_* */
+	const uint32_t *len;   /* skb->len */
+	const uint16_t *ep;    /* endpoint id: selects the policy map */
+} cgpu_tuples_v4;
+
+/*
+ * For every tuple: ipcache LPM of the remote address, identity fallback,
+ * the three-probe policy cascade of __policy_can_access (policy.h:46-110),
+ * the per-entry packets/bytes counters and the {reason, dir} metrics.
+ *   verdict[i]  : proxy port (raw be16 as int, e.g. 4000 -> 40975), 0 allow,
+ *                 DROP_POLICY (-133), DROP_CT_UNKNOWN_PROTO (-137)
+ *   identity[i] : label given to policy (dstID on egress, secctx on ingress)
+ *   stage[i]    : optional (NULL ok): 1 exact, 2 L3-only, 3 identity-wildcard
+ *                 L4, 0 miss, 4 protocol-gated
+ */
+int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
+		     uint32_t *identity, uint8_t *stage, void *stream);
+
+/* XDP prefilter over pre-parsed packets (bpf_xdp.c:88-184).
+ * flags: 0 IP packet of this family, 1 truncated (-> XDP_DROP),
+ *        2 not IPv4/IPv6 (-> XDP_PASS).  verdict: XDP_DROP 1 / XDP_PASS 2. */
+#define CGPU_PKT_OK 0u
+#define CGPU_PKT_TRUNCATED 1u
+#define CGPU_PKT_NOT_IP 2u
+int cgpu_prefilter_v4(cgpu_ctx *ctx, const uint32_t *saddr, const uint32_t *daddr,
+		      const uint8_t *flags, size_t n, uint8_t *verdict, void *stream);
+/* saddr/daddr: 16 bytes per packet, contiguous */
+int cgpu_prefilter_v6(cgpu_ctx *ctx, const uint8_t *saddr, const uint8_t *daddr,
+		      const uint8_t *flags, size_t n, uint8_t *verdict, void *stream);
+
+/* ------------------------------------------------------------------ */
+/* counters                                                             */
+/* ------------------------------------------------------------------ */
+/*
+ * Batch launches accumulate into a DELTA buffer of cgpu_counter_delta_bytes()
+ * bytes: u64 {packets, bytes} per policy slot, then u64 {count, bytes} per
+ * {reason 0..255, dir 0..3} metrics key.  By default the context owns it;
+ * cgpu_counter_bind() points launches at a caller-owned device buffer (e.g.
+ * a torch tensor that is all-reduced over RCCL across ranks holding the same
+ * committed tables).  cgpu_counter_fold() adds the delta into the
+ * totals reported by cgpu_policy_lookup / cgpu_metrics_read and zeroes it.
+ */
+size_t cgpu_counter_delta_bytes(cgpu_ctx *ctx);
+int cgpu_counter_bind(cgpu_ctx *ctx, void *device_buf, size_t bytes);
+int cgpu_counter_fold(cgpu_ctx *ctx, void *stream);
+/* out: [256][4][2] u64 {count, bytes} (folds and synchronizes first) */
+int cgpu_metrics_read(cgpu_ctx *ctx, uint64_t *out);
+int cgpu_counters_reset(cgpu_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CGPU_H */

@@ -1,0 +1,148 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol
+include/cgpu.h declares, and the host mirror follows bpf(2) map semantics
+(pkg/bpf/bpf.go conventions: 0 or -errno).  No compute call is made here;
+batch entry points on a host-only context must fail loudly (-ENODEV)."""
+import ctypes as C
+import errno
+import os
+import re
+
+import numpy as np
+import pytest
+
+from cilium_amd import build, layouts as L
+from cilium_amd._abi import PROTOS, TuplesV4, lib
+from cilium_amd.engine import (CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX, BPF_EXIST,
+                               BPF_NOEXIST, CIDRMap, Engine, IPCacheMap, PolicyMap)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    build.build()
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "cgpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cgpu_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 30
+    L_ = C.CDLL(build.LIB)
+    missing = [s for s in syms if not hasattr(L_, s)]
+    assert not missing, missing
+    # the ctypes table covers the whole header too
+    assert set(syms) == set(PROTOS), set(syms) ^ set(PROTOS)
+
+
+def test_library_is_gfx950():
+    data = open(build.LIB, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_host_only_context_has_no_cpu_path():
+    e = Engine(device=-1)
+    L_ = lib()
+    tv = TuplesV4()
+    v = np.zeros(4, np.int32)
+    rc = L_.cgpu_classify_v4(e.h, C.byref(tv), 4, v.ctypes.data, v.ctypes.data, None, None)
+    assert rc == -errno.ENODEV
+    assert b"no CPU classification path" in L_.cgpu_last_error()
+    assert L_.cgpu_prefilter_v4(e.h, None, None, None, 1, None, None) == -errno.ENODEV
+    assert L_.cgpu_commit(e.h, None) == -errno.ENODEV
+
+
+def test_policy_map_semantics():
+    e = Engine(device=-1, policy_max_per_ep=4, max_endpoints=8)
+    k = L.policy_key(300, 80, 6, 0)
+    assert e.policy_update(0, k, L.policy_entry(4000)) == 0
+    assert e.policy_update(0, k, L.policy_entry(0), BPF_NOEXIST) == -errno.EEXIST
+    assert e.policy_update(0, L.policy_key(1, 1, 6, 0), L.policy_entry(), BPF_EXIST) == -errno.ENOENT
+    rc, ent = e.policy_lookup(0, k)
+    assert rc == 0 and ent["proxy_port"] == L.htons(4000)
+    # pad bits are part of the key (kernel htab memcmp)
+    assert e.policy_lookup(0, L.policy_key(300, 80, 6, 0, pad_bits=1))[0] == -errno.ENOENT
+    for i in range(3):
+        assert e.policy_update(0, L.policy_key(400 + i, 0, 0, 1), L.policy_entry()) == 0
+    assert e.policy_update(0, L.policy_key(999, 0, 0, 1), L.policy_entry()) == -errno.E2BIG
+    assert len(e.policy_keys(0)) == 4
+    assert e.policy_delete(0, L.policy_key(999, 0, 0, 1)) == -errno.ENOENT
+    assert e.policy_update(9, k, L.policy_entry()) == -errno.EINVAL
+    assert e.policy_flush(0) == 0 and e.policy_keys(0) == []
+    # Go mirror
+    pm = PolicyMap(e, 1)
+    pm.Allow(256, 443, 6, 1, proxy_port=15001)
+    assert pm.Exists(256, 443, 6, 1) and not pm.Exists(256, 443, 17, 1)
+    d = pm.DumpToSlice()
+    assert len(d) == 1 and d[0][1]["proxy_port"] == L.htons(15001)
+    pm.Delete(256, 443, 6, 1)
+    assert pm.DumpToSlice() == []
+
+
+def test_ipcache_lpm_semantics():
+    e = Engine(device=-1, ipcache_max=3)
+    assert e.ipcache_update(L.ipcache_key("10.0.0.0/8"), L.remote_info(100)) == 0
+    # same prefix with different host bits is the same LPM element
+    assert e.ipcache_update(L.ipcache_key("10.9.9.9/8"), L.remote_info(101)) == 0
+    assert len(e.ipcache_keys()) == 1
+    assert e.ipcache_update(L.ipcache_key("10.1.0.0/16"), L.remote_info(0)) == 0  # tombstone
+    assert e.ipcache_update(L.ipcache_key("192.168.0.0/16"), L.remote_info(7)) == 0
+    assert e.ipcache_update(L.ipcache_key("172.16.0.0/12"), L.remote_info(7)) == -errno.ENOSPC
+    rc, v = e.ipcache_lookup(L.ipcache_key("10.1.2.3/32"))
+    assert rc == 0 and v["sec_label"] == 0  # tombstone shadows 10/8
+    rc, v = e.ipcache_lookup(L.ipcache_key("10.2.2.3/32"))
+    assert rc == 0 and v["sec_label"] == 101
+    assert e.ipcache_lookup(L.ipcache_key("11.0.0.1/32"))[0] == -errno.ENOENT
+    bad = L.ipcache_key("10.0.0.0/8")
+    bad["prefixlen"] = 161
+    assert e.ipcache_update(bad, L.remote_info(1)) == -errno.EINVAL
+    assert e.ipcache_delete(L.ipcache_key("10.0.0.0/9")) == -errno.ENOENT
+    m = IPCacheMap(e)
+    m.OnIPIdentityCacheChange("delete", "10.1.0.0/16", 0)
+    assert e.ipcache_lookup(L.ipcache_key("10.1.2.3/32"))[1]["sec_label"] == 101
+    m.OnIPIdentityCacheChange("delete", "10.1.0.0/16", 0)  # ENOENT tolerated
+    tomb = IPCacheMap(e, supports_delete=False)
+    tomb.Delete("192.168.0.0/16")
+    assert e.ipcache_lookup(L.ipcache_key("192.168.1.1/32"))[1]["sec_label"] == 0
+
+
+def test_cidr_and_endpoint_maps():
+    e = Engine(device=-1)
+    dyn = CIDRMap(e, CIDR_V4_DYN)
+    fix = CIDRMap(e, CIDR_V4_FIX)
+    dyn.InsertCIDR("192.0.2.0/24")
+    fix.InsertCIDR("198.51.100.7/32")
+    with pytest.raises(ValueError):
+        fix.InsertCIDR("198.51.100.0/24")  # checkPrefixlen: fix maps are /32 only
+    assert dyn.CIDRExists("192.0.2.77/32")  # LPM lookup
+    assert fix.CIDRExists("198.51.100.7/32") and not fix.CIDRExists("198.51.100.8/32")
+    assert dyn.CIDRDump() == ["192.0.2.0/24"] and fix.CIDRDump() == ["198.51.100.7/32"]
+    dyn6 = CIDRMap(e, CIDR_V6_DYN)
+    dyn6.InsertCIDR("2001:db8::/32")
+    assert dyn6.CIDRExists("2001:db8::1/128")
+    CIDRMap(e, CIDR_V6_FIX).InsertCIDR("2001:db8::5/128")
+    assert CIDRMap(e, CIDR_V6_FIX).CIDRDump() == ["2001:db8::5/128"]
+    dyn.DeleteCIDR("192.0.2.0/24")
+    assert dyn.CIDRDump() == []
+    k = L.lpm_key("10.0.0.0/8")
+    k["prefixlen"] = 33
+    assert e.cidr_update(CIDR_V4_DYN, k) == -errno.EINVAL
+    ek = L.endpoint_key("10.0.0.5")
+    assert e.endpoint_update(ek) == 0 and e.endpoint_lookup(ek) == 0
+    assert e.endpoint_update(ek, BPF_NOEXIST) == -errno.EEXIST
+    assert e.endpoint_delete(ek) == 0 and e.endpoint_lookup(ek) == -errno.ENOENT
+
+
+def test_bad_flags_and_abi_version():
+    e = Engine(device=-1)
+    assert e.policy_update(0, L.policy_key(1, 1, 6, 0), L.policy_entry(), 3) == -errno.EINVAL
+    from cilium_amd._abi import CgpuConfig
+    cfg = CgpuConfig()
+    lib().cgpu_config_default(C.byref(cfg))
+    cfg.abi_version = 99
+    h = C.c_void_p()
+    assert lib().cgpu_ctx_create(C.byref(cfg), -1, C.byref(h)) == -errno.EINVAL

@@ -1,0 +1,304 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's
+golden vectors and, at larger sizes, against the CPU restatement (oracle).
+Every comparison is bit-exact (integer path)."""
+import numpy as np
+import pytest
+
+from cilium_amd import build, layouts as L, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU test needs a device"
+    build.build()
+    return torch
+
+
+def _engine(**kw):
+    from cilium_amd.engine import Engine
+    return Engine(device=0, **kw)
+
+
+def _np(t, dt=None):
+    a = t.cpu().numpy()
+    return a.view(dt) if dt is not None else a
+
+
+def _classify(torch, e, t, stage=True):
+    d = synth.to_device(t)
+    out = e.classify_v4(d, stage=stage)
+    torch.cuda.synchronize()
+    return (_np(out["verdict"]), _np(out["identity"], np.uint32),
+            _np(out["stage"]) if stage else None)
+
+
+@pytest.mark.parametrize("ci", range(5))
+def test_classify_v4_golden(torch_cuda, golden, ci):
+    g = golden("classify_v4.npz")
+    gate, src, sw = (int(x) for x in g["configs"][ci])
+    e = _engine(ct_proto_gate=gate, ingress_src_identity=src, ingress_secctx_world=sw)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert e.ipcache_update(k, v) == 0
+    for k, en, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert e.policy_update(int(ep), k, en) == 0
+    e.commit()
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    v, idt, st = _classify(torch_cuda, e, t)
+    np.testing.assert_array_equal(v, g[f"c{ci}_verdict"])
+    np.testing.assert_array_equal(idt, g[f"c{ci}_identity"])
+    np.testing.assert_array_equal(st, g[f"c{ci}_stage"])
+    for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
+        rc, got = e.policy_lookup(int(ep), k)
+        assert rc == 0
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+    m = e.metrics()
+    verdict, ln = g[f"c{ci}_verdict"], t["len"].astype(np.uint64)
+    dirs = np.where(t["flags"] & 1, L.METRIC_EGRESS, L.METRIC_INGRESS)
+    reason = np.where(verdict < 0, -verdict, 0)
+    exp = np.zeros((256, 4, 2), np.uint64)
+    np.add.at(exp, (reason, dirs, 0), 1)
+    np.add.at(exp, (reason, dirs, 1), ln)
+    np.testing.assert_array_equal(m, exp)
+    e.close()
+
+
+def test_prefilter_golden(torch_cuda, golden):
+    from test_oracle_golden import parse_frames
+    torch = torch_cuda
+    g = golden("xdp_prefilter.npz")
+    e = _engine()
+    for w, name in enumerate(("dyn4", "fix4", "dyn6", "fix6")):
+        for k in g[name]:
+            assert e.cidr_update(w, k) == 0
+    for k in g["endpoints"]:
+        assert e.endpoint_update(k) == 0
+    e.commit()
+    fam, flags, s4, d4, s6, d6 = parse_frames(g)
+    v4, v6 = fam == 4, fam == 6
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
+    o4 = e.prefilter_v4(dev(s4[v4], np.int32), dev(d4[v4], np.int32), dev(flags[v4], np.uint8))
+    o6 = e.prefilter_v6(dev(s6[v6], np.uint8), dev(d6[v6], np.uint8), dev(flags[v6], np.uint8))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(o4), g["verdict"][v4])
+    np.testing.assert_array_equal(_np(o6), g["verdict"][v6])
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def cfg1():
+    T = synth.make_tables(**synth.CONFIGS["cpu"])
+    t = synth.make_tuples(T, 1 << 20)
+    return T, t
+
+
+def _oracle_run(T, t, **cfg):
+    from oracle import Oracle
+    o = Oracle(**T.oracle_config(), **cfg)
+    synth.load_oracle(o, T)
+    v, idt, st, probes = o.classify_v4(t, nthreads=8)
+    return o, v, idt, st, probes
+
+
+def test_classify_config1_vs_oracle(torch_cuda, cfg1):
+    """SURVEY §8d config 1 (10k prefixes, 16k MapState, 1M tuples)."""
+    T, t = cfg1
+    o, v0, i0, s0, _ = _oracle_run(T, t)
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    v, idt, st = _classify(torch_cuda, e, t)
+    np.testing.assert_array_equal(v, v0)
+    np.testing.assert_array_equal(idt, i0)
+    np.testing.assert_array_equal(st, s0)
+    # every per-entry counter
+    for k, ep in zip(T.pol_keys, T.pol_ep):
+        rc, got = e.policy_lookup(int(ep), k)
+        rc0, raw = o.policy_lookup(int(ep), k)
+        exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert rc == 0 and rc0 == 0
+        assert (int(got["packets"]), int(got["bytes"])) == (int(exp["packets"]), int(exp["bytes"]))
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 257, 100_003])
+def test_ragged_sizes(torch_cuda, cfg1, n):
+    T, t_full = cfg1
+    t = {k: v[:n] for k, v in t_full.items()}
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    if n == 0:
+        d = synth.to_device(t)
+        out = e.classify_v4(d)
+        torch_cuda.cuda.synchronize()
+        assert out["verdict"].numel() == 0
+        return
+    o, v0, i0, s0, _ = _oracle_run(T, t)
+    v, idt, st = _classify(torch_cuda, e, t)
+    np.testing.assert_array_equal(v, v0)
+    np.testing.assert_array_equal(idt, i0)
+    np.testing.assert_array_equal(st, s0)
+    e.close()
+
+
+def test_counter_bind_fold_and_reset(torch_cuda, cfg1):
+    torch = torch_cuda
+    T, t = cfg1
+    t = {k: v[:200_000] for k, v in t.items()}
+    o, v0, _, _, _ = _oracle_run(T, t)
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    buf = torch.zeros(e.counter_delta_bytes() // 8, dtype=torch.int64, device="cuda")
+    e.counter_bind(buf)
+    d = synth.to_device(t)
+    for _ in range(3):
+        e.classify_v4(d, stage=False)
+    torch.cuda.synchronize()
+    # the bound buffer holds exactly 3x the oracle's metrics
+    met = buf[-256 * 4 * 2:].cpu().numpy().view(np.uint64).reshape(256, 4, 2)
+    np.testing.assert_array_equal(met, 3 * o.metrics())
+    e.counter_fold()
+    torch.cuda.synchronize()
+    assert int(buf.abs().sum()) == 0
+    np.testing.assert_array_equal(e.metrics(), 3 * o.metrics())
+    k, ep = T.pol_keys[0], int(T.pol_ep[0])
+    rc, got = e.policy_lookup(ep, k)
+    _, raw = o.policy_lookup(ep, k)
+    exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+    assert int(got["packets"]) == 3 * int(exp["packets"])
+    e.counters_reset()
+    assert int(e.metrics().sum()) == 0
+    e.counter_bind(None)
+    e.close()
+
+
+def test_update_commit_sequences(torch_cuda, cfg1):
+    """Random upsert/delete rounds (ipcache + policy), commit after each, the
+    GPU agrees with the restatement fed the same operations; re-adding a key
+    restarts its counters from the supplied entry (kernel htab replace)."""
+    from oracle import Oracle
+    torch = torch_cuda
+    T, t_full = cfg1
+    t = {k: v[:50_000] for k, v in t_full.items()}
+    rng = np.random.default_rng(7)
+    e = _engine(**T.engine_config())
+    o = Oracle(**T.oracle_config())
+    synth.load_engine(e, T)
+    synth.load_oracle(o, T)
+    d = synth.to_device(t)
+    for rnd in range(4):
+        # delete 5% of ipcache entries and policy keys, re-add some with new labels
+        for i in rng.choice(len(T.ipc_keys), len(T.ipc_keys) // 20, replace=False):
+            k = T.ipc_keys[i]
+            r1, r2 = e.ipcache_delete(k), o.ipcache_delete(k)
+            assert (r1 == 0) == (r2 == 0)
+            if rng.random() < 0.5:
+                v = L.remote_info(int(rng.integers(256, 1256)))
+                assert e.ipcache_update(k, v) == 0 and o.ipcache_update(k, v) == 0
+        for i in rng.choice(len(T.pol_keys), len(T.pol_keys) // 20, replace=False):
+            k, ep = T.pol_keys[i], int(T.pol_ep[i])
+            r1, r2 = e.policy_delete(ep, k), o.policy_delete(ep, k)
+            assert (r1 == 0) == (r2 == 0)
+            if rng.random() < 0.5:
+                en = L.policy_entry(int(rng.integers(0, 3)) * 1000, 5, 500)
+                assert e.policy_update(ep, k, en) == 0 and o.policy_update(ep, k, en) == 0
+        e.commit()
+        out = e.classify_v4(d)
+        v0, i0, s0, _ = o.classify_v4(t, nthreads=8)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(_np(out["verdict"]), v0, err_msg=f"round {rnd}")
+        np.testing.assert_array_equal(_np(out["identity"], np.uint32), i0)
+        np.testing.assert_array_equal(_np(out["stage"]), s0)
+    for k, ep in zip(T.pol_keys, T.pol_ep):
+        rc, got = e.policy_lookup(int(ep), k)
+        rc0, raw = o.policy_lookup(int(ep), k)
+        assert (rc == 0) == (rc0 == 0)
+        if rc == 0:
+            exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+            assert (int(got["packets"]), int(got["bytes"]), int(got["proxy_port"])) == \
+                (int(exp["packets"]), int(exp["bytes"]), int(exp["proxy_port"]))
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
+
+
+def _v6(rng, n, roots):
+    a = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    r = roots[rng.integers(0, len(roots), n)]
+    a[:, :3] = r
+    return a
+
+
+def test_prefilter_scale_vs_oracle(torch_cuda):
+    """Larger prefilter sets (v4 dyn/fix, v6 dyn over few /24 roots + /128
+    fix, endpoints) against the restatement, incl. disabled-dyn configs."""
+    from oracle import Oracle
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    n = 300_000
+    roots = rng.integers(0, 256, (64, 3), dtype=np.uint8)
+    dyn6 = []
+    for _ in range(20_000):
+        k = np.zeros((), L.LPM_V6_KEY)
+        k["prefixlen"] = int(rng.choice([8, 16, 20, 32, 48, 56, 64, 96, 127]))
+        k["addr"][:] = _v6(rng, 1, roots)[0]
+        dyn6.append(k)
+    fix6 = []
+    for _ in range(5_000):
+        k = np.zeros((), L.LPM_V6_KEY)
+        k["prefixlen"] = 128
+        k["addr"][:] = _v6(rng, 1, roots)[0]
+        fix6.append(k)
+    dyn4, fix4 = [], []
+    for _ in range(20_000):
+        k = np.zeros((), L.LPM_V4_KEY)
+        k["prefixlen"] = int(rng.choice([8, 16, 20, 24, 28, 30, 32]))
+        k["addr"][:] = rng.integers(0, 256, 4, dtype=np.uint8)
+        dyn4.append(k)
+    for _ in range(5_000):
+        k = np.zeros((), L.LPM_V4_KEY)
+        k["prefixlen"] = 32
+        k["addr"][:] = rng.integers(0, 256, 4, dtype=np.uint8)
+        fix4.append(k)
+    ep4 = rng.integers(0, 2**32, 4000, dtype=np.uint64).astype(np.uint32)
+    ep6 = _v6(rng, 4000, roots)
+    s6 = np.where(rng.random((n, 1)) < 0.5,
+                  np.array([k["addr"] for k in dyn6])[rng.integers(0, len(dyn6), n)],
+                  _v6(rng, n, roots))
+    s6[: n // 10] = np.array([k["addr"] for k in fix6])[rng.integers(0, len(fix6), n // 10)]
+    d6 = np.where(rng.random((n, 1)) < 0.3, ep6[rng.integers(0, 4000, n)], _v6(rng, n, roots))
+    s4 = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d4 = np.where(rng.random(n) < 0.3, ep4[rng.integers(0, 4000, n)],
+                  rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32))
+    flags = rng.choice(np.array([0] * 30 + [1, 2], np.uint8), n)
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
+    for dyn_on in (1, 0):
+        e = _engine(prefilter_dyn4=dyn_on, prefilter_dyn6=dyn_on)
+        o = Oracle(dyn4=dyn_on, dyn6=dyn_on)
+        for w, ks in ((0, dyn4), (1, fix4), (2, dyn6), (3, fix6)):
+            for k in ks:
+                assert e.cidr_update(w, k) == 0 and o.cidr_update(w, k) == 0
+        for a in ep4:
+            ek = np.zeros((), L.ENDPOINT_KEY)
+            ek["ip"][:4] = np.frombuffer(int(a).to_bytes(4, "little"), np.uint8)
+            ek["family"] = 1
+            assert e.endpoint_update(ek) == 0 and o.endpoint_update(ek) == 0
+        for a in ep6:
+            ek = np.zeros((), L.ENDPOINT_KEY)
+            ek["ip"][:] = a
+            ek["family"] = 2
+            assert e.endpoint_update(ek) == 0 and o.endpoint_update(ek) == 0
+        e.commit()
+        g4 = e.prefilter_v4(dev(s4, np.int32), dev(d4, np.int32), dev(flags, np.uint8))
+        g6 = e.prefilter_v6(dev(s6, np.uint8), dev(d6, np.uint8), dev(flags, np.uint8))
+        torch.cuda.synchronize()
+        r4, _ = o.prefilter_v4(s4, d4, flags, nthreads=8)
+        r6, _ = o.prefilter_v6(s6, d6, flags, nthreads=8)
+        np.testing.assert_array_equal(_np(g4), r4)
+        np.testing.assert_array_equal(_np(g6), r6)
+        assert (r6 == L.XDP_DROP).mean() > 0.2 and (r6 == L.XDP_PASS).mean() > 0.05
+        e.close()
