@@ -52,7 +52,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from cilium_amd import synth
+    from cilium_amd import shard, synth
     from cilium_amd.engine import Engine
 
     torch.cuda.set_device(local)
@@ -87,7 +87,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            dist.all_reduce(delta)  # RCCL over xGMI: integer SUM, order-independent
+            shard.allreduce_counters(delta)  # RCCL over xGMI: integer SUM, order-independent
         e.counter_fold(stream)
 
     for _ in range(args.warmup):

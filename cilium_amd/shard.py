@@ -1,0 +1,53 @@
+"""Multi-GPU plumbing for the classification path.
+
+* Tuples are independent units: a stream is partitioned by a flow hash of
+  the 5-tuple, so all packets of a flow land on the same GPU (the property
+  RSS gives the reference's per-CPU datapath) and shards need no exchange.
+* Tables are replicated on every rank (identical update sequences; compare
+  `Engine.checksum()` across ranks).
+* The only collective is the integer SUM of the counter delta buffer
+  (per-policy-entry packets/bytes + {reason, dir} metrics), after which every
+  rank folds the same global delta into its totals.  Integer addition is
+  order-independent, so the result is bit-exact against one GPU processing
+  the whole stream.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def flowhash_np(saddr, daddr, sport, dport, proto) -> np.ndarray:
+    """Deterministic 32-bit flow hash (murmur3 finalizer over the 5-tuple).
+    Direction-sensitive, like skb->hash for the reference's RSS spreading."""
+    h = (saddr.astype(np.uint64) * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
+    h ^= daddr.astype(np.uint64)
+    h = (h * np.uint64(0x85EBCA77)) & np.uint64(0xFFFFFFFF)
+    h ^= (sport.astype(np.uint64) << np.uint64(16)) | dport.astype(np.uint64)
+    h = (h * np.uint64(0xC2B2AE3D)) & np.uint64(0xFFFFFFFF)
+    h ^= proto.astype(np.uint64)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return h.astype(np.uint32)
+
+
+def shard_of(t: dict, world: int) -> np.ndarray:
+    """Owning rank of every tuple: flowhash(5-tuple) % world."""
+    sport = t.get("sport", np.zeros_like(t["dport"]))
+    return (flowhash_np(t["saddr"], t["daddr"], sport, t["dport"], t["proto"]) %
+            np.uint32(world)).astype(np.int64)
+
+
+def take(t: dict, idx) -> dict:
+    return {k: np.ascontiguousarray(v[idx]) for k, v in t.items()}
+
+
+def allreduce_counters(delta, group=None):
+    """SUM the int64 counter delta across ranks in place (RCCL on GPU
+    tensors, gloo on CPU tensors).  u64 counters travel as their int64 bit
+    pattern: two's-complement addition is the same modulo 2^64."""
+    import torch.distributed as dist
+    dist.all_reduce(delta, op=dist.ReduceOp.SUM, group=group)
+    return delta

@@ -1,0 +1,106 @@
+"""N>1 path on CPU: world_size 2 over gloo.
+
+Each rank takes its flow-hash shard of one tuple stream, classifies it (the
+CPU restatement stands in for the GPU here: the test is about the
+shard/merge protocol, not the kernel), packs its per-entry counters into a
+delta buffer, and the delta is SUM-all-reduced with the same helper bench.py
+uses.  The merged counters and the concatenated verdicts must equal one
+process classifying the whole stream."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from cilium_amd import layouts as L, shard, synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _counters(o, T):
+    out = np.zeros(2 * len(T.pol_keys) + 256 * 4 * 2, np.uint64)
+    for i, (k, ep) in enumerate(zip(T.pol_keys, T.pol_ep)):
+        rc, raw = o.policy_lookup(int(ep), k)
+        e = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        out[2 * i], out[2 * i + 1] = e["packets"], e["bytes"]
+    out[2 * len(T.pol_keys):] = o.metrics().ravel()
+    return out
+
+
+def _worker(rank, world, port, q):
+    import sys
+    import torch
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    from oracle import Oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    T = synth.make_tables(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+    t = synth.make_tuples(T, 200_000)
+    t["sport"] = np.random.default_rng(5).integers(1024, 65536, len(t["saddr"])).astype(np.uint16)
+    owner = shard.shard_of(t, world)
+    mine = np.nonzero(owner == rank)[0]
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    part = shard.take({k: v for k, v in t.items() if k != "sport"}, mine)
+    v, idt, st, _ = o.classify_v4(part, nthreads=2)
+    delta = torch.from_numpy(_counters(o, T).view(np.int64).copy())
+    shard.allreduce_counters(delta)
+    # gather verdicts to rank 0 (test only; the product keeps them sharded)
+    objs = [None] * world
+    dist.all_gather_object(objs, (mine, v, idt))
+    if rank == 0:
+        q.put((delta.numpy().view(np.uint64).copy(), objs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_partition_is_exact():
+    T = synth.make_tables(n_prefixes=500, n_identities=50, keys_per_ep=300)
+    t = synth.make_tuples(T, 50_000)
+    for world in (1, 2, 3, 8):
+        own = shard.shard_of(t, world)
+        assert own.min() >= 0 and own.max() < world
+        counts = np.bincount(own, minlength=world)
+        assert counts.sum() == 50_000
+        if world > 1:  # roughly balanced
+            assert counts.min() > 0.8 * 50_000 / world
+    # deterministic and flow-consistent
+    assert np.array_equal(shard.shard_of(t, 8), shard.shard_of(t, 8))
+
+
+def test_gloo_world2_counters_match_single_process():
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "oracle"))
+    from oracle import Oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    merged, objs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    T = synth.make_tables(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+    t = synth.make_tuples(T, 200_000)
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    v, idt, _, _ = o.classify_v4(t, nthreads=2)
+    np.testing.assert_array_equal(merged, _counters(o, T))
+    v2 = np.empty_like(v)
+    i2 = np.empty_like(idt)
+    for mine, vv, ii in objs:
+        v2[mine], i2[mine] = vv, ii
+    np.testing.assert_array_equal(v2, v)
+    np.testing.assert_array_equal(i2, idt)
