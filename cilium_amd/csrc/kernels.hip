@@ -10,6 +10,8 @@
  */
 #include "launch.h"
 
+#include <cstdlib>
+
 #define DROP_POLICY (-133)           /* bpf/lib/common.h:240 */
 #define DROP_CT_UNKNOWN_PROTO (-137) /* bpf/lib/common.h:244 */
 #define XDP_DROP 1
@@ -114,6 +116,45 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v)
 	return v;
 }
 
+/* One 64-byte policy bucket (4 slots) held in registers. */
+struct pol_bucket {
+	uint4 s[4];
+};
+
+__device__ __forceinline__ pol_bucket pol_load(const pol_table &t, uint32_t b)
+{
+	const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
+	pol_bucket r;
+#pragma unroll
+	for (int k = 0; k < 4; k++)
+		r.s[k] = bk[k];
+	return r;
+}
+
+/* Resolve a probe whose first bucket is already loaded: -1 miss, else the
+ * counter slot.  Continues down the probe sequence only if the first bucket
+ * is full and does not hold the key (rare at load <= 0.5). */
+__device__ __forceinline__ int pol_resolve(const pol_table &t, const pol_bucket &first, uint32_t b,
+					   uint32_t lo, uint32_t hi, uint32_t ep, uint32_t *z)
+{
+	pol_bucket cur = first;
+	for (uint32_t p = 0;;) {
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			if (cur.s[k].w == POL_EMPTY)
+				return -1;
+			if (cur.s[k].x == lo && cur.s[k].y == hi && (cur.s[k].z & 0xFFFFu) == ep) {
+				*z = cur.s[k].z;
+				return (int)cur.s[k].w;
+			}
+		}
+		if (++p >= t.max_probe)
+			return -1;
+		b = (b + 1) & t.bucket_mask;
+		cur = pol_load(t, b);
+	}
+}
+
 /*
  * Stateless IPv4 classification (see cgpu.h cgpu_classify_v4).
  *   egress : bpf_lxc.c:484-505   dstID = ipcache(daddr) | CLUSTER | WORLD
@@ -123,7 +164,17 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v)
  *   gate   : bpf/lib/conntrack.h:526-528 DROP_CT_UNKNOWN_PROTO
  *   metrics: bpf/lib/drop.h:104 update_metrics(len, dir, -reason); forwarded
  *            at the verdict with reason 0
+ *
+ * SPEC = 0: the cascade exactly as the reference walks it (probe k+1 is
+ *           issued only after probe k missed).
+ * SPEC = 1: same results, different schedule: the identity-wildcard probe's
+ *           bucket {0, dport, proto, dir} does not depend on the identity, so
+ *           it is loaded before the ipcache lookup; the exact and L3 buckets
+ *           are loaded together once the identity is known.  The dependent
+ *           chain shrinks from up to 5 loads to 2-3, at the price of reading
+ *           buckets the reference would not have probed.
  */
+template <int SPEC>
 __global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify_v4_args a)
 {
 	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
@@ -148,7 +199,15 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify
 			id = 0;
 			st = 4;
 		} else {
-			bool frag = false;
+			const bool frag = !egress && ((fl >> 1) & 1u);
+			const uint32_t eg = egress ? (1u << 24) : 0u;
+			const uint32_t hi4 = dport | (proto << 16) | eg;
+			pol_bucket b3;
+			uint32_t bi3 = 0;
+			if (SPEC) {
+				bi3 = pol_hash(0u, hi4, ep) & s.pol.bucket_mask;
+				b3 = pol_load(s.pol, bi3);
+			}
 			if (egress) {
 				uint32_t label;
 				uint32_t e = dir_lookup(s.ipc4, da, &label);
@@ -160,7 +219,6 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify
 					id = s.world_id;
 			} else {
 				uint32_t src = s.ingress_src_identity;
-				frag = (fl >> 1) & 1u;
 				if (src < s.health_id) {
 					uint32_t label;
 					uint32_t e = dir_lookup(s.ipc4, sa, &label);
@@ -169,21 +227,38 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify
 				}
 				id = s.ingress_secctx_world ? s.world_id : src;
 			}
-			const uint32_t eg = egress ? (1u << 24) : 0u;
-			const uint32_t hi4 = dport | (proto << 16) | eg;
 			uint32_t z = 0;
 			int ctr = -1;
-			if (!frag) {
-				ctr = pol_lookup(s.pol, id, hi4, ep, &z);
-				st = 1;
-			}
-			if (ctr < 0) {
-				ctr = pol_lookup(s.pol, id, eg, ep, &z);
-				st = 2;
-			}
-			if (ctr < 0 && !frag) {
-				ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
-				st = 3;
+			if (SPEC) {
+				const uint32_t bi1 = pol_hash(id, hi4, ep) & s.pol.bucket_mask;
+				const uint32_t bi2 = pol_hash(id, eg, ep) & s.pol.bucket_mask;
+				pol_bucket b1 = pol_load(s.pol, bi1);
+				pol_bucket b2 = pol_load(s.pol, bi2);
+				if (!frag) {
+					ctr = pol_resolve(s.pol, b1, bi1, id, hi4, ep, &z);
+					st = 1;
+				}
+				if (ctr < 0) {
+					ctr = pol_resolve(s.pol, b2, bi2, id, eg, ep, &z);
+					st = 2;
+				}
+				if (ctr < 0 && !frag) {
+					ctr = pol_resolve(s.pol, b3, bi3, 0u, hi4, ep, &z);
+					st = 3;
+				}
+			} else {
+				if (!frag) {
+					ctr = pol_lookup(s.pol, id, hi4, ep, &z);
+					st = 1;
+				}
+				if (ctr < 0) {
+					ctr = pol_lookup(s.pol, id, eg, ep, &z);
+					st = 2;
+				}
+				if (ctr < 0 && !frag) {
+					ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
+					st = 3;
+				}
 			}
 			if (ctr >= 0) {
 				atomicAdd((unsigned long long *)&pctr[2u * (uint32_t)ctr], 1ull);
@@ -335,9 +410,20 @@ unsigned grid_for(uint64_t n)
 
 } // namespace
 
+/* CGPU_CLASSIFY_VARIANT selects the probe schedule (A/B in one process);
+ * every variant computes identical results. */
+static int classify_variant()
+{
+	const char *v = getenv("CGPU_CLASSIFY_VARIANT");
+	return v ? atoi(v) : 1;
+}
+
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st)
 {
-	hipLaunchKernelGGL(k_classify_v4, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	if (classify_variant() == 0)
+		hipLaunchKernelGGL(k_classify_v4<0>, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	else
+		hipLaunchKernelGGL(k_classify_v4<1>, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 	return hipGetLastError();
 }
 
