@@ -364,6 +364,11 @@ void or_default_config(or_config *cfg)
 	cfg->ingress_src_identity = 0; /* from_netdev: identity = 0 (bpf_netdev.c:487) */
 	cfg->ingress_secctx_world = 0;
 	cfg->dyn4 = cfg->fix4 = cfg->dyn6 = cfg->fix6 = 1; /* bpf/filter_config.h */
+	{
+		static const uint8_t r[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1,
+					      0x0, 0x1, 0x0, 0x0}; /* node_config.h:30 */
+		memcpy(cfg->router_ip, r, 16);
+	}
 }
 
 or_ctx *or_create(void)
@@ -508,6 +513,18 @@ static const uint8_t *ipcache4(const or_ctx *c, uint32_t addr_be)
 	memcpy(key, &plen, 4);
 	key[7] = 1; /* ENDPOINT_KEY_IPV4, bpf/lib/common.h:139 */
 	memcpy(key + 8, &addr_be, 4);
+	return lpm_lookup(&c->ipcache, key);
+}
+
+/* ipcache_lookup6 (bpf/lib/eps.h:56-66): {prefixlen 32 + 128, family 2, ip6} */
+static const uint8_t *ipcache6(const or_ctx *c, const uint8_t *addr16)
+{
+	uint8_t key[24];
+	uint32_t plen = 160;
+	memset(key, 0, sizeof(key));
+	memcpy(key, &plen, 4);
+	key[7] = 2; /* ENDPOINT_KEY_IPV6 */
+	memcpy(key + 8, addr16, 16);
 	return lpm_lookup(&c->ipcache, key);
 }
 
@@ -697,6 +714,140 @@ int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *d
 			cls_worker(j);
 		else
 			pthread_create(&th[t], NULL, cls_worker, j);
+	}
+	for (int t = 0; t < nthreads; t++) {
+		if (nthreads > 1)
+			pthread_join(th[t], NULL);
+		probes += jobs[t].probes;
+		for (int k = 0; k < N_METRICS; k++)
+			c->metrics[k] += jobs[t].metrics[k];
+	}
+	if (probe_sum)
+		*probe_sum = probes;
+	free(jobs);
+	free(th);
+	return 0;
+}
+
+struct cls6_job {
+	or_ctx *c;
+	size_t lo, hi;
+	const uint8_t *s6, *d6, *proto, *flags;
+	const uint32_t *len;
+	const uint16_t *dport, *ep;
+	int32_t *verdict;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t probes;
+	uint64_t metrics[N_METRICS];
+};
+
+static void *cls6_worker(void *arg)
+{
+	struct cls6_job *j = arg;
+	const or_ctx *c = j->c;
+	const or_config *cfg = &c->cfg;
+	for (size_t i = j->lo; i < j->hi; i++) {
+		int egress = j->flags[i] & 1;
+		uint8_t proto = j->proto[i];
+		uint32_t id, ep = j->ep[i];
+		int32_t v;
+		int st, dir = egress ? METRIC_EGRESS : METRIC_INGRESS;
+		struct ohash *h = ep < c->n_ep ? &c->policy[ep] : NULL;
+		const uint8_t *sa = j->s6 + 16 * i, *da = j->d6 + 16 * i;
+
+		if (cfg->ct_proto_gate && proto != 58 && proto != PROTO_TCP && proto != PROTO_UDP) {
+			/* ct_lookup6 default case, bpf/lib/conntrack.h:376-378 */
+			v = DROP_CT_UNKNOWN_PROTO;
+			id = 0;
+			st = 4;
+		} else if (egress) {
+			/* bpf_lxc.c:170-191; ipv6_match_prefix_64 (bpf/lib/ipv6.h:166-175) */
+			const uint8_t *info = ipcache6(c, da);
+			uint32_t label = 0;
+			struct pol_res r;
+			if (info)
+				memcpy(&label, info, 4);
+			if (info && label)
+				id = label;
+			else if (!memcmp(da, cfg->router_ip, 8))
+				id = cfg->cluster_id;
+			else
+				id = cfg->world_id;
+			j->probes += 1;
+			r = policy_access(h, id, j->dport[i], proto, 1, 0, j->len[i]);
+			v = r.ret >= 0 ? r.ret : DROP_POLICY;
+			st = r.stage;
+			j->probes += r.probes;
+		} else {
+			/* bpf_netdev.c:203-211: no HOST_ID exception on IPv6 */
+			uint32_t src = cfg->ingress_src_identity;
+			struct pol_res r;
+			if (src < cfg->health_id) {
+				const uint8_t *info = ipcache6(c, sa);
+				j->probes += 1;
+				if (info) {
+					uint32_t label;
+					memcpy(&label, info, 4);
+					if (label && label != cfg->cluster_id)
+						src = label;
+				}
+			}
+			/* IPv6 ingress passes is_fragment = false (bpf_lxc.c:787-789) */
+			r = policy_access(h, src, j->dport[i], proto, 0, 0, j->len[i]);
+			v = r.ret >= 0 ? r.ret : DROP_POLICY;
+			id = src;
+			st = r.stage;
+			j->probes += r.probes;
+		}
+		j->verdict[i] = v;
+		if (j->identity)
+			j->identity[i] = id;
+		if (j->stage)
+			j->stage[i] = (uint8_t)st;
+		{
+			uint32_t reason = v < 0 ? (uint32_t)(-v) & 0xff : 0;
+			uint64_t *m = &j->metrics[(reason * 4 + dir) * 2];
+			m[0] += 1;
+			m[1] += j->len[i];
+		}
+	}
+	return NULL;
+}
+
+int or_classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
+{
+	struct cls6_job *jobs;
+	pthread_t *th;
+	uint64_t probes = 0;
+	if (nthreads <= 0)
+		nthreads = 1;
+	if ((size_t)nthreads > n && n > 0)
+		nthreads = (int)n;
+	jobs = calloc((size_t)nthreads, sizeof(*jobs));
+	th = calloc((size_t)nthreads, sizeof(*th));
+	for (int t = 0; t < nthreads; t++) {
+		struct cls6_job *j = &jobs[t];
+		j->c = c;
+		j->lo = n * (size_t)t / (size_t)nthreads;
+		j->hi = n * (size_t)(t + 1) / (size_t)nthreads;
+		j->s6 = saddr16;
+		j->d6 = daddr16;
+		j->len = len;
+		j->dport = dport;
+		j->ep = ep;
+		j->proto = proto;
+		j->flags = flags;
+		j->verdict = verdict;
+		j->identity = identity;
+		j->stage = stage;
+		if (nthreads == 1)
+			cls6_worker(j);
+		else
+			pthread_create(&th[t], NULL, cls6_worker, j);
 	}
 	for (int t = 0; t < nthreads; t++) {
 		if (nthreads > 1)

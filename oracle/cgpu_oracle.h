@@ -31,6 +31,7 @@ typedef struct or_config {
 	uint32_t ingress_src_identity; /* identity handed to handle_ipv4 */
 	int ingress_secctx_world;      /* non-FROM_HOST netdev: label = WORLD_ID */
 	int dyn4, fix4, dyn6, fix6;    /* CIDR{4,6}_LPM_PREFILTER / CIDR{4,6}_FILTER */
+	uint8_t router_ip[16];         /* ROUTER_IP (node_config.h:30) */
 } or_config;
 
 or_ctx *or_create(void);
@@ -64,6 +65,12 @@ int or_endpoint_delete(or_ctx *c, const void *key20);
  * stage / identity may be NULL.  nthreads <= 0 means 1.
  */
 int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum);
+
+/* Stateless IPv6 classification: addresses 16 bytes per tuple. */
+int or_classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
 		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
 		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
 		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum);

@@ -54,6 +54,10 @@ def load_ref():
                                     C.c_uint32, C.c_int, C.c_int, C.c_uint32, C.c_int, u32p, ip,
                                     ip, ip]
     pol.ref_constants.argtypes = [u32p, C.c_int]
+    pol.ref_classify_v6.argtypes = [C.c_void_p, C.c_void_p, C.c_uint16, C.c_uint8, C.c_uint8,
+                                    C.c_uint32, C.c_int, C.c_int, C.c_uint32, u32p, ip, ip, ip]
+    pol.ref_router_ip.argtypes = [C.c_void_p]
+    pol.ref_router_ip.restype = None
     xdp.ref_xdp_reset.restype = None
     xdp.ref_xdp_cidr_update.argtypes = [C.c_int, C.c_void_p]
     xdp.ref_xdp_endpoint_update.argtypes = [C.c_void_p]
@@ -334,6 +338,111 @@ def gen_classify_fixture(pol, rng):
                 configs=np.array(CONFIGS, np.int64), **{"t_" + k: v for k, v in t.items()}, **out)
 
 
+# ------------------------------------------------------------- classify v6
+CONFIGS6 = [(1, 0), (0, 2), (1, 256), (1, 3)]  # (ct_proto_gate, ingress_src_identity)
+
+
+def gen_classify_v6_fixture(pol, rng):
+    router = C.create_string_buffer(16)
+    pol.ref_router_ip(router)
+    router = np.frombuffer(router.raw, np.uint8).copy()
+    ikeys, ivals = gen_ipcache_entries(rng, 60, 500, static=False)
+    keep = ikeys["prefixlen"] > 32 + 4
+    ikeys, ivals = ikeys[keep], ivals[keep]
+    # entries inside the router's /64 (cluster range) and the router itself
+    extra_k, extra_v = [], []
+    for ln, lab in ((64, 0), (96, 3), (112, 5000), (128, 1)):
+        k = np.zeros((), L.IPCACHE_KEY)
+        k["family"] = L.ENDPOINT_KEY_IPV6
+        k["prefixlen"] = 32 + ln
+        a = router.copy()
+        a[12:] = rng.integers(0, 256, 4, dtype=np.uint8)
+        k["ip"][:] = a
+        extra_k.append(k)
+        extra_v.append(L.remote_info(lab))
+    ikeys = np.concatenate([np.array(extra_k, L.IPCACHE_KEY), ikeys])
+    ivals = np.concatenate([np.array(extra_v, L.REMOTE_ENDPOINT_INFO), ivals])
+    v6 = ikeys["family"] == L.ENDPOINT_KEY_IPV6
+    hot = rng.choice(np.nonzero(v6)[0], 40, replace=False)
+    labels = np.unique(ivals["sec_label"][hot])
+    pk, pe, pep = [], [], []
+    for ep in range(3):
+        seen = set()
+        for _ in range(120):
+            kind = rng.integers(0, 3)
+            ident = int(rng.choice(labels)) if rng.random() < 0.8 else int(rng.choice(IDENTS))
+            port = int(rng.choice(PORTS[1:6])) if rng.random() < 0.7 else int(rng.choice(PORTS))
+            proto = int(rng.choice(np.array([6, 17, 58, 6, 6, 132], np.uint8)))
+            egress = int(rng.integers(0, 2))
+            if kind == 1:
+                port, proto = 0, 0
+            elif kind == 2:
+                ident = 0
+            k = L.policy_key(ident, port, proto, egress)
+            if b(k) in seen:
+                continue
+            seen.add(b(k))
+            pk.append(k)
+            pe.append(L.policy_entry(int(rng.integers(1, 65536)) if rng.random() < 0.1 else 0))
+            pep.append(ep)
+    pk, pe, pep = (np.array(pk, L.POLICY_KEY), np.array(pe, L.POLICY_ENTRY),
+                   np.array(pep, np.uint16))
+    n = 5000
+
+    def addrs():
+        a = np.where(rng.random((n, 1)) < 0.5, v6_queries_near(rng, ikeys[hot], n),
+                     v6_queries_near(rng, ikeys, n))
+        inr = rng.random(n) < 0.1
+        r = np.tile(router, (n, 1))
+        r[:, 8:] = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+        a[inr] = r[inr]
+        return a.astype(np.uint8)
+
+    t = {
+        "saddr": addrs(), "daddr": addrs(),
+        "dport": np.array([L.htons(int(p)) for p in np.where(
+            rng.random(n) < 0.9, rng.choice(PORTS[:6], n), rng.integers(0, 65536, n))], np.uint16),
+        "proto": rng.choice(np.array([6, 6, 6, 6, 17, 17, 58, 58, 1, 47, 0], np.uint8), n),
+        "flags": ((rng.random(n) < 0.5).astype(np.uint8) |
+                  ((rng.random(n) < 0.08).astype(np.uint8) << 1)),
+        "len": rng.integers(0, 70000, n).astype(np.uint32),
+        "ep": rng.integers(0, 4, n).astype(np.uint16),
+    }
+    out = {}
+    for ci, (gate, src) in enumerate(CONFIGS6):
+        pol.ref_reset()
+        for k, v in zip(ikeys, ivals):
+            pol.ref_ipcache_update(b(k), b(v))
+        for k, e, ep in zip(pk, pe, pep):
+            pol.ref_policy_update(int(ep), b(k), b(e))
+        verdict = np.empty(n, np.int32)
+        ident = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        nprobes = np.empty(n, np.int32)
+        naddr = np.empty(n, np.int32)
+        idv, st, npb, na = C.c_uint32(), C.c_int(), C.c_int(), C.c_int()
+        for i in range(n):
+            verdict[i] = pol.ref_classify_v6(
+                t["saddr"][i].tobytes(), t["daddr"][i].tobytes(), int(t["dport"][i]),
+                int(t["proto"][i]), int(t["flags"][i]), int(t["len"][i]), int(t["ep"][i]),
+                gate, src, C.byref(idv), C.byref(st), C.byref(npb), C.byref(na))
+            ident[i], stage[i], nprobes[i], naddr[i] = idv.value, st.value, npb.value, na.value
+        final = np.zeros(len(pk), L.POLICY_ENTRY)
+        for i, (k, ep) in enumerate(zip(pk, pep)):
+            buf = C.create_string_buffer(24)
+            assert pol.ref_policy_read(int(ep), b(k), buf) == 0
+            final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+        out[f"c{ci}_verdict"] = verdict
+        out[f"c{ci}_identity"] = ident
+        out[f"c{ci}_stage"] = stage
+        out[f"c{ci}_nprobes"] = nprobes
+        out[f"c{ci}_naddr"] = naddr
+        out[f"c{ci}_final_entries"] = final
+    return dict(router_ip=router, ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe,
+                pol_ep=pep, configs=np.array(CONFIGS6, np.int64),
+                **{"t_" + k: v for k, v in t.items()}, **out)
+
+
 # --------------------------------------------------------------------- xdp
 def eth(ethertype, payload):
     return bytes(6) + bytes([2, 0, 0, 0, 0, 1]) + ethertype.to_bytes(2, "big") + payload
@@ -475,6 +584,7 @@ def main():
     manifest["files"]["ipcache_lpm.npz"] = save("ipcache_lpm.npz", gen_ipcache_fixture(pol, rng))
     manifest["files"]["classify_v4.npz"] = save("classify_v4.npz", gen_classify_fixture(pol, rng))
     manifest["files"]["xdp_prefilter.npz"] = save("xdp_prefilter.npz", gen_xdp_fixture(xdp, rng))
+    manifest["files"]["classify_v6.npz"] = save("classify_v6.npz", gen_classify_v6_fixture(pol, rng))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -22,6 +22,7 @@ class OrConfig(C.Structure):
         ("ipv4_cluster_range", C.c_uint32), ("ct_proto_gate", C.c_int),
         ("ingress_src_identity", C.c_uint32), ("ingress_secctx_world", C.c_int),
         ("dyn4", C.c_int), ("fix4", C.c_int), ("dyn6", C.c_int), ("fix6", C.c_int),
+        ("router_ip", C.c_uint8 * 16),
     ]
 
 
@@ -56,6 +57,7 @@ def lib():
         L.or_endpoint_update.argtypes = [vp, vp]
         L.or_endpoint_delete.argtypes = [vp, vp]
         L.or_classify_v4.argtypes = [vp, sz] + [vp] * 10 + [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_classify_v6.argtypes = [vp, sz] + [vp] * 10 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_prefilter_v4.argtypes = [vp, sz, vp, vp, vp, vp, C.c_int, C.POINTER(C.c_uint64)]
         L.or_prefilter_v6.argtypes = [vp, sz, vp, vp, vp, vp, C.c_int, C.POINTER(C.c_uint64)]
         L.or_metrics_read.argtypes = [vp, vp]
@@ -83,6 +85,9 @@ class Oracle:
 
     def configure(self, **kw):
         for k, v in kw.items():
+            if k == "router_ip":
+                self.cfg.router_ip[:] = bytes(v)
+                continue
             setattr(self.cfg, k, v)
         self.L.or_set_config(self.h, C.byref(self.cfg))
 
@@ -143,6 +148,19 @@ class Oracle:
             ("saddr", np.uint32), ("daddr", np.uint32), ("dport", np.uint16),
             ("proto", np.uint8), ("flags", np.uint8), ("len", np.uint32), ("ep", np.uint16))]
         self.L.or_classify_v4(self.h, n, *[_p(a) for a in arrs], _p(verdict), _p(identity),
+                              _p(stage), nthreads, C.byref(probes))
+        return verdict, identity, stage, probes.value
+
+    def classify_v6(self, t, nthreads=1):
+        n = len(t["flags"])
+        verdict = np.empty(n, np.int32)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint8), ("daddr", np.uint8), ("dport", np.uint16),
+            ("proto", np.uint8), ("flags", np.uint8), ("len", np.uint32), ("ep", np.uint16))]
+        self.L.or_classify_v6(self.h, n, *[_p(a) for a in arrs], _p(verdict), _p(identity),
                               _p(stage), nthreads, C.byref(probes))
         return verdict, identity, stage, probes.value
 

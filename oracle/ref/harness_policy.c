@@ -283,3 +283,71 @@ int ref_constants(uint32_t *out, int n)
 		out[i] = c[i];
 	return k;
 }
+
+/*
+ * One stateless IPv6 tuple.  Glue restated from the callers:
+ *  gate: ct_lookup6 accepts ICMPv6/TCP/UDP only (bpf/lib/conntrack.h:330-378).
+ *  Egress (bpf_lxc.c:170-191): dstID = ipcache6(daddr) sec_label if nonzero,
+ *    else CLUSTER_ID if ipv6_match_prefix_64(daddr, ROUTER_IP), else WORLD_ID;
+ *    verdict = policy_can_egress6(dstID, dport, nexthdr).
+ *  Ingress (bpf_netdev.c:203-211, then bpf_lxc.c:787-789): if
+ *    identity_is_reserved(src), ipcache6(saddr) replaces it when sec_label
+ *    is nonzero and not CLUSTER_ID (no HOST_ID exception on v6); the label
+ *    is the resolved src (FROM_HOST form, :222); IPv6 passes is_fragment =
+ *    false.
+ */
+int ref_classify_v6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t dport_be,
+		    uint8_t proto, uint8_t flags, uint32_t len, int ep, int cfg_gate,
+		    uint32_t cfg_src_identity, uint32_t *identity_out, int *stage_out,
+		    int *nprobes_out, int *naddr_out)
+{
+	int egress = flags & 1;
+	int ret, probes = 0, hit = 0;
+	uint32_t label, tun;
+	union v6addr sa, da;
+	union v6addr router_ip;
+	BPF_V6(router_ip, ROUTER_IP);
+
+	memcpy(&sa, saddr16, 16);
+	memcpy(&da, daddr16, 16);
+	*naddr_out = 0;
+	if (cfg_gate && proto != IPPROTO_ICMPV6 && proto != IPPROTO_TCP &&
+	    proto != IPPROTO_UDP) {
+		*identity_out = 0;
+		*stage_out = 4;
+		*nprobes_out = 0;
+		return DROP_CT_UNKNOWN_PROTO;
+	}
+	if (egress) {
+		uint32_t dst_id;
+		*naddr_out = 1;
+		if (ref_ipcache_lookup6(daddr16, &label, &tun) && label)
+			dst_id = label;
+		else if (ipv6_match_prefix_64(&da, &router_ip))
+			dst_id = CLUSTER_ID;
+		else
+			dst_id = WORLD_ID;
+		ret = ref_policy_egress(ep, dst_id, dport_be, proto, len, &probes, &hit);
+		*identity_out = dst_id;
+	} else {
+		uint32_t src = cfg_src_identity;
+		if (identity_is_reserved(src)) {
+			*naddr_out = 1;
+			if (ref_ipcache_lookup6(saddr16, &label, &tun) && label &&
+			    label != CLUSTER_ID)
+				src = label;
+		}
+		ret = ref_policy_ingress(ep, src, dport_be, proto, 0, len, &probes, &hit);
+		*identity_out = src;
+	}
+	*nprobes_out = probes;
+	*stage_out = hit;
+	return ret;
+}
+
+void ref_router_ip(uint8_t *out16)
+{
+	union v6addr router_ip;
+	BPF_V6(router_ip, ROUTER_IP);
+	memcpy(out16, &router_ip, 16);
+}

@@ -251,3 +251,24 @@ def test_oracle_table_ops_errno():
     bad["prefixlen"] = 161
     assert o.ipcache_update(bad, L.remote_info(5)) == -22
     assert o.ipcache_delete(L.ipcache_key("10.0.0.0/8")) == -2
+
+
+@pytest.mark.parametrize("ci", range(4))
+def test_classify_v6_vs_reference(golden, ci):
+    g = golden("classify_v6.npz")
+    gate, src = (int(x) for x in g["configs"][ci])
+    o = Oracle(ct_proto_gate=gate, ingress_src_identity=src, router_ip=g["router_ip"].tobytes())
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert o.ipcache_update(k, v) == 0
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert o.policy_update(int(ep), k, e) == 0
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    v, idt, st, probes = o.classify_v6(t, nthreads=3)
+    np.testing.assert_array_equal(v, g[f"c{ci}_verdict"])
+    np.testing.assert_array_equal(idt, g[f"c{ci}_identity"])
+    np.testing.assert_array_equal(st, g[f"c{ci}_stage"])
+    assert probes == int(g[f"c{ci}_nprobes"].sum() + g[f"c{ci}_naddr"].sum())
+    for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
+        rc, raw = o.policy_lookup(int(ep), k)
+        got = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (got["packets"], got["bytes"]) == (fe["packets"], fe["bytes"])
