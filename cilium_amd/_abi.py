@@ -38,6 +38,11 @@ class TuplesV4(C.Structure):
                 ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")]
 
 
+class TuplesV6(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")]
+
+
 vp, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
 
 # name -> (restype, argtypes)
@@ -68,6 +73,7 @@ PROTOS = {
     "cgpu_commit": (i32, [vp, C.POINTER(u64)]),
     "cgpu_table_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
+    "cgpu_classify_v6": (i32, [vp, C.POINTER(TuplesV6), sz, vp, vp, vp, vp]),
     "cgpu_prefilter_v4": (i32, [vp, vp, vp, vp, sz, vp, vp]),
     "cgpu_prefilter_v6": (i32, [vp, vp, vp, vp, sz, vp, vp]),
     "cgpu_counter_delta_bytes": (sz, [vp]),

@@ -239,6 +239,9 @@ CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
 	c->prefilter_fix4 = c->prefilter_dyn4 = 1; /* bpf/filter_config.h */
 	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
 	c->ingress_src_identity = 0;
+	static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1,
+					   0x0, 0x1, 0x0, 0x0}; /* ROUTER_IP, bpf/node_config.h:30 */
+	memcpy(c->ipv6_router_ip, router, 16);
 }
 
 CGPU_EXPORT const char *cgpu_last_error(void) { return g_last_error.c_str(); }
@@ -887,8 +890,9 @@ void build_set4(const std::vector<uint32_t> &keys, Set4Build &b)
 	}
 }
 
-/* keys: 4 u32 words + tag (tag goes to `used` bits 8..15; hashed as salt) */
-void build_set16(const std::vector<std::array<uint32_t, 5>> &keys, Set16Build &b)
+/* keys: 4 u32 words + tag + entry (tag goes to `used` bits 8..15 and is
+ * hashed as salt; entry goes to pad[0]) */
+void build_set16(const std::vector<std::array<uint32_t, 6>> &keys, Set16Build &b)
 {
 	uint32_t nb = next_pow2(std::max<uint64_t>(8, keys.size() + 1));
 	b.slots.assign((size_t)nb * 2, set16_slot{});
@@ -905,6 +909,7 @@ void build_set16(const std::vector<std::array<uint32_t, 5>> &keys, Set16Build &b
 				set16_slot v{};
 				memcpy(v.a, k.data(), 16);
 				v.used = 1u | (k[4] << 8);
+				v.pad[0] = k[5];
 				s[j] = v;
 				break;
 			}
@@ -931,78 +936,126 @@ void mask_v6(const uint8_t *addr, uint32_t len, uint32_t out[4])
 	memcpy(out, m, 16);
 }
 
-struct Pf6Build {
-	std::vector<uint16_t> root;
+struct Rank6 {
+	uint32_t rank; /* apply order: < 32 static-part entries, else 32 + len */
+	uint32_t len;  /* IP prefix length 0..128 (static entries: 0) */
+	std::array<uint8_t, 16> addr;
+	uint32_t label;
+};
+
+struct V6Build {
+	std::vector<uint32_t> root; /* 2 x 65536: {row, short} */
 	std::vector<uint32_t> masks;
+	std::vector<uint32_t> vals;
 	Set16Build set;
 	bool any = false;
 };
 
-/* prefilter v6 any-match set (bpf_xdp.c:132-156): dyn6 (if
- * CIDR6_LPM_PREFILTER) + fix6 keys with prefixlen 128. */
-void build_pf6(const cgpu_ctx *c, Pf6Build &b)
+uint32_t v6_encode(std::vector<uint32_t> &vals, uint32_t label)
 {
-	b.any = false;
-	if (!c->cfg.prefilter_fix6)
+	if (label < (1u << DIR_TAG_SHIFT))
+		return DIR_TAG_DIRECT | label;
+	vals.push_back(label);
+	return DIR_TAG_INDIRECT | (uint32_t)(vals.size() - 1);
+}
+
+/* Longest-prefix table over (len, address) candidates; see tables.h v6_lpm. */
+void build_v6(std::vector<Rank6> cand, V6Build &b)
+{
+	b.any = !cand.empty();
+	if (!b.any)
 		return;
-	std::set<std::pair<uint32_t, std::array<uint8_t, 16>>> pfx; /* (len, masked) */
-	if (c->cfg.prefilter_dyn6)
-		for (auto &kv : c->dyn6)
-			pfx.insert({kv.first.plen, kv.first.data});
-	for (auto &k : c->fix6) {
-		uint32_t plen;
-		memcpy(&plen, k.data(), 4);
-		if (plen != 128)
-			continue;
-		std::array<uint8_t, 16> a;
-		memcpy(a.data(), k.data() + 4, 16);
-		pfx.insert({128, a});
-	}
-	if (pfx.empty())
-		return;
-	b.any = true;
+	std::stable_sort(cand.begin(), cand.end(),
+			 [](const Rank6 &x, const Rank6 &y) { return x.rank < y.rank; });
+	std::vector<uint32_t> shortv(65536, 0);
 	std::vector<std::array<uint32_t, 4>> rootmask(65536, std::array<uint32_t, 4>{0, 0, 0, 0});
-	std::vector<uint8_t> covered(65536, 0);
-	std::vector<std::array<uint32_t, 5>> keys;
-	for (auto &p : pfx) {
-		uint32_t len = p.first;
-		uint32_t top = (uint32_t)p.second[0] << 8 | p.second[1];
-		if (len <= 16) {
-			uint32_t cnt = 1u << (16 - len);
-			uint32_t base = len == 0 ? 0 : (top & ~(cnt - 1));
-			for (uint32_t r = base; r < base + cnt; r++)
-				covered[r] = 1;
+	std::map<std::pair<uint32_t, std::array<uint32_t, 4>>, uint32_t> longer; /* (len, masked) */
+	b.vals.clear();
+	for (auto &c : cand) {
+		uint32_t enc = v6_encode(b.vals, c.label);
+		uint32_t top = (uint32_t)c.addr[0] << 8 | c.addr[1];
+		if (c.len <= 16) {
+			uint32_t cnt = 1u << (16 - c.len);
+			uint32_t base = c.len == 0 ? 0 : (top & ~(cnt - 1));
+			std::fill(shortv.begin() + base, shortv.begin() + base + cnt, enc);
 			continue;
 		}
-		uint32_t bit = len - 17;
+		uint32_t bit = c.len - 17;
 		rootmask[top][bit / 32] |= 1u << (bit % 32);
-		std::array<uint32_t, 5> k;
-		uint32_t w[4];
-		mask_v6(p.second.data(), len, w);
-		memcpy(k.data(), w, 16);
-		k[4] = len;
-		keys.push_back(k);
+		std::array<uint32_t, 4> w;
+		mask_v6(c.addr.data(), c.len, w.data());
+		longer[{c.len, w}] = enc; /* canonical keys are unique; later rank wins */
 	}
-	std::map<std::array<uint32_t, 4>, uint16_t> ids;
-	b.masks.assign(4, 0); /* row 0: nothing */
+	std::map<std::array<uint32_t, 4>, uint32_t> ids;
+	b.masks.assign(4, 0); /* row 0: no lengths */
 	ids[{0, 0, 0, 0}] = 0;
-	b.root.assign(65536, 0);
+	b.root.assign(2 * 65536, 0);
 	for (uint32_t r = 0; r < 65536; r++) {
-		if (covered[r]) {
-			b.root[r] = V6_ROOT_COVERED;
-			continue;
-		}
 		auto it = ids.find(rootmask[r]);
+		uint32_t id;
 		if (it == ids.end()) {
-			uint16_t id = (uint16_t)(b.masks.size() / 4);
+			id = (uint32_t)(b.masks.size() / 4);
 			ids[rootmask[r]] = id;
 			b.masks.insert(b.masks.end(), rootmask[r].begin(), rootmask[r].end());
-			b.root[r] = id;
 		} else {
-			b.root[r] = it->second;
+			id = it->second;
 		}
+		b.root[2 * r] = id;
+		b.root[2 * r + 1] = shortv[r];
+	}
+	std::vector<std::array<uint32_t, 6>> keys;
+	keys.reserve(longer.size());
+	for (auto &kv : longer) {
+		auto &w = kv.first.second;
+		keys.push_back({w[0], w[1], w[2], w[3], kv.first.first, kv.second});
 	}
 	build_set16(keys, b.set);
+}
+
+/* prefilter v6 any-match set (bpf_xdp.c:132-156): dyn6 (if
+ * CIDR6_LPM_PREFILTER) + fix6 keys with prefixlen 128. */
+void build_pf6(const cgpu_ctx *c, V6Build &b)
+{
+	std::vector<Rank6> cand;
+	if (c->cfg.prefilter_fix6) {
+		if (c->cfg.prefilter_dyn6)
+			for (auto &kv : c->dyn6)
+				cand.push_back(Rank6{kv.first.plen, kv.first.plen, kv.first.data, 1});
+		for (auto &k : c->fix6) {
+			uint32_t plen;
+			memcpy(&plen, k.data(), 4);
+			if (plen != 128)
+				continue;
+			Rank6 r{128, 128, {}, 1};
+			memcpy(r.addr.data(), k.data() + 4, 16);
+			cand.push_back(r);
+		}
+	}
+	build_v6(std::move(cand), b);
+}
+
+/* ipcache -> v6 LPM for IPv6 lookups (ipcache_lookup6, eps.h:56-66): a
+ * lookup key is {prefixlen 160, pad 0, family 2, ip6}; entries ending inside
+ * the static part rank below /0, exactly as build_ipc4. */
+void build_ipc6(const cgpu_ctx *c, V6Build &b)
+{
+	static const uint8_t static_v6[4] = {0, 0, 0, 2};
+	std::vector<Rank6> cand;
+	for (auto &kv : c->ipc) {
+		const IpcEntry &e = kv.second;
+		uint32_t p = e.raw.prefixlen;
+		const uint8_t *data = (const uint8_t *)&e.raw + 4;
+		if (!prefix_eq(data, static_v6, std::min<uint32_t>(p, 32)))
+			continue;
+		Rank6 r{p, 0, {}, e.val.sec_label};
+		if (p >= 32) {
+			r.len = p - 32;
+			/* canonical (masked) address bits from the mirror key */
+			memcpy(r.addr.data(), kv.first.data.data() + 4, 16);
+		}
+		cand.push_back(r);
+	}
+	build_v6(std::move(cand), b);
 }
 
 } // namespace
@@ -1019,12 +1072,13 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	PolBuild pol;
 	Set4Build ep4;
 	Set16Build ep6;
-	Pf6Build pf6;
+	V6Build pf6, ipc6;
 	build_ipc4(c, ipc4);
+	build_ipc6(c, ipc6);
 	bool have_pf4 = build_pf4(c, pf4);
 	build_pol(c, pol);
 	std::vector<uint32_t> e4;
-	std::vector<std::array<uint32_t, 5>> e6;
+	std::vector<std::array<uint32_t, 6>> e6;
 	for (auto &k : c->lxc) {
 		const cgpu_endpoint_key *ek = (const cgpu_endpoint_key *)k.data();
 		if (ek->pad4 || ek->pad5)
@@ -1034,7 +1088,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 		if (ek->family == 1 && !w[1] && !w[2] && !w[3])
 			e4.push_back(w[0]);
 		else if (ek->family == 2)
-			e6.push_back({w[0], w[1], w[2], w[3], 0});
+			e6.push_back({w[0], w[1], w[2], w[3], 0, 0});
 	}
 	build_set4(e4, ep4);
 	build_set16(e6, ep6);
@@ -1052,12 +1106,19 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	}
 	size_t o_e4 = ar.add(ep4.slots.data(), ep4.slots.size() * sizeof(set4_slot));
 	size_t o_e6 = ar.add(ep6.slots.data(), ep6.slots.size() * sizeof(set16_slot));
-	size_t o_r6 = 0, o_m6 = 0, o_s6 = 0;
-	if (pf6.any) {
-		o_r6 = ar.add(pf6.root.data(), pf6.root.size() * 2);
-		o_m6 = ar.add(pf6.masks.data(), pf6.masks.size() * 4);
-		o_s6 = ar.add(pf6.set.slots.data(), pf6.set.slots.size() * sizeof(set16_slot));
-	}
+	struct V6Offs {
+		size_t root = 0, masks = 0, vals = 0, set = 0;
+	} o_pf6, o_ipc6;
+	auto add_v6 = [&](V6Build &v, V6Offs &o) {
+		if (!v.any)
+			return;
+		o.root = ar.add(v.root.data(), v.root.size() * 4);
+		o.masks = ar.add(v.masks.data(), v.masks.size() * 4);
+		o.vals = ar.add(v.vals.data(), v.vals.size() * 4);
+		o.set = ar.add(v.set.slots.data(), v.set.slots.size() * sizeof(set16_slot));
+	};
+	add_v6(pf6, o_pf6);
+	add_v6(ipc6, o_ipc6);
 	std::vector<uint32_t> init_slot;
 	std::vector<uint64_t> init_pk, init_by;
 	for (auto &s : c->slot_inits) {
@@ -1099,11 +1160,18 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 			       nullptr, (uint32_t)(pf4.tbl8.size() / 256), 0};
 	s.ep4 = addr_set4{(const set4_slot *)(arena + o_e4), ep4.mask, ep4.max_probe};
 	s.ep6 = addr_set16{(const set16_slot *)(arena + o_e6), ep6.mask, ep6.max_probe};
-	if (pf6.any)
-		s.pf6 = v6_anyset{(const uint16_t *)(arena + o_r6), (const uint32_t *)(arena + o_m6),
-				  addr_set16{(const set16_slot *)(arena + o_s6), pf6.set.mask,
-					     pf6.set.max_probe},
-				  (uint32_t)(pf6.masks.size() / 4)};
+	auto mk_v6 = [&](const V6Build &v, const V6Offs &o) {
+		v6_lpm t{};
+		if (v.any)
+			t = v6_lpm{(const uint2 *)(arena + o.root), (const uint32_t *)(arena + o.masks),
+				   (const uint32_t *)(arena + o.vals),
+				   addr_set16{(const set16_slot *)(arena + o.set), v.set.mask, v.set.max_probe},
+				   (uint32_t)(v.masks.size() / 4)};
+		return t;
+	};
+	s.pf6 = mk_v6(pf6, o_pf6);
+	s.ipc6 = mk_v6(ipc6, o_ipc6);
+	memcpy(s.router_ip64, c->cfg.ipv6_router_ip, 8);
 	s.pf4_enabled = c->cfg.prefilter_fix4;
 	s.pf6_enabled = c->cfg.prefilter_fix6;
 	s.world_id = c->cfg.world_id;
@@ -1187,6 +1255,27 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
 	return 0;
 }
 
+CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n, int32_t *verdict,
+				 uint32_t *identity, uint8_t *stage, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
+			 !t->ep || !verdict || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (((uintptr_t)t->saddr | (uintptr_t)t->daddr) & 15)
+		return fail(-EINVAL, "v6 address columns must be 16-byte aligned");
+	if (!n)
+		return 0;
+	classify_v6_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
+			   verdict, identity, stage, delta, (uint64_t)n};
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_classify_v6(s, a, (hipStream_t)stream));
+	return 0;
+}
+
 CGPU_EXPORT int cgpu_prefilter_v4(cgpu_ctx *c, const uint32_t *saddr, const uint32_t *daddr,
 				  const uint8_t *flags, size_t n, uint8_t *verdict, void *stream)
 {
@@ -1213,6 +1302,8 @@ CGPU_EXPORT int cgpu_prefilter_v6(cgpu_ctx *c, const uint8_t *saddr, const uint8
 		return r;
 	if (n && (!saddr || !daddr || !flags || !verdict))
 		return fail(-EINVAL, "null column");
+	if (((uintptr_t)saddr | (uintptr_t)daddr) & 15)
+		return fail(-EINVAL, "v6 address columns must be 16-byte aligned");
 	if (!n)
 		return 0;
 	prefilter_args a{nullptr, nullptr, saddr, daddr, flags, verdict, (uint64_t)n};

@@ -108,6 +108,107 @@ __device__ __forceinline__ bool set16_has(const addr_set16 &t, uint4 a, uint32_t
 	return false;
 }
 
+/* Resolve a 16-byte-key probe whose first bucket is loaded: returns the
+ * slot's entry word (pad[0], nonzero for prefix sets) or 0 on a miss. */
+__device__ __forceinline__ uint32_t set16_resolve(const addr_set16 &t, const uint4 (&first)[4],
+						  uint32_t b, uint4 key, uint32_t want)
+{
+	uint4 k0 = first[0], m0 = first[1], k1 = first[2], m1 = first[3];
+	for (uint32_t p = 0;;) {
+		if (!(m0.x & 1u))
+			return 0;
+		if (m0.x == want && k0.x == key.x && k0.y == key.y && k0.z == key.z && k0.w == key.w)
+			return m0.y;
+		if (!(m1.x & 1u))
+			return 0;
+		if (m1.x == want && k1.x == key.x && k1.y == key.y && k1.z == key.z && k1.w == key.w)
+			return m1.y;
+		if (++p >= t.max_probe)
+			return 0;
+		b = (b + 1) & t.bucket_mask;
+		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
+		k0 = bk[0];
+		m0 = bk[1];
+		k1 = bk[2];
+		m1 = bk[3];
+	}
+}
+
+__device__ __forceinline__ uint4 mask6(uint4 w, uint32_t len)
+{
+	uint32_t m[4];
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		int bits = (int)len - 32 * k;
+		uint32_t mh = bits <= 0 ? 0u : (bits >= 32 ? 0xFFFFFFFFu : (0xFFFFFFFFu << (32 - bits)));
+		m[k] = bswap32(mh);
+	}
+	return make_uint4(w.x & m[0], w.y & m[1], w.z & m[2], w.w & m[3]);
+}
+
+/* IPv6 longest-prefix lookup (tables.h v6_lpm): the prefix lengths present
+ * under the address's /16 are probed longest first, four independent
+ * bucket loads in flight per round; the first hit is the longest match.
+ * Returns the DIR-encoded entry (0 = no match). */
+__device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
+{
+	if (!t.root)
+		return 0;
+	const uint32_t top = ((a.x & 0xFFu) << 8) | ((a.x >> 8) & 0xFFu);
+	const uint2 r = t.root[top];
+	if (r.x) {
+		const uint4 m = reinterpret_cast<const uint4 *>(t.masks)[r.x];
+		uint64_t hi = ((uint64_t)m.w << 32) | m.z, lo = ((uint64_t)m.y << 32) | m.x;
+		while (hi | lo) {
+			uint32_t L[4];
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				uint32_t len = 0;
+				if (hi) {
+					int bit = 63 - __clzll(hi);
+					hi &= ~(1ull << bit);
+					len = 17u + 64u + (uint32_t)bit;
+				} else if (lo) {
+					int bit = 63 - __clzll(lo);
+					lo &= ~(1ull << bit);
+					len = 17u + (uint32_t)bit;
+				}
+				L[j] = len;
+			}
+			uint4 key[4], bk[4][4];
+			uint32_t bi[4];
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				if (L[j]) {
+					key[j] = mask6(a, L[j]);
+					bi[j] = hash16(key[j].x, key[j].y, key[j].z, key[j].w, L[j]) &
+						t.set.bucket_mask;
+					const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) +
+							 (size_t)bi[j] * 4u;
+#pragma unroll
+					for (int k = 0; k < 4; k++)
+						bk[j][k] = p[k];
+				}
+			}
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				if (L[j]) {
+					uint32_t e = set16_resolve(t.set, bk[j], bi[j], key[j], 1u | (L[j] << 8));
+					if (e)
+						return e;
+				}
+			}
+		}
+	}
+	return r.y;
+}
+
+__device__ __forceinline__ uint32_t entry_label(const uint32_t *vals, uint32_t e)
+{
+	uint32_t p = e & DIR_PAYLOAD_MASK;
+	return (e & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? vals[p] : p;
+}
+
 template <typename T> __device__ __forceinline__ T wave_sum(T v)
 {
 #pragma unroll
@@ -174,8 +275,21 @@ __device__ __forceinline__ int pol_resolve(const pol_table &t, const pol_bucket 
  *           chain shrinks from up to 5 loads to 2-3, at the price of reading
  *           buckets the reference would not have probed.
  */
-template <int SPEC>
-__global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify_v4_args a)
+struct cls_args {
+	const void *saddr, *daddr; /* u32 (v4) or uint4 (v6) per tuple */
+	const uint16_t *dport;
+	const uint8_t *proto, *flags;
+	const uint32_t *len;
+	const uint16_t *ep;
+	int32_t *verdict;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t *delta;
+	uint64_t n;
+};
+
+template <int V6, int SPEC>
+__global__ __launch_bounds__(BLOCK) void k_classify(cgpu_snapshot s, cls_args a)
 {
 	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
 	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
@@ -187,19 +301,21 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify
 		const uint32_t len = a.len[i];
 		const uint32_t dport = a.dport[i];
 		const uint32_t ep = a.ep[i];
-		const uint32_t sa = a.saddr[i];
-		const uint32_t da = a.daddr[i];
 		const bool egress = fl & 1u;
 		int32_t v;
 		uint32_t id;
 		uint32_t st = 0;
+		/* ct_lookup{4,6} protocol gate: ICMP (v4: 1, v6: 58), TCP, UDP */
+		const bool gated = s.ct_proto_gate && proto != (V6 ? 58u : 1u) && proto != 6u &&
+				   proto != 17u;
 
-		if (s.ct_proto_gate && proto != 1u && proto != 6u && proto != 17u) {
+		if (gated) {
 			v = DROP_CT_UNKNOWN_PROTO;
 			id = 0;
 			st = 4;
 		} else {
-			const bool frag = !egress && ((fl >> 1) & 1u);
+			/* IPv6 passes is_fragment = false (bpf_lxc.c:787-789) */
+			const bool frag = !V6 && !egress && ((fl >> 1) & 1u);
 			const uint32_t eg = egress ? (1u << 24) : 0u;
 			const uint32_t hi4 = dport | (proto << 16) | eg;
 			pol_bucket b3;
@@ -208,24 +324,38 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(cgpu_snapshot s, classify
 				bi3 = pol_hash(0u, hi4, ep) & s.pol.bucket_mask;
 				b3 = pol_load(s.pol, bi3);
 			}
+			uint32_t e, label;
+			bool in_cluster;
+			if (V6) {
+				const uint4 ad = egress ? static_cast<const uint4 *>(a.daddr)[i]
+							: static_cast<const uint4 *>(a.saddr)[i];
+				e = v6_lookup(s.ipc6, ad);
+				label = entry_label(s.ipc6.vals, e);
+				/* ipv6_match_prefix_64(daddr, ROUTER_IP), bpf/lib/ipv6.h:166-175 */
+				in_cluster = ad.x == s.router_ip64[0] && ad.y == s.router_ip64[1];
+			} else {
+				const uint32_t ad = egress ? static_cast<const uint32_t *>(a.daddr)[i]
+							   : static_cast<const uint32_t *>(a.saddr)[i];
+				e = dir_lookup(s.ipc4, ad, &label);
+				in_cluster = (ad & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
+			}
 			if (egress) {
-				uint32_t label;
-				uint32_t e = dir_lookup(s.ipc4, da, &label);
+				/* bpf_lxc.c:488-496 (v4) / :170-187 (v6) */
 				if (e && label)
 					id = label;
-				else if ((da & s.ipv4_cluster_mask) == s.ipv4_cluster_range)
+				else if (in_cluster)
 					id = s.cluster_id;
 				else
 					id = s.world_id;
 			} else {
+				/* bpf_netdev.c:374-398 (v4) / :203-211 (v6, no HOST_ID case).
+				 * The lookup above ran unconditionally; it only decides
+				 * when the handed-in identity is reserved. */
 				uint32_t src = s.ingress_src_identity;
-				if (src < s.health_id) {
-					uint32_t label;
-					uint32_t e = dir_lookup(s.ipc4, sa, &label);
-					if (e && label && label != s.cluster_id && label != s.host_id)
-						src = label;
-				}
-				id = s.ingress_secctx_world ? s.world_id : src;
+				if (src < s.health_id && e && label && label != s.cluster_id &&
+				    (V6 || label != s.host_id))
+					src = label;
+				id = (!V6 && s.ingress_secctx_world) ? s.world_id : src;
 			}
 			uint32_t z = 0;
 			int ctr = -1;
@@ -322,18 +452,6 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilt
 	}
 }
 
-__device__ __forceinline__ uint4 mask6(uint4 w, uint32_t len)
-{
-	uint32_t m[4];
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		int bits = (int)len - 32 * k;
-		uint32_t mh = bits <= 0 ? 0u : (bits >= 32 ? 0xFFFFFFFFu : (0xFFFFFFFFu << (32 - bits)));
-		m[k] = bswap32(mh);
-	}
-	return make_uint4(w.x & m[0], w.y & m[1], w.z & m[2], w.w & m[3]);
-}
-
 /* XDP prefilter IPv6 (bpf/bpf_xdp.c:132-156): any-match over dyn6 + fix6 */
 __global__ __launch_bounds__(BLOCK) void k_prefilter_v6(cgpu_snapshot s, prefilter_args a)
 {
@@ -349,26 +467,7 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v6(cgpu_snapshot s, prefilt
 		} else if (f != 0u) {
 			v = XDP_DROP;
 		} else {
-			bool drop = false;
-			if (s.pf6_enabled && s.pf6.root) {
-				const uint32_t top = ((sa.x & 0xFFu) << 8) | ((sa.x >> 8) & 0xFFu);
-				const uint32_t r = s.pf6.root[top];
-				if (r == V6_ROOT_COVERED) {
-					drop = true;
-				} else if (r) {
-					const uint4 m = reinterpret_cast<const uint4 *>(s.pf6.masks)[r];
-					uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-#pragma unroll
-					for (int k = 0; k < 4; k++) {
-						while (mw[k] && !drop) {
-							uint32_t bit = __builtin_ctz(mw[k]);
-							mw[k] &= mw[k] - 1u;
-							uint32_t len = 17u + 32u * (uint32_t)k + bit;
-							drop = set16_has(s.pf6.set, mask6(sa, len), len);
-						}
-					}
-				}
-			}
+			const bool drop = s.pf6_enabled && v6_lookup(s.pf6, sa) != 0;
 			v = drop ? XDP_DROP : (set16_has(s.ep6, da, 0u) ? XDP_PASS : XDP_DROP);
 		}
 		a.verdict[i] = v;
@@ -418,12 +517,25 @@ static int classify_variant()
 	return v ? atoi(v) : 1;
 }
 
-hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st)
+hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x, hipStream_t st)
 {
+	cls_args a{x.saddr, x.daddr, x.dport, x.proto, x.flags, x.len, x.ep,
+		   x.verdict, x.identity, x.stage, x.delta, x.n};
 	if (classify_variant() == 0)
-		hipLaunchKernelGGL(k_classify_v4<0>, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+		hipLaunchKernelGGL((k_classify<0, 0>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 	else
-		hipLaunchKernelGGL(k_classify_v4<1>, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+		hipLaunchKernelGGL((k_classify<0, 1>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)
+{
+	cls_args a{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len, x.ep,
+		   x.verdict, x.identity, x.stage, x.delta, x.n};
+	if (classify_variant() == 0)
+		hipLaunchKernelGGL((k_classify<1, 0>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	else
+		hipLaunchKernelGGL((k_classify<1, 1>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 	return hipGetLastError();
 }
 

@@ -24,6 +24,21 @@ struct classify_v4_args {
 
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st);
 
+struct classify_v6_args {
+	const uint8_t *saddr16, *daddr16;
+	const uint16_t *dport;
+	const uint8_t *proto, *flags;
+	const uint32_t *len;
+	const uint16_t *ep;
+	int32_t *verdict;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t *delta;
+	uint64_t n;
+};
+
+hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &a, hipStream_t st);
+
 struct prefilter_args {
 	const uint32_t *saddr4, *daddr4;
 	const uint8_t *saddr16, *daddr16;

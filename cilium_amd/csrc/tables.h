@@ -112,22 +112,23 @@ static inline __host__ __device__ uint32_t hash16(uint32_t a0, uint32_t a1, uint
 	return mix32(mix32(a0, a1) ^ salt, mix32(a2, a3));
 }
 
-/* ---- IPv6 any-match prefix set (prefilter dyn6 + fix6) ----
- * root[addr >> 112] (65536 x u16) selects a row of `masks`: the set of
- * prefix lengths 17..128 present under that /16 (bit L-17 of 128 bits);
- * row 0 = none, ROOT_COVERED = a prefix of length <= 16 covers the root.
- * Each present length L is then ONE independent probe of `set`, keyed by
- * (addr masked to L, L): the probes of one packet have no dependence on
- * each other, so they are issued together (memory-level parallelism
- * instead of a pointer chase down a trie). */
-#define V6_ROOT_COVERED 0xFFFFu
-
-typedef struct v6_anyset {
-	const uint16_t *root;  /* 65536 */
-	const uint32_t *masks; /* n_masks x 4 u32 */
-	addr_set16 set;        /* used word: bit0 used, bits 8..15 length */
+/* ---- IPv6 longest-prefix table (ipcache v6, prefilter v6) ----
+ * root[addr >> 112] (65536 x {row, short}): `short` is the longest entry of
+ * length <= 16 covering that /16 (DIR-24-8 entry encoding, 0 = none) and
+ * `row` selects a 128-bit row of `masks`: the prefix lengths 17..128 present
+ * under that /16 (bit L-17).  Each present length L is ONE probe of `set`,
+ * keyed by (address masked to L, L); a slot's pad[0] holds the entry.  The
+ * probes of one address do not depend on each other, so they are issued in
+ * groups of four, longest first (memory-level parallelism instead of a
+ * 128-level pointer chase); the first hit in descending length order is the
+ * longest match, else `short`. */
+typedef struct v6_lpm {
+	const uint2 *root;     /* 65536 x {row, short entry}; NULL = empty table */
+	const uint32_t *masks; /* n_masks x 4 u32 (row 0 = no lengths) */
+	const uint32_t *vals;  /* indirect labels (>= 2^30) */
+	addr_set16 set;        /* used: bit0 used, bits 8..15 length; pad[0] entry */
 	uint32_t n_masks;
-} v6_anyset;
+} v6_lpm;
 
 /* ---- one committed snapshot ---- */
 typedef struct cgpu_snapshot {
@@ -136,12 +137,14 @@ typedef struct cgpu_snapshot {
 	dir248 pf4;      /* any-match: dyn4 (if enabled) + fix4 /32 */
 	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
 	addr_set16 ep6;  /* cilium_lxc IPv6 keys */
-	v6_anyset pf6;   /* any-match: dyn6 (if enabled) + fix6 /128 */
+	v6_lpm pf6;      /* any-match: dyn6 (if enabled) + fix6 /128 */
+	v6_lpm ipc6;     /* ipcache, IPv6 lookups */
 	uint32_t pf4_enabled; /* CIDR4_FILTER */
 	uint32_t pf6_enabled; /* CIDR6_FILTER */
 	/* config */
 	uint32_t world_id, cluster_id, host_id, health_id;
 	uint32_t ipv4_cluster_mask, ipv4_cluster_range;
+	uint32_t router_ip64[2]; /* first 8 bytes of ROUTER_IP (ipv6_match_prefix_64) */
 	uint32_t ct_proto_gate, ingress_secctx_world, ingress_src_identity;
 	uint32_t n_ctr_slots;
 	uint64_t epoch;

@@ -23,7 +23,7 @@ import ipaddress
 import numpy as np
 
 from . import layouts as L
-from ._abi import CgpuConfig, CgpuError, TuplesV4, check, lib
+from ._abi import CgpuConfig, CgpuError, TuplesV4, TuplesV6, check, lib
 
 CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX = 0, 1, 2, 3
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
@@ -54,6 +54,9 @@ class Engine:
         for k, v in cfg.items():
             if not hasattr(self.cfg, k):
                 raise TypeError(f"unknown config field {k}")
+            if k == "ipv6_router_ip":
+                self.cfg.ipv6_router_ip[:] = bytes(v)
+                continue
             setattr(self.cfg, k, v)
         h = C.c_void_p()
         check(self.L.cgpu_ctx_create(C.byref(self.cfg), device, C.byref(h)), "cgpu_ctx_create")
@@ -172,6 +175,23 @@ class Engine:
         check(self.L.cgpu_classify_v4(self.h, C.byref(tv), n, _ptr(out["verdict"]),
                                       _ptr(out["identity"]), _ptr(out.get("stage")),
                                       _stream(stream)), "cgpu_classify_v4")
+        return out
+
+    def classify_v6(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """t: saddr/daddr uint8 CUDA tensors of shape (n, 16) (16-byte
+        aligned), the other columns as classify_v4."""
+        import torch
+        n = t["flags"].numel()
+        dev = t["flags"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
+        tv = TuplesV6(*[t[k].data_ptr() for k in
+                        ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")])
+        check(self.L.cgpu_classify_v6(self.h, C.byref(tv), n, _ptr(out["verdict"]),
+                                      _ptr(out["identity"]), _ptr(out.get("stage")),
+                                      _stream(stream)), "cgpu_classify_v6")
         return out
 
     def prefilter_v4(self, saddr, daddr, flags, out=None, stream=None):

@@ -212,11 +212,15 @@ TUPLE_DTYPES = {"saddr": np.uint32, "daddr": np.uint32, "dport": np.uint16, "pro
 
 
 def to_device(t: dict, device="cuda"):
-    """numpy SoA -> torch device tensors (bit-identical views)."""
+    """numpy SoA -> torch device tensors (bit-identical views).  IPv6
+    address columns ((n, 16) uint8) stay uint8."""
     import torch
     view = {np.uint32: np.int32, np.uint16: np.int16, np.uint8: np.uint8}
     out = {}
     for k, dt in TUPLE_DTYPES.items():
-        a = np.ascontiguousarray(t[k], dt).view(view[dt])
+        if k in ("saddr", "daddr") and np.asarray(t[k]).ndim == 2:
+            a = np.ascontiguousarray(t[k], np.uint8)
+        else:
+            a = np.ascontiguousarray(t[k], dt).view(view[dt])
         out[k] = torch.from_numpy(a).to(device, non_blocking=False)
     return out

@@ -235,6 +235,26 @@ typedef struct cgpu_tuples_v4 {
 int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
 		     uint32_t *identity, uint8_t *stage, void *stream);
 
+typedef struct cgpu_tuples_v6 {
+	const uint8_t *saddr;  /* 16 bytes per tuple, network order */
+	const uint8_t *daddr;  /* 16 bytes per tuple */
+	const uint16_t *dport; /* network order */
+	const uint8_t *proto;  /* nexthdr */
+	const uint8_t *flags;  /* CGPU_F_EGRESS (fragments: IPv6 passes false) */
+	const uint32_t *len;
+	const uint16_t *ep;
+} cgpu_tuples_v6;
+
+/*
+ * IPv6 form of cgpu_classify_v4: ipcache_lookup6 (eps.h:56-66), egress
+ * fallback CLUSTER_ID when ipv6_match_prefix_64(daddr, ROUTER_IP)
+ * (bpf_lxc.c:170-191), ingress identity without the HOST_ID exception
+ * (bpf_netdev.c:203-211), protocol gate ICMPv6/TCP/UDP (conntrack.h:330-378).
+ * The ingress label is the resolved source identity (FROM_HOST form).
+ */
+int cgpu_classify_v6(cgpu_ctx *ctx, const cgpu_tuples_v6 *t, size_t n, int32_t *verdict,
+		     uint32_t *identity, uint8_t *stage, void *stream);
+
 /* XDP prefilter over pre-parsed packets (bpf_xdp.c:88-184).
  * flags: 0 IP packet of this family, 1 truncated (-> XDP_DROP),
  *        2 not IPv4/IPv6 (-> XDP_PASS).  verdict: XDP_DROP 1 / XDP_PASS 2. */

@@ -302,3 +302,87 @@ def test_prefilter_scale_vs_oracle(torch_cuda):
         np.testing.assert_array_equal(_np(g6), r6)
         assert (r6 == L.XDP_DROP).mean() > 0.2 and (r6 == L.XDP_PASS).mean() > 0.05
         e.close()
+
+
+def _classify6(torch, e, t, stage=True):
+    d = synth.to_device(t)
+    out = e.classify_v6(d, stage=stage)
+    torch.cuda.synchronize()
+    return (_np(out["verdict"]), _np(out["identity"], np.uint32),
+            _np(out["stage"]) if stage else None)
+
+
+@pytest.mark.parametrize("ci", range(4))
+def test_classify_v6_golden(torch_cuda, golden, ci):
+    g = golden("classify_v6.npz")
+    gate, src = (int(x) for x in g["configs"][ci])
+    e = _engine(ct_proto_gate=gate, ingress_src_identity=src,
+                ipv6_router_ip=g["router_ip"].tobytes())
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert e.ipcache_update(k, v) == 0
+    for k, en, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert e.policy_update(int(ep), k, en) == 0
+    e.commit()
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    v, idt, st = _classify6(torch_cuda, e, t)
+    np.testing.assert_array_equal(v, g[f"c{ci}_verdict"])
+    np.testing.assert_array_equal(idt, g[f"c{ci}_identity"])
+    np.testing.assert_array_equal(st, g[f"c{ci}_stage"])
+    for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
+        rc, got = e.policy_lookup(int(ep), k)
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+    e.close()
+
+
+def test_classify_v6_scale_vs_oracle(torch_cuda):
+    """20k IPv6 ipcache prefixes (lengths 0..128, tombstones, static-part
+    entries) + policy, 400k tuples: GPU == restatement, bit-exact."""
+    from oracle import Oracle
+    rng = np.random.default_rng(21)
+    T = synth.make_tables(n_prefixes=100, n_identities=500, n_endpoints=3, keys_per_ep=6000)
+    roots = rng.integers(0, 256, (32, 4), dtype=np.uint8)
+    keys = np.zeros(20_000, L.IPCACHE_KEY)
+    keys["family"] = 2
+    lens = rng.choice([0, 8, 16, 20, 32, 40, 48, 56, 64, 72, 96, 112, 120, 127, 128], len(keys))
+    keys["prefixlen"] = 32 + lens
+    addr = rng.integers(0, 256, (len(keys), 16), dtype=np.uint8)
+    addr[:, :4] = roots[rng.integers(0, len(roots), len(keys))]
+    keys["ip"] = addr
+    keys[:3]["prefixlen"] = [0, 24, 30]          # static-part entries
+    keys[:3]["family"] = [0, 0, 2]
+    vals = np.zeros(len(keys), L.REMOTE_ENDPOINT_INFO)
+    vals["sec_label"] = rng.integers(256, 756, len(keys))
+    vals["sec_label"][rng.random(len(keys)) < 0.03] = 0
+    vals["sec_label"][rng.random(len(keys)) < 0.01] = 0xF0000000  # >= 2^30: indirect
+    router = bytes(addr[5][:8]) + bytes(8)
+    n = 400_000
+    base = addr[rng.integers(0, len(keys), n)].copy()
+    cut = rng.integers(0, 17, n)
+    noise = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    mask = np.arange(16)[None, :] >= cut[:, None]
+    sa = np.where(mask, noise, base).astype(np.uint8)
+    base = addr[rng.integers(0, len(keys), n)].copy()
+    da = np.where(np.arange(16)[None, :] >= rng.integers(0, 17, n)[:, None], noise[::-1], base)
+    da[: n // 20, :8] = np.frombuffer(router[:8], np.uint8)
+    t = {"saddr": sa, "daddr": da.astype(np.uint8),
+         "dport": synth.zipf_ports(rng, n).byteswap(),
+         "proto": rng.choice(np.array([6, 6, 17, 58, 1], np.uint8), n),
+         "flags": rng.integers(0, 4, n).astype(np.uint8),
+         "len": rng.integers(64, 9000, n).astype(np.uint32),
+         "ep": rng.integers(0, 3, n).astype(np.uint16)}
+    cfg_e = dict(T.engine_config(), ipv6_router_ip=router)
+    e = _engine(**cfg_e)
+    o = Oracle(router_ip=router)
+    for k, v in zip(keys, vals):
+        assert e.ipcache_update(k, v) == 0 and o.ipcache_update(k, v) == 0
+    for k, en, ep in zip(T.pol_keys, T.pol_entries, T.pol_ep):
+        assert e.policy_update(int(ep), k, en) == 0 and o.policy_update(int(ep), k, en) == 0
+    e.commit()
+    v0, i0, s0, _ = o.classify_v6(t, nthreads=8)
+    v, idt, st = _classify6(torch_cuda, e, t)
+    np.testing.assert_array_equal(v, v0)
+    np.testing.assert_array_equal(idt, i0)
+    np.testing.assert_array_equal(st, s0)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    assert len(np.unique(i0)) > 100
+    e.close()
