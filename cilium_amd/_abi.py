@@ -29,7 +29,8 @@ class CgpuConfig(C.Structure):
         ("prefilter_fix6", C.c_uint8), ("prefilter_dyn6", C.c_uint8),
         ("reserved0", C.c_uint8 * 2),
         ("ingress_src_identity", C.c_uint32),
-        ("reserved", C.c_uint32 * 8),
+        ("hot_counter_slots", C.c_uint32),
+        ("reserved", C.c_uint32 * 7),
     ]
 
 

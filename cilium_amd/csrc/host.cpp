@@ -193,8 +193,10 @@ struct cgpu_ctx {
 	std::map<LpmKey<20>, IpcEntry> ipc;
 	std::vector<std::map<uint64_t, PolEntry>> pol;
 	size_t pol_total = 0;
-	std::vector<uint32_t> free_slots;
-	uint32_t next_slot = 0;
+	/* counter slots: hot class [0, hot_cap) for L3-only / wildcard keys,
+	 * cold class [hot_cap, n_ctr_slots) for the rest */
+	std::vector<uint32_t> free_hot, free_cold;
+	uint32_t next_hot = 0, next_cold = 0, hot_cap = 0;
 	std::vector<SlotInit> slot_inits;
 	std::map<LpmKey<4>, cgpu_cidr_key> dyn4;
 	std::map<LpmKey<16>, cgpu_cidr_key> dyn6;
@@ -239,6 +241,7 @@ CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
 	c->prefilter_fix4 = c->prefilter_dyn4 = 1; /* bpf/filter_config.h */
 	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
 	c->ingress_src_identity = 0;
+	c->hot_counter_slots = 8192;
 	static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1,
 					   0x0, 0x1, 0x0, 0x0}; /* ROUTER_IP, bpf/node_config.h:30 */
 	memcpy(c->ipv6_router_ip, router, 16);
@@ -259,6 +262,8 @@ CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **o
 	c->cfg = *cfg;
 	c->pol.resize(cfg->max_endpoints);
 	c->n_ctr_slots = cfg->policy_max_total;
+	c->hot_cap = std::min(cfg->hot_counter_slots, cfg->policy_max_total / 2);
+	c->next_cold = c->hot_cap;
 	if (device >= 0) {
 		int ndev = 0;
 		if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
@@ -414,13 +419,21 @@ CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_k
 			return fail(-ENOENT, "policy key not present");
 		if (m.size() >= c->cfg.policy_max_per_ep)
 			return fail(-E2BIG, "policy map of ep %u full (%u)", ep, c->cfg.policy_max_per_ep);
-		if (c->free_slots.empty() && c->next_slot >= c->n_ctr_slots)
-			return fail(-E2BIG, "policy device slots exhausted (%u)", c->n_ctr_slots);
-		if (!c->free_slots.empty()) {
-			slot = c->free_slots.back();
-			c->free_slots.pop_back();
+		/* L3-only {id, 0, 0, dir} and wildcard {0, port, proto, dir} keys
+		 * absorb most hits: give them hot (LDS-accumulated) slots */
+		bool hot = (key->dport == 0 && key->protocol == 0) || key->sec_label == 0;
+		if (hot && !c->free_hot.empty()) {
+			slot = c->free_hot.back();
+			c->free_hot.pop_back();
+		} else if (hot && c->next_hot < c->hot_cap) {
+			slot = c->next_hot++;
+		} else if (!c->free_cold.empty()) {
+			slot = c->free_cold.back();
+			c->free_cold.pop_back();
+		} else if (c->next_cold < c->n_ctr_slots) {
+			slot = c->next_cold++;
 		} else {
-			slot = c->next_slot++;
+			return fail(-E2BIG, "policy device slots exhausted (%u)", c->n_ctr_slots);
 		}
 		m.emplace(k, PolEntry{e->proxy_port, slot});
 		c->pol_total++;
@@ -438,7 +451,10 @@ CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_k
 static void pol_erase(cgpu_ctx *c, std::map<uint64_t, PolEntry> &m,
 		      std::map<uint64_t, PolEntry>::iterator it)
 {
-	c->free_slots.push_back(it->second.slot);
+	if (it->second.slot < c->hot_cap)
+		c->free_hot.push_back(it->second.slot);
+	else
+		c->free_cold.push_back(it->second.slot);
 	m.erase(it);
 	c->pol_total--;
 }
@@ -1184,6 +1200,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.ingress_secctx_world = c->cfg.ingress_secctx_world;
 	s.ingress_src_identity = c->cfg.ingress_src_identity;
 	s.n_ctr_slots = c->n_ctr_slots;
+	s.hot_slots = c->hot_cap;
 	s.epoch = ++c->epoch;
 	c->snap = s;
 	c->committed = true;

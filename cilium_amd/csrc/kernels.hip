@@ -10,6 +10,7 @@
  */
 #include "launch.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 #define DROP_POLICY (-133)           /* bpf/lib/common.h:240 */
@@ -288,14 +289,36 @@ struct cls_args {
 	uint64_t n;
 };
 
-template <int V6, int SPEC>
-__global__ __launch_bounds__(BLOCK) void k_classify(cgpu_snapshot s, cls_args a)
-{
-	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
-	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-	uint64_t *pctr = a.delta;
+/* Packed per-workgroup counter: packets in bits 41..63, bytes in 0..40.
+ * Exact while a workgroup adds < 2^23 hits of < 2^18 bytes to one slot
+ * (the launcher bounds tuples per workgroup; longer packets take the
+ * global path). */
+#define PK_SHIFT 41
+#define PK_BYTES_MASK ((1ull << PK_SHIFT) - 1ull)
+#define PK_MAX_LEN (1u << 18)
 
-	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < a.n; i += stride) {
+/*
+ * CTR = 0: two global u64 atomics per policy hit (packets, bytes).
+ * CTR = 1: hits on hot slots [0, s.hot_slots) (L3-only / wildcard keys) go
+ *          to one packed LDS atomic; the workgroup flushes its LDS counters
+ *          to the delta buffer once at the end; cold slots as CTR = 0.
+ * CTR = 2: no policy-entry counters (diagnostic ablation only; the results
+ *          are NOT the reference's: its counters are part of the contract).
+ */
+template <int V6, int SPEC, int CTR, int NT>
+__global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
+{
+	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
+	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
+	const uint64_t stride = (uint64_t)gridDim.x * NT;
+	uint64_t *pctr = a.delta;
+	if (CTR == 1) {
+		for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
+			lctr[k] = 0;
+		__syncthreads();
+	}
+
+	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) {
 		const uint32_t fl = a.flags[i];
 		const uint32_t proto = a.proto[i];
 		const uint32_t len = a.len[i];
@@ -391,9 +414,15 @@ __global__ __launch_bounds__(BLOCK) void k_classify(cgpu_snapshot s, cls_args a)
 				}
 			}
 			if (ctr >= 0) {
-				atomicAdd((unsigned long long *)&pctr[2u * (uint32_t)ctr], 1ull);
-				atomicAdd((unsigned long long *)&pctr[2u * (uint32_t)ctr + 1u],
-					  (unsigned long long)len);
+				const uint32_t c = (uint32_t)ctr;
+				if (CTR == 1 && c < s.hot_slots && len < PK_MAX_LEN) {
+					atomicAdd((unsigned long long *)&lctr[c],
+						  (1ull << PK_SHIFT) | (unsigned long long)len);
+				} else if (CTR != 2) {
+					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
+					atomicAdd((unsigned long long *)&pctr[2u * c + 1u],
+						  (unsigned long long)len);
+				}
 				v = st == 2 ? 0 : (int32_t)(z >> 16);
 			} else {
 				st = 0;
@@ -424,6 +453,16 @@ __global__ __launch_bounds__(BLOCK) void k_classify(cgpu_snapshot s, cls_args a)
 			uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
 			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
 			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
+		}
+	}
+	if (CTR == 1) {
+		__syncthreads();
+		for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
+			const uint64_t v = lctr[k];
+			if (v) {
+				atomicAdd((unsigned long long *)&pctr[2u * k], v >> PK_SHIFT);
+				atomicAdd((unsigned long long *)&pctr[2u * k + 1u], v & PK_BYTES_MASK);
+			}
 		}
 	}
 }
@@ -517,26 +556,59 @@ static int classify_variant()
 	return v ? atoi(v) : 1;
 }
 
+template <int V6>
+static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_t st)
+{
+	const int var = classify_variant();
+	if (var == 2 || var == 3) {
+		/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at
+		 * most 2^22 tuples per workgroup (packed-counter exactness) */
+		constexpr int NT = 1024;
+		const size_t lds = (size_t)s.hot_slots * 8u;
+		const uint64_t cap = 2ull * 256ull;
+		const uint64_t per_launch = cap * (1ull << 22);
+		for (uint64_t off = 0; off < a.n; off += per_launch) {
+			cls_args c = a;
+			const uint64_t m = std::min<uint64_t>(a.n - off, per_launch);
+			c.n = m;
+			c.verdict += off;
+			c.identity += off;
+			if (c.stage)
+				c.stage += off;
+			c.dport += off;
+			c.proto += off;
+			c.flags += off;
+			c.len += off;
+			c.ep += off;
+			c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
+			c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
+			const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
+			if (var == 2)
+				hipLaunchKernelGGL((k_classify<V6, 1, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
+			else
+				hipLaunchKernelGGL((k_classify<V6, 0, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
+		}
+		return hipGetLastError();
+	}
+	if (var == 0)
+		hipLaunchKernelGGL((k_classify<V6, 0, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	else if (var == 9)
+		hipLaunchKernelGGL((k_classify<V6, 1, 2, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	else
+		hipLaunchKernelGGL((k_classify<V6, 1, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x, hipStream_t st)
 {
-	cls_args a{x.saddr, x.daddr, x.dport, x.proto, x.flags, x.len, x.ep,
-		   x.verdict, x.identity, x.stage, x.delta, x.n};
-	if (classify_variant() == 0)
-		hipLaunchKernelGGL((k_classify<0, 0>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
-	else
-		hipLaunchKernelGGL((k_classify<0, 1>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
-	return hipGetLastError();
+	return launch_classify<0>(s, cls_args{x.saddr, x.daddr, x.dport, x.proto, x.flags, x.len, x.ep,
+					      x.verdict, x.identity, x.stage, x.delta, x.n}, st);
 }
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)
 {
-	cls_args a{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len, x.ep,
-		   x.verdict, x.identity, x.stage, x.delta, x.n};
-	if (classify_variant() == 0)
-		hipLaunchKernelGGL((k_classify<1, 0>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
-	else
-		hipLaunchKernelGGL((k_classify<1, 1>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
-	return hipGetLastError();
+	return launch_classify<1>(s, cls_args{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len,
+					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n}, st);
 }
 
 hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)

@@ -147,6 +147,7 @@ typedef struct cgpu_snapshot {
 	uint32_t router_ip64[2]; /* first 8 bytes of ROUTER_IP (ipv6_match_prefix_64) */
 	uint32_t ct_proto_gate, ingress_secctx_world, ingress_src_identity;
 	uint32_t n_ctr_slots;
+	uint32_t hot_slots;      /* counter slots [0, hot_slots) may live in LDS */
 	uint64_t epoch;
 } cgpu_snapshot;
 

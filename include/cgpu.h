@@ -138,7 +138,11 @@ typedef struct cgpu_config {
 	uint8_t reserved0[2];
 	/* identity handed to handle_ipv4 on ingress (from_netdev: 0) */
 	uint32_t ingress_src_identity;
-	uint32_t reserved[8];
+	/* counter slots [0, hot_counter_slots) are reserved for L3-only and
+	 * identity-wildcard policy keys (the entries most tuples hit) and are
+	 * accumulated in LDS per workgroup before one flush to HBM */
+	uint32_t hot_counter_slots;
+	uint32_t reserved[7];
 } cgpu_config;
 
 typedef struct cgpu_ctx cgpu_ctx;

@@ -386,3 +386,26 @@ def test_classify_v6_scale_vs_oracle(torch_cuda):
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     assert len(np.unique(i0)) > 100
     e.close()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_kernel_variants_exact(torch_cuda, cfg1, variant, monkeypatch):
+    """Every classify schedule / counter strategy gives the reference's
+    verdicts, identities, stages, per-entry counters and metrics."""
+    T, t = cfg1
+    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    o, v0, i0, s0, _ = _oracle_run(T, t)
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    v, idt, st = _classify(torch_cuda, e, t)
+    np.testing.assert_array_equal(v, v0)
+    np.testing.assert_array_equal(idt, i0)
+    np.testing.assert_array_equal(st, s0)
+    for k, ep in zip(T.pol_keys[::7], T.pol_ep[::7]):
+        rc, got = e.policy_lookup(int(ep), k)
+        _, raw = o.policy_lookup(int(ep), k)
+        exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(exp["packets"]), int(exp["bytes"]))
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
