@@ -1,0 +1,14 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+ok() { case $1 in 0|1) return 0;; *) echo "stopping: rc=$1"; exit $1;; esac; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; ok $rc
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; ok $rc
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench1.json 2> gpurun_out/bench1.err
+rc=$?; echo "bench rc=$rc"; ok $rc
+cat gpurun_out/bench1.json
+timeout -k 10 300 python -u tools/ab_classify.py --rounds 3 --iters 3 > gpurun_out/ab1.json 2> gpurun_out/ab1.err
+rc=$?; echo "ab rc=$rc"; cat gpurun_out/ab1.json
