@@ -157,10 +157,14 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 		return 0;
 	const uint32_t top = ((a.x & 0xFFu) << 8) | ((a.x >> 8) & 0xFFu);
 	const uint2 r = t.root[top];
+	uint32_t res = 0;
 	if (r.x) {
 		const uint4 m = reinterpret_cast<const uint4 *>(t.masks)[r.x];
 		uint64_t hi = ((uint64_t)m.w << 32) | m.z, lo = ((uint64_t)m.y << 32) | m.x;
-		while (hi | lo) {
+		/* NB: the result is carried, never returned from inside the
+		 * unrolled loop: a divergent early return there miscompiled on
+		 * gfx950 / ROCm 7.2 (tools/dbg/dbg_v6.hip reproduces it). */
+		while ((hi | lo) && !res) {
 			uint32_t L[4];
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
@@ -178,8 +182,14 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 			}
 			uint4 key[4], bk[4][4];
 			uint32_t bi[4];
+			/* issue every probe's bucket load before resolving any */
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
+				key[j] = make_uint4(0, 0, 0, 0);
+				bi[j] = 0;
+#pragma unroll
+				for (int k = 0; k < 4; k++)
+					bk[j][k] = make_uint4(0, 0, 0, 0);
 				if (L[j]) {
 					key[j] = mask6(a, L[j]);
 					bi[j] = hash16(key[j].x, key[j].y, key[j].z, key[j].w, L[j]) &
@@ -191,17 +201,14 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 						bk[j][k] = p[k];
 				}
 			}
+			/* longest first: the first hit is the longest match */
 #pragma unroll
-			for (int j = 0; j < 4; j++) {
-				if (L[j]) {
-					uint32_t e = set16_resolve(t.set, bk[j], bi[j], key[j], 1u | (L[j] << 8));
-					if (e)
-						return e;
-				}
-			}
+			for (int j = 0; j < 4; j++)
+				if (!res && L[j])
+					res = set16_resolve(t.set, bk[j], bi[j], key[j], 1u | (L[j] << 8));
 		}
 	}
-	return r.y;
+	return res ? res : r.y;
 }
 
 __device__ __forceinline__ uint32_t entry_label(const uint32_t *vals, uint32_t e)
