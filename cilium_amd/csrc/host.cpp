@@ -1135,12 +1135,21 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	};
 	add_v6(pf6, o_pf6);
 	add_v6(ipc6, o_ipc6);
+	/* a slot freed and reused before this commit has several inits queued:
+	 * only the most recent one may reach the device (the init kernel writes
+	 * all of them in parallel) */
 	std::vector<uint32_t> init_slot;
 	std::vector<uint64_t> init_pk, init_by;
-	for (auto &s : c->slot_inits) {
-		init_slot.push_back(s.slot);
-		init_pk.push_back(s.packets);
-		init_by.push_back(s.bytes);
+	{
+		std::vector<uint8_t> seen(c->n_ctr_slots, 0);
+		for (auto s = c->slot_inits.rbegin(); s != c->slot_inits.rend(); ++s) {
+			if (seen[s->slot])
+				continue;
+			seen[s->slot] = 1;
+			init_slot.push_back(s->slot);
+			init_pk.push_back(s->packets);
+			init_by.push_back(s->bytes);
+		}
 	}
 	size_t o_is = ar.add(init_slot.data(), init_slot.size() * 4);
 	size_t o_ip = ar.add(init_pk.data(), init_pk.size() * 8);

@@ -409,3 +409,19 @@ def test_kernel_variants_exact(torch_cuda, cfg1, variant, monkeypatch):
         assert (int(got["packets"]), int(got["bytes"])) == (int(exp["packets"]), int(exp["bytes"]))
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     e.close()
+
+
+def test_slot_reuse_within_one_commit(torch_cuda):
+    """A counter slot freed and reused before one commit: the newest entry's
+    supplied counters win (kernel htab: the update replaces the value)."""
+    e = _engine(policy_max_total=64, hot_counter_slots=0)
+    a, b = L.policy_key(300, 80, 6, 0), L.policy_key(301, 443, 6, 0)
+    assert e.policy_update(0, a, L.policy_entry(0, 0, 0)) == 0
+    assert e.policy_delete(0, a) == 0
+    assert e.policy_update(0, b, L.policy_entry(0, 5, 500)) == 0   # reuses a's slot
+    assert e.policy_update(0, a, L.policy_entry(0, 7, 700)) == 0
+    assert e.policy_update(0, a, L.policy_entry(0, 9, 900)) == 0   # same key twice
+    e.commit()
+    assert [int(x) for x in e.policy_lookup(0, b)[1][["packets", "bytes"]].item()] == [5, 500]
+    assert [int(x) for x in e.policy_lookup(0, a)[1][["packets", "bytes"]].item()] == [9, 900]
+    e.close()
