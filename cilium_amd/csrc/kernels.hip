@@ -560,7 +560,7 @@ unsigned grid_for(uint64_t n)
 static int classify_variant()
 {
 	const char *v = getenv("CGPU_CLASSIFY_VARIANT");
-	return v ? atoi(v) : 1;
+	return v ? atoi(v) : 3;
 }
 
 template <int V6>

@@ -242,10 +242,13 @@ def test_prefilter_scale_vs_oracle(torch_cuda):
     n = 300_000
     roots = rng.integers(0, 256, (64, 3), dtype=np.uint8)
     dyn6 = []
-    for _ in range(20_000):
+    for i in range(20_000):
         k = np.zeros((), L.LPM_V6_KEY)
-        k["prefixlen"] = int(rng.choice([8, 16, 20, 32, 48, 56, 64, 96, 127]))
+        k["prefixlen"] = int(rng.choice([20, 24, 32, 48, 56, 64, 96, 127]))
         k["addr"][:] = _v6(rng, 1, roots)[0]
+        if i < 4:  # a few short prefixes (root-level "short" entries) on 2 roots
+            k["prefixlen"] = [8, 16, 12, 16][i]
+            k["addr"][:3] = roots[i % 2]
         dyn6.append(k)
     fix6 = []
     for _ in range(5_000):
@@ -268,7 +271,7 @@ def test_prefilter_scale_vs_oracle(torch_cuda):
     ep6 = _v6(rng, 4000, roots)
     s6 = np.where(rng.random((n, 1)) < 0.5,
                   np.array([k["addr"] for k in dyn6])[rng.integers(0, len(dyn6), n)],
-                  _v6(rng, n, roots))
+                  rng.integers(0, 256, (n, 16), dtype=np.uint8))  # mostly uncovered
     s6[: n // 10] = np.array([k["addr"] for k in fix6])[rng.integers(0, len(fix6), n // 10)]
     d6 = np.where(rng.random((n, 1)) < 0.3, ep6[rng.integers(0, 4000, n)], _v6(rng, n, roots))
     s4 = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
