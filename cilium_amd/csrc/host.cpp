@@ -17,6 +17,7 @@
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -843,13 +844,26 @@ bool build_pf4(const cgpu_ctx *c, Dir248 &d)
 
 struct PolBuild {
 	std::vector<pol_slot> slots;
-	uint32_t mask = 0, max_probe = 1;
+	uint32_t mask = 0, max_probe = 1, bpb = 4;
 };
 
+static uint32_t env_u32(const char *name, uint32_t dflt)
+{
+	const char *v = getenv(name);
+	return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
+}
+
+/* Policy hash layout.  Default: 16-byte single-slot buckets (one random
+ * dwordx4 load per probe) at <= 25% load, so most probes resolve on the
+ * first slot; CGPU_POL_BPB=4 selects 64-byte 4-slot buckets at <= 50%. */
 void build_pol(const cgpu_ctx *c, PolBuild &b)
 {
-	uint32_t nb = next_pow2(std::max<uint64_t>(64, (c->pol_total + 1) / 2 + 1));
-	b.slots.assign((size_t)nb * POL_SLOTS_PER_BUCKET, pol_slot{0, 0, 0, POL_EMPTY});
+	b.bpb = env_u32("CGPU_POL_BPB", 1) == 4 ? 4 : 1;
+	const uint32_t load_pct = std::max<uint32_t>(5, std::min<uint32_t>(
+		env_u32("CGPU_POL_LOAD_PCT", b.bpb == 1 ? 25 : 50), 90));
+	const uint64_t want_slots = (c->pol_total * 100 + load_pct - 1) / load_pct + 1;
+	uint32_t nb = next_pow2(std::max<uint64_t>(64, (want_slots + b.bpb - 1) / b.bpb));
+	b.slots.assign((size_t)nb * b.bpb, pol_slot{0, 0, 0, POL_EMPTY});
 	b.mask = nb - 1;
 	b.max_probe = 1;
 	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
@@ -857,11 +871,11 @@ void build_pol(const cgpu_ctx *c, PolBuild &b)
 			uint32_t lo = (uint32_t)kv.first, hi = (uint32_t)(kv.first >> 32);
 			uint32_t bk = pol_hash(lo, hi, ep) & b.mask, probe = 1;
 			for (;;) {
-				pol_slot *s = &b.slots[(size_t)bk * POL_SLOTS_PER_BUCKET];
-				int k = 0;
-				while (k < (int)POL_SLOTS_PER_BUCKET && s[k].ctr != POL_EMPTY)
+				pol_slot *s = &b.slots[(size_t)bk * b.bpb];
+				uint32_t k = 0;
+				while (k < b.bpb && s[k].ctr != POL_EMPTY)
 					k++;
-				if (k < (int)POL_SLOTS_PER_BUCKET) {
+				if (k < b.bpb) {
 					s[k] = pol_slot{lo, hi, ep | (uint32_t)kv.second.proxy_port << 16,
 							kv.second.slot};
 					break;
@@ -1179,7 +1193,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.ipc4 = dir248{(const uint32_t *)(arena + o_t24), (const uint32_t *)(arena + o_t8),
 			(const uint32_t *)(arena + o_v), (uint32_t)(ipc4.tbl8.size() / 256),
 			(uint32_t)ipc4.vals.size()};
-	s.pol = pol_table{(const pol_slot *)(arena + o_pol), pol.mask, pol.max_probe};
+	s.pol = pol_table{(const pol_slot *)(arena + o_pol), pol.mask, pol.max_probe, pol.bpb, 0};
 	if (have_pf4)
 		s.pf4 = dir248{(const uint32_t *)(arena + o_p24), (const uint32_t *)(arena + o_p8),
 			       nullptr, (uint32_t)(pf4.tbl8.size() / 256), 0};

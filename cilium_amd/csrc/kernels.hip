@@ -38,11 +38,26 @@ __device__ __forceinline__ uint32_t dir_lookup(const dir248 &d, uint32_t addr_be
 }
 
 /* Policy hash probe: exact 8-byte policy_key + endpoint.  Returns the
- * counter slot, or -1 (map_lookup_elem NULL); *z receives ep|proxy<<16. */
+ * counter slot, or -1 (map_lookup_elem NULL); *z receives ep|proxy<<16.
+ * The layout branch is on a kernarg (wave-uniform, scalar). */
 __device__ __forceinline__ int pol_lookup(const pol_table &t, uint32_t lo, uint32_t hi, uint32_t ep,
 					  uint32_t *z)
 {
 	uint32_t b = pol_hash(lo, hi, ep) & t.bucket_mask;
+	if (t.slots_per_bucket == 1) {
+		const uint4 *sl = reinterpret_cast<const uint4 *>(t.slots);
+		for (uint32_t p = 0; p < t.max_probe; p++) {
+			const uint4 s = sl[b];
+			if (s.w == POL_EMPTY)
+				return -1;
+			if (s.x == lo && s.y == hi && (s.z & 0xFFFFu) == ep) {
+				*z = s.z;
+				return (int)s.w;
+			}
+			b = (b + 1) & t.bucket_mask;
+		}
+		return -1;
+	}
 	for (uint32_t p = 0; p < t.max_probe; p++) {
 		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
 		uint4 s[4];
@@ -225,63 +240,20 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v)
 	return v;
 }
 
-/* One 64-byte policy bucket (4 slots) held in registers. */
-struct pol_bucket {
-	uint4 s[4];
-};
-
-__device__ __forceinline__ pol_bucket pol_load(const pol_table &t, uint32_t b)
-{
-	const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
-	pol_bucket r;
-#pragma unroll
-	for (int k = 0; k < 4; k++)
-		r.s[k] = bk[k];
-	return r;
-}
-
-/* Resolve a probe whose first bucket is already loaded: -1 miss, else the
- * counter slot.  Continues down the probe sequence only if the first bucket
- * is full and does not hold the key (rare at load <= 0.5). */
-__device__ __forceinline__ int pol_resolve(const pol_table &t, const pol_bucket &first, uint32_t b,
-					   uint32_t lo, uint32_t hi, uint32_t ep, uint32_t *z)
-{
-	pol_bucket cur = first;
-	for (uint32_t p = 0;;) {
-#pragma unroll
-		for (int k = 0; k < 4; k++) {
-			if (cur.s[k].w == POL_EMPTY)
-				return -1;
-			if (cur.s[k].x == lo && cur.s[k].y == hi && (cur.s[k].z & 0xFFFFu) == ep) {
-				*z = cur.s[k].z;
-				return (int)cur.s[k].w;
-			}
-		}
-		if (++p >= t.max_probe)
-			return -1;
-		b = (b + 1) & t.bucket_mask;
-		cur = pol_load(t, b);
-	}
-}
-
 /*
- * Stateless IPv4 classification (see cgpu.h cgpu_classify_v4).
- *   egress : bpf_lxc.c:484-505   dstID = ipcache(daddr) | CLUSTER | WORLD
- *   ingress: bpf_netdev.c:374-404 src identity from ipcache(saddr)
- *   policy : bpf/lib/policy.h:46-110 (3 probes), collapsed to DROP_POLICY by
- *            policy_can_access_ingress / policy_can_egress (:126-163)
- *   gate   : bpf/lib/conntrack.h:526-528 DROP_CT_UNKNOWN_PROTO
+ * Stateless classification (see cgpu.h cgpu_classify_v4 / _v6).
+ *   egress : bpf_lxc.c:484-505 (v4) / :170-191 (v6)
+ *            dstID = ipcache(daddr) | CLUSTER | WORLD
+ *   ingress: bpf_netdev.c:374-404 (v4) / :203-211 (v6) src identity from ipcache(saddr)
+ *   policy : bpf/lib/policy.h:46-110 (3 probes, issued in the reference's
+ *            order: probe k+1 only after probe k missed), collapsed to
+ *            DROP_POLICY by policy_can_access_ingress / policy_can_egress
+ *   gate   : bpf/lib/conntrack.h DROP_CT_UNKNOWN_PROTO
  *   metrics: bpf/lib/drop.h:104 update_metrics(len, dir, -reason); forwarded
  *            at the verdict with reason 0
- *
- * SPEC = 0: the cascade exactly as the reference walks it (probe k+1 is
- *           issued only after probe k missed).
- * SPEC = 1: same results, different schedule: the identity-wildcard probe's
- *           bucket {0, dport, proto, dir} does not depend on the identity, so
- *           it is loaded before the ipcache lookup; the exact and L3 buckets
- *           are loaded together once the identity is known.  The dependent
- *           chain shrinks from up to 5 loads to 2-3, at the price of reading
- *           buckets the reference would not have probed.
+ * A speculative schedule (all three policy buckets loaded before the first
+ * was resolved) was measured 1.4x slower: the extra random loads cost more
+ * address-unit (TA) time than the shorter dependence chain saved.
  */
 struct cls_args {
 	const void *saddr, *daddr; /* u32 (v4) or uint4 (v6) per tuple */
@@ -312,7 +284,7 @@ struct cls_args {
  * CTR = 2: no policy-entry counters (diagnostic ablation only; the results
  *          are NOT the reference's: its counters are part of the contract).
  */
-template <int V6, int SPEC, int CTR, int NT>
+template <int V6, int CTR, int NT>
 __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
@@ -348,12 +320,6 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 			const bool frag = !V6 && !egress && ((fl >> 1) & 1u);
 			const uint32_t eg = egress ? (1u << 24) : 0u;
 			const uint32_t hi4 = dport | (proto << 16) | eg;
-			pol_bucket b3;
-			uint32_t bi3 = 0;
-			if (SPEC) {
-				bi3 = pol_hash(0u, hi4, ep) & s.pol.bucket_mask;
-				b3 = pol_load(s.pol, bi3);
-			}
 			uint32_t e, label;
 			bool in_cluster;
 			if (V6) {
@@ -389,36 +355,17 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 			}
 			uint32_t z = 0;
 			int ctr = -1;
-			if (SPEC) {
-				const uint32_t bi1 = pol_hash(id, hi4, ep) & s.pol.bucket_mask;
-				const uint32_t bi2 = pol_hash(id, eg, ep) & s.pol.bucket_mask;
-				pol_bucket b1 = pol_load(s.pol, bi1);
-				pol_bucket b2 = pol_load(s.pol, bi2);
-				if (!frag) {
-					ctr = pol_resolve(s.pol, b1, bi1, id, hi4, ep, &z);
-					st = 1;
-				}
-				if (ctr < 0) {
-					ctr = pol_resolve(s.pol, b2, bi2, id, eg, ep, &z);
-					st = 2;
-				}
-				if (ctr < 0 && !frag) {
-					ctr = pol_resolve(s.pol, b3, bi3, 0u, hi4, ep, &z);
-					st = 3;
-				}
-			} else {
-				if (!frag) {
-					ctr = pol_lookup(s.pol, id, hi4, ep, &z);
-					st = 1;
-				}
-				if (ctr < 0) {
-					ctr = pol_lookup(s.pol, id, eg, ep, &z);
-					st = 2;
-				}
-				if (ctr < 0 && !frag) {
-					ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
-					st = 3;
-				}
+			if (!frag) {
+				ctr = pol_lookup(s.pol, id, hi4, ep, &z);
+				st = 1;
+			}
+			if (ctr < 0) {
+				ctr = pol_lookup(s.pol, id, eg, ep, &z);
+				st = 2;
+			}
+			if (ctr < 0 && !frag) {
+				ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
+				st = 3;
 			}
 			if (ctr >= 0) {
 				const uint32_t c = (uint32_t)ctr;
@@ -563,46 +510,47 @@ static int classify_variant()
 	return v ? atoi(v) : 3;
 }
 
+/* CGPU_CLASSIFY_VARIANT selects the counter strategy (A/B in one process):
+ *   3 (default): LDS-privatized hot counters, 1024-thread workgroups
+ *   0: global atomics for every hit, 256-thread workgroups
+ *   9: no policy-entry counters (diagnostic ablation only; not the contract)
+ * Every variant but 9 computes identical results. */
 template <int V6>
 static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_t st)
 {
 	const int var = classify_variant();
-	if (var == 2 || var == 3) {
-		/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at
-		 * most 2^22 tuples per workgroup (packed-counter exactness) */
-		constexpr int NT = 1024;
-		const size_t lds = (size_t)s.hot_slots * 8u;
-		const uint64_t cap = 2ull * 256ull;
-		const uint64_t per_launch = cap * (1ull << 22);
-		for (uint64_t off = 0; off < a.n; off += per_launch) {
-			cls_args c = a;
-			const uint64_t m = std::min<uint64_t>(a.n - off, per_launch);
-			c.n = m;
-			c.verdict += off;
-			c.identity += off;
-			if (c.stage)
-				c.stage += off;
-			c.dport += off;
-			c.proto += off;
-			c.flags += off;
-			c.len += off;
-			c.ep += off;
-			c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
-			c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
-			const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
-			if (var == 2)
-				hipLaunchKernelGGL((k_classify<V6, 1, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
-			else
-				hipLaunchKernelGGL((k_classify<V6, 0, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
-		}
+	if (var == 0) {
+		hipLaunchKernelGGL((k_classify<V6, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 		return hipGetLastError();
 	}
-	if (var == 0)
-		hipLaunchKernelGGL((k_classify<V6, 0, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
-	else if (var == 9)
-		hipLaunchKernelGGL((k_classify<V6, 1, 2, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
-	else
-		hipLaunchKernelGGL((k_classify<V6, 1, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	if (var == 9) {
+		hipLaunchKernelGGL((k_classify<V6, 2, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+		return hipGetLastError();
+	}
+	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
+	 * 2^22 tuples per workgroup (packed-counter exactness) */
+	constexpr int NT = 1024;
+	const size_t lds = (size_t)s.hot_slots * 8u;
+	const uint64_t cap = 2ull * 256ull;
+	const uint64_t per_launch = cap * (1ull << 22);
+	for (uint64_t off = 0; off < a.n; off += per_launch) {
+		cls_args c = a;
+		const uint64_t m = std::min<uint64_t>(a.n - off, per_launch);
+		c.n = m;
+		c.verdict += off;
+		c.identity += off;
+		if (c.stage)
+			c.stage += off;
+		c.dport += off;
+		c.proto += off;
+		c.flags += off;
+		c.len += off;
+		c.ep += off;
+		c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
+		c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
+		const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
+		hipLaunchKernelGGL((k_classify<V6, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
+	}
 	return hipGetLastError();
 }
 

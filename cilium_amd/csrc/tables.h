@@ -55,9 +55,11 @@ typedef struct pol_slot {
 } pol_slot;
 
 typedef struct pol_table {
-	const pol_slot *slots; /* n_buckets * 4 */
+	const pol_slot *slots; /* n_buckets * slots_per_bucket */
 	uint32_t bucket_mask;
 	uint32_t max_probe;    /* longest probe sequence in buckets (>= 1) */
+	uint32_t slots_per_bucket; /* 4: 64-B buckets; 1: 16-B slots, one load per probe */
+	uint32_t pad_;
 } pol_table;
 
 static inline __host__ __device__ uint32_t pol_hash(uint32_t key_lo, uint32_t key_hi, uint32_t ep)
