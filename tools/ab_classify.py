@@ -1,10 +1,12 @@
-"""Interleaved same-process A/B of classify kernel variants (HIP events).
+"""Interleaved same-process A/B of classify configurations (HIP events).
 
-    python tools/ab_classify.py [--variants 0,1] [--rounds 5] [--iters 5] [--tuples N]
+    python tools/ab_classify.py [--configs 3:1,3:4,0:1] [--rounds 5] [--iters 5]
 
-Each round runs every variant `iters` times back to back; reports the median
-and min kernel time per variant over rounds and checks that every variant's
-outputs are bit-identical.
+A configuration is VARIANT:BPB[:LOADPCT] — the kernel counter strategy
+(CGPU_CLASSIFY_VARIANT) and the policy-table layout chosen at commit
+(CGPU_POL_BPB slots per bucket, CGPU_POL_LOAD_PCT load factor).  Each round
+runs every configuration `iters` times back to back; reports median / min
+kernel time and checks that every configuration's outputs are bit-identical.
 """
 import argparse
 import json
@@ -18,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,3,9")
+    ap.add_argument("--configs", default="3:1,3:4,0:1,9:1")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--tuples", type=int, default=64 << 20)
@@ -33,17 +35,30 @@ def main():
     cfg = dict(synth.CONFIGS[args.config])
     T = synth.make_tables(**cfg)
     t = synth.make_tuples(T, args.tuples)
-    e = Engine(device=0, **T.engine_config())
-    synth.load_engine(e, T)
-    e.commit()
     d = synth.to_device(t)
     n = args.tuples
-    variants = [int(v) for v in args.variants.split(",")]
-    outs = {}
-    times = {v: [] for v in variants}
+    confs = list(args.configs.split(","))
+    engines = {}
+    for c in confs:
+        parts = c.split(":")
+        key = tuple(parts[1:])
+        if key in engines:
+            continue
+        os.environ["CGPU_POL_BPB"] = parts[1] if len(parts) > 1 else "1"
+        if len(parts) > 2:
+            os.environ["CGPU_POL_LOAD_PCT"] = parts[2]
+        else:
+            os.environ.pop("CGPU_POL_LOAD_PCT", None)
+        e = Engine(device=0, **T.engine_config())
+        synth.load_engine(e, T)
+        e.commit()
+        engines[key] = e
+    outs, times = {}, {c: [] for c in confs}
     for r in range(args.rounds):
-        for v in variants:
-            os.environ["CGPU_CLASSIFY_VARIANT"] = str(v)
+        for c in confs:
+            parts = c.split(":")
+            os.environ["CGPU_CLASSIFY_VARIANT"] = parts[0]
+            e = engines[tuple(parts[1:])]
             out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
                    "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
             e.classify_v4(d, out=out)  # warm
@@ -54,15 +69,15 @@ def main():
                 e.classify_v4(d, out=out)
             b.record()
             torch.cuda.synchronize()
-            times[v].append(a.elapsed_time(b) / args.iters)
+            times[c].append(a.elapsed_time(b) / args.iters)
             if r == 0:
-                outs[v] = (out["verdict"].cpu().numpy(), out["identity"].cpu().numpy())
-    ref = outs[variants[0]]
+                outs[c] = (out["verdict"].cpu().numpy(), out["identity"].cpu().numpy())
+    ref = outs[confs[0]]
     res = {}
-    for v in variants:
-        same = all(np.array_equal(x, y) for x, y in zip(outs[v], ref))
-        med = statistics.median(times[v])
-        res[v] = {"median_ms": round(med, 4), "min_ms": round(min(times[v]), 4),
+    for c in confs:
+        same = all(np.array_equal(x, y) for x, y in zip(outs[c], ref))
+        med = statistics.median(times[c])
+        res[c] = {"median_ms": round(med, 4), "min_ms": round(min(times[c]), 4),
                   "gpps": round(n / med / 1e6, 3), "identical": same}
     print(json.dumps(res))
 
