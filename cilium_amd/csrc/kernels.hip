@@ -284,7 +284,7 @@ struct cls_args {
  * CTR = 2: no policy-entry counters (diagnostic ablation only; the results
  *          are NOT the reference's: its counters are part of the contract).
  */
-template <int V6, int CTR, int NT>
+template <int V6, int CTR, int NT, int ABL = 0>
 __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
@@ -311,7 +311,11 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		const bool gated = s.ct_proto_gate && proto != (V6 ? 58u : 1u) && proto != 6u &&
 				   proto != 17u;
 
-		if (gated) {
+		if (ABL == 1) {
+			/* diagnostic: columns in, outputs out, no table access */
+			v = (int32_t)(dport ^ proto ^ ep);
+			id = static_cast<const uint32_t *>(egress ? a.daddr : a.saddr)[i];
+		} else if (gated) {
 			v = DROP_CT_UNKNOWN_PROTO;
 			id = 0;
 			st = 4;
@@ -355,7 +359,9 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 			}
 			uint32_t z = 0;
 			int ctr = -1;
-			if (!frag) {
+			if (ABL == 2) {
+				/* diagnostic: identity resolution only */
+			} else if (!frag) {
 				ctr = pol_lookup(s.pol, id, hi4, ep, &z);
 				st = 1;
 			}
@@ -525,6 +531,18 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 	}
 	if (var == 9) {
 		hipLaunchKernelGGL((k_classify<V6, 2, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+		return hipGetLastError();
+	}
+	if (var == 20 || var == 21 || var == 22) {
+		/* diagnostic ablations at the default geometry, no counters:
+		 * 20 columns only, 21 + identity resolution, 22 + policy */
+		const unsigned g = (unsigned)std::min<uint64_t>((a.n + 1023) / 1024, 512);
+		if (var == 20)
+			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 1>), dim3(g), dim3(1024), 0, st, s, a);
+		else if (var == 21)
+			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 2>), dim3(g), dim3(1024), 0, st, s, a);
+		else
+			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 0>), dim3(g), dim3(1024), 0, st, s, a);
 		return hipGetLastError();
 	}
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
