@@ -427,6 +427,219 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 	}
 }
 
+/* Resolve one probe of the single-slot policy table whose first slot is
+ * already in registers; continues down the probe sequence (dependent loads)
+ * only when that slot holds another key. */
+__device__ __forceinline__ int pol_resolve1(const pol_table &t, uint4 sl, uint32_t b, uint32_t lo,
+					    uint32_t hi, uint32_t ep, uint32_t *z)
+{
+	const uint4 *tab = reinterpret_cast<const uint4 *>(t.slots);
+	for (uint32_t p = 0;;) {
+		if (sl.w == POL_EMPTY)
+			return -1;
+		if (sl.x == lo && sl.y == hi && (sl.z & 0xFFFFu) == ep) {
+			*z = sl.z;
+			return (int)sl.w;
+		}
+		if (++p >= t.max_probe)
+			return -1;
+		b = (b + 1) & t.bucket_mask;
+		sl = tab[b];
+	}
+}
+
+/*
+ * IPv4 classification with U tuples in flight per lane.  Same semantics as
+ * k_classify<0, 1, 1024> (the reference cascade, LDS hot counters); the
+ * U tuples of a lane advance stage by stage — columns, tbl24, tbl8, probe 1,
+ * probe 2, probe 3 — so each stage issues U independent loads before any
+ * of them is waited for.  Needs the single-slot policy layout.
+ * Tuple of lane t, step j, member u: i = (j * U + u) * T + t (T = lanes in
+ * the grid), so every member's column loads stay coalesced.
+ */
+template <int U, int MINW = 1>
+__global__ __launch_bounds__(1024, MINW) void k_classify_v4_ilp(cgpu_snapshot s, cls_args a)
+{
+	constexpr int NT = 1024;
+	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
+	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
+	const uint64_t T = (uint64_t)gridDim.x * NT;
+	const uint64_t t0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
+	uint64_t *pctr = a.delta;
+	const uint32_t *sa4 = static_cast<const uint32_t *>(a.saddr);
+	const uint32_t *da4 = static_cast<const uint32_t *>(a.daddr);
+	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
+	const uint32_t pmask = s.pol.bucket_mask;
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
+		lctr[k] = 0;
+	__syncthreads();
+
+	for (uint64_t base = 0; base * T + t0 < a.n; base += U) {
+		uint64_t idx[U];
+		bool ok[U], eg[U], gated[U], frag[U];
+		uint32_t fl[U], proto[U], len[U], dport[U], ep[U], ad[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			idx[u] = (base + u) * T + t0;
+			ok[u] = idx[u] < a.n;
+			const uint64_t i = ok[u] ? idx[u] : 0;
+			fl[u] = a.flags[i];
+			proto[u] = a.proto[i];
+			len[u] = a.len[i];
+			dport[u] = a.dport[i];
+			ep[u] = a.ep[i];
+			const uint32_t sv = sa4[i], dv = da4[i];
+			eg[u] = fl[u] & 1u;
+			ad[u] = eg[u] ? dv : sv;
+		}
+		/* stage: ipcache tbl24 */
+		uint32_t e[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			gated[u] = s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u;
+			frag[u] = !eg[u] && ((fl[u] >> 1) & 1u);
+			e[u] = 0;
+			if (ok[u] && !gated[u])
+				e[u] = s.ipc4.tbl24[bswap32(ad[u]) >> 8];
+		}
+		/* stage: tbl8 */
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP)
+				e[u] = s.ipc4.tbl8[(size_t)(e[u] & DIR_PAYLOAD_MASK) * 256u +
+						   (bswap32(ad[u]) & 255u)];
+		/* identity (bpf_lxc.c:488-496 / bpf_netdev.c:374-404) */
+		uint32_t id[U], hi4[U], egb[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t p = e[u] & DIR_PAYLOAD_MASK;
+			const uint32_t label =
+				(e[u] & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? s.ipc4.vals[p] : p;
+			if (eg[u]) {
+				if (e[u] && label)
+					id[u] = label;
+				else if ((ad[u] & s.ipv4_cluster_mask) == s.ipv4_cluster_range)
+					id[u] = s.cluster_id;
+				else
+					id[u] = s.world_id;
+			} else {
+				uint32_t src = s.ingress_src_identity;
+				if (src < s.health_id && e[u] && label && label != s.cluster_id &&
+				    label != s.host_id)
+					src = label;
+				id[u] = s.ingress_secctx_world ? s.world_id : src;
+			}
+			egb[u] = eg[u] ? (1u << 24) : 0u;
+			hi4[u] = dport[u] | (proto[u] << 16) | egb[u];
+		}
+		/* probe 1: exact {id, dport, proto, dir} (policy.h:61-72) */
+		int ctr[U];
+		uint32_t z[U], st[U], bk[U];
+		uint4 sl[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			ctr[u] = -1;
+			z[u] = 0;
+			st[u] = 0;
+			if (ok[u] && !gated[u] && !frag[u]) {
+				bk[u] = pol_hash(id[u], hi4[u], ep[u]) & pmask;
+				sl[u] = ptab[bk[u]];
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (ok[u] && !gated[u] && !frag[u]) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u], ep[u], &z[u]);
+				st[u] = 1;
+			}
+		/* probe 2: L3-only {id, 0, 0, dir} (policy.h:74-83) */
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0) {
+				bk[u] = pol_hash(id[u], egb[u], ep[u]) & pmask;
+				sl[u] = ptab[bk[u]];
+			}
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], egb[u], ep[u], &z[u]);
+				st[u] = 2;
+			}
+		/* probe 3: identity-wildcard L4 {0, dport, proto, dir} (policy.h:85-96) */
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
+				bk[u] = pol_hash(0u, hi4[u], ep[u]) & pmask;
+				sl[u] = ptab[bk[u]];
+			}
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], 0u, hi4[u], ep[u], &z[u]);
+				st[u] = 3;
+			}
+		/* counters, outputs, metrics */
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			if (!ok[u])
+				continue;
+			int32_t v;
+			if (gated[u]) {
+				v = DROP_CT_UNKNOWN_PROTO;
+				id[u] = 0;
+				st[u] = 4;
+			} else if (ctr[u] >= 0) {
+				const uint32_t c = (uint32_t)ctr[u];
+				if (c < s.hot_slots && len[u] < PK_MAX_LEN) {
+					atomicAdd((unsigned long long *)&lctr[c],
+						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
+				} else {
+					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
+					atomicAdd((unsigned long long *)&pctr[2u * c + 1u],
+						  (unsigned long long)len[u]);
+				}
+				v = st[u] == 2 ? 0 : (int32_t)(z[u] >> 16);
+			} else {
+				st[u] = 0;
+				v = DROP_POLICY;
+			}
+			const uint64_t i = idx[u];
+			a.verdict[i] = v;
+			a.identity[i] = id[u];
+			if (a.stage)
+				a.stage[i] = (uint8_t)st[u];
+			const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : 2u);
+			const uint32_t mi = r * 2u + (eg[u] ? 1u : 0u);
+#pragma unroll
+			for (int k = 0; k < 6; k++) {
+				mcnt[k] += (mi == (uint32_t)k) ? 1u : 0u;
+				mbyt[k] += (mi == (uint32_t)k) ? len[u] : 0u;
+			}
+		}
+	}
+
+	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
+	const uint32_t reasons[3] = {0u, 133u, 137u};
+#pragma unroll
+	for (int k = 0; k < 6; k++) {
+		uint64_t c = wave_sum(mcnt[k]);
+		uint64_t b = wave_sum(mbyt[k]);
+		if ((threadIdx.x & 63) == 0 && c) {
+			uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
+			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
+			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
+		}
+	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
+		const uint64_t v = lctr[k];
+		if (v) {
+			atomicAdd((unsigned long long *)&pctr[2u * k], v >> PK_SHIFT);
+			atomicAdd((unsigned long long *)&pctr[2u * k + 1u], v & PK_BYTES_MASK);
+		}
+	}
+}
+
 /* XDP prefilter IPv4 (bpf/bpf_xdp.c:97-121, :158-178) */
 __global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilter_args a)
 {
@@ -545,6 +758,7 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 0>), dim3(g), dim3(1024), 0, st, s, a);
 		return hipGetLastError();
 	}
+	const bool ilp = !V6 && s.pol.slots_per_bucket == 1 && (var >= 4 && var <= 7);
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
 	constexpr int NT = 1024;
@@ -567,7 +781,16 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 		c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
 		c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
 		const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
-		hipLaunchKernelGGL((k_classify<V6, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
+		if (ilp && var == 4)
+			hipLaunchKernelGGL((k_classify_v4_ilp<2>), dim3(g), dim3(NT), lds, st, s, c);
+		else if (ilp && var == 5)
+			hipLaunchKernelGGL((k_classify_v4_ilp<4>), dim3(g), dim3(NT), lds, st, s, c);
+		else if (ilp && var == 6)
+			hipLaunchKernelGGL((k_classify_v4_ilp<2, 8>), dim3(g), dim3(NT), lds, st, s, c);
+		else if (ilp)
+			hipLaunchKernelGGL((k_classify_v4_ilp<4, 4>), dim3(g), dim3(NT), lds, st, s, c);
+		else
+			hipLaunchKernelGGL((k_classify<V6, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
 	}
 	return hipGetLastError();
 }
