@@ -215,6 +215,9 @@ struct cgpu_ctx {
 	uint64_t *d_totals = nullptr; /* [2*slots + METRICS] */
 	uint64_t *d_delta_own = nullptr;
 	uint64_t *d_delta = nullptr;  /* own or bound */
+	/* [n_ctr_slots] packed counter accumulator per stream (zero between
+	 * classify calls; one per stream keeps its exactness bound per call) */
+	std::map<void *, uint64_t *> d_pk;
 };
 
 /* ======================================================================= */
@@ -299,6 +302,8 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 		(void)hipFree(c->arena);
 		(void)hipFree(c->d_totals);
 		(void)hipFree(c->d_delta_own);
+		for (auto &kv : c->d_pk)
+			(void)hipFree(kv.second);
 	}
 	delete c;
 }
@@ -1224,6 +1229,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.ingress_src_identity = c->cfg.ingress_src_identity;
 	s.n_ctr_slots = c->n_ctr_slots;
 	s.hot_slots = c->hot_cap;
+	s.cold_hi = c->next_cold;
 	s.epoch = ++c->epoch;
 	c->snap = s;
 	c->committed = true;
@@ -1262,7 +1268,8 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
 /* ======================================================================= */
 /* batch entry points                                                        */
 /* ======================================================================= */
-static int snapshot_for_launch(cgpu_ctx *c, cgpu_snapshot &s, uint64_t *&delta)
+static int snapshot_for_launch(cgpu_ctx *c, cgpu_snapshot &s, uint64_t *&delta,
+			       void *stream = nullptr, uint64_t **pk = nullptr)
 {
 	if (!c)
 		return fail(-EINVAL, "null context");
@@ -1273,6 +1280,21 @@ static int snapshot_for_launch(cgpu_ctx *c, cgpu_snapshot &s, uint64_t *&delta)
 		return fail(-ENOENT, "no committed snapshot (call cgpu_commit)");
 	s = c->snap;
 	delta = c->d_delta;
+	if (pk) {
+		auto it = c->d_pk.find(stream);
+		if (it == c->d_pk.end()) {
+			uint64_t *p = nullptr;
+			const size_t bytes = (size_t)c->n_ctr_slots * 8;
+			HIP_OR_EIO(hipSetDevice(c->device));
+			HIP_OR_EIO(hipMalloc((void **)&p, bytes));
+			if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+				(void)hipFree(p);
+				return fail(-EIO, "packed counter buffer init failed");
+			}
+			it = c->d_pk.emplace(stream, p).first;
+		}
+		*pk = it->second;
+	}
 	return 0;
 }
 
@@ -1280,8 +1302,8 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
 				 uint32_t *identity, uint8_t *stage, void *stream)
 {
 	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	uint64_t *delta, *pk = nullptr;
+	if (int r = snapshot_for_launch(c, s, delta, stream, &pk))
 		return r;
 	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
 			 !t->ep || !verdict || !identity)))
@@ -1289,7 +1311,7 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
 	if (!n)
 		return 0;
 	classify_v4_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
-			   verdict, identity, stage, delta, (uint64_t)n};
+			   verdict, identity, stage, delta, (uint64_t)n, pk};
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(launch_classify_v4(s, a, (hipStream_t)stream));
 	return 0;
@@ -1413,6 +1435,8 @@ CGPU_EXPORT int cgpu_counters_reset(cgpu_ctx *c)
 	HIP_OR_EIO(hipDeviceSynchronize());
 	HIP_OR_EIO(hipMemset(c->d_totals, 0, bytes));
 	HIP_OR_EIO(hipMemset(c->d_delta, 0, bytes));
+	for (auto &kv : c->d_pk)
+		HIP_OR_EIO(hipMemset(kv.second, 0, (size_t)c->n_ctr_slots * 8));
 	HIP_OR_EIO(hipDeviceSynchronize());
 	return 0;
 }

@@ -266,6 +266,7 @@ struct cls_args {
 	uint8_t *stage;
 	uint64_t *delta;
 	uint64_t n;
+	uint64_t *pk; /* packed cold-slot accumulator (k_classify_v4_x4 only) */
 };
 
 /* Packed per-workgroup counter: packets in bits 41..63, bytes in 0..40.
@@ -640,6 +641,261 @@ __global__ __launch_bounds__(1024, MINW) void k_classify_v4_ilp(cgpu_snapshot s,
 	}
 }
 
+/* Packed per-slot accumulator of k_classify_v4_x4 (pk): one u64 per counter
+ * slot, packets in bits 37..63, bytes in 0..36.  Exact while one launch adds
+ * at most PKC_CHUNK = 2^26 hits of < 2^11 bytes to a slot (2^26 * 2047 <
+ * 2^37): the launcher caps a launch at PKC_CHUNK tuples and unpacks pk into
+ * the delta buffer after it.  A packet of >= PKC_MAX_LEN bytes takes the
+ * two-word path into delta directly.  Each stream has its own pk buffer
+ * (host.cpp), so concurrent calls on one context never share the bound. */
+#define PKC_SHIFT 37
+#define PKC_BYTES_MASK ((1ull << PKC_SHIFT) - 1ull)
+#define PKC_MAX_LEN (1u << 11)
+#define PKC_CHUNK (1ull << 26)
+
+/*
+ * IPv4 classification, four consecutive tuples per lane per step.
+ * Same semantics as k_classify<0, 1, NT> (the reference cascade of
+ * policy.h:46-110 behind the identity resolution of bpf_lxc.c:484-500 /
+ * bpf_netdev.c:374-404).  Differences are all in the memory schedule:
+ *   - every column is read with one 4/8/16-byte load per lane (the wave reads
+ *     256 B .. 1 KiB contiguous per instruction instead of 64 B .. 256 B);
+ *   - the four tuples of a lane advance stage by stage (tbl24, tbl8, probe 1,
+ *     probe 2, probe 3), so each stage has four independent gathers in flight;
+ *   - a hit on a cold counter slot is ONE packed u64 atomic (pk), not two.
+ * Lane t of the grid (T lanes) handles tuples 4 * (j * T + t) + {0..3} at
+ * step j.  The launcher guarantees 16-byte aligned 4-byte columns, 8-byte
+ * aligned 2-byte columns and 4-byte aligned 1-byte columns; the one partial
+ * group at the end of the batch is read element by element.
+ */
+template <int NT, int CM = 0>
+__global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
+{
+	constexpr int Q = 4;
+	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
+	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
+	const uint64_t T = (uint64_t)gridDim.x * NT;
+	const uint64_t t0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
+	uint64_t *pctr = a.delta;
+	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
+	const uint32_t pmask = s.pol.bucket_mask;
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
+		lctr[k] = 0;
+	__syncthreads();
+
+	for (uint64_t g = t0; g * Q < a.n; g += T) {
+		const uint64_t i0 = g * Q;
+		const bool full = i0 + Q <= a.n;
+		uint32_t fl[Q], proto[Q], len[Q], dport[Q], ep[Q], sa[Q], da[Q];
+		if (full) {
+			const uint32_t f4 = *reinterpret_cast<const uint32_t *>(a.flags + i0);
+			const uint32_t p4 = *reinterpret_cast<const uint32_t *>(a.proto + i0);
+			const uint2 d4 = *reinterpret_cast<const uint2 *>(a.dport + i0);
+			const uint2 e4 = *reinterpret_cast<const uint2 *>(a.ep + i0);
+			const uint4 l4 = *reinterpret_cast<const uint4 *>(a.len + i0);
+			const uint4 s4 = *reinterpret_cast<const uint4 *>(static_cast<const uint32_t *>(a.saddr) + i0);
+			const uint4 a4 = *reinterpret_cast<const uint4 *>(static_cast<const uint32_t *>(a.daddr) + i0);
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				fl[u] = (f4 >> (8 * u)) & 0xFFu;
+				proto[u] = (p4 >> (8 * u)) & 0xFFu;
+			}
+			dport[0] = d4.x & 0xFFFFu, dport[1] = d4.x >> 16, dport[2] = d4.y & 0xFFFFu, dport[3] = d4.y >> 16;
+			ep[0] = e4.x & 0xFFFFu, ep[1] = e4.x >> 16, ep[2] = e4.y & 0xFFFFu, ep[3] = e4.y >> 16;
+			len[0] = l4.x, len[1] = l4.y, len[2] = l4.z, len[3] = l4.w;
+			sa[0] = s4.x, sa[1] = s4.y, sa[2] = s4.z, sa[3] = s4.w;
+			da[0] = a4.x, da[1] = a4.y, da[2] = a4.z, da[3] = a4.w;
+		} else {
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				const uint64_t i = i0 + u < a.n ? i0 + u : i0;
+				fl[u] = a.flags[i];
+				proto[u] = a.proto[i];
+				dport[u] = a.dport[i];
+				ep[u] = a.ep[i];
+				len[u] = a.len[i];
+				sa[u] = static_cast<const uint32_t *>(a.saddr)[i];
+				da[u] = static_cast<const uint32_t *>(a.daddr)[i];
+			}
+		}
+		bool ok[Q], eg[Q], gated[Q], frag[Q];
+		uint32_t ad[Q], e[Q];
+		/* stage: ipcache tbl24 */
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			ok[u] = i0 + u < a.n;
+			eg[u] = fl[u] & 1u;
+			ad[u] = eg[u] ? da[u] : sa[u];
+			gated[u] = s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u;
+			frag[u] = !eg[u] && ((fl[u] >> 1) & 1u);
+			e[u] = 0;
+			if (ok[u] && !gated[u])
+				e[u] = s.ipc4.tbl24[bswap32(ad[u]) >> 8];
+		}
+		/* stage: tbl8 */
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP)
+				e[u] = s.ipc4.tbl8[(size_t)(e[u] & DIR_PAYLOAD_MASK) * 256u + (bswap32(ad[u]) & 255u)];
+		/* identity (bpf_lxc.c:488-496 / bpf_netdev.c:374-404) */
+		uint32_t id[Q], hi4[Q], egb[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint32_t p = e[u] & DIR_PAYLOAD_MASK;
+			const uint32_t label = (e[u] & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? s.ipc4.vals[p] : p;
+			if (eg[u]) {
+				if (e[u] && label)
+					id[u] = label;
+				else if ((ad[u] & s.ipv4_cluster_mask) == s.ipv4_cluster_range)
+					id[u] = s.cluster_id;
+				else
+					id[u] = s.world_id;
+			} else {
+				uint32_t src = s.ingress_src_identity;
+				if (src < s.health_id && e[u] && label && label != s.cluster_id && label != s.host_id)
+					src = label;
+				id[u] = s.ingress_secctx_world ? s.world_id : src;
+			}
+			egb[u] = eg[u] ? (1u << 24) : 0u;
+			hi4[u] = dport[u] | (proto[u] << 16) | egb[u];
+		}
+		/* probe 1: exact {id, dport, proto, dir} (policy.h:61-72) */
+		int ctr[Q];
+		uint32_t z[Q], st[Q], bk[Q];
+		uint4 sl[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			ctr[u] = -1;
+			z[u] = 0;
+			st[u] = 0;
+			if (ok[u] && !gated[u] && !frag[u]) {
+				bk[u] = pol_hash(id[u], hi4[u], ep[u]) & pmask;
+				sl[u] = ptab[bk[u]];
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (ok[u] && !gated[u] && !frag[u]) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u], ep[u], &z[u]);
+				st[u] = 1;
+			}
+		/* probe 2: L3-only {id, 0, 0, dir} (policy.h:74-83) */
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0) {
+				bk[u] = pol_hash(id[u], egb[u], ep[u]) & pmask;
+				sl[u] = ptab[bk[u]];
+			}
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], egb[u], ep[u], &z[u]);
+				st[u] = 2;
+			}
+		/* probe 3: identity-wildcard L4 {0, dport, proto, dir} (policy.h:85-96) */
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
+				bk[u] = pol_hash(0u, hi4[u], ep[u]) & pmask;
+				sl[u] = ptab[bk[u]];
+			}
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], 0u, hi4[u], ep[u], &z[u]);
+				st[u] = 3;
+			}
+		/* counters, outputs, metrics */
+		int32_t v[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (gated[u]) {
+				v[u] = DROP_CT_UNKNOWN_PROTO;
+				id[u] = 0;
+				st[u] = 4;
+			} else if (ctr[u] >= 0) {
+				const uint32_t c = (uint32_t)ctr[u];
+				if (CM == 2) {
+					/* diagnostic: no policy-entry counters */
+				} else if (len[u] >= PKC_MAX_LEN) {
+					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
+					atomicAdd((unsigned long long *)&pctr[2u * c + 1u], (unsigned long long)len[u]);
+				} else if (c < s.hot_slots) {
+					atomicAdd((unsigned long long *)&lctr[c],
+						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
+				} else {
+					atomicAdd((unsigned long long *)&pk[c],
+						  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
+				}
+				v[u] = st[u] == 2 ? 0 : (int32_t)(z[u] >> 16);
+			} else {
+				st[u] = 0;
+				v[u] = DROP_POLICY;
+			}
+			if (ok[u]) {
+				const uint32_t r = v[u] >= 0 ? 0u : (v[u] == DROP_POLICY ? 1u : 2u);
+				const uint32_t mi = r * 2u + (eg[u] ? 1u : 0u);
+#pragma unroll
+				for (int k = 0; k < 6; k++) {
+					mcnt[k] += (mi == (uint32_t)k) ? 1u : 0u;
+					mbyt[k] += (mi == (uint32_t)k) ? len[u] : 0u;
+				}
+			}
+		}
+		if (full) {
+			*reinterpret_cast<int4 *>(a.verdict + i0) = make_int4(v[0], v[1], v[2], v[3]);
+			*reinterpret_cast<uint4 *>(a.identity + i0) = make_uint4(id[0], id[1], id[2], id[3]);
+			if (a.stage)
+				*reinterpret_cast<uint32_t *>(a.stage + i0) =
+					st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24);
+		} else {
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				if (ok[u]) {
+					a.verdict[i0 + u] = v[u];
+					a.identity[i0 + u] = id[u];
+					if (a.stage)
+						a.stage[i0 + u] = (uint8_t)st[u];
+				}
+		}
+	}
+
+	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
+	const uint32_t reasons[3] = {0u, 133u, 137u};
+#pragma unroll
+	for (int k = 0; k < 6; k++) {
+		uint64_t c = wave_sum(mcnt[k]);
+		uint64_t b = wave_sum(mbyt[k]);
+		if ((threadIdx.x & 63) == 0 && c) {
+			uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
+			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
+			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
+		}
+	}
+	__syncthreads();
+	/* one packed atomic per touched hot slot: PK (LDS) -> PKC (pk) format;
+	 * a workgroup's bytes per slot stay < 2^37 (<= 2^26 tuples of < 2^11) */
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
+		const uint64_t x = lctr[k];
+		if (x)
+			atomicAdd((unsigned long long *)&pk[k],
+				  ((x >> PK_SHIFT) << PKC_SHIFT) | (x & PK_BYTES_MASK));
+	}
+}
+
+/* delta[2s] += pk[s] >> 40; delta[2s+1] += pk[s] & (2^40-1); pk[s] = 0 */
+__global__ void k_unpack(uint64_t *delta, uint64_t *pk, uint32_t lo, uint32_t hi)
+{
+	for (uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x; s < hi; s += gridDim.x * blockDim.x) {
+		if (!pk[s])
+			continue;
+		/* atomic: classify calls on other streams may add meanwhile */
+		const uint64_t x = atomicExch((unsigned long long *)&pk[s], 0ull);
+		atomicAdd((unsigned long long *)&delta[2u * s], x >> PKC_SHIFT);
+		atomicAdd((unsigned long long *)&delta[2u * s + 1u], x & PKC_BYTES_MASK);
+	}
+}
+
 /* XDP prefilter IPv4 (bpf/bpf_xdp.c:97-121, :158-178) */
 __global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilter_args a)
 {
@@ -726,14 +982,89 @@ unsigned grid_for(uint64_t n)
 static int classify_variant()
 {
 	const char *v = getenv("CGPU_CLASSIFY_VARIANT");
-	return v ? atoi(v) : 3;
+	return v ? atoi(v) : 8;
 }
 
-/* CGPU_CLASSIFY_VARIANT selects the counter strategy (A/B in one process):
- *   3 (default): LDS-privatized hot counters, 1024-thread workgroups
+/* k_classify_v4_x4 reads columns as 4/8/16-byte vectors at tuple index
+ * multiples of 4: the column base pointers must be aligned to match. */
+static bool x4_aligned(const cls_args &a)
+{
+	const uintptr_t a16 = (uintptr_t)a.saddr | (uintptr_t)a.daddr | (uintptr_t)a.len |
+			      (uintptr_t)a.verdict | (uintptr_t)a.identity;
+	const uintptr_t a8 = (uintptr_t)a.dport | (uintptr_t)a.ep;
+	const uintptr_t a4 = (uintptr_t)a.proto | (uintptr_t)a.flags | (uintptr_t)a.stage;
+	return !(a16 & 15) && !(a8 & 7) && !(a4 & 3);
+}
+
+/* Workgroups of NT threads that k_classify_v4_x4 keeps resident on the
+ * device (CUs x occupancy), queried once per device. */
+template <int CM> static unsigned x4_resident_blocks(int NT, size_t lds)
+{
+	static unsigned cached[64];
+	int dev = 0;
+	(void)hipGetDevice(&dev);
+	if (dev >= 0 && dev < 64 && cached[dev])
+		return cached[dev];
+	int cus = 0, per_cu = 0;
+	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+		cus = 256;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_classify_v4_x4<1024, CM>, NT, lds) !=
+		    hipSuccess || per_cu <= 0)
+		per_cu = 1;
+	const unsigned r = (unsigned)(cus * per_cu);
+	if (dev >= 0 && dev < 64)
+		cached[dev] = r;
+	return r;
+}
+
+/* x4 schedule: one persistent-size grid (every workgroup resident, so the
+ * per-workgroup LDS counter flush is paid once per resident workgroup) per
+ * launch of <= PKC_CHUNK tuples, then the unpack of pk into delta. */
+static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream_t st, int var)
+{
+	constexpr int NT = 1024;
+	const size_t lds = (size_t)s.hot_slots * 8u;
+	const unsigned res = var == 12 ? x4_resident_blocks<2>(NT, lds) : x4_resident_blocks<0>(NT, lds);
+	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
+	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
+	for (uint64_t off = 0; off < a.n; off += chunk) {
+		cls_args c = a;
+		const uint64_t m = std::min<uint64_t>(a.n - off, chunk);
+		c.n = m;
+		c.verdict += off;
+		c.identity += off;
+		if (c.stage)
+			c.stage += off;
+		c.dport += off;
+		c.proto += off;
+		c.flags += off;
+		c.len += off;
+		c.ep += off;
+		c.saddr = static_cast<const uint32_t *>(a.saddr) + off;
+		c.daddr = static_cast<const uint32_t *>(a.daddr) + off;
+		const unsigned g = (unsigned)std::min<uint64_t>((m + 4 * NT - 1) / (4 * NT), res);
+		if (var == 12)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 2>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		else
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		if (s.cold_hi) {
+			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
+			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
+		}
+	}
+	return hipGetLastError();
+}
+
+/* CGPU_CLASSIFY_VARIANT selects the schedule (A/B in one process):
+ *   8 (default, IPv4): k_classify_v4_x4 — four tuples per lane, vector column
+ *      loads, LDS hot counters + one packed atomic per cold hit, resident grid
+ *      (needs aligned columns and the single-slot policy layout, else 3)
+ *   3 (default, IPv6 / fallback): one tuple per lane, LDS hot counters
  *   0: global atomics for every hit, 256-thread workgroups
- *   9: no policy-entry counters (diagnostic ablation only; not the contract)
- * Every variant but 9 computes identical results. */
+ *   4-7: k_classify_v4_ilp (U strided tuples per lane)
+ *   9, 12, 20-22: diagnostic ablations (no counters / partial work); their
+ *      results are NOT the reference's and they are never the default.
+ * Every non-diagnostic variant computes identical results. */
 template <int V6>
 static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_t st)
 {
@@ -758,6 +1089,8 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 0>), dim3(g), dim3(1024), 0, st, s, a);
 		return hipGetLastError();
 	}
+	if (!V6 && (var == 8 || var == 12) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
+		return launch_x4(s, a, st, var);
 	const bool ilp = !V6 && s.pol.slots_per_bucket == 1 && (var >= 4 && var <= 7);
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
@@ -798,13 +1131,13 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x, hipStream_t st)
 {
 	return launch_classify<0>(s, cls_args{x.saddr, x.daddr, x.dport, x.proto, x.flags, x.len, x.ep,
-					      x.verdict, x.identity, x.stage, x.delta, x.n}, st);
+					      x.verdict, x.identity, x.stage, x.delta, x.n, x.pk}, st);
 }
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)
 {
 	return launch_classify<1>(s, cls_args{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len,
-					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n}, st);
+					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, nullptr}, st);
 }
 
 hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)

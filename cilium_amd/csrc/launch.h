@@ -20,6 +20,7 @@ struct classify_v4_args {
 	uint8_t *stage;
 	uint64_t *delta; /* [2 * n_ctr_slots] policy + [CGPU_METRICS_WORDS] metrics */
 	uint64_t n;
+	uint64_t *pk;    /* [n_ctr_slots] packed cold-slot accumulator, zero between calls */
 };
 
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st);

@@ -150,6 +150,7 @@ typedef struct cgpu_snapshot {
 	uint32_t ct_proto_gate, ingress_secctx_world, ingress_src_identity;
 	uint32_t n_ctr_slots;
 	uint32_t hot_slots;      /* counter slots [0, hot_slots) may live in LDS */
+	uint32_t cold_hi;        /* counter slots >= cold_hi are unassigned */
 	uint64_t epoch;
 } cgpu_snapshot;
 

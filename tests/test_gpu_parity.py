@@ -391,7 +391,7 @@ def test_classify_v6_scale_vs_oracle(torch_cuda):
     e.close()
 
 
-@pytest.mark.parametrize("variant", [0, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 3, 4, 5, 6, 8])
 def test_kernel_variants_exact(torch_cuda, cfg1, variant, monkeypatch):
     """Every classify schedule / counter strategy gives the reference's
     verdicts, identities, stages, per-entry counters and metrics."""
@@ -427,4 +427,55 @@ def test_slot_reuse_within_one_commit(torch_cuda):
     e.commit()
     assert [int(x) for x in e.policy_lookup(0, b)[1][["packets", "bytes"]].item()] == [5, 500]
     assert [int(x) for x in e.policy_lookup(0, a)[1][["packets", "bytes"]].item()] == [9, 900]
+    e.close()
+
+
+@pytest.mark.parametrize("n", [1, 5, 4099, (1 << 20) - 3])
+@pytest.mark.parametrize("variant", [3, 8])
+def test_ragged_batches_long_packets(torch_cuda, cfg1, n, variant, monkeypatch):
+    """Batch sizes that are not a multiple of the per-lane group, and packet
+    lengths past every packed-counter bound (2^16 cold, 2^18 hot): verdicts,
+    identities, stages, per-entry counters and metrics stay exact."""
+    T, t_full = cfg1
+    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    t = {k: np.ascontiguousarray(v[:n]) for k, v in t_full.items()}
+    rng = np.random.default_rng(n)
+    t["len"] = rng.choice(np.array([64, 1500, 65535, 65536, 70000, 262143, 262144, 9_000_000],
+                                   np.uint32), n)
+    o, v0, i0, s0, _ = _oracle_run(T, t)
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    v, idt, st = _classify(torch_cuda, e, t)
+    np.testing.assert_array_equal(v, v0)
+    np.testing.assert_array_equal(idt, i0)
+    np.testing.assert_array_equal(st, s0)
+    for k, ep in zip(T.pol_keys[::5], T.pol_ep[::5]):
+        _, got = e.policy_lookup(int(ep), k)
+        _, raw = o.policy_lookup(int(ep), k)
+        exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(exp["packets"]), int(exp["bytes"]))
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
+
+
+def test_unaligned_columns_take_scalar_schedule(torch_cuda, cfg1, monkeypatch):
+    """Column views that start off a 16-byte boundary cannot use the vector
+    schedule; the launcher picks the per-element one and results stay exact."""
+    T, t_full = cfg1
+    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", "8")
+    n = 100_001
+    t = {k: np.ascontiguousarray(v[1:n + 1]) for k, v in t_full.items()}
+    o, v0, i0, s0, _ = _oracle_run(T, t)
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    d = synth.to_device({k: np.concatenate([x[:1], x]) for k, x in t.items()})
+    d = {k: x[1:] for k, x in d.items()}  # views one element past an aligned base
+    out = e.classify_v4(d, stage=True)
+    torch_cuda.cuda.synchronize()
+    np.testing.assert_array_equal(_np(out["verdict"]), v0)
+    np.testing.assert_array_equal(_np(out["identity"], np.uint32), i0)
+    np.testing.assert_array_equal(_np(out["stage"]), s0)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
     e.close()
