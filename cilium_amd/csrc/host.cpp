@@ -161,6 +161,136 @@ struct Dir248 {
 	}
 };
 
+/* ---------------- DIR-24-8 -> compressed LPM (tables.h lpm16c) ---------- */
+struct Lpm16cBuild {
+	std::vector<uint32_t> d16, nodes;
+	/* run list over one block: (start, leaf) with distinct neighbours */
+	typedef std::vector<std::pair<uint32_t, uint32_t>> Runs;
+	static void push(Runs &r, uint32_t start, uint32_t v)
+	{
+		if (r.empty() || r.back().second != v)
+			r.push_back({start, v});
+	}
+	/* a run node of kind 0..2 for <= LPMC_MAX_RUN_BOUNDS boundaries */
+	uint32_t emit_node(const Runs &r)
+	{
+		const uint32_t k = (uint32_t)r.size() - 1;
+		const uint32_t kind = k <= 2 ? 0u : (k <= 4 ? 1u : 2u);
+		const uint32_t nb = kind == 0 ? 1u : (kind == 1 ? 2u : 5u);
+		const uint32_t words = kind == 0 ? 4u : (kind == 1 ? 8u : 16u);
+		const uint32_t off = (uint32_t)(nodes.size() / 4);
+		nodes.resize(nodes.size() + words, 0u);
+		uint32_t *w = &nodes[(size_t)off * 4];
+		for (uint32_t i = 0; i < 2 * nb; i++) {
+			uint32_t b = i < k ? r[i + 1].first : 0xFFFFu;
+			w[i / 2] |= (i & 1) ? (b << 16) : b;
+		}
+		for (uint32_t i = 0; i <= 2 * nb && nb + i < words; i++)
+			w[nb + i] = r[std::min<uint32_t>(i, k)].second;
+		return DIR_TAG_GROUP | (kind << LPMC_KIND_SHIFT) | off;
+	}
+	uint32_t emit_array(const uint32_t *ent)
+	{
+		const uint32_t off = (uint32_t)(nodes.size() / 4);
+		nodes.insert(nodes.end(), ent, ent + 256);
+		return DIR_TAG_GROUP | (3u << LPMC_KIND_SHIFT) | off;
+	}
+	/* entry for 256 leaves over the last address byte */
+	uint32_t byte_level(const uint32_t *leaf)
+	{
+		Runs r;
+		for (uint32_t j = 0; j < 256; j++)
+			push(r, j, leaf[j]);
+		if (r.size() == 1)
+			return r[0].second;
+		if (r.size() - 1 <= LPMC_MAX_RUN_BOUNDS)
+			return emit_node(r);
+		return emit_array(leaf);
+	}
+	std::vector<uint32_t> x16, dict;
+	/* inline entries (x16) over the finished d16 + nodes */
+	void build_inline(const std::vector<Runs> &runs)
+	{
+		std::map<uint32_t, uint64_t> freq;
+		for (auto &r : runs)
+			if (r.size() <= 5)
+				for (auto &x : r)
+					freq[x.second]++;
+		std::vector<std::pair<uint64_t, uint32_t>> byf;
+		for (auto &kv : freq)
+			byf.push_back({kv.second, kv.first});
+		std::sort(byf.begin(), byf.end(), [](const std::pair<uint64_t, uint32_t> &a,
+						     const std::pair<uint64_t, uint32_t> &b) {
+			return a.first != b.first ? a.first > b.first : a.second < b.second;
+		});
+		dict.clear();
+		std::map<uint32_t, uint32_t> code;
+		for (auto &f : byf) {
+			if (dict.size() >= LPMC_DICT)
+				break;
+			code[f.second] = (uint32_t)dict.size();
+			dict.push_back(f.second);
+		}
+		x16.assign((size_t)65536 * 4, 0u);
+		for (uint32_t p = 0; p < 65536; p++) {
+			const Runs &r = runs[p];
+			uint32_t *w = &x16[(size_t)p * 4];
+			bool inl = r.size() <= 5;
+			for (size_t i = 0; inl && i < r.size(); i++)
+				inl = code.count(r[i].second) != 0;
+			if (!inl) {
+				w[0] = d16[p];
+				w[3] = LPMC_OVERFLOW;
+				continue;
+			}
+			const uint32_t k = (uint32_t)r.size() - 1;
+			uint64_t v = 0;
+			for (uint32_t i = 0; i < 4; i++) {
+				uint32_t b = i < k ? r[i + 1].first : 0xFFFFu;
+				w[i / 2] |= (i & 1) ? (b << 16) : b;
+			}
+			for (uint32_t i = 0; i < 5; i++)
+				v |= (uint64_t)code[r[std::min(i, k)].second] << (12 * i);
+			w[2] = (uint32_t)v;
+			w[3] = (uint32_t)(v >> 32);
+		}
+	}
+	void build(const std::vector<uint32_t> &tbl24, const std::vector<uint32_t> &tbl8)
+	{
+		d16.assign(65536, 0u);
+		nodes.clear();
+		std::vector<Runs> all(65536);
+		Runs r;
+		for (uint32_t p = 0; p < 65536; p++) {
+			const uint32_t *t = &tbl24[(size_t)p * 256];
+			r.clear();
+			for (uint32_t j = 0; j < 256 && r.size() <= LPMC_MAX_RUN_BOUNDS + 1; j++) {
+				if ((t[j] & DIR_TAG_MASK) != DIR_TAG_GROUP) {
+					push(r, j << 8, t[j]);
+					continue;
+				}
+				const uint32_t *g = &tbl8[(size_t)(t[j] & DIR_PAYLOAD_MASK) * 256];
+				for (uint32_t b = 0; b < 256; b++)
+					push(r, (j << 8) | b, g[b]);
+			}
+			if (r.size() == 1) {
+				d16[p] = r[0].second;
+			} else if (r.size() - 1 <= LPMC_MAX_RUN_BOUNDS) {
+				d16[p] = emit_node(r);
+			} else {
+				uint32_t ent[256];
+				for (uint32_t j = 0; j < 256; j++)
+					ent[j] = (t[j] & DIR_TAG_MASK) != DIR_TAG_GROUP
+							 ? t[j]
+							 : byte_level(&tbl8[(size_t)(t[j] & DIR_PAYLOAD_MASK) * 256]);
+				d16[p] = emit_array(ent);
+			}
+			all[p] = r;
+		}
+		build_inline(all);
+	}
+};
+
 struct Rank4 {
 	uint32_t rank; /* < 32: static-part entry (acts as /0 below every IP prefix) */
 	uint32_t addr; /* host order */
@@ -1130,6 +1260,12 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	build_pf6(c, pf6);
 
 	Arena ar;
+	Lpm16cBuild ipc4c;
+	ipc4c.build(ipc4.tbl24, ipc4.tbl8);
+	size_t o_c16 = ar.add(ipc4c.d16.data(), ipc4c.d16.size() * 4);
+	size_t o_cn = ar.add(ipc4c.nodes.data(), ipc4c.nodes.size() * 4);
+	size_t o_cx = ar.add(ipc4c.x16.data(), ipc4c.x16.size() * 4);
+	size_t o_cd = ar.add(ipc4c.dict.data(), ipc4c.dict.size() * 4);
 	size_t o_t24 = ar.add(ipc4.tbl24.data(), ipc4.tbl24.size() * 4);
 	size_t o_t8 = ar.add(ipc4.tbl8.data(), ipc4.tbl8.size() * 4);
 	size_t o_v = ar.add(ipc4.vals.data(), ipc4.vals.size() * 4);
@@ -1170,6 +1306,11 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 			init_by.push_back(s->bytes);
 		}
 	}
+	std::vector<uint8_t> slot_dir(c->n_ctr_slots, 0);
+	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+		for (auto &kv : c->pol[ep])
+			slot_dir[kv.second.slot] = ((kv.first >> 56) & 1u) ? 2 : 1;
+	size_t o_sd = ar.add(slot_dir.data(), slot_dir.size());
 	size_t o_is = ar.add(init_slot.data(), init_slot.size() * 4);
 	size_t o_ip = ar.add(init_pk.data(), init_pk.size() * 8);
 	size_t o_ib = ar.add(init_by.data(), init_by.size() * 8);
@@ -1198,6 +1339,10 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.ipc4 = dir248{(const uint32_t *)(arena + o_t24), (const uint32_t *)(arena + o_t8),
 			(const uint32_t *)(arena + o_v), (uint32_t)(ipc4.tbl8.size() / 256),
 			(uint32_t)ipc4.vals.size()};
+	s.ipc4c = lpm16c{(const uint32_t *)(arena + o_c16), (const uint32_t *)(arena + o_cn),
+			 (const uint32_t *)(arena + o_v), (const uint32_t *)(arena + o_cx),
+			 (const uint32_t *)(arena + o_cd), (uint32_t)ipc4c.nodes.size(),
+			 (uint32_t)ipc4c.dict.size()};
 	s.pol = pol_table{(const pol_slot *)(arena + o_pol), pol.mask, pol.max_probe, pol.bpb, 0};
 	if (have_pf4)
 		s.pf4 = dir248{(const uint32_t *)(arena + o_p24), (const uint32_t *)(arena + o_p8),
@@ -1230,6 +1375,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.n_ctr_slots = c->n_ctr_slots;
 	s.hot_slots = c->hot_cap;
 	s.cold_hi = c->next_cold;
+	s.slot_dir = (const uint8_t *)(arena + o_sd);
 	s.epoch = ++c->epoch;
 	c->snap = s;
 	c->committed = true;

@@ -37,6 +37,70 @@ __device__ __forceinline__ uint32_t dir_lookup(const dir248 &d, uint32_t addr_be
 	return e;
 }
 
+/* Streamed column access: with NTL the loads / stores carry the nontemporal
+ * hint (`nt`), so the 26 B/tuple stream does not evict table lines. */
+typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u_t __attribute__((ext_vector_type(2)));
+template <bool NTL> __device__ __forceinline__ uint4 ld_x4(const void *p)
+{
+	if (NTL) {
+		const v4u_t v = __builtin_nontemporal_load(static_cast<const v4u_t *>(p));
+		return make_uint4(v.x, v.y, v.z, v.w);
+	}
+	return *static_cast<const uint4 *>(p);
+}
+template <bool NTL> __device__ __forceinline__ uint2 ld_x2(const void *p)
+{
+	if (NTL) {
+		const v2u_t v = __builtin_nontemporal_load(static_cast<const v2u_t *>(p));
+		return make_uint2(v.x, v.y);
+	}
+	return *static_cast<const uint2 *>(p);
+}
+template <bool NTL> __device__ __forceinline__ uint32_t ld_x1(const void *p)
+{
+	if (NTL)
+		return __builtin_nontemporal_load(static_cast<const uint32_t *>(p));
+	return *static_cast<const uint32_t *>(p);
+}
+template <bool NTL> __device__ __forceinline__ void st_x4(void *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+	if (NTL) {
+		v4u_t v = {a, b, c, d};
+		__builtin_nontemporal_store(v, static_cast<v4u_t *>(p));
+	} else {
+		*static_cast<uint4 *>(p) = make_uint4(a, b, c, d);
+	}
+}
+template <bool NTL> __device__ __forceinline__ void st_x1(void *p, uint32_t a)
+{
+	if (NTL)
+		__builtin_nontemporal_store(a, static_cast<uint32_t *>(p));
+	else
+		*static_cast<uint32_t *>(p) = a;
+}
+
+/* Run-node search of the compressed LPM (tables.h lpm16c): q0..q3 hold the
+ * node's words (only the first 1 / 2 / 4 loaded for kind 0 / 1 / 2). */
+__device__ __forceinline__ uint32_t lpmc_search(uint4 q0, uint4 q1, uint4 q2, uint4 q3, uint32_t kind,
+						uint32_t x)
+{
+	const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+				q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+	const uint32_t nb = kind == 0 ? 1u : (kind == 1 ? 2u : 5u);
+	uint32_t cnt = 0;
+#pragma unroll
+	for (uint32_t i = 0; i < 5; i++)
+		if (i < nb)
+			cnt += (x >= (w[i] & 0xFFFFu) ? 1u : 0u) + (x >= (w[i] >> 16) ? 1u : 0u);
+	const uint32_t idx = nb + cnt;
+	uint32_t v = w[1];
+#pragma unroll
+	for (uint32_t j = 2; j < 16; j++)
+		v = j == idx ? w[j] : v;
+	return v;
+}
+
 /* Policy hash probe: exact 8-byte policy_key + endpoint.  Returns the
  * counter slot, or -1 (map_lookup_elem NULL); *z receives ep|proxy<<16.
  * The layout branch is on a kernarg (wave-uniform, scalar). */
@@ -668,82 +732,196 @@ __global__ __launch_bounds__(1024, MINW) void k_classify_v4_ilp(cgpu_snapshot s,
  * aligned 2-byte columns and 4-byte aligned 1-byte columns; the one partial
  * group at the end of the batch is read element by element.
  */
-template <int NT, int CM = 0>
-__global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
+template <int NT, int CM = 0, int LP = 1, bool NTL = false, int Q = 4, int MINW = 1>
+__global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
 {
-	constexpr int Q = 4;
+	/* per-tuple flag word */
+	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u;
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
-	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
+	/* metrics (drop.h:94-118) kept here only for drops and long forwarded
+	 * packets: [reason 0 / 133 / 137][ingress, egress] x {count, bytes};
+	 * every other forwarded packet is counted by k_unpack from pk, per the
+	 * direction of the entry it hit (metrics of the verdict = its entry's) */
+	__shared__ unsigned long long lmet[12];
 	const uint64_t T = (uint64_t)gridDim.x * NT;
 	const uint64_t t0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
 	uint64_t *pctr = a.delta;
 	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
 	const uint32_t pmask = s.pol.bucket_mask;
+	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots); /* LP == 2 */
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
+	if (threadIdx.x < 12)
+		lmet[threadIdx.x] = 0;
+	if (LP == 2)
+		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
+			ldict[k] = s.ipc4c.dict[k];
 	__syncthreads();
 
 	for (uint64_t g = t0; g * Q < a.n; g += T) {
 		const uint64_t i0 = g * Q;
 		const bool full = i0 + Q <= a.n;
-		uint32_t fl[Q], proto[Q], len[Q], dport[Q], ep[Q], sa[Q], da[Q];
-		if (full) {
-			const uint32_t f4 = *reinterpret_cast<const uint32_t *>(a.flags + i0);
-			const uint32_t p4 = *reinterpret_cast<const uint32_t *>(a.proto + i0);
-			const uint2 d4 = *reinterpret_cast<const uint2 *>(a.dport + i0);
-			const uint2 e4 = *reinterpret_cast<const uint2 *>(a.ep + i0);
-			const uint4 l4 = *reinterpret_cast<const uint4 *>(a.len + i0);
-			const uint4 s4 = *reinterpret_cast<const uint4 *>(static_cast<const uint32_t *>(a.saddr) + i0);
-			const uint4 a4 = *reinterpret_cast<const uint4 *>(static_cast<const uint32_t *>(a.daddr) + i0);
+		/* decode: hi4 = the policy key's upper word {dport, proto, egress}
+		 * (policy.h:61-64), fw = flag word, ad = the looked-up address */
+		uint32_t fw[Q], ad[Q], hi4[Q], ep[Q], len[Q];
+		{
+			uint32_t fl[Q], proto[Q], dport[Q], sa[Q], da[Q];
+			if (full && Q == 4) {
+				const uint32_t f4 = ld_x1<NTL>(a.flags + i0);
+				const uint32_t p4 = ld_x1<NTL>(a.proto + i0);
+				const uint2 d4 = ld_x2<NTL>(a.dport + i0);
+				const uint2 e4 = ld_x2<NTL>(a.ep + i0);
+				const uint4 l4 = ld_x4<NTL>(a.len + i0);
+				const uint4 s4 = ld_x4<NTL>(static_cast<const uint32_t *>(a.saddr) + i0);
+				const uint4 a4 = ld_x4<NTL>(static_cast<const uint32_t *>(a.daddr) + i0);
+				const uint32_t dd[4] = {d4.x & 0xFFFFu, d4.x >> 16, d4.y & 0xFFFFu, d4.y >> 16};
+				const uint32_t ee[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
+				const uint32_t ll[4] = {l4.x, l4.y, l4.z, l4.w};
+				const uint32_t ss[4] = {s4.x, s4.y, s4.z, s4.w};
+				const uint32_t aa[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					fl[u] = (f4 >> (8 * u)) & 0xFFu;
+					proto[u] = (p4 >> (8 * u)) & 0xFFu;
+					dport[u] = dd[u];
+					ep[u] = ee[u];
+					len[u] = ll[u];
+					sa[u] = ss[u];
+					da[u] = aa[u];
+				}
+			} else if (full && Q == 2) {
+				const uint32_t f2 = *reinterpret_cast<const uint16_t *>(a.flags + i0);
+				const uint32_t p2 = *reinterpret_cast<const uint16_t *>(a.proto + i0);
+				const uint32_t d2 = ld_x1<NTL>(a.dport + i0);
+				const uint32_t e2 = ld_x1<NTL>(a.ep + i0);
+				const uint2 l2 = ld_x2<NTL>(a.len + i0);
+				const uint2 s2 = ld_x2<NTL>(static_cast<const uint32_t *>(a.saddr) + i0);
+				const uint2 a2 = ld_x2<NTL>(static_cast<const uint32_t *>(a.daddr) + i0);
+				const uint32_t dd[2] = {d2 & 0xFFFFu, d2 >> 16}, ee[2] = {e2 & 0xFFFFu, e2 >> 16};
+				const uint32_t ll[2] = {l2.x, l2.y}, ss[2] = {s2.x, s2.y}, aa[2] = {a2.x, a2.y};
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					fl[u] = (f2 >> (8 * u)) & 0xFFu;
+					proto[u] = (p2 >> (8 * u)) & 0xFFu;
+					dport[u] = dd[u];
+					ep[u] = ee[u];
+					len[u] = ll[u];
+					sa[u] = ss[u];
+					da[u] = aa[u];
+				}
+			} else {
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					const uint64_t i = i0 + u < a.n ? i0 + u : i0;
+					fl[u] = a.flags[i];
+					proto[u] = a.proto[i];
+					dport[u] = a.dport[i];
+					ep[u] = a.ep[i];
+					len[u] = a.len[i];
+					sa[u] = static_cast<const uint32_t *>(a.saddr)[i];
+					da[u] = static_cast<const uint32_t *>(a.daddr)[i];
+				}
+			}
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
-				fl[u] = (f4 >> (8 * u)) & 0xFFu;
-				proto[u] = (p4 >> (8 * u)) & 0xFFu;
+				const bool eg = fl[u] & 1u;
+				const bool gated =
+					s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u;
+				fw[u] = (i0 + u < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) |
+					(!eg && ((fl[u] >> 1) & 1u) ? F_FRAG : 0u);
+				ad[u] = eg ? da[u] : sa[u];
+				hi4[u] = dport[u] | (proto[u] << 16) | (eg ? (1u << 24) : 0u);
 			}
-			dport[0] = d4.x & 0xFFFFu, dport[1] = d4.x >> 16, dport[2] = d4.y & 0xFFFFu, dport[3] = d4.y >> 16;
-			ep[0] = e4.x & 0xFFFFu, ep[1] = e4.x >> 16, ep[2] = e4.y & 0xFFFFu, ep[3] = e4.y >> 16;
-			len[0] = l4.x, len[1] = l4.y, len[2] = l4.z, len[3] = l4.w;
-			sa[0] = s4.x, sa[1] = s4.y, sa[2] = s4.z, sa[3] = s4.w;
-			da[0] = a4.x, da[1] = a4.y, da[2] = a4.z, da[3] = a4.w;
+		}
+		/* ipcache lookup (eps.h:70-80): first level (x16, d16 or tbl24) */
+		uint32_t e[Q];
+		if (LP == 2) {
+			/* one 16-byte gather: the /16's inline run node (tables.h) */
+			uint4 q[Q];
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				q[u] = make_uint4(0, 0, 0, 0);
+				if ((fw[u] & (F_OK | F_GATED)) == F_OK)
+					q[u] = reinterpret_cast<const uint4 *>(s.ipc4c.x16)[bswap32(ad[u]) >> 16];
+			}
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				if (q[u].w & LPMC_OVERFLOW) {
+					e[u] = q[u].x;
+					continue;
+				}
+				const uint32_t x = bswap32(ad[u]) & 0xFFFFu;
+				const uint32_t cnt = (x >= (q[u].x & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].x >> 16) ? 1u : 0u) +
+						     (x >= (q[u].y & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].y >> 16) ? 1u : 0u);
+				const uint64_t v = ((uint64_t)q[u].w << 32) | q[u].z;
+				e[u] = (fw[u] & (F_OK | F_GATED)) == F_OK ? ldict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
+			}
 		} else {
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
-				const uint64_t i = i0 + u < a.n ? i0 + u : i0;
-				fl[u] = a.flags[i];
-				proto[u] = a.proto[i];
-				dport[u] = a.dport[i];
-				ep[u] = a.ep[i];
-				len[u] = a.len[i];
-				sa[u] = static_cast<const uint32_t *>(a.saddr)[i];
-				da[u] = static_cast<const uint32_t *>(a.daddr)[i];
+				e[u] = 0;
+				if ((fw[u] & (F_OK | F_GATED)) == F_OK)
+					e[u] = LP ? s.ipc4c.d16[bswap32(ad[u]) >> 16] : s.ipc4.tbl24[bswap32(ad[u]) >> 8];
 			}
 		}
-		bool ok[Q], eg[Q], gated[Q], frag[Q];
-		uint32_t ad[Q], e[Q];
-		/* stage: ipcache tbl24 */
+		if (LP) {
+			/* compressed LPM (tables.h lpm16c): arrays (rare), then one run node */
+			constexpr uint32_t ARR = (DIR_TAG_GROUP >> LPMC_KIND_SHIFT) | 3u;
 #pragma unroll
-		for (int u = 0; u < Q; u++) {
-			ok[u] = i0 + u < a.n;
-			eg[u] = fl[u] & 1u;
-			ad[u] = eg[u] ? da[u] : sa[u];
-			gated[u] = s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u;
-			frag[u] = !eg[u] && ((fl[u] >> 1) & 1u);
-			e[u] = 0;
-			if (ok[u] && !gated[u])
-				e[u] = s.ipc4.tbl24[bswap32(ad[u]) >> 8];
+			for (int u = 0; u < Q; u++)
+				if ((e[u] >> LPMC_KIND_SHIFT) == ARR) {
+					e[u] = s.ipc4c.nodes[(size_t)(e[u] & LPMC_OFF_MASK) * 4u +
+							     ((bswap32(ad[u]) >> 8) & 255u)];
+					fw[u] |= F_LVL8; /* below an array: x is the last byte */
+				}
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				if ((e[u] >> LPMC_KIND_SHIFT) == ARR)
+					e[u] = s.ipc4c.nodes[(size_t)(e[u] & LPMC_OFF_MASK) * 4u + (bswap32(ad[u]) & 255u)];
+			/* the first 32 bytes of every node in flight together; the
+			 * rare 64-byte node reads its second half one tuple at a time */
+			uint4 q[Q][2];
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				q[u][0] = q[u][1] = make_uint4(0, 0, 0, 0);
+				if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP) {
+					const uint4 *nd = reinterpret_cast<const uint4 *>(s.ipc4c.nodes) +
+							  (e[u] & LPMC_OFF_MASK);
+					q[u][0] = nd[0];
+					if ((e[u] >> LPMC_KIND_SHIFT) & 3u)
+						q[u][1] = nd[1];
+				}
+			}
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				if ((e[u] & DIR_TAG_MASK) != DIR_TAG_GROUP)
+					continue;
+				const uint32_t kind = (e[u] >> LPMC_KIND_SHIFT) & 3u;
+				uint4 q2 = make_uint4(0, 0, 0, 0), q3 = q2;
+				if (kind == 2) {
+					const uint4 *nd = reinterpret_cast<const uint4 *>(s.ipc4c.nodes) +
+							  (e[u] & LPMC_OFF_MASK);
+					q2 = nd[2];
+					q3 = nd[3];
+				}
+				const uint32_t h = bswap32(ad[u]);
+				e[u] = lpmc_search(q[u][0], q[u][1], q2, q3, kind,
+						   (fw[u] & F_LVL8) ? (h & 255u) : (h & 0xFFFFu));
+			}
+		} else {
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP)
+					e[u] = s.ipc4.tbl8[(size_t)(e[u] & DIR_PAYLOAD_MASK) * 256u +
+							   (bswap32(ad[u]) & 255u)];
 		}
-		/* stage: tbl8 */
-#pragma unroll
-		for (int u = 0; u < Q; u++)
-			if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP)
-				e[u] = s.ipc4.tbl8[(size_t)(e[u] & DIR_PAYLOAD_MASK) * 256u + (bswap32(ad[u]) & 255u)];
 		/* identity (bpf_lxc.c:488-496 / bpf_netdev.c:374-404) */
-		uint32_t id[Q], hi4[Q], egb[Q];
+		uint32_t id[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint32_t p = e[u] & DIR_PAYLOAD_MASK;
 			const uint32_t label = (e[u] & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? s.ipc4.vals[p] : p;
-			if (eg[u]) {
+			if (fw[u] & F_EG) {
 				if (e[u] && label)
 					id[u] = label;
 				else if ((ad[u] & s.ipv4_cluster_mask) == s.ipv4_cluster_range)
@@ -756,8 +934,6 @@ __global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args
 					src = label;
 				id[u] = s.ingress_secctx_world ? s.world_id : src;
 			}
-			egb[u] = eg[u] ? (1u << 24) : 0u;
-			hi4[u] = dport[u] | (proto[u] << 16) | egb[u];
 		}
 		/* probe 1: exact {id, dport, proto, dir} (policy.h:61-72) */
 		int ctr[Q];
@@ -768,40 +944,40 @@ __global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args
 			ctr[u] = -1;
 			z[u] = 0;
 			st[u] = 0;
-			if (ok[u] && !gated[u] && !frag[u]) {
+			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK) {
 				bk[u] = pol_hash(id[u], hi4[u], ep[u]) & pmask;
 				sl[u] = ptab[bk[u]];
 			}
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if (ok[u] && !gated[u] && !frag[u]) {
+			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK) {
 				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u], ep[u], &z[u]);
 				st[u] = 1;
 			}
 		/* probe 2: L3-only {id, 0, 0, dir} (policy.h:74-83) */
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0) {
-				bk[u] = pol_hash(id[u], egb[u], ep[u]) & pmask;
+			if ((fw[u] & (F_OK | F_GATED)) == F_OK && ctr[u] < 0) {
+				bk[u] = pol_hash(id[u], hi4[u] & (1u << 24), ep[u]) & pmask;
 				sl[u] = ptab[bk[u]];
 			}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0) {
-				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], egb[u], ep[u], &z[u]);
+			if ((fw[u] & (F_OK | F_GATED)) == F_OK && ctr[u] < 0) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u] & (1u << 24), ep[u], &z[u]);
 				st[u] = 2;
 			}
 		/* probe 3: identity-wildcard L4 {0, dport, proto, dir} (policy.h:85-96) */
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
+			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK && ctr[u] < 0) {
 				bk[u] = pol_hash(0u, hi4[u], ep[u]) & pmask;
 				sl[u] = ptab[bk[u]];
 			}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
+			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK && ctr[u] < 0) {
 				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], 0u, hi4[u], ep[u], &z[u]);
 				st[u] = 3;
 			}
@@ -809,7 +985,7 @@ __global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args
 		int32_t v[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			if (gated[u]) {
+			if (fw[u] & F_GATED) {
 				v[u] = DROP_CT_UNKNOWN_PROTO;
 				id[u] = 0;
 				st[u] = 4;
@@ -820,6 +996,9 @@ __global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args
 				} else if (len[u] >= PKC_MAX_LEN) {
 					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
 					atomicAdd((unsigned long long *)&pctr[2u * c + 1u], (unsigned long long)len[u]);
+					const uint32_t mi = (fw[u] & F_EG) ? 2u : 0u;
+					atomicAdd(&lmet[mi], 1ull);
+					atomicAdd(&lmet[mi + 1u], (unsigned long long)len[u]);
 				} else if (c < s.hot_slots) {
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
@@ -832,26 +1011,26 @@ __global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args
 				st[u] = 0;
 				v[u] = DROP_POLICY;
 			}
-			if (ok[u]) {
-				const uint32_t r = v[u] >= 0 ? 0u : (v[u] == DROP_POLICY ? 1u : 2u);
-				const uint32_t mi = r * 2u + (eg[u] ? 1u : 0u);
-#pragma unroll
-				for (int k = 0; k < 6; k++) {
-					mcnt[k] += (mi == (uint32_t)k) ? 1u : 0u;
-					mbyt[k] += (mi == (uint32_t)k) ? len[u] : 0u;
-				}
+			if ((fw[u] & F_OK) && v[u] < 0) {
+				const uint32_t mi = ((v[u] == DROP_POLICY ? 1u : 2u) * 2u + ((fw[u] & F_EG) ? 1u : 0u)) * 2u;
+				atomicAdd(&lmet[mi], 1ull);
+				atomicAdd(&lmet[mi + 1u], (unsigned long long)len[u]);
 			}
 		}
-		if (full) {
-			*reinterpret_cast<int4 *>(a.verdict + i0) = make_int4(v[0], v[1], v[2], v[3]);
-			*reinterpret_cast<uint4 *>(a.identity + i0) = make_uint4(id[0], id[1], id[2], id[3]);
+		if (full && Q == 4) {
+			st_x4<NTL>(a.verdict + i0, (uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+			st_x4<NTL>(a.identity + i0, id[0], id[1], id[2], id[3]);
 			if (a.stage)
-				*reinterpret_cast<uint32_t *>(a.stage + i0) =
-					st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24);
+				st_x1<NTL>(a.stage + i0, st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24));
+		} else if (full && Q == 2) {
+			*reinterpret_cast<int2 *>(a.verdict + i0) = make_int2(v[0], v[1]);
+			*reinterpret_cast<uint2 *>(a.identity + i0) = make_uint2(id[0], id[1]);
+			if (a.stage)
+				*reinterpret_cast<uint16_t *>(a.stage + i0) = (uint16_t)(st[0] | (st[1] << 8));
 		} else {
 #pragma unroll
 			for (int u = 0; u < Q; u++)
-				if (ok[u]) {
+				if (fw[u] & F_OK) {
 					a.verdict[i0 + u] = v[u];
 					a.identity[i0 + u] = id[u];
 					if (a.stage)
@@ -861,16 +1040,12 @@ __global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args
 	}
 
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
-	const uint32_t reasons[3] = {0u, 133u, 137u};
-#pragma unroll
-	for (int k = 0; k < 6; k++) {
-		uint64_t c = wave_sum(mcnt[k]);
-		uint64_t b = wave_sum(mbyt[k]);
-		if ((threadIdx.x & 63) == 0 && c) {
-			uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
-			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
-			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
-		}
+	__syncthreads();
+	if (threadIdx.x < 12 && lmet[threadIdx.x]) {
+		const uint32_t reasons[3] = {0u, 133u, 137u};
+		const uint32_t c = threadIdx.x >> 1;
+		const uint32_t key = (reasons[c >> 1] * 4u + ((c & 1) ? 2u : 1u)) * 2u + (threadIdx.x & 1u);
+		atomicAdd((unsigned long long *)&met[key], lmet[threadIdx.x]);
 	}
 	__syncthreads();
 	/* one packed atomic per touched hot slot: PK (LDS) -> PKC (pk) format;
@@ -883,16 +1058,30 @@ __global__ __launch_bounds__(NT) void k_classify_v4_x4(cgpu_snapshot s, cls_args
 	}
 }
 
-/* delta[2s] += pk[s] >> 40; delta[2s+1] += pk[s] & (2^40-1); pk[s] = 0 */
-__global__ void k_unpack(uint64_t *delta, uint64_t *pk, uint32_t lo, uint32_t hi)
+/* delta[2s] += pk[s] >> 37; delta[2s+1] += pk[s] & (2^37-1); pk[s] = 0, and
+ * the forwarded metrics (reason 0, drop.h:104 / l3.h:119-130) of the packets
+ * unpacked, by the direction of their entry (slot_dir: 1 ingress, 2 egress) */
+__global__ __launch_bounds__(256) void k_unpack(uint64_t *delta, uint64_t *pk, uint32_t lo, uint32_t hi,
+						  const uint8_t *slot_dir, uint64_t *met)
 {
+	uint64_t sum[4] = {0, 0, 0, 0}; /* ingress pk, bytes, egress pk, bytes */
 	for (uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x; s < hi; s += gridDim.x * blockDim.x) {
 		if (!pk[s])
 			continue;
 		/* atomic: classify calls on other streams may add meanwhile */
 		const uint64_t x = atomicExch((unsigned long long *)&pk[s], 0ull);
-		atomicAdd((unsigned long long *)&delta[2u * s], x >> PKC_SHIFT);
-		atomicAdd((unsigned long long *)&delta[2u * s + 1u], x & PKC_BYTES_MASK);
+		const uint64_t np = x >> PKC_SHIFT, nb = x & PKC_BYTES_MASK;
+		atomicAdd((unsigned long long *)&delta[2u * s], np);
+		atomicAdd((unsigned long long *)&delta[2u * s + 1u], nb);
+		const bool eg = slot_dir[s] == 2;
+		sum[eg ? 2 : 0] += np;
+		sum[eg ? 3 : 1] += nb;
+	}
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		const uint64_t v = wave_sum(sum[k]);
+		if ((threadIdx.x & 63) == 0 && v)
+			atomicAdd((unsigned long long *)&met[(k < 2 ? 1u : 2u) * 2u + (k & 1)], v);
 	}
 }
 
@@ -1008,7 +1197,7 @@ template <int CM> static unsigned x4_resident_blocks(int NT, size_t lds)
 	int cus = 0, per_cu = 0;
 	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
 		cus = 256;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_classify_v4_x4<1024, CM>, NT, lds) !=
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_classify_v4_x4<1024, CM, 2, true>, NT, lds) !=
 		    hipSuccess || per_cu <= 0)
 		per_cu = 1;
 	const unsigned r = (unsigned)(cus * per_cu);
@@ -1024,7 +1213,8 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 {
 	constexpr int NT = 1024;
 	const size_t lds = (size_t)s.hot_slots * 8u;
-	const unsigned res = var == 12 ? x4_resident_blocks<2>(NT, lds) : x4_resident_blocks<0>(NT, lds);
+	const size_t lds2 = lds + (size_t)s.ipc4c.n_dict * 4u; /* + LDS leaf dictionary */
+	const unsigned res = var == 12 ? x4_resident_blocks<2>(NT, lds2) : x4_resident_blocks<0>(NT, lds2);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
 	for (uint64_t off = 0; off < a.n; off += chunk) {
@@ -1043,13 +1233,29 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 		c.saddr = static_cast<const uint32_t *>(a.saddr) + off;
 		c.daddr = static_cast<const uint32_t *>(a.daddr) + off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + 4 * NT - 1) / (4 * NT), res);
-		if (var == 12)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 2>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		const unsigned g2 = (unsigned)std::min<uint64_t>((m + 2 * NT - 1) / (2 * NT), 2 * res); /* Q=2 */
+		if (var == 8 && s.ipc4c.x16)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
+		else if (var == 17 && s.ipc4c.x16)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true, 2, 8>), dim3(g2), dim3(NT), lds2, st, s, c, a.pk);
+		else if (var == 18)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0, true, 2, 8>), dim3(g2), dim3(NT), lds, st, s, c, a.pk);
+		else if (var == 16 && s.ipc4c.x16)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, false>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
+		else if (var == 12)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 2, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
+		else if (var == 14)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 1, true>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		else if (var == 15)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0, true>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		else if (var == 13 || !s.ipc4c.d16)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		else
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 1>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
-			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
+			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi,
+					   s.slot_dir, a.delta + 2ull * s.n_ctr_slots);
 		}
 	}
 	return hipGetLastError();
@@ -1089,7 +1295,7 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 0>), dim3(g), dim3(1024), 0, st, s, a);
 		return hipGetLastError();
 	}
-	if (!V6 && (var == 8 || var == 12) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
+	if (!V6 && (var == 8 || (var >= 12 && var <= 18)) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
 		return launch_x4(s, a, st, var);
 	const bool ilp = !V6 && s.pol.slots_per_bucket == 1 && (var >= 4 && var <= 7);
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most

@@ -37,6 +37,48 @@ typedef struct dir248 {
 	uint32_t n_vals;
 } dir248;
 
+/* ---- compressed IPv4 longest-prefix table (L2-resident ipcache) ----
+ * The same function as a dir248 (it is compiled FROM one), in ~1/50 of the
+ * bytes, so that it stays in every XCD's 4 MiB L2 instead of being served
+ * from the Infinity Cache.  d16[addr >> 16] holds a DIR entry (0 / direct /
+ * indirect leaf, as dir248) or a GROUP reference
+ *   bits 28..29 kind, bits 0..27 offset in 16-byte units into `nodes`:
+ *   kind 0/1/2: a run node of 16 / 32 / 64 bytes over the low 16 bits (or,
+ *               below an array, the low 8 bits) x of the address:
+ *               NB = 1 / 2 / 5 words of u16 run starts b_1 < .. < b_2NB
+ *               (unused ones 0xFFFF, whose value repeats the last), then
+ *               2NB + 1 u32 leaf values; result = value[#{i : b_i <= x}]
+ *   kind 3:     an array of 256 u32 entries indexed by the next address
+ *               byte; an entry is a leaf, a run node (kind 0..2) over the
+ *               last byte, or (below d16 only) another kind-3 array of 256
+ *               leaves (the last byte, like a tbl8 group).
+ * Leaves use the dir248 entry encoding and share its `vals`. */
+#define LPMC_KIND_SHIFT 28u
+#define LPMC_OFF_MASK ((1u << LPMC_KIND_SHIFT) - 1u)
+#define LPMC_MAX_RUN_BOUNDS 10u
+
+/* x16[addr >> 16]: a 16-byte INLINE run node per /16, so that most lookups
+ * are ONE 16-byte gather from a 1 MiB table:
+ *   words 0..1: u16 run starts b_1..b_4 (unused 0xFFFF, value repeats)
+ *   words 2..3: u64 V, code_i = (V >> 12 i) & 0xFFF for i = 0..4, the
+ *               leaf of run i as an index into `dict` (kept in LDS);
+ *               bit 63 set = overflow: word 0 is then a d16-style entry
+ *               (leaf, or GROUP reference into `nodes`).
+ * A /16 goes inline when it has <= 4 run starts and every leaf has a code
+ * (the LPMC_DICT most frequent leaves get one). */
+#define LPMC_DICT 4095u
+#define LPMC_OVERFLOW (1u << 31)
+
+typedef struct lpm16c {
+	const uint32_t *d16;   /* 65536 entries; NULL = not compiled */
+	const uint32_t *nodes; /* 16-byte aligned */
+	const uint32_t *vals;
+	const uint32_t *x16;   /* 65536 x 4 words (inline run nodes) */
+	const uint32_t *dict;  /* leaf per code */
+	uint32_t n_node_words;
+	uint32_t n_dict;
+} lpm16c;
+
 /* ---- policy hash: one open-addressing table for all endpoints ----
  * 64-byte buckets (one cache-line sector) of 4 x 16-byte slots:
  *   x = sec_label, y = dport | proto << 16 | egress_pad << 24,
@@ -135,6 +177,7 @@ typedef struct v6_lpm {
 /* ---- one committed snapshot ---- */
 typedef struct cgpu_snapshot {
 	dir248 ipc4;
+	lpm16c ipc4c;    /* the same ipcache v4 function, compressed */
 	pol_table pol;
 	dir248 pf4;      /* any-match: dyn4 (if enabled) + fix4 /32 */
 	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
@@ -151,6 +194,7 @@ typedef struct cgpu_snapshot {
 	uint32_t n_ctr_slots;
 	uint32_t hot_slots;      /* counter slots [0, hot_slots) may live in LDS */
 	uint32_t cold_hi;        /* counter slots >= cold_hi are unassigned */
+	const uint8_t *slot_dir; /* per counter slot: 1 ingress, 2 egress key, 0 free */
 	uint64_t epoch;
 } cgpu_snapshot;
 

@@ -479,3 +479,64 @@ def test_unaligned_columns_take_scalar_schedule(torch_cuda, cfg1, monkeypatch):
     np.testing.assert_array_equal(_np(out["stage"]), s0)
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     e.close()
+
+
+def _lpm_shapes_tables(rng):
+    """ipcache contents that force every compressed-LPM shape (tables.h
+    lpm16c): uniform /16 leaves, 16/32/64-byte run nodes, /16 arrays whose
+    /24 entries are leaves, byte-level run nodes or 256-leaf arrays, run
+    starts at the last address of a /16, tombstones and labels >= 2^30."""
+    cidrs = [("0.0.0.0/0", L.WORLD_ID), ("10.7.0.0/16", L.CLUSTER_ID)]
+    lab = lambda: int(rng.choice([rng.integers(256, 70000), rng.integers(1 << 30, 1 << 32)]))
+    cidrs += [(f"20.1.{16 * i}.0/20", lab()) for i in range(2)]            # kind 0/1 nodes
+    cidrs += [(f"20.2.{3 * i}.0/24", lab()) for i in range(5)]             # kind 2 node
+    cidrs += [(f"20.3.{7 * i}.0/24", lab()) for i in range(11)]            # /16 array of leaves
+    cidrs += [("20.4.255.255/32", lab()), ("20.4.0.0/32", lab()), ("20.5.128.0/17", 0)]
+    cidrs += [(f"20.6.{i}.{j}/32", lab()) for i in range(0, 256, 3) for j in rng.choice(256, 40, replace=False)]
+    cidrs += [(f"20.6.{i}.{16 * j}/28", lab()) for i in range(1, 256, 3) for j in range(0, 16, 5)]
+    cidrs += [(f"20.7.{i}.{4 * j}/30", lab()) for i in range(8) for j in range(0, 64, 2)]
+    cidrs += [("20.8.0.0/16", 0), ("20.8.1.0/24", lab()), ("20.9.0.0/15", lab())]
+    seen, keys, vals = set(), [], []
+    for c, v in cidrs:
+        if c in seen:
+            continue
+        seen.add(c)
+        keys.append(L.ipcache_key(c))
+        vals.append(L.remote_info(v, 0))
+    return np.array(keys), np.array(vals)
+
+
+@pytest.mark.parametrize("variant", [3, 8])
+def test_lpm_shapes_exact(torch_cuda, variant, monkeypatch):
+    """Every ipcache LPM table shape resolves the same identity as the
+    restatement (egress lookups of daddr; ingress of saddr)."""
+    from oracle import Oracle
+    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    rng = np.random.default_rng(7)
+    keys, vals = _lpm_shapes_tables(rng)
+    n = 1 << 18
+    hi = rng.choice(np.array([0x1401, 0x1402, 0x1403, 0x1404, 0x1405, 0x1406, 0x1407, 0x1408,
+                              0x1409, 0x140A, 0x0A07, 0x0B00], np.uint32), n)
+    lo = rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    edge = rng.random(n) < 0.2
+    lo = np.where(edge, rng.choice(np.array([0, 1, 255, 256, 0x7FFF, 0x8000, 0xFFFE, 0xFFFF],
+                                            np.uint32), n), lo)
+    addr = ((hi << 16) | lo).astype(np.uint32).byteswap()
+    t = {"saddr": addr, "daddr": addr[::-1].copy(),
+         "dport": np.full(n, L.htons(80), np.uint16), "proto": np.full(n, 6, np.uint8),
+         "flags": (rng.random(n) < 0.5).astype(np.uint8), "len": np.full(n, 100, np.uint32),
+         "ep": np.zeros(n, np.uint16)}
+    e = _engine(policy_max_total=1 << 12, max_endpoints=4)
+    o = Oracle()
+    for k, v in zip(keys, vals):
+        assert e.ipcache_update(k, v) == 0 and o.ipcache_update(k, v) == 0
+    pk, pe = L.policy_key(0, 80, 6, 1), L.policy_entry(0)
+    assert e.policy_update(0, pk, pe) == 0 and o.policy_update(0, pk, pe) == 0
+    e.commit()
+    v0, i0, s0, _ = o.classify_v4(t, nthreads=8)
+    v, idt, st = _classify(torch_cuda, e, t)
+    np.testing.assert_array_equal(idt, i0)
+    np.testing.assert_array_equal(v, v0)
+    np.testing.assert_array_equal(st, s0)
+    assert len(np.unique(i0)) > 1000
+    e.close()
