@@ -392,6 +392,8 @@ CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **o
 		return fail(-EINVAL, "abi_version %u != %u", cfg->abi_version, CGPU_ABI_VERSION);
 	if (!cfg->max_endpoints || !cfg->policy_max_total)
 		return fail(-EINVAL, "zero capacity");
+	if (cfg->policy_max_total >= POL_CTR_EMPTY)
+		return fail(-EINVAL, "policy_max_total %u >= 2^24 - 1", cfg->policy_max_total);
 	cgpu_ctx *c = new cgpu_ctx();
 	c->cfg = *cfg;
 	c->pol.resize(cfg->max_endpoints);
@@ -988,19 +990,58 @@ static uint32_t env_u32(const char *name, uint32_t dflt)
 	return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
 }
 
-/* Policy hash layout.  Default: 16-byte single-slot buckets (one random
- * dwordx4 load per probe) at <= 25% load, so most probes resolve on the
- * first slot; CGPU_POL_BPB=4 selects 64-byte 4-slot buckets at <= 50%. */
+/* Policy hash layout.  Default: 16-byte single-slot neighbourhood hashing
+ * (tables.h POL_HOP) at <= 50% load: a lookup is one random 16-byte gather
+ * unless the home slot's hop bits name other slots.  CGPU_POL_BPB=4 selects
+ * 64-byte 4-slot buckets with linear bucket probing at <= 50% load. */
+static void place_pol_hop(PolBuild &b, const std::vector<std::array<uint32_t, 4>> &keys, uint32_t nb)
+{
+	for (;;) {
+		b.slots.assign(nb, pol_slot{0, 0, 0, POL_CTR_EMPTY});
+		b.mask = nb - 1;
+		bool ok = true;
+		for (auto &k : keys) {
+			const uint32_t home = pol_hash(k[0], k[1], k[2] & 0xFFFFu) & b.mask;
+			uint32_t d = 0;
+			while (d < POL_HOP && (b.slots[(home + d) & b.mask].ctr & POL_CTR_MASK) != POL_CTR_EMPTY)
+				d++;
+			if (d == POL_HOP) {
+				ok = false; /* neighbourhood full: grow */
+				break;
+			}
+			pol_slot &sl = b.slots[(home + d) & b.mask];
+			sl.key_lo = k[0];
+			sl.key_hi = k[1];
+			sl.ep_proxy = k[2];
+			sl.ctr = (sl.ctr & ~POL_CTR_MASK) | k[3];
+			b.slots[home].ctr |= 1u << (POL_HOP_SHIFT + d);
+		}
+		if (ok)
+			return;
+		nb *= 2;
+	}
+}
+
 void build_pol(const cgpu_ctx *c, PolBuild &b)
 {
 	b.bpb = env_u32("CGPU_POL_BPB", 1) == 4 ? 4 : 1;
 	const uint32_t load_pct = std::max<uint32_t>(5, std::min<uint32_t>(
-		env_u32("CGPU_POL_LOAD_PCT", b.bpb == 1 ? 25 : 50), 90));
+		env_u32("CGPU_POL_LOAD_PCT", 50), 90));
 	const uint64_t want_slots = (c->pol_total * 100 + load_pct - 1) / load_pct + 1;
 	uint32_t nb = next_pow2(std::max<uint64_t>(64, (want_slots + b.bpb - 1) / b.bpb));
+	b.max_probe = 1;
+	if (b.bpb == 1) {
+		std::vector<std::array<uint32_t, 4>> keys;
+		keys.reserve(c->pol_total);
+		for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+			for (auto &kv : c->pol[ep])
+				keys.push_back({(uint32_t)kv.first, (uint32_t)(kv.first >> 32),
+						ep | (uint32_t)kv.second.proxy_port << 16, kv.second.slot});
+		place_pol_hop(b, keys, nb);
+		return;
+	}
 	b.slots.assign((size_t)nb * b.bpb, pol_slot{0, 0, 0, POL_EMPTY});
 	b.mask = nb - 1;
-	b.max_probe = 1;
 	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
 		for (auto &kv : c->pol[ep]) {
 			uint32_t lo = (uint32_t)kv.first, hi = (uint32_t)(kv.first >> 32);

@@ -101,6 +101,33 @@ __device__ __forceinline__ uint32_t lpmc_search(uint4 q0, uint4 q1, uint4 q2, ui
 	return v;
 }
 
+/* Resolve a lookup in the single-slot (neighbourhood) policy table whose home
+ * slot b is already in registers (tables.h POL_HOP): returns the counter slot
+ * or -1 (map_lookup_elem NULL); *z receives ep | proxy_port << 16.  Further
+ * (dependent) loads only for the hop bits beyond the home slot itself. */
+__device__ __forceinline__ int pol_resolve1(const pol_table &t, uint4 sl, uint32_t b, uint32_t lo,
+					    uint32_t hi, uint32_t ep, uint32_t *z)
+{
+	uint32_t hop = sl.w >> POL_HOP_SHIFT;
+	if ((hop & 1u) && sl.x == lo && sl.y == hi && (sl.z & 0xFFFFu) == ep) {
+		*z = sl.z;
+		return (int)(sl.w & POL_CTR_MASK);
+	}
+	hop &= ~1u;
+	const uint4 *tab = reinterpret_cast<const uint4 *>(t.slots);
+	int r = -1;
+	while (hop && r < 0) {
+		const uint32_t j = __builtin_ctz(hop);
+		hop &= hop - 1u;
+		const uint4 x = tab[(b + j) & t.bucket_mask];
+		if (x.x == lo && x.y == hi && (x.z & 0xFFFFu) == ep) {
+			*z = x.z;
+			r = (int)(x.w & POL_CTR_MASK);
+		}
+	}
+	return r;
+}
+
 /* Policy hash probe: exact 8-byte policy_key + endpoint.  Returns the
  * counter slot, or -1 (map_lookup_elem NULL); *z receives ep|proxy<<16.
  * The layout branch is on a kernarg (wave-uniform, scalar). */
@@ -108,20 +135,8 @@ __device__ __forceinline__ int pol_lookup(const pol_table &t, uint32_t lo, uint3
 					  uint32_t *z)
 {
 	uint32_t b = pol_hash(lo, hi, ep) & t.bucket_mask;
-	if (t.slots_per_bucket == 1) {
-		const uint4 *sl = reinterpret_cast<const uint4 *>(t.slots);
-		for (uint32_t p = 0; p < t.max_probe; p++) {
-			const uint4 s = sl[b];
-			if (s.w == POL_EMPTY)
-				return -1;
-			if (s.x == lo && s.y == hi && (s.z & 0xFFFFu) == ep) {
-				*z = s.z;
-				return (int)s.w;
-			}
-			b = (b + 1) & t.bucket_mask;
-		}
-		return -1;
-	}
+	if (t.slots_per_bucket == 1)
+		return pol_resolve1(t, reinterpret_cast<const uint4 *>(t.slots)[b], b, lo, hi, ep, z);
 	for (uint32_t p = 0; p < t.max_probe; p++) {
 		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
 		uint4 s[4];
@@ -492,218 +507,6 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 	}
 }
 
-/* Resolve one probe of the single-slot policy table whose first slot is
- * already in registers; continues down the probe sequence (dependent loads)
- * only when that slot holds another key. */
-__device__ __forceinline__ int pol_resolve1(const pol_table &t, uint4 sl, uint32_t b, uint32_t lo,
-					    uint32_t hi, uint32_t ep, uint32_t *z)
-{
-	const uint4 *tab = reinterpret_cast<const uint4 *>(t.slots);
-	for (uint32_t p = 0;;) {
-		if (sl.w == POL_EMPTY)
-			return -1;
-		if (sl.x == lo && sl.y == hi && (sl.z & 0xFFFFu) == ep) {
-			*z = sl.z;
-			return (int)sl.w;
-		}
-		if (++p >= t.max_probe)
-			return -1;
-		b = (b + 1) & t.bucket_mask;
-		sl = tab[b];
-	}
-}
-
-/*
- * IPv4 classification with U tuples in flight per lane.  Same semantics as
- * k_classify<0, 1, 1024> (the reference cascade, LDS hot counters); the
- * U tuples of a lane advance stage by stage — columns, tbl24, tbl8, probe 1,
- * probe 2, probe 3 — so each stage issues U independent loads before any
- * of them is waited for.  Needs the single-slot policy layout.
- * Tuple of lane t, step j, member u: i = (j * U + u) * T + t (T = lanes in
- * the grid), so every member's column loads stay coalesced.
- */
-template <int U, int MINW = 1>
-__global__ __launch_bounds__(1024, MINW) void k_classify_v4_ilp(cgpu_snapshot s, cls_args a)
-{
-	constexpr int NT = 1024;
-	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
-	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
-	const uint64_t T = (uint64_t)gridDim.x * NT;
-	const uint64_t t0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
-	uint64_t *pctr = a.delta;
-	const uint32_t *sa4 = static_cast<const uint32_t *>(a.saddr);
-	const uint32_t *da4 = static_cast<const uint32_t *>(a.daddr);
-	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
-	const uint32_t pmask = s.pol.bucket_mask;
-	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
-		lctr[k] = 0;
-	__syncthreads();
-
-	for (uint64_t base = 0; base * T + t0 < a.n; base += U) {
-		uint64_t idx[U];
-		bool ok[U], eg[U], gated[U], frag[U];
-		uint32_t fl[U], proto[U], len[U], dport[U], ep[U], ad[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			idx[u] = (base + u) * T + t0;
-			ok[u] = idx[u] < a.n;
-			const uint64_t i = ok[u] ? idx[u] : 0;
-			fl[u] = a.flags[i];
-			proto[u] = a.proto[i];
-			len[u] = a.len[i];
-			dport[u] = a.dport[i];
-			ep[u] = a.ep[i];
-			const uint32_t sv = sa4[i], dv = da4[i];
-			eg[u] = fl[u] & 1u;
-			ad[u] = eg[u] ? dv : sv;
-		}
-		/* stage: ipcache tbl24 */
-		uint32_t e[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			gated[u] = s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u;
-			frag[u] = !eg[u] && ((fl[u] >> 1) & 1u);
-			e[u] = 0;
-			if (ok[u] && !gated[u])
-				e[u] = s.ipc4.tbl24[bswap32(ad[u]) >> 8];
-		}
-		/* stage: tbl8 */
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP)
-				e[u] = s.ipc4.tbl8[(size_t)(e[u] & DIR_PAYLOAD_MASK) * 256u +
-						   (bswap32(ad[u]) & 255u)];
-		/* identity (bpf_lxc.c:488-496 / bpf_netdev.c:374-404) */
-		uint32_t id[U], hi4[U], egb[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t p = e[u] & DIR_PAYLOAD_MASK;
-			const uint32_t label =
-				(e[u] & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? s.ipc4.vals[p] : p;
-			if (eg[u]) {
-				if (e[u] && label)
-					id[u] = label;
-				else if ((ad[u] & s.ipv4_cluster_mask) == s.ipv4_cluster_range)
-					id[u] = s.cluster_id;
-				else
-					id[u] = s.world_id;
-			} else {
-				uint32_t src = s.ingress_src_identity;
-				if (src < s.health_id && e[u] && label && label != s.cluster_id &&
-				    label != s.host_id)
-					src = label;
-				id[u] = s.ingress_secctx_world ? s.world_id : src;
-			}
-			egb[u] = eg[u] ? (1u << 24) : 0u;
-			hi4[u] = dport[u] | (proto[u] << 16) | egb[u];
-		}
-		/* probe 1: exact {id, dport, proto, dir} (policy.h:61-72) */
-		int ctr[U];
-		uint32_t z[U], st[U], bk[U];
-		uint4 sl[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			ctr[u] = -1;
-			z[u] = 0;
-			st[u] = 0;
-			if (ok[u] && !gated[u] && !frag[u]) {
-				bk[u] = pol_hash(id[u], hi4[u], ep[u]) & pmask;
-				sl[u] = ptab[bk[u]];
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			if (ok[u] && !gated[u] && !frag[u]) {
-				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u], ep[u], &z[u]);
-				st[u] = 1;
-			}
-		/* probe 2: L3-only {id, 0, 0, dir} (policy.h:74-83) */
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0) {
-				bk[u] = pol_hash(id[u], egb[u], ep[u]) & pmask;
-				sl[u] = ptab[bk[u]];
-			}
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0) {
-				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], egb[u], ep[u], &z[u]);
-				st[u] = 2;
-			}
-		/* probe 3: identity-wildcard L4 {0, dport, proto, dir} (policy.h:85-96) */
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
-				bk[u] = pol_hash(0u, hi4[u], ep[u]) & pmask;
-				sl[u] = ptab[bk[u]];
-			}
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			if (ok[u] && !gated[u] && ctr[u] < 0 && !frag[u]) {
-				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], 0u, hi4[u], ep[u], &z[u]);
-				st[u] = 3;
-			}
-		/* counters, outputs, metrics */
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			if (!ok[u])
-				continue;
-			int32_t v;
-			if (gated[u]) {
-				v = DROP_CT_UNKNOWN_PROTO;
-				id[u] = 0;
-				st[u] = 4;
-			} else if (ctr[u] >= 0) {
-				const uint32_t c = (uint32_t)ctr[u];
-				if (c < s.hot_slots && len[u] < PK_MAX_LEN) {
-					atomicAdd((unsigned long long *)&lctr[c],
-						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
-				} else {
-					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
-					atomicAdd((unsigned long long *)&pctr[2u * c + 1u],
-						  (unsigned long long)len[u]);
-				}
-				v = st[u] == 2 ? 0 : (int32_t)(z[u] >> 16);
-			} else {
-				st[u] = 0;
-				v = DROP_POLICY;
-			}
-			const uint64_t i = idx[u];
-			a.verdict[i] = v;
-			a.identity[i] = id[u];
-			if (a.stage)
-				a.stage[i] = (uint8_t)st[u];
-			const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : 2u);
-			const uint32_t mi = r * 2u + (eg[u] ? 1u : 0u);
-#pragma unroll
-			for (int k = 0; k < 6; k++) {
-				mcnt[k] += (mi == (uint32_t)k) ? 1u : 0u;
-				mbyt[k] += (mi == (uint32_t)k) ? len[u] : 0u;
-			}
-		}
-	}
-
-	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
-	const uint32_t reasons[3] = {0u, 133u, 137u};
-#pragma unroll
-	for (int k = 0; k < 6; k++) {
-		uint64_t c = wave_sum(mcnt[k]);
-		uint64_t b = wave_sum(mbyt[k]);
-		if ((threadIdx.x & 63) == 0 && c) {
-			uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
-			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
-			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
-		}
-	}
-	__syncthreads();
-	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
-		const uint64_t v = lctr[k];
-		if (v) {
-			atomicAdd((unsigned long long *)&pctr[2u * k], v >> PK_SHIFT);
-			atomicAdd((unsigned long long *)&pctr[2u * k + 1u], v & PK_BYTES_MASK);
-		}
-	}
-}
 
 /* Packed per-slot accumulator of k_classify_v4_x4 (pk): one u64 per counter
  * slot, packets in bits 37..63, bytes in 0..36.  Exact while one launch adds
@@ -1233,25 +1036,12 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 		c.saddr = static_cast<const uint32_t *>(a.saddr) + off;
 		c.daddr = static_cast<const uint32_t *>(a.daddr) + off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + 4 * NT - 1) / (4 * NT), res);
-		const unsigned g2 = (unsigned)std::min<uint64_t>((m + 2 * NT - 1) / (2 * NT), 2 * res); /* Q=2 */
-		if (var == 8 && s.ipc4c.x16)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
-		else if (var == 17 && s.ipc4c.x16)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true, 2, 8>), dim3(g2), dim3(NT), lds2, st, s, c, a.pk);
-		else if (var == 18)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0, true, 2, 8>), dim3(g2), dim3(NT), lds, st, s, c, a.pk);
-		else if (var == 16 && s.ipc4c.x16)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, false>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
-		else if (var == 12)
+		if (var == 12)
 			hipLaunchKernelGGL((k_classify_v4_x4<NT, 2, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
-		else if (var == 14)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 1, true>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		else if (var == 15)
 			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0, true>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
-		else if (var == 13 || !s.ipc4c.d16)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		else
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 1>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi,
@@ -1267,7 +1057,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
  *      (needs aligned columns and the single-slot policy layout, else 3)
  *   3 (default, IPv6 / fallback): one tuple per lane, LDS hot counters
  *   0: global atomics for every hit, 256-thread workgroups
- *   4-7: k_classify_v4_ilp (U strided tuples per lane)
+ *   15: k_classify_v4_x4 over the DIR-24-8 ipcache (LPM layout A/B)
  *   9, 12, 20-22: diagnostic ablations (no counters / partial work); their
  *      results are NOT the reference's and they are never the default.
  * Every non-diagnostic variant computes identical results. */
@@ -1295,9 +1085,8 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 0>), dim3(g), dim3(1024), 0, st, s, a);
 		return hipGetLastError();
 	}
-	if (!V6 && (var == 8 || (var >= 12 && var <= 18)) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
+	if (!V6 && (var == 8 || var == 12 || var == 15) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
 		return launch_x4(s, a, st, var);
-	const bool ilp = !V6 && s.pol.slots_per_bucket == 1 && (var >= 4 && var <= 7);
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
 	constexpr int NT = 1024;
@@ -1320,16 +1109,7 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 		c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
 		c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
 		const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
-		if (ilp && var == 4)
-			hipLaunchKernelGGL((k_classify_v4_ilp<2>), dim3(g), dim3(NT), lds, st, s, c);
-		else if (ilp && var == 5)
-			hipLaunchKernelGGL((k_classify_v4_ilp<4>), dim3(g), dim3(NT), lds, st, s, c);
-		else if (ilp && var == 6)
-			hipLaunchKernelGGL((k_classify_v4_ilp<2, 8>), dim3(g), dim3(NT), lds, st, s, c);
-		else if (ilp)
-			hipLaunchKernelGGL((k_classify_v4_ilp<4, 4>), dim3(g), dim3(NT), lds, st, s, c);
-		else
-			hipLaunchKernelGGL((k_classify<V6, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
+		hipLaunchKernelGGL((k_classify<V6, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
 	}
 	return hipGetLastError();
 }

@@ -88,6 +88,16 @@ typedef struct lpm16c {
  * probing over buckets; a bucket with an empty slot ends the probe. */
 #define POL_SLOTS_PER_BUCKET 4u
 #define POL_EMPTY 0xFFFFFFFFu
+/* Single-slot layout (slots_per_bucket 1, the default): neighbourhood
+ * ("hop") hashing.  A key lives within POL_HOP slots of its home slot h;
+ * w = counter slot (bits 0..23, POL_CTR_EMPTY = empty) | hop << 24, where
+ * bit j of home slot h's hop says "slot h + j holds a key whose home is h".
+ * A lookup loads the home slot (one 16-byte gather): hop == 0 is a miss,
+ * bit 0 + key match a hit; only other set bits cost further loads. */
+#define POL_HOP 8u
+#define POL_HOP_SHIFT 24u
+#define POL_CTR_MASK 0x00FFFFFFu
+#define POL_CTR_EMPTY POL_CTR_MASK
 
 typedef struct pol_slot {
 	uint32_t key_lo;  /* sec_label */
@@ -99,7 +109,7 @@ typedef struct pol_slot {
 typedef struct pol_table {
 	const pol_slot *slots; /* n_buckets * slots_per_bucket */
 	uint32_t bucket_mask;
-	uint32_t max_probe;    /* longest probe sequence in buckets (>= 1) */
+	uint32_t max_probe;    /* 4-slot layout: longest probe sequence in buckets */
 	uint32_t slots_per_bucket; /* 4: 64-B buckets; 1: 16-B slots, one load per probe */
 	uint32_t pad_;
 } pol_table;
