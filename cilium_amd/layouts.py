@@ -15,6 +15,9 @@ cgo caller can pass ``unsafe.Pointer`` straight through.
   pkg/maps/cidrmap/cidrmap.go:49-52 (``cidrKey`` truncated to 4 + AddrSize).
 * ``endpoint_key`` 20 B — bpf/lib/common.h:147-160.
 * ``metrics`` {reason, dir} -> {count, bytes} — bpf/lib/common.h:195-206.
+* ``lb4_key`` 8 B / ``lb4_service`` 12 B — bpf/lib/common.h:427-439, Go
+  pkg/maps/lbmap/ipv4.go:78-190 (key port, value port / rev_nat / weight in
+  network order after ToNetwork; slave and count stay host order).
 """
 from __future__ import annotations
 
@@ -38,6 +41,10 @@ ENDPOINT_KEY = np.dtype([("ip", "u1", (16,)), ("family", "u1"), ("pad4", "u1"),
 
 assert POLICY_KEY.itemsize == 8 and POLICY_ENTRY.itemsize == 24
 assert IPCACHE_KEY.itemsize == 24 and REMOTE_ENDPOINT_INFO.itemsize == 8
+LB4_KEY = np.dtype([("address", "<u4"), ("dport", "<u2"), ("slave", "<u2")])
+LB4_SERVICE = np.dtype([("target", "<u4"), ("port", "<u2"), ("count", "<u2"),
+                        ("rev_nat_index", "<u2"), ("weight", "<u2")])
+assert LB4_KEY.itemsize == 8 and LB4_SERVICE.itemsize == 12
 assert LPM_V4_KEY.itemsize == 8 and LPM_V6_KEY.itemsize == 20
 assert ENDPOINT_KEY.itemsize == 20
 
@@ -59,6 +66,15 @@ METRIC_INGRESS, METRIC_EGRESS = 1, 2
 CT_EGRESS, CT_INGRESS = 0, 1
 
 PROTO_ICMP, PROTO_TCP, PROTO_UDP = 1, 6, 17
+
+DROP_NO_SERVICE = -158
+TC_ACT_OK, TC_ACT_REDIRECT = 0, 7
+# IPV4_LOOPBACK (bpf/node_config.h:45), network-order u32 as written
+IPV4_LOOPBACK = 0x1ffff50a
+# cgpu_lb4_select modes and LXC result codes (include/cgpu.h)
+LB_NETDEV, LB_LXC = 0, 1
+LB_NONE, LB_XLATED, LB_XLATED_LOOPBACK = 0, 1, 2
+LB_L3, LB_L4 = 1, 2
 
 # tuple flag bits of the classify SoA
 F_EGRESS = 1
@@ -171,3 +187,24 @@ def ipv6_addr_clear_suffix(addr16: bytes, prefix: int) -> bytes:
         words[i] &= get_prefix_mask_be(prefix)
         prefix -= 32
     return struct.pack("<4I", *words)
+
+
+def lb4_key(address: str | int, dport_host: int = 0, slave: int = 0) -> np.ndarray:
+    """lbmap.NewService4Key(ip, port, slave).ToNetwork() (ipv4.go:99-126)."""
+    k = np.zeros((), LB4_KEY)
+    k["address"] = ip4_be(address)
+    k["dport"] = htons(dport_host)
+    k["slave"] = slave
+    return k
+
+
+def lb4_service(target: str | int = 0, port_host: int = 0, count: int = 0, rev_nat: int = 0,
+                weight: int = 0) -> np.ndarray:
+    """lbmap.NewService4Value(...).ToNetwork() (ipv4.go:144-181)."""
+    v = np.zeros((), LB4_SERVICE)
+    v["target"] = ip4_be(target)
+    v["port"] = htons(port_host)
+    v["count"] = count
+    v["rev_nat_index"] = htons(rev_nat)
+    v["weight"] = htons(weight)
+    return v

@@ -21,6 +21,10 @@
 #define PROTO_ICMP 1
 #define PROTO_TCP 6
 #define PROTO_UDP 17
+#define PROTO_ICMPV6 58
+#define TC_ACT_OK 0
+#define TC_ACT_REDIRECT 7
+#define DROP_NO_SERVICE (-158)
 
 /* ====================================================================== */
 /* Path-compressed binary LPM trie, restating kernel/bpf/lpm_trie.c:       */
@@ -348,6 +352,7 @@ struct or_ctx {
 	struct lpm_trie dyn4, dyn6; /* lpm_v{4,6}_key -> lpm_val */
 	struct ohash fix4, fix6;
 	struct ohash lxc;           /* endpoint_key -> present */
+	struct ohash lb;            /* lb4_key (8 B) -> lb4_service (12 B) */
 	uint64_t metrics[N_METRICS];
 };
 
@@ -369,6 +374,8 @@ void or_default_config(or_config *cfg)
 					      0x0, 0x1, 0x0, 0x0}; /* node_config.h:30 */
 		memcpy(cfg->router_ip, r, 16);
 	}
+	cfg->lb_l3 = cfg->lb_l4 = 1;       /* lxc_config.h:44-45, init.sh:352 */
+	cfg->ipv4_loopback = 0x1ffff50a;   /* node_config.h:45 */
 }
 
 or_ctx *or_create(void)
@@ -381,6 +388,7 @@ or_ctx *or_create(void)
 	oh_init(&c->fix4, 8, 1);
 	oh_init(&c->fix6, 20, 1);
 	oh_init(&c->lxc, 20, 1);
+	oh_init(&c->lb, 8, 12);
 	return c;
 }
 
@@ -394,6 +402,7 @@ void or_destroy(or_ctx *c)
 	oh_destroy(&c->fix4);
 	oh_destroy(&c->fix6);
 	oh_destroy(&c->lxc);
+	oh_destroy(&c->lb);
 	for (size_t i = 0; i < c->n_ep; i++)
 		oh_destroy(&c->policy[i]);
 	free(c->policy);
@@ -589,12 +598,254 @@ static struct pol_res policy_access(struct ohash *h, uint32_t identity, uint16_t
 	return r;
 }
 
+/* ====================================================================== */
+/* Service load balancer (bpf/lib/lb.h, bpf/bpf_lb.c, bpf_lxc.c:444-469)  */
+/* ====================================================================== */
+int or_lb_update(or_ctx *c, const void *key8, const void *val12)
+{
+	return oh_update(&c->lb, key8, val12);
+}
+
+int or_lb_delete(or_ctx *c, const void *key8)
+{
+	return oh_delete(&c->lb, key8);
+}
+
+/* murmur3-finalizer flow hash over the stored (network-order) 5-tuple;
+ * identical to cilium_amd/shard.py flowhash_np and tables.h cgpu_flow_hash */
+uint32_t or_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport, uint8_t proto)
+{
+	uint32_t h = saddr * 0x9E3779B1u;
+	h ^= daddr;
+	h *= 0x85EBCA77u;
+	h ^= ((uint32_t)sport << 16) | dport;
+	h *= 0xC2B2AE3Du;
+	h ^= proto;
+	h ^= h >> 16;
+	h *= 0x85EBCA6Bu;
+	h ^= h >> 13;
+	h *= 0xC2B2AE35u;
+	h ^= h >> 16;
+	return h;
+}
+
+/* struct lb4_service fields (packed, bpf/lib/common.h:433-439) */
+static inline uint32_t lbv_target(const uint8_t *v) { uint32_t x; memcpy(&x, v, 4); return x; }
+static inline uint16_t lbv_port(const uint8_t *v) { uint16_t x; memcpy(&x, v + 4, 2); return x; }
+static inline uint16_t lbv_count(const uint8_t *v) { uint16_t x; memcpy(&x, v + 6, 2); return x; }
+static inline uint16_t lbv_rev_nat(const uint8_t *v) { uint16_t x; memcpy(&x, v + 8, 2); return x; }
+
+/* map_lookup_elem(&cilium_lb4_services, {address, dport, slave}) */
+static const uint8_t *lb_get(const or_ctx *c, uint32_t addr, uint16_t dport, uint16_t slave,
+			     uint64_t *probes)
+{
+	uint8_t key[8];
+	memcpy(key, &addr, 4);
+	memcpy(key + 4, &dport, 2);
+	memcpy(key + 6, &slave, 2);
+	(*probes)++;
+	return oh_get(&c->lb, key);
+}
+
+/* lb4_lookup_service (lb.h:604-635): the L4 key if its count is nonzero;
+ * else key->dport is cleared and the L3 key is tried.  *kd is key->dport. */
+static const uint8_t *lb_lookup_service(const or_ctx *c, uint32_t addr, uint16_t *kd,
+					uint16_t slave, uint64_t *probes)
+{
+	const uint8_t *v;
+	if (c->cfg.lb_l4 && *kd) {
+		v = lb_get(c, addr, *kd, slave, probes);
+		if (v && lbv_count(v))
+			return v;
+		*kd = 0;
+	}
+	if (c->cfg.lb_l3) {
+		v = lb_get(c, addr, *kd, slave, probes);
+		if (v && lbv_count(v))
+			return v;
+	}
+	return NULL;
+}
+
+struct lb_res {
+	int32_t ret;
+	uint32_t saddr, daddr, tdaddr;
+	uint16_t dport, rev_nat, slave;
+};
+
+static struct lb_res lb4_one(const or_ctx *c, int mode, uint32_t saddr, uint32_t daddr,
+			     uint16_t dport, uint8_t proto, uint32_t hash, uint64_t *probes)
+{
+	struct lb_res r = { 0, saddr, daddr, daddr, dport, 0, 0 };
+	const uint8_t *svc, *be;
+	uint16_t kd = 0, slave;
+	uint32_t target;
+
+	/* lb4_extract_key / extract_l4_port (lb.h:192-216, :590-602): only
+	 * under LB_L4 is the port read, and only then are other protocols
+	 * DROP_UNKNOWN_L4 -> TC_ACT_OK (bpf_lb.c:144-151) / skip_service_lookup
+	 * (bpf_lxc.c:444-450) */
+	if (c->cfg.lb_l4) {
+		if (proto == PROTO_TCP || proto == PROTO_UDP)
+			kd = dport;
+		else if (proto != PROTO_ICMP && proto != PROTO_ICMPV6)
+			return r;
+	}
+	svc = lb_lookup_service(c, daddr, &kd, 0, probes);
+	if (!svc)
+		return r; /* not a service: passed on unchanged (bpf_lb.c:154-158) */
+	if (mode == OR_LB_LXC && c->cfg.ct_proto_gate && proto != PROTO_ICMP && proto != PROTO_TCP &&
+	    proto != PROTO_UDP) {
+		/* lb4_local's CT_SERVICE ct_lookup4 returns DROP_CT_UNKNOWN_PROTO
+		 * (conntrack.h:526-528), which lb4_local maps to DROP_NO_SERVICE
+		 * (lb.h:711-731) */
+		r.ret = DROP_NO_SERVICE;
+		return r;
+	}
+	/* lb4_select_slave (lb.h:158-190; weighted RR is compiled out) */
+	slave = (uint16_t)(hash % lbv_count(svc) + 1);
+	be = lb_get(c, daddr, kd, slave, probes); /* lb4_lookup_slave (lb.h:637-651) */
+	if (!be) {
+		if (mode == OR_LB_NETDEV) {
+			r.ret = DROP_NO_SERVICE; /* bpf_lb.c:161-162 */
+			return r;
+		}
+		/* lb4_local (lb.h:737-744): the key keeps the slave just tried */
+		be = lb_lookup_service(c, daddr, &kd, slave, probes);
+		if (!be) {
+			r.ret = DROP_NO_SERVICE;
+			return r;
+		}
+		slave = (uint16_t)(hash % lbv_count(be) + 1);
+	}
+	target = lbv_target(be);
+	r.slave = slave;
+	r.rev_nat = lbv_rev_nat(be);
+	r.daddr = target;
+	if (mode == OR_LB_LXC) {
+		/* loopback (lb.h:753-771): the source becomes IPV4_LOOPBACK and
+		 * tuple.daddr keeps the service address */
+		if (saddr == target) {
+			r.saddr = c->cfg.ipv4_loopback;
+			r.ret = 2;
+		} else {
+			r.tdaddr = target;
+			r.ret = 1;
+		}
+	} else {
+		r.tdaddr = target;
+		r.ret = TC_ACT_REDIRECT;
+	}
+	/* lb4_xlate port rewrite (lb.h:685-694) */
+	if (c->cfg.lb_l4 && lbv_port(be) && kd != lbv_port(be) &&
+	    (proto == PROTO_TCP || proto == PROTO_UDP))
+		r.dport = lbv_port(be);
+	return r;
+}
+
+struct lb_job {
+	const or_ctx *c;
+	int mode;
+	size_t lo, hi;
+	const uint32_t *saddr, *daddr, *hash;
+	const uint16_t *sport, *dport;
+	const uint8_t *proto;
+	int32_t *ret;
+	uint32_t *saddr_out, *daddr_out, *tdaddr_out;
+	uint16_t *dport_out, *rev_nat_out, *slave_out;
+	uint64_t probes;
+};
+
+static void *lb_worker(void *arg)
+{
+	struct lb_job *j = arg;
+	for (size_t i = j->lo; i < j->hi; i++) {
+		uint32_t h = j->hash ? j->hash[i]
+				     : or_flow_hash(j->saddr[i], j->daddr[i], j->sport[i], j->dport[i],
+						    j->proto[i]);
+		struct lb_res r = lb4_one(j->c, j->mode, j->saddr[i], j->daddr[i], j->dport[i],
+					  j->proto[i], h, &j->probes);
+		j->ret[i] = r.ret;
+		if (j->saddr_out)
+			j->saddr_out[i] = r.saddr;
+		if (j->daddr_out)
+			j->daddr_out[i] = r.daddr;
+		if (j->tdaddr_out)
+			j->tdaddr_out[i] = r.tdaddr;
+		if (j->dport_out)
+			j->dport_out[i] = r.dport;
+		if (j->rev_nat_out)
+			j->rev_nat_out[i] = r.rev_nat;
+		if (j->slave_out)
+			j->slave_out[i] = r.slave;
+	}
+	return NULL;
+}
+
+int or_lb4(or_ctx *c, int mode, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+	   const uint16_t *sport, const uint16_t *dport, const uint8_t *proto, const uint32_t *hash,
+	   int32_t *ret, uint32_t *saddr_out, uint32_t *daddr_out, uint32_t *tdaddr_out,
+	   uint16_t *dport_out, uint16_t *rev_nat_out, uint16_t *slave_out, int nthreads,
+	   uint64_t *probe_sum)
+{
+	struct lb_job *jobs;
+	pthread_t *th;
+	uint64_t probes = 0;
+	if (mode != OR_LB_NETDEV && mode != OR_LB_LXC)
+		return -EINVAL;
+	if (!hash && !sport && n)
+		return -EINVAL;
+	if (nthreads <= 0)
+		nthreads = 1;
+	if ((size_t)nthreads > n && n > 0)
+		nthreads = (int)n;
+	jobs = calloc((size_t)nthreads, sizeof(*jobs));
+	th = calloc((size_t)nthreads, sizeof(*th));
+	for (int t = 0; t < nthreads; t++) {
+		struct lb_job *j = &jobs[t];
+		j->c = c;
+		j->mode = mode;
+		j->lo = n * (size_t)t / (size_t)nthreads;
+		j->hi = n * (size_t)(t + 1) / (size_t)nthreads;
+		j->saddr = saddr;
+		j->daddr = daddr;
+		j->hash = hash;
+		j->sport = sport;
+		j->dport = dport;
+		j->proto = proto;
+		j->ret = ret;
+		j->saddr_out = saddr_out;
+		j->daddr_out = daddr_out;
+		j->tdaddr_out = tdaddr_out;
+		j->dport_out = dport_out;
+		j->rev_nat_out = rev_nat_out;
+		j->slave_out = slave_out;
+		if (nthreads == 1)
+			lb_worker(j);
+		else
+			pthread_create(&th[t], NULL, lb_worker, j);
+	}
+	for (int t = 0; t < nthreads; t++) {
+		if (nthreads > 1)
+			pthread_join(th[t], NULL);
+		probes += jobs[t].probes;
+	}
+	if (probe_sum)
+		*probe_sum = probes;
+	free(jobs);
+	free(th);
+	return 0;
+}
+
 struct cls_job {
 	or_ctx *c;
 	size_t lo, hi;
 	const uint32_t *saddr, *daddr, *len;
 	const uint16_t *dport, *ep;
 	const uint8_t *proto, *flags;
+	int lb;                  /* egress service step first (or_classify_v4_lb) */
+	const uint16_t *sport;
+	const uint32_t *hash;
 	int32_t *verdict;
 	uint32_t *identity;
 	uint8_t *stage;
@@ -615,30 +866,55 @@ static void *cls_worker(void *arg)
 		int st, dir = egress ? METRIC_EGRESS : METRIC_INGRESS;
 		uint32_t ep = j->ep[i];
 		struct ohash *h = ep < c->n_ep ? &c->policy[ep] : NULL;
+		uint32_t daddr = j->daddr[i];
+		uint16_t dport = j->dport[i];
+		int lbdrop = 0;
 
-		if (cfg->ct_proto_gate && proto != PROTO_ICMP && proto != PROTO_TCP &&
-		    proto != PROTO_UDP) {
+		if (j->lb && egress) {
+			/* service translation before conntrack and policy
+			 * (bpf_lxc.c:444-469): ipcache resolves tuple.daddr
+			 * (orig_dip), policy sees the rewritten dport */
+			uint32_t hh = j->hash ? j->hash[i]
+					      : or_flow_hash(j->saddr[i], daddr, j->sport[i], dport, proto);
+			struct lb_res lr = lb4_one(c, OR_LB_LXC, j->saddr[i], daddr, dport, proto, hh,
+						   &j->probes);
+			if (lr.ret == DROP_NO_SERVICE) {
+				lbdrop = 1;
+			} else {
+				daddr = lr.tdaddr;
+				dport = lr.dport;
+			}
+		}
+
+		if (lbdrop) {
+			/* tail_handle_ipv4 -> send_drop_notify(.., METRIC_EGRESS), dstID 0
+			 * (bpf_lxc.c:659-666) */
+			v = DROP_NO_SERVICE;
+			id = 0;
+			st = 6;
+		} else if (cfg->ct_proto_gate && proto != PROTO_ICMP && proto != PROTO_TCP &&
+			   proto != PROTO_UDP) {
 			/* ct_lookup4 default case, bpf/lib/conntrack.h:526-528 */
 			v = DROP_CT_UNKNOWN_PROTO;
 			id = 0;
 			st = 4;
 		} else if (egress) {
 			/* bpf_lxc.c:484-505 */
-			const uint8_t *info = ipcache4(c, j->daddr[i]);
+			const uint8_t *info = ipcache4(c, daddr);
 			uint32_t label = 0;
 			struct pol_res r;
 			if (info)
 				memcpy(&label, info, 4);
 			if (info && label)
 				id = label;
-			else if ((j->daddr[i] & cfg->ipv4_cluster_mask) == cfg->ipv4_cluster_range)
+			else if ((daddr & cfg->ipv4_cluster_mask) == cfg->ipv4_cluster_range)
 				id = cfg->cluster_id;
 			else
 				id = cfg->world_id;
 			j->probes += 1;
 			/* policy_can_egress (policy.h:150-163): is_fragment = false,
 			 * negative collapsed to DROP_POLICY */
-			r = policy_access(h, id, j->dport[i], proto, 1, 0, j->len[i]);
+			r = policy_access(h, id, dport, proto, 1, 0, j->len[i]);
 			v = r.ret >= 0 ? r.ret : DROP_POLICY;
 			st = r.stage;
 			j->probes += r.probes;
@@ -658,7 +934,7 @@ static void *cls_worker(void *arg)
 			}
 			secctx = cfg->ingress_secctx_world ? cfg->world_id : src;
 			/* policy_can_access_ingress (policy.h:126-146) */
-			r = policy_access(h, secctx, j->dport[i], proto, 0, frag, j->len[i]);
+			r = policy_access(h, secctx, dport, proto, 0, frag, j->len[i]);
 			v = r.ret >= 0 ? r.ret : DROP_POLICY;
 			id = secctx;
 			st = r.stage;
@@ -681,10 +957,11 @@ static void *cls_worker(void *arg)
 	return NULL;
 }
 
-int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
-		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
-		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
-		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
+static int classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		       const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		       const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		       uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum,
+		       int lb, const uint16_t *sport, const uint32_t *hash)
 {
 	struct cls_job *jobs;
 	pthread_t *th;
@@ -710,6 +987,9 @@ int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *d
 		j->verdict = verdict;
 		j->identity = identity;
 		j->stage = stage;
+		j->lb = lb;
+		j->sport = sport;
+		j->hash = hash;
 		if (nthreads == 1)
 			cls_worker(j);
 		else
@@ -727,6 +1007,27 @@ int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *d
 	free(jobs);
 	free(th);
 	return 0;
+}
+
+int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
+{
+	return classify_v4(c, n, saddr, daddr, dport, proto, flags, len, ep, verdict, identity,
+			   stage, nthreads, probe_sum, 0, NULL, NULL);
+}
+
+int or_classify_v4_lb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint8_t *flags, const uint32_t *len, const uint16_t *ep,
+		      const uint32_t *hash, int32_t *verdict, uint32_t *identity, uint8_t *stage,
+		      int nthreads, uint64_t *probe_sum)
+{
+	if (!hash && !sport && n)
+		return -EINVAL;
+	return classify_v4(c, n, saddr, daddr, dport, proto, flags, len, ep, verdict, identity,
+			   stage, nthreads, probe_sum, 1, sport, hash);
 }
 
 struct cls6_job {

@@ -32,6 +32,8 @@ typedef struct or_config {
 	int ingress_secctx_world;      /* non-FROM_HOST netdev: label = WORLD_ID */
 	int dyn4, fix4, dyn6, fix6;    /* CIDR{4,6}_LPM_PREFILTER / CIDR{4,6}_FILTER */
 	uint8_t router_ip[16];         /* ROUTER_IP (node_config.h:30) */
+	int lb_l3, lb_l4;              /* LB_L3 / LB_L4 (lxc_config.h:44-45, init.sh:352) */
+	uint32_t ipv4_loopback;        /* IPV4_LOOPBACK (node_config.h:45), network order */
 } or_config;
 
 or_ctx *or_create(void);
@@ -86,6 +88,49 @@ int or_prefilter_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *
 		    const uint8_t *flags, uint8_t *verdict, int nthreads, uint64_t *probe_sum);
 int or_prefilter_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
 		    const uint8_t *flags, uint8_t *verdict, int nthreads, uint64_t *probe_sum);
+
+/*
+ * Service load balancer: the map cilium_lb4_services with
+ * raw struct lb4_key (8 B) -> struct lb4_service (12 B), bpf/lib/common.h:427-439.
+ */
+int or_lb_update(or_ctx *c, const void *key8, const void *val12);
+int or_lb_delete(or_ctx *c, const void *key8);
+/* kernel skb->hash stand-in used when no hash column is given (the kernel's
+ * flow-dissector hash is unpinned); = cilium_amd.shard.flowhash_np */
+uint32_t or_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport, uint8_t proto);
+
+#define OR_LB_NETDEV 0 /* bpf_lb.c handle_ipv4 (bpf_lb.c:118-170) */
+#define OR_LB_LXC 1    /* lb4_local from handle_ipv4_from_lxc, CT_NEW (bpf_lxc.c:444-460) */
+/*
+ * Per tuple (addresses / ports in network order; hash NULL = or_flow_hash):
+ * ret  NETDEV: TC_ACT_OK (0, not load-balanced), TC_ACT_REDIRECT (7), or
+ *              DROP_NO_SERVICE (-158)
+ *      LXC:    0 no service, 1 translated, 2 translated with the loopback
+ *              source NAT, or DROP_NO_SERVICE
+ * saddr/daddr/dport_out: the packet's fields after lb4_xlate; tdaddr_out
+ * (LXC): tuple.daddr afterwards (the backend, or the service address on
+ * loopback); rev_nat/slave_out: the selected entry's rev_nat_index and slave.
+ * Any output except ret may be NULL.  *probe_sum: service-map lookups.
+ */
+int or_lb4(or_ctx *c, int mode, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+	   const uint16_t *sport, const uint16_t *dport, const uint8_t *proto, const uint32_t *hash,
+	   int32_t *ret, uint32_t *saddr_out, uint32_t *daddr_out, uint32_t *tdaddr_out,
+	   uint16_t *dport_out, uint16_t *rev_nat_out, uint16_t *slave_out, int nthreads,
+	   uint64_t *probe_sum);
+
+/*
+ * or_classify_v4 with the egress service step of handle_ipv4_from_lxc in
+ * front (bpf_lxc.c:444-469, BASELINE config 5): egress tuples are translated
+ * by lb4_local (OR_LB_LXC) first; ipcache then resolves tuple.daddr and the
+ * policy sees the translated dport.  DROP_NO_SERVICE ends the tuple (verdict
+ * -158, identity 0, stage 6, metrics reason 158 egress, bpf_lxc.c:659-666).
+ * sport is needed only when hash is NULL.  *probe_sum includes the LB lookups.
+ */
+int or_classify_v4_lb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint8_t *flags, const uint32_t *len, const uint16_t *ep,
+		      const uint32_t *hash, int32_t *verdict, uint32_t *identity, uint8_t *stage,
+		      int nthreads, uint64_t *probe_sum);
 
 /* metrics {reason, dir} -> {count, bytes}; out is [256][4][2] u64 */
 void or_metrics_read(or_ctx *c, uint64_t *out);

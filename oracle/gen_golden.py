@@ -4,9 +4,10 @@ Run in the development container only (needs /root/reference):
 
     make -C oracle ref && python oracle/gen_golden.py
 
-It loads oracle/_ref/libref_{policy,xdp}.so — the reference's
-bpf/lib/policy.h, bpf/lib/eps.h and bpf/bpf_xdp.c compiled as host C with
-mocked kernel maps (oracle/ref/) — feeds them seeded scenarios, and writes
+It loads oracle/_ref/libref_{policy,xdp,lb_*,lbl}.so — the reference's
+bpf/lib/policy.h, bpf/lib/eps.h, bpf/bpf_xdp.c, bpf/bpf_lb.c and bpf/lib/lb.h
+(+ conntrack.h) compiled as host C with mocked kernel maps and helpers
+(oracle/ref/) — feeds them seeded scenarios, and writes
 inputs + reference outputs as small .npz files (plain arrays, no pickles)
 under tests/golden/, plus tests/golden/MANIFEST.json.  The fixtures are data;
 nothing from the reference's sources is stored.
@@ -562,6 +563,244 @@ def gen_xdp_fixture(xdp, rng):
                 frame_bytes=blob, frame_len=lens, verdict=verdict, probes=probes)
 
 
+# ---------------------------------------------------------------------- lb
+def load_ref_lb():
+    variants = {}
+    for v in ("both", "l3", "l4"):
+        L_ = C.CDLL(os.path.join(HERE, "_ref", f"libref_lb_{v}.so"))
+        L_.ref_lb_reset.restype = None
+        L_.ref_lb_update.argtypes = [C.c_void_p, C.c_void_p]
+        L_.ref_lb_netdev.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]
+        variants[v] = L_
+    lbls = {}
+    for v, f in ((1, "libref_lbl.so"), (0, "libref_lbl_noct.so")):
+        lbl = C.CDLL(os.path.join(HERE, "_ref", f))
+        lbl.ref_lbl_reset.restype = None
+        lbl.ref_lbl_update.argtypes = [C.c_void_p, C.c_void_p]
+        u16p = C.POINTER(C.c_uint16)
+        lbl.ref_lbl_run.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int),
+                                    C.POINTER(C.c_uint32), u16p, u16p, C.POINTER(C.c_int),
+                                    C.POINTER(C.c_uint64)]
+        lbls[v] = lbl
+    return variants, lbls  # lbls[1]: CONNTRACK build, lbls[0]: without
+
+
+LB_PROTOS = np.array([6, 6, 6, 6, 6, 17, 17, 17, 1, 1, 58, 47, 132, 0], np.uint8)
+
+
+def gen_lb_services(rng, n_vip, targets, clients):
+    """Service map contents as lbmap.UpdateService writes them (lbmap.go:350-428:
+    slave 0 = master {count, weight}, slaves 1..count = backends), plus the
+    irregular contents the map can also hold: a master with count 0, a master
+    whose count exceeds its backends, backends with a nonzero count (reached by
+    lb4_local's fallback), and sparse slave numbers."""
+    keys, vals = [], []
+    vips = []
+
+    def put(addr_be, dport_be, slave, target_be, port_be, count, rev, weight):
+        k = np.zeros((), L.LB4_KEY)
+        k["address"], k["dport"], k["slave"] = addr_be, dport_be, slave
+        v = np.zeros((), L.LB4_SERVICE)
+        v["target"], v["port"], v["count"] = target_be, port_be, count
+        v["rev_nat_index"], v["weight"] = rev, weight
+        keys.append(k)
+        vals.append(v)
+
+    for i in range(n_vip):
+        vip = L.ip4_be(0x0A600000 | int(rng.integers(1, 1 << 20)))  # 10.96.0.0/12
+        vips.append(vip)
+        kinds = ["l4"] if rng.random() < 0.5 else (["l3"] if rng.random() < 0.4 else ["l4", "l3"])
+        for kind in kinds:
+            dport = L.htons(int(rng.choice(PORTS[1:6]))) if kind == "l4" else 0
+            nb = int(rng.integers(1, 6))
+            rev = int(rng.integers(1, 65536))
+            count = nb
+            r = rng.random()
+            if r < 0.08:
+                count = 0          # a master with count 0 is not a service
+            elif r < 0.2:
+                count = nb + 1     # one selectable slave has no backend entry
+            put(vip, dport, 0, 0, 0, count, 0, int(rng.integers(0, 3)))
+            slaves = list(range(1, nb + 1))
+            if rng.random() < 0.1:
+                slaves[-1] = int(rng.integers(nb + 1, 40))  # sparse slave number
+            for s in slaves:
+                tgt = int(rng.choice(clients)) if rng.random() < 0.25 else int(rng.choice(targets))
+                pr = rng.random()
+                port = 0 if pr < 0.3 else (dport if pr < 0.5 else L.htons(int(rng.integers(1, 65536))))
+                bc = int(rng.integers(1, 4)) if (kind == "l3" and rng.random() < 0.5) else 0
+                put(vip, dport, s, tgt, port, bc, rev, int(rng.integers(0, 65536)))
+    return (np.array(keys, L.LB4_KEY), np.array(vals, L.LB4_SERVICE),
+            np.array(vips, np.uint32))
+
+
+def l4_frame(saddr_be, daddr_be, sport_be, dport_be, proto, opts=False):
+    """Ethernet + IPv4 (optionally with 4 option bytes) + an L4 header
+    carrying the ports at offsets 0 / 2 (TCP, UDP) or an ICMP echo."""
+    h = bytearray(24 if opts else 20)
+    h[0] = 0x46 if opts else 0x45
+    h[9] = proto
+    h[12:16] = int(saddr_be).to_bytes(4, "little")
+    h[16:20] = int(daddr_be).to_bytes(4, "little")
+    if proto == 1:
+        l4 = bytes([8, 0]) + bytes(6)
+    else:
+        l4 = int(sport_be).to_bytes(2, "little") + int(dport_be).to_bytes(2, "little") + \
+             bytes(16 if proto == 6 else 4)
+    return bytearray(eth(0x0800, bytes(h) + l4)), 14 + len(h)
+
+
+def lb_tuples(rng, n, keys, vips, clients):
+    fe = {}
+    for k in keys:
+        fe.setdefault(int(k["address"]), set()).add(int(k["dport"]))
+    vsel = vips[rng.integers(0, len(vips), n)]
+    daddr = np.where(rng.random(n) < 0.75, vsel,
+                     rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)).astype(np.uint32)
+    dport = np.empty(n, np.uint16)
+    for i in range(n):
+        ports = [p for p in fe.get(int(daddr[i]), ()) if p]
+        dport[i] = int(rng.choice(ports)) if ports and rng.random() < 0.8 else \
+            L.htons(int(rng.choice(PORTS)) if rng.random() < 0.5 else int(rng.integers(0, 65536)))
+    saddr = np.where(rng.random(n) < 0.3, rng.choice(clients, n),
+                     rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)).astype(np.uint32)
+    h = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    h[:8] = [0, 1, 2, 0xFFFFFFFF, 0x7FFFFFFF, 65535, 65536, 0x80000000]
+    return {"saddr": saddr, "daddr": daddr,
+            "sport": rng.integers(0, 65536, n).astype(np.uint16), "dport": dport,
+            "proto": rng.choice(LB_PROTOS, n), "hash": h,
+            "opts": (rng.random(n) < 0.1).astype(np.uint8)}
+
+
+def run_lb_netdev(lbv, keys, vals, t):
+    lbv.ref_lb_reset()
+    for k, v in zip(keys, vals):
+        lbv.ref_lb_update(b(k), b(v))
+    n = len(t["daddr"])
+    ret = np.empty(n, np.int32)
+    daddr = np.empty(n, np.uint32)
+    dport = np.empty(n, np.uint16)
+    lookups = np.empty(n, np.uint32)
+    cnt = C.c_uint64()
+    for i in range(n):
+        fr, l4 = l4_frame(t["saddr"][i], t["daddr"][i], t["sport"][i], t["dport"][i],
+                          int(t["proto"][i]), bool(t["opts"][i]))
+        buf = (C.c_uint8 * len(fr)).from_buffer(fr)
+        ret[i] = lbv.ref_lb_netdev(buf, len(fr), int(t["hash"][i]), C.byref(cnt))
+        daddr[i] = int.from_bytes(bytes(fr[30:34]), "little")
+        dport[i] = int.from_bytes(bytes(fr[l4 + 2:l4 + 4]), "little") \
+            if int(t["proto"][i]) in (6, 17) else t["dport"][i]
+        lookups[i] = cnt.value
+    return ret, daddr, dport, lookups
+
+
+def run_lb_lxc(lbl, keys, vals, t):
+    lbl.ref_lbl_reset()
+    for k, v in zip(keys, vals):
+        lbl.ref_lbl_update(b(k), b(v))
+    n = len(t["daddr"])
+    out = {k: np.empty(n, dt) for k, dt in (
+        ("ret", np.int32), ("svc_hit", np.uint8), ("tdaddr", np.uint32), ("rev_nat", np.uint16),
+        ("slave", np.uint16), ("loopback", np.uint8), ("saddr", np.uint32), ("daddr", np.uint32),
+        ("dport", np.uint16), ("lookups", np.uint32))}
+    hit, td, lo, cnt = C.c_int(), C.c_uint32(), C.c_int(), C.c_uint64()
+    rn, sl = C.c_uint16(), C.c_uint16()
+    for i in range(n):
+        fr, l4 = l4_frame(t["saddr"][i], t["daddr"][i], t["sport"][i], t["dport"][i],
+                          int(t["proto"][i]), bool(t["opts"][i]))
+        buf = (C.c_uint8 * len(fr)).from_buffer(fr)
+        r = lbl.ref_lbl_run(buf, len(fr), int(t["hash"][i]), C.byref(hit), C.byref(td),
+                            C.byref(rn), C.byref(sl), C.byref(lo), C.byref(cnt))
+        out["ret"][i], out["svc_hit"][i], out["tdaddr"][i] = r, hit.value, td.value
+        out["rev_nat"][i], out["slave"][i], out["loopback"][i] = rn.value, sl.value, lo.value
+        out["saddr"][i] = int.from_bytes(bytes(fr[26:30]), "little")
+        out["daddr"][i] = int.from_bytes(bytes(fr[30:34]), "little")
+        out["dport"][i] = int.from_bytes(bytes(fr[l4 + 2:l4 + 4]), "little") \
+            if int(t["proto"][i]) in (6, 17) else t["dport"][i]
+        out["lookups"][i] = cnt.value
+    return out
+
+
+def gen_lb_fixture(lbvars, lbls, rng):
+    targets = rng.integers(0, 2**32, 200, dtype=np.uint64).astype(np.uint32)
+    clients = rng.integers(0, 2**32, 4, dtype=np.uint64).astype(np.uint32)
+    keys, vals, vips = gen_lb_services(rng, 70, targets, clients)
+    t = lb_tuples(rng, 5000, keys, vips, clients)
+    out = dict(keys=keys, vals=vals, **{"t_" + k: v for k, v in t.items()})
+    for name, lbv in lbvars.items():
+        r, d, p, nl = run_lb_netdev(lbv, keys, vals, t)
+        out.update({f"nd_{name}_ret": r, f"nd_{name}_daddr": d, f"nd_{name}_dport": p,
+                    f"nd_{name}_lookups": nl})
+    for ct, lbl in lbls.items():
+        lx = run_lb_lxc(lbl, keys, vals, t)
+        out.update({("lx_" if ct else "lxnoct_") + k: v for k, v in lx.items()})
+    return out
+
+
+def gen_classify_lb_fixture(pol, lbls, rng):
+    """The egress path of BASELINE config 5 composed from the reference's own
+    steps in bpf_lxc.c order: the service step (libref_lbl, bpf_lxc.c:444-469),
+    then ipcache on tuple.daddr and policy on the rewritten dport (libref_policy
+    ref_classify_v4 = bpf_lxc.c:484-505).  DROP_NO_SERVICE ends the packet
+    before conntrack (bpf_lxc.c:455-458) and is counted by send_drop_notify with
+    METRIC_EGRESS (:659-666).  Ingress tuples run the unchanged ingress path."""
+    base = gen_classify_fixture(pol, rng)
+    ikeys, ivals = base["ipc_keys"], base["ipc_vals"]
+    pk, pe, pep = base["pol_keys"], base["pol_entries"], base["pol_ep"]
+    v4 = ikeys["prefixlen"] >= 32
+    pfx = ikeys[v4]["ip"][:, :4].copy().view("<u4").ravel()
+    targets = pfx[rng.integers(0, len(pfx), 200)]
+    clients = rng.integers(0, 2**32, 4, dtype=np.uint64).astype(np.uint32)
+    keys, vals, vips = gen_lb_services(rng, 60, targets, clients)
+    n = 5000
+    lt = lb_tuples(rng, n, keys, vips, clients)
+    t = {"saddr": lt["saddr"], "daddr": lt["daddr"], "sport": lt["sport"], "dport": lt["dport"],
+         "proto": lt["proto"], "hash": lt["hash"],
+         "flags": ((rng.random(n) < 0.7).astype(np.uint8) |
+                   ((rng.random(n) < 0.05).astype(np.uint8) << 1)),
+         "len": rng.integers(0, 70000, n).astype(np.uint32),
+         "ep": rng.integers(0, 5, n).astype(np.uint16), "opts": lt["opts"]}
+    out = {}
+    idv, st, npb, na = C.c_uint32(), C.c_int(), C.c_int(), C.c_int()
+    for ci, (gate, src, sw) in enumerate(CONFIGS[:2]):
+        # the CONNTRACK switch decides both the policy protocol gate and
+        # lb4_local's conntrack step
+        lx = run_lb_lxc(lbls[gate], keys, vals, t)
+        pol.ref_reset()
+        for k, v in zip(ikeys, ivals):
+            pol.ref_ipcache_update(b(k), b(v))
+        for k, e, ep in zip(pk, pe, pep):
+            pol.ref_policy_update(int(ep), b(k), b(e))
+        verdict = np.empty(n, np.int32)
+        ident = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        nprobes = np.empty(n, np.int32)
+        for i in range(n):
+            eg = int(t["flags"][i]) & 1
+            if eg and lx["ret"][i] < 0:
+                verdict[i], ident[i], stage[i], nprobes[i] = lx["ret"][i], 0, 6, lx["lookups"][i]
+                continue
+            da = int(lx["tdaddr"][i]) if eg else int(t["daddr"][i])
+            dp = int(lx["dport"][i]) if eg else int(t["dport"][i])
+            verdict[i] = pol.ref_classify_v4(
+                int(t["saddr"][i]), da, dp, int(t["proto"][i]), int(t["flags"][i]),
+                int(t["len"][i]), int(t["ep"][i]), gate, src, sw,
+                C.byref(idv), C.byref(st), C.byref(npb), C.byref(na))
+            ident[i], stage[i] = idv.value, st.value
+            nprobes[i] = npb.value + na.value + (int(lx["lookups"][i]) if eg else 0)
+        final = np.zeros(len(pk), L.POLICY_ENTRY)
+        for i, (k, ep) in enumerate(zip(pk, pep)):
+            buf = C.create_string_buffer(24)
+            assert pol.ref_policy_read(int(ep), b(k), buf) == 0
+            final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+        out[f"c{ci}_verdict"], out[f"c{ci}_identity"] = verdict, ident
+        out[f"c{ci}_stage"], out[f"c{ci}_nprobes"] = stage, nprobes
+        out[f"c{ci}_final_entries"] = final
+    return dict(ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe, pol_ep=pep,
+                lb_keys=keys, lb_vals=vals, configs=np.array(CONFIGS[:2], np.int64),
+                **{"t_" + k: v for k, v in t.items()}, **out)
+
+
 def save(name, d):
     path = os.path.join(OUT, name)
     np.savez_compressed(path, **d)
@@ -585,6 +824,13 @@ def main():
     manifest["files"]["classify_v4.npz"] = save("classify_v4.npz", gen_classify_fixture(pol, rng))
     manifest["files"]["xdp_prefilter.npz"] = save("xdp_prefilter.npz", gen_xdp_fixture(xdp, rng))
     manifest["files"]["classify_v6.npz"] = save("classify_v6.npz", gen_classify_v6_fixture(pol, rng))
+    # service load balancer; a separate stream keeps the
+    # fixtures above byte-identical to earlier generations
+    lbvars, lbls = load_ref_lb()
+    rng_lb = np.random.Generator(np.random.PCG64(SEED + 0x1B))
+    manifest["files"]["lb4.npz"] = save("lb4.npz", gen_lb_fixture(lbvars, lbls, rng_lb))
+    manifest["files"]["classify_v4_lb.npz"] = save(
+        "classify_v4_lb.npz", gen_classify_lb_fixture(pol, lbls, rng_lb))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -23,6 +23,7 @@ class OrConfig(C.Structure):
         ("ingress_src_identity", C.c_uint32), ("ingress_secctx_world", C.c_int),
         ("dyn4", C.c_int), ("fix4", C.c_int), ("dyn6", C.c_int), ("fix6", C.c_int),
         ("router_ip", C.c_uint8 * 16),
+        ("lb_l3", C.c_int), ("lb_l4", C.c_int), ("ipv4_loopback", C.c_uint32),
     ]
 
 
@@ -60,6 +61,12 @@ def lib():
         L.or_classify_v6.argtypes = [vp, sz] + [vp] * 10 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_prefilter_v4.argtypes = [vp, sz, vp, vp, vp, vp, C.c_int, C.POINTER(C.c_uint64)]
         L.or_prefilter_v6.argtypes = [vp, sz, vp, vp, vp, vp, C.c_int, C.POINTER(C.c_uint64)]
+        L.or_lb_update.argtypes = [vp, vp, vp]
+        L.or_lb_delete.argtypes = [vp, vp]
+        L.or_flow_hash.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_uint8]
+        L.or_flow_hash.restype = C.c_uint32
+        L.or_lb4.argtypes = [vp, C.c_int, sz] + [vp] * 13 + [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_classify_v4_lb.argtypes = [vp, sz] + [vp] * 12 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_metrics_read.argtypes = [vp, vp]
         L.or_counters_reset.argtypes = [vp]
         _lib = L
@@ -181,6 +188,53 @@ class Oracle:
                    np.ascontiguousarray(flags, np.uint8))
         self.L.or_prefilter_v6(self.h, n, _p(s), _p(d), _p(f), _p(out), nthreads, C.byref(probes))
         return out, probes.value
+
+    # --- service load balancer ---
+    def lb_update(self, key, val):
+        return self.L.or_lb_update(self.h, _b(key), _b(val))
+
+    def lb_delete(self, key):
+        return self.L.or_lb_delete(self.h, _b(key))
+
+    def flow_hash(self, saddr, daddr, sport, dport, proto):
+        return self.L.or_flow_hash(saddr, daddr, sport, dport, proto)
+
+    def lb4(self, t, mode, nthreads=1):
+        """t: saddr/daddr (u32 network order), sport/dport (u16 network order),
+        proto, optional hash.  mode 0 = bpf_lb.c handle_ipv4, 1 = lb4_local."""
+        n = len(t["daddr"])
+        cols = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint32), ("daddr", np.uint32), ("sport", np.uint16),
+            ("dport", np.uint16), ("proto", np.uint8))]
+        h = None if t.get("hash") is None else np.ascontiguousarray(t["hash"], np.uint32)
+        out = {"ret": np.empty(n, np.int32), "saddr": np.empty(n, np.uint32),
+               "daddr": np.empty(n, np.uint32), "tdaddr": np.empty(n, np.uint32),
+               "dport": np.empty(n, np.uint16), "rev_nat": np.empty(n, np.uint16),
+               "slave": np.empty(n, np.uint16)}
+        probes = C.c_uint64(0)
+        rc = self.L.or_lb4(self.h, mode, n, *[_p(a) for a in cols], _p(h),
+                           *[_p(out[k]) for k in ("ret", "saddr", "daddr", "tdaddr", "dport",
+                                                  "rev_nat", "slave")],
+                           nthreads, C.byref(probes))
+        assert rc == 0, rc
+        return out, probes.value
+
+    def classify_v4_lb(self, t, nthreads=1):
+        """classify_v4 with the egress service step first (config 5)."""
+        n = len(t["saddr"])
+        verdict = np.empty(n, np.int32)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint32), ("daddr", np.uint32), ("sport", np.uint16),
+            ("dport", np.uint16), ("proto", np.uint8), ("flags", np.uint8), ("len", np.uint32),
+            ("ep", np.uint16))]
+        h = None if t.get("hash") is None else np.ascontiguousarray(t["hash"], np.uint32)
+        rc = self.L.or_classify_v4_lb(self.h, n, *[_p(a) for a in arrs], _p(h), _p(verdict),
+                                      _p(identity), _p(stage), nthreads, C.byref(probes))
+        assert rc == 0, rc
+        return verdict, identity, stage, probes.value
 
     def metrics(self):
         out = np.zeros((256, 4, 2), np.uint64)
