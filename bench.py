@@ -11,6 +11,13 @@ all-reduce of the per-entry/per-reason counter deltas (N > 1) and their fold
 into the totals.  Tables are replicated (same seed on every rank); tuple
 streams are seeded per rank, so per-GPU work is fixed (weak scaling).
 Rank 0 prints one JSON line.
+
+Other BASELINE configs (not the headline line; run them explicitly):
+  --config cascade   config 5: 1M IPv4 services in front of config 2 (the
+                     egress service step of bpf_lxc.c:444-469 fused into the
+                     classify kernel, cgpu_classify_v4_lb)
+  --config pf6       config 3: XDP IPv6 prefilter over 1M deny prefixes
+  --config cpu       config 1 sizes
 """
 from __future__ import annotations
 
@@ -26,10 +33,23 @@ sys.path.insert(0, ROOT)
 METRIC = "Mpps classified (LPM ipcache + policy map) at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 B_IN, B_OUT = 18, 8    # v4 classify tuple bytes in / out
+B_IN_PF6, B_OUT_PF6 = 33, 1  # v6 prefilter
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+WORKLOADS = {
+    "gpu": "config2: 100k IPv4 ipcache LPM + 64k policy entries (4 ep x 16k), "
+           "64M-tuple batches per GPU, bit-exact verdicts",
+    "cpu": "config1 (CPU-scale)",
+    "cascade": "config5: 1M IPv4 services (lb4_local, backends ~Geom(0.3) cap 16, 30% of egress "
+               "tuples to a service) -> ipcache(post-DNAT) -> policy over config-2 tables, "
+               "64M-tuple batches per GPU, bit-exact verdicts",
+    "pf6": "config3: XDP IPv6 prefilter, 1M deny prefixes (/32..../128, /128 in fix) under 256 "
+           "/24 roots + 4k endpoints, 64M packets per GPU",
+}
 
 
 def main():
@@ -37,7 +57,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--config", default="gpu", choices=sorted(WORKLOADS))
     ap.add_argument("--tuples", type=int, default=0, help="tuples per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -60,22 +80,46 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    cfg = synth.CONFIGS[args.config]
+    pf6 = args.config == "pf6"
+    cascade = args.config == "cascade"
+    cfg = synth.CONFIGS["gpu" if pf6 else args.config]
     n = args.tuples or cfg["n_tuples"]
     t0 = time.time()
-    T = synth.make_tables(**cfg)
-    tup = synth.make_tuples(T, n, gpu_id=rank)
-    log(f"[rank {rank}] synthetic tables ({len(T.ipc_keys)} ipcache, {len(T.pol_keys)} policy) "
-        f"+ {n} tuples in {time.time() - t0:.1f}s")
-
-    e = Engine(device=local, **T.engine_config())
-    synth.load_engine(e, T)
+    S = None
+    if pf6:
+        P = synth.make_prefilter6(**synth.PF6_CONFIG)
+        tup = synth.make_packets6(P, n, gpu_id=rank)
+        log(f"[rank {rank}] v6 prefilter sets ({len(P.dyn6)} dyn, {len(P.fix6)} fix, "
+            f"{len(P.ep6)} endpoints) + {n} packets in {time.time() - t0:.1f}s")
+        e = Engine(device=local, **P.engine_config())
+        synth.load_prefilter6(e, P)
+    else:
+        T = synth.make_tables(**cfg)
+        tup = synth.make_tuples(T, n, gpu_id=rank)
+        if cascade:
+            S = synth.make_services(T, cfg["n_services"])
+            tup = synth.add_service_traffic(tup, S, gpu_id=rank)
+            del tup["hash"]  # skb->hash stand-in computed in the kernel from sport
+        log(f"[rank {rank}] synthetic tables ({len(T.ipc_keys)} ipcache, {len(T.pol_keys)} policy"
+            f"{', %d service-map entries' % len(S.keys) if S is not None else ''}) "
+            f"+ {n} tuples in {time.time() - t0:.1f}s")
+        ecfg = T.engine_config()
+        if S is not None:
+            ecfg["lb_max_entries"] = len(S.keys)
+        e = Engine(device=local, **ecfg)
+        synth.load_engine(e, T)
+        if S is not None:
+            synth.load_services(e, S)
     t0 = time.time()
     e.commit()
     log(f"[rank {rank}] commit {time.time() - t0:.2f}s, checksum {e.checksum():#x}")
-    d = synth.to_device(tup, dev)
-    out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
-           "identity": torch.empty(n, dtype=torch.int32, device=dev), "stage": None}
+    if pf6:
+        d = synth.packets6_to_device(tup, dev)
+        out = {"verdict": torch.empty(n, dtype=torch.uint8, device=dev)}
+    else:
+        d = synth.to_device(tup, dev)
+        out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+               "identity": torch.empty(n, dtype=torch.int32, device=dev), "stage": None}
     delta = torch.zeros(e.counter_delta_bytes() // 8, dtype=torch.int64, device=dev)
     e.counter_bind(delta)
     stream = torch.cuda.current_stream()
@@ -83,7 +127,12 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        e.classify_v4(d, out=out, stream=stream)
+        if pf6:
+            e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
+        elif cascade:
+            e.classify_v4_lb(d, out=out, stream=stream)
+        else:
+            e.classify_v4(d, out=out, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
@@ -125,43 +174,65 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from oracle import Oracle  # CPU restatement: checker + CPU baseline only
 
-        o = Oracle(**T.oracle_config())
-        synth.load_oracle(o, T)
         threads = args.cpu_threads or min(int(os.environ.get("OMP_NUM_THREADS", "0")) or
                                           os.cpu_count(), os.cpu_count())
-        cpu = None
+        if pf6:
+            o = Oracle(**P.oracle_config())
+            synth.load_prefilter6(o, P)
+        else:
+            o = Oracle(**T.oracle_config())
+            synth.load_oracle(o, T)
+            if S is not None:
+                synth.load_services(o, S)
         c0 = time.perf_counter()
-        v0, i0, _, probes = o.classify_v4(tup, nthreads=threads)
+        if pf6:
+            v0, probes = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
+        elif cascade:
+            v0, i0, _, probes = o.classify_v4_lb(tup, nthreads=threads)
+        else:
+            v0, i0, _, probes = o.classify_v4(tup, nthreads=threads)
         c_el = time.perf_counter() - c0
+        cpu = None
         if not args.no_cpu_baseline:
+            what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
+                    "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash"}.get(
+                args.config, "oracle/cgpu_oracle.c (kernel-like LPM trie + open hash)")
             cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
                    "kind": "port",
-                   "sample": f"rank-0 batch, all {n} tuples, config-2 tables; oracle/cgpu_oracle.c "
-                             f"(kernel-like LPM trie + open hash), {threads} threads, "
-                             f"{c_el:.2f}s wall"}
-        parity = bool(np.array_equal(out["verdict"].cpu().numpy(), v0) and
-                      np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0))
+                   "sample": f"rank-0 batch, all {n} tuples, {args.config} tables; {what}, "
+                             f"{threads} threads, {c_el:.2f}s wall"}
+        parity = bool(np.array_equal(out["verdict"].cpu().numpy(), v0))
+        if not pf6:
+            parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
         probes_per = probes / n
-        b_alg = B_IN + B_OUT + 64.0 * probes_per
+        b_in, b_out = (B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN + (2 if cascade else 0), B_OUT)
+        b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
         traffic = None
-        if os.path.exists(args.traffic_json):
+        if args.config == "gpu" and os.path.exists(args.traffic_json):
             try:
                 traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
+        conf = {"workload": WORKLOADS[args.config], "tuples_per_gpu": n,
+                "parallelism": f"shard{world}", "kernel_ms": round(kern_ms, 4),
+                "probes_per_tuple": round(probes_per, 4), "b_alg_per_tuple": round(b_alg, 2),
+                "parity_vs_oracle": parity}
+        if pf6:
+            conf.update(dyn6_prefixes=len(P.dyn6), fix6_prefixes=len(P.fix6),
+                        endpoints=len(P.ep6))
+        else:
+            conf.update(ipcache_prefixes=int(len(T.ipc_keys)), policy_entries=int(len(T.pol_keys)))
+            if S is not None:
+                conf.update(services=int(len(S.vip)), lb_map_entries=int(len(S.keys)))
         result = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mpps", "n_gpus": world,
+            "metric": METRIC if not pf6 else "Mpps XDP IPv6 prefilter verdicts; % HBM roofline",
+            "value": round(value, 2), "unit": "Mpps", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8" if pf6 else "u32",
             "data": "synthetic (seeded PCG64 tables + tuples, SURVEY §8d)",
-            "config": {"workload": "config2: 100k IPv4 ipcache LPM + 64k policy entries "
-                                   "(4 ep x 16k), 64M-tuple batches per GPU, bit-exact verdicts"
-                       if args.config == "gpu" else "config1 (CPU-scale)",
-                       "tuples_per_gpu": n, "ipcache_prefixes": int(len(T.ipc_keys)),
-                       "policy_entries": int(len(T.pol_keys)), "parallelism": f"shard{world}",
-                       "kernel_ms": round(kern_ms, 4), "probes_per_tuple": round(probes_per, 4),
-                       "b_alg_per_tuple": round(b_alg, 2), "parity_vs_oracle": parity},
+            "config": conf,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic},

@@ -30,7 +30,9 @@ class CgpuConfig(C.Structure):
         ("reserved0", C.c_uint8 * 2),
         ("ingress_src_identity", C.c_uint32),
         ("hot_counter_slots", C.c_uint32),
-        ("reserved", C.c_uint32 * 7),
+        ("lb_max_entries", C.c_uint32), ("ipv4_loopback", C.c_uint32),
+        ("lb_flags", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
     ]
 
 
@@ -42,6 +44,14 @@ class TuplesV4(C.Structure):
 class TuplesV6(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")]
+
+
+class Lb4Tuples(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("saddr", "daddr", "sport", "dport", "proto", "hash")]
+
+
+class Lb4Out(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("ret", "saddr", "daddr", "dport", "rev_nat", "slave")]
 
 
 vp, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
@@ -71,10 +81,19 @@ PROTOS = {
     "cgpu_endpoint_update": (i32, [vp, vp, u64]),
     "cgpu_endpoint_delete": (i32, [vp, vp]),
     "cgpu_endpoint_lookup": (i32, [vp, vp]),
+    "cgpu_lb4_update": (i32, [vp, vp, vp, u64]),
+    "cgpu_lb4_update_batch": (i32, [vp, vp, vp, sz, u64]),
+    "cgpu_lb4_delete": (i32, [vp, vp]),
+    "cgpu_lb4_lookup": (i32, [vp, vp, vp]),
+    "cgpu_lb4_get_next_key": (i32, [vp, vp, vp]),
+    "cgpu_lb4_count": (sz, [vp]),
+    "cgpu_flow_hash": (u32, [u32, u32, C.c_uint16, C.c_uint16, C.c_uint8]),
     "cgpu_commit": (i32, [vp, C.POINTER(u64)]),
     "cgpu_table_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
     "cgpu_classify_v6": (i32, [vp, C.POINTER(TuplesV6), sz, vp, vp, vp, vp]),
+    "cgpu_classify_v4_lb": (i32, [vp, C.POINTER(TuplesV4), vp, vp, sz, vp, vp, vp, vp]),
+    "cgpu_lb4_select": (i32, [vp, i32, C.POINTER(Lb4Tuples), sz, C.POINTER(Lb4Out), vp]),
     "cgpu_prefilter_v4": (i32, [vp, vp, vp, vp, sz, vp, vp]),
     "cgpu_prefilter_v6": (i32, [vp, vp, vp, vp, sz, vp, vp]),
     "cgpu_counter_delta_bytes": (sz, [vp]),

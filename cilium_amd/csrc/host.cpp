@@ -38,6 +38,8 @@ static_assert(sizeof(cgpu_remote_endpoint_info) == 8, "remote_endpoint_info layo
 static_assert(sizeof(cgpu_endpoint_key) == 20, "endpoint_key layout");
 static_assert(sizeof(pol_slot) == 16, "policy slot");
 static_assert(sizeof(set16_slot) == 32, "set16 slot");
+static_assert(sizeof(cgpu_lb4_key) == 8, "lb4_key layout");
+static_assert(sizeof(cgpu_lb4_service) == 12, "lb4_service layout");
 
 namespace {
 
@@ -334,6 +336,9 @@ struct cgpu_ctx {
 	std::set<std::array<uint8_t, 8>> fix4;
 	std::set<std::array<uint8_t, 20>> fix6;
 	std::set<std::array<uint8_t, 20>> lxc;
+	/* cilium_lb4_services, keyed address << 32 | dport << 16 | slave so that
+	 * a frontend's entries are adjacent */
+	std::map<uint64_t, cgpu_lb4_service> lb;
 
 	/* ---- device ---- */
 	void *arena = nullptr;
@@ -376,6 +381,9 @@ CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
 	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
 	c->ingress_src_identity = 0;
 	c->hot_counter_slots = 8192;
+	c->lb_max_entries = 65536;        /* CILIUM_LB_MAP_MAX_ENTRIES, bpf/node_config.h:60 */
+	c->ipv4_loopback = 0x1ffff50a;    /* IPV4_LOOPBACK, bpf/node_config.h:45 */
+	c->lb_flags = CGPU_LB_L3 | CGPU_LB_L4; /* bpf/lxc_config.h:44-45 */
 	static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1,
 					   0x0, 0x1, 0x0, 0x0}; /* ROUTER_IP, bpf/node_config.h:30 */
 	memcpy(c->ipv6_router_ip, router, 16);
@@ -895,6 +903,112 @@ CGPU_EXPORT int cgpu_endpoint_lookup(cgpu_ctx *c, const cgpu_endpoint_key *key)
 }
 
 /* ======================================================================= */
+/* service map (pkg/maps/lbmap; bpf(2) htab semantics, whole-key compare)    */
+/* ======================================================================= */
+static inline uint64_t lb_mkey(const cgpu_lb4_key *k)
+{
+	return (uint64_t)k->address << 32 | (uint64_t)k->dport << 16 | k->slave;
+}
+
+static inline cgpu_lb4_key lb_unkey(uint64_t m)
+{
+	cgpu_lb4_key k;
+	k.address = (uint32_t)(m >> 32);
+	k.dport = (uint16_t)(m >> 16);
+	k.slave = (uint16_t)m;
+	return k;
+}
+
+static int lb_put(cgpu_ctx *c, const cgpu_lb4_key *key, const cgpu_lb4_service *val, uint64_t flags)
+{
+	const uint64_t m = lb_mkey(key);
+	auto it = c->lb.find(m);
+	if (it == c->lb.end()) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "lb4 key not present");
+		if (c->lb.size() >= c->cfg.lb_max_entries)
+			return fail(-E2BIG, "lb4 service map full (%u)", c->cfg.lb_max_entries);
+		c->lb.emplace(m, *val);
+	} else {
+		if (flags == CGPU_NOEXIST)
+			return fail(-EEXIST, "lb4 key exists");
+		it->second = *val;
+	}
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_update(cgpu_ctx *c, const cgpu_lb4_key *key, const cgpu_lb4_service *val,
+				uint64_t flags)
+{
+	if (!c || !key || !val)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	return lb_put(c, key, val, flags);
+}
+
+CGPU_EXPORT int cgpu_lb4_update_batch(cgpu_ctx *c, const cgpu_lb4_key *keys,
+				      const cgpu_lb4_service *vals, size_t n, uint64_t flags)
+{
+	if (!c || (n && (!keys || !vals)))
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	for (size_t i = 0; i < n; i++)
+		if (int r = lb_put(c, &keys[i], &vals[i], flags))
+			return r;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_delete(cgpu_ctx *c, const cgpu_lb4_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lb.erase(lb_mkey(key)) ? 0 : -ENOENT;
+}
+
+CGPU_EXPORT int cgpu_lb4_lookup(cgpu_ctx *c, const cgpu_lb4_key *key, cgpu_lb4_service *out)
+{
+	if (!c || !key || !out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = c->lb.find(lb_mkey(key));
+	if (it == c->lb.end())
+		return -ENOENT;
+	*out = it->second;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_get_next_key(cgpu_ctx *c, const cgpu_lb4_key *key, cgpu_lb4_key *next)
+{
+	if (!c || !next)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = key ? c->lb.upper_bound(lb_mkey(key)) : c->lb.begin();
+	if (it == c->lb.end())
+		return -ENOENT;
+	*next = lb_unkey(it->first);
+	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_lb4_count(cgpu_ctx *c)
+{
+	if (!c)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lb.size();
+}
+
+CGPU_EXPORT uint32_t cgpu_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
+				    uint8_t proto)
+{
+	return flow_hash(saddr, daddr, sport, dport, proto);
+}
+
+/* ======================================================================= */
 /* compiler: mirror -> device layouts                                        */
 /* ======================================================================= */
 namespace {
@@ -1264,6 +1378,76 @@ void build_ipc6(const cgpu_ctx *c, V6Build &b)
 	build_v6(std::move(cand), b);
 }
 
+/* Service map -> frontend hash + dense backend rows (tables.h lb_table).
+ * Returns -E2BIG when sparse slave numbers would need more than
+ * 4 * lb_max_entries + 65536 backend rows. */
+struct LbBuild {
+	std::vector<std::array<uint32_t, 4>> fe, be;
+	uint32_t mask = 0;
+};
+
+int build_lb(const cgpu_ctx *c, LbBuild &b)
+{
+	std::vector<std::array<uint32_t, 4>> fes;
+	const uint64_t cap = 4ull * c->cfg.lb_max_entries + 65536ull;
+	for (auto it = c->lb.begin(); it != c->lb.end();) {
+		const uint64_t fk = it->first >> 16;
+		uint32_t mcount = 0, maxs = 0;
+		auto jt = it;
+		for (; jt != c->lb.end() && (jt->first >> 16) == fk; ++jt) {
+			const uint32_t s = (uint32_t)(jt->first & 0xFFFFu);
+			if (s == 0)
+				mcount = jt->second.count;
+			else
+				maxs = s; /* ascending: the last is the largest */
+		}
+		const uint64_t base = b.be.size();
+		if (base + maxs > cap)
+			return fail(-E2BIG, "lb4 backend rows exceed %llu (sparse slave numbers)",
+				    (unsigned long long)cap);
+		b.be.resize(base + maxs, std::array<uint32_t, 4>{0, 0, 0, 0});
+		for (auto kt = it; kt != jt; ++kt) {
+			const uint32_t s = (uint32_t)(kt->first & 0xFFFFu);
+			if (!s)
+				continue;
+			const cgpu_lb4_service &v = kt->second;
+			b.be[base + s - 1] = {v.target, (uint32_t)v.port | (uint32_t)v.count << 16,
+					      (uint32_t)v.rev_nat_index | (uint32_t)v.weight << 16, 1u};
+		}
+		fes.push_back({(uint32_t)(fk >> 16), (uint32_t)(fk & 0xFFFFu) | mcount << 16, (uint32_t)base,
+			       maxs});
+		it = jt;
+	}
+	uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * fes.size()));
+	for (;;) {
+		b.fe.assign(nb, std::array<uint32_t, 4>{0, 0, 0, 0});
+		b.mask = nb - 1;
+		bool ok = true;
+		for (auto &f : fes) {
+			const uint32_t home = lb_hash(f[0], f[1] & 0xFFFFu) & b.mask;
+			uint32_t d = 0;
+			while (d < POL_HOP && (b.fe[(home + d) & b.mask][3] & LB_FE_USED))
+				d++;
+			if (d == POL_HOP) {
+				ok = false;
+				break;
+			}
+			auto &sl = b.fe[(home + d) & b.mask];
+			sl[0] = f[0];
+			sl[1] = f[1];
+			sl[2] = f[2];
+			sl[3] = (sl[3] & ~0xFFFFFFu) | f[3] | LB_FE_USED;
+			b.fe[home][3] |= 1u << (POL_HOP_SHIFT + d);
+		}
+		if (ok)
+			break;
+		nb *= 2;
+	}
+	if (b.be.empty())
+		b.be.push_back({0, 0, 0, 0});
+	return 0;
+}
+
 } // namespace
 
 CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
@@ -1299,6 +1483,9 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	build_set4(e4, ep4);
 	build_set16(e6, ep6);
 	build_pf6(c, pf6);
+	LbBuild lbb;
+	if (int r = build_lb(c, lbb))
+		return r;
 
 	Arena ar;
 	Lpm16cBuild ipc4c;
@@ -1352,6 +1539,8 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 		for (auto &kv : c->pol[ep])
 			slot_dir[kv.second.slot] = ((kv.first >> 56) & 1u) ? 2 : 1;
 	size_t o_sd = ar.add(slot_dir.data(), slot_dir.size());
+	size_t o_lfe = ar.add(lbb.fe.data(), lbb.fe.size() * 16);
+	size_t o_lbe = ar.add(lbb.be.data(), lbb.be.size() * 16);
 	size_t o_is = ar.add(init_slot.data(), init_slot.size() * 4);
 	size_t o_ip = ar.add(init_pk.data(), init_pk.size() * 8);
 	size_t o_ib = ar.add(init_by.data(), init_by.size() * 8);
@@ -1417,6 +1606,10 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.hot_slots = c->hot_cap;
 	s.cold_hi = c->next_cold;
 	s.slot_dir = (const uint8_t *)(arena + o_sd);
+	s.lb = lb_table{(const uint4 *)(arena + o_lfe), (const uint4 *)(arena + o_lbe), lbb.mask,
+			(uint32_t)lbb.be.size()};
+	s.lb_flags = c->cfg.lb_flags;
+	s.ipv4_loopback = c->cfg.ipv4_loopback;
 	s.epoch = ++c->epoch;
 	c->snap = s;
 	c->committed = true;
@@ -1435,6 +1628,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	for (auto &k : c->fix4) sum += fnv(13, k.data(), k.size());
 	for (auto &k : c->fix6) sum += fnv(17, k.data(), k.size());
 	for (auto &k : c->lxc) sum += fnv(19, k.data(), k.size());
+	for (auto &kv : c->lb) sum += fnv(fnv(23, &kv.first, 8), &kv.second, sizeof(kv.second));
 	c->checksum = sum;
 	if (epoch_out)
 		*epoch_out = s.epoch;
@@ -1498,9 +1692,56 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
 	if (!n)
 		return 0;
 	classify_v4_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
-			   verdict, identity, stage, delta, (uint64_t)n, pk};
+			   verdict, identity, stage, delta, (uint64_t)n, pk, 0, nullptr, nullptr};
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(launch_classify_v4(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_classify_v4_lb(cgpu_ctx *c, const cgpu_tuples_v4 *t, const uint16_t *sport,
+				    const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+				    uint8_t *stage, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta, *pk = nullptr;
+	if (int r = snapshot_for_launch(c, s, delta, stream, &pk))
+		return r;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
+			 !t->ep || !verdict || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n && !hash && !sport)
+		return fail(-EINVAL, "either a hash or an sport column is needed");
+	if (!n)
+		return 0;
+	classify_v4_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
+			   verdict, identity, stage, delta, (uint64_t)n, pk};
+	a.lb = 1;
+	a.sport = sport;
+	a.hash = hash;
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_classify_v4(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_select(cgpu_ctx *c, int mode, const cgpu_lb4_tuples *t, size_t n,
+				const cgpu_lb4_out *out, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (mode != CGPU_LB_NETDEV && mode != CGPU_LB_LXC)
+		return fail(-EINVAL, "bad lb mode %d", mode);
+	if (!t || !out || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !out->ret)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n && !t->hash && !t->sport)
+		return fail(-EINVAL, "either a hash or an sport column is needed");
+	if (!n)
+		return 0;
+	lb4_args a{t->saddr, t->daddr, t->sport, t->dport, t->proto, t->hash, out->ret, out->saddr,
+		   out->daddr, out->dport, out->rev_nat, out->slave, (uint64_t)n, mode};
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_lb4(s, a, (hipStream_t)stream));
 	return 0;
 }
 

@@ -8,6 +8,7 @@
  * waves in flight, independent loads issued together, and 64-byte-aligned
  * table buckets (one cache-line sector per probe).  See DESIGN.md §4.
  */
+#include "cgpu.h"
 #include "launch.h"
 
 #include <algorithm>
@@ -15,8 +16,11 @@
 
 #define DROP_POLICY (-133)           /* bpf/lib/common.h:240 */
 #define DROP_CT_UNKNOWN_PROTO (-137) /* bpf/lib/common.h:244 */
+#define DROP_NO_SERVICE (-158)      /* bpf/lib/common.h:265 */
 #define XDP_DROP 1
 #define XDP_PASS 2
+#define TC_ACT_OK 0
+#define TC_ACT_REDIRECT 7
 
 namespace {
 
@@ -305,6 +309,162 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 	return res ? res : r.y;
 }
 
+/* ---- service load balancer (bpf/lib/lb.h, bpf/bpf_lb.c) ---- */
+
+/* frontend slot of {addr, dport} (tables.h lb_table); w == 0: no frontend */
+__device__ __forceinline__ uint4 lb_frontend(const lb_table &t, uint32_t addr, uint32_t dport)
+{
+	const uint32_t home = lb_hash(addr, dport) & t.fe_mask;
+	const uint4 s = t.fe[home];
+	uint32_t hop = s.w >> POL_HOP_SHIFT;
+	if ((hop & 1u) && s.x == addr && (s.y & 0xFFFFu) == dport)
+		return s;
+	hop &= ~1u;
+	uint4 r = make_uint4(0, 0, 0, 0);
+	while (hop && !r.w) {
+		const uint32_t j = __builtin_ctz(hop);
+		hop &= hop - 1u;
+		const uint4 x = t.fe[(home + j) & t.fe_mask];
+		if (x.x == addr && (x.y & 0xFFFFu) == dport)
+			r = x;
+	}
+	return r;
+}
+
+/* map_lookup_elem(&cilium_lb4_services, {addr, dport, slave}) given the
+ * frontend f of {addr, dport}; *v = {target, port | count << 16,
+ * rev_nat | weight << 16, present}.  For slave 0 only the count is kept
+ * (its only reader is lb4_lookup_service). */
+__device__ __forceinline__ bool lb_entry(const lb_table &t, uint4 f, uint32_t slave, uint4 *v)
+{
+	if (!f.w)
+		return false;
+	if (slave == 0) {
+		*v = make_uint4(0, f.y & 0xFFFF0000u, 0, 1);
+		return true;
+	}
+	if (slave > (f.w & 0xFFFFu))
+		return false;
+	*v = t.be[f.z + slave - 1u];
+	return v->w != 0;
+}
+
+/* lb4_lookup_service (lb.h:604-635): the L4 key {addr, *kd, slave} if its
+ * count is nonzero, else *kd = 0 and the L3 key; *f: the frontend searched
+ * last.  *probes counts map lookups as the reference issues them. */
+__device__ __forceinline__ bool lb_service(const cgpu_snapshot &s, uint32_t addr, uint32_t *kd,
+					   uint32_t slave, uint4 *v, uint4 *f, uint32_t *probes)
+{
+	if ((s.lb_flags & CGPU_LB_L4) && *kd) {
+		*f = lb_frontend(s.lb, addr, *kd);
+		(*probes)++;
+		if (lb_entry(s.lb, *f, slave, v) && (v->y >> 16))
+			return true;
+		*kd = 0;
+	}
+	if (s.lb_flags & CGPU_LB_L3) {
+		*f = lb_frontend(s.lb, addr, *kd);
+		(*probes)++;
+		if (lb_entry(s.lb, *f, slave, v) && (v->y >> 16))
+			return true;
+	}
+	return false;
+}
+
+struct lb_res {
+	int32_t ret;
+	uint32_t saddr, daddr, tdaddr, dport, rev_nat, slave, probes;
+};
+
+/*
+ * One tuple through the service step.  MODE CGPU_LB_NETDEV: bpf_lb.c
+ * handle_ipv4 (:118-170); CGPU_LB_LXC: lb4_local as handle_ipv4_from_lxc
+ * calls it (bpf_lxc.c:444-460) with an empty conntrack table (CT_NEW).
+ * Same decisions as oracle/cgpu_oracle.c lb4_one, which the golden vectors
+ * of the reference pin.  tdaddr is tuple.daddr afterwards (LXC: the service
+ * address is kept on loopback).
+ */
+template <int MODE>
+__device__ __forceinline__ lb_res lb4_one(const cgpu_snapshot &s, uint32_t sa, uint32_t da, uint32_t dp,
+					  uint32_t proto, uint32_t hash)
+{
+	lb_res r = {0, sa, da, da, dp, 0, 0, 0};
+	uint32_t kd = 0;
+	/* lb4_extract_key / extract_l4_port (lb.h:192-216): under LB_L4 only
+	 * TCP/UDP carry a port, ICMP/ICMPv6 go on with 0, the rest are
+	 * DROP_UNKNOWN_L4 = not load-balanced */
+	if (s.lb_flags & CGPU_LB_L4) {
+		if (proto == 6u || proto == 17u)
+			kd = dp;
+		else if (proto != 1u && proto != 58u)
+			return r;
+	}
+	uint4 f, v;
+	if (!lb_service(s, da, &kd, 0, &v, &f, &r.probes))
+		return r;
+	if (MODE == CGPU_LB_LXC && s.ct_proto_gate && proto != 1u && proto != 6u && proto != 17u) {
+		/* lb4_local's CT_SERVICE ct_lookup4: DROP_CT_UNKNOWN_PROTO ->
+		 * DROP_NO_SERVICE (conntrack.h:526-528, lb.h:711-731) */
+		r.ret = DROP_NO_SERVICE;
+		return r;
+	}
+	uint32_t slave = hash % (v.y >> 16) + 1u; /* lb4_select_slave, lb.h:158-190 */
+	uint4 b;
+	r.probes++;
+	if (!lb_entry(s.lb, f, slave, &b)) { /* lb4_lookup_slave, lb.h:637-651 */
+		if (MODE == CGPU_LB_NETDEV) {
+			r.ret = DROP_NO_SERVICE;
+			return r;
+		}
+		/* lb4_local fallback (lb.h:737-744): the key keeps the slave */
+		if (!lb_service(s, da, &kd, slave, &b, &f, &r.probes)) {
+			r.ret = DROP_NO_SERVICE;
+			return r;
+		}
+		slave = hash % (b.y >> 16) + 1u;
+	}
+	r.slave = slave;
+	r.rev_nat = b.z & 0xFFFFu;
+	r.daddr = b.x;
+	if (MODE == CGPU_LB_LXC) {
+		if (sa == b.x) { /* loopback source NAT, lb.h:753-771 */
+			r.saddr = s.ipv4_loopback;
+			r.ret = CGPU_LB_XLATED_LOOPBACK;
+		} else {
+			r.tdaddr = b.x;
+			r.ret = CGPU_LB_XLATED;
+		}
+	} else {
+		r.tdaddr = b.x;
+		r.ret = TC_ACT_REDIRECT;
+	}
+	const uint32_t port = b.y & 0xFFFFu;
+	if ((s.lb_flags & CGPU_LB_L4) && port && kd != port && (proto == 6u || proto == 17u))
+		r.dport = port; /* lb4_xlate, lb.h:685-694 */
+	return r;
+}
+
+template <int MODE> __global__ __launch_bounds__(BLOCK) void k_lb4(cgpu_snapshot s, lb4_args a)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t sa = a.saddr[i], da = a.daddr[i], dp = a.dport[i], pr = a.proto[i];
+		const uint32_t h = a.hash ? a.hash[i] : flow_hash(sa, da, a.sport[i], dp, pr);
+		const lb_res r = lb4_one<MODE>(s, sa, da, dp, pr, h);
+		a.ret[i] = r.ret;
+		if (a.saddr_out)
+			a.saddr_out[i] = r.saddr;
+		if (a.daddr_out)
+			a.daddr_out[i] = r.daddr;
+		if (a.dport_out)
+			a.dport_out[i] = (uint16_t)r.dport;
+		if (a.rev_nat_out)
+			a.rev_nat_out[i] = (uint16_t)r.rev_nat;
+		if (a.slave_out)
+			a.slave_out[i] = (uint16_t)r.slave;
+	}
+}
+
 __device__ __forceinline__ uint32_t entry_label(const uint32_t *vals, uint32_t e)
 {
 	uint32_t p = e & DIR_PAYLOAD_MASK;
@@ -346,6 +506,9 @@ struct cls_args {
 	uint64_t *delta;
 	uint64_t n;
 	uint64_t *pk; /* packed cold-slot accumulator (k_classify_v4_x4 only) */
+	int lb;       /* v4: egress service step first (cgpu_classify_v4_lb) */
+	const uint16_t *sport;
+	const uint32_t *hash;
 };
 
 /* Packed per-workgroup counter: packets in bits 41..63, bytes in 0..40.
@@ -368,7 +531,8 @@ template <int V6, int CTR, int NT, int ABL = 0>
 __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
-	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
+	/* metrics {reason 0 / 133 / 137 / 158} x {ingress, egress} */
+	uint64_t mcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mbyt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	const uint64_t stride = (uint64_t)gridDim.x * NT;
 	uint64_t *pctr = a.delta;
 	if (CTR == 1) {
@@ -381,12 +545,30 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		const uint32_t fl = a.flags[i];
 		const uint32_t proto = a.proto[i];
 		const uint32_t len = a.len[i];
-		const uint32_t dport = a.dport[i];
+		uint32_t dport = a.dport[i];
 		const uint32_t ep = a.ep[i];
 		const bool egress = fl & 1u;
 		int32_t v;
 		uint32_t id;
 		uint32_t st = 0;
+		/* egress service step (bpf_lxc.c:444-469): ipcache resolves
+		 * tuple.daddr afterwards and policy sees the rewritten dport */
+		bool lbdrop = false;
+		uint32_t eda = 0;
+		if (!V6) {
+			eda = static_cast<const uint32_t *>(a.daddr)[i];
+			if (a.lb && egress && ABL == 0) {
+				const uint32_t sa = static_cast<const uint32_t *>(a.saddr)[i];
+				const uint32_t h = a.hash ? a.hash[i] : flow_hash(sa, eda, a.sport[i], dport, proto);
+				const lb_res r = lb4_one<CGPU_LB_LXC>(s, sa, eda, dport, proto, h);
+				if (r.ret == DROP_NO_SERVICE) {
+					lbdrop = true;
+				} else {
+					eda = r.tdaddr;
+					dport = r.dport;
+				}
+			}
+		}
 		/* ct_lookup{4,6} protocol gate: ICMP (v4: 1, v6: 58), TCP, UDP */
 		const bool gated = s.ct_proto_gate && proto != (V6 ? 58u : 1u) && proto != 6u &&
 				   proto != 17u;
@@ -395,6 +577,10 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 			/* diagnostic: columns in, outputs out, no table access */
 			v = (int32_t)(dport ^ proto ^ ep);
 			id = static_cast<const uint32_t *>(egress ? a.daddr : a.saddr)[i];
+		} else if (lbdrop) {
+			v = DROP_NO_SERVICE;
+			id = 0;
+			st = 6;
 		} else if (gated) {
 			v = DROP_CT_UNKNOWN_PROTO;
 			id = 0;
@@ -414,8 +600,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 				/* ipv6_match_prefix_64(daddr, ROUTER_IP), bpf/lib/ipv6.h:166-175 */
 				in_cluster = ad.x == s.router_ip64[0] && ad.y == s.router_ip64[1];
 			} else {
-				const uint32_t ad = egress ? static_cast<const uint32_t *>(a.daddr)[i]
-							   : static_cast<const uint32_t *>(a.saddr)[i];
+				const uint32_t ad = egress ? eda : static_cast<const uint32_t *>(a.saddr)[i];
 				e = dir_lookup(s.ipc4, ad, &label);
 				in_cluster = (ad & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
 			}
@@ -473,10 +658,10 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		a.identity[i] = id;
 		if (a.stage)
 			a.stage[i] = (uint8_t)st;
-		const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : 2u);
+		const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_NO_SERVICE ? 3u : 2u));
 		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
 #pragma unroll
-		for (int k = 0; k < 6; k++) {
+		for (int k = 0; k < 8; k++) {
 			mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
 			mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
 		}
@@ -484,9 +669,9 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 
 	/* metrics: wave-reduce, one atomic per nonzero {reason, dir} per wave */
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
-	const uint32_t reasons[3] = {0u, 133u, 137u};
+	const uint32_t reasons[4] = {0u, 133u, 137u, 158u};
 #pragma unroll
-	for (int k = 0; k < 6; k++) {
+	for (int k = 0; k < 8; k++) {
 		uint64_t c = wave_sum(mcnt[k]);
 		uint64_t b = wave_sum(mbyt[k]);
 		if ((threadIdx.x & 63) == 0 && c) {
@@ -535,17 +720,17 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  * aligned 2-byte columns and 4-byte aligned 1-byte columns; the one partial
  * group at the end of the batch is read element by element.
  */
-template <int NT, int CM = 0, int LP = 1, bool NTL = false, int Q = 4, int MINW = 1>
+template <int NT, int CM = 0, int LP = 1, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false>
 __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
 {
 	/* per-tuple flag word */
-	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u;
+	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u, F_LBDROP = 32u;
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* metrics (drop.h:94-118) kept here only for drops and long forwarded
 	 * packets: [reason 0 / 133 / 137][ingress, egress] x {count, bytes};
 	 * every other forwarded packet is counted by k_unpack from pk, per the
 	 * direction of the entry it hit (metrics of the verdict = its entry's) */
-	__shared__ unsigned long long lmet[12];
+	__shared__ unsigned long long lmet[16];
 	const uint64_t T = (uint64_t)gridDim.x * NT;
 	const uint64_t t0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
 	uint64_t *pctr = a.delta;
@@ -554,7 +739,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots); /* LP == 2 */
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
-	if (threadIdx.x < 12)
+	if (threadIdx.x < 16)
 		lmet[threadIdx.x] = 0;
 	if (LP == 2)
 		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
@@ -625,12 +810,56 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 					da[u] = static_cast<const uint32_t *>(a.daddr)[i];
 				}
 			}
+			uint32_t lbf[Q];
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				lbf[u] = 0;
+			if (LB) {
+				/* egress service step first (bpf_lxc.c:444-469): the
+				 * translated tuple.daddr and dport feed ipcache / policy */
+				uint32_t hh[Q], sp[Q];
+#pragma unroll
+				for (int u = 0; u < Q; u++)
+					hh[u] = sp[u] = 0;
+				if (full && Q == 4) {
+					if (a.hash) {
+						const uint4 h4 = ld_x4<NTL>(a.hash + i0);
+						hh[0] = h4.x, hh[1] = h4.y, hh[2] = h4.z, hh[3] = h4.w;
+					} else {
+						const uint2 s4 = ld_x2<NTL>(a.sport + i0);
+						sp[0] = s4.x & 0xFFFFu, sp[1] = s4.x >> 16;
+						sp[2] = s4.y & 0xFFFFu, sp[3] = s4.y >> 16;
+					}
+				} else {
+#pragma unroll
+					for (int u = 0; u < Q; u++) {
+						const uint64_t i = i0 + u < a.n ? i0 + u : i0;
+						if (a.hash)
+							hh[u] = a.hash[i];
+						else
+							sp[u] = a.sport[i];
+					}
+				}
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					if (!(fl[u] & 1u) || i0 + u >= a.n)
+						continue;
+					const uint32_t h = a.hash ? hh[u] : flow_hash(sa[u], da[u], sp[u], dport[u], proto[u]);
+					const lb_res r = lb4_one<CGPU_LB_LXC>(s, sa[u], da[u], dport[u], proto[u], h);
+					if (r.ret == DROP_NO_SERVICE) {
+						lbf[u] = F_LBDROP;
+					} else {
+						da[u] = r.tdaddr;
+						dport[u] = r.dport;
+					}
+				}
+			}
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
 				const bool eg = fl[u] & 1u;
 				const bool gated =
 					s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u;
-				fw[u] = (i0 + u < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) |
+				fw[u] = (i0 + u < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) | lbf[u] |
 					(!eg && ((fl[u] >> 1) & 1u) ? F_FRAG : 0u);
 				ad[u] = eg ? da[u] : sa[u];
 				hi4[u] = dport[u] | (proto[u] << 16) | (eg ? (1u << 24) : 0u);
@@ -644,7 +873,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
 				q[u] = make_uint4(0, 0, 0, 0);
-				if ((fw[u] & (F_OK | F_GATED)) == F_OK)
+				if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK)
 					q[u] = reinterpret_cast<const uint4 *>(s.ipc4c.x16)[bswap32(ad[u]) >> 16];
 			}
 #pragma unroll
@@ -657,13 +886,13 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				const uint32_t cnt = (x >= (q[u].x & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].x >> 16) ? 1u : 0u) +
 						     (x >= (q[u].y & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].y >> 16) ? 1u : 0u);
 				const uint64_t v = ((uint64_t)q[u].w << 32) | q[u].z;
-				e[u] = (fw[u] & (F_OK | F_GATED)) == F_OK ? ldict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
+				e[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK ? ldict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
 			}
 		} else {
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
 				e[u] = 0;
-				if ((fw[u] & (F_OK | F_GATED)) == F_OK)
+				if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK)
 					e[u] = LP ? s.ipc4c.d16[bswap32(ad[u]) >> 16] : s.ipc4.tbl24[bswap32(ad[u]) >> 8];
 			}
 		}
@@ -747,40 +976,40 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 			ctr[u] = -1;
 			z[u] = 0;
 			st[u] = 0;
-			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP | F_FRAG)) == F_OK) {
 				bk[u] = pol_hash(id[u], hi4[u], ep[u]) & pmask;
 				sl[u] = ptab[bk[u]];
 			}
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP | F_FRAG)) == F_OK) {
 				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u], ep[u], &z[u]);
 				st[u] = 1;
 			}
 		/* probe 2: L3-only {id, 0, 0, dir} (policy.h:74-83) */
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if ((fw[u] & (F_OK | F_GATED)) == F_OK && ctr[u] < 0) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK && ctr[u] < 0) {
 				bk[u] = pol_hash(id[u], hi4[u] & (1u << 24), ep[u]) & pmask;
 				sl[u] = ptab[bk[u]];
 			}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if ((fw[u] & (F_OK | F_GATED)) == F_OK && ctr[u] < 0) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK && ctr[u] < 0) {
 				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u] & (1u << 24), ep[u], &z[u]);
 				st[u] = 2;
 			}
 		/* probe 3: identity-wildcard L4 {0, dport, proto, dir} (policy.h:85-96) */
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK && ctr[u] < 0) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP | F_FRAG)) == F_OK && ctr[u] < 0) {
 				bk[u] = pol_hash(0u, hi4[u], ep[u]) & pmask;
 				sl[u] = ptab[bk[u]];
 			}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
-			if ((fw[u] & (F_OK | F_GATED | F_FRAG)) == F_OK && ctr[u] < 0) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP | F_FRAG)) == F_OK && ctr[u] < 0) {
 				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], 0u, hi4[u], ep[u], &z[u]);
 				st[u] = 3;
 			}
@@ -788,7 +1017,11 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 		int32_t v[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			if (fw[u] & F_GATED) {
+			if (fw[u] & F_LBDROP) {
+				v[u] = DROP_NO_SERVICE;
+				id[u] = 0;
+				st[u] = 6;
+			} else if (fw[u] & F_GATED) {
 				v[u] = DROP_CT_UNKNOWN_PROTO;
 				id[u] = 0;
 				st[u] = 4;
@@ -815,7 +1048,8 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				v[u] = DROP_POLICY;
 			}
 			if ((fw[u] & F_OK) && v[u] < 0) {
-				const uint32_t mi = ((v[u] == DROP_POLICY ? 1u : 2u) * 2u + ((fw[u] & F_EG) ? 1u : 0u)) * 2u;
+				const uint32_t mr = v[u] == DROP_POLICY ? 1u : (v[u] == DROP_NO_SERVICE ? 3u : 2u);
+				const uint32_t mi = (mr * 2u + ((fw[u] & F_EG) ? 1u : 0u)) * 2u;
 				atomicAdd(&lmet[mi], 1ull);
 				atomicAdd(&lmet[mi + 1u], (unsigned long long)len[u]);
 			}
@@ -844,8 +1078,8 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
 	__syncthreads();
-	if (threadIdx.x < 12 && lmet[threadIdx.x]) {
-		const uint32_t reasons[3] = {0u, 133u, 137u};
+	if (threadIdx.x < 16 && lmet[threadIdx.x]) {
+		const uint32_t reasons[4] = {0u, 133u, 137u, 158u};
 		const uint32_t c = threadIdx.x >> 1;
 		const uint32_t key = (reasons[c >> 1] * 4u + ((c & 1) ? 2u : 1u)) * 2u + (threadIdx.x & 1u);
 		atomicAdd((unsigned long long *)&met[key], lmet[threadIdx.x]);
@@ -982,8 +1216,8 @@ static int classify_variant()
 static bool x4_aligned(const cls_args &a)
 {
 	const uintptr_t a16 = (uintptr_t)a.saddr | (uintptr_t)a.daddr | (uintptr_t)a.len |
-			      (uintptr_t)a.verdict | (uintptr_t)a.identity;
-	const uintptr_t a8 = (uintptr_t)a.dport | (uintptr_t)a.ep;
+			      (uintptr_t)a.verdict | (uintptr_t)a.identity | (uintptr_t)a.hash;
+	const uintptr_t a8 = (uintptr_t)a.dport | (uintptr_t)a.ep | (uintptr_t)a.sport;
 	const uintptr_t a4 = (uintptr_t)a.proto | (uintptr_t)a.flags | (uintptr_t)a.stage;
 	return !(a16 & 15) && !(a8 & 7) && !(a4 & 3);
 }
@@ -1035,8 +1269,15 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 		c.ep += off;
 		c.saddr = static_cast<const uint32_t *>(a.saddr) + off;
 		c.daddr = static_cast<const uint32_t *>(a.daddr) + off;
+		if (c.sport)
+			c.sport += off;
+		if (c.hash)
+			c.hash += off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + 4 * NT - 1) / (4 * NT), res);
-		if (var == 12)
+		if (a.lb)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true, 4, 1, true>), dim3(g), dim3(NT), lds2, st, s,
+					   c, a.pk);
+		else if (var == 12)
 			hipLaunchKernelGGL((k_classify_v4_x4<NT, 2, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
 		else if (var == 15)
 			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0, true>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
@@ -1108,6 +1349,10 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 		c.ep += off;
 		c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
 		c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
+		if (c.sport)
+			c.sport += off;
+		if (c.hash)
+			c.hash += off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
 		hipLaunchKernelGGL((k_classify<V6, 1, NT>), dim3(g), dim3(NT), lds, st, s, c);
 	}
@@ -1117,13 +1362,24 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x, hipStream_t st)
 {
 	return launch_classify<0>(s, cls_args{x.saddr, x.daddr, x.dport, x.proto, x.flags, x.len, x.ep,
-					      x.verdict, x.identity, x.stage, x.delta, x.n, x.pk}, st);
+					      x.verdict, x.identity, x.stage, x.delta, x.n, x.pk, x.lb, x.sport,
+					      x.hash}, st);
 }
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)
 {
 	return launch_classify<1>(s, cls_args{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len,
-					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, nullptr}, st);
+					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, nullptr, 0, nullptr,
+					      nullptr}, st);
+}
+
+hipError_t launch_lb4(const cgpu_snapshot &s, const lb4_args &a, hipStream_t st)
+{
+	if (a.mode == CGPU_LB_NETDEV)
+		hipLaunchKernelGGL(k_lb4<CGPU_LB_NETDEV>, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	else
+		hipLaunchKernelGGL(k_lb4<CGPU_LB_LXC>, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
 }
 
 hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)

@@ -21,6 +21,10 @@ struct classify_v4_args {
 	uint64_t *delta; /* [2 * n_ctr_slots] policy + [CGPU_METRICS_WORDS] metrics */
 	uint64_t n;
 	uint64_t *pk;    /* [n_ctr_slots] packed cold-slot accumulator, zero between calls */
+	/* egress service step first (cgpu_classify_v4_lb) */
+	int lb;
+	const uint16_t *sport;
+	const uint32_t *hash; /* NULL: flow_hash(saddr, daddr, sport, dport, proto) */
 };
 
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st);
@@ -50,6 +54,20 @@ struct prefilter_args {
 
 hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st);
 hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st);
+
+struct lb4_args {
+	const uint32_t *saddr, *daddr;
+	const uint16_t *sport, *dport;
+	const uint8_t *proto;
+	const uint32_t *hash;
+	int32_t *ret;
+	uint32_t *saddr_out, *daddr_out;
+	uint16_t *dport_out, *rev_nat_out, *slave_out;
+	uint64_t n;
+	int mode; /* CGPU_LB_NETDEV / CGPU_LB_LXC */
+};
+
+hipError_t launch_lb4(const cgpu_snapshot &s, const lb4_args &a, hipStream_t st);
 
 /* totals[i] += delta[i]; delta[i] = 0 over n u64 words */
 hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st);

@@ -184,6 +184,52 @@ typedef struct v6_lpm {
 	uint32_t n_masks;
 } v6_lpm;
 
+/* ---- service map (cilium_lb4_services, bpf/lib/lb.h:70-76) ----
+ * Grouped by frontend {address, dport}: one 16-byte frontend slot per
+ * frontend in a single-slot neighbourhood hash (POL_HOP scheme, hop bits
+ * 24..31 of w), and the frontend's backends in a dense array:
+ *   fe: x = address, y = dport | master_count << 16, z = base (index in `be`
+ *       of slave 1), w = nslaves (bits 0..15) | LB_FE_USED | hop << 24.
+ *       master_count = count of the slave-0 entry, 0 when there is none:
+ *       slave 0 is only ever read by lb4_lookup_service, which treats count
+ *       0 and "no entry" alike (lb.h:613-629).
+ *   be[base + s - 1], s = 1..nslaves: {target, port | count << 16,
+ *       rev_nat_index | weight << 16, present}.
+ * A service lookup is one 16-byte gather (the frontend slot, usually its
+ * home slot) and a backend lookup one more, dependent, 16-byte gather. */
+#define LB_FE_USED (1u << 16)
+
+typedef struct lb_table {
+	const uint4 *fe; /* fe_mask + 1 slots, never NULL once committed */
+	const uint4 *be;
+	uint32_t fe_mask;
+	uint32_t n_be;
+} lb_table;
+
+static inline __host__ __device__ uint32_t lb_hash(uint32_t addr, uint32_t dport)
+{
+	return mix32(addr, dport ^ 0x1b5e0000u);
+}
+
+/* cgpu_flow_hash (include/cgpu.h): murmur3 finalizer over the stored
+ * 5-tuple, = cilium_amd/shard.py flowhash_np */
+static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t daddr, uint32_t sport,
+						     uint32_t dport, uint32_t proto)
+{
+	uint32_t h = saddr * 0x9E3779B1u;
+	h ^= daddr;
+	h *= 0x85EBCA77u;
+	h ^= (sport << 16) | dport;
+	h *= 0xC2B2AE3Du;
+	h ^= proto;
+	h ^= h >> 16;
+	h *= 0x85EBCA6Bu;
+	h ^= h >> 13;
+	h *= 0xC2B2AE35u;
+	h ^= h >> 16;
+	return h;
+}
+
 /* ---- one committed snapshot ---- */
 typedef struct cgpu_snapshot {
 	dir248 ipc4;
@@ -205,6 +251,9 @@ typedef struct cgpu_snapshot {
 	uint32_t hot_slots;      /* counter slots [0, hot_slots) may live in LDS */
 	uint32_t cold_hi;        /* counter slots >= cold_hi are unassigned */
 	const uint8_t *slot_dir; /* per counter slot: 1 ingress, 2 egress key, 0 free */
+	lb_table lb;
+	uint32_t lb_flags;       /* CGPU_LB_L3 | CGPU_LB_L4 */
+	uint32_t ipv4_loopback;  /* IPV4_LOOPBACK, network order */
 	uint64_t epoch;
 } cgpu_snapshot;
 

@@ -10,6 +10,8 @@ that tests read like the reference's own callers:
   (pkg/ipcache/listener.go:36-48, pkg/datapath/ipcache/listener.go:78-127)
 * :class:`CIDRMap`    — pkg/maps/cidrmap/cidrmap.go (InsertCIDR/DeleteCIDR/
   CIDRExists/CIDRDump, checkPrefixlen)
+* :class:`LBMap`      — pkg/maps/lbmap/lbmap.go (UpdateService/DeleteService/
+  LookupService/DumpServiceMapsToUserspace over cilium_lb4_services)
 
 Batch entry points take torch CUDA tensors (device memory) and launch on the
 caller's current HIP stream.  Nothing here computes a verdict on the CPU.
@@ -23,7 +25,7 @@ import ipaddress
 import numpy as np
 
 from . import layouts as L
-from ._abi import CgpuConfig, CgpuError, TuplesV4, TuplesV6, check, lib
+from ._abi import CgpuConfig, CgpuError, Lb4Out, Lb4Tuples, TuplesV4, TuplesV6, check, lib
 
 CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX = 0, 1, 2, 3
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
@@ -149,6 +151,37 @@ class Engine:
     def endpoint_lookup(self, key) -> int:
         return self.L.cgpu_endpoint_lookup(self.h, _buf(key))
 
+    def lb4_update(self, key, val, flags=BPF_ANY) -> int:
+        return self.L.cgpu_lb4_update(self.h, _buf(key), _buf(val), flags)
+
+    def lb4_update_batch(self, keys, vals, flags=BPF_ANY) -> int:
+        k = np.ascontiguousarray(keys, L.LB4_KEY)
+        v = np.ascontiguousarray(vals, L.LB4_SERVICE)
+        assert len(k) == len(v)
+        return self.L.cgpu_lb4_update_batch(self.h, k.ctypes.data, v.ctypes.data, len(k), flags)
+
+    def lb4_delete(self, key) -> int:
+        return self.L.cgpu_lb4_delete(self.h, _buf(key))
+
+    def lb4_lookup(self, key):
+        out = C.create_string_buffer(12)
+        rc = self.L.cgpu_lb4_lookup(self.h, _buf(key), out)
+        return rc, (np.frombuffer(out.raw, L.LB4_SERVICE)[0] if rc == 0 else None)
+
+    def lb4_keys(self):
+        keys, prev = [], None
+        out = C.create_string_buffer(8)
+        while self.L.cgpu_lb4_get_next_key(self.h, prev, out) == 0:
+            prev = out.raw
+            keys.append(np.frombuffer(prev, L.LB4_KEY)[0])
+        return keys
+
+    def lb4_count(self) -> int:
+        return self.L.cgpu_lb4_count(self.h)
+
+    def flow_hash(self, saddr, daddr, sport, dport, proto) -> int:
+        return self.L.cgpu_flow_hash(saddr, daddr, sport, dport, proto)
+
     def commit(self) -> int:
         ep = C.c_uint64()
         check(self.L.cgpu_commit(self.h, C.byref(ep)), "cgpu_commit")
@@ -175,6 +208,45 @@ class Engine:
         check(self.L.cgpu_classify_v4(self.h, C.byref(tv), n, _ptr(out["verdict"]),
                                       _ptr(out["identity"]), _ptr(out.get("stage")),
                                       _stream(stream)), "cgpu_classify_v4")
+        return out
+
+    def classify_v4_lb(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """classify_v4 with the egress service step first (BASELINE config 5).
+        t additionally holds "hash" (int32 view of skb->hash) or "sport"."""
+        import torch
+        n = t["saddr"].numel()
+        dev = t["saddr"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
+        tv = TuplesV4(*[t[k].data_ptr() for k in
+                        ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")])
+        check(self.L.cgpu_classify_v4_lb(self.h, C.byref(tv), _ptr(t.get("sport")),
+                                         _ptr(t.get("hash")), n, _ptr(out["verdict"]),
+                                         _ptr(out["identity"]), _ptr(out.get("stage")),
+                                         _stream(stream)), "cgpu_classify_v4_lb")
+        return out
+
+    def lb4_select(self, t: dict, mode: int, out: dict | None = None, stream=None):
+        """Service translation alone: t holds saddr/daddr (int32 views),
+        dport/sport (int16 views), proto (uint8), optional hash (int32)."""
+        import torch
+        n = t["daddr"].numel()
+        dev = t["daddr"].device
+        if out is None:
+            out = {"ret": torch.empty(n, dtype=torch.int32, device=dev),
+                   "saddr": torch.empty(n, dtype=torch.int32, device=dev),
+                   "daddr": torch.empty(n, dtype=torch.int32, device=dev),
+                   "dport": torch.empty(n, dtype=torch.int16, device=dev),
+                   "rev_nat": torch.empty(n, dtype=torch.int16, device=dev),
+                   "slave": torch.empty(n, dtype=torch.int16, device=dev)}
+        tv = Lb4Tuples(*[_ptr(t.get(k)) for k in ("saddr", "daddr", "sport", "dport", "proto",
+                                                  "hash")])
+        ov = Lb4Out(*[_ptr(out.get(k)) for k in ("ret", "saddr", "daddr", "dport", "rev_nat",
+                                                 "slave")])
+        check(self.L.cgpu_lb4_select(self.h, mode, C.byref(tv), n, C.byref(ov), _stream(stream)),
+              "cgpu_lb4_select")
         return out
 
     def classify_v6(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
@@ -348,3 +420,47 @@ class CIDRMap:
             addr = ipaddress.ip_address(raw)
             out.append(f"{addr}/{int(k['prefixlen'])}")
         return out
+
+
+class LBMap:
+    """pkg/maps/lbmap over cilium_lb4_services (IPv4): the frontend/backend
+    writes of UpdateService (lbmap.go:350-428: backends at slaves 1..n, then
+    the master slot 0 {count, weight}, then stale slaves removed) and
+    DeleteService."""
+
+    def __init__(self, engine: Engine):
+        self.e = engine
+
+    def UpdateService(self, vip: str, port: int, backends, rev_nat: int = 0):  # noqa: N802
+        """backends: [(target, port, weight), ...] (ports host order)."""
+        rc, old = self.e.lb4_lookup(L.lb4_key(vip, port, 0))
+        existing = int(old["count"]) if rc == 0 else 0
+        for i, (tgt, bport, w) in enumerate(backends):
+            check(self.e.lb4_update(L.lb4_key(vip, port, i + 1),
+                                    L.lb4_service(tgt, bport, 0, rev_nat, w)), "UpdateService")
+        nonzero = sum(1 for b in backends if b[2])
+        check(self.e.lb4_update(L.lb4_key(vip, port, 0),
+                                L.lb4_service(0, 0, len(backends), 0, nonzero)), "UpdateService")
+        for s in range(len(backends) + 1, existing + 1):
+            self.e.lb4_delete(L.lb4_key(vip, port, s))
+
+    def DeleteService(self, vip: str, port: int):  # noqa: N802
+        rc, old = self.e.lb4_lookup(L.lb4_key(vip, port, 0))
+        if rc != 0:
+            raise CgpuError(errno.ENOENT, f"service {vip}:{port} not found")
+        for s in range(int(old["count"]), -1, -1):
+            self.e.lb4_delete(L.lb4_key(vip, port, s))
+
+    def LookupService(self, vip: str, port: int):  # noqa: N802
+        rc, master = self.e.lb4_lookup(L.lb4_key(vip, port, 0))
+        if rc != 0:
+            return None
+        out = []
+        for s in range(1, int(master["count"]) + 1):
+            rc, be = self.e.lb4_lookup(L.lb4_key(vip, port, s))
+            if rc == 0:
+                out.append(be)
+        return out
+
+    def DumpServiceMapsToUserspace(self):  # noqa: N802
+        return [(k, self.e.lb4_lookup(k)[1]) for k in self.e.lb4_keys()]

@@ -36,6 +36,9 @@ CONFIGS = {
                 n_tuples=1 << 20),
     "gpu": dict(n_prefixes=100_000, n_identities=1000, n_endpoints=4, keys_per_ep=16_000,
                 n_tuples=64 << 20),
+    # config 5: config-2 tables + 1M IPv4 services in front
+    "cascade": dict(n_prefixes=100_000, n_identities=1000, n_endpoints=4, keys_per_ep=16_000,
+                    n_tuples=64 << 20, n_services=1_000_000),
 }
 
 # cluster CIDR 10.0.0.0/8 expressed like node_config.h's IPV4_CLUSTER_MASK /
@@ -208,7 +211,8 @@ def load_oracle(oracle, t: Tables):
 
 
 TUPLE_DTYPES = {"saddr": np.uint32, "daddr": np.uint32, "dport": np.uint16, "proto": np.uint8,
-                "flags": np.uint8, "len": np.uint32, "ep": np.uint16}
+                "flags": np.uint8, "len": np.uint32, "ep": np.uint16, "sport": np.uint16,
+                "hash": np.uint32}
 
 
 def to_device(t: dict, device="cuda"):
@@ -218,9 +222,182 @@ def to_device(t: dict, device="cuda"):
     view = {np.uint32: np.int32, np.uint16: np.int16, np.uint8: np.uint8}
     out = {}
     for k, dt in TUPLE_DTYPES.items():
+        if k not in t:
+            continue
         if k in ("saddr", "daddr") and np.asarray(t[k]).ndim == 2:
             a = np.ascontiguousarray(t[k], np.uint8)
         else:
             a = np.ascontiguousarray(t[k], dt).view(view[dt])
         out[k] = torch.from_numpy(a).to(device, non_blocking=False)
     return out
+
+
+# ---------------------------------------------------------------------------
+# services: VIPs in 100.64.0.0/10, 90% L4 (Zipf port
+# set) / 10% L3 (dport 0) frontends, backends per service ~Geom(p=0.3) capped
+# at 16, backend targets inside installed ipcache prefixes (so the post-DNAT
+# identity is meaningful), 30% of backends on a different target port.
+# Written as lbmap.UpdateService writes them: slave 0 = {count}, 1..n = backends.
+# ---------------------------------------------------------------------------
+@dataclass
+class Services:
+    keys: np.ndarray   # LB4_KEY
+    vals: np.ndarray   # LB4_SERVICE
+    vip: np.ndarray    # network-order u32 per service
+    port: np.ndarray   # network-order u16 per service (0 = L3 service)
+
+
+def make_services(tables: Tables, n_services: int, seed=SEED, max_backends=16, p=0.3,
+                  l3_frac=0.1) -> Services:
+    rng = np.random.Generator(np.random.PCG64(seed + 0x5E))
+    host = rng.choice(1 << 22, n_services, replace=False).astype(np.uint32)
+    vip = (np.uint32(0x64400000) | host).byteswap()        # 100.64.0.0/10
+    port = np.where(rng.random(n_services) < l3_frac, 0,
+                    zipf_ports(rng, n_services)).astype(np.uint16).byteswap()
+    nb = np.minimum(rng.geometric(p, n_services), max_backends).astype(np.int64)
+    nbt = int(nb.sum())
+    keys = np.zeros(n_services + nbt, L.LB4_KEY)
+    vals = np.zeros(n_services + nbt, L.LB4_SERVICE)
+    keys["address"][:n_services] = vip
+    keys["dport"][:n_services] = port
+    vals["count"][:n_services] = nb
+    svc = np.repeat(np.arange(n_services), nb)
+    first = np.repeat(np.cumsum(nb) - nb, nb)
+    slave = np.arange(nbt) - first + 1
+    kb, vb = keys[n_services:], vals[n_services:]
+    kb["address"] = vip[svc]
+    kb["dport"] = port[svc]
+    kb["slave"] = slave
+    pi = rng.integers(0, len(tables.pfx_addr), nbt)
+    ln = tables.pfx_len[pi].astype(np.uint64)
+    hmask = (np.uint64(1) << (np.uint64(32) - ln)) - np.uint64(1)
+    tgt = (tables.pfx_addr[pi].astype(np.uint64) |
+           (rng.integers(0, 2**32, nbt, dtype=np.uint64) & hmask)).astype(np.uint32)
+    vb["target"] = tgt.byteswap()
+    svc_port = port[svc]
+    other = rng.integers(1024, 65536, nbt).astype(np.uint16).byteswap()
+    vb["port"] = np.where(rng.random(nbt) < 0.3, other, svc_port)
+    vb["rev_nat_index"] = ((svc % 65535) + 1).astype(np.uint16).byteswap()
+    vb["weight"] = np.uint16(1).byteswap()
+    return Services(keys, vals, vip, port)
+
+
+def add_service_traffic(t: dict, svcs: Services, frac=0.3, seed=SEED, gpu_id: int = 0):
+    """sport + hash columns, and `frac` of the egress tuples aimed at a
+    service (daddr = VIP, dport = its port, or any port for L3 services)."""
+    from .shard import flowhash_np
+    rng = np.random.Generator(np.random.PCG64(seed + 0x77 + gpu_id))
+    n = len(t["saddr"])
+    t = dict(t)
+    t["sport"] = rng.integers(1024, 65536, n).astype(np.uint16).byteswap()
+    hit = ((t["flags"] & 1) == 1) & (rng.random(n) < frac)
+    si = rng.integers(0, len(svcs.vip), n)
+    t["daddr"] = np.where(hit, svcs.vip[si], t["daddr"]).astype(np.uint32)
+    t["dport"] = np.where(hit & (svcs.port[si] != 0), svcs.port[si], t["dport"]).astype(np.uint16)
+    t["hash"] = flowhash_np(t["saddr"], t["daddr"], t["sport"], t["dport"], t["proto"])
+    return t
+
+
+def load_services(target, svcs: Services):
+    """Engine (cgpu_lb4_update_batch) or Oracle (or_lb_update_many)."""
+    if hasattr(target, "lb4_update_batch"):
+        rc = target.lb4_update_batch(svcs.keys, svcs.vals)
+    else:
+        rc = target.lb_update_batch(svcs.keys, svcs.vals)
+    assert rc == 0, rc
+
+
+# ---------------------------------------------------------------------------
+# config 3 (SURVEY §8d): XDP IPv6 prefilter, 1M deny prefixes with lengths
+# /32 5%, /48 45%, /56 20%, /64 20%, /128 10% (the /128s go to the "fix" hash,
+# the rest to the "dyn" LPM), under 256 random /24 roots; 4k local endpoint
+# IPs; packets 50% sourced inside a deny prefix, 30% addressed to an endpoint.
+# ---------------------------------------------------------------------------
+PF6_CONFIG = dict(n_prefixes=1_000_000, n_roots=256, n_endpoints=4096)
+
+
+@dataclass
+class Prefilter6:
+    dyn6: np.ndarray    # LPM_V6_KEY
+    fix6: np.ndarray    # LPM_V6_KEY, prefixlen 128
+    ep6: np.ndarray     # ENDPOINT_KEY (family 2)
+    roots: np.ndarray   # (n_roots, 3) uint8
+
+    def engine_config(self):
+        return dict(cidr_dyn_max=max(1 << 20, len(self.dyn6)),
+                    cidr_fix_max=max(1 << 20, len(self.fix6)),
+                    endpoints_max=max(65536, len(self.ep6)))
+
+    def oracle_config(self):
+        return {}
+
+
+def make_prefilter6(n_prefixes=1_000_000, n_roots=256, n_endpoints=4096, seed=SEED, **_):
+    rng = np.random.Generator(np.random.PCG64(seed + 0x36))
+    roots = rng.integers(0, 256, (n_roots, 3), dtype=np.uint8)
+    m = int(n_prefixes * 1.05) + 16
+    ln = rng.choice(np.array([32, 48, 56, 64, 128]), m, p=[0.05, 0.45, 0.20, 0.20, 0.10])
+    a = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+    a[:, :3] = roots[rng.integers(0, n_roots, m)]
+    # canonical (masked) prefixes, deduplicated on (len, masked address)
+    bits = np.unpackbits(a, axis=1)
+    bits[np.arange(128)[None, :] >= ln[:, None]] = 0
+    a = np.packbits(bits, axis=1)
+    rec = np.zeros(m, np.dtype([("len", "u1"), ("a", "u1", (16,))]))
+    rec["len"], rec["a"] = ln, a
+    _, first = np.unique(rec.view(np.dtype((np.void, 17))), return_index=True)
+    first = np.sort(first)[:n_prefixes]
+    ln, a = ln[first], a[first]
+    keys = np.zeros(len(ln), L.LPM_V6_KEY)
+    keys["prefixlen"] = ln
+    keys["addr"] = a
+    fix = ln == 128
+    ep_a = rng.integers(0, 256, (n_endpoints, 16), dtype=np.uint8)
+    ep_a[:, :3] = roots[rng.integers(0, n_roots, n_endpoints)]
+    ep = np.zeros(n_endpoints, L.ENDPOINT_KEY)
+    ep["ip"] = ep_a
+    ep["family"] = L.ENDPOINT_KEY_IPV6
+    return Prefilter6(keys[~fix], keys[fix], ep, roots)
+
+
+def make_packets6(P: Prefilter6, n: int, seed=SEED, gpu_id: int = 0, chunk=1 << 22):
+    rng = np.random.Generator(np.random.PCG64(seed + 0x66 + gpu_id))
+    allk = np.concatenate([P.dyn6, P.fix6])
+    sa = np.empty((n, 16), np.uint8)
+    da = np.empty((n, 16), np.uint8)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        m = hi - lo
+        s = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+        inside = rng.random(m) < 0.5
+        k = allk[rng.integers(0, len(allk), m)]
+        bits = np.unpackbits(s, axis=1)
+        kb = np.unpackbits(np.ascontiguousarray(k["addr"]), axis=1)
+        keep = np.arange(128)[None, :] < k["prefixlen"][:, None].astype(np.int64)
+        bits = np.where(inside[:, None] & keep, kb, bits)
+        s = np.packbits(bits, axis=1)
+        outside = ~inside
+        s[outside, :3] = P.roots[rng.integers(0, len(P.roots), int(outside.sum()))]
+        sa[lo:hi] = s
+        d = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+        to_ep = rng.random(m) < 0.3
+        d[to_ep] = P.ep6["ip"][rng.integers(0, len(P.ep6), int(to_ep.sum()))]
+        da[lo:hi] = d
+    return {"saddr": sa, "daddr": da, "flags": np.zeros(n, np.uint8)}
+
+
+def load_prefilter6(target, P: Prefilter6):
+    """Engine or Oracle: dyn6 / fix6 CIDR maps (pkg/maps/cidrmap) + cilium_lxc."""
+    for which, keys in ((2, P.dyn6), (3, P.fix6)):
+        for k in keys:
+            rc = target.cidr_update(which, k)
+            assert rc == 0, rc
+    for k in P.ep6:
+        rc = target.endpoint_update(k)
+        assert rc == 0, rc
+
+
+def packets6_to_device(p: dict, device="cuda"):
+    import torch
+    return {k: torch.from_numpy(np.ascontiguousarray(v, np.uint8)).to(device)
+            for k, v in p.items()}

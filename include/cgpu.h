@@ -142,8 +142,19 @@ typedef struct cgpu_config {
 	 * identity-wildcard policy keys (the entries most tuples hit) and are
 	 * accumulated in LDS per workgroup before one flush to HBM */
 	uint32_t hot_counter_slots;
-	uint32_t reserved[7];
+	/* service map cilium_lb4_services: max_elem (CILIUM_LB_MAP_MAX_ENTRIES,
+	 * bpf/node_config.h:60; raise it for the 1M-service config) */
+	uint32_t lb_max_entries;
+	/* IPV4_LOOPBACK (bpf/node_config.h:45), network-order u32 as written */
+	uint32_t ipv4_loopback;
+	/* CGPU_LB_L3 | CGPU_LB_L4: the LB_L3 / LB_L4 build switches of lib/lb.h
+	 * (bpf/lxc_config.h:44-45 and bpf/init.sh:352 set both) */
+	uint32_t lb_flags;
+	uint32_t reserved[4];
 } cgpu_config;
+
+#define CGPU_LB_L3 1u
+#define CGPU_LB_L4 2u
 
 typedef struct cgpu_ctx cgpu_ctx;
 
@@ -199,6 +210,46 @@ int cgpu_endpoint_delete(cgpu_ctx *ctx, const cgpu_endpoint_key *key);
 int cgpu_endpoint_lookup(cgpu_ctx *ctx, const cgpu_endpoint_key *key);
 
 /* ------------------------------------------------------------------ */
+/* service map cilium_lb4_services: pkg/maps/lbmap (UpdateService /     */
+/* DeleteService, lbmap.go:341-429), bpf/lib/lb.h:70-76                  */
+/* ------------------------------------------------------------------ */
+/* struct lb4_key, bpf/lib/common.h:427-431: address and dport in network
+ * order, slave host order (Go Service4Key.ToNetwork, lbmap/ipv4.go:99-104) */
+typedef struct cgpu_lb4_key {
+	uint32_t address;
+	uint16_t dport;
+	uint16_t slave; /* 0 = the service ("master"), 1.. = backends */
+} cgpu_lb4_key;
+
+/* struct lb4_service, bpf/lib/common.h:433-439: target, port, rev_nat_index,
+ * weight in network order; count host order (lbmap/ipv4.go:135-181) */
+typedef struct cgpu_lb4_service {
+	uint32_t target;
+	uint16_t port;
+	uint16_t count;
+	uint16_t rev_nat_index;
+	uint16_t weight;
+} cgpu_lb4_service;
+
+int cgpu_lb4_update(cgpu_ctx *ctx, const cgpu_lb4_key *key, const cgpu_lb4_service *val,
+		    uint64_t flags);
+/* n updates in order; stops at the first failure (its -errno is returned,
+ * the entries before it stay applied).  The Go writer issues one bpf(2)
+ * call per entry; this is the same sequence in one call. */
+int cgpu_lb4_update_batch(cgpu_ctx *ctx, const cgpu_lb4_key *keys, const cgpu_lb4_service *vals,
+			  size_t n, uint64_t flags);
+int cgpu_lb4_delete(cgpu_ctx *ctx, const cgpu_lb4_key *key);
+int cgpu_lb4_lookup(cgpu_ctx *ctx, const cgpu_lb4_key *key, cgpu_lb4_service *val_out);
+int cgpu_lb4_get_next_key(cgpu_ctx *ctx, const cgpu_lb4_key *key, cgpu_lb4_key *next_out);
+size_t cgpu_lb4_count(cgpu_ctx *ctx);
+
+/* The flow hash the batch entry points use when no hash column is given
+ * (skb->hash comes from the kernel's flow dissector, which the reference
+ * does not contain: SURVEY §8c).  Over the stored (network-order) fields. */
+uint32_t cgpu_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
+			uint8_t proto);
+
+/* ------------------------------------------------------------------ */
 /* publication                                                          */
 /* ------------------------------------------------------------------ */
 /* Compile the host mirror into device tables and publish them as the new
@@ -234,7 +285,7 @@ typedef struct cgpu_tuples_v4 {
  *                 DROP_POLICY (-133), DROP_CT_UNKNOWN_PROTO (-137)
  *   identity[i] : label given to policy (dstID on egress, secctx on ingress)
  *   stage[i]    : optional (NULL ok): 1 exact, 2 L3-only, 3 identity-wildcard
- *                 L4, 0 miss, 4 protocol-gated
+ *                 L4, 0 miss, 4 protocol-gated (6: service drop, _lb only)
  */
 int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
 		     uint32_t *identity, uint8_t *stage, void *stream);
@@ -258,6 +309,49 @@ typedef struct cgpu_tuples_v6 {
  */
 int cgpu_classify_v6(cgpu_ctx *ctx, const cgpu_tuples_v6 *t, size_t n, int32_t *verdict,
 		     uint32_t *identity, uint8_t *stage, void *stream);
+
+/*
+ * cgpu_classify_v4 with the egress service step of handle_ipv4_from_lxc in
+ * front (bpf_lxc.c:444-469; BASELINE config 5): every egress tuple is first
+ * translated by lb4_local (stateless: conntrack empty, CT_NEW), ipcache then
+ * resolves the translated tuple.daddr and policy sees the rewritten dport.
+ * A DROP_NO_SERVICE (-158) ends the tuple: identity 0, stage 6, metrics
+ * reason 158 egress (bpf_lxc.c:659-666).  Ingress tuples are as in
+ * cgpu_classify_v4.  hash: skb->hash per tuple, or NULL for cgpu_flow_hash
+ * over (saddr, daddr, sport, dport, proto); sport may be NULL when hash is
+ * given.
+ */
+int cgpu_classify_v4_lb(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, const uint16_t *sport,
+			const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+			uint8_t *stage, void *stream);
+
+/* Service translation alone (device pointers). */
+#define CGPU_LB_NETDEV 0 /* bpf_lb.c handle_ipv4 (bpf_lb.c:118-170) */
+#define CGPU_LB_LXC 1    /* lb4_local on the endpoint egress path (bpf_lxc.c:444-460) */
+/* ret codes of CGPU_LB_LXC (CGPU_LB_NETDEV returns TC_ACT_OK 0 when the
+ * packet is not load-balanced, TC_ACT_REDIRECT 7 when it is) */
+#define CGPU_LB_NONE 0
+#define CGPU_LB_XLATED 1
+#define CGPU_LB_XLATED_LOOPBACK 2 /* source NAT to IPV4_LOOPBACK, lb.h:753-767 */
+#define CGPU_DROP_NO_SERVICE (-158)
+
+typedef struct cgpu_lb4_tuples {
+	const uint32_t *saddr, *daddr; /* network order */
+	const uint16_t *sport, *dport; /* network order; sport only for the default hash */
+	const uint8_t *proto;
+	const uint32_t *hash;          /* NULL: cgpu_flow_hash */
+} cgpu_lb4_tuples;
+
+/* outputs (device pointers; all but ret may be NULL): the packet's saddr /
+ * daddr / dport after lb4_xlate, the chosen entry's rev_nat_index and slave */
+typedef struct cgpu_lb4_out {
+	int32_t *ret;
+	uint32_t *saddr, *daddr;
+	uint16_t *dport, *rev_nat, *slave;
+} cgpu_lb4_out;
+
+int cgpu_lb4_select(cgpu_ctx *ctx, int mode, const cgpu_lb4_tuples *t, size_t n,
+		    const cgpu_lb4_out *out, void *stream);
 
 /* XDP prefilter over pre-parsed packets (bpf_xdp.c:88-184).
  * flags: 0 IP packet of this family, 1 truncated (-> XDP_DROP),

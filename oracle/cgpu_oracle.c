@@ -606,6 +606,16 @@ int or_lb_update(or_ctx *c, const void *key8, const void *val12)
 	return oh_update(&c->lb, key8, val12);
 }
 
+int or_lb_update_many(or_ctx *c, const void *keys, const void *vals, size_t n)
+{
+	for (size_t i = 0; i < n; i++) {
+		int r = oh_update(&c->lb, (const uint8_t *)keys + 8 * i, (const uint8_t *)vals + 12 * i);
+		if (r)
+			return r;
+	}
+	return 0;
+}
+
 int or_lb_delete(or_ctx *c, const void *key8)
 {
 	return oh_delete(&c->lb, key8);

@@ -94,6 +94,7 @@ int or_prefilter_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *
  * raw struct lb4_key (8 B) -> struct lb4_service (12 B), bpf/lib/common.h:427-439.
  */
 int or_lb_update(or_ctx *c, const void *key8, const void *val12);
+int or_lb_update_many(or_ctx *c, const void *keys8, const void *vals12, size_t n);
 int or_lb_delete(or_ctx *c, const void *key8);
 /* kernel skb->hash stand-in used when no hash column is given (the kernel's
  * flow-dissector hash is unpinned); = cilium_amd.shard.flowhash_np */

@@ -63,6 +63,7 @@ def lib():
         L.or_prefilter_v6.argtypes = [vp, sz, vp, vp, vp, vp, C.c_int, C.POINTER(C.c_uint64)]
         L.or_lb_update.argtypes = [vp, vp, vp]
         L.or_lb_delete.argtypes = [vp, vp]
+        L.or_lb_update_many.argtypes = [vp, vp, vp, sz]
         L.or_flow_hash.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_uint8]
         L.or_flow_hash.restype = C.c_uint32
         L.or_lb4.argtypes = [vp, C.c_int, sz] + [vp] * 13 + [C.c_int, C.POINTER(C.c_uint64)]
@@ -192,6 +193,11 @@ class Oracle:
     # --- service load balancer ---
     def lb_update(self, key, val):
         return self.L.or_lb_update(self.h, _b(key), _b(val))
+
+    def lb_update_batch(self, keys, vals):
+        k, v = np.ascontiguousarray(keys), np.ascontiguousarray(vals)
+        assert k.itemsize == 8 and v.itemsize == 12 and len(k) == len(v)
+        return self.L.or_lb_update_many(self.h, _p(k), _p(v), len(k))
 
     def lb_delete(self, key):
         return self.L.or_lb_delete(self.h, _b(key))

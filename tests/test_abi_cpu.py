@@ -137,6 +137,53 @@ def test_cidr_and_endpoint_maps():
     assert e.endpoint_delete(ek) == 0 and e.endpoint_lookup(ek) == -errno.ENOENT
 
 
+def test_lb4_map_semantics():
+    """cilium_lb4_services through the C ABI: bpf(2) flags, capacity (E2BIG
+    like the kernel htab), exact lookup, GetNextKey order, and the lbmap
+    UpdateService / DeleteService write sequence (lbmap.go:350-428)."""
+    from cilium_amd.engine import LBMap
+    e = Engine(device=-1, lb_max_entries=8)
+    k = L.lb4_key("10.96.0.10", 80, 0)
+    assert e.lb4_update(k, L.lb4_service(0, 0, 2)) == 0
+    assert e.lb4_update(k, L.lb4_service(), BPF_NOEXIST) == -errno.EEXIST
+    assert e.lb4_update(L.lb4_key("10.96.0.11", 80, 0), L.lb4_service(), BPF_EXIST) == -errno.ENOENT
+    rc, v = e.lb4_lookup(k)
+    assert rc == 0 and int(v["count"]) == 2
+    # the slave number is part of the key
+    assert e.lb4_lookup(L.lb4_key("10.96.0.10", 80, 1))[0] == -errno.ENOENT
+    m = LBMap(e)
+    m.UpdateService("10.96.0.10", 80, [("10.1.0.1", 8080, 1), ("10.1.0.2", 8080, 0)], rev_nat=3)
+    assert e.lb4_count() == 3
+    bes = m.LookupService("10.96.0.10", 80)
+    assert [L.be_to_host4(int(b["target"])) for b in bes] == [0x0A010001, 0x0A010002]
+    assert int(e.lb4_lookup(k)[1]["weight"]) == L.htons(1)  # nNonZeroWeights, network order
+    m.UpdateService("10.96.0.10", 80, [("10.1.0.3", 0, 0)])  # shrink: slave 2 removed
+    assert e.lb4_count() == 2
+    m.UpdateService("10.96.0.20", 0, [("10.1.0.4", 0, 0)] * 5)
+    assert e.lb4_count() == 8
+    assert e.lb4_update(L.lb4_key("10.96.0.30", 0, 0), L.lb4_service()) == -errno.E2BIG
+    keys = e.lb4_keys()
+    assert len(keys) == 8 and len({bytes(k) for k in keys}) == 8
+    m.DeleteService("10.96.0.20", 0)
+    assert e.lb4_count() == 2
+    kk = np.array([L.lb4_key("10.96.1.1", 53, s) for s in range(3)], L.LB4_KEY)
+    vv = np.array([L.lb4_service("10.2.0.1", 53, 2)] * 3, L.LB4_SERVICE)
+    assert e.lb4_update_batch(kk, vv) == 0 and e.lb4_count() == 5
+    assert e.lb4_update_batch(kk, vv, BPF_NOEXIST) == -errno.EEXIST
+    assert e.lb4_delete(L.lb4_key("10.96.1.1", 53, 7)) == -errno.ENOENT
+    # the default flow hash equals the sharder's
+    from cilium_amd.shard import flowhash_np
+    a = [np.array([x], dt) for x, dt in ((0x0100000A, np.uint32), (0x0200000A, np.uint32),
+                                          (1234, np.uint16), (80, np.uint16), (6, np.uint8))]
+    assert e.flow_hash(*(int(x[0]) for x in a)) == int(flowhash_np(*a)[0])
+    # batch entry points have no CPU path
+    from cilium_amd._abi import Lb4Out, Lb4Tuples
+    assert lib().cgpu_lb4_select(e.h, 0, C.byref(Lb4Tuples()), 1, C.byref(Lb4Out()), None) == \
+        -errno.ENODEV
+    assert lib().cgpu_classify_v4_lb(e.h, C.byref(TuplesV4()), None, None, 1, None, None, None,
+                                     None) == -errno.ENODEV
+
+
 def test_bad_flags_and_abi_version():
     e = Engine(device=-1)
     assert e.policy_update(0, L.policy_key(1, 1, 6, 0), L.policy_entry(), 3) == -errno.EINVAL
