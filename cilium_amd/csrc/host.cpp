@@ -1332,9 +1332,227 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 	build_set16(keys, b.set);
 }
 
+/* ---- IPv6 any-match cover (tables.h cover6) ---- */
+struct Cover6Build {
+	std::vector<uint32_t> root, pool;
+	std::vector<std::array<uint32_t, 4>> h32;
+	std::vector<std::array<uint32_t, 8>> h64;
+	uint32_t m32 = 0, m64 = 0;
+	bool any = false;
+};
+
+struct P6 {
+	uint64_t hi, lo;
+	uint32_t len;
+	bool operator<(const P6 &o) const { return hi != o.hi ? hi < o.hi : lo < o.lo; }
+};
+
+/* sorted, merged (overlapping or adjacent) closed intervals */
+template <typename T> std::vector<std::pair<T, T>> merge_iv(std::vector<std::pair<T, T>> v)
+{
+	std::sort(v.begin(), v.end());
+	std::vector<std::pair<T, T>> out;
+	for (auto &x : v) {
+		if (!out.empty() && (x.first <= out.back().second ||
+				     (out.back().second != (T)~(T)0 && x.first == out.back().second + 1)))
+			out.back().second = std::max(out.back().second, x.second);
+		else
+			out.push_back(x);
+	}
+	return out;
+}
+
+/* node {nb, rest_deep, 0, 0} + boundaries: covered iff #(b <= x) is odd */
+uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uint32_t>> &iv, bool deep)
+{
+	std::vector<uint32_t> bnd;
+	for (auto &x : iv) {
+		bnd.push_back(x.first);
+		if (x.second != 0xFFFFFFFFu)
+			bnd.push_back(x.second + 1u);
+	}
+	const uint32_t off = (uint32_t)(b.pool.size() / 4);
+	b.pool.insert(b.pool.end(), {(uint32_t)bnd.size(), deep ? 1u : 0u, 0u, 0u});
+	b.pool.insert(b.pool.end(), bnd.begin(), bnd.end());
+	while (b.pool.size() % 4)
+		b.pool.push_back(0);
+	return COVER6_NODE << 30 | off;
+}
+
+uint32_t cover6_node64(Cover6Build &b, const std::vector<std::pair<uint64_t, uint64_t>> &iv)
+{
+	std::vector<uint64_t> bnd;
+	for (auto &x : iv) {
+		bnd.push_back(x.first);
+		if (x.second != ~0ull)
+			bnd.push_back(x.second + 1u);
+	}
+	const uint32_t off = (uint32_t)(b.pool.size() / 4);
+	b.pool.insert(b.pool.end(), {(uint32_t)bnd.size(), 0u, 0u, 0u});
+	for (uint64_t x : bnd) {
+		b.pool.push_back((uint32_t)(x >> 32));
+		b.pool.push_back((uint32_t)x);
+	}
+	while (b.pool.size() % 4)
+		b.pool.push_back(0);
+	return COVER6_NODE << 30 | off;
+}
+
+template <size_t W>
+void hop_place(std::vector<std::array<uint32_t, W>> &tab, uint32_t &mask,
+	       const std::vector<std::array<uint32_t, W>> &recs, uint32_t (*home_of)(const std::array<uint32_t, W> &))
+{
+	uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * recs.size()));
+	for (;;) {
+		tab.assign(nb, std::array<uint32_t, W>{});
+		mask = nb - 1;
+		bool ok = true;
+		for (auto &r : recs) {
+			const uint32_t home = home_of(r) & mask;
+			uint32_t d = 0;
+			while (d < POL_HOP && (tab[(home + d) & mask][3] & COVER6_USED))
+				d++;
+			if (d == POL_HOP) {
+				ok = false;
+				break;
+			}
+			auto &sl = tab[(home + d) & mask];
+			const uint32_t hop = sl[3] & ~0xFFFFFFu;
+			sl = r;
+			sl[3] = hop | COVER6_USED;
+			tab[home][3] |= 1u << (POL_HOP_SHIFT + d);
+		}
+		if (ok)
+			return;
+		nb *= 2;
+	}
+}
+
+uint32_t h32_home(const std::array<uint32_t, 4> &r) { return mix32(r[0], 0xC0E6u); }
+uint32_t h64_home(const std::array<uint32_t, 8> &r) { return mix32(r[0], r[1]); }
+
+/* Any-match cover of (len, address) prefixes, see tables.h cover6. */
+void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
+{
+	b.any = !cand.empty();
+	if (!b.any)
+		return;
+	std::vector<P6> ps;
+	ps.reserve(cand.size());
+	for (auto &c : cand) {
+		uint64_t hi = 0, lo = 0;
+		for (int i = 0; i < 8; i++) {
+			hi = hi << 8 | c.addr[i];
+			lo = lo << 8 | c.addr[8 + i];
+		}
+		ps.push_back(P6{hi, lo, c.len});
+	}
+	std::sort(ps.begin(), ps.end());
+	b.root.assign(65536, 0);
+	for (auto &p : ps)
+		if (p.len <= 16) {
+			const uint32_t cnt = 1u << (16 - p.len);
+			const uint32_t base = p.len == 0 ? 0 : ((uint32_t)(p.hi >> 48) & ~(cnt - 1));
+			std::fill(b.root.begin() + base, b.root.begin() + base + cnt, COVER6_FULL << 30);
+		}
+	std::vector<std::array<uint32_t, 4>> r32;
+	std::vector<std::array<uint32_t, 8>> r64;
+	size_t i = 0;
+	while (i < ps.size()) {
+		const uint32_t top16 = (uint32_t)(ps[i].hi >> 48);
+		size_t j = i;
+		while (j < ps.size() && (uint32_t)(ps[j].hi >> 48) == top16)
+			j++;
+		if ((b.root[top16] >> 30) == COVER6_FULL) {
+			i = j;
+			continue;
+		}
+		std::vector<std::pair<uint32_t, uint32_t>> s1;
+		bool deeper = false;
+		for (size_t k = i; k < j; k++) {
+			const P6 &p = ps[k];
+			if (p.len > 16 && p.len <= 32) {
+				const uint32_t st = (uint32_t)(p.hi >> 32) & 0xFFFFu;
+				s1.push_back({st, st + (1u << (32 - p.len)) - 1u});
+			} else if (p.len > 32) {
+				deeper = true;
+			}
+		}
+		if (s1.empty() && !deeper) {
+			i = j;
+			continue;
+		}
+		b.root[top16] = s1.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s1), deeper);
+		/* /32 groups of the deeper prefixes (sorted by hi: contiguous) */
+		size_t k = i;
+		while (k < j) {
+			if (ps[k].len <= 32) {
+				k++;
+				continue;
+			}
+			const uint32_t top32 = (uint32_t)(ps[k].hi >> 32);
+			size_t l = k;
+			std::vector<std::pair<uint32_t, uint32_t>> s2;
+			bool deeper2 = false;
+			size_t first64 = ps.size();
+			for (; l < j && (uint32_t)(ps[l].hi >> 32) == top32; l++) {
+				const P6 &p = ps[l];
+				if (p.len > 32 && p.len <= 64) {
+					const uint32_t st = (uint32_t)p.hi;
+					const uint32_t span = 64 - p.len;
+					s2.push_back({st, span == 32 ? 0xFFFFFFFFu : st + ((1u << span) - 1u)});
+				} else if (p.len > 64) {
+					deeper2 = true;
+					if (first64 == ps.size())
+						first64 = l;
+				}
+			}
+			const uint32_t e2 = s2.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s2), deeper2);
+			r32.push_back({top32, e2, 0u, 0u});
+			/* /64 groups */
+			size_t m = first64;
+			while (m < l) {
+				if (ps[m].len <= 64) {
+					m++;
+					continue;
+				}
+				const uint64_t top64 = ps[m].hi;
+				std::vector<std::pair<uint64_t, uint64_t>> s3;
+				size_t q = m;
+				for (; q < l && ps[q].hi == top64; q++) {
+					const P6 &p = ps[q];
+					if (p.len > 64) {
+						const uint32_t span = 128 - p.len;
+						s3.push_back({p.lo, span == 64 ? ~0ull : p.lo + ((1ull << span) - 1ull)});
+					}
+				}
+				auto iv = merge_iv(s3);
+				std::array<uint32_t, 8> r{(uint32_t)(top64 >> 32), (uint32_t)top64, 0u, 0u, 0u, 0u, 0u, 0u};
+				if (iv.size() == 1) {
+					r[2] = COVER6_FULL << 30; /* inline [lo, hi] */
+					r[4] = (uint32_t)(iv[0].first >> 32);
+					r[5] = (uint32_t)iv[0].first;
+					r[6] = (uint32_t)(iv[0].second >> 32);
+					r[7] = (uint32_t)iv[0].second;
+				} else {
+					r[2] = cover6_node64(b, iv);
+				}
+				r64.push_back(r);
+				m = q;
+			}
+			k = l;
+		}
+		i = j;
+	}
+	hop_place<4>(b.h32, b.m32, r32, h32_home);
+	hop_place<8>(b.h64, b.m64, r64, h64_home);
+	if (b.pool.empty())
+		b.pool.assign(4, 0);
+}
+
 /* prefilter v6 any-match set (bpf_xdp.c:132-156): dyn6 (if
  * CIDR6_LPM_PREFILTER) + fix6 keys with prefixlen 128. */
-void build_pf6(const cgpu_ctx *c, V6Build &b)
+void build_pf6(const cgpu_ctx *c, Cover6Build &b)
 {
 	std::vector<Rank6> cand;
 	if (c->cfg.prefilter_fix6) {
@@ -1351,7 +1569,7 @@ void build_pf6(const cgpu_ctx *c, V6Build &b)
 			cand.push_back(r);
 		}
 	}
-	build_v6(std::move(cand), b);
+	build_cover6(cand, b);
 }
 
 /* ipcache -> v6 LPM for IPv6 lookups (ipcache_lookup6, eps.h:56-66): a
@@ -1462,7 +1680,8 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	PolBuild pol;
 	Set4Build ep4;
 	Set16Build ep6;
-	V6Build pf6, ipc6;
+	V6Build ipc6;
+	Cover6Build pf6;
 	build_ipc4(c, ipc4);
 	build_ipc6(c, ipc6);
 	bool have_pf4 = build_pf4(c, pf4);
@@ -1507,7 +1726,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	size_t o_e6 = ar.add(ep6.slots.data(), ep6.slots.size() * sizeof(set16_slot));
 	struct V6Offs {
 		size_t root = 0, masks = 0, vals = 0, set = 0;
-	} o_pf6, o_ipc6;
+	} o_ipc6;
 	auto add_v6 = [&](V6Build &v, V6Offs &o) {
 		if (!v.any)
 			return;
@@ -1516,7 +1735,13 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 		o.vals = ar.add(v.vals.data(), v.vals.size() * 4);
 		o.set = ar.add(v.set.slots.data(), v.set.slots.size() * sizeof(set16_slot));
 	};
-	add_v6(pf6, o_pf6);
+	size_t o_c6r = 0, o_c6p = 0, o_c632 = 0, o_c664 = 0;
+	if (pf6.any) {
+		o_c6r = ar.add(pf6.root.data(), pf6.root.size() * 4);
+		o_c6p = ar.add(pf6.pool.data(), pf6.pool.size() * 4);
+		o_c632 = ar.add(pf6.h32.data(), pf6.h32.size() * 16);
+		o_c664 = ar.add(pf6.h64.data(), pf6.h64.size() * 32);
+	}
 	add_v6(ipc6, o_ipc6);
 	/* a slot freed and reused before this commit has several inits queued:
 	 * only the most recent one may reach the device (the init kernel writes
@@ -1588,7 +1813,9 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 				   (uint32_t)(v.masks.size() / 4)};
 		return t;
 	};
-	s.pf6 = mk_v6(pf6, o_pf6);
+	if (pf6.any)
+		s.pf6 = cover6{(const uint32_t *)(arena + o_c6r), (const uint32_t *)(arena + o_c6p),
+			       (const uint4 *)(arena + o_c632), (const uint4 *)(arena + o_c664), pf6.m32, pf6.m64};
 	s.ipc6 = mk_v6(ipc6, o_ipc6);
 	memcpy(s.router_ip64, c->cfg.ipv6_router_ip, 8);
 	s.pf4_enabled = c->cfg.prefilter_fix4;

@@ -465,6 +465,126 @@ template <int MODE> __global__ __launch_bounds__(BLOCK) void k_lb4(cgpu_snapshot
 	}
 }
 
+/* ---- IPv6 any-match cover (tables.h cover6) ---- */
+
+/* covered iff #(boundaries <= x) is odd; *deep = node's rest_deep */
+__device__ __forceinline__ bool c6_node32(const uint32_t *pool, uint32_t off, uint32_t x, bool *deep)
+{
+	const uint4 *nd = reinterpret_cast<const uint4 *>(pool) + off;
+	const uint4 h = nd[0];
+	const uint32_t nb = h.x;
+	*deep = h.y != 0;
+	uint32_t cnt = 0;
+	for (uint32_t k = 0; k < nb; k += 16) {
+		uint4 q[4];
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++)
+			q[j] = k + 4 * j < nb ? nd[1 + k / 4 + j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++) {
+			const uint32_t i = k + 4 * j;
+			cnt += (i < nb && q[j].x <= x ? 1u : 0u) + (i + 1 < nb && q[j].y <= x ? 1u : 0u) +
+			       (i + 2 < nb && q[j].z <= x ? 1u : 0u) + (i + 3 < nb && q[j].w <= x ? 1u : 0u);
+		}
+	}
+	return cnt & 1u;
+}
+
+__device__ __forceinline__ bool le64(uint32_t ah, uint32_t al, uint32_t bh, uint32_t bl)
+{
+	return ah < bh || (ah == bh && al <= bl);
+}
+
+__device__ __forceinline__ bool c6_node64(const uint32_t *pool, uint32_t off, uint32_t xh, uint32_t xl)
+{
+	const uint4 *nd = reinterpret_cast<const uint4 *>(pool) + off;
+	const uint32_t nb = nd[0].x;
+	uint32_t cnt = 0;
+	for (uint32_t k = 0; k < nb; k += 8) {
+		uint4 q[4];
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++)
+			q[j] = k + 2 * j < nb ? nd[1 + k / 2 + j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++) {
+			const uint32_t i = k + 2 * j;
+			cnt += (i < nb && le64(q[j].x, q[j].y, xh, xl) ? 1u : 0u) +
+			       (i + 1 < nb && le64(q[j].z, q[j].w, xh, xl) ? 1u : 0u);
+		}
+	}
+	return cnt & 1u;
+}
+
+/* does any prefix of the cover contain the (network-order) address a */
+__device__ __forceinline__ bool cover6_any(const cover6 &t, uint4 a)
+{
+	if (!t.root)
+		return false;
+	const uint32_t w0 = bswap32(a.x), w1 = bswap32(a.y), w2 = bswap32(a.z), w3 = bswap32(a.w);
+	bool hit = false, deep = false;
+	/* /16 */
+	uint32_t e = t.root[w0 >> 16];
+	uint32_t tag = e >> 30;
+	if (tag == COVER6_NODE) {
+		hit = c6_node32(t.pool, e & 0x3FFFFFFFu, w0 & 0xFFFFu, &deep);
+		tag = !hit && deep ? COVER6_DEEP : COVER6_NONE;
+	} else if (tag == COVER6_FULL) {
+		hit = true;
+	}
+	/* /32 */
+	if (tag == COVER6_DEEP) {
+		const uint32_t home = mix32(w0, 0xC0E6u) & t.m32;
+		const uint4 s = t.h32[home];
+		uint32_t hop = s.w >> POL_HOP_SHIFT;
+		uint4 r = make_uint4(0, 0, 0, 0);
+		if ((hop & 1u) && s.x == w0)
+			r = s;
+		hop &= ~1u;
+		while (hop && !r.w) {
+			const uint32_t j = __builtin_ctz(hop);
+			hop &= hop - 1u;
+			const uint4 x = t.h32[(home + j) & t.m32];
+			if (x.x == w0)
+				r = x;
+		}
+		tag = r.w ? (r.y >> 30) : COVER6_NONE;
+		e = r.y;
+		if (tag == COVER6_NODE) {
+			hit = c6_node32(t.pool, e & 0x3FFFFFFFu, w1, &deep);
+			tag = !hit && deep ? COVER6_DEEP : COVER6_NONE;
+		} else if (tag == COVER6_FULL) {
+			hit = true;
+		}
+	}
+	/* /64 */
+	if (tag == COVER6_DEEP) {
+		const uint32_t home = mix32(w0, w1) & t.m64;
+		uint4 s0 = t.h64[2u * home], s1 = t.h64[2u * home + 1u];
+		uint32_t hop = s0.w >> POL_HOP_SHIFT;
+		bool found = (hop & 1u) && s0.x == w0 && s0.y == w1;
+		hop &= ~1u;
+		while (hop && !found) {
+			const uint32_t j = __builtin_ctz(hop);
+			hop &= hop - 1u;
+			const uint32_t sl = (home + j) & t.m64;
+			const uint4 x = t.h64[2u * sl];
+			if (x.x == w0 && x.y == w1) {
+				s0 = x;
+				s1 = t.h64[2u * sl + 1u];
+				found = true;
+			}
+		}
+		if (found) {
+			tag = s0.z >> 30;
+			if (tag == COVER6_FULL)
+				hit = le64(s1.x, s1.y, w2, w3) && le64(w2, w3, s1.z, s1.w);
+			else if (tag == COVER6_NODE)
+				hit = c6_node64(t.pool, s0.z & 0x3FFFFFFFu, w2, w3);
+		}
+	}
+	return hit;
+}
+
 __device__ __forceinline__ uint32_t entry_label(const uint32_t *vals, uint32_t e)
 {
 	uint32_t p = e & DIR_PAYLOAD_MASK;
@@ -1161,7 +1281,7 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v6(cgpu_snapshot s, prefilt
 		} else if (f != 0u) {
 			v = XDP_DROP;
 		} else {
-			const bool drop = s.pf6_enabled && v6_lookup(s.pf6, sa) != 0;
+			const bool drop = s.pf6_enabled && cover6_any(s.pf6, sa);
 			v = drop ? XDP_DROP : (set16_has(s.ep6, da, 0u) ? XDP_PASS : XDP_DROP);
 		}
 		a.verdict[i] = v;

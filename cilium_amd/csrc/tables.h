@@ -230,6 +230,38 @@ static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t da
 	return h;
 }
 
+/* ---- IPv6 any-match cover (XDP prefilter v6) ----
+ * The prefilter only asks "does ANY deny prefix cover saddr" (bpf_xdp.c:
+ * 142-152: both the dyn LPM and the fix /128 hash lead to XDP_DROP), so the
+ * union of the prefixes is compiled into covered intervals at strides
+ * 16 / 32 / 64 / 128 bits:
+ *   root[top16]: entry (below) for the /16;
+ *   h32: hop-hashed 16-B slots {top32, entry, 0, used | hop << 24} for the
+ *        /32s holding prefixes longer than /32;
+ *   h64: hop-hashed 32-B slots {top64.hi, top64.lo, entry, used | hop << 24,
+ *        lo.hi, lo.lo, hi.hi, hi.lo} for the /64s holding prefixes longer
+ *        than /64 (an INLINE entry covers [lo, hi] of the low 64 bits).
+ * entry: tag << 30 | payload, tag COVER6_NONE / _FULL / _DEEP (consult the
+ * next level) / _NODE (payload = offset in 16-B units into `pool`).
+ * A node is {nb, rest_deep, 0, 0} + nb sorted boundaries (u32 at levels
+ * 16/32, u64 as {hi, lo} at level 64) of merged covered intervals: an address
+ * is covered iff #(boundaries <= x) is odd; otherwise it descends when
+ * rest_deep is set.  Typical config-3 packet: root (L2) + h32 slot (L2) +
+ * one node (2 lines) + at most one h64 slot. */
+#define COVER6_NONE 0u
+#define COVER6_FULL 1u
+#define COVER6_DEEP 2u
+#define COVER6_NODE 3u
+#define COVER6_USED (1u << 16)
+
+typedef struct cover6 {
+	const uint32_t *root; /* 65536 entries; NULL = empty set */
+	const uint32_t *pool; /* 16-B aligned nodes */
+	const uint4 *h32;     /* m32 + 1 slots */
+	const uint4 *h64;     /* (m64 + 1) x 2 uint4 */
+	uint32_t m32, m64;
+} cover6;
+
 /* ---- one committed snapshot ---- */
 typedef struct cgpu_snapshot {
 	dir248 ipc4;
@@ -238,7 +270,7 @@ typedef struct cgpu_snapshot {
 	dir248 pf4;      /* any-match: dyn4 (if enabled) + fix4 /32 */
 	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
 	addr_set16 ep6;  /* cilium_lxc IPv6 keys */
-	v6_lpm pf6;      /* any-match: dyn6 (if enabled) + fix6 /128 */
+	cover6 pf6;      /* any-match: dyn6 (if enabled) + fix6 /128 */
 	v6_lpm ipc6;     /* ipcache, IPv6 lookups */
 	uint32_t pf4_enabled; /* CIDR4_FILTER */
 	uint32_t pf6_enabled; /* CIDR6_FILTER */

@@ -540,3 +540,66 @@ def test_lpm_shapes_exact(torch_cuda, variant, monkeypatch):
     np.testing.assert_array_equal(st, s0)
     assert len(np.unique(i0)) > 1000
     e.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_prefilter6_cover_shapes(torch_cuda, seed):
+    """The v6 any-match cover (tables.h cover6) over every prefix-length class
+    and stride boundary: /0../16 (root fill), /17../32 (root node), /33../64
+    (/32 node), /65../128 (/64 node or inline), nested and overlapping
+    prefixes, all-ones boundaries; addresses drawn at and around the edges of
+    every prefix.  Bit-exact against the restatement's kernel-like LPM trie."""
+    from oracle import Oracle
+    torch = torch_cuda
+    rng = np.random.default_rng(100 + seed)
+    roots = rng.integers(0, 256, (6, 2), dtype=np.uint8)
+    lens = [0, 1, 8, 15, 16, 17, 20, 31, 32, 33, 40, 48, 63, 64, 65, 80, 96, 112, 127, 128]
+    keys = []
+    for i in range(3000):
+        k = np.zeros((), L.LPM_V6_KEY)
+        ln = int(rng.choice(lens[5:])) if i > 3 else [0, 8, 16, 1][i] if seed == 3 else 17
+        a = rng.integers(0, 256, 16, dtype=np.uint8)
+        a[:2] = roots[rng.integers(0, len(roots))]
+        if rng.random() < 0.2:
+            a[2:] = 0xFF
+        k["prefixlen"] = ln
+        k["addr"][:] = a
+        keys.append(k)
+    keys = np.array(keys, L.LPM_V6_KEY)
+    n = 200_000
+    base = keys["addr"][rng.integers(0, len(keys), n)].copy()
+    bits = np.unpackbits(base, axis=1)
+    cut = rng.integers(0, 129, n)
+    noise = np.unpackbits(rng.integers(0, 256, (n, 16), dtype=np.uint8), axis=1)
+    mode = rng.integers(0, 3, n)  # 0: random below the cut, 1: all zeros, 2: all ones
+    below = np.arange(128)[None, :] >= cut[:, None]
+    fill = np.where(mode[:, None] == 0, noise, np.where(mode[:, None] == 1, 0, 1)).astype(np.uint8)
+    bits = np.where(below, fill, bits)
+    s6 = np.packbits(bits, axis=1)
+    s6[: n // 20] = rng.integers(0, 256, (n // 20, 16), dtype=np.uint8)
+    eps = rng.integers(0, 256, (16, 16), dtype=np.uint8)
+    d6 = eps[rng.integers(0, len(eps), n)]  # uncovered sources then PASS
+    flags = np.zeros(n, np.uint8)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    for dyn_on in (1, 0):
+        e = _engine(prefilter_dyn6=dyn_on)
+        o = Oracle(dyn6=dyn_on)
+        for a in eps:
+            ek = np.zeros((), L.ENDPOINT_KEY)
+            ek["ip"][:] = a
+            ek["family"] = L.ENDPOINT_KEY_IPV6
+            assert e.endpoint_update(ek) == 0 and o.endpoint_update(ek) == 0
+        for k in keys:
+            assert e.cidr_update(2, k) == 0 and o.cidr_update(2, k) == 0
+            if int(k["prefixlen"]) == 128:
+                assert e.cidr_update(3, k) == 0 and o.cidr_update(3, k) == 0
+        e.commit()
+        g = e.prefilter_v6(dev(s6), dev(d6), dev(flags))
+        torch.cuda.synchronize()
+        r, _ = o.prefilter_v6(s6, d6, flags, nthreads=8)
+        np.testing.assert_array_equal(_np(g), r)
+        if dyn_on and seed != 3:
+            assert 0.1 < (r == L.XDP_DROP).mean() < 0.99
+        elif dyn_on:
+            assert (r == L.XDP_DROP).all()  # the /0 deny prefix covers everything
+        e.close()
