@@ -1288,6 +1288,241 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v6(cgpu_snapshot s, prefilt
 	}
 }
 
+/*
+ * XDP prefilter IPv6, Q packets per lane with the cover lookup advanced
+ * stage by stage across them (root, /32 record, interval node in chunks of
+ * 12 / 16 / 16 boundaries, /64 record, endpoint bucket), so each stage has Q
+ * independent gathers in flight per lane.  Same decisions as k_prefilter_v6
+ * (bpf/bpf_xdp.c:132-156 then check_v6_endpoint :123-130).
+ */
+__device__ __forceinline__ uint32_t c6_count4(uint4 q, uint32_t base, uint32_t nb, uint32_t x)
+{
+	return (base < nb && q.x <= x ? 1u : 0u) + (base + 1 < nb && q.y <= x ? 1u : 0u) +
+	       (base + 2 < nb && q.z <= x ? 1u : 0u) + (base + 3 < nb && q.w <= x ? 1u : 0u);
+}
+
+template <int Q>
+__device__ __forceinline__ void c6_node32_q(const uint32_t *pool, const uint32_t (&e)[Q], const uint32_t (&x)[Q],
+					    uint32_t (&tag)[Q], bool (&hit)[Q])
+{
+	const uint4 *P = reinterpret_cast<const uint4 *>(pool);
+	uint4 q[Q][4];
+	uint32_t cnt[Q], nb[Q];
+	bool deep[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		cnt[u] = 0;
+		nb[u] = 0;
+#pragma unroll
+		for (int j = 0; j < 4; j++)
+			q[u][j] = tag[u] == COVER6_NODE ? P[(e[u] & 0x3FFFFFFFu) + j] : make_uint4(0, 0, 0, 0);
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		nb[u] = q[u][0].x;
+		deep[u] = q[u][0].y != 0;
+#pragma unroll
+		for (int j = 1; j < 4; j++)
+			cnt[u] += c6_count4(q[u][j], 4u * (j - 1), nb[u], x[u]);
+	}
+	/* boundaries 12..27 of every node at once */
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+#pragma unroll
+		for (int j = 0; j < 4; j++)
+			q[u][j] = (tag[u] == COVER6_NODE && nb[u] > 12u + 4u * j)
+					  ? P[(e[u] & 0x3FFFFFFFu) + 4 + j]
+					  : make_uint4(0, 0, 0, 0);
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+#pragma unroll
+		for (int j = 0; j < 4; j++)
+			cnt[u] += c6_count4(q[u][j], 12u + 4u * j, nb[u], x[u]);
+		/* rare long nodes: the rest one chunk at a time */
+		for (uint32_t k = 28; k < nb[u]; k += 4) {
+			const uint4 r = P[(e[u] & 0x3FFFFFFFu) + 1 + k / 4];
+			cnt[u] += c6_count4(r, k, nb[u], x[u]);
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (tag[u] != COVER6_NODE)
+			continue;
+		hit[u] = cnt[u] & 1u;
+		tag[u] = !hit[u] && deep[u] ? COVER6_DEEP : COVER6_NONE;
+	}
+}
+
+/* set16_has whose first bucket is already loaded (tag 0: exact keys) */
+__device__ __forceinline__ bool set16_has_first(const addr_set16 &t, const uint4 (&first)[4], uint32_t b, uint4 key)
+{
+	uint4 k0 = first[0], m0 = first[1], k1 = first[2], m1 = first[3];
+	bool res = false, done = false;
+	for (uint32_t p = 0; !done;) {
+		if (!(m0.x & 1u)) {
+			done = true;
+		} else if (m0.x == 1u && k0.x == key.x && k0.y == key.y && k0.z == key.z && k0.w == key.w) {
+			res = done = true;
+		} else if (!(m1.x & 1u)) {
+			done = true;
+		} else if (m1.x == 1u && k1.x == key.x && k1.y == key.y && k1.z == key.z && k1.w == key.w) {
+			res = done = true;
+		} else if (++p >= t.max_probe) {
+			done = true;
+		} else {
+			b = (b + 1) & t.bucket_mask;
+			const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
+			k0 = bk[0];
+			m0 = bk[1];
+			k1 = bk[2];
+			m1 = bk[3];
+		}
+	}
+	return res;
+}
+
+template <int Q>
+__device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q], const bool (&act)[Q], bool (&hit)[Q])
+{
+	uint32_t w0[Q], w1[Q], w2[Q], w3[Q], e[Q], tag[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		w0[u] = bswap32(a[u].x);
+		w1[u] = bswap32(a[u].y);
+		w2[u] = bswap32(a[u].z);
+		w3[u] = bswap32(a[u].w);
+		hit[u] = false;
+		e[u] = act[u] && t.root ? t.root[w0[u] >> 16] : 0u;
+	}
+	/* /16: a node there is rare (prefixes of 17..32 bits) */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		tag[u] = e[u] >> 30;
+		hit[u] = tag[u] == COVER6_FULL;
+		if (tag[u] == COVER6_NODE) {
+			bool deep;
+			hit[u] = c6_node32(t.pool, e[u] & 0x3FFFFFFFu, w0[u] & 0xFFFFu, &deep);
+			tag[u] = !hit[u] && deep ? COVER6_DEEP : COVER6_NONE;
+		}
+	}
+	/* /32 records */
+	uint4 sl[Q];
+	uint32_t home[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		home[u] = mix32(w0[u], 0xC0E6u) & t.m32;
+		sl[u] = tag[u] == COVER6_DEEP ? t.h32[home[u]] : make_uint4(0, 0, 0, 0);
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (tag[u] != COVER6_DEEP)
+			continue;
+		uint32_t hop = sl[u].w >> POL_HOP_SHIFT;
+		uint4 r = make_uint4(0, 0, 0, 0);
+		if ((hop & 1u) && sl[u].x == w0[u])
+			r = sl[u];
+		hop &= ~1u;
+		while (hop && !r.w) {
+			const uint32_t j = __builtin_ctz(hop);
+			hop &= hop - 1u;
+			const uint4 x = t.h32[(home[u] + j) & t.m32];
+			if (x.x == w0[u])
+				r = x;
+		}
+		e[u] = r.y;
+		tag[u] = r.w ? (r.y >> 30) : COVER6_NONE;
+		hit[u] = tag[u] == COVER6_FULL;
+	}
+	c6_node32_q<Q>(t.pool, e, w1, tag, hit);
+	/* /64 records */
+	uint4 s0[Q], s1[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		home[u] = mix32(w0[u], w1[u]) & t.m64;
+		s0[u] = s1[u] = make_uint4(0, 0, 0, 0);
+		if (tag[u] == COVER6_DEEP) {
+			s0[u] = t.h64[2u * home[u]];
+			s1[u] = t.h64[2u * home[u] + 1u];
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (tag[u] != COVER6_DEEP)
+			continue;
+		uint32_t hop = s0[u].w >> POL_HOP_SHIFT;
+		bool found = (hop & 1u) && s0[u].x == w0[u] && s0[u].y == w1[u];
+		hop &= ~1u;
+		while (hop && !found) {
+			const uint32_t j = __builtin_ctz(hop);
+			hop &= hop - 1u;
+			const uint32_t k = (home[u] + j) & t.m64;
+			const uint4 x = t.h64[2u * k];
+			if (x.x == w0[u] && x.y == w1[u]) {
+				s0[u] = x;
+				s1[u] = t.h64[2u * k + 1u];
+				found = true;
+			}
+		}
+		if (found) {
+			const uint32_t tg = s0[u].z >> 30;
+			if (tg == COVER6_FULL)
+				hit[u] = le64(s1[u].x, s1[u].y, w2[u], w3[u]) && le64(w2[u], w3[u], s1[u].z, s1[u].w);
+			else if (tg == COVER6_NODE)
+				hit[u] = c6_node64(t.pool, s0[u].z & 0x3FFFFFFFu, w2[u], w3[u]);
+		}
+	}
+}
+
+template <int Q> __global__ __launch_bounds__(256) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a)
+{
+	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
+	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
+	const uint64_t T = (uint64_t)gridDim.x * 256;
+	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g * Q < a.n; g += T) {
+		const uint64_t i0 = g * Q;
+		uint4 sa[Q], da[Q];
+		uint32_t f[Q];
+		bool act[Q], hit[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = i0 + u < a.n ? i0 + u : a.n - 1;
+			const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(sa16 + i));
+			const v4u_t y = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(da16 + i));
+			sa[u] = make_uint4(x.x, x.y, x.z, x.w);
+			da[u] = make_uint4(y.x, y.y, y.z, y.w);
+			f[u] = a.flags[i];
+			act[u] = i0 + u < a.n && f[u] == 0u && s.pf6_enabled;
+		}
+		cover6_any_q<Q>(s.pf6, sa, act, hit);
+		/* check_v6_endpoint: cilium_lxc on daddr (bucket loads for all first) */
+		uint4 bk[Q][4];
+		uint32_t b[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			b[u] = hash16(da[u].x, da[u].y, da[u].z, da[u].w, 0u) & s.ep6.bucket_mask;
+			const bool need = i0 + u < a.n && f[u] == 0u && !hit[u];
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				bk[u][k] = need ? reinterpret_cast<const uint4 *>(s.ep6.slots)[(size_t)b[u] * 4u + k]
+						: make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (i0 + u >= a.n)
+				continue;
+			uint8_t v;
+			if (f[u] == 2u) {
+				v = XDP_PASS;
+			} else if (f[u] != 0u || hit[u]) {
+				v = XDP_DROP;
+			} else {
+				v = set16_has_first(s.ep6, bk[u], b[u], da[u]) ? XDP_PASS : XDP_DROP;
+			}
+			a.verdict[i0 + u] = v;
+		}
+	}
+}
+
 __global__ void k_fold(uint64_t *totals, uint64_t *delta, uint64_t n)
 {
 	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -1510,7 +1745,15 @@ hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, 
 
 hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)
 {
-	hipLaunchKernelGGL(k_prefilter_v6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	/* CGPU_PF6_Q: packets per lane (1 = k_prefilter_v6; default 4) */
+	const char *qs = getenv("CGPU_PF6_Q");
+	const int q = qs ? atoi(qs) : 4;
+	if (q == 2)
+		hipLaunchKernelGGL(k_prefilter_v6_q<2>, dim3(grid_for((a.n + 1) / 2)), dim3(BLOCK), 0, st, s, a);
+	else if (q == 4)
+		hipLaunchKernelGGL(k_prefilter_v6_q<4>, dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
+	else
+		hipLaunchKernelGGL(k_prefilter_v6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 	return hipGetLastError();
 }
 
