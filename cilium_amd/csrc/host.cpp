@@ -1830,7 +1830,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.ingress_secctx_world = c->cfg.ingress_secctx_world;
 	s.ingress_src_identity = c->cfg.ingress_src_identity;
 	s.n_ctr_slots = c->n_ctr_slots;
-	s.hot_slots = c->hot_cap;
+	s.hot_slots = c->next_hot; /* LDS per workgroup: only the hot slots in use */
 	s.cold_hi = c->next_cold;
 	s.slot_dir = (const uint8_t *)(arena + o_sd);
 	s.lb = lb_table{(const uint4 *)(arena + o_lfe), (const uint4 *)(arena + o_lbe), lbb.mask,

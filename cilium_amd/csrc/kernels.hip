@@ -13,6 +13,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #define DROP_POLICY (-133)           /* bpf/lib/common.h:240 */
 #define DROP_CT_UNKNOWN_PROTO (-137) /* bpf/lib/common.h:244 */
@@ -1158,7 +1161,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				} else if (c < s.hot_slots) {
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
-				} else {
+				} else if (CM != 3) { /* CM 3: diagnostic, cold counters skipped */
 					atomicAdd((unsigned long long *)&pk[c],
 						  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
 				}
@@ -1577,24 +1580,27 @@ static bool x4_aligned(const cls_args &a)
 	return !(a16 & 15) && !(a8 & 7) && !(a4 & 3);
 }
 
-/* Workgroups of NT threads that k_classify_v4_x4 keeps resident on the
- * device (CUs x occupancy), queried once per device. */
-template <int CM> static unsigned x4_resident_blocks(int NT, size_t lds)
+/* Workgroups of NT threads of kernel `kern` that stay resident on the
+ * current device with `lds` bytes of dynamic LDS (CUs x occupancy); cached
+ * per (device, kernel, lds). */
+static unsigned resident_blocks(const void *kern, int NT, size_t lds)
 {
-	static unsigned cached[64];
+	static std::mutex mu;
+	static std::map<std::tuple<int, const void *, size_t>, unsigned> cache;
 	int dev = 0;
 	(void)hipGetDevice(&dev);
-	if (dev >= 0 && dev < 64 && cached[dev])
-		return cached[dev];
+	std::lock_guard<std::mutex> g(mu);
+	auto key = std::make_tuple(dev, kern, lds);
+	auto it = cache.find(key);
+	if (it != cache.end())
+		return it->second;
 	int cus = 0, per_cu = 0;
 	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
 		cus = 256;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_classify_v4_x4<1024, CM, 2, true>, NT, lds) !=
-		    hipSuccess || per_cu <= 0)
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, lds) != hipSuccess || per_cu <= 0)
 		per_cu = 1;
 	const unsigned r = (unsigned)(cus * per_cu);
-	if (dev >= 0 && dev < 64)
-		cached[dev] = r;
+	cache[key] = r;
 	return r;
 }
 
@@ -1606,7 +1612,12 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 	constexpr int NT = 1024;
 	const size_t lds = (size_t)s.hot_slots * 8u;
 	const size_t lds2 = lds + (size_t)s.ipc4c.n_dict * 4u; /* + LDS leaf dictionary */
-	const unsigned res = var == 12 ? x4_resident_blocks<2>(NT, lds2) : x4_resident_blocks<0>(NT, lds2);
+	const void *kern = a.lb ? (const void *)k_classify_v4_x4<NT, 0, 2, true, 4, 1, true>
+			   : var == 12 ? (const void *)k_classify_v4_x4<NT, 2, 2, true>
+			   : var == 13 ? (const void *)k_classify_v4_x4<NT, 3, 2, true>
+			   : var == 15 ? (const void *)k_classify_v4_x4<NT, 0, 0, true>
+				       : (const void *)k_classify_v4_x4<NT, 0, 2, true>;
+	const unsigned res = resident_blocks(kern, NT, var == 15 ? lds : lds2);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
 	for (uint64_t off = 0; off < a.n; off += chunk) {
@@ -1634,6 +1645,8 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 					   c, a.pk);
 		else if (var == 12)
 			hipLaunchKernelGGL((k_classify_v4_x4<NT, 2, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
+		else if (var == 13)
+			hipLaunchKernelGGL((k_classify_v4_x4<NT, 3, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
 		else if (var == 15)
 			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0, true>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		else
@@ -1681,7 +1694,7 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 0>), dim3(g), dim3(1024), 0, st, s, a);
 		return hipGetLastError();
 	}
-	if (!V6 && (var == 8 || var == 12 || var == 15) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
+	if (!V6 && (var == 8 || var == 12 || var == 13 || var == 15) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
 		return launch_x4(s, a, st, var);
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
