@@ -17,6 +17,9 @@ Other BASELINE configs (not the headline line; run them explicitly):
                      egress service step of bpf_lxc.c:444-469 fused into the
                      classify kernel, cgpu_classify_v4_lb)
   --config pf6       config 3: XDP IPv6 prefilter over 1M deny prefixes
+  --config frames    config 2 tables, the batch as raw Ethernet frames in
+                     64-byte ring slots (cgpu_classify_frames: header parse
+                     of bpf_lxc.c / conntrack.h fused with the classify)
   --config cpu       config 1 sizes
 """
 from __future__ import annotations
@@ -34,6 +37,8 @@ METRIC = "Mpps classified (LPM ipcache + policy map) at 1/2/4/8 GPUs; % HBM roof
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 B_IN, B_OUT = 18, 8    # v4 classify tuple bytes in / out
 B_IN_PF6, B_OUT_PF6 = 33, 1  # v6 prefilter
+FRAME_STRIDE = 64      # --config frames: ring slot bytes (Ethernet + IPv4 + TCP fit)
+B_IN_FRAMES = FRAME_STRIDE + 4 + 1 + 2  # slot + len + flags + ep
 
 
 def log(*a):
@@ -49,6 +54,9 @@ WORKLOADS = {
                "64M-tuple batches per GPU, bit-exact verdicts",
     "pf6": "config3: XDP IPv6 prefilter, 1M deny prefixes (/32..../128, /128 in fix) under 256 "
            "/24 roots + 4k endpoints, 64M packets per GPU",
+    "frames": "config2 tables, 64M raw Ethernet/IPv4/TCP|UDP frames per GPU in 64-byte slots: "
+              "header parse (revalidate, ihl, frag, ct_lookup4 ports) fused with ipcache + policy, "
+              "bit-exact verdicts",
 }
 
 
@@ -82,7 +90,8 @@ def main():
 
     pf6 = args.config == "pf6"
     cascade = args.config == "cascade"
-    cfg = synth.CONFIGS["gpu" if pf6 else args.config]
+    frames = args.config == "frames"
+    cfg = synth.CONFIGS["gpu" if (pf6 or frames) else args.config]
     n = args.tuples or cfg["n_tuples"]
     t0 = time.time()
     S = None
@@ -116,6 +125,11 @@ def main():
     if pf6:
         d = synth.packets6_to_device(tup, dev)
         out = {"verdict": torch.empty(n, dtype=torch.uint8, device=dev)}
+    elif frames:
+        fr = synth.frames_from_tuples(tup, stride=FRAME_STRIDE)
+        d = synth.frames_to_device(fr, dev)
+        out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+               "identity": torch.empty(n, dtype=torch.int32, device=dev), "stage": None}
     else:
         d = synth.to_device(tup, dev)
         out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
@@ -131,6 +145,8 @@ def main():
             e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
         elif cascade:
             e.classify_v4_lb(d, out=out, stream=stream)
+        elif frames:
+            e.classify_frames(d, out=out, stream=stream)
         else:
             e.classify_v4(d, out=out, stream=stream)
         if ev is not None:
@@ -184,18 +200,32 @@ def main():
             synth.load_oracle(o, T)
             if S is not None:
                 synth.load_services(o, S)
+        def cpu_run(sl):
+            if pf6:
+                return o.prefilter_v6(tup["saddr"][sl], tup["daddr"][sl], tup["flags"][sl],
+                                      nthreads=threads)
+            if cascade:
+                return o.classify_v4_lb({k: v[sl] for k, v in tup.items()}, nthreads=threads)
+            if frames:
+                return o.classify_frames({k: v[sl] for k, v in fr.items()}, nthreads=threads)
+            return o.classify_v4({k: v[sl] for k, v in tup.items()}, nthreads=threads)
+
+        cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
         c0 = time.perf_counter()
         if pf6:
             v0, probes = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
         elif cascade:
             v0, i0, _, probes = o.classify_v4_lb(tup, nthreads=threads)
+        elif frames:
+            v0, i0, _, probes = o.classify_frames(fr, nthreads=threads)
         else:
             v0, i0, _, probes = o.classify_v4(tup, nthreads=threads)
         c_el = time.perf_counter() - c0
         cpu = None
         if not args.no_cpu_baseline:
             what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
-                    "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash"}.get(
+                    "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash",
+                    "frames": "oracle/cgpu_oracle.c frame parse + LPM trie + open hash"}.get(
                 args.config, "oracle/cgpu_oracle.c (kernel-like LPM trie + open hash)")
             cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
                    "kind": "port",
@@ -205,7 +235,8 @@ def main():
         if not pf6:
             parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
         probes_per = probes / n
-        b_in, b_out = (B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN + (2 if cascade else 0), B_OUT)
+        b_in, b_out = ((B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN_FRAMES, B_OUT) if frames
+                       else (B_IN + (2 if cascade else 0), B_OUT))
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
         traffic = None

@@ -32,7 +32,8 @@ class CgpuConfig(C.Structure):
         ("hot_counter_slots", C.c_uint32),
         ("lb_max_entries", C.c_uint32), ("ipv4_loopback", C.c_uint32),
         ("lb_flags", C.c_uint32),
-        ("reserved", C.c_uint32 * 4),
+        ("node_mac", C.c_uint8 * 6), ("reserved1", C.c_uint8 * 2),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -52,6 +53,16 @@ class Lb4Tuples(C.Structure):
 
 class Lb4Out(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("ret", "saddr", "daddr", "dport", "rev_nat", "slave")]
+
+
+class Frames(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("len", C.c_void_p), ("flags", C.c_void_p),
+                ("ep", C.c_void_p), ("stride", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class FrameTuples(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ("status", "family", "saddr", "daddr", "dport", "proto", "flags")]
 
 
 vp, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
@@ -96,6 +107,11 @@ PROTOS = {
     "cgpu_lb4_select": (i32, [vp, i32, C.POINTER(Lb4Tuples), sz, C.POINTER(Lb4Out), vp]),
     "cgpu_prefilter_v4": (i32, [vp, vp, vp, vp, sz, vp, vp]),
     "cgpu_prefilter_v6": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+    "cgpu_lxc_update": (i32, [vp, u32, vp]),
+    "cgpu_lxc_delete": (i32, [vp, u32]),
+    "cgpu_lxc_lookup": (i32, [vp, u32, vp]),
+    "cgpu_frames_parse": (i32, [vp, C.POINTER(Frames), sz, C.POINTER(FrameTuples), vp]),
+    "cgpu_classify_frames": (i32, [vp, C.POINTER(Frames), sz, vp, vp, vp, vp]),
     "cgpu_counter_delta_bytes": (sz, [vp]),
     "cgpu_counter_bind": (i32, [vp, vp, sz]),
     "cgpu_counter_fold": (i32, [vp, vp]),

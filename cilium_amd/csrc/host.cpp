@@ -339,6 +339,8 @@ struct cgpu_ctx {
 	/* cilium_lb4_services, keyed address << 32 | dport << 16 | slave so that
 	 * a frontend's entries are adjacent */
 	std::map<uint64_t, cgpu_lb4_service> lb;
+	/* per-endpoint lxc_config.h identity (cgpu_lxc_update) */
+	std::map<uint32_t, cgpu_lxc_info> lxcinfo;
 
 	/* ---- device ---- */
 	void *arena = nullptr;
@@ -387,6 +389,8 @@ CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
 	static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1,
 					   0x0, 0x1, 0x0, 0x0}; /* ROUTER_IP, bpf/node_config.h:30 */
 	memcpy(c->ipv6_router_ip, router, 16);
+	static const uint8_t node_mac[6] = {0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde}; /* NODE_MAC, node_config.h:51 */
+	memcpy(c->node_mac, node_mac, 6);
 }
 
 CGPU_EXPORT const char *cgpu_last_error(void) { return g_last_error.c_str(); }
@@ -900,6 +904,40 @@ CGPU_EXPORT int cgpu_endpoint_lookup(cgpu_ctx *c, const cgpu_endpoint_key *key)
 	memcpy(k.data(), key, 20);
 	std::lock_guard<std::mutex> g(c->mu);
 	return c->lxc.count(k) ? 0 : -ENOENT;
+}
+
+/* per-endpoint identity of the endpoint program (lib/lxc.h:31-89) */
+CGPU_EXPORT int cgpu_lxc_update(cgpu_ctx *c, uint32_t ep, const cgpu_lxc_info *info)
+{
+	if (!c || !info)
+		return fail(-EINVAL, "null argument");
+	if (ep >= 65536u)
+		return fail(-EINVAL, "endpoint id beyond the u16 ep column");
+	if (info->verify & ~(CGPU_VERIFY_SMAC | CGPU_VERIFY_DMAC | CGPU_VERIFY_SIP))
+		return fail(-EINVAL, "unknown verify bits");
+	std::lock_guard<std::mutex> g(c->mu);
+	c->lxcinfo[ep] = *info;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lxc_delete(cgpu_ctx *c, uint32_t ep)
+{
+	if (!c)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lxcinfo.erase(ep) ? 0 : -ENOENT;
+}
+
+CGPU_EXPORT int cgpu_lxc_lookup(cgpu_ctx *c, uint32_t ep, cgpu_lxc_info *out)
+{
+	if (!c || !out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = c->lxcinfo.find(ep);
+	if (it == c->lxcinfo.end())
+		return -ENOENT;
+	*out = it->second;
+	return 0;
 }
 
 /* ======================================================================= */
@@ -1769,6 +1807,14 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	size_t o_is = ar.add(init_slot.data(), init_slot.size() * 4);
 	size_t o_ip = ar.add(init_pk.data(), init_pk.size() * 8);
 	size_t o_ib = ar.add(init_by.data(), init_by.size() * 8);
+	/* dense per-endpoint lxc identity, 32 B each; absent endpoints verify nothing */
+	const uint32_t n_lxc = c->lxcinfo.empty() ? 0u : c->lxcinfo.rbegin()->first + 1u;
+	std::vector<cgpu_lxc_info> lxcv(n_lxc);
+	memset(lxcv.data(), 0, lxcv.size() * sizeof(cgpu_lxc_info));
+	for (auto &kv : c->lxcinfo)
+		lxcv[kv.first] = kv.second;
+	static_assert(sizeof(cgpu_lxc_info) == 32, "cgpu_lxc_info is 2 x uint4");
+	size_t o_lxc = ar.add(lxcv.data(), lxcv.size() * sizeof(cgpu_lxc_info));
 
 	HIP_OR_EIO(hipSetDevice(c->device));
 	/* launches on the previous snapshot must drain before it is freed */
@@ -1837,6 +1883,10 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 			(uint32_t)lbb.be.size()};
 	s.lb_flags = c->cfg.lb_flags;
 	s.ipv4_loopback = c->cfg.ipv4_loopback;
+	s.lxc = (const uint4 *)(arena + o_lxc);
+	s.n_lxc = n_lxc;
+	memcpy(&s.node_mac_lo, c->cfg.node_mac, 4);
+	s.node_mac_hi = (uint32_t)c->cfg.node_mac[4] | ((uint32_t)c->cfg.node_mac[5] << 8);
 	s.epoch = ++c->epoch;
 	c->snap = s;
 	c->committed = true;
@@ -1856,6 +1906,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	for (auto &k : c->fix6) sum += fnv(17, k.data(), k.size());
 	for (auto &k : c->lxc) sum += fnv(19, k.data(), k.size());
 	for (auto &kv : c->lb) sum += fnv(fnv(23, &kv.first, 8), &kv.second, sizeof(kv.second));
+	for (auto &kv : c->lxcinfo) sum += fnv(fnv(29, &kv.first, 4), &kv.second, sizeof(kv.second));
 	c->checksum = sum;
 	if (epoch_out)
 		*epoch_out = s.epoch;
@@ -1990,6 +2041,59 @@ CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n,
 			   verdict, identity, stage, delta, (uint64_t)n};
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(launch_classify_v6(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+static int frames_check(cgpu_ctx *c, const cgpu_frames *f, size_t n)
+{
+	if (!f || (n && (!f->data || !f->len || !f->flags || !f->ep)))
+		return fail(-EINVAL, "null frame column");
+	if (f->stride < 64 || (f->stride & 15))
+		return fail(-EINVAL, "frame stride must be a multiple of 16 and >= 64");
+	if ((uintptr_t)f->data & 15)
+		return fail(-EINVAL, "frame buffer must be 16-byte aligned");
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_frames_parse(cgpu_ctx *c, const cgpu_frames *f, size_t n,
+				  const cgpu_frame_tuples *o, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (int r = frames_check(c, f, n))
+		return r;
+	if (!o || (n && !o->status))
+		return fail(-EINVAL, "null status output");
+	if (!n)
+		return 0;
+	frames_args a{f->data, f->len, f->flags, f->ep, f->stride, (uint64_t)n,
+		      o->status, o->family, o->saddr, o->daddr, o->dport, o->proto, o->flags,
+		      nullptr, nullptr, nullptr, nullptr};
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_frames_parse(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n, int32_t *verdict,
+				     uint32_t *identity, uint8_t *stage, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (int r = frames_check(c, f, n))
+		return r;
+	if (n && (!verdict || !identity))
+		return fail(-EINVAL, "null output");
+	if (!n)
+		return 0;
+	frames_args a{f->data, f->len, f->flags, f->ep, f->stride, (uint64_t)n,
+		      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+		      verdict, identity, stage, delta};
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_classify_frames(s, a, (hipStream_t)stream));
 	return 0;
 }
 

@@ -634,6 +634,86 @@ struct cls_args {
 	const uint32_t *hash;
 };
 
+/* The identity resolution and the three-probe policy cascade for one tuple
+ * that passed the protocol gate (shared by k_classify and k_frames).
+ *   egress : dstID = ipcache(daddr) label | CLUSTER | WORLD (bpf_lxc.c:484-500
+ *            v4, :170-187 v6)
+ *   ingress: src = ipcache(saddr) label when the handed-in identity is
+ *            reserved and the label is not CLUSTER (nor HOST on v4)
+ *            (bpf_netdev.c:374-398 / :203-211); v4 secctx quirk (:278-290)
+ *   policy : policy.h:46-110, negative collapsed to DROP_POLICY
+ * v: verdict; id: label given to policy; st: 1 exact, 2 L3-only, 3 wildcard,
+ * 0 miss; ctr: the hit entry's counter slot or -1.  NOPOL: identity only
+ * (diagnostic ablation). */
+struct decision {
+	int32_t v;
+	uint32_t id, st;
+	int ctr;
+};
+
+template <int V6, bool NOPOL = false>
+__device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, bool frag, uint32_t sa4,
+					   uint32_t da4, uint4 sa6, uint4 da6, uint32_t dport, uint32_t proto,
+					   uint32_t ep)
+{
+	decision d;
+	const uint32_t eg = egress ? (1u << 24) : 0u;
+	const uint32_t hi4 = dport | (proto << 16) | eg;
+	uint32_t e, label;
+	bool in_cluster;
+	if (V6) {
+		const uint4 ad = egress ? da6 : sa6;
+		e = v6_lookup(s.ipc6, ad);
+		label = entry_label(s.ipc6.vals, e);
+		/* ipv6_match_prefix_64(daddr, ROUTER_IP), bpf/lib/ipv6.h:166-175 */
+		in_cluster = ad.x == s.router_ip64[0] && ad.y == s.router_ip64[1];
+	} else {
+		const uint32_t ad = egress ? da4 : sa4;
+		e = dir_lookup(s.ipc4, ad, &label);
+		in_cluster = (ad & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
+	}
+	if (egress) {
+		if (e && label)
+			d.id = label;
+		else if (in_cluster)
+			d.id = s.cluster_id;
+		else
+			d.id = s.world_id;
+	} else {
+		/* the lookup above ran unconditionally; it only decides when the
+		 * handed-in identity is reserved */
+		uint32_t src = s.ingress_src_identity;
+		if (src < s.health_id && e && label && label != s.cluster_id && (V6 || label != s.host_id))
+			src = label;
+		d.id = (!V6 && s.ingress_secctx_world) ? s.world_id : src;
+	}
+	uint32_t z = 0;
+	int ctr = -1;
+	d.st = 0;
+	if (NOPOL) {
+		/* diagnostic: identity resolution only */
+	} else if (!frag) {
+		ctr = pol_lookup(s.pol, d.id, hi4, ep, &z);
+		d.st = 1;
+	}
+	if (ctr < 0) {
+		ctr = pol_lookup(s.pol, d.id, eg, ep, &z);
+		d.st = 2;
+	}
+	if (ctr < 0 && !frag) {
+		ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
+		d.st = 3;
+	}
+	if (ctr >= 0) {
+		d.v = d.st == 2 ? 0 : (int32_t)(z >> 16);
+	} else {
+		d.st = 0;
+		d.v = DROP_POLICY;
+	}
+	d.ctr = ctr;
+	return d;
+}
+
 /* Packed per-workgroup counter: packets in bits 41..63, bytes in 0..40.
  * Exact while a workgroup adds < 2^23 hits of < 2^18 bytes to one slot
  * (the launcher bounds tuples per workgroup; longer packets take the
@@ -711,58 +791,22 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		} else {
 			/* IPv6 passes is_fragment = false (bpf_lxc.c:787-789) */
 			const bool frag = !V6 && !egress && ((fl >> 1) & 1u);
-			const uint32_t eg = egress ? (1u << 24) : 0u;
-			const uint32_t hi4 = dport | (proto << 16) | eg;
-			uint32_t e, label;
-			bool in_cluster;
+			uint4 sa6{}, da6{};
+			uint32_t sa4 = 0;
 			if (V6) {
-				const uint4 ad = egress ? static_cast<const uint4 *>(a.daddr)[i]
-							: static_cast<const uint4 *>(a.saddr)[i];
-				e = v6_lookup(s.ipc6, ad);
-				label = entry_label(s.ipc6.vals, e);
-				/* ipv6_match_prefix_64(daddr, ROUTER_IP), bpf/lib/ipv6.h:166-175 */
-				in_cluster = ad.x == s.router_ip64[0] && ad.y == s.router_ip64[1];
-			} else {
-				const uint32_t ad = egress ? eda : static_cast<const uint32_t *>(a.saddr)[i];
-				e = dir_lookup(s.ipc4, ad, &label);
-				in_cluster = (ad & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
-			}
-			if (egress) {
-				/* bpf_lxc.c:488-496 (v4) / :170-187 (v6) */
-				if (e && label)
-					id = label;
-				else if (in_cluster)
-					id = s.cluster_id;
+				if (egress)
+					da6 = static_cast<const uint4 *>(a.daddr)[i];
 				else
-					id = s.world_id;
-			} else {
-				/* bpf_netdev.c:374-398 (v4) / :203-211 (v6, no HOST_ID case).
-				 * The lookup above ran unconditionally; it only decides
-				 * when the handed-in identity is reserved. */
-				uint32_t src = s.ingress_src_identity;
-				if (src < s.health_id && e && label && label != s.cluster_id &&
-				    (V6 || label != s.host_id))
-					src = label;
-				id = (!V6 && s.ingress_secctx_world) ? s.world_id : src;
+					sa6 = static_cast<const uint4 *>(a.saddr)[i];
+			} else if (!egress) {
+				sa4 = static_cast<const uint32_t *>(a.saddr)[i];
 			}
-			uint32_t z = 0;
-			int ctr = -1;
-			if (ABL == 2) {
-				/* diagnostic: identity resolution only */
-			} else if (!frag) {
-				ctr = pol_lookup(s.pol, id, hi4, ep, &z);
-				st = 1;
-			}
-			if (ctr < 0) {
-				ctr = pol_lookup(s.pol, id, eg, ep, &z);
-				st = 2;
-			}
-			if (ctr < 0 && !frag) {
-				ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
-				st = 3;
-			}
-			if (ctr >= 0) {
-				const uint32_t c = (uint32_t)ctr;
+			const decision d = decide<V6, ABL == 2>(s, egress, frag, sa4, eda, sa6, da6, dport, proto, ep);
+			v = d.v;
+			id = d.id;
+			st = d.st;
+			if (d.ctr >= 0) {
+				const uint32_t c = (uint32_t)d.ctr;
 				if (CTR == 1 && c < s.hot_slots && len < PK_MAX_LEN) {
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len);
@@ -771,10 +815,6 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 					atomicAdd((unsigned long long *)&pctr[2u * c + 1u],
 						  (unsigned long long)len);
 				}
-				v = st == 2 ? 0 : (int32_t)(z >> 16);
-			} else {
-				st = 0;
-				v = DROP_POLICY;
 			}
 		}
 		a.verdict[i] = v;
@@ -1221,6 +1261,328 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 /* delta[2s] += pk[s] >> 37; delta[2s+1] += pk[s] & (2^37-1); pk[s] = 0, and
  * the forwarded metrics (reason 0, drop.h:104 / l3.h:119-130) of the packets
  * unpacked, by the direction of their entry (slot_dir: 1 ingress, 2 egress) */
+/* ------------------------------------------------------------------ */
+/* raw Ethernet frames -> policy tuple -> verdict   */
+/* ------------------------------------------------------------------ */
+#define DROP_INVALID_SMAC (-130) /* bpf/lib/common.h:237-264 */
+#define DROP_INVALID_DMAC (-131)
+#define DROP_INVALID_SIP (-132)
+#define DROP_INVALID (-134)
+#define DROP_CT_INVALID_HDR (-135)
+#define DROP_UNKNOWN_L3 (-139)
+#define DROP_INVALID_EXTHDR (-156)
+#define DROP_FRAG_NOSUPPORT (-157)
+#define EFAULT_LOAD (-14)        /* bpf_skb_load_bytes past skb->len */
+#define FRAME_NOT_CLASSIFIED 1   /* CGPU_FRAME_NOT_CLASSIFIED */
+#define DROP_SNAPLEN (-4096)     /* CGPU_DROP_SNAPLEN */
+
+/* The first 64 bytes of a frame slot as 16 little-endian words: Ethernet,
+ * the IPv4 header without options / the IPv6 header, and the L4 type and
+ * ports right behind them.  Offsets are compile-time constants after
+ * inlining, so the words stay in VGPRs. */
+struct fwin {
+	uint32_t w[16];
+	__device__ __forceinline__ uint32_t b(int o) const { return (w[o >> 2] >> ((o & 3) * 8)) & 0xffu; }
+	/* raw (memory-order) u16 at an even offset */
+	__device__ __forceinline__ uint32_t h(int o) const { return (w[o >> 2] >> ((o & 2) * 8)) & 0xffffu; }
+	/* raw u32 at an even offset */
+	__device__ __forceinline__ uint32_t d(int o) const
+	{
+		return (o & 2) ? ((w[o >> 2] >> 16) | (w[(o >> 2) + 1] << 16)) : w[o >> 2];
+	}
+};
+
+struct ftuple {
+	int32_t status; /* 0 reached policy, FRAME_NOT_CLASSIFIED, or a drop */
+	uint32_t fam;   /* 4 / 6 / 0 */
+	uint4 sa, da;   /* IPv4 in .x */
+	uint32_t dport, proto;
+	bool frag;
+};
+
+/* A header read of [off, off + sz): the reference bounds it by skb->len
+ * (revalidate_data / skb_load_bytes) and returns `err` past it; within len
+ * the bytes must also lie in the stored slot (cap = min(len, stride)). */
+__device__ __forceinline__ int32_t fchk(uint32_t off, uint32_t sz, uint32_t len, uint32_t cap, int32_t err)
+{
+	return off + sz > len ? err : (off + sz > cap ? DROP_SNAPLEN : 0);
+}
+
+/* One frame through the endpoint programs' steps before ipcache (cgpu.h
+ * cgpu_frames_parse).  Window reads when the L4 header sits right behind
+ * an option-less IPv4 / extension-less IPv6 header, global loads (L2) for
+ * IPv4 options and IPv6 extension headers. */
+__device__ __forceinline__ ftuple parse_frame(const cgpu_snapshot &s, const uint8_t *f, uint32_t len,
+					      uint32_t cap, bool egress, uint32_t ep)
+{
+	ftuple t;
+	t.status = 0;
+	t.fam = 0;
+	t.sa = uint4{0, 0, 0, 0};
+	t.da = uint4{0, 0, 0, 0};
+	t.dport = 0;
+	t.proto = 0;
+	t.frag = false;
+	fwin W;
+	{
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const uint4 v = ld_x4<true>(f + 16 * k);
+			W.w[4 * k] = v.x;
+			W.w[4 * k + 1] = v.y;
+			W.w[4 * k + 2] = v.z;
+			W.w[4 * k + 3] = v.w;
+		}
+	}
+	if (len < 14u) { /* no Ethernet header to dispatch on */
+		t.status = DROP_INVALID;
+		return t;
+	}
+	/* skb->protocol dispatch: egress bpf_lxc.c:690-710 (ARP to the ARP
+	 * responder, others DROP_UNKNOWN_L3); ingress bpf_netdev.c:494-521
+	 * (non-IP passed to the stack) */
+	const uint32_t et = W.h(12);
+	const bool v4 = et == 0x0008u;
+	if (!v4 && et != 0xDD86u) {
+		t.status = (egress && et != 0x0608u) ? DROP_UNKNOWN_L3 : FRAME_NOT_CLASSIFIED;
+		return t;
+	}
+	t.fam = v4 ? 4u : 6u;
+	/* revalidate_data: ETH_HLEN + sizeof(iphdr / ipv6hdr) <= len
+	 * (bpf/lib/common.h:71-91); the window holds both headers */
+	if (len < (v4 ? 34u : 54u)) {
+		t.status = DROP_INVALID;
+		return t;
+	}
+	if (v4) {
+		t.sa.x = W.d(26);
+		t.da.x = W.d(30);
+		t.proto = W.b(23);
+	} else {
+		t.sa = uint4{W.d(22), W.d(26), W.d(30), W.d(34)};
+		t.da = uint4{W.d(38), W.d(42), W.d(46), W.d(50)};
+		t.proto = W.b(20);
+	}
+	if (egress && ep < s.n_lxc) {
+		/* SMAC / DMAC / SIP checks of the endpoint (bpf_lxc.c:431-437,
+		 * :100-105; lib/lxc.h:31-89) */
+		const uint4 i0 = s.lxc[2u * ep];
+		const uint32_t verify = (i0.y >> 16) & 0xffu;
+		if ((verify & CGPU_VERIFY_SMAC) && (W.d(6) != i0.x || W.h(10) != (i0.y & 0xffffu))) {
+			t.status = DROP_INVALID_SMAC;
+			return t;
+		}
+		if ((verify & CGPU_VERIFY_DMAC) && (W.d(0) != s.node_mac_lo || W.h(4) != s.node_mac_hi)) {
+			t.status = DROP_INVALID_DMAC;
+			return t;
+		}
+		if (verify & CGPU_VERIFY_SIP) {
+			bool ok;
+			if (v4) {
+				ok = t.sa.x == i0.z;
+			} else {
+				const uint4 i1 = s.lxc[2u * ep + 1u];
+				ok = t.sa.x == i0.w && t.sa.y == i1.x && t.sa.z == i1.y && t.sa.w == i1.z;
+			}
+			if (!ok) {
+				t.status = DROP_INVALID_SIP;
+				return t;
+			}
+		}
+	}
+	uint32_t l4;
+	bool inwin;
+	if (v4) {
+		/* ipv4_hdrlen (ipv4.h:45-48): ihl * 4, not validated by the
+		 * reference; ipv4_is_fragment (ipv4.h:50-61): ingress only,
+		 * policy_can_egress4 passes false */
+		l4 = 14u + 4u * (W.b(14) & 15u);
+		inwin = l4 == 34u;
+		t.frag = !egress && (W.h(20) & 0xFFBFu) != 0u;
+	} else {
+		/* ipv6_hdrlen (ipv6.h:61-98): at most IPV6_MAX_HEADERS (4)
+		 * extension headers.  The length rule follows the reference
+		 * exactly: the AUTH formula applies when the NEXT header is AUTH. */
+		uint32_t nh = t.proto, off = 40u;
+		int32_t r = 1;
+		for (int k = 0; k < 4 && r == 1; k++) {
+			if (nh == 59u) {
+				r = DROP_INVALID_EXTHDR;
+			} else if (nh == 44u) {
+				r = DROP_FRAG_NOSUPPORT;
+			} else if (nh == 0u || nh == 43u || nh == 51u || nh == 60u) {
+				const uint32_t o = 14u + off;
+				r = fchk(o, 2, len, cap, DROP_INVALID);
+				if (!r) {
+					const uint32_t hl = f[o + 1];
+					nh = f[o];
+					off += nh == 51u ? (hl + 2u) << 2 : (hl + 1u) << 3;
+					r = 1;
+				}
+			} else {
+				r = 0;
+			}
+		}
+		if (r == 1)
+			r = DROP_INVALID_EXTHDR;
+		if (r) {
+			t.status = r;
+			return t;
+		}
+		t.proto = nh;
+		l4 = 14u + off;
+		inwin = l4 == 54u;
+	}
+	int32_t r;
+	/* extract_l4_port of lb{4,6}_extract_key under LB_L4 (lib/lb.h:192-215,
+	 * :590-599): TCP/UDP load the dport; a short frame returns the -EFAULT
+	 * of skb_load_bytes, which the egress program returns */
+	if (egress && (s.lb_flags & CGPU_LB_L4) && (t.proto == 6u || t.proto == 17u) &&
+	    (r = fchk(l4 + 2u, 2, len, cap, EFAULT_LOAD))) {
+		t.status = r;
+		return t;
+	}
+	/* ct_lookup{4,6} (conntrack.h:470-528 / :317-378) for the CT_NEW tuple:
+	 * built reversed, both lookups miss, the reverse leaves tuple.dport =
+	 * the packet's dport.  ICMP echo request: sport = type -> dport 8
+	 * (ICMPv6: 128); echo reply and other types: 0.  TCP also loads the
+	 * flags at l4 + 12 (bounds only: the action does not reach policy).
+	 * Without CONNTRACK the stubs leave the tuple ports 0. */
+	if (s.ct_proto_gate) {
+		if (t.proto == (v4 ? 1u : 58u)) {
+			if ((r = fchk(l4, 1, len, cap, DROP_CT_INVALID_HDR))) {
+				t.status = r;
+				return t;
+			}
+			const uint32_t type = inwin ? (v4 ? W.b(34) : W.b(54)) : (uint32_t)f[l4];
+			t.dport = type == (v4 ? 8u : 128u) ? type : 0u;
+		} else if (t.proto == 6u || t.proto == 17u) {
+			if ((r = fchk(l4, t.proto == 6u ? 14u : 4u, len, cap, DROP_CT_INVALID_HDR))) {
+				t.status = r;
+				return t;
+			}
+			t.dport = inwin ? (v4 ? W.h(36) : W.h(56))
+					: (uint32_t) * reinterpret_cast<const uint16_t *>(f + l4 + 2u);
+		} else {
+			t.status = DROP_CT_UNKNOWN_PROTO;
+		}
+	}
+	return t;
+}
+
+/*
+ * MODE 0: cgpu_frames_parse — write the policy tuple columns.
+ * MODE 1: cgpu_classify_frames — parse, then decide<> (the cgpu_classify_v4 /
+ *         _v6 decision) with the k_classify<.., CTR = 1> counters (hot
+ *         policy slots in LDS) and metrics.  One frame per lane; v4 and v6
+ *         frames of a batch share waves.
+ */
+template <int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_frames(cgpu_snapshot s, frames_args a)
+{
+	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
+	/* metrics {reason 0 / 133 / 137} x {ingress, egress}; others direct */
+	uint64_t mcnt[6] = {0, 0, 0, 0, 0, 0}, mbyt[6] = {0, 0, 0, 0, 0, 0};
+	uint64_t *met = MODE == 1 ? a.delta + 2ull * s.n_ctr_slots : nullptr;
+	if (MODE == 1) {
+		for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
+			lctr[k] = 0;
+		__syncthreads();
+	}
+	const uint64_t gstride = (uint64_t)gridDim.x * NT;
+	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += gstride) {
+		const uint32_t len = a.len[i];
+		const bool egress = a.flags[i] & 1u;
+		const uint32_t ep = a.ep[i];
+		const ftuple t = parse_frame(s, a.data + i * (uint64_t)a.stride, len, min(len, a.stride), egress, ep);
+		if (MODE == 0) {
+			a.status[i] = t.status;
+			if (a.family)
+				a.family[i] = (uint8_t)t.fam;
+			if (a.saddr16)
+				reinterpret_cast<uint4 *>(a.saddr16)[i] = t.sa;
+			if (a.daddr16)
+				reinterpret_cast<uint4 *>(a.daddr16)[i] = t.da;
+			if (a.dport)
+				a.dport[i] = (uint16_t)t.dport;
+			if (a.proto)
+				a.proto[i] = (uint8_t)t.proto;
+			if (a.tflags)
+				a.tflags[i] = (uint8_t)((egress ? 1u : 0u) | (t.frag ? 2u : 0u));
+			continue;
+		}
+		int32_t v;
+		uint32_t id = 0, st;
+		if (t.status == 0) {
+			const decision d = t.fam == 4u
+				? decide<0>(s, egress, t.frag, t.sa.x, t.da.x, uint4{}, uint4{}, t.dport, t.proto, ep)
+				: decide<1>(s, egress, false, 0u, 0u, t.sa, t.da, t.dport, t.proto, ep);
+			v = d.v;
+			id = d.id;
+			st = d.st;
+			if (d.ctr >= 0) {
+				const uint32_t c = (uint32_t)d.ctr;
+				if (c < s.hot_slots && len < PK_MAX_LEN) {
+					atomicAdd((unsigned long long *)&lctr[c],
+						  (1ull << PK_SHIFT) | (unsigned long long)len);
+				} else {
+					atomicAdd((unsigned long long *)&a.delta[2u * c], 1ull);
+					atomicAdd((unsigned long long *)&a.delta[2u * c + 1u], (unsigned long long)len);
+				}
+			}
+		} else if (t.status == FRAME_NOT_CLASSIFIED) {
+			v = 0;
+			st = 7;
+		} else {
+			v = t.status;
+			st = v == DROP_CT_UNKNOWN_PROTO ? 4u : 5u;
+		}
+		a.verdict[i] = v;
+		a.identity[i] = id;
+		if (a.stage)
+			a.stage[i] = (uint8_t)st;
+		if (st == 7u || v == DROP_SNAPLEN)
+			continue;
+		/* update_metrics(len, dir, -reason) (bpf/lib/drop.h:104), reason as u8 */
+		const uint32_t reason = v < 0 ? (uint32_t)(-v) & 0xffu : 0u;
+		const uint32_t dir = egress ? 1u : 0u;
+		const int b = reason == 0u ? 0 : reason == 133u ? 1 : reason == 137u ? 2 : -1;
+		if (b < 0) {
+			const uint32_t key = (reason * 4u + dir + 1u) * 2u;
+			atomicAdd((unsigned long long *)&met[key], 1ull);
+			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)len);
+		} else {
+#pragma unroll
+			for (int k = 0; k < 6; k++) {
+				const bool hit = k == 2 * b + (int)dir;
+				mcnt[k] += hit ? 1u : 0u;
+				mbyt[k] += hit ? len : 0u;
+			}
+		}
+	}
+	if (MODE == 0)
+		return;
+	const uint32_t reasons[3] = {0u, 133u, 137u};
+#pragma unroll
+	for (int k = 0; k < 6; k++) {
+		const uint64_t c = wave_sum(mcnt[k]);
+		const uint64_t b = wave_sum(mbyt[k]);
+		if ((threadIdx.x & 63) == 0 && c) {
+			const uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
+			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
+			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
+		}
+	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
+		const uint64_t v = lctr[k];
+		if (v) {
+			atomicAdd((unsigned long long *)&a.delta[2u * k], v >> PK_SHIFT);
+			atomicAdd((unsigned long long *)&a.delta[2u * k + 1u], v & PK_BYTES_MASK);
+		}
+	}
+}
+
 __global__ __launch_bounds__(256) void k_unpack(uint64_t *delta, uint64_t *pk, uint32_t lo, uint32_t hi,
 						  const uint8_t *slot_dir, uint64_t *met)
 {
@@ -1767,6 +2129,38 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 		hipLaunchKernelGGL(k_prefilter_v6_q<4>, dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
 	else
 		hipLaunchKernelGGL(k_prefilter_v6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hipStream_t st)
+{
+	hipLaunchKernelGGL((k_frames<0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
+/* as the k_classify<.., CTR = 1> launcher: 1024-thread workgroups, <= 2 per
+ * CU (LDS), at most 2^22 frames per workgroup (packed LDS counters) */
+hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, hipStream_t st)
+{
+	constexpr int NT = 1024;
+	const size_t lds = (size_t)s.hot_slots * 8u;
+	const uint64_t cap = 2ull * 256ull;
+	const uint64_t per_launch = cap * (1ull << 22);
+	for (uint64_t off = 0; off < a.n; off += per_launch) {
+		frames_args c = a;
+		const uint64_t m = std::min<uint64_t>(a.n - off, per_launch);
+		c.n = m;
+		c.data += off * a.stride;
+		c.len += off;
+		c.flags += off;
+		c.ep += off;
+		c.verdict += off;
+		c.identity += off;
+		if (c.stage)
+			c.stage += off;
+		const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
+		hipLaunchKernelGGL((k_frames<1, NT>), dim3(g), dim3(NT), lds, st, s, c);
+	}
 	return hipGetLastError();
 }
 

@@ -69,6 +69,29 @@ struct lb4_args {
 
 hipError_t launch_lb4(const cgpu_snapshot &s, const lb4_args &a, hipStream_t st);
 
+/* raw frames (cgpu_frames_parse / cgpu_classify_frames) */
+struct frames_args {
+	const uint8_t *data;
+	const uint32_t *len;
+	const uint8_t *flags;
+	const uint16_t *ep;
+	uint32_t stride;
+	uint64_t n;
+	/* parse outputs (any but status may be NULL) */
+	int32_t *status;
+	uint8_t *family, *saddr16, *daddr16;
+	uint16_t *dport;
+	uint8_t *proto, *tflags;
+	/* classify outputs */
+	int32_t *verdict;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t *delta;
+};
+
+hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hipStream_t st);
+hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, hipStream_t st);
+
 /* totals[i] += delta[i]; delta[i] = 0 over n u64 words */
 hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st);
 /* totals[2*slot[i]] = pk[i]; totals[2*slot[i]+1] = by[i]; delta[..] = 0 */

@@ -286,6 +286,11 @@ typedef struct cgpu_snapshot {
 	lb_table lb;
 	uint32_t lb_flags;       /* CGPU_LB_L3 | CGPU_LB_L4 */
 	uint32_t ipv4_loopback;  /* IPV4_LOOPBACK, network order */
+	/* per-endpoint lxc_config.h identity (cgpu_lxc_info, 32 B = 2 x uint4
+	 * per endpoint id, dense over [0, n_lxc)) and NODE_MAC */
+	const uint4 *lxc;
+	uint32_t n_lxc;
+	uint32_t node_mac_lo, node_mac_hi; /* bytes 0-3, 4-5 of NODE_MAC (LE words) */
 	uint64_t epoch;
 } cgpu_snapshot;
 

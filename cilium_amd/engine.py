@@ -25,7 +25,8 @@ import ipaddress
 import numpy as np
 
 from . import layouts as L
-from ._abi import CgpuConfig, CgpuError, Lb4Out, Lb4Tuples, TuplesV4, TuplesV6, check, lib
+from ._abi import (CgpuConfig, CgpuError, FrameTuples, Frames, Lb4Out, Lb4Tuples, TuplesV4, TuplesV6,
+                   check, lib)
 
 CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX = 0, 1, 2, 3
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
@@ -56,8 +57,8 @@ class Engine:
         for k, v in cfg.items():
             if not hasattr(self.cfg, k):
                 raise TypeError(f"unknown config field {k}")
-            if k == "ipv6_router_ip":
-                self.cfg.ipv6_router_ip[:] = bytes(v)
+            if k in ("ipv6_router_ip", "node_mac"):
+                getattr(self.cfg, k)[:] = bytes(v)
                 continue
             setattr(self.cfg, k, v)
         h = C.c_void_p()
@@ -282,6 +283,62 @@ class Engine:
             out = torch.empty(n, dtype=torch.uint8, device=flags.device)
         check(self.L.cgpu_prefilter_v6(self.h, _ptr(saddr16), _ptr(daddr16), _ptr(flags), n,
                                        _ptr(out), _stream(stream)), "cgpu_prefilter_v6")
+        return out
+
+    # ---------------------------------------------------------- raw frames
+    def lxc_update(self, ep: int, info) -> int:
+        """info: a layouts.LXC_INFO record (lxc_config.h of endpoint ep)."""
+        return check(self.L.cgpu_lxc_update(self.h, ep, _buf(info)), "cgpu_lxc_update")
+
+    def lxc_delete(self, ep: int) -> int:
+        return self.L.cgpu_lxc_delete(self.h, ep)
+
+    def lxc_lookup(self, ep: int):
+        out = np.zeros((), L.LXC_INFO)
+        rc = self.L.cgpu_lxc_lookup(self.h, ep, out.ctypes.data_as(C.c_void_p))
+        return None if rc == -errno.ENOENT else (check(rc, "cgpu_lxc_lookup"), out)[1]
+
+    @staticmethod
+    def _frames(f: dict) -> Frames:
+        data = f["data"]
+        assert data.dim() == 2 and data.is_contiguous()
+        return Frames(data.data_ptr(), f["len"].data_ptr(), f["flags"].data_ptr(),
+                      f["ep"].data_ptr(), data.shape[1], 0)
+
+    def frames_parse(self, f: dict, out: dict | None = None, stream=None):
+        """f: CUDA tensors data (n, stride) uint8, len int32, flags uint8,
+        ep int16.  Returns the policy tuple columns (cgpu_frames_parse)."""
+        import torch
+        n = f["len"].numel()
+        dev = f["len"].device
+        if out is None:
+            out = {"status": torch.empty(n, dtype=torch.int32, device=dev),
+                   "family": torch.empty(n, dtype=torch.uint8, device=dev),
+                   "saddr": torch.empty((n, 16), dtype=torch.uint8, device=dev),
+                   "daddr": torch.empty((n, 16), dtype=torch.uint8, device=dev),
+                   "dport": torch.empty(n, dtype=torch.int16, device=dev),
+                   "proto": torch.empty(n, dtype=torch.uint8, device=dev),
+                   "flags": torch.empty(n, dtype=torch.uint8, device=dev)}
+        fr = self._frames(f)
+        ot = FrameTuples(*[_ptr(out.get(k)) for k in ("status", "family", "saddr", "daddr",
+                                                      "dport", "proto", "flags")])
+        check(self.L.cgpu_frames_parse(self.h, C.byref(fr), n, C.byref(ot), _stream(stream)),
+              "cgpu_frames_parse")
+        return out
+
+    def classify_frames(self, f: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """Raw frames to verdicts in one pass (cgpu_classify_frames)."""
+        import torch
+        n = f["len"].numel()
+        dev = f["len"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
+        fr = self._frames(f)
+        check(self.L.cgpu_classify_frames(self.h, C.byref(fr), n, _ptr(out["verdict"]),
+                                          _ptr(out["identity"]), _ptr(out.get("stage")),
+                                          _stream(stream)), "cgpu_classify_frames")
         return out
 
     # ------------------------------------------------------------- counters

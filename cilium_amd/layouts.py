@@ -82,6 +82,31 @@ F_FRAGMENT = 2
 # prefilter packet flags
 PKT_OK, PKT_TRUNCATED, PKT_NOT_IP = 0, 1, 2
 
+# per-endpoint identity of the endpoint program (cgpu_lxc_info, include/cgpu.h;
+# lxc_config.h LXC_MAC / LXC_IPV4 / LXC_IP, bpf/lib/lxc.h:31-89)
+LXC_INFO = np.dtype([("mac", "u1", (6,)), ("verify", "u1"), ("pad", "u1"), ("ipv4", "<u4"),
+                     ("ipv6", "u1", (16,)), ("reserved", "<u4")])
+assert LXC_INFO.itemsize == 32
+VERIFY_SMAC, VERIFY_DMAC, VERIFY_SIP = 1, 2, 4
+# NODE_MAC, bpf/node_config.h:51
+NODE_MAC = bytes([0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde])
+# frame path status / verdict values (include/cgpu.h) and the drops it adds
+FRAME_NOT_CLASSIFIED = 1
+DROP_SNAPLEN = -4096
+DROP_INVALID_SMAC, DROP_INVALID_DMAC, DROP_INVALID_SIP = -130, -131, -132
+DROP_INVALID, DROP_CT_INVALID_HDR, DROP_UNKNOWN_L3 = -134, -135, -139
+DROP_INVALID_EXTHDR = -156
+EFAULT_LOAD = -14
+
+
+def lxc_info(mac: bytes, ipv4_raw: int, ipv6: bytes, verify: int) -> np.ndarray:
+    x = np.zeros((), LXC_INFO)
+    x["mac"] = np.frombuffer(bytes(mac), np.uint8)
+    x["verify"] = verify
+    x["ipv4"] = ipv4_raw
+    x["ipv6"] = np.frombuffer(bytes(ipv6), np.uint8)
+    return x
+
 
 def htons(x: int) -> int:
     return socket.htons(x)

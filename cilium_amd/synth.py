@@ -401,3 +401,188 @@ def packets6_to_device(p: dict, device="cuda"):
     import torch
     return {k: torch.from_numpy(np.ascontiguousarray(v, np.uint8)).to(device)
             for k, v in p.items()}
+
+
+# ---------------------------------------------------------------------------
+# raw Ethernet frames
+# ---------------------------------------------------------------------------
+# The endpoint identity of the reference's bpf/lxc_config.h (LXC_MAC, LXC_IPV4
+# as the raw u32 the program compares, LXC_IP) -- what the golden harness is
+# compiled with, and what the tests install through cgpu_lxc_update.
+LXC_MAC = bytes([0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff])
+LXC_IPV4_RAW = 0x10203040
+LXC_IP6 = bytes([0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1, 0x1, 0x65, 0x82, 0xbc])
+
+ICMP4_TYPES = np.array([0, 8, 8, 3, 11, 12, 5, 13, 0, 8], np.uint8)
+ICMP6_TYPES = np.array([128, 128, 129, 1, 2, 3, 4, 135, 136, 128], np.uint8)
+V4_PROTOS = np.array([6, 6, 6, 6, 17, 17, 17, 1, 1, 58, 132, 47, 0], np.uint8)
+V6_PROTOS = np.array([6, 6, 6, 17, 17, 58, 58, 132, 47], np.uint8)
+FRAG_OFFS = np.array([0, 0, 0, 0, 0, 0, 0x4000, 0x4000, 0x2000, 0x0001, 0x8000, 0xC000,
+                      0x4001, 0x1fff], np.uint16)
+EXT_TYPES = np.array([0, 43, 60, 51, 0, 43, 60, 51, 44, 59], np.uint8)
+
+
+def _put(D, rows, off, vals):
+    """D[rows, off + j] = vals[:, j] for variable per-row offsets (clipped to
+    the buffer width: bytes past the slot are not stored)."""
+    if len(rows) == 0:
+        return
+    vals = np.asarray(vals, np.uint8).reshape(len(rows), -1)
+    cols = np.asarray(off, np.int64).reshape(-1, 1) + np.arange(vals.shape[1])
+    ok = cols < D.shape[1]
+    r = np.broadcast_to(np.asarray(rows).reshape(-1, 1), cols.shape)
+    D[r[ok], cols[ok]] = vals[ok]
+
+
+def _be16(x):
+    x = np.asarray(x, np.uint16)
+    return np.stack([x >> 8, x & 0xff], 1).astype(np.uint8)
+
+
+def make_frames(rng, n: int, width: int = 256, n_ep: int = 5, addr4=None, edge: bool = True):
+    """Diverse Ethernet frames for the frame-path parity tests (vectorized).
+
+    Mix: IPv4 (options, ihl < 5, every frag_off class, TCP/UDP/ICMP/other,
+    ICMP types), IPv6 (0-5 extension headers incl. FRAGMENT / NONE / AUTH),
+    ARP, other ethertypes; egress frames mostly carry the endpoint's MAC /
+    address (LXC_* above) with some corrupted; 20% truncated at a random
+    length (edge=True also makes frames shorter than an Ethernet header).
+    Returns dict data (n, width) u8, len u32, flags u8 (egress bit), ep u16;
+    len may exceed what a narrower slot stores.  addr4: optional pool of
+    network-order u32 addresses to draw v4 addresses from.
+    """
+    D = rng.integers(0, 256, (n, width), dtype=np.uint8)
+    egress = rng.random(n) < 0.5
+    p = [0.58, 0.28, 0.07, 0.07] if edge else [0.8, 0.2, 0.0, 0.0]
+    kind = rng.choice(4, n, p=p)
+    full = np.zeros(n, np.int64)
+    # Ethernet: egress frames address the gateway from the endpoint's MAC
+    ok_d = egress & (rng.random(n) < 0.95)
+    ok_s = egress & (rng.random(n) < 0.95)
+    D[ok_d, 0:6] = np.frombuffer(L.NODE_MAC, np.uint8)
+    D[ok_s, 6:12] = np.frombuffer(LXC_MAC, np.uint8)
+    other = np.array([0x88cc, 0x8100, 0x0000, 0x86dc, 0x0801, 0xdd86], np.uint16)
+    et = np.select([kind == 0, kind == 1, kind == 2], [0x0800, 0x86DD, 0x0806],
+                   rng.choice(other, n).astype(np.int64)).astype(np.uint16)
+    D[:, 12:14] = _be16(et)
+    full[kind >= 2] = 14 + 28
+
+    def addr4_draw(m):
+        if addr4 is not None and len(addr4):
+            a = rng.choice(np.asarray(addr4, np.uint32), m)
+            return np.where(rng.random(m) < 0.8, a, rng.integers(0, 2**32, m, dtype=np.uint64)
+                            ).astype(np.uint32)
+        return rng.integers(0, 2**32, m, dtype=np.uint64).astype(np.uint32)
+
+    def l4(rows, off, proto, v6):
+        """TCP 20 / UDP 8 / ICMP 8 / other 8 bytes at `off`; returns the length."""
+        m = len(rows)
+        ln = np.full(m, 8, np.int64)
+        sport = rng.integers(1, 65536, m).astype(np.uint16)
+        dport = np.where(rng.random(m) < 0.8, rng.choice(PORTS64, m),
+                         rng.integers(0, 65536, m)).astype(np.uint16)
+        hdr = rng.integers(0, 256, (m, 20), dtype=np.uint8)
+        tcpudp = (proto == 6) | (proto == 17)
+        hdr[tcpudp, 0:2] = _be16(sport[tcpudp])
+        hdr[tcpudp, 2:4] = _be16(dport[tcpudp])
+        icmp = proto == (58 if v6 else 1)
+        hdr[icmp, 0] = rng.choice(ICMP6_TYPES if v6 else ICMP4_TYPES, int(icmp.sum()))
+        ln[proto == 6] = 20
+        _put(D, rows, off, hdr)
+        return ln
+
+    # ---- IPv4
+    r4 = np.flatnonzero(kind == 0)
+    m = len(r4)
+    ihl = np.where(rng.random(m) < 0.82, 5, np.where(rng.random(m) < 0.6,
+                                                      rng.integers(6, 16, m), rng.integers(0, 5, m)))
+    proto = rng.choice(V4_PROTOS, m)
+    sa = addr4_draw(m)
+    lxc_src = egress[r4] & (rng.random(m) < 0.9)
+    sa = np.where(lxc_src, np.uint32(LXC_IPV4_RAW), sa).astype(np.uint32)  # stored (raw) u32
+    da = addr4_draw(m)
+    D[r4, 14] = (0x40 | ihl).astype(np.uint8)
+    D[r4, 20:22] = _be16(rng.choice(FRAG_OFFS, m))
+    D[r4, 23] = proto
+    D[r4, 26:30] = sa.view(np.uint8).reshape(m, 4)
+    D[r4, 30:34] = da.view(np.uint8).reshape(m, 4)
+    off = 14 + 4 * ihl
+    has_l4 = ihl >= 5  # shorter headers leave the reference reading the IP header as L4
+    ln = np.full(m, 8, np.int64)
+    ln[has_l4] = l4(r4[has_l4], off[has_l4], proto[has_l4], False)
+    full[r4] = np.maximum(off, 34) + ln
+
+    # ---- IPv6
+    r6 = np.flatnonzero(kind == 1)
+    m = len(r6)
+    proto = rng.choice(V6_PROTOS, m)
+    next_chain = np.where(rng.random(m) < 0.6, 0, rng.integers(1, 6, m))
+    chain = rng.choice(EXT_TYPES, (m, 6))
+    D[r6, 14] = 0x60
+    sa6 = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+    sa6[egress[r6] & (rng.random(m) < 0.9)] = np.frombuffer(LXC_IP6, np.uint8)
+    D[r6, 22:38] = sa6
+    first = np.where(next_chain > 0, chain[:, 0], proto)
+    D[r6, 20] = first
+    off = np.full(m, 54, np.int64)
+    cur = first.copy()
+    live = next_chain > 0
+    for j in range(6):
+        rows = np.flatnonzero(live)
+        if len(rows) == 0:
+            break
+        nxt = np.where(j + 1 < next_chain[rows], chain[rows, min(j + 1, 5)], proto[rows])
+        hl = rng.integers(0, 3, len(rows))
+        _put(D, r6[rows], off[rows], np.stack([nxt, hl], 1))
+        # advance as ipv6_hdrlen does (the AUTH rule keys on the NEXT header)
+        step = np.where(nxt == 51, (hl + 2) << 2, (hl + 1) << 3)
+        stop = (cur[rows] == 44) | (cur[rows] == 59)
+        off[rows] += np.where(stop, 0, step)
+        cur[rows] = nxt
+        live[rows] = (j + 1 < next_chain[rows]) & ~stop
+    ln = l4(r6, off, proto, True)
+    full[r6] = off + ln
+
+    full += rng.integers(0, 24, n)  # payload
+    lens = np.minimum(full, 65535)
+    trunc = rng.random(n) < 0.2
+    lo = np.where(edge, 0, 14)
+    lens[trunc] = rng.integers(lo, np.maximum(full[trunc], lo + 1))
+    return {"data": D, "len": lens.astype(np.uint32), "flags": egress.astype(np.uint8),
+            "ep": rng.integers(0, n_ep, n).astype(np.uint16)}
+
+
+def frames_from_tuples(t: dict, stride: int = 64, seed=SEED):
+    """The IPv4 tuples of make_tuples as Ethernet frames: IPv4 without
+    options, TCP (20 B) / UDP (8 B) header, MF set on fragments, the tuple's
+    len as the wire length.  Every frame reaches policy with the tuple it
+    came from (classify_frames == classify_v4 on TCP/UDP tuples)."""
+    n = len(t["saddr"])
+    rng = np.random.Generator(np.random.PCG64(seed ^ 0xF4A3E))
+    D = np.zeros((n, stride), np.uint8)
+    D[:, 0:6] = np.frombuffer(L.NODE_MAC, np.uint8)
+    D[:, 6:12] = np.frombuffer(LXC_MAC, np.uint8)
+    D[:, 12] = 0x08
+    D[:, 14] = 0x45
+    frag = (np.asarray(t["flags"]) >> 1) & 1
+    D[:, 20] = np.where(frag == 1, 0x20, 0x00)
+    D[:, 22] = 64
+    D[:, 23] = t["proto"]
+    D[:, 26:30] = np.ascontiguousarray(t["saddr"], np.uint32).view(np.uint8).reshape(n, 4)
+    D[:, 30:34] = np.ascontiguousarray(t["daddr"], np.uint32).view(np.uint8).reshape(n, 4)
+    D[:, 34:36] = _be16(rng.integers(1024, 65536, n))
+    D[:, 36:38] = np.ascontiguousarray(t["dport"], np.uint16).view(np.uint8).reshape(n, 2)
+    tcp = np.asarray(t["proto"]) == 6
+    D[tcp, 46] = 0x50
+    D[tcp, 47] = 0x10
+    return {"data": D, "len": np.asarray(t["len"], np.uint32).copy(),
+            "flags": (np.asarray(t["flags"]) & 1).astype(np.uint8),
+            "ep": np.asarray(t["ep"], np.uint16).copy()}
+
+
+def frames_to_device(f: dict, device="cuda"):
+    import torch
+    return {"data": torch.from_numpy(np.ascontiguousarray(f["data"])).to(device),
+            "len": torch.from_numpy(np.ascontiguousarray(f["len"], np.uint32).view(np.int32)).to(device),
+            "flags": torch.from_numpy(np.ascontiguousarray(f["flags"], np.uint8)).to(device),
+            "ep": torch.from_numpy(np.ascontiguousarray(f["ep"], np.uint16).view(np.int16)).to(device)}

@@ -150,7 +150,11 @@ typedef struct cgpu_config {
 	/* CGPU_LB_L3 | CGPU_LB_L4: the LB_L3 / LB_L4 build switches of lib/lb.h
 	 * (bpf/lxc_config.h:44-45 and bpf/init.sh:352 set both) */
 	uint32_t lb_flags;
-	uint32_t reserved[4];
+	/* NODE_MAC (bpf/node_config.h:51): the gateway MAC an endpoint's egress
+	 * frames must be addressed to (is_valid_gw_dst_mac, lib/lxc.h:77-90) */
+	uint8_t node_mac[6];
+	uint8_t reserved1[2];
+	uint32_t reserved[2];
 } cgpu_config;
 
 #define CGPU_LB_L3 1u
@@ -248,6 +252,31 @@ size_t cgpu_lb4_count(cgpu_ctx *ctx);
  * does not contain: SURVEY §8c).  Over the stored (network-order) fields. */
 uint32_t cgpu_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
 			uint8_t proto);
+
+/* ------------------------------------------------------------------ */
+/* per-endpoint identity of the endpoint program (lxc_config.h)         */
+/* ------------------------------------------------------------------ */
+/* The #defines the agent writes per endpoint into lxc_config.h and that the
+ * from-container program checks on every frame (bpf/lib/lxc.h:31-89):
+ * LXC_MAC, LXC_IPV4, LXC_IP, and which checks are compiled in (the absence
+ * of DISABLE_SMAC_VERIFICATION / DISABLE_DMAC_VERIFICATION /
+ * DISABLE_SIP_VERIFICATION).  An endpoint without an entry verifies nothing. */
+#define CGPU_VERIFY_SMAC 1u /* h_source == LXC_MAC      -> else DROP_INVALID_SMAC (-130) */
+#define CGPU_VERIFY_DMAC 2u /* h_dest == NODE_MAC       -> else DROP_INVALID_DMAC (-131) */
+#define CGPU_VERIFY_SIP 4u  /* saddr == LXC_IPV4/LXC_IP -> else DROP_INVALID_SIP (-132) */
+
+typedef struct cgpu_lxc_info {
+	uint8_t mac[6];   /* LXC_MAC */
+	uint8_t verify;   /* CGPU_VERIFY_* */
+	uint8_t pad;
+	uint32_t ipv4;    /* LXC_IPV4: raw u32 compared with ip4->saddr (lxc.h:55-62) */
+	uint8_t ipv6[16]; /* LXC_IP, network order */
+	uint32_t reserved;
+} cgpu_lxc_info;
+
+int cgpu_lxc_update(cgpu_ctx *ctx, uint32_t ep, const cgpu_lxc_info *info);
+int cgpu_lxc_delete(cgpu_ctx *ctx, uint32_t ep);
+int cgpu_lxc_lookup(cgpu_ctx *ctx, uint32_t ep, cgpu_lxc_info *info_out);
 
 /* ------------------------------------------------------------------ */
 /* publication                                                          */
@@ -364,6 +393,79 @@ int cgpu_prefilter_v4(cgpu_ctx *ctx, const uint32_t *saddr, const uint32_t *dadd
 /* saddr/daddr: 16 bytes per packet, contiguous */
 int cgpu_prefilter_v6(cgpu_ctx *ctx, const uint8_t *saddr, const uint8_t *daddr,
 		      const uint8_t *flags, size_t n, uint8_t *verdict, void *stream);
+
+/* ------------------------------------------------------------------ */
+/* raw Ethernet frames                               */
+/* ------------------------------------------------------------------ */
+/*
+ * A batch of frames in one device buffer: frame i is the first
+ * min(len[i], stride) bytes at data + i * stride (a fixed-size receive ring
+ * slot; the rest of the slot is ignored).  stride is a multiple of 16 and
+ * >= 64; data is 16-byte aligned.  len[i] is the wire length (skb->len), the
+ * bound of every header read as in skb_load_bytes / revalidate_data.
+ * flags[i]: CGPU_F_EGRESS = from-container (the endpoint's egress program),
+ * else to-container (ingress); other bits are ignored.  ep[i] selects the
+ * policy map and the cgpu_lxc_info of the endpoint.
+ */
+typedef struct cgpu_frames {
+	const uint8_t *data;
+	const uint32_t *len;
+	const uint8_t *flags;
+	const uint16_t *ep;
+	uint32_t stride;
+	uint32_t reserved;
+} cgpu_frames;
+
+/* frame status / verdict values beyond the reference's DROP_* codes */
+#define CGPU_FRAME_NOT_CLASSIFIED 1 /* egress ARP (tail call to the ARP responder,
+				       bpf_lxc.c:703-706) or ingress non-IP (passed
+				       to the stack, bpf_netdev.c:518-520) */
+#define CGPU_DROP_SNAPLEN (-4096)   /* a header the reference would read lies past
+				       the stored slot (stride < len): re-submit
+				       with a larger stride */
+
+/* The policy tuple a frame reaches the ipcache / policy step with. */
+typedef struct cgpu_frame_tuples {
+	int32_t *status;   /* 0 reached policy; CGPU_FRAME_NOT_CLASSIFIED; or the
+			      DROP_* / -errno the program returned before policy */
+	uint8_t *family;   /* 4, 6, or 0 (not IP) */
+	uint8_t *saddr;    /* 16 bytes per frame (IPv4: first 4, rest zero) */
+	uint8_t *daddr;    /* 16 bytes per frame */
+	uint16_t *dport;   /* tuple.dport after ct_lookup (network order; 0 without
+			      CONNTRACK, i.e. ct_proto_gate = 0) */
+	uint8_t *proto;    /* tuple.nexthdr (after the IPv6 extension-header walk) */
+	uint8_t *flags;    /* CGPU_F_EGRESS | CGPU_F_FRAGMENT (ingress IPv4 only) */
+} cgpu_frame_tuples;
+
+/*
+ * Per frame, the steps of the endpoint programs before the ipcache lookup
+ * (stateless: conntrack empty, every packet CT_NEW):
+ *   egress : skb->protocol dispatch (bpf_lxc.c:683-711; other than IPv4,
+ *            IPv6, ARP -> DROP_UNKNOWN_L3 -139), revalidate_data (-134), the
+ *            SMAC / DMAC / SIP checks (-130 / -131 / -132), ipv6_hdrlen
+ *            (-156, -157, -134), extract_l4_port of lb{4,6}_extract_key
+ *            (TCP/UDP dport past len -> -14, -EFAULT of skb_load_bytes),
+ *            ct_lookup{4,6} port extraction (-135 truncated L4, -137 other
+ *            than ICMP/ICMPv6/TCP/UDP; with ct_proto_gate = 0 the
+ *            non-CONNTRACK stubs: no port load, no gate)
+ *   ingress: bpf_netdev.c dispatch (non-IP passed), ipv4_policy /
+ *            ipv6_policy up to ct_lookup (bpf_lxc.c:876-897, :731-773)
+ * All outputs are device pointers; any but status may be NULL.
+ */
+int cgpu_frames_parse(cgpu_ctx *ctx, const cgpu_frames *f, size_t n,
+		      const cgpu_frame_tuples *out, void *stream);
+
+/*
+ * Raw frames to verdicts in one pass: cgpu_frames_parse, then for frames
+ * that reach policy the decision of cgpu_classify_v4 / cgpu_classify_v6 on
+ * that tuple (mixed IPv4 / IPv6 batches).  Frames that end before policy get
+ * verdict = their status, identity 0 and stage 5 (DROP_CT_UNKNOWN_PROTO keeps
+ * stage 4 as in cgpu_classify_v4; NOT_CLASSIFIED: verdict 0, stage 7, not
+ * counted in the metrics).  Metrics count every other frame
+ * once at {reason = -verdict (u8) or 0, dir}; SNAPLEN frames are not counted.
+ */
+int cgpu_classify_frames(cgpu_ctx *ctx, const cgpu_frames *f, size_t n, int32_t *verdict,
+			 uint32_t *identity, uint8_t *stage, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* counters                                                             */

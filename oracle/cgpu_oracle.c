@@ -353,6 +353,8 @@ struct or_ctx {
 	struct ohash fix4, fix6;
 	struct ohash lxc;           /* endpoint_key -> present */
 	struct ohash lb;            /* lb4_key (8 B) -> lb4_service (12 B) */
+	uint8_t *lxcinfo;           /* [n_lxcinfo][32] per-endpoint identity */
+	size_t n_lxcinfo;
 	uint64_t metrics[N_METRICS];
 };
 
@@ -376,6 +378,10 @@ void or_default_config(or_config *cfg)
 	}
 	cfg->lb_l3 = cfg->lb_l4 = 1;       /* lxc_config.h:44-45, init.sh:352 */
 	cfg->ipv4_loopback = 0x1ffff50a;   /* node_config.h:45 */
+	{
+		static const uint8_t m[6] = {0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde}; /* node_config.h:51 */
+		memcpy(cfg->node_mac, m, 6);
+	}
 }
 
 or_ctx *or_create(void)
@@ -406,6 +412,7 @@ void or_destroy(or_ctx *c)
 	for (size_t i = 0; i < c->n_ep; i++)
 		oh_destroy(&c->policy[i]);
 	free(c->policy);
+	free(c->lxcinfo);
 	free(c);
 }
 
@@ -1309,4 +1316,315 @@ void or_counters_reset(or_ctx *c)
 			if (h->used[i])
 				memset(h->vals + i * h->vsz + 8, 0, 16);
 	}
+}
+
+/* ====================================================================== */
+/* Raw frames                                           */
+/* ====================================================================== */
+#define DROP_INVALID_SMAC (-130) /* bpf/lib/common.h:237-264 */
+#define DROP_INVALID_DMAC (-131)
+#define DROP_INVALID_SIP (-132)
+#define DROP_INVALID (-134)
+#define DROP_CT_INVALID_HDR (-135)
+#define DROP_UNKNOWN_L3 (-139)
+#define DROP_INVALID_EXTHDR (-156)
+#define EFAULT_LOAD (-14)      /* bpf_skb_load_bytes past skb->len */
+#define FRAME_NOT_CLASSIFIED 1
+#define DROP_SNAPLEN (-4096)
+
+int or_lxc_update(or_ctx *c, uint32_t ep, const void *info32)
+{
+	if (ep >= 65536)
+		return -EINVAL;
+	if (ep >= c->n_lxcinfo) {
+		uint8_t *p = realloc(c->lxcinfo, (size_t)(ep + 1) * 32);
+		if (!p)
+			return -ENOMEM;
+		memset(p + c->n_lxcinfo * 32, 0, (ep + 1 - c->n_lxcinfo) * 32);
+		c->lxcinfo = p;
+		c->n_lxcinfo = ep + 1;
+	}
+	memcpy(c->lxcinfo + (size_t)ep * 32, info32, 32);
+	return 0;
+}
+
+/* A frame as the skb helpers see it: bytes [0, len) of which [0, cap) are
+ * stored.  ld() is skb_load_bytes / a revalidated direct read: past len it
+ * fails with the caller's error; within len but past the stored slot the
+ * frame cannot be parsed here (DROP_SNAPLEN). */
+struct frame {
+	const uint8_t *p;
+	uint32_t len, cap;
+};
+
+static int fr_ld(const struct frame *f, uint32_t off, uint32_t n, void *to, int err)
+{
+	if ((uint64_t)off + n > f->len)
+		return err;
+	if ((uint64_t)off + n > f->cap)
+		return DROP_SNAPLEN;
+	memcpy(to, f->p + off, n);
+	return 0;
+}
+
+struct ftuple {
+	int family;
+	uint8_t sa[16], da[16];
+	uint16_t dport;
+	uint8_t proto, frag;
+};
+
+/* ipv6_hdrlen (bpf/lib/ipv6.h:61-98): IPV6_MAX_HEADERS = 4; the length
+ * of an option header uses ipv6_authlen when the header it POINTS TO is
+ * NEXTHDR_AUTH (the reference tests the new nexthdr). */
+static int ipv6_hdrlen_r(const struct frame *f, uint8_t *nexthdr)
+{
+	int len = 40;
+	uint8_t nh = *nexthdr;
+	for (int i = 0; i < 4; i++) {
+		uint8_t opt[2];
+		int r;
+		switch (nh) {
+		case 59: /* NEXTHDR_NONE */
+			return DROP_INVALID_EXTHDR;
+		case 44: /* NEXTHDR_FRAGMENT */
+			return DROP_FRAG_NOSUPPORT;
+		case 0: case 43: case 51: case 60: /* HOP, ROUTING, AUTH, DEST */
+			if ((r = fr_ld(f, 14 + (uint32_t)len, 2, opt, DROP_INVALID)))
+				return r;
+			nh = opt[0];
+			len += nh == 51 ? (opt[1] + 2) << 2 : (opt[1] + 1) << 3;
+			break;
+		default:
+			*nexthdr = nh;
+			return len;
+		}
+	}
+	return DROP_INVALID_EXTHDR;
+}
+
+/*
+ * One frame (cgpu.h cgpu_frames_parse):
+ *  dispatch   bpf_lxc.c:683-711 (egress) / bpf_netdev.c:494-521 (ingress)
+ *  revalidate bpf/lib/common.h:71-91
+ *  SMAC/DMAC/SIP bpf_lxc.c:431-437, :100-105; bpf/lib/lxc.h:31-89
+ *  hdrlen     ipv4.h:45-48 / ipv6.h:61-98; fragment ipv4.h:50-61 (ingress v4)
+ *  LB_L4 port lb.h:192-215 via lb{4,6}_extract_key (egress)
+ *  ports      conntrack.h:470-528 / :317-378, CT_NEW + ipv{4,6}_ct_tuple_reverse
+ */
+static int frame_parse_one(const or_ctx *c, const struct frame *f, int egress, uint32_t ep,
+			   struct ftuple *t)
+{
+	const or_config *cfg = &c->cfg;
+	uint16_t et;
+	int v4, r;
+	uint32_t l4;
+	const uint8_t *info = (egress && ep < c->n_lxcinfo) ? c->lxcinfo + (size_t)ep * 32 : NULL;
+	memset(t, 0, sizeof(*t));
+	if (f->len < 14)
+		return DROP_INVALID;
+	memcpy(&et, f->p + 12, 2);
+	et = (uint16_t)((et >> 8) | (et << 8)); /* host order */
+	if (et != 0x0800 && et != 0x86DD)
+		return (egress && et != 0x0806) ? DROP_UNKNOWN_L3 : FRAME_NOT_CLASSIFIED;
+	v4 = et == 0x0800;
+	t->family = v4 ? 4 : 6;
+	if (f->len < (v4 ? 34u : 54u))
+		return DROP_INVALID;
+	if (v4) {
+		memcpy(t->sa, f->p + 26, 4);
+		memcpy(t->da, f->p + 30, 4);
+		t->proto = f->p[23];
+	} else {
+		memcpy(t->sa, f->p + 22, 16);
+		memcpy(t->da, f->p + 38, 16);
+		t->proto = f->p[20];
+	}
+	if (info) {
+		uint8_t verify = info[6];
+		if ((verify & 1) && memcmp(f->p + 6, info, 6))
+			return DROP_INVALID_SMAC;
+		if ((verify & 2) && memcmp(f->p, cfg->node_mac, 6))
+			return DROP_INVALID_DMAC;
+		if ((verify & 4) && (v4 ? memcmp(t->sa, info + 8, 4) : memcmp(t->sa, info + 12, 16)))
+			return DROP_INVALID_SIP;
+	}
+	if (v4) {
+		uint16_t fo = (uint16_t)((f->p[20] << 8) | f->p[21]);
+		l4 = 14u + 4u * (f->p[14] & 15u);
+		t->frag = !egress && (fo & 0xBFFF) != 0;
+	} else {
+		int hl = ipv6_hdrlen_r(f, &t->proto);
+		if (hl < 0)
+			return hl;
+		l4 = 14u + (uint32_t)hl;
+	}
+	if (egress && cfg->lb_l4 && (t->proto == PROTO_TCP || t->proto == PROTO_UDP)) {
+		uint16_t port;
+		if ((r = fr_ld(f, l4 + 2, 2, &port, EFAULT_LOAD)))
+			return r;
+	}
+	if (cfg->ct_proto_gate) {
+		uint8_t b[14];
+		if (t->proto == (v4 ? PROTO_ICMP : PROTO_ICMPV6)) {
+			if ((r = fr_ld(f, l4, 1, b, DROP_CT_INVALID_HDR)))
+				return r;
+			/* echo request: tuple.sport = type, reversed to dport */
+			t->dport = b[0] == (v4 ? 8 : 128) ? b[0] : 0;
+		} else if (t->proto == PROTO_TCP || t->proto == PROTO_UDP) {
+			/* TCP: flags at l4 + 12, then sport + dport */
+			if ((r = fr_ld(f, l4, t->proto == PROTO_TCP ? 14 : 4, b, DROP_CT_INVALID_HDR)))
+				return r;
+			memcpy(&t->dport, b + 2, 2);
+		} else {
+			return DROP_CT_UNKNOWN_PROTO;
+		}
+	}
+	return 0;
+}
+
+int or_frames_parse(or_ctx *c, size_t n, const uint8_t *data, uint32_t stride, const uint32_t *len,
+		    const uint8_t *flags, const uint16_t *ep, int32_t *status, uint8_t *family,
+		    uint8_t *saddr16, uint8_t *daddr16, uint16_t *dport, uint8_t *proto,
+		    uint8_t *tflags)
+{
+	for (size_t i = 0; i < n; i++) {
+		struct frame f = {data + i * stride, len[i], len[i] < stride ? len[i] : stride};
+		struct ftuple t;
+		int egress = flags[i] & 1;
+		status[i] = frame_parse_one(c, &f, egress, ep[i], &t);
+		if (family)
+			family[i] = (uint8_t)t.family;
+		if (saddr16)
+			memcpy(saddr16 + 16 * i, t.sa, 16);
+		if (daddr16)
+			memcpy(daddr16 + 16 * i, t.da, 16);
+		if (dport)
+			dport[i] = t.dport;
+		if (proto)
+			proto[i] = t.proto;
+		if (tflags)
+			tflags[i] = (uint8_t)(egress | (t.frag << 1));
+	}
+	return 0;
+}
+
+struct fp_job {
+	or_ctx *c;
+	size_t lo, hi;
+	const uint8_t *data, *flags;
+	uint32_t stride;
+	const uint32_t *len;
+	const uint16_t *ep;
+	int32_t *st;
+	uint8_t *fam, *sa, *da, *pr, *tf;
+	uint16_t *dp;
+};
+
+static void *fp_worker(void *arg)
+{
+	struct fp_job *j = arg;
+	size_t lo = j->lo, m = j->hi - j->lo;
+	or_frames_parse(j->c, m, j->data + lo * j->stride, j->stride, j->len + lo, j->flags + lo,
+			j->ep + lo, j->st + lo, j->fam + lo, j->sa + 16 * lo, j->da + 16 * lo, j->dp + lo,
+			j->pr + lo, j->tf + lo);
+	return NULL;
+}
+
+int or_classify_frames(or_ctx *c, size_t n, const uint8_t *data, uint32_t stride,
+		       const uint32_t *len, const uint8_t *flags, const uint16_t *ep, int32_t *verdict,
+		       uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
+{
+	int32_t *st = malloc(n * sizeof(int32_t) + 1);
+	uint8_t *fam = malloc(n + 1), *sa = malloc(16 * n + 16), *da = malloc(16 * n + 16);
+	uint8_t *pr = malloc(n + 1), *tf = malloc(n + 1);
+	uint16_t *dp = malloc(2 * n + 2);
+	size_t *idx = malloc(n * sizeof(size_t) + 1);
+	uint64_t ps = 0, p2 = 0;
+	{
+		int nt = nthreads <= 0 ? 1 : nthreads;
+		struct fp_job *jobs = calloc((size_t)nt, sizeof(*jobs));
+		pthread_t *th = calloc((size_t)nt, sizeof(*th));
+		for (int t = 0; t < nt; t++) {
+			struct fp_job *j = &jobs[t];
+			*j = (struct fp_job){c, n * (size_t)t / (size_t)nt, n * (size_t)(t + 1) / (size_t)nt,
+					     data, flags, stride, len, ep, st, fam, sa, da, pr, tf, dp};
+			if (nt == 1)
+				fp_worker(j);
+			else
+				pthread_create(&th[t], NULL, fp_worker, j);
+		}
+		for (int t = 0; nt > 1 && t < nt; t++)
+			pthread_join(th[t], NULL);
+		free(jobs);
+		free(th);
+	}
+	for (int v6 = 0; v6 < 2; v6++) {
+		/* the tuples of one family that reach policy, through or_classify_v{4,6} */
+		size_t m = 0;
+		for (size_t i = 0; i < n; i++)
+			if (!st[i] && fam[i] == (v6 ? 6 : 4))
+				idx[m++] = i;
+		if (!m)
+			continue;
+		uint8_t *gs = malloc(16 * m), *gd = malloc(16 * m), *gp = malloc(m), *gf = malloc(m);
+		uint16_t *gdp = malloc(2 * m), *gep = malloc(2 * m);
+		uint32_t *gl = malloc(4 * m), *gid = malloc(4 * m), *gs4 = malloc(4 * m), *gd4 = malloc(4 * m);
+		int32_t *gv = malloc(4 * m);
+		uint8_t *gst = malloc(m);
+		for (size_t k = 0; k < m; k++) {
+			size_t i = idx[k];
+			memcpy(gs + 16 * k, sa + 16 * i, 16);
+			memcpy(gd + 16 * k, da + 16 * i, 16);
+			memcpy(&gs4[k], sa + 16 * i, 4);
+			memcpy(&gd4[k], da + 16 * i, 4);
+			gp[k] = pr[i];
+			gf[k] = tf[i];
+			gdp[k] = dp[i];
+			gep[k] = ep[i];
+			gl[k] = len[i];
+		}
+		if (v6)
+			or_classify_v6(c, m, gs, gd, gdp, gp, gf, gl, gep, gv, gid, gst, nthreads, &p2);
+		else
+			or_classify_v4(c, m, gs4, gd4, gdp, gp, gf, gl, gep, gv, gid, gst, nthreads, &p2);
+		ps += p2;
+		for (size_t k = 0; k < m; k++) {
+			size_t i = idx[k];
+			verdict[i] = gv[k];
+			if (identity)
+				identity[i] = gid[k];
+			if (stage)
+				stage[i] = gst[k];
+		}
+		free(gs); free(gd); free(gp); free(gf); free(gdp); free(gep);
+		free(gl); free(gid); free(gs4); free(gd4); free(gv); free(gst);
+	}
+	for (size_t i = 0; i < n; i++) {
+		uint32_t reason;
+		int dir = (flags[i] & 1) ? METRIC_EGRESS : METRIC_INGRESS;
+		if (!st[i])
+			continue;
+		if (st[i] == FRAME_NOT_CLASSIFIED) {
+			verdict[i] = 0;
+			if (stage)
+				stage[i] = 7;
+		} else {
+			verdict[i] = st[i];
+			if (stage)
+				stage[i] = st[i] == DROP_CT_UNKNOWN_PROTO ? 4 : 5;
+		}
+		if (identity)
+			identity[i] = 0;
+		if (st[i] == FRAME_NOT_CLASSIFIED || st[i] == DROP_SNAPLEN)
+			continue;
+		/* send_drop_notify -> update_metrics(len, dir, -reason), drop.h:104 */
+		reason = (uint32_t)(-st[i]) & 0xff;
+		c->metrics[(reason * 4 + dir) * 2] += 1;
+		c->metrics[(reason * 4 + dir) * 2 + 1] += len[i];
+	}
+	if (probe_sum)
+		*probe_sum = ps;
+	free(st); free(fam); free(sa); free(da); free(pr); free(tf); free(dp); free(idx);
+	return 0;
 }

@@ -34,6 +34,7 @@ typedef struct or_config {
 	uint8_t router_ip[16];         /* ROUTER_IP (node_config.h:30) */
 	int lb_l3, lb_l4;              /* LB_L3 / LB_L4 (lxc_config.h:44-45, init.sh:352) */
 	uint32_t ipv4_loopback;        /* IPV4_LOOPBACK (node_config.h:45), network order */
+	uint8_t node_mac[6];           /* NODE_MAC (node_config.h:51) */
 } or_config;
 
 or_ctx *or_create(void);
@@ -132,6 +133,34 @@ int or_classify_v4_lb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 		      const uint8_t *flags, const uint32_t *len, const uint16_t *ep,
 		      const uint32_t *hash, int32_t *verdict, uint32_t *identity, uint8_t *stage,
 		      int nthreads, uint64_t *probe_sum);
+
+/*
+ * Raw Ethernet frames.  Per-endpoint identity of the
+ * endpoint program (lxc_config.h LXC_MAC / LXC_IPV4 / LXC_IP and which of
+ * the SMAC / DMAC / SIP checks are compiled in), 32 bytes in the layout of
+ * cgpu_lxc_info: mac[6], verify (1 SMAC, 2 DMAC, 4 SIP), pad, ipv4 (raw u32),
+ * ipv6[16], reserved.  An endpoint without one verifies nothing.
+ */
+int or_lxc_update(or_ctx *c, uint32_t ep, const void *info32);
+
+/*
+ * Frame i = the first min(len[i], stride) bytes at data + i * stride; flags
+ * bit0 = egress.  Restates, per frame, the endpoint programs' steps before
+ * ipcache (stateless, conntrack empty): see cgpu.h cgpu_frames_parse.
+ * status: 0 reached policy, 1 not classified, or the DROP_* / -errno
+ * (-4096 = a header past the stored slot).  Tuple outputs may be NULL.
+ */
+int or_frames_parse(or_ctx *c, size_t n, const uint8_t *data, uint32_t stride, const uint32_t *len,
+		    const uint8_t *flags, const uint16_t *ep, int32_t *status, uint8_t *family,
+		    uint8_t *saddr16, uint8_t *daddr16, uint16_t *dport, uint8_t *proto,
+		    uint8_t *tflags);
+
+/* or_frames_parse, then or_classify_v4 / or_classify_v6 of the tuples that
+ * reach policy; the others get verdict = status, identity 0, stage 5 (4 for
+ * DROP_CT_UNKNOWN_PROTO), or verdict 0 / stage 7 when not classified. */
+int or_classify_frames(or_ctx *c, size_t n, const uint8_t *data, uint32_t stride,
+		       const uint32_t *len, const uint8_t *flags, const uint16_t *ep, int32_t *verdict,
+		       uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum);
 
 /* metrics {reason, dir} -> {count, bytes}; out is [256][4][2] u64 */
 void or_metrics_read(or_ctx *c, uint64_t *out);

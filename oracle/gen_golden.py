@@ -801,6 +801,59 @@ def gen_classify_lb_fixture(pol, lbls, rng):
                 **{"t_" + k: v for k, v in t.items()}, **out)
 
 
+# ------------------------------------------------------------- raw frames
+FRAME_VARIANTS = ("_ct", "_noct", "_nover")  # oracle/Makefile FRAME_VARIANTS
+
+
+def load_ref_frame():
+    libs = {}
+    for v in FRAME_VARIANTS:
+        lib = C.CDLL(os.path.join(HERE, "_ref", f"libref_frame{v}.so"))
+        lib.ref_frame_parse.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_int),
+                                        C.c_void_p, C.c_void_p, C.POINTER(C.c_uint16),
+                                        C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]
+        lib.ref_frame_config.argtypes = [C.c_void_p]
+        lib.ref_frame_config.restype = None
+        libs[v] = lib
+    return libs
+
+
+def gen_frames_fixture(libs, rng, n=6000):
+    """Frames (synth.make_frames: every header class and truncation point)
+    through the reference's endpoint-program steps before ipcache, under the
+    endpoint config as written, without CONNTRACK, and without the
+    SMAC/DMAC/SIP checks (harness_frame.c)."""
+    from cilium_amd import synth
+    f = synth.make_frames(rng, n, width=256)
+    f["len"] = np.maximum(f["len"], 14).astype(np.uint32)  # the skb always holds an Ethernet header
+    out = {"data": f["data"], "len": f["len"], "flags": f["flags"], "ep": f["ep"]}
+    fam, dp, pr, fg = C.c_int(), C.c_uint16(), C.c_uint8(), C.c_uint8()
+    sa, da = C.create_string_buffer(16), C.create_string_buffer(16)
+    for v, lib in libs.items():
+        cfg = C.create_string_buffer(33)
+        lib.ref_frame_config(cfg)
+        out[f"{v[1:]}_config"] = np.frombuffer(cfg.raw, np.uint8).copy()
+        res = {k: np.zeros(n, dt) for k, dt in (("status", np.int32), ("family", np.uint8),
+                                                ("dport", np.uint16), ("proto", np.uint8),
+                                                ("frag", np.uint8))}
+        res["saddr"] = np.zeros((n, 16), np.uint8)
+        res["daddr"] = np.zeros((n, 16), np.uint8)
+        for i in range(n):
+            ln = int(f["len"][i])
+            buf = f["data"][i].tobytes()[:ln].ljust(ln, b"\0")
+            r = lib.ref_frame_parse(buf, ln, int(f["flags"][i]), C.byref(fam), sa, da,
+                                    C.byref(dp), C.byref(pr), C.byref(fg))
+            res["status"][i] = r
+            if r == 0:
+                res["family"][i], res["dport"][i] = fam.value, dp.value
+                res["proto"][i], res["frag"][i] = pr.value, fg.value
+                res["saddr"][i] = np.frombuffer(sa.raw, np.uint8)
+                res["daddr"][i] = np.frombuffer(da.raw, np.uint8)
+        for k, a in res.items():
+            out[f"{v[1:]}_{k}"] = a
+    return out
+
+
 def save(name, d):
     path = os.path.join(OUT, name)
     np.savez_compressed(path, **d)
@@ -831,6 +884,9 @@ def main():
     manifest["files"]["lb4.npz"] = save("lb4.npz", gen_lb_fixture(lbvars, lbls, rng_lb))
     manifest["files"]["classify_v4_lb.npz"] = save(
         "classify_v4_lb.npz", gen_classify_lb_fixture(pol, lbls, rng_lb))
+    # raw frames, its own stream
+    rng_fr = np.random.Generator(np.random.PCG64(SEED + 0xF2))
+    manifest["files"]["frames.npz"] = save("frames.npz", gen_frames_fixture(load_ref_frame(), rng_fr))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -24,6 +24,7 @@ class OrConfig(C.Structure):
         ("dyn4", C.c_int), ("fix4", C.c_int), ("dyn6", C.c_int), ("fix6", C.c_int),
         ("router_ip", C.c_uint8 * 16),
         ("lb_l3", C.c_int), ("lb_l4", C.c_int), ("ipv4_loopback", C.c_uint32),
+        ("node_mac", C.c_uint8 * 6),
     ]
 
 
@@ -68,6 +69,10 @@ def lib():
         L.or_flow_hash.restype = C.c_uint32
         L.or_lb4.argtypes = [vp, C.c_int, sz] + [vp] * 13 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_classify_v4_lb.argtypes = [vp, sz] + [vp] * 12 + [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_lxc_update.argtypes = [vp, C.c_uint32, vp]
+        L.or_frames_parse.argtypes = [vp, sz, vp, C.c_uint32] + [vp] * 10
+        L.or_classify_frames.argtypes = [vp, sz, vp, C.c_uint32] + [vp] * 6 + [
+            C.c_int, C.POINTER(C.c_uint64)]
         L.or_metrics_read.argtypes = [vp, vp]
         L.or_counters_reset.argtypes = [vp]
         _lib = L
@@ -93,8 +98,8 @@ class Oracle:
 
     def configure(self, **kw):
         for k, v in kw.items():
-            if k == "router_ip":
-                self.cfg.router_ip[:] = bytes(v)
+            if k in ("router_ip", "node_mac"):
+                getattr(self.cfg, k)[:] = bytes(v)
                 continue
             setattr(self.cfg, k, v)
         self.L.or_set_config(self.h, C.byref(self.cfg))
@@ -240,6 +245,41 @@ class Oracle:
         rc = self.L.or_classify_v4_lb(self.h, n, *[_p(a) for a in arrs], _p(h), _p(verdict),
                                       _p(identity), _p(stage), nthreads, C.byref(probes))
         assert rc == 0, rc
+        return verdict, identity, stage, probes.value
+
+    # --- raw frames ---
+    def lxc_update(self, ep, info):
+        return self.L.or_lxc_update(self.h, ep, _b(info))
+
+    @staticmethod
+    def _frame_cols(f):
+        data = np.ascontiguousarray(f["data"], np.uint8)
+        assert data.ndim == 2
+        return (data, np.ascontiguousarray(f["len"], np.uint32),
+                np.ascontiguousarray(f["flags"], np.uint8), np.ascontiguousarray(f["ep"], np.uint16))
+
+    def frames_parse(self, f):
+        data, ln, fl, ep = self._frame_cols(f)
+        n = len(ln)
+        out = {"status": np.empty(n, np.int32), "family": np.empty(n, np.uint8),
+               "saddr": np.empty((n, 16), np.uint8), "daddr": np.empty((n, 16), np.uint8),
+               "dport": np.empty(n, np.uint16), "proto": np.empty(n, np.uint8),
+               "flags": np.empty(n, np.uint8)}
+        self.L.or_frames_parse(self.h, n, _p(data), data.shape[1], _p(ln), _p(fl), _p(ep),
+                               *[_p(out[k]) for k in ("status", "family", "saddr", "daddr",
+                                                      "dport", "proto", "flags")])
+        return out
+
+    def classify_frames(self, f, nthreads=1):
+        data, ln, fl, ep = self._frame_cols(f)
+        n = len(ln)
+        verdict = np.empty(n, np.int32)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        self.L.or_classify_frames(self.h, n, _p(data), data.shape[1], _p(ln), _p(fl), _p(ep),
+                                  _p(verdict), _p(identity), _p(stage), nthreads,
+                                  C.byref(probes))
         return verdict, identity, stage, probes.value
 
     def metrics(self):

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from cilium_amd import build, layouts as L
-from cilium_amd._abi import PROTOS, TuplesV4, lib
+from cilium_amd._abi import Frames, PROTOS, TuplesV4, lib
 from cilium_amd.engine import (CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX, BPF_EXIST,
                                BPF_NOEXIST, CIDRMap, Engine, IPCacheMap, PolicyMap)
 
@@ -54,6 +54,35 @@ def test_host_only_context_has_no_cpu_path():
     assert b"no CPU classification path" in L_.cgpu_last_error()
     assert L_.cgpu_prefilter_v4(e.h, None, None, None, 1, None, None) == -errno.ENODEV
     assert L_.cgpu_commit(e.h, None) == -errno.ENODEV
+    fr = Frames(0, 0, 0, 0, 64, 0)
+    assert L_.cgpu_classify_frames(e.h, C.byref(fr), 1, None, None, None, None) == -errno.ENODEV
+    assert L_.cgpu_frames_parse(e.h, C.byref(fr), 1, None, None) == -errno.ENODEV
+
+
+def test_lxc_info_semantics():
+    """Per-endpoint lxc_config.h identity (cgpu_lxc_*): update replaces,
+    lookup round-trips the 32-byte record, delete of a missing id is
+    -ENOENT, unknown verify bits / ids beyond the u16 ep column are -EINVAL,
+    and the record counts in the replica checksum."""
+    from cilium_amd import synth
+    e = Engine(device=-1)
+    info = L.lxc_info(synth.LXC_MAC, synth.LXC_IPV4_RAW, synth.LXC_IP6, 7)
+    assert e.lxc_lookup(3) is None
+    assert e.lxc_update(3, info) == 0
+    got = e.lxc_lookup(3)
+    assert got.tobytes() == info.tobytes()
+    info2 = info.copy()
+    info2["verify"] = 1
+    assert e.lxc_update(3, info2) == 0
+    assert e.lxc_lookup(3)["verify"] == 1
+    assert e.lxc_delete(3) == 0
+    assert e.lxc_delete(3) == -errno.ENOENT
+    bad = info.copy()
+    bad["verify"] = 8
+    rc = lib().cgpu_lxc_update(e.h, 1, bad.tobytes())
+    assert rc == -errno.EINVAL
+    assert lib().cgpu_lxc_update(e.h, 65536, info.tobytes()) == -errno.EINVAL
+    assert bytes(e.cfg.node_mac) == L.NODE_MAC
 
 
 def test_policy_map_semantics():
