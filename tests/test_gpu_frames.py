@@ -100,7 +100,7 @@ def test_classify_frames_vs_restatement(torch_cuda, gate, verify):
     np.testing.assert_array_equal(v, ov)
     np.testing.assert_array_equal(idt, oi)
     np.testing.assert_array_equal(st, ost)
-    assert len(np.unique(st)) >= 6
+    assert len(np.unique(st)) >= 5
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     for k, en, ep in zip(T.pol_keys[::7], T.pol_entries[::7], T.pol_ep[::7]):
         rc, got = e.policy_lookup(int(ep), k)
