@@ -82,10 +82,38 @@ F_FRAGMENT = 2
 # prefilter packet flags
 PKT_OK, PKT_TRUNCATED, PKT_NOT_IP = 0, 1, 2
 
+# conntrack: struct ipv4_ct_tuple (packed, 14 B) and struct
+# ct_entry (56 B), bpf/lib/common.h:359-408; the map cilium_ct4_global
+CT4_TUPLE = np.dtype([("daddr", "<u4"), ("saddr", "<u4"), ("dport", "<u2"), ("sport", "<u2"),
+                      ("nexthdr", "u1"), ("flags", "u1")])
+assert CT4_TUPLE.itemsize == 14
+CT_ENTRY = np.dtype([("rx_packets", "<u8"), ("rx_bytes", "<u8"), ("tx_packets", "<u8"),
+                     ("tx_bytes", "<u8"), ("lifetime", "<u4"), ("bits", "<u2"),
+                     ("rev_nat_index", "<u2"), ("slave", "<u2"), ("tx_flags_seen", "u1"),
+                     ("rx_flags_seen", "u1"), ("src_sec_id", "<u4"), ("last_tx_report", "<u4"),
+                     ("last_rx_report", "<u4")])
+assert CT_ENTRY.itemsize == 56
+# ct_entry bit field (common.h:385-390)
+CTB_RX_CLOSING, CTB_TX_CLOSING, CTB_NAT46, CTB_LB_LOOPBACK, CTB_SEEN_NON_SYN = 1, 2, 4, 8, 16
+# ct_lookup4 results (common.h:331-336); 255 = ct_lookup4 failed (DROP_CT_UNKNOWN_PROTO)
+CT_NEW, CT_ESTABLISHED, CT_REPLY, CT_RELATED, CT_NONE = 0, 1, 2, 3, 255
+TUPLE_F_OUT, TUPLE_F_IN, TUPLE_F_RELATED = 0, 1, 2
+DROP_CT_CREATE_FAILED = -155
+TCP_FIN, TCP_SYN, TCP_RST, TCP_PSH, TCP_ACK = 0x01, 0x02, 0x04, 0x08, 0x10
+CT_MAX_GLOBAL = 1000000  # pkg/maps/ctmap/ctmap.go:101 MapNumEntriesGlobal
+
+
+def ct_sorted(keys: np.ndarray, vals: np.ndarray):
+    """Dump of a CT map in a canonical order (key bytes) for comparisons."""
+    kb = np.ascontiguousarray(keys).view(np.uint8).reshape(len(keys), 14)
+    order = np.lexsort(kb.T[::-1])
+    return keys[order], vals[order]
+
+
 # per-endpoint identity of the endpoint program (cgpu_lxc_info, include/cgpu.h;
 # lxc_config.h LXC_MAC / LXC_IPV4 / LXC_IP, bpf/lib/lxc.h:31-89)
 LXC_INFO = np.dtype([("mac", "u1", (6,)), ("verify", "u1"), ("pad", "u1"), ("ipv4", "<u4"),
-                     ("ipv6", "u1", (16,)), ("reserved", "<u4")])
+                     ("ipv6", "u1", (16,)), ("sec_label", "<u4")])
 assert LXC_INFO.itemsize == 32
 VERIFY_SMAC, VERIFY_DMAC, VERIFY_SIP = 1, 2, 4
 # NODE_MAC, bpf/node_config.h:51
@@ -99,8 +127,9 @@ DROP_INVALID_EXTHDR = -156
 EFAULT_LOAD = -14
 
 
-def lxc_info(mac: bytes, ipv4_raw: int, ipv6: bytes, verify: int) -> np.ndarray:
+def lxc_info(mac: bytes, ipv4_raw: int, ipv6: bytes, verify: int, sec_label: int = 0) -> np.ndarray:
     x = np.zeros((), LXC_INFO)
+    x["sec_label"] = sec_label
     x["mac"] = np.frombuffer(bytes(mac), np.uint8)
     x["verify"] = verify
     x["ipv4"] = ipv4_raw

@@ -586,3 +586,74 @@ def frames_to_device(f: dict, device="cuda"):
             "len": torch.from_numpy(np.ascontiguousarray(f["len"], np.uint32).view(np.int32)).to(device),
             "flags": torch.from_numpy(np.ascontiguousarray(f["flags"], np.uint8)).to(device),
             "ep": torch.from_numpy(np.ascontiguousarray(f["ep"], np.uint16).view(np.int16)).to(device)}
+
+
+# ---------------------------------------------------------------- conntrack
+def make_ct_stream(rng, n_conn: int, locals_be: np.ndarray, remotes_be: np.ndarray,
+                   mean_pkts: float = 8.0, span: float = 0.02, frag_frac: float = 0.005,
+                   icmp_err_frac: float = 0.03, other_frac: float = 0.01):
+    """A packet stream of n_conn connections for the stateful path (SURVEY §8f
+    row 3), vectorized.  Each connection is between a local endpoint address
+    (locals_be[ep], network order) and a remote address, opened from either
+    side, with ~Geom(1/mean_pkts) packets that alternate direction: TCP with
+    SYN / SYN-ACK / ACK / PSH-ACK and a closing FIN or RST, UDP, ICMP echo
+    (request, reply) and, in the reply direction, ICMP errors (types 3, 11,
+    12) that conntrack relates to the connection; a few packets of an
+    untracked protocol.  Connections overlap in time (start uniform in
+    [0, 1), lifetime ~span), so packets of one connection are interleaved
+    with others but stay in order.  Columns as cgpu_classify_v4_ct takes
+    them: saddr, daddr, sport, dport (network order), proto, l4b (TCP header
+    bytes 12-13 as a little-endian u16, or the ICMP type), flags (CGPU_F_EGRESS | CGPU_F_FRAGMENT), len, ep."""
+    E = len(locals_be)
+    ep = rng.integers(0, E, n_conn)
+    loc = np.asarray(locals_be, np.uint32)[ep]
+    rem = np.asarray(remotes_be, np.uint32)[rng.integers(0, len(remotes_be), n_conn)]
+    u = rng.random(n_conn)
+    cproto = np.select([u < 0.70, u < 0.90, u < 1.0 - other_frac], [6, 17, 1], 47).astype(np.uint8)
+    init_eg = rng.random(n_conn) < 0.6
+    eph = rng.integers(1024, 65536, n_conn)
+    well = zipf_ports(rng, n_conn)
+    lport = np.where(init_eg, eph, well).astype(np.uint16)
+    rport = np.where(init_eg, well, eph).astype(np.uint16)
+    k = rng.geometric(1.0 / mean_pkts, n_conn).astype(np.int64)
+    total = int(k.sum())
+    conn = np.repeat(np.arange(n_conn), k)
+    first = np.cumsum(k) - k
+    j = np.arange(total) - np.repeat(first, k)
+    last = j == k[conn] - 1
+    orig = (j == 0) | (rng.random(total) < 0.55)
+    egress = np.where(orig, init_eg[conn], ~init_eg[conn])
+    proto = cproto[conn].copy()
+    r = rng.random(total)
+    # TCP flags byte (tcphdr byte 13)
+    tcpf = np.where(j == 0, L.TCP_SYN, np.where((j == 1) & ~orig, L.TCP_SYN | L.TCP_ACK,
+                    np.where(r < 0.5, L.TCP_ACK, L.TCP_ACK | L.TCP_PSH)))
+    r2 = rng.random(total)
+    tcpf = np.where(last & (j > 0) & (r2 < 0.3), L.TCP_FIN | L.TCP_ACK, tcpf)
+    tcpf = np.where(last & (j > 0) & (r2 > 0.95), L.TCP_RST, tcpf)
+    # ICMP: echo request (8, some timestamp 13) one way, echo reply (0) back
+    icmpt = np.where(orig, np.where(r < 0.9, 8, 13), 0)
+    # errors related to any connection, in the reply direction
+    err = ~orig & (rng.random(total) < icmp_err_frac)
+    proto = np.where(err, 1, proto).astype(np.uint8)
+    icmpt = np.where(err, rng.choice(np.array([3, 11, 12]), total), icmpt)
+    # TCP: header bytes 12-13 as loaded (doff << 4, NS bit sometimes set | flags << 8)
+    ns = (rng.random(total) < 0.02).astype(np.int64)
+    tcpw = (5 << 4) | ns | (tcpf.astype(np.int64) << 8)
+    l4b = np.where(proto == 6, tcpw, np.where(proto == 1, icmpt, 0)).astype(np.uint16)
+    lc, rc = loc[conn], rem[conn]
+    saddr = np.where(egress, lc, rc).astype(np.uint32)
+    daddr = np.where(egress, rc, lc).astype(np.uint32)
+    lp, rp = lport[conn].byteswap(), rport[conn].byteswap()
+    sport = np.where(egress, lp, rp).astype(np.uint16)
+    dport = np.where(egress, rp, lp).astype(np.uint16)
+    frag = (~egress) & (rng.random(total) < frag_frac)
+    # interleave: connection start + in-connection gaps, stable by time
+    t = rng.random(n_conn)[conn] + span * (j + rng.random(total)) / k[conn]
+    order = np.argsort(t, kind="stable")
+    out = {
+        "saddr": saddr, "daddr": daddr, "sport": sport, "dport": dport, "proto": proto,
+        "l4b": l4b, "flags": (egress.astype(np.uint8) | (frag.astype(np.uint8) << 1)),
+        "len": rng.integers(64, 1501, total).astype(np.uint32), "ep": ep[conn].astype(np.uint16),
+    }
+    return {key: np.ascontiguousarray(v[order]) for key, v in out.items()}

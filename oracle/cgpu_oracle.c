@@ -355,6 +355,8 @@ struct or_ctx {
 	struct ohash lb;            /* lb4_key (8 B) -> lb4_service (12 B) */
 	uint8_t *lxcinfo;           /* [n_lxcinfo][32] per-endpoint identity */
 	size_t n_lxcinfo;
+	struct ohash ct;            /* ipv4_ct_tuple (14 B) -> ct_entry (56 B) */
+	size_t ct_max;              /* CT_MAP_SIZE */
 	uint64_t metrics[N_METRICS];
 };
 
@@ -395,6 +397,8 @@ or_ctx *or_create(void)
 	oh_init(&c->fix6, 20, 1);
 	oh_init(&c->lxc, 20, 1);
 	oh_init(&c->lb, 8, 12);
+	oh_init(&c->ct, 14, 56);
+	c->ct_max = 1000000; /* ctmap.go:101 MapNumEntriesGlobal */
 	return c;
 }
 
@@ -409,6 +413,7 @@ void or_destroy(or_ctx *c)
 	oh_destroy(&c->fix6);
 	oh_destroy(&c->lxc);
 	oh_destroy(&c->lb);
+	oh_destroy(&c->ct);
 	for (size_t i = 0; i < c->n_ep; i++)
 		oh_destroy(&c->policy[i]);
 	free(c->policy);
@@ -1626,5 +1631,394 @@ int or_classify_frames(or_ctx *c, size_t n, const uint8_t *data, uint32_t stride
 	if (probe_sum)
 		*probe_sum = ps;
 	free(st); free(fam); free(sa); free(da); free(pr); free(tf); free(dp); free(idx);
+	return 0;
+}
+
+/* ====================================================================== */
+/* Conntrack on the classification path                 */
+/* bpf/lib/conntrack.h:61-744 under lxc_config.h (CONNTRACK,               */
+/* CONNTRACK_ACCOUNTING) with NEEDS_TIMEOUT (lib/common.h:33)              */
+/* ====================================================================== */
+#define CT_LIFETIME_TCP 21600   /* conntrack.h:31-35 */
+#define CT_LIFETIME_NONTCP 60
+#define CT_SYN_TIMEOUT 60
+#define CT_CLOSE_TIMEOUT 10
+#define CT_REPORT_INTERVAL 5
+#define TUPLE_F_OUT 0           /* conntrack.h:63-66 */
+#define TUPLE_F_IN 1
+#define TUPLE_F_RELATED 2
+#define CT_EGRESS 0             /* common.h:327-329 */
+#define CT_INGRESS 1
+#define CT_NEW 0                /* common.h:331-336 */
+#define CT_ESTABLISHED 1
+#define CT_REPLY 2
+#define CT_RELATED 3
+#define ACTION_UNSPEC 0         /* conntrack.h:68-72 */
+#define ACTION_CREATE 1
+#define ACTION_CLOSE 2
+#define DROP_CT_CREATE_FAILED (-155)
+/*
+ * union tcp_flags (conntrack.h:74-88) declares fin, syn, rst ... as bit-field
+ * MEMBERS OF A UNION, so every one of them sits at bit 0 of the loaded
+ * 16-bit word (C11 6.7.2.1: each union member starts at offset 0): .fin,
+ * .syn and .rst all read bit 0 of TCP header byte 12 (the NS bit below doff),
+ * and only .lower_bits (byte 13) carries the real flags.  The restatement
+ * keeps that behaviour: l4w = bytes 12-13 as loaded.
+ */
+#define TF_BIT0(w) ((w) & 1u)
+#define TF_LOWER(w) ((uint8_t)((w) >> 8))
+
+/* struct ct_entry, bpf/lib/common.h:380-408 (56 B) */
+struct ct_val {
+	uint64_t rx_packets, rx_bytes, tx_packets, tx_bytes;
+	uint32_t lifetime;
+	uint16_t bits; /* rx_closing:1 tx_closing:1 nat46:1 lb_loopback:1 seen_non_syn:1 */
+	uint16_t rev_nat_index, slave;
+	uint8_t tx_flags_seen, rx_flags_seen;
+	uint32_t src_sec_id, last_tx_report, last_rx_report;
+};
+_Static_assert(sizeof(struct ct_val) == 56, "ct_entry layout");
+#define CTB_RX_CLOSING 1u
+#define CTB_TX_CLOSING 2u
+#define CTB_SEEN_NON_SYN 16u
+
+/* struct ipv4_ct_tuple, common.h:359-366 (14 B, packed) */
+struct ct_key {
+	uint32_t daddr, saddr;
+	uint16_t dport, sport;
+	uint8_t nexthdr, flags;
+};
+
+static void ct_key_bytes(const struct ct_key *k, uint8_t *b)
+{
+	memcpy(b, &k->daddr, 4);
+	memcpy(b + 4, &k->saddr, 4);
+	memcpy(b + 8, &k->dport, 2);
+	memcpy(b + 10, &k->sport, 2);
+	b[12] = k->nexthdr;
+	b[13] = k->flags;
+}
+
+void or_ct_set_max(or_ctx *c, size_t max_elem) { c->ct_max = max_elem; }
+size_t or_ct4_count(or_ctx *c) { return c->ct.n; }
+
+/* bpf(2) BPF_ANY update of cilium_ct4_*: -E2BIG for a new key past max_elem
+ * (kernel htab_map_update_elem) */
+int or_ct4_update(or_ctx *c, const void *key14, const void *val56)
+{
+	if (!oh_get(&c->ct, key14) && c->ct.n >= c->ct_max)
+		return -E2BIG;
+	return oh_update(&c->ct, key14, val56);
+}
+
+int or_ct4_delete(or_ctx *c, const void *key14) { return oh_delete(&c->ct, key14); }
+
+int or_ct4_lookup(or_ctx *c, const void *key14, void *val56_out)
+{
+	const uint8_t *v = oh_get(&c->ct, key14);
+	if (!v)
+		return -ENOENT;
+	memcpy(val56_out, v, 56);
+	return 0;
+}
+
+size_t or_ct4_dump(or_ctx *c, void *keys14, void *vals56, size_t max)
+{
+	size_t k = 0;
+	for (size_t i = 0; i < c->ct.cap && k < max; i++) {
+		if (!c->ct.used[i])
+			continue;
+		memcpy((uint8_t *)keys14 + k * 14, c->ct.keys + i * 14, 14);
+		memcpy((uint8_t *)vals56 + k * 56, c->ct.vals + i * 56, 56);
+		k++;
+	}
+	return k;
+}
+
+/* ctmap.go:306-327 doFiltering with RemoveExpired: delete entries whose
+ * lifetime < time; returns the number deleted */
+size_t or_ct4_gc(or_ctx *c, uint32_t time)
+{
+	size_t del = 0;
+	for (int again = 1; again;) {
+		again = 0;
+		for (size_t i = 0; i < c->ct.cap; i++) {
+			struct ct_val v;
+			uint8_t key[14];
+			if (!c->ct.used[i])
+				continue;
+			memcpy(&v, c->ct.vals + i * 56, 56);
+			if (v.lifetime < time) {
+				memcpy(key, c->ct.keys + i * 14, 14);
+				oh_delete(&c->ct, key);
+				del++;
+				again = 1; /* backward-shift deletion moved entries */
+				break;
+			}
+		}
+	}
+	return del;
+}
+
+/* __ct_update_timeout, conntrack.h:104-161 (seen = flags.lower_bits) */
+static int ct_touch(struct ct_val *e, uint32_t now, uint32_t lifetime, int dir, uint8_t seen)
+{
+	uint8_t *acc = dir == CT_INGRESS ? &e->rx_flags_seen : &e->tx_flags_seen;
+	uint32_t *last = dir == CT_INGRESS ? &e->last_rx_report : &e->last_tx_report;
+	e->lifetime = now + lifetime;
+	seen |= *acc;
+	if (*last + CT_REPORT_INTERVAL < now || *acc != seen) {
+		*last = now;
+		*acc = seen;
+		return 1;
+	}
+	return 0;
+}
+
+/* ct_update_timeout, conntrack.h:169-185 (syn = flags.syn = bit 0) */
+static int ct_timeout(struct ct_val *e, uint32_t now, int tcp, int dir, uint16_t w)
+{
+	uint32_t lifetime = CT_LIFETIME_NONTCP;
+	if (tcp) {
+		if (!TF_BIT0(w))
+			e->bits |= CTB_SEEN_NON_SYN;
+		lifetime = (e->bits & CTB_SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+	}
+	return ct_touch(e, now, lifetime, dir, TF_LOWER(w));
+}
+
+static inline int ct_alive(const struct ct_val *e)
+{
+	return !(e->bits & CTB_RX_CLOSING) || !(e->bits & CTB_TX_CLOSING);
+}
+
+/* __ct_lookup, conntrack.h:198-259: 1 = found (entry updated), 0 = miss */
+static int ct_lookup_one(or_ctx *c, const struct ct_key *k, int action, int dir, int tcp,
+			 uint16_t w, uint32_t len, uint32_t now)
+{
+	uint8_t kb[14];
+	uint8_t *p;
+	struct ct_val e;
+	ct_key_bytes(k, kb);
+	p = oh_get(&c->ct, kb);
+	if (!p)
+		return 0;
+	memcpy(&e, p, 56);
+	if (ct_alive(&e))
+		ct_timeout(&e, now, tcp, dir, w);
+	if (dir == CT_INGRESS) { /* CONNTRACK_ACCOUNTING */
+		e.rx_packets += 1;
+		e.rx_bytes += len;
+	} else {
+		e.tx_packets += 1;
+		e.tx_bytes += len;
+	}
+	if (action == ACTION_CREATE) {
+		if (e.bits & (CTB_RX_CLOSING | CTB_TX_CLOSING)) {
+			e.bits &= (uint16_t)~(CTB_RX_CLOSING | CTB_TX_CLOSING);
+			ct_timeout(&e, now, tcp, dir, w);
+		}
+	} else if (action == ACTION_CLOSE) {
+		e.bits |= dir == CT_INGRESS ? CTB_RX_CLOSING : CTB_TX_CLOSING;
+		if (!ct_alive(&e))
+			ct_touch(&e, now, CT_CLOSE_TIMEOUT, dir, TF_LOWER(w));
+	}
+	memcpy(p, &e, 56);
+	return 1;
+}
+
+static void ct_reverse(struct ct_key *k)
+{
+	uint32_t a = k->saddr;
+	uint16_t p = k->sport;
+	k->saddr = k->daddr;
+	k->daddr = a;
+	k->sport = k->dport;
+	k->dport = p;
+	k->flags ^= TUPLE_F_IN;
+}
+
+/* ct_create4, conntrack.h:653-744 (ct_state: no service, addr 0) */
+static int ct_create(or_ctx *c, const struct ct_key *k, int dir, uint32_t src_sec_id,
+		     uint32_t len, uint32_t now, uint64_t *ops)
+{
+	struct ct_val e;
+	struct ct_key ik;
+	uint8_t kb[14];
+	int tcp = k->nexthdr == PROTO_TCP;
+	memset(&e, 0, sizeof(e));
+	ct_timeout(&e, now, tcp, dir, tcp ? 1u : 0u); /* seen_flags.syn = is_tcp: bit 0 */
+	if (dir == CT_INGRESS) {
+		e.rx_packets = 1;
+		e.rx_bytes = len;
+	} else {
+		e.tx_packets = 1;
+		e.tx_bytes = len;
+	}
+	e.src_sec_id = src_sec_id;
+	ct_key_bytes(k, kb);
+	*ops += 1;
+	if (or_ct4_update(c, kb, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	ik.daddr = k->daddr;
+	ik.saddr = k->saddr;
+	ik.nexthdr = PROTO_ICMP;
+	ik.sport = ik.dport = 0;
+	ik.flags = k->flags | TUPLE_F_RELATED;
+	e.bits |= CTB_SEEN_NON_SYN;
+	ct_key_bytes(&ik, kb);
+	*ops += 1;
+	if (or_ct4_update(c, kb, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	return 0;
+}
+
+/*
+ * Stateful IPv4 classification, packets in order (the sequence the
+ * reference's programs see): see cgpu.h cgpu_classify_v4_ct and
+ * oracle/ref/harness_ct.c for the composition.  l4b: TCP flags byte
+ * (tcphdr byte 13) or ICMP type.  ct_ret: CT_NEW..CT_RELATED, or 255 when
+ * ct_lookup4 failed (DROP_CT_UNKNOWN_PROTO).  *probe_sum counts the
+ * reference's map operations: ipcache, policy probes, CT lookups / updates /
+ * deletes.
+ */
+int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+		      const uint16_t *ep, uint32_t now, int32_t *verdict, uint8_t *ct_ret,
+		      uint32_t *identity, uint8_t *stage, uint64_t *probe_sum)
+{
+	const or_config *cfg = &c->cfg;
+	uint64_t ops = 0;
+	for (size_t i = 0; i < n; i++) {
+		int egress = flags[i] & 1, frag = (flags[i] >> 1) & 1;
+		int dir = egress ? CT_EGRESS : CT_INGRESS;
+		int mdir = egress ? METRIC_EGRESS : METRIC_INGRESS;
+		uint8_t pr = proto[i];
+		struct ohash *h = ep[i] < c->n_ep ? &c->policy[ep[i]] : NULL;
+		struct ct_key k;
+		int action = ACTION_UNSPEC, tcp = pr == PROTO_TCP, ret;
+		uint16_t w = 0; /* union tcp_flags as loaded (zero unless TCP) */
+		int32_t v, fin;
+		uint32_t id;
+		struct pol_res r;
+
+		/* ct_lookup4, conntrack.h:441-561 */
+		k.daddr = daddr[i];
+		k.saddr = saddr[i];
+		k.nexthdr = pr;
+		k.flags = egress ? TUPLE_F_IN : TUPLE_F_OUT;
+		if (pr == PROTO_ICMP) {
+			uint8_t type = (uint8_t)l4b[i];
+			k.sport = k.dport = 0;
+			if (type == 3 || type == 11 || type == 12) { /* DEST_UNREACH, TIME_EXCEEDED, PARAMETERPROB */
+				k.flags |= TUPLE_F_RELATED;
+			} else if (type == 0) { /* ECHOREPLY */
+				k.dport = 8;   /* ICMP_ECHO */
+			} else {
+				if (type == 8)
+					k.sport = 8;
+				action = ACTION_CREATE;
+			}
+		} else if (pr == PROTO_TCP || pr == PROTO_UDP) {
+			k.dport = sport[i]; /* skb_load_bytes(off, &tuple->dport, 4) */
+			k.sport = dport[i];
+			if (tcp) {
+				w = l4b[i];
+				/* tcp_flags.rst || tcp_flags.fin: both bit 0 */
+				action = TF_BIT0(w) ? ACTION_CLOSE : ACTION_CREATE;
+			} else {
+				action = ACTION_CREATE;
+			}
+		} else {
+			verdict[i] = DROP_CT_UNKNOWN_PROTO;
+			ct_ret[i] = 255;
+			if (identity)
+				identity[i] = 0;
+			if (stage)
+				stage[i] = 4;
+			c->metrics[(137 * 4 + mdir) * 2] += 1;
+			c->metrics[(137 * 4 + mdir) * 2 + 1] += len[i];
+			continue;
+		}
+		ops += 1;
+		if (ct_lookup_one(c, &k, action, dir, tcp, w, len[i], now)) {
+			ret = (k.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+		} else {
+			ct_reverse(&k);
+			ops += 1;
+			ret = ct_lookup_one(c, &k, action, dir, tcp, w, len[i], now) ? CT_ESTABLISHED
+											 : CT_NEW;
+		}
+
+		if (egress) { /* bpf_lxc.c:484-500 */
+			const uint8_t *info = ipcache4(c, daddr[i]);
+			uint32_t label = 0;
+			if (info)
+				memcpy(&label, info, 4);
+			if (info && label)
+				id = label;
+			else if ((daddr[i] & cfg->ipv4_cluster_mask) == cfg->ipv4_cluster_range)
+				id = cfg->cluster_id;
+			else
+				id = cfg->world_id;
+			ops += 1;
+			r = policy_access(h, id, k.dport, pr, 1, 0, len[i]);
+		} else { /* bpf_netdev.c:374-404 */
+			uint32_t src = cfg->ingress_src_identity;
+			if (src < cfg->health_id) {
+				const uint8_t *info = ipcache4(c, saddr[i]);
+				ops += 1;
+				if (info) {
+					uint32_t label;
+					memcpy(&label, info, 4);
+					if (label && label != cfg->cluster_id && label != cfg->host_id)
+						src = label;
+				}
+			}
+			id = cfg->ingress_secctx_world ? cfg->world_id : src;
+			r = policy_access(h, id, k.dport, pr, 0, frag, len[i]);
+		}
+		ops += (uint64_t)r.probes;
+		v = r.ret >= 0 ? r.ret : DROP_POLICY;
+
+		/* bpf_lxc.c:506-537 (egress), :918-950 (ingress) */
+		if (ret != CT_REPLY && ret != CT_RELATED && v < 0) {
+			if (ret == CT_ESTABLISHED) {
+				uint8_t kb[14];
+				ct_key_bytes(&k, kb);
+				ops += 1;
+				oh_delete(&c->ct, kb);
+			}
+			fin = DROP_POLICY;
+		} else {
+			int cr = 0;
+			if (ret == CT_NEW) {
+				uint32_t sec = 0;
+				if (egress && ep[i] < c->n_lxcinfo)
+					memcpy(&sec, c->lxcinfo + (size_t)ep[i] * 32 + 28, 4); /* SECLABEL */
+				cr = ct_create(c, &k, dir, egress ? sec : id, len[i], now, &ops);
+			}
+			if (cr < 0)
+				fin = cr;
+			else if (v > 0 && (egress || ret == CT_NEW || ret == CT_ESTABLISHED))
+				fin = v; /* redirect_to_proxy */
+			else
+				fin = 0;
+		}
+		verdict[i] = fin;
+		ct_ret[i] = (uint8_t)ret;
+		if (identity)
+			identity[i] = id;
+		if (stage)
+			stage[i] = (uint8_t)r.stage;
+		{
+			uint32_t reason = fin < 0 ? (uint32_t)(-fin) & 0xff : 0;
+			c->metrics[(reason * 4 + mdir) * 2] += 1;
+			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
+		}
+	}
+	if (probe_sum)
+		*probe_sum = ops;
 	return 0;
 }

@@ -162,6 +162,36 @@ int or_classify_frames(or_ctx *c, size_t n, const uint8_t *data, uint32_t stride
 		       const uint32_t *len, const uint8_t *flags, const uint16_t *ep, int32_t *verdict,
 		       uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum);
 
+/*
+ * Conntrack: the map cilium_ct4_global with raw struct
+ * ipv4_ct_tuple (14 B) -> struct ct_entry (56 B), bpf/lib/common.h:359-408.
+ * Updates are BPF_ANY; a new key past max_elem fails with -E2BIG.
+ */
+void or_ct_set_max(or_ctx *c, size_t max_elem);
+int or_ct4_update(or_ctx *c, const void *key14, const void *val56);
+int or_ct4_delete(or_ctx *c, const void *key14);
+int or_ct4_lookup(or_ctx *c, const void *key14, void *val56_out);
+size_t or_ct4_count(or_ctx *c);
+size_t or_ct4_dump(or_ctx *c, void *keys14, void *vals56, size_t max);
+/* ctmap.go GC with RemoveExpired: delete entries with lifetime < time */
+size_t or_ct4_gc(or_ctx *c, uint32_t time);
+
+/*
+ * Stateful IPv4 classification of n packets IN ORDER (the sequence the
+ * reference's programs see): ct_lookup4 -> ipcache -> policy -> reply /
+ * related skip, delete on a denied ESTABLISHED flow, ct_create4 for an
+ * allowed CT_NEW (see cgpu.h cgpu_classify_v4_ct).  sport/dport are the L4
+ * header's ports (network order), l4b TCP header bytes 12-13 as loaded
+ * (little-endian u16: byte 12 low) or the ICMP type, now
+ * the bpf_ktime_get_sec() of the batch.  The egress src_sec_id is the
+ * endpoint's SECLABEL (cgpu_lxc_info.sec_label).
+ */
+int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+		      const uint16_t *ep, uint32_t now, int32_t *verdict, uint8_t *ct_ret,
+		      uint32_t *identity, uint8_t *stage, uint64_t *probe_sum);
+
 /* metrics {reason, dir} -> {count, bytes}; out is [256][4][2] u64 */
 void or_metrics_read(or_ctx *c, uint64_t *out);
 void or_counters_reset(or_ctx *c);

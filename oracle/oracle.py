@@ -73,6 +73,19 @@ def lib():
         L.or_frames_parse.argtypes = [vp, sz, vp, C.c_uint32] + [vp] * 10
         L.or_classify_frames.argtypes = [vp, sz, vp, C.c_uint32] + [vp] * 6 + [
             C.c_int, C.POINTER(C.c_uint64)]
+        L.or_ct_set_max.argtypes = [vp, sz]
+        L.or_ct_set_max.restype = None
+        L.or_ct4_update.argtypes = [vp, vp, vp]
+        L.or_ct4_delete.argtypes = [vp, vp]
+        L.or_ct4_lookup.argtypes = [vp, vp, vp]
+        L.or_ct4_count.argtypes = [vp]
+        L.or_ct4_count.restype = sz
+        L.or_ct4_dump.argtypes = [vp, vp, vp, sz]
+        L.or_ct4_dump.restype = sz
+        L.or_ct4_gc.argtypes = [vp, C.c_uint32]
+        L.or_ct4_gc.restype = sz
+        L.or_classify_v4_ct.argtypes = [vp, sz] + [vp] * 9 + [C.c_uint32] + [vp] * 4 + [
+            C.POINTER(C.c_uint64)]
         L.or_metrics_read.argtypes = [vp, vp]
         L.or_counters_reset.argtypes = [vp]
         _lib = L
@@ -281,6 +294,52 @@ class Oracle:
                                   _p(verdict), _p(identity), _p(stage), nthreads,
                                   C.byref(probes))
         return verdict, identity, stage, probes.value
+
+    # --- conntrack ---
+    def ct_set_max(self, n):
+        self.L.or_ct_set_max(self.h, n)
+
+    def ct4_update(self, key, val):
+        return self.L.or_ct4_update(self.h, _b(key), _b(val))
+
+    def ct4_delete(self, key):
+        return self.L.or_ct4_delete(self.h, _b(key))
+
+    def ct4_lookup(self, key):
+        out = C.create_string_buffer(56)
+        r = self.L.or_ct4_lookup(self.h, _b(key), out)
+        return r, out.raw
+
+    def ct4_count(self):
+        return self.L.or_ct4_count(self.h)
+
+    def ct4_dump(self):
+        from cilium_amd import layouts as Ly
+        n = self.ct4_count()
+        keys = np.zeros(n, Ly.CT4_TUPLE)
+        vals = np.zeros(n, Ly.CT_ENTRY)
+        k = self.L.or_ct4_dump(self.h, _p(keys), _p(vals), n)
+        assert k == n
+        return Ly.ct_sorted(keys, vals)
+
+    def ct4_gc(self, time):
+        return self.L.or_ct4_gc(self.h, time)
+
+    def classify_v4_ct(self, t, now):
+        n = len(t["saddr"])
+        verdict = np.empty(n, np.int32)
+        ct_ret = np.empty(n, np.uint8)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint32), ("daddr", np.uint32), ("sport", np.uint16),
+            ("dport", np.uint16), ("proto", np.uint8), ("l4b", np.uint16), ("flags", np.uint8),
+            ("len", np.uint32), ("ep", np.uint16))]
+        rc = self.L.or_classify_v4_ct(self.h, n, *[_p(a) for a in arrs], now, _p(verdict),
+                                      _p(ct_ret), _p(identity), _p(stage), C.byref(probes))
+        assert rc == 0, rc
+        return verdict, ct_ret, identity, stage, probes.value
 
     def metrics(self):
         out = np.zeros((256, 4, 2), np.uint64)

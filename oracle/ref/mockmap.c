@@ -107,3 +107,16 @@ void *mockmap_lookup(struct mockmap *m, const void *key)
 	}
 	return best < 0 ? NULL : m->vals + best * m->vsz;
 }
+
+int mockmap_delete(struct mockmap *m, const void *key)
+{
+	long i = find_same(m, key);
+	if (i < 0)
+		return 0;
+	m->n--;
+	if ((size_t)i != m->n) {
+		memmove(m->keys + i * m->ksz, m->keys + (i + 1) * m->ksz, (m->n - i) * m->ksz);
+		memmove(m->vals + i * m->vsz, m->vals + (i + 1) * m->vsz, (m->n - i) * m->vsz);
+	}
+	return 1;
+}

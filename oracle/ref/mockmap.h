@@ -36,5 +36,7 @@ void mockmap_free(struct mockmap *m);
 /* returns 0 on insert, 1 on replace */
 int mockmap_update(struct mockmap *m, const void *key, const void *val);
 void *mockmap_lookup(struct mockmap *m, const void *key);
+/* exact-key removal (kernel htab_map_delete_elem); returns 1 if removed */
+int mockmap_delete(struct mockmap *m, const void *key);
 
 #endif
