@@ -33,7 +33,7 @@ class CgpuConfig(C.Structure):
         ("lb_max_entries", C.c_uint32), ("ipv4_loopback", C.c_uint32),
         ("lb_flags", C.c_uint32),
         ("node_mac", C.c_uint8 * 6), ("reserved1", C.c_uint8 * 2),
-        ("reserved", C.c_uint32 * 2),
+        ("ct_max", C.c_uint32), ("reserved", C.c_uint32 * 1),
     ]
 
 
@@ -45,6 +45,11 @@ class TuplesV4(C.Structure):
 class TuplesV6(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")]
+
+
+class TuplesV4Ct(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ("saddr", "daddr", "sport", "dport", "proto", "l4", "flags", "len", "ep")]
 
 
 class Lb4Tuples(C.Structure):
@@ -112,6 +117,14 @@ PROTOS = {
     "cgpu_lxc_lookup": (i32, [vp, u32, vp]),
     "cgpu_frames_parse": (i32, [vp, C.POINTER(Frames), sz, C.POINTER(FrameTuples), vp]),
     "cgpu_classify_frames": (i32, [vp, C.POINTER(Frames), sz, vp, vp, vp, vp]),
+    "cgpu_ct4_update": (i32, [vp, vp, vp, u64]),
+    "cgpu_ct4_delete": (i32, [vp, vp]),
+    "cgpu_ct4_lookup": (i32, [vp, vp, vp]),
+    "cgpu_ct4_get_next_key": (i32, [vp, vp, vp]),
+    "cgpu_ct4_count": (sz, [vp]),
+    "cgpu_ct4_gc": (i32, [vp, u32, C.POINTER(u64)]),
+    "cgpu_ct4_flush": (i32, [vp]),
+    "cgpu_classify_v4_ct": (i32, [vp, C.POINTER(TuplesV4Ct), sz, u32, vp, vp, vp, vp, vp]),
     "cgpu_counter_delta_bytes": (sz, [vp]),
     "cgpu_counter_bind": (i32, [vp, vp, sz]),
     "cgpu_counter_fold": (i32, [vp, vp]),

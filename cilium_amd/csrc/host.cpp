@@ -355,6 +355,18 @@ struct cgpu_ctx {
 	/* [n_ctr_slots] packed counter accumulator per stream (zero between
 	 * classify calls; one per stream keeps its exactness bound per call) */
 	std::map<void *, uint64_t *> d_pk;
+
+	/* ---- conntrack map cilium_ct4_global (tables.h ct_table layout) ----
+	 * A host shadow serves the bpf(2)-style map calls; the device copy is
+	 * authoritative once a batch ran (ct_dev_newer) and is refreshed from
+	 * the shadow before the next batch after host edits (ct_host_newer). */
+	std::vector<uint4> ct_keys, ct_vals; /* [nslots], [4 * nslots] */
+	uint32_t ct_mask = 0, ct_live = 0, ct_tombs = 0;
+	bool ct_dev_newer = false, ct_host_newer = false;
+	uint4 *d_ct_keys = nullptr, *d_ct_vals = nullptr;
+	uint32_t *d_ct_count = nullptr;
+	void *d_ct_scratch = nullptr;
+	size_t ct_scratch_cap = 0;
 };
 
 /* ======================================================================= */
@@ -391,6 +403,7 @@ CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
 	memcpy(c->ipv6_router_ip, router, 16);
 	static const uint8_t node_mac[6] = {0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde}; /* NODE_MAC, node_config.h:51 */
 	memcpy(c->node_mac, node_mac, 6);
+	c->ct_max = 1000000; /* CT_MAP_SIZE = MapNumEntriesGlobal, pkg/maps/ctmap/ctmap.go:101 */
 }
 
 CGPU_EXPORT const char *cgpu_last_error(void) { return g_last_error.c_str(); }
@@ -406,6 +419,8 @@ CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **o
 		return fail(-EINVAL, "zero capacity");
 	if (cfg->policy_max_total >= POL_CTR_EMPTY)
 		return fail(-EINVAL, "policy_max_total %u >= 2^24 - 1", cfg->policy_max_total);
+	if (!cfg->ct_max || cfg->ct_max > (1u << 28))
+		return fail(-EINVAL, "ct_max %u out of range (1 .. 2^28)", cfg->ct_max);
 	cgpu_ctx *c = new cgpu_ctx();
 	c->cfg = *cfg;
 	c->pol.resize(cfg->max_endpoints);
@@ -448,6 +463,10 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 		(void)hipFree(c->d_delta_own);
 		for (auto &kv : c->d_pk)
 			(void)hipFree(kv.second);
+		(void)hipFree(c->d_ct_keys);
+		(void)hipFree(c->d_ct_vals);
+		(void)hipFree(c->d_ct_count);
+		(void)hipFree(c->d_ct_scratch);
 	}
 	delete c;
 }
@@ -2197,5 +2216,359 @@ CGPU_EXPORT int cgpu_counters_reset(cgpu_ctx *c)
 	for (auto &kv : c->d_pk)
 		HIP_OR_EIO(hipMemset(kv.second, 0, (size_t)c->n_ctr_slots * 8));
 	HIP_OR_EIO(hipDeviceSynchronize());
+	return 0;
+}
+
+/* ======================================================================= */
+/* conntrack map cilium_ct4_global                        */
+/* ======================================================================= */
+static_assert(sizeof(cgpu_ct4_tuple) == 14, "ipv4_ct_tuple layout");
+static_assert(sizeof(cgpu_ct_entry) == 56, "ct_entry layout");
+
+static inline uint4 ct_key4(const cgpu_ct4_tuple *k)
+{
+	return uint4{k->daddr, k->saddr, (uint32_t)k->dport | ((uint32_t)k->sport << 16),
+		     (uint32_t)k->nexthdr | ((uint32_t)k->flags << 8)};
+}
+
+static inline cgpu_ct4_tuple ct_unkey(uint4 s)
+{
+	cgpu_ct4_tuple k;
+	k.daddr = s.x;
+	k.saddr = s.y;
+	k.dport = (uint16_t)s.z;
+	k.sport = (uint16_t)(s.z >> 16);
+	k.nexthdr = (uint8_t)s.w;
+	k.flags = (uint8_t)(s.w >> 8);
+	return k;
+}
+
+static void ct_alloc_shadow(cgpu_ctx *c)
+{
+	if (!c->ct_keys.empty())
+		return;
+	const uint32_t nslots = next_pow2((uint64_t)c->cfg.ct_max * 2u);
+	c->ct_mask = nslots - 1u;
+	c->ct_keys.assign(nslots, uint4{0, 0, 0, 0});
+	c->ct_vals.assign((size_t)nslots * 4u, uint4{0, 0, 0, 0});
+}
+
+/* the probe of k_ct_walk's ct_find, on the shadow */
+static int ct_h_find(const cgpu_ctx *c, uint4 k, uint32_t *free_at)
+{
+	uint32_t h = ct_hash(k.x, k.y, k.z, k.w) & c->ct_mask;
+	uint32_t ff = UINT32_MAX;
+	for (uint32_t probe = 0; probe <= c->ct_mask; probe++) {
+		const uint4 s = c->ct_keys[h];
+		const uint32_t tag = s.w >> 16;
+		if (tag == CT_TAG_EMPTY) {
+			*free_at = ff != UINT32_MAX ? ff : h;
+			return -1;
+		}
+		if (tag == CT_TAG_LIVE && s.x == k.x && s.y == k.y && s.z == k.z &&
+		    (s.w & 0xFFFFu) == (k.w & 0xFFFFu))
+			return (int)h;
+		if (tag == CT_TAG_TOMB && ff == UINT32_MAX)
+			ff = h;
+		h = (h + 1u) & c->ct_mask;
+	}
+	*free_at = ff;
+	return -1;
+}
+
+/* re-insert the live entries into clean arrays (drops tombstones) */
+static void ct_rebuild(cgpu_ctx *c)
+{
+	std::vector<uint4> ok(c->ct_keys.size(), uint4{0, 0, 0, 0}), ov(c->ct_vals.size(), uint4{0, 0, 0, 0});
+	ok.swap(c->ct_keys);
+	ov.swap(c->ct_vals);
+	for (size_t i = 0; i < ok.size(); i++) {
+		if ((ok[i].w >> 16) != CT_TAG_LIVE)
+			continue;
+		uint32_t h = ct_hash(ok[i].x, ok[i].y, ok[i].z, ok[i].w) & c->ct_mask;
+		while ((c->ct_keys[h].w >> 16) != CT_TAG_EMPTY)
+			h = (h + 1u) & c->ct_mask;
+		c->ct_keys[h] = ok[i];
+		for (int j = 0; j < 4; j++)
+			c->ct_vals[4u * h + j] = ov[4u * i + j];
+	}
+	c->ct_tombs = 0;
+}
+
+/* device -> shadow after batches ran */
+static int ct_pull(cgpu_ctx *c)
+{
+	ct_alloc_shadow(c);
+	if (c->device < 0 || !c->ct_dev_newer)
+		return 0;
+	uint32_t cnt[2];
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipDeviceSynchronize());
+	HIP_OR_EIO(hipMemcpy(c->ct_keys.data(), c->d_ct_keys, c->ct_keys.size() * 16, hipMemcpyDeviceToHost));
+	HIP_OR_EIO(hipMemcpy(c->ct_vals.data(), c->d_ct_vals, c->ct_vals.size() * 16, hipMemcpyDeviceToHost));
+	HIP_OR_EIO(hipMemcpy(cnt, c->d_ct_count, 8, hipMemcpyDeviceToHost));
+	c->ct_live = cnt[0];
+	c->ct_tombs = cnt[1];
+	c->ct_dev_newer = false;
+	return 0;
+}
+
+/* shadow -> device before a batch (allocates the device map on first use) */
+static int ct_push(cgpu_ctx *c)
+{
+	ct_alloc_shadow(c);
+	const size_t nslots = c->ct_keys.size();
+	if (!c->d_ct_keys) {
+		HIP_OR_EIO(hipMalloc((void **)&c->d_ct_keys, nslots * 16));
+		HIP_OR_EIO(hipMalloc((void **)&c->d_ct_vals, nslots * 64));
+		HIP_OR_EIO(hipMalloc((void **)&c->d_ct_count, 8));
+		c->ct_host_newer = true;
+	}
+	if (!c->ct_host_newer)
+		return 0;
+	const uint32_t cnt[2] = {c->ct_live, c->ct_tombs};
+	HIP_OR_EIO(hipMemcpy(c->d_ct_keys, c->ct_keys.data(), nslots * 16, hipMemcpyHostToDevice));
+	HIP_OR_EIO(hipMemcpy(c->d_ct_vals, c->ct_vals.data(), nslots * 64, hipMemcpyHostToDevice));
+	HIP_OR_EIO(hipMemcpy(c->d_ct_count, cnt, 8, hipMemcpyHostToDevice));
+	c->ct_host_newer = false;
+	return 0;
+}
+
+static int ct_check(cgpu_ctx *c, const void *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_ct4_update(cgpu_ctx *c, const cgpu_ct4_tuple *key, const cgpu_ct_entry *val,
+				uint64_t flags)
+{
+	if (int r = ct_check(c, key))
+		return r;
+	if (!val)
+		return fail(-EINVAL, "null value");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c))
+		return r;
+	const uint4 k = ct_key4(key);
+	uint32_t free_at;
+	int slot = ct_h_find(c, k, &free_at);
+	if (slot >= 0 && flags == CGPU_NOEXIST)
+		return fail(-EEXIST, "conntrack entry exists");
+	if (slot < 0) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "no such conntrack entry");
+		if (c->ct_live >= c->cfg.ct_max)
+			return fail(-E2BIG, "conntrack map full (%u entries)", c->cfg.ct_max);
+		if (free_at == UINT32_MAX) {
+			ct_rebuild(c);
+			(void)ct_h_find(c, k, &free_at);
+		}
+		if ((c->ct_keys[free_at].w >> 16) == CT_TAG_TOMB)
+			c->ct_tombs--;
+		slot = (int)free_at;
+		c->ct_keys[slot] = uint4{k.x, k.y, k.z, k.w | (CT_TAG_LIVE << 16)};
+		c->ct_live++;
+	}
+	uint4 row[4] = {};
+	memcpy(row, val, sizeof(*val));
+	for (int j = 0; j < 4; j++)
+		c->ct_vals[4u * slot + j] = row[j];
+	c->ct_host_newer = true;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_ct4_delete(cgpu_ctx *c, const cgpu_ct4_tuple *key)
+{
+	if (int r = ct_check(c, key))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c))
+		return r;
+	uint32_t free_at;
+	const int slot = ct_h_find(c, ct_key4(key), &free_at);
+	if (slot < 0)
+		return fail(-ENOENT, "no such conntrack entry");
+	c->ct_keys[slot] = uint4{0, 0, 0, CT_TAG_TOMB << 16};
+	for (int j = 0; j < 4; j++)
+		c->ct_vals[4u * slot + j] = uint4{0, 0, 0, 0};
+	c->ct_live--;
+	c->ct_tombs++;
+	if (c->ct_tombs > (c->ct_mask + 1u) / 4u)
+		ct_rebuild(c);
+	c->ct_host_newer = true;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_ct4_lookup(cgpu_ctx *c, const cgpu_ct4_tuple *key, cgpu_ct_entry *val_out)
+{
+	if (int r = ct_check(c, key))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c))
+		return r;
+	uint32_t free_at;
+	const int slot = ct_h_find(c, ct_key4(key), &free_at);
+	if (slot < 0)
+		return fail(-ENOENT, "no such conntrack entry");
+	if (val_out)
+		memcpy(val_out, &c->ct_vals[4u * slot], sizeof(*val_out));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_ct4_get_next_key(cgpu_ctx *c, const cgpu_ct4_tuple *key, cgpu_ct4_tuple *next_out)
+{
+	if (!c || !next_out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c))
+		return r;
+	size_t from = 0;
+	if (key) { /* bpf(2) GetNextKey: a missing key restarts from the first */
+		uint32_t free_at;
+		const int slot = ct_h_find(c, ct_key4(key), &free_at);
+		if (slot >= 0)
+			from = (size_t)slot + 1u;
+	}
+	for (size_t i = from; i < c->ct_keys.size(); i++)
+		if ((c->ct_keys[i].w >> 16) == CT_TAG_LIVE) {
+			*next_out = ct_unkey(c->ct_keys[i]);
+			return 0;
+		}
+	return -ENOENT;
+}
+
+CGPU_EXPORT size_t cgpu_ct4_count(cgpu_ctx *c)
+{
+	if (!c)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	if (ct_pull(c))
+		return 0;
+	return c->ct_live;
+}
+
+CGPU_EXPORT int cgpu_ct4_gc(cgpu_ctx *c, uint32_t time, uint64_t *deleted_out)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c))
+		return r;
+	uint64_t del = 0;
+	for (size_t i = 0; i < c->ct_keys.size(); i++) {
+		if ((c->ct_keys[i].w >> 16) != CT_TAG_LIVE)
+			continue;
+		const uint32_t lifetime = c->ct_vals[4u * i + 2u].x;
+		if (lifetime < time) { /* doFiltering: RemoveExpired && Lifetime < Time */
+			c->ct_keys[i] = uint4{0, 0, 0, CT_TAG_TOMB << 16};
+			for (int j = 0; j < 4; j++)
+				c->ct_vals[4u * i + j] = uint4{0, 0, 0, 0};
+			c->ct_live--;
+			del++;
+		}
+	}
+	ct_rebuild(c);
+	c->ct_host_newer = true;
+	if (deleted_out)
+		*deleted_out = del;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_ct4_flush(cgpu_ctx *c)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	std::lock_guard<std::mutex> g(c->mu);
+	ct_alloc_shadow(c);
+	std::fill(c->ct_keys.begin(), c->ct_keys.end(), uint4{0, 0, 0, 0});
+	std::fill(c->ct_vals.begin(), c->ct_vals.end(), uint4{0, 0, 0, 0});
+	c->ct_live = c->ct_tombs = 0;
+	c->ct_dev_newer = false;
+	c->ct_host_newer = true;
+	return 0;
+}
+
+/* scratch of one cgpu_classify_v4_ct launch over n packets */
+struct CtScratch {
+	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, head, temp, temp_bytes, total;
+};
+
+static CtScratch ct_scratch_layout(uint64_t n)
+{
+	CtScratch L{};
+	auto take = [&](size_t bytes) {
+		size_t off = L.total;
+		L.total += (bytes + 255) & ~(size_t)255;
+		return off;
+	};
+	L.rec = take(n * 32);
+	L.gkey = take(n * 4);
+	L.gkey_sorted = take(n * 4);
+	L.idx = take(n * 4);
+	L.idx_sorted = take(n * 4);
+	L.heads = take(n * 4);
+	L.n_heads = take(4);
+	L.head = take(n);
+	L.temp_bytes = ct_temp_bytes(n);
+	L.temp = take(L.temp_bytes);
+	return L;
+}
+
+CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, size_t n, uint32_t now,
+				    int32_t *verdict, uint8_t *ct_ret, uint32_t *identity,
+				    uint8_t *stage, void *stream)
+{
+	cgpu_snapshot s;
+	uint64_t *delta;
+	if (int r = snapshot_for_launch(c, s, delta))
+		return r;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->sport || !t->dport || !t->proto || !t->l4 ||
+			 !t->flags || !t->len || !t->ep || !verdict || !ct_ret || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n > (size_t)INT32_MAX)
+		return fail(-EINVAL, "batch of %zu packets exceeds 2^31 - 1", n);
+	if (!n)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	HIP_OR_EIO(hipSetDevice(c->device));
+	if (c->d_ct_count && !c->ct_host_newer) {
+		/* tombstones left by the device's deletes: compact before they
+		 * lengthen every probe chain */
+		uint32_t cnt[2];
+		HIP_OR_EIO(hipMemcpyAsync(cnt, c->d_ct_count, 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
+		HIP_OR_EIO(hipStreamSynchronize((hipStream_t)stream));
+		if (cnt[1] > (c->ct_mask + 1u) / 4u) {
+			if (int r = ct_pull(c))
+				return r;
+			ct_rebuild(c);
+			c->ct_host_newer = true;
+		}
+	}
+	if (int r = ct_push(c))
+		return r;
+	const CtScratch L = ct_scratch_layout(n);
+	if (L.total > c->ct_scratch_cap) {
+		HIP_OR_EIO(hipDeviceSynchronize());
+		(void)hipFree(c->d_ct_scratch);
+		c->d_ct_scratch = nullptr;
+		c->ct_scratch_cap = 0;
+		HIP_OR_EIO(hipMalloc(&c->d_ct_scratch, L.total));
+		c->ct_scratch_cap = L.total;
+	}
+	uint8_t *b = static_cast<uint8_t *>(c->d_ct_scratch);
+	ct_table T{c->d_ct_keys, c->d_ct_vals, c->ct_mask, c->cfg.ct_max, c->d_ct_count};
+	ct_launch a{t->saddr, t->daddr, t->sport, t->dport, t->proto, t->l4, t->flags, t->len, t->ep,
+		    verdict, ct_ret, identity, stage, delta, (uint64_t)n, now,
+		    reinterpret_cast<uint4 *>(b + L.rec), reinterpret_cast<uint32_t *>(b + L.gkey),
+		    reinterpret_cast<uint32_t *>(b + L.gkey_sorted), reinterpret_cast<uint32_t *>(b + L.idx),
+		    reinterpret_cast<uint32_t *>(b + L.idx_sorted), b + L.head,
+		    reinterpret_cast<uint32_t *>(b + L.heads), reinterpret_cast<uint32_t *>(b + L.n_heads),
+		    b + L.temp, L.temp_bytes};
+	HIP_OR_EIO(launch_classify_v4_ct(s, T, a, (hipStream_t)stream));
+	c->ct_dev_newer = true;
 	return 0;
 }

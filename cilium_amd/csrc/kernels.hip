@@ -2178,3 +2178,494 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 			   pk, by, n);
 	return hipGetLastError();
 }
+
+/* ======================================================================= */
+/* Conntrack on the classification path                  */
+/*                                                                          */
+/* cgpu_classify_v4_ct in four steps on one stream:                         */
+/*  1 k_ct_prep    per packet (parallel): the reply-direction tuple of      */
+/*                 ct_lookup4, the ct action, whether policy allows the     */
+/*                 forward tuple (no counters), and the conntrack GROUP =   */
+/*                 the packet's unordered address pair: every CT key a      */
+/*                 packet reads or writes (forward, reply, ICMP related)    */
+/*                 carries that pair, so groups never share a key.          */
+/*  2 radix sort of (group, packet index): stable, so each group's packets  */
+/*                 stay in batch order; then the group heads are selected.  */
+/*  3 k_ct_walk    one lane per group replays its packets IN ORDER against  */
+/*                 the device CT map (lookups, entry updates, creates,      */
+/*                 deletes) = the sequential semantics of the reference.    */
+/*  4 k_ct_finish  per packet (parallel): policy on the tuple ct_lookup4    */
+/*                 left (reply tuple for CT_REPLY / CT_RELATED) with the    */
+/*                 entry counters, the reply/related skip, the verdict and  */
+/*                 the metrics.                                             */
+/*                                                                          */
+/* Memory protocol of the map (per-XCD L2s are not coherent): a slot's tag  */
+/* changes only by agent-scope atomics (EMPTY -> LIVE, LIVE -> TOMB,        */
+/* TOMB -> LIVE; never back to EMPTY, so a lane that once saw a slot in use */
+/* never sees it empty again); key words and entry rows are written         */
+/* write-through (sc1) and read past L1 (nt); a key is only ever inserted,  */
+/* updated or deleted by the lane that owns its group.                      */
+/* ======================================================================= */
+#include <hipcub/hipcub.hpp>
+
+#define CT_LIFETIME_TCP 21600u /* bpf/lib/conntrack.h:31-35 */
+#define CT_LIFETIME_NONTCP 60u
+#define CT_SYN_TIMEOUT 60u
+#define CT_CLOSE_TIMEOUT 10u
+#define CT_REPORT_INTERVAL 5u
+#define DROP_CT_CREATE_FAILED (-155) /* bpf/lib/common.h:262 */
+#define CTB_RX_CLOSING 1u
+#define CTB_TX_CLOSING 2u
+#define CTB_SEEN_NON_SYN 16u
+#define TUPLE_F_IN 1u      /* conntrack.h:63-66 */
+#define TUPLE_F_RELATED 2u
+#define CT_NEW 0u          /* common.h:331-336 */
+#define CT_ESTABLISHED 1u
+#define CT_REPLY 2u
+#define CT_RELATED 3u
+#define CT_FAIL 0x80u      /* walker -> finish: the create failed */
+/* rec meta bits (rec.w >> 16) */
+#define CTM_EGRESS 1u
+#define CTM_ACT_CREATE 2u
+#define CTM_ACT_CLOSE 4u
+#define CTM_TCP 8u
+#define CTM_GATED 16u
+#define CTM_ALLOWED 32u
+
+/* 8-byte write-through store (global_store_dwordx2 sc1) */
+__device__ __forceinline__ void st_wt64(void *p, uint32_t lo, uint32_t hi)
+{
+	__hip_atomic_store(static_cast<uint64_t *>(p), (uint64_t)lo | ((uint64_t)hi << 32),
+			   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt32(void *p, uint32_t v)
+{
+	__hip_atomic_store(static_cast<uint32_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* one struct ct_entry row: a,b = rx/tx packets|bytes, c = {lifetime,
+ * bits | rev_nat << 16, slave | tx_flags_seen << 16 | rx_flags_seen << 24,
+ * src_sec_id}, d = {last_tx_report, last_rx_report, 0, 0} */
+struct ct_row {
+	uint4 a, b, c, d;
+};
+
+__device__ __forceinline__ ct_row ct_row_load(const ct_table &T, uint32_t slot)
+{
+	const uint4 *p = T.vals + 4u * slot;
+	return ct_row{ld_x4<true>(p), ld_x4<true>(p + 1), ld_x4<true>(p + 2), ld_x4<true>(p + 3)};
+}
+
+__device__ __forceinline__ void ct_row_store(const ct_table &T, uint32_t slot, const ct_row &e)
+{
+	uint32_t *p = reinterpret_cast<uint32_t *>(T.vals + 4u * slot);
+	st_wt64(p + 0, e.a.x, e.a.y);
+	st_wt64(p + 2, e.a.z, e.a.w);
+	st_wt64(p + 4, e.b.x, e.b.y);
+	st_wt64(p + 6, e.b.z, e.b.w);
+	st_wt64(p + 8, e.c.x, e.c.y);
+	st_wt64(p + 10, e.c.z, e.c.w);
+	st_wt64(p + 12, e.d.x, e.d.y);
+}
+
+__device__ __forceinline__ void add64(uint32_t &lo, uint32_t &hi, uint32_t v)
+{
+	const uint64_t x = ((uint64_t)hi << 32 | lo) + v;
+	lo = (uint32_t)x;
+	hi = (uint32_t)(x >> 32);
+}
+
+/* __ct_update_timeout, conntrack.h:104-161 (seen = union tcp_flags.lower_bits) */
+__device__ __forceinline__ void ct_touch(ct_row &e, uint32_t now, uint32_t lifetime, bool ingress,
+					 uint32_t seen)
+{
+	e.c.x = now + lifetime;
+	const uint32_t sh = ingress ? 24u : 16u;
+	const uint32_t acc = (e.c.z >> sh) & 0xFFu;
+	const uint32_t last = ingress ? e.d.y : e.d.x;
+	seen = (seen | acc) & 0xFFu;
+	if (last + CT_REPORT_INTERVAL < now || acc != seen) {
+		if (ingress)
+			e.d.y = now;
+		else
+			e.d.x = now;
+		e.c.z = (e.c.z & ~(0xFFu << sh)) | (seen << sh);
+	}
+}
+
+/* ct_update_timeout, conntrack.h:169-185.  w = union tcp_flags as loaded:
+ * .syn (like .fin and .rst, a bit-field member of a union) is bit 0. */
+__device__ __forceinline__ void ct_timeout(ct_row &e, uint32_t now, bool tcp, bool ingress, uint32_t w)
+{
+	uint32_t lifetime = CT_LIFETIME_NONTCP;
+	if (tcp) {
+		if (!(w & 1u))
+			e.c.y |= CTB_SEEN_NON_SYN;
+		lifetime = (e.c.y & CTB_SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+	}
+	ct_touch(e, now, lifetime, ingress, w >> 8);
+}
+
+/* __ct_lookup's update of a found entry, conntrack.h:205-256 (with
+ * CONNTRACK_ACCOUNTING) */
+__device__ __forceinline__ void ct_hit(ct_row &e, uint32_t meta, bool ingress, uint32_t w,
+				       uint32_t len, uint32_t now)
+{
+	const bool tcp = meta & CTM_TCP;
+	if ((e.c.y & 3u) != 3u) /* ct_entry_alive */
+		ct_timeout(e, now, tcp, ingress, w);
+	if (ingress) {
+		add64(e.a.x, e.a.y, 1u);
+		add64(e.a.z, e.a.w, len);
+	} else {
+		add64(e.b.x, e.b.y, 1u);
+		add64(e.b.z, e.b.w, len);
+	}
+	if (meta & CTM_ACT_CREATE) {
+		if (e.c.y & 3u) {
+			e.c.y &= ~3u; /* ct_reset_closing */
+			ct_timeout(e, now, tcp, ingress, w);
+		}
+	} else if (meta & CTM_ACT_CLOSE) {
+		e.c.y |= ingress ? CTB_RX_CLOSING : CTB_TX_CLOSING;
+		if ((e.c.y & 3u) == 3u)
+			ct_touch(e, now, CT_CLOSE_TIMEOUT, ingress, w >> 8);
+	}
+}
+
+__device__ __forceinline__ bool ct_same(uint4 s, uint4 k)
+{
+	return s.x == k.x && s.y == k.y && s.z == k.z && (s.w & 0xFFFFu) == (k.w & 0xFFFFu);
+}
+
+/* Probe for k (low 16 bits of .w = nexthdr | flags << 8).  Returns the slot
+ * or -1; *free_at = the first tombstone on the chain, else the empty slot
+ * that ended it (where an insert of k may start). */
+__device__ __forceinline__ int ct_find(const ct_table &T, uint4 k, uint32_t *free_at)
+{
+	uint32_t h = ct_hash(k.x, k.y, k.z, k.w) & T.mask;
+	uint32_t ff = 0xFFFFFFFFu;
+	for (uint32_t probe = 0; probe <= T.mask; probe++) {
+		const uint4 s = ld_x4<true>(T.keys + h);
+		const uint32_t tag = s.w >> 16;
+		if (tag == CT_TAG_EMPTY) {
+			*free_at = ff != 0xFFFFFFFFu ? ff : h;
+			return -1;
+		}
+		if (tag == CT_TAG_LIVE && ct_same(s, k))
+			return (int)h;
+		if (tag == CT_TAG_TOMB && ff == 0xFFFFFFFFu)
+			ff = h;
+		h = (h + 1u) & T.mask;
+	}
+	*free_at = ff;
+	return -1;
+}
+
+/* Insert absent k at the first free slot from `from` on (htab_map_update_elem
+ * of a new key: -E2BIG past max_elem).  Returns the slot or -1. */
+__device__ __forceinline__ int ct_insert(const ct_table &T, uint4 k, uint32_t from)
+{
+	if (atomicAdd(&T.count[0], 1u) >= T.max) {
+		atomicSub(&T.count[0], 1u);
+		return -1;
+	}
+	uint32_t h = from & T.mask;
+	for (uint32_t probe = 0; probe <= T.mask; probe++) {
+		const uint4 s = ld_x4<true>(T.keys + h);
+		const uint32_t tag = s.w >> 16;
+		if (tag == CT_TAG_EMPTY || tag == CT_TAG_TOMB) {
+			const uint32_t expect = tag << 16;
+			const uint32_t want = (k.w & 0xFFFFu) | (CT_TAG_LIVE << 16);
+			if (atomicCAS(&T.keys[h].w, expect, want) == expect) {
+				if (tag == CT_TAG_TOMB)
+					atomicSub(&T.count[1], 1u);
+				uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + h);
+				st_wt64(p, k.x, k.y);
+				st_wt32(p + 2, k.z);
+				return (int)h;
+			}
+		}
+		h = (h + 1u) & T.mask;
+	}
+	atomicSub(&T.count[0], 1u);
+	return -1;
+}
+
+/* map_delete_elem: the row and key words are retired before the tag turns
+ * into a tombstone another lane may claim (release at agent scope) */
+__device__ __forceinline__ void ct_erase(const ct_table &T, uint32_t slot)
+{
+	uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + slot);
+	st_wt64(p, 0u, 0u);
+	st_wt32(p + 2, 0u);
+	__hip_atomic_exchange(&T.keys[slot].w, CT_TAG_TOMB << 16, __ATOMIC_RELEASE,
+			      __HIP_MEMORY_SCOPE_AGENT);
+	atomicSub(&T.count[0], 1u);
+	atomicAdd(&T.count[1], 1u);
+}
+
+/* map_update_elem(BPF_ANY): replace k's row or insert k */
+__device__ __forceinline__ bool ct_put(const ct_table &T, uint4 k, const ct_row &e)
+{
+	uint32_t from;
+	int slot = ct_find(T, k, &from);
+	if (slot < 0) {
+		if (from == 0xFFFFFFFFu)
+			return false;
+		slot = ct_insert(T, k, from);
+		if (slot < 0)
+			return false;
+	}
+	ct_row_store(T, (uint32_t)slot, e);
+	return true;
+}
+
+struct ct_args {
+	const uint32_t *saddr, *daddr;
+	const uint16_t *sport, *dport;
+	const uint8_t *proto;
+	const uint16_t *l4;
+	const uint8_t *flags;
+	const uint32_t *len;
+	const uint16_t *ep;
+	int32_t *verdict;
+	uint8_t *ct_ret;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t *delta;
+	uint64_t n;
+	uint32_t now;
+	/* scratch */
+	uint4 *rec;                  /* [2n] */
+	uint32_t *gkey, *gkey_sorted; /* [n] */
+	uint32_t *idx, *idx_sorted;   /* [n] */
+	uint8_t *head;               /* [n] */
+	uint32_t *heads, *n_heads;   /* [n], [1] */
+};
+
+/* ct_lookup4's tuple setup, conntrack.h:461-528 */
+__global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t fl = a.flags[i], pr = a.proto[i], w = a.l4[i], len = a.len[i];
+		const uint32_t sa = a.saddr[i], da = a.daddr[i], ep = a.ep[i];
+		const bool egress = fl & 1u;
+		uint32_t tfl = egress ? TUPLE_F_IN : 0u, z = 0, meta = egress ? CTM_EGRESS : 0u;
+		if (pr == 1u) {
+			const uint32_t type = w & 0xFFu;
+			if (type == 3u || type == 11u || type == 12u) /* DEST_UNREACH, TIME_EXCEEDED, PARAMETERPROB */
+				tfl |= TUPLE_F_RELATED;
+			else if (type == 0u) /* ECHOREPLY: tuple->dport = ICMP_ECHO */
+				z = 8u;
+			else {
+				if (type == 8u) /* ECHO: tuple->sport = type */
+					z = 8u << 16;
+				meta |= CTM_ACT_CREATE;
+			}
+		} else if (pr == 6u || pr == 17u) {
+			/* skb_load_bytes(off, &tuple->dport, 4): dport <- sport, sport <- dport */
+			z = (uint32_t)a.sport[i] | ((uint32_t)a.dport[i] << 16);
+			if (pr == 6u) {
+				meta |= CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE);
+			} else {
+				meta |= CTM_ACT_CREATE;
+			}
+		} else {
+			meta |= CTM_GATED;
+		}
+		uint32_t sec = 0;
+		if (!(meta & CTM_GATED)) {
+			const bool frag = !egress && ((fl >> 1) & 1u);
+			const decision d = decide<0, false>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
+							    pr, ep);
+			if (d.v >= 0)
+				meta |= CTM_ALLOWED;
+			if (egress)
+				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
+			else
+				sec = d.id;
+		}
+		a.rec[2u * i] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
+		a.rec[2u * i + 1u] = uint4{w, len, sec, 0u};
+		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : ct_group(sa, da);
+		a.idx[i] = (uint32_t)i;
+	}
+}
+
+__global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *head, uint64_t n)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	for (uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x; p < n; p += stride)
+		head[p] = (p == 0 || g[p] != g[p - 1]) ? 1u : 0u;
+}
+
+/* One packet of a group, conntrack.h:441-561 and ct_create4 :653-744, with
+ * the policy outcome of bpf_lxc.c:506-537 / :918-937. */
+__device__ __forceinline__ uint32_t ct_step(const ct_table &T, uint4 r0, uint4 r1, uint32_t now)
+{
+	const uint32_t meta = r0.w >> 16;
+	const bool ingress = !(meta & CTM_EGRESS);
+	const uint32_t w = r1.x, len = r1.y;
+	uint4 k{r0.x, r0.y, r0.z, r0.w & 0xFFFFu};
+	uint32_t from, ret;
+	int slot = ct_find(T, k, &from);
+	if (slot >= 0) {
+		ret = ((k.w >> 8) & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+	} else {
+		/* ipv4_ct_tuple_reverse */
+		k = uint4{r0.y, r0.x, (r0.z >> 16) | (r0.z << 16), k.w ^ (TUPLE_F_IN << 8)};
+		slot = ct_find(T, k, &from);
+		ret = slot >= 0 ? CT_ESTABLISHED : CT_NEW;
+	}
+	if (slot >= 0) {
+		ct_row e = ct_row_load(T, (uint32_t)slot);
+		ct_hit(e, meta, ingress, w, len, now);
+		ct_row_store(T, (uint32_t)slot, e);
+	}
+	if (ret < CT_REPLY && !(meta & CTM_ALLOWED)) {
+		if (ret == CT_ESTABLISHED)
+			ct_erase(T, (uint32_t)slot); /* ct_delete4 */
+		return ret;
+	}
+	if (ret != CT_NEW)
+		return ret;
+	/* ct_create4: the forward entry, then the ICMP entry relating errors */
+	const bool tcp = meta & CTM_TCP;
+	ct_row e{};
+	ct_timeout(e, now, tcp, ingress, tcp ? 1u : 0u); /* seen_flags.syn = is_tcp: bit 0 */
+	if (ingress)
+		e.a = uint4{1u, 0u, len, 0u};
+	else
+		e.b = uint4{1u, 0u, len, 0u};
+	e.c.w = r1.z; /* src_sec_id */
+	if (from == 0xFFFFFFFFu || (slot = ct_insert(T, k, from)) < 0)
+		return CT_NEW | CT_FAIL;
+	ct_row_store(T, (uint32_t)slot, e);
+	e.c.y |= CTB_SEEN_NON_SYN;
+	const uint4 ik{k.x, k.y, 0u, 1u | ((((k.w >> 8) & 0xFFu) | TUPLE_F_RELATED) << 8)};
+	if (!ct_put(T, ik, e))
+		return CT_NEW | CT_FAIL;
+	return CT_NEW;
+}
+
+__global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
+{
+	const uint32_t nh = *a.n_heads;
+	const uint32_t stride = gridDim.x * 256u;
+	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {
+		const uint64_t p0 = a.heads[h];
+		const uint64_t p1 = h + 1u < nh ? a.heads[h + 1u] : a.n;
+		for (uint64_t p = p0; p < p1; p++) {
+			const uint32_t i = a.idx_sorted[p];
+			const uint4 r0 = a.rec[2u * i];
+			if ((r0.w >> 16) & CTM_GATED)
+				continue;
+			a.ct_ret[i] = (uint8_t)ct_step(T, r0, a.rec[2u * i + 1u], a.now);
+		}
+	}
+}
+
+/* policy on the tuple ct_lookup4 left, counters, the reply / related skip */
+__global__ __launch_bounds__(256) void k_ct_finish(cgpu_snapshot s, ct_args a)
+{
+	/* metrics {reason 0 / 133 / 137 / 155} x {ingress, egress} */
+	uint64_t mcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mbyt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+		const uint4 r0 = a.rec[2u * i];
+		const uint32_t meta = r0.w >> 16, len = a.len[i];
+		const bool egress = meta & CTM_EGRESS;
+		int32_t v;
+		uint32_t id = 0, st = 4, cr = 255u;
+		if (meta & CTM_GATED) {
+			v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup4 default case */
+		} else {
+			const uint32_t c = a.ct_ret[i];
+			cr = c & 3u;
+			const bool reply = cr >= CT_REPLY;
+			const uint32_t fl = a.flags[i];
+			const bool frag = !egress && ((fl >> 1) & 1u);
+			const uint32_t dport = reply ? (r0.z & 0xFFFFu) : (r0.z >> 16);
+			const decision d = decide<0, false>(s, egress, frag, r0.y, r0.x, uint4{}, uint4{},
+							    dport, r0.w & 0xFFu, a.ep[i]);
+			if (d.ctr >= 0) {
+				atomicAdd((unsigned long long *)&a.delta[2u * (uint32_t)d.ctr], 1ull);
+				atomicAdd((unsigned long long *)&a.delta[2u * (uint32_t)d.ctr + 1u],
+					  (unsigned long long)len);
+			}
+			id = d.id;
+			st = d.st;
+			if (reply)
+				v = (egress && d.v > 0) ? d.v : 0;
+			else if (d.v < 0)
+				v = DROP_POLICY;
+			else if (c & CT_FAIL)
+				v = DROP_CT_CREATE_FAILED;
+			else
+				v = d.v;
+		}
+		a.verdict[i] = v;
+		a.identity[i] = id;
+		a.ct_ret[i] = (uint8_t)cr;
+		if (a.stage)
+			a.stage[i] = (uint8_t)st;
+		const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : 3u));
+		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
+			mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
+		}
+	}
+	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
+	const uint32_t reasons[4] = {0u, 133u, 137u, 155u};
+#pragma unroll
+	for (int k = 0; k < 8; k++) {
+		const uint64_t c = wave_sum(mcnt[k]);
+		const uint64_t b = wave_sum(mbyt[k]);
+		if ((threadIdx.x & 63) == 0 && c) {
+			const uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
+			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
+			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
+		}
+	}
+}
+
+/* hipcub temporary storage for the sort and the head selection of n packets */
+size_t ct_temp_bytes(uint64_t n)
+{
+	size_t a = 0, b = 0;
+	(void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+						 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
+	hipcub::CountingInputIterator<uint32_t> it(0);
+	(void)hipcub::DeviceSelect::Flagged(nullptr, b, it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
+					    (uint32_t *)nullptr, (int)n);
+	return std::max(a, b);
+}
+
+hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				 hipStream_t st)
+{
+	ct_args a{L.saddr, L.daddr, L.sport, L.dport, L.proto, L.l4, L.flags, L.len, L.ep,
+		  L.verdict, L.ct_ret, L.identity, L.stage, L.delta, L.n, L.now,
+		  L.rec, L.gkey, L.gkey_sorted, L.idx, L.idx_sorted, L.head, L.heads, L.n_heads};
+	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
+	hipLaunchKernelGGL(k_ct_prep, dim3(g), dim3(256), 0, st, s, a);
+	size_t tb = L.temp_bytes;
+	hipError_t e = hipcub::DeviceRadixSort::SortPairs(L.temp, tb, L.gkey, L.gkey_sorted, L.idx,
+							   L.idx_sorted, (int)L.n, 0, 32, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_ct_heads, dim3(g), dim3(256), 0, st, L.gkey_sorted, L.head, L.n);
+	hipcub::CountingInputIterator<uint32_t> it(0);
+	tb = L.temp_bytes;
+	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.head, L.heads, L.n_heads, (int)L.n, st);
+	if (e != hipSuccess)
+		return e;
+	/* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
+	hipLaunchKernelGGL(k_ct_walk, dim3(2048), dim3(256), 0, st, T, a);
+	hipLaunchKernelGGL(k_ct_finish, dim3(g), dim3(256), 0, st, s, a);
+	return hipGetLastError();
+}

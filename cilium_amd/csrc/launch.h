@@ -92,6 +92,35 @@ struct frames_args {
 hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hipStream_t st);
 hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, hipStream_t st);
 
+/* stateful classification (cgpu_classify_v4_ct): packet columns, outputs,
+ * and the caller-allocated scratch (ct_scratch_layout in host.cpp) */
+struct ct_launch {
+	const uint32_t *saddr, *daddr;
+	const uint16_t *sport, *dport;
+	const uint8_t *proto;
+	const uint16_t *l4;
+	const uint8_t *flags;
+	const uint32_t *len;
+	const uint16_t *ep;
+	int32_t *verdict;
+	uint8_t *ct_ret;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint64_t *delta;
+	uint64_t n;
+	uint32_t now;
+	uint4 *rec;
+	uint32_t *gkey, *gkey_sorted, *idx, *idx_sorted;
+	uint8_t *head;
+	uint32_t *heads, *n_heads;
+	void *temp;
+	size_t temp_bytes;
+};
+
+size_t ct_temp_bytes(uint64_t n);
+hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				 hipStream_t st);
+
 /* totals[i] += delta[i]; delta[i] = 0 over n u64 words */
 hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st);
 /* totals[2*slot[i]] = pk[i]; totals[2*slot[i]+1] = by[i]; delta[..] = 0 */

@@ -294,6 +294,63 @@ typedef struct cgpu_snapshot {
 	uint64_t epoch;
 } cgpu_snapshot;
 
+/* ---- conntrack map cilium_ct4_global ----
+ * Open addressing with linear probing over nslots = 2^k >= 2 * max slots.
+ * keys[slot] (16 B, one gather per probe) = the 14-byte struct ipv4_ct_tuple
+ * (bpf/lib/common.h:359-366) plus a 16-bit slot tag in the top half of .w:
+ *   .x daddr  .y saddr  .z dport | sport << 16  .w nexthdr | flags << 8 | tag << 16
+ *   tag 0 empty, CT_TAG_LIVE occupied, CT_TAG_CLAIM being written, CT_TAG_TOMB
+ *   deleted (probe chains run through it; inserts reuse it).
+ * vals[slot] (64 B = 4 x uint4, one row per slot) = struct ct_entry
+ * (common.h:380-408, 56 B) in its own byte layout, then 8 spare bytes.
+ * The device table is authoritative after a batch: the walker kernel
+ * inserts, updates and deletes entries in place. */
+#define CT_TAG_EMPTY 0u
+#define CT_TAG_LIVE 1u
+#define CT_TAG_CLAIM 0xFFFEu
+#define CT_TAG_TOMB 0xFFFFu
+
+typedef struct ct_table {
+	uint4 *keys;
+	uint4 *vals;
+	uint32_t mask;      /* nslots - 1 */
+	uint32_t max;       /* CT_MAP_SIZE: live entries allowed */
+	uint32_t *count;    /* [0] live entries, [1] tombstones */
+} ct_table;
+
+#if defined(__HIPCC__)
+#define CT_HD __host__ __device__ __forceinline__
+#else
+#define CT_HD static inline
+#endif
+
+CT_HD uint32_t ct_fmix(uint32_t h)
+{
+	h ^= h >> 16;
+	h *= 0x85ebca6bu;
+	h ^= h >> 13;
+	h *= 0xc2b2ae35u;
+	h ^= h >> 16;
+	return h;
+}
+
+/* home slot hash of a 14-byte tuple (tag bits excluded) */
+CT_HD uint32_t ct_hash(uint32_t x, uint32_t y, uint32_t z, uint32_t w)
+{
+	uint32_t h = ct_fmix(x ^ 0x7f4a7c15u);
+	h = ct_fmix(h ^ y);
+	h = ct_fmix(h ^ z);
+	return ct_fmix(h ^ (w & 0xFFFFu));
+}
+
+/* the conntrack group of a packet: every map key its ct_lookup4 /
+ * ct_create4 / ct_delete4 touch has the same unordered address pair */
+CT_HD uint32_t ct_group(uint32_t a, uint32_t b)
+{
+	const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+	return ct_fmix(ct_fmix(lo ^ 0x2545f491u) ^ hi);
+}
+
 /* counters: u64 {packets, bytes} per policy slot, then metrics */
 #define CGPU_METRICS_WORDS (256u * 4u * 2u)
 

@@ -25,8 +25,8 @@ import ipaddress
 import numpy as np
 
 from . import layouts as L
-from ._abi import (CgpuConfig, CgpuError, FrameTuples, Frames, Lb4Out, Lb4Tuples, TuplesV4, TuplesV6,
-                   check, lib)
+from ._abi import (CgpuConfig, CgpuError, FrameTuples, Frames, Lb4Out, Lb4Tuples, TuplesV4,
+                   TuplesV4Ct, TuplesV6, check, lib)
 
 CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX = 0, 1, 2, 3
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
@@ -180,6 +180,42 @@ class Engine:
     def lb4_count(self) -> int:
         return self.L.cgpu_lb4_count(self.h)
 
+    # --- conntrack map cilium_ct4_global ---
+    def ct4_update(self, key, val, flags=BPF_ANY) -> int:
+        return self.L.cgpu_ct4_update(self.h, _buf(key), _buf(val), flags)
+
+    def ct4_delete(self, key) -> int:
+        return self.L.cgpu_ct4_delete(self.h, _buf(key))
+
+    def ct4_lookup(self, key):
+        out = C.create_string_buffer(56)
+        rc = self.L.cgpu_ct4_lookup(self.h, _buf(key), out)
+        return rc, (np.frombuffer(out.raw, L.CT_ENTRY)[0] if rc == 0 else None)
+
+    def ct4_count(self) -> int:
+        return self.L.cgpu_ct4_count(self.h)
+
+    def ct4_gc(self, time: int) -> int:
+        d = C.c_uint64()
+        check(self.L.cgpu_ct4_gc(self.h, time, C.byref(d)), "cgpu_ct4_gc")
+        return d.value
+
+    def ct4_flush(self) -> None:
+        check(self.L.cgpu_ct4_flush(self.h), "cgpu_ct4_flush")
+
+    def ct4_dump(self):
+        """(keys, vals) of the whole map via get_next_key + lookup, sorted
+        canonically (layouts.ct_sorted)."""
+        keys, vals, prev = [], [], None
+        out = C.create_string_buffer(14)
+        while self.L.cgpu_ct4_get_next_key(self.h, prev, out) == 0:
+            prev = out.raw
+            rc, v = self.ct4_lookup(np.frombuffer(prev, L.CT4_TUPLE)[0])
+            assert rc == 0
+            keys.append(np.frombuffer(prev, L.CT4_TUPLE)[0])
+            vals.append(v)
+        return L.ct_sorted(np.array(keys, L.CT4_TUPLE), np.array(vals, L.CT_ENTRY))
+
     def flow_hash(self, saddr, daddr, sport, dport, proto) -> int:
         return self.L.cgpu_flow_hash(saddr, daddr, sport, dport, proto)
 
@@ -209,6 +245,28 @@ class Engine:
         check(self.L.cgpu_classify_v4(self.h, C.byref(tv), n, _ptr(out["verdict"]),
                                       _ptr(out["identity"]), _ptr(out.get("stage")),
                                       _stream(stream)), "cgpu_classify_v4")
+        return out
+
+    def classify_v4_ct(self, t: dict, now: int, out: dict | None = None, stage: bool = True,
+                       stream=None):
+        """Stateful classification (cgpu_classify_v4_ct): t holds CUDA tensors
+        saddr/daddr (int32), sport/dport (int16, network order), proto/flags
+        (uint8), l4b (int16: TCP header bytes 12-13 / ICMP type), len (int32),
+        ep (int16); now = bpf_ktime_get_sec() of the batch."""
+        import torch
+        n = t["saddr"].numel()
+        dev = t["saddr"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "ct_ret": torch.empty(n, dtype=torch.uint8, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
+        tv = TuplesV4Ct(*[t[k].data_ptr() for k in
+                          ("saddr", "daddr", "sport", "dport", "proto", "l4b", "flags", "len", "ep")])
+        check(self.L.cgpu_classify_v4_ct(self.h, C.byref(tv), n, now, _ptr(out["verdict"]),
+                                         _ptr(out["ct_ret"]), _ptr(out["identity"]),
+                                         _ptr(out.get("stage")), _stream(stream)),
+              "cgpu_classify_v4_ct")
         return out
 
     def classify_v4_lb(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):

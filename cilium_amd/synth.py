@@ -212,7 +212,7 @@ def load_oracle(oracle, t: Tables):
 
 TUPLE_DTYPES = {"saddr": np.uint32, "daddr": np.uint32, "dport": np.uint16, "proto": np.uint8,
                 "flags": np.uint8, "len": np.uint32, "ep": np.uint16, "sport": np.uint16,
-                "hash": np.uint32}
+                "hash": np.uint32, "l4b": np.uint16}
 
 
 def to_device(t: dict, device="cuda"):
@@ -657,3 +657,37 @@ def make_ct_stream(rng, n_conn: int, locals_be: np.ndarray, remotes_be: np.ndarr
         "len": rng.integers(64, 1501, total).astype(np.uint32), "ep": ep[conn].astype(np.uint16),
     }
     return {key: np.ascontiguousarray(v[order]) for key, v in out.items()}
+
+
+def ct_endpoints(n_endpoints: int):
+    """Local endpoint addresses (network order, inside the cluster /8) and
+    their SECLABELs (lxc_config.h) for the stateful workloads."""
+    locals_be = np.array([L.ip4_be(CLUSTER_V4 | (200 << 16) | (ep + 1)) for ep in range(n_endpoints)],
+                         np.uint32)
+    seclabels = (np.arange(n_endpoints, dtype=np.uint32) * 7 + 5000).astype(np.uint32)
+    return locals_be, seclabels
+
+
+def make_ct_workload(tables: Tables, n_conn: int, seed=SEED, gpu_id: int = 0, n_remote=None,
+                     mean_pkts: float = 8.0, span: float = 0.02):
+    """The stateful stream over `tables`: n_conn connections
+    between the tables' endpoints and remote addresses (80% inside installed
+    ipcache prefixes), seeded per GPU like make_tuples."""
+    rng = np.random.Generator(np.random.PCG64(seed + 0xC7000 + gpu_id))
+    locals_be, seclabels = ct_endpoints(tables.n_endpoints)
+    nr = n_remote or max(16, n_conn // 4)
+    pi = rng.integers(0, len(tables.pfx_addr), nr)
+    base = tables.pfx_addr[pi].astype(np.uint64)
+    ln = tables.pfx_len[pi].astype(np.uint64)
+    host = rng.integers(0, 2**32, nr, dtype=np.uint64)
+    hmask = (np.uint64(1) << (np.uint64(32) - ln)) - np.uint64(1)
+    rem = np.where(rng.random(nr) < 0.8, base | (host & hmask), host).astype(np.uint32).byteswap()
+    t = make_ct_stream(rng, n_conn, locals_be, rem, mean_pkts=mean_pkts, span=span)
+    return t, locals_be, seclabels
+
+
+def load_lxc(target, seclabels):
+    """cgpu_lxc_update / or_lxc_update: the SECLABEL of every endpoint."""
+    for ep, sl in enumerate(seclabels):
+        rc = target.lxc_update(ep, L.lxc_info(b"\0" * 6, 0, b"\0" * 16, 0, int(sl)))
+        assert rc == 0, rc

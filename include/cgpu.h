@@ -154,7 +154,11 @@ typedef struct cgpu_config {
 	 * frames must be addressed to (is_valid_gw_dst_mac, lib/lxc.h:77-90) */
 	uint8_t node_mac[6];
 	uint8_t reserved1[2];
-	uint32_t reserved[2];
+	/* CT_MAP_SIZE of cilium_ct4_global: live conntrack entries the map
+	 * holds (MapNumEntriesGlobal 1000000, pkg/maps/ctmap/ctmap.go:101);
+	 * device slots are 2x this, rounded up to a power of two */
+	uint32_t ct_max;
+	uint32_t reserved[1];
 } cgpu_config;
 
 #define CGPU_LB_L3 1u
@@ -271,7 +275,8 @@ typedef struct cgpu_lxc_info {
 	uint8_t pad;
 	uint32_t ipv4;    /* LXC_IPV4: raw u32 compared with ip4->saddr (lxc.h:55-62) */
 	uint8_t ipv6[16]; /* LXC_IP, network order */
-	uint32_t reserved;
+	uint32_t sec_label; /* SECLABEL: src_sec_id of the entries the endpoint's egress
+			       creates (bpf_lxc.c:517, conntrack.h:705) */
 } cgpu_lxc_info;
 
 int cgpu_lxc_update(cgpu_ctx *ctx, uint32_t ep, const cgpu_lxc_info *info);
@@ -466,6 +471,105 @@ int cgpu_frames_parse(cgpu_ctx *ctx, const cgpu_frames *f, size_t n,
  */
 int cgpu_classify_frames(cgpu_ctx *ctx, const cgpu_frames *f, size_t n, int32_t *verdict,
 			 uint32_t *identity, uint8_t *stage, void *stream);
+
+/* ------------------------------------------------------------------ */
+/* conntrack: the map cilium_ct4_global               */
+/* ------------------------------------------------------------------ */
+/* struct ipv4_ct_tuple (bpf/lib/common.h:359-366), packed, 14 B */
+#pragma pack(push, 1)
+typedef struct cgpu_ct4_tuple {
+	uint32_t daddr;  /* network order */
+	uint32_t saddr;
+	uint16_t dport;  /* network order */
+	uint16_t sport;
+	uint8_t nexthdr;
+	uint8_t flags;   /* TUPLE_F_OUT 0 / TUPLE_F_IN 1 | TUPLE_F_RELATED 2 */
+} cgpu_ct4_tuple;
+#pragma pack(pop)
+
+/* struct ct_entry (bpf/lib/common.h:380-408), 56 B */
+typedef struct cgpu_ct_entry {
+	uint64_t rx_packets, rx_bytes, tx_packets, tx_bytes;
+	uint32_t lifetime;
+	uint16_t bits;   /* rx_closing:1 tx_closing:1 nat46:1 lb_loopback:1 seen_non_syn:1 */
+	uint16_t rev_nat_index;
+	uint16_t slave;
+	uint8_t tx_flags_seen, rx_flags_seen;
+	uint32_t src_sec_id;
+	uint32_t last_tx_report, last_rx_report;
+} cgpu_ct_entry;
+
+/*
+ * Map operations with the bpf(2) semantics the agent's ctmap package uses
+ * (pkg/maps/ctmap/ctmap.go, pkg/bpf/bpf.go:153-245): update with
+ * CGPU_ANY/NOEXIST/EXIST (-EEXIST / -ENOENT), -E2BIG for a new key past
+ * ct_max; delete / lookup -ENOENT; get_next_key (NULL key = first) walks the
+ * map in slot order.  The device table is authoritative once a batch ran:
+ * these calls synchronize with it (they are control-plane operations).
+ */
+int cgpu_ct4_update(cgpu_ctx *ctx, const cgpu_ct4_tuple *key, const cgpu_ct_entry *val,
+		    uint64_t flags);
+int cgpu_ct4_delete(cgpu_ctx *ctx, const cgpu_ct4_tuple *key);
+int cgpu_ct4_lookup(cgpu_ctx *ctx, const cgpu_ct4_tuple *key, cgpu_ct_entry *val_out);
+int cgpu_ct4_get_next_key(cgpu_ctx *ctx, const cgpu_ct4_tuple *key, cgpu_ct4_tuple *next_out);
+size_t cgpu_ct4_count(cgpu_ctx *ctx);
+/* ctmap.GC with RemoveExpired (ctmap.go:306-310, :345-357): delete every
+ * entry whose lifetime < time; *deleted_out (optional) = how many */
+int cgpu_ct4_gc(cgpu_ctx *ctx, uint32_t time, uint64_t *deleted_out);
+/* ctmap Flush (ctmap.go:361-367): delete every entry */
+int cgpu_ct4_flush(cgpu_ctx *ctx);
+
+/* A batch of IPv4 packets for the stateful path (device pointers). */
+typedef struct cgpu_tuples_v4_ct {
+	const uint32_t *saddr; /* network order */
+	const uint32_t *daddr;
+	const uint16_t *sport; /* L4 header ports as on the wire (TCP/UDP) */
+	const uint16_t *dport;
+	const uint8_t *proto;
+	const uint16_t *l4;    /* TCP: header bytes 12-13 as loaded (byte 12 in the
+				  low half: doff/NS, byte 13 in the high half: flags);
+				  ICMP: the type in the low byte; else ignored */
+	const uint8_t *flags;  /* CGPU_F_EGRESS | CGPU_F_FRAGMENT */
+	const uint32_t *len;
+	const uint16_t *ep;
+} cgpu_tuples_v4_ct;
+
+/* ct_lookup4 results (bpf/lib/common.h:331-336) as reported in ct_ret[] */
+#define CGPU_CT_NEW 0
+#define CGPU_CT_ESTABLISHED 1
+#define CGPU_CT_REPLY 2
+#define CGPU_CT_RELATED 3
+#define CGPU_CT_NONE 255 /* ct_lookup4 failed (DROP_CT_UNKNOWN_PROTO) */
+#define CGPU_DROP_CT_CREATE_FAILED (-155)
+
+/*
+ * The stateful decision of the endpoint programs for n packets, with the
+ * result of processing them IN ORDER (packet i sees every conntrack change
+ * of packets < i, as the reference's programs do for a packet sequence):
+ *   ct_lookup4 (bpf/lib/conntrack.h:441-561): the reply-direction tuple,
+ *     then the forward one; on a hit the entry's timeout / TCP flags /
+ *     closing bits / rx|tx counters are updated (:198-259);
+ *   identity as cgpu_classify_v4; policy on the tuple as ct_lookup4 left it
+ *     (the reply tuple's dport for CT_REPLY / CT_RELATED);
+ *   CT_REPLY / CT_RELATED pass whatever policy says; otherwise a denied
+ *     packet is dropped (DROP_POLICY) and, if CT_ESTABLISHED, its entry
+ *     deleted; an allowed CT_NEW creates the forward entry and its ICMP
+ *     related entry (ct_create4, :653-744; src_sec_id = the endpoint's
+ *     SECLABEL on egress, the source identity on ingress), or fails with
+ *     DROP_CT_CREATE_FAILED when the map is full;
+ *   bpf_lxc.c:506-576 (egress), :918-950 (ingress).
+ *   verdict[i]: DROP_* (-133, -137, -155), the proxy port (egress: any
+ *               ct state; ingress: CT_NEW / CT_ESTABLISHED), else 0
+ *   ct_ret[i] : CGPU_CT_*; identity[i], stage[i] as cgpu_classify_v4
+ *               (stage may be NULL)
+ * now = bpf_ktime_get_sec() for the batch.  Packets of one address pair are
+ * resolved in order by one lane; pairs are independent.  The one departure
+ * from a sequential run: which creates fail when the map fills up DURING a
+ * batch depends on the order lanes reach the capacity check.
+ */
+int cgpu_classify_v4_ct(cgpu_ctx *ctx, const cgpu_tuples_v4_ct *t, size_t n, uint32_t now,
+			int32_t *verdict, uint8_t *ct_ret, uint32_t *identity, uint8_t *stage,
+			void *stream);
 
 /* ------------------------------------------------------------------ */
 /* counters                                                             */

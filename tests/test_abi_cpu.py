@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from cilium_amd import build, layouts as L
-from cilium_amd._abi import Frames, PROTOS, TuplesV4, lib
+from cilium_amd._abi import Frames, PROTOS, TuplesV4, TuplesV4Ct, lib
 from cilium_amd.engine import (CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX, BPF_EXIST,
                                BPF_NOEXIST, CIDRMap, Engine, IPCacheMap, PolicyMap)
 
@@ -57,6 +57,9 @@ def test_host_only_context_has_no_cpu_path():
     fr = Frames(0, 0, 0, 0, 64, 0)
     assert L_.cgpu_classify_frames(e.h, C.byref(fr), 1, None, None, None, None) == -errno.ENODEV
     assert L_.cgpu_frames_parse(e.h, C.byref(fr), 1, None, None) == -errno.ENODEV
+    tc = TuplesV4Ct()
+    assert L_.cgpu_classify_v4_ct(e.h, C.byref(tc), 1, 0, None, None, None, None,
+                                  None) == -errno.ENODEV
 
 
 def test_lxc_info_semantics():
@@ -222,3 +225,72 @@ def test_bad_flags_and_abi_version():
     cfg.abi_version = 99
     h = C.c_void_p()
     assert lib().cgpu_ctx_create(C.byref(cfg), -1, C.byref(h)) == -errno.EINVAL
+
+
+def _ct_key(i, proto=6, flags=0):
+    k = np.zeros((), L.CT4_TUPLE)
+    k["daddr"], k["saddr"], k["dport"], k["sport"] = 0x0A000001 + i, 0x0B000001, 80, 1000 + i
+    k["nexthdr"], k["flags"] = proto, flags
+    return k
+
+
+def test_ct_map_semantics():
+    """cilium_ct4_global through the bpf(2)-style calls (pkg/maps/ctmap):
+    BPF_ANY/NOEXIST/EXIST, -E2BIG past CT_MAP_SIZE, delete, get_next_key
+    walking the whole map, GC by lifetime (ctmap.go doFiltering), Flush."""
+    e = Engine(device=-1, ct_max=8)
+    v = np.zeros((), L.CT_ENTRY)
+    for i in range(8):
+        v["lifetime"] = 100 + i
+        v["rx_packets"] = i
+        assert e.ct4_update(_ct_key(i), v) == 0
+    assert e.ct4_count() == 8
+    assert e.ct4_update(_ct_key(8), v) == -errno.E2BIG
+    assert e.ct4_update(_ct_key(3), v, BPF_NOEXIST) == -errno.EEXIST
+    assert e.ct4_update(_ct_key(9), v, BPF_EXIST) == -errno.ENOENT
+    rc, got = e.ct4_lookup(_ct_key(2))
+    assert rc == 0 and got["rx_packets"] == 2 and got["lifetime"] == 102
+    # the key is the whole 14-byte tuple: flags and nexthdr distinguish entries
+    assert e.ct4_lookup(_ct_key(2, flags=1))[0] == -errno.ENOENT
+    assert e.ct4_lookup(_ct_key(2, proto=17))[0] == -errno.ENOENT
+    assert e.ct4_delete(_ct_key(2)) == 0 and e.ct4_delete(_ct_key(2)) == -errno.ENOENT
+    assert e.ct4_update(_ct_key(8), v) == 0  # room again
+    keys, vals = e.ct4_dump()
+    assert len(keys) == 8 and sorted(keys["daddr"].tolist()) == sorted(
+        [0x0A000001 + i for i in (0, 1, 3, 4, 5, 6, 7, 8)])
+    assert e.ct4_gc(104) == 3  # lifetimes 100, 101, 103
+    assert e.ct4_count() == 5
+    assert sorted(e.ct4_dump()[1]["lifetime"].tolist()) == [104, 105, 106, 107, 107]
+    e.ct4_flush()
+    assert e.ct4_count() == 0 and len(e.ct4_dump()[0]) == 0
+    with pytest.raises(Exception):
+        Engine(device=-1, ct_max=0)
+
+
+def test_ct_map_matches_restatement_under_churn():
+    """Random update/delete/GC churn: the engine's map (open addressing with
+    tombstones and compaction) holds exactly what the restatement holds."""
+    from oracle import Oracle
+    rng = np.random.Generator(np.random.PCG64(7))
+    e = Engine(device=-1, ct_max=64)
+    o = Oracle()
+    o.ct_set_max(64)
+    for step in range(3000):
+        i = int(rng.integers(0, 96))
+        k = _ct_key(i, proto=int(rng.choice([1, 6, 17])), flags=int(rng.integers(0, 4)))
+        op = rng.random()
+        if op < 0.6:
+            v = np.zeros((), L.CT_ENTRY)
+            v["lifetime"] = int(rng.integers(0, 1000))
+            v["tx_bytes"] = step
+            assert e.ct4_update(k, v) == o.ct4_update(k, v)
+        elif op < 0.98:
+            assert e.ct4_delete(k) == o.ct4_delete(k)
+        else:
+            t = int(rng.integers(0, 1000))
+            assert e.ct4_gc(t) == o.ct4_gc(t)
+        assert e.ct4_count() == o.ct4_count()
+    ek, ev = e.ct4_dump()
+    ok, ov = o.ct4_dump()
+    np.testing.assert_array_equal(ek, ok)
+    np.testing.assert_array_equal(ev, ov)

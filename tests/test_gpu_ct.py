@@ -1,0 +1,217 @@
+"""GPU parity of stateful conntrack through the C ABI:
+cgpu_classify_v4_ct + the cilium_ct4_global map calls against the reference's
+conntrack.h / policy.h golden vectors (tests/golden/ct4.npz, a 4-batch
+stream with pre-installed entries and policy deletes between batches) and
+against the CPU restatement (pinned to that fixture) on larger streams.
+Every packet's verdict, ct_lookup4 result, identity and policy stage, the
+whole CT map after every batch, the policy counters and the metrics are
+compared bit for bit."""
+import numpy as np
+import pytest
+
+from cilium_amd import build, layouts as L, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU test needs a device"
+    build.build()
+    return torch
+
+
+def _engine(**kw):
+    from cilium_amd.engine import Engine
+    return Engine(device=0, **kw)
+
+
+def _run(torch, e, t, now):
+    out = e.classify_v4_ct(synth.to_device(t), now)
+    torch.cuda.synchronize()
+    return (out["verdict"].cpu().numpy(), out["ct_ret"].cpu().numpy(),
+            out["identity"].cpu().numpy().view(np.uint32), out["stage"].cpu().numpy())
+
+
+def _golden_engine(g, ct_max=1 << 20):
+    e = _engine(ct_max=ct_max)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert e.ipcache_update(k, v) == 0
+    for k, en, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert e.policy_update(int(ep), k, en) == 0
+    synth.load_lxc(e, g["seclabels"])
+    e.commit()
+    return e
+
+
+def test_ct_golden_stream(torch_cuda, golden):
+    g = golden("ct4.npz")
+    e = _golden_engine(g)
+    for k, v in zip(g["pre_keys"], g["pre_vals"]):
+        assert e.ct4_update(k, v) == 0
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    cuts, nows = g["cuts"], g["nows"]
+    off = 0
+    for bi in range(4):
+        if bi == 2:
+            for d in g["pol_del"]:
+                assert e.policy_delete(int(g["pol_ep"][d]), g["pol_keys"][d]) == 0
+            e.commit()
+        sl = slice(int(cuts[bi]), int(cuts[bi + 1]))
+        v, cr, idt, st = _run(torch_cuda, e, {k: x[sl] for k, x in t.items()}, int(nows[bi]))
+        np.testing.assert_array_equal(v, g["b_verdict"][sl], err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(cr, g["b_ct_ret"][sl], err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(idt, g["b_identity"][sl], err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(st, g["b_stage"][sl], err_msg=f"batch {bi}")
+        n = int(g["dump_n"][bi])
+        keys, vals = e.ct4_dump()
+        np.testing.assert_array_equal(keys, g["dump_keys"][off:off + n], err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(vals, g["dump_vals"][off:off + n], err_msg=f"batch {bi}")
+        assert e.ct4_count() == n
+        off += n
+    deleted = set(g["pol_del"].tolist())
+    for i, (k, ep, fe) in enumerate(zip(g["pol_keys"], g["pol_ep"], g["final_entries"])):
+        if i in deleted:
+            continue
+        rc, got = e.policy_lookup(int(ep), k)
+        assert rc == 0
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+    e.close()
+
+
+def test_ct_golden_small_map(torch_cuda, golden):
+    """At CT_MAP_SIZE 64 the map fills during the batch.  Which creates fail
+    then depends on the order lanes reach the capacity check (cgpu.h), so
+    the checks are the order-free ones: the map holds exactly 64 entries,
+    every DROP_CT_CREATE_FAILED is an allowed CT_NEW, and packets the map's
+    capacity cannot influence (policy drops, protocol gate) match."""
+    g = golden("ct4.npz")
+    e = _golden_engine(g, ct_max=64)
+    t = {k[3:]: g[k] for k in g.files if k.startswith("t2_")}
+    v, cr, idt, st = _run(torch_cuda, e, t, 500)
+    assert e.ct4_count() == 64
+    fail = v == L.DROP_CT_CREATE_FAILED
+    assert fail.sum() > 0 and (cr[fail] == L.CT_NEW).all()
+    gated = g["s_ct_ret"] == L.CT_NONE
+    np.testing.assert_array_equal(v[gated], g["s_verdict"][gated])
+    np.testing.assert_array_equal(idt[~gated & (cr == L.CT_NEW)],
+                                  g["s_identity"][~gated & (cr == L.CT_NEW)])
+    e.close()
+
+
+def _pair(torch, T, t, locals_be, seclabels, batches, nows, ct_max=1 << 18, pre=None,
+          deletes=None):
+    """Engine and restatement side by side over consecutive batches."""
+    from oracle import Oracle
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_lxc(o, seclabels)
+    o.ct_set_max(ct_max)
+    e = _engine(**T.engine_config(), ct_max=ct_max)
+    synth.load_engine(e, T)
+    synth.load_lxc(e, seclabels)
+    e.commit()
+    for k, v in (pre or ()):
+        assert e.ct4_update(k, v) == 0 and o.ct4_update(k, v) == 0
+    n = len(t["saddr"])
+    cuts = np.linspace(0, n, batches + 1).astype(np.int64)
+    for bi in range(batches):
+        if deletes is not None and bi == batches // 2:
+            for k, ep in deletes:
+                assert e.policy_delete(int(ep), k) == 0 and o.policy_delete(int(ep), k) == 0
+            e.commit()
+        tb = {k: x[cuts[bi]:cuts[bi + 1]] for k, x in t.items()}
+        v, cr, idt, st = _run(torch, e, tb, int(nows[bi]))
+        v0, cr0, i0, s0, _ = o.classify_v4_ct(tb, int(nows[bi]))
+        np.testing.assert_array_equal(v, v0, err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(cr, cr0, err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(idt, i0, err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(st, s0, err_msg=f"batch {bi}")
+        assert e.ct4_count() == o.ct4_count()
+    return e, o
+
+
+def _assert_same_map(e, o):
+    ek, ev = e.ct4_dump()
+    ok, ov = o.ct4_dump()
+    np.testing.assert_array_equal(ek, ok)
+    np.testing.assert_array_equal(ev, ov)
+
+
+@pytest.fixture(scope="module")
+def cfg_ct():
+    T = synth.make_tables(**synth.CONFIGS["cpu"])
+    T.n_endpoints = 1
+    t, locals_be, seclabels = synth.make_ct_workload(T, 60_000, mean_pkts=10.0, span=0.05)
+    return T, t, locals_be, seclabels
+
+
+def test_ct_stream_vs_restatement(torch_cuda, cfg_ct):
+    """~600k packets of 60k connections in 3 batches (connections span batch
+    boundaries), 2000 policy keys deleted before the middle batch, then
+    GC: everything bit-exact, counters and metrics included."""
+    T, t, locals_be, seclabels = cfg_ct
+    rng = np.random.Generator(np.random.PCG64(11))
+    dels = rng.choice(len(T.pol_keys), 2000, replace=False)
+    e, o = _pair(torch_cuda, T, t, locals_be, seclabels, 3, [1000, 1004, 1100],
+                 deletes=[(T.pol_keys[d], T.pol_ep[d]) for d in dels])
+    _assert_same_map(e, o)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    gone = set(dels.tolist())
+    for i, (k, ep) in enumerate(zip(T.pol_keys[:6000], T.pol_ep[:6000])):
+        if i in gone:
+            continue
+        rc, got = e.policy_lookup(int(ep), k)
+        _, raw = o.policy_lookup(int(ep), k)
+        exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(exp["packets"]), int(exp["bytes"]))
+    # ctmap GC on the map the device wrote, then another batch on the result
+    assert e.ct4_gc(1100 + 61) == o.ct4_gc(1100 + 61)
+    _assert_same_map(e, o)
+    tb = {k: x[:50_000] for k, x in t.items()}
+    v, cr, idt, st = _run(torch_cuda, e, tb, 1200)
+    v0, cr0, i0, s0, _ = o.classify_v4_ct(tb, 1200)
+    np.testing.assert_array_equal(v, v0)
+    np.testing.assert_array_equal(cr, cr0)
+    _assert_same_map(e, o)
+    e.close()
+
+
+def test_ct_elephant_and_edges(torch_cuda, cfg_ct):
+    """One connection with 200k packets in a batch (one long lane), a batch
+    of untracked protocols only, pre-installed closing entries, an empty
+    batch."""
+    T, t, locals_be, seclabels = cfg_ct
+    n = 200_000
+    rng = np.random.Generator(np.random.PCG64(5))
+    eg = rng.random(n) < 0.5
+    a, b = int(locals_be[0]), int(t["daddr"][t["flags"] & 1 == 1][0])
+    ele = {
+        "saddr": np.where(eg, a, b).astype(np.uint32), "daddr": np.where(eg, b, a).astype(np.uint32),
+        "sport": np.where(eg, 0x3930, 0x5000).astype(np.uint16),
+        "dport": np.where(eg, 0x5000, 0x3930).astype(np.uint16),
+        "proto": np.full(n, 6, np.uint8),
+        "l4b": ((5 << 4) | (rng.random(n) < 0.01) | (rng.choice([2, 16, 24, 17], n) << 8)).astype(np.uint16),
+        "flags": eg.astype(np.uint8), "len": rng.integers(64, 1500, n).astype(np.uint32),
+        "ep": np.zeros(n, np.uint16),
+    }
+    pre = []
+    for i in range(64):  # closing / half-closed entries on pairs the stream uses
+        k = np.zeros((), L.CT4_TUPLE)
+        k["daddr"], k["saddr"] = t["saddr"][i], t["daddr"][i]
+        k["dport"], k["sport"], k["nexthdr"] = t["dport"][i], t["sport"][i], t["proto"][i]
+        k["flags"] = L.TUPLE_F_OUT if t["flags"][i] & 1 else L.TUPLE_F_IN
+        v = np.zeros((), L.CT_ENTRY)
+        v["bits"] = [1, 2, 3, 19][i % 4]
+        v["lifetime"] = 10
+        pre.append((k, v))
+    gated = {k: x[:1000].copy() for k, x in t.items()}
+    gated["proto"][:] = 47
+    mix = {k: np.concatenate([ele[k], gated[k], t[k][:100_000]]) for k in ele}
+    e, o = _pair(torch_cuda, T, mix, locals_be, seclabels, 2, [2000, 2001], pre=pre)
+    _assert_same_map(e, o)
+    out = e.classify_v4_ct({k: synth.to_device({k: x[:0]})[k] for k, x in mix.items()}, 2002)
+    torch_cuda.cuda.synchronize()
+    assert out["verdict"].numel() == 0
+    e.close()
