@@ -20,6 +20,13 @@ Other BASELINE configs (not the headline line; run them explicitly):
   --config frames    config 2 tables, the batch as raw Ethernet frames in
                      64-byte ring slots (cgpu_classify_frames: header parse
                      of bpf_lxc.c / conntrack.h fused with the classify)
+  --config ct        config 2 tables + stateful conntrack:
+                     cgpu_classify_v4_ct over 64M packets of 2M connections,
+                     the cilium_ct4_global map emptied at the start of every
+                     step (cgpu_ct4_flush, timed), so each step creates,
+                     updates and reply-skips the same way; parity and the
+                     CPU baseline on the packets of 1/64 of the address pairs
+                     (pairs are independent conntrack groups)
   --config cpu       config 1 sizes
 """
 from __future__ import annotations
@@ -39,6 +46,9 @@ B_IN, B_OUT = 18, 8    # v4 classify tuple bytes in / out
 B_IN_PF6, B_OUT_PF6 = 33, 1  # v6 prefilter
 FRAME_STRIDE = 64      # --config frames: ring slot bytes (Ethernet + IPv4 + TCP fit)
 B_IN_FRAMES = FRAME_STRIDE + 4 + 1 + 2  # slot + len + flags + ep
+B_IN_CT, B_OUT_CT = 22, 9  # saddr daddr sport dport proto l4(2) flags len ep / verdict identity ct_ret
+CT_PKTS_PER_CONN = 32
+CT_SAMPLE = 64  # parity / CPU baseline on the packets of 1 in CT_SAMPLE address pairs
 
 
 def log(*a):
@@ -57,6 +67,10 @@ WORKLOADS = {
     "frames": "config2 tables, 64M raw Ethernet/IPv4/TCP|UDP frames per GPU in 64-byte slots: "
               "header parse (revalidate, ihl, frag, ct_lookup4 ports) fused with ipcache + policy, "
               "bit-exact verdicts",
+    "ct": "config2 tables + stateful conntrack (cilium_ct4_global, SURVEY §8f row 3): 64M packets "
+          "per GPU of 2M TCP/UDP/ICMP connections (~32 packets each, both directions, ICMP errors), "
+          "map emptied each step: ct_lookup4 -> ipcache -> policy -> reply/related skip, "
+          "ct_create4 / delete, bit-exact",
 }
 
 
@@ -91,7 +105,8 @@ def main():
     pf6 = args.config == "pf6"
     cascade = args.config == "cascade"
     frames = args.config == "frames"
-    cfg = synth.CONFIGS["gpu" if (pf6 or frames) else args.config]
+    ct = args.config == "ct"
+    cfg = synth.CONFIGS["gpu" if (pf6 or frames or ct) else args.config]
     n = args.tuples or cfg["n_tuples"]
     t0 = time.time()
     S = None
@@ -102,6 +117,19 @@ def main():
             f"{len(P.ep6)} endpoints) + {n} packets in {time.time() - t0:.1f}s")
         e = Engine(device=local, **P.engine_config())
         synth.load_prefilter6(e, P)
+    elif ct:
+        T = synth.make_tables(**cfg)
+        tup, _, seclabels = synth.make_ct_workload(T, n // CT_PKTS_PER_CONN, gpu_id=rank,
+                                                   mean_pkts=CT_PKTS_PER_CONN)
+        n = min(n, len(tup["saddr"]))
+        tup = {k: np.ascontiguousarray(v[:n]) for k, v in tup.items()}
+        ct_max = 1 << max(20, int(np.ceil(np.log2(2.5 * n / CT_PKTS_PER_CONN))))
+        log(f"[rank {rank}] synthetic tables ({len(T.ipc_keys)} ipcache, {len(T.pol_keys)} policy) "
+            f"+ {n} packets of {n // CT_PKTS_PER_CONN} connections in {time.time() - t0:.1f}s, "
+            f"ct_max {ct_max}")
+        e = Engine(device=local, **T.engine_config(), ct_max=ct_max)
+        synth.load_engine(e, T)
+        synth.load_lxc(e, seclabels)
     else:
         T = synth.make_tables(**cfg)
         tup = synth.make_tuples(T, n, gpu_id=rank)
@@ -134,14 +162,21 @@ def main():
         d = synth.to_device(tup, dev)
         out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
                "identity": torch.empty(n, dtype=torch.int32, device=dev), "stage": None}
+        if ct:
+            out["ct_ret"] = torch.empty(n, dtype=torch.uint8, device=dev)
+    CT_NOW = 1000
     delta = torch.zeros(e.counter_delta_bytes() // 8, dtype=torch.int64, device=dev)
     e.counter_bind(delta)
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
+        if ct:
+            e.ct4_flush()  # every step starts from an empty conntrack map
         if ev is not None:
             ev[0].record(stream)
-        if pf6:
+        if ct:
+            e.classify_v4_ct(d, CT_NOW, out=out, stream=stream)
+        elif pf6:
             e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
         elif cascade:
             e.classify_v4_lb(d, out=out, stream=stream)
@@ -195,6 +230,11 @@ def main():
         if pf6:
             o = Oracle(**P.oracle_config())
             synth.load_prefilter6(o, P)
+        elif ct:
+            o = Oracle(**T.oracle_config())
+            synth.load_oracle(o, T)
+            synth.load_lxc(o, seclabels)
+            o.ct_set_max(ct_max)
         else:
             o = Oracle(**T.oracle_config())
             synth.load_oracle(o, T)
@@ -210,9 +250,22 @@ def main():
                 return o.classify_frames({k: v[sl] for k, v in fr.items()}, nthreads=threads)
             return o.classify_v4({k: v[sl] for k, v in tup.items()}, nthreads=threads)
 
-        cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
+        if ct:
+            # conntrack groups (unordered address pairs) are independent: the
+            # packets of 1 in CT_SAMPLE pairs, in batch order, replayed by the
+            # sequential restatement from an empty map are the reference's
+            # result for exactly those packets
+            lo = np.minimum(tup["saddr"], tup["daddr"]).astype(np.uint64)
+            hi = np.maximum(tup["saddr"], tup["daddr"]).astype(np.uint64)
+            hsh = ((lo * np.uint64(0x9E3779B97F4A7C15)) ^ hi) * np.uint64(0xC2B2AE3D27D4EB4F)
+            sub = np.nonzero((hsh >> np.uint64(58)) == 0)[0]
+            tsub = {k: v[sub] for k, v in tup.items()}
+        else:
+            cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
         c0 = time.perf_counter()
-        if pf6:
+        if ct:
+            v0, cr0, i0, _, probes = o.classify_v4_ct(tsub, CT_NOW)
+        elif pf6:
             v0, probes = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
         elif cascade:
             v0, i0, _, probes = o.classify_v4_lb(tup, nthreads=threads)
@@ -221,8 +274,16 @@ def main():
         else:
             v0, i0, _, probes = o.classify_v4(tup, nthreads=threads)
         c_el = time.perf_counter() - c0
+        n_cpu = len(sub) if ct else n
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and ct:
+            cpu = {"value": round(n_cpu / c_el / 1e6, 3), "unit": "Mpps", "cores": 1,
+                   "kind": "port",
+                   "sample": f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
+                             f"pairs from an empty map; oracle/cgpu_oracle.c or_classify_v4_ct "
+                             f"(sequential conntrack + LPM trie + open hash), 1 thread, "
+                             f"{c_el:.2f}s wall"}
+        elif not args.no_cpu_baseline:
             what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
                     "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash",
                     "frames": "oracle/cgpu_oracle.c frame parse + LPM trie + open hash"}.get(
@@ -231,12 +292,17 @@ def main():
                    "kind": "port",
                    "sample": f"rank-0 batch, all {n} tuples, {args.config} tables; {what}, "
                              f"{threads} threads, {c_el:.2f}s wall"}
-        parity = bool(np.array_equal(out["verdict"].cpu().numpy(), v0))
-        if not pf6:
-            parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
-        probes_per = probes / n
+        if ct:
+            parity = bool(np.array_equal(out["verdict"].cpu().numpy()[sub], v0) and
+                          np.array_equal(out["ct_ret"].cpu().numpy()[sub], cr0) and
+                          np.array_equal(out["identity"].cpu().numpy().view(np.uint32)[sub], i0))
+        else:
+            parity = bool(np.array_equal(out["verdict"].cpu().numpy(), v0))
+            if not pf6:
+                parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
+        probes_per = probes / n_cpu
         b_in, b_out = ((B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN_FRAMES, B_OUT) if frames
-                       else (B_IN + (2 if cascade else 0), B_OUT))
+                       else (B_IN_CT, B_OUT_CT) if ct else (B_IN + (2 if cascade else 0), B_OUT))
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
         traffic = None
@@ -256,6 +322,16 @@ def main():
             conf.update(ipcache_prefixes=int(len(T.ipc_keys)), policy_entries=int(len(T.pol_keys)))
             if S is not None:
                 conf.update(services=int(len(S.vip)), lb_map_entries=int(len(S.keys)))
+            if ct:
+                ctr = out["ct_ret"].cpu().numpy()
+                conf.update(ct_max=ct_max, ct_entries_after_step=int(e.ct4_count()),
+                            parity_sample_packets=int(len(sub)),
+                            ct_state_frac={s_: round(float((ctr == c_).mean()), 4) for s_, c_ in
+                                           (("new", 0), ("established", 1), ("reply", 2),
+                                            ("related", 3), ("none", 255))},
+                            ops_per_packet_note="probes = ipcache + policy probes + CT map "
+                                                "lookups/updates/deletes of the reference, "
+                                                "counted on the parity sample")
         result = {
             "metric": METRIC if not pf6 else "Mpps XDP IPv6 prefilter verdicts; % HBM roofline",
             "value": round(value, 2), "unit": "Mpps", "n_gpus": world,

@@ -2489,12 +2489,23 @@ CGPU_EXPORT int cgpu_ct4_flush(cgpu_ctx *c)
 	c->ct_live = c->ct_tombs = 0;
 	c->ct_dev_newer = false;
 	c->ct_host_newer = true;
+	if (c->device >= 0 && c->d_ct_keys) {
+		/* empty the device map in place (tags and counts; rows are
+		 * rewritten whole by every insert) instead of re-uploading */
+		HIP_OR_EIO(hipSetDevice(c->device));
+		HIP_OR_EIO(hipDeviceSynchronize());
+		HIP_OR_EIO(hipMemset(c->d_ct_keys, 0, c->ct_keys.size() * 16));
+		HIP_OR_EIO(hipMemset(c->d_ct_count, 0, 8));
+		HIP_OR_EIO(hipDeviceSynchronize());
+		c->ct_host_newer = false;
+	}
 	return 0;
 }
 
 /* scratch of one cgpu_classify_v4_ct launch over n packets */
 struct CtScratch {
-	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, head, temp, temp_bytes, total;
+	size_t rec, rec_s, cr_s, inv, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, head, temp, temp_bytes,
+		total;
 };
 
 static CtScratch ct_scratch_layout(uint64_t n)
@@ -2506,6 +2517,9 @@ static CtScratch ct_scratch_layout(uint64_t n)
 		return off;
 	};
 	L.rec = take(n * 32);
+	L.rec_s = take(n * 32);
+	L.cr_s = take(n);
+	L.inv = take(n * 4);
 	L.gkey = take(n * 4);
 	L.gkey_sorted = take(n * 4);
 	L.idx = take(n * 4);
@@ -2535,12 +2549,14 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 		return 0;
 	std::lock_guard<std::mutex> g(c->mu);
 	HIP_OR_EIO(hipSetDevice(c->device));
+	uint32_t live = c->ct_live;
 	if (c->d_ct_count && !c->ct_host_newer) {
 		/* tombstones left by the device's deletes: compact before they
 		 * lengthen every probe chain */
 		uint32_t cnt[2];
 		HIP_OR_EIO(hipMemcpyAsync(cnt, c->d_ct_count, 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
 		HIP_OR_EIO(hipStreamSynchronize((hipStream_t)stream));
+		live = cnt[0];
 		if (cnt[1] > (c->ct_mask + 1u) / 4u) {
 			if (int r = ct_pull(c))
 				return r;
@@ -2560,10 +2576,18 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 		c->ct_scratch_cap = L.total;
 	}
 	uint8_t *b = static_cast<uint8_t *>(c->d_ct_scratch);
-	ct_table T{c->d_ct_keys, c->d_ct_vals, c->ct_mask, c->cfg.ct_max, c->d_ct_count};
+	/* every walker wave (2048 x 4) holding a chunk stays under a quarter
+	 * of the headroom */
+	const uint32_t headroom = c->cfg.ct_max > live ? c->cfg.ct_max - live : 0u;
+	uint32_t chunk = std::min<uint32_t>(256u, std::max<uint32_t>(1u, headroom / 32768u));
+	if (const char *e = getenv("CGPU_CT_CHUNK")) /* diagnostic override */
+		chunk = (uint32_t)std::max(1, atoi(e));
+	ct_table T{c->d_ct_keys, c->d_ct_vals, c->ct_mask, c->cfg.ct_max, c->d_ct_count, chunk};
 	ct_launch a{t->saddr, t->daddr, t->sport, t->dport, t->proto, t->l4, t->flags, t->len, t->ep,
 		    verdict, ct_ret, identity, stage, delta, (uint64_t)n, now,
-		    reinterpret_cast<uint4 *>(b + L.rec), reinterpret_cast<uint32_t *>(b + L.gkey),
+		    reinterpret_cast<uint4 *>(b + L.rec), reinterpret_cast<uint4 *>(b + L.rec_s), b + L.cr_s,
+		    reinterpret_cast<uint32_t *>(b + L.inv),
+		    reinterpret_cast<uint32_t *>(b + L.gkey),
 		    reinterpret_cast<uint32_t *>(b + L.gkey_sorted), reinterpret_cast<uint32_t *>(b + L.idx),
 		    reinterpret_cast<uint32_t *>(b + L.idx_sorted), b + L.head,
 		    reinterpret_cast<uint32_t *>(b + L.heads), reinterpret_cast<uint32_t *>(b + L.n_heads),

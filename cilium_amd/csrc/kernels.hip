@@ -2231,6 +2231,7 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_TCP 8u
 #define CTM_GATED 16u
 #define CTM_ALLOWED 32u
+#define CTM_FRAG 64u
 
 /* 8-byte write-through store (global_store_dwordx2 sc1) */
 __device__ __forceinline__ void st_wt64(void *p, uint32_t lo, uint32_t hi)
@@ -2362,14 +2363,60 @@ __device__ __forceinline__ int ct_find(const ct_table &T, uint4 k, uint32_t *fre
 	return -1;
 }
 
+/* Per-workgroup accounting of the map's live / tombstone counts.  One
+ * global word takes every insert's capacity check otherwise (~10^2 atomics
+ * per us on one address): a workgroup instead reserves capacity from
+ * count[0] in chunks and keeps the rest in LDS, and nets its tombstone and
+ * delete changes in LDS, all flushed once at the end.  Exact while the map
+ * is not about to fill; at the edge an unused reservation of another
+ * workgroup can fail a create early (the documented order dependence).
+ * The chunk (T.res_chunk) is sized by the host so that all waves'
+ * outstanding reservations stay under a quarter of the headroom. */
+struct ct_acct {
+	int *res;   /* LDS: reserved, unused capacity */
+	int *live;  /* LDS: live entries removed (deletes), to return */
+	int *tombs; /* LDS: tombstone delta */
+};
+
+__device__ __forceinline__ bool ct_take(const ct_table &T, const ct_acct &A)
+{
+	if (atomicSub(A.res, 1) > 0)
+		return true;
+	atomicAdd(A.res, 1);
+	/* one refill per wave for all the lanes that found the pool empty:
+	 * a refill per lane would hold 64 chunks per wave */
+	const uint64_t m = __ballot(1);
+	const int leader = __ffsll((unsigned long long)m) - 1;
+	const uint32_t need = (uint32_t)__popcll(m);
+	const bool lead = (int)__lane_id() == leader;
+	uint32_t got = 0;
+	if (lead) {
+		const uint32_t ask = need + T.res_chunk - 1u;
+		if (atomicAdd(&T.count[0], ask) + ask <= T.max) {
+			got = ask;
+		} else {
+			atomicSub(&T.count[0], ask);
+			got = 0xFFFFFFFFu; /* at the edge: one exact check per lane */
+		}
+	}
+	got = __shfl(got, leader, 64);
+	if (got != 0xFFFFFFFFu) {
+		if (lead && got > need)
+			atomicAdd(A.res, (int)(got - need));
+		return true;
+	}
+	if (atomicAdd(&T.count[0], 1u) < T.max)
+		return true;
+	atomicSub(&T.count[0], 1u);
+	return false;
+}
+
 /* Insert absent k at the first free slot from `from` on (htab_map_update_elem
  * of a new key: -E2BIG past max_elem).  Returns the slot or -1. */
-__device__ __forceinline__ int ct_insert(const ct_table &T, uint4 k, uint32_t from)
+__device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, uint4 k, uint32_t from)
 {
-	if (atomicAdd(&T.count[0], 1u) >= T.max) {
-		atomicSub(&T.count[0], 1u);
+	if (!ct_take(T, A))
 		return -1;
-	}
 	uint32_t h = from & T.mask;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
 		const uint4 s = ld_x4<true>(T.keys + h);
@@ -2379,7 +2426,7 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, uint4 k, uint32_t fr
 			const uint32_t want = (k.w & 0xFFFFu) | (CT_TAG_LIVE << 16);
 			if (atomicCAS(&T.keys[h].w, expect, want) == expect) {
 				if (tag == CT_TAG_TOMB)
-					atomicSub(&T.count[1], 1u);
+					atomicSub(A.tombs, 1);
 				uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + h);
 				st_wt64(p, k.x, k.y);
 				st_wt32(p + 2, k.z);
@@ -2388,37 +2435,21 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, uint4 k, uint32_t fr
 		}
 		h = (h + 1u) & T.mask;
 	}
-	atomicSub(&T.count[0], 1u);
+	atomicAdd(A.res, 1);
 	return -1;
 }
 
 /* map_delete_elem: the row and key words are retired before the tag turns
  * into a tombstone another lane may claim (release at agent scope) */
-__device__ __forceinline__ void ct_erase(const ct_table &T, uint32_t slot)
+__device__ __forceinline__ void ct_erase(const ct_table &T, const ct_acct &A, uint32_t slot)
 {
 	uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + slot);
 	st_wt64(p, 0u, 0u);
 	st_wt32(p + 2, 0u);
 	__hip_atomic_exchange(&T.keys[slot].w, CT_TAG_TOMB << 16, __ATOMIC_RELEASE,
 			      __HIP_MEMORY_SCOPE_AGENT);
-	atomicSub(&T.count[0], 1u);
-	atomicAdd(&T.count[1], 1u);
-}
-
-/* map_update_elem(BPF_ANY): replace k's row or insert k */
-__device__ __forceinline__ bool ct_put(const ct_table &T, uint4 k, const ct_row &e)
-{
-	uint32_t from;
-	int slot = ct_find(T, k, &from);
-	if (slot < 0) {
-		if (from == 0xFFFFFFFFu)
-			return false;
-		slot = ct_insert(T, k, from);
-		if (slot < 0)
-			return false;
-	}
-	ct_row_store(T, (uint32_t)slot, e);
-	return true;
+	atomicAdd(A.live, 1);
+	atomicAdd(A.tombs, 1);
 }
 
 struct ct_args {
@@ -2437,7 +2468,10 @@ struct ct_args {
 	uint64_t n;
 	uint32_t now;
 	/* scratch */
-	uint4 *rec;                  /* [2n] */
+	uint4 *rec;                  /* [2n] per packet, batch order */
+	uint4 *rec_s;                /* [2n] the same, in group order */
+	uint8_t *cr_s;               /* [n] walker result, group order */
+	uint32_t *inv;               /* [n] batch position -> group-order position */
 	uint32_t *gkey, *gkey_sorted; /* [n] */
 	uint32_t *idx, *idx_sorted;   /* [n] */
 	uint8_t *head;               /* [n] */
@@ -2475,20 +2509,29 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 		} else {
 			meta |= CTM_GATED;
 		}
-		uint32_t sec = 0;
+		uint32_t sec = 0, port = 0, cst = 0, id = 0;
 		if (!(meta & CTM_GATED)) {
+			/* the forward tuple's decision (what CT_NEW / CT_ESTABLISHED
+			 * packets see); k_ct_finish bumps its counter */
 			const bool frag = !egress && ((fl >> 1) & 1u);
+			if (frag)
+				meta |= CTM_FRAG;
 			const decision d = decide<0, false>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
 							    pr, ep);
-			if (d.v >= 0)
+			if (d.v >= 0) {
 				meta |= CTM_ALLOWED;
+				port = (uint32_t)d.v;
+			}
+			id = d.id;
 			if (egress)
 				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
 			else
 				sec = d.id;
+			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
 		}
+		a.identity[i] = id;
 		a.rec[2u * i] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
-		a.rec[2u * i + 1u] = uint4{w, len, sec, 0u};
+		a.rec[2u * i + 1u] = uint4{w | (port << 16), len, sec, cst};
 		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : ct_group(sa, da);
 		a.idx[i] = (uint32_t)i;
 	}
@@ -2501,32 +2544,213 @@ __global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *he
 		head[p] = (p == 0 || g[p] != g[p - 1]) ? 1u : 0u;
 }
 
+/* records into group order, so that each walker lane reads its group's
+ * packets sequentially instead of gathering them one by one */
+__global__ __launch_bounds__(256) void k_ct_gather(ct_args a)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	for (uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x; p < a.n; p += stride) {
+		const uint32_t i = a.idx_sorted[p];
+		const uint4 r0 = a.rec[2u * i], r1 = a.rec[2u * i + 1u];
+		a.rec_s[2u * p] = r0;
+		a.rec_s[2u * p + 1u] = r1;
+		a.inv[i] = (uint32_t)p;
+	}
+}
+
+/* A lane's cache of the map entries its group touched.  The lane owns every
+ * key of its group (no other lane inserts, updates or deletes one), so a
+ * cached entry - present with its row, or absent with the slot an insert
+ * may start from - stays exact for the whole group: a connection's packets
+ * cost one probe per distinct key instead of one per packet.  Rows are
+ * written back (write-through) when evicted and at the end of the group.
+ * CTC entries, round-robin replacement, every access an unrolled select so
+ * the cache lives in VGPRs. */
+#define CTC 4
+#define CTC_VALID 0x10000u
+#define CTC_NEG 0x20000u
+#define CTC_DIRTY 0x40000u
+
+/* One cache entry.  The CTC entries are SEPARATE locals of the walker (not
+ * an array, not members of one aggregate) and every access below names
+ * them one by one: with an array, instcombine folds the unrolled
+ * selects back into a dynamically indexed load and the cache lands in
+ * scratch memory. */
+struct ctc_ent {
+	uint4 key; /* .w = nexthdr | flags << 8 | CTC_* */
+	uint32_t pos;
+	ct_row row;
+};
+
+struct ct_cache {
+	ctc_ent &e0, &e1, &e2, &e3;
+	uint32_t next;
+};
+
+template <typename F> __device__ __forceinline__ void ctc_each(ct_cache &c, F &&f)
+{
+	f(c.e0, 0);
+	f(c.e1, 1);
+	f(c.e2, 2);
+	f(c.e3, 3);
+}
+
+/* Every helper reads all entries unconditionally and writes them back
+ * through selects: a branch per entry would let SimplifyCFG sink the four
+ * identical stores into one store through a phi of entry addresses, which
+ * again keeps the cache out of registers. */
+__device__ __forceinline__ bool ctc_dirty(uint32_t w)
+{
+	return (w & (CTC_VALID | CTC_NEG | CTC_DIRTY)) == (CTC_VALID | CTC_DIRTY);
+}
+
+__device__ __forceinline__ void ctc_flush(const ct_table &T, ct_cache &c)
+{
+	ctc_each(c, [&](ctc_ent &e, int) {
+		const uint32_t w = e.key.w, p = e.pos;
+		const ct_row r = e.row;
+		if (ctc_dirty(w))
+			ct_row_store(T, p, r);
+		e.key.w = 0;
+	});
+	c.next = 0;
+}
+
+__device__ __forceinline__ uint32_t ctc_state(ct_cache &c, int i)
+{
+	uint32_t w = 0;
+	ctc_each(c, [&](ctc_ent &e, int j) { w = i == j ? e.key.w : w; });
+	return w;
+}
+
+__device__ __forceinline__ uint32_t ctc_pos(ct_cache &c, int i)
+{
+	uint32_t p = 0;
+	ctc_each(c, [&](ctc_ent &e, int j) { p = i == j ? e.pos : p; });
+	return p;
+}
+
+__device__ __forceinline__ uint4 sel4(bool t, uint4 a, uint4 b)
+{
+	return uint4{t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z, t ? a.w : b.w};
+}
+
+__device__ __forceinline__ ct_row selrow(bool t, const ct_row &a, const ct_row &b)
+{
+	return ct_row{sel4(t, a.a, b.a), sel4(t, a.b, b.b), sel4(t, a.c, b.c), sel4(t, a.d, b.d)};
+}
+
+__device__ __forceinline__ ct_row ctc_row(ct_cache &c, int i)
+{
+	ct_row r{};
+	ctc_each(c, [&](ctc_ent &e, int j) { r = selrow(i == j, e.row, r); });
+	return r;
+}
+
+/* entry i := present at pos with row r (dirty) */
+__device__ __forceinline__ void ctc_put(ct_cache &c, int i, uint32_t pos, const ct_row &r)
+{
+	ctc_each(c, [&](ctc_ent &e, int j) {
+		const bool t = i == j;
+		e.key.w = t ? (e.key.w & 0xFFFFu) | CTC_VALID | CTC_DIRTY : e.key.w;
+		e.pos = t ? pos : e.pos;
+		e.row = selrow(t, r, e.row);
+	});
+}
+
+/* entry i := absent, inserts may start at pos */
+__device__ __forceinline__ void ctc_drop(ct_cache &c, int i, uint32_t pos)
+{
+	ctc_each(c, [&](ctc_ent &e, int j) {
+		const bool t = i == j;
+		e.key.w = t ? (e.key.w & 0xFFFFu) | CTC_VALID | CTC_NEG : e.key.w;
+		e.pos = t ? pos : e.pos;
+	});
+}
+
+/* the cache entry of k, probing the map on a miss */
+__device__ __forceinline__ int ctc_get(const ct_table &T, ct_cache &c, uint4 k)
+{
+	int hit = -1;
+	ctc_each(c, [&](ctc_ent &e, int j) {
+		hit = ((e.key.w & CTC_VALID) && ct_same(e.key, k)) ? j : hit;
+	});
+	if (hit >= 0)
+		return hit;
+	const int v = (int)c.next;
+	c.next = v + 1 == CTC ? 0u : (uint32_t)v + 1u;
+	/* write back the victim */
+	uint32_t vw = 0, vp = 0;
+	ct_row vr{};
+	ctc_each(c, [&](ctc_ent &e, int j) {
+		vw = j == v ? e.key.w : vw;
+		vp = j == v ? e.pos : vp;
+		vr = selrow(j == v, e.row, vr);
+	});
+	if (ctc_dirty(vw))
+		ct_row_store(T, vp, vr);
+	uint32_t from;
+	const int slot = ct_find(T, k, &from);
+	ct_row r{};
+	if (slot >= 0)
+		r = ct_row_load(T, (uint32_t)slot);
+	const uint4 nk{k.x, k.y, k.z, (k.w & 0xFFFFu) | CTC_VALID | (slot < 0 ? CTC_NEG : 0u)};
+	const uint32_t np = slot >= 0 ? (uint32_t)slot : from;
+	ctc_each(c, [&](ctc_ent &e, int j) {
+		const bool t = j == v;
+		e.key = sel4(t, nk, e.key);
+		e.pos = t ? np : e.pos;
+		e.row = selrow(t, r, e.row);
+	});
+	return v;
+}
+
+/* BPF_ANY update of k (ct_create4's map_update_elem) through the cache */
+__device__ __forceinline__ bool ctc_update(const ct_table &T, const ct_acct &A, ct_cache &c, uint4 k,
+					   const ct_row &e)
+{
+	const int i = ctc_get(T, c, k);
+	uint32_t pos = ctc_pos(c, i);
+	if (ctc_state(c, i) & CTC_NEG) {
+		const int slot = pos == 0xFFFFFFFFu ? -1 : ct_insert(T, A, k, pos);
+		if (slot < 0)
+			return false;
+		pos = (uint32_t)slot;
+	}
+	ctc_put(c, i, pos, e);
+	return true;
+}
+
 /* One packet of a group, conntrack.h:441-561 and ct_create4 :653-744, with
  * the policy outcome of bpf_lxc.c:506-537 / :918-937. */
-__device__ __forceinline__ uint32_t ct_step(const ct_table &T, uint4 r0, uint4 r1, uint32_t now)
+__device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A, ct_cache &c, uint4 r0,
+					   uint4 r1, uint32_t now)
 {
 	const uint32_t meta = r0.w >> 16;
 	const bool ingress = !(meta & CTM_EGRESS);
-	const uint32_t w = r1.x, len = r1.y;
+	const uint32_t w = r1.x & 0xFFFFu, len = r1.y;
 	uint4 k{r0.x, r0.y, r0.z, r0.w & 0xFFFFu};
-	uint32_t from, ret;
-	int slot = ct_find(T, k, &from);
-	if (slot >= 0) {
+	int ci = ctc_get(T, c, k);
+	uint32_t ret;
+	if (!(ctc_state(c, ci) & CTC_NEG)) {
 		ret = ((k.w >> 8) & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
 	} else {
 		/* ipv4_ct_tuple_reverse */
 		k = uint4{r0.y, r0.x, (r0.z >> 16) | (r0.z << 16), k.w ^ (TUPLE_F_IN << 8)};
-		slot = ct_find(T, k, &from);
-		ret = slot >= 0 ? CT_ESTABLISHED : CT_NEW;
+		ci = ctc_get(T, c, k);
+		ret = (ctc_state(c, ci) & CTC_NEG) ? CT_NEW : CT_ESTABLISHED;
 	}
-	if (slot >= 0) {
-		ct_row e = ct_row_load(T, (uint32_t)slot);
+	if (ret != CT_NEW) {
+		ct_row e = ctc_row(c, ci);
 		ct_hit(e, meta, ingress, w, len, now);
-		ct_row_store(T, (uint32_t)slot, e);
+		ctc_put(c, ci, ctc_pos(c, ci), e);
 	}
 	if (ret < CT_REPLY && !(meta & CTM_ALLOWED)) {
-		if (ret == CT_ESTABLISHED)
-			ct_erase(T, (uint32_t)slot); /* ct_delete4 */
+		if (ret == CT_ESTABLISHED) { /* ct_delete4 */
+			const uint32_t slot = ctc_pos(c, ci);
+			ct_erase(T, A, slot);
+			ctc_drop(c, ci, slot);
+		}
 		return ret;
 	}
 	if (ret != CT_NEW)
@@ -2540,74 +2764,106 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, uint4 r0, uint4 r
 	else
 		e.b = uint4{1u, 0u, len, 0u};
 	e.c.w = r1.z; /* src_sec_id */
-	if (from == 0xFFFFFFFFu || (slot = ct_insert(T, k, from)) < 0)
+	if (!ctc_update(T, A, c, k, e))
 		return CT_NEW | CT_FAIL;
-	ct_row_store(T, (uint32_t)slot, e);
 	e.c.y |= CTB_SEEN_NON_SYN;
 	const uint4 ik{k.x, k.y, 0u, 1u | ((((k.w >> 8) & 0xFFu) | TUPLE_F_RELATED) << 8)};
-	if (!ct_put(T, ik, e))
+	if (!ctc_update(T, A, c, ik, e))
 		return CT_NEW | CT_FAIL;
 	return CT_NEW;
 }
 
 __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
 {
+	__shared__ int s_acct[3];
+	if (threadIdx.x < 3)
+		s_acct[threadIdx.x] = 0;
+	__syncthreads();
+	const ct_acct A{&s_acct[0], &s_acct[1], &s_acct[2]};
 	const uint32_t nh = *a.n_heads;
 	const uint32_t stride = gridDim.x * 256u;
+	ctc_ent e0{}, e1{}, e2{}, e3{};
+	ct_cache c{e0, e1, e2, e3, 0u};
 	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {
 		const uint64_t p0 = a.heads[h];
 		const uint64_t p1 = h + 1u < nh ? a.heads[h + 1u] : a.n;
 		for (uint64_t p = p0; p < p1; p++) {
-			const uint32_t i = a.idx_sorted[p];
-			const uint4 r0 = a.rec[2u * i];
+			const uint4 r0 = ld_x4<true>(a.rec_s + 2u * p);
+			const uint4 r1 = ld_x4<true>(a.rec_s + 2u * p + 1u);
 			if ((r0.w >> 16) & CTM_GATED)
 				continue;
-			a.ct_ret[i] = (uint8_t)ct_step(T, r0, a.rec[2u * i + 1u], a.now);
+			a.cr_s[p] = (uint8_t)ct_step(T, A, c, r0, r1, a.now);
 		}
+		ctc_flush(T, c);
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		const int back = s_acct[0] + s_acct[1]; /* unused reservation + deletes */
+		if (back)
+			atomicSub(&T.count[0], (uint32_t)back);
+		if (s_acct[2])
+			atomicAdd(&T.count[1], (uint32_t)s_acct[2]);
 	}
 }
 
-/* policy on the tuple ct_lookup4 left, counters, the reply / related skip */
-__global__ __launch_bounds__(256) void k_ct_finish(cgpu_snapshot s, ct_args a)
+/* policy on the tuple ct_lookup4 left, counters, the reply / related skip.
+ * CT_NEW / CT_ESTABLISHED packets reuse k_ct_prep's forward decision; only
+ * CT_REPLY / CT_RELATED ones run the cascade again, on the reply tuple.
+ * Hot counter slots accumulate in LDS (packed, as k_classify CTR = 1). */
+template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a)
 {
+	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* metrics {reason 0 / 133 / 137 / 155} x {ingress, egress} */
 	uint64_t mcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mbyt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-	const uint64_t stride = (uint64_t)gridDim.x * 256u;
-	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint4 r0 = a.rec[2u * i];
-		const uint32_t meta = r0.w >> 16, len = a.len[i];
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
+		lctr[k] = 0;
+	__syncthreads();
+	const uint64_t stride = (uint64_t)gridDim.x * NT;
+	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) {
+		/* batch order: records stream in, the walker's result is read
+		 * through the inverse permutation */
+		const uint4 r0 = ld_x4<true>(a.rec + 2u * i);
+		const uint4 r1 = ld_x4<true>(a.rec + 2u * i + 1u);
+		const uint32_t meta = r0.w >> 16;
 		const bool egress = meta & CTM_EGRESS;
+		const uint32_t len = r1.y;
 		int32_t v;
-		uint32_t id = 0, st = 4, cr = 255u;
+		uint32_t st = 4, cr = 255u;
 		if (meta & CTM_GATED) {
 			v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup4 default case */
 		} else {
-			const uint32_t c = a.ct_ret[i];
+			const uint32_t c = a.cr_s[a.inv[i]];
 			cr = c & 3u;
-			const bool reply = cr >= CT_REPLY;
-			const uint32_t fl = a.flags[i];
-			const bool frag = !egress && ((fl >> 1) & 1u);
-			const uint32_t dport = reply ? (r0.z & 0xFFFFu) : (r0.z >> 16);
-			const decision d = decide<0, false>(s, egress, frag, r0.y, r0.x, uint4{}, uint4{},
-							    dport, r0.w & 0xFFu, a.ep[i]);
-			if (d.ctr >= 0) {
-				atomicAdd((unsigned long long *)&a.delta[2u * (uint32_t)d.ctr], 1ull);
-				atomicAdd((unsigned long long *)&a.delta[2u * (uint32_t)d.ctr + 1u],
-					  (unsigned long long)len);
-			}
-			id = d.id;
-			st = d.st;
-			if (reply)
+			int ctr;
+			if (cr >= CT_REPLY) {
+				const bool frag = meta & CTM_FRAG;
+				const decision d = decide<0, false>(s, egress, frag, r0.y, r0.x, uint4{}, uint4{},
+								    r0.z & 0xFFFFu, r0.w & 0xFFu, a.ep[i]);
+				ctr = d.ctr;
+				st = d.st;
 				v = (egress && d.v > 0) ? d.v : 0;
-			else if (d.v < 0)
-				v = DROP_POLICY;
-			else if (c & CT_FAIL)
-				v = DROP_CT_CREATE_FAILED;
-			else
-				v = d.v;
+			} else {
+				ctr = (int)(r1.w & 0xFFFFFFu) - 1;
+				st = r1.w >> 24;
+				if (!(meta & CTM_ALLOWED))
+					v = DROP_POLICY;
+				else if (c & CT_FAIL)
+					v = DROP_CT_CREATE_FAILED;
+				else
+					v = (int32_t)(r1.x >> 16);
+			}
+			if (ctr >= 0) {
+				const uint32_t cs = (uint32_t)ctr;
+				if (cs < s.hot_slots && len < PK_MAX_LEN) {
+					atomicAdd((unsigned long long *)&lctr[cs],
+						  (1ull << PK_SHIFT) | (unsigned long long)len);
+				} else {
+					atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
+					atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u], (unsigned long long)len);
+				}
+			}
 		}
 		a.verdict[i] = v;
-		a.identity[i] = id;
 		a.ct_ret[i] = (uint8_t)cr;
 		if (a.stage)
 			a.stage[i] = (uint8_t)st;
@@ -2631,6 +2887,14 @@ __global__ __launch_bounds__(256) void k_ct_finish(cgpu_snapshot s, ct_args a)
 			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
 		}
 	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
+		const uint64_t x = lctr[k];
+		if (x) {
+			atomicAdd((unsigned long long *)&a.delta[2u * k], x >> PK_SHIFT);
+			atomicAdd((unsigned long long *)&a.delta[2u * k + 1u], x & PK_BYTES_MASK);
+		}
+	}
 }
 
 /* hipcub temporary storage for the sort and the head selection of n packets */
@@ -2650,7 +2914,8 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 {
 	ct_args a{L.saddr, L.daddr, L.sport, L.dport, L.proto, L.l4, L.flags, L.len, L.ep,
 		  L.verdict, L.ct_ret, L.identity, L.stage, L.delta, L.n, L.now,
-		  L.rec, L.gkey, L.gkey_sorted, L.idx, L.idx_sorted, L.head, L.heads, L.n_heads};
+		  L.rec, L.rec_s, L.cr_s, L.inv, L.gkey, L.gkey_sorted, L.idx, L.idx_sorted, L.head, L.heads,
+		  L.n_heads};
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_ct_prep, dim3(g), dim3(256), 0, st, s, a);
 	size_t tb = L.temp_bytes;
@@ -2664,8 +2929,14 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.head, L.heads, L.n_heads, (int)L.n, st);
 	if (e != hipSuccess)
 		return e;
+	hipLaunchKernelGGL(k_ct_gather, dim3(g), dim3(256), 0, st, a);
 	/* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
 	hipLaunchKernelGGL(k_ct_walk, dim3(2048), dim3(256), 0, st, T, a);
-	hipLaunchKernelGGL(k_ct_finish, dim3(g), dim3(256), 0, st, s, a);
+	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
+	constexpr int NF = 1024;
+	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((L.n + NF - 1) / NF, 512),
+					       (L.n >> 22) + 1);
+	hipLaunchKernelGGL((k_ct_finish<NF>), dim3((unsigned)gf), dim3(NF), (size_t)s.hot_slots * 8u, st,
+			   s, a);
 	return hipGetLastError();
 }

@@ -316,6 +316,7 @@ typedef struct ct_table {
 	uint32_t mask;      /* nslots - 1 */
 	uint32_t max;       /* CT_MAP_SIZE: live entries allowed */
 	uint32_t *count;    /* [0] live entries, [1] tombstones */
+	uint32_t res_chunk; /* capacity a workgroup reserves at a time (headroom-sized) */
 } ct_table;
 
 #if defined(__HIPCC__)

@@ -1,0 +1,27 @@
+"""Diagnostic: batch 0 of test_ct_stream_vs_restatement, GPU vs restatement."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "oracle"))
+import numpy as np
+import torch
+from cilium_amd import synth
+from cilium_amd.engine import Engine
+from oracle import Oracle
+
+T = synth.make_tables(**synth.CONFIGS["cpu"])
+t, lb, sl = synth.make_ct_workload(T, 60_000, mean_pkts=10.0, span=0.05)
+n = len(t["saddr"]) // 3
+tb = {k: v[:n] for k, v in t.items()}
+o = Oracle(**T.oracle_config()); synth.load_oracle(o, T); synth.load_lxc(o, sl); o.ct_set_max(1 << 18)
+v0, cr0, i0, s0, _ = o.classify_v4_ct(tb, 1000)
+e = Engine(device=0, **T.engine_config(), ct_max=1 << 18)
+synth.load_engine(e, T); synth.load_lxc(e, sl); e.commit()
+out = e.classify_v4_ct(synth.to_device(tb), 1000)
+torch.cuda.synchronize()
+v = out["verdict"].cpu().numpy(); cr = out["ct_ret"].cpu().numpy()
+bad = np.nonzero(v != v0)[0]
+print("chunk env", os.environ.get("CGPU_CT_CHUNK"), "mismatch", len(bad), "of", n,
+      "gpu count", e.ct4_count(), "oracle count", o.ct4_count())
+for i in bad[:10]:
+    print(i, v[i], v0[i], cr[i], cr0[i], tb["proto"][i], tb["flags"][i])
+print("gpu -155:", (v == -155).sum(), "oracle -155:", (v0 == -155).sum())
