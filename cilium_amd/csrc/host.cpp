@@ -2504,8 +2504,8 @@ CGPU_EXPORT int cgpu_ct4_flush(cgpu_ctx *c)
 
 /* scratch of one cgpu_classify_v4_ct launch over n packets */
 struct CtScratch {
-	size_t rec, rec_s, cr_s, inv, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, head, temp, temp_bytes,
-		total;
+	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, heads_pos, head,
+		temp, temp_bytes, total;
 };
 
 static CtScratch ct_scratch_layout(uint64_t n)
@@ -2517,15 +2517,13 @@ static CtScratch ct_scratch_layout(uint64_t n)
 		return off;
 	};
 	L.rec = take(n * 32);
-	L.rec_s = take(n * 32);
-	L.cr_s = take(n);
-	L.inv = take(n * 4);
 	L.gkey = take(n * 4);
 	L.gkey_sorted = take(n * 4);
 	L.idx = take(n * 4);
 	L.idx_sorted = take(n * 4);
 	L.heads = take(n * 4);
 	L.n_heads = take(4);
+	L.heads_pos = take(n * 4);
 	L.head = take(n);
 	L.temp_bytes = ct_temp_bytes(n);
 	L.temp = take(L.temp_bytes);
@@ -2585,13 +2583,12 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 	ct_table T{c->d_ct_keys, c->d_ct_vals, c->ct_mask, c->cfg.ct_max, c->d_ct_count, chunk};
 	ct_launch a{t->saddr, t->daddr, t->sport, t->dport, t->proto, t->l4, t->flags, t->len, t->ep,
 		    verdict, ct_ret, identity, stage, delta, (uint64_t)n, now,
-		    reinterpret_cast<uint4 *>(b + L.rec), reinterpret_cast<uint4 *>(b + L.rec_s), b + L.cr_s,
-		    reinterpret_cast<uint32_t *>(b + L.inv),
+		    reinterpret_cast<uint4 *>(b + L.rec),
 		    reinterpret_cast<uint32_t *>(b + L.gkey),
 		    reinterpret_cast<uint32_t *>(b + L.gkey_sorted), reinterpret_cast<uint32_t *>(b + L.idx),
 		    reinterpret_cast<uint32_t *>(b + L.idx_sorted), b + L.head,
 		    reinterpret_cast<uint32_t *>(b + L.heads), reinterpret_cast<uint32_t *>(b + L.n_heads),
-		    b + L.temp, L.temp_bytes};
+		    reinterpret_cast<uint32_t *>(b + L.heads_pos), b + L.temp, L.temp_bytes};
 	HIP_OR_EIO(launch_classify_v4_ct(s, T, a, (hipStream_t)stream));
 	c->ct_dev_newer = true;
 	return 0;

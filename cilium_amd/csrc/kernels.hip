@@ -2246,17 +2246,24 @@ __device__ __forceinline__ void st_wt32(void *p, uint32_t v)
 
 /* one struct ct_entry row: a,b = rx/tx packets|bytes, c = {lifetime,
  * bits | rev_nat << 16, slave | tx_flags_seen << 16 | rx_flags_seen << 24,
- * src_sec_id}, d = {last_tx_report, last_rx_report, 0, 0} */
+ * src_sec_id}, d = {last_tx_report, last_rx_report} (the row's last 8 bytes
+ * are padding) */
 struct ct_row {
-	uint4 a, b, c, d;
+	uint4 a, b, c;
+	uint2 d;
 };
 
 __device__ __forceinline__ ct_row ct_row_load(const ct_table &T, uint32_t slot)
 {
 	const uint4 *p = T.vals + 4u * slot;
-	return ct_row{ld_x4<true>(p), ld_x4<true>(p + 1), ld_x4<true>(p + 2), ld_x4<true>(p + 3)};
+	const uint4 d = ld_x4<true>(p + 3);
+	return ct_row{ld_x4<true>(p), ld_x4<true>(p + 1), ld_x4<true>(p + 2), uint2{d.x, d.y}};
 }
 
+/* Write-through stores complete asynchronously: a later load of the same
+ * bytes by this lane (after the entry was evicted from its cache and is
+ * probed again) could be served from memory before the store lands.  Every
+ * store burst to the map therefore ends with a wait for its completion. */
 __device__ __forceinline__ void ct_row_store(const ct_table &T, uint32_t slot, const ct_row &e)
 {
 	uint32_t *p = reinterpret_cast<uint32_t *>(T.vals + 4u * slot);
@@ -2267,6 +2274,7 @@ __device__ __forceinline__ void ct_row_store(const ct_table &T, uint32_t slot, c
 	st_wt64(p + 8, e.c.x, e.c.y);
 	st_wt64(p + 10, e.c.z, e.c.w);
 	st_wt64(p + 12, e.d.x, e.d.y);
+	__builtin_amdgcn_s_waitcnt(0);
 }
 
 __device__ __forceinline__ void add64(uint32_t &lo, uint32_t &hi, uint32_t v)
@@ -2430,6 +2438,7 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, ui
 				uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + h);
 				st_wt64(p, k.x, k.y);
 				st_wt32(p + 2, k.z);
+				__builtin_amdgcn_s_waitcnt(0);
 				return (int)h;
 			}
 		}
@@ -2440,13 +2449,17 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, ui
 }
 
 /* map_delete_elem: the row and key words are retired before the tag turns
- * into a tombstone another lane may claim (release at agent scope) */
+ * into a tombstone another lane may claim.  Every store to the map is
+ * write-through, so draining this lane's outstanding stores (vmcnt 0) is
+ * the whole release: no L2 write-back (an agent-scope release fence would
+ * write back the XCD's entire L2 for every delete). */
 __device__ __forceinline__ void ct_erase(const ct_table &T, const ct_acct &A, uint32_t slot)
 {
 	uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + slot);
 	st_wt64(p, 0u, 0u);
 	st_wt32(p + 2, 0u);
-	__hip_atomic_exchange(&T.keys[slot].w, CT_TAG_TOMB << 16, __ATOMIC_RELEASE,
+	__builtin_amdgcn_s_waitcnt(0);
+	__hip_atomic_exchange(&T.keys[slot].w, CT_TAG_TOMB << 16, __ATOMIC_RELAXED,
 			      __HIP_MEMORY_SCOPE_AGENT);
 	atomicAdd(A.live, 1);
 	atomicAdd(A.tombs, 1);
@@ -2469,13 +2482,11 @@ struct ct_args {
 	uint32_t now;
 	/* scratch */
 	uint4 *rec;                  /* [2n] per packet, batch order */
-	uint4 *rec_s;                /* [2n] the same, in group order */
-	uint8_t *cr_s;               /* [n] walker result, group order */
-	uint32_t *inv;               /* [n] batch position -> group-order position */
 	uint32_t *gkey, *gkey_sorted; /* [n] */
 	uint32_t *idx, *idx_sorted;   /* [n] */
 	uint8_t *head;               /* [n] */
 	uint32_t *heads, *n_heads;   /* [n], [1] */
+	const uint32_t *gpos, *glen; /* [n_heads] group start / length, longest first */
 };
 
 /* ct_lookup4's tuple setup, conntrack.h:461-528 */
@@ -2537,25 +2548,25 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 	}
 }
 
-__global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *head, uint64_t n)
+/* length of every group (keys) and its start (values), for the longest-
+ * first sort */
+__global__ __launch_bounds__(256) void k_ct_lens(const uint32_t *heads, uint32_t nh, uint64_t n,
+						 uint32_t *len, uint32_t *pos)
+{
+	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += gridDim.x * 256u) {
+		const uint32_t p0 = heads[h];
+		len[h] = (uint32_t)((h + 1u < nh ? (uint64_t)heads[h + 1u] : n) - p0);
+		pos[h] = p0;
+	}
+}
+
+/* a group starts where the SORTED bits of the key change (keys that agree
+ * on them are one group even if their other bits differ) */
+__global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *head, uint64_t n, uint32_t mask)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
 	for (uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x; p < n; p += stride)
-		head[p] = (p == 0 || g[p] != g[p - 1]) ? 1u : 0u;
-}
-
-/* records into group order, so that each walker lane reads its group's
- * packets sequentially instead of gathering them one by one */
-__global__ __launch_bounds__(256) void k_ct_gather(ct_args a)
-{
-	const uint64_t stride = (uint64_t)gridDim.x * 256u;
-	for (uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x; p < a.n; p += stride) {
-		const uint32_t i = a.idx_sorted[p];
-		const uint4 r0 = a.rec[2u * i], r1 = a.rec[2u * i + 1u];
-		a.rec_s[2u * p] = r0;
-		a.rec_s[2u * p + 1u] = r1;
-		a.inv[i] = (uint32_t)p;
-	}
+		head[p] = (p == 0 || ((g[p] ^ g[p - 1]) & mask)) ? 1u : 0u;
 }
 
 /* A lane's cache of the map entries its group touched.  The lane owns every
@@ -2637,7 +2648,8 @@ __device__ __forceinline__ uint4 sel4(bool t, uint4 a, uint4 b)
 
 __device__ __forceinline__ ct_row selrow(bool t, const ct_row &a, const ct_row &b)
 {
-	return ct_row{sel4(t, a.a, b.a), sel4(t, a.b, b.b), sel4(t, a.c, b.c), sel4(t, a.d, b.d)};
+	return ct_row{sel4(t, a.a, b.a), sel4(t, a.b, b.b), sel4(t, a.c, b.c),
+		      uint2{t ? a.d.x : b.d.x, t ? a.d.y : b.d.y}};
 }
 
 __device__ __forceinline__ ct_row ctc_row(ct_cache &c, int i)
@@ -2784,15 +2796,30 @@ __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
 	const uint32_t stride = gridDim.x * 256u;
 	ctc_ent e0{}, e1{}, e2{}, e3{};
 	ct_cache c{e0, e1, e2, e3, 0u};
+	/* groups longest first (a.glen / a.gpos, sorted by length): the
+	 * elephants start in the first round and the rest fill in behind */
 	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {
-		const uint64_t p0 = a.heads[h];
-		const uint64_t p1 = h + 1u < nh ? a.heads[h + 1u] : a.n;
+		const uint64_t p0 = a.gpos[h];
+		const uint64_t p1 = p0 + a.glen[h];
+		/* packets in batch order through the sort permutation, software-
+		 * pipelined: the record of p + 1 and the index of p + 2 are in
+		 * flight while packet p runs */
+		uint32_t ni = a.idx_sorted[p0];
+		uint32_t nni = p0 + 1u < p1 ? a.idx_sorted[p0 + 1u] : 0u;
+		uint4 n0 = a.rec[2u * ni], n1 = a.rec[2u * ni + 1u];
 		for (uint64_t p = p0; p < p1; p++) {
-			const uint4 r0 = ld_x4<true>(a.rec_s + 2u * p);
-			const uint4 r1 = ld_x4<true>(a.rec_s + 2u * p + 1u);
+			const uint32_t i = ni;
+			const uint4 r0 = n0, r1 = n1;
+			if (p + 1u < p1) {
+				ni = nni;
+				n0 = a.rec[2u * ni];
+				n1 = a.rec[2u * ni + 1u];
+				if (p + 2u < p1)
+					nni = a.idx_sorted[p + 2u];
+			}
 			if ((r0.w >> 16) & CTM_GATED)
 				continue;
-			a.cr_s[p] = (uint8_t)ct_step(T, A, c, r0, r1, a.now);
+			a.ct_ret[i] = (uint8_t)ct_step(T, A, c, r0, r1, a.now);
 		}
 		ctc_flush(T, c);
 	}
@@ -2820,8 +2847,7 @@ template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapsho
 	__syncthreads();
 	const uint64_t stride = (uint64_t)gridDim.x * NT;
 	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) {
-		/* batch order: records stream in, the walker's result is read
-		 * through the inverse permutation */
+		/* batch order: records and the walker's results stream in */
 		const uint4 r0 = ld_x4<true>(a.rec + 2u * i);
 		const uint4 r1 = ld_x4<true>(a.rec + 2u * i + 1u);
 		const uint32_t meta = r0.w >> 16;
@@ -2832,7 +2858,7 @@ template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapsho
 		if (meta & CTM_GATED) {
 			v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup4 default case */
 		} else {
-			const uint32_t c = a.cr_s[a.inv[i]];
+			const uint32_t c = a.ct_ret[i];
 			cr = c & 3u;
 			int ctr;
 			if (cr >= CT_REPLY) {
@@ -2897,6 +2923,16 @@ template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapsho
 	}
 }
 
+static int ct_sort_bits()
+{
+	static int bits = -1;
+	if (bits < 0) {
+		const char *e = getenv("CGPU_CT_SORT_BITS"); /* diagnostic override */
+		bits = e ? std::max(8, std::min(32, atoi(e))) : 24;
+	}
+	return bits;
+}
+
 /* hipcub temporary storage for the sort and the head selection of n packets */
 size_t ct_temp_bytes(uint64_t n)
 {
@@ -2914,22 +2950,40 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 {
 	ct_args a{L.saddr, L.daddr, L.sport, L.dport, L.proto, L.l4, L.flags, L.len, L.ep,
 		  L.verdict, L.ct_ret, L.identity, L.stage, L.delta, L.n, L.now,
-		  L.rec, L.rec_s, L.cr_s, L.inv, L.gkey, L.gkey_sorted, L.idx, L.idx_sorted, L.head, L.heads,
+		  L.rec, L.gkey, L.gkey_sorted, L.idx, L.idx_sorted, L.head, L.heads,
 		  L.n_heads};
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_ct_prep, dim3(g), dim3(256), 0, st, s, a);
 	size_t tb = L.temp_bytes;
+	/* 24 key bits: three passes; pairs sharing a 24-bit hash merge into
+	 * one group, which only lengthens that lane's walk */
 	hipError_t e = hipcub::DeviceRadixSort::SortPairs(L.temp, tb, L.gkey, L.gkey_sorted, L.idx,
-							   L.idx_sorted, (int)L.n, 0, 32, st);
+							   L.idx_sorted, (int)L.n, 0, ct_sort_bits(), st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL(k_ct_heads, dim3(g), dim3(256), 0, st, L.gkey_sorted, L.head, L.n);
+	const int bits = ct_sort_bits();
+	const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+	hipLaunchKernelGGL(k_ct_heads, dim3(g), dim3(256), 0, st, L.gkey_sorted, L.head, L.n, mask);
 	hipcub::CountingInputIterator<uint32_t> it(0);
 	tb = L.temp_bytes;
 	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.head, L.heads, L.n_heads, (int)L.n, st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL(k_ct_gather, dim3(g), dim3(256), 0, st, a);
+	/* groups longest first: gkey / idx are free again and hold (length,
+	 * start) before the sort, gkey_sorted / idx the sorted pairs after */
+	uint32_t nh = 0;
+	e = hipMemcpyAsync(&nh, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+		return e;
+	const unsigned gh = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nh + 255) / 256, 8192));
+	hipLaunchKernelGGL(k_ct_lens, dim3(gh), dim3(256), 0, st, L.heads, nh, L.n, L.gkey, L.heads_pos);
+	tb = L.temp_bytes;
+	e = hipcub::DeviceRadixSort::SortPairsDescending(L.temp, tb, L.gkey, L.gkey_sorted, L.heads_pos,
+							 L.idx, (int)nh, 0, 32, st);
+	if (e != hipSuccess)
+		return e;
+	a.glen = L.gkey_sorted;
+	a.gpos = L.idx;
 	/* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
 	hipLaunchKernelGGL(k_ct_walk, dim3(2048), dim3(256), 0, st, T, a);
 	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */

@@ -109,12 +109,11 @@ struct ct_launch {
 	uint64_t *delta;
 	uint64_t n;
 	uint32_t now;
-	uint4 *rec, *rec_s;
-	uint8_t *cr_s;
-	uint32_t *inv;
+	uint4 *rec;
 	uint32_t *gkey, *gkey_sorted, *idx, *idx_sorted;
 	uint8_t *head;
 	uint32_t *heads, *n_heads;
+	uint32_t *heads_pos; /* [n] scratch for the longest-first group sort */
 	void *temp;
 	size_t temp_bytes;
 };

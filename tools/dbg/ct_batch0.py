@@ -19,9 +19,12 @@ synth.load_engine(e, T); synth.load_lxc(e, sl); e.commit()
 out = e.classify_v4_ct(synth.to_device(tb), 1000)
 torch.cuda.synchronize()
 v = out["verdict"].cpu().numpy(); cr = out["ct_ret"].cpu().numpy()
-bad = np.nonzero(v != v0)[0]
-print("chunk env", os.environ.get("CGPU_CT_CHUNK"), "mismatch", len(bad), "of", n,
+bad = np.nonzero((v != v0) | (cr != cr0))[0]
+print("sort bits", os.environ.get("CGPU_CT_SORT_BITS"), "chunk env", os.environ.get("CGPU_CT_CHUNK"), "mismatch", len(bad), "of", n,
       "gpu count", e.ct4_count(), "oracle count", o.ct4_count())
 for i in bad[:10]:
-    print(i, v[i], v0[i], cr[i], cr0[i], tb["proto"][i], tb["flags"][i])
+    sa, da = tb["saddr"][i], tb["daddr"][i]
+    same = np.nonzero(((tb["saddr"] == sa) & (tb["daddr"] == da)) | ((tb["saddr"] == da) & (tb["daddr"] == sa)))[0]
+    print(i, v[i], v0[i], cr[i], cr0[i], tb["proto"][i], tb["flags"][i], tb["l4b"][i], "pair pkts", len(same),
+          "pos", int(np.searchsorted(same, i)))
 print("gpu -155:", (v == -155).sum(), "oracle -155:", (v0 == -155).sum())
