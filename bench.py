@@ -119,8 +119,10 @@ def main():
         synth.load_prefilter6(e, P)
     elif ct:
         T = synth.make_tables(**cfg)
+        # each rank's stream is its conntrack shard (address pairs with
+        # pairhash % world == rank): per-rank maps, no shared state
         tup, _, seclabels = synth.make_ct_workload(T, n // CT_PKTS_PER_CONN, gpu_id=rank,
-                                                   mean_pkts=CT_PKTS_PER_CONN)
+                                                   mean_pkts=CT_PKTS_PER_CONN, world=world)
         n = min(n, len(tup["saddr"]))
         tup = {k: np.ascontiguousarray(v[:n]) for k, v in tup.items()}
         ct_max = 1 << max(20, int(np.ceil(np.log2(2.5 * n / CT_PKTS_PER_CONN))))

@@ -40,6 +40,29 @@ def shard_of(t: dict, world: int) -> np.ndarray:
             np.uint32(world)).astype(np.int64)
 
 
+def pairhash_np(saddr, daddr) -> np.ndarray:
+    """Direction-free 32-bit hash of the unordered address pair.  The
+    stateful path (cgpu_classify_v4_ct) shards by it: every
+    conntrack key a packet reads or writes (forward, reply and ICMP-related
+    tuples) carries that pair, so each rank's conntrack map holds exactly the
+    entries of its own packets and the shards never exchange state."""
+    a = np.asarray(saddr).astype(np.uint64)
+    b = np.asarray(daddr).astype(np.uint64)
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    h = (lo * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
+    h ^= hi
+    h = (h * np.uint64(0x85EBCA77)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(15)
+    h = (h * np.uint64(0xC2B2AE3D)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return h.astype(np.uint32)
+
+
+def ct_shard_of(t: dict, world: int) -> np.ndarray:
+    """Owning rank of every packet of the stateful path: pairhash % world."""
+    return (pairhash_np(t["saddr"], t["daddr"]) % np.uint32(world)).astype(np.int64)
+
+
 def take(t: dict, idx) -> dict:
     return {k: np.ascontiguousarray(v[idx]) for k, v in t.items()}
 

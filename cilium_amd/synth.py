@@ -591,7 +591,7 @@ def frames_to_device(f: dict, device="cuda"):
 # ---------------------------------------------------------------- conntrack
 def make_ct_stream(rng, n_conn: int, locals_be: np.ndarray, remotes_be: np.ndarray,
                    mean_pkts: float = 8.0, span: float = 0.02, frag_frac: float = 0.005,
-                   icmp_err_frac: float = 0.03, other_frac: float = 0.01):
+                   icmp_err_frac: float = 0.03, other_frac: float = 0.01, pair_ok=None):
     """A packet stream of n_conn connections for the stateful path (SURVEY §8f
     row 3), vectorized.  Each connection is between a local endpoint address
     (locals_be[ep], network order) and a remote address, opened from either
@@ -608,6 +608,11 @@ def make_ct_stream(rng, n_conn: int, locals_be: np.ndarray, remotes_be: np.ndarr
     ep = rng.integers(0, E, n_conn)
     loc = np.asarray(locals_be, np.uint32)[ep]
     rem = np.asarray(remotes_be, np.uint32)[rng.integers(0, len(remotes_be), n_conn)]
+    if pair_ok is not None:  # e.g. this rank's conntrack shard: redraw the others
+        bad = ~pair_ok(loc, rem)
+        while bad.any():
+            rem[bad] = np.asarray(remotes_be, np.uint32)[rng.integers(0, len(remotes_be), int(bad.sum()))]
+            bad[bad] = ~pair_ok(loc[bad], rem[bad])
     u = rng.random(n_conn)
     cproto = np.select([u < 0.70, u < 0.90, u < 1.0 - other_frac], [6, 17, 1], 47).astype(np.uint8)
     init_eg = rng.random(n_conn) < 0.6
@@ -669,10 +674,13 @@ def ct_endpoints(n_endpoints: int):
 
 
 def make_ct_workload(tables: Tables, n_conn: int, seed=SEED, gpu_id: int = 0, n_remote=None,
-                     mean_pkts: float = 8.0, span: float = 0.02):
+                     mean_pkts: float = 8.0, span: float = 0.02, world: int = 1):
     """The stateful stream over `tables`: n_conn connections
     between the tables' endpoints and remote addresses (80% inside installed
-    ipcache prefixes), seeded per GPU like make_tuples."""
+    ipcache prefixes), seeded per GPU like make_tuples.  With world > 1 every
+    connection's address pair belongs to rank gpu_id's conntrack shard
+    (shard.pairhash_np % world), so the rank streams are shards of one
+    stream and no conntrack state is shared between ranks."""
     rng = np.random.Generator(np.random.PCG64(seed + 0xC7000 + gpu_id))
     locals_be, seclabels = ct_endpoints(tables.n_endpoints)
     nr = n_remote or max(16, n_conn // 4)
@@ -682,7 +690,11 @@ def make_ct_workload(tables: Tables, n_conn: int, seed=SEED, gpu_id: int = 0, n_
     host = rng.integers(0, 2**32, nr, dtype=np.uint64)
     hmask = (np.uint64(1) << (np.uint64(32) - ln)) - np.uint64(1)
     rem = np.where(rng.random(nr) < 0.8, base | (host & hmask), host).astype(np.uint32).byteswap()
-    t = make_ct_stream(rng, n_conn, locals_be, rem, mean_pkts=mean_pkts, span=span)
+    ok = None
+    if world > 1:
+        from .shard import pairhash_np
+        ok = lambda a, b: (pairhash_np(a, b) % np.uint32(world)) == gpu_id  # noqa: E731
+    t = make_ct_stream(rng, n_conn, locals_be, rem, mean_pkts=mean_pkts, span=span, pair_ok=ok)
     return t, locals_be, seclabels
 
 

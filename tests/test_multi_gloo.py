@@ -104,3 +104,79 @@ def test_gloo_world2_counters_match_single_process():
         v2[mine], i2[mine] = vv, ii
     np.testing.assert_array_equal(v2, v)
     np.testing.assert_array_equal(i2, idt)
+
+
+def _ct_worker(rank, world, port, q):
+    import sys
+    import torch
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    from oracle import Oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    T = synth.make_tables(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+    t, _, sl = synth.make_ct_workload(T, 20_000, mean_pkts=6.0, span=0.05)
+    mine = np.nonzero(shard.ct_shard_of(t, world) == rank)[0]
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_lxc(o, sl)
+    part = shard.take(t, mine)
+    v, cr, idt, st, _ = o.classify_v4_ct(part, 1000)
+    delta = torch.from_numpy(_counters(o, T).view(np.int64).copy())
+    shard.allreduce_counters(delta)
+    keys, vals = o.ct4_dump()
+    objs = [None] * world
+    dist.all_gather_object(objs, (mine, v, cr, keys, vals))
+    if rank == 0:
+        q.put((delta.numpy().view(np.uint64).copy(), objs))
+    dist.destroy_process_group()
+
+
+def test_ct_pair_shards_world2():
+    """Stateful path sharded by address pair (shard.ct_shard_of): each rank
+    runs conntrack over its own packets with its own map.  The verdicts,
+    ct_lookup4 results, merged counters and the union of the two maps equal
+    one process running the whole stream in order."""
+    import multiprocessing as mp
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    from oracle import Oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ct_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    delta, objs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    T = synth.make_tables(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+    t, _, sl = synth.make_ct_workload(T, 20_000, mean_pkts=6.0, span=0.05)
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_lxc(o, sl)
+    v, cr, idt, st, _ = o.classify_v4_ct(t, 1000)
+    gv, gcr = np.empty_like(v), np.empty_like(cr)
+    keys, vals = [], []
+    for mine, pv, pcr, k, vv in objs:
+        gv[mine], gcr[mine] = pv, pcr
+        keys.append(k)
+        vals.append(vv)
+    np.testing.assert_array_equal(gv, v)
+    np.testing.assert_array_equal(gcr, cr)
+    np.testing.assert_array_equal(delta, _counters(o, T))
+    uk, uv = L.ct_sorted(np.concatenate(keys), np.concatenate(vals))
+    ok, ov = o.ct4_dump()
+    np.testing.assert_array_equal(uk, ok)
+    np.testing.assert_array_equal(uv, ov)
+    assert (cr == L.CT_REPLY).sum() > 0 and len(objs[0][0]) > 0 and len(objs[1][0]) > 0
+
+
+def test_ct_workload_rank_streams_are_pair_shards():
+    T = synth.make_tables(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+    for r in range(3):
+        t, _, _ = synth.make_ct_workload(T, 2000, gpu_id=r, world=3)
+        assert (shard.ct_shard_of(t, 3) == r).all()
