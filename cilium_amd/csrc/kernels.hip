@@ -2577,7 +2577,9 @@ __global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *he
  * written back (write-through) when evicted and at the end of the group.
  * CTC entries, round-robin replacement, every access an unrolled select so
  * the cache lives in VGPRs. */
-#define CTC 4
+#ifndef CTC
+#define CTC 4 /* 3 ways measured 14 % slower (more re-probes) */
+#endif
 #define CTC_VALID 0x10000u
 #define CTC_NEG 0x20000u
 #define CTC_DIRTY 0x40000u
@@ -2594,7 +2596,10 @@ struct ctc_ent {
 };
 
 struct ct_cache {
-	ctc_ent &e0, &e1, &e2, &e3;
+	ctc_ent &e0, &e1, &e2;
+#if CTC == 4
+	ctc_ent &e3;
+#endif
 	uint32_t next;
 };
 
@@ -2603,7 +2608,9 @@ template <typename F> __device__ __forceinline__ void ctc_each(ct_cache &c, F &&
 	f(c.e0, 0);
 	f(c.e1, 1);
 	f(c.e2, 2);
+#if CTC == 4
 	f(c.e3, 3);
+#endif
 }
 
 /* Every helper reads all entries unconditionally and writes them back
@@ -2794,8 +2801,13 @@ __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
 	const ct_acct A{&s_acct[0], &s_acct[1], &s_acct[2]};
 	const uint32_t nh = *a.n_heads;
 	const uint32_t stride = gridDim.x * 256u;
+#if CTC == 4
 	ctc_ent e0{}, e1{}, e2{}, e3{};
 	ct_cache c{e0, e1, e2, e3, 0u};
+#else
+	ctc_ent e0{}, e1{}, e2{};
+	ct_cache c{e0, e1, e2, 0u};
+#endif
 	/* groups longest first (a.glen / a.gpos, sorted by length): the
 	 * elephants start in the first round and the rest fill in behind */
 	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {

@@ -572,6 +572,78 @@ int cgpu_classify_v4_ct(cgpu_ctx *ctx, const cgpu_tuples_v4_ct *t, size_t n, uin
 			void *stream);
 
 /* ------------------------------------------------------------------ */
+/* L3 MapState compilation                           */
+/* ------------------------------------------------------------------ */
+/* The label decision computeDesiredL3PolicyMapEntries asks of the policy
+ * repository for every (endpoint, identity) pair (pkg/endpoint/policy.go:
+ * 317-390): Repository.AllowsIngressLabelAccess / AllowsEgressLabelAccess
+ * (pkg/policy/repository.go:80-130, :443-490) over rule.canReachIngress /
+ * canReachEgress (pkg/policy/rule.go:323-405).  Strings are interned by the
+ * caller (cilium_amd/policy.py); every id below is such an interned id. */
+#define CGPU_SEL_IN 0         /* In / = / ==: Has(key) && Get(key) in values */
+#define CGPU_SEL_NOT_IN 1     /* NotIn / !=: !Has(key) || Get(key) not in values */
+#define CGPU_SEL_EXISTS 2
+#define CGPU_SEL_NOT_EXISTS 3 /* DoesNotExist */
+
+/* a label of a LabelArray: ids of its key, of "source.key" and of its value */
+typedef struct cgpu_label {
+	uint32_t key, ext_key, value;
+} cgpu_label;
+
+/* labels.Requirement: any_source -> key is a key id matched against every
+ * label's key (LabelArray.Has/Get with source "any", pkg/labels/array.go:
+ * 92-130); else key is an ext_key id matched against "source.key" */
+typedef struct cgpu_requirement {
+	uint32_t any_source, key, op, values_off, n_values;
+} cgpu_requirement;
+
+/* EndpointSelector: requirements [reqs_off, +n_reqs), all must match;
+ * match_all = matchLabels holds "reserved.all" (selector.go:290-294) */
+typedef struct cgpu_selector {
+	uint32_t reqs_off, n_reqs, match_all;
+} cgpu_selector;
+
+#define CGPU_L3_INGRESS 0
+#define CGPU_L3_EGRESS 1
+#define CGPU_L3_REQUIRES 0 /* FromRequires / ToRequires: must match, else Denied */
+#define CGPU_L3_ALLOWS 1   /* FromEndpoints / ToEndpoints: match without ToPorts -> Allowed */
+typedef struct cgpu_l3_clause {
+	uint32_t dir, kind, selector, has_ports;
+} cgpu_l3_clause;
+
+typedef struct cgpu_l3_program {
+	const cgpu_selector *selectors;
+	uint32_t n_selectors;
+	const cgpu_requirement *reqs;
+	uint32_t n_reqs;
+	const uint32_t *values;
+	uint32_t n_values;
+	const uint32_t *rule_subject; /* per rule: its EndpointSelector */
+	const uint32_t *rule_clauses; /* n_rules + 1 offsets into clauses */
+	uint32_t n_rules;
+	const cgpu_l3_clause *clauses;
+	uint32_t n_clauses;
+} cgpu_l3_program;
+
+/* label arrays: set i = labels[offsets[i] .. offsets[i + 1]) in array order */
+typedef struct cgpu_label_sets {
+	const uint32_t *offsets;
+	const cgpu_label *labels;
+	uint32_t n_sets;
+} cgpu_label_sets;
+
+#define CGPU_L3_INGRESS_ENFORCED 1u /* else ingress allows all (policy.go:351-360) */
+#define CGPU_L3_EGRESS_ENFORCED 2u
+/*
+ * allow_out[e * n_identities + i] (host memory) = bit 0: ingress from
+ * identity i to endpoint e is Allowed; bit 1: egress from e to i is Allowed.
+ * All inputs are host pointers (a control-plane call: it uploads, evaluates
+ * every pair on the device, one lane per pair, and copies the result back).
+ */
+int cgpu_l3_compile(cgpu_ctx *ctx, const cgpu_l3_program *prog, const cgpu_label_sets *endpoints,
+		    const cgpu_label_sets *identities, uint32_t flags, uint8_t *allow_out);
+
+/* ------------------------------------------------------------------ */
 /* counters                                                             */
 /* ------------------------------------------------------------------ */
 /*

@@ -2022,3 +2022,100 @@ int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 		*probe_sum = ops;
 	return 0;
 }
+
+/* ====================================================================== */
+/* L3 MapState compilation                              */
+/* ====================================================================== */
+struct or_label { uint32_t key, ext_key, value; };
+struct or_req { uint32_t any_source, key, op, values_off, n_values; };
+struct or_sel { uint32_t reqs_off, n_reqs, match_all; };
+struct or_clause { uint32_t dir, kind, selector, has_ports; };
+
+/* LabelArray.Has / Get (pkg/labels/array.go:92-130): the FIRST label whose
+ * key (any source) or "source.key" matches */
+static const struct or_label *l3_get(const struct or_label *ls, uint32_t n, const struct or_req *r)
+{
+	for (uint32_t i = 0; i < n; i++)
+		if (r->any_source ? ls[i].key == r->key : ls[i].ext_key == r->key)
+			return &ls[i];
+	return NULL;
+}
+
+/* EndpointSelector.Matches (pkg/policy/api/selector.go:277-302) over
+ * labels.Requirement.Matches (k8s.io/apimachinery labels/selector.go:193-208) */
+static int l3_match(const struct or_sel *s, const struct or_req *reqs, const uint32_t *vals,
+		    const struct or_label *ls, uint32_t n)
+{
+	if (s->match_all)
+		return 1;
+	for (uint32_t q = 0; q < s->n_reqs; q++) {
+		const struct or_req *r = &reqs[s->reqs_off + q];
+		const struct or_label *l = l3_get(ls, n, r);
+		int in = 0;
+		if (l)
+			for (uint32_t v = 0; v < r->n_values; v++)
+				in |= vals[r->values_off + v] == l->value;
+		switch (r->op) {
+		case 0: if (!l || !in) return 0; break;   /* In */
+		case 1: if (l && in) return 0; break;     /* NotIn */
+		case 2: if (!l) return 0; break;          /* Exists */
+		default: if (l) return 0; break;          /* DoesNotExist */
+		}
+	}
+	return 1;
+}
+
+/* Repository.AllowsIngressLabelAccess / AllowsEgressLabelAccess
+ * (pkg/policy/repository.go:80-130, :443-490) over rule.canReachIngress /
+ * canReachEgress (pkg/policy/rule.go:323-405), for every (endpoint,
+ * identity) pair; policy disabled in a direction = allow-all
+ * (pkg/endpoint/policy.go:351-389). */
+int or_l3_compile(const void *selectors, const void *reqs, const uint32_t *values,
+		  const uint32_t *rule_subject, const uint32_t *rule_clauses, uint32_t n_rules,
+		  const void *clauses, const uint32_t *ep_off, const void *ep_labels, uint32_t n_ep,
+		  const uint32_t *id_off, const void *id_labels, uint32_t n_id, uint32_t flags,
+		  uint8_t *allow)
+{
+	const struct or_sel *S = selectors;
+	const struct or_req *R = reqs;
+	const struct or_clause *CL = clauses;
+	const struct or_label *EL = ep_labels, *IL = id_labels;
+	for (uint32_t e = 0; e < n_ep; e++) {
+		const struct or_label *el = EL + ep_off[e];
+		const uint32_t en = ep_off[e + 1] - ep_off[e];
+		for (uint32_t i = 0; i < n_id; i++) {
+			const struct or_label *il = IL + id_off[i];
+			const uint32_t in = id_off[i + 1] - id_off[i];
+			int dec[2] = {0, 0}; /* 0 Undecided, 1 Allowed, -1 Denied */
+			for (uint32_t r = 0; r < n_rules; r++) {
+				/* the subject selector matches ctx.To (ingress) and ctx.From
+				 * (egress): both are the endpoint's labels */
+				if (!l3_match(&S[rule_subject[r]], R, values, el, en))
+					continue;
+				for (int d = 0; d < 2; d++) {
+					int rd = 0, denied = 0;
+					if (dec[d] < 0)
+						continue; /* CanReach*RLocked: Denied ends the walk */
+					for (uint32_t c = rule_clauses[r]; c < rule_clauses[r + 1]; c++)
+						if (CL[c].dir == (uint32_t)d && CL[c].kind == 0 &&
+						    !l3_match(&S[CL[c].selector], R, values, il, in))
+							denied = 1;
+					if (denied) {
+						dec[d] = -1;
+						continue;
+					}
+					for (uint32_t c = rule_clauses[r]; c < rule_clauses[r + 1]; c++)
+						if (CL[c].dir == (uint32_t)d && CL[c].kind == 1 && !CL[c].has_ports &&
+						    l3_match(&S[CL[c].selector], R, values, il, in))
+							rd = 1;
+					if (rd)
+						dec[d] = 1;
+				}
+			}
+			allow[(size_t)e * n_id + i] =
+				(uint8_t)((!(flags & 1u) || dec[0] == 1 ? 1 : 0) |
+					  (!(flags & 2u) || dec[1] == 1 ? 2 : 0));
+		}
+	}
+	return 0;
+}

@@ -192,6 +192,17 @@ int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 		      const uint16_t *ep, uint32_t now, int32_t *verdict, uint8_t *ct_ret,
 		      uint32_t *identity, uint8_t *stage, uint64_t *probe_sum);
 
+/*
+ * L3 MapState compilation: the tables of cgpu.h
+ * cgpu_l3_program / cgpu_label_sets (interned ids, see cilium_amd/policy.py);
+ * allow[e * n_id + i] bit 0 = ingress Allowed, bit 1 = egress Allowed.
+ */
+int or_l3_compile(const void *selectors, const void *reqs, const uint32_t *values,
+		  const uint32_t *rule_subject, const uint32_t *rule_clauses, uint32_t n_rules,
+		  const void *clauses, const uint32_t *ep_off, const void *ep_labels, uint32_t n_ep,
+		  const uint32_t *id_off, const void *id_labels, uint32_t n_id, uint32_t flags,
+		  uint8_t *allow);
+
 /* metrics {reason, dir} -> {count, bytes}; out is [256][4][2] u64 */
 void or_metrics_read(or_ctx *c, uint64_t *out);
 void or_counters_reset(or_ctx *c);

@@ -86,6 +86,8 @@ def lib():
         L.or_ct4_gc.restype = sz
         L.or_classify_v4_ct.argtypes = [vp, sz] + [vp] * 9 + [C.c_uint32] + [vp] * 4 + [
             C.POINTER(C.c_uint64)]
+        u32 = C.c_uint32
+        L.or_l3_compile.argtypes = [vp, vp, vp, vp, vp, u32, vp, vp, vp, u32, vp, vp, u32, u32, vp]
         L.or_metrics_read.argtypes = [vp, vp]
         L.or_counters_reset.argtypes = [vp]
         _lib = L
@@ -340,6 +342,22 @@ class Oracle:
                                       _p(ct_ret), _p(identity), _p(stage), C.byref(probes))
         assert rc == 0, rc
         return verdict, ct_ret, identity, stage, probes.value
+
+    # --- L3 MapState compilation ---
+    @staticmethod
+    def l3_compile(prog, ep_sets, id_sets, flags=3):
+        """prog: cilium_amd.policy.L3Program; *_sets: [[Label]].
+        -> allow (n_ep, n_id) uint8: bit 0 ingress, bit 1 egress."""
+        eo, el = prog.label_sets(ep_sets)
+        io, il = prog.label_sets(id_sets)
+        allow = np.zeros((len(ep_sets), len(id_sets)), np.uint8)
+
+        def p(a):
+            return None if a is None or len(a) == 0 else a.ctypes.data_as(C.c_void_p)
+        lib().or_l3_compile(p(prog.selectors), p(prog.reqs), p(prog.values), p(prog.rule_subject),
+                            p(prog.rule_clauses), len(prog.rule_subject), p(prog.clauses), p(eo),
+                            p(el), len(ep_sets), p(io), p(il), len(id_sets), flags, p(allow))
+        return allow
 
     def metrics(self):
         out = np.zeros((256, 4, 2), np.uint64)
