@@ -2593,3 +2593,88 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 	c->ct_dev_newer = true;
 	return 0;
 }
+
+/* ======================================================================= */
+/* L3 MapState compilation                               */
+/* ======================================================================= */
+CGPU_EXPORT int cgpu_l3_compile(cgpu_ctx *c, const cgpu_l3_program *p, const cgpu_label_sets *eps,
+				const cgpu_label_sets *ids, uint32_t flags, uint8_t *allow_out)
+{
+	if (!c || !p || !eps || !ids || (!allow_out && eps->n_sets && ids->n_sets))
+		return fail(-EINVAL, "null argument");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device (host-only); no CPU path");
+	if (!p->rule_clauses || !eps->offsets || !ids->offsets)
+		return fail(-EINVAL, "null offsets");
+	/* validate every index the kernels follow */
+	for (uint32_t r = 0; r < p->n_rules; r++)
+		if (p->rule_subject[r] >= p->n_selectors || p->rule_clauses[r] > p->rule_clauses[r + 1])
+			return fail(-EINVAL, "rule %u out of range", r);
+	if (p->rule_clauses[p->n_rules] > p->n_clauses)
+		return fail(-EINVAL, "clause offsets past n_clauses");
+	for (uint32_t k = 0; k < p->n_clauses; k++)
+		if (p->clauses[k].selector >= p->n_selectors || p->clauses[k].dir > 1 || p->clauses[k].kind > 1)
+			return fail(-EINVAL, "clause %u out of range", k);
+	for (uint32_t k = 0; k < p->n_selectors; k++)
+		if ((uint64_t)p->selectors[k].reqs_off + p->selectors[k].n_reqs > p->n_reqs)
+			return fail(-EINVAL, "selector %u out of range", k);
+	for (uint32_t k = 0; k < p->n_reqs; k++)
+		if ((uint64_t)p->reqs[k].values_off + p->reqs[k].n_values > p->n_values || p->reqs[k].op > 3)
+			return fail(-EINVAL, "requirement %u out of range", k);
+	const uint32_t ne = eps->n_sets, ni = ids->n_sets;
+	for (uint32_t k = 0; k < ne; k++)
+		if (eps->offsets[k] > eps->offsets[k + 1])
+			return fail(-EINVAL, "endpoint label offsets not monotone");
+	for (uint32_t k = 0; k < ni; k++)
+		if (ids->offsets[k] > ids->offsets[k + 1])
+			return fail(-EINVAL, "identity label offsets not monotone");
+	if (!ne || !ni)
+		return 0;
+	const size_t nel = eps->offsets[ne], nil = ids->offsets[ni];
+	/* one device buffer: program, label sets, subject bits, result */
+	size_t off = 0;
+	auto take = [&](size_t b) { size_t o = off; off += (b + 255) & ~(size_t)255; return o; };
+	const size_t o_sel = take(sizeof(cgpu_selector) * p->n_selectors);
+	const size_t o_req = take(sizeof(cgpu_requirement) * p->n_reqs);
+	const size_t o_val = take(4ull * p->n_values);
+	const size_t o_rs = take(4ull * p->n_rules);
+	const size_t o_rc = take(4ull * (p->n_rules + 1));
+	const size_t o_cl = take(sizeof(cgpu_l3_clause) * p->n_clauses);
+	const size_t o_eo = take(4ull * (ne + 1)), o_io = take(4ull * (ni + 1));
+	const size_t o_el = take(sizeof(cgpu_label) * nel), o_il = take(sizeof(cgpu_label) * nil);
+	const size_t o_subj = take((size_t)ne * p->n_rules), o_allow = take((size_t)ne * ni);
+	std::lock_guard<std::mutex> g(c->mu);
+	HIP_OR_EIO(hipSetDevice(c->device));
+	uint8_t *d = nullptr;
+	HIP_OR_EIO(hipMalloc((void **)&d, off));
+	auto up = [&](size_t o, const void *src, size_t b) {
+		return b ? hipMemcpy(d + o, src, b, hipMemcpyHostToDevice) : hipSuccess;
+	};
+	hipError_t e = hipSuccess;
+	if ((e = up(o_sel, p->selectors, sizeof(cgpu_selector) * p->n_selectors)) == hipSuccess &&
+	    (e = up(o_req, p->reqs, sizeof(cgpu_requirement) * p->n_reqs)) == hipSuccess &&
+	    (e = up(o_val, p->values, 4ull * p->n_values)) == hipSuccess &&
+	    (e = up(o_rs, p->rule_subject, 4ull * p->n_rules)) == hipSuccess &&
+	    (e = up(o_rc, p->rule_clauses, 4ull * (p->n_rules + 1))) == hipSuccess &&
+	    (e = up(o_cl, p->clauses, sizeof(cgpu_l3_clause) * p->n_clauses)) == hipSuccess &&
+	    (e = up(o_eo, eps->offsets, 4ull * (ne + 1))) == hipSuccess &&
+	    (e = up(o_io, ids->offsets, 4ull * (ni + 1))) == hipSuccess &&
+	    (e = up(o_el, eps->labels, sizeof(cgpu_label) * nel)) == hipSuccess &&
+	    (e = up(o_il, ids->labels, sizeof(cgpu_label) * nil)) == hipSuccess) {
+		l3_launch L{reinterpret_cast<const cgpu_selector *>(d + o_sel),
+			    reinterpret_cast<const cgpu_requirement *>(d + o_req),
+			    reinterpret_cast<const uint32_t *>(d + o_val),
+			    reinterpret_cast<const uint32_t *>(d + o_rs),
+			    reinterpret_cast<const uint32_t *>(d + o_rc), p->n_rules,
+			    reinterpret_cast<const cgpu_l3_clause *>(d + o_cl),
+			    reinterpret_cast<const uint32_t *>(d + o_eo), reinterpret_cast<const uint32_t *>(d + o_io),
+			    reinterpret_cast<const cgpu_label *>(d + o_el), reinterpret_cast<const cgpu_label *>(d + o_il),
+			    ne, ni, flags, d + o_subj, d + o_allow};
+		if ((e = launch_l3_compile(L, nullptr)) == hipSuccess && (e = hipDeviceSynchronize()) == hipSuccess)
+			e = hipMemcpy(allow_out, d + o_allow, (size_t)ne * ni, hipMemcpyDeviceToHost);
+	}
+	(void)hipFree(d);
+	if (e != hipSuccess)
+		return fail(-EIO, "cgpu_l3_compile: %s", hipGetErrorString(e));
+	return 0;
+}

@@ -3006,3 +3006,128 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 			   s, a);
 	return hipGetLastError();
 }
+
+/* ======================================================================= */
+/* L3 MapState compilation                               */
+/* The batched selector match behind computeDesiredL3PolicyMapEntries      */
+/* (pkg/endpoint/policy.go:317-390): one lane per (endpoint, identity).    */
+/* ======================================================================= */
+struct l3_dev {
+	const cgpu_selector *sel;
+	const cgpu_requirement *req;
+	const uint32_t *val;
+	const uint32_t *rule_subject, *rule_clauses;
+	uint32_t n_rules;
+	const cgpu_l3_clause *cl;
+	const uint32_t *ep_off, *id_off;
+	const cgpu_label *ep_lab, *id_lab;
+	uint32_t n_ep, n_id, flags;
+	uint8_t *subj;  /* [n_ep][n_rules] rule subject matches the endpoint */
+	uint8_t *allow; /* [n_ep][n_id] */
+};
+
+/* EndpointSelector.Matches (api/selector.go:277-302) of labels [l0, l1):
+ * Requirement.Matches (k8s labels/selector.go:193-208) with
+ * LabelArray.Has / Get (pkg/labels/array.go:92-130: the first label whose
+ * key, for the "any" source, or "source.key" matches) */
+__device__ __forceinline__ bool l3_match(const l3_dev &P, uint32_t s, const cgpu_label *lab, uint32_t l0,
+					 uint32_t l1)
+{
+	const cgpu_selector S = P.sel[s];
+	if (S.match_all)
+		return true;
+	for (uint32_t q = 0; q < S.n_reqs; q++) {
+		const cgpu_requirement R = P.req[S.reqs_off + q];
+		int hit = -1;
+		for (uint32_t l = l0; l < l1 && hit < 0; l++) {
+			const cgpu_label L = lab[l];
+			if ((R.any_source ? L.key : L.ext_key) == R.key)
+				hit = (int)L.value;
+		}
+		bool in = false;
+		if (hit >= 0)
+			for (uint32_t v = 0; v < R.n_values; v++)
+				in |= P.val[R.values_off + v] == (uint32_t)hit;
+		const bool has = hit >= 0;
+		bool ok;
+		if (R.op == CGPU_SEL_IN)
+			ok = has && in;
+		else if (R.op == CGPU_SEL_NOT_IN)
+			ok = !(has && in);
+		else if (R.op == CGPU_SEL_EXISTS)
+			ok = has;
+		else
+			ok = !has;
+		if (!ok)
+			return false;
+	}
+	return true;
+}
+
+/* rule subjects against every endpoint: the EndpointSelector is matched
+ * against ctx.To (ingress) and ctx.From (egress), both the endpoint */
+__global__ __launch_bounds__(256) void k_l3_subject(l3_dev P)
+{
+	const uint64_t n = (uint64_t)P.n_ep * P.n_rules;
+	for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256u) {
+		const uint32_t e = (uint32_t)(t / P.n_rules), r = (uint32_t)(t % P.n_rules);
+		P.subj[t] = l3_match(P, P.rule_subject[r], P.ep_lab, P.ep_off[e], P.ep_off[e + 1]) ? 1u : 0u;
+	}
+}
+
+/* Repository.Allows{Ingress,Egress}LabelAccess (repository.go:80-130,
+ * :443-490) over rule.canReach{Ingress,Egress} (rule.go:323-405): a rule
+ * with a failing Requires ends the walk Denied; one whose Endpoints match
+ * without ToPorts makes it Allowed; Allowed only if the walk ends Allowed */
+__global__ __launch_bounds__(256) void k_l3_pairs(l3_dev P)
+{
+	const uint64_t n = (uint64_t)P.n_ep * P.n_id;
+	for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256u) {
+		const uint32_t e = (uint32_t)(t / P.n_id), i = (uint32_t)(t % P.n_id);
+		const uint32_t l0 = P.id_off[i], l1 = P.id_off[i + 1];
+		int dec0 = 0, dec1 = 0; /* 0 undecided, 1 allowed, -1 denied */
+		for (uint32_t r = 0; r < P.n_rules && (dec0 >= 0 || dec1 >= 0); r++) {
+			if (!P.subj[(uint64_t)e * P.n_rules + r])
+				continue;
+			bool den0 = false, den1 = false, al0 = false, al1 = false;
+			for (uint32_t c = P.rule_clauses[r]; c < P.rule_clauses[r + 1]; c++) {
+				const cgpu_l3_clause C = P.cl[c];
+				const bool live = C.dir == CGPU_L3_INGRESS ? dec0 >= 0 : dec1 >= 0;
+				if (!live || (C.kind == CGPU_L3_ALLOWS && C.has_ports))
+					continue;
+				const bool m = l3_match(P, C.selector, P.id_lab, l0, l1);
+				if (C.kind == CGPU_L3_REQUIRES && !m) {
+					if (C.dir == CGPU_L3_INGRESS)
+						den0 = true;
+					else
+						den1 = true;
+				} else if (C.kind == CGPU_L3_ALLOWS && m) {
+					if (C.dir == CGPU_L3_INGRESS)
+						al0 = true;
+					else
+						al1 = true;
+				}
+			}
+			if (dec0 >= 0)
+				dec0 = den0 ? -1 : (al0 ? 1 : dec0);
+			if (dec1 >= 0)
+				dec1 = den1 ? -1 : (al1 ? 1 : dec1);
+		}
+		P.allow[t] = (uint8_t)(((!(P.flags & CGPU_L3_INGRESS_ENFORCED) || dec0 == 1) ? 1u : 0u) |
+				       ((!(P.flags & CGPU_L3_EGRESS_ENFORCED) || dec1 == 1) ? 2u : 0u));
+	}
+}
+
+hipError_t launch_l3_compile(const l3_launch &L, hipStream_t st)
+{
+	const l3_dev P{L.sel, L.req, L.val, L.rule_subject, L.rule_clauses, L.n_rules, L.cl,
+		       L.ep_off, L.id_off, L.ep_lab, L.id_lab, L.n_ep, L.n_id, L.flags, L.subj, L.allow};
+	const uint64_t ns = (uint64_t)L.n_ep * L.n_rules, np = (uint64_t)L.n_ep * L.n_id;
+	if (ns)
+		hipLaunchKernelGGL(k_l3_subject, dim3((unsigned)std::min<uint64_t>((ns + 255) / 256, 8192)),
+				   dim3(256), 0, st, P);
+	if (np)
+		hipLaunchKernelGGL(k_l3_pairs, dim3((unsigned)std::min<uint64_t>((np + 255) / 256, 16384)),
+				   dim3(256), 0, st, P);
+	return hipGetLastError();
+}

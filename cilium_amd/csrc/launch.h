@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "tables.h"
+#include "../../include/cgpu.h"
 
 struct classify_v4_args {
 	const uint32_t *saddr, *daddr;
@@ -121,6 +122,22 @@ struct ct_launch {
 size_t ct_temp_bytes(uint64_t n);
 hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
 				 hipStream_t st);
+
+/* L3 MapState compilation (cgpu_l3_compile): device copies of the program */
+struct l3_launch {
+	const cgpu_selector *sel;
+	const cgpu_requirement *req;
+	const uint32_t *val;
+	const uint32_t *rule_subject, *rule_clauses;
+	uint32_t n_rules;
+	const cgpu_l3_clause *cl;
+	const uint32_t *ep_off, *id_off;
+	const cgpu_label *ep_lab, *id_lab;
+	uint32_t n_ep, n_id, flags;
+	uint8_t *subj, *allow;
+};
+
+hipError_t launch_l3_compile(const l3_launch &L, hipStream_t st);
 
 /* totals[i] += delta[i]; delta[i] = 0 over n u64 words */
 hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st);

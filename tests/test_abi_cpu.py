@@ -57,6 +57,7 @@ def test_host_only_context_has_no_cpu_path():
     fr = Frames(0, 0, 0, 0, 64, 0)
     assert L_.cgpu_classify_frames(e.h, C.byref(fr), 1, None, None, None, None) == -errno.ENODEV
     assert L_.cgpu_frames_parse(e.h, C.byref(fr), 1, None, None) == -errno.ENODEV
+    assert L_.cgpu_l3_compile(e.h, None, None, None, 3, None) == -errno.EINVAL
     tc = TuplesV4Ct()
     assert L_.cgpu_classify_v4_ct(e.h, C.byref(tc), 1, 0, None, None, None, None,
                                   None) == -errno.ENODEV
