@@ -27,6 +27,10 @@ Other BASELINE configs (not the headline line; run them explicitly):
                      updates and reply-skips the same way; parity and the
                      CPU baseline on the packets of 1/64 of the address pairs
                      (pairs are independent conntrack groups)
+  --config mapstate  L3 MapState compilation: the label
+                     decision of computeDesiredL3PolicyMapEntries for 100
+                     endpoints x 65536 identities over a 1000-rule repository
+                     (cgpu_l3_compile, host tables in, allow matrix out)
   --config cpu       config 1 sizes
 """
 from __future__ import annotations
@@ -67,6 +71,9 @@ WORKLOADS = {
     "frames": "config2 tables, 64M raw Ethernet/IPv4/TCP|UDP frames per GPU in 64-byte slots: "
               "header parse (revalidate, ihl, frag, ct_lookup4 ports) fused with ipcache + policy, "
               "bit-exact verdicts",
+    "mapstate": "L3 MapState compilation: 1000 rules (selectors over 3 label sources, In/NotIn/"
+                "Exists/DoesNotExist, FromRequires, L4-restricted blocks) x 100 endpoints x 65536 "
+                "identities, both directions, bit-exact vs the restatement",
     "ct": "config2 tables + stateful conntrack (cilium_ct4_global, SURVEY §8f row 3): 64M packets "
           "per GPU of 2M TCP/UDP/ICMP connections (~32 packets each, both directions, ICMP errors), "
           "map emptied each step: ct_lookup4 -> ipcache -> policy -> reply/related skip, "
@@ -90,6 +97,8 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if args.config == "mapstate":
+        return bench_mapstate(args, rank, world, local)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -352,6 +361,74 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    e.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def bench_mapstate(args, rank, world, local):
+    """one step = cgpu_l3_compile of every (endpoint,
+    identity) pair (upload of the interned tables, the device walk, the
+    allow matrix back).  Ranks take disjoint endpoint slices (weak: each
+    rank compiles its own 100 endpoints against all identities)."""
+    import numpy as np
+    import torch
+
+    from cilium_amd import synth
+    from cilium_amd.engine import Engine
+
+    torch.cuda.set_device(local)
+    t0 = time.time()
+    repo, eps, ids = synth.make_l3_workload(seed=synth.SEED + rank)
+    prog = repo.compile()
+    log(f"[rank {rank}] {len(repo.rules)} rules ({len(prog.clauses)} clauses, {len(prog.selectors)} "
+        f"selectors), {len(eps)} endpoints x {len(ids)} identities in {time.time() - t0:.1f}s")
+    e = Engine(device=local)
+    # the label arrays are interned once, as the agent's identity cache
+    # holds them; a step is the compile of every pair
+    eps_i, ids_i = prog.label_sets(eps), prog.label_sets(ids)
+    for _ in range(args.warmup):
+        allow = e.l3_compile(prog, eps_i, ids_i)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        allow = e.l3_compile(prog, eps_i, ids_i)
+    elapsed = time.perf_counter() - t_start
+    pairs = len(eps) * len(ids)
+    result = None
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle import Oracle
+        c0 = time.perf_counter()
+        ref = Oracle.l3_compile(prog, eps[:2], ids)
+        c_el = time.perf_counter() - c0
+        parity = bool(np.array_equal(allow[:2], ref))
+        value = world * pairs * args.steps / elapsed / 1e6
+        # bytes the walk must read per pair: the identity's labels (12 B
+        # each) and the allow byte; the program and endpoint labels stay
+        # in cache across pairs
+        nlab = sum(len(x) for x in ids) / len(ids)
+        b_pair = 12.0 * nlab + 1.0
+        achieved = b_pair * pairs / (elapsed / args.steps) / 1e9
+        result = {
+            "metric": "M (endpoint, identity) L3 policy decisions/s (computeDesiredL3PolicyMapEntries)",
+            "value": round(value, 2), "unit": "M decisions/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded repository + label sets)",
+            "config": {"workload": WORKLOADS["mapstate"], "rules": len(repo.rules),
+                       "clauses": int(len(prog.clauses)), "selectors": int(len(prog.selectors)),
+                       "endpoints": len(eps), "identities": len(ids), "parity_vs_oracle": parity,
+                       "allowed_frac": {"ingress": round(float((allow & 1).mean()), 4),
+                                        "egress": round(float((allow & 2).astype(bool).mean()), 4)},
+                       "note": "host-pointer control-plane call: the step includes the table "
+                               "upload and the allow-matrix download"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None},
+            "cpu_baseline": {"value": round(2 * len(ids) / c_el / 1e6, 4), "unit": "M decisions/s",
+                             "cores": 1, "kind": "port",
+                             "sample": f"2 endpoints x {len(ids)} identities; oracle/cgpu_oracle.c "
+                                       f"or_l3_compile, 1 thread, {c_el:.2f}s wall"},
+        }
     e.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -219,12 +219,13 @@ class Engine:
     # --- L3 MapState compilation ---
     def l3_compile(self, prog, ep_sets, id_sets, flags: int = 3) -> np.ndarray:
         """cgpu_l3_compile: prog = cilium_amd.policy.L3Program, *_sets =
-        [[Label]] (endpoint / identity label arrays).  -> (n_ep, n_id) uint8,
+        [[Label]] (endpoint / identity label arrays) or their interned form
+        prog.label_sets(...) (offsets, LABEL records).  -> (n_ep, n_id) uint8,
         bit 0 ingress Allowed, bit 1 egress Allowed."""
         from . import policy as P
-        eo, el = prog.label_sets(ep_sets)
-        io, il = prog.label_sets(id_sets)
-        allow = np.zeros((len(ep_sets), len(id_sets)), np.uint8)
+        eo, el = ep_sets if isinstance(ep_sets, tuple) else prog.label_sets(ep_sets)
+        io, il = id_sets if isinstance(id_sets, tuple) else prog.label_sets(id_sets)
+        allow = np.zeros((len(eo) - 1, len(io) - 1), np.uint8)
         cp, ce, ci = P.c_program(prog), P.c_label_sets(eo, el), P.c_label_sets(io, il)
         check(self.L.cgpu_l3_compile(self.h, C.byref(cp), C.byref(ce), C.byref(ci), flags,
                                      allow.ctypes.data), "cgpu_l3_compile")

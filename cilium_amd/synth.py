@@ -703,3 +703,54 @@ def load_lxc(target, seclabels):
     for ep, sl in enumerate(seclabels):
         rc = target.lxc_update(ep, L.lxc_info(b"\0" * 6, 0, b"\0" * 16, 0, int(sl)))
         assert rc == 0, rc
+
+
+# --------------------------------------------------- L3 MapState compilation
+def make_l3_workload(n_rules=1000, n_endpoints=100, n_identities=65536, seed=SEED, n_keys=16,
+                     n_vals=8, requires_frac=0.03):
+    """A policy repository and label sets for cgpu_l3_compile (SURVEY §8f
+    row 4): rules whose subject / peer selectors mix matchLabels over three
+    sources ("k8s", "container", "any") with In / NotIn / Exists /
+    DoesNotExist expressions, some FromRequires and L4-restricted blocks, a
+    few "reserved.all" selectors; endpoints and identities carry 1-5 labels."""
+    from . import policy as P
+    rng = np.random.Generator(np.random.PCG64(seed + 0x13))
+    keys = [f"k{i}" for i in range(n_keys)]
+    srcs = ["k8s", "container", "any"]
+
+    def sel(lo=0):
+        ml = {}
+        for _ in range(rng.integers(lo, 3)):
+            ml[f"{rng.choice(srcs)}.{rng.choice(keys)}"] = f"v{rng.integers(0, n_vals)}"
+        ex = []
+        for _ in range(rng.integers(0, 2)):
+            op = str(rng.choice(["In", "NotIn", "Exists", "DoesNotExist"]))
+            vals = [f"v{x}" for x in rng.integers(0, n_vals, rng.integers(1, 3))] if op in (
+                "In", "NotIn") else []
+            ex.append((f"{rng.choice(srcs)}.{rng.choice(keys)}", op, vals))
+        if rng.random() < 0.02:
+            ml["reserved.all"] = ""
+        return P.EndpointSelector(ml, ex)
+
+    repo = P.Repository()
+    for _ in range(n_rules):
+        ing = [P.IngressRule([sel(1) for _ in range(1 if rng.random() < requires_frac else 0)],
+                             [sel(1) for _ in range(rng.integers(0, 3))], bool(rng.random() < 0.2))
+               for _ in range(rng.integers(0, 3))]
+        eg = [P.EgressRule([sel(1) for _ in range(1 if rng.random() < requires_frac else 0)],
+                           [sel(1) for _ in range(rng.integers(0, 3))], bool(rng.random() < 0.2))
+              for _ in range(rng.integers(0, 3))]
+        repo.add(P.Rule(sel(1), ing, eg))
+
+    def sets(n):
+        nl = rng.integers(1, 6, n)
+        src = rng.choice(np.array(srcs[:2]), int(nl.sum()))
+        key = rng.integers(0, n_keys, int(nl.sum()))
+        val = rng.integers(0, n_vals, int(nl.sum()))
+        out, o = [], 0
+        for c in nl:
+            out.append([P.Label(str(src[o + j]), keys[key[o + j]], f"v{val[o + j]}") for j in range(c)])
+            o += c
+        return out
+
+    return repo, sets(n_endpoints), sets(n_identities)

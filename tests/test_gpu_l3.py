@@ -36,51 +36,15 @@ def test_l3_known_answers_gpu(engine, case):
         assert ("Allowed" if a else "Denied") == ch["expect"], ch
 
 
-def random_repo(rng, n_rules=400, n_keys=12, n_vals=6):
-    keys = [f"k{i}" for i in range(n_keys)]
-    srcs = ["k8s", "container", "any"]
-
-    def sel(lo=0):
-        ml = {}
-        for _ in range(rng.integers(lo, 3)):
-            ml[f"{rng.choice(srcs)}.{rng.choice(keys)}"] = f"v{rng.integers(0, n_vals)}"
-        ex = []
-        for _ in range(rng.integers(0, 2)):
-            op = str(rng.choice(["In", "NotIn", "Exists", "DoesNotExist"]))
-            vals = [f"v{x}" for x in rng.integers(0, n_vals, rng.integers(1, 3))] if op in (
-                "In", "NotIn") else []
-            ex.append((f"{rng.choice(srcs)}.{rng.choice(keys)}", op, vals))
-        if rng.random() < 0.02:
-            ml["reserved.all"] = ""
-        return P.EndpointSelector(ml, ex)
-
-    repo = P.Repository()
-    for _ in range(n_rules):
-        ing = [P.IngressRule([sel(1) for _ in range(1 if rng.random() < 0.03 else 0)],
-                             [sel(1) for _ in range(rng.integers(0, 3))], bool(rng.random() < 0.2))
-               for _ in range(rng.integers(0, 3))]
-        eg = [P.EgressRule([sel(1) for _ in range(1 if rng.random() < 0.03 else 0)],
-                           [sel(1) for _ in range(rng.integers(0, 3))], bool(rng.random() < 0.2))
-              for _ in range(rng.integers(0, 3))]
-        repo.add(P.Rule(sel(1), ing, eg))
-    return repo, keys, srcs, n_vals
-
-
-def random_sets(rng, n, keys, srcs, n_vals):
-    out = []
-    for _ in range(n):
-        out.append([P.Label(str(rng.choice(srcs[:2])), str(rng.choice(keys)),
-                            f"v{rng.integers(0, n_vals)}") for _ in range(rng.integers(1, 6))])
-    return out
+def random_workload(seed):
+    from cilium_amd import synth
+    return synth.make_l3_workload(n_rules=400, n_endpoints=24, n_identities=3000, seed=seed)
 
 
 @pytest.mark.parametrize("flags", [3, 1, 0])
 def test_l3_random_vs_restatement(engine, flags):
-    rng = np.random.Generator(np.random.PCG64(42 + flags))
-    repo, keys, srcs, nv = random_repo(rng)
+    repo, eps, ids = random_workload(42 + flags)
     prog = repo.compile()
-    eps = random_sets(rng, 24, keys, srcs, nv)
-    ids = random_sets(rng, 3000, keys, srcs, nv)
     got = engine.l3_compile(prog, eps, ids, flags)
     ref = Oracle.l3_compile(prog, eps, ids, flags)
     np.testing.assert_array_equal(got, ref)
