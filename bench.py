@@ -317,9 +317,11 @@ def main():
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
         traffic = None
-        if args.config == "gpu" and os.path.exists(args.traffic_json):
+        tj = (args.traffic_json if args.config == "gpu"
+              else os.path.join(ROOT, "profiles", f"traffic_{args.config}.json"))
+        if os.path.exists(tj):
             try:
-                traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+                traffic = json.load(open(tj)).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         conf = {"workload": WORKLOADS[args.config], "tuples_per_gpu": n,

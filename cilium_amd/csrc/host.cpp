@@ -1428,6 +1428,11 @@ uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uin
 		if (x.second != 0xFFFFFFFFu)
 			bnd.push_back(x.second + 1u);
 	}
+	/* a node of <= 8 units (header + 28 boundaries) never straddles a
+	 * 128-B line: k_prefilter_v6_q reads it with one coalesced octet load */
+	const size_t units = 1 + (bnd.size() + 3) / 4;
+	if (units <= 8 && (b.pool.size() / 4) % 8 + units > 8)
+		b.pool.resize((b.pool.size() / 32 + 1) * 32, 0u);
 	const uint32_t off = (uint32_t)(b.pool.size() / 4);
 	b.pool.insert(b.pool.end(), {(uint32_t)bnd.size(), deep ? 1u : 0u, 0u, 0u});
 	b.pool.insert(b.pool.end(), bnd.begin(), bnd.end());
@@ -1603,8 +1608,9 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 	}
 	hop_place<4>(b.h32, b.m32, r32, h32_home);
 	hop_place<8>(b.h64, b.m64, r64, h64_home);
-	if (b.pool.empty())
-		b.pool.assign(4, 0);
+	/* 8 zero units past the last node: the octet load of a node reads
+	 * 128 B from its start whatever its length */
+	b.pool.insert(b.pool.end(), 32, 0u);
 }
 
 /* prefilter v6 any-match set (bpf_xdp.c:132-156): dyn6 (if

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -315,10 +316,9 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 /* ---- service load balancer (bpf/lib/lb.h, bpf/bpf_lb.c) ---- */
 
 /* frontend slot of {addr, dport} (tables.h lb_table); w == 0: no frontend */
-__device__ __forceinline__ uint4 lb_frontend(const lb_table &t, uint32_t addr, uint32_t dport)
+__device__ __forceinline__ uint4 lb_fe_resolve(const lb_table &t, uint32_t home, uint4 s, uint32_t addr,
+					      uint32_t dport)
 {
-	const uint32_t home = lb_hash(addr, dport) & t.fe_mask;
-	const uint4 s = t.fe[home];
 	uint32_t hop = s.w >> POL_HOP_SHIFT;
 	if ((hop & 1u) && s.x == addr && (s.y & 0xFFFFu) == dport)
 		return s;
@@ -332,6 +332,12 @@ __device__ __forceinline__ uint4 lb_frontend(const lb_table &t, uint32_t addr, u
 			r = x;
 	}
 	return r;
+}
+
+__device__ __forceinline__ uint4 lb_frontend(const lb_table &t, uint32_t addr, uint32_t dport)
+{
+	const uint32_t home = lb_hash(addr, dport) & t.fe_mask;
+	return lb_fe_resolve(t, home, t.fe[home], addr, dport);
 }
 
 /* map_lookup_elem(&cilium_lb4_services, {addr, dport, slave}) given the
@@ -445,6 +451,118 @@ __device__ __forceinline__ lb_res lb4_one(const cgpu_snapshot &s, uint32_t sa, u
 	if ((s.lb_flags & CGPU_LB_L4) && port && kd != port && (proto == 6u || proto == 17u))
 		r.dport = port; /* lb4_xlate, lb.h:685-694 */
 	return r;
+}
+
+/*
+ * lb4_one<CGPU_LB_LXC> for the Q tuples of a lane, with each step's gathers
+ * issued together: the first frontend home slots, the L3 retry after a failed
+ * L4 key (lb.h:604-635), then the chosen backend rows.  A tuple whose backend
+ * row is missing (the lb4_local fallback, lb.h:737-744) or whose frontend
+ * needs it leaves for lb4_one itself, so every decision is lb4_one's.  Only
+ * what the classify cascade reads comes back: *drop (DROP_NO_SERVICE), the
+ * translated tuple.daddr and dport.
+ */
+template <int Q>
+__device__ __forceinline__ void lb4_lxc_q(const cgpu_snapshot &s, const uint32_t *sa, uint32_t *da, uint32_t *dp,
+					  const uint32_t *proto, const uint32_t *h, const bool *act, bool *drop)
+{
+	constexpr uint32_t NONE = 0, L4K = 1, L3K = 2, RETRY = 3, FOUND = 4, SLOW = 5;
+	const lb_table &t = s.lb;
+	const bool l4 = s.lb_flags & CGPU_LB_L4, l3 = s.lb_flags & CGPU_LB_L3;
+	uint32_t st[Q], kd[Q], home[Q];
+	uint4 f[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		st[u] = NONE;
+		kd[u] = 0;
+		home[u] = 0;
+		drop[u] = false;
+		if (!act[u])
+			continue;
+		if (l4) { /* lb4_extract_key / extract_l4_port (lb.h:192-216) */
+			if (proto[u] == 6u || proto[u] == 17u)
+				kd[u] = dp[u];
+			else if (proto[u] != 1u && proto[u] != 58u)
+				continue;
+		}
+		if (l4 && kd[u])
+			st[u] = L4K;
+		else if (l3)
+			st[u] = L3K;
+		else
+			continue;
+		home[u] = lb_hash(da[u], kd[u]) & t.fe_mask;
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		f[u] = st[u] != NONE ? t.fe[home[u]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (st[u] == NONE)
+			continue;
+		f[u] = lb_fe_resolve(t, home[u], f[u], da[u], kd[u]);
+		if (f[u].w && (f[u].y >> 16)) {
+			st[u] = FOUND;
+		} else if (st[u] == L4K && l3) {
+			kd[u] = 0;
+			st[u] = RETRY;
+			home[u] = lb_hash(da[u], 0u) & t.fe_mask;
+		} else {
+			st[u] = NONE;
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		if (st[u] == RETRY)
+			f[u] = t.fe[home[u]];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (st[u] != RETRY)
+			continue;
+		f[u] = lb_fe_resolve(t, home[u], f[u], da[u], 0u);
+		st[u] = f[u].w && (f[u].y >> 16) ? FOUND : NONE;
+	}
+	uint32_t bi[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		bi[u] = 0;
+		if (st[u] != FOUND)
+			continue;
+		if (s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u) {
+			drop[u] = true; /* lb4_local's CT_SERVICE lookup (conntrack.h:526-528) */
+			st[u] = NONE;
+			continue;
+		}
+		const uint32_t slave = h[u] % (f[u].y >> 16) + 1u; /* lb4_select_slave, lb.h:158-190 */
+		if (slave > (f[u].w & 0xFFFFu))
+			st[u] = SLOW;
+		else
+			bi[u] = f[u].z + slave - 1u;
+	}
+	uint4 b[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		b[u] = st[u] == FOUND ? t.be[bi[u]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (st[u] == FOUND && !b[u].w)
+			st[u] = SLOW;
+		if (st[u] == FOUND) {
+			if (sa[u] != b[u].x) /* else loopback source NAT: daddr stays (lb.h:753-771) */
+				da[u] = b[u].x;
+			const uint32_t port = b[u].y & 0xFFFFu;
+			if (l4 && port && kd[u] != port && (proto[u] == 6u || proto[u] == 17u))
+				dp[u] = port; /* lb4_xlate, lb.h:685-694 */
+		} else if (st[u] == SLOW) {
+			const lb_res r = lb4_one<CGPU_LB_LXC>(s, sa[u], da[u], dp[u], proto[u], h[u]);
+			if (r.ret == DROP_NO_SERVICE) {
+				drop[u] = true;
+			} else {
+				da[u] = r.tdaddr;
+				dp[u] = r.dport;
+			}
+		}
+	}
 }
 
 template <int MODE> __global__ __launch_bounds__(BLOCK) void k_lb4(cgpu_snapshot s, lb4_args a)
@@ -1003,19 +1121,18 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 							sp[u] = a.sport[i];
 					}
 				}
+				bool act[Q], drop[Q];
 #pragma unroll
 				for (int u = 0; u < Q; u++) {
-					if (!(fl[u] & 1u) || i0 + u >= a.n)
-						continue;
-					const uint32_t h = a.hash ? hh[u] : flow_hash(sa[u], da[u], sp[u], dport[u], proto[u]);
-					const lb_res r = lb4_one<CGPU_LB_LXC>(s, sa[u], da[u], dport[u], proto[u], h);
-					if (r.ret == DROP_NO_SERVICE) {
-						lbf[u] = F_LBDROP;
-					} else {
-						da[u] = r.tdaddr;
-						dport[u] = r.dport;
-					}
+					act[u] = (fl[u] & 1u) && i0 + u < a.n;
+					if (!a.hash)
+						hh[u] = flow_hash(sa[u], da[u], sp[u], dport[u], proto[u]);
 				}
+				lb4_lxc_q<Q>(s, sa, da, dport, proto, hh, act, drop);
+#pragma unroll
+				for (int u = 0; u < Q; u++)
+					if (drop[u])
+						lbf[u] = F_LBDROP;
 			}
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
@@ -1718,6 +1835,61 @@ __device__ __forceinline__ void c6_node32_q(const uint32_t *pool, const uint32_t
 	}
 }
 
+/*
+ * c6_node32_q with each node read cooperatively: the 8 lanes of an octet take
+ * the octet's Q x 8 nodes in turn, lane j loading 16-B unit j of the node, so
+ * one load instruction touches one 128-B line per node instead of one line
+ * per lane and unit (the node pass was 8 L2 requests per packet; the kernel is
+ * bound by L2 request rate, profiles/r1_pf6).  Lane j counts the boundaries of
+ * its unit (4j-4 .. 4j-1) that are <= x, the octet sums them, and the owner
+ * keeps the sum; nodes longer than 28 boundaries finish on the owner lane.
+ * Every lane of the wave must call this (cross-lane reads).  The pool holds
+ * 128 B of padding past its last node (host.cpp cover6 build).
+ */
+template <int Q>
+__device__ __forceinline__ void c6_node32_coop(const uint32_t *pool, const uint32_t (&e)[Q], const uint32_t (&x)[Q],
+					       uint32_t (&tag)[Q], bool (&hit)[Q])
+{
+	const uint4 *P = reinterpret_cast<const uint4 *>(pool);
+	const int lane = (int)__lane_id();
+	const int j = lane & 7, base = lane & ~7;
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		const uint32_t mine = tag[u] == COVER6_NODE ? e[u] & 0x3FFFFFFFu : 0xFFFFFFFFu;
+		uint32_t eo[8], xo[8];
+		uint4 q[8];
+#pragma unroll
+		for (int o = 0; o < 8; o++) {
+			eo[o] = __shfl(mine, base | o);
+			xo[o] = __shfl(x[u], base | o);
+		}
+#pragma unroll
+		for (int o = 0; o < 8; o++)
+			q[o] = eo[o] != 0xFFFFFFFFu ? P[eo[o] + (uint32_t)j] : make_uint4(0, 0, 0, 0);
+		uint32_t cnt = 0, hdr = 0;
+#pragma unroll
+		for (int o = 0; o < 8; o++) {
+			/* node o's header {nb, rest_deep} sits in lane 0's unit */
+			const uint32_t h = __shfl(q[o].x | (q[o].y ? 0x80000000u : 0u), base);
+			uint32_t c = j ? c6_count4(q[o], 4u * (uint32_t)(j - 1), h & 0x7FFFFFFFu, xo[o]) : 0u;
+			c += __shfl_xor(c, 1);
+			c += __shfl_xor(c, 2);
+			c += __shfl_xor(c, 4);
+			if (j == o) {
+				cnt = c;
+				hdr = h;
+			}
+		}
+		if (tag[u] == COVER6_NODE) {
+			const uint32_t nb = hdr & 0x7FFFFFFFu;
+			for (uint32_t k = 28; k < nb; k += 4)
+				cnt += c6_count4(P[(e[u] & 0x3FFFFFFFu) + 1 + k / 4], k, nb, x[u]);
+			hit[u] = cnt & 1u;
+			tag[u] = !hit[u] && (hdr >> 31) ? COVER6_DEEP : COVER6_NONE;
+		}
+	}
+}
+
 /* set16_has whose first bucket is already loaded (tag 0: exact keys) */
 __device__ __forceinline__ bool set16_has_first(const addr_set16 &t, const uint4 (&first)[4], uint32_t b, uint4 key)
 {
@@ -1746,7 +1918,7 @@ __device__ __forceinline__ bool set16_has_first(const addr_set16 &t, const uint4
 	return res;
 }
 
-template <int Q>
+template <int Q, bool COOP = false>
 __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q], const bool (&act)[Q], bool (&hit)[Q])
 {
 	uint32_t w0[Q], w1[Q], w2[Q], w3[Q], e[Q], tag[Q];
@@ -1798,7 +1970,10 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 		tag[u] = r.w ? (r.y >> 30) : COVER6_NONE;
 		hit[u] = tag[u] == COVER6_FULL;
 	}
-	c6_node32_q<Q>(t.pool, e, w1, tag, hit);
+	if (COOP)
+		c6_node32_coop<Q>(t.pool, e, w1, tag, hit);
+	else
+		c6_node32_q<Q>(t.pool, e, w1, tag, hit);
 	/* /64 records */
 	uint4 s0[Q], s1[Q];
 #pragma unroll
@@ -1838,13 +2013,19 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 	}
 }
 
-template <int Q> __global__ __launch_bounds__(256) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a)
+/* W: minimum resident waves per SIMD the registers are fitted to.  COOP:
+ * octet-cooperative /32 node reads (c6_node32_coop); the loop trip count is
+ * then uniform per wave, lanes past the batch end carry inactive packets. */
+template <int Q, int W = 1, bool COOP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_prefilter_v6_q(cgpu_snapshot s,
+												     prefilter_args a)
 {
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
 	const uint64_t T = (uint64_t)gridDim.x * 256;
-	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g * Q < a.n; g += T) {
-		const uint64_t i0 = g * Q;
+	const uint64_t lane0 = COOP ? (threadIdx.x & 63u) : 0u; /* COOP: loop on the wave's first lane */
+	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x - lane0; g * Q < a.n; g += T) {
+		const uint64_t i0 = (g + lane0) * Q;
 		uint4 sa[Q], da[Q];
 		uint32_t f[Q];
 		bool act[Q], hit[Q];
@@ -1858,7 +2039,7 @@ template <int Q> __global__ __launch_bounds__(256) void k_prefilter_v6_q(cgpu_sn
 			f[u] = a.flags[i];
 			act[u] = i0 + u < a.n && f[u] == 0u && s.pf6_enabled;
 		}
-		cover6_any_q<Q>(s.pf6, sa, act, hit);
+		cover6_any_q<Q, COOP>(s.pf6, sa, act, hit);
 		/* check_v6_endpoint: cilium_lxc on daddr (bucket loads for all first) */
 		uint4 bk[Q][4];
 		uint32_t b[Q];
@@ -2120,13 +2301,24 @@ hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, 
 
 hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)
 {
-	/* CGPU_PF6_Q: packets per lane (1 = k_prefilter_v6; default 4) */
+	/* CGPU_PF6_Q = "Q[:V]": packets per lane (1 = k_prefilter_v6) and the
+	 * variant.  Default "4": octet-cooperative node reads.  A/B on config 3
+	 * (Gpps): 4 8.81; 4:1 (per-lane node reads) 8.43; 2 7.34; 4:5 (fitted to
+	 * 5 waves/SIMD) 7.41; per-lane at 5-7 waves/SIMD (Q=3, daddr re-read,
+	 * 4:6, 8:3) 6.5-7.4 -- more resident waves do not help this kernel. */
 	const char *qs = getenv("CGPU_PF6_Q");
 	const int q = qs ? atoi(qs) : 4;
-	if (q == 2)
-		hipLaunchKernelGGL(k_prefilter_v6_q<2>, dim3(grid_for((a.n + 1) / 2)), dim3(BLOCK), 0, st, s, a);
+	const char *vs = qs ? strchr(qs, ':') : nullptr;
+	const int v = vs ? atoi(vs + 1) : 0;
+	if (q == 4 && v == 0)
+		hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st,
+				   s, a);
+	else if (q == 4 && v == 5)
+		hipLaunchKernelGGL((k_prefilter_v6_q<4, 5>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
 	else if (q == 4)
 		hipLaunchKernelGGL(k_prefilter_v6_q<4>, dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
+	else if (q == 2)
+		hipLaunchKernelGGL(k_prefilter_v6_q<2>, dim3(grid_for((a.n + 1) / 2)), dim3(BLOCK), 0, st, s, a);
 	else
 		hipLaunchKernelGGL(k_prefilter_v6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 	return hipGetLastError();

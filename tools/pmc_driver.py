@@ -1,5 +1,6 @@
-"""Minimal driver for rocprofv3 PMC passes: config-2 tables, one 64M-tuple
-batch resident in HBM, 3 classify launches (variant from CGPU_CLASSIFY_VARIANT)."""
+"""Minimal driver for rocprofv3 PMC passes: one bench workload (CGPU_PMC_CONFIG =
+gpu (config 2, default) / cascade (config 5) / pf6 (config 3)), one 64M-tuple
+batch resident in HBM, 3 launches (classify variant from CGPU_CLASSIFY_VARIANT)."""
 import os
 import sys
 
@@ -11,17 +12,40 @@ import torch  # noqa: E402
 from cilium_amd import synth  # noqa: E402
 from cilium_amd.engine import Engine  # noqa: E402
 
-cfg = synth.CONFIGS[os.environ.get("CGPU_PMC_CONFIG", "gpu")]
+name = os.environ.get("CGPU_PMC_CONFIG", "gpu")
+cfg = synth.CONFIGS["gpu" if name == "pf6" else name]
 n = int(os.environ.get("CGPU_PMC_TUPLES", cfg["n_tuples"]))
-T = synth.make_tables(**cfg)
-t = synth.make_tuples(T, n)
-e = Engine(device=0, **T.engine_config())
-synth.load_engine(e, T)
-e.commit()
-d = synth.to_device(t)
-out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
-       "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
-for _ in range(3):
-    e.classify_v4(d, out=out)
+if name == "pf6":
+    # config 3: the v6 prefilter sets of bench.py --config pf6
+    P = synth.make_prefilter6(**synth.PF6_CONFIG)
+    t = synth.make_packets6(P, n)
+    e = Engine(device=0, **P.engine_config())
+    synth.load_prefilter6(e, P)
+    e.commit()
+    d = synth.packets6_to_device(t, "cuda")
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for _ in range(3):
+        e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=v)
+else:
+    T = synth.make_tables(**cfg)
+    t = synth.make_tuples(T, n)
+    ecfg = T.engine_config()
+    S = None
+    if name == "cascade":
+        # config 5: bench.py --config cascade's services and traffic
+        S = synth.make_services(T, cfg["n_services"])
+        t = synth.add_service_traffic(t, S)
+        del t["hash"]
+        ecfg["lb_max_entries"] = len(S.keys)
+    e = Engine(device=0, **ecfg)
+    synth.load_engine(e, T)
+    if S is not None:
+        synth.load_services(e, S)
+    e.commit()
+    d = synth.to_device(t)
+    out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+           "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
+    for _ in range(3):
+        (e.classify_v4_lb if S is not None else e.classify_v4)(d, out=out)
 torch.cuda.synchronize()
-print("ok", n)
+print("ok", name, n)
