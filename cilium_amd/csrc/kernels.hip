@@ -491,6 +491,18 @@ __device__ __forceinline__ void lb4_lxc_q(const cgpu_snapshot &s, const uint32_t
 			st[u] = L3K;
 		else
 			continue;
+		home[u] = lb_vip_bit(da[u]) & t.vip_mask;
+	}
+	/* no frontend has this address (tables.h lb_table.vip): every key of
+	 * lb4_lookup_service misses, the tuple is not load-balanced */
+	uint32_t vw[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		vw[u] = st[u] != NONE ? t.vip[home[u] >> 5] : 0u;
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (!((vw[u] >> (home[u] & 31u)) & 1u))
+			st[u] = NONE;
 		home[u] = lb_hash(da[u], kd[u]) & t.fe_mask;
 	}
 #pragma unroll

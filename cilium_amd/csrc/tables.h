@@ -204,7 +204,20 @@ typedef struct lb_table {
 	const uint4 *be;
 	uint32_t fe_mask;
 	uint32_t n_be;
+	/* presence bitmap over the frontend ADDRESSES (bit lb_vip_bit(addr) &
+	 * vip_mask set for every frontend, any dport): a clear bit proves both
+	 * the L4 and the L3 key of that daddr are absent, so a tuple aimed at no
+	 * service skips its frontend probes.  ~8 bits per frontend (1 MiB at 1M
+	 * services) so it mostly stays in L2 while the 32-MiB frontend table
+	 * does not. */
+	const uint32_t *vip;
+	uint32_t vip_mask;
 } lb_table;
+
+static inline __host__ __device__ uint32_t lb_vip_bit(uint32_t addr)
+{
+	return mix32(addr, 0x5f1b7e11u);
+}
 
 static inline __host__ __device__ uint32_t lb_hash(uint32_t addr, uint32_t dport)
 {
