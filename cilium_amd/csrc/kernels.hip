@@ -2028,7 +2028,7 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 /* W: minimum resident waves per SIMD the registers are fitted to.  COOP:
  * octet-cooperative /32 node reads (c6_node32_coop); the loop trip count is
  * then uniform per wave, lanes past the batch end carry inactive packets. */
-template <int Q, int W = 1, bool COOP = false>
+template <int Q, int W = 1, bool COOP = false, int ABL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_prefilter_v6_q(cgpu_snapshot s,
 												     prefilter_args a)
 {
@@ -2051,14 +2051,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			f[u] = a.flags[i];
 			act[u] = i0 + u < a.n && f[u] == 0u && s.pf6_enabled;
 		}
-		cover6_any_q<Q, COOP>(s.pf6, sa, act, hit);
+		if (ABL == 2) { /* diagnostic ablation: no cover lookup */
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				hit[u] = false;
+		} else {
+			cover6_any_q<Q, COOP>(s.pf6, sa, act, hit);
+		}
 		/* check_v6_endpoint: cilium_lxc on daddr (bucket loads for all first) */
 		uint4 bk[Q][4];
 		uint32_t b[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			b[u] = hash16(da[u].x, da[u].y, da[u].z, da[u].w, 0u) & s.ep6.bucket_mask;
-			const bool need = i0 + u < a.n && f[u] == 0u && !hit[u];
+			const bool need = ABL != 1 && i0 + u < a.n && f[u] == 0u && !hit[u]; /* ABL 1: no endpoint step */
 #pragma unroll
 			for (int k = 0; k < 4; k++)
 				bk[u][k] = need ? reinterpret_cast<const uint4 *>(s.ep6.slots)[(size_t)b[u] * 4u + k]
@@ -2325,6 +2331,10 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 	if (q == 4 && v == 0)
 		hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st,
 				   s, a);
+	else if (q == 4 && v == 8) /* diagnostic ablations (wrong verdicts): no endpoint step / no cover */
+		hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true, 1>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
+	else if (q == 4 && v == 9)
+		hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true, 2>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
 	else if (q == 4 && v == 5)
 		hipLaunchKernelGGL((k_prefilter_v6_q<4, 5>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
 	else if (q == 4)
