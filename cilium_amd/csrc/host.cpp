@@ -1419,8 +1419,13 @@ template <typename T> std::vector<std::pair<T, T>> merge_iv(std::vector<std::pai
 	return out;
 }
 
-/* node {nb, rest_deep, 0, 0} + boundaries: covered iff #(b <= x) is odd */
-uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uint32_t>> &iv, bool deep)
+/* node {nb, rest_deep, nd, 0} + nb boundaries + nd deep points: covered iff
+ * #(b <= x) is odd.  At the /32 level the deep points are the sorted bits
+ * 32..63 of every /64 that has an h64 record, so a reader can tell WHICH
+ * uncovered x descend (c6_node32_coop); readers that ignore them descend on
+ * rest_deep, which is always safe (the h64 probe then misses). */
+uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uint32_t>> &iv, bool deep,
+		       const std::vector<uint32_t> &points = {})
 {
 	std::vector<uint32_t> bnd;
 	for (auto &x : iv) {
@@ -1428,13 +1433,15 @@ uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uin
 		if (x.second != 0xFFFFFFFFu)
 			bnd.push_back(x.second + 1u);
 	}
-	/* a node of <= 8 units (header + 28 boundaries) never straddles a
+	const uint32_t nb = (uint32_t)bnd.size();
+	bnd.insert(bnd.end(), points.begin(), points.end());
+	/* a node of <= 8 units (header + 28 entries) never straddles a
 	 * 128-B line: k_prefilter_v6_q reads it with one coalesced octet load */
 	const size_t units = 1 + (bnd.size() + 3) / 4;
 	if (units <= 8 && (b.pool.size() / 4) % 8 + units > 8)
 		b.pool.resize((b.pool.size() / 32 + 1) * 32, 0u);
 	const uint32_t off = (uint32_t)(b.pool.size() / 4);
-	b.pool.insert(b.pool.end(), {(uint32_t)bnd.size(), deep ? 1u : 0u, 0u, 0u});
+	b.pool.insert(b.pool.end(), {nb, deep ? 1u : 0u, (uint32_t)points.size(), 0u});
 	b.pool.insert(b.pool.end(), bnd.begin(), bnd.end());
 	while (b.pool.size() % 4)
 		b.pool.push_back(0);
@@ -1557,6 +1564,7 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 			std::vector<std::pair<uint32_t, uint32_t>> s2;
 			bool deeper2 = false;
 			size_t first64 = ps.size();
+			std::vector<uint32_t> pts; /* the /64s with an h64 record (sorted by hi) */
 			for (; l < j && (uint32_t)(ps[l].hi >> 32) == top32; l++) {
 				const P6 &p = ps[l];
 				if (p.len > 32 && p.len <= 64) {
@@ -1567,9 +1575,12 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 					deeper2 = true;
 					if (first64 == ps.size())
 						first64 = l;
+					if (pts.empty() || pts.back() != (uint32_t)p.hi)
+						pts.push_back((uint32_t)p.hi);
 				}
 			}
-			const uint32_t e2 = s2.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s2), deeper2);
+			const uint32_t e2 =
+				s2.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s2), deeper2, pts);
 			r32.push_back({top32, e2, 0u, 0u});
 			/* /64 groups */
 			size_t m = first64;

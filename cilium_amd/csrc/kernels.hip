@@ -1878,26 +1878,51 @@ __device__ __forceinline__ void c6_node32_coop(const uint32_t *pool, const uint3
 #pragma unroll
 		for (int o = 0; o < 8; o++)
 			q[o] = eo[o] != 0xFFFFFFFFu ? P[eo[o] + (uint32_t)j] : make_uint4(0, 0, 0, 0);
-		uint32_t cnt = 0, hdr = 0;
+		uint32_t cnt = 0, hdr = 0, nd = 0;
 #pragma unroll
 		for (int o = 0; o < 8; o++) {
-			/* node o's header {nb, rest_deep} sits in lane 0's unit */
+			/* node o's header {nb, rest_deep, nd} sits in lane 0's unit */
 			const uint32_t h = __shfl(q[o].x | (q[o].y ? 0x80000000u : 0u), base);
-			uint32_t c = j ? c6_count4(q[o], 4u * (uint32_t)(j - 1), h & 0x7FFFFFFFu, xo[o]) : 0u;
+			const uint32_t hn = __shfl(q[o].z, base);
+			const uint32_t nb = h & 0x7FFFFFFFu;
+			uint32_t c = 0;
+			if (j) {
+				const uint32_t k0 = 4u * (uint32_t)(j - 1);
+				const uint32_t v[4] = {q[o].x, q[o].y, q[o].z, q[o].w};
+#pragma unroll
+				for (int i = 0; i < 4; i++) {
+					const uint32_t k = k0 + (uint32_t)i;
+					/* boundaries count in bits 0..15, deep points equal to x in 16.. */
+					c += k < nb ? (v[i] <= xo[o] ? 1u : 0u)
+						    : (k < nb + hn && v[i] == xo[o] ? 0x10000u : 0u);
+				}
+			}
 			c += __shfl_xor(c, 1);
 			c += __shfl_xor(c, 2);
 			c += __shfl_xor(c, 4);
 			if (j == o) {
 				cnt = c;
 				hdr = h;
+				nd = hn;
 			}
 		}
 		if (tag[u] == COVER6_NODE) {
 			const uint32_t nb = hdr & 0x7FFFFFFFu;
-			for (uint32_t k = 28; k < nb; k += 4)
-				cnt += c6_count4(P[(e[u] & 0x3FFFFFFFu) + 1 + k / 4], k, nb, x[u]);
-			hit[u] = cnt & 1u;
-			tag[u] = !hit[u] && (hdr >> 31) ? COVER6_DEEP : COVER6_NONE;
+			uint32_t par = cnt & 1u, dp = cnt >> 16;
+			for (uint32_t k = 28; k < nb + nd; k += 4) {
+				const uint4 r = P[(e[u] & 0x3FFFFFFFu) + 1 + k / 4];
+				const uint32_t v[4] = {r.x, r.y, r.z, r.w};
+				for (uint32_t i = 0; i < 4; i++) {
+					if (k + i < nb)
+						par ^= v[i] <= x[u] ? 1u : 0u;
+					else if (k + i < nb + nd)
+						dp |= v[i] == x[u] ? 1u : 0u;
+				}
+			}
+			hit[u] = par;
+			/* with deep points: descend only when x's /64 has a record */
+			const bool deep = nd ? dp != 0 : (hdr >> 31) != 0;
+			tag[u] = !hit[u] && deep ? COVER6_DEEP : COVER6_NONE;
 		}
 	}
 }

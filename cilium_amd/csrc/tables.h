@@ -256,10 +256,12 @@ static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t da
  *        than /64 (an INLINE entry covers [lo, hi] of the low 64 bits).
  * entry: tag << 30 | payload, tag COVER6_NONE / _FULL / _DEEP (consult the
  * next level) / _NODE (payload = offset in 16-B units into `pool`).
- * A node is {nb, rest_deep, 0, 0} + nb sorted boundaries (u32 at levels
+ * A node is {nb, rest_deep, nd, 0} + nb sorted boundaries (u32 at levels
  * 16/32, u64 as {hi, lo} at level 64) of merged covered intervals: an address
  * is covered iff #(boundaries <= x) is odd; otherwise it descends when
- * rest_deep is set.  Typical config-3 packet: root (L2) + h32 slot (L2) +
+ * rest_deep is set.  /32-level nodes then list nd "deep points" (bits 32..63
+ * of each /64 with an h64 record): an uncovered x descends only if it is one
+ * of them (c6_node32_coop; other readers use rest_deep, a safe superset).  Typical config-3 packet: root (L2) + h32 slot (L2) +
  * one node (2 lines) + at most one h64 slot. */
 #define COVER6_NONE 0u
 #define COVER6_FULL 1u
