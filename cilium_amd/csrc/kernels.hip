@@ -393,7 +393,7 @@ struct lb_res {
  * of the reference pin.  tdaddr is tuple.daddr afterwards (LXC: the service
  * address is kept on loopback).
  */
-template <int MODE>
+template <int MODE, bool VIP = true>
 __device__ __forceinline__ lb_res lb4_one(const cgpu_snapshot &s, uint32_t sa, uint32_t da, uint32_t dp,
 					  uint32_t proto, uint32_t hash)
 {
@@ -407,6 +407,13 @@ __device__ __forceinline__ lb_res lb4_one(const cgpu_snapshot &s, uint32_t sa, u
 			kd = dp;
 		else if (proto != 1u && proto != 58u)
 			return r;
+	}
+	/* no frontend has this address (tables.h lb_table.vip): every key
+	 * lb4_lookup_service would try misses */
+	const uint32_t vb = lb_vip_bit(da) & s.lb.vip_mask;
+	if (VIP && !((s.lb.vip[vb >> 5] >> (vb & 31u)) & 1u)) {
+		r.probes = ((s.lb_flags & CGPU_LB_L4) && kd ? 1u : 0u) + ((s.lb_flags & CGPU_LB_L3) ? 1u : 0u);
+		return r;
 	}
 	uint4 f, v;
 	if (!lb_service(s, da, &kd, 0, &v, &f, &r.probes))
@@ -566,7 +573,7 @@ __device__ __forceinline__ void lb4_lxc_q(const cgpu_snapshot &s, const uint32_t
 			if (l4 && port && kd[u] != port && (proto[u] == 6u || proto[u] == 17u))
 				dp[u] = port; /* lb4_xlate, lb.h:685-694 */
 		} else if (st[u] == SLOW) {
-			const lb_res r = lb4_one<CGPU_LB_LXC>(s, sa[u], da[u], dp[u], proto[u], h[u]);
+			const lb_res r = lb4_one<CGPU_LB_LXC, false>(s, sa[u], da[u], dp[u], proto[u], h[u]);
 			if (r.ret == DROP_NO_SERVICE) {
 				drop[u] = true;
 			} else {
