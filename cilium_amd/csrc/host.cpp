@@ -1551,7 +1551,33 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 			i = j;
 			continue;
 		}
-		b.root[top16] = s1.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s1), deeper);
+		/* A /16 node longer than one 128-B line (> 28 boundaries) would be
+		 * scanned by every packet under the /16.  Its long prefixes
+		 * (/28../32, at most 16 /32s each) move down instead: every /32
+		 * they cover gets an h32 record tagged FULL, and the /16 keeps only
+		 * /17../27 intervals. */
+		std::vector<uint32_t> full32; /* sorted low 16 bits of the FULL /32s */
+		auto iv1 = merge_iv(s1);
+		if (iv1.size() > 14) {
+			std::vector<std::pair<uint32_t, uint32_t>> keep;
+			for (auto &x : s1) {
+				if (x.second - x.first < 16u) {
+					for (uint32_t v = x.first; v <= x.second; v++)
+						full32.push_back(v);
+				} else {
+					keep.push_back(x);
+				}
+			}
+			std::sort(full32.begin(), full32.end());
+			full32.erase(std::unique(full32.begin(), full32.end()), full32.end());
+			iv1 = merge_iv(keep);
+			s1.swap(keep);
+		}
+		const bool down = deeper || !full32.empty();
+		b.root[top16] = s1.empty() ? COVER6_DEEP << 30 : cover6_node32(b, iv1, down);
+		auto is_full32 = [&](uint32_t top32) {
+			return std::binary_search(full32.begin(), full32.end(), top32 & 0xFFFFu);
+		};
 		/* /32 groups of the deeper prefixes (sorted by hi: contiguous) */
 		size_t k = i;
 		while (k < j) {
@@ -1561,6 +1587,12 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 			}
 			const uint32_t top32 = (uint32_t)(ps[k].hi >> 32);
 			size_t l = k;
+			if (is_full32(top32)) { /* covered whole: deeper prefixes are moot */
+				while (l < j && (uint32_t)(ps[l].hi >> 32) == top32)
+					l++;
+				k = l;
+				continue;
+			}
 			std::vector<std::pair<uint32_t, uint32_t>> s2;
 			bool deeper2 = false;
 			size_t first64 = ps.size();
@@ -1615,6 +1647,8 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 			}
 			k = l;
 		}
+		for (uint32_t v : full32)
+			r32.push_back({top16 << 16 | v, COVER6_FULL << 30, 0u, 0u});
 		i = j;
 	}
 	hop_place<4>(b.h32, b.m32, r32, h32_home);
