@@ -548,12 +548,15 @@ def test_prefilter6_cover_shapes(torch_cuda, seed):
     and stride boundary: /0../16 (root fill), /17../32 (root node), /33../64
     (/32 node), /65../128 (/64 node or inline), nested and overlapping
     prefixes, all-ones boundaries; addresses drawn at and around the edges of
-    every prefix.  Bit-exact against the restatement's kernel-like LPM trie."""
+    every prefix.  Each /16 root holds enough /17../32 prefixes that its node
+    would exceed one line, so its /28../32 prefixes move down to FULL /32
+    records (also over /32s with deeper prefixes) while /17../27 stay in the
+    /16 node.  Bit-exact against the restatement's kernel-like LPM trie."""
     from oracle import Oracle
     torch = torch_cuda
     rng = np.random.default_rng(100 + seed)
     roots = rng.integers(0, 256, (6, 2), dtype=np.uint8)
-    lens = [0, 1, 8, 15, 16, 17, 20, 31, 32, 33, 40, 48, 63, 64, 65, 80, 96, 112, 127, 128]
+    lens = [0, 1, 8, 15, 16, 17, 20, 27, 28, 29, 30, 31, 32, 33, 40, 48, 63, 64, 65, 80, 96, 112, 127, 128]
     keys = []
     for i in range(3000):
         k = np.zeros((), L.LPM_V6_KEY)
