@@ -2353,9 +2353,10 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 {
 	/* CGPU_PF6_Q = "Q[:V]": packets per lane (1 = k_prefilter_v6) and the
 	 * variant.  Default "4": octet-cooperative node reads.  A/B on config 3
-	 * (Gpps): 4 8.81; 4:1 (per-lane node reads) 8.43; 2 7.34; 4:5 (fitted to
-	 * 5 waves/SIMD) 7.41; per-lane at 5-7 waves/SIMD (Q=3, daddr re-read,
-	 * 4:6, 8:3) 6.5-7.4 -- more resident waves do not help this kernel. */
+	 * with the current cover (Gpps): 4 24.8; 4:1 (per-lane node reads) 21.1;
+	 * 4:5 (fitted to 5 waves/SIMD) 20.4; 2 20.9; 1 20.5.  (Before long /16
+	 * nodes were pushed down: 4 8.81, 4:1 8.43, 2 7.34, 4:5 7.41, and 5-7
+	 * waves/SIMD variants 6.5-7.4.) */
 	const char *qs = getenv("CGPU_PF6_Q");
 	const int q = qs ? atoi(qs) : 4;
 	const char *vs = qs ? strchr(qs, ':') : nullptr;
