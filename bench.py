@@ -59,6 +59,27 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpu():
+    """The timing host: CPU model, nproc, usable CPUs (affinity) and the
+    cgroup CPU quota, for cpu_baseline.sample."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = "none"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = "none" if q == "max" else f"{int(q) / int(per):.1f} CPUs"
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return f"{model}; nproc {os.cpu_count()}, affinity {aff}, cgroup quota {quota}"
+
+
 WORKLOADS = {
     "gpu": "config2: 100k IPv4 ipcache LPM + 64k policy entries (4 ep x 16k), "
            "64M-tuple batches per GPU, bit-exact verdicts",
@@ -273,18 +294,32 @@ def main():
             tsub = {k: v[sub] for k, v in tup.items()}
         else:
             cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
-        c0 = time.perf_counter()
+        # the median of 3 timed runs (the first also yields the reference result)
+        runs = []
+        for rep in range(3):
+            c0 = time.perf_counter()
+            if ct:
+                res = o.classify_v4_ct(tsub, CT_NOW)
+            elif pf6:
+                res = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
+            elif cascade:
+                res = o.classify_v4_lb(tup, nthreads=threads)
+            elif frames:
+                res = o.classify_frames(fr, nthreads=threads)
+            else:
+                res = o.classify_v4(tup, nthreads=threads)
+            runs.append(time.perf_counter() - c0)
+            if rep == 0:
+                first = res
+            if ct or args.no_cpu_baseline:
+                break  # the sequential conntrack replay mutates its map
+        c_el = float(np.median(runs))
         if ct:
-            v0, cr0, i0, _, probes = o.classify_v4_ct(tsub, CT_NOW)
+            v0, cr0, i0, _, probes = first
         elif pf6:
-            v0, probes = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
-        elif cascade:
-            v0, i0, _, probes = o.classify_v4_lb(tup, nthreads=threads)
-        elif frames:
-            v0, i0, _, probes = o.classify_frames(fr, nthreads=threads)
+            v0, probes = first
         else:
-            v0, i0, _, probes = o.classify_v4(tup, nthreads=threads)
-        c_el = time.perf_counter() - c0
+            v0, i0, _, probes = first
         n_cpu = len(sub) if ct else n
         cpu = None
         if not args.no_cpu_baseline and ct:
@@ -293,7 +328,7 @@ def main():
                    "sample": f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
                              f"pairs from an empty map; oracle/cgpu_oracle.c or_classify_v4_ct "
                              f"(sequential conntrack + LPM trie + open hash), 1 thread, "
-                             f"{c_el:.2f}s wall"}
+                             f"{c_el:.2f}s wall (one run); host: {host_cpu()}"}
         elif not args.no_cpu_baseline:
             what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
                     "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash",
@@ -302,7 +337,8 @@ def main():
             cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
                    "kind": "port",
                    "sample": f"rank-0 batch, all {n} tuples, {args.config} tables; {what}, "
-                             f"{threads} threads, {c_el:.2f}s wall"}
+                             f"{threads} threads, median of {len(runs)} runs "
+                             f"{'/'.join(f'{x:.2f}' for x in runs)} s; host: {host_cpu()}"}
         if ct:
             parity = bool(np.array_equal(out["verdict"].cpu().numpy()[sub], v0) and
                           np.array_equal(out["ct_ret"].cpu().numpy()[sub], cr0) and

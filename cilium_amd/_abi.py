@@ -84,16 +84,21 @@ PROTOS = {
     "cgpu_ipcache_lookup": (i32, [vp, vp, vp]),
     "cgpu_ipcache_get_next_key": (i32, [vp, vp, vp]),
     "cgpu_ipcache_count": (sz, [vp]),
+    "cgpu_ipcache_update_batch": (i32, [vp, vp, vp, sz, u64]),
     "cgpu_policy_update": (i32, [vp, u32, vp, vp, u64]),
     "cgpu_policy_delete": (i32, [vp, u32, vp]),
     "cgpu_policy_lookup": (i32, [vp, u32, vp, vp]),
     "cgpu_policy_get_next_key": (i32, [vp, u32, vp, vp]),
     "cgpu_policy_flush": (i32, [vp, u32]),
     "cgpu_policy_count": (sz, [vp, u32]),
+    "cgpu_policy_update_batch": (i32, [vp, vp, vp, vp, sz, u64]),
+    "cgpu_policy_lookup_batch": (i32, [vp, vp, vp, sz, vp, vp]),
+    "cgpu_policy_dump": (i32, [vp, u32, vp, vp, sz, C.POINTER(sz)]),
     "cgpu_cidr_update": (i32, [vp, i32, vp, u64]),
     "cgpu_cidr_delete": (i32, [vp, i32, vp]),
     "cgpu_cidr_lookup": (i32, [vp, i32, vp]),
     "cgpu_cidr_get_next_key": (i32, [vp, i32, vp, vp]),
+    "cgpu_cidr_update_batch": (i32, [vp, i32, vp, sz, u64]),
     "cgpu_endpoint_update": (i32, [vp, vp, u64]),
     "cgpu_endpoint_delete": (i32, [vp, vp]),
     "cgpu_endpoint_lookup": (i32, [vp, vp]),
@@ -131,6 +136,9 @@ PROTOS = {
     "cgpu_counter_fold": (i32, [vp, vp]),
     "cgpu_metrics_read": (i32, [vp, vp]),
     "cgpu_counters_reset": (i32, [vp]),
+    "cgpu_comm_id_create": (i32, [vp]),
+    "cgpu_comm_init": (i32, [vp, vp, i32, i32]),
+    "cgpu_counters_allreduce": (i32, [vp, vp]),
 }
 
 _lib = None

@@ -52,7 +52,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         subprocess.run(cmd, check=True)
         objs.append(obj)
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+    # RCCL (cgpu_counters_allreduce) from the ROCm install the library runs on
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,
+           "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrccl"]
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     for o in objs:

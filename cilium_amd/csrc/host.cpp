@@ -11,6 +11,7 @@
  *   BPF_MAP_TYPE_HASH      kernel/bpf/hashtab.c  (policy, prefilter fix, lxc)
  */
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <array>
@@ -19,10 +20,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cgpu.h"
@@ -124,6 +128,7 @@ struct IpcEntry {
 struct PolEntry {
 	uint16_t proxy_port;
 	uint32_t slot;
+	uint64_t first_epoch; /* first snapshot whose inputs hold this key */
 };
 struct SlotInit {
 	uint32_t slot;
@@ -163,9 +168,14 @@ struct Dir248 {
 	}
 };
 
-/* ---------------- DIR-24-8 -> compressed LPM (tables.h lpm16c) ---------- */
+/* ---------------- DIR-24-8 -> compressed LPM (tables.h lpm16c) ----------
+ * Compiled from the host DIR-24-8 image one /16 at a time, so that a commit
+ * of a few ipcache changes recompiles only the /16s their prefixes cover
+ * (patch); nodes of replaced /16s become garbage until the next full build. */
 struct Lpm16cBuild {
-	std::vector<uint32_t> d16, nodes;
+	std::vector<uint32_t> d16, nodes, x16, dict;
+	std::unordered_map<uint32_t, uint32_t> code; /* leaf -> dict index */
+	size_t nodes_at_build = 0;
 	/* run list over one block: (start, leaf) with distinct neighbours */
 	typedef std::vector<std::pair<uint32_t, uint32_t>> Runs;
 	static void push(Runs &r, uint32_t start, uint32_t v)
@@ -209,12 +219,75 @@ struct Lpm16cBuild {
 			return emit_node(r);
 		return emit_array(leaf);
 	}
-	std::vector<uint32_t> x16, dict;
-	/* inline entries (x16) over the finished d16 + nodes */
-	void build_inline(const std::vector<Runs> &runs)
+	/* the runs of /16 p (stops collecting past LPMC_MAX_RUN_BOUNDS + 1) */
+	static Runs runs16(uint32_t p, const std::vector<uint32_t> &tbl24, const std::vector<uint32_t> &tbl8)
 	{
+		Runs r;
+		const uint32_t *t = &tbl24[(size_t)p * 256];
+		for (uint32_t j = 0; j < 256 && r.size() <= LPMC_MAX_RUN_BOUNDS + 1; j++) {
+			if ((t[j] & DIR_TAG_MASK) != DIR_TAG_GROUP) {
+				push(r, j << 8, t[j]);
+				continue;
+			}
+			const uint32_t *g = &tbl8[(size_t)(t[j] & DIR_PAYLOAD_MASK) * 256];
+			for (uint32_t b = 0; b < 256; b++)
+				push(r, (j << 8) | b, g[b]);
+		}
+		return r;
+	}
+	/* d16 entry of /16 p (emits its nodes) */
+	uint32_t entry16(uint32_t p, const Runs &r, const std::vector<uint32_t> &tbl24,
+			 const std::vector<uint32_t> &tbl8)
+	{
+		if (r.size() == 1)
+			return r[0].second;
+		if (r.size() - 1 <= LPMC_MAX_RUN_BOUNDS)
+			return emit_node(r);
+		const uint32_t *t = &tbl24[(size_t)p * 256];
+		uint32_t ent[256];
+		for (uint32_t j = 0; j < 256; j++)
+			ent[j] = (t[j] & DIR_TAG_MASK) != DIR_TAG_GROUP
+					 ? t[j]
+					 : byte_level(&tbl8[(size_t)(t[j] & DIR_PAYLOAD_MASK) * 256]);
+		return emit_array(ent);
+	}
+	/* x16[p]: inline when <= 4 run starts and every leaf has a dict code */
+	void inline16(uint32_t p, const Runs &r)
+	{
+		uint32_t *w = &x16[(size_t)p * 4];
+		w[0] = w[1] = w[2] = w[3] = 0;
+		bool inl = r.size() <= 5;
+		for (size_t i = 0; inl && i < r.size(); i++)
+			inl = code.count(r[i].second) != 0;
+		if (!inl) {
+			w[0] = d16[p];
+			w[3] = LPMC_OVERFLOW;
+			return;
+		}
+		const uint32_t k = (uint32_t)r.size() - 1;
+		uint64_t v = 0;
+		for (uint32_t i = 0; i < 4; i++) {
+			uint32_t b = i < k ? r[i + 1].first : 0xFFFFu;
+			w[i / 2] |= (i & 1) ? (b << 16) : b;
+		}
+		for (uint32_t i = 0; i < 5; i++)
+			v |= (uint64_t)code.at(r[std::min(i, k)].second) << (12 * i);
+		w[2] = (uint32_t)v;
+		w[3] = (uint32_t)(v >> 32);
+	}
+	/* full build: dictionary = the LPMC_DICT most frequent leaves of
+	 * inline-able /16s */
+	void build(const std::vector<uint32_t> &tbl24, const std::vector<uint32_t> &tbl8)
+	{
+		d16.assign(65536, 0u);
+		nodes.clear();
+		std::vector<Runs> all(65536);
+		for (uint32_t p = 0; p < 65536; p++) {
+			all[p] = runs16(p, tbl24, tbl8);
+			d16[p] = entry16(p, all[p], tbl24, tbl8);
+		}
 		std::map<uint32_t, uint64_t> freq;
-		for (auto &r : runs)
+		for (auto &r : all)
 			if (r.size() <= 5)
 				for (auto &x : r)
 					freq[x.second]++;
@@ -226,7 +299,7 @@ struct Lpm16cBuild {
 			return a.first != b.first ? a.first > b.first : a.second < b.second;
 		});
 		dict.clear();
-		std::map<uint32_t, uint32_t> code;
+		code.clear();
 		for (auto &f : byf) {
 			if (dict.size() >= LPMC_DICT)
 				break;
@@ -234,63 +307,28 @@ struct Lpm16cBuild {
 			dict.push_back(f.second);
 		}
 		x16.assign((size_t)65536 * 4, 0u);
-		for (uint32_t p = 0; p < 65536; p++) {
-			const Runs &r = runs[p];
-			uint32_t *w = &x16[(size_t)p * 4];
-			bool inl = r.size() <= 5;
-			for (size_t i = 0; inl && i < r.size(); i++)
-				inl = code.count(r[i].second) != 0;
-			if (!inl) {
-				w[0] = d16[p];
-				w[3] = LPMC_OVERFLOW;
-				continue;
-			}
-			const uint32_t k = (uint32_t)r.size() - 1;
-			uint64_t v = 0;
-			for (uint32_t i = 0; i < 4; i++) {
-				uint32_t b = i < k ? r[i + 1].first : 0xFFFFu;
-				w[i / 2] |= (i & 1) ? (b << 16) : b;
-			}
-			for (uint32_t i = 0; i < 5; i++)
-				v |= (uint64_t)code[r[std::min(i, k)].second] << (12 * i);
-			w[2] = (uint32_t)v;
-			w[3] = (uint32_t)(v >> 32);
-		}
+		for (uint32_t p = 0; p < 65536; p++)
+			inline16(p, all[p]);
+		nodes_at_build = nodes.size();
 	}
-	void build(const std::vector<uint32_t> &tbl24, const std::vector<uint32_t> &tbl8)
+	/* recompile /16s [lo, hi] after their DIR-24-8 entries changed; new
+	 * leaves join the dictionary while it has room */
+	void patch(uint32_t lo, uint32_t hi, const std::vector<uint32_t> &tbl24, const std::vector<uint32_t> &tbl8)
 	{
-		d16.assign(65536, 0u);
-		nodes.clear();
-		std::vector<Runs> all(65536);
-		Runs r;
-		for (uint32_t p = 0; p < 65536; p++) {
-			const uint32_t *t = &tbl24[(size_t)p * 256];
-			r.clear();
-			for (uint32_t j = 0; j < 256 && r.size() <= LPMC_MAX_RUN_BOUNDS + 1; j++) {
-				if ((t[j] & DIR_TAG_MASK) != DIR_TAG_GROUP) {
-					push(r, j << 8, t[j]);
-					continue;
-				}
-				const uint32_t *g = &tbl8[(size_t)(t[j] & DIR_PAYLOAD_MASK) * 256];
-				for (uint32_t b = 0; b < 256; b++)
-					push(r, (j << 8) | b, g[b]);
-			}
-			if (r.size() == 1) {
-				d16[p] = r[0].second;
-			} else if (r.size() - 1 <= LPMC_MAX_RUN_BOUNDS) {
-				d16[p] = emit_node(r);
-			} else {
-				uint32_t ent[256];
-				for (uint32_t j = 0; j < 256; j++)
-					ent[j] = (t[j] & DIR_TAG_MASK) != DIR_TAG_GROUP
-							 ? t[j]
-							 : byte_level(&tbl8[(size_t)(t[j] & DIR_PAYLOAD_MASK) * 256]);
-				d16[p] = emit_array(ent);
-			}
-			all[p] = r;
+		for (uint32_t p = lo; p <= hi; p++) {
+			const Runs r = runs16(p, tbl24, tbl8);
+			d16[p] = entry16(p, r, tbl24, tbl8);
+			if (r.size() <= 5)
+				for (auto &x : r)
+					if (!code.count(x.second) && dict.size() < LPMC_DICT) {
+						code[x.second] = (uint32_t)dict.size();
+						dict.push_back(x.second);
+					}
+			inline16(p, r);
 		}
-		build_inline(all);
 	}
+	/* replaced nodes outweigh live ones: time for a full build */
+	bool bloated() const { return nodes.size() > 2 * nodes_at_build + (1u << 16); }
 };
 
 struct Rank4 {
@@ -317,754 +355,6 @@ struct Arena {
 
 } // namespace
 
-struct cgpu_ctx {
-	cgpu_config cfg;
-	int device = -1;
-	std::mutex mu;
-
-	/* ---- host mirror ---- */
-	std::map<LpmKey<20>, IpcEntry> ipc;
-	std::vector<std::map<uint64_t, PolEntry>> pol;
-	size_t pol_total = 0;
-	/* counter slots: hot class [0, hot_cap) for L3-only / wildcard keys,
-	 * cold class [hot_cap, n_ctr_slots) for the rest */
-	std::vector<uint32_t> free_hot, free_cold;
-	uint32_t next_hot = 0, next_cold = 0, hot_cap = 0;
-	std::vector<SlotInit> slot_inits;
-	std::map<LpmKey<4>, cgpu_cidr_key> dyn4;
-	std::map<LpmKey<16>, cgpu_cidr_key> dyn6;
-	std::set<std::array<uint8_t, 8>> fix4;
-	std::set<std::array<uint8_t, 20>> fix6;
-	std::set<std::array<uint8_t, 20>> lxc;
-	/* cilium_lb4_services, keyed address << 32 | dport << 16 | slave so that
-	 * a frontend's entries are adjacent */
-	std::map<uint64_t, cgpu_lb4_service> lb;
-	/* per-endpoint lxc_config.h identity (cgpu_lxc_update) */
-	std::map<uint32_t, cgpu_lxc_info> lxcinfo;
-
-	/* ---- device ---- */
-	void *arena = nullptr;
-	cgpu_snapshot snap{};
-	bool committed = false;
-	uint64_t epoch = 0;
-	uint64_t checksum = 0;
-	uint32_t n_ctr_slots = 0;
-	uint64_t *d_totals = nullptr; /* [2*slots + METRICS] */
-	uint64_t *d_delta_own = nullptr;
-	uint64_t *d_delta = nullptr;  /* own or bound */
-	/* [n_ctr_slots] packed counter accumulator per stream (zero between
-	 * classify calls; one per stream keeps its exactness bound per call) */
-	std::map<void *, uint64_t *> d_pk;
-
-	/* ---- conntrack map cilium_ct4_global (tables.h ct_table layout) ----
-	 * A host shadow serves the bpf(2)-style map calls; the device copy is
-	 * authoritative once a batch ran (ct_dev_newer) and is refreshed from
-	 * the shadow before the next batch after host edits (ct_host_newer). */
-	std::vector<uint4> ct_keys, ct_vals; /* [nslots], [4 * nslots] */
-	uint32_t ct_mask = 0, ct_live = 0, ct_tombs = 0;
-	bool ct_dev_newer = false, ct_host_newer = false;
-	uint4 *d_ct_keys = nullptr, *d_ct_vals = nullptr;
-	uint32_t *d_ct_count = nullptr;
-	void *d_ct_scratch = nullptr;
-	size_t ct_scratch_cap = 0;
-};
-
-/* ======================================================================= */
-/* config / context                                                          */
-/* ======================================================================= */
-CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
-{
-	memset(c, 0, sizeof(*c));
-	c->abi_version = CGPU_ABI_VERSION;
-	c->ipcache_max = 512000;      /* pkg/maps/ipcache/ipcache.go:36 */
-	c->policy_max_per_ep = 16384; /* pkg/maps/policymap/policymap.go:37 */
-	c->policy_max_total = 1u << 20;
-	c->max_endpoints = 65536;     /* ENDPOINTS_MAP_SIZE */
-	c->cidr_dyn_max = 1u << 20;   /* > maxLKeys: device capacity, configurable */
-	c->cidr_fix_max = 20u << 20;  /* maxHKeys (pkg/policy/prefilter.go:44) */
-	c->endpoints_max = 65536;
-	c->host_id = 1;
-	c->world_id = 2;
-	c->cluster_id = 3;
-	c->health_id = 4;
-	c->ipv4_cluster_mask = 0xff0000;  /* bpf/node_config.h:42 */
-	c->ipv4_cluster_range = 0x100000; /* bpf/node_config.h:43 */
-	c->ct_proto_gate = 1;             /* CONNTRACK (bpf/lxc_config.h:46) */
-	c->ingress_secctx_world = 0;
-	c->prefilter_fix4 = c->prefilter_dyn4 = 1; /* bpf/filter_config.h */
-	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
-	c->ingress_src_identity = 0;
-	c->hot_counter_slots = 8192;
-	c->lb_max_entries = 65536;        /* CILIUM_LB_MAP_MAX_ENTRIES, bpf/node_config.h:60 */
-	c->ipv4_loopback = 0x1ffff50a;    /* IPV4_LOOPBACK, bpf/node_config.h:45 */
-	c->lb_flags = CGPU_LB_L3 | CGPU_LB_L4; /* bpf/lxc_config.h:44-45 */
-	static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1,
-					   0x0, 0x1, 0x0, 0x0}; /* ROUTER_IP, bpf/node_config.h:30 */
-	memcpy(c->ipv6_router_ip, router, 16);
-	static const uint8_t node_mac[6] = {0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde}; /* NODE_MAC, node_config.h:51 */
-	memcpy(c->node_mac, node_mac, 6);
-	c->ct_max = 1000000; /* CT_MAP_SIZE = MapNumEntriesGlobal, pkg/maps/ctmap/ctmap.go:101 */
-}
-
-CGPU_EXPORT const char *cgpu_last_error(void) { return g_last_error.c_str(); }
-CGPU_EXPORT const char *cgpu_version(void) { return "cgpu 0.1 gfx950 abi1"; }
-
-CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **out)
-{
-	if (!cfg || !out)
-		return fail(-EINVAL, "null argument");
-	if (cfg->abi_version != CGPU_ABI_VERSION)
-		return fail(-EINVAL, "abi_version %u != %u", cfg->abi_version, CGPU_ABI_VERSION);
-	if (!cfg->max_endpoints || !cfg->policy_max_total)
-		return fail(-EINVAL, "zero capacity");
-	if (cfg->policy_max_total >= POL_CTR_EMPTY)
-		return fail(-EINVAL, "policy_max_total %u >= 2^24 - 1", cfg->policy_max_total);
-	if (!cfg->ct_max || cfg->ct_max > (1u << 28))
-		return fail(-EINVAL, "ct_max %u out of range (1 .. 2^28)", cfg->ct_max);
-	cgpu_ctx *c = new cgpu_ctx();
-	c->cfg = *cfg;
-	c->pol.resize(cfg->max_endpoints);
-	c->n_ctr_slots = cfg->policy_max_total;
-	c->hot_cap = std::min(cfg->hot_counter_slots, cfg->policy_max_total / 2);
-	c->next_cold = c->hot_cap;
-	if (device >= 0) {
-		int ndev = 0;
-		if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
-			delete c;
-			return fail(-ENODEV, "HIP device %d not present", device);
-		}
-		c->device = device;
-		size_t words = (size_t)2 * c->n_ctr_slots + CGPU_METRICS_WORDS;
-		if (hipSetDevice(device) != hipSuccess ||
-		    hipMalloc((void **)&c->d_totals, words * 8) != hipSuccess ||
-		    hipMalloc((void **)&c->d_delta_own, words * 8) != hipSuccess ||
-		    hipMemset(c->d_totals, 0, words * 8) != hipSuccess ||
-		    hipMemset(c->d_delta_own, 0, words * 8) != hipSuccess) {
-			(void)hipFree(c->d_totals);
-			(void)hipFree(c->d_delta_own);
-			delete c;
-			return fail(-EIO, "device counter allocation failed");
-		}
-		c->d_delta = c->d_delta_own;
-	}
-	*out = c;
-	return 0;
-}
-
-CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
-{
-	if (!c)
-		return;
-	if (c->device >= 0) {
-		(void)hipSetDevice(c->device);
-		(void)hipDeviceSynchronize();
-		(void)hipFree(c->arena);
-		(void)hipFree(c->d_totals);
-		(void)hipFree(c->d_delta_own);
-		for (auto &kv : c->d_pk)
-			(void)hipFree(kv.second);
-		(void)hipFree(c->d_ct_keys);
-		(void)hipFree(c->d_ct_vals);
-		(void)hipFree(c->d_ct_count);
-		(void)hipFree(c->d_ct_scratch);
-	}
-	delete c;
-}
-
-static int check_flags(uint64_t flags)
-{
-	return flags > CGPU_EXIST ? fail(-EINVAL, "bad update flags %llu", (unsigned long long)flags) : 0;
-}
-
-/* ======================================================================= */
-/* ipcache                                                                   */
-/* ======================================================================= */
-CGPU_EXPORT int cgpu_ipcache_update(cgpu_ctx *c, const cgpu_ipcache_key *key,
-				    const cgpu_remote_endpoint_info *val, uint64_t flags)
-{
-	if (!c || !key || !val)
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	if (key->prefixlen > 160) /* data is 20 bytes: lpm_trie max_prefixlen */
-		return fail(-EINVAL, "ipcache prefixlen %u > 160", key->prefixlen);
-	std::lock_guard<std::mutex> g(c->mu);
-	auto k = lpm_canon<20>(key->prefixlen, (const uint8_t *)key + 4);
-	auto it = c->ipc.find(k);
-	if (it == c->ipc.end()) {
-		if (flags == CGPU_EXIST)
-			return fail(-ENOENT, "ipcache key not present");
-		if (c->ipc.size() >= c->cfg.ipcache_max)
-			return fail(-ENOSPC, "ipcache full (%u)", c->cfg.ipcache_max);
-		c->ipc.emplace(k, IpcEntry{*key, *val});
-	} else {
-		if (flags == CGPU_NOEXIST)
-			return fail(-EEXIST, "ipcache key exists");
-		it->second = IpcEntry{*key, *val};
-	}
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_ipcache_delete(cgpu_ctx *c, const cgpu_ipcache_key *key)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	if (key->prefixlen > 160)
-		return fail(-EINVAL, "ipcache prefixlen %u > 160", key->prefixlen);
-	std::lock_guard<std::mutex> g(c->mu);
-	auto n = c->ipc.erase(lpm_canon<20>(key->prefixlen, (const uint8_t *)key + 4));
-	return n ? 0 : fail(-ENOENT, "ipcache key not present");
-}
-
-/* bpf(2) lookup on an LPM trie = longest prefix match of the given key */
-CGPU_EXPORT int cgpu_ipcache_lookup(cgpu_ctx *c, const cgpu_ipcache_key *key,
-				    cgpu_remote_endpoint_info *out)
-{
-	if (!c || !key || !out)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	const uint8_t *q = (const uint8_t *)key + 4;
-	uint32_t qlen = std::min<uint32_t>(key->prefixlen, 160);
-	/* probe each shorter-or-equal prefix length, longest first */
-	for (int64_t p = qlen; p >= 0; p--) {
-		auto it = c->ipc.find(lpm_canon<20>((uint32_t)p, q));
-		if (it != c->ipc.end()) {
-			*out = it->second.val;
-			return 0;
-		}
-	}
-	return -ENOENT;
-}
-
-CGPU_EXPORT int cgpu_ipcache_get_next_key(cgpu_ctx *c, const cgpu_ipcache_key *key,
-					  cgpu_ipcache_key *next)
-{
-	if (!c || !next)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	auto it = c->ipc.begin();
-	if (key) {
-		auto k = lpm_canon<20>(std::min<uint32_t>(key->prefixlen, 160), (const uint8_t *)key + 4);
-		it = c->ipc.upper_bound(k);
-	}
-	if (it == c->ipc.end())
-		return -ENOENT;
-	*next = it->second.raw;
-	return 0;
-}
-
-CGPU_EXPORT size_t cgpu_ipcache_count(cgpu_ctx *c)
-{
-	std::lock_guard<std::mutex> g(c->mu);
-	return c->ipc.size();
-}
-
-/* ======================================================================= */
-/* policy                                                                    */
-/* ======================================================================= */
-static inline uint64_t pol_key64(const cgpu_policy_key *k)
-{
-	uint64_t x;
-	memcpy(&x, k, 8);
-	return x;
-}
-
-CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
-				   const cgpu_policy_entry *e, uint64_t flags)
-{
-	if (!c || !key || !e)
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	if (ep >= c->cfg.max_endpoints)
-		return fail(-EINVAL, "endpoint %u >= max_endpoints %u", ep, c->cfg.max_endpoints);
-	std::lock_guard<std::mutex> g(c->mu);
-	auto &m = c->pol[ep];
-	uint64_t k = pol_key64(key);
-	auto it = m.find(k);
-	uint32_t slot;
-	if (it == m.end()) {
-		if (flags == CGPU_EXIST)
-			return fail(-ENOENT, "policy key not present");
-		if (m.size() >= c->cfg.policy_max_per_ep)
-			return fail(-E2BIG, "policy map of ep %u full (%u)", ep, c->cfg.policy_max_per_ep);
-		/* L3-only {id, 0, 0, dir} and wildcard {0, port, proto, dir} keys
-		 * absorb most hits: give them hot (LDS-accumulated) slots */
-		bool hot = (key->dport == 0 && key->protocol == 0) || key->sec_label == 0;
-		if (hot && !c->free_hot.empty()) {
-			slot = c->free_hot.back();
-			c->free_hot.pop_back();
-		} else if (hot && c->next_hot < c->hot_cap) {
-			slot = c->next_hot++;
-		} else if (!c->free_cold.empty()) {
-			slot = c->free_cold.back();
-			c->free_cold.pop_back();
-		} else if (c->next_cold < c->n_ctr_slots) {
-			slot = c->next_cold++;
-		} else {
-			return fail(-E2BIG, "policy device slots exhausted (%u)", c->n_ctr_slots);
-		}
-		m.emplace(k, PolEntry{e->proxy_port, slot});
-		c->pol_total++;
-	} else {
-		if (flags == CGPU_NOEXIST)
-			return fail(-EEXIST, "policy key exists");
-		it->second.proxy_port = e->proxy_port;
-		slot = it->second.slot;
-	}
-	/* kernel htab replaces the whole value: counters restart from it */
-	c->slot_inits.push_back(SlotInit{slot, e->packets, e->bytes});
-	return 0;
-}
-
-static void pol_erase(cgpu_ctx *c, std::map<uint64_t, PolEntry> &m,
-		      std::map<uint64_t, PolEntry>::iterator it)
-{
-	if (it->second.slot < c->hot_cap)
-		c->free_hot.push_back(it->second.slot);
-	else
-		c->free_cold.push_back(it->second.slot);
-	m.erase(it);
-	c->pol_total--;
-}
-
-CGPU_EXPORT int cgpu_policy_delete(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	if (ep >= c->cfg.max_endpoints)
-		return fail(-EINVAL, "endpoint %u out of range", ep);
-	std::lock_guard<std::mutex> g(c->mu);
-	auto &m = c->pol[ep];
-	auto it = m.find(pol_key64(key));
-	if (it == m.end())
-		return fail(-ENOENT, "policy key not present");
-	pol_erase(c, m, it);
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_policy_flush(cgpu_ctx *c, uint32_t ep)
-{
-	if (!c || ep >= c->cfg.max_endpoints)
-		return fail(-EINVAL, "bad argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	auto &m = c->pol[ep];
-	while (!m.empty())
-		pol_erase(c, m, m.begin());
-	return 0;
-}
-
-static int read_counter_words(cgpu_ctx *c, size_t word, size_t nwords, uint64_t *out)
-{
-	/* totals + delta; pending launches complete first */
-	std::vector<uint64_t> a(nwords), b(nwords);
-	HIP_OR_EIO(hipSetDevice(c->device));
-	HIP_OR_EIO(hipDeviceSynchronize());
-	HIP_OR_EIO(hipMemcpy(a.data(), c->d_totals + word, nwords * 8, hipMemcpyDeviceToHost));
-	HIP_OR_EIO(hipMemcpy(b.data(), c->d_delta + word, nwords * 8, hipMemcpyDeviceToHost));
-	for (size_t i = 0; i < nwords; i++)
-		out[i] = a[i] + b[i];
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_policy_lookup(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
-				   cgpu_policy_entry *out)
-{
-	if (!c || !key || !out)
-		return fail(-EINVAL, "null argument");
-	if (ep >= c->cfg.max_endpoints)
-		return fail(-EINVAL, "endpoint %u out of range", ep);
-	std::lock_guard<std::mutex> g(c->mu);
-	auto &m = c->pol[ep];
-	auto it = m.find(pol_key64(key));
-	if (it == m.end())
-		return -ENOENT;
-	memset(out, 0, sizeof(*out));
-	out->proxy_port = it->second.proxy_port;
-	/* the most recent update's counter values until the next commit */
-	uint64_t pk = 0, by = 0;
-	bool pending = false;
-	for (auto s = c->slot_inits.rbegin(); s != c->slot_inits.rend(); ++s)
-		if (s->slot == it->second.slot) {
-			pk = s->packets;
-			by = s->bytes;
-			pending = true;
-			break;
-		}
-	if (!pending && c->device >= 0 && c->committed) {
-		uint64_t w[2];
-		if (int r = read_counter_words(c, (size_t)2 * it->second.slot, 2, w))
-			return r;
-		pk = w[0];
-		by = w[1];
-	}
-	out->packets = pk;
-	out->bytes = by;
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_policy_get_next_key(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
-					 cgpu_policy_key *next)
-{
-	if (!c || !next || ep >= c->cfg.max_endpoints)
-		return fail(-EINVAL, "bad argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	auto &m = c->pol[ep];
-	auto it = key ? m.upper_bound(pol_key64(key)) : m.begin();
-	if (it == m.end())
-		return -ENOENT;
-	memcpy(next, &it->first, 8);
-	return 0;
-}
-
-CGPU_EXPORT size_t cgpu_policy_count(cgpu_ctx *c, uint32_t ep)
-{
-	if (!c || ep >= c->cfg.max_endpoints)
-		return 0;
-	std::lock_guard<std::mutex> g(c->mu);
-	return c->pol[ep].size();
-}
-
-/* ======================================================================= */
-/* prefilter CIDR maps + endpoint map                                        */
-/* ======================================================================= */
-CGPU_EXPORT int cgpu_cidr_update(cgpu_ctx *c, int which, const cgpu_cidr_key *key, uint64_t flags)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	std::lock_guard<std::mutex> g(c->mu);
-	bool exists;
-	switch (which) {
-	case CGPU_CIDR_V4_DYN:
-	case CGPU_CIDR_V6_DYN: {
-		uint32_t maxp = which == CGPU_CIDR_V4_DYN ? 32 : 128;
-		if (key->prefixlen > maxp)
-			return fail(-EINVAL, "prefixlen %u > %u", key->prefixlen, maxp);
-		if (which == CGPU_CIDR_V4_DYN) {
-			auto k = lpm_canon<4>(key->prefixlen, key->addr);
-			exists = c->dyn4.count(k);
-			if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
-			if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
-			if (!exists && c->dyn4.size() >= c->cfg.cidr_dyn_max) return fail(-ENOSPC, "dyn4 full");
-			c->dyn4[k] = *key;
-		} else {
-			auto k = lpm_canon<16>(key->prefixlen, key->addr);
-			exists = c->dyn6.count(k);
-			if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
-			if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
-			if (!exists && c->dyn6.size() >= c->cfg.cidr_dyn_max) return fail(-ENOSPC, "dyn6 full");
-			c->dyn6[k] = *key;
-		}
-		return 0;
-	}
-	case CGPU_CIDR_V4_FIX: {
-		std::array<uint8_t, 8> k;
-		memcpy(k.data(), key, 8);
-		exists = c->fix4.count(k);
-		if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
-		if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
-		if (!exists && c->fix4.size() >= c->cfg.cidr_fix_max) return fail(-E2BIG, "fix4 full");
-		c->fix4.insert(k);
-		return 0;
-	}
-	case CGPU_CIDR_V6_FIX: {
-		std::array<uint8_t, 20> k;
-		memcpy(k.data(), key, 20);
-		exists = c->fix6.count(k);
-		if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
-		if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
-		if (!exists && c->fix6.size() >= c->cfg.cidr_fix_max) return fail(-E2BIG, "fix6 full");
-		c->fix6.insert(k);
-		return 0;
-	}
-	}
-	return fail(-EINVAL, "bad cidr map %d", which);
-}
-
-CGPU_EXPORT int cgpu_cidr_delete(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	size_t n = 0;
-	switch (which) {
-	case CGPU_CIDR_V4_DYN:
-		if (key->prefixlen > 32) return fail(-EINVAL, "prefixlen");
-		n = c->dyn4.erase(lpm_canon<4>(key->prefixlen, key->addr));
-		break;
-	case CGPU_CIDR_V6_DYN:
-		if (key->prefixlen > 128) return fail(-EINVAL, "prefixlen");
-		n = c->dyn6.erase(lpm_canon<16>(key->prefixlen, key->addr));
-		break;
-	case CGPU_CIDR_V4_FIX: {
-		std::array<uint8_t, 8> k;
-		memcpy(k.data(), key, 8);
-		n = c->fix4.erase(k);
-		break;
-	}
-	case CGPU_CIDR_V6_FIX: {
-		std::array<uint8_t, 20> k;
-		memcpy(k.data(), key, 20);
-		n = c->fix6.erase(k);
-		break;
-	}
-	default:
-		return fail(-EINVAL, "bad cidr map %d", which);
-	}
-	return n ? 0 : -ENOENT;
-}
-
-CGPU_EXPORT int cgpu_cidr_lookup(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	switch (which) {
-	case CGPU_CIDR_V4_DYN:
-		for (int64_t p = std::min<uint32_t>(key->prefixlen, 32); p >= 0; p--)
-			if (c->dyn4.count(lpm_canon<4>((uint32_t)p, key->addr)))
-				return 0;
-		return -ENOENT;
-	case CGPU_CIDR_V6_DYN:
-		for (int64_t p = std::min<uint32_t>(key->prefixlen, 128); p >= 0; p--)
-			if (c->dyn6.count(lpm_canon<16>((uint32_t)p, key->addr)))
-				return 0;
-		return -ENOENT;
-	case CGPU_CIDR_V4_FIX: {
-		std::array<uint8_t, 8> k;
-		memcpy(k.data(), key, 8);
-		return c->fix4.count(k) ? 0 : -ENOENT;
-	}
-	case CGPU_CIDR_V6_FIX: {
-		std::array<uint8_t, 20> k;
-		memcpy(k.data(), key, 20);
-		return c->fix6.count(k) ? 0 : -ENOENT;
-	}
-	}
-	return fail(-EINVAL, "bad cidr map %d", which);
-}
-
-CGPU_EXPORT int cgpu_cidr_get_next_key(cgpu_ctx *c, int which, const cgpu_cidr_key *key,
-				       cgpu_cidr_key *next)
-{
-	if (!c || !next)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	memset(next, 0, sizeof(*next));
-	switch (which) {
-	case CGPU_CIDR_V4_DYN: {
-		auto it = key ? c->dyn4.upper_bound(lpm_canon<4>(std::min<uint32_t>(key->prefixlen, 32), key->addr))
-			      : c->dyn4.begin();
-		if (it == c->dyn4.end()) return -ENOENT;
-		*next = it->second;
-		return 0;
-	}
-	case CGPU_CIDR_V6_DYN: {
-		auto it = key ? c->dyn6.upper_bound(lpm_canon<16>(std::min<uint32_t>(key->prefixlen, 128), key->addr))
-			      : c->dyn6.begin();
-		if (it == c->dyn6.end()) return -ENOENT;
-		*next = it->second;
-		return 0;
-	}
-	case CGPU_CIDR_V4_FIX: {
-		std::array<uint8_t, 8> k{};
-		if (key) memcpy(k.data(), key, 8);
-		auto it = key ? c->fix4.upper_bound(k) : c->fix4.begin();
-		if (it == c->fix4.end()) return -ENOENT;
-		memcpy(next, it->data(), 8);
-		return 0;
-	}
-	case CGPU_CIDR_V6_FIX: {
-		std::array<uint8_t, 20> k{};
-		if (key) memcpy(k.data(), key, 20);
-		auto it = key ? c->fix6.upper_bound(k) : c->fix6.begin();
-		if (it == c->fix6.end()) return -ENOENT;
-		memcpy(next, it->data(), 20);
-		return 0;
-	}
-	}
-	return fail(-EINVAL, "bad cidr map %d", which);
-}
-
-CGPU_EXPORT int cgpu_endpoint_update(cgpu_ctx *c, const cgpu_endpoint_key *key, uint64_t flags)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	std::array<uint8_t, 20> k;
-	memcpy(k.data(), key, 20);
-	std::lock_guard<std::mutex> g(c->mu);
-	bool exists = c->lxc.count(k);
-	if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
-	if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
-	if (!exists && c->lxc.size() >= c->cfg.endpoints_max) return fail(-E2BIG, "endpoint map full");
-	c->lxc.insert(k);
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_endpoint_delete(cgpu_ctx *c, const cgpu_endpoint_key *key)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	std::array<uint8_t, 20> k;
-	memcpy(k.data(), key, 20);
-	std::lock_guard<std::mutex> g(c->mu);
-	return c->lxc.erase(k) ? 0 : -ENOENT;
-}
-
-CGPU_EXPORT int cgpu_endpoint_lookup(cgpu_ctx *c, const cgpu_endpoint_key *key)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	std::array<uint8_t, 20> k;
-	memcpy(k.data(), key, 20);
-	std::lock_guard<std::mutex> g(c->mu);
-	return c->lxc.count(k) ? 0 : -ENOENT;
-}
-
-/* per-endpoint identity of the endpoint program (lib/lxc.h:31-89) */
-CGPU_EXPORT int cgpu_lxc_update(cgpu_ctx *c, uint32_t ep, const cgpu_lxc_info *info)
-{
-	if (!c || !info)
-		return fail(-EINVAL, "null argument");
-	if (ep >= 65536u)
-		return fail(-EINVAL, "endpoint id beyond the u16 ep column");
-	if (info->verify & ~(CGPU_VERIFY_SMAC | CGPU_VERIFY_DMAC | CGPU_VERIFY_SIP))
-		return fail(-EINVAL, "unknown verify bits");
-	std::lock_guard<std::mutex> g(c->mu);
-	c->lxcinfo[ep] = *info;
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_lxc_delete(cgpu_ctx *c, uint32_t ep)
-{
-	if (!c)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	return c->lxcinfo.erase(ep) ? 0 : -ENOENT;
-}
-
-CGPU_EXPORT int cgpu_lxc_lookup(cgpu_ctx *c, uint32_t ep, cgpu_lxc_info *out)
-{
-	if (!c || !out)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	auto it = c->lxcinfo.find(ep);
-	if (it == c->lxcinfo.end())
-		return -ENOENT;
-	*out = it->second;
-	return 0;
-}
-
-/* ======================================================================= */
-/* service map (pkg/maps/lbmap; bpf(2) htab semantics, whole-key compare)    */
-/* ======================================================================= */
-static inline uint64_t lb_mkey(const cgpu_lb4_key *k)
-{
-	return (uint64_t)k->address << 32 | (uint64_t)k->dport << 16 | k->slave;
-}
-
-static inline cgpu_lb4_key lb_unkey(uint64_t m)
-{
-	cgpu_lb4_key k;
-	k.address = (uint32_t)(m >> 32);
-	k.dport = (uint16_t)(m >> 16);
-	k.slave = (uint16_t)m;
-	return k;
-}
-
-static int lb_put(cgpu_ctx *c, const cgpu_lb4_key *key, const cgpu_lb4_service *val, uint64_t flags)
-{
-	const uint64_t m = lb_mkey(key);
-	auto it = c->lb.find(m);
-	if (it == c->lb.end()) {
-		if (flags == CGPU_EXIST)
-			return fail(-ENOENT, "lb4 key not present");
-		if (c->lb.size() >= c->cfg.lb_max_entries)
-			return fail(-E2BIG, "lb4 service map full (%u)", c->cfg.lb_max_entries);
-		c->lb.emplace(m, *val);
-	} else {
-		if (flags == CGPU_NOEXIST)
-			return fail(-EEXIST, "lb4 key exists");
-		it->second = *val;
-	}
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_lb4_update(cgpu_ctx *c, const cgpu_lb4_key *key, const cgpu_lb4_service *val,
-				uint64_t flags)
-{
-	if (!c || !key || !val)
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	std::lock_guard<std::mutex> g(c->mu);
-	return lb_put(c, key, val, flags);
-}
-
-CGPU_EXPORT int cgpu_lb4_update_batch(cgpu_ctx *c, const cgpu_lb4_key *keys,
-				      const cgpu_lb4_service *vals, size_t n, uint64_t flags)
-{
-	if (!c || (n && (!keys || !vals)))
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	std::lock_guard<std::mutex> g(c->mu);
-	for (size_t i = 0; i < n; i++)
-		if (int r = lb_put(c, &keys[i], &vals[i], flags))
-			return r;
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_lb4_delete(cgpu_ctx *c, const cgpu_lb4_key *key)
-{
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	return c->lb.erase(lb_mkey(key)) ? 0 : -ENOENT;
-}
-
-CGPU_EXPORT int cgpu_lb4_lookup(cgpu_ctx *c, const cgpu_lb4_key *key, cgpu_lb4_service *out)
-{
-	if (!c || !key || !out)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	auto it = c->lb.find(lb_mkey(key));
-	if (it == c->lb.end())
-		return -ENOENT;
-	*out = it->second;
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_lb4_get_next_key(cgpu_ctx *c, const cgpu_lb4_key *key, cgpu_lb4_key *next)
-{
-	if (!c || !next)
-		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	auto it = key ? c->lb.upper_bound(lb_mkey(key)) : c->lb.begin();
-	if (it == c->lb.end())
-		return -ENOENT;
-	*next = lb_unkey(it->first);
-	return 0;
-}
-
-CGPU_EXPORT size_t cgpu_lb4_count(cgpu_ctx *c)
-{
-	if (!c)
-		return 0;
-	std::lock_guard<std::mutex> g(c->mu);
-	return c->lb.size();
-}
-
-CGPU_EXPORT uint32_t cgpu_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
-				    uint8_t proto)
-{
-	return flow_hash(saddr, daddr, sport, dport, proto);
-}
-
 /* ======================================================================= */
 /* compiler: mirror -> device layouts                                        */
 /* ======================================================================= */
@@ -1083,156 +373,157 @@ uint64_t fnv(uint64_t h, const void *p, size_t n)
  * An entry is a candidate iff its prefixlen <= 64 and its first prefixlen
  * bits equal the lookup key's.  Entries with prefixlen < 32 end inside the
  * static {pad, family} part: they match every IPv4 address and rank below
- * any entry that reaches the address bits. */
-void build_ipc4(const cgpu_ctx *c, Dir248 &d)
+ * any entry that reaches the address bits.  Returns false for a key that
+ * IPv4 lookups never match. */
+static const uint8_t kStaticV4[4] = {0, 0, 0, 1};
+bool ipc4_candidate(const cgpu_ipcache_key &raw, uint32_t label, Rank4 *r)
 {
-	static const uint8_t static_v4[4] = {0, 0, 0, 1};
-	std::vector<Rank4> cand;
-	for (auto &kv : c->ipc) {
-		const IpcEntry &e = kv.second;
-		uint32_t p = e.raw.prefixlen;
-		const uint8_t *data = (const uint8_t *)&e.raw + 4;
-		if (p > 64)
-			continue;
-		if (!prefix_eq(data, static_v4, std::min<uint32_t>(p, 32)))
-			continue;
-		Rank4 r;
-		r.label = e.val.sec_label;
-		if (p < 32) {
-			r.rank = p;
-			r.addr = 0;
-			r.len = 0;
-		} else {
-			r.rank = p;
-			r.len = p - 32;
-			uint32_t a;
-			memcpy(&a, data + 4, 4);
-			r.addr = bswap32(a);
-		}
-		cand.push_back(r);
+	const uint32_t p = raw.prefixlen;
+	const uint8_t *data = (const uint8_t *)&raw + 4;
+	if (p > 64 || !prefix_eq(data, kStaticV4, std::min<uint32_t>(p, 32)))
+		return false;
+	r->label = label;
+	r->rank = p;
+	if (p < 32) {
+		r->addr = 0;
+		r->len = 0;
+	} else {
+		r->len = p - 32;
+		uint32_t a;
+		memcpy(&a, data + 4, 4);
+		r->addr = bswap32(a) & (r->len ? ~0u << (32 - r->len) : 0u);
 	}
+	return true;
+}
+
+void build_dir(std::vector<Rank4> cand, Dir248 &d, bool any_match)
+{
 	std::stable_sort(cand.begin(), cand.end(),
 			 [](const Rank4 &a, const Rank4 &b) { return a.rank < b.rank; });
 	d.init();
 	for (auto &r : cand)
+		d.apply(r.addr, r.len, any_match ? (DIR_TAG_DIRECT | 1u) : d.encode(r.label));
+}
+
+/* One ipcache change recompiled over the address range of its prefix: the
+ * range is refilled with the best entry covering all of it (shorter
+ * prefixes or static-part entries), then every entry inside the range is
+ * re-applied in rank order -- for each address the highest-ranked covering
+ * entry wins, exactly as in the full build. */
+struct Ipc4Patch {
+	uint32_t addr, len;     /* host order, IP prefix length */
+	bool has_cover;
+	uint32_t cover_label;
+	std::vector<Rank4> subs;
+};
+
+void apply_ipc4_patch(const Ipc4Patch &pt, Dir248 &d, Lpm16cBuild &lc)
+{
+	d.apply(pt.addr, pt.len, pt.has_cover ? d.encode(pt.cover_label) : 0u);
+	std::vector<Rank4> subs = pt.subs;
+	std::stable_sort(subs.begin(), subs.end(), [](const Rank4 &a, const Rank4 &b) { return a.rank < b.rank; });
+	for (auto &r : subs)
 		d.apply(r.addr, r.len, d.encode(r.label));
+	const uint32_t last = pt.len ? pt.addr + ((pt.len == 32 ? 1u : (1u << (32 - pt.len))) - 1u) : 0xFFFFFFFFu;
+	lc.patch(pt.addr >> 16, last >> 16, d.tbl24, d.tbl8);
 }
 
 /* prefilter v4 any-match: dyn4 (if CIDR4_LPM_PREFILTER) + fix4 keys with
  * prefixlen 32 (a hash key with another prefixlen never equals the lookup
  * key {32, saddr}); both lead to XDP_DROP (bpf_xdp.c:107-117). */
-bool build_pf4(const cgpu_ctx *c, Dir248 &d)
+struct PfIn {
+	bool fix4, dyn4, fix6, dyn6;
+	std::vector<cgpu_cidr_key> dyn4k, fix4k, dyn6k, fix6k;
+};
+
+std::vector<Rank4> pf4_candidates(const PfIn &in)
 {
 	std::vector<Rank4> cand;
-	if (!c->cfg.prefilter_fix4)
-		return false;
-	if (c->cfg.prefilter_dyn4)
-		for (auto &kv : c->dyn4) {
+	if (!in.fix4)
+		return cand;
+	if (in.dyn4)
+		for (auto &k : in.dyn4k) {
 			uint32_t a;
-			memcpy(&a, kv.first.data.data(), 4);
-			cand.push_back(Rank4{kv.first.plen, bswap32(a), kv.first.plen, 1});
+			memcpy(&a, k.addr, 4);
+			const uint32_t h = bswap32(a);
+			cand.push_back(Rank4{k.prefixlen, k.prefixlen ? h & (~0u << (32 - k.prefixlen)) : 0u,
+					     k.prefixlen, 1});
 		}
-	for (auto &k : c->fix4) {
-		uint32_t plen, a;
-		memcpy(&plen, k.data(), 4);
-		if (plen != 32)
+	for (auto &k : in.fix4k) {
+		if (k.prefixlen != 32)
 			continue;
-		memcpy(&a, k.data() + 4, 4);
+		uint32_t a;
+		memcpy(&a, k.addr, 4);
 		cand.push_back(Rank4{32, bswap32(a), 32, 1});
 	}
-	if (cand.empty())
-		return false;
-	std::stable_sort(cand.begin(), cand.end(),
-			 [](const Rank4 &a, const Rank4 &b) { return a.rank < b.rank; });
-	d.init();
-	for (auto &r : cand)
-		d.apply(r.addr, r.len, DIR_TAG_DIRECT | 1u);
-	return true;
+	return cand;
 }
+
+/* ---- policy table (tables.h pol_table): neighbourhood hashing ---- */
+struct PolKey {
+	uint32_t lo, hi, z, slot; /* key words, ep | proxy << 16, counter slot */
+};
 
 struct PolBuild {
 	std::vector<pol_slot> slots;
-	uint32_t mask = 0, max_probe = 1, bpb = 4;
+	uint32_t mask = 0;
+	size_t count = 0;
+	/* place one key; false when its neighbourhood is full */
+	bool insert(const PolKey &k)
+	{
+		const uint32_t home = pol_hash(k.lo, k.hi, k.z & 0xFFFFu) & mask;
+		uint32_t d = 0;
+		while (d < POL_HOP && (slots[(home + d) & mask].ctr & POL_CTR_MASK) != POL_CTR_EMPTY)
+			d++;
+		if (d == POL_HOP)
+			return false;
+		pol_slot &sl = slots[(home + d) & mask];
+		sl.key_lo = k.lo;
+		sl.key_hi = k.hi;
+		sl.ep_proxy = k.z;
+		sl.ctr = (sl.ctr & ~POL_CTR_MASK) | k.slot;
+		slots[home].ctr |= 1u << (POL_HOP_SHIFT + d);
+		count++;
+		return true;
+	}
+	/* remove {lo, hi, ep} if present (the slot keeps its own hop bits) */
+	bool erase(uint32_t lo, uint32_t hi, uint32_t ep)
+	{
+		const uint32_t home = pol_hash(lo, hi, ep) & mask;
+		const uint32_t hop = slots[home].ctr >> POL_HOP_SHIFT;
+		for (uint32_t d = 0; d < POL_HOP; d++) {
+			if (!((hop >> d) & 1u))
+				continue;
+			pol_slot &sl = slots[(home + d) & mask];
+			if (sl.key_lo == lo && sl.key_hi == hi && (sl.ep_proxy & 0xFFFFu) == ep) {
+				sl.key_lo = sl.key_hi = sl.ep_proxy = 0;
+				sl.ctr = (sl.ctr & ~POL_CTR_MASK) | POL_CTR_EMPTY;
+				slots[home].ctr &= ~(1u << (POL_HOP_SHIFT + d));
+				count--;
+				return true;
+			}
+		}
+		return false;
+	}
+	/* <= 50 % load: a lookup almost always finds its key in the home slot */
+	void build(const std::vector<PolKey> &keys)
+	{
+		uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * keys.size() + 2));
+		for (;;) {
+			slots.assign(nb, pol_slot{0, 0, 0, POL_CTR_EMPTY});
+			mask = nb - 1;
+			count = 0;
+			bool ok = true;
+			for (auto &k : keys)
+				if (!(ok = insert(k)))
+					break; /* a neighbourhood is full: grow */
+			if (ok)
+				return;
+			nb *= 2;
+		}
+	}
+	bool overloaded() const { return 2 * count + 2 > slots.size(); }
 };
-
-static uint32_t env_u32(const char *name, uint32_t dflt)
-{
-	const char *v = getenv(name);
-	return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
-}
-
-/* Policy hash layout.  Default: 16-byte single-slot neighbourhood hashing
- * (tables.h POL_HOP) at <= 50% load: a lookup is one random 16-byte gather
- * unless the home slot's hop bits name other slots.  CGPU_POL_BPB=4 selects
- * 64-byte 4-slot buckets with linear bucket probing at <= 50% load. */
-static void place_pol_hop(PolBuild &b, const std::vector<std::array<uint32_t, 4>> &keys, uint32_t nb)
-{
-	for (;;) {
-		b.slots.assign(nb, pol_slot{0, 0, 0, POL_CTR_EMPTY});
-		b.mask = nb - 1;
-		bool ok = true;
-		for (auto &k : keys) {
-			const uint32_t home = pol_hash(k[0], k[1], k[2] & 0xFFFFu) & b.mask;
-			uint32_t d = 0;
-			while (d < POL_HOP && (b.slots[(home + d) & b.mask].ctr & POL_CTR_MASK) != POL_CTR_EMPTY)
-				d++;
-			if (d == POL_HOP) {
-				ok = false; /* neighbourhood full: grow */
-				break;
-			}
-			pol_slot &sl = b.slots[(home + d) & b.mask];
-			sl.key_lo = k[0];
-			sl.key_hi = k[1];
-			sl.ep_proxy = k[2];
-			sl.ctr = (sl.ctr & ~POL_CTR_MASK) | k[3];
-			b.slots[home].ctr |= 1u << (POL_HOP_SHIFT + d);
-		}
-		if (ok)
-			return;
-		nb *= 2;
-	}
-}
-
-void build_pol(const cgpu_ctx *c, PolBuild &b)
-{
-	b.bpb = env_u32("CGPU_POL_BPB", 1) == 4 ? 4 : 1;
-	const uint32_t load_pct = std::max<uint32_t>(5, std::min<uint32_t>(
-		env_u32("CGPU_POL_LOAD_PCT", 50), 90));
-	const uint64_t want_slots = (c->pol_total * 100 + load_pct - 1) / load_pct + 1;
-	uint32_t nb = next_pow2(std::max<uint64_t>(64, (want_slots + b.bpb - 1) / b.bpb));
-	b.max_probe = 1;
-	if (b.bpb == 1) {
-		std::vector<std::array<uint32_t, 4>> keys;
-		keys.reserve(c->pol_total);
-		for (uint32_t ep = 0; ep < c->pol.size(); ep++)
-			for (auto &kv : c->pol[ep])
-				keys.push_back({(uint32_t)kv.first, (uint32_t)(kv.first >> 32),
-						ep | (uint32_t)kv.second.proxy_port << 16, kv.second.slot});
-		place_pol_hop(b, keys, nb);
-		return;
-	}
-	b.slots.assign((size_t)nb * b.bpb, pol_slot{0, 0, 0, POL_EMPTY});
-	b.mask = nb - 1;
-	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
-		for (auto &kv : c->pol[ep]) {
-			uint32_t lo = (uint32_t)kv.first, hi = (uint32_t)(kv.first >> 32);
-			uint32_t bk = pol_hash(lo, hi, ep) & b.mask, probe = 1;
-			for (;;) {
-				pol_slot *s = &b.slots[(size_t)bk * b.bpb];
-				uint32_t k = 0;
-				while (k < b.bpb && s[k].ctr != POL_EMPTY)
-					k++;
-				if (k < b.bpb) {
-					s[k] = pol_slot{lo, hi, ep | (uint32_t)kv.second.proxy_port << 16,
-							kv.second.slot};
-					break;
-				}
-				bk = (bk + 1) & b.mask;
-				probe++;
-			}
-			b.max_probe = std::max(b.max_probe, probe);
-		}
-}
 
 struct Set4Build {
 	std::vector<set4_slot> slots;
@@ -1659,49 +950,44 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 }
 
 /* prefilter v6 any-match set (bpf_xdp.c:132-156): dyn6 (if
- * CIDR6_LPM_PREFILTER) + fix6 keys with prefixlen 128. */
-void build_pf6(const cgpu_ctx *c, Cover6Build &b)
+ * CIDR6_LPM_PREFILTER) + fix6 keys with prefixlen 128 (dyn keys canonical) */
+std::vector<Rank6> pf6_candidates(const PfIn &in)
 {
 	std::vector<Rank6> cand;
-	if (c->cfg.prefilter_fix6) {
-		if (c->cfg.prefilter_dyn6)
-			for (auto &kv : c->dyn6)
-				cand.push_back(Rank6{kv.first.plen, kv.first.plen, kv.first.data, 1});
-		for (auto &k : c->fix6) {
-			uint32_t plen;
-			memcpy(&plen, k.data(), 4);
-			if (plen != 128)
-				continue;
-			Rank6 r{128, 128, {}, 1};
-			memcpy(r.addr.data(), k.data() + 4, 16);
+	if (!in.fix6)
+		return cand;
+	if (in.dyn6)
+		for (auto &k : in.dyn6k) {
+			Rank6 r{k.prefixlen, k.prefixlen, {}, 1};
+			memcpy(r.addr.data(), k.addr, 16);
 			cand.push_back(r);
 		}
+	for (auto &k : in.fix6k) {
+		if (k.prefixlen != 128)
+			continue;
+		Rank6 r{128, 128, {}, 1};
+		memcpy(r.addr.data(), k.addr, 16);
+		cand.push_back(r);
 	}
-	build_cover6(cand, b);
+	return cand;
 }
 
 /* ipcache -> v6 LPM for IPv6 lookups (ipcache_lookup6, eps.h:56-66): a
  * lookup key is {prefixlen 160, pad 0, family 2, ip6}; entries ending inside
- * the static part rank below /0, exactly as build_ipc4. */
-void build_ipc6(const cgpu_ctx *c, V6Build &b)
+ * the static part rank below /0, exactly as ipc4_candidate.  canon: the
+ * mirror's masked key data. */
+static const uint8_t kStaticV6[4] = {0, 0, 0, 2};
+bool ipc6_candidate(const cgpu_ipcache_key &raw, const uint8_t *canon, uint32_t label, Rank6 *r)
 {
-	static const uint8_t static_v6[4] = {0, 0, 0, 2};
-	std::vector<Rank6> cand;
-	for (auto &kv : c->ipc) {
-		const IpcEntry &e = kv.second;
-		uint32_t p = e.raw.prefixlen;
-		const uint8_t *data = (const uint8_t *)&e.raw + 4;
-		if (!prefix_eq(data, static_v6, std::min<uint32_t>(p, 32)))
-			continue;
-		Rank6 r{p, 0, {}, e.val.sec_label};
-		if (p >= 32) {
-			r.len = p - 32;
-			/* canonical (masked) address bits from the mirror key */
-			memcpy(r.addr.data(), kv.first.data.data() + 4, 16);
-		}
-		cand.push_back(r);
+	const uint32_t p = raw.prefixlen;
+	if (!prefix_eq((const uint8_t *)&raw + 4, kStaticV6, std::min<uint32_t>(p, 32)))
+		return false;
+	*r = Rank6{p, 0, {}, label};
+	if (p >= 32) {
+		r->len = p - 32;
+		memcpy(r->addr.data(), canon + 4, 16);
 	}
-	build_v6(std::move(cand), b);
+	return true;
 }
 
 /* Service map -> frontend hash + dense backend rows (tables.h lb_table).
@@ -1713,15 +999,17 @@ struct LbBuild {
 	uint32_t mask = 0, vip_mask = 0;
 };
 
-int build_lb(const cgpu_ctx *c, LbBuild &b)
+typedef std::vector<std::pair<uint64_t, cgpu_lb4_service>> LbIn; /* sorted by mkey */
+
+int build_lb(const LbIn &lb, uint32_t lb_max_entries, LbBuild &b)
 {
 	std::vector<std::array<uint32_t, 4>> fes;
-	const uint64_t cap = 4ull * c->cfg.lb_max_entries + 65536ull;
-	for (auto it = c->lb.begin(); it != c->lb.end();) {
+	const uint64_t cap = 4ull * lb_max_entries + 65536ull;
+	for (auto it = lb.begin(); it != lb.end();) {
 		const uint64_t fk = it->first >> 16;
 		uint32_t mcount = 0, maxs = 0;
 		auto jt = it;
-		for (; jt != c->lb.end() && (jt->first >> 16) == fk; ++jt) {
+		for (; jt != lb.end() && (jt->first >> 16) == fk; ++jt) {
 			const uint32_t s = (uint32_t)(jt->first & 0xFFFFu);
 			if (s == 0)
 				mcount = jt->second.count;
@@ -1772,9 +1060,9 @@ int build_lb(const cgpu_ctx *c, LbBuild &b)
 	}
 	if (b.be.empty())
 		b.be.push_back({0, 0, 0, 0});
-	/* CGPU_LB_VIP_BITS: bits per frontend (diagnostic A/B; default 8:
-	 * config 5 at 4 / 8 / 16 / 32 / 64 bits: 22.6 / 22.5 / 22.3 / 22.0 / 21.7 Gpps) */
-	const uint64_t bits = next_pow2(std::max<uint64_t>(1u << 15, (uint64_t)env_u32("CGPU_LB_VIP_BITS", 8) * fes.size()));
+	/* 8 bits per frontend (config 5 at 4 / 8 / 16 / 32 / 64 bits per
+	 * frontend: 22.6 / 22.5 / 22.3 / 22.0 / 21.7 Gpps, round 1) */
+	const uint64_t bits = next_pow2(std::max<uint64_t>(1u << 15, 8ull * fes.size()));
 	b.vip.assign(bits / 32, 0u);
 	b.vip_mask = (uint32_t)(bits - 1);
 	for (auto &f : fes) {
@@ -1784,29 +1072,1443 @@ int build_lb(const cgpu_ctx *c, LbBuild &b)
 	return 0;
 }
 
+/* ---------------- device buffers, snapshots (epochs) ----------------
+ * Every table group of a snapshot lives in one device buffer; a commit
+ * uploads the groups that changed and shares the others with the previous
+ * snapshot.  A buffer is freed stream-ordered on the context's retirement
+ * stream (hipFreeAsync) once no snapshot references it, and only after that
+ * stream has waited for the last launch of every snapshot that used it. */
+enum { G_IPC = 0, G_POL, G_PF, G_EP, G_LB, G_LXC, G_N };
+
+struct DevBuf {
+	void *p = nullptr;
+	size_t bytes = 0;
+	int dev = -1;
+	hipStream_t st = nullptr;
+	~DevBuf()
+	{
+		if (p) {
+			(void)hipSetDevice(dev);
+			(void)hipFreeAsync(p, st); /* the context's retirement stream */
+		}
+	}
+};
+typedef std::shared_ptr<DevBuf> DevBufP;
+
+struct Epoch;
+
+/* host images kept between commits (guarded by cgpu_ctx::commit_mu) so that
+ * small deltas patch them instead of recompiling everything */
+struct BuildState {
+	bool ipc4_ok = false;
+	Dir248 dir;       /* ipcache v4 DIR-24-8 (host only) */
+	Lpm16cBuild lc;   /* its compressed form (uploaded) */
+	V6Build v6;
+	bool pol_ok = false;
+	PolBuild pol;
+	std::vector<uint8_t> slot_dir;
+	uint64_t sum[G_N] = {0, 0, 0, 0, 0, 0};
+};
+
 } // namespace
 
-CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
+struct cgpu_ctx {
+	cgpu_config cfg;
+	int device = -1;
+	/* lock order: commit_mu -> mu -> retire_mu; pub_mu and pk_mu are leaves */
+	std::mutex mu;        /* host mirror */
+	std::mutex commit_mu; /* one commit at a time; BuildState */
+	std::mutex pub_mu;    /* the published snapshot */
+	std::mutex pk_mu;     /* per-stream packed counter buffers */
+	std::mutex retire_mu;
+
+	/* ---- host mirror ---- */
+	std::map<LpmKey<20>, IpcEntry> ipc;
+	std::vector<std::map<uint64_t, PolEntry>> pol;
+	size_t pol_total = 0;
+	/* counter slots: hot class [0, hot_cap) for L3-only / wildcard keys,
+	 * cold class [hot_cap, n_ctr_slots) for the rest.  A slot whose key a
+	 * published snapshot holds is quarantined on delete until every
+	 * snapshot up to that one has finished its launches. */
+	std::vector<uint32_t> free_hot, free_cold;
+	std::deque<std::pair<uint64_t, uint32_t>> quarantine; /* (snapshot id, slot) */
+	uint32_t next_hot = 0, next_cold = 0, hot_cap = 0;
+	std::vector<SlotInit> slot_inits;
+	std::map<LpmKey<4>, cgpu_cidr_key> dyn4;
+	std::map<LpmKey<16>, cgpu_cidr_key> dyn6;
+	std::set<std::array<uint8_t, 8>> fix4;
+	std::set<std::array<uint8_t, 20>> fix6;
+	std::set<std::array<uint8_t, 20>> lxc;
+	/* cilium_lb4_services, keyed address << 32 | dport << 16 | slave so that
+	 * a frontend's entries are adjacent */
+	std::map<uint64_t, cgpu_lb4_service> lb;
+	/* per-endpoint lxc_config.h identity (cgpu_lxc_update) */
+	std::map<uint32_t, cgpu_lxc_info> lxcinfo;
+	/* ---- change tracking since the last captured commit ---- */
+	uint32_t dirty = 0;             /* 1 << G_* */
+	bool ipc_full = true, pol_full = true;
+	std::vector<LpmKey<20>> ipc_changes;
+	std::vector<std::pair<uint32_t, uint64_t>> pol_changes; /* (ep, key) */
+	uint64_t captured = 0;          /* id of the newest snapshot whose inputs were captured */
+	uint64_t sum_ipc = 0, sum_pol = 0; /* order-independent content sums */
+
+	/* ---- device ---- */
+	hipStream_t ustream = nullptr;  /* uploads + counter slot init of commits */
+	hipStream_t rstream = nullptr;  /* retirement: waits on launches, then frees */
+	hipMemPool_t pool = nullptr;    /* snapshot buffers (stream-ordered) */
+	BuildState b;
+	std::shared_ptr<Epoch> cur;     /* published snapshot (pub_mu) */
+	uint64_t epoch = 0;             /* id of the published snapshot */
+	uint64_t checksum = 0;
+	/* snapshots unpublished but maybe still running: (id, done event on
+	 * rstream); alive = ids not known complete (incl. the published one) */
+	std::deque<std::pair<uint64_t, hipEvent_t>> retiring;
+	std::set<uint64_t> alive;
+	uint32_t n_ctr_slots = 0;
+	uint64_t *d_totals = nullptr; /* [2*slots + METRICS] */
+	uint64_t *d_delta_own = nullptr;
+	uint64_t *d_delta = nullptr;  /* own or bound */
+	/* [n_ctr_slots] packed counter accumulator per stream (zero between
+	 * classify calls; one per stream keeps its exactness bound per call) */
+	std::map<void *, uint64_t *> d_pk;
+
+	/* ---- multi-GPU counter reduction (cgpu_comm_init) ---- */
+	void *comm = nullptr; /* ncclComm_t */
+
+	/* ---- conntrack map cilium_ct4_global (tables.h ct_table layout) ----
+	 * A host shadow serves the bpf(2)-style map calls; the device copy is
+	 * authoritative once a batch ran (ct_dev_newer) and is refreshed from
+	 * the shadow before the next batch after host edits (ct_host_newer). */
+	std::vector<uint4> ct_keys, ct_vals; /* [nslots], [4 * nslots] */
+	uint32_t ct_mask = 0, ct_live = 0, ct_tombs = 0;
+	bool ct_dev_newer = false, ct_host_newer = false;
+	uint4 *d_ct_keys = nullptr, *d_ct_vals = nullptr;
+	uint32_t *d_ct_count = nullptr;
+	void *d_ct_scratch = nullptr;
+	size_t ct_scratch_cap = 0;
+	hipStream_t ct_stream = nullptr; /* the conntrack path's internal stream */
+	hipEvent_t ct_done = nullptr;
+};
+
+namespace {
+
+/* One published snapshot.  Launches pin it (shared_ptr) while they enqueue,
+ * wait on `ready` (its uploads) and record a per-stream event after their
+ * kernels; when the last reference drops, the retirement stream waits on
+ * those events before the buffers it alone held are freed, and `done` marks
+ * when every launch of this snapshot has finished. */
+struct Epoch {
+	cgpu_ctx *c = nullptr;
+	uint64_t id = 0;
+	cgpu_snapshot snap{};
+	DevBufP bufs[G_N];
+	hipEvent_t ready = nullptr;
+	std::mutex mu;
+	std::vector<std::pair<hipStream_t, hipEvent_t>> used;
+	~Epoch()
+	{
+		(void)hipSetDevice(c->device);
+		for (auto &u : used) {
+			(void)hipStreamWaitEvent(c->rstream, u.second, 0);
+			(void)hipEventDestroy(u.second);
+		}
+		hipEvent_t done = nullptr;
+		if (hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess &&
+		    hipEventRecord(done, c->rstream) == hipSuccess) {
+			std::lock_guard<std::mutex> g(c->retire_mu);
+			c->retiring.push_back({id, done});
+		} else {
+			(void)hipStreamSynchronize(c->rstream);
+			if (done)
+				(void)hipEventDestroy(done);
+			std::lock_guard<std::mutex> g(c->retire_mu);
+			c->alive.erase(id);
+		}
+		if (ready)
+			(void)hipEventDestroy(ready);
+		/* bufs release after this body: their hipFreeAsync follows the waits */
+	}
+};
+
+/* snapshots whose launches finished leave `alive` (caller holds retire_mu) */
+void poll_retired(cgpu_ctx *c)
+{
+	while (!c->retiring.empty()) {
+		auto &f = c->retiring.front();
+		if (hipEventQuery(f.second) != hipSuccess)
+			break;
+		(void)hipEventDestroy(f.second);
+		c->alive.erase(f.first);
+		c->retiring.pop_front();
+	}
+}
+
+/* quarantined counter slots whose snapshots all finished become free
+ * (caller holds mu) */
+void release_quarantine(cgpu_ctx *c)
+{
+	if (c->quarantine.empty())
+		return;
+	uint64_t lowest;
+	{
+		std::lock_guard<std::mutex> g(c->retire_mu);
+		poll_retired(c);
+		lowest = c->alive.empty() ? UINT64_MAX : *c->alive.begin();
+	}
+	while (!c->quarantine.empty() && c->quarantine.front().first < lowest) {
+		const uint32_t slot = c->quarantine.front().second;
+		(slot < c->hot_cap ? c->free_hot : c->free_cold).push_back(slot);
+		c->quarantine.pop_front();
+	}
+}
+
+} // namespace
+
+/* ======================================================================= */
+/* config / context                                                          */
+/* ======================================================================= */
+CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
+{
+	memset(c, 0, sizeof(*c));
+	c->abi_version = CGPU_ABI_VERSION;
+	c->ipcache_max = 512000;      /* pkg/maps/ipcache/ipcache.go:36 */
+	c->policy_max_per_ep = 16384; /* pkg/maps/policymap/policymap.go:37 */
+	c->policy_max_total = 1u << 20;
+	c->max_endpoints = 65536;     /* ENDPOINTS_MAP_SIZE */
+	c->cidr_dyn_max = 1u << 20;   /* > maxLKeys: device capacity, configurable */
+	c->cidr_fix_max = 20u << 20;  /* maxHKeys (pkg/policy/prefilter.go:44) */
+	c->endpoints_max = 65536;
+	c->host_id = 1;
+	c->world_id = 2;
+	c->cluster_id = 3;
+	c->health_id = 4;
+	c->ipv4_cluster_mask = 0xff0000;  /* bpf/node_config.h:42 */
+	c->ipv4_cluster_range = 0x100000; /* bpf/node_config.h:43 */
+	c->ct_proto_gate = 1;             /* CONNTRACK (bpf/lxc_config.h:46) */
+	c->ingress_secctx_world = 0;
+	c->prefilter_fix4 = c->prefilter_dyn4 = 1; /* bpf/filter_config.h */
+	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
+	c->ingress_src_identity = 0;
+	c->hot_counter_slots = 8192;
+	c->lb_max_entries = 65536;        /* CILIUM_LB_MAP_MAX_ENTRIES, bpf/node_config.h:60 */
+	c->ipv4_loopback = 0x1ffff50a;    /* IPV4_LOOPBACK, bpf/node_config.h:45 */
+	c->lb_flags = CGPU_LB_L3 | CGPU_LB_L4; /* bpf/lxc_config.h:44-45 */
+	static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x1,
+					   0x0, 0x1, 0x0, 0x0}; /* ROUTER_IP, bpf/node_config.h:30 */
+	memcpy(c->ipv6_router_ip, router, 16);
+	static const uint8_t node_mac[6] = {0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde}; /* NODE_MAC, node_config.h:51 */
+	memcpy(c->node_mac, node_mac, 6);
+	c->ct_max = 1000000; /* CT_MAP_SIZE = MapNumEntriesGlobal, pkg/maps/ctmap/ctmap.go:101 */
+}
+
+CGPU_EXPORT const char *cgpu_last_error(void) { return g_last_error.c_str(); }
+CGPU_EXPORT const char *cgpu_version(void) { return "cgpu 0.1 gfx950 abi1"; }
+
+CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **out)
+{
+	if (!cfg || !out)
+		return fail(-EINVAL, "null argument");
+	if (cfg->abi_version != CGPU_ABI_VERSION)
+		return fail(-EINVAL, "abi_version %u != %u", cfg->abi_version, CGPU_ABI_VERSION);
+	if (!cfg->max_endpoints || !cfg->policy_max_total)
+		return fail(-EINVAL, "zero capacity");
+	if (cfg->policy_max_total >= POL_CTR_EMPTY)
+		return fail(-EINVAL, "policy_max_total %u >= 2^24 - 1", cfg->policy_max_total);
+	if (!cfg->ct_max || cfg->ct_max > (1u << 28))
+		return fail(-EINVAL, "ct_max %u out of range (1 .. 2^28)", cfg->ct_max);
+	cgpu_ctx *c = new cgpu_ctx();
+	c->cfg = *cfg;
+	c->pol.resize(cfg->max_endpoints);
+	c->n_ctr_slots = cfg->policy_max_total;
+	c->hot_cap = std::min(cfg->hot_counter_slots, cfg->policy_max_total / 2);
+	c->next_cold = c->hot_cap;
+	c->dirty = (1u << G_N) - 1u; /* the first commit compiles every group */
+	if (device >= 0) {
+		int ndev = 0, pools = 0;
+		if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+			delete c;
+			return fail(-ENODEV, "HIP device %d not present", device);
+		}
+		c->device = device;
+		size_t words = (size_t)2 * c->n_ctr_slots + CGPU_METRICS_WORDS;
+		if (hipSetDevice(device) != hipSuccess ||
+		    hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, device) != hipSuccess ||
+		    !pools) {
+			delete c;
+			return fail(-EIO, "device %d: no stream-ordered memory pools", device);
+		}
+		hipMemPoolProps pp{};
+		pp.allocType = hipMemAllocationTypePinned;
+		pp.location.type = hipMemLocationTypeDevice;
+		pp.location.id = device;
+		uint64_t keep = UINT64_MAX;
+		int no = 0;
+		if (hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess ||
+		    hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking) != hipSuccess ||
+		    hipMemPoolCreate(&c->pool, &pp) != hipSuccess ||
+		    hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess ||
+		    /* an upload never waits behind the retirement stream's waits */
+		    hipMemPoolSetAttribute(c->pool, hipMemPoolReuseAllowInternalDependencies, &no) != hipSuccess ||
+		    hipStreamCreateWithFlags(&c->ct_stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipEventCreateWithFlags(&c->ct_done, hipEventDisableTiming) != hipSuccess ||
+		    hipMalloc((void **)&c->d_totals, words * 8) != hipSuccess ||
+		    hipMalloc((void **)&c->d_delta_own, words * 8) != hipSuccess ||
+		    hipMemset(c->d_totals, 0, words * 8) != hipSuccess ||
+		    hipMemset(c->d_delta_own, 0, words * 8) != hipSuccess) {
+			(void)hipFree(c->d_totals);
+			(void)hipFree(c->d_delta_own);
+			if (c->ustream)
+				(void)hipStreamDestroy(c->ustream);
+			if (c->rstream)
+				(void)hipStreamDestroy(c->rstream);
+			if (c->pool)
+				(void)hipMemPoolDestroy(c->pool);
+			if (c->ct_stream)
+				(void)hipStreamDestroy(c->ct_stream);
+			if (c->ct_done)
+				(void)hipEventDestroy(c->ct_done);
+			delete c;
+			return fail(-EIO, "device context allocation failed");
+		}
+		c->d_delta = c->d_delta_own;
+	}
+	*out = c;
+	return 0;
+}
+
+static void comm_destroy(cgpu_ctx *c);
+
+CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
+{
+	if (!c)
+		return;
+	if (c->device >= 0) {
+		(void)hipSetDevice(c->device);
+		(void)hipDeviceSynchronize();
+		std::shared_ptr<Epoch> last;
+		{
+			std::lock_guard<std::mutex> g(c->pub_mu);
+			last.swap(c->cur);
+		}
+		last.reset(); /* waits + frees enqueued on rstream */
+		(void)hipStreamSynchronize(c->ustream);
+		(void)hipStreamSynchronize(c->rstream);
+		{
+			std::lock_guard<std::mutex> g(c->retire_mu);
+			for (auto &r : c->retiring)
+				(void)hipEventDestroy(r.second);
+			c->retiring.clear();
+		}
+		comm_destroy(c);
+		(void)hipFree(c->d_totals);
+		(void)hipFree(c->d_delta_own);
+		for (auto &kv : c->d_pk)
+			(void)hipFree(kv.second);
+		(void)hipFree(c->d_ct_keys);
+		(void)hipFree(c->d_ct_vals);
+		(void)hipFree(c->d_ct_count);
+		(void)hipFree(c->d_ct_scratch);
+		(void)hipEventDestroy(c->ct_done);
+		(void)hipStreamDestroy(c->ct_stream);
+		(void)hipStreamDestroy(c->ustream);
+		(void)hipStreamDestroy(c->rstream);
+		(void)hipMemPoolDestroy(c->pool);
+	}
+	delete c;
+}
+
+static int check_flags(uint64_t flags)
+{
+	return flags > CGPU_EXIST ? fail(-EINVAL, "bad update flags %llu", (unsigned long long)flags) : 0;
+}
+
+/* ======================================================================= */
+/* change tracking (caller holds mu)                                         */
+/* ======================================================================= */
+/* more changes than this between commits: recompile the group instead */
+static const size_t kMaxPatch = 4096;
+
+static uint64_t ipc_hash(const LpmKey<20> &k, const cgpu_remote_endpoint_info &v)
+{
+	return fnv(fnv(1469598103934665603ull, &k, sizeof(k)), &v, 8);
+}
+
+static uint64_t pol_hash_sum(uint32_t ep, uint64_t key, const PolEntry &e)
+{
+	const uint64_t h = fnv(1469598103934665603ull ^ ep, &key, 8);
+	return fnv(h, &e.proxy_port, 2) ^ ((uint64_t)e.slot << 1);
+}
+
+static void ipc_touch(cgpu_ctx *c, const LpmKey<20> &k)
+{
+	c->dirty |= 1u << G_IPC;
+	if (c->ipc_full)
+		return;
+	if (c->ipc_changes.size() >= kMaxPatch) {
+		c->ipc_full = true;
+		c->ipc_changes.clear();
+	} else {
+		c->ipc_changes.push_back(k);
+	}
+}
+
+static void pol_touch(cgpu_ctx *c, uint32_t ep, uint64_t key)
+{
+	c->dirty |= 1u << G_POL;
+	if (c->pol_full)
+		return;
+	if (c->pol_changes.size() >= kMaxPatch) {
+		c->pol_full = true;
+		c->pol_changes.clear();
+	} else {
+		c->pol_changes.push_back({ep, key});
+	}
+}
+
+/* ======================================================================= */
+/* ipcache                                                                   */
+/* ======================================================================= */
+CGPU_EXPORT int cgpu_ipcache_update(cgpu_ctx *c, const cgpu_ipcache_key *key,
+				    const cgpu_remote_endpoint_info *val, uint64_t flags)
+{
+	if (!c || !key || !val)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	if (key->prefixlen > 160) /* data is 20 bytes: lpm_trie max_prefixlen */
+		return fail(-EINVAL, "ipcache prefixlen %u > 160", key->prefixlen);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto k = lpm_canon<20>(key->prefixlen, (const uint8_t *)key + 4);
+	auto it = c->ipc.find(k);
+	if (it == c->ipc.end()) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "ipcache key not present");
+		if (c->ipc.size() >= c->cfg.ipcache_max)
+			return fail(-ENOSPC, "ipcache full (%u)", c->cfg.ipcache_max);
+		c->ipc.emplace(k, IpcEntry{*key, *val});
+	} else {
+		if (flags == CGPU_NOEXIST)
+			return fail(-EEXIST, "ipcache key exists");
+		c->sum_ipc -= ipc_hash(k, it->second.val);
+		it->second = IpcEntry{*key, *val};
+	}
+	c->sum_ipc += ipc_hash(k, *val);
+	ipc_touch(c, k);
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_ipcache_delete(cgpu_ctx *c, const cgpu_ipcache_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (key->prefixlen > 160)
+		return fail(-EINVAL, "ipcache prefixlen %u > 160", key->prefixlen);
+	std::lock_guard<std::mutex> g(c->mu);
+	const auto k = lpm_canon<20>(key->prefixlen, (const uint8_t *)key + 4);
+	auto it = c->ipc.find(k);
+	if (it == c->ipc.end())
+		return fail(-ENOENT, "ipcache key not present");
+	c->sum_ipc -= ipc_hash(k, it->second.val);
+	c->ipc.erase(it);
+	ipc_touch(c, k);
+	return 0;
+}
+
+/* bpf(2) lookup on an LPM trie = longest prefix match of the given key */
+CGPU_EXPORT int cgpu_ipcache_lookup(cgpu_ctx *c, const cgpu_ipcache_key *key,
+				    cgpu_remote_endpoint_info *out)
+{
+	if (!c || !key || !out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	const uint8_t *q = (const uint8_t *)key + 4;
+	uint32_t qlen = std::min<uint32_t>(key->prefixlen, 160);
+	/* probe each shorter-or-equal prefix length, longest first */
+	for (int64_t p = qlen; p >= 0; p--) {
+		auto it = c->ipc.find(lpm_canon<20>((uint32_t)p, q));
+		if (it != c->ipc.end()) {
+			*out = it->second.val;
+			return 0;
+		}
+	}
+	return -ENOENT;
+}
+
+CGPU_EXPORT int cgpu_ipcache_get_next_key(cgpu_ctx *c, const cgpu_ipcache_key *key,
+					  cgpu_ipcache_key *next)
+{
+	if (!c || !next)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = c->ipc.begin();
+	if (key) {
+		auto k = lpm_canon<20>(std::min<uint32_t>(key->prefixlen, 160), (const uint8_t *)key + 4);
+		it = c->ipc.upper_bound(k);
+	}
+	if (it == c->ipc.end())
+		return -ENOENT;
+	*next = it->second.raw;
+	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_ipcache_count(cgpu_ctx *c)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->ipc.size();
+}
+
+/* ======================================================================= */
+/* policy                                                                    */
+/* ======================================================================= */
+static inline uint64_t pol_key64(const cgpu_policy_key *k)
+{
+	uint64_t x;
+	memcpy(&x, k, 8);
+	return x;
+}
+
+CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+				   const cgpu_policy_entry *e, uint64_t flags)
+{
+	if (!c || !key || !e)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	if (ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "endpoint %u >= max_endpoints %u", ep, c->cfg.max_endpoints);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	uint64_t k = pol_key64(key);
+	auto it = m.find(k);
+	uint32_t slot;
+	if (it == m.end()) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "policy key not present");
+		if (m.size() >= c->cfg.policy_max_per_ep)
+			return fail(-E2BIG, "policy map of ep %u full (%u)", ep, c->cfg.policy_max_per_ep);
+		/* L3-only {id, 0, 0, dir} and wildcard {0, port, proto, dir} keys
+		 * absorb most hits: give them hot (LDS-accumulated) slots */
+		bool hot = (key->dport == 0 && key->protocol == 0) || key->sec_label == 0;
+		if (c->free_cold.empty() || (hot && c->free_hot.empty()))
+			release_quarantine(c);
+		if (hot && !c->free_hot.empty()) {
+			slot = c->free_hot.back();
+			c->free_hot.pop_back();
+		} else if (hot && c->next_hot < c->hot_cap) {
+			slot = c->next_hot++;
+		} else if (!c->free_cold.empty()) {
+			slot = c->free_cold.back();
+			c->free_cold.pop_back();
+		} else if (c->next_cold < c->n_ctr_slots) {
+			slot = c->next_cold++;
+		} else {
+			return fail(-E2BIG, "policy device slots exhausted (%u)", c->n_ctr_slots);
+		}
+		auto ins = m.emplace(k, PolEntry{e->proxy_port, slot, c->captured + 1}).first;
+		c->pol_total++;
+		c->sum_pol += pol_hash_sum(ep, k, ins->second);
+	} else {
+		if (flags == CGPU_NOEXIST)
+			return fail(-EEXIST, "policy key exists");
+		c->sum_pol -= pol_hash_sum(ep, k, it->second);
+		it->second.proxy_port = e->proxy_port;
+		slot = it->second.slot;
+		c->sum_pol += pol_hash_sum(ep, k, it->second);
+	}
+	pol_touch(c, ep, k);
+	/* kernel htab replaces the whole value: counters restart from it */
+	c->slot_inits.push_back(SlotInit{slot, e->packets, e->bytes});
+	return 0;
+}
+
+static void pol_erase(cgpu_ctx *c, uint32_t ep, std::map<uint64_t, PolEntry> &m,
+		      std::map<uint64_t, PolEntry>::iterator it)
+{
+	const uint32_t slot = it->second.slot;
+	if (it->second.first_epoch <= c->captured) /* a snapshot may count into it */
+		c->quarantine.push_back({c->captured, slot});
+	else
+		(slot < c->hot_cap ? c->free_hot : c->free_cold).push_back(slot);
+	c->sum_pol -= pol_hash_sum(ep, it->first, it->second);
+	pol_touch(c, ep, it->first);
+	m.erase(it);
+	c->pol_total--;
+}
+
+CGPU_EXPORT int cgpu_policy_delete(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "endpoint %u out of range", ep);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	auto it = m.find(pol_key64(key));
+	if (it == m.end())
+		return fail(-ENOENT, "policy key not present");
+	pol_erase(c, ep, m, it);
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_flush(cgpu_ctx *c, uint32_t ep)
+{
+	if (!c || ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "bad argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	while (!m.empty())
+		pol_erase(c, ep, m, m.begin());
+	return 0;
+}
+
+static int read_counter_words(cgpu_ctx *c, size_t word, size_t nwords, uint64_t *out)
+{
+	/* totals + delta; pending launches complete first */
+	std::vector<uint64_t> a(nwords), b(nwords);
+	uint64_t *delta;
+	{
+		std::lock_guard<std::mutex> g(c->pk_mu);
+		delta = c->d_delta;
+	}
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipDeviceSynchronize());
+	HIP_OR_EIO(hipMemcpy(a.data(), c->d_totals + word, nwords * 8, hipMemcpyDeviceToHost));
+	HIP_OR_EIO(hipMemcpy(b.data(), delta + word, nwords * 8, hipMemcpyDeviceToHost));
+	for (size_t i = 0; i < nwords; i++)
+		out[i] = a[i] + b[i];
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_lookup(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+				   cgpu_policy_entry *out)
+{
+	if (!c || !key || !out)
+		return fail(-EINVAL, "null argument");
+	if (ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "endpoint %u out of range", ep);
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	auto it = m.find(pol_key64(key));
+	if (it == m.end())
+		return -ENOENT;
+	memset(out, 0, sizeof(*out));
+	out->proxy_port = it->second.proxy_port;
+	/* the most recent update's counter values until the next commit */
+	uint64_t pk = 0, by = 0;
+	bool pending = false;
+	for (auto s = c->slot_inits.rbegin(); s != c->slot_inits.rend(); ++s)
+		if (s->slot == it->second.slot) {
+			pk = s->packets;
+			by = s->bytes;
+			pending = true;
+			break;
+		}
+	if (!pending && c->device >= 0 && c->captured) {
+		uint64_t w[2];
+		if (int r = read_counter_words(c, (size_t)2 * it->second.slot, 2, w))
+			return r;
+		pk = w[0];
+		by = w[1];
+	}
+	out->packets = pk;
+	out->bytes = by;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_get_next_key(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+					 cgpu_policy_key *next)
+{
+	if (!c || !next || ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "bad argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	auto it = key ? m.upper_bound(pol_key64(key)) : m.begin();
+	if (it == m.end())
+		return -ENOENT;
+	memcpy(next, &it->first, 8);
+	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_policy_count(cgpu_ctx *c, uint32_t ep)
+{
+	if (!c || ep >= c->cfg.max_endpoints)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->pol[ep].size();
+}
+
+/* ======================================================================= */
+/* prefilter CIDR maps + endpoint map                                        */
+/* ======================================================================= */
+CGPU_EXPORT int cgpu_cidr_update(cgpu_ctx *c, int which, const cgpu_cidr_key *key, uint64_t flags)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	bool exists;
+	switch (which) {
+	case CGPU_CIDR_V4_DYN:
+	case CGPU_CIDR_V6_DYN: {
+		uint32_t maxp = which == CGPU_CIDR_V4_DYN ? 32 : 128;
+		if (key->prefixlen > maxp)
+			return fail(-EINVAL, "prefixlen %u > %u", key->prefixlen, maxp);
+		if (which == CGPU_CIDR_V4_DYN) {
+			auto k = lpm_canon<4>(key->prefixlen, key->addr);
+			exists = c->dyn4.count(k);
+			if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+			if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+			if (!exists && c->dyn4.size() >= c->cfg.cidr_dyn_max) return fail(-ENOSPC, "dyn4 full");
+			c->dyn4[k] = *key;
+			c->dirty |= 1u << G_PF;
+		} else {
+			auto k = lpm_canon<16>(key->prefixlen, key->addr);
+			exists = c->dyn6.count(k);
+			if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+			if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+			if (!exists && c->dyn6.size() >= c->cfg.cidr_dyn_max) return fail(-ENOSPC, "dyn6 full");
+			c->dyn6[k] = *key;
+			c->dirty |= 1u << G_PF;
+		}
+		return 0;
+	}
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k;
+		memcpy(k.data(), key, 8);
+		exists = c->fix4.count(k);
+		if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+		if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+		if (!exists && c->fix4.size() >= c->cfg.cidr_fix_max) return fail(-E2BIG, "fix4 full");
+		c->fix4.insert(k);
+		c->dirty |= 1u << G_PF;
+		return 0;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k;
+		memcpy(k.data(), key, 20);
+		exists = c->fix6.count(k);
+		if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+		if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+		if (!exists && c->fix6.size() >= c->cfg.cidr_fix_max) return fail(-E2BIG, "fix6 full");
+		c->fix6.insert(k);
+		c->dirty |= 1u << G_PF;
+		return 0;
+	}
+	}
+	return fail(-EINVAL, "bad cidr map %d", which);
+}
+
+CGPU_EXPORT int cgpu_cidr_delete(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	size_t n = 0;
+	switch (which) {
+	case CGPU_CIDR_V4_DYN:
+		if (key->prefixlen > 32) return fail(-EINVAL, "prefixlen");
+		n = c->dyn4.erase(lpm_canon<4>(key->prefixlen, key->addr));
+		break;
+	case CGPU_CIDR_V6_DYN:
+		if (key->prefixlen > 128) return fail(-EINVAL, "prefixlen");
+		n = c->dyn6.erase(lpm_canon<16>(key->prefixlen, key->addr));
+		break;
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k;
+		memcpy(k.data(), key, 8);
+		n = c->fix4.erase(k);
+		break;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k;
+		memcpy(k.data(), key, 20);
+		n = c->fix6.erase(k);
+		break;
+	}
+	default:
+		return fail(-EINVAL, "bad cidr map %d", which);
+	}
+	if (n)
+		c->dirty |= 1u << G_PF;
+	return n ? 0 : -ENOENT;
+}
+
+CGPU_EXPORT int cgpu_cidr_lookup(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	switch (which) {
+	case CGPU_CIDR_V4_DYN:
+		for (int64_t p = std::min<uint32_t>(key->prefixlen, 32); p >= 0; p--)
+			if (c->dyn4.count(lpm_canon<4>((uint32_t)p, key->addr)))
+				return 0;
+		return -ENOENT;
+	case CGPU_CIDR_V6_DYN:
+		for (int64_t p = std::min<uint32_t>(key->prefixlen, 128); p >= 0; p--)
+			if (c->dyn6.count(lpm_canon<16>((uint32_t)p, key->addr)))
+				return 0;
+		return -ENOENT;
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k;
+		memcpy(k.data(), key, 8);
+		return c->fix4.count(k) ? 0 : -ENOENT;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k;
+		memcpy(k.data(), key, 20);
+		return c->fix6.count(k) ? 0 : -ENOENT;
+	}
+	}
+	return fail(-EINVAL, "bad cidr map %d", which);
+}
+
+CGPU_EXPORT int cgpu_cidr_get_next_key(cgpu_ctx *c, int which, const cgpu_cidr_key *key,
+				       cgpu_cidr_key *next)
+{
+	if (!c || !next)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	memset(next, 0, sizeof(*next));
+	switch (which) {
+	case CGPU_CIDR_V4_DYN: {
+		auto it = key ? c->dyn4.upper_bound(lpm_canon<4>(std::min<uint32_t>(key->prefixlen, 32), key->addr))
+			      : c->dyn4.begin();
+		if (it == c->dyn4.end()) return -ENOENT;
+		*next = it->second;
+		return 0;
+	}
+	case CGPU_CIDR_V6_DYN: {
+		auto it = key ? c->dyn6.upper_bound(lpm_canon<16>(std::min<uint32_t>(key->prefixlen, 128), key->addr))
+			      : c->dyn6.begin();
+		if (it == c->dyn6.end()) return -ENOENT;
+		*next = it->second;
+		return 0;
+	}
+	case CGPU_CIDR_V4_FIX: {
+		std::array<uint8_t, 8> k{};
+		if (key) memcpy(k.data(), key, 8);
+		auto it = key ? c->fix4.upper_bound(k) : c->fix4.begin();
+		if (it == c->fix4.end()) return -ENOENT;
+		memcpy(next, it->data(), 8);
+		return 0;
+	}
+	case CGPU_CIDR_V6_FIX: {
+		std::array<uint8_t, 20> k{};
+		if (key) memcpy(k.data(), key, 20);
+		auto it = key ? c->fix6.upper_bound(k) : c->fix6.begin();
+		if (it == c->fix6.end()) return -ENOENT;
+		memcpy(next, it->data(), 20);
+		return 0;
+	}
+	}
+	return fail(-EINVAL, "bad cidr map %d", which);
+}
+
+CGPU_EXPORT int cgpu_endpoint_update(cgpu_ctx *c, const cgpu_endpoint_key *key, uint64_t flags)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::array<uint8_t, 20> k;
+	memcpy(k.data(), key, 20);
+	std::lock_guard<std::mutex> g(c->mu);
+	bool exists = c->lxc.count(k);
+	if (exists && flags == CGPU_NOEXIST) return fail(-EEXIST, "exists");
+	if (!exists && flags == CGPU_EXIST) return fail(-ENOENT, "missing");
+	if (!exists && c->lxc.size() >= c->cfg.endpoints_max) return fail(-E2BIG, "endpoint map full");
+	c->lxc.insert(k);
+	c->dirty |= 1u << G_EP;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_endpoint_delete(cgpu_ctx *c, const cgpu_endpoint_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::array<uint8_t, 20> k;
+	memcpy(k.data(), key, 20);
+	std::lock_guard<std::mutex> g(c->mu);
+	if (!c->lxc.erase(k))
+		return -ENOENT;
+	c->dirty |= 1u << G_EP;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_endpoint_lookup(cgpu_ctx *c, const cgpu_endpoint_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::array<uint8_t, 20> k;
+	memcpy(k.data(), key, 20);
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lxc.count(k) ? 0 : -ENOENT;
+}
+
+/* per-endpoint identity of the endpoint program (lib/lxc.h:31-89) */
+CGPU_EXPORT int cgpu_lxc_update(cgpu_ctx *c, uint32_t ep, const cgpu_lxc_info *info)
+{
+	if (!c || !info)
+		return fail(-EINVAL, "null argument");
+	if (ep >= 65536u)
+		return fail(-EINVAL, "endpoint id beyond the u16 ep column");
+	if (info->verify & ~(CGPU_VERIFY_SMAC | CGPU_VERIFY_DMAC | CGPU_VERIFY_SIP))
+		return fail(-EINVAL, "unknown verify bits");
+	std::lock_guard<std::mutex> g(c->mu);
+	c->lxcinfo[ep] = *info;
+	c->dirty |= 1u << G_LXC;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lxc_delete(cgpu_ctx *c, uint32_t ep)
 {
 	if (!c)
 		return fail(-EINVAL, "null argument");
 	std::lock_guard<std::mutex> g(c->mu);
-	if (c->device < 0)
-		return fail(-ENODEV, "context has no device");
+	if (!c->lxcinfo.erase(ep))
+		return -ENOENT;
+	c->dirty |= 1u << G_LXC;
+	return 0;
+}
 
-	Dir248 ipc4, pf4;
-	PolBuild pol;
-	Set4Build ep4;
-	Set16Build ep6;
-	V6Build ipc6;
+CGPU_EXPORT int cgpu_lxc_lookup(cgpu_ctx *c, uint32_t ep, cgpu_lxc_info *out)
+{
+	if (!c || !out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = c->lxcinfo.find(ep);
+	if (it == c->lxcinfo.end())
+		return -ENOENT;
+	*out = it->second;
+	return 0;
+}
+
+/* ======================================================================= */
+/* service map (pkg/maps/lbmap; bpf(2) htab semantics, whole-key compare)    */
+/* ======================================================================= */
+static inline uint64_t lb_mkey(const cgpu_lb4_key *k)
+{
+	return (uint64_t)k->address << 32 | (uint64_t)k->dport << 16 | k->slave;
+}
+
+static inline cgpu_lb4_key lb_unkey(uint64_t m)
+{
+	cgpu_lb4_key k;
+	k.address = (uint32_t)(m >> 32);
+	k.dport = (uint16_t)(m >> 16);
+	k.slave = (uint16_t)m;
+	return k;
+}
+
+static int lb_put(cgpu_ctx *c, const cgpu_lb4_key *key, const cgpu_lb4_service *val, uint64_t flags)
+{
+	const uint64_t m = lb_mkey(key);
+	auto it = c->lb.find(m);
+	if (it == c->lb.end()) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "lb4 key not present");
+		if (c->lb.size() >= c->cfg.lb_max_entries)
+			return fail(-E2BIG, "lb4 service map full (%u)", c->cfg.lb_max_entries);
+		c->lb.emplace(m, *val);
+	} else {
+		if (flags == CGPU_NOEXIST)
+			return fail(-EEXIST, "lb4 key exists");
+		it->second = *val;
+	}
+	c->dirty |= 1u << G_LB;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_update(cgpu_ctx *c, const cgpu_lb4_key *key, const cgpu_lb4_service *val,
+				uint64_t flags)
+{
+	if (!c || !key || !val)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	return lb_put(c, key, val, flags);
+}
+
+CGPU_EXPORT int cgpu_lb4_update_batch(cgpu_ctx *c, const cgpu_lb4_key *keys,
+				      const cgpu_lb4_service *vals, size_t n, uint64_t flags)
+{
+	if (!c || (n && (!keys || !vals)))
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	for (size_t i = 0; i < n; i++)
+		if (int r = lb_put(c, &keys[i], &vals[i], flags))
+			return r;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_delete(cgpu_ctx *c, const cgpu_lb4_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (!c->lb.erase(lb_mkey(key)))
+		return -ENOENT;
+	c->dirty |= 1u << G_LB;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_lookup(cgpu_ctx *c, const cgpu_lb4_key *key, cgpu_lb4_service *out)
+{
+	if (!c || !key || !out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = c->lb.find(lb_mkey(key));
+	if (it == c->lb.end())
+		return -ENOENT;
+	*out = it->second;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb4_get_next_key(cgpu_ctx *c, const cgpu_lb4_key *key, cgpu_lb4_key *next)
+{
+	if (!c || !next)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = key ? c->lb.upper_bound(lb_mkey(key)) : c->lb.begin();
+	if (it == c->lb.end())
+		return -ENOENT;
+	*next = lb_unkey(it->first);
+	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_lb4_count(cgpu_ctx *c)
+{
+	if (!c)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lb.size();
+}
+
+CGPU_EXPORT uint32_t cgpu_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
+				    uint8_t proto)
+{
+	return flow_hash(saddr, daddr, sport, dport, proto);
+}
+
+
+/* ======================================================================= */
+/* commit: capture (mirror lock) -> compile (no lock) -> upload -> publish   */
+/* ======================================================================= */
+namespace {
+
+struct PolChange {
+	uint32_t ep;
+	uint64_t key;
+	bool present;
+	PolEntry e;
+};
+
+/* everything a commit compiles, copied out of the mirror under mu */
+struct CommitIn {
+	uint64_t id = 0;
+	uint32_t dirty = 0;
+	cgpu_config cfg{};
+	/* ipcache */
+	bool ipc4_full = false, ipc6_build = false;
+	std::vector<Rank4> ipc4_cand;
+	std::vector<Ipc4Patch> ipc4_patches;
+	std::vector<Rank6> ipc6_cand;
+	/* policy */
+	bool pol_full = false;
+	std::vector<PolKey> pol_keys;
+	std::vector<PolChange> pol_changes;
+	uint32_t next_hot = 0, next_cold = 0;
+	std::vector<SlotInit> inits;
+	/* other groups (full copies when dirty) */
+	PfIn pf{};
+	std::vector<std::array<uint8_t, 20>> lxc;
+	LbIn lb;
+	std::vector<std::pair<uint32_t, cgpu_lxc_info>> lxcinfo;
+	uint64_t sum_ipc = 0, sum_pol = 0;
+};
+
+static uint8_t key_dir(uint64_t key) { return ((key >> 56) & 1u) ? 2 : 1; }
+
+static PolKey pol_key_of(uint32_t ep, uint64_t key, const PolEntry &e)
+{
+	return PolKey{(uint32_t)key, (uint32_t)(key >> 32), ep | (uint32_t)e.proxy_port << 16, e.slot};
+}
+
+/* every candidate of one family, in map order (static-part entries first) */
+template <typename R, typename F>
+static void ipc_family(const cgpu_ctx *c, const uint8_t *stat, std::vector<R> &out, F cand)
+{
+	uint8_t d[20] = {0};
+	memcpy(d, stat, 4);
+	for (uint32_t p = 0; p < 32; p++) {
+		auto it = c->ipc.find(lpm_canon<20>(p, d));
+		R r;
+		if (it != c->ipc.end() && cand(it->second, it->first, &r))
+			out.push_back(r);
+	}
+	LpmKey<20> lo = lpm_canon<20>(0, d);
+	lo.data = {};
+	memcpy(lo.data.data(), stat, 4);
+	LpmKey<20> hi = lo;
+	hi.data[3]++;
+	for (auto it = c->ipc.lower_bound(lo); it != c->ipc.end() && it->first < hi; ++it) {
+		R r;
+		if (it->second.raw.prefixlen >= 32 && cand(it->second, it->first, &r))
+			out.push_back(r);
+	}
+}
+
+static void capture_ipc(cgpu_ctx *c, CommitIn &in, const BuildState &b)
+{
+	auto c4 = [](const IpcEntry &e, const LpmKey<20> &, Rank4 *r) {
+		return ipc4_candidate(e.raw, e.val.sec_label, r);
+	};
+	auto c6 = [](const IpcEntry &e, const LpmKey<20> &k, Rank6 *r) {
+		return ipc6_candidate(e.raw, k.data.data(), e.val.sec_label, r);
+	};
+	in.ipc4_full = c->ipc_full || !b.ipc4_ok || b.lc.bloated();
+	in.ipc6_build = c->ipc_full || !b.ipc4_ok;
+	std::set<LpmKey<20>> seen;
+	for (const auto &k : c->ipc_changes) {
+		if (in.ipc4_full && in.ipc6_build)
+			break;
+		if (!seen.insert(k).second)
+			continue;
+		const uint8_t *d = k.data.data();
+		if (k.plen < 32) { /* a static-part entry: under every address */
+			if (prefix_eq(d, kStaticV4, k.plen))
+				in.ipc4_full = true;
+			if (prefix_eq(d, kStaticV6, k.plen))
+				in.ipc6_build = true;
+			continue;
+		}
+		if (!memcmp(d, kStaticV6, 4)) {
+			in.ipc6_build = true;
+			continue;
+		}
+		if (memcmp(d, kStaticV4, 4) || k.plen > 64 || in.ipc4_full)
+			continue; /* no IPv4 lookup reaches it */
+		Ipc4Patch pt;
+		pt.len = k.plen - 32;
+		uint32_t a;
+		memcpy(&a, d + 4, 4);
+		pt.addr = bswap32(a);
+		pt.has_cover = false;
+		pt.cover_label = 0;
+		for (int64_t l = (int64_t)pt.len - 1; l >= 0 && !pt.has_cover; l--) {
+			auto it = c->ipc.find(lpm_canon<20>(32 + (uint32_t)l, d));
+			if (it != c->ipc.end()) {
+				pt.has_cover = true;
+				pt.cover_label = it->second.val.sec_label;
+			}
+		}
+		for (int64_t p = 31; p >= 0 && !pt.has_cover; p--) {
+			auto it = c->ipc.find(lpm_canon<20>((uint32_t)p, d));
+			if (it != c->ipc.end() && prefix_eq(it->first.data.data(), kStaticV4, (uint32_t)p)) {
+				pt.has_cover = true;
+				pt.cover_label = it->second.val.sec_label;
+			}
+		}
+		/* every entry inside the range (this key included, if present) */
+		LpmKey<20> lo{};
+		lo.plen = 0;
+		memcpy(lo.data.data(), d, 8);
+		const uint32_t last = pt.len ? pt.addr + ((pt.len == 32 ? 1u : (1u << (32 - pt.len))) - 1u)
+					     : 0xFFFFFFFFu;
+		for (auto it = c->ipc.lower_bound(lo); it != c->ipc.end(); ++it) {
+			const uint8_t *e = it->first.data.data();
+			if (memcmp(e, kStaticV4, 4))
+				break;
+			uint32_t ea;
+			memcpy(&ea, e + 4, 4);
+			if (bswap32(ea) > last)
+				break;
+			Rank4 r;
+			if (it->first.plen >= k.plen && it->first.plen <= 64 &&
+			    ipc4_candidate(it->second.raw, it->second.val.sec_label, &r))
+				pt.subs.push_back(r);
+		}
+		in.ipc4_patches.push_back(std::move(pt));
+	}
+	if (in.ipc4_full) {
+		in.ipc4_patches.clear();
+		ipc_family<Rank4>(c, kStaticV4, in.ipc4_cand, c4);
+	}
+	if (in.ipc6_build)
+		ipc_family<Rank6>(c, kStaticV6, in.ipc6_cand, c6);
+	c->ipc_changes.clear();
+	c->ipc_full = false;
+}
+
+static void capture_pol(cgpu_ctx *c, CommitIn &in, const BuildState &b)
+{
+	in.pol_full = c->pol_full || !b.pol_ok;
+	if (!in.pol_full) {
+		std::set<std::pair<uint32_t, uint64_t>> seen;
+		for (auto &ch : c->pol_changes) {
+			if (!seen.insert(ch).second)
+				continue;
+			PolChange pc{ch.first, ch.second, false, PolEntry{0, 0, 0}};
+			auto &m = c->pol[ch.first];
+			auto it = m.find(ch.second);
+			if (it != m.end()) {
+				pc.present = true;
+				pc.e = it->second;
+			}
+			in.pol_changes.push_back(pc);
+		}
+		if (b.pol.count + in.pol_changes.size() > b.pol.slots.size() / 2)
+			in.pol_full = true; /* could pass 50 % load: grow */
+	}
+	if (in.pol_full) {
+		in.pol_changes.clear();
+		in.pol_keys.reserve(c->pol_total);
+		for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+			for (auto &kv : c->pol[ep])
+				in.pol_keys.push_back(pol_key_of(ep, kv.first, kv.second));
+	}
+	c->pol_changes.clear();
+	c->pol_full = false;
+}
+
+static void capture(cgpu_ctx *c, CommitIn &in, const BuildState &b)
+{
+	in.dirty = c->dirty;
+	in.cfg = c->cfg;
+	if (in.dirty & (1u << G_IPC))
+		capture_ipc(c, in, b);
+	if (in.dirty & (1u << G_POL))
+		capture_pol(c, in, b);
+	in.next_hot = c->next_hot;
+	in.next_cold = c->next_cold;
+	in.inits.swap(c->slot_inits);
+	if (in.dirty & (1u << G_PF)) {
+		in.pf.fix4 = c->cfg.prefilter_fix4;
+		in.pf.dyn4 = c->cfg.prefilter_dyn4;
+		in.pf.fix6 = c->cfg.prefilter_fix6;
+		in.pf.dyn6 = c->cfg.prefilter_dyn6;
+		for (auto &kv : c->dyn4) { /* canonical (masked) addresses */
+			cgpu_cidr_key k{};
+			k.prefixlen = kv.first.plen;
+			memcpy(k.addr, kv.first.data.data(), 4);
+			in.pf.dyn4k.push_back(k);
+		}
+		for (auto &kv : c->dyn6) {
+			cgpu_cidr_key k{};
+			k.prefixlen = kv.first.plen;
+			memcpy(k.addr, kv.first.data.data(), 16);
+			in.pf.dyn6k.push_back(k);
+		}
+		for (auto &x : c->fix4) {
+			cgpu_cidr_key k{};
+			memcpy(&k, x.data(), 8);
+			in.pf.fix4k.push_back(k);
+		}
+		for (auto &x : c->fix6) {
+			cgpu_cidr_key k{};
+			memcpy(&k, x.data(), 20);
+			in.pf.fix6k.push_back(k);
+		}
+	}
+	if (in.dirty & (1u << G_EP))
+		in.lxc.assign(c->lxc.begin(), c->lxc.end());
+	if (in.dirty & (1u << G_LB))
+		in.lb.assign(c->lb.begin(), c->lb.end());
+	if (in.dirty & (1u << G_LXC))
+		in.lxcinfo.assign(c->lxcinfo.begin(), c->lxcinfo.end());
+	in.sum_ipc = c->sum_ipc;
+	in.sum_pol = c->sum_pol;
+	c->dirty = 0;
+	in.id = ++c->captured;
+}
+
+/* a failed commit leaves its groups to be recompiled whole next time */
+static void uncapture(cgpu_ctx *c, const CommitIn &in)
+{
+	c->dirty |= in.dirty;
+	if (in.dirty & (1u << G_IPC)) {
+		c->ipc_full = true;
+		c->ipc_changes.clear();
+	}
+	if (in.dirty & (1u << G_POL)) {
+		c->pol_full = true;
+		c->pol_changes.clear();
+	}
+	c->slot_inits.insert(c->slot_inits.begin(), in.inits.begin(), in.inits.end());
+}
+
+static int upload(cgpu_ctx *c, const Arena &ar, DevBufP &out)
+{
+	auto b = std::make_shared<DevBuf>();
+	b->dev = c->device;
+	b->st = c->rstream;
+	b->bytes = ar.total ? ar.total : 256;
+	HIP_OR_EIO(hipMallocFromPoolAsync(&b->p, b->bytes, c->pool, c->ustream));
+	for (size_t i = 0; i < ar.parts.size(); i++)
+		if (ar.parts[i].second)
+			HIP_OR_EIO(hipMemcpyAsync((char *)b->p + ar.offs[i], ar.parts[i].first, ar.parts[i].second,
+						  hipMemcpyHostToDevice, c->ustream));
+	out = b;
+	return 0;
+}
+
+template <typename T> static const T *at(const DevBufP &b, size_t off)
+{
+	return reinterpret_cast<const T *>(static_cast<const char *>(b->p) + off);
+}
+
+/* group IPC: compressed ipcache v4 (+ DIR-24-8 leaves' vals) and v6 LPM */
+static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
+{
+	BuildState &b = c->b;
+	if (in.ipc4_full) {
+		build_dir(std::move(in.ipc4_cand), b.dir, false);
+		b.lc.build(b.dir.tbl24, b.dir.tbl8);
+		b.ipc4_ok = true;
+	} else {
+		for (auto &pt : in.ipc4_patches)
+			apply_ipc4_patch(pt, b.dir, b.lc);
+	}
+	if (in.ipc6_build) {
+		b.v6 = V6Build();
+		build_v6(std::move(in.ipc6_cand), b.v6);
+	}
+	Arena ar;
+	const size_t o_x = ar.add(b.lc.x16.data(), b.lc.x16.size() * 4);
+	const size_t o_d = ar.add(b.lc.d16.data(), b.lc.d16.size() * 4);
+	const size_t o_n = ar.add(b.lc.nodes.data(), b.lc.nodes.size() * 4);
+	const size_t o_c = ar.add(b.lc.dict.data(), b.lc.dict.size() * 4);
+	const size_t o_v = ar.add(b.dir.vals.data(), b.dir.vals.size() * 4);
+	size_t o6[4] = {0, 0, 0, 0};
+	if (b.v6.any) {
+		o6[0] = ar.add(b.v6.root.data(), b.v6.root.size() * 4);
+		o6[1] = ar.add(b.v6.masks.data(), b.v6.masks.size() * 4);
+		o6[2] = ar.add(b.v6.vals.data(), b.v6.vals.size() * 4);
+		o6[3] = ar.add(b.v6.set.slots.data(), b.v6.set.slots.size() * sizeof(set16_slot));
+	}
+	if (int r = upload(c, ar, buf))
+		return r;
+	s.ipc4c = lpm16c{at<uint32_t>(buf, o_d), at<uint32_t>(buf, o_n), at<uint32_t>(buf, o_v),
+			 at<uint32_t>(buf, o_x), at<uint32_t>(buf, o_c), (uint32_t)b.lc.nodes.size(),
+			 (uint32_t)b.lc.dict.size()};
+	s.ipc6 = v6_lpm{};
+	if (b.v6.any)
+		s.ipc6 = v6_lpm{at<uint2>(buf, o6[0]), at<uint32_t>(buf, o6[1]), at<uint32_t>(buf, o6[2]),
+				addr_set16{at<set16_slot>(buf, o6[3]), b.v6.set.mask, b.v6.set.max_probe},
+				(uint32_t)(b.v6.masks.size() / 4)};
+	b.sum[G_IPC] = in.sum_ipc;
+	return 0;
+}
+
+/* group POL: the policy hash + per-counter-slot direction */
+static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
+{
+	BuildState &b = c->b;
+	bool full = in.pol_full;
+	if (!full) {
+		for (auto &ch : in.pol_changes) {
+			const uint32_t lo = (uint32_t)ch.key, hi = (uint32_t)(ch.key >> 32);
+			b.pol.erase(lo, hi, ch.ep);
+			if (ch.present && !b.pol.insert(pol_key_of(ch.ep, ch.key, ch.e))) {
+				full = true; /* a full neighbourhood: rebuild from the mirror */
+				break;
+			}
+		}
+	}
+	if (full) {
+		if (in.pol_keys.empty() && !in.pol_full) {
+			std::lock_guard<std::mutex> g(c->mu);
+			for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+				for (auto &kv : c->pol[ep])
+					in.pol_keys.push_back(pol_key_of(ep, kv.first, kv.second));
+		}
+		b.pol.build(in.pol_keys);
+		b.slot_dir.assign(c->n_ctr_slots, 0);
+		for (auto &k : in.pol_keys)
+			b.slot_dir[k.slot] = key_dir((uint64_t)k.hi << 32 | k.lo);
+		b.pol_ok = true;
+	} else {
+		if (b.slot_dir.size() != c->n_ctr_slots)
+			b.slot_dir.assign(c->n_ctr_slots, 0);
+		for (auto &ch : in.pol_changes)
+			if (ch.present)
+				b.slot_dir[ch.e.slot] = key_dir(ch.key);
+	}
+	Arena ar;
+	const size_t o_p = ar.add(b.pol.slots.data(), b.pol.slots.size() * sizeof(pol_slot));
+	const size_t o_s = ar.add(b.slot_dir.data(), b.slot_dir.size());
+	if (int r = upload(c, ar, buf))
+		return r;
+	s.pol = pol_table{at<pol_slot>(buf, o_p), b.pol.mask, 0};
+	s.slot_dir = at<uint8_t>(buf, o_s);
+	b.sum[G_POL] = in.sum_pol;
+	return 0;
+}
+
+/* group PF: XDP prefilter any-match tables (v4 compressed like the ipcache,
+ * v6 interval cover) */
+static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
+{
+	std::vector<Rank4> c4 = pf4_candidates(in.pf);
+	const bool have4 = !c4.empty();
+	Dir248 d;
+	Lpm16cBuild lc;
+	if (have4) {
+		build_dir(std::move(c4), d, true);
+		lc.build(d.tbl24, d.tbl8);
+		d.tbl24.clear();
+		d.tbl24.shrink_to_fit();
+		d.tbl8.clear();
+		d.tbl8.shrink_to_fit();
+	}
 	Cover6Build pf6;
-	build_ipc4(c, ipc4);
-	build_ipc6(c, ipc6);
-	bool have_pf4 = build_pf4(c, pf4);
-	build_pol(c, pol);
+	build_cover6(pf6_candidates(in.pf), pf6);
+	Arena ar;
+	size_t o4[4] = {0, 0, 0, 0}, o6[4] = {0, 0, 0, 0};
+	if (have4) {
+		o4[0] = ar.add(lc.x16.data(), lc.x16.size() * 4);
+		o4[1] = ar.add(lc.d16.data(), lc.d16.size() * 4);
+		o4[2] = ar.add(lc.nodes.data(), lc.nodes.size() * 4);
+		o4[3] = ar.add(lc.dict.data(), lc.dict.size() * 4);
+	}
+	if (pf6.any) {
+		o6[0] = ar.add(pf6.root.data(), pf6.root.size() * 4);
+		o6[1] = ar.add(pf6.pool.data(), pf6.pool.size() * 4);
+		o6[2] = ar.add(pf6.h32.data(), pf6.h32.size() * 16);
+		o6[3] = ar.add(pf6.h64.data(), pf6.h64.size() * 32);
+	}
+	if (int r = upload(c, ar, buf))
+		return r;
+	s.pf4c = lpm16c{};
+	if (have4)
+		s.pf4c = lpm16c{at<uint32_t>(buf, o4[1]), at<uint32_t>(buf, o4[2]), nullptr, at<uint32_t>(buf, o4[0]),
+				at<uint32_t>(buf, o4[3]), (uint32_t)lc.nodes.size(), (uint32_t)lc.dict.size()};
+	s.pf6 = cover6{};
+	if (pf6.any)
+		s.pf6 = cover6{at<uint32_t>(buf, o6[0]), at<uint32_t>(buf, o6[1]), at<uint4>(buf, o6[2]),
+			       at<uint4>(buf, o6[3]), pf6.m32, pf6.m64};
+	uint64_t sum = 0;
+	for (auto &k : in.pf.dyn4k) sum += fnv(7, &k, 8);
+	for (auto &k : in.pf.dyn6k) sum += fnv(11, &k, 20);
+	for (auto &k : in.pf.fix4k) sum += fnv(13, &k, 8);
+	for (auto &k : in.pf.fix6k) sum += fnv(17, &k, 20);
+	c->b.sum[G_PF] = sum;
+	return 0;
+}
+
+/* group EP: cilium_lxc endpoint sets */
+static int commit_ep(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
+{
 	std::vector<uint32_t> e4;
 	std::vector<std::array<uint32_t, 6>> e6;
-	for (auto &k : c->lxc) {
+	uint64_t sum = 0;
+	for (auto &k : in.lxc) {
+		sum += fnv(19, k.data(), k.size());
 		const cgpu_endpoint_key *ek = (const cgpu_endpoint_key *)k.data();
 		if (ek->pad4 || ek->pad5)
 			continue; /* lookup keys have zero padding: never matches */
@@ -1817,178 +2519,199 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 		else if (ek->family == 2)
 			e6.push_back({w[0], w[1], w[2], w[3], 0, 0});
 	}
+	Set4Build ep4;
+	Set16Build ep6;
 	build_set4(e4, ep4);
 	build_set16(e6, ep6);
-	build_pf6(c, pf6);
-	LbBuild lbb;
-	if (int r = build_lb(c, lbb))
-		return r;
-
 	Arena ar;
-	Lpm16cBuild ipc4c;
-	ipc4c.build(ipc4.tbl24, ipc4.tbl8);
-	size_t o_c16 = ar.add(ipc4c.d16.data(), ipc4c.d16.size() * 4);
-	size_t o_cn = ar.add(ipc4c.nodes.data(), ipc4c.nodes.size() * 4);
-	size_t o_cx = ar.add(ipc4c.x16.data(), ipc4c.x16.size() * 4);
-	size_t o_cd = ar.add(ipc4c.dict.data(), ipc4c.dict.size() * 4);
-	size_t o_t24 = ar.add(ipc4.tbl24.data(), ipc4.tbl24.size() * 4);
-	size_t o_t8 = ar.add(ipc4.tbl8.data(), ipc4.tbl8.size() * 4);
-	size_t o_v = ar.add(ipc4.vals.data(), ipc4.vals.size() * 4);
-	size_t o_pol = ar.add(pol.slots.data(), pol.slots.size() * sizeof(pol_slot));
-	size_t o_p24 = 0, o_p8 = 0;
-	if (have_pf4) {
-		o_p24 = ar.add(pf4.tbl24.data(), pf4.tbl24.size() * 4);
-		o_p8 = ar.add(pf4.tbl8.data(), pf4.tbl8.size() * 4);
-	}
-	size_t o_e4 = ar.add(ep4.slots.data(), ep4.slots.size() * sizeof(set4_slot));
-	size_t o_e6 = ar.add(ep6.slots.data(), ep6.slots.size() * sizeof(set16_slot));
-	struct V6Offs {
-		size_t root = 0, masks = 0, vals = 0, set = 0;
-	} o_ipc6;
-	auto add_v6 = [&](V6Build &v, V6Offs &o) {
-		if (!v.any)
-			return;
-		o.root = ar.add(v.root.data(), v.root.size() * 4);
-		o.masks = ar.add(v.masks.data(), v.masks.size() * 4);
-		o.vals = ar.add(v.vals.data(), v.vals.size() * 4);
-		o.set = ar.add(v.set.slots.data(), v.set.slots.size() * sizeof(set16_slot));
-	};
-	size_t o_c6r = 0, o_c6p = 0, o_c632 = 0, o_c664 = 0;
-	if (pf6.any) {
-		o_c6r = ar.add(pf6.root.data(), pf6.root.size() * 4);
-		o_c6p = ar.add(pf6.pool.data(), pf6.pool.size() * 4);
-		o_c632 = ar.add(pf6.h32.data(), pf6.h32.size() * 16);
-		o_c664 = ar.add(pf6.h64.data(), pf6.h64.size() * 32);
-	}
-	add_v6(ipc6, o_ipc6);
-	/* a slot freed and reused before this commit has several inits queued:
-	 * only the most recent one may reach the device (the init kernel writes
-	 * all of them in parallel) */
-	std::vector<uint32_t> init_slot;
-	std::vector<uint64_t> init_pk, init_by;
-	{
-		std::vector<uint8_t> seen(c->n_ctr_slots, 0);
-		for (auto s = c->slot_inits.rbegin(); s != c->slot_inits.rend(); ++s) {
-			if (seen[s->slot])
-				continue;
-			seen[s->slot] = 1;
-			init_slot.push_back(s->slot);
-			init_pk.push_back(s->packets);
-			init_by.push_back(s->bytes);
-		}
-	}
-	std::vector<uint8_t> slot_dir(c->n_ctr_slots, 0);
-	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
-		for (auto &kv : c->pol[ep])
-			slot_dir[kv.second.slot] = ((kv.first >> 56) & 1u) ? 2 : 1;
-	size_t o_sd = ar.add(slot_dir.data(), slot_dir.size());
-	size_t o_lfe = ar.add(lbb.fe.data(), lbb.fe.size() * 16);
-	size_t o_lbe = ar.add(lbb.be.data(), lbb.be.size() * 16);
-	size_t o_lvip = ar.add(lbb.vip.data(), lbb.vip.size() * 4);
-	size_t o_is = ar.add(init_slot.data(), init_slot.size() * 4);
-	size_t o_ip = ar.add(init_pk.data(), init_pk.size() * 8);
-	size_t o_ib = ar.add(init_by.data(), init_by.size() * 8);
-	/* dense per-endpoint lxc identity, 32 B each; absent endpoints verify nothing */
-	const uint32_t n_lxc = c->lxcinfo.empty() ? 0u : c->lxcinfo.rbegin()->first + 1u;
-	std::vector<cgpu_lxc_info> lxcv(n_lxc);
-	memset(lxcv.data(), 0, lxcv.size() * sizeof(cgpu_lxc_info));
-	for (auto &kv : c->lxcinfo)
-		lxcv[kv.first] = kv.second;
-	static_assert(sizeof(cgpu_lxc_info) == 32, "cgpu_lxc_info is 2 x uint4");
-	size_t o_lxc = ar.add(lxcv.data(), lxcv.size() * sizeof(cgpu_lxc_info));
+	const size_t o4 = ar.add(ep4.slots.data(), ep4.slots.size() * sizeof(set4_slot));
+	const size_t o6 = ar.add(ep6.slots.data(), ep6.slots.size() * sizeof(set16_slot));
+	if (int r = upload(c, ar, buf))
+		return r;
+	s.ep4 = addr_set4{at<set4_slot>(buf, o4), ep4.mask, ep4.max_probe};
+	s.ep6 = addr_set16{at<set16_slot>(buf, o6), ep6.mask, ep6.max_probe};
+	c->b.sum[G_EP] = sum;
+	return 0;
+}
 
-	HIP_OR_EIO(hipSetDevice(c->device));
-	/* launches on the previous snapshot must drain before it is freed */
-	HIP_OR_EIO(hipDeviceSynchronize());
-	char *arena = nullptr;
-	HIP_OR_EIO(hipMalloc((void **)&arena, ar.total ? ar.total : 256));
-	for (size_t i = 0; i < ar.parts.size(); i++)
-		if (ar.parts[i].second)
-			HIP_OR_EIO(hipMemcpy(arena + ar.offs[i], ar.parts[i].first, ar.parts[i].second,
-					     hipMemcpyHostToDevice));
-	if (!init_slot.empty()) {
-		HIP_OR_EIO(launch_slot_init(c->d_totals, c->d_delta, (const uint32_t *)(arena + o_is),
-					    (const uint64_t *)(arena + o_ip),
-					    (const uint64_t *)(arena + o_ib), (uint32_t)init_slot.size(),
-					    nullptr));
-	}
-	HIP_OR_EIO(hipDeviceSynchronize());
-	(void)hipFree(c->arena);
-	c->arena = arena;
-	c->slot_inits.clear();
-
-	cgpu_snapshot s{};
-	s.ipc4 = dir248{(const uint32_t *)(arena + o_t24), (const uint32_t *)(arena + o_t8),
-			(const uint32_t *)(arena + o_v), (uint32_t)(ipc4.tbl8.size() / 256),
-			(uint32_t)ipc4.vals.size()};
-	s.ipc4c = lpm16c{(const uint32_t *)(arena + o_c16), (const uint32_t *)(arena + o_cn),
-			 (const uint32_t *)(arena + o_v), (const uint32_t *)(arena + o_cx),
-			 (const uint32_t *)(arena + o_cd), (uint32_t)ipc4c.nodes.size(),
-			 (uint32_t)ipc4c.dict.size()};
-	s.pol = pol_table{(const pol_slot *)(arena + o_pol), pol.mask, pol.max_probe, pol.bpb, 0};
-	if (have_pf4)
-		s.pf4 = dir248{(const uint32_t *)(arena + o_p24), (const uint32_t *)(arena + o_p8),
-			       nullptr, (uint32_t)(pf4.tbl8.size() / 256), 0};
-	s.ep4 = addr_set4{(const set4_slot *)(arena + o_e4), ep4.mask, ep4.max_probe};
-	s.ep6 = addr_set16{(const set16_slot *)(arena + o_e6), ep6.mask, ep6.max_probe};
-	auto mk_v6 = [&](const V6Build &v, const V6Offs &o) {
-		v6_lpm t{};
-		if (v.any)
-			t = v6_lpm{(const uint2 *)(arena + o.root), (const uint32_t *)(arena + o.masks),
-				   (const uint32_t *)(arena + o.vals),
-				   addr_set16{(const set16_slot *)(arena + o.set), v.set.mask, v.set.max_probe},
-				   (uint32_t)(v.masks.size() / 4)};
-		return t;
-	};
-	if (pf6.any)
-		s.pf6 = cover6{(const uint32_t *)(arena + o_c6r), (const uint32_t *)(arena + o_c6p),
-			       (const uint4 *)(arena + o_c632), (const uint4 *)(arena + o_c664), pf6.m32, pf6.m64};
-	s.ipc6 = mk_v6(ipc6, o_ipc6);
-	memcpy(s.router_ip64, c->cfg.ipv6_router_ip, 8);
-	s.pf4_enabled = c->cfg.prefilter_fix4;
-	s.pf6_enabled = c->cfg.prefilter_fix6;
-	s.world_id = c->cfg.world_id;
-	s.cluster_id = c->cfg.cluster_id;
-	s.host_id = c->cfg.host_id;
-	s.health_id = c->cfg.health_id;
-	s.ipv4_cluster_mask = c->cfg.ipv4_cluster_mask;
-	s.ipv4_cluster_range = c->cfg.ipv4_cluster_range;
-	s.ct_proto_gate = c->cfg.ct_proto_gate;
-	s.ingress_secctx_world = c->cfg.ingress_secctx_world;
-	s.ingress_src_identity = c->cfg.ingress_src_identity;
-	s.n_ctr_slots = c->n_ctr_slots;
-	s.hot_slots = c->next_hot; /* LDS per workgroup: only the hot slots in use */
-	s.cold_hi = c->next_cold;
-	s.slot_dir = (const uint8_t *)(arena + o_sd);
-	s.lb = lb_table{(const uint4 *)(arena + o_lfe), (const uint4 *)(arena + o_lbe), lbb.mask,
-			(uint32_t)lbb.be.size(), (const uint32_t *)(arena + o_lvip), lbb.vip_mask};
-	s.lb_flags = c->cfg.lb_flags;
-	s.ipv4_loopback = c->cfg.ipv4_loopback;
-	s.lxc = (const uint4 *)(arena + o_lxc);
-	s.n_lxc = n_lxc;
-	memcpy(&s.node_mac_lo, c->cfg.node_mac, 4);
-	s.node_mac_hi = (uint32_t)c->cfg.node_mac[4] | ((uint32_t)c->cfg.node_mac[5] << 8);
-	s.epoch = ++c->epoch;
-	c->snap = s;
-	c->committed = true;
-
-	/* content checksum: order-independent over the mirror */
+/* group LB: cilium_lb4_services frontends + backends */
+static int commit_lb(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
+{
+	LbBuild lbb;
+	if (int r = build_lb(in.lb, in.cfg.lb_max_entries, lbb))
+		return r;
+	Arena ar;
+	const size_t o_f = ar.add(lbb.fe.data(), lbb.fe.size() * 16);
+	const size_t o_b = ar.add(lbb.be.data(), lbb.be.size() * 16);
+	const size_t o_v = ar.add(lbb.vip.data(), lbb.vip.size() * 4);
+	if (int r = upload(c, ar, buf))
+		return r;
+	s.lb = lb_table{at<uint4>(buf, o_f), at<uint4>(buf, o_b), lbb.mask, (uint32_t)lbb.be.size(),
+			at<uint32_t>(buf, o_v), lbb.vip_mask};
 	uint64_t sum = 0;
-	for (auto &kv : c->ipc)
-		sum += fnv(fnv(1469598103934665603ull, &kv.first, sizeof(kv.first)), &kv.second.val, 8);
-	for (uint32_t ep = 0; ep < c->pol.size(); ep++)
-		for (auto &kv : c->pol[ep]) {
-			uint64_t h = fnv(1469598103934665603ull ^ ep, &kv.first, 8);
-			sum += fnv(h, &kv.second.proxy_port, 2) ^ ((uint64_t)kv.second.slot << 1);
+	for (auto &kv : in.lb)
+		sum += fnv(fnv(23, &kv.first, 8), &kv.second, sizeof(kv.second));
+	c->b.sum[G_LB] = sum;
+	return 0;
+}
+
+/* group LXC: dense per-endpoint lxc identity, 32 B each (absent: verify nothing) */
+static int commit_lxc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
+{
+	static_assert(sizeof(cgpu_lxc_info) == 32, "cgpu_lxc_info is 2 x uint4");
+	const uint32_t n = in.lxcinfo.empty() ? 0u : in.lxcinfo.back().first + 1u;
+	std::vector<cgpu_lxc_info> v(n);
+	if (n)
+		memset(v.data(), 0, v.size() * sizeof(cgpu_lxc_info));
+	uint64_t sum = 0;
+	for (auto &kv : in.lxcinfo) {
+		v[kv.first] = kv.second;
+		sum += fnv(fnv(29, &kv.first, 4), &kv.second, sizeof(kv.second));
+	}
+	Arena ar;
+	const size_t o = ar.add(v.data(), v.size() * sizeof(cgpu_lxc_info));
+	if (int r = upload(c, ar, buf))
+		return r;
+	s.lxc = at<uint4>(buf, o);
+	s.n_lxc = n;
+	c->b.sum[G_LXC] = sum;
+	return 0;
+}
+
+/* counter slots whose entry was (re)written: their totals restart from the
+ * supplied packets/bytes (kernel htab update replaces the value); the newest
+ * write of a slot wins */
+static int commit_inits(cgpu_ctx *c, const CommitIn &in)
+{
+	if (in.inits.empty())
+		return 0;
+	std::vector<uint32_t> slot;
+	std::vector<uint64_t> pk, by;
+	std::vector<uint8_t> seen(c->n_ctr_slots, 0);
+	for (auto it = in.inits.rbegin(); it != in.inits.rend(); ++it) {
+		if (seen[it->slot])
+			continue;
+		seen[it->slot] = 1;
+		slot.push_back(it->slot);
+		pk.push_back(it->packets);
+		by.push_back(it->bytes);
+	}
+	Arena ar;
+	const size_t o_s = ar.add(slot.data(), slot.size() * 4);
+	const size_t o_p = ar.add(pk.data(), pk.size() * 8);
+	const size_t o_b = ar.add(by.data(), by.size() * 8);
+	DevBufP buf;
+	if (int r = upload(c, ar, buf))
+		return r;
+	HIP_OR_EIO(launch_slot_init(c->d_totals, c->d_delta, at<uint32_t>(buf, o_s), at<uint64_t>(buf, o_p),
+				    at<uint64_t>(buf, o_b), (uint32_t)slot.size(), c->ustream));
+	/* the scratch buffer's free (on rstream) must follow the init kernel */
+	hipEvent_t ev;
+	HIP_OR_EIO(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+	(void)hipEventRecord(ev, c->ustream);
+	(void)hipStreamWaitEvent(c->rstream, ev, 0);
+	(void)hipEventDestroy(ev);
+	return 0;
+}
+
+} // namespace
+
+CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
+{
+	if (!c)
+		return fail(-EINVAL, "null argument");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	std::lock_guard<std::mutex> cg(c->commit_mu);
+	CommitIn in;
+	{
+		std::lock_guard<std::mutex> g(c->mu);
+		capture(c, in, c->b);
+	}
+	HIP_OR_EIO(hipSetDevice(c->device));
+	std::shared_ptr<Epoch> prev;
+	{
+		std::lock_guard<std::mutex> g(c->pub_mu);
+		prev = c->cur;
+	}
+	auto e = std::make_shared<Epoch>();
+	e->c = c;
+	e->id = in.id;
+	if (prev) {
+		e->snap = prev->snap;
+		for (int k = 0; k < G_N; k++)
+			e->bufs[k] = prev->bufs[k];
+	}
+	cgpu_snapshot &s = e->snap;
+	int (*const step[G_N])(cgpu_ctx *, CommitIn &, cgpu_snapshot &, DevBufP &) = {
+		commit_ipc, commit_pol, commit_pf, commit_ep, commit_lb, commit_lxc};
+	int rc = 0;
+	for (int k = 0; k < G_N && !rc; k++)
+		if (in.dirty & (1u << k)) {
+			rc = step[k](c, in, s, e->bufs[k]);
+			/* a host image half-patched by a failed step is rebuilt */
+			if (rc && k == G_IPC)
+				c->b.ipc4_ok = false;
+			if (rc && k == G_POL)
+				c->b.pol_ok = false;
 		}
-	for (auto &kv : c->dyn4) sum += fnv(7, &kv.first, sizeof(kv.first));
-	for (auto &kv : c->dyn6) sum += fnv(11, &kv.first, sizeof(kv.first));
-	for (auto &k : c->fix4) sum += fnv(13, k.data(), k.size());
-	for (auto &k : c->fix6) sum += fnv(17, k.data(), k.size());
-	for (auto &k : c->lxc) sum += fnv(19, k.data(), k.size());
-	for (auto &kv : c->lb) sum += fnv(fnv(23, &kv.first, 8), &kv.second, sizeof(kv.second));
-	for (auto &kv : c->lxcinfo) sum += fnv(fnv(29, &kv.first, 4), &kv.second, sizeof(kv.second));
-	c->checksum = sum;
+	if (!rc)
+		rc = commit_inits(c, in);
+	hipError_t he = hipSuccess;
+	if (!rc && ((he = hipEventCreateWithFlags(&e->ready, hipEventDisableTiming)) != hipSuccess ||
+		    (he = hipEventRecord(e->ready, c->ustream)) != hipSuccess ||
+		    (he = hipEventSynchronize(e->ready)) != hipSuccess))
+		rc = fail(-EIO, "commit upload: %s", hipGetErrorString(he));
+	if (rc) {
+		std::string msg = g_last_error;
+		{
+			std::lock_guard<std::mutex> g(c->mu);
+			uncapture(c, in);
+		}
+		{
+			std::lock_guard<std::mutex> g(c->retire_mu);
+			c->alive.insert(e->id); /* its destructor retires the id */
+		}
+		e.reset();
+		g_last_error = msg;
+		return rc;
+	}
+	const cgpu_config &cf = in.cfg;
+	memcpy(s.router_ip64, cf.ipv6_router_ip, 8);
+	s.pf4_enabled = cf.prefilter_fix4;
+	s.pf6_enabled = cf.prefilter_fix6;
+	s.world_id = cf.world_id;
+	s.cluster_id = cf.cluster_id;
+	s.host_id = cf.host_id;
+	s.health_id = cf.health_id;
+	s.ipv4_cluster_mask = cf.ipv4_cluster_mask;
+	s.ipv4_cluster_range = cf.ipv4_cluster_range;
+	s.ct_proto_gate = cf.ct_proto_gate;
+	s.ingress_secctx_world = cf.ingress_secctx_world;
+	s.ingress_src_identity = cf.ingress_src_identity;
+	s.n_ctr_slots = c->n_ctr_slots;
+	s.hot_slots = in.next_hot; /* LDS per workgroup: only the hot slots in use */
+	s.cold_hi = in.next_cold;
+	s.lb_flags = cf.lb_flags;
+	s.ipv4_loopback = cf.ipv4_loopback;
+	memcpy(&s.node_mac_lo, cf.node_mac, 4);
+	s.node_mac_hi = (uint32_t)cf.node_mac[4] | ((uint32_t)cf.node_mac[5] << 8);
+	s.epoch = e->id;
+	uint64_t sum = 0;
+	for (int k = 0; k < G_N; k++)
+		sum += c->b.sum[k];
+	{
+		std::lock_guard<std::mutex> g(c->retire_mu);
+		c->alive.insert(e->id);
+	}
+	{
+		std::lock_guard<std::mutex> g(c->pub_mu);
+		c->cur.swap(e); /* e now holds the previous snapshot */
+		c->epoch = s.epoch;
+		c->checksum = sum;
+	}
+	e.reset();
+	prev.reset(); /* the last reference retires it (waits + frees on rstream) */
 	if (epoch_out)
 		*epoch_out = s.epoch;
 	return 0;
@@ -1998,8 +2721,8 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
 {
 	if (!c || !sum)
 		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	if (!c->committed)
+	std::lock_guard<std::mutex> g(c->pub_mu);
+	if (!c->cur)
 		return fail(-ENOENT, "nothing committed");
 	*sum = c->checksum;
 	return 0;
@@ -2008,32 +2731,62 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
 /* ======================================================================= */
 /* batch entry points                                                        */
 /* ======================================================================= */
-static int snapshot_for_launch(cgpu_ctx *c, cgpu_snapshot &s, uint64_t *&delta,
-			       void *stream = nullptr, uint64_t **pk = nullptr)
+/* A launch pins the published snapshot for as long as it enqueues: the
+ * stream first waits for the snapshot's uploads, and afterwards an event
+ * recorded on it tells the snapshot's retirement when these kernels end.
+ * Launches never take the mirror lock, so commits (and table updates) do
+ * not block them. */
+struct Pinned {
+	std::shared_ptr<Epoch> ep;
+	hipStream_t st = nullptr;
+	uint64_t *delta = nullptr, *pk = nullptr;
+	const cgpu_snapshot &snap() const { return ep->snap; }
+	~Pinned()
+	{
+		if (!ep)
+			return;
+		std::lock_guard<std::mutex> g(ep->mu);
+		hipEvent_t ev = nullptr;
+		for (auto &u : ep->used)
+			if (u.first == st)
+				ev = u.second;
+		if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess)
+			ep->used.push_back({st, ev});
+		if (ev)
+			(void)hipEventRecord(ev, st);
+	}
+};
+
+static int pin(cgpu_ctx *c, void *stream, Pinned &p, bool want_pk = false)
 {
 	if (!c)
 		return fail(-EINVAL, "null context");
-	std::lock_guard<std::mutex> g(c->mu);
 	if (c->device < 0)
 		return fail(-ENODEV, "context has no device (host-only); no CPU classification path");
-	if (!c->committed)
+	{
+		std::lock_guard<std::mutex> g(c->pub_mu);
+		p.ep = c->cur;
+	}
+	if (!p.ep)
 		return fail(-ENOENT, "no committed snapshot (call cgpu_commit)");
-	s = c->snap;
-	delta = c->d_delta;
-	if (pk) {
+	p.st = (hipStream_t)stream;
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipStreamWaitEvent(p.st, p.ep->ready, 0));
+	std::lock_guard<std::mutex> g(c->pk_mu);
+	p.delta = c->d_delta;
+	if (want_pk) {
 		auto it = c->d_pk.find(stream);
 		if (it == c->d_pk.end()) {
-			uint64_t *p = nullptr;
+			uint64_t *b = nullptr;
 			const size_t bytes = (size_t)c->n_ctr_slots * 8;
-			HIP_OR_EIO(hipSetDevice(c->device));
-			HIP_OR_EIO(hipMalloc((void **)&p, bytes));
-			if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-				(void)hipFree(p);
+			HIP_OR_EIO(hipMalloc((void **)&b, bytes));
+			if (hipMemsetAsync(b, 0, bytes, p.st) != hipSuccess) {
+				(void)hipFree(b);
 				return fail(-EIO, "packed counter buffer init failed");
 			}
-			it = c->d_pk.emplace(stream, p).first;
+			it = c->d_pk.emplace(stream, b).first;
 		}
-		*pk = it->second;
+		p.pk = it->second;
 	}
 	return 0;
 }
@@ -2041,10 +2794,11 @@ static int snapshot_for_launch(cgpu_ctx *c, cgpu_snapshot &s, uint64_t *&delta,
 CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
 				 uint32_t *identity, uint8_t *stage, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta, *pk = nullptr;
-	if (int r = snapshot_for_launch(c, s, delta, stream, &pk))
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
 		return r;
+	const cgpu_snapshot &s = P.snap();
+	uint64_t *delta = P.delta, *pk = P.pk;
 	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
 			 !t->ep || !verdict || !identity)))
 		return fail(-EINVAL, "null tuple column or output");
@@ -2061,10 +2815,11 @@ CGPU_EXPORT int cgpu_classify_v4_lb(cgpu_ctx *c, const cgpu_tuples_v4 *t, const 
 				    const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
 				    uint8_t *stage, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta, *pk = nullptr;
-	if (int r = snapshot_for_launch(c, s, delta, stream, &pk))
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
 		return r;
+	const cgpu_snapshot &s = P.snap();
+	uint64_t *delta = P.delta, *pk = P.pk;
 	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
 			 !t->ep || !verdict || !identity)))
 		return fail(-EINVAL, "null tuple column or output");
@@ -2085,10 +2840,10 @@ CGPU_EXPORT int cgpu_classify_v4_lb(cgpu_ctx *c, const cgpu_tuples_v4 *t, const 
 CGPU_EXPORT int cgpu_lb4_select(cgpu_ctx *c, int mode, const cgpu_lb4_tuples *t, size_t n,
 				const cgpu_lb4_out *out, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	Pinned P;
+	if (int r = pin(c, stream, P))
 		return r;
+	const cgpu_snapshot &s = P.snap();
 	if (mode != CGPU_LB_NETDEV && mode != CGPU_LB_LXC)
 		return fail(-EINVAL, "bad lb mode %d", mode);
 	if (!t || !out || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !out->ret)))
@@ -2107,10 +2862,11 @@ CGPU_EXPORT int cgpu_lb4_select(cgpu_ctx *c, int mode, const cgpu_lb4_tuples *t,
 CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n, int32_t *verdict,
 				 uint32_t *identity, uint8_t *stage, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	Pinned P;
+	if (int r = pin(c, stream, P))
 		return r;
+	const cgpu_snapshot &s = P.snap();
+	uint64_t *delta = P.delta;
 	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
 			 !t->ep || !verdict || !identity)))
 		return fail(-EINVAL, "null tuple column or output");
@@ -2139,10 +2895,10 @@ static int frames_check(cgpu_ctx *c, const cgpu_frames *f, size_t n)
 CGPU_EXPORT int cgpu_frames_parse(cgpu_ctx *c, const cgpu_frames *f, size_t n,
 				  const cgpu_frame_tuples *o, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	Pinned P;
+	if (int r = pin(c, stream, P))
 		return r;
+	const cgpu_snapshot &s = P.snap();
 	if (int r = frames_check(c, f, n))
 		return r;
 	if (!o || (n && !o->status))
@@ -2160,10 +2916,11 @@ CGPU_EXPORT int cgpu_frames_parse(cgpu_ctx *c, const cgpu_frames *f, size_t n,
 CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n, int32_t *verdict,
 				     uint32_t *identity, uint8_t *stage, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	Pinned P;
+	if (int r = pin(c, stream, P))
 		return r;
+	const cgpu_snapshot &s = P.snap();
+	uint64_t *delta = P.delta;
 	if (int r = frames_check(c, f, n))
 		return r;
 	if (n && (!verdict || !identity))
@@ -2181,10 +2938,10 @@ CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n
 CGPU_EXPORT int cgpu_prefilter_v4(cgpu_ctx *c, const uint32_t *saddr, const uint32_t *daddr,
 				  const uint8_t *flags, size_t n, uint8_t *verdict, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	Pinned P;
+	if (int r = pin(c, stream, P))
 		return r;
+	const cgpu_snapshot &s = P.snap();
 	if (n && (!saddr || !daddr || !flags || !verdict))
 		return fail(-EINVAL, "null column");
 	if (!n)
@@ -2198,10 +2955,10 @@ CGPU_EXPORT int cgpu_prefilter_v4(cgpu_ctx *c, const uint32_t *saddr, const uint
 CGPU_EXPORT int cgpu_prefilter_v6(cgpu_ctx *c, const uint8_t *saddr, const uint8_t *daddr,
 				  const uint8_t *flags, size_t n, uint8_t *verdict, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	Pinned P;
+	if (int r = pin(c, stream, P))
 		return r;
+	const cgpu_snapshot &s = P.snap();
 	if (n && (!saddr || !daddr || !flags || !verdict))
 		return fail(-EINVAL, "null column");
 	if (((uintptr_t)saddr | (uintptr_t)daddr) & 15)
@@ -2228,7 +2985,7 @@ CGPU_EXPORT int cgpu_counter_bind(cgpu_ctx *c, void *buf, size_t bytes)
 		return fail(-EINVAL, "null context");
 	if (c->device < 0)
 		return fail(-ENODEV, "context has no device");
-	std::lock_guard<std::mutex> g(c->mu);
+	std::lock_guard<std::mutex> g(c->pk_mu);
 	if (!buf) {
 		c->d_delta = c->d_delta_own;
 		return 0;
@@ -2278,6 +3035,187 @@ CGPU_EXPORT int cgpu_counters_reset(cgpu_ctx *c)
 	for (auto &kv : c->d_pk)
 		HIP_OR_EIO(hipMemset(kv.second, 0, (size_t)c->n_ctr_slots * 8));
 	HIP_OR_EIO(hipDeviceSynchronize());
+	return 0;
+}
+
+/* ======================================================================= */
+/* batched map writes and counter reads (the same per-key semantics)         */
+/* ======================================================================= */
+CGPU_EXPORT int cgpu_ipcache_update_batch(cgpu_ctx *c, const cgpu_ipcache_key *keys,
+					  const cgpu_remote_endpoint_info *vals, size_t n, uint64_t flags)
+{
+	if (!c || (n && (!keys || !vals)))
+		return fail(-EINVAL, "null argument");
+	for (size_t i = 0; i < n; i++)
+		if (int r = cgpu_ipcache_update(c, &keys[i], &vals[i], flags))
+			return r;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_update_batch(cgpu_ctx *c, const uint32_t *eps, const cgpu_policy_key *keys,
+					 const cgpu_policy_entry *entries, size_t n, uint64_t flags)
+{
+	if (!c || (n && (!eps || !keys || !entries)))
+		return fail(-EINVAL, "null argument");
+	for (size_t i = 0; i < n; i++)
+		if (int r = cgpu_policy_update(c, eps[i], &keys[i], &entries[i], flags))
+			return r;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_cidr_update_batch(cgpu_ctx *c, int which, const cgpu_cidr_key *keys, size_t n,
+				       uint64_t flags)
+{
+	if (!c || (n && !keys))
+		return fail(-EINVAL, "null argument");
+	for (size_t i = 0; i < n; i++)
+		if (int r = cgpu_cidr_update(c, which, &keys[i], flags))
+			return r;
+	return 0;
+}
+
+/* entries of n (ep, key) pairs with ONE read of the device counters */
+static int policy_fill(cgpu_ctx *c, const std::vector<std::pair<const PolEntry *, size_t>> &hit,
+		       cgpu_policy_entry *out)
+{
+	std::vector<uint64_t> w;
+	const bool dev = c->device >= 0 && c->captured;
+	if (dev && !hit.empty()) {
+		w.resize((size_t)2 * c->n_ctr_slots);
+		if (int r = read_counter_words(c, 0, w.size(), w.data()))
+			return r;
+	}
+	std::unordered_map<uint32_t, const SlotInit *> pending;
+	for (auto &s : c->slot_inits)
+		pending[s.slot] = &s; /* the most recent write of a slot wins */
+	for (auto &h : hit) {
+		cgpu_policy_entry &o = out[h.second];
+		memset(&o, 0, sizeof(o));
+		o.proxy_port = h.first->proxy_port;
+		auto it = pending.find(h.first->slot);
+		if (it != pending.end()) {
+			o.packets = it->second->packets;
+			o.bytes = it->second->bytes;
+		} else if (dev) {
+			o.packets = w[2u * h.first->slot];
+			o.bytes = w[2u * h.first->slot + 1u];
+		}
+	}
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_lookup_batch(cgpu_ctx *c, const uint32_t *eps, const cgpu_policy_key *keys,
+					 size_t n, cgpu_policy_entry *out, int32_t *rc_out)
+{
+	if (!c || (n && (!eps || !keys || !out || !rc_out)))
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	std::vector<std::pair<const PolEntry *, size_t>> hit;
+	for (size_t i = 0; i < n; i++) {
+		rc_out[i] = -ENOENT;
+		if (eps[i] >= c->cfg.max_endpoints) {
+			rc_out[i] = -EINVAL;
+			continue;
+		}
+		auto &m = c->pol[eps[i]];
+		auto it = m.find(pol_key64(&keys[i]));
+		if (it != m.end()) {
+			rc_out[i] = 0;
+			hit.push_back({&it->second, i});
+		} else {
+			memset(&out[i], 0, sizeof(out[i]));
+		}
+	}
+	return policy_fill(c, hit, out);
+}
+
+CGPU_EXPORT int cgpu_policy_dump(cgpu_ctx *c, uint32_t ep, cgpu_policy_key *keys, cgpu_policy_entry *entries,
+				 size_t cap, size_t *n_out)
+{
+	if (!c || !n_out || (cap && (!keys || !entries)) || ep >= (c ? c->cfg.max_endpoints : 0))
+		return fail(-EINVAL, "bad argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto &m = c->pol[ep];
+	*n_out = m.size();
+	if (m.size() > cap)
+		return fail(-ENOSPC, "policy map of ep %u holds %zu keys > %zu", ep, m.size(), cap);
+	std::vector<std::pair<const PolEntry *, size_t>> hit;
+	size_t i = 0;
+	for (auto &kv : m) {
+		memcpy(&keys[i], &kv.first, 8);
+		hit.push_back({&kv.second, i});
+		i++;
+	}
+	return policy_fill(c, hit, entries);
+}
+
+/* ======================================================================= */
+/* multi-GPU counter reduction: RCCL over xGMI                  */
+/* ======================================================================= */
+static_assert(CGPU_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "ncclUniqueId size");
+
+static void comm_destroy(cgpu_ctx *c)
+{
+	if (c->comm) {
+		(void)ncclCommDestroy((ncclComm_t)c->comm);
+		c->comm = nullptr;
+	}
+}
+
+CGPU_EXPORT int cgpu_comm_id_create(uint8_t *id_out)
+{
+	if (!id_out)
+		return fail(-EINVAL, "null argument");
+	ncclUniqueId id;
+	const ncclResult_t r = ncclGetUniqueId(&id);
+	if (r != ncclSuccess)
+		return fail(-EIO, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+	memcpy(id_out, &id, sizeof(id));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_comm_init(cgpu_ctx *c, const uint8_t *id, int nranks, int rank)
+{
+	if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks)
+		return fail(-EINVAL, "bad argument");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	std::lock_guard<std::mutex> g(c->pk_mu);
+	if (c->comm)
+		return fail(-EEXIST, "context already has a communicator");
+	ncclUniqueId uid;
+	memcpy(&uid, id, sizeof(uid));
+	HIP_OR_EIO(hipSetDevice(c->device));
+	ncclComm_t comm = nullptr;
+	const ncclResult_t r = ncclCommInitRank(&comm, nranks, uid, rank);
+	if (r != ncclSuccess)
+		return fail(-EIO, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
+	c->comm = comm;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_counters_allreduce(cgpu_ctx *c, void *stream)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	uint64_t *delta;
+	void *comm;
+	{
+		std::lock_guard<std::mutex> g(c->pk_mu);
+		delta = c->d_delta;
+		comm = c->comm;
+	}
+	if (!comm)
+		return fail(-ENOENT, "no communicator (cgpu_comm_init)");
+	HIP_OR_EIO(hipSetDevice(c->device));
+	const size_t words = (size_t)2 * c->n_ctr_slots + CGPU_METRICS_WORDS;
+	/* u64 SUM: order-independent, so every rank ends with the same bits */
+	const ncclResult_t r = ncclAllReduce(delta, delta, words, ncclUint64, ncclSum, (ncclComm_t)comm,
+					     (hipStream_t)stream);
+	if (r != ncclSuccess)
+		return fail(-EIO, "ncclAllReduce: %s", ncclGetErrorString(r));
 	return 0;
 }
 
@@ -2596,10 +3534,11 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 				    int32_t *verdict, uint8_t *ct_ret, uint32_t *identity,
 				    uint8_t *stage, void *stream)
 {
-	cgpu_snapshot s;
-	uint64_t *delta;
-	if (int r = snapshot_for_launch(c, s, delta))
+	Pinned P;
+	if (int r = pin(c, stream, P))
 		return r;
+	const cgpu_snapshot &s = P.snap();
+	uint64_t *delta = P.delta;
 	if (!t || (n && (!t->saddr || !t->daddr || !t->sport || !t->dport || !t->proto || !t->l4 ||
 			 !t->flags || !t->len || !t->ep || !verdict || !ct_ret || !identity)))
 		return fail(-EINVAL, "null tuple column or output");
@@ -2607,15 +3546,22 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 		return fail(-EINVAL, "batch of %zu packets exceeds 2^31 - 1", n);
 	if (!n)
 		return 0;
+	/* One conntrack map, one scratch: every batch runs on the context's
+	 * conntrack stream, after the caller's stream reaches this call (its
+	 * inputs), and the caller's stream then waits for the batch. */
 	std::lock_guard<std::mutex> g(c->mu);
 	HIP_OR_EIO(hipSetDevice(c->device));
+	const hipStream_t cs = c->ct_stream;
+	HIP_OR_EIO(hipEventRecord(c->ct_done, (hipStream_t)stream));
+	HIP_OR_EIO(hipStreamWaitEvent(cs, c->ct_done, 0));
 	uint32_t live = c->ct_live;
 	if (c->d_ct_count && !c->ct_host_newer) {
 		/* tombstones left by the device's deletes: compact before they
-		 * lengthen every probe chain */
+		 * lengthen every probe chain (the host reads the count after the
+		 * previous batch: the one host synchronisation of this call) */
 		uint32_t cnt[2];
-		HIP_OR_EIO(hipMemcpyAsync(cnt, c->d_ct_count, 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
-		HIP_OR_EIO(hipStreamSynchronize((hipStream_t)stream));
+		HIP_OR_EIO(hipMemcpyAsync(cnt, c->d_ct_count, 8, hipMemcpyDeviceToHost, cs));
+		HIP_OR_EIO(hipStreamSynchronize(cs));
 		live = cnt[0];
 		if (cnt[1] > (c->ct_mask + 1u) / 4u) {
 			if (int r = ct_pull(c))
@@ -2628,7 +3574,7 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 		return r;
 	const CtScratch L = ct_scratch_layout(n);
 	if (L.total > c->ct_scratch_cap) {
-		HIP_OR_EIO(hipDeviceSynchronize());
+		HIP_OR_EIO(hipStreamSynchronize(cs));
 		(void)hipFree(c->d_ct_scratch);
 		c->d_ct_scratch = nullptr;
 		c->ct_scratch_cap = 0;
@@ -2639,9 +3585,7 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 	/* every walker wave (2048 x 4) holding a chunk stays under a quarter
 	 * of the headroom */
 	const uint32_t headroom = c->cfg.ct_max > live ? c->cfg.ct_max - live : 0u;
-	uint32_t chunk = std::min<uint32_t>(256u, std::max<uint32_t>(1u, headroom / 32768u));
-	if (const char *e = getenv("CGPU_CT_CHUNK")) /* diagnostic override */
-		chunk = (uint32_t)std::max(1, atoi(e));
+	const uint32_t chunk = std::min<uint32_t>(256u, std::max<uint32_t>(1u, headroom / 32768u));
 	ct_table T{c->d_ct_keys, c->d_ct_vals, c->ct_mask, c->cfg.ct_max, c->d_ct_count, chunk};
 	ct_launch a{t->saddr, t->daddr, t->sport, t->dport, t->proto, t->l4, t->flags, t->len, t->ep,
 		    verdict, ct_ret, identity, stage, delta, (uint64_t)n, now,
@@ -2651,7 +3595,9 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 		    reinterpret_cast<uint32_t *>(b + L.idx_sorted), b + L.head,
 		    reinterpret_cast<uint32_t *>(b + L.heads), reinterpret_cast<uint32_t *>(b + L.n_heads),
 		    reinterpret_cast<uint32_t *>(b + L.heads_pos), b + L.temp, L.temp_bytes};
-	HIP_OR_EIO(launch_classify_v4_ct(s, T, a, (hipStream_t)stream));
+	HIP_OR_EIO(launch_classify_v4_ct(s, T, a, cs));
+	HIP_OR_EIO(hipEventRecord(c->ct_done, cs));
+	HIP_OR_EIO(hipStreamWaitEvent((hipStream_t)stream, c->ct_done, 0));
 	c->ct_dev_newer = true;
 	return 0;
 }

@@ -32,19 +32,6 @@ constexpr int BLOCK = 256;
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-/* DIR-24-8 longest-prefix lookup of a network-order address.
- * Returns the entry (0 = no match); *label receives sec_label. */
-__device__ __forceinline__ uint32_t dir_lookup(const dir248 &d, uint32_t addr_be, uint32_t *label)
-{
-	uint32_t h = bswap32(addr_be);
-	uint32_t e = d.tbl24[h >> 8];
-	if ((e & DIR_TAG_MASK) == DIR_TAG_GROUP)
-		e = d.tbl8[(size_t)(e & DIR_PAYLOAD_MASK) * 256u + (h & 255u)];
-	uint32_t p = e & DIR_PAYLOAD_MASK;
-	*label = (e & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? d.vals[p] : p;
-	return e;
-}
-
 /* Streamed column access: with NTL the loads / stores carry the nontemporal
  * hint (`nt`), so the 26 B/tuple stream does not evict table lines. */
 typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
@@ -109,6 +96,43 @@ __device__ __forceinline__ uint32_t lpmc_search(uint4 q0, uint4 q1, uint4 q2, ui
 	return v;
 }
 
+/* Longest-prefix lookup of a network-order IPv4 address in the compressed
+ * ipcache table (tables.h lpm16c): the /16's inline run node (x16), or on
+ * overflow its d16-style entry, a 256-entry array per address byte (at most
+ * two levels) and one run node.  dict: the leaf dictionary (LDS copy or
+ * t.dict).  Returns the DIR-encoded leaf (0 = no match). */
+__device__ __forceinline__ uint32_t lpmc_lookup(const lpm16c &t, const uint32_t *dict, uint32_t addr_be)
+{
+	const uint32_t h = bswap32(addr_be);
+	const uint4 q = reinterpret_cast<const uint4 *>(t.x16)[h >> 16];
+	if (!(q.w & LPMC_OVERFLOW)) {
+		const uint32_t x = h & 0xFFFFu;
+		const uint32_t cnt = (x >= (q.x & 0xFFFFu) ? 1u : 0u) + (x >= (q.x >> 16) ? 1u : 0u) +
+				     (x >= (q.y & 0xFFFFu) ? 1u : 0u) + (x >= (q.y >> 16) ? 1u : 0u);
+		const uint64_t v = ((uint64_t)q.w << 32) | q.z;
+		return dict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu];
+	}
+	constexpr uint32_t ARR = (DIR_TAG_GROUP >> LPMC_KIND_SHIFT) | 3u;
+	uint32_t e = q.x;
+	bool lvl8 = false;
+	if ((e >> LPMC_KIND_SHIFT) == ARR) {
+		e = t.nodes[(size_t)(e & LPMC_OFF_MASK) * 4u + ((h >> 8) & 255u)];
+		lvl8 = true;
+		if ((e >> LPMC_KIND_SHIFT) == ARR)
+			e = t.nodes[(size_t)(e & LPMC_OFF_MASK) * 4u + (h & 255u)];
+	}
+	if ((e & DIR_TAG_MASK) == DIR_TAG_GROUP) {
+		const uint32_t kind = (e >> LPMC_KIND_SHIFT) & 3u;
+		const uint4 *nd = reinterpret_cast<const uint4 *>(t.nodes) + (e & LPMC_OFF_MASK);
+		const uint4 q0 = nd[0];
+		const uint4 q1 = kind ? nd[1] : make_uint4(0, 0, 0, 0);
+		const uint4 q2 = kind == 2 ? nd[2] : make_uint4(0, 0, 0, 0);
+		const uint4 q3 = kind == 2 ? nd[3] : make_uint4(0, 0, 0, 0);
+		e = lpmc_search(q0, q1, q2, q3, kind, lvl8 ? (h & 255u) : (h & 0xFFFFu));
+	}
+	return e;
+}
+
 /* Resolve a lookup in the single-slot (neighbourhood) policy table whose home
  * slot b is already in registers (tables.h POL_HOP): returns the counter slot
  * or -1 (map_lookup_elem NULL); *z receives ep | proxy_port << 16.  Further
@@ -137,32 +161,12 @@ __device__ __forceinline__ int pol_resolve1(const pol_table &t, uint4 sl, uint32
 }
 
 /* Policy hash probe: exact 8-byte policy_key + endpoint.  Returns the
- * counter slot, or -1 (map_lookup_elem NULL); *z receives ep|proxy<<16.
- * The layout branch is on a kernarg (wave-uniform, scalar). */
+ * counter slot, or -1 (map_lookup_elem NULL); *z receives ep|proxy<<16. */
 __device__ __forceinline__ int pol_lookup(const pol_table &t, uint32_t lo, uint32_t hi, uint32_t ep,
 					  uint32_t *z)
 {
-	uint32_t b = pol_hash(lo, hi, ep) & t.bucket_mask;
-	if (t.slots_per_bucket == 1)
-		return pol_resolve1(t, reinterpret_cast<const uint4 *>(t.slots)[b], b, lo, hi, ep, z);
-	for (uint32_t p = 0; p < t.max_probe; p++) {
-		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
-		uint4 s[4];
-#pragma unroll
-		for (int k = 0; k < 4; k++)
-			s[k] = bk[k];
-#pragma unroll
-		for (int k = 0; k < 4; k++) {
-			if (s[k].w == POL_EMPTY)
-				return -1;
-			if (s[k].x == lo && s[k].y == hi && (s[k].z & 0xFFFFu) == ep) {
-				*z = s[k].z;
-				return (int)s[k].w;
-			}
-		}
-		b = (b + 1) & t.bucket_mask;
-	}
-	return -1;
+	const uint32_t b = pol_hash(lo, hi, ep) & t.bucket_mask;
+	return pol_resolve1(t, reinterpret_cast<const uint4 *>(t.slots)[b], b, lo, hi, ep, z);
 }
 
 __device__ __forceinline__ bool set4_has(const addr_set4 &t, uint32_t a)
@@ -185,27 +189,6 @@ __device__ __forceinline__ bool set4_has(const addr_set4 &t, uint32_t a)
 			if (s[k].z == a)
 				return true;
 		}
-		b = (b + 1) & t.bucket_mask;
-	}
-	return false;
-}
-
-/* 16-byte key set probe; tag in used bits 8..15 (prefix length or 0) */
-__device__ __forceinline__ bool set16_has(const addr_set16 &t, uint4 a, uint32_t tag)
-{
-	uint32_t b = hash16(a.x, a.y, a.z, a.w, tag) & t.bucket_mask;
-	uint32_t want = 1u | (tag << 8);
-	for (uint32_t p = 0; p < t.max_probe; p++) {
-		const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
-		uint4 k0 = bk[0], m0 = bk[1], k1 = bk[2], m1 = bk[3];
-		if (!(m0.x & 1u))
-			return false;
-		if (m0.x == want && k0.x == a.x && k0.y == a.y && k0.z == a.z && k0.w == a.w)
-			return true;
-		if (!(m1.x & 1u))
-			return false;
-		if (m1.x == want && k1.x == a.x && k1.y == a.y && k1.z == a.z && k1.w == a.w)
-			return true;
 		b = (b + 1) & t.bucket_mask;
 	}
 	return false;
@@ -265,7 +248,7 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 		uint64_t hi = ((uint64_t)m.w << 32) | m.z, lo = ((uint64_t)m.y << 32) | m.x;
 		/* NB: the result is carried, never returned from inside the
 		 * unrolled loop: a divergent early return there miscompiled on
-		 * gfx950 / ROCm 7.2 (tools/dbg/dbg_v6.hip reproduces it). */
+		 * gfx950 / ROCm 7.2 (round 1, reproduced in isolation). */
 		while ((hi | lo) && !res) {
 			uint32_t L[4];
 #pragma unroll
@@ -655,76 +638,6 @@ __device__ __forceinline__ bool c6_node64(const uint32_t *pool, uint32_t off, ui
 	return cnt & 1u;
 }
 
-/* does any prefix of the cover contain the (network-order) address a */
-__device__ __forceinline__ bool cover6_any(const cover6 &t, uint4 a)
-{
-	if (!t.root)
-		return false;
-	const uint32_t w0 = bswap32(a.x), w1 = bswap32(a.y), w2 = bswap32(a.z), w3 = bswap32(a.w);
-	bool hit = false, deep = false;
-	/* /16 */
-	uint32_t e = t.root[w0 >> 16];
-	uint32_t tag = e >> 30;
-	if (tag == COVER6_NODE) {
-		hit = c6_node32(t.pool, e & 0x3FFFFFFFu, w0 & 0xFFFFu, &deep);
-		tag = !hit && deep ? COVER6_DEEP : COVER6_NONE;
-	} else if (tag == COVER6_FULL) {
-		hit = true;
-	}
-	/* /32 */
-	if (tag == COVER6_DEEP) {
-		const uint32_t home = mix32(w0, 0xC0E6u) & t.m32;
-		const uint4 s = t.h32[home];
-		uint32_t hop = s.w >> POL_HOP_SHIFT;
-		uint4 r = make_uint4(0, 0, 0, 0);
-		if ((hop & 1u) && s.x == w0)
-			r = s;
-		hop &= ~1u;
-		while (hop && !r.w) {
-			const uint32_t j = __builtin_ctz(hop);
-			hop &= hop - 1u;
-			const uint4 x = t.h32[(home + j) & t.m32];
-			if (x.x == w0)
-				r = x;
-		}
-		tag = r.w ? (r.y >> 30) : COVER6_NONE;
-		e = r.y;
-		if (tag == COVER6_NODE) {
-			hit = c6_node32(t.pool, e & 0x3FFFFFFFu, w1, &deep);
-			tag = !hit && deep ? COVER6_DEEP : COVER6_NONE;
-		} else if (tag == COVER6_FULL) {
-			hit = true;
-		}
-	}
-	/* /64 */
-	if (tag == COVER6_DEEP) {
-		const uint32_t home = mix32(w0, w1) & t.m64;
-		uint4 s0 = t.h64[2u * home], s1 = t.h64[2u * home + 1u];
-		uint32_t hop = s0.w >> POL_HOP_SHIFT;
-		bool found = (hop & 1u) && s0.x == w0 && s0.y == w1;
-		hop &= ~1u;
-		while (hop && !found) {
-			const uint32_t j = __builtin_ctz(hop);
-			hop &= hop - 1u;
-			const uint32_t sl = (home + j) & t.m64;
-			const uint4 x = t.h64[2u * sl];
-			if (x.x == w0 && x.y == w1) {
-				s0 = x;
-				s1 = t.h64[2u * sl + 1u];
-				found = true;
-			}
-		}
-		if (found) {
-			tag = s0.z >> 30;
-			if (tag == COVER6_FULL)
-				hit = le64(s1.x, s1.y, w2, w3) && le64(w2, w3, s1.z, s1.w);
-			else if (tag == COVER6_NODE)
-				hit = c6_node64(t.pool, s0.z & 0x3FFFFFFFu, w2, w3);
-		}
-	}
-	return hit;
-}
-
 __device__ __forceinline__ uint32_t entry_label(const uint32_t *vals, uint32_t e)
 {
 	uint32_t p = e & DIR_PAYLOAD_MASK;
@@ -780,15 +693,14 @@ struct cls_args {
  *            (bpf_netdev.c:374-398 / :203-211); v4 secctx quirk (:278-290)
  *   policy : policy.h:46-110, negative collapsed to DROP_POLICY
  * v: verdict; id: label given to policy; st: 1 exact, 2 L3-only, 3 wildcard,
- * 0 miss; ctr: the hit entry's counter slot or -1.  NOPOL: identity only
- * (diagnostic ablation). */
+ * 0 miss; ctr: the hit entry's counter slot or -1. */
 struct decision {
 	int32_t v;
 	uint32_t id, st;
 	int ctr;
 };
 
-template <int V6, bool NOPOL = false>
+template <int V6>
 __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, bool frag, uint32_t sa4,
 					   uint32_t da4, uint4 sa6, uint4 da6, uint32_t dport, uint32_t proto,
 					   uint32_t ep)
@@ -806,7 +718,8 @@ __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, 
 		in_cluster = ad.x == s.router_ip64[0] && ad.y == s.router_ip64[1];
 	} else {
 		const uint32_t ad = egress ? da4 : sa4;
-		e = dir_lookup(s.ipc4, ad, &label);
+		e = lpmc_lookup(s.ipc4c, s.ipc4c.dict, ad);
+		label = entry_label(s.ipc4c.vals, e);
 		in_cluster = (ad & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
 	}
 	if (egress) {
@@ -827,9 +740,7 @@ __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, 
 	uint32_t z = 0;
 	int ctr = -1;
 	d.st = 0;
-	if (NOPOL) {
-		/* diagnostic: identity resolution only */
-	} else if (!frag) {
+	if (!frag) {
 		ctr = pol_lookup(s.pol, d.id, hi4, ep, &z);
 		d.st = 1;
 	}
@@ -864,10 +775,8 @@ __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, 
  * CTR = 1: hits on hot slots [0, s.hot_slots) (L3-only / wildcard keys) go
  *          to one packed LDS atomic; the workgroup flushes its LDS counters
  *          to the delta buffer once at the end; cold slots as CTR = 0.
- * CTR = 2: no policy-entry counters (diagnostic ablation only; the results
- *          are NOT the reference's: its counters are part of the contract).
  */
-template <int V6, int CTR, int NT, int ABL = 0>
+template <int V6, int CTR, int NT>
 __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
@@ -897,7 +806,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		uint32_t eda = 0;
 		if (!V6) {
 			eda = static_cast<const uint32_t *>(a.daddr)[i];
-			if (a.lb && egress && ABL == 0) {
+			if (a.lb && egress) {
 				const uint32_t sa = static_cast<const uint32_t *>(a.saddr)[i];
 				const uint32_t h = a.hash ? a.hash[i] : flow_hash(sa, eda, a.sport[i], dport, proto);
 				const lb_res r = lb4_one<CGPU_LB_LXC>(s, sa, eda, dport, proto, h);
@@ -913,11 +822,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		const bool gated = s.ct_proto_gate && proto != (V6 ? 58u : 1u) && proto != 6u &&
 				   proto != 17u;
 
-		if (ABL == 1) {
-			/* diagnostic: columns in, outputs out, no table access */
-			v = (int32_t)(dport ^ proto ^ ep);
-			id = static_cast<const uint32_t *>(egress ? a.daddr : a.saddr)[i];
-		} else if (lbdrop) {
+		if (lbdrop) {
 			v = DROP_NO_SERVICE;
 			id = 0;
 			st = 6;
@@ -938,7 +843,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 			} else if (!egress) {
 				sa4 = static_cast<const uint32_t *>(a.saddr)[i];
 			}
-			const decision d = decide<V6, ABL == 2>(s, egress, frag, sa4, eda, sa6, da6, dport, proto, ep);
+			const decision d = decide<V6>(s, egress, frag, sa4, eda, sa6, da6, dport, proto, ep);
 			v = d.v;
 			id = d.id;
 			st = d.st;
@@ -947,7 +852,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 				if (CTR == 1 && c < s.hot_slots && len < PK_MAX_LEN) {
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len);
-				} else if (CTR != 2) {
+				} else {
 					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
 					atomicAdd((unsigned long long *)&pctr[2u * c + 1u],
 						  (unsigned long long)len);
@@ -1012,7 +917,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  * bpf_netdev.c:374-404).  Differences are all in the memory schedule:
  *   - every column is read with one 4/8/16-byte load per lane (the wave reads
  *     256 B .. 1 KiB contiguous per instruction instead of 64 B .. 256 B);
- *   - the four tuples of a lane advance stage by stage (tbl24, tbl8, probe 1,
+ *   - the four tuples of a lane advance stage by stage (x16, node, probe 1,
  *     probe 2, probe 3), so each stage has four independent gathers in flight;
  *   - a hit on a cold counter slot is ONE packed u64 atomic (pk), not two.
  * Lane t of the grid (T lanes) handles tuples 4 * (j * T + t) + {0..3} at
@@ -1020,7 +925,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  * aligned 2-byte columns and 4-byte aligned 1-byte columns; the one partial
  * group at the end of the batch is read element by element.
  */
-template <int NT, int CM = 0, int LP = 1, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false>
+template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false>
 __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
 {
 	/* per-tuple flag word */
@@ -1036,14 +941,13 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 	uint64_t *pctr = a.delta;
 	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
 	const uint32_t pmask = s.pol.bucket_mask;
-	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots); /* LP == 2 */
+	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots); /* LPM leaf dictionary */
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
 	if (threadIdx.x < 16)
 		lmet[threadIdx.x] = 0;
-	if (LP == 2)
-		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
-			ldict[k] = s.ipc4c.dict[k];
+	for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
+		ldict[k] = s.ipc4c.dict[k];
 	__syncthreads();
 
 	for (uint64_t g = t0; g * Q < a.n; g += T) {
@@ -1164,9 +1068,9 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				hi4[u] = dport[u] | (proto[u] << 16) | (eg ? (1u << 24) : 0u);
 			}
 		}
-		/* ipcache lookup (eps.h:70-80): first level (x16, d16 or tbl24) */
+		/* ipcache lookup (eps.h:70-80): the /16's inline node (x16) */
 		uint32_t e[Q];
-		if (LP == 2) {
+		{
 			/* one 16-byte gather: the /16's inline run node (tables.h) */
 			uint4 q[Q];
 #pragma unroll
@@ -1187,15 +1091,8 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				const uint64_t v = ((uint64_t)q[u].w << 32) | q[u].z;
 				e[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK ? ldict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
 			}
-		} else {
-#pragma unroll
-			for (int u = 0; u < Q; u++) {
-				e[u] = 0;
-				if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK)
-					e[u] = LP ? s.ipc4c.d16[bswap32(ad[u]) >> 16] : s.ipc4.tbl24[bswap32(ad[u]) >> 8];
-			}
 		}
-		if (LP) {
+		{
 			/* compressed LPM (tables.h lpm16c): arrays (rare), then one run node */
 			constexpr uint32_t ARR = (DIR_TAG_GROUP >> LPMC_KIND_SHIFT) | 3u;
 #pragma unroll
@@ -1239,19 +1136,13 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				e[u] = lpmc_search(q[u][0], q[u][1], q2, q3, kind,
 						   (fw[u] & F_LVL8) ? (h & 255u) : (h & 0xFFFFu));
 			}
-		} else {
-#pragma unroll
-			for (int u = 0; u < Q; u++)
-				if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP)
-					e[u] = s.ipc4.tbl8[(size_t)(e[u] & DIR_PAYLOAD_MASK) * 256u +
-							   (bswap32(ad[u]) & 255u)];
 		}
 		/* identity (bpf_lxc.c:488-496 / bpf_netdev.c:374-404) */
 		uint32_t id[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint32_t p = e[u] & DIR_PAYLOAD_MASK;
-			const uint32_t label = (e[u] & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? s.ipc4.vals[p] : p;
+			const uint32_t label = (e[u] & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? s.ipc4c.vals[p] : p;
 			if (fw[u] & F_EG) {
 				if (e[u] && label)
 					id[u] = label;
@@ -1326,9 +1217,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				st[u] = 4;
 			} else if (ctr[u] >= 0) {
 				const uint32_t c = (uint32_t)ctr[u];
-				if (CM == 2) {
-					/* diagnostic: no policy-entry counters */
-				} else if (len[u] >= PKC_MAX_LEN) {
+				if (len[u] >= PKC_MAX_LEN) {
 					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
 					atomicAdd((unsigned long long *)&pctr[2u * c + 1u], (unsigned long long)len[u]);
 					const uint32_t mi = (fw[u] & F_EG) ? 2u : 0u;
@@ -1337,7 +1226,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				} else if (c < s.hot_slots) {
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
-				} else if (CM != 3) { /* CM 3: diagnostic, cold counters skipped */
+				} else {
 					atomicAdd((unsigned long long *)&pk[c],
 						  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
 				}
@@ -1756,34 +1645,8 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilt
 		} else if (f != 0u) {
 			v = XDP_DROP;
 		} else {
-			bool drop = false;
-			if (s.pf4_enabled && s.pf4.tbl24) {
-				uint32_t label;
-				drop = dir_lookup(s.pf4, sa, &label) != 0;
-			}
+			const bool drop = s.pf4_enabled && s.pf4c.x16 && lpmc_lookup(s.pf4c, s.pf4c.dict, sa) != 0;
 			v = drop ? XDP_DROP : (set4_has(s.ep4, da) ? XDP_PASS : XDP_DROP);
-		}
-		a.verdict[i] = v;
-	}
-}
-
-/* XDP prefilter IPv6 (bpf/bpf_xdp.c:132-156): any-match over dyn6 + fix6 */
-__global__ __launch_bounds__(BLOCK) void k_prefilter_v6(cgpu_snapshot s, prefilter_args a)
-{
-	const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
-	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
-	for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t f = a.flags[i];
-		const uint4 sa = sa16[i], da = da16[i];
-		uint8_t v;
-		if (f == 2u) {
-			v = XDP_PASS;
-		} else if (f != 0u) {
-			v = XDP_DROP;
-		} else {
-			const bool drop = s.pf6_enabled && cover6_any(s.pf6, sa);
-			v = drop ? XDP_DROP : (set16_has(s.ep6, da, 0u) ? XDP_PASS : XDP_DROP);
 		}
 		a.verdict[i] = v;
 	}
@@ -1793,8 +1656,8 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v6(cgpu_snapshot s, prefilt
  * XDP prefilter IPv6, Q packets per lane with the cover lookup advanced
  * stage by stage across them (root, /32 record, interval node in chunks of
  * 12 / 16 / 16 boundaries, /64 record, endpoint bucket), so each stage has Q
- * independent gathers in flight per lane.  Same decisions as k_prefilter_v6
- * (bpf/bpf_xdp.c:132-156 then check_v6_endpoint :123-130).
+ * independent gathers in flight per lane: bpf/bpf_xdp.c:132-156 (any deny
+ * prefix covers saddr -> XDP_DROP), then check_v6_endpoint :123-130.
  */
 __device__ __forceinline__ uint32_t c6_count4(uint4 q, uint32_t base, uint32_t nb, uint32_t x)
 {
@@ -2060,7 +1923,7 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 /* W: minimum resident waves per SIMD the registers are fitted to.  COOP:
  * octet-cooperative /32 node reads (c6_node32_coop); the loop trip count is
  * then uniform per wave, lanes past the batch end carry inactive packets. */
-template <int Q, int W = 1, bool COOP = false, int ABL = 0>
+template <int Q, int W = 1, bool COOP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_prefilter_v6_q(cgpu_snapshot s,
 												     prefilter_args a)
 {
@@ -2083,20 +1946,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			f[u] = a.flags[i];
 			act[u] = i0 + u < a.n && f[u] == 0u && s.pf6_enabled;
 		}
-		if (ABL == 2) { /* diagnostic ablation: no cover lookup */
-#pragma unroll
-			for (int u = 0; u < Q; u++)
-				hit[u] = false;
-		} else {
-			cover6_any_q<Q, COOP>(s.pf6, sa, act, hit);
-		}
+		cover6_any_q<Q, COOP>(s.pf6, sa, act, hit);
 		/* check_v6_endpoint: cilium_lxc on daddr (bucket loads for all first) */
 		uint4 bk[Q][4];
 		uint32_t b[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			b[u] = hash16(da[u].x, da[u].y, da[u].z, da[u].w, 0u) & s.ep6.bucket_mask;
-			const bool need = ABL != 1 && i0 + u < a.n && f[u] == 0u && !hit[u]; /* ABL 1: no endpoint step */
+			const bool need = i0 + u < a.n && f[u] == 0u && !hit[u];
 #pragma unroll
 			for (int k = 0; k < 4; k++)
 				bk[u][k] = need ? reinterpret_cast<const uint4 *>(s.ep6.slots)[(size_t)b[u] * 4u + k]
@@ -2154,8 +2011,7 @@ unsigned grid_for(uint64_t n)
 
 } // namespace
 
-/* CGPU_CLASSIFY_VARIANT selects the probe schedule (A/B in one process);
- * every variant computes identical results. */
+/* CGPU_CLASSIFY_VARIANT: the classify schedule (see launch_classify). */
 static int classify_variant()
 {
 	const char *v = getenv("CGPU_CLASSIFY_VARIANT");
@@ -2200,17 +2056,14 @@ static unsigned resident_blocks(const void *kern, int NT, size_t lds)
 /* x4 schedule: one persistent-size grid (every workgroup resident, so the
  * per-workgroup LDS counter flush is paid once per resident workgroup) per
  * launch of <= PKC_CHUNK tuples, then the unpack of pk into delta. */
-static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream_t st, int var)
+template <bool LB>
+static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024;
-	const size_t lds = (size_t)s.hot_slots * 8u;
-	const size_t lds2 = lds + (size_t)s.ipc4c.n_dict * 4u; /* + LDS leaf dictionary */
-	const void *kern = a.lb ? (const void *)k_classify_v4_x4<NT, 0, 2, true, 4, 1, true>
-			   : var == 12 ? (const void *)k_classify_v4_x4<NT, 2, 2, true>
-			   : var == 13 ? (const void *)k_classify_v4_x4<NT, 3, 2, true>
-			   : var == 15 ? (const void *)k_classify_v4_x4<NT, 0, 0, true>
-				       : (const void *)k_classify_v4_x4<NT, 0, 2, true>;
-	const unsigned res = resident_blocks(kern, NT, var == 15 ? lds : lds2);
+	/* LDS: hot counters + the ipcache leaf dictionary */
+	const size_t lds = (size_t)s.hot_slots * 8u + (size_t)s.ipc4c.n_dict * 4u;
+	const void *kern = (const void *)k_classify_v4_x4<NT, true, 4, 1, LB>;
+	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
 	for (uint64_t off = 0; off < a.n; off += chunk) {
@@ -2233,17 +2086,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 		if (c.hash)
 			c.hash += off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + 4 * NT - 1) / (4 * NT), res);
-		if (a.lb)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true, 4, 1, true>), dim3(g), dim3(NT), lds2, st, s,
-					   c, a.pk);
-		else if (var == 12)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 2, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
-		else if (var == 13)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 3, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
-		else if (var == 15)
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 0, true>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
-		else
-			hipLaunchKernelGGL((k_classify_v4_x4<NT, 0, 2, true>), dim3(g), dim3(NT), lds2, st, s, c, a.pk);
+		hipLaunchKernelGGL((k_classify_v4_x4<NT, true, 4, 1, LB>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi,
@@ -2253,16 +2096,13 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 	return hipGetLastError();
 }
 
-/* CGPU_CLASSIFY_VARIANT selects the schedule (A/B in one process):
- *   8 (default, IPv4): k_classify_v4_x4 — four tuples per lane, vector column
- *      loads, LDS hot counters + one packed atomic per cold hit, resident grid
- *      (needs aligned columns and the single-slot policy layout, else 3)
+/* CGPU_CLASSIFY_VARIANT selects the schedule (A/B in one process); every
+ * variant computes the reference's results (tests/test_gpu_parity.py):
+ *   8 (default, IPv4): k_classify_v4_x4 -- four tuples per lane, vector
+ *      column loads, LDS hot counters + one packed atomic per cold hit,
+ *      resident grid (needs aligned columns, else 3)
  *   3 (default, IPv6 / fallback): one tuple per lane, LDS hot counters
- *   0: global atomics for every hit, 256-thread workgroups
- *   15: k_classify_v4_x4 over the DIR-24-8 ipcache (LPM layout A/B)
- *   9, 12, 20-22: diagnostic ablations (no counters / partial work); their
- *      results are NOT the reference's and they are never the default.
- * Every non-diagnostic variant computes identical results. */
+ *   0: global atomics for every hit, 256-thread workgroups */
 template <int V6>
 static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_t st)
 {
@@ -2271,24 +2111,8 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 		hipLaunchKernelGGL((k_classify<V6, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 		return hipGetLastError();
 	}
-	if (var == 9) {
-		hipLaunchKernelGGL((k_classify<V6, 2, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
-		return hipGetLastError();
-	}
-	if (var == 20 || var == 21 || var == 22) {
-		/* diagnostic ablations at the default geometry, no counters:
-		 * 20 columns only, 21 + identity resolution, 22 + policy */
-		const unsigned g = (unsigned)std::min<uint64_t>((a.n + 1023) / 1024, 512);
-		if (var == 20)
-			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 1>), dim3(g), dim3(1024), 0, st, s, a);
-		else if (var == 21)
-			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 2>), dim3(g), dim3(1024), 0, st, s, a);
-		else
-			hipLaunchKernelGGL((k_classify<V6, 2, 1024, 0>), dim3(g), dim3(1024), 0, st, s, a);
-		return hipGetLastError();
-	}
-	if (!V6 && (var == 8 || var == 12 || var == 13 || var == 15) && s.pol.slots_per_bucket == 1 && a.pk && x4_aligned(a))
-		return launch_x4(s, a, st, var);
+	if (!V6 && var == 8 && a.pk && x4_aligned(a))
+		return a.lb ? launch_x4<true>(s, a, st) : launch_x4<false>(s, a, st);
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
 	constexpr int NT = 1024;
@@ -2351,31 +2175,10 @@ hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, 
 
 hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)
 {
-	/* CGPU_PF6_Q = "Q[:V]": packets per lane (1 = k_prefilter_v6) and the
-	 * variant.  Default "4": octet-cooperative node reads.  A/B on config 3
-	 * with the current cover (Gpps): 4 24.8; 4:1 (per-lane node reads) 21.1;
-	 * 4:5 (fitted to 5 waves/SIMD) 20.4; 2 20.9; 1 20.5.  (Before long /16
-	 * nodes were pushed down: 4 8.81, 4:1 8.43, 2 7.34, 4:5 7.41, and 5-7
-	 * waves/SIMD variants 6.5-7.4.) */
-	const char *qs = getenv("CGPU_PF6_Q");
-	const int q = qs ? atoi(qs) : 4;
-	const char *vs = qs ? strchr(qs, ':') : nullptr;
-	const int v = vs ? atoi(vs + 1) : 0;
-	if (q == 4 && v == 0)
-		hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st,
-				   s, a);
-	else if (q == 4 && v == 8) /* diagnostic ablations (wrong verdicts): no endpoint step / no cover */
-		hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true, 1>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
-	else if (q == 4 && v == 9)
-		hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true, 2>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
-	else if (q == 4 && v == 5)
-		hipLaunchKernelGGL((k_prefilter_v6_q<4, 5>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
-	else if (q == 4)
-		hipLaunchKernelGGL(k_prefilter_v6_q<4>, dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
-	else if (q == 2)
-		hipLaunchKernelGGL(k_prefilter_v6_q<2>, dim3(grid_for((a.n + 1) / 2)), dim3(BLOCK), 0, st, s, a);
-	else
-		hipLaunchKernelGGL(k_prefilter_v6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	/* four packets per lane, octet-cooperative node reads.  A/B on config 3
+	 * (Gpps, round 1): Q=4 coop 24.8; Q=4 per-lane nodes 21.1; Q=4 fitted
+	 * to 5 waves/SIMD 20.4; Q=2 20.9; Q=1 20.5. */
+	hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
 	return hipGetLastError();
 }
 
@@ -2774,7 +2577,7 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 			const bool frag = !egress && ((fl >> 1) & 1u);
 			if (frag)
 				meta |= CTM_FRAG;
-			const decision d = decide<0, false>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
+			const decision d = decide<0>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
 							    pr, ep);
 			if (d.v >= 0) {
 				meta |= CTM_ALLOWED;
@@ -3122,7 +2925,7 @@ template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapsho
 			int ctr;
 			if (cr >= CT_REPLY) {
 				const bool frag = meta & CTM_FRAG;
-				const decision d = decide<0, false>(s, egress, frag, r0.y, r0.x, uint4{}, uint4{},
+				const decision d = decide<0>(s, egress, frag, r0.y, r0.x, uint4{}, uint4{},
 								    r0.z & 0xFFFFu, r0.w & 0xFFu, a.ep[i]);
 				ctr = d.ctr;
 				st = d.st;

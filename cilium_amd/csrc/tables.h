@@ -11,7 +11,8 @@
 
 #include <stdint.h>
 
-/* ---- DIR-24-8 longest-prefix table (ipcache v4, prefilter v4) ----
+/* ---- DIR-24-8 entry encoding (host.cpp builds a DIR-24-8 image per LPM
+ * table and compiles it into the compressed lpm16c form below) ----
  * tbl24[addr >> 8] (2^24 u32 = 64 MiB) and 256-entry tbl8 groups for
  * prefixes longer than /24.  Entry encoding (u32):
  *   0                      no match (NULL from map_lookup_elem)
@@ -29,19 +30,11 @@
 #define DIR_PAYLOAD_MASK ((1u << DIR_TAG_SHIFT) - 1u)
 #define DIR_TBL24_ENTRIES (1u << 24)
 
-typedef struct dir248 {
-	const uint32_t *tbl24;
-	const uint32_t *tbl8;
-	const uint32_t *vals;
-	uint32_t n_groups;
-	uint32_t n_vals;
-} dir248;
-
 /* ---- compressed IPv4 longest-prefix table (L2-resident ipcache) ----
- * The same function as a dir248 (it is compiled FROM one), in ~1/50 of the
+ * The same function as a DIR-24-8 image (it is compiled FROM one), in ~1/50 of the
  * bytes, so that it stays in every XCD's 4 MiB L2 instead of being served
  * from the Infinity Cache.  d16[addr >> 16] holds a DIR entry (0 / direct /
- * indirect leaf, as dir248) or a GROUP reference
+ * indirect leaf, DIR encoding) or a GROUP reference
  *   bits 28..29 kind, bits 0..27 offset in 16-byte units into `nodes`:
  *   kind 0/1/2: a run node of 16 / 32 / 64 bytes over the low 16 bits (or,
  *               below an array, the low 8 bits) x of the address:
@@ -52,7 +45,7 @@ typedef struct dir248 {
  *               byte; an entry is a leaf, a run node (kind 0..2) over the
  *               last byte, or (below d16 only) another kind-3 array of 256
  *               leaves (the last byte, like a tbl8 group).
- * Leaves use the dir248 entry encoding and share its `vals`. */
+ * Leaves use the DIR entry encoding and share its `vals`. */
 #define LPMC_KIND_SHIFT 28u
 #define LPMC_OFF_MASK ((1u << LPMC_KIND_SHIFT) - 1u)
 #define LPMC_MAX_RUN_BOUNDS 10u
@@ -80,20 +73,16 @@ typedef struct lpm16c {
 } lpm16c;
 
 /* ---- policy hash: one open-addressing table for all endpoints ----
- * 64-byte buckets (one cache-line sector) of 4 x 16-byte slots:
- *   x = sec_label, y = dport | proto << 16 | egress_pad << 24,
- *   z = ep | proxy_port << 16, w = counter slot (0xFFFFFFFF = empty).
- * (x, y) is the raw 8-byte policy_key, compared whole like the kernel htab
- * memcmp (pad bits included).  Bucket index = mix(key, ep) & mask, linear
- * probing over buckets; a bucket with an empty slot ends the probe. */
-#define POL_SLOTS_PER_BUCKET 4u
-#define POL_EMPTY 0xFFFFFFFFu
-/* Single-slot layout (slots_per_bucket 1, the default): neighbourhood
- * ("hop") hashing.  A key lives within POL_HOP slots of its home slot h;
- * w = counter slot (bits 0..23, POL_CTR_EMPTY = empty) | hop << 24, where
- * bit j of home slot h's hop says "slot h + j holds a key whose home is h".
- * A lookup loads the home slot (one 16-byte gather): hop == 0 is a miss,
- * bit 0 + key match a hit; only other set bits cost further loads. */
+ * 16-byte slots {x = sec_label, y = dport | proto << 16 | egress_pad << 24,
+ * z = ep | proxy_port << 16, w = counter slot | hop << 24}.  (x, y) is the
+ * raw 8-byte policy_key, compared whole like the kernel htab memcmp (pad
+ * bits included).  Neighbourhood ("hop") hashing: a key lives within
+ * POL_HOP slots of its home slot h = pol_hash(key, ep) & mask; w bits 0..23
+ * hold the counter slot (POL_CTR_EMPTY = empty slot) and bit 24 + j of home
+ * slot h says "slot h + j holds a key whose home is h".  A lookup loads the
+ * home slot (one 16-byte gather): hop == 0 is a miss, bit 0 + key match a
+ * hit; only other set bits cost further loads.  Kept at <= 50 % load; a
+ * commit patches keys in place (host.cpp pol_patch) or rebuilds. */
 #define POL_HOP 8u
 #define POL_HOP_SHIFT 24u
 #define POL_CTR_MASK 0x00FFFFFFu
@@ -103,14 +92,12 @@ typedef struct pol_slot {
 	uint32_t key_lo;  /* sec_label */
 	uint32_t key_hi;  /* dport | protocol << 16 | egress_pad << 24 */
 	uint32_t ep_proxy;/* ep | proxy_port << 16 */
-	uint32_t ctr;     /* counter slot or POL_EMPTY */
+	uint32_t ctr;     /* counter slot | hop << 24 (POL_CTR_EMPTY: free) */
 } pol_slot;
 
 typedef struct pol_table {
-	const pol_slot *slots; /* n_buckets * slots_per_bucket */
+	const pol_slot *slots; /* bucket_mask + 1 slots */
 	uint32_t bucket_mask;
-	uint32_t max_probe;    /* 4-slot layout: longest probe sequence in buckets */
-	uint32_t slots_per_bucket; /* 4: 64-B buckets; 1: 16-B slots, one load per probe */
 	uint32_t pad_;
 } pol_table;
 
@@ -279,10 +266,9 @@ typedef struct cover6 {
 
 /* ---- one committed snapshot ---- */
 typedef struct cgpu_snapshot {
-	dir248 ipc4;
-	lpm16c ipc4c;    /* the same ipcache v4 function, compressed */
+	lpm16c ipc4c;    /* ipcache, IPv4 lookups (compiled from a host DIR-24-8) */
 	pol_table pol;
-	dir248 pf4;      /* any-match: dyn4 (if enabled) + fix4 /32 */
+	lpm16c pf4c;     /* any-match: dyn4 (if enabled) + fix4 /32; leaves 0 / 1 */
 	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
 	addr_set16 ep6;  /* cilium_lxc IPv6 keys */
 	cover6 pf6;      /* any-match: dyn6 (if enabled) + fix6 /128 */

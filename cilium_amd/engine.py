@@ -90,6 +90,12 @@ class Engine:
         rc = self.L.cgpu_ipcache_lookup(self.h, _buf(key), out)
         return rc, (np.frombuffer(out.raw, L.REMOTE_ENDPOINT_INFO)[0] if rc == 0 else None)
 
+    def ipcache_update_batch(self, keys, vals, flags=BPF_ANY) -> int:
+        k = np.ascontiguousarray(keys, L.IPCACHE_KEY)
+        v = np.ascontiguousarray(vals, L.REMOTE_ENDPOINT_INFO)
+        assert len(k) == len(v)
+        return self.L.cgpu_ipcache_update_batch(self.h, k.ctypes.data, v.ctypes.data, len(k), flags)
+
     def ipcache_keys(self):
         keys, prev = [], None
         out = C.create_string_buffer(24)
@@ -120,6 +126,44 @@ class Engine:
     def policy_flush(self, ep) -> int:
         return self.L.cgpu_policy_flush(self.h, ep)
 
+    def policy_update_batch(self, eps, keys, entries, flags=BPF_ANY) -> int:
+        e = np.ascontiguousarray(eps, np.uint32)
+        k = np.ascontiguousarray(keys, L.POLICY_KEY)
+        v = np.ascontiguousarray(entries, L.POLICY_ENTRY)
+        assert len(e) == len(k) == len(v)
+        return self.L.cgpu_policy_update_batch(self.h, e.ctypes.data, k.ctypes.data, v.ctypes.data,
+                                               len(k), flags)
+
+    def policy_lookup_batch(self, eps, keys):
+        """(rc[n], entries[n]) of cgpu_policy_lookup_batch (one device read)."""
+        e = np.ascontiguousarray(eps, np.uint32)
+        k = np.ascontiguousarray(keys, L.POLICY_KEY)
+        out = np.zeros(len(k), L.POLICY_ENTRY)
+        rc = np.zeros(len(k), np.int32)
+        check(self.L.cgpu_policy_lookup_batch(self.h, e.ctypes.data, k.ctypes.data, len(k),
+                                              out.ctypes.data, rc.ctypes.data),
+              "cgpu_policy_lookup_batch")
+        return rc, out
+
+    def policy_counters(self, eps, keys) -> np.ndarray:
+        """(n, 2) uint64 {packets, bytes} of present keys (raises if any is absent)."""
+        rc, out = self.policy_lookup_batch(eps, keys)
+        assert (rc == 0).all(), "policy key absent"
+        return np.stack([out["packets"], out["bytes"]], 1).astype(np.uint64)
+
+    def policy_dump(self, ep):
+        """DumpToSlice of one endpoint's map: (keys, entries)."""
+        n = C.c_size_t()
+        rc = self.L.cgpu_policy_dump(self.h, ep, None, None, 0, C.byref(n))
+        keys = np.zeros(n.value, L.POLICY_KEY)
+        ents = np.zeros(n.value, L.POLICY_ENTRY)
+        if n.value:
+            check(self.L.cgpu_policy_dump(self.h, ep, keys.ctypes.data, ents.ctypes.data, n.value,
+                                          C.byref(n)), "cgpu_policy_dump")
+        elif rc < 0:
+            check(rc, "cgpu_policy_dump")
+        return keys, ents
+
     @staticmethod
     def _cidr_buf(key) -> bytes:
         raw = _buf(key)
@@ -127,6 +171,13 @@ class Engine:
 
     def cidr_update(self, which, key, flags=BPF_ANY) -> int:
         return self.L.cgpu_cidr_update(self.h, which, self._cidr_buf(key), flags)
+
+    def cidr_update_batch(self, which, keys, flags=BPF_ANY) -> int:
+        """keys: LPM_V4_KEY / LPM_V6_KEY records (padded to 20-byte keys)."""
+        k = np.ascontiguousarray(keys)
+        buf = np.zeros((len(k), 20), np.uint8)
+        buf[:, :k.dtype.itemsize] = k.view(np.uint8).reshape(len(k), k.dtype.itemsize)
+        return self.L.cgpu_cidr_update_batch(self.h, which, buf.ctypes.data, len(k), flags)
 
     def cidr_delete(self, which, key) -> int:
         return self.L.cgpu_cidr_delete(self.h, which, self._cidr_buf(key))
@@ -439,6 +490,22 @@ class Engine:
 
     def counters_reset(self) -> None:
         check(self.L.cgpu_counters_reset(self.h), "cgpu_counters_reset")
+
+    # ------------------------------------------- multi-GPU
+    @staticmethod
+    def comm_id() -> bytes:
+        """A fresh communicator id (rank 0 creates it and shares it)."""
+        buf = C.create_string_buffer(128)
+        check(lib().cgpu_comm_id_create(buf), "cgpu_comm_id_create")
+        return buf.raw
+
+    def comm_init(self, comm_id: bytes, nranks: int, rank: int) -> None:
+        assert len(comm_id) == 128
+        check(self.L.cgpu_comm_init(self.h, comm_id, nranks, rank), "cgpu_comm_init")
+
+    def counters_allreduce(self, stream=None) -> None:
+        """RCCL SUM of the delta buffer over the communicator's ranks."""
+        check(self.L.cgpu_counters_allreduce(self.h, _stream(stream)), "cgpu_counters_allreduce")
 
 
 # ---------------------------------------------------------------------------

@@ -195,12 +195,10 @@ def make_tuples(tables: Tables, n: int, seed=SEED, gpu_id: int = 0):
 
 
 def load_engine(engine, t: Tables):
-    for k, v in zip(t.ipc_keys, t.ipc_vals):
-        rc = engine.ipcache_update(k, v)
-        assert rc == 0, rc
-    for k, e, ep in zip(t.pol_keys, t.pol_entries, t.pol_ep):
-        rc = engine.policy_update(int(ep), k, e)
-        assert rc == 0, rc
+    rc = engine.ipcache_update_batch(t.ipc_keys, t.ipc_vals)
+    assert rc == 0, rc
+    rc = engine.policy_update_batch(t.pol_ep, t.pol_keys, t.pol_entries)
+    assert rc == 0, rc
 
 
 def load_oracle(oracle, t: Tables):
@@ -389,6 +387,10 @@ def make_packets6(P: Prefilter6, n: int, seed=SEED, gpu_id: int = 0, chunk=1 << 
 def load_prefilter6(target, P: Prefilter6):
     """Engine or Oracle: dyn6 / fix6 CIDR maps (pkg/maps/cidrmap) + cilium_lxc."""
     for which, keys in ((2, P.dyn6), (3, P.fix6)):
+        if hasattr(target, "cidr_update_batch"):
+            rc = target.cidr_update_batch(which, keys)
+            assert rc == 0, rc
+            continue
         for k in keys:
             rc = target.cidr_update(which, k)
             assert rc == 0, rc

@@ -19,7 +19,9 @@
  *   - table updates are thread-safe (one mutex on the host mirror) and become
  *     visible to classification only at cgpu_commit(), which publishes a new
  *     immutable device snapshot (epoch).  Classification launches read the
- *     latest committed snapshot and may run concurrently with updates.
+ *     latest published snapshot and never take the mirror lock: they run
+ *     concurrently with updates and with commits (a launch pins the snapshot
+ *     it started on; its buffers are freed only after its kernels finish).
  *     Like the reference (pkg/endpoint/bpf.go:459-465), a set of updates is
  *     not atomic unless it is committed at once.
  *   - batch entry points take DEVICE pointers (HBM-resident SoA columns) and
@@ -187,6 +189,11 @@ int cgpu_ipcache_lookup(cgpu_ctx *ctx, const cgpu_ipcache_key *key,
 int cgpu_ipcache_get_next_key(cgpu_ctx *ctx, const cgpu_ipcache_key *key,
 			      cgpu_ipcache_key *next_out);
 size_t cgpu_ipcache_count(cgpu_ctx *ctx);
+/* n updates in order; stops at the first failure (its -errno is returned,
+ * the updates before it stay applied): the listener's sequence of
+ * OnIPIdentityCacheChange writes in one call */
+int cgpu_ipcache_update_batch(cgpu_ctx *ctx, const cgpu_ipcache_key *keys,
+			      const cgpu_remote_endpoint_info *vals, size_t n, uint64_t flags);
 
 /* ------------------------------------------------------------------ */
 /* policy maps: pkg/maps/policymap (AllowKey/DeleteKey/DumpToSlice/     */
@@ -202,6 +209,18 @@ int cgpu_policy_get_next_key(cgpu_ctx *ctx, uint32_t ep, const cgpu_policy_key *
 			     cgpu_policy_key *next_out);
 int cgpu_policy_flush(cgpu_ctx *ctx, uint32_t ep);
 size_t cgpu_policy_count(cgpu_ctx *ctx, uint32_t ep);
+/* AllowKey for n (ep, key) pairs in order (stops at the first failure) */
+int cgpu_policy_update_batch(cgpu_ctx *ctx, const uint32_t *eps, const cgpu_policy_key *keys,
+			     const cgpu_policy_entry *entries, size_t n, uint64_t flags);
+/* cgpu_policy_lookup of n (ep, key) pairs with one read of the device
+ * counters: rc_out[i] = 0 or -ENOENT (-EINVAL for an ep out of range) */
+int cgpu_policy_lookup_batch(cgpu_ctx *ctx, const uint32_t *eps, const cgpu_policy_key *keys,
+			     size_t n, cgpu_policy_entry *entries_out, int32_t *rc_out);
+/* DumpToSlice (pkg/maps/policymap/policymap.go:208-240): every key of ep's
+ * map with its entry, in GetNextKey order; *n_out = the key count
+ * (-ENOSPC when it exceeds cap, nothing written) */
+int cgpu_policy_dump(cgpu_ctx *ctx, uint32_t ep, cgpu_policy_key *keys_out,
+		     cgpu_policy_entry *entries_out, size_t cap, size_t *n_out);
 
 /* ------------------------------------------------------------------ */
 /* prefilter CIDR maps: pkg/maps/cidrmap (InsertCIDR/DeleteCIDR/        */
@@ -213,6 +232,9 @@ int cgpu_cidr_delete(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key);
 int cgpu_cidr_lookup(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key);
 int cgpu_cidr_get_next_key(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key,
 			   cgpu_cidr_key *next_out);
+/* n InsertCIDR writes in order (stops at the first failure) */
+int cgpu_cidr_update_batch(cgpu_ctx *ctx, int which, const cgpu_cidr_key *keys, size_t n,
+			   uint64_t flags);
 int cgpu_endpoint_update(cgpu_ctx *ctx, const cgpu_endpoint_key *key, uint64_t flags);
 int cgpu_endpoint_delete(cgpu_ctx *ctx, const cgpu_endpoint_key *key);
 int cgpu_endpoint_lookup(cgpu_ctx *ctx, const cgpu_endpoint_key *key);
@@ -288,7 +310,16 @@ int cgpu_lxc_lookup(cgpu_ctx *ctx, uint32_t ep, cgpu_lxc_info *info_out);
 /* ------------------------------------------------------------------ */
 /* Compile the host mirror into device tables and publish them as the new
  * snapshot read by later batch launches.  *epoch_out (optional) receives
- * the snapshot number.  Blocks until the upload completes. */
+ * the snapshot number.  Only the table groups that changed since the last
+ * commit are uploaded (the rest is shared with the previous snapshot); a
+ * few ipcache / policy changes patch the previous tables instead of
+ * recompiling them, the way the reference writes each map key in place
+ * (pkg/endpoint/endpoint.go:2572-2652 syncPolicyMap,
+ * pkg/datapath/ipcache/listener.go:78-127).  Returns once the upload (on the
+ * context's own stream) is complete; launches in flight on the previous
+ * snapshot are never waited for.  Counter values supplied with a rewritten
+ * policy entry reach the device here; hits that launches still running on
+ * the previous snapshot add to that entry may land before or after. */
 int cgpu_commit(cgpu_ctx *ctx, uint64_t *epoch_out);
 /* order-independent checksum of the committed table contents; replicas on
  * different GPUs/ranks holding the same tables report the same value */
@@ -566,6 +597,10 @@ typedef struct cgpu_tuples_v4_ct {
  * resolved in order by one lane; pairs are independent.  The one departure
  * from a sequential run: which creates fail when the map fills up DURING a
  * batch depends on the order lanes reach the capacity check.
+ * The context has ONE conntrack map: batches of every caller run in order
+ * on the context's internal conntrack stream (after `stream` reaches the
+ * call; `stream` then waits for the batch).  The host reads the map's
+ * tombstone count once per call, which waits for the previous batch.
  */
 int cgpu_classify_v4_ct(cgpu_ctx *ctx, const cgpu_tuples_v4_ct *t, size_t n, uint32_t now,
 			int32_t *verdict, uint8_t *ct_ret, uint32_t *identity, uint8_t *stage,
@@ -661,6 +696,23 @@ int cgpu_counter_fold(cgpu_ctx *ctx, void *stream);
 /* out: [256][4][2] u64 {count, bytes} (folds and synchronizes first) */
 int cgpu_metrics_read(cgpu_ctx *ctx, uint64_t *out);
 int cgpu_counters_reset(cgpu_ctx *ctx);
+
+/* ------------------------------------------------------------------ */
+/* multi-GPU counter reduction (consumer: the agent's      */
+/* metrics export, pkg/maps/metricsmap/metricsmap.go:170 SyncMetricsMap)*/
+/* ------------------------------------------------------------------ */
+/* One process (or context) per GPU holds the same committed tables and
+ * classifies its own shard of the stream.  Rank 0 creates a communicator id
+ * and hands it to every rank out of band (the agent's own channel); each
+ * rank then joins with cgpu_comm_init (collective: blocks until all
+ * nranks joined).  cgpu_counters_allreduce enqueues the RCCL SUM (over
+ * xGMI) of the delta buffer on `stream`; after it every rank's delta holds
+ * the counts of all ranks, and cgpu_counter_fold adds them to the totals
+ * (integer sums: bit-exact against one GPU classifying the whole stream). */
+#define CGPU_COMM_ID_BYTES 128
+int cgpu_comm_id_create(uint8_t *id_out /* [CGPU_COMM_ID_BYTES] */);
+int cgpu_comm_init(cgpu_ctx *ctx, const uint8_t *id, int nranks, int rank);
+int cgpu_counters_allreduce(cgpu_ctx *ctx, void *stream);
 
 #ifdef __cplusplus
 }

@@ -295,3 +295,43 @@ def test_ct_map_matches_restatement_under_churn():
     ok, ov = o.ct4_dump()
     np.testing.assert_array_equal(ek, ok)
     np.testing.assert_array_equal(ev, ov)
+
+
+def test_no_diagnostic_variants_ship():
+    """Only schedules that compute the reference's results ship in the
+    product library: no ablation switches are read from the environment."""
+    data = open(build.LIB, "rb").read()
+    for knob in (b"CGPU_PF6_Q", b"CGPU_CT_CHUNK", b"CGPU_POL_BPB", b"CGPU_POL_LOAD_PCT", b"CGPU_LB_VIP_BITS"):
+        assert knob not in data, knob
+
+
+def test_batch_ops_and_dump_host_only():
+    """cgpu_*_update_batch apply in order and stop at the first failure;
+    cgpu_policy_dump / cgpu_policy_lookup_batch mirror DumpToSlice /
+    per-key lookups (host-only context: counters are the supplied ones)."""
+    e = Engine(device=-1, max_endpoints=4, policy_max_per_ep=8)
+    keys = np.array([L.policy_key(300 + i, 80, 6, i & 1) for i in range(10)])
+    ents = np.array([L.policy_entry(i, 10 * i, 100 * i) for i in range(10)])
+    eps = np.zeros(10, np.uint32)
+    rc = e.policy_update_batch(eps, keys, ents)
+    assert rc == -errno.E2BIG  # the 9th write hits policy_max_per_ep
+    assert e.L.cgpu_policy_count(e.h, 0) == 8
+    k, v = e.policy_dump(0)
+    assert len(k) == 8
+    order = np.argsort(k.view(np.uint64))
+    assert (k.view(np.uint64)[order] == k.view(np.uint64)).all()  # GetNextKey order
+    got = {int(x["sec_label"]): (int(y["packets"]), int(y["bytes"]), L.ntohs(int(y["proxy_port"])))
+           for x, y in zip(k, v)}
+    assert got == {300 + i: (10 * i, 100 * i, i) for i in range(8)}
+    rc, out = e.policy_lookup_batch(np.array([0, 0, 9], np.uint32), keys[[1, 9, 0]])
+    assert list(rc) == [0, -errno.ENOENT, -errno.EINVAL]
+    assert int(out[0]["packets"]) == 10
+    ik = np.array([L.ipcache_key(f"10.0.{i}.0/24") for i in range(5)])
+    iv = np.array([L.remote_info(500 + i) for i in range(5)])
+    assert e.ipcache_update_batch(ik, iv) == 0
+    assert e.ipcache_update_batch(ik[:2], iv[:2], BPF_NOEXIST) == -errno.EEXIST
+    assert len(e.ipcache_keys()) == 5
+    ck = np.array([L.lpm_key(f"2001:db8:{i}::/48") for i in range(4)])
+    assert e.cidr_update_batch(CIDR_V6_DYN, ck) == 0
+    assert len(e.cidr_keys(CIDR_V6_DYN)) == 4
+    e.close()

@@ -391,7 +391,7 @@ def test_classify_v6_scale_vs_oracle(torch_cuda):
     e.close()
 
 
-@pytest.mark.parametrize("variant", [0, 3, 8, 15])
+@pytest.mark.parametrize("variant", [0, 3, 8])
 def test_kernel_variants_exact(torch_cuda, cfg1, variant, monkeypatch):
     """Every classify schedule / counter strategy gives the reference's
     verdicts, identities, stages, per-entry counters and metrics."""
