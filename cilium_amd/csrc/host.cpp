@@ -1433,10 +1433,12 @@ static uint64_t ipc_hash(const LpmKey<20> &k, const cgpu_remote_endpoint_info &v
 	return fnv(fnv(1469598103934665603ull, &k, sizeof(k)), &v, 8);
 }
 
+/* over the map contents only (not the counter slot a key happened to get),
+ * so replicas holding the same maps agree whatever their update history */
 static uint64_t pol_hash_sum(uint32_t ep, uint64_t key, const PolEntry &e)
 {
 	const uint64_t h = fnv(1469598103934665603ull ^ ep, &key, 8);
-	return fnv(h, &e.proxy_port, 2) ^ ((uint64_t)e.slot << 1);
+	return fnv(h, &e.proxy_port, 2);
 }
 
 static void ipc_touch(cgpu_ctx *c, const LpmKey<20> &k)

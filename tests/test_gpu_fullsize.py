@@ -182,5 +182,5 @@ def test_config3_fullsize(torch_cuda):
     g = e.prefilter_v6(d["saddr"], d["daddr"], d["flags"])
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_np(g), r0)
-    assert 0.4 < (r0 == L.XDP_DROP).mean() < 0.9
+    assert 0.5 < (r0 == L.XDP_DROP).mean() < 0.97  # 50% inside a deny prefix + non-endpoint daddrs
     e.close()

@@ -11,7 +11,7 @@ TAG=${1:-run}
 shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "$@" > $OUT/pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -le 1 ] || exit $rc
