@@ -36,14 +36,19 @@ def stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not stale():
+def build(force: bool = False, verbose: bool = False, defines=(), out: str = LIB) -> str:
+    """defines: extra -D flags for timing-only tool builds (tools/diag_ab.py),
+    written to another path; the product library never gets them."""
+    if out == LIB and defines:
+        raise ValueError("diagnostic defines only for a separate output path")
+    if out == LIB and not force and not stale():
         return LIB
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
+        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + (".o" if out == LIB else ".diag.o"))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+               *[f"-D{d}" for d in defines],
                "-I", os.path.join(ROOT, "include"), "-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".cpp"):
             cmd[1:1] = ["-x", "hip"]
@@ -51,15 +56,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     # RCCL (cgpu_counters_allreduce) from the ROCm install the library runs on
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,
            "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrccl"]
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     for o in objs:
         os.remove(o)
-    return LIB
+    return out
 
 
 if __name__ == "__main__":

@@ -525,6 +525,85 @@ struct PolBuild {
 	bool overloaded() const { return 2 * count + 2 > slots.size(); }
 };
 
+/* ---- policy groups (tables.h pol_groups) ---- */
+struct PgBuild {
+	std::vector<uint4> slots;
+	uint32_t mask = 0;
+	size_t count = 0;
+	static bool groupable(const PolKey &k) { return !((k.hi >> 25) & 0x7Fu); } /* pad bits 0 */
+	static uint32_t ep_dir(const PolKey &k) { return (k.z & 0xFFFFu) | (((k.hi >> 24) & 1u) << 16); }
+	/* the group slot of (id, ep | dir << 16), inserted if absent; -1: full */
+	int64_t find(uint32_t id, uint32_t ed, bool add)
+	{
+		const uint32_t home = pg_hash(id, ed) & mask;
+		const uint32_t hop = slots[home].y >> POL_HOP_SHIFT;
+		for (uint32_t d = 0; d < POL_HOP; d++) {
+			const uint4 &x = slots[(home + d) & mask];
+			if (((hop >> d) & 1u) && x.x == id && (x.y & 0x1FFFFu) == ed)
+				return (home + d) & mask;
+		}
+		if (!add)
+			return -1;
+		uint32_t d = 0;
+		while (d < POL_HOP && (slots[(home + d) & mask].y & PG_USED))
+			d++;
+		if (d == POL_HOP)
+			return -1;
+		uint4 &x = slots[(home + d) & mask];
+		x.x = id;
+		x.y = (x.y & 0xFF000000u) | ed | PG_USED;
+		x.z = POL_CTR_EMPTY;
+		x.w = 0;
+		slots[home].y |= 1u << (POL_HOP_SHIFT + d);
+		count++;
+		return (home + d) & mask;
+	}
+	/* key k (present): its bloom bits, and the counter slot of an L3 key */
+	bool add(const PolKey &k)
+	{
+		if (!groupable(k))
+			return true;
+		const int64_t g = find(k.lo, ep_dir(k), true);
+		if (g < 0)
+			return false;
+		const uint32_t dport = k.hi & 0xFFFFu, proto = (k.hi >> 16) & 0xFFu;
+		slots[g].w |= pg_bloom(dport, proto);
+		if (!dport && !proto)
+			slots[g].z = k.slot;
+		return true;
+	}
+	/* key k deleted: an L3 key leaves its group (bloom bits stay) */
+	void remove(const PolKey &k)
+	{
+		if (!groupable(k) || (k.hi & 0xFFFFFFu))
+			return;
+		const int64_t g = find(k.lo, ep_dir(k), false);
+		if (g >= 0)
+			slots[g].z = POL_CTR_EMPTY;
+	}
+	void build(const std::vector<PolKey> &keys)
+	{
+		std::set<std::pair<uint32_t, uint32_t>> groups;
+		for (auto &k : keys)
+			if (groupable(k))
+				groups.insert({k.lo, ep_dir(k)});
+		uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * groups.size() + 2));
+		for (;;) {
+			slots.assign(nb, uint4{0, 0, POL_CTR_EMPTY, 0});
+			mask = nb - 1;
+			count = 0;
+			bool ok = true;
+			for (auto &k : keys)
+				if (!(ok = add(k)))
+					break;
+			if (ok)
+				return;
+			nb *= 2;
+		}
+	}
+	bool overloaded() const { return 2 * count + 2 > slots.size(); }
+};
+
 struct Set4Build {
 	std::vector<set4_slot> slots;
 	uint32_t mask = 0, max_probe = 1;
@@ -1106,6 +1185,7 @@ struct BuildState {
 	V6Build v6;
 	bool pol_ok = false;
 	PolBuild pol;
+	PgBuild pg;
 	std::vector<uint8_t> slot_dir;
 	uint64_t sum[G_N] = {0, 0, 0, 0, 0, 0};
 };
@@ -2264,7 +2344,8 @@ static void capture_pol(cgpu_ctx *c, CommitIn &in, const BuildState &b)
 			}
 			in.pol_changes.push_back(pc);
 		}
-		if (b.pol.count + in.pol_changes.size() > b.pol.slots.size() / 2)
+		if (b.pol.count + in.pol_changes.size() > b.pol.slots.size() / 2 ||
+		    b.pg.count + in.pol_changes.size() > b.pg.slots.size() / 2)
 			in.pol_full = true; /* could pass 50 % load: grow */
 	}
 	if (in.pol_full) {
@@ -2407,7 +2488,7 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	return 0;
 }
 
-/* group POL: the policy hash + per-counter-slot direction */
+/* group POL: the policy hash, its groups and per-counter-slot direction */
 static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 {
 	BuildState &b = c->b;
@@ -2416,7 +2497,10 @@ static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		for (auto &ch : in.pol_changes) {
 			const uint32_t lo = (uint32_t)ch.key, hi = (uint32_t)(ch.key >> 32);
 			b.pol.erase(lo, hi, ch.ep);
-			if (ch.present && !b.pol.insert(pol_key_of(ch.ep, ch.key, ch.e))) {
+			const PolKey k = pol_key_of(ch.ep, ch.key, ch.e);
+			if (!ch.present) {
+				b.pg.remove(k);
+			} else if (!b.pol.insert(k) || !b.pg.add(k) || b.pg.overloaded()) {
 				full = true; /* a full neighbourhood: rebuild from the mirror */
 				break;
 			}
@@ -2430,6 +2514,7 @@ static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 					in.pol_keys.push_back(pol_key_of(ep, kv.first, kv.second));
 		}
 		b.pol.build(in.pol_keys);
+		b.pg.build(in.pol_keys);
 		b.slot_dir.assign(c->n_ctr_slots, 0);
 		for (auto &k : in.pol_keys)
 			b.slot_dir[k.slot] = key_dir((uint64_t)k.hi << 32 | k.lo);
@@ -2443,10 +2528,12 @@ static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	}
 	Arena ar;
 	const size_t o_p = ar.add(b.pol.slots.data(), b.pol.slots.size() * sizeof(pol_slot));
+	const size_t o_g = ar.add(b.pg.slots.data(), b.pg.slots.size() * sizeof(uint4));
 	const size_t o_s = ar.add(b.slot_dir.data(), b.slot_dir.size());
 	if (int r = upload(c, ar, buf))
 		return r;
 	s.pol = pol_table{at<pol_slot>(buf, o_p), b.pol.mask, 0};
+	s.pg = pol_groups{at<uint4>(buf, o_g), b.pg.mask, 0};
 	s.slot_dir = at<uint8_t>(buf, o_s);
 	b.sum[G_POL] = in.sum_pol;
 	return 0;

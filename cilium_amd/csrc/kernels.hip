@@ -169,6 +169,28 @@ __device__ __forceinline__ int pol_lookup(const pol_table &t, uint32_t lo, uint3
 	return pol_resolve1(t, reinterpret_cast<const uint4 *>(t.slots)[b], b, lo, hi, ep, z);
 }
 
+/* The group slot of {id, ep | dir << 16} whose home slot g (index b) is in
+ * registers (tables.h pol_groups), or {0, 0, EMPTY, 0} when the endpoint's
+ * map holds no key of that identity and direction. */
+__device__ __forceinline__ uint4 pg_resolve(const pol_groups &t, uint4 g, uint32_t b, uint32_t id, uint32_t ed)
+{
+	uint32_t hop = g.y >> POL_HOP_SHIFT;
+	if ((hop & 1u) && g.x == id && (g.y & 0x1FFFFu) == ed)
+		return g;
+	hop &= ~1u;
+	uint4 r = make_uint4(0, 0, POL_CTR_EMPTY, 0);
+	while (hop) {
+		const uint32_t j = __builtin_ctz(hop);
+		hop &= hop - 1u;
+		const uint4 x = t.slots[(b + j) & t.mask];
+		if (x.x == id && (x.y & 0x1FFFFu) == ed) {
+			r = x;
+			break;
+		}
+	}
+	return r;
+}
+
 __device__ __forceinline__ bool set4_has(const addr_set4 &t, uint32_t a)
 {
 	uint32_t b = mix32(a, 0x5e7) & t.bucket_mask;
@@ -910,6 +932,24 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 #define PKC_MAX_LEN (1u << 11)
 #define PKC_CHUNK (1ull << 26)
 
+/* timing-only tool builds (tools/diag_ab.py; wrong results): confine a
+ * gather to the first 1024 entries of its table, i.e. make it an L2 hit */
+#ifdef CGPU_DIAG_P1_SMALL
+#define DIAG_P1(b) ((b) & 1023u)
+#else
+#define DIAG_P1(b) (b)
+#endif
+#ifdef CGPU_DIAG_P2_SMALL
+#define DIAG_P2(b) ((b) & 1023u)
+#else
+#define DIAG_P2(b) (b)
+#endif
+#ifdef CGPU_DIAG_LPM_SMALL
+#define DIAG_LPM(b) ((b) & 1023u)
+#else
+#define DIAG_LPM(b) (b)
+#endif
+
 /*
  * IPv4 classification, four consecutive tuples per lane per step.
  * Same semantics as k_classify<0, 1, NT> (the reference cascade of
@@ -1077,7 +1117,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 			for (int u = 0; u < Q; u++) {
 				q[u] = make_uint4(0, 0, 0, 0);
 				if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK)
-					q[u] = reinterpret_cast<const uint4 *>(s.ipc4c.x16)[bswap32(ad[u]) >> 16];
+					q[u] = reinterpret_cast<const uint4 *>(s.ipc4c.x16)[DIAG_LPM(bswap32(ad[u]) >> 16)];
 			}
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
@@ -1157,38 +1197,56 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				id[u] = s.ingress_secctx_world ? s.world_id : src;
 			}
 		}
-		/* probe 1: exact {id, dport, proto, dir} (policy.h:61-72) */
+		/* The cascade of policy.h:46-110 over the group of {ep, id, dir}
+		 * (tables.h pol_groups): one gather of the group slot gives probe 2
+		 * (the L3 key) and a bloom over the group's (dport, proto); probe 1
+		 * gathers the exact key only when the bloom admits it; probe 3
+		 * (identity 0) gathers directly.  Stages and counters are the
+		 * reference's: st = the probe that hit. */
 		int ctr[Q];
-		uint32_t z[Q], st[Q], bk[Q];
-		uint4 sl[Q];
+		uint32_t z[Q], st[Q], bk[Q], need[Q];
+		uint4 sl[Q], grp[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			ctr[u] = -1;
 			z[u] = 0;
 			st[u] = 0;
-			if ((fw[u] & (F_OK | F_GATED | F_LBDROP | F_FRAG)) == F_OK) {
-				bk[u] = pol_hash(id[u], hi4[u], ep[u]) & pmask;
-				sl[u] = ptab[bk[u]];
+			grp[u] = make_uint4(0, 0, POL_CTR_EMPTY, 0);
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK) {
+				bk[u] = pg_hash(id[u], ep[u] | (hi4[u] >> 24) << 16) & s.pg.mask;
+				grp[u] = s.pg.slots[DIAG_P2(bk[u])];
 			}
 		}
 #pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) != F_OK)
+				continue;
+			grp[u] = pg_resolve(s.pg, grp[u], bk[u], id[u], ep[u] | (hi4[u] >> 24) << 16);
+			const uint32_t bl = pg_bloom(hi4[u] & 0xFFFFu, (hi4[u] >> 16) & 0xFFu);
+			need[u] = !(fw[u] & F_FRAG) && (grp[u].w & bl) == bl;
+		}
+		/* probe 1: exact {id, dport, proto, dir} (policy.h:61-72) */
+#pragma unroll
 		for (int u = 0; u < Q; u++)
-			if ((fw[u] & (F_OK | F_GATED | F_LBDROP | F_FRAG)) == F_OK) {
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK && need[u]) {
+				bk[u] = pol_hash(id[u], hi4[u], ep[u]) & pmask;
+				sl[u] = ptab[DIAG_P1(bk[u])];
+			}
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK && need[u]) {
 				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u], ep[u], &z[u]);
 				st[u] = 1;
 			}
-		/* probe 2: L3-only {id, 0, 0, dir} (policy.h:74-83) */
+		/* probe 2: L3-only {id, 0, 0, dir} (policy.h:74-83), from the group */
 #pragma unroll
 		for (int u = 0; u < Q; u++)
 			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK && ctr[u] < 0) {
-				bk[u] = pol_hash(id[u], hi4[u] & (1u << 24), ep[u]) & pmask;
-				sl[u] = ptab[bk[u]];
-			}
-#pragma unroll
-		for (int u = 0; u < Q; u++)
-			if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK && ctr[u] < 0) {
-				ctr[u] = pol_resolve1(s.pol, sl[u], bk[u], id[u], hi4[u] & (1u << 24), ep[u], &z[u]);
 				st[u] = 2;
+				if ((grp[u].z & POL_CTR_MASK) != POL_CTR_EMPTY) {
+					ctr[u] = (int)(grp[u].z & POL_CTR_MASK);
+					z[u] = 0;
+				}
 			}
 		/* probe 3: identity-wildcard L4 {0, dport, proto, dir} (policy.h:85-96) */
 #pragma unroll
@@ -1227,8 +1285,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
 				} else {
+#ifndef CGPU_DIAG_NO_COLD /* timing-only tool build (tools/diag_ab.py): counters wrong */
 					atomicAdd((unsigned long long *)&pk[c],
 						  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
+#endif
 				}
 				v[u] = st[u] == 2 ? 0 : (int32_t)(z[u] >> 16);
 			} else {

@@ -72,6 +72,16 @@ typedef struct lpm16c {
 	uint32_t n_dict;
 } lpm16c;
 
+/* 32-bit mixer of two words (hash tables below) */
+static inline __host__ __device__ uint32_t mix32(uint32_t a, uint32_t b)
+{
+	uint64_t h = ((uint64_t)b << 32 | a) * 0x9E3779B97F4A7C15ull;
+	h ^= h >> 29;
+	h *= 0xbf58476d1ce4e5b9ull;
+	h ^= h >> 32;
+	return (uint32_t)h;
+}
+
 /* ---- policy hash: one open-addressing table for all endpoints ----
  * 16-byte slots {x = sec_label, y = dport | proto << 16 | egress_pad << 24,
  * z = ep | proxy_port << 16, w = counter slot | hop << 24}.  (x, y) is the
@@ -100,6 +110,40 @@ typedef struct pol_table {
 	uint32_t bucket_mask;
 	uint32_t pad_;
 } pol_table;
+
+/* ---- policy groups: one 16-B slot per (endpoint, identity, direction) ----
+ * The reference's cascade (bpf/lib/policy.h:46-110) keys probe 1 and probe 2
+ * on the same {identity, direction} of one endpoint's map: probe 2 is the
+ * L3-only key {id, 0, 0, dir}, probe 1 the exact {id, dport, proto, dir}.
+ * A group slot answers probe 2 directly (the L3 key's counter slot) and
+ * filters probe 1 with a bloom over the (dport, proto) of the group's keys,
+ * so the exact-key table is gathered only when a key may exist:
+ *   x = sec_label, y = ep | egress << 16 | PG_USED | hop << 24,
+ *   z = counter slot of the L3 key (POL_CTR_EMPTY: none), w = bloom.
+ * Neighbourhood hashing as the policy table.  Only keys with pad bits 0 are
+ * grouped (a datapath lookup key always has pad 0).  A bloom bit is never
+ * cleared by a delete (a stale bit costs one exact probe, never a verdict);
+ * a full rebuild recomputes them. */
+#define PG_EGRESS (1u << 16)
+#define PG_USED (1u << 17)
+
+typedef struct pol_groups {
+	const uint4 *slots; /* mask + 1 slots */
+	uint32_t mask;
+	uint32_t pad_;
+} pol_groups;
+
+static inline __host__ __device__ uint32_t pg_hash(uint32_t id, uint32_t ep_dir)
+{
+	return mix32(id, ep_dir ^ 0x6a09e667u);
+}
+
+/* the two bloom bits of a (network-order dport, proto) pair */
+static inline __host__ __device__ uint32_t pg_bloom(uint32_t dport, uint32_t proto)
+{
+	const uint32_t h = mix32(dport | proto << 16, 0x3c6ef372u);
+	return (1u << (h & 31u)) | (1u << ((h >> 8) & 31u));
+}
 
 static inline __host__ __device__ uint32_t pol_hash(uint32_t key_lo, uint32_t key_hi, uint32_t ep)
 {
@@ -137,15 +181,6 @@ typedef struct addr_set16 {
 	uint32_t bucket_mask;
 	uint32_t max_probe;
 } addr_set16;
-
-static inline __host__ __device__ uint32_t mix32(uint32_t a, uint32_t b)
-{
-	uint64_t h = ((uint64_t)b << 32 | a) * 0x9E3779B97F4A7C15ull;
-	h ^= h >> 29;
-	h *= 0xbf58476d1ce4e5b9ull;
-	h ^= h >> 32;
-	return (uint32_t)h;
-}
 
 static inline __host__ __device__ uint32_t hash16(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
 						  uint32_t salt)
@@ -267,7 +302,8 @@ typedef struct cover6 {
 /* ---- one committed snapshot ---- */
 typedef struct cgpu_snapshot {
 	lpm16c ipc4c;    /* ipcache, IPv4 lookups (compiled from a host DIR-24-8) */
-	pol_table pol;
+	pol_table pol;   /* every policy key (probe 1 / 3 gathers) */
+	pol_groups pg;   /* per (ep, identity, dir): probe 2 + probe 1 filter */
 	lpm16c pf4c;     /* any-match: dyn4 (if enabled) + fix4 /32; leaves 0 / 1 */
 	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
 	addr_set16 ep6;  /* cilium_lxc IPv6 keys */

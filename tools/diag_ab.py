@@ -1,0 +1,77 @@
+"""Timing-only A/B of diagnostic builds of the classify kernel (never the
+product library: these builds drop work and give wrong counters).
+
+    python tools/diag_ab.py build            # in the dev container: tools/_diag/*.so
+    python tools/diag_ab.py run [variants]   # on the GPU box
+
+Each variant is cilium_amd/csrc compiled with extra -D flags into
+tools/_diag/libcgpu_<name>.so; `run` loads each in turn into the Engine
+(cilium_amd._abi's loader is pointed at it), commits the config-2 tables and
+times 10 launches of the 64M-tuple batch with HIP events."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+DIAG = os.path.join(ROOT, "tools", "_diag")
+VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
+            "nc_p1_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_P1_SMALL"),
+            "nc_p2_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_P2_SMALL"),
+            "nc_lpm_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_LPM_SMALL"),
+            "nc_all_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_P1_SMALL", "CGPU_DIAG_P2_SMALL",
+                          "CGPU_DIAG_LPM_SMALL")}
+
+
+def build(names):
+    from cilium_amd import build as b
+    os.makedirs(DIAG, exist_ok=True)
+    for n in names:
+        if n != "product":
+            b.build(force=True, defines=VARIANTS[n], out=os.path.join(DIAG, f"libcgpu_{n}.so"))
+
+
+def load(name):
+    from cilium_amd import _abi
+    path = _abi.LIB_PATH if name == "product" else os.path.join(DIAG, f"libcgpu_{name}.so")
+    L = C.CDLL(path)
+    for fn, (res, args) in _abi.PROTOS.items():
+        f = getattr(L, fn)
+        f.restype, f.argtypes = res, args
+    _abi._lib = L
+
+
+def run(names):
+    import torch
+    from cilium_amd import synth
+    T = synth.make_tables(**synth.CONFIGS["gpu"])
+    t = synth.make_tuples(T, synth.CONFIGS["gpu"]["n_tuples"])
+    d = synth.to_device(t)
+    n = len(t["saddr"])
+    out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+           "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
+    for name in names:
+        load(name)
+        from cilium_amd.engine import Engine
+        e = Engine(device=0, **T.engine_config())
+        synth.load_engine(e, T)
+        e.commit()
+        for _ in range(3):
+            e.classify_v4(d, out=out)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        for a, b in ev:
+            a.record()
+            e.classify_v4(d, out=out)
+            b.record()
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)
+        print(json.dumps({"variant": name, "median_ms": round(ms[5], 4), "min_ms": round(ms[0], 4),
+                          "gpps": round(n / ms[5] / 1e6, 2)}), flush=True)
+        e.close()
+
+
+if __name__ == "__main__":
+    names = sys.argv[2:] or list(VARIANTS)
+    (build if sys.argv[1] == "build" else run)(names)
