@@ -99,6 +99,9 @@ PROTOS = {
     "cgpu_cidr_lookup": (i32, [vp, i32, vp]),
     "cgpu_cidr_get_next_key": (i32, [vp, i32, vp, vp]),
     "cgpu_cidr_update_batch": (i32, [vp, i32, vp, sz, u64]),
+    "cgpu_prefilter_insert": (i32, [vp, C.c_int64, vp, sz]),
+    "cgpu_prefilter_delete": (i32, [vp, C.c_int64, vp, sz]),
+    "cgpu_prefilter_revision": (i32, [vp, C.POINTER(C.c_int64)]),
     "cgpu_endpoint_update": (i32, [vp, vp, u64]),
     "cgpu_endpoint_delete": (i32, [vp, vp]),
     "cgpu_endpoint_lookup": (i32, [vp, vp]),

@@ -1224,6 +1224,7 @@ struct cgpu_ctx {
 	std::map<uint64_t, cgpu_lb4_service> lb;
 	/* per-endpoint lxc_config.h identity (cgpu_lxc_update) */
 	std::map<uint32_t, cgpu_lxc_info> lxcinfo;
+	int64_t pf_revision = 1; /* PreFilter revision (pkg/policy/prefilter.go:283) */
 	/* ---- change tracking since the last captured commit ---- */
 	uint32_t dirty = 0;             /* 1 << G_* */
 	bool ipc_full = true, pol_full = true;
@@ -1822,13 +1823,9 @@ CGPU_EXPORT size_t cgpu_policy_count(cgpu_ctx *c, uint32_t ep)
 /* ======================================================================= */
 /* prefilter CIDR maps + endpoint map                                        */
 /* ======================================================================= */
-CGPU_EXPORT int cgpu_cidr_update(cgpu_ctx *c, int which, const cgpu_cidr_key *key, uint64_t flags)
+/* the map operations with mu held (cgpu_prefilter_* runs several under one lock) */
+static int cidr_update_l(cgpu_ctx *c, int which, const cgpu_cidr_key *key, uint64_t flags)
 {
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	std::lock_guard<std::mutex> g(c->mu);
 	bool exists;
 	switch (which) {
 	case CGPU_CIDR_V4_DYN:
@@ -1881,11 +1878,18 @@ CGPU_EXPORT int cgpu_cidr_update(cgpu_ctx *c, int which, const cgpu_cidr_key *ke
 	return fail(-EINVAL, "bad cidr map %d", which);
 }
 
-CGPU_EXPORT int cgpu_cidr_delete(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+CGPU_EXPORT int cgpu_cidr_update(cgpu_ctx *c, int which, const cgpu_cidr_key *key, uint64_t flags)
 {
 	if (!c || !key)
 		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
 	std::lock_guard<std::mutex> g(c->mu);
+	return cidr_update_l(c, which, key, flags);
+}
+
+static int cidr_delete_l(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+{
 	size_t n = 0;
 	switch (which) {
 	case CGPU_CIDR_V4_DYN:
@@ -1916,11 +1920,16 @@ CGPU_EXPORT int cgpu_cidr_delete(cgpu_ctx *c, int which, const cgpu_cidr_key *ke
 	return n ? 0 : -ENOENT;
 }
 
-CGPU_EXPORT int cgpu_cidr_lookup(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+CGPU_EXPORT int cgpu_cidr_delete(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
 {
 	if (!c || !key)
 		return fail(-EINVAL, "null argument");
 	std::lock_guard<std::mutex> g(c->mu);
+	return cidr_delete_l(c, which, key);
+}
+
+static int cidr_lookup_l(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+{
 	switch (which) {
 	case CGPU_CIDR_V4_DYN:
 		for (int64_t p = std::min<uint32_t>(key->prefixlen, 32); p >= 0; p--)
@@ -1944,6 +1953,107 @@ CGPU_EXPORT int cgpu_cidr_lookup(cgpu_ctx *c, int which, const cgpu_cidr_key *ke
 	}
 	}
 	return fail(-EINVAL, "bad cidr map %d", which);
+}
+
+CGPU_EXPORT int cgpu_cidr_lookup(cgpu_ctx *c, int which, const cgpu_cidr_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	return cidr_lookup_l(c, which, key);
+}
+
+/* ---- PreFilter (pkg/policy/prefilter.go:30-203) over the four maps ---- */
+/* selectMap (prefilter.go:108-122): /32 and /128 to the exact maps, shorter
+ * prefixes to the LPM maps; -1: no such map enabled (maps exist iff their
+ * config switch is on, prefilter.go:206-250; the v6 exact map follows its
+ * own switch, not fix4 as the reference's initOneMap does, :237) */
+static int prefilter_select(const cgpu_ctx *c, const cgpu_prefix &p)
+{
+	int which;
+	if (p.bits == 32)
+		which = p.key.prefixlen == 32 ? CGPU_CIDR_V4_FIX : CGPU_CIDR_V4_DYN;
+	else if (p.bits == 128)
+		which = p.key.prefixlen == 128 ? CGPU_CIDR_V6_FIX : CGPU_CIDR_V6_DYN;
+	else
+		return -1;
+	const bool on[4] = {c->cfg.prefilter_dyn4 != 0, c->cfg.prefilter_fix4 != 0,
+			    c->cfg.prefilter_dyn6 != 0, c->cfg.prefilter_fix6 != 0};
+	return on[which] ? which : -1;
+}
+
+CGPU_EXPORT int cgpu_prefilter_insert(cgpu_ctx *c, int64_t revision, const cgpu_prefix *cidrs, size_t n)
+{
+	if (!c || (n && !cidrs))
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (revision != 0 && c->pf_revision != revision)
+		return fail(-ESTALE, "Latest revision is %lld not %lld", (long long)c->pf_revision,
+			    (long long)revision);
+	size_t done = 0;
+	int rc = 0;
+	for (; done < n; done++) {
+		const int which = prefilter_select(c, cidrs[done]);
+		if (which < 0) {
+			rc = fail(-EOPNOTSUPP, "No map enabled for CIDR %zu", done);
+			break;
+		}
+		if ((rc = cidr_update_l(c, which, &cidrs[done].key, CGPU_ANY)) != 0)
+			break;
+	}
+	if (!rc) {
+		c->pf_revision++;
+		return 0;
+	}
+	const std::string msg = g_last_error;
+	for (size_t i = 0; i < done; i++) /* undo (prefilter.go:152-156) */
+		(void)cidr_delete_l(c, prefilter_select(c, cidrs[i]), &cidrs[i].key);
+	g_last_error = msg;
+	return rc;
+}
+
+CGPU_EXPORT int cgpu_prefilter_delete(cgpu_ctx *c, int64_t revision, const cgpu_prefix *cidrs, size_t n)
+{
+	if (!c || (n && !cidrs))
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (revision != 0 && c->pf_revision != revision)
+		return fail(-ESTALE, "Latest revision is %lld not %lld", (long long)c->pf_revision,
+			    (long long)revision);
+	/* the obvious cases first, so nothing needs unrolling (prefilter.go:171-181):
+	 * CIDRExists is a map lookup, longest-prefix on the LPM maps */
+	for (size_t i = 0; i < n; i++) {
+		const int which = prefilter_select(c, cidrs[i]);
+		if (which < 0)
+			return fail(-EOPNOTSUPP, "No map enabled for CIDR %zu", i);
+		if (cidr_lookup_l(c, which, &cidrs[i].key) != 0)
+			return fail(-ENOENT, "No map entry for CIDR %zu", i);
+	}
+	size_t done = 0;
+	int rc = 0;
+	for (; done < n; done++)
+		if ((rc = cidr_delete_l(c, prefilter_select(c, cidrs[done]), &cidrs[done].key)) != 0) {
+			rc = fail(rc, "Error deleting CIDR %zu", done);
+			break;
+		}
+	if (!rc) {
+		c->pf_revision++;
+		return 0;
+	}
+	const std::string msg = g_last_error;
+	for (size_t i = 0; i < done; i++) /* undo (prefilter.go:196-200) */
+		(void)cidr_update_l(c, prefilter_select(c, cidrs[i]), &cidrs[i].key, CGPU_ANY);
+	g_last_error = msg;
+	return rc;
+}
+
+CGPU_EXPORT int cgpu_prefilter_revision(cgpu_ctx *c, int64_t *revision_out)
+{
+	if (!c || !revision_out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	*revision_out = c->pf_revision;
+	return 0;
 }
 
 CGPU_EXPORT int cgpu_cidr_get_next_key(cgpu_ctx *c, int which, const cgpu_cidr_key *key,

@@ -1303,8 +1303,19 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 			}
 		}
 		if (full && Q == 4) {
+#ifdef CGPU_DIAG_STORE_SC1 /* write-through stores that leave the XCD's L2 */
+			{
+				const auto rv = __builtin_amdgcn_make_buffer_rsrc(a.verdict, 0, (int)(a.n * 4u), 0x00020000);
+				const auto ri = __builtin_amdgcn_make_buffer_rsrc(a.identity, 0, (int)(a.n * 4u), 0x00020000);
+				v4u_t vv = {(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]};
+				v4u_t vi = {id[0], id[1], id[2], id[3]};
+				__builtin_amdgcn_raw_buffer_store_b128(vv, rv, (int)(i0 * 4u), 0, 16);
+				__builtin_amdgcn_raw_buffer_store_b128(vi, ri, (int)(i0 * 4u), 0, 16);
+			}
+#else
 			st_x4<NTL>(a.verdict + i0, (uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
 			st_x4<NTL>(a.identity + i0, id[0], id[1], id[2], id[3]);
+#endif
 			if (a.stage)
 				st_x1<NTL>(a.stage + i0, st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24));
 		} else if (full && Q == 2) {
@@ -2121,7 +2132,10 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 {
 	constexpr int NT = 1024;
 	/* LDS: hot counters + the ipcache leaf dictionary */
-	const size_t lds = (size_t)s.hot_slots * 8u + (size_t)s.ipc4c.n_dict * 4u;
+	size_t lds = (size_t)s.hot_slots * 8u + (size_t)s.ipc4c.n_dict * 4u;
+#ifdef CGPU_DIAG_LDS_PAD /* timing-only: fewer resident workgroups per CU */
+	lds += CGPU_DIAG_LDS_PAD;
+#endif
 	const void *kern = (const void *)k_classify_v4_x4<NT, true, 4, 1, LB>;
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */

@@ -619,6 +619,52 @@ class CIDRMap:
         return out
 
 
+class PreFilter:
+    """pkg/policy/prefilter.go PreFilter (Insert / Delete / Dump with the
+    revision check, selectMap routing and undo), over cgpu_prefilter_*.
+    CIDRs are strings; IPv4 ones go to the v4 maps (net.IPNet mask of 32
+    bits), IPv6 ones to the v6 maps."""
+
+    PREFIX = np.dtype([("bits", "<u4"), ("prefixlen", "<u4"), ("addr", "u1", (16,))])
+
+    def __init__(self, engine: Engine):
+        self.e = engine
+
+    @classmethod
+    def _prefixes(cls, cidrs):
+        out = np.zeros(len(cidrs), cls.PREFIX)
+        for i, c in enumerate(cidrs):
+            net = ipaddress.ip_network(c, strict=False)
+            raw = net.network_address.packed
+            out[i]["bits"] = net.max_prefixlen
+            out[i]["prefixlen"] = net.prefixlen
+            out[i]["addr"][:len(raw)] = np.frombuffer(raw, np.uint8)
+        return out
+
+    def Insert(self, revision: int, cidrs):  # noqa: N802
+        p = self._prefixes(cidrs)
+        check(self.e.L.cgpu_prefilter_insert(self.e.h, revision, p.ctypes.data, len(p)),
+              "PreFilter.Insert")
+
+    def Delete(self, revision: int, cidrs):  # noqa: N802
+        p = self._prefixes(cidrs)
+        check(self.e.L.cgpu_prefilter_delete(self.e.h, revision, p.ctypes.data, len(p)),
+              "PreFilter.Delete")
+
+    def Revision(self) -> int:  # noqa: N802
+        r = C.c_int64()
+        check(self.e.L.cgpu_prefilter_revision(self.e.h, C.byref(r)), "PreFilter.Revision")
+        return r.value
+
+    def Dump(self):  # noqa: N802
+        """(CIDR strings of the maps in prefilter.go order v4 dyn, v4 fix,
+        v6 dyn, v6 fix; revision)"""
+        out = []
+        for which in (CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX):
+            out += CIDRMap(self.e, which).CIDRDump()
+        return out, self.Revision()
+
+
 class LBMap:
     """pkg/maps/lbmap over cilium_lb4_services (IPv4): the frontend/backend
     writes of UpdateService (lbmap.go:350-428: backends at slaves 1..n, then

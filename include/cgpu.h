@@ -235,6 +235,27 @@ int cgpu_cidr_get_next_key(cgpu_ctx *ctx, int which, const cgpu_cidr_key *key,
 /* n InsertCIDR writes in order (stops at the first failure) */
 int cgpu_cidr_update_batch(cgpu_ctx *ctx, int which, const cgpu_cidr_key *keys, size_t n,
 			   uint64_t flags);
+/* PreFilter (pkg/policy/prefilter.go:30-203): the revisioned CIDR set the
+ * agent's PATCH/DELETE /prefilter handlers drive (daemon/prefilter.go).
+ * A prefix carries its address family as the mask size of net.IPNet
+ * (bits 32 / 128).  selectMap (prefilter.go:108-122) routes /32 and /128 to
+ * the exact ("fix") maps and shorter prefixes to the LPM ("dyn") maps; a map
+ * whose cgpu_config switch is off does not exist (-EOPNOTSUPP, "No map
+ * enabled").  revision != 0 must equal the current revision (else -ESTALE,
+ * "Latest revision is ..."); it starts at 1 and each successful call adds 1.
+ * insert: every prefix or none -- on the first failure the prefixes already
+ * inserted are deleted again (prefilter.go:124-159).  delete: every prefix
+ * must exist first (a map lookup: longest-prefix on the LPM maps, -ENOENT
+ * before anything changed); a later failure re-inserts the deleted ones
+ * (:161-203).  The map contents reach the device at cgpu_commit. */
+typedef struct cgpu_prefix {
+	uint32_t bits; /* 32: IPv4, 128: IPv6 */
+	cgpu_cidr_key key;
+} cgpu_prefix;
+int cgpu_prefilter_insert(cgpu_ctx *ctx, int64_t revision, const cgpu_prefix *cidrs, size_t n);
+int cgpu_prefilter_delete(cgpu_ctx *ctx, int64_t revision, const cgpu_prefix *cidrs, size_t n);
+int cgpu_prefilter_revision(cgpu_ctx *ctx, int64_t *revision_out);
+
 int cgpu_endpoint_update(cgpu_ctx *ctx, const cgpu_endpoint_key *key, uint64_t flags);
 int cgpu_endpoint_delete(cgpu_ctx *ctx, const cgpu_endpoint_key *key);
 int cgpu_endpoint_lookup(cgpu_ctx *ctx, const cgpu_endpoint_key *key);

@@ -335,3 +335,53 @@ def test_batch_ops_and_dump_host_only():
     assert e.cidr_update_batch(CIDR_V6_DYN, ck) == 0
     assert len(e.cidr_keys(CIDR_V6_DYN)) == 4
     e.close()
+
+
+def test_prefilter_revision_routing_and_undo():
+    """pkg/policy/prefilter.go: selectMap routes /32 and /128 to the exact
+    maps and shorter prefixes to the LPM maps; a stale revision is refused;
+    a failed Insert leaves nothing behind and a failed Delete re-inserts
+    what it removed; Delete checks existence first (LPM lookup)."""
+    from cilium_amd.engine import PreFilter
+    e = Engine(device=-1, cidr_fix_max=3)
+    pf = PreFilter(e)
+    assert pf.Revision() == 1
+    pf.Insert(1, ["10.0.0.0/8", "192.168.1.1/32", "2001:db8::/32", "2001:db8::1/128"])
+    assert pf.Revision() == 2
+    assert CIDRMap(e, CIDR_V4_DYN).CIDRDump() == ["10.0.0.0/8"]
+    assert CIDRMap(e, CIDR_V4_FIX).CIDRDump() == ["192.168.1.1/32"]
+    assert CIDRMap(e, CIDR_V6_DYN).CIDRDump() == ["2001:db8::/32"]
+    assert CIDRMap(e, CIDR_V6_FIX).CIDRDump() == ["2001:db8::1/128"]
+    with pytest.raises(OSError) as ex:
+        pf.Insert(1, ["10.1.0.0/16"])  # revision 1 is stale
+    assert ex.value.errno == errno.ESTALE and "Latest revision is 2 not 1" in str(ex.value)
+    pf.Insert(0, ["10.1.0.0/16"])  # revision 0: no check
+    assert pf.Revision() == 3
+    # fix4 holds at most 3 keys: the 3rd /32 fails, the two before it are undone
+    with pytest.raises(OSError) as ex:
+        pf.Insert(3, ["172.16.0.1/32", "172.16.0.2/32", "172.16.0.3/32", "172.16.9.0/24"])
+    assert ex.value.errno == errno.E2BIG
+    assert CIDRMap(e, CIDR_V4_FIX).CIDRDump() == ["192.168.1.1/32"]
+    assert CIDRMap(e, CIDR_V4_DYN).CIDRDump() == ["10.0.0.0/8", "10.1.0.0/16"]
+    assert pf.Revision() == 3
+    # Delete: existence first; a /24 under 10.0.0.0/8 "exists" (LPM lookup)
+    # but its exact delete fails, so the /16 removed before it comes back
+    with pytest.raises(OSError) as ex:
+        pf.Delete(3, ["10.1.0.0/16", "10.2.3.0/24"])
+    assert ex.value.errno == errno.ENOENT
+    assert CIDRMap(e, CIDR_V4_DYN).CIDRDump() == ["10.0.0.0/8", "10.1.0.0/16"]
+    with pytest.raises(OSError) as ex:
+        pf.Delete(3, ["10.1.0.0/16", "11.0.0.0/8"])  # 11/8 missing: nothing deleted
+    assert ex.value.errno == errno.ENOENT
+    pf.Delete(3, ["10.1.0.0/16", "2001:db8::1/128"])
+    assert pf.Revision() == 4
+    dump, rev = pf.Dump()
+    assert dump == ["10.0.0.0/8", "192.168.1.1/32", "2001:db8::/32"] and rev == 4
+    e.close()
+    # the reference's default config disables the LPM maps (prefilter.go:284-289)
+    e2 = Engine(device=-1, prefilter_dyn4=0, prefilter_dyn6=0)
+    with pytest.raises(OSError) as ex:
+        PreFilter(e2).Insert(0, ["10.0.0.0/8"])
+    assert ex.value.errno == errno.EOPNOTSUPP
+    PreFilter(e2).Insert(0, ["10.0.0.1/32"])
+    e2.close()

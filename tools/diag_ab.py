@@ -22,7 +22,9 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "nc_p2_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_P2_SMALL"),
             "nc_lpm_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_LPM_SMALL"),
             "nc_all_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_P1_SMALL", "CGPU_DIAG_P2_SMALL",
-                          "CGPU_DIAG_LPM_SMALL")}
+                          "CGPU_DIAG_LPM_SMALL"),
+            "one_wg_per_cu": ("CGPU_DIAG_LDS_PAD=65536",),
+            "store_sc1": ("CGPU_DIAG_STORE_SC1",)}
 
 
 def build(names):
