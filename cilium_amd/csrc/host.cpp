@@ -1186,7 +1186,6 @@ struct BuildState {
 	bool pol_ok = false;
 	PolBuild pol;
 	PgBuild pg;
-	std::vector<uint8_t> slot_dir;
 	uint64_t sum[G_N] = {0, 0, 0, 0, 0, 0};
 };
 
@@ -2324,7 +2323,6 @@ struct CommitIn {
 	uint64_t sum_ipc = 0, sum_pol = 0;
 };
 
-static uint8_t key_dir(uint64_t key) { return ((key >> 56) & 1u) ? 2 : 1; }
 
 static PolKey pol_key_of(uint32_t ep, uint64_t key, const PolEntry &e)
 {
@@ -2598,7 +2596,7 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	return 0;
 }
 
-/* group POL: the policy hash, its groups and per-counter-slot direction */
+/* group POL: the policy hash and its groups */
 static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 {
 	BuildState &b = c->b;
@@ -2625,26 +2623,15 @@ static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		}
 		b.pol.build(in.pol_keys);
 		b.pg.build(in.pol_keys);
-		b.slot_dir.assign(c->n_ctr_slots, 0);
-		for (auto &k : in.pol_keys)
-			b.slot_dir[k.slot] = key_dir((uint64_t)k.hi << 32 | k.lo);
 		b.pol_ok = true;
-	} else {
-		if (b.slot_dir.size() != c->n_ctr_slots)
-			b.slot_dir.assign(c->n_ctr_slots, 0);
-		for (auto &ch : in.pol_changes)
-			if (ch.present)
-				b.slot_dir[ch.e.slot] = key_dir(ch.key);
 	}
 	Arena ar;
 	const size_t o_p = ar.add(b.pol.slots.data(), b.pol.slots.size() * sizeof(pol_slot));
 	const size_t o_g = ar.add(b.pg.slots.data(), b.pg.slots.size() * sizeof(uint4));
-	const size_t o_s = ar.add(b.slot_dir.data(), b.slot_dir.size());
 	if (int r = upload(c, ar, buf))
 		return r;
 	s.pol = pol_table{at<pol_slot>(buf, o_p), b.pol.mask, 0};
 	s.pg = pol_groups{at<uint4>(buf, o_g), b.pg.mask, 0};
-	s.slot_dir = at<uint8_t>(buf, o_s);
 	b.sum[G_POL] = in.sum_pol;
 	return 0;
 }

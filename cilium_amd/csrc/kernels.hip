@@ -885,7 +885,8 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		a.identity[i] = id;
 		if (a.stage)
 			a.stage[i] = (uint8_t)st;
-		const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_NO_SERVICE ? 3u : 2u));
+		/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
+		const uint32_t r = v > 0 ? 4u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_NO_SERVICE ? 3u : 2u));
 		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
 #pragma unroll
 		for (int k = 0; k < 8; k++) {
@@ -971,11 +972,14 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 	/* per-tuple flag word */
 	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u, F_LBDROP = 32u;
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
-	/* metrics (drop.h:94-118) kept here only for drops and long forwarded
-	 * packets: [reason 0 / 133 / 137][ingress, egress] x {count, bytes};
-	 * every other forwarded packet is counted by k_unpack from pk, per the
-	 * direction of the entry it hit (metrics of the verdict = its entry's) */
+	/* drop metrics (send_drop_notify -> update_metrics, drop.h:94-118):
+	 * [reason 133 / 137 / 158][ingress, egress] x {count, bytes} in LDS
+	 * (index 0..3 unused); forwards (verdict 0: TRACE_TO_LXC / _STACK,
+	 * trace.h) per lane in registers, wave-reduced at the end; a proxy
+	 * redirect (verdict > 0, TRACE_TO_PROXY) counts nothing */
 	__shared__ unsigned long long lmet[16];
+	uint32_t fwd_n[2] = {0u, 0u};
+	uint64_t fwd_b[2] = {0ull, 0ull};
 	const uint64_t T = (uint64_t)gridDim.x * NT;
 	const uint64_t t0 = (uint64_t)blockIdx.x * NT + threadIdx.x;
 	uint64_t *pctr = a.delta;
@@ -1278,9 +1282,6 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				if (len[u] >= PKC_MAX_LEN) {
 					atomicAdd((unsigned long long *)&pctr[2u * c], 1ull);
 					atomicAdd((unsigned long long *)&pctr[2u * c + 1u], (unsigned long long)len[u]);
-					const uint32_t mi = (fw[u] & F_EG) ? 2u : 0u;
-					atomicAdd(&lmet[mi], 1ull);
-					atomicAdd(&lmet[mi + 1u], (unsigned long long)len[u]);
 				} else if (c < s.hot_slots) {
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
@@ -1294,6 +1295,11 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 			} else {
 				st[u] = 0;
 				v[u] = DROP_POLICY;
+			}
+			if ((fw[u] & F_OK) && v[u] == 0) {
+				const uint32_t e = (fw[u] & F_EG) ? 1u : 0u;
+				fwd_n[e] += 1u;
+				fwd_b[e] += len[u];
 			}
 			if ((fw[u] & F_OK) && v[u] < 0) {
 				const uint32_t mr = v[u] == DROP_POLICY ? 1u : (v[u] == DROP_NO_SERVICE ? 3u : 2u);
@@ -1336,8 +1342,17 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 	}
 
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
+#pragma unroll
+	for (int e = 0; e < 2; e++) {
+		const uint64_t c = wave_sum((uint64_t)fwd_n[e]);
+		const uint64_t b = wave_sum(fwd_b[e]);
+		if ((threadIdx.x & 63) == 0 && c) {
+			atomicAdd((unsigned long long *)&met[(e + 1u) * 2u], (unsigned long long)c);
+			atomicAdd((unsigned long long *)&met[(e + 1u) * 2u + 1u], (unsigned long long)b);
+		}
+	}
 	__syncthreads();
-	if (threadIdx.x < 16 && lmet[threadIdx.x]) {
+	if (threadIdx.x >= 4 && threadIdx.x < 16 && lmet[threadIdx.x]) {
 		const uint32_t reasons[4] = {0u, 133u, 137u, 158u};
 		const uint32_t c = threadIdx.x >> 1;
 		const uint32_t key = (reasons[c >> 1] * 4u + ((c & 1) ? 2u : 1u)) * 2u + (threadIdx.x & 1u);
@@ -1354,9 +1369,6 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 	}
 }
 
-/* delta[2s] += pk[s] >> 37; delta[2s+1] += pk[s] & (2^37-1); pk[s] = 0, and
- * the forwarded metrics (reason 0, drop.h:104 / l3.h:119-130) of the packets
- * unpacked, by the direction of their entry (slot_dir: 1 ingress, 2 egress) */
 /* ------------------------------------------------------------------ */
 /* raw Ethernet frames -> policy tuple -> verdict   */
 /* ------------------------------------------------------------------ */
@@ -1637,7 +1649,9 @@ __global__ __launch_bounds__(NT) void k_frames(cgpu_snapshot s, frames_args a)
 		a.identity[i] = id;
 		if (a.stage)
 			a.stage[i] = (uint8_t)st;
-		if (st == 7u || v == DROP_SNAPLEN)
+		/* not classified, snap-length, or a proxy redirect (TRACE_TO_PROXY
+		 * counts nothing): no metrics */
+		if (st == 7u || v == DROP_SNAPLEN || v > 0)
 			continue;
 		/* update_metrics(len, dir, -reason) (bpf/lib/drop.h:104), reason as u8 */
 		const uint32_t reason = v < 0 ? (uint32_t)(-v) & 0xffu : 0u;
@@ -1679,10 +1693,9 @@ __global__ __launch_bounds__(NT) void k_frames(cgpu_snapshot s, frames_args a)
 	}
 }
 
-__global__ __launch_bounds__(256) void k_unpack(uint64_t *delta, uint64_t *pk, uint32_t lo, uint32_t hi,
-						  const uint8_t *slot_dir, uint64_t *met)
+/* delta[2s] += pk[s] >> 37; delta[2s+1] += pk[s] & (2^37-1); pk[s] = 0 */
+__global__ __launch_bounds__(256) void k_unpack(uint64_t *delta, uint64_t *pk, uint32_t lo, uint32_t hi)
 {
-	uint64_t sum[4] = {0, 0, 0, 0}; /* ingress pk, bytes, egress pk, bytes */
 	for (uint32_t s = lo + blockIdx.x * blockDim.x + threadIdx.x; s < hi; s += gridDim.x * blockDim.x) {
 		if (!pk[s])
 			continue;
@@ -1691,15 +1704,6 @@ __global__ __launch_bounds__(256) void k_unpack(uint64_t *delta, uint64_t *pk, u
 		const uint64_t np = x >> PKC_SHIFT, nb = x & PKC_BYTES_MASK;
 		atomicAdd((unsigned long long *)&delta[2u * s], np);
 		atomicAdd((unsigned long long *)&delta[2u * s + 1u], nb);
-		const bool eg = slot_dir[s] == 2;
-		sum[eg ? 2 : 0] += np;
-		sum[eg ? 3 : 1] += nb;
-	}
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		const uint64_t v = wave_sum(sum[k]);
-		if ((threadIdx.x & 63) == 0 && v)
-			atomicAdd((unsigned long long *)&met[(k < 2 ? 1u : 2u) * 2u + (k & 1)], v);
 	}
 }
 
@@ -2163,8 +2167,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 		hipLaunchKernelGGL((k_classify_v4_x4<NT, true, 4, 1, LB>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
-			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi,
-					   s.slot_dir, a.delta + 2ull * s.n_ctr_slots);
+			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
 		}
 	}
 	return hipGetLastError();
@@ -3029,7 +3032,8 @@ template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapsho
 		a.ct_ret[i] = (uint8_t)cr;
 		if (a.stage)
 			a.stage[i] = (uint8_t)st;
-		const uint32_t r = v >= 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : 3u));
+		/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
+		const uint32_t r = v > 0 ? 4u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : 3u));
 		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
 #pragma unroll
 		for (int k = 0; k < 8; k++) {

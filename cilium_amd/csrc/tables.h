@@ -319,7 +319,6 @@ typedef struct cgpu_snapshot {
 	uint32_t n_ctr_slots;
 	uint32_t hot_slots;      /* counter slots [0, hot_slots) may live in LDS */
 	uint32_t cold_hi;        /* counter slots >= cold_hi are unassigned */
-	const uint8_t *slot_dir; /* per counter slot: 1 ingress, 2 egress key, 0 free */
 	lb_table lb;
 	uint32_t lb_flags;       /* CGPU_LB_L3 | CGPU_LB_L4 */
 	uint32_t ipv4_loopback;  /* IPV4_LOOPBACK, network order */

@@ -968,8 +968,12 @@ static void *cls_worker(void *arg)
 		if (j->stage)
 			j->stage[i] = (uint8_t)st;
 		/* drop: send_drop_notify -> update_metrics(len, dir, -reason)
-		 * (bpf/lib/drop.h:104); forward: REASON_FORWARDED (0) at the verdict */
-		{
+		 * (bpf/lib/drop.h:113-118); forward: REASON_FORWARDED (0) at the
+		 * TRACE_TO_STACK / TRACE_TO_LXC observation point (trace.h:163-186,
+		 * bpf_lxc.c:652 / :969; local delivery l3.h:128); a proxy redirect
+		 * (verdict > 0) traces TRACE_TO_PROXY, which counts nothing
+		 * (lib/lxc.h:115-117) */
+		if (v <= 0) {
 			uint32_t reason = v < 0 ? (uint32_t)(-v) & 0xff : 0;
 			uint64_t *m = &j->metrics[(reason * 4 + dir) * 2];
 			m[0] += 1;
@@ -1128,7 +1132,7 @@ static void *cls6_worker(void *arg)
 			j->identity[i] = id;
 		if (j->stage)
 			j->stage[i] = (uint8_t)st;
-		{
+		if (v <= 0) { /* as classify_v4: a proxy redirect counts nothing */
 			uint32_t reason = v < 0 ? (uint32_t)(-v) & 0xff : 0;
 			uint64_t *m = &j->metrics[(reason * 4 + dir) * 2];
 			m[0] += 1;
@@ -2012,7 +2016,7 @@ int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 			identity[i] = id;
 		if (stage)
 			stage[i] = (uint8_t)r.stage;
-		{
+		if (fin <= 0) { /* a proxy redirect traces TRACE_TO_PROXY: no metrics */
 			uint32_t reason = fin < 0 ? (uint32_t)(-fin) & 0xff : 0;
 			c->metrics[(reason * 4 + mdir) * 2] += 1;
 			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];

@@ -58,6 +58,10 @@ def load_ref():
     pol.ref_constants.argtypes = [u32p, C.c_int]
     pol.ref_classify_v6.argtypes = [C.c_void_p, C.c_void_p, C.c_uint16, C.c_uint8, C.c_uint8,
                                     C.c_uint32, C.c_int, C.c_int, C.c_uint32, u32p, ip, ip, ip]
+    pol.ref_metrics_read.argtypes = [C.c_void_p]
+    pol.ref_metrics_read.restype = None
+    pol.ref_metrics_packet.argtypes = [C.c_int, C.c_uint32, C.c_int]
+    pol.ref_metrics_packet.restype = None
     pol.ref_router_ip.argtypes = [C.c_void_p]
     pol.ref_router_ip.restype = None
     xdp.ref_xdp_reset.restype = None
@@ -65,6 +69,14 @@ def load_ref():
     xdp.ref_xdp_endpoint_update.argtypes = [C.c_void_p]
     xdp.ref_xdp_run.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
     return pol, xdp
+
+
+def ref_metrics(pol):
+    """cilium_metrics as the reference's update_metrics call sites left it
+    (send_drop_notify / send_trace_notify, oracle/ref/harness_policy.c)."""
+    m = np.zeros((256, 4, 2), np.uint64)
+    pol.ref_metrics_read(m.ctypes.data)
+    return m
 
 
 def b(x):
@@ -336,6 +348,7 @@ def gen_classify_fixture(pol, rng):
         out[f"c{ci}_nprobes"] = nprobes
         out[f"c{ci}_naddr"] = naddr
         out[f"c{ci}_final_entries"] = final
+        out[f"c{ci}_metrics"] = ref_metrics(pol)
     return dict(ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe, pol_ep=pep,
                 configs=np.array(CONFIGS, np.int64), **{"t_" + k: v for k, v in t.items()}, **out)
 
@@ -440,6 +453,7 @@ def gen_classify_v6_fixture(pol, rng):
         out[f"c{ci}_nprobes"] = nprobes
         out[f"c{ci}_naddr"] = naddr
         out[f"c{ci}_final_entries"] = final
+        out[f"c{ci}_metrics"] = ref_metrics(pol)
     return dict(router_ip=router, ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe,
                 pol_ep=pep, configs=np.array(CONFIGS6, np.int64),
                 **{"t_" + k: v for k, v in t.items()}, **out)
@@ -780,6 +794,7 @@ def gen_classify_lb_fixture(pol, lbls, rng):
             eg = int(t["flags"][i]) & 1
             if eg and lx["ret"][i] < 0:
                 verdict[i], ident[i], stage[i], nprobes[i] = lx["ret"][i], 0, 6, lx["lookups"][i]
+                pol.ref_metrics_packet(int(lx["ret"][i]), int(t["len"][i]), 1)
                 continue
             da = int(lx["tdaddr"][i]) if eg else int(t["daddr"][i])
             dp = int(lx["dport"][i]) if eg else int(t["dport"][i])
@@ -797,6 +812,7 @@ def gen_classify_lb_fixture(pol, lbls, rng):
         out[f"c{ci}_verdict"], out[f"c{ci}_identity"] = verdict, ident
         out[f"c{ci}_stage"], out[f"c{ci}_nprobes"] = stage, nprobes
         out[f"c{ci}_final_entries"] = final
+        out[f"c{ci}_metrics"] = ref_metrics(pol)
     return dict(ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe, pol_ep=pep,
                 lb_keys=keys, lb_vals=vals, configs=np.array(CONFIGS[:2], np.int64),
                 **{"t_" + k: v for k, v in t.items()}, **out)

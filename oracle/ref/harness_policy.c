@@ -11,6 +11,12 @@
  *   - identity_is_reserved (bpf/lib/policy.h:41-44)
  * with map_lookup_elem pointed at the mock map store (mockmap.c), because
  * the map implementations live in the Linux kernel, not in the reference.
+ * The metrics the reference keeps (cilium_metrics, bpf/lib/maps.h:35-41)
+ * come from its own call sites: send_drop_notify on a drop
+ * (bpf/lib/drop.h:113-118 -> update_metrics, metrics.h:41-59) and
+ * send_trace_notify at the forwarding observation point
+ * (bpf/lib/trace.h:163-186: TRACE_TO_LXC ingress, TRACE_TO_STACK egress,
+ * TRACE_TO_PROXY nothing), with map_update_elem pointed at the mock too.
  *
  * The per-tuple composition (which address feeds ipcache, the identity
  * fallback, the protocol gate) is glue restated from the reference's
@@ -31,6 +37,8 @@
 #include "lib/common.h"
 #include "lib/policy.h"
 #include "lib/eps.h"
+#include "lib/drop.h"
+#include "lib/trace.h"
 
 #include "mockmap.h"
 
@@ -38,6 +46,8 @@
 
 static struct mockmap policy_maps[REF_MAX_EP];
 static struct mockmap ipcache;
+static struct mockmap metrics; /* cilium_metrics (one CPU: a plain hash) */
+static void fresh_skb(struct __sk_buff *skb, uint32_t len);
 static int cur_ep;
 static int inited;
 /* probe accounting: index (1-based) of the policy probe that hit, and count */
@@ -55,8 +65,19 @@ static void *mock_lookup(void *map, const void *key)
 	}
 	if (map == &cilium_ipcache)
 		return mockmap_lookup(&ipcache, key);
+	if (map == &cilium_metrics)
+		return mockmap_lookup(&metrics, key);
 	fprintf(stderr, "ref harness: lookup on unexpected map %p\n", map);
 	return NULL;
+}
+
+static int mock_update(void *map, const void *key, const void *val, __u32 flags)
+{
+	(void)flags;
+	if (map == &cilium_metrics)
+		return mockmap_update(&metrics, key, val) < 0 ? -1 : 0;
+	fprintf(stderr, "ref harness: update on unexpected map %p\n", map);
+	return -1;
 }
 
 static void ensure_init(void)
@@ -68,7 +89,9 @@ static void ensure_init(void)
 			     sizeof(struct policy_entry));
 	mockmap_init(&ipcache, MOCK_LPM, sizeof(struct ipcache_key),
 		     sizeof(struct remote_endpoint_info));
+	mockmap_init(&metrics, MOCK_HASH, sizeof(struct metrics_key), sizeof(struct metrics_value));
 	map_lookup_elem = mock_lookup;
+	map_update_elem = mock_update;
 	inited = 1;
 }
 
@@ -78,6 +101,41 @@ void ref_reset(void)
 	for (int i = 0; i < REF_MAX_EP; i++)
 		mockmap_clear(&policy_maps[i]);
 	mockmap_clear(&ipcache);
+	mockmap_clear(&metrics);
+}
+
+/* cilium_metrics as [reason 256][dir 4][count, bytes] (u64) */
+void ref_metrics_read(uint64_t *out)
+{
+	ensure_init();
+	memset(out, 0, 256 * 4 * 2 * sizeof(uint64_t));
+	for (size_t i = 0; i < metrics.n; i++) {
+		const struct metrics_key *k = (const void *)(metrics.keys + i * metrics.ksz);
+		const struct metrics_value *v = (const void *)(metrics.vals + i * metrics.vsz);
+		out[(k->reason * 4 + k->dir) * 2] += v->count;
+		out[(k->reason * 4 + k->dir) * 2 + 1] += v->bytes;
+	}
+}
+
+/* The metrics of one packet whose program ended with `ret` (bpf_lxc.c):
+ * a drop is reported by the tail-call wrapper with send_drop_notify
+ * (egress tail_handle_ipv4 :659-666 / tail_handle_ipv6, ingress
+ * tail_ipv4_policy :980-988 / tail_ipv6_policy); a proxy redirect traces
+ * TRACE_TO_PROXY in ipv4_redirect_to_host_port (lib/lxc.h:115-117); any
+ * other egress packet leaves through TRACE_TO_STACK (:652) or local
+ * delivery (lib/l3.h:128, an egress forward as well); an allowed ingress
+ * packet traces TRACE_TO_LXC (:969). */
+void ref_metrics_packet(int ret, uint32_t len, int egress)
+{
+	struct __sk_buff skb;
+	ensure_init();
+	fresh_skb(&skb, len);
+	if (ret < 0)
+		send_drop_notify(&skb, 0, 0, 0, 0, ret, TC_ACT_SHOT, egress ? METRIC_EGRESS : METRIC_INGRESS);
+	else if (ret > 0)
+		send_trace_notify(&skb, TRACE_TO_PROXY, 0, 0, 0, 0, 0, false);
+	else
+		send_trace_notify(&skb, egress ? TRACE_TO_STACK : TRACE_TO_LXC, 0, 0, 0, 0, 0, false);
 }
 
 int ref_sizes(int *policy_key_sz, int *policy_entry_sz, int *ipcache_key_sz,
@@ -240,6 +298,7 @@ int ref_classify_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t dport_be,
 		*identity_out = 0;
 		*stage_out = 4;
 		*nprobes_out = 0;
+		ref_metrics_packet(DROP_CT_UNKNOWN_PROTO, len, egress);
 		return DROP_CT_UNKNOWN_PROTO;
 	}
 	if (egress) {
@@ -268,6 +327,7 @@ int ref_classify_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t dport_be,
 	}
 	*nprobes_out = probes;
 	*stage_out = hit ? (frag && !egress ? 2 : hit) : 0;
+	ref_metrics_packet(ret, len, egress);
 	return ret;
 }
 
@@ -316,6 +376,7 @@ int ref_classify_v6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t dpo
 		*identity_out = 0;
 		*stage_out = 4;
 		*nprobes_out = 0;
+		ref_metrics_packet(DROP_CT_UNKNOWN_PROTO, len, egress);
 		return DROP_CT_UNKNOWN_PROTO;
 	}
 	if (egress) {
@@ -342,6 +403,7 @@ int ref_classify_v6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t dpo
 	}
 	*nprobes_out = probes;
 	*stage_out = hit;
+	ref_metrics_packet(ret, len, egress);
 	return ret;
 }
 

@@ -104,12 +104,7 @@ def test_classify_v4_lb_golden(torch_cuda, golden, ci):
     for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
         rc, got = e.policy_lookup(int(ep), k)
         assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
-    verdict, ln = g[f"c{ci}_verdict"], t["len"].astype(np.uint64)
-    dirs = np.where(t["flags"] & 1, L.METRIC_EGRESS, L.METRIC_INGRESS)
-    exp = np.zeros((256, 4, 2), np.uint64)
-    np.add.at(exp, (np.where(verdict < 0, -verdict, 0), dirs, 0), 1)
-    np.add.at(exp, (np.where(verdict < 0, -verdict, 0), dirs, 1), ln)
-    np.testing.assert_array_equal(e.metrics(), exp)
+    np.testing.assert_array_equal(e.metrics(), g[f"c{ci}_metrics"])  # the reference's
     e.close()
 
 
