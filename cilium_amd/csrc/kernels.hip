@@ -2482,11 +2482,27 @@ __device__ __forceinline__ int ct_find(const ct_table &T, uint4 k, uint32_t *fre
 	uint32_t h = ct_hash(k.x, k.y, k.z, k.w) & T.mask;
 	uint32_t ff = 0xFFFFFFFFu;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
-		const uint4 s = ld_x4<true>(T.keys + h);
-		const uint32_t tag = s.w >> 16;
+		uint4 s = ld_x4<true>(T.keys + h);
+		uint32_t tag = s.w >> 16;
 		if (tag == CT_TAG_EMPTY) {
-			*free_at = ff != 0xFFFFFFFFu ? ff : h;
-			return -1;
+			/* the chain ends only on an EMPTY read at the coherence point:
+			 * the plain load may be a line this XCD's L2 holds from before
+			 * another XCD's lane claimed the slot (a claim's CAS happens at
+			 * memory), which would end the chain early and hide a key this
+			 * lane inserted past it.  Tags never return to EMPTY, so one
+			 * agent-scope re-read settles it; key words written after a
+			 * claim are re-read the same way. */
+			s.w = __hip_atomic_load(&T.keys[h].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			tag = s.w >> 16;
+			if (tag == CT_TAG_EMPTY) {
+				*free_at = ff != 0xFFFFFFFFu ? ff : h;
+				return -1;
+			}
+			const uint64_t xy = __hip_atomic_load(reinterpret_cast<uint64_t *>(T.keys + h),
+							      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			s.x = (uint32_t)xy;
+			s.y = (uint32_t)(xy >> 32);
+			s.z = __hip_atomic_load(&T.keys[h].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 		if (tag == CT_TAG_LIVE && ct_same(s, k))
 			return (int)h;

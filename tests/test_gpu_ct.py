@@ -215,3 +215,23 @@ def test_ct_elephant_and_edges(torch_cuda, cfg_ct):
     torch_cuda.cuda.synchronize()
     assert out["verdict"].numel() == 0
     e.close()
+
+
+def test_ct_crowded_map_no_duplicates(torch_cuda, cfg_ct):
+    """A crowded, contended map: 2,000 connections with ~40
+    packets each into a CT_MAP_SIZE of 4,096 (8,192 slots; ~2,900 live
+    entries and their tombstones at the end, so long linear-probe clusters),
+    below capacity so that no create can fail, over 4 batches so entries are found, closed into tombstones and
+    reclaimed across batches, with lanes of every XCD claiming neighbouring
+    slots.  A chain ended early by a stale EMPTY read would store a key twice:
+    every dumped key is unique, and map, verdicts and counts equal the
+    restatement's."""
+    T, _, _, _ = cfg_ct
+    t, locals_be, seclabels = synth.make_ct_workload(T, 2_000, seed=77, mean_pkts=40.0, span=0.5)
+    e, o = _pair(torch_cuda, T, t, locals_be, seclabels, 4, [3000, 3010, 3020, 3030], ct_max=4096)
+    keys, _ = e.ct4_dump()
+    assert len(keys) > 2_000
+    assert len(np.unique(keys.view(np.uint8).reshape(len(keys), -1), axis=0)) == len(keys)
+    _assert_same_map(e, o)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
