@@ -48,6 +48,7 @@ METRIC = "Mpps classified (LPM ipcache + policy map) at 1/2/4/8 GPUs; % HBM roof
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 B_IN, B_OUT = 18, 8    # v4 classify tuple bytes in / out
 B_IN_PF6, B_OUT_PF6 = 33, 1  # v6 prefilter
+B_IN_V6 = 42           # v6 classify: saddr 16 + daddr 16 + dport proto flags len ep
 FRAME_STRIDE = 64      # --config frames: ring slot bytes (Ethernet + IPv4 + TCP fit)
 B_IN_FRAMES = FRAME_STRIDE + 4 + 1 + 2  # slot + len + flags + ep
 B_IN_CT, B_OUT_CT = 22, 9  # saddr daddr sport dport proto l4(2) flags len ep / verdict identity ct_ret
@@ -84,6 +85,9 @@ WORKLOADS = {
     "gpu": "config2: 100k IPv4 ipcache LPM + 64k policy entries (4 ep x 16k), "
            "64M-tuple batches per GPU, bit-exact verdicts",
     "cpu": "config1 (CPU-scale)",
+    "v6": "IPv6 classify at config-2 size: 100k IPv6 ipcache prefixes (1024 /48 sites under 64 "
+          "/16 roots; /128 40%, /64 30%, /56 10%, /48 7%, /96 5%, /112 5%, /32 3%) + 64k policy "
+          "entries (4 ep x 16k), 64M-tuple batches per GPU, bit-exact verdicts",
     "cascade": "config5: 1M IPv4 services (lb4_local, backends ~Geom(0.3) cap 16, 30% of egress "
                "tuples to a service) -> ipcache(post-DNAT) -> policy over config-2 tables, "
                "64M-tuple batches per GPU, bit-exact verdicts",
@@ -136,6 +140,7 @@ def main():
     cascade = args.config == "cascade"
     frames = args.config == "frames"
     ct = args.config == "ct"
+    v6 = args.config == "v6"
     cfg = synth.CONFIGS["gpu" if (pf6 or frames or ct) else args.config]
     n = args.tuples or cfg["n_tuples"]
     t0 = time.time()
@@ -162,6 +167,13 @@ def main():
         e = Engine(device=local, **T.engine_config(), ct_max=ct_max)
         synth.load_engine(e, T)
         synth.load_lxc(e, seclabels)
+    elif v6:
+        T = synth.make_tables6(**cfg)
+        tup = synth.make_tuples6(T, n, gpu_id=rank)
+        log(f"[rank {rank}] synthetic v6 tables ({len(T.ipc_keys)} ipcache, {len(T.pol_keys)} "
+            f"policy) + {n} tuples in {time.time() - t0:.1f}s")
+        e = Engine(device=local, **T.engine_config())
+        synth.load_engine(e, T)
     else:
         T = synth.make_tables(**cfg)
         tup = synth.make_tuples(T, n, gpu_id=rank)
@@ -212,6 +224,8 @@ def main():
             e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
         elif cascade:
             e.classify_v4_lb(d, out=out, stream=stream)
+        elif v6:
+            e.classify_v6(d, out=out, stream=stream)
         elif frames:
             e.classify_frames(d, out=out, stream=stream)
         else:
@@ -278,6 +292,8 @@ def main():
                                       nthreads=threads)
             if cascade:
                 return o.classify_v4_lb({k: v[sl] for k, v in tup.items()}, nthreads=threads)
+            if v6:
+                return o.classify_v6({k: v[sl] for k, v in tup.items()}, nthreads=threads)
             if frames:
                 return o.classify_frames({k: v[sl] for k, v in fr.items()}, nthreads=threads)
             return o.classify_v4({k: v[sl] for k, v in tup.items()}, nthreads=threads)
@@ -304,6 +320,8 @@ def main():
                 res = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
             elif cascade:
                 res = o.classify_v4_lb(tup, nthreads=threads)
+            elif v6:
+                res = o.classify_v6(tup, nthreads=threads)
             elif frames:
                 res = o.classify_frames(fr, nthreads=threads)
             else:
@@ -332,6 +350,7 @@ def main():
         elif not args.no_cpu_baseline:
             what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
                     "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash",
+                    "v6": "oracle/cgpu_oracle.c IPv6 LPM trie + open hash",
                     "frames": "oracle/cgpu_oracle.c frame parse + LPM trie + open hash"}.get(
                 args.config, "oracle/cgpu_oracle.c (kernel-like LPM trie + open hash)")
             cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
@@ -349,7 +368,8 @@ def main():
                 parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
         probes_per = probes / n_cpu
         b_in, b_out = ((B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN_FRAMES, B_OUT) if frames
-                       else (B_IN_CT, B_OUT_CT) if ct else (B_IN + (2 if cascade else 0), B_OUT))
+                       else (B_IN_CT, B_OUT_CT) if ct else (B_IN_V6, B_OUT) if v6
+                       else (B_IN + (2 if cascade else 0), B_OUT))
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
         traffic = None

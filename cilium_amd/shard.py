@@ -59,7 +59,16 @@ def pairhash_np(saddr, daddr) -> np.ndarray:
 
 
 def ct_shard_of(t: dict, world: int) -> np.ndarray:
-    """Owning rank of every packet of the stateful path: pairhash % world."""
+    """Owning rank of every packet of the stateful path: pairhash % world.
+
+    Capacity: every rank's conntrack map is a whole CT_MAP_SIZE (cfg.ct_max),
+    as every node's cilium_ct4_global is in the reference, so the ranks
+    together hold up to world x ct_max entries.  The union of the rank maps
+    equals the one-process map while no map reaches ct_max; past that the
+    DROP_CT_CREATE_FAILED set depends on which shard fills first (and, within
+    one map, on lane order: cgpu.h), so parity is defined below capacity
+    only.  A deployment that wants the aggregate of one map passes
+    ct_max // world per rank."""
     return (pairhash_np(t["saddr"], t["daddr"]) % np.uint32(world)).astype(np.int64)
 
 

@@ -39,6 +39,9 @@ CONFIGS = {
     # config 5: config-2 tables + 1M IPv4 services in front
     "cascade": dict(n_prefixes=100_000, n_identities=1000, n_endpoints=4, keys_per_ep=16_000,
                     n_tuples=64 << 20, n_services=1_000_000),
+    # IPv6 classify at config-2 size (make_tables6)
+    "v6": dict(n_prefixes=100_000, n_identities=1000, n_endpoints=4, keys_per_ep=16_000,
+               n_tuples=64 << 20),
 }
 
 # cluster CIDR 10.0.0.0/8 expressed like node_config.h's IPV4_CLUSTER_MASK /
@@ -303,6 +306,120 @@ def load_services(target, svcs: Services):
     else:
         rc = target.lb_update_batch(svcs.keys, svcs.vals)
     assert rc == 0, rc
+
+
+# ---------------------------------------------------------------------------
+# IPv6 classify at config-2 size (ipcache_lookup6 of
+# bpf/lib/eps.h:56-66 behind bpf_lxc.c:170-187 / bpf_netdev.c:203-211):
+# 100k IPv6 ipcache prefixes laid out like a dual-stack cluster's ipcache --
+# 1024 /48 sites under 64 /16 roots; /128 40% (pod and node addresses), /64
+# 30% (node pod CIDRs), /56 10%, /48 7%, /96 5%, /112 5%, /32 3% (CIDR
+# policy) -- plus ::/0 -> WORLD and 4 HOST /128s, and the config-2 MapState
+# (4 endpoints x 16k keys).  Tuples: 80% inside an installed prefix, 20%
+# random under a root; the rest as make_tuples.
+# ---------------------------------------------------------------------------
+V6_LENS = np.array([32, 48, 56, 64, 96, 112, 128])
+V6_LENS_P = np.array([0.03, 0.07, 0.10, 0.30, 0.05, 0.05, 0.40])
+# MASK6[L] = the 16 network-order bytes of a /L netmask
+MASK6 = np.packbits((np.arange(128)[None, :] < np.arange(129)[:, None]).astype(np.uint8), axis=1)
+
+
+@dataclass
+class Tables6:
+    ipc_keys: np.ndarray      # IPCACHE_KEY (family 2)
+    ipc_vals: np.ndarray
+    pfx_addr: np.ndarray      # (n, 16) uint8 masked base of every non-reserved prefix
+    pfx_len: np.ndarray
+    roots: np.ndarray         # (n_roots, 2) uint8
+    router: bytes             # ROUTER_IP (16 bytes; its /64 is the cluster test)
+    pol_keys: np.ndarray
+    pol_entries: np.ndarray
+    pol_ep: np.ndarray
+    n_endpoints: int
+
+    def engine_config(self):
+        return dict(ipv6_router_ip=self.router,
+                    policy_max_total=max(1 << 16, 2 * len(self.pol_keys)),
+                    max_endpoints=max(64, self.n_endpoints))
+
+    def oracle_config(self):
+        return dict(router_ip=self.router)
+
+
+def make_tables6(n_prefixes=100_000, n_identities=1000, n_endpoints=4, keys_per_ep=16_000,
+                 seed=SEED, n_roots=64, n_sites=1024, **_):
+    T = make_tables(n_prefixes=16, n_identities=n_identities, n_endpoints=n_endpoints,
+                    keys_per_ep=keys_per_ep, seed=seed)  # the MapState (same as config 2)
+    rng = np.random.Generator(np.random.PCG64(seed + 0x6C))
+    idents = np.arange(256, 256 + n_identities, dtype=np.uint32)
+    roots = rng.integers(0, 256, (n_roots, 2), dtype=np.uint8)
+    sites = rng.integers(0, 256, (n_sites, 16), dtype=np.uint8)
+    sites[:, :2] = roots[rng.integers(0, n_roots, n_sites)]
+    m = int(n_prefixes * 1.2) + 64
+    ln = rng.choice(V6_LENS, m, p=V6_LENS_P)
+    a = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+    a[:, :6] = sites[rng.integers(0, n_sites, m), :6]
+    a &= MASK6[ln]
+    rec = np.zeros(m, np.dtype([("len", "u1"), ("a", "u1", (16,))]))
+    rec["len"], rec["a"] = ln, a
+    _, first = np.unique(rec.view(np.dtype((np.void, 17))), return_index=True)
+    first = np.sort(first)[:n_prefixes]
+    ln, a = ln[first], a[first]
+    labels = rng.choice(idents, len(ln)).astype(np.uint32)
+    labels[rng.random(len(ln)) < 0.005] = 0  # tombstones
+    hosts = sites[:4].copy()
+    hosts[:, 8:] = rng.integers(0, 256, (4, 8), dtype=np.uint8)
+    r_addr = np.concatenate([np.zeros((1, 16), np.uint8), hosts])
+    r_len = np.array([0, 128, 128, 128, 128])
+    r_lab = np.array([L.WORLD_ID] + [L.HOST_ID] * 4, np.uint32)
+    keys = np.zeros(len(r_len) + len(ln), L.IPCACHE_KEY)
+    vals = np.zeros(len(keys), L.REMOTE_ENDPOINT_INFO)
+    keys["family"] = L.ENDPOINT_KEY_IPV6
+    keys["prefixlen"] = L.IPCACHE_STATIC_PREFIX + np.concatenate([r_len, ln])
+    keys["ip"] = np.concatenate([r_addr, a])
+    vals["sec_label"] = np.concatenate([r_lab, labels])
+    vals["tunnel_endpoint"] = rng.integers(0, 2**32, len(vals), dtype=np.uint64).astype(np.uint32)
+    canon = np.zeros(len(keys), np.dtype([("len", "u1"), ("a", "u1", (16,))]))
+    canon["len"], canon["a"] = keys["prefixlen"], keys["ip"]
+    _, keep = np.unique(canon.view(np.dtype((np.void, 17))), return_index=True)
+    keep = np.sort(keep)
+    keys, vals = keys[keep], vals[keep]
+    router = bytes(sites[5, :8]) + bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+    return Tables6(keys, vals, a, ln, roots, router, T.pol_keys, T.pol_entries, T.pol_ep,
+                   n_endpoints)
+
+
+def make_tuples6(tables: Tables6, n: int, seed=SEED, gpu_id: int = 0, chunk=1 << 22):
+    """SoA IPv6 tuple batch: saddr / daddr (n, 16) uint8, the rest as make_tuples."""
+    rng = np.random.Generator(np.random.PCG64(seed + 0x600 + gpu_id))
+    npfx = len(tables.pfx_len)
+
+    def addrs(m):
+        inside = rng.random(m) < 0.8
+        pi = rng.integers(0, npfx, m)
+        mk = MASK6[tables.pfx_len[pi]]
+        r = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+        out = (tables.pfx_addr[pi] & mk) | (r & ~mk)
+        rr = ~inside
+        out[rr] = r[rr]
+        out[rr, :2] = tables.roots[rng.integers(0, len(tables.roots), int(rr.sum()))]
+        return out
+
+    sa = np.empty((n, 16), np.uint8)
+    da = np.empty((n, 16), np.uint8)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        sa[lo:hi] = addrs(hi - lo)
+        da[lo:hi] = addrs(hi - lo)
+    egress = (rng.random(n) < 0.5).astype(np.uint8)
+    port = np.where(rng.random(n) < 0.9, zipf_ports(rng, n),
+                    rng.integers(1, 65536, n)).astype(np.uint16)
+    proto = np.where(rng.random(n) < 0.85, L.PROTO_TCP, L.PROTO_UDP).astype(np.uint8)
+    return {
+        "saddr": sa, "daddr": da, "dport": port.byteswap(), "proto": proto,
+        "flags": egress, "len": rng.integers(64, 1501, n).astype(np.uint32),
+        "ep": rng.integers(0, tables.n_endpoints, n).astype(np.uint16),
+    }
 
 
 # ---------------------------------------------------------------------------
