@@ -695,6 +695,7 @@ struct V6Build {
 	std::vector<uint32_t> masks;
 	std::vector<uint32_t> vals;
 	Set16Build set;
+	std::vector<uint32_t> bloom; /* tables.h v6_lpm.bloom */
 	bool any = false;
 };
 
@@ -757,6 +758,14 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 		keys.push_back({w[0], w[1], w[2], w[3], kv.first.first, kv.second});
 	}
 	build_set16(keys, b.set);
+	/* ~12 bits per key, at most V6_BLOOM_MAX_WORDS words */
+	const uint32_t nw = (uint32_t)std::min<uint64_t>(
+		V6_BLOOM_MAX_WORDS, next_pow2(std::max<uint64_t>(64, keys.size() * 12 / 32 + 1)));
+	b.bloom.assign(nw, 0);
+	for (auto &k : keys) {
+		const uint32_t g = v6_bloom_h(hash16(k[0], k[1], k[2], k[3], k[4]));
+		b.bloom[g & (nw - 1)] |= v6_bloom_bits(g);
+	}
 }
 
 /* ---- IPv6 any-match cover (tables.h cover6) ---- */
@@ -2575,8 +2584,9 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o_n = ar.add(b.lc.nodes.data(), b.lc.nodes.size() * 4);
 	const size_t o_c = ar.add(b.lc.dict.data(), b.lc.dict.size() * 4);
 	const size_t o_v = ar.add(b.dir.vals.data(), b.dir.vals.size() * 4);
-	size_t o6[4] = {0, 0, 0, 0};
+	size_t o6[5] = {0, 0, 0, 0, 0};
 	if (b.v6.any) {
+		o6[4] = ar.add(b.v6.bloom.data(), b.v6.bloom.size() * 4);
 		o6[0] = ar.add(b.v6.root.data(), b.v6.root.size() * 4);
 		o6[1] = ar.add(b.v6.masks.data(), b.v6.masks.size() * 4);
 		o6[2] = ar.add(b.v6.vals.data(), b.v6.vals.size() * 4);
@@ -2591,7 +2601,8 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	if (b.v6.any)
 		s.ipc6 = v6_lpm{at<uint2>(buf, o6[0]), at<uint32_t>(buf, o6[1]), at<uint32_t>(buf, o6[2]),
 				addr_set16{at<set16_slot>(buf, o6[3]), b.v6.set.mask, b.v6.set.max_probe},
-				(uint32_t)(b.v6.masks.size() / 4)};
+				(uint32_t)(b.v6.masks.size() / 4), at<uint32_t>(buf, o6[4]),
+				(uint32_t)b.v6.bloom.size() - 1u};
 	b.sum[G_IPC] = in.sum_ipc;
 	return 0;
 }
@@ -3049,10 +3060,10 @@ CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n,
 				 uint32_t *identity, uint8_t *stage, void *stream)
 {
 	Pinned P;
-	if (int r = pin(c, stream, P))
+	if (int r = pin(c, stream, P, true))
 		return r;
 	const cgpu_snapshot &s = P.snap();
-	uint64_t *delta = P.delta;
+	uint64_t *delta = P.delta, *pk = P.pk;
 	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
 			 !t->ep || !verdict || !identity)))
 		return fail(-EINVAL, "null tuple column or output");
@@ -3061,7 +3072,7 @@ CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n,
 	if (!n)
 		return 0;
 	classify_v6_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
-			   verdict, identity, stage, delta, (uint64_t)n};
+			   verdict, identity, stage, delta, (uint64_t)n, pk};
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(launch_classify_v6(s, a, (hipStream_t)stream));
 	return 0;

@@ -254,9 +254,41 @@ __device__ __forceinline__ uint4 mask6(uint4 w, uint32_t len)
 	return make_uint4(w.x & m[0], w.y & m[1], w.z & m[2], w.w & m[3]);
 }
 
+/* Next candidate length of an IPv6 lookup, longest first: pops lengths off
+ * the root's mask (hi: 81..128, lo: 17..80) until one passes the bloom
+ * filter (tables.h v6_lpm), and returns it with its masked key and set
+ * bucket (0: none left).  bloom: the filter words (LDS or global). */
+__device__ __forceinline__ uint32_t v6_next(const v6_lpm &t, const uint32_t *bloom, uint4 a, uint64_t &hi,
+					    uint64_t &lo, uint4 &key, uint32_t &bucket)
+{
+	while (hi | lo) {
+		uint32_t len;
+		if (hi) {
+			const int bit = 63 - __clzll(hi);
+			hi &= ~(1ull << bit);
+			len = 17u + 64u + (uint32_t)bit;
+		} else {
+			const int bit = 63 - __clzll(lo);
+			lo &= ~(1ull << bit);
+			len = 17u + (uint32_t)bit;
+		}
+		const uint4 k = mask6(a, len);
+		const uint32_t h = hash16(k.x, k.y, k.z, k.w, len);
+		const uint32_t g = v6_bloom_h(h);
+		const uint32_t bits = v6_bloom_bits(g);
+		if ((bloom[g & t.bloom_mask] & bits) == bits) {
+			key = k;
+			bucket = h & t.set.bucket_mask;
+			return len;
+		}
+	}
+	return 0;
+}
+
 /* IPv6 longest-prefix lookup (tables.h v6_lpm): the prefix lengths present
- * under the address's /16 are probed longest first, four independent
- * bucket loads in flight per round; the first hit is the longest match.
+ * under the address's /16 are tried longest first; lengths the bloom filter
+ * rules out cost no memory access, the others are probed four at a time
+ * (independent bucket loads in flight); the first hit is the longest match.
  * Returns the DIR-encoded entry (0 = no match). */
 __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 {
@@ -272,37 +304,22 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 		 * unrolled loop: a divergent early return there miscompiled on
 		 * gfx950 / ROCm 7.2 (round 1, reproduced in isolation). */
 		while ((hi | lo) && !res) {
-			uint32_t L[4];
-#pragma unroll
-			for (int j = 0; j < 4; j++) {
-				uint32_t len = 0;
-				if (hi) {
-					int bit = 63 - __clzll(hi);
-					hi &= ~(1ull << bit);
-					len = 17u + 64u + (uint32_t)bit;
-				} else if (lo) {
-					int bit = 63 - __clzll(lo);
-					lo &= ~(1ull << bit);
-					len = 17u + (uint32_t)bit;
-				}
-				L[j] = len;
-			}
+			uint32_t L[4], bi[4];
 			uint4 key[4], bk[4][4];
-			uint32_t bi[4];
-			/* issue every probe's bucket load before resolving any */
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
 				key[j] = make_uint4(0, 0, 0, 0);
 				bi[j] = 0;
+				L[j] = v6_next(t, t.bloom, a, hi, lo, key[j], bi[j]);
+			}
+			/* issue every probe's bucket load before resolving any */
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
 #pragma unroll
 				for (int k = 0; k < 4; k++)
 					bk[j][k] = make_uint4(0, 0, 0, 0);
 				if (L[j]) {
-					key[j] = mask6(a, L[j]);
-					bi[j] = hash16(key[j].x, key[j].y, key[j].z, key[j].w, L[j]) &
-						t.set.bucket_mask;
-					const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) +
-							 (size_t)bi[j] * 4u;
+					const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[j] * 4u;
 #pragma unroll
 					for (int k = 0; k < 4; k++)
 						bk[j][k] = p[k];
@@ -700,7 +717,7 @@ struct cls_args {
 	uint8_t *stage;
 	uint64_t *delta;
 	uint64_t n;
-	uint64_t *pk; /* packed cold-slot accumulator (k_classify_v4_x4 only) */
+	uint64_t *pk; /* packed cold-slot accumulator (k_classify_x4 only) */
 	int lb;       /* v4: egress service step first (cgpu_classify_v4_lb) */
 	const uint16_t *sport;
 	const uint32_t *hash;
@@ -921,7 +938,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 }
 
 
-/* Packed per-slot accumulator of k_classify_v4_x4 (pk): one u64 per counter
+/* Packed per-slot accumulator of k_classify_x4 (pk): one u64 per counter
  * slot, packets in bits 37..63, bytes in 0..36.  Exact while one launch adds
  * at most PKC_CHUNK = 2^26 hits of < 2^11 bytes to a slot (2^26 * 2047 <
  * 2^37): the launcher caps a launch at PKC_CHUNK tuples and unpacks pk into
@@ -951,6 +968,74 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 #define DIAG_LPM(b) (b)
 #endif
 
+/* v6_lookup for the Q tuples of a lane (k_classify_x4<.., V6>): root
+ * gathers, then mask rows (the first nm rows from LDS), then rounds of one
+ * bloom-admitted probe per unresolved tuple, Q bucket loads in flight.  The
+ * filter leaves about one probe per tuple (the hit), so a round is usually
+ * the last.  act[u] false: e[u] = 0 and no memory access. */
+template <int Q>
+__device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *bloom, const uint4 *lmasks,
+					    uint32_t nm, const uint4 (&a)[Q], const bool (&act)[Q], uint32_t (&e)[Q])
+{
+	uint2 r[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		r[u] = make_uint2(0, 0);
+		if (act[u] && t.root)
+			r[u] = t.root[((a[u].x & 0xFFu) << 8) | ((a[u].x >> 8) & 0xFFu)];
+	}
+	uint64_t hi[Q], lo[Q];
+	uint32_t res[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		uint4 m = make_uint4(0, 0, 0, 0);
+		if (r[u].x)
+			m = r[u].x < nm ? lmasks[r[u].x] : reinterpret_cast<const uint4 *>(t.masks)[r[u].x];
+		hi[u] = ((uint64_t)m.w << 32) | m.z;
+		lo[u] = ((uint64_t)m.y << 32) | m.x;
+		res[u] = 0;
+	}
+	for (;;) {
+		uint32_t L[Q], bi[Q];
+		uint4 key[Q];
+		bool more = false;
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			L[u] = 0;
+			bi[u] = 0;
+			key[u] = make_uint4(0, 0, 0, 0);
+			if (!res[u])
+				L[u] = v6_next(t, bloom, a[u], hi[u], lo[u], key[u], bi[u]);
+			more |= L[u] != 0;
+		}
+		if (!more)
+			break;
+		uint4 bk[Q][4];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				bk[u][k] = make_uint4(0, 0, 0, 0);
+			if (L[u]) {
+				const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[u] * 4u;
+#pragma unroll
+				for (int k = 0; k < 4; k++)
+					bk[u][k] = p[k];
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (L[u])
+				res[u] = set16_resolve(t.set, bk[u], bi[u], key[u], 1u | (L[u] << 8));
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		e[u] = res[u] ? res[u] : r[u].y;
+}
+
+/* mask rows of the v6 ipcache staged in LDS by k_classify_x4<.., V6> */
+#define V6_LDS_MASK_ROWS 256u
+
 /*
  * IPv4 classification, four consecutive tuples per lane per step.
  * Same semantics as k_classify<0, 1, NT> (the reference cascade of
@@ -966,9 +1051,10 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  * aligned 2-byte columns and 4-byte aligned 1-byte columns; the one partial
  * group at the end of the batch is read element by element.
  */
-template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false>
-__global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
+template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false>
+__global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
 {
+	static_assert(!(LB && V6), "the service step is IPv4");
 	/* per-tuple flag word */
 	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u, F_LBDROP = 32u;
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
@@ -985,13 +1071,25 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 	uint64_t *pctr = a.delta;
 	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
 	const uint32_t pmask = s.pol.bucket_mask;
-	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots); /* LPM leaf dictionary */
+	/* after the hot counters: v4 the LPM leaf dictionary; v6 the bloom
+	 * filter and the first mask rows of the ipcache */
+	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots);
+	const uint32_t nbw = V6 && s.ipc6.root ? s.ipc6.bloom_mask + 1u : 0u;
+	const uint32_t nm = V6 ? min(s.ipc6.n_masks, V6_LDS_MASK_ROWS) : 0u;
+	uint4 *lmasks = reinterpret_cast<uint4 *>(ldict + nbw); /* nbw: a multiple of 64 */
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
 	if (threadIdx.x < 16)
 		lmet[threadIdx.x] = 0;
-	for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
-		ldict[k] = s.ipc4c.dict[k];
+	if (V6) {
+		for (uint32_t k = threadIdx.x; k < nbw; k += NT)
+			ldict[k] = s.ipc6.bloom[k];
+		for (uint32_t k = threadIdx.x; k < nm; k += NT)
+			lmasks[k] = reinterpret_cast<const uint4 *>(s.ipc6.masks)[k];
+	} else {
+		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
+			ldict[k] = s.ipc4c.dict[k];
+	}
 	__syncthreads();
 
 	for (uint64_t g = t0; g * Q < a.n; g += T) {
@@ -1000,6 +1098,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 		/* decode: hi4 = the policy key's upper word {dport, proto, egress}
 		 * (policy.h:61-64), fw = flag word, ad = the looked-up address */
 		uint32_t fw[Q], ad[Q], hi4[Q], ep[Q], len[Q];
+		uint4 ad6[Q];
 		{
 			uint32_t fl[Q], proto[Q], dport[Q], sa[Q], da[Q];
 			if (full && Q == 4) {
@@ -1008,8 +1107,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				const uint2 d4 = ld_x2<NTL>(a.dport + i0);
 				const uint2 e4 = ld_x2<NTL>(a.ep + i0);
 				const uint4 l4 = ld_x4<NTL>(a.len + i0);
-				const uint4 s4 = ld_x4<NTL>(static_cast<const uint32_t *>(a.saddr) + i0);
-				const uint4 a4 = ld_x4<NTL>(static_cast<const uint32_t *>(a.daddr) + i0);
+				const uint4 s4 = V6 ? make_uint4(0, 0, 0, 0)
+						    : ld_x4<NTL>(static_cast<const uint32_t *>(a.saddr) + i0);
+				const uint4 a4 = V6 ? make_uint4(0, 0, 0, 0)
+						    : ld_x4<NTL>(static_cast<const uint32_t *>(a.daddr) + i0);
 				const uint32_t dd[4] = {d4.x & 0xFFFFu, d4.x >> 16, d4.y & 0xFFFFu, d4.y >> 16};
 				const uint32_t ee[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
 				const uint32_t ll[4] = {l4.x, l4.y, l4.z, l4.w};
@@ -1031,8 +1132,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 				const uint32_t d2 = ld_x1<NTL>(a.dport + i0);
 				const uint32_t e2 = ld_x1<NTL>(a.ep + i0);
 				const uint2 l2 = ld_x2<NTL>(a.len + i0);
-				const uint2 s2 = ld_x2<NTL>(static_cast<const uint32_t *>(a.saddr) + i0);
-				const uint2 a2 = ld_x2<NTL>(static_cast<const uint32_t *>(a.daddr) + i0);
+				const uint2 s2 = V6 ? make_uint2(0, 0)
+						    : ld_x2<NTL>(static_cast<const uint32_t *>(a.saddr) + i0);
+				const uint2 a2 = V6 ? make_uint2(0, 0)
+						    : ld_x2<NTL>(static_cast<const uint32_t *>(a.daddr) + i0);
 				const uint32_t dd[2] = {d2 & 0xFFFFu, d2 >> 16}, ee[2] = {e2 & 0xFFFFu, e2 >> 16};
 				const uint32_t ll[2] = {l2.x, l2.y}, ss[2] = {s2.x, s2.y}, aa[2] = {a2.x, a2.y};
 #pragma unroll
@@ -1054,8 +1157,16 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 					dport[u] = a.dport[i];
 					ep[u] = a.ep[i];
 					len[u] = a.len[i];
-					sa[u] = static_cast<const uint32_t *>(a.saddr)[i];
-					da[u] = static_cast<const uint32_t *>(a.daddr)[i];
+					sa[u] = V6 ? 0u : static_cast<const uint32_t *>(a.saddr)[i];
+					da[u] = V6 ? 0u : static_cast<const uint32_t *>(a.daddr)[i];
+				}
+			}
+			if (V6) {
+				/* the looked-up address only: daddr egress, saddr ingress */
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					const uint64_t i = i0 + u < a.n ? i0 + u : i0;
+					ad6[u] = ld_x4<NTL>(static_cast<const uint4 *>((fl[u] & 1u) ? a.daddr : a.saddr) + i);
 				}
 			}
 			uint32_t lbf[Q];
@@ -1104,101 +1215,114 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_v4_x4(cgpu_snapshot s, cl
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
 				const bool eg = fl[u] & 1u;
-				const bool gated =
-					s.ct_proto_gate && proto[u] != 1u && proto[u] != 6u && proto[u] != 17u;
+				/* ct_lookup{4,6} protocol gate: ICMP (v4: 1, v6: 58), TCP, UDP */
+				const bool gated = s.ct_proto_gate && proto[u] != (V6 ? 58u : 1u) && proto[u] != 6u &&
+						   proto[u] != 17u;
+				/* IPv6 passes is_fragment = false (bpf_lxc.c:787-789) */
 				fw[u] = (i0 + u < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) | lbf[u] |
-					(!eg && ((fl[u] >> 1) & 1u) ? F_FRAG : 0u);
+					(!V6 && !eg && ((fl[u] >> 1) & 1u) ? F_FRAG : 0u);
 				ad[u] = eg ? da[u] : sa[u];
 				hi4[u] = dport[u] | (proto[u] << 16) | (eg ? (1u << 24) : 0u);
 			}
 		}
-		/* ipcache lookup (eps.h:70-80): the /16's inline node (x16) */
+		/* ipcache lookup (eps.h:56-80) */
 		uint32_t e[Q];
-		{
-			/* one 16-byte gather: the /16's inline run node (tables.h) */
-			uint4 q[Q];
-#pragma unroll
-			for (int u = 0; u < Q; u++) {
-				q[u] = make_uint4(0, 0, 0, 0);
-				if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK)
-					q[u] = reinterpret_cast<const uint4 *>(s.ipc4c.x16)[DIAG_LPM(bswap32(ad[u]) >> 16)];
-			}
-#pragma unroll
-			for (int u = 0; u < Q; u++) {
-				if (q[u].w & LPMC_OVERFLOW) {
-					e[u] = q[u].x;
-					continue;
-				}
-				const uint32_t x = bswap32(ad[u]) & 0xFFFFu;
-				const uint32_t cnt = (x >= (q[u].x & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].x >> 16) ? 1u : 0u) +
-						     (x >= (q[u].y & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].y >> 16) ? 1u : 0u);
-				const uint64_t v = ((uint64_t)q[u].w << 32) | q[u].z;
-				e[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK ? ldict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
-			}
-		}
-		{
-			/* compressed LPM (tables.h lpm16c): arrays (rare), then one run node */
-			constexpr uint32_t ARR = (DIR_TAG_GROUP >> LPMC_KIND_SHIFT) | 3u;
+		if (V6) {
+			bool act[Q];
 #pragma unroll
 			for (int u = 0; u < Q; u++)
-				if ((e[u] >> LPMC_KIND_SHIFT) == ARR) {
-					e[u] = s.ipc4c.nodes[(size_t)(e[u] & LPMC_OFF_MASK) * 4u +
-							     ((bswap32(ad[u]) >> 8) & 255u)];
-					fw[u] |= F_LVL8; /* below an array: x is the last byte */
+				act[u] = (fw[u] & (F_OK | F_GATED)) == F_OK;
+			v6_lookup_q<Q>(s.ipc6, ldict, lmasks, nm, ad6, act, e);
+		} else {
+			/* v4: the /16's inline node (x16), then the compressed LPM */
+			{
+				/* one 16-byte gather: the /16's inline run node (tables.h) */
+				uint4 q[Q];
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					q[u] = make_uint4(0, 0, 0, 0);
+					if ((fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK)
+						q[u] = reinterpret_cast<const uint4 *>(s.ipc4c.x16)[DIAG_LPM(bswap32(ad[u]) >> 16)];
 				}
 #pragma unroll
-			for (int u = 0; u < Q; u++)
-				if ((e[u] >> LPMC_KIND_SHIFT) == ARR)
-					e[u] = s.ipc4c.nodes[(size_t)(e[u] & LPMC_OFF_MASK) * 4u + (bswap32(ad[u]) & 255u)];
-			/* the first 32 bytes of every node in flight together; the
-			 * rare 64-byte node reads its second half one tuple at a time */
-			uint4 q[Q][2];
-#pragma unroll
-			for (int u = 0; u < Q; u++) {
-				q[u][0] = q[u][1] = make_uint4(0, 0, 0, 0);
-				if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP) {
-					const uint4 *nd = reinterpret_cast<const uint4 *>(s.ipc4c.nodes) +
-							  (e[u] & LPMC_OFF_MASK);
-					q[u][0] = nd[0];
-					if ((e[u] >> LPMC_KIND_SHIFT) & 3u)
-						q[u][1] = nd[1];
+				for (int u = 0; u < Q; u++) {
+					if (q[u].w & LPMC_OVERFLOW) {
+						e[u] = q[u].x;
+						continue;
+					}
+					const uint32_t x = bswap32(ad[u]) & 0xFFFFu;
+					const uint32_t cnt = (x >= (q[u].x & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].x >> 16) ? 1u : 0u) +
+							     (x >= (q[u].y & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].y >> 16) ? 1u : 0u);
+					const uint64_t v = ((uint64_t)q[u].w << 32) | q[u].z;
+					e[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK ? ldict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
 				}
 			}
+			{
+				/* compressed LPM (tables.h lpm16c): arrays (rare), then one run node */
+				constexpr uint32_t ARR = (DIR_TAG_GROUP >> LPMC_KIND_SHIFT) | 3u;
 #pragma unroll
-			for (int u = 0; u < Q; u++) {
-				if ((e[u] & DIR_TAG_MASK) != DIR_TAG_GROUP)
-					continue;
-				const uint32_t kind = (e[u] >> LPMC_KIND_SHIFT) & 3u;
-				uint4 q2 = make_uint4(0, 0, 0, 0), q3 = q2;
-				if (kind == 2) {
-					const uint4 *nd = reinterpret_cast<const uint4 *>(s.ipc4c.nodes) +
-							  (e[u] & LPMC_OFF_MASK);
-					q2 = nd[2];
-					q3 = nd[3];
+				for (int u = 0; u < Q; u++)
+					if ((e[u] >> LPMC_KIND_SHIFT) == ARR) {
+						e[u] = s.ipc4c.nodes[(size_t)(e[u] & LPMC_OFF_MASK) * 4u +
+								     ((bswap32(ad[u]) >> 8) & 255u)];
+						fw[u] |= F_LVL8; /* below an array: x is the last byte */
+					}
+#pragma unroll
+				for (int u = 0; u < Q; u++)
+					if ((e[u] >> LPMC_KIND_SHIFT) == ARR)
+						e[u] = s.ipc4c.nodes[(size_t)(e[u] & LPMC_OFF_MASK) * 4u + (bswap32(ad[u]) & 255u)];
+				/* the first 32 bytes of every node in flight together; the
+				 * rare 64-byte node reads its second half one tuple at a time */
+				uint4 q[Q][2];
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					q[u][0] = q[u][1] = make_uint4(0, 0, 0, 0);
+					if ((e[u] & DIR_TAG_MASK) == DIR_TAG_GROUP) {
+						const uint4 *nd = reinterpret_cast<const uint4 *>(s.ipc4c.nodes) +
+								  (e[u] & LPMC_OFF_MASK);
+						q[u][0] = nd[0];
+						if ((e[u] >> LPMC_KIND_SHIFT) & 3u)
+							q[u][1] = nd[1];
+					}
 				}
-				const uint32_t h = bswap32(ad[u]);
-				e[u] = lpmc_search(q[u][0], q[u][1], q2, q3, kind,
-						   (fw[u] & F_LVL8) ? (h & 255u) : (h & 0xFFFFu));
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					if ((e[u] & DIR_TAG_MASK) != DIR_TAG_GROUP)
+						continue;
+					const uint32_t kind = (e[u] >> LPMC_KIND_SHIFT) & 3u;
+					uint4 q2 = make_uint4(0, 0, 0, 0), q3 = q2;
+					if (kind == 2) {
+						const uint4 *nd = reinterpret_cast<const uint4 *>(s.ipc4c.nodes) +
+								  (e[u] & LPMC_OFF_MASK);
+						q2 = nd[2];
+						q3 = nd[3];
+					}
+					const uint32_t h = bswap32(ad[u]);
+					e[u] = lpmc_search(q[u][0], q[u][1], q2, q3, kind,
+							   (fw[u] & F_LVL8) ? (h & 255u) : (h & 0xFFFFu));
+				}
 			}
 		}
 		/* identity (bpf_lxc.c:488-496 / bpf_netdev.c:374-404) */
 		uint32_t id[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			const uint32_t p = e[u] & DIR_PAYLOAD_MASK;
-			const uint32_t label = (e[u] & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? s.ipc4c.vals[p] : p;
+			const uint32_t label = entry_label(V6 ? s.ipc6.vals : s.ipc4c.vals, e[u]);
+			/* v6: ipv6_match_prefix_64(daddr, ROUTER_IP), bpf/lib/ipv6.h:166-175 */
+			const bool in_cluster = V6 ? ad6[u].x == s.router_ip64[0] && ad6[u].y == s.router_ip64[1]
+						   : (ad[u] & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
 			if (fw[u] & F_EG) {
 				if (e[u] && label)
 					id[u] = label;
-				else if ((ad[u] & s.ipv4_cluster_mask) == s.ipv4_cluster_range)
+				else if (in_cluster)
 					id[u] = s.cluster_id;
 				else
 					id[u] = s.world_id;
 			} else {
 				uint32_t src = s.ingress_src_identity;
-				if (src < s.health_id && e[u] && label && label != s.cluster_id && label != s.host_id)
+				if (src < s.health_id && e[u] && label && label != s.cluster_id && (V6 || label != s.host_id))
 					src = label;
-				id[u] = s.ingress_secctx_world ? s.world_id : src;
+				id[u] = (!V6 && s.ingress_secctx_world) ? s.world_id : src;
 			}
 		}
 		/* The cascade of policy.h:46-110 over the group of {ep, id, dir}
@@ -2093,7 +2217,7 @@ static int classify_variant()
 	return v ? atoi(v) : 8;
 }
 
-/* k_classify_v4_x4 reads columns as 4/8/16-byte vectors at tuple index
+/* k_classify_x4 reads columns as 4/8/16-byte vectors at tuple index
  * multiples of 4: the column base pointers must be aligned to match. */
 static bool x4_aligned(const cls_args &a)
 {
@@ -2131,16 +2255,23 @@ static unsigned resident_blocks(const void *kern, int NT, size_t lds)
 /* x4 schedule: one persistent-size grid (every workgroup resident, so the
  * per-workgroup LDS counter flush is paid once per resident workgroup) per
  * launch of <= PKC_CHUNK tuples, then the unpack of pk into delta. */
-template <bool LB>
+template <bool LB, bool V6>
 static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024;
-	/* LDS: hot counters + the ipcache leaf dictionary */
-	size_t lds = (size_t)s.hot_slots * 8u + (size_t)s.ipc4c.n_dict * 4u;
+	/* LDS: hot counters + the ipcache leaf dictionary (v4) / bloom filter
+	 * and mask rows (v6) */
+	size_t lds = (size_t)s.hot_slots * 8u;
+	if (V6)
+		lds += s.ipc6.root ? (size_t)(s.ipc6.bloom_mask + 1u) * 4u +
+					     (size_t)std::min(s.ipc6.n_masks, V6_LDS_MASK_ROWS) * 16u
+				   : 0u;
+	else
+		lds += (size_t)s.ipc4c.n_dict * 4u;
 #ifdef CGPU_DIAG_LDS_PAD /* timing-only: fewer resident workgroups per CU */
 	lds += CGPU_DIAG_LDS_PAD;
 #endif
-	const void *kern = (const void *)k_classify_v4_x4<NT, true, 4, 1, LB>;
+	const void *kern = (const void *)k_classify_x4<NT, true, 4, 1, LB, V6>;
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
@@ -2157,14 +2288,14 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 		c.flags += off;
 		c.len += off;
 		c.ep += off;
-		c.saddr = static_cast<const uint32_t *>(a.saddr) + off;
-		c.daddr = static_cast<const uint32_t *>(a.daddr) + off;
+		c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
+		c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
 		if (c.sport)
 			c.sport += off;
 		if (c.hash)
 			c.hash += off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + 4 * NT - 1) / (4 * NT), res);
-		hipLaunchKernelGGL((k_classify_v4_x4<NT, true, 4, 1, LB>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		hipLaunchKernelGGL((k_classify_x4<NT, true, 4, 1, LB, V6>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
@@ -2175,10 +2306,10 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 
 /* CGPU_CLASSIFY_VARIANT selects the schedule (A/B in one process); every
  * variant computes the reference's results (tests/test_gpu_parity.py):
- *   8 (default, IPv4): k_classify_v4_x4 -- four tuples per lane, vector
- *      column loads, LDS hot counters + one packed atomic per cold hit,
- *      resident grid (needs aligned columns, else 3)
- *   3 (default, IPv6 / fallback): one tuple per lane, LDS hot counters
+ *   8 (default): k_classify_x4 -- four tuples per lane, vector column
+ *      loads, LDS hot counters + one packed atomic per cold hit, resident
+ *      grid (needs aligned columns, else 3)
+ *   3 (fallback): one tuple per lane, LDS hot counters
  *   0: global atomics for every hit, 256-thread workgroups */
 template <int V6>
 static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_t st)
@@ -2188,8 +2319,11 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 		hipLaunchKernelGGL((k_classify<V6, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 		return hipGetLastError();
 	}
-	if (!V6 && var == 8 && a.pk && x4_aligned(a))
-		return a.lb ? launch_x4<true>(s, a, st) : launch_x4<false>(s, a, st);
+	if (var == 8 && a.pk && x4_aligned(a)) {
+		if (V6)
+			return launch_x4<false, true>(s, a, st);
+		return a.lb ? launch_x4<true, false>(s, a, st) : launch_x4<false, false>(s, a, st);
+	}
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
 	constexpr int NT = 1024;
@@ -2231,7 +2365,7 @@ hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x,
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)
 {
 	return launch_classify<1>(s, cls_args{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len,
-					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, nullptr, 0, nullptr,
+					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, x.pk, 0, nullptr,
 					      nullptr}, st);
 }
 

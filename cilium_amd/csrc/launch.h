@@ -40,7 +40,7 @@ struct classify_v6_args {
 	uint32_t *identity;
 	uint8_t *stage;
 	uint64_t *delta;
-	uint64_t n;
+	uint64_t n;	uint64_t *pk; /* packed cold-slot accumulator (per stream) */
 };
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &a, hipStream_t st);

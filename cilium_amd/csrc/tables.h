@@ -204,7 +204,21 @@ typedef struct v6_lpm {
 	const uint32_t *vals;  /* indirect labels (>= 2^30) */
 	addr_set16 set;        /* used: bit0 used, bits 8..15 length; pad[0] entry */
 	uint32_t n_masks;
+	/* blocked bloom filter over the set's (masked address, length) keys:
+	 * one 32-bit word per key (v6_bloom_word), three bits in it
+	 * (v6_bloom_bits).  A probe whose bits are not all set cannot hit and
+	 * is not issued; no false negatives, so results never depend on it. */
+	const uint32_t *bloom;
+	uint32_t bloom_mask;   /* n_words - 1 (n_words a power of two <= 2^14) */
 } v6_lpm;
+
+#define V6_BLOOM_MAX_WORDS 16384u /* 64 KiB: staged in LDS by the x4 kernel */
+
+static inline __host__ __device__ uint32_t v6_bloom_h(uint32_t h) { return mix32(h, 0xB100Fu); }
+static inline __host__ __device__ uint32_t v6_bloom_bits(uint32_t g)
+{
+	return (1u << ((g >> 17) & 31u)) | (1u << ((g >> 22) & 31u)) | (1u << (g >> 27));
+}
 
 /* ---- service map (cilium_lb4_services, bpf/lib/lb.h:70-76) ----
  * Grouped by frontend {address, dport}: one 16-byte frontend slot per

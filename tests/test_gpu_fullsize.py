@@ -184,3 +184,32 @@ def test_config3_fullsize(torch_cuda):
     np.testing.assert_array_equal(_np(g), r0)
     assert 0.5 < (r0 == L.XDP_DROP).mean() < 0.97  # 50% inside a deny prefix + non-endpoint daddrs
     e.close()
+
+
+def test_v6_config2_size(torch_cuda):
+    """IPv6 classify at config-2 size (bench.py --config v6): 100k IPv6
+    ipcache prefixes + the 64k-entry MapState over a 4M slice; verdict,
+    identity, stage, per-entry counters and metrics (bpf/lib/eps.h:56-66,
+    bpf_lxc.c:170-187, policy.h:46-110)."""
+    from oracle import Oracle
+    torch = torch_cuda
+    T = synth.make_tables6(**synth.CONFIGS["v6"])
+    t = synth.make_tuples6(T, N_SLICE)
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    v0, i0, s0, _ = o.classify_v6(t, nthreads=16)
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    out = e.classify_v6(synth.to_device(t))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(out["verdict"]), v0)
+    np.testing.assert_array_equal(_np(out["identity"], np.uint32), i0)
+    np.testing.assert_array_equal(_np(out["stage"]), s0)
+    gp, gb = _entry_counters(e, T)
+    op, ob = _oracle_counters(o, T)
+    np.testing.assert_array_equal(gp, op)
+    np.testing.assert_array_equal(gb, ob)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    assert len(T.ipc_keys) >= 100_000 and set(np.unique(s0)) >= {0, 1, 2, 3}
+    e.close()

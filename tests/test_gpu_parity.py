@@ -332,9 +332,12 @@ def test_classify_v6_golden(torch_cuda, golden, ci):
     e.close()
 
 
-def test_classify_v6_scale_vs_oracle(torch_cuda):
+@pytest.mark.parametrize("variant", [3, 8])
+def test_classify_v6_scale_vs_oracle(torch_cuda, variant, monkeypatch):
     """20k IPv6 ipcache prefixes (lengths 0..128, tombstones, static-part
-    entries) + policy, 400k tuples: GPU == restatement, bit-exact."""
+    entries) + policy, 400k tuples: GPU == restatement, bit-exact, on the
+    one-tuple-per-lane kernel (3) and the x4 schedule (8, the default)."""
+    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
     from oracle import Oracle
     rng = np.random.default_rng(21)
     T = synth.make_tables(n_prefixes=100, n_identities=500, n_endpoints=3, keys_per_ep=6000)
