@@ -218,10 +218,9 @@ __device__ __forceinline__ bool set4_has(const addr_set4 &t, uint32_t a)
 
 /* Resolve a 16-byte-key probe whose first bucket is loaded: returns the
  * slot's entry word (pad[0], nonzero for prefix sets) or 0 on a miss. */
-__device__ __forceinline__ uint32_t set16_resolve(const addr_set16 &t, const uint4 (&first)[4],
+__device__ __forceinline__ uint32_t set16_resolve(const addr_set16 &t, uint4 k0, uint4 m0, uint4 k1, uint4 m1,
 						  uint32_t b, uint4 key, uint32_t want)
 {
-	uint4 k0 = first[0], m0 = first[1], k1 = first[2], m1 = first[3];
 	for (uint32_t p = 0;;) {
 		if (!(m0.x & 1u))
 			return 0;
@@ -305,7 +304,7 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 		 * gfx950 / ROCm 7.2 (round 1, reproduced in isolation). */
 		while ((hi | lo) && !res) {
 			uint32_t L[4], bi[4];
-			uint4 key[4], bk[4][4];
+			uint4 key[4], k0[4], m0[4], k1[4], m1[4];
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
 				key[j] = make_uint4(0, 0, 0, 0);
@@ -315,21 +314,18 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 			/* issue every probe's bucket load before resolving any */
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
-#pragma unroll
-				for (int k = 0; k < 4; k++)
-					bk[j][k] = make_uint4(0, 0, 0, 0);
-				if (L[j]) {
-					const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[j] * 4u;
-#pragma unroll
-					for (int k = 0; k < 4; k++)
-						bk[j][k] = p[k];
-				}
+				const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[j] * 4u;
+				const uint4 z = make_uint4(0, 0, 0, 0);
+				k0[j] = L[j] ? p[0] : z;
+				m0[j] = L[j] ? p[1] : z;
+				k1[j] = L[j] ? p[2] : z;
+				m1[j] = L[j] ? p[3] : z;
 			}
 			/* longest first: the first hit is the longest match */
 #pragma unroll
 			for (int j = 0; j < 4; j++)
 				if (!res && L[j])
-					res = set16_resolve(t.set, bk[j], bi[j], key[j], 1u | (L[j] << 8));
+					res = set16_resolve(t.set, k0[j], m0[j], k1[j], m1[j], bi[j], key[j], 1u | (L[j] << 8));
 		}
 	}
 	return res ? res : r.y;
@@ -997,36 +993,34 @@ __device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *blo
 	}
 	for (;;) {
 		uint32_t L[Q], bi[Q];
-		uint4 key[Q];
 		bool more = false;
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			L[u] = 0;
 			bi[u] = 0;
-			key[u] = make_uint4(0, 0, 0, 0);
-			if (!res[u])
-				L[u] = v6_next(t, bloom, a[u], hi[u], lo[u], key[u], bi[u]);
+			if (!res[u]) {
+				uint4 key;
+				L[u] = v6_next(t, bloom, a[u], hi[u], lo[u], key, bi[u]);
+			}
 			more |= L[u] != 0;
 		}
 		if (!more)
 			break;
-		uint4 bk[Q][4];
+		uint4 k0[Q], m0[Q], k1[Q], m1[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				bk[u][k] = make_uint4(0, 0, 0, 0);
-			if (L[u]) {
-				const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[u] * 4u;
-#pragma unroll
-				for (int k = 0; k < 4; k++)
-					bk[u][k] = p[k];
-			}
+			const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[u] * 4u;
+			const uint4 z = make_uint4(0, 0, 0, 0);
+			k0[u] = L[u] ? p[0] : z;
+			m0[u] = L[u] ? p[1] : z;
+			k1[u] = L[u] ? p[2] : z;
+			m1[u] = L[u] ? p[3] : z;
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
 			if (L[u])
-				res[u] = set16_resolve(t.set, bk[u], bi[u], key[u], 1u | (L[u] << 8));
+				res[u] = set16_resolve(t.set, k0[u], m0[u], k1[u], m1[u], bi[u], mask6(a[u], L[u]),
+						       1u | (L[u] << 8));
 	}
 #pragma unroll
 	for (int u = 0; u < Q; u++)
@@ -2271,7 +2265,8 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 #ifdef CGPU_DIAG_LDS_PAD /* timing-only: fewer resident workgroups per CU */
 	lds += CGPU_DIAG_LDS_PAD;
 #endif
-	const void *kern = (const void *)k_classify_x4<NT, true, 4, 1, LB, V6>;
+	constexpr int Q = V6 ? 2 : 4; /* v6: Q = 4 spills (16-byte addresses, 64-byte buckets) */
+	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6>;
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
@@ -2294,8 +2289,8 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 			c.sport += off;
 		if (c.hash)
 			c.hash += off;
-		const unsigned g = (unsigned)std::min<uint64_t>((m + 4 * NT - 1) / (4 * NT), res);
-		hipLaunchKernelGGL((k_classify_x4<NT, true, 4, 1, LB, V6>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		const unsigned g = (unsigned)std::min<uint64_t>((m + Q * NT - 1) / (Q * NT), res);
+		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);

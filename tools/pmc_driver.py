@@ -1,5 +1,6 @@
 """Minimal driver for rocprofv3 PMC passes: one bench workload (CGPU_PMC_CONFIG =
-gpu (config 2, default) / cascade (config 5) / pf6 (config 3)), one 64M-tuple
+gpu (config 2, default) / cascade (config 5) / pf6 (config 3) / v6 (IPv6
+classify at config-2 size)), one 64M-tuple
 batch resident in HBM, 3 launches (classify variant from CGPU_CLASSIFY_VARIANT)."""
 import os
 import sys
@@ -15,6 +16,20 @@ from cilium_amd.engine import Engine  # noqa: E402
 name = os.environ.get("CGPU_PMC_CONFIG", "gpu")
 cfg = synth.CONFIGS["gpu" if name == "pf6" else name]
 n = int(os.environ.get("CGPU_PMC_TUPLES", cfg["n_tuples"]))
+if name == "v6":
+    T = synth.make_tables6(**cfg)
+    t = synth.make_tuples6(T, n)
+    e = Engine(device=0, **T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    d = synth.to_device(t)
+    out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+           "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
+    for _ in range(3):
+        e.classify_v6(d, out=out)
+    torch.cuda.synchronize()
+    print("ok", name, n)
+    sys.exit(0)
 if name == "pf6":
     # config 3: the v6 prefilter sets of bench.py --config pf6
     P = synth.make_prefilter6(**synth.PF6_CONFIG)
