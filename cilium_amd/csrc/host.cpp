@@ -638,15 +638,18 @@ void build_set4(const std::vector<uint32_t> &keys, Set4Build &b)
 }
 
 /* keys: 4 u32 words + tag + entry (tag goes to `used` bits 8..15 and is
- * hashed as salt; entry goes to pad[0]) */
-void build_set16(const std::vector<std::array<uint32_t, 6>> &keys, Set16Build &b)
+ * hashed as salt; entry goes to pad[0]); pfx6: bucket by pfx6_hash (v6_lpm
+ * prefix keys), else hash16 */
+void build_set16(const std::vector<std::array<uint32_t, 6>> &keys, Set16Build &b, bool pfx6 = false)
 {
 	uint32_t nb = next_pow2(std::max<uint64_t>(8, keys.size() + 1));
 	b.slots.assign((size_t)nb * 2, set16_slot{});
 	b.mask = nb - 1;
 	b.max_probe = 1;
 	for (auto &k : keys) {
-		uint32_t bk = hash16(k[0], k[1], k[2], k[3], k[4]) & b.mask, probe = 1;
+		uint32_t bk = (pfx6 ? pfx6_hash(k[0], k[1], k[2], k[3], k[4]) : hash16(k[0], k[1], k[2], k[3], k[4])) &
+			      b.mask,
+			 probe = 1;
 		for (;;) {
 			set16_slot *s = &b.slots[(size_t)bk * 2];
 			int j = 0;
@@ -665,22 +668,6 @@ void build_set16(const std::vector<std::array<uint32_t, 6>> &keys, Set16Build &b
 		}
 		b.max_probe = std::max(b.max_probe, probe);
 	}
-}
-
-/* IPv6 address words as stored (network byte order in memory, u32 LE view) */
-void mask_v6(const uint8_t *addr, uint32_t len, uint32_t out[4])
-{
-	uint8_t m[16];
-	for (int i = 0; i < 16; i++) {
-		uint32_t bit0 = (uint32_t)i * 8;
-		uint8_t b = addr[i];
-		if (len <= bit0)
-			b = 0;
-		else if (len < bit0 + 8)
-			b &= (uint8_t)(0xFFu << (8 - (len - bit0)));
-		m[i] = b;
-	}
-	memcpy(out, m, 16);
 }
 
 struct Rank6 {
@@ -730,8 +717,13 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 		}
 		uint32_t bit = c.len - 17;
 		rootmask[top][bit / 32] |= 1u << (bit % 32);
-		std::array<uint32_t, 4> w;
-		mask_v6(c.addr.data(), c.len, w.data());
+		std::array<uint32_t, 4> w; /* the prefix key: host-order words, masked */
+		for (uint32_t i = 0; i < 4; i++) {
+			const uint32_t x = (uint32_t)c.addr[4 * i] << 24 | (uint32_t)c.addr[4 * i + 1] << 16 |
+					   (uint32_t)c.addr[4 * i + 2] << 8 | c.addr[4 * i + 3];
+			const uint32_t keep = c.len > 32 * i ? std::min(32u, c.len - 32 * i) : 0u;
+			w[i] = keep == 0 ? 0u : x & (0xFFFFFFFFu << (32 - keep));
+		}
 		longer[{c.len, w}] = enc; /* canonical keys are unique; later rank wins */
 	}
 	std::map<std::array<uint32_t, 4>, uint32_t> ids;
@@ -757,14 +749,14 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 		auto &w = kv.first.second;
 		keys.push_back({w[0], w[1], w[2], w[3], kv.first.first, kv.second});
 	}
-	build_set16(keys, b.set);
+	build_set16(keys, b.set, true);
 	/* ~12 bits per key, at most V6_BLOOM_MAX_WORDS words */
 	const uint32_t nw = (uint32_t)std::min<uint64_t>(
 		V6_BLOOM_MAX_WORDS, next_pow2(std::max<uint64_t>(64, keys.size() * 12 / 32 + 1)));
 	b.bloom.assign(nw, 0);
 	for (auto &k : keys) {
-		const uint32_t g = v6_bloom_h(hash16(k[0], k[1], k[2], k[3], k[4]));
-		b.bloom[g & (nw - 1)] |= v6_bloom_bits(g);
+		const uint32_t h = pfx6_hash(k[0], k[1], k[2], k[3], k[4]);
+		b.bloom[v6_bloom_word(h, nw - 1)] |= v6_bloom_bits(h);
 	}
 }
 

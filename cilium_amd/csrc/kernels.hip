@@ -241,24 +241,39 @@ __device__ __forceinline__ uint32_t set16_resolve(const addr_set16 &t, uint4 k0,
 	}
 }
 
-__device__ __forceinline__ uint4 mask6(uint4 w, uint32_t len)
+/* The IPv6 address words as stored (network-order bytes, little-endian u32
+ * view) -> host-order words (x = address bits 0..31), the prefix-key domain
+ * of tables.h pfx6_hash */
+__device__ __forceinline__ uint4 v6_host_words(uint4 a)
 {
-	uint32_t m[4];
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		int bits = (int)len - 32 * k;
-		uint32_t mh = bits <= 0 ? 0u : (bits >= 32 ? 0xFFFFFFFFu : (0xFFFFFFFFu << (32 - bits)));
-		m[k] = bswap32(mh);
-	}
-	return make_uint4(w.x & m[0], w.y & m[1], w.z & m[2], w.w & m[3]);
+	return make_uint4(bswap32(a.x), bswap32(a.y), bswap32(a.z), bswap32(a.w));
+}
+
+/* Running sums of pfx6_hash's word products: P.x = w0 C0, P.y = P.x + w1 C1,
+ * P.z = P.y + w2 C2 (a prefix cut in word k adds P_k + masked w_k C_k) */
+__device__ __forceinline__ uint3 pfx6_sums(uint4 w)
+{
+	const uint32_t p0 = w.x * PFX6_C0, p1 = p0 + w.y * PFX6_C1;
+	return make_uint3(p0, p1, p1 + w.z * PFX6_C2);
+}
+
+/* the prefix key of w at length len (17..128): words past the cut are 0 */
+__device__ __forceinline__ uint4 pfx6_key(uint4 w, uint32_t len)
+{
+	const uint32_t k = (len - 1u) >> 5;
+	const uint32_t m = 0xFFFFFFFFu << (32u - (len - 32u * k));
+	return make_uint4(k == 0 ? w.x & m : w.x, k < 1 ? 0u : (k == 1 ? w.y & m : w.y),
+			  k < 2 ? 0u : (k == 2 ? w.z & m : w.z), k < 3 ? 0u : w.w & m);
 }
 
 /* Next candidate length of an IPv6 lookup, longest first: pops lengths off
  * the root's mask (hi: 81..128, lo: 17..80) until one passes the bloom
- * filter (tables.h v6_lpm), and returns it with its masked key and set
- * bucket (0: none left).  bloom: the filter words (LDS or global). */
-__device__ __forceinline__ uint32_t v6_next(const v6_lpm &t, const uint32_t *bloom, uint4 a, uint64_t &hi,
-					    uint64_t &lo, uint4 &key, uint32_t &bucket)
+ * filter (tables.h v6_lpm) and returns it with its set bucket (0: none
+ * left).  w: host-order address words, P: pfx6_sums(w); bloom: the filter
+ * words (LDS or global).  Per length: one masked word, one multiply-add and
+ * the finalizer. */
+__device__ __forceinline__ uint32_t v6_next(const v6_lpm &t, const uint32_t *bloom, uint4 w, uint3 P,
+					    uint64_t &hi, uint64_t &lo, uint32_t &bucket)
 {
 	while (hi | lo) {
 		uint32_t len;
@@ -271,12 +286,14 @@ __device__ __forceinline__ uint32_t v6_next(const v6_lpm &t, const uint32_t *blo
 			lo &= ~(1ull << bit);
 			len = 17u + (uint32_t)bit;
 		}
-		const uint4 k = mask6(a, len);
-		const uint32_t h = hash16(k.x, k.y, k.z, k.w, len);
-		const uint32_t g = v6_bloom_h(h);
-		const uint32_t bits = v6_bloom_bits(g);
-		if ((bloom[g & t.bloom_mask] & bits) == bits) {
-			key = k;
+		const uint32_t k = (len - 1u) >> 5;
+		const uint32_t wk = k == 0 ? w.x : (k == 1 ? w.y : (k == 2 ? w.z : w.w));
+		const uint32_t pk = k == 0 ? 0u : (k == 1 ? P.x : (k == 2 ? P.y : P.z));
+		const uint32_t ck = k == 0 ? PFX6_C0 : (k == 1 ? PFX6_C1 : (k == 2 ? PFX6_C2 : PFX6_C3));
+		const uint32_t mk = wk & (0xFFFFFFFFu << (32u - (len - 32u * k)));
+		const uint32_t h = fmix32(pk + mk * ck + len * PFX6_CL);
+		const uint32_t bits = v6_bloom_bits(h);
+		if ((bloom[v6_bloom_word(h, t.bloom_mask)] & bits) == bits) {
 			bucket = h & t.set.bucket_mask;
 			return len;
 		}
@@ -288,15 +305,16 @@ __device__ __forceinline__ uint32_t v6_next(const v6_lpm &t, const uint32_t *blo
  * under the address's /16 are tried longest first; lengths the bloom filter
  * rules out cost no memory access, the others are probed four at a time
  * (independent bucket loads in flight); the first hit is the longest match.
- * Returns the DIR-encoded entry (0 = no match). */
+ * a: the address as stored.  Returns the DIR-encoded entry (0 = no match). */
 __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 {
 	if (!t.root)
 		return 0;
-	const uint32_t top = ((a.x & 0xFFu) << 8) | ((a.x >> 8) & 0xFFu);
-	const uint2 r = t.root[top];
+	const uint4 w = v6_host_words(a);
+	const uint2 r = t.root[w.x >> 16];
 	uint32_t res = 0;
 	if (r.x) {
+		const uint3 P = pfx6_sums(w);
 		const uint4 m = reinterpret_cast<const uint4 *>(t.masks)[r.x];
 		uint64_t hi = ((uint64_t)m.w << 32) | m.z, lo = ((uint64_t)m.y << 32) | m.x;
 		/* NB: the result is carried, never returned from inside the
@@ -304,12 +322,11 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 		 * gfx950 / ROCm 7.2 (round 1, reproduced in isolation). */
 		while ((hi | lo) && !res) {
 			uint32_t L[4], bi[4];
-			uint4 key[4], k0[4], m0[4], k1[4], m1[4];
+			uint4 k0[4], m0[4], k1[4], m1[4];
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
-				key[j] = make_uint4(0, 0, 0, 0);
 				bi[j] = 0;
-				L[j] = v6_next(t, t.bloom, a, hi, lo, key[j], bi[j]);
+				L[j] = v6_next(t, t.bloom, w, P, hi, lo, bi[j]);
 			}
 			/* issue every probe's bucket load before resolving any */
 #pragma unroll
@@ -325,7 +342,8 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 #pragma unroll
 			for (int j = 0; j < 4; j++)
 				if (!res && L[j])
-					res = set16_resolve(t.set, k0[j], m0[j], k1[j], m1[j], bi[j], key[j], 1u | (L[j] << 8));
+					res = set16_resolve(t.set, k0[j], m0[j], k1[j], m1[j], bi[j], pfx6_key(w, L[j]),
+							    1u | (L[j] << 8));
 		}
 	}
 	return res ? res : r.y;
@@ -968,20 +986,22 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  * gathers, then mask rows (the first nm rows from LDS), then rounds of one
  * bloom-admitted probe per unresolved tuple, Q bucket loads in flight.  The
  * filter leaves about one probe per tuple (the hit), so a round is usually
- * the last.  act[u] false: e[u] = 0 and no memory access. */
+ * the last.  w: host-order address words; act[u] false: e[u] = 0 and no
+ * memory access. */
 template <int Q>
 __device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *bloom, const uint4 *lmasks,
-					    uint32_t nm, const uint4 (&a)[Q], const bool (&act)[Q], uint32_t (&e)[Q])
+					    uint32_t nm, const uint4 (&w)[Q], const bool (&act)[Q], uint32_t (&e)[Q])
 {
 	uint2 r[Q];
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		r[u] = make_uint2(0, 0);
 		if (act[u] && t.root)
-			r[u] = t.root[((a[u].x & 0xFFu) << 8) | ((a[u].x >> 8) & 0xFFu)];
+			r[u] = t.root[w[u].x >> 16];
 	}
 	uint64_t hi[Q], lo[Q];
 	uint32_t res[Q];
+	uint3 P[Q];
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		uint4 m = make_uint4(0, 0, 0, 0);
@@ -990,6 +1010,7 @@ __device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *blo
 		hi[u] = ((uint64_t)m.w << 32) | m.z;
 		lo[u] = ((uint64_t)m.y << 32) | m.x;
 		res[u] = 0;
+		P[u] = pfx6_sums(w[u]);
 	}
 	for (;;) {
 		uint32_t L[Q], bi[Q];
@@ -998,10 +1019,8 @@ __device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *blo
 		for (int u = 0; u < Q; u++) {
 			L[u] = 0;
 			bi[u] = 0;
-			if (!res[u]) {
-				uint4 key;
-				L[u] = v6_next(t, bloom, a[u], hi[u], lo[u], key, bi[u]);
-			}
+			if (!res[u])
+				L[u] = v6_next(t, bloom, w[u], P[u], hi[u], lo[u], bi[u]);
 			more |= L[u] != 0;
 		}
 		if (!more)
@@ -1019,7 +1038,7 @@ __device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *blo
 #pragma unroll
 		for (int u = 0; u < Q; u++)
 			if (L[u])
-				res[u] = set16_resolve(t.set, k0[u], m0[u], k1[u], m1[u], bi[u], mask6(a[u], L[u]),
+				res[u] = set16_resolve(t.set, k0[u], m0[u], k1[u], m1[u], bi[u], pfx6_key(w[u], L[u]),
 						       1u | (L[u] << 8));
 	}
 #pragma unroll
@@ -1160,7 +1179,8 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 				for (int u = 0; u < Q; u++) {
 					const uint64_t i = i0 + u < a.n ? i0 + u : i0;
-					ad6[u] = ld_x4<NTL>(static_cast<const uint4 *>((fl[u] & 1u) ? a.daddr : a.saddr) + i);
+					ad6[u] = v6_host_words(
+						ld_x4<NTL>(static_cast<const uint4 *>((fl[u] & 1u) ? a.daddr : a.saddr) + i));
 				}
 			}
 			uint32_t lbf[Q];
@@ -1302,8 +1322,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint32_t label = entry_label(V6 ? s.ipc6.vals : s.ipc4c.vals, e[u]);
-			/* v6: ipv6_match_prefix_64(daddr, ROUTER_IP), bpf/lib/ipv6.h:166-175 */
-			const bool in_cluster = V6 ? ad6[u].x == s.router_ip64[0] && ad6[u].y == s.router_ip64[1]
+			/* v6: ipv6_match_prefix_64(daddr, ROUTER_IP), bpf/lib/ipv6.h:166-175
+			 * (ad6: host-order words) */
+			const bool in_cluster = V6 ? ad6[u].x == bswap32(s.router_ip64[0]) &&
+							     ad6[u].y == bswap32(s.router_ip64[1])
 						   : (ad[u] & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
 			if (fw[u] & F_EG) {
 				if (e[u] && label)

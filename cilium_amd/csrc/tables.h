@@ -188,35 +188,65 @@ static inline __host__ __device__ uint32_t hash16(uint32_t a0, uint32_t a1, uint
 	return mix32(mix32(a0, a1) ^ salt, mix32(a2, a3));
 }
 
-/* ---- IPv6 longest-prefix table (ipcache v6, prefilter v6) ----
+/* ---- IPv6 prefix keys of v6_lpm ----
+ * A prefix is keyed by its address as four host-order words (w0 = address
+ * bits 0..31), masked to its length, plus the length.  The hash is a
+ * multiply-sum over the words and the length with one 32-bit finalizer, so a
+ * lookup trying many lengths of one address recomputes only the word the
+ * length cuts (kernels.hip v6_next) instead of a full 16-byte hash. */
+#define PFX6_C0 0x9E3779B1u
+#define PFX6_C1 0x85EBCA77u
+#define PFX6_C2 0xC2B2AE3Du
+#define PFX6_C3 0x27D4EB2Fu
+#define PFX6_CL 0x165667B1u
+
+static inline __host__ __device__ uint32_t fmix32(uint32_t h)
+{
+	h ^= h >> 16;
+	h *= 0x85ebca6bu;
+	h ^= h >> 13;
+	h *= 0xc2b2ae35u;
+	h ^= h >> 16;
+	return h;
+}
+
+static inline __host__ __device__ uint32_t pfx6_hash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+						     uint32_t len)
+{
+	return fmix32(w0 * PFX6_C0 + w1 * PFX6_C1 + w2 * PFX6_C2 + w3 * PFX6_C3 + len * PFX6_CL);
+}
+
+/* ---- IPv6 longest-prefix table (ipcache v6) ----
  * root[addr >> 112] (65536 x {row, short}): `short` is the longest entry of
  * length <= 16 covering that /16 (DIR-24-8 entry encoding, 0 = none) and
  * `row` selects a 128-bit row of `masks`: the prefix lengths 17..128 present
  * under that /16 (bit L-17).  Each present length L is ONE probe of `set`,
- * keyed by (address masked to L, L); a slot's pad[0] holds the entry.  The
- * probes of one address do not depend on each other, so they are issued in
- * groups of four, longest first (memory-level parallelism instead of a
- * 128-level pointer chase); the first hit in descending length order is the
- * longest match, else `short`. */
+ * keyed by the prefix key (host-order words masked to L, L; bucket =
+ * pfx6_hash & bucket_mask); a slot's pad[0] holds the entry.  A bloom
+ * filter over the same keys rules most lengths out without a memory access;
+ * the probes left do not depend on each other and are issued together,
+ * longest first; the first hit in descending length order is the longest
+ * match, else `short`. */
 typedef struct v6_lpm {
 	const uint2 *root;     /* 65536 x {row, short entry}; NULL = empty table */
 	const uint32_t *masks; /* n_masks x 4 u32 (row 0 = no lengths) */
 	const uint32_t *vals;  /* indirect labels (>= 2^30) */
 	addr_set16 set;        /* used: bit0 used, bits 8..15 length; pad[0] entry */
 	uint32_t n_masks;
-	/* blocked bloom filter over the set's (masked address, length) keys:
-	 * one 32-bit word per key (v6_bloom_word), three bits in it
-	 * (v6_bloom_bits).  A probe whose bits are not all set cannot hit and
-	 * is not issued; no false negatives, so results never depend on it. */
+	/* blocked bloom filter over the set's prefix keys: one 32-bit word per
+	 * key (bits 16.. of its pfx6_hash), three bits in it (v6_bloom_bits).
+	 * A probe whose bits are not all set cannot hit and is not issued; no
+	 * false negatives, so results never depend on it. */
 	const uint32_t *bloom;
 	uint32_t bloom_mask;   /* n_words - 1 (n_words a power of two <= 2^14) */
 } v6_lpm;
 
 #define V6_BLOOM_MAX_WORDS 16384u /* 64 KiB: staged in LDS by the x4 kernel */
 
-static inline __host__ __device__ uint32_t v6_bloom_h(uint32_t h) { return mix32(h, 0xB100Fu); }
-static inline __host__ __device__ uint32_t v6_bloom_bits(uint32_t g)
+static inline __host__ __device__ uint32_t v6_bloom_word(uint32_t h, uint32_t mask) { return (h >> 16) & mask; }
+static inline __host__ __device__ uint32_t v6_bloom_bits(uint32_t h)
 {
+	const uint32_t g = h * 0x2545F491u;
 	return (1u << ((g >> 17) & 31u)) | (1u << ((g >> 22) & 31u)) | (1u << (g >> 27));
 }
 
