@@ -762,10 +762,9 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 
 /* ---- IPv6 any-match cover (tables.h cover6) ---- */
 struct Cover6Build {
-	std::vector<uint32_t> root, pool;
-	std::vector<std::array<uint32_t, 4>> h32;
+	std::vector<uint32_t> root, b24, b32, pool;
 	std::vector<std::array<uint32_t, 8>> h64;
-	uint32_t m32 = 0, m64 = 0;
+	uint32_t m64 = 0;
 	bool any = false;
 };
 
@@ -790,13 +789,12 @@ template <typename T> std::vector<std::pair<T, T>> merge_iv(std::vector<std::pai
 	return out;
 }
 
-/* node {nb, rest_deep, nd, 0} + nb boundaries + nd deep points: covered iff
- * #(b <= x) is odd.  At the /32 level the deep points are the sorted bits
- * 32..63 of every /64 that has an h64 record, so a reader can tell WHICH
- * uncovered x descend (c6_node32_coop); readers that ignore them descend on
- * rest_deep, which is always safe (the h64 probe then misses). */
+/* /32 node {nb, rest_deep, nd, 0} + nb boundaries + nd deep points: covered
+ * iff #(b <= x) is odd.  The deep points are the sorted bits 32..63 of every
+ * /64 that has an h64 record, so a reader can tell WHICH uncovered x descend
+ * (c6_node32_coop). */
 uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uint32_t>> &iv, bool deep,
-		       const std::vector<uint32_t> &points = {})
+		       const std::vector<uint32_t> &points)
 {
 	std::vector<uint32_t> bnd;
 	for (auto &x : iv) {
@@ -868,10 +866,68 @@ void hop_place(std::vector<std::array<uint32_t, W>> &tab, uint32_t &mask,
 	}
 }
 
-uint32_t h32_home(const std::array<uint32_t, 4> &r) { return mix32(r[0], 0xC0E6u); }
 uint32_t h64_home(const std::array<uint32_t, 8> &r) { return mix32(r[0], r[1]); }
 
-/* Any-match cover of (len, address) prefixes, see tables.h cover6. */
+/* The /32 entry of the prefixes longer than /32 among ps[k, l) (one /32,
+ * sorted; shorter ones are skipped): an interval node over bits 32..63 (/33../64) with the
+ * deep points of its /64 records, or DEEP when only /65+ prefixes exist;
+ * appends the /64 records to r64. */
+uint32_t cover6_group32(Cover6Build &b, const std::vector<P6> &ps, size_t k, size_t l,
+			std::vector<std::array<uint32_t, 8>> &r64)
+{
+	std::vector<std::pair<uint32_t, uint32_t>> s2;
+	std::vector<uint32_t> pts; /* the /64s with an h64 record (sorted by hi) */
+	for (size_t q = k; q < l; q++) {
+		const P6 &p = ps[q];
+		if (p.len <= 32)
+			continue;
+		if (p.len <= 64) {
+			const uint32_t st = (uint32_t)p.hi;
+			const uint32_t span = 64 - p.len;
+			s2.push_back({st, span == 32 ? 0xFFFFFFFFu : st + ((1u << span) - 1u)});
+		} else if (pts.empty() || pts.back() != (uint32_t)p.hi) {
+			pts.push_back((uint32_t)p.hi);
+		}
+	}
+	/* /64 groups */
+	size_t m = k;
+	while (m < l) {
+		if (ps[m].len <= 64) {
+			m++;
+			continue;
+		}
+		const uint64_t top64 = ps[m].hi;
+		std::vector<std::pair<uint64_t, uint64_t>> s3;
+		size_t q = m;
+		for (; q < l && ps[q].hi == top64; q++) {
+			const P6 &p = ps[q];
+			if (p.len > 64) {
+				const uint32_t span = 128 - p.len;
+				s3.push_back({p.lo, span == 64 ? ~0ull : p.lo + ((1ull << span) - 1ull)});
+			}
+		}
+		auto iv = merge_iv(s3);
+		std::array<uint32_t, 8> r{(uint32_t)(top64 >> 32), (uint32_t)top64, 0u, 0u, 0u, 0u, 0u, 0u};
+		if (iv.size() == 1) {
+			r[2] = COVER6_FULL << 30; /* inline [lo, hi] */
+			r[4] = (uint32_t)(iv[0].first >> 32);
+			r[5] = (uint32_t)iv[0].first;
+			r[6] = (uint32_t)(iv[0].second >> 32);
+			r[7] = (uint32_t)iv[0].second;
+		} else {
+			r[2] = cover6_node64(b, iv);
+		}
+		r64.push_back(r);
+		m = q;
+	}
+	return s2.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s2), !pts.empty(), pts);
+}
+
+/* Any-match cover of (len, address) prefixes, see tables.h cover6: /0../16
+ * fill root entries, /17../24 fill entries of the /16's 256-entry b24 block,
+ * /25../32 entries of the /24's b32 block (controlled prefix expansion: an
+ * any-match set needs no priorities), longer prefixes become the node or
+ * DEEP entry of their /32 unless a shorter prefix covers it whole. */
 void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 {
 	b.any = !cand.empty();
@@ -888,14 +944,16 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 		ps.push_back(P6{hi, lo, c.len});
 	}
 	std::sort(ps.begin(), ps.end());
+	const uint32_t FULL = COVER6_FULL << 30, DEEP = COVER6_DEEP << 30;
 	b.root.assign(65536, 0);
+	b.b24.clear();
+	b.b32.clear();
 	for (auto &p : ps)
 		if (p.len <= 16) {
 			const uint32_t cnt = 1u << (16 - p.len);
 			const uint32_t base = p.len == 0 ? 0 : ((uint32_t)(p.hi >> 48) & ~(cnt - 1));
-			std::fill(b.root.begin() + base, b.root.begin() + base + cnt, COVER6_FULL << 30);
+			std::fill(b.root.begin() + base, b.root.begin() + base + cnt, FULL);
 		}
-	std::vector<std::array<uint32_t, 4>> r32;
 	std::vector<std::array<uint32_t, 8>> r64;
 	size_t i = 0;
 	while (i < ps.size()) {
@@ -903,126 +961,63 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 		size_t j = i;
 		while (j < ps.size() && (uint32_t)(ps[j].hi >> 48) == top16)
 			j++;
-		if ((b.root[top16] >> 30) == COVER6_FULL) {
+		bool below16 = false;
+		for (size_t k = i; k < j; k++)
+			below16 |= ps[k].len > 16;
+		if (b.root[top16] == FULL || !below16) {
 			i = j;
 			continue;
 		}
-		std::vector<std::pair<uint32_t, uint32_t>> s1;
-		bool deeper = false;
-		for (size_t k = i; k < j; k++) {
-			const P6 &p = ps[k];
-			if (p.len > 16 && p.len <= 32) {
-				const uint32_t st = (uint32_t)(p.hi >> 32) & 0xFFFFu;
-				s1.push_back({st, st + (1u << (32 - p.len)) - 1u});
-			} else if (p.len > 32) {
-				deeper = true;
+		/* the /16's b24 block: /17../24 prefixes */
+		std::array<uint32_t, 256> e24{};
+		for (size_t k = i; k < j; k++)
+			if (ps[k].len > 16 && ps[k].len <= 24) {
+				const uint32_t cnt = 1u << (24 - ps[k].len);
+				const uint32_t base = (uint32_t)(ps[k].hi >> 40) & 0xFFu & ~(cnt - 1);
+				std::fill(e24.begin() + base, e24.begin() + base + cnt, FULL);
 			}
-		}
-		if (s1.empty() && !deeper) {
-			i = j;
-			continue;
-		}
-		/* A /16 node longer than one 128-B line (> 28 boundaries) would be
-		 * scanned by every packet under the /16.  Its long prefixes
-		 * (/28../32, at most 16 /32s each) move down instead: every /32
-		 * they cover gets an h32 record tagged FULL, and the /16 keeps only
-		 * /17../27 intervals. */
-		std::vector<uint32_t> full32; /* sorted low 16 bits of the FULL /32s */
-		auto iv1 = merge_iv(s1);
-		if (iv1.size() > 14) {
-			std::vector<std::pair<uint32_t, uint32_t>> keep;
-			for (auto &x : s1) {
-				if (x.second - x.first < 16u) {
-					for (uint32_t v = x.first; v <= x.second; v++)
-						full32.push_back(v);
-				} else {
-					keep.push_back(x);
-				}
-			}
-			std::sort(full32.begin(), full32.end());
-			full32.erase(std::unique(full32.begin(), full32.end()), full32.end());
-			iv1 = merge_iv(keep);
-			s1.swap(keep);
-		}
-		const bool down = deeper || !full32.empty();
-		b.root[top16] = s1.empty() ? COVER6_DEEP << 30 : cover6_node32(b, iv1, down);
-		auto is_full32 = [&](uint32_t top32) {
-			return std::binary_search(full32.begin(), full32.end(), top32 & 0xFFFFu);
-		};
-		/* /32 groups of the deeper prefixes (sorted by hi: contiguous) */
+		/* /24 groups (contiguous in sorted order) */
 		size_t k = i;
 		while (k < j) {
-			if (ps[k].len <= 32) {
-				k++;
-				continue;
-			}
-			const uint32_t top32 = (uint32_t)(ps[k].hi >> 32);
+			const uint32_t x24 = (uint32_t)(ps[k].hi >> 40) & 0xFFu;
 			size_t l = k;
-			if (is_full32(top32)) { /* covered whole: deeper prefixes are moot */
-				while (l < j && (uint32_t)(ps[l].hi >> 32) == top32)
-					l++;
+			while (l < j && ((uint32_t)(ps[l].hi >> 40) & 0xFFu) == x24)
+				l++;
+			bool below = false;
+			for (size_t q = k; q < l; q++)
+				below |= ps[q].len > 24;
+			if (e24[x24] == FULL || !below) {
 				k = l;
 				continue;
 			}
-			std::vector<std::pair<uint32_t, uint32_t>> s2;
-			bool deeper2 = false;
-			size_t first64 = ps.size();
-			std::vector<uint32_t> pts; /* the /64s with an h64 record (sorted by hi) */
-			for (; l < j && (uint32_t)(ps[l].hi >> 32) == top32; l++) {
-				const P6 &p = ps[l];
-				if (p.len > 32 && p.len <= 64) {
-					const uint32_t st = (uint32_t)p.hi;
-					const uint32_t span = 64 - p.len;
-					s2.push_back({st, span == 32 ? 0xFFFFFFFFu : st + ((1u << span) - 1u)});
-				} else if (p.len > 64) {
-					deeper2 = true;
-					if (first64 == ps.size())
-						first64 = l;
-					if (pts.empty() || pts.back() != (uint32_t)p.hi)
-						pts.push_back((uint32_t)p.hi);
+			std::array<uint32_t, 256> e32{};
+			for (size_t q = k; q < l; q++)
+				if (ps[q].len > 24 && ps[q].len <= 32) {
+					const uint32_t cnt = 1u << (32 - ps[q].len);
+					const uint32_t base = (uint32_t)(ps[q].hi >> 32) & 0xFFu & ~(cnt - 1);
+					std::fill(e32.begin() + base, e32.begin() + base + cnt, FULL);
 				}
+			size_t q = k;
+			while (q < l) {
+				const uint32_t x32 = (uint32_t)(ps[q].hi >> 32) & 0xFFu;
+				size_t r = q;
+				while (r < l && ((uint32_t)(ps[r].hi >> 32) & 0xFFu) == x32)
+					r++;
+				bool below32 = false;
+				for (size_t t = q; t < r; t++)
+					below32 |= ps[t].len > 32;
+				if (e32[x32] != FULL && below32)
+					e32[x32] = cover6_group32(b, ps, q, r, r64);
+				q = r;
 			}
-			const uint32_t e2 =
-				s2.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s2), deeper2, pts);
-			r32.push_back({top32, e2, 0u, 0u});
-			/* /64 groups */
-			size_t m = first64;
-			while (m < l) {
-				if (ps[m].len <= 64) {
-					m++;
-					continue;
-				}
-				const uint64_t top64 = ps[m].hi;
-				std::vector<std::pair<uint64_t, uint64_t>> s3;
-				size_t q = m;
-				for (; q < l && ps[q].hi == top64; q++) {
-					const P6 &p = ps[q];
-					if (p.len > 64) {
-						const uint32_t span = 128 - p.len;
-						s3.push_back({p.lo, span == 64 ? ~0ull : p.lo + ((1ull << span) - 1ull)});
-					}
-				}
-				auto iv = merge_iv(s3);
-				std::array<uint32_t, 8> r{(uint32_t)(top64 >> 32), (uint32_t)top64, 0u, 0u, 0u, 0u, 0u, 0u};
-				if (iv.size() == 1) {
-					r[2] = COVER6_FULL << 30; /* inline [lo, hi] */
-					r[4] = (uint32_t)(iv[0].first >> 32);
-					r[5] = (uint32_t)iv[0].first;
-					r[6] = (uint32_t)(iv[0].second >> 32);
-					r[7] = (uint32_t)iv[0].second;
-				} else {
-					r[2] = cover6_node64(b, iv);
-				}
-				r64.push_back(r);
-				m = q;
-			}
+			e24[x24] = DEEP | (uint32_t)(b.b32.size() / 256);
+			b.b32.insert(b.b32.end(), e32.begin(), e32.end());
 			k = l;
 		}
-		for (uint32_t v : full32)
-			r32.push_back({top16 << 16 | v, COVER6_FULL << 30, 0u, 0u});
+		b.root[top16] = DEEP | (uint32_t)(b.b24.size() / 256);
+		b.b24.insert(b.b24.end(), e24.begin(), e24.end());
 		i = j;
 	}
-	hop_place<4>(b.h32, b.m32, r32, h32_home);
 	hop_place<8>(b.h64, b.m64, r64, h64_home);
 	/* 8 zero units past the last node: the octet load of a node reads
 	 * 128 B from its start whatever its length */
@@ -2658,7 +2653,7 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	Cover6Build pf6;
 	build_cover6(pf6_candidates(in.pf), pf6);
 	Arena ar;
-	size_t o4[4] = {0, 0, 0, 0}, o6[4] = {0, 0, 0, 0};
+	size_t o4[4] = {0, 0, 0, 0}, o6[5] = {0, 0, 0, 0, 0};
 	if (have4) {
 		o4[0] = ar.add(lc.x16.data(), lc.x16.size() * 4);
 		o4[1] = ar.add(lc.d16.data(), lc.d16.size() * 4);
@@ -2668,8 +2663,9 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	if (pf6.any) {
 		o6[0] = ar.add(pf6.root.data(), pf6.root.size() * 4);
 		o6[1] = ar.add(pf6.pool.data(), pf6.pool.size() * 4);
-		o6[2] = ar.add(pf6.h32.data(), pf6.h32.size() * 16);
-		o6[3] = ar.add(pf6.h64.data(), pf6.h64.size() * 32);
+		o6[2] = ar.add(pf6.b24.data(), pf6.b24.size() * 4);
+		o6[3] = ar.add(pf6.b32.data(), pf6.b32.size() * 4);
+		o6[4] = ar.add(pf6.h64.data(), pf6.h64.size() * 32);
 	}
 	if (int r = upload(c, ar, buf))
 		return r;
@@ -2679,8 +2675,8 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 				at<uint32_t>(buf, o4[3]), (uint32_t)lc.nodes.size(), (uint32_t)lc.dict.size()};
 	s.pf6 = cover6{};
 	if (pf6.any)
-		s.pf6 = cover6{at<uint32_t>(buf, o6[0]), at<uint32_t>(buf, o6[1]), at<uint4>(buf, o6[2]),
-			       at<uint4>(buf, o6[3]), pf6.m32, pf6.m64};
+		s.pf6 = cover6{at<uint32_t>(buf, o6[0]), at<uint32_t>(buf, o6[2]), at<uint32_t>(buf, o6[3]),
+			       at<uint32_t>(buf, o6[1]), at<uint4>(buf, o6[4]), pf6.m64};
 	uint64_t sum = 0;
 	for (auto &k : in.pf.dyn4k) sum += fnv(7, &k, 8);
 	for (auto &k : in.pf.dyn6k) sum += fnv(11, &k, 20);

@@ -643,29 +643,6 @@ template <int MODE> __global__ __launch_bounds__(BLOCK) void k_lb4(cgpu_snapshot
 
 /* ---- IPv6 any-match cover (tables.h cover6) ---- */
 
-/* covered iff #(boundaries <= x) is odd; *deep = node's rest_deep */
-__device__ __forceinline__ bool c6_node32(const uint32_t *pool, uint32_t off, uint32_t x, bool *deep)
-{
-	const uint4 *nd = reinterpret_cast<const uint4 *>(pool) + off;
-	const uint4 h = nd[0];
-	const uint32_t nb = h.x;
-	*deep = h.y != 0;
-	uint32_t cnt = 0;
-	for (uint32_t k = 0; k < nb; k += 16) {
-		uint4 q[4];
-#pragma unroll
-		for (uint32_t j = 0; j < 4; j++)
-			q[j] = k + 4 * j < nb ? nd[1 + k / 4 + j] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-		for (uint32_t j = 0; j < 4; j++) {
-			const uint32_t i = k + 4 * j;
-			cnt += (i < nb && q[j].x <= x ? 1u : 0u) + (i + 1 < nb && q[j].y <= x ? 1u : 0u) +
-			       (i + 2 < nb && q[j].z <= x ? 1u : 0u) + (i + 3 < nb && q[j].w <= x ? 1u : 0u);
-		}
-	}
-	return cnt & 1u;
-}
-
 __device__ __forceinline__ bool le64(uint32_t ah, uint32_t al, uint32_t bh, uint32_t bl)
 {
 	return ah < bh || (ah == bh && al <= bl);
@@ -1110,10 +1087,13 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		const bool full = i0 + Q <= a.n;
 		/* decode: hi4 = the policy key's upper word {dport, proto, egress}
 		 * (policy.h:61-64), fw = flag word, ad = the looked-up address */
-		uint32_t fw[Q], ad[Q], hi4[Q], ep[Q], len[Q];
+		/* QA: the vector-load branches below are written for Q = 4; arrays
+		 * they fill are sized for them whatever Q (dead when Q != 4) */
+		constexpr int QA = Q < 4 ? 4 : Q;
+		uint32_t fw[Q], ad[Q], hi4[Q], ep[QA], len[QA];
 		uint4 ad6[Q];
 		{
-			uint32_t fl[Q], proto[Q], dport[Q], sa[Q], da[Q];
+			uint32_t fl[QA], proto[QA], dport[QA], sa[QA], da[QA];
 			if (full && Q == 4) {
 				const uint32_t f4 = ld_x1<NTL>(a.flags + i0);
 				const uint32_t p4 = ld_x1<NTL>(a.proto + i0);
@@ -1190,7 +1170,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 			if (LB) {
 				/* egress service step first (bpf_lxc.c:444-469): the
 				 * translated tuple.daddr and dport feed ipcache / policy */
-				uint32_t hh[Q], sp[Q];
+				uint32_t hh[QA], sp[QA];
 #pragma unroll
 				for (int u = 0; u < Q; u++)
 					hh[u] = sp[u] = 0;
@@ -1318,7 +1298,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 			}
 		}
 		/* identity (bpf_lxc.c:488-496 / bpf_netdev.c:374-404) */
-		uint32_t id[Q];
+		uint32_t id[QA];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint32_t label = entry_label(V6 ? s.ipc6.vals : s.ipc4c.vals, e[u]);
@@ -1348,7 +1328,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		 * (identity 0) gathers directly.  Stages and counters are the
 		 * reference's: st = the probe that hit. */
 		int ctr[Q];
-		uint32_t z[Q], st[Q], bk[Q], need[Q];
+		uint32_t z[Q], st[QA], bk[Q], need[Q];
 		uint4 sl[Q], grp[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
@@ -1406,7 +1386,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				st[u] = 3;
 			}
 		/* counters, outputs, metrics */
-		int32_t v[Q];
+		int32_t v[QA];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			if (fw[u] & F_LBDROP) {
@@ -1869,71 +1849,14 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilt
 
 /*
  * XDP prefilter IPv6, Q packets per lane with the cover lookup advanced
- * stage by stage across them (root, /32 record, interval node in chunks of
- * 12 / 16 / 16 boundaries, /64 record, endpoint bucket), so each stage has Q
- * independent gathers in flight per lane: bpf/bpf_xdp.c:132-156 (any deny
- * prefix covers saddr -> XDP_DROP), then check_v6_endpoint :123-130.
+ * stage by stage across them (root, b24, b32, interval node, /64 record,
+ * endpoint bucket), so each stage has Q independent gathers in flight per
+ * lane: bpf/bpf_xdp.c:132-156 (any deny prefix covers saddr -> XDP_DROP),
+ * then check_v6_endpoint :123-130.
  */
-__device__ __forceinline__ uint32_t c6_count4(uint4 q, uint32_t base, uint32_t nb, uint32_t x)
-{
-	return (base < nb && q.x <= x ? 1u : 0u) + (base + 1 < nb && q.y <= x ? 1u : 0u) +
-	       (base + 2 < nb && q.z <= x ? 1u : 0u) + (base + 3 < nb && q.w <= x ? 1u : 0u);
-}
-
-template <int Q>
-__device__ __forceinline__ void c6_node32_q(const uint32_t *pool, const uint32_t (&e)[Q], const uint32_t (&x)[Q],
-					    uint32_t (&tag)[Q], bool (&hit)[Q])
-{
-	const uint4 *P = reinterpret_cast<const uint4 *>(pool);
-	uint4 q[Q][4];
-	uint32_t cnt[Q], nb[Q];
-	bool deep[Q];
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		cnt[u] = 0;
-		nb[u] = 0;
-#pragma unroll
-		for (int j = 0; j < 4; j++)
-			q[u][j] = tag[u] == COVER6_NODE ? P[(e[u] & 0x3FFFFFFFu) + j] : make_uint4(0, 0, 0, 0);
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		nb[u] = q[u][0].x;
-		deep[u] = q[u][0].y != 0;
-#pragma unroll
-		for (int j = 1; j < 4; j++)
-			cnt[u] += c6_count4(q[u][j], 4u * (j - 1), nb[u], x[u]);
-	}
-	/* boundaries 12..27 of every node at once */
-#pragma unroll
-	for (int u = 0; u < Q; u++)
-#pragma unroll
-		for (int j = 0; j < 4; j++)
-			q[u][j] = (tag[u] == COVER6_NODE && nb[u] > 12u + 4u * j)
-					  ? P[(e[u] & 0x3FFFFFFFu) + 4 + j]
-					  : make_uint4(0, 0, 0, 0);
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-#pragma unroll
-		for (int j = 0; j < 4; j++)
-			cnt[u] += c6_count4(q[u][j], 12u + 4u * j, nb[u], x[u]);
-		/* rare long nodes: the rest one chunk at a time */
-		for (uint32_t k = 28; k < nb[u]; k += 4) {
-			const uint4 r = P[(e[u] & 0x3FFFFFFFu) + 1 + k / 4];
-			cnt[u] += c6_count4(r, k, nb[u], x[u]);
-		}
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (tag[u] != COVER6_NODE)
-			continue;
-		hit[u] = cnt[u] & 1u;
-		tag[u] = !hit[u] && deep[u] ? COVER6_DEEP : COVER6_NONE;
-	}
-}
 
 /*
- * c6_node32_q with each node read cooperatively: the 8 lanes of an octet take
+ * The /32 interval nodes of Q packets per lane, each node read cooperatively: the 8 lanes of an octet take
  * the octet's Q x 8 nodes in turn, lane j loading 16-B unit j of the node, so
  * one load instruction touches one 128-B line per node instead of one line
  * per lane and unit (the node pass was 8 L2 requests per packet; the kernel is
@@ -2040,7 +1963,7 @@ __device__ __forceinline__ bool set16_has_first(const addr_set16 &t, const uint4
 	return res;
 }
 
-template <int Q, bool COOP = false>
+template <int Q>
 __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q], const bool (&act)[Q], bool (&hit)[Q])
 {
 	uint32_t w0[Q], w1[Q], w2[Q], w3[Q], e[Q], tag[Q];
@@ -2050,54 +1973,26 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 		w1[u] = bswap32(a[u].y);
 		w2[u] = bswap32(a[u].z);
 		w3[u] = bswap32(a[u].w);
-		hit[u] = false;
 		e[u] = act[u] && t.root ? t.root[w0[u] >> 16] : 0u;
 	}
-	/* /16: a node there is rare (prefixes of 17..32 bits) */
+	/* the two direct-indexed levels: bits 16..23, then 24..31 */
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		if ((e[u] >> 30) == COVER6_DEEP)
+			e[u] = t.b24[(e[u] & 0x3FFFFFFFu) * 256u + ((w0[u] >> 8) & 0xFFu)];
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		if ((e[u] >> 30) == COVER6_DEEP)
+			e[u] = t.b32[(e[u] & 0x3FFFFFFFu) * 256u + (w0[u] & 0xFFu)];
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		tag[u] = e[u] >> 30;
 		hit[u] = tag[u] == COVER6_FULL;
-		if (tag[u] == COVER6_NODE) {
-			bool deep;
-			hit[u] = c6_node32(t.pool, e[u] & 0x3FFFFFFFu, w0[u] & 0xFFFFu, &deep);
-			tag[u] = !hit[u] && deep ? COVER6_DEEP : COVER6_NONE;
-		}
 	}
-	/* /32 records */
-	uint4 sl[Q];
-	uint32_t home[Q];
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		home[u] = mix32(w0[u], 0xC0E6u) & t.m32;
-		sl[u] = tag[u] == COVER6_DEEP ? t.h32[home[u]] : make_uint4(0, 0, 0, 0);
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (tag[u] != COVER6_DEEP)
-			continue;
-		uint32_t hop = sl[u].w >> POL_HOP_SHIFT;
-		uint4 r = make_uint4(0, 0, 0, 0);
-		if ((hop & 1u) && sl[u].x == w0[u])
-			r = sl[u];
-		hop &= ~1u;
-		while (hop && !r.w) {
-			const uint32_t j = __builtin_ctz(hop);
-			hop &= hop - 1u;
-			const uint4 x = t.h32[(home[u] + j) & t.m32];
-			if (x.x == w0[u])
-				r = x;
-		}
-		e[u] = r.y;
-		tag[u] = r.w ? (r.y >> 30) : COVER6_NONE;
-		hit[u] = tag[u] == COVER6_FULL;
-	}
-	if (COOP)
-		c6_node32_coop<Q>(t.pool, e, w1, tag, hit);
-	else
-		c6_node32_q<Q>(t.pool, e, w1, tag, hit);
+	c6_node32_coop<Q>(t.pool, e, w1, tag, hit);
 	/* /64 records */
 	uint4 s0[Q], s1[Q];
+	uint32_t home[Q];
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		home[u] = mix32(w0[u], w1[u]) & t.m64;
@@ -2135,17 +2030,17 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 	}
 }
 
-/* W: minimum resident waves per SIMD the registers are fitted to.  COOP:
- * octet-cooperative /32 node reads (c6_node32_coop); the loop trip count is
- * then uniform per wave, lanes past the batch end carry inactive packets. */
-template <int Q, int W = 1, bool COOP = false>
+/* W: minimum resident waves per SIMD the registers are fitted to.  The /32
+ * node reads are octet-cooperative (c6_node32_coop), so the loop trip count
+ * is uniform per wave; lanes past the batch end carry inactive packets. */
+template <int Q, int W = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_prefilter_v6_q(cgpu_snapshot s,
 												     prefilter_args a)
 {
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
 	const uint64_t T = (uint64_t)gridDim.x * 256;
-	const uint64_t lane0 = COOP ? (threadIdx.x & 63u) : 0u; /* COOP: loop on the wave's first lane */
+	const uint64_t lane0 = threadIdx.x & 63u; /* the loop runs on the wave's first lane */
 	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x - lane0; g * Q < a.n; g += T) {
 		const uint64_t i0 = (g + lane0) * Q;
 		uint4 sa[Q], da[Q];
@@ -2161,7 +2056,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			f[u] = a.flags[i];
 			act[u] = i0 + u < a.n && f[u] == 0u && s.pf6_enabled;
 		}
-		cover6_any_q<Q, COOP>(s.pf6, sa, act, hit);
+		cover6_any_q<Q>(s.pf6, sa, act, hit);
 		/* check_v6_endpoint: cilium_lxc on daddr (bucket loads for all first) */
 		uint4 bk[Q][4];
 		uint32_t b[Q];
@@ -2406,7 +2301,7 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 	/* four packets per lane, octet-cooperative node reads.  A/B on config 3
 	 * (Gpps, round 1): Q=4 coop 24.8; Q=4 per-lane nodes 21.1; Q=4 fitted
 	 * to 5 waves/SIMD 20.4; Q=2 20.9; Q=1 20.5. */
-	hipLaunchKernelGGL((k_prefilter_v6_q<4, 1, true>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
+	hipLaunchKernelGGL((k_prefilter_v6_q<4, 1>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
 	return hipGetLastError();
 }
 

@@ -312,23 +312,24 @@ static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t da
 /* ---- IPv6 any-match cover (XDP prefilter v6) ----
  * The prefilter only asks "does ANY deny prefix cover saddr" (bpf_xdp.c:
  * 142-152: both the dyn LPM and the fix /128 hash lead to XDP_DROP), so the
- * union of the prefixes is compiled into covered intervals at strides
- * 16 / 32 / 64 / 128 bits:
- *   root[top16]: entry (below) for the /16;
- *   h32: hop-hashed 16-B slots {top32, entry, 0, used | hop << 24} for the
- *        /32s holding prefixes longer than /32;
+ * union of the prefixes is compiled into a multibit trie of strides
+ * 16 / 8 / 8 with covered intervals below /32:
+ *   root[bits 0..15] -> b24[block * 256 + bits 16..23] -> b32[block * 256 +
+ *   bits 24..31]: direct-indexed u32 entries; prefixes of /17../32 are
+ *   expanded into the entries they cover (an any-match set has no
+ *   priorities, so expansion is exact).  b32 entries of /32s holding
+ *   longer prefixes are NODEs: {nb, rest_deep, nd, 0} + nb sorted u32
+ *   boundaries of the merged covered intervals of bits 32..63 (covered iff
+ *   #(boundaries <= x) is odd) + nd "deep points" (bits 32..63 of every /64
+ *   with an h64 record: an uncovered x descends only if it is one of them).
  *   h64: hop-hashed 32-B slots {top64.hi, top64.lo, entry, used | hop << 24,
  *        lo.hi, lo.lo, hi.hi, hi.lo} for the /64s holding prefixes longer
- *        than /64 (an INLINE entry covers [lo, hi] of the low 64 bits).
- * entry: tag << 30 | payload, tag COVER6_NONE / _FULL / _DEEP (consult the
- * next level) / _NODE (payload = offset in 16-B units into `pool`).
- * A node is {nb, rest_deep, nd, 0} + nb sorted boundaries (u32 at levels
- * 16/32, u64 as {hi, lo} at level 64) of merged covered intervals: an address
- * is covered iff #(boundaries <= x) is odd; otherwise it descends when
- * rest_deep is set.  /32-level nodes then list nd "deep points" (bits 32..63
- * of each /64 with an h64 record): an uncovered x descends only if it is one
- * of them (c6_node32_coop; other readers use rest_deep, a safe superset).  Typical config-3 packet: root (L2) + h32 slot (L2) +
- * one node (2 lines) + at most one h64 slot. */
+ *        than /64 (an INLINE FULL entry covers [lo, hi] of the low 64 bits).
+ * entry: tag << 30 | payload, tag COVER6_NONE / _FULL / _DEEP (root, b24:
+ * payload = the next level's block; b32: consult h64) / _NODE (payload =
+ * offset in 16-B units into `pool`).  Typical config-3 packet: root, b24,
+ * b32 (768 KiB together, L2-resident) + one 128-B node + rarely one h64
+ * slot. */
 #define COVER6_NONE 0u
 #define COVER6_FULL 1u
 #define COVER6_DEEP 2u
@@ -337,10 +338,11 @@ static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t da
 
 typedef struct cover6 {
 	const uint32_t *root; /* 65536 entries; NULL = empty set */
+	const uint32_t *b24;  /* 256-entry blocks */
+	const uint32_t *b32;  /* 256-entry blocks */
 	const uint32_t *pool; /* 16-B aligned nodes */
-	const uint4 *h32;     /* m32 + 1 slots */
 	const uint4 *h64;     /* (m64 + 1) x 2 uint4 */
-	uint32_t m32, m64;
+	uint32_t m64;
 } cover6;
 
 /* ---- one committed snapshot ---- */

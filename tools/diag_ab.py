@@ -3,11 +3,12 @@ product library: these builds drop work and give wrong counters).
 
     python tools/diag_ab.py build            # in the dev container: tools/_diag/*.so
     python tools/diag_ab.py run [variants]   # on the GPU box
+    (CGPU_AB_CONFIG = gpu (config 2, default) / pf6 (config 3) / v6)
 
 Each variant is cilium_amd/csrc compiled with extra -D flags into
 tools/_diag/libcgpu_<name>.so; `run` loads each in turn into the Engine
-(cilium_amd._abi's loader is pointed at it), commits the config-2 tables and
-times 10 launches of the 64M-tuple batch with HIP events."""
+(cilium_amd._abi's loader is pointed at it), commits the workload's tables and
+times 10 launches of its 64M-tuple batch with HIP events.""" 
 import ctypes as C
 import json
 import os
@@ -45,27 +46,49 @@ def load(name):
     _abi._lib = L
 
 
-def run(names):
+def _workload(conf):
+    """(engine factory, launch fn, n) for CGPU_AB_CONFIG = gpu / pf6 / v6."""
     import torch
     from cilium_amd import synth
-    T = synth.make_tables(**synth.CONFIGS["gpu"])
-    t = synth.make_tuples(T, synth.CONFIGS["gpu"]["n_tuples"])
-    d = synth.to_device(t)
-    n = len(t["saddr"])
+    from cilium_amd.engine import Engine
+    if conf == "pf6":
+        P = synth.make_prefilter6(**synth.PF6_CONFIG)
+        n = synth.CONFIGS["gpu"]["n_tuples"]
+        d = synth.packets6_to_device(synth.make_packets6(P, n), "cuda")
+        v = torch.empty(n, dtype=torch.uint8, device="cuda")
+
+        def make():
+            e = Engine(device=0, **P.engine_config())
+            synth.load_prefilter6(e, P)
+            return e
+        return make, lambda e: e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=v), n
+    v6 = conf == "v6"
+    T = (synth.make_tables6 if v6 else synth.make_tables)(**synth.CONFIGS[conf])
+    n = synth.CONFIGS[conf]["n_tuples"]
+    d = synth.to_device((synth.make_tuples6 if v6 else synth.make_tuples)(T, n))
     out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
            "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
-    for name in names:
-        load(name)
-        from cilium_amd.engine import Engine
+
+    def make():
         e = Engine(device=0, **T.engine_config())
         synth.load_engine(e, T)
+        return e
+    return make, lambda e: (e.classify_v6 if v6 else e.classify_v4)(d, out=out), n
+
+
+def run(names):
+    import torch
+    make, launch, n = _workload(os.environ.get("CGPU_AB_CONFIG", "gpu"))
+    for name in names:
+        load(name)
+        e = make()
         e.commit()
         for _ in range(3):
-            e.classify_v4(d, out=out)
+            launch(e)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
         for a, b in ev:
             a.record()
-            e.classify_v4(d, out=out)
+            launch(e)
             b.record()
         torch.cuda.synchronize()
         ms = sorted(a.elapsed_time(b) for a, b in ev)
