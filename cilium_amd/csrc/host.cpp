@@ -2707,14 +2707,25 @@ static int commit_ep(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	Set4Build ep4;
 	Set16Build ep6;
 	build_set4(e4, ep4);
-	build_set16(e6, ep6);
+	build_set16(e6, ep6, true); /* bucket = pfx6_hash(raw words, 0) */
+	/* the v6 endpoint bloom filter (tables.h ep6_bloom): ~12 bits per key */
+	const uint32_t nw = (uint32_t)std::min<uint64_t>(
+		EP6_BLOOM_MAX_WORDS, next_pow2(std::max<uint64_t>(64, e6.size() * 12 / 32 + 1)));
+	std::vector<uint32_t> bloom(nw, 0);
+	for (auto &k : e6) {
+		const uint32_t h = pfx6_hash(k[0], k[1], k[2], k[3], 0);
+		bloom[v6_bloom_word(h, nw - 1)] |= v6_bloom_bits(h);
+	}
 	Arena ar;
 	const size_t o4 = ar.add(ep4.slots.data(), ep4.slots.size() * sizeof(set4_slot));
 	const size_t o6 = ar.add(ep6.slots.data(), ep6.slots.size() * sizeof(set16_slot));
+	const size_t ob = ar.add(bloom.data(), bloom.size() * 4);
 	if (int r = upload(c, ar, buf))
 		return r;
 	s.ep4 = addr_set4{at<set4_slot>(buf, o4), ep4.mask, ep4.max_probe};
 	s.ep6 = addr_set16{at<set16_slot>(buf, o6), ep6.mask, ep6.max_probe};
+	s.ep6_bloom = at<uint32_t>(buf, ob);
+	s.ep6_bloom_mask = nw - 1;
 	c->b.sum[G_EP] = sum;
 	return 0;
 }

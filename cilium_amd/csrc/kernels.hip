@@ -1936,9 +1936,9 @@ __device__ __forceinline__ void c6_node32_coop(const uint32_t *pool, const uint3
 }
 
 /* set16_has whose first bucket is already loaded (tag 0: exact keys) */
-__device__ __forceinline__ bool set16_has_first(const addr_set16 &t, const uint4 (&first)[4], uint32_t b, uint4 key)
+__device__ __forceinline__ bool set16_has_first(const addr_set16 &t, uint4 k0, uint4 m0, uint4 k1, uint4 m1,
+						uint32_t b, uint4 key)
 {
-	uint4 k0 = first[0], m0 = first[1], k1 = first[2], m1 = first[3];
 	bool res = false, done = false;
 	for (uint32_t p = 0; !done;) {
 		if (!(m0.x & 1u)) {
@@ -2039,6 +2039,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 {
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
+	extern __shared__ uint32_t lbloom[]; /* the endpoint bloom filter */
+	for (uint32_t k = threadIdx.x; k <= s.ep6_bloom_mask; k += 256)
+		lbloom[k] = s.ep6_bloom[k];
+	__syncthreads();
 	const uint64_t T = (uint64_t)gridDim.x * 256;
 	const uint64_t lane0 = threadIdx.x & 63u; /* the loop runs on the wave's first lane */
 	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x - lane0; g * Q < a.n; g += T) {
@@ -2057,17 +2061,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			act[u] = i0 + u < a.n && f[u] == 0u && s.pf6_enabled;
 		}
 		cover6_any_q<Q>(s.pf6, sa, act, hit);
-		/* check_v6_endpoint: cilium_lxc on daddr (bucket loads for all first) */
-		uint4 bk[Q][4];
+		/* check_v6_endpoint: cilium_lxc on daddr; the LDS bloom filter
+		 * settles most misses, the rest load their first bucket together */
+		uint4 k0[Q], m0[Q], k1[Q], m1[Q];
 		uint32_t b[Q];
+		bool need[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			b[u] = hash16(da[u].x, da[u].y, da[u].z, da[u].w, 0u) & s.ep6.bucket_mask;
-			const bool need = i0 + u < a.n && f[u] == 0u && !hit[u];
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				bk[u][k] = need ? reinterpret_cast<const uint4 *>(s.ep6.slots)[(size_t)b[u] * 4u + k]
-						: make_uint4(0, 0, 0, 0);
+			const uint32_t h = pfx6_hash(da[u].x, da[u].y, da[u].z, da[u].w, 0u);
+			const uint32_t bits = v6_bloom_bits(h);
+			b[u] = h & s.ep6.bucket_mask;
+			need[u] = i0 + u < a.n && f[u] == 0u && !hit[u] &&
+				  (lbloom[v6_bloom_word(h, s.ep6_bloom_mask)] & bits) == bits;
+			const uint4 *p = reinterpret_cast<const uint4 *>(s.ep6.slots) + (size_t)b[u] * 4u;
+			const uint4 z = make_uint4(0, 0, 0, 0);
+			k0[u] = need[u] ? p[0] : z;
+			m0[u] = need[u] ? p[1] : z;
+			k1[u] = need[u] ? p[2] : z;
+			m1[u] = need[u] ? p[3] : z;
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
@@ -2076,10 +2087,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			uint8_t v;
 			if (f[u] == 2u) {
 				v = XDP_PASS;
-			} else if (f[u] != 0u || hit[u]) {
+			} else if (f[u] != 0u || hit[u] || !need[u]) {
 				v = XDP_DROP;
 			} else {
-				v = set16_has_first(s.ep6, bk[u], b[u], da[u]) ? XDP_PASS : XDP_DROP;
+				v = set16_has_first(s.ep6, k0[u], m0[u], k1[u], m1[u], b[u], da[u]) ? XDP_PASS : XDP_DROP;
 			}
 			a.verdict[i0 + u] = v;
 		}
@@ -2301,7 +2312,8 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 	/* four packets per lane, octet-cooperative node reads.  A/B on config 3
 	 * (Gpps, round 1): Q=4 coop 24.8; Q=4 per-lane nodes 21.1; Q=4 fitted
 	 * to 5 waves/SIMD 20.4; Q=2 20.9; Q=1 20.5. */
-	hipLaunchKernelGGL((k_prefilter_v6_q<4, 1>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), 0, st, s, a);
+	const size_t lds = (size_t)(s.ep6_bloom_mask + 1u) * 4u;
+	hipLaunchKernelGGL((k_prefilter_v6_q<4, 1>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), lds, st, s, a);
 	return hipGetLastError();
 }
 

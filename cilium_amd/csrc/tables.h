@@ -242,6 +242,7 @@ typedef struct v6_lpm {
 } v6_lpm;
 
 #define V6_BLOOM_MAX_WORDS 16384u /* 64 KiB: staged in LDS by the x4 kernel */
+#define EP6_BLOOM_MAX_WORDS 8192u /* 32 KiB: staged in LDS by k_prefilter_v6_q */
 
 static inline __host__ __device__ uint32_t v6_bloom_word(uint32_t h, uint32_t mask) { return (h >> 16) & mask; }
 static inline __host__ __device__ uint32_t v6_bloom_bits(uint32_t h)
@@ -352,7 +353,12 @@ typedef struct cgpu_snapshot {
 	pol_groups pg;   /* per (ep, identity, dir): probe 2 + probe 1 filter */
 	lpm16c pf4c;     /* any-match: dyn4 (if enabled) + fix4 /32; leaves 0 / 1 */
 	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
-	addr_set16 ep6;  /* cilium_lxc IPv6 keys */
+	addr_set16 ep6;  /* cilium_lxc IPv6 keys (bucket: pfx6_hash(raw words, 0)) */
+	/* bloom filter over ep6 keys (v6_bloom_word / v6_bloom_bits of the same
+	 * hash), staged in LDS by k_prefilter_v6_q: a daddr it rules out is no
+	 * endpoint without a bucket read */
+	const uint32_t *ep6_bloom;
+	uint32_t ep6_bloom_mask;
 	cover6 pf6;      /* any-match: dyn6 (if enabled) + fix6 /128 */
 	v6_lpm ipc6;     /* ipcache, IPv6 lookups */
 	uint32_t pf4_enabled; /* CIDR4_FILTER */
