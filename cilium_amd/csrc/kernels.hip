@@ -332,11 +332,10 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
 				const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[j] * 4u;
-				const uint4 z = make_uint4(0, 0, 0, 0);
-				k0[j] = L[j] ? p[0] : z;
-				m0[j] = L[j] ? p[1] : z;
-				k1[j] = L[j] ? p[2] : z;
-				m1[j] = L[j] ? p[3] : z;
+				k0[j] = L[j] ? p[0] : make_uint4(0, 0, 0, 0);
+				m0[j] = L[j] ? p[1] : make_uint4(0, 0, 0, 0);
+				k1[j] = L[j] ? p[2] : make_uint4(0, 0, 0, 0);
+				m1[j] = L[j] ? p[3] : make_uint4(0, 0, 0, 0);
 			}
 			/* longest first: the first hit is the longest match */
 #pragma unroll
@@ -1006,11 +1005,10 @@ __device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *blo
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[u] * 4u;
-			const uint4 z = make_uint4(0, 0, 0, 0);
-			k0[u] = L[u] ? p[0] : z;
-			m0[u] = L[u] ? p[1] : z;
-			k1[u] = L[u] ? p[2] : z;
-			m1[u] = L[u] ? p[3] : z;
+			k0[u] = L[u] ? p[0] : make_uint4(0, 0, 0, 0);
+			m0[u] = L[u] ? p[1] : make_uint4(0, 0, 0, 0);
+			k1[u] = L[u] ? p[2] : make_uint4(0, 0, 0, 0);
+			m1[u] = L[u] ? p[3] : make_uint4(0, 0, 0, 0);
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
@@ -2074,11 +2072,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			need[u] = i0 + u < a.n && f[u] == 0u && !hit[u] &&
 				  (lbloom[v6_bloom_word(h, s.ep6_bloom_mask)] & bits) == bits;
 			const uint4 *p = reinterpret_cast<const uint4 *>(s.ep6.slots) + (size_t)b[u] * 4u;
-			const uint4 z = make_uint4(0, 0, 0, 0);
-			k0[u] = need[u] ? p[0] : z;
-			m0[u] = need[u] ? p[1] : z;
-			k1[u] = need[u] ? p[2] : z;
-			m1[u] = need[u] ? p[3] : z;
+			k0[u] = need[u] ? p[0] : make_uint4(0, 0, 0, 0);
+			m0[u] = need[u] ? p[1] : make_uint4(0, 0, 0, 0);
+			k1[u] = need[u] ? p[2] : make_uint4(0, 0, 0, 0);
+			m1[u] = need[u] ? p[3] : make_uint4(0, 0, 0, 0);
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
