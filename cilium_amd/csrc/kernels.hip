@@ -2042,21 +2042,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 		lbloom[k] = s.ep6_bloom[k];
 	__syncthreads();
 	const uint64_t T = (uint64_t)gridDim.x * 256;
-	const uint64_t lane0 = threadIdx.x & 63u; /* the loop runs on the wave's first lane */
-	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x - lane0; g * Q < a.n; g += T) {
-		const uint64_t i0 = (g + lane0) * Q;
+	const uint64_t lane = threadIdx.x & 63u;
+	/* wave-step g covers packets [g * Q, g * Q + 64 Q): packet u of a lane
+	 * is g * Q + 64 u + lane, so each column load of a wave reads 64
+	 * consecutive packets (1 KiB of addresses, 64 B of flags) */
+	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x - lane; g * Q < a.n; g += T) {
 		uint4 sa[Q], da[Q];
 		uint32_t f[Q];
+		uint64_t ix[Q];
 		bool act[Q], hit[Q];
 #pragma unroll
+		for (int u = 0; u < Q; u++)
+			ix[u] = g * Q + 64u * u + lane;
+#pragma unroll
 		for (int u = 0; u < Q; u++) {
-			const uint64_t i = i0 + u < a.n ? i0 + u : a.n - 1;
+			const uint64_t i = ix[u] < a.n ? ix[u] : a.n - 1;
 			const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(sa16 + i));
 			const v4u_t y = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(da16 + i));
 			sa[u] = make_uint4(x.x, x.y, x.z, x.w);
 			da[u] = make_uint4(y.x, y.y, y.z, y.w);
 			f[u] = a.flags[i];
-			act[u] = i0 + u < a.n && f[u] == 0u && s.pf6_enabled;
+			act[u] = ix[u] < a.n && f[u] == 0u && s.pf6_enabled;
 		}
 		cover6_any_q<Q>(s.pf6, sa, act, hit);
 		/* check_v6_endpoint: cilium_lxc on daddr; the LDS bloom filter
@@ -2069,7 +2075,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			const uint32_t h = pfx6_hash(da[u].x, da[u].y, da[u].z, da[u].w, 0u);
 			const uint32_t bits = v6_bloom_bits(h);
 			b[u] = h & s.ep6.bucket_mask;
-			need[u] = i0 + u < a.n && f[u] == 0u && !hit[u] &&
+			need[u] = ix[u] < a.n && f[u] == 0u && !hit[u] &&
 				  (lbloom[v6_bloom_word(h, s.ep6_bloom_mask)] & bits) == bits;
 			const uint4 *p = reinterpret_cast<const uint4 *>(s.ep6.slots) + (size_t)b[u] * 4u;
 			k0[u] = need[u] ? p[0] : make_uint4(0, 0, 0, 0);
@@ -2079,7 +2085,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			if (i0 + u >= a.n)
+			if (ix[u] >= a.n)
 				continue;
 			uint8_t v;
 			if (f[u] == 2u) {
@@ -2089,7 +2095,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			} else {
 				v = set16_has_first(s.ep6, k0[u], m0[u], k1[u], m1[u], b[u], da[u]) ? XDP_PASS : XDP_DROP;
 			}
-			a.verdict[i0 + u] = v;
+			a.verdict[ix[u]] = v;
 		}
 	}
 }
