@@ -763,6 +763,7 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 /* ---- IPv6 any-match cover (tables.h cover6) ---- */
 struct Cover6Build {
 	std::vector<uint32_t> root, b24, b32, pool;
+	std::vector<uint16_t> root16; /* empty: not representable */
 	std::vector<std::array<uint32_t, 8>> h64;
 	uint32_t m64 = 0;
 	bool any = false;
@@ -1022,6 +1023,15 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 	/* 8 zero units past the last node: the octet load of a node reads
 	 * 128 B from its start whatever its length */
 	b.pool.insert(b.pool.end(), 32, 0u);
+	b.root16.clear();
+	if (b.b24.size() / 256 <= 0xFFFDu) {
+		b.root16.resize(65536);
+		for (uint32_t x = 0; x < 65536; x++) {
+			const uint32_t e = b.root[x];
+			b.root16[x] = (uint16_t)((e >> 30) == COVER6_DEEP ? 2u + (e & 0x3FFFFFFFu)
+									  : ((e >> 30) == COVER6_FULL ? 1u : 0u));
+		}
+	}
 }
 
 /* prefilter v6 any-match set (bpf_xdp.c:132-156): dyn6 (if
@@ -2653,7 +2663,7 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	Cover6Build pf6;
 	build_cover6(pf6_candidates(in.pf), pf6);
 	Arena ar;
-	size_t o4[4] = {0, 0, 0, 0}, o6[5] = {0, 0, 0, 0, 0};
+	size_t o4[4] = {0, 0, 0, 0}, o6[6] = {0, 0, 0, 0, 0, 0};
 	if (have4) {
 		o4[0] = ar.add(lc.x16.data(), lc.x16.size() * 4);
 		o4[1] = ar.add(lc.d16.data(), lc.d16.size() * 4);
@@ -2666,6 +2676,7 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		o6[2] = ar.add(pf6.b24.data(), pf6.b24.size() * 4);
 		o6[3] = ar.add(pf6.b32.data(), pf6.b32.size() * 4);
 		o6[4] = ar.add(pf6.h64.data(), pf6.h64.size() * 32);
+		o6[5] = ar.add(pf6.root16.data(), pf6.root16.size() * 2);
 	}
 	if (int r = upload(c, ar, buf))
 		return r;
@@ -2675,8 +2686,9 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 				at<uint32_t>(buf, o4[3]), (uint32_t)lc.nodes.size(), (uint32_t)lc.dict.size()};
 	s.pf6 = cover6{};
 	if (pf6.any)
-		s.pf6 = cover6{at<uint32_t>(buf, o6[0]), at<uint32_t>(buf, o6[2]), at<uint32_t>(buf, o6[3]),
-			       at<uint32_t>(buf, o6[1]), at<uint4>(buf, o6[4]), pf6.m64};
+		s.pf6 = cover6{at<uint32_t>(buf, o6[0]), pf6.root16.empty() ? nullptr : at<uint16_t>(buf, o6[5]),
+			       at<uint32_t>(buf, o6[2]), at<uint32_t>(buf, o6[3]), at<uint32_t>(buf, o6[1]),
+			       at<uint4>(buf, o6[4]), pf6.m64};
 	uint64_t sum = 0;
 	for (auto &k : in.pf.dyn4k) sum += fnv(7, &k, 8);
 	for (auto &k : in.pf.dyn6k) sum += fnv(11, &k, 20);

@@ -1961,8 +1961,10 @@ __device__ __forceinline__ bool set16_has_first(const addr_set16 &t, uint4 k0, u
 	return res;
 }
 
+/* lroot: the root as u16 entries in LDS (cover6.root16), or NULL */
 template <int Q>
-__device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q], const bool (&act)[Q], bool (&hit)[Q])
+__device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint16_t *lroot, const uint4 (&a)[Q],
+					     const bool (&act)[Q], bool (&hit)[Q])
 {
 	uint32_t w0[Q], w1[Q], w2[Q], w3[Q], e[Q], tag[Q];
 #pragma unroll
@@ -1971,7 +1973,15 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 		w1[u] = bswap32(a[u].y);
 		w2[u] = bswap32(a[u].z);
 		w3[u] = bswap32(a[u].w);
-		e[u] = act[u] && t.root ? t.root[w0[u] >> 16] : 0u;
+		e[u] = 0u;
+		if (act[u] && t.root) {
+			if (lroot) {
+				const uint32_t r = lroot[w0[u] >> 16];
+				e[u] = r >= 2u ? (COVER6_DEEP << 30) | (r - 2u) : (r ? COVER6_FULL << 30 : 0u);
+			} else {
+				e[u] = t.root[w0[u] >> 16];
+			}
+		}
 	}
 	/* the two direct-indexed levels: bits 16..23, then 24..31 */
 #pragma unroll
@@ -2031,22 +2041,26 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint4 (&a)[Q
 /* W: minimum resident waves per SIMD the registers are fitted to.  The /32
  * node reads are octet-cooperative (c6_node32_coop), so the loop trip count
  * is uniform per wave; lanes past the batch end carry inactive packets. */
-template <int Q, int W = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_prefilter_v6_q(cgpu_snapshot s,
-												     prefilter_args a)
+template <int Q, int NT>
+__global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a)
 {
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
-	extern __shared__ uint32_t lbloom[]; /* the endpoint bloom filter */
-	for (uint32_t k = threadIdx.x; k <= s.ep6_bloom_mask; k += 256)
+	/* LDS: the endpoint bloom filter, then the cover root (u16) */
+	extern __shared__ uint32_t lbloom[];
+	uint16_t *lroot = s.pf6.root16 ? reinterpret_cast<uint16_t *>(lbloom + s.ep6_bloom_mask + 1u) : nullptr;
+	for (uint32_t k = threadIdx.x; k <= s.ep6_bloom_mask; k += NT)
 		lbloom[k] = s.ep6_bloom[k];
+	if (lroot)
+		for (uint32_t k = threadIdx.x; k < 65536u / 8u; k += NT)
+			reinterpret_cast<uint4 *>(lroot)[k] = reinterpret_cast<const uint4 *>(s.pf6.root16)[k];
 	__syncthreads();
-	const uint64_t T = (uint64_t)gridDim.x * 256;
+	const uint64_t T = (uint64_t)gridDim.x * NT;
 	const uint64_t lane = threadIdx.x & 63u;
 	/* wave-step g covers packets [g * Q, g * Q + 64 Q): packet u of a lane
 	 * is g * Q + 64 u + lane, so each column load of a wave reads 64
 	 * consecutive packets (1 KiB of addresses, 64 B of flags) */
-	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x - lane; g * Q < a.n; g += T) {
+	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x - lane; g * Q < a.n; g += T) {
 		uint4 sa[Q], da[Q];
 		uint32_t f[Q];
 		uint64_t ix[Q];
@@ -2064,7 +2078,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 			f[u] = a.flags[i];
 			act[u] = ix[u] < a.n && f[u] == 0u && s.pf6_enabled;
 		}
-		cover6_any_q<Q>(s.pf6, sa, act, hit);
+		cover6_any_q<Q>(s.pf6, lroot, sa, act, hit);
 		/* check_v6_endpoint: cilium_lxc on daddr; the LDS bloom filter
 		 * settles most misses, the rest load their first bucket together */
 		uint4 k0[Q], m0[Q], k1[Q], m1[Q];
@@ -2312,11 +2326,16 @@ hipError_t launch_prefilter_v4(const cgpu_snapshot &s, const prefilter_args &a, 
 
 hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, hipStream_t st)
 {
-	/* four packets per lane, octet-cooperative node reads.  A/B on config 3
-	 * (Gpps, round 1): Q=4 coop 24.8; Q=4 per-lane nodes 21.1; Q=4 fitted
-	 * to 5 waves/SIMD 20.4; Q=2 20.9; Q=1 20.5. */
-	const size_t lds = (size_t)(s.ep6_bloom_mask + 1u) * 4u;
-	hipLaunchKernelGGL((k_prefilter_v6_q<4, 1>), dim3(grid_for((a.n + 3) / 4)), dim3(BLOCK), lds, st, s, a);
+	/* four packets per lane, octet-cooperative node reads, a resident grid
+	 * of 1024-thread workgroups (the LDS root is loaded once per
+	 * workgroup).  A/B on config 3 (Gpps, round 1): Q=4 coop 24.8; Q=4
+	 * per-lane nodes 21.1; Q=4 fitted to 5 waves/SIMD 20.4; Q=2 20.9. */
+	constexpr int NT = 1024;
+	const size_t lds = (size_t)(s.ep6_bloom_mask + 1u) * 4u + (s.pf6.root16 ? 65536u * 2u : 0u);
+	const void *kern = (const void *)k_prefilter_v6_q<4, NT>;
+	const unsigned res = resident_blocks(kern, NT, lds);
+	const unsigned g = (unsigned)std::min<uint64_t>((a.n + 4 * NT - 1) / (4 * NT), res);
+	hipLaunchKernelGGL((k_prefilter_v6_q<4, NT>), dim3(g ? g : 1), dim3(NT), lds, st, s, a);
 	return hipGetLastError();
 }
 

@@ -339,6 +339,9 @@ static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t da
 
 typedef struct cover6 {
 	const uint32_t *root; /* 65536 entries; NULL = empty set */
+	/* the root as 65536 u16 (0 NONE, 1 FULL, 2 + b24 block: DEEP), staged
+	 * in LDS by k_prefilter_v6_q; NULL when the b24 blocks do not fit */
+	const uint16_t *root16;
 	const uint32_t *b24;  /* 256-entry blocks */
 	const uint32_t *b32;  /* 256-entry blocks */
 	const uint32_t *pool; /* 16-B aligned nodes */
