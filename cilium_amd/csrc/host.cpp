@@ -763,7 +763,8 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 /* ---- IPv6 any-match cover (tables.h cover6) ---- */
 struct Cover6Build {
 	std::vector<uint32_t> root, b24, b32, pool;
-	std::vector<uint16_t> root16; /* empty: not representable */
+	std::vector<uint16_t> root16, b24_16; /* empty: not representable */
+	std::vector<uint32_t> rbits;
 	std::vector<std::array<uint32_t, 8>> h64;
 	uint32_t m64 = 0;
 	bool any = false;
@@ -1023,14 +1024,38 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 	/* 8 zero units past the last node: the octet load of a node reads
 	 * 128 B from its start whatever its length */
 	b.pool.insert(b.pool.end(), 32, 0u);
+	/* the LDS-staged forms (tables.h cover6) */
+	auto u16e = [](uint32_t e) {
+		return (uint16_t)((e >> 30) == COVER6_DEEP ? 2u + (e & 0x3FFFFFFFu)
+							   : ((e >> 30) == COVER6_FULL ? 1u : 0u));
+	};
 	b.root16.clear();
+	b.rbits.clear();
+	b.b24_16.clear();
 	if (b.b24.size() / 256 <= 0xFFFDu) {
 		b.root16.resize(65536);
-		for (uint32_t x = 0; x < 65536; x++) {
-			const uint32_t e = b.root[x];
-			b.root16[x] = (uint16_t)((e >> 30) == COVER6_DEEP ? 2u + (e & 0x3FFFFFFFu)
-									  : ((e >> 30) == COVER6_FULL ? 1u : 0u));
+		for (uint32_t x = 0; x < 65536; x++)
+			b.root16[x] = u16e(b.root[x]);
+	}
+	if (b.b32.size() / 256 <= 0xFFFDu && b.b24.size() / 256 <= 0xFFFFu) {
+		b.rbits.assign(COVER6_RBITS_WORDS, 0u);
+		uint32_t rank = 0;
+		for (uint32_t w = 0; w < 2048; w++) {
+			b.rbits[4096 + w / 2] |= rank << (16 * (w & 1));
+			for (uint32_t k = 0; k < 32; k++) {
+				const uint32_t e = b.root[32 * w + k];
+				if ((e >> 30) == COVER6_DEEP) {
+					b.rbits[w] |= 1u << k;
+					rank++;
+				} else if ((e >> 30) == COVER6_FULL) {
+					b.rbits[2048 + w] |= 1u << k;
+				}
+			}
 		}
+		/* b24 blocks were appended in root order: block = rank */
+		b.b24_16.resize(b.b24.size());
+		for (size_t x = 0; x < b.b24.size(); x++)
+			b.b24_16[x] = u16e(b.b24[x]);
 	}
 }
 
@@ -2663,7 +2688,7 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	Cover6Build pf6;
 	build_cover6(pf6_candidates(in.pf), pf6);
 	Arena ar;
-	size_t o4[4] = {0, 0, 0, 0}, o6[6] = {0, 0, 0, 0, 0, 0};
+	size_t o4[4] = {0, 0, 0, 0}, o6[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	if (have4) {
 		o4[0] = ar.add(lc.x16.data(), lc.x16.size() * 4);
 		o4[1] = ar.add(lc.d16.data(), lc.d16.size() * 4);
@@ -2677,6 +2702,8 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		o6[3] = ar.add(pf6.b32.data(), pf6.b32.size() * 4);
 		o6[4] = ar.add(pf6.h64.data(), pf6.h64.size() * 32);
 		o6[5] = ar.add(pf6.root16.data(), pf6.root16.size() * 2);
+		o6[6] = ar.add(pf6.rbits.data(), pf6.rbits.size() * 4);
+		o6[7] = ar.add(pf6.b24_16.data(), pf6.b24_16.size() * 2);
 	}
 	if (int r = upload(c, ar, buf))
 		return r;
@@ -2686,7 +2713,11 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 				at<uint32_t>(buf, o4[3]), (uint32_t)lc.nodes.size(), (uint32_t)lc.dict.size()};
 	s.pf6 = cover6{};
 	if (pf6.any)
-		s.pf6 = cover6{at<uint32_t>(buf, o6[0]), pf6.root16.empty() ? nullptr : at<uint16_t>(buf, o6[5]),
+		s.pf6 = cover6{at<uint32_t>(buf, o6[0]),
+			       pf6.root16.empty() ? nullptr : at<uint16_t>(buf, o6[5]),
+			       pf6.rbits.empty() ? nullptr : at<uint32_t>(buf, o6[6]),
+			       pf6.rbits.empty() ? nullptr : at<uint16_t>(buf, o6[7]),
+			       (uint32_t)(pf6.b24.size() / 256),
 			       at<uint32_t>(buf, o6[2]), at<uint32_t>(buf, o6[3]), at<uint32_t>(buf, o6[1]),
 			       at<uint4>(buf, o6[4]), pf6.m64};
 	uint64_t sum = 0;

@@ -1961,9 +1961,16 @@ __device__ __forceinline__ bool set16_has_first(const addr_set16 &t, uint4 k0, u
 	return res;
 }
 
-/* lroot: the root as u16 entries in LDS (cover6.root16), or NULL */
+/* a u16 LDS entry (tables.h cover6 root16 / b24_16) as a cover6 entry */
+__device__ __forceinline__ uint32_t c6_from16(uint32_t r)
+{
+	return r >= 2u ? (COVER6_DEEP << 30) | (r - 2u) : (r ? COVER6_FULL << 30 : 0u);
+}
+
+/* mode (k_prefilter_v6_q): 0 the root in global memory; 1 lds = root16;
+ * 2 lds = rbits then the b24_16 blocks (root and b24 resolved in LDS) */
 template <int Q>
-__device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint16_t *lroot, const uint4 (&a)[Q],
+__device__ __forceinline__ void cover6_any_q(const cover6 &t, int mode, const uint32_t *lds, const uint4 (&a)[Q],
 					     const bool (&act)[Q], bool (&hit)[Q])
 {
 	uint32_t w0[Q], w1[Q], w2[Q], w3[Q], e[Q], tag[Q];
@@ -1974,20 +1981,34 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint16_t *lr
 		w2[u] = bswap32(a[u].z);
 		w3[u] = bswap32(a[u].w);
 		e[u] = 0u;
-		if (act[u] && t.root) {
-			if (lroot) {
-				const uint32_t r = lroot[w0[u] >> 16];
-				e[u] = r >= 2u ? (COVER6_DEEP << 30) | (r - 2u) : (r ? COVER6_FULL << 30 : 0u);
-			} else {
-				e[u] = t.root[w0[u] >> 16];
+		if (!act[u] || !t.root)
+			continue;
+		const uint32_t x = w0[u] >> 16;
+		if (mode == 2) {
+			/* root bitmaps and rank, then the /16's b24 block: all LDS */
+			const uint32_t deep = lds[x >> 5], full = lds[2048u + (x >> 5)];
+			const uint32_t bit = 1u << (x & 31u);
+			if (full & bit) {
+				e[u] = COVER6_FULL << 30;
+			} else if (deep & bit) {
+				const uint32_t rank = reinterpret_cast<const uint16_t *>(lds + 4096u)[x >> 5] +
+						      __popc(deep & (bit - 1u));
+				const uint16_t *b24 = reinterpret_cast<const uint16_t *>(lds + COVER6_RBITS_WORDS);
+				e[u] = c6_from16(b24[rank * 256u + ((w0[u] >> 8) & 0xFFu)]);
 			}
+		} else if (mode == 1) {
+			e[u] = c6_from16(reinterpret_cast<const uint16_t *>(lds)[x]);
+		} else {
+			e[u] = t.root[x];
 		}
 	}
-	/* the two direct-indexed levels: bits 16..23, then 24..31 */
+	/* the direct-indexed levels: bits 16..23 (unless resolved in LDS), 24..31 */
+	if (mode != 2) {
 #pragma unroll
-	for (int u = 0; u < Q; u++)
-		if ((e[u] >> 30) == COVER6_DEEP)
-			e[u] = t.b24[(e[u] & 0x3FFFFFFFu) * 256u + ((w0[u] >> 8) & 0xFFu)];
+		for (int u = 0; u < Q; u++)
+			if ((e[u] >> 30) == COVER6_DEEP)
+				e[u] = t.b24[(e[u] & 0x3FFFFFFFu) * 256u + ((w0[u] >> 8) & 0xFFu)];
+	}
 #pragma unroll
 	for (int u = 0; u < Q; u++)
 		if ((e[u] >> 30) == COVER6_DEEP)
@@ -2042,18 +2063,25 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint16_t *lr
  * node reads are octet-cooperative (c6_node32_coop), so the loop trip count
  * is uniform per wave; lanes past the batch end carry inactive packets. */
 template <int Q, int NT>
-__global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a)
+__global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a, int mode)
 {
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
-	/* LDS: the endpoint bloom filter, then the cover root (u16) */
-	extern __shared__ uint32_t lbloom[];
-	uint16_t *lroot = s.pf6.root16 ? reinterpret_cast<uint16_t *>(lbloom + s.ep6_bloom_mask + 1u) : nullptr;
+	/* LDS: the endpoint bloom filter, then the cover's staged levels (mode) */
+	extern __shared__ __attribute__((aligned(16))) uint32_t lbloom[];
+	uint32_t *lc = lbloom + s.ep6_bloom_mask + 1u; /* 16-B aligned: >= 64 words */
 	for (uint32_t k = threadIdx.x; k <= s.ep6_bloom_mask; k += NT)
 		lbloom[k] = s.ep6_bloom[k];
-	if (lroot)
-		for (uint32_t k = threadIdx.x; k < 65536u / 8u; k += NT)
-			reinterpret_cast<uint4 *>(lroot)[k] = reinterpret_cast<const uint4 *>(s.pf6.root16)[k];
+	if (mode == 1) {
+		for (uint32_t k = threadIdx.x; k < 65536u * 2u / 16u; k += NT)
+			reinterpret_cast<uint4 *>(lc)[k] = reinterpret_cast<const uint4 *>(s.pf6.root16)[k];
+	} else if (mode == 2) {
+		for (uint32_t k = threadIdx.x; k < COVER6_RBITS_WORDS / 4u; k += NT)
+			reinterpret_cast<uint4 *>(lc)[k] = reinterpret_cast<const uint4 *>(s.pf6.rbits)[k];
+		for (uint32_t k = threadIdx.x; k < s.pf6.n_b24 * 256u * 2u / 16u; k += NT)
+			reinterpret_cast<uint4 *>(lc + COVER6_RBITS_WORDS)[k] =
+				reinterpret_cast<const uint4 *>(s.pf6.b24_16)[k];
+	}
 	__syncthreads();
 	const uint64_t T = (uint64_t)gridDim.x * NT;
 	const uint64_t lane = threadIdx.x & 63u;
@@ -2078,7 +2106,7 @@ __global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilte
 			f[u] = a.flags[i];
 			act[u] = ix[u] < a.n && f[u] == 0u && s.pf6_enabled;
 		}
-		cover6_any_q<Q>(s.pf6, lroot, sa, act, hit);
+		cover6_any_q<Q>(s.pf6, mode, lc, sa, act, hit);
 		/* check_v6_endpoint: cilium_lxc on daddr; the LDS bloom filter
 		 * settles most misses, the rest load their first bucket together */
 		uint4 k0[Q], m0[Q], k1[Q], m1[Q];
@@ -2331,11 +2359,27 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 	 * workgroup).  A/B on config 3 (Gpps, round 1): Q=4 coop 24.8; Q=4
 	 * per-lane nodes 21.1; Q=4 fitted to 5 waves/SIMD 20.4; Q=2 20.9. */
 	constexpr int NT = 1024;
-	const size_t lds = (size_t)(s.ep6_bloom_mask + 1u) * 4u + (s.pf6.root16 ? 65536u * 2u : 0u);
+	constexpr size_t LDS_MAX = 160u * 1024u;
+	/* stage the deepest cover levels that fit next to the bloom filter */
+	const size_t bloom = (size_t)(s.ep6_bloom_mask + 1u) * 4u;
+	const size_t l2 = (size_t)COVER6_RBITS_WORDS * 4u + (size_t)s.pf6.n_b24 * 512u;
+	/* CGPU_PF6_LDS caps the mode (every mode computes the same verdicts;
+	 * tests/test_gpu_parity.py runs each) */
+	const char *cap = getenv("CGPU_PF6_LDS");
+	const int max_mode = cap ? atoi(cap) : 2;
+	int mode = 0;
+	size_t lds = bloom;
+	if (max_mode >= 2 && s.pf6.rbits && bloom + l2 <= LDS_MAX) {
+		mode = 2;
+		lds += l2;
+	} else if (max_mode >= 1 && s.pf6.root16 && bloom + 65536u * 2u <= LDS_MAX) {
+		mode = 1;
+		lds += 65536u * 2u;
+	}
 	const void *kern = (const void *)k_prefilter_v6_q<4, NT>;
 	const unsigned res = resident_blocks(kern, NT, lds);
 	const unsigned g = (unsigned)std::min<uint64_t>((a.n + 4 * NT - 1) / (4 * NT), res);
-	hipLaunchKernelGGL((k_prefilter_v6_q<4, NT>), dim3(g ? g : 1), dim3(NT), lds, st, s, a);
+	hipLaunchKernelGGL((k_prefilter_v6_q<4, NT>), dim3(g ? g : 1), dim3(NT), lds, st, s, a, mode);
 	return hipGetLastError();
 }
 

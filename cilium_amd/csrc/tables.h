@@ -336,12 +336,19 @@ static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t da
 #define COVER6_DEEP 2u
 #define COVER6_NODE 3u
 #define COVER6_USED (1u << 16)
+#define COVER6_RBITS_WORDS (2048u * 2u + 1024u) /* DEEP, FULL bitmaps + u16 ranks */
 
 typedef struct cover6 {
 	const uint32_t *root; /* 65536 entries; NULL = empty set */
-	/* the root as 65536 u16 (0 NONE, 1 FULL, 2 + b24 block: DEEP), staged
-	 * in LDS by k_prefilter_v6_q; NULL when the b24 blocks do not fit */
+	/* LDS-staged forms (k_prefilter_v6_q picks the deepest that fits):
+	 * root16: the root as 65536 u16 (0 NONE, 1 FULL, 2 + b24 block);
+	 * rbits + b24_16: the root as bitmaps {DEEP[2048], FULL[2048] words,
+	 * rank[2048] u16 = DEEP bits before word k} and every b24 block as u16
+	 * entries (0 NONE, 1 FULL, 2 + b32 block); NULL when not representable */
 	const uint16_t *root16;
+	const uint32_t *rbits;
+	const uint16_t *b24_16;
+	uint32_t n_b24;
 	const uint32_t *b24;  /* 256-entry blocks */
 	const uint32_t *b32;  /* 256-entry blocks */
 	const uint32_t *pool; /* 16-B aligned nodes */

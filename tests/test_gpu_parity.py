@@ -540,18 +540,21 @@ def test_lpm_shapes_exact(torch_cuda, variant, monkeypatch):
     e.close()
 
 
+@pytest.mark.parametrize("lds_mode", [0, 1, 2])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_prefilter6_cover_shapes(torch_cuda, seed):
+def test_prefilter6_cover_shapes(torch_cuda, seed, lds_mode, monkeypatch):
     """The v6 any-match cover (tables.h cover6) over every prefix-length class
-    and stride boundary: /0../16 (root fill), /17../32 (root node), /33../64
-    (/32 node), /65../128 (/64 node or inline), nested and overlapping
-    prefixes, all-ones boundaries; addresses drawn at and around the edges of
-    every prefix.  Each /16 root holds enough /17../32 prefixes that its node
-    would exceed one line, so its /28../32 prefixes move down to FULL /32
-    records (also over /32s with deeper prefixes) while /17../27 stay in the
-    /16 node.  Bit-exact against the restatement's kernel-like LPM trie."""
+    and stride boundary: /0../16 (root fill), /17../24 (expanded into b24
+    entries), /25../32 (expanded into b32 entries, also over /32s with deeper
+    prefixes), /33../64 (/32 node), /65../128 (/64 node or inline), nested
+    and overlapping prefixes, all-ones boundaries; addresses drawn at and
+    around the edges of every prefix.  Under each LDS staging mode of
+    k_prefilter_v6_q (0: root in HBM, 1: u16 root in LDS, 2: root bitmaps +
+    u16 b24 blocks in LDS).  Bit-exact against the restatement's kernel-like
+    LPM trie."""
     from oracle import Oracle
     torch = torch_cuda
+    monkeypatch.setenv("CGPU_PF6_LDS", str(lds_mode))
     rng = np.random.default_rng(100 + seed)
     roots = rng.integers(0, 256, (6, 2), dtype=np.uint8)
     lens = [0, 1, 8, 15, 16, 17, 20, 27, 28, 29, 30, 31, 32, 33, 40, 48, 63, 64, 65, 80, 96, 112, 127, 128]
