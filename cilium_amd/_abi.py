@@ -134,6 +134,7 @@ PROTOS = {
     "cgpu_ct4_flush": (i32, [vp]),
     "cgpu_classify_v4_ct": (i32, [vp, C.POINTER(TuplesV4Ct), sz, u32, vp, vp, vp, vp, vp]),
     "cgpu_l3_compile": (i32, [vp, vp, vp, vp, u32, vp]),
+    "cgpu_mapstate_sync": (i32, [vp, vp, vp, vp, vp, vp]),
     "cgpu_counter_delta_bytes": (sz, [vp]),
     "cgpu_counter_bind": (i32, [vp, vp, sz]),
     "cgpu_counter_fold": (i32, [vp, vp]),

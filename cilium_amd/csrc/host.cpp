@@ -1680,16 +1680,11 @@ static inline uint64_t pol_key64(const cgpu_policy_key *k)
 	return x;
 }
 
-CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
-				   const cgpu_policy_entry *e, uint64_t flags)
+/* BPF_MAP_UPDATE_ELEM on an endpoint's policy map; caller holds c->mu and
+ * has checked the flags and the endpoint index */
+static int pol_update_locked(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+			     const cgpu_policy_entry *e, uint64_t flags)
 {
-	if (!c || !key || !e)
-		return fail(-EINVAL, "null argument");
-	if (int r = check_flags(flags))
-		return r;
-	if (ep >= c->cfg.max_endpoints)
-		return fail(-EINVAL, "endpoint %u >= max_endpoints %u", ep, c->cfg.max_endpoints);
-	std::lock_guard<std::mutex> g(c->mu);
 	auto &m = c->pol[ep];
 	uint64_t k = pol_key64(key);
 	auto it = m.find(k);
@@ -1732,6 +1727,19 @@ CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_k
 	/* kernel htab replaces the whole value: counters restart from it */
 	c->slot_inits.push_back(SlotInit{slot, e->packets, e->bytes});
 	return 0;
+}
+
+CGPU_EXPORT int cgpu_policy_update(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *key,
+				   const cgpu_policy_entry *e, uint64_t flags)
+{
+	if (!c || !key || !e)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	if (ep >= c->cfg.max_endpoints)
+		return fail(-EINVAL, "endpoint %u >= max_endpoints %u", ep, c->cfg.max_endpoints);
+	std::lock_guard<std::mutex> g(c->mu);
+	return pol_update_locked(c, ep, key, e, flags);
 }
 
 static void pol_erase(cgpu_ctx *c, uint32_t ep, std::map<uint64_t, PolEntry> &m,
@@ -3844,11 +3852,13 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 /* ======================================================================= */
 /* L3 MapState compilation                               */
 /* ======================================================================= */
-CGPU_EXPORT int cgpu_l3_compile(cgpu_ctx *c, const cgpu_l3_program *p, const cgpu_label_sets *eps,
-				const cgpu_label_sets *ids, uint32_t flags, uint8_t *allow_out)
+/* validate a program + label sets (+ a MapState spec), upload them, run
+ * the selector kernels and copy back allow bytes [ne][ni] and, with a spec,
+ * the L4 identity bitmaps [n_filters][ceil(ni / 64)] */
+static int l3_run(cgpu_ctx *c, const cgpu_l3_program *p, const cgpu_label_sets *eps,
+		  const cgpu_label_sets *ids, uint32_t flags, const cgpu_mapstate_spec *ms,
+		  uint8_t *allow_out, uint64_t *l4_out)
 {
-	if (!c || !p || !eps || !ids || (!allow_out && eps->n_sets && ids->n_sets))
-		return fail(-EINVAL, "null argument");
 	if (c->device < 0)
 		return fail(-ENODEV, "context has no device (host-only); no CPU path");
 	if (!p->rule_clauses || !eps->offsets || !ids->offsets)
@@ -3875,10 +3885,20 @@ CGPU_EXPORT int cgpu_l3_compile(cgpu_ctx *c, const cgpu_l3_program *p, const cgp
 	for (uint32_t k = 0; k < ni; k++)
 		if (ids->offsets[k] > ids->offsets[k + 1])
 			return fail(-EINVAL, "identity label offsets not monotone");
+	const uint32_t nf = ms ? ms->n_filters : 0;
+	for (uint32_t k = 0; k < nf; k++) {
+		const cgpu_l4_filter &F = ms->filters[k];
+		if (F.endpoint >= ne || F.dir > 1 || (uint64_t)F.sels_off + F.n_sels > ms->n_filter_sels)
+			return fail(-EINVAL, "filter %u out of range", k);
+	}
+	for (uint32_t k = 0; ms && k < ms->n_filter_sels; k++)
+		if (ms->filter_sels[k] >= p->n_selectors)
+			return fail(-EINVAL, "filter selector %u out of range", k);
 	if (!ne || !ni)
 		return 0;
 	const size_t nel = eps->offsets[ne], nil = ids->offsets[ni];
-	/* one device buffer: program, label sets, subject bits, result */
+	const size_t nw = ((size_t)ni + 63) / 64;
+	/* one device buffer: program, label sets, subject bits, results */
 	size_t off = 0;
 	auto take = [&](size_t b) { size_t o = off; off += (b + 255) & ~(size_t)255; return o; };
 	const size_t o_sel = take(sizeof(cgpu_selector) * p->n_selectors);
@@ -3890,6 +3910,8 @@ CGPU_EXPORT int cgpu_l3_compile(cgpu_ctx *c, const cgpu_l3_program *p, const cgp
 	const size_t o_eo = take(4ull * (ne + 1)), o_io = take(4ull * (ni + 1));
 	const size_t o_el = take(sizeof(cgpu_label) * nel), o_il = take(sizeof(cgpu_label) * nil);
 	const size_t o_subj = take((size_t)ne * p->n_rules), o_allow = take((size_t)ne * ni);
+	const size_t o_ef = take(ms ? 4ull * ne : 0), o_ft = take(sizeof(cgpu_l4_filter) * nf);
+	const size_t o_fs = take(ms ? 4ull * ms->n_filter_sels : 0), o_l4 = take(8ull * nf * nw);
 	std::lock_guard<std::mutex> g(c->mu);
 	HIP_OR_EIO(hipSetDevice(c->device));
 	uint8_t *d = nullptr;
@@ -3907,7 +3929,10 @@ CGPU_EXPORT int cgpu_l3_compile(cgpu_ctx *c, const cgpu_l3_program *p, const cgp
 	    (e = up(o_eo, eps->offsets, 4ull * (ne + 1))) == hipSuccess &&
 	    (e = up(o_io, ids->offsets, 4ull * (ni + 1))) == hipSuccess &&
 	    (e = up(o_el, eps->labels, sizeof(cgpu_label) * nel)) == hipSuccess &&
-	    (e = up(o_il, ids->labels, sizeof(cgpu_label) * nil)) == hipSuccess) {
+	    (e = up(o_il, ids->labels, sizeof(cgpu_label) * nil)) == hipSuccess &&
+	    (!ms || ((e = up(o_ef, ms->ep_flags, 4ull * ne)) == hipSuccess &&
+		     (e = up(o_ft, ms->filters, sizeof(cgpu_l4_filter) * nf)) == hipSuccess &&
+		     (e = up(o_fs, ms->filter_sels, 4ull * ms->n_filter_sels)) == hipSuccess))) {
 		l3_launch L{reinterpret_cast<const cgpu_selector *>(d + o_sel),
 			    reinterpret_cast<const cgpu_requirement *>(d + o_req),
 			    reinterpret_cast<const uint32_t *>(d + o_val),
@@ -3916,12 +3941,126 @@ CGPU_EXPORT int cgpu_l3_compile(cgpu_ctx *c, const cgpu_l3_program *p, const cgp
 			    reinterpret_cast<const cgpu_l3_clause *>(d + o_cl),
 			    reinterpret_cast<const uint32_t *>(d + o_eo), reinterpret_cast<const uint32_t *>(d + o_io),
 			    reinterpret_cast<const cgpu_label *>(d + o_el), reinterpret_cast<const cgpu_label *>(d + o_il),
-			    ne, ni, flags, d + o_subj, d + o_allow};
-		if ((e = launch_l3_compile(L, nullptr)) == hipSuccess && (e = hipDeviceSynchronize()) == hipSuccess)
-			e = hipMemcpy(allow_out, d + o_allow, (size_t)ne * ni, hipMemcpyDeviceToHost);
+			    ne, ni, flags, d + o_subj, d + o_allow,
+			    ms ? reinterpret_cast<const uint32_t *>(d + o_ef) : nullptr,
+			    reinterpret_cast<const cgpu_l4_filter *>(d + o_ft),
+			    reinterpret_cast<const uint32_t *>(d + o_fs), nf,
+			    nf ? reinterpret_cast<uint64_t *>(d + o_l4) : nullptr};
+		if ((e = launch_l3_compile(L, nullptr)) == hipSuccess && (e = hipDeviceSynchronize()) == hipSuccess &&
+		    (e = hipMemcpy(allow_out, d + o_allow, (size_t)ne * ni, hipMemcpyDeviceToHost)) == hipSuccess &&
+		    nf)
+			e = hipMemcpy(l4_out, d + o_l4, 8ull * nf * nw, hipMemcpyDeviceToHost);
 	}
 	(void)hipFree(d);
 	if (e != hipSuccess)
-		return fail(-EIO, "cgpu_l3_compile: %s", hipGetErrorString(e));
+		return fail(-EIO, "L3/L4 selector kernels: %s", hipGetErrorString(e));
 	return 0;
+}
+
+CGPU_EXPORT int cgpu_l3_compile(cgpu_ctx *c, const cgpu_l3_program *p, const cgpu_label_sets *eps,
+				const cgpu_label_sets *ids, uint32_t flags, uint8_t *allow_out)
+{
+	if (!c || !p || !eps || !ids || (!allow_out && eps->n_sets && ids->n_sets))
+		return fail(-EINVAL, "null argument");
+	return l3_run(c, p, eps, ids, flags, nullptr, allow_out, nullptr);
+}
+
+static inline uint64_t ms_key(uint32_t id, uint16_t dport_host, uint8_t proto, uint8_t dir)
+{
+	cgpu_policy_key k{id, __builtin_bswap16(dport_host), proto, dir};
+	return pol_key64(&k);
+}
+
+CGPU_EXPORT int cgpu_mapstate_sync(cgpu_ctx *c, const cgpu_l3_program *p, const cgpu_label_sets *eps,
+				   const cgpu_label_sets *ids, const cgpu_mapstate_spec *ms,
+				   cgpu_mapstate_stats *stats)
+{
+	if (!c || !p || !eps || !ids || !ms)
+		return fail(-EINVAL, "null argument");
+	const uint32_t ne = eps->n_sets, ni = ids->n_sets;
+	if (ne && (!ms->ep_map || !ms->ep_flags))
+		return fail(-EINVAL, "null endpoint arrays");
+	if (ni && !ms->identity)
+		return fail(-EINVAL, "null identity array");
+	if ((ms->n_filters && !ms->filters) || (ms->n_filter_sels && !ms->filter_sels))
+		return fail(-EINVAL, "null filter arrays");
+	for (uint32_t k = 0; k < ne; k++)
+		if (ms->ep_map[k] >= c->cfg.max_endpoints)
+			return fail(-EINVAL, "endpoint row %u: map %u >= max_endpoints", k, ms->ep_map[k]);
+	const size_t nw = ((size_t)ni + 63) / 64;
+	std::vector<uint8_t> allow((size_t)ne * ni);
+	std::vector<uint64_t> l4((size_t)ms->n_filters * nw);
+	if (int r = l3_run(c, p, eps, ids, 0, ms, allow.data(), l4.data()))
+		return r;
+	std::vector<std::vector<uint32_t>> ep_filters(ne);
+	for (uint32_t f = 0; f < ms->n_filters; f++)
+		ep_filters[ms->filters[f].endpoint].push_back(f);
+	cgpu_mapstate_stats st{};
+	int first_err = 0;
+	std::map<uint64_t, uint16_t> want; /* key -> proxy port (network order) */
+	std::vector<uint64_t> drop;
+	for (uint32_t e = 0; e < ne; e++) {
+		/* computeDesiredPolicyMapState (policy.go:273-280), in its order */
+		want.clear();
+		for (uint32_t f : ep_filters[e]) {
+			const cgpu_l4_filter &F = ms->filters[f];
+			if (F.redirect && F.proxy_port == 0)
+				continue;
+			const uint64_t *bits = &l4[(size_t)f * nw];
+			for (size_t w = 0; w < nw; w++)
+				for (uint64_t b = bits[w]; b; b &= b - 1) {
+					const size_t i = w * 64 + (size_t)__builtin_ctzll(b);
+					want[ms_key(ms->identity[i], F.port, F.proto, F.dir)] =
+						F.redirect ? __builtin_bswap16(F.proxy_port) : (uint16_t)0;
+				}
+		}
+		const uint32_t fl = ms->ep_flags[e];
+		if (fl & CGPU_MS_ALLOW_LOCALHOST) {
+			want[ms_key(1 /* HOST_ID */, 0, 0, 0)] = 0;
+			if (fl & CGPU_MS_HOST_ALLOWS_WORLD)
+				want[ms_key(2 /* WORLD_ID */, 0, 0, 0)] = 0;
+		}
+		const uint8_t *row = &allow[(size_t)e * ni];
+		for (uint32_t i = 0; i < ni; i++) {
+			if (row[i] & 1)
+				want[ms_key(ms->identity[i], 0, 0, 0)] = 0;
+			if (row[i] & 2)
+				want[ms_key(ms->identity[i], 0, 0, 1)] = 0;
+		}
+		st.desired += want.size();
+		/* syncPolicyMap (endpoint.go:2572-2652): deletes first, then adds */
+		const uint32_t m = ms->ep_map[e];
+		std::lock_guard<std::mutex> g(c->mu);
+		auto &cur = c->pol[m];
+		drop.clear();
+		for (auto &kv : cur)
+			if (!want.count(kv.first))
+				drop.push_back(kv.first);
+		for (uint64_t k : drop) {
+			pol_erase(c, m, cur, cur.find(k));
+			st.deleted++;
+		}
+		for (auto &kv : want) {
+			auto it = cur.find(kv.first);
+			if (it != cur.end() && it->second.proxy_port == kv.second) {
+				st.unchanged++;
+				continue;
+			}
+			const bool had = it != cur.end();
+			cgpu_policy_key k;
+			memcpy(&k, &kv.first, 8);
+			cgpu_policy_entry v{};
+			v.proxy_port = kv.second;
+			if (int r = pol_update_locked(c, m, &k, &v, CGPU_ANY)) {
+				st.failed++;
+				if (!first_err)
+					first_err = r;
+			} else {
+				(had ? st.updated : st.added)++;
+			}
+		}
+	}
+	if (stats)
+		*stats = st;
+	return first_err;
 }

@@ -3292,6 +3292,11 @@ struct l3_dev {
 	uint32_t n_ep, n_id, flags;
 	uint8_t *subj;  /* [n_ep][n_rules] rule subject matches the endpoint */
 	uint8_t *allow; /* [n_ep][n_id] */
+	const uint32_t *ep_flags; /* per-endpoint enforcement (cgpu_mapstate_sync) or nullptr */
+	const cgpu_l4_filter *flt;
+	const uint32_t *flt_sels;
+	uint32_t n_flt;
+	uint64_t *l4bits;
 };
 
 /* EndpointSelector.Matches (api/selector.go:277-302) of labels [l0, l1):
@@ -3381,21 +3386,55 @@ __global__ __launch_bounds__(256) void k_l3_pairs(l3_dev P)
 			if (dec1 >= 0)
 				dec1 = den1 ? -1 : (al1 ? 1 : dec1);
 		}
-		P.allow[t] = (uint8_t)(((!(P.flags & CGPU_L3_INGRESS_ENFORCED) || dec0 == 1) ? 1u : 0u) |
-				       ((!(P.flags & CGPU_L3_EGRESS_ENFORCED) || dec1 == 1) ? 2u : 0u));
+		const uint32_t fl = P.ep_flags ? P.ep_flags[e] : P.flags;
+		P.allow[t] = (uint8_t)(((!(fl & CGPU_L3_INGRESS_ENFORCED) || dec0 == 1) ? 1u : 0u) |
+				       ((!(fl & CGPU_L3_EGRESS_ENFORCED) || dec1 == 1) ? 2u : 0u));
+	}
+}
+
+/* computeDesiredL4PolicyMapEntries (pkg/endpoint/policy.go:110-129,143-192):
+ * a filter yields the key {identity, port, proto, dir} for every identity
+ * one of its Endpoints selectors matches (getSecurityIdentities).  One wave
+ * per (filter, 64 consecutive identities): each lane ORs the filter's
+ * selectors over its identity's labels and the wave's ballot is the bitmap
+ * word, so the output is 1 bit per pair and the store is one u64 per wave. */
+__global__ __launch_bounds__(256) void k_ms_l4(l3_dev P)
+{
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint64_t nw = ((uint64_t)P.n_id + 63u) >> 6;
+	const uint64_t n = (uint64_t)P.n_flt * nw;
+	for (uint64_t w = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6; w < n;
+	     w += ((uint64_t)gridDim.x * 256u) >> 6) {
+		const uint32_t f = (uint32_t)(w / nw);
+		const uint32_t i = (uint32_t)((w % nw) << 6) + lane;
+		bool m = false;
+		if (i < P.n_id) {
+			const cgpu_l4_filter F = P.flt[f];
+			const uint32_t l0 = P.id_off[i], l1 = P.id_off[i + 1];
+			for (uint32_t k = 0; k < F.n_sels && !m; k++)
+				m = l3_match(P, P.flt_sels[F.sels_off + k], P.id_lab, l0, l1);
+		}
+		const uint64_t b = __ballot(m);
+		if (lane == 0)
+			P.l4bits[w] = b;
 	}
 }
 
 hipError_t launch_l3_compile(const l3_launch &L, hipStream_t st)
 {
 	const l3_dev P{L.sel, L.req, L.val, L.rule_subject, L.rule_clauses, L.n_rules, L.cl,
-		       L.ep_off, L.id_off, L.ep_lab, L.id_lab, L.n_ep, L.n_id, L.flags, L.subj, L.allow};
+		       L.ep_off, L.id_off, L.ep_lab, L.id_lab, L.n_ep, L.n_id, L.flags, L.subj, L.allow,
+		       L.ep_flags, L.flt, L.flt_sels, L.n_flt, L.l4bits};
 	const uint64_t ns = (uint64_t)L.n_ep * L.n_rules, np = (uint64_t)L.n_ep * L.n_id;
 	if (ns)
 		hipLaunchKernelGGL(k_l3_subject, dim3((unsigned)std::min<uint64_t>((ns + 255) / 256, 8192)),
 				   dim3(256), 0, st, P);
 	if (np)
 		hipLaunchKernelGGL(k_l3_pairs, dim3((unsigned)std::min<uint64_t>((np + 255) / 256, 16384)),
+				   dim3(256), 0, st, P);
+	const uint64_t nfw = (uint64_t)L.n_flt * (((uint64_t)L.n_id + 63u) >> 6); /* waves */
+	if (nfw && L.l4bits)
+		hipLaunchKernelGGL(k_ms_l4, dim3((unsigned)std::min<uint64_t>((nfw + 3) / 4, 16384)),
 				   dim3(256), 0, st, P);
 	return hipGetLastError();
 }

@@ -135,6 +135,12 @@ struct l3_launch {
 	const cgpu_label *ep_lab, *id_lab;
 	uint32_t n_ep, n_id, flags;
 	uint8_t *subj, *allow;
+	/* cgpu_mapstate_sync only (nullptr / 0 for cgpu_l3_compile) */
+	const uint32_t *ep_flags; /* per endpoint: replaces `flags` */
+	const cgpu_l4_filter *flt;
+	const uint32_t *flt_sels;
+	uint32_t n_flt;
+	uint64_t *l4bits; /* [n_flt][ceil(n_id / 64)] identity bitmaps */
 };
 
 hipError_t launch_l3_compile(const l3_launch &L, hipStream_t st);

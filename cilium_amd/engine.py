@@ -282,6 +282,22 @@ class Engine:
                                      allow.ctypes.data), "cgpu_l3_compile")
         return allow
 
+    def mapstate_sync(self, msp) -> dict:
+        """cgpu_mapstate_sync: msp = cilium_amd.policy.compile_mapstate(...).
+        Computes every endpoint's desired MapState on the device and syncs
+        it into the host mirror's policy maps (visible after commit()).
+        -> the sync counts {desired, added, updated, deleted, unchanged,
+        failed}; raises on the first failing key like syncPolicyMap's error."""
+        from . import policy as P
+        m = msp
+        cp, ce, ci = P.c_program(m.prog), P.c_label_sets(*m.ep_sets), P.c_label_sets(*m.id_sets)
+        spec, stats = P.c_mapstate_spec(m), P.CMapStateStats()
+        rc = self.L.cgpu_mapstate_sync(self.h, C.byref(cp), C.byref(ce), C.byref(ci),
+                                       C.byref(spec), C.byref(stats))
+        out = {n: getattr(stats, n) for n, _ in P.CMapStateStats._fields_}
+        check(rc, "cgpu_mapstate_sync")
+        return out
+
     def flow_hash(self, saddr, daddr, sport, dport, proto) -> int:
         return self.L.cgpu_flow_hash(saddr, daddr, sport, dport, proto)
 

@@ -873,3 +873,104 @@ def make_l3_workload(n_rules=1000, n_endpoints=100, n_identities=65536, seed=SEE
         return out
 
     return repo, sets(n_endpoints), sets(n_identities)
+
+
+# ------------------------------------------- full MapState (L4 + L3 + CIDR)
+def make_mapstate_workload(n_rules=120, n_endpoints=16, n_identities=400, seed=SEED, n_keys=8,
+                           n_vals=4):
+    """A repository exercising every input of computeDesiredPolicyMapState:
+    FromEndpoints / FromRequires / FromEntities / FromCIDR / FromCIDRSet (and
+    the To* forms), ToPorts over TCP / UDP / ANY with HTTP or Kafka L7 rules on
+    some ports (one L7 kind per port, so merges never conflict), L3-only
+    blocks that wildcardL3L4Rules folds into L7 filters; identities with label
+    sets, the reserved identities and CIDR identities
+    (labels/cidr.GetCIDRLabels); endpoints with mixed enforcement and some
+    redirects left unallocated (proxy port 0).
+    -> (repo, [EndpointPolicy], [(identity, [Label])])"""
+    from . import policy as P
+    rng = np.random.Generator(np.random.PCG64(seed + 0x14))
+    keys = [f"k{i}" for i in range(n_keys)]
+    srcs = ["k8s", "container", "any"]
+    l7_of = {"80": "http", "8080": "http", "9092": "kafka", "53": None, "443": None, "5000": None}
+    ports = list(l7_of)
+    cidrs = ["10.0.0.0/8", "10.1.0.0/16", "192.168.0.0/16", "0.0.0.0/0", "172.16.5.0/24"]
+
+    def sel(lo=0):
+        ml = {}
+        for _ in range(rng.integers(lo, 3)):
+            ml[f"{rng.choice(srcs)}.{rng.choice(keys)}"] = f"v{rng.integers(0, n_vals)}"
+        ex = []
+        if rng.random() < 0.3:
+            op = str(rng.choice(["In", "NotIn", "Exists", "DoesNotExist"]))
+            vals = [f"v{x}" for x in rng.integers(0, n_vals, rng.integers(1, 3))] if op in (
+                "In", "NotIn") else []
+            ex.append((f"{rng.choice(srcs)}.{rng.choice(keys)}", op, vals))
+        if rng.random() < 0.01:
+            ml["reserved.all"] = ""
+        return P.EndpointSelector(ml, ex)
+
+    def port_rules():
+        out = []
+        for _ in range(rng.integers(1, 3)):
+            ps = [(str(p), str(rng.choice(["TCP", "TCP", "UDP", "ANY"])))
+                  for p in rng.choice(ports, rng.integers(1, 3), replace=False)]
+            pr = P.PortRule(ps)
+            kinds = {l7_of[p] for p, _ in ps} - {None}
+            if len(kinds) == 1 and rng.random() < 0.6:
+                kind = kinds.pop()
+                if kind == "http":
+                    pr.http = [("GET", "/")]
+                else:
+                    pr.kafka = [("produce",)]
+                pr.ports = [(p, pr_) for p, pr_ in ps if l7_of[p] == kind]
+            out.append(pr)
+        return out
+
+    def block(ingress):
+        kw = {}
+        has_ports = rng.random() < 0.5
+        kind = rng.choice(["ep", "ep", "ep", "ent", "cidr", "cidrset", "none"])
+        pre = "from_" if ingress else "to_"
+        if kind == "ep":
+            kw[pre + "endpoints"] = [sel(0) for _ in range(rng.integers(1, 3))]
+        elif kind == "ent":
+            kw[pre + "entities"] = list(rng.choice(["world", "host", "cluster", "all", "init"],
+                                                   rng.integers(1, 3), replace=False))
+        elif kind == "cidr" and (not ingress or not has_ports):  # Sanitize: no FromCIDR + ToPorts
+            kw[pre + "cidr"] = list(rng.choice(cidrs, rng.integers(1, 3), replace=False))
+        elif kind == "cidrset" and (not ingress or not has_ports):
+            kw[pre + "cidr_set"] = [("10.0.0.0/8", ["10.96.0.0/12", "10.1.2.0/24"])]
+        if rng.random() < 0.04 and kind == "ep":
+            kw[pre + "requires"] = [sel(1)]
+        if has_ports:
+            kw["to_ports"] = port_rules()
+        return (P.IngressRule if ingress else P.EgressRule)(**kw)
+
+    repo = P.Repository()
+    for _ in range(n_rules):
+        repo.add(P.Rule(sel(1), [block(True) for _ in range(rng.integers(0, 3))],
+                        [block(False) for _ in range(rng.integers(0, 3))]))
+
+    def labels_of():
+        nl = rng.integers(1, 5)
+        return [P.Label(str(rng.choice(srcs[:2])), keys[rng.integers(0, n_keys)],
+                        f"v{rng.integers(0, n_vals)}") for _ in range(nl)]
+
+    ids = [(1, [P.parse_label("reserved:host")]), (2, [P.parse_label("reserved:world")]),
+           (3, [P.parse_label("reserved:cluster")]), (5, [P.parse_label("reserved:init")])]
+    cidr_ids = ["10.1.2.0/24", "10.1.0.0/16", "10.97.0.0/16", "192.168.4.0/24", "8.8.8.8/32",
+                "172.16.5.7/32", "10.200.0.0/16"]
+    for k, c in enumerate(cidr_ids):
+        ids.append(((1 << 24) + 1 + k, P.cidr_identity_labels(c, "10.0.0.0/8")))
+    while len(ids) < n_identities:
+        ids.append((256 + len(ids), labels_of()))
+    eps = []
+    for i in range(n_endpoints):
+        red = {}
+        for ing in (True, False):
+            for p in ("80", "8080", "9092"):
+                if rng.random() < 0.8:
+                    red[(ing, "TCP", int(p))] = int(10000 + 100 * i + int(p) % 97)
+        eps.append(P.EndpointPolicy(labels_of(), i, bool(rng.random() < 0.85),
+                                    bool(rng.random() < 0.85), red))
+    return repo, eps, ids

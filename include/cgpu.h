@@ -700,6 +700,70 @@ int cgpu_l3_compile(cgpu_ctx *ctx, const cgpu_l3_program *prog, const cgpu_label
 		    const cgpu_label_sets *identities, uint32_t flags, uint8_t *allow_out);
 
 /* ------------------------------------------------------------------ */
+/* full MapState: L4 + localhost/world + L3 keys, synced into the maps  */
+/* (pkg/endpoint/policy.go:143-390, endpoint.go:2572)   */
+/* ------------------------------------------------------------------ */
+/* One L4Filter of an endpoint's resolved L4 policy (pkg/policy/l4.go:83-103),
+ * as Repository.ResolveL4{Ingress,Egress}Policy (repository.go:240-329) left
+ * it, wildcardL3L4Rules included; the caller (cilium_amd/policy.py) resolves
+ * the filters, which is O(rules) per endpoint.  Its Endpoints selectors are
+ * ids into the program's selector table. */
+typedef struct cgpu_l4_filter {
+	uint32_t endpoint;         /* row of the endpoint label sets */
+	uint32_t sels_off, n_sels; /* selectors filter_sels[sels_off, +n_sels) */
+	uint16_t port;             /* L4Filter.Port, host order */
+	uint8_t proto;             /* L4Filter.U8Proto */
+	uint8_t dir;               /* CGPU_L3_INGRESS / CGPU_L3_EGRESS */
+	uint16_t proxy_port;       /* realizedRedirects[ProxyID] (host order) of a redirect */
+	uint8_t redirect;          /* L7Parser != "": no keys while proxy_port is 0 (policy.go:158-166) */
+	uint8_t pad;
+} cgpu_l4_filter;
+
+#define CGPU_MS_ALLOW_LOCALHOST 4u   /* AlwaysAllowLocalhost() || DesiredL4Policy.HasRedirect() */
+#define CGPU_MS_HOST_ALLOWS_WORLD 8u /* option HostAllowsWorld (policy.go:305-315) */
+typedef struct cgpu_mapstate_spec {
+	const cgpu_l4_filter *filters;
+	uint32_t n_filters;
+	const uint32_t *filter_sels;
+	uint32_t n_filter_sels;
+	const uint32_t *ep_map;   /* [n_endpoints] the policy-map index (`ep`) of each endpoint row */
+	const uint32_t *ep_flags; /* [n_endpoints] CGPU_L3_*_ENFORCED | CGPU_MS_* */
+	const uint32_t *identity; /* [n_identities] NumericIdentity of each identity row */
+} cgpu_mapstate_spec;
+
+typedef struct cgpu_mapstate_stats {
+	uint64_t desired;   /* keys in the desired MapStates */
+	uint64_t added;     /* AllowKey of a key the map did not hold */
+	uint64_t updated;   /* AllowKey of a held key with another proxy port (counters restart) */
+	uint64_t deleted;   /* DeleteKey of a held key no longer desired */
+	uint64_t unchanged; /* desired keys already held with the same proxy port */
+	uint64_t failed;    /* AllowKey / DeleteKey errors (e.g. -E2BIG) */
+} cgpu_mapstate_stats;
+
+/*
+ * computeDesiredPolicyMapState for every endpoint row, then syncPolicyMap
+ * into that endpoint's policy map:
+ *   1. L4 keys {identity, port, proto, dir} -> proxy_port for every identity
+ *      any of a filter's selectors matches (computeDesiredL4PolicyMapEntries,
+ *      policy.go:143-192); one wave per (filter, 64 identities) on the device;
+ *   2. {HOST_ID, 0, 0, ingress} if CGPU_MS_ALLOW_LOCALHOST, then
+ *      {WORLD_ID, 0, 0, ingress} if also CGPU_MS_HOST_ALLOWS_WORLD
+ *      (determineAllowLocalhost / determineAllowFromWorld, policy.go:284-315);
+ *   3. the L3 keys of cgpu_l3_compile under the endpoint's enforcement bits
+ *      (policy.go:317-390).
+ * Sync (endpoint.go:2572-2652): held keys not desired are deleted; desired
+ * keys absent or held with another proxy port are written (the value, and
+ * with it the counters, restart); the rest are left alone.  Like the
+ * reference, a failing key does not stop the others: the first error is
+ * returned after all keys were tried.  Changes go to the host mirror and
+ * become visible to classify at the next cgpu_commit (a small delta patches
+ * the device tables in place).  All inputs are host pointers.
+ */
+int cgpu_mapstate_sync(cgpu_ctx *ctx, const cgpu_l3_program *prog, const cgpu_label_sets *endpoints,
+		       const cgpu_label_sets *identities, const cgpu_mapstate_spec *spec,
+		       cgpu_mapstate_stats *stats);
+
+/* ------------------------------------------------------------------ */
 /* counters                                                             */
 /* ------------------------------------------------------------------ */
 /*
