@@ -45,6 +45,11 @@ LB4_KEY = np.dtype([("address", "<u4"), ("dport", "<u2"), ("slave", "<u2")])
 LB4_SERVICE = np.dtype([("target", "<u4"), ("port", "<u2"), ("count", "<u2"),
                         ("rev_nat_index", "<u2"), ("weight", "<u2")])
 assert LB4_KEY.itemsize == 8 and LB4_SERVICE.itemsize == 12
+# struct lb6_key / lb6_service, bpf/lib/common.h:408-420 (packed)
+LB6_KEY = np.dtype([("address", "u1", 16), ("dport", "<u2"), ("slave", "<u2")])
+LB6_SERVICE = np.dtype([("target", "u1", 16), ("port", "<u2"), ("count", "<u2"),
+                        ("rev_nat_index", "<u2"), ("weight", "<u2")])
+assert LB6_KEY.itemsize == 20 and LB6_SERVICE.itemsize == 24
 assert LPM_V4_KEY.itemsize == 8 and LPM_V6_KEY.itemsize == 20
 assert ENDPOINT_KEY.itemsize == 20
 

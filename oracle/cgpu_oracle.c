@@ -353,6 +353,7 @@ struct or_ctx {
 	struct ohash fix4, fix6;
 	struct ohash lxc;           /* endpoint_key -> present */
 	struct ohash lb;            /* lb4_key (8 B) -> lb4_service (12 B) */
+	struct ohash lb6;           /* lb6_key (20 B) -> lb6_service (24 B) */
 	uint8_t *lxcinfo;           /* [n_lxcinfo][32] per-endpoint identity */
 	size_t n_lxcinfo;
 	struct ohash ct;            /* ipv4_ct_tuple (14 B) -> ct_entry (56 B) */
@@ -397,6 +398,7 @@ or_ctx *or_create(void)
 	oh_init(&c->fix6, 20, 1);
 	oh_init(&c->lxc, 20, 1);
 	oh_init(&c->lb, 8, 12);
+	oh_init(&c->lb6, 20, 24);
 	oh_init(&c->ct, 14, 56);
 	c->ct_max = 1000000; /* ctmap.go:101 MapNumEntriesGlobal */
 	return c;
@@ -765,6 +767,132 @@ static struct lb_res lb4_one(const or_ctx *c, int mode, uint32_t saddr, uint32_t
 	return r;
 }
 
+/* ---- IPv6 service map (cilium_lb6_services, lb.h:46-52) ---- */
+int or_lb6_update(or_ctx *c, const void *key20, const void *val24)
+{
+	return oh_update(&c->lb6, key20, val24);
+}
+
+int or_lb6_delete(or_ctx *c, const void *key20)
+{
+	return oh_delete(&c->lb6, key20);
+}
+
+static inline uint32_t fmix32(uint32_t h)
+{
+	h ^= h >> 16;
+	h *= 0x85EBCA6Bu;
+	h ^= h >> 13;
+	h *= 0xC2B2AE35u;
+	h ^= h >> 16;
+	return h;
+}
+
+/* one 32-bit word standing for a 16-byte address (raw bytes read as four
+ * little-endian words); = tables.h fold6 */
+static uint32_t fold6(const uint8_t *a)
+{
+	uint32_t w[4];
+	memcpy(w, a, 16);
+	return fmix32(w[0] ^ fmix32(w[1] ^ fmix32(w[2] ^ fmix32(w[3] ^ 0x6B43A9B5u))));
+}
+
+/* cgpu_flow_hash6: or_flow_hash over the folded addresses */
+uint32_t or_flow_hash6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t sport, uint16_t dport,
+		       uint8_t proto)
+{
+	return or_flow_hash(fold6(saddr16), fold6(daddr16), sport, dport, proto);
+}
+
+/* struct lb6_service fields (packed, bpf/lib/common.h:414-420) */
+static inline uint16_t lb6v_port(const uint8_t *v) { uint16_t x; memcpy(&x, v + 16, 2); return x; }
+static inline uint16_t lb6v_count(const uint8_t *v) { uint16_t x; memcpy(&x, v + 18, 2); return x; }
+static inline uint16_t lb6v_rev_nat(const uint8_t *v) { uint16_t x; memcpy(&x, v + 20, 2); return x; }
+
+static const uint8_t *lb6_get(const or_ctx *c, const uint8_t *addr, uint16_t dport, uint16_t slave,
+			      uint64_t *probes)
+{
+	uint8_t key[20];
+	memcpy(key, addr, 16);
+	memcpy(key + 16, &dport, 2);
+	memcpy(key + 18, &slave, 2);
+	(*probes)++;
+	return oh_get(&c->lb6, key);
+}
+
+/* lb6_lookup_service (lb.h:351-380) */
+static const uint8_t *lb6_lookup_service(const or_ctx *c, const uint8_t *addr, uint16_t *kd,
+					 uint16_t slave, uint64_t *probes)
+{
+	const uint8_t *v;
+	if (c->cfg.lb_l4 && *kd) {
+		v = lb6_get(c, addr, *kd, slave, probes);
+		if (v && lb6v_count(v))
+			return v;
+		*kd = 0;
+	}
+	if (c->cfg.lb_l3) {
+		v = lb6_get(c, addr, *kd, slave, probes);
+		if (v && lb6v_count(v))
+			return v;
+	}
+	return NULL;
+}
+
+struct lb6_res {
+	int32_t ret; /* 0 not a service, 1 translated, DROP_NO_SERVICE */
+	uint8_t tdaddr[16];
+	uint16_t dport, rev_nat, slave;
+};
+
+/* The service step of ipv6_l3_from_lxc (bpf_lxc.c:117-139) with an empty
+ * conntrack table (CT_NEW): lb6_extract_key (lb.h:334-349), lb6_lookup_service,
+ * lb6_local (lb.h:426-483).  IPv6 has no loopback case. */
+static struct lb6_res lb6_one(const or_ctx *c, const uint8_t *daddr, uint16_t dport, uint8_t proto,
+			      uint32_t hash, uint64_t *probes)
+{
+	struct lb6_res r;
+	const uint8_t *svc, *be;
+	uint16_t kd = 0, slave;
+	memset(&r, 0, sizeof(r));
+	memcpy(r.tdaddr, daddr, 16);
+	r.dport = dport;
+	if (c->cfg.lb_l4) { /* extract_l4_port (lb.h:191-215) */
+		if (proto == PROTO_TCP || proto == PROTO_UDP)
+			kd = dport;
+		else if (proto != PROTO_ICMP && proto != PROTO_ICMPV6)
+			return r; /* DROP_UNKNOWN_L4 -> skip_service_lookup */
+	}
+	svc = lb6_lookup_service(c, daddr, &kd, 0, probes);
+	if (!svc)
+		return r;
+	if (c->cfg.ct_proto_gate && proto != PROTO_ICMPV6 && proto != PROTO_TCP && proto != PROTO_UDP) {
+		/* lb6_local's CT_SERVICE ct_lookup6: DROP_CT_UNKNOWN_PROTO
+		 * (conntrack.h:376-378) -> DROP_NO_SERVICE (lb.h:436-456) */
+		r.ret = DROP_NO_SERVICE;
+		return r;
+	}
+	slave = (uint16_t)(hash % lb6v_count(svc) + 1); /* lb6_select_slave, lb.h:124-156 */
+	be = lb6_get(c, daddr, kd, slave, probes);     /* lb6_lookup_slave, lb.h:382-396 */
+	if (!be) {
+		/* lb.h:462-469: the key keeps the slave just tried */
+		be = lb6_lookup_service(c, daddr, &kd, slave, probes);
+		if (!be) {
+			r.ret = DROP_NO_SERVICE;
+			return r;
+		}
+		slave = (uint16_t)(hash % lb6v_count(be) + 1);
+	}
+	memcpy(r.tdaddr, be, 16); /* tuple->daddr = svc->target (lb.h:475) */
+	r.slave = slave;
+	r.rev_nat = lb6v_rev_nat(be);
+	r.ret = 1;
+	/* lb6_xlate port rewrite (lb.h:410-420) */
+	if (c->cfg.lb_l4 && lb6v_port(be) && kd != lb6v_port(be) && (proto == PROTO_TCP || proto == PROTO_UDP))
+		r.dport = lb6v_port(be);
+	return r;
+}
+
 struct lb_job {
 	const or_ctx *c;
 	int mode;
@@ -1062,6 +1190,9 @@ struct cls6_job {
 	const uint8_t *s6, *d6, *proto, *flags;
 	const uint32_t *len;
 	const uint16_t *dport, *ep;
+	int lb;                  /* egress service step first (or_classify_v6_lb) */
+	const uint16_t *sport;
+	const uint32_t *hash;
 	int32_t *verdict;
 	uint32_t *identity;
 	uint8_t *stage;
@@ -1082,8 +1213,33 @@ static void *cls6_worker(void *arg)
 		int st, dir = egress ? METRIC_EGRESS : METRIC_INGRESS;
 		struct ohash *h = ep < c->n_ep ? &c->policy[ep] : NULL;
 		const uint8_t *sa = j->s6 + 16 * i, *da = j->d6 + 16 * i;
+		uint8_t tda[16];
+		uint16_t dport = j->dport[i];
+		int lbdrop = 0;
 
-		if (cfg->ct_proto_gate && proto != 58 && proto != PROTO_TCP && proto != PROTO_UDP) {
+		if (j->lb && egress) {
+			/* lb6_extract_key / lb6_lookup_service / lb6_local before
+			 * conntrack and policy (bpf_lxc.c:117-149): ipcache resolves
+			 * tuple->daddr (orig_dip), ct_lookup6 reloads the rewritten
+			 * dport from the packet for policy */
+			uint32_t hh = j->hash ? j->hash[i] : or_flow_hash6(sa, da, j->sport[i], dport, proto);
+			struct lb6_res lr = lb6_one(c, da, dport, proto, hh, &j->probes);
+			if (lr.ret == DROP_NO_SERVICE) {
+				lbdrop = 1;
+			} else {
+				memcpy(tda, lr.tdaddr, 16);
+				da = tda;
+				dport = lr.dport;
+			}
+		}
+
+		if (lbdrop) {
+			/* ipv6_l3_from_lxc returns DROP_NO_SERVICE -> send_drop_notify
+			 * (.., METRIC_EGRESS), dstID 0 (bpf_lxc.c:136-138, :659-666) */
+			v = DROP_NO_SERVICE;
+			id = 0;
+			st = 6;
+		} else if (cfg->ct_proto_gate && proto != 58 && proto != PROTO_TCP && proto != PROTO_UDP) {
 			/* ct_lookup6 default case, bpf/lib/conntrack.h:376-378 */
 			v = DROP_CT_UNKNOWN_PROTO;
 			id = 0;
@@ -1102,7 +1258,7 @@ static void *cls6_worker(void *arg)
 			else
 				id = cfg->world_id;
 			j->probes += 1;
-			r = policy_access(h, id, j->dport[i], proto, 1, 0, j->len[i]);
+			r = policy_access(h, id, dport, proto, 1, 0, j->len[i]);
 			v = r.ret >= 0 ? r.ret : DROP_POLICY;
 			st = r.stage;
 			j->probes += r.probes;
@@ -1142,10 +1298,11 @@ static void *cls6_worker(void *arg)
 	return NULL;
 }
 
-int or_classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
-		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
-		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
-		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
+static int classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		       const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		       const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		       uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum,
+		       int lb, const uint16_t *sport, const uint32_t *hash)
 {
 	struct cls6_job *jobs;
 	pthread_t *th;
@@ -1171,6 +1328,9 @@ int or_classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *d
 		j->verdict = verdict;
 		j->identity = identity;
 		j->stage = stage;
+		j->lb = lb;
+		j->sport = sport;
+		j->hash = hash;
 		if (nthreads == 1)
 			cls6_worker(j);
 		else
@@ -1188,6 +1348,27 @@ int or_classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *d
 	free(jobs);
 	free(th);
 	return 0;
+}
+
+int or_classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		   const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+		   const uint32_t *len, const uint16_t *ep, int32_t *verdict,
+		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
+{
+	return classify_v6(c, n, saddr16, daddr16, dport, proto, flags, len, ep, verdict, identity,
+			   stage, nthreads, probe_sum, 0, NULL, NULL);
+}
+
+int or_classify_v6_lb(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint8_t *flags, const uint32_t *len, const uint16_t *ep,
+		      const uint32_t *hash, int32_t *verdict, uint32_t *identity, uint8_t *stage,
+		      int nthreads, uint64_t *probe_sum)
+{
+	if (!hash && !sport && n)
+		return -EINVAL;
+	return classify_v6(c, n, saddr16, daddr16, dport, proto, flags, len, ep, verdict, identity,
+			   stage, nthreads, probe_sum, 1, sport, hash);
 }
 
 /* ---- XDP prefilter (bpf/bpf_xdp.c:88-184) ---- */

@@ -100,6 +100,18 @@ int or_lb_delete(or_ctx *c, const void *key8);
 /* kernel skb->hash stand-in used when no hash column is given (the kernel's
  * flow-dissector hash is unpinned); = cilium_amd.shard.flowhash_np */
 uint32_t or_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport, uint8_t proto);
+/* IPv6 service map (lb6_key 20 B -> lb6_service 24 B) and the IPv6 flow hash */
+int or_lb6_update(or_ctx *c, const void *key20, const void *val24);
+int or_lb6_delete(or_ctx *c, const void *key20);
+uint32_t or_flow_hash6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t sport, uint16_t dport,
+		       uint8_t proto);
+/* or_classify_v6 with the egress service step of ipv6_l3_from_lxc in front
+ * (bpf_lxc.c:117-139; lb6_local, lb.h:426-483): hash NULL = or_flow_hash6 */
+int or_classify_v6_lb(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint8_t *flags, const uint32_t *len, const uint16_t *ep,
+		      const uint32_t *hash, int32_t *verdict, uint32_t *identity, uint8_t *stage,
+		      int nthreads, uint64_t *probe_sum);
 
 #define OR_LB_NETDEV 0 /* bpf_lb.c handle_ipv4 (bpf_lb.c:118-170) */
 #define OR_LB_LXC 1    /* lb4_local from handle_ipv4_from_lxc, CT_NEW (bpf_lxc.c:444-460) */

@@ -818,6 +818,173 @@ def gen_classify_lb_fixture(pol, lbls, rng):
                 **{"t_" + k: v for k, v in t.items()}, **out)
 
 
+# ------------------------------------------------ IPv6 service translation
+def load_ref_lbl6():
+    libs = {}
+    for v, f in ((1, "libref_lbl6.so"), (0, "libref_lbl6_noct.so")):
+        lib = C.CDLL(os.path.join(HERE, "_ref", f))
+        lib.ref_lbl6_reset.restype = None
+        lib.ref_lbl6_update.argtypes = [C.c_void_p, C.c_void_p]
+        u16p = C.POINTER(C.c_uint16)
+        lib.ref_lbl6_run.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int),
+                                     C.c_void_p, u16p, u16p, C.POINTER(C.c_int),
+                                     C.POINTER(C.c_uint64)]
+        libs[v] = lib
+    return libs  # [1]: CONNTRACK build, [0]: without
+
+
+def gen_lb6_services(rng, n_vip, targets):
+    """cilium_lb6_services contents (lbmap.UpdateService's layout, plus the
+    irregular contents gen_lb_services also covers: count-0 masters, masters
+    counting more slaves than exist, backends with a count, sparse slaves)."""
+    keys, vals, vips = [], [], []
+
+    def put(addr, dport_be, slave, target, port_be, count, rev, weight):
+        k = np.zeros((), L.LB6_KEY)
+        k["address"][:] = addr
+        k["dport"], k["slave"] = dport_be, slave
+        v = np.zeros((), L.LB6_SERVICE)
+        v["target"][:] = target
+        v["port"], v["count"], v["rev_nat_index"], v["weight"] = port_be, count, rev, weight
+        keys.append(k)
+        vals.append(v)
+
+    for _ in range(n_vip):
+        vip = np.zeros(16, np.uint8)
+        vip[:6] = [0xFD, 0x00, 0x00, 0x96, 0, 0]
+        vip[6:] = rng.integers(0, 256, 10, dtype=np.uint8)
+        vips.append(vip)
+        kinds = ["l4"] if rng.random() < 0.5 else (["l3"] if rng.random() < 0.4 else ["l4", "l3"])
+        for kind in kinds:
+            dport = L.htons(int(rng.choice(PORTS[1:6]))) if kind == "l4" else 0
+            nb = int(rng.integers(1, 6))
+            rev = int(rng.integers(1, 65536))
+            count = nb
+            r = rng.random()
+            if r < 0.08:
+                count = 0
+            elif r < 0.2:
+                count = nb + 1
+            put(vip, dport, 0, np.zeros(16, np.uint8), 0, count, 0, int(rng.integers(0, 3)))
+            slaves = list(range(1, nb + 1))
+            if rng.random() < 0.1:
+                slaves[-1] = int(rng.integers(nb + 1, 40))
+            for sl in slaves:
+                tgt = targets[int(rng.integers(0, len(targets)))]
+                pr = rng.random()
+                port = 0 if pr < 0.3 else (dport if pr < 0.5 else L.htons(int(rng.integers(1, 65536))))
+                bc = int(rng.integers(1, 4)) if (kind == "l3" and rng.random() < 0.5) else 0
+                put(vip, dport, sl, tgt, port, bc, rev, int(rng.integers(0, 65536)))
+    return np.array(keys, L.LB6_KEY), np.array(vals, L.LB6_SERVICE), np.array(vips, np.uint8)
+
+
+def l4_frame6(s16, d16, sport_be, dport_be, proto):
+    """Ethernet + IPv6 (nexthdr = proto) + an L4 header carrying the ports at
+    offsets 0 / 2 (TCP, UDP) or an ICMPv6 echo request."""
+    if proto == 58:
+        l4 = bytes([128, 0]) + bytes(6)
+    else:
+        l4 = int(sport_be).to_bytes(2, "little") + int(dport_be).to_bytes(2, "little") + \
+            bytes(16 if proto == 6 else 4)
+    h = bytearray(40)
+    h[0] = 0x60
+    h[4:6] = len(l4).to_bytes(2, "big")
+    h[6] = proto
+    h[8:24] = bytes(s16)
+    h[24:40] = bytes(d16)
+    return bytearray(eth(0x86DD, bytes(h) + l4)), 54
+
+
+def gen_classify_v6_lb_fixture(pol, lbl6s, rng):
+    """The IPv6 egress path with the service step, composed from the
+    reference's own steps in ipv6_l3_from_lxc order: lb6_local
+    (libref_lbl6, bpf_lxc.c:108-139), then ipcache on tuple->daddr and policy
+    on the dport ct_lookup6 reloads from the rewritten packet (libref_policy
+    ref_classify_v6 = bpf_lxc.c:158-203).  DROP_NO_SERVICE ends the packet
+    before conntrack (bpf_lxc.c:136-138), counted with METRIC_EGRESS."""
+    base = gen_classify_v6_fixture(pol, rng)
+    ikeys, ivals = base["ipc_keys"], base["ipc_vals"]
+    pk, pe, pep = base["pol_keys"], base["pol_entries"], base["pol_ep"]
+    v6 = ikeys["family"] == L.ENDPOINT_KEY_IPV6
+    targets = ikeys[v6]["ip"][rng.integers(0, int(v6.sum()), 200)].astype(np.uint8)
+    keys, vals, vips = gen_lb6_services(rng, 60, targets)
+    n = 5000
+    fe = {}
+    for k in keys:
+        fe.setdefault(k["address"].tobytes(), set()).add(int(k["dport"]))
+    vsel = vips[rng.integers(0, len(vips), n)]
+    daddr = np.where(rng.random((n, 1)) < 0.75, vsel, base["t_daddr"]).astype(np.uint8)
+    dport = np.empty(n, np.uint16)
+    for i in range(n):
+        ports = [p for p in fe.get(daddr[i].tobytes(), ()) if p]
+        dport[i] = int(rng.choice(ports)) if ports and rng.random() < 0.8 else base["t_dport"][i]
+    h = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    h[:8] = [0, 1, 2, 0xFFFFFFFF, 0x7FFFFFFF, 65535, 65536, 0x80000000]
+    t = {"saddr": base["t_saddr"], "daddr": daddr, "sport": rng.integers(0, 65536, n).astype(np.uint16),
+         # final L4 protocols only: the frame carries no extension header, so
+         # an extension-header number (0 = hop-by-hop ...) is not a tuple protocol
+         "dport": dport, "proto": rng.choice(np.array([6, 6, 6, 6, 17, 17, 58, 58, 1, 47, 132], np.uint8), n),
+         "hash": h, "flags": (rng.random(n) < 0.7).astype(np.uint8),
+         "len": rng.integers(0, 70000, n).astype(np.uint32), "ep": rng.integers(0, 4, n).astype(np.uint16)}
+    out = {}
+    idv, st, npb, na = C.c_uint32(), C.c_int(), C.c_int(), C.c_int()
+    hit, rn, sl, l4o, cnt = C.c_int(), C.c_uint16(), C.c_uint16(), C.c_int(), C.c_uint64()
+    td = C.create_string_buffer(16)
+    for ci, (gate, src) in enumerate(CONFIGS6[:2]):
+        lib = lbl6s[gate]
+        lib.ref_lbl6_reset()
+        for k, v in zip(keys, vals):
+            lib.ref_lbl6_update(b(k), b(v))
+        pol.ref_reset()
+        for k, v in zip(ikeys, ivals):
+            pol.ref_ipcache_update(b(k), b(v))
+        for k, e, ep in zip(pk, pe, pep):
+            pol.ref_policy_update(int(ep), b(k), b(e))
+        verdict = np.empty(n, np.int32)
+        ident = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        nprobes = np.empty(n, np.int32)
+        lbret = np.zeros(n, np.int32)
+        tdaddr = np.array(t["daddr"], np.uint8)
+        for i in range(n):
+            eg = int(t["flags"][i]) & 1
+            da, dp, nl = t["daddr"][i].tobytes(), int(t["dport"][i]), 0
+            if eg:
+                fr, l4 = l4_frame6(t["saddr"][i], t["daddr"][i], t["sport"][i], t["dport"][i],
+                                   int(t["proto"][i]))
+                buf = (C.c_uint8 * len(fr)).from_buffer(fr)
+                r = lib.ref_lbl6_run(buf, len(fr), int(t["hash"][i]), C.byref(hit), td, C.byref(rn),
+                                     C.byref(sl), C.byref(l4o), C.byref(cnt))
+                lbret[i], nl = r, cnt.value
+                if r < 0:
+                    verdict[i], ident[i], stage[i], nprobes[i] = r, 0, 6, nl
+                    pol.ref_metrics_packet(int(r), int(t["len"][i]), 1)
+                    continue
+                da = td.raw
+                tdaddr[i] = np.frombuffer(da, np.uint8)
+                if int(t["proto"][i]) in (6, 17):
+                    dp = int.from_bytes(bytes(fr[l4 + 2:l4 + 4]), "little")
+            verdict[i] = pol.ref_classify_v6(
+                t["saddr"][i].tobytes(), da, dp, int(t["proto"][i]), int(t["flags"][i]),
+                int(t["len"][i]), int(t["ep"][i]), gate, src, C.byref(idv), C.byref(st),
+                C.byref(npb), C.byref(na))
+            ident[i], stage[i] = idv.value, st.value
+            nprobes[i] = npb.value + na.value + nl
+        final = np.zeros(len(pk), L.POLICY_ENTRY)
+        for i, (k, ep) in enumerate(zip(pk, pep)):
+            buf = C.create_string_buffer(24)
+            assert pol.ref_policy_read(int(ep), b(k), buf) == 0
+            final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+        out[f"c{ci}_verdict"], out[f"c{ci}_identity"] = verdict, ident
+        out[f"c{ci}_stage"], out[f"c{ci}_nprobes"] = stage, nprobes
+        out[f"c{ci}_lbret"], out[f"c{ci}_tdaddr"] = lbret, tdaddr
+        out[f"c{ci}_final_entries"] = final
+        out[f"c{ci}_metrics"] = ref_metrics(pol)
+    return dict(router_ip=base["router_ip"], ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk,
+                pol_entries=pe, pol_ep=pep, lb_keys=keys, lb_vals=vals,
+                configs=np.array(CONFIGS6[:2], np.int64), **{"t_" + k: v for k, v in t.items()}, **out)
+
+
 # ------------------------------------------------------------- raw frames
 FRAME_VARIANTS = ("_ct", "_noct", "_nover")  # oracle/Makefile FRAME_VARIANTS
 
@@ -1075,6 +1242,10 @@ def main():
     # conntrack, its own stream
     rng_ct = np.random.Generator(np.random.PCG64(SEED + 0xC7))
     manifest["files"]["ct4.npz"] = save("ct4.npz", gen_ct_fixture(load_ref_ct(), rng_ct))
+    # IPv6 service translation (SURVEY §8f row 1 widened to IPv6), its own stream
+    rng_lb6 = np.random.Generator(np.random.PCG64(SEED + 0x6B))
+    manifest["files"]["classify_v6_lb.npz"] = save(
+        "classify_v6_lb.npz", gen_classify_v6_lb_fixture(pol, load_ref_lbl6(), rng_lb6))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -69,6 +69,11 @@ def lib():
         L.or_flow_hash.restype = C.c_uint32
         L.or_lb4.argtypes = [vp, C.c_int, sz] + [vp] * 13 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_classify_v4_lb.argtypes = [vp, sz] + [vp] * 12 + [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_classify_v6_lb.argtypes = [vp, sz] + [vp] * 12 + [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_lb6_update.argtypes = [vp, vp, vp]
+        L.or_lb6_delete.argtypes = [vp, vp]
+        L.or_flow_hash6.argtypes = [vp, vp, C.c_uint16, C.c_uint16, C.c_uint8]
+        L.or_flow_hash6.restype = C.c_uint32
         L.or_lxc_update.argtypes = [vp, C.c_uint32, vp]
         L.or_frames_parse.argtypes = [vp, sz, vp, C.c_uint32] + [vp] * 10
         L.or_classify_frames.argtypes = [vp, sz, vp, C.c_uint32] + [vp] * 6 + [
@@ -258,6 +263,40 @@ class Oracle:
             ("ep", np.uint16))]
         h = None if t.get("hash") is None else np.ascontiguousarray(t["hash"], np.uint32)
         rc = self.L.or_classify_v4_lb(self.h, n, *[_p(a) for a in arrs], _p(h), _p(verdict),
+                                      _p(identity), _p(stage), nthreads, C.byref(probes))
+        assert rc == 0, rc
+        return verdict, identity, stage, probes.value
+
+    # --- IPv6 service map ---
+    def lb6_update(self, key, val):
+        return self.L.or_lb6_update(self.h, _b(key), _b(val))
+
+    def lb6_update_batch(self, keys, vals):
+        for k, v in zip(keys, vals):
+            rc = self.lb6_update(k, v)
+            if rc:
+                return rc
+        return 0
+
+    def lb6_delete(self, key):
+        return self.L.or_lb6_delete(self.h, _b(key))
+
+    def flow_hash6(self, saddr16, daddr16, sport, dport, proto):
+        return self.L.or_flow_hash6(bytes(saddr16), bytes(daddr16), sport, dport, proto)
+
+    def classify_v6_lb(self, t, nthreads=1):
+        """classify_v6 with the egress service step of ipv6_l3_from_lxc first."""
+        n = len(t["flags"])
+        verdict = np.empty(n, np.int32)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint8), ("daddr", np.uint8), ("sport", np.uint16),
+            ("dport", np.uint16), ("proto", np.uint8), ("flags", np.uint8), ("len", np.uint32),
+            ("ep", np.uint16))]
+        h = None if t.get("hash") is None else np.ascontiguousarray(t["hash"], np.uint32)
+        rc = self.L.or_classify_v6_lb(self.h, n, *[_p(a) for a in arrs], _p(h), _p(verdict),
                                       _p(identity), _p(stage), nthreads, C.byref(probes))
         assert rc == 0, rc
         return verdict, identity, stage, probes.value

@@ -108,3 +108,31 @@ def test_classify_v4_lb_vs_reference(golden, ci):
     # reference's update_metrics call sites
     np.testing.assert_array_equal(o.metrics(), g[f"c{ci}_metrics"])
     assert (st == 6).sum() > 0
+
+
+@pytest.mark.parametrize("ci", range(2))
+def test_classify_v6_lb_vs_reference(golden, ci):
+    """the IPv6 egress path with lb6_local in front (bpf_lxc.c:108-203):
+    tests/golden/classify_v6_lb.npz composes libref_lbl6 (lib/lb.h's IPv6
+    service step with and without CONNTRACK) and libref_policy's v6 decision"""
+    g = golden("classify_v6_lb.npz")
+    gate, src = (int(x) for x in g["configs"][ci])
+    o = Oracle(ct_proto_gate=gate, ingress_src_identity=src, router_ip=g["router_ip"].tobytes())
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert o.ipcache_update(k, v) == 0
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert o.policy_update(int(ep), k, e) == 0
+    for k, v in zip(g["lb_keys"], g["lb_vals"]):
+        assert o.lb6_update(k, v) == 0
+    t = _tuples(g)
+    v, idt, st, probes = o.classify_v6_lb(t, nthreads=3)
+    np.testing.assert_array_equal(v, g[f"c{ci}_verdict"])
+    np.testing.assert_array_equal(idt, g[f"c{ci}_identity"])
+    np.testing.assert_array_equal(st, g[f"c{ci}_stage"])
+    assert probes == int(g[f"c{ci}_nprobes"].sum())
+    for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
+        rc, raw = o.policy_lookup(int(ep), k)
+        got = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+    np.testing.assert_array_equal(o.metrics(), g[f"c{ci}_metrics"])
+    assert (st == 6).sum() > 0 and (g[f"c{ci}_tdaddr"] != g["t_daddr"]).any()
