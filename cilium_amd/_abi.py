@@ -111,11 +111,19 @@ PROTOS = {
     "cgpu_lb4_lookup": (i32, [vp, vp, vp]),
     "cgpu_lb4_get_next_key": (i32, [vp, vp, vp]),
     "cgpu_lb4_count": (sz, [vp]),
+    "cgpu_lb6_update": (i32, [vp, vp, vp, u64]),
+    "cgpu_lb6_update_batch": (i32, [vp, vp, vp, sz, u64]),
+    "cgpu_lb6_delete": (i32, [vp, vp]),
+    "cgpu_lb6_lookup": (i32, [vp, vp, vp]),
+    "cgpu_lb6_get_next_key": (i32, [vp, vp, vp]),
+    "cgpu_lb6_count": (sz, [vp]),
+    "cgpu_flow_hash6": (u32, [vp, vp, C.c_uint16, C.c_uint16, C.c_uint8]),
     "cgpu_flow_hash": (u32, [u32, u32, C.c_uint16, C.c_uint16, C.c_uint8]),
     "cgpu_commit": (i32, [vp, C.POINTER(u64)]),
     "cgpu_table_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
     "cgpu_classify_v6": (i32, [vp, C.POINTER(TuplesV6), sz, vp, vp, vp, vp]),
+    "cgpu_classify_v6_lb": (i32, [vp, C.POINTER(TuplesV6), vp, vp, sz, vp, vp, vp, vp]),
     "cgpu_classify_v4_lb": (i32, [vp, C.POINTER(TuplesV4), vp, vp, sz, vp, vp, vp, vp]),
     "cgpu_lb4_select": (i32, [vp, i32, C.POINTER(Lb4Tuples), sz, C.POINTER(Lb4Out), vp]),
     "cgpu_prefilter_v4": (i32, [vp, vp, vp, vp, sz, vp, vp]),

@@ -44,6 +44,8 @@ static_assert(sizeof(pol_slot) == 16, "policy slot");
 static_assert(sizeof(set16_slot) == 32, "set16 slot");
 static_assert(sizeof(cgpu_lb4_key) == 8, "lb4_key layout");
 static_assert(sizeof(cgpu_lb4_service) == 12, "lb4_service layout");
+static_assert(sizeof(cgpu_lb6_key) == 20, "lb6_key layout");
+static_assert(sizeof(cgpu_lb6_service) == 24, "lb6_service layout");
 
 namespace {
 
@@ -1182,13 +1184,124 @@ int build_lb(const LbIn &lb, uint32_t lb_max_entries, LbBuild &b)
 	return 0;
 }
 
+/* the lb6 mirror's key: address, dport (network order), then the slave
+ * BIG-endian so a frontend's entries sort by slave number */
+typedef std::array<uint8_t, 20> Lb6K;
+typedef std::vector<std::pair<Lb6K, cgpu_lb6_service>> Lb6In; /* sorted by key */
+
+static inline Lb6K lb6_mkey(const cgpu_lb6_key *k)
+{
+	Lb6K m;
+	memcpy(m.data(), k, 18);
+	m[18] = (uint8_t)(k->slave >> 8);
+	m[19] = (uint8_t)k->slave;
+	return m;
+}
+
+static inline cgpu_lb6_key lb6_unkey(const Lb6K &m)
+{
+	cgpu_lb6_key k;
+	memcpy(&k, m.data(), 18);
+	k.slave = (uint16_t)(m[18] << 8 | m[19]);
+	return k;
+}
+
+struct Lb6Build {
+	std::vector<std::array<uint32_t, 8>> fe, be;
+	std::vector<uint32_t> vip;
+	uint32_t mask = 0, vip_mask = 0;
+};
+
+/* cilium_lb6_services -> frontend hash + dense backend rows (tables.h
+ * lb6_table): the build_lb scheme with 32-byte rows */
+int build_lb6(const Lb6In &lb, uint32_t lb_max_entries, Lb6Build &b)
+{
+	struct Fe {
+		uint32_t a[4], dport, mcount, base, nslaves;
+	};
+	std::vector<Fe> fes;
+	const uint64_t cap = 4ull * lb_max_entries + 65536ull;
+	for (auto it = lb.begin(); it != lb.end();) {
+		auto jt = it;
+		uint32_t mcount = 0, maxs = 0;
+		for (; jt != lb.end() && !memcmp(jt->first.data(), it->first.data(), 18); ++jt) {
+			const uint32_t sl = (uint32_t)jt->first[18] << 8 | jt->first[19];
+			if (sl == 0)
+				mcount = jt->second.count;
+			else
+				maxs = sl; /* ascending */
+		}
+		const uint64_t base = b.be.size();
+		if (base + maxs > cap)
+			return fail(-E2BIG, "lb6 backend rows exceed %llu (sparse slave numbers)",
+				    (unsigned long long)cap);
+		b.be.resize(base + maxs, std::array<uint32_t, 8>{});
+		for (auto kt = it; kt != jt; ++kt) {
+			const uint32_t sl = (uint32_t)kt->first[18] << 8 | kt->first[19];
+			if (!sl)
+				continue;
+			const cgpu_lb6_service &v = kt->second;
+			auto &row = b.be[base + sl - 1];
+			memcpy(row.data(), v.target, 16);
+			row[4] = (uint32_t)v.port | (uint32_t)v.count << 16;
+			row[5] = (uint32_t)v.rev_nat_index | (uint32_t)v.weight << 16;
+			row[6] = 1u;
+		}
+		Fe f{};
+		memcpy(f.a, it->first.data(), 16);
+		uint16_t dp;
+		memcpy(&dp, it->first.data() + 16, 2);
+		f.dport = dp;
+		f.mcount = mcount;
+		f.base = (uint32_t)base;
+		f.nslaves = maxs;
+		fes.push_back(f);
+		it = jt;
+	}
+	uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * fes.size()));
+	for (;;) {
+		b.fe.assign(nb, std::array<uint32_t, 8>{});
+		b.mask = nb - 1;
+		bool ok = true;
+		for (auto &f : fes) {
+			const uint32_t home = lb6_hash(fold6(f.a[0], f.a[1], f.a[2], f.a[3]), f.dport) & b.mask;
+			uint32_t d = 0;
+			while (d < POL_HOP && (b.fe[(home + d) & b.mask][6] & LB_FE_USED))
+				d++;
+			if (d == POL_HOP) {
+				ok = false;
+				break;
+			}
+			auto &sl = b.fe[(home + d) & b.mask];
+			memcpy(sl.data(), f.a, 16);
+			sl[4] = f.dport | f.mcount << 16;
+			sl[5] = f.base;
+			sl[6] = (sl[6] & ~0xFFFFFFu) | f.nslaves | LB_FE_USED;
+			b.fe[home][6] |= 1u << (POL_HOP_SHIFT + d);
+		}
+		if (ok)
+			break;
+		nb *= 2;
+	}
+	if (b.be.empty())
+		b.be.push_back(std::array<uint32_t, 8>{});
+	const uint64_t bits = next_pow2(std::max<uint64_t>(1u << 15, 8ull * fes.size()));
+	b.vip.assign(bits / 32, 0u);
+	b.vip_mask = (uint32_t)(bits - 1);
+	for (auto &f : fes) {
+		const uint32_t k = lb6_vip_bit(fold6(f.a[0], f.a[1], f.a[2], f.a[3])) & b.vip_mask;
+		b.vip[k >> 5] |= 1u << (k & 31u);
+	}
+	return 0;
+}
+
 /* ---------------- device buffers, snapshots (epochs) ----------------
  * Every table group of a snapshot lives in one device buffer; a commit
  * uploads the groups that changed and shares the others with the previous
  * snapshot.  A buffer is freed stream-ordered on the context's retirement
  * stream (hipFreeAsync) once no snapshot references it, and only after that
  * stream has waited for the last launch of every snapshot that used it. */
-enum { G_IPC = 0, G_POL, G_PF, G_EP, G_LB, G_LXC, G_N };
+enum { G_IPC = 0, G_POL, G_PF, G_EP, G_LB, G_LXC, G_LB6, G_N };
 
 struct DevBuf {
 	void *p = nullptr;
@@ -1217,7 +1330,7 @@ struct BuildState {
 	bool pol_ok = false;
 	PolBuild pol;
 	PgBuild pg;
-	uint64_t sum[G_N] = {0, 0, 0, 0, 0, 0};
+	uint64_t sum[G_N] = {};
 };
 
 } // namespace
@@ -1252,6 +1365,7 @@ struct cgpu_ctx {
 	/* cilium_lb4_services, keyed address << 32 | dport << 16 | slave so that
 	 * a frontend's entries are adjacent */
 	std::map<uint64_t, cgpu_lb4_service> lb;
+	std::map<Lb6K, cgpu_lb6_service> lb6;
 	/* per-endpoint lxc_config.h identity (cgpu_lxc_update) */
 	std::map<uint32_t, cgpu_lxc_info> lxcinfo;
 	int64_t pf_revision = 1; /* PreFilter revision (pkg/policy/prefilter.go:283) */
@@ -2319,6 +2433,105 @@ CGPU_EXPORT size_t cgpu_lb4_count(cgpu_ctx *c)
 	return c->lb.size();
 }
 
+static int lb6_put(cgpu_ctx *c, const cgpu_lb6_key *key, const cgpu_lb6_service *val, uint64_t flags)
+{
+	const Lb6K m = lb6_mkey(key);
+	auto it = c->lb6.find(m);
+	if (it == c->lb6.end()) {
+		if (flags == CGPU_EXIST)
+			return fail(-ENOENT, "lb6 key not present");
+		if (c->lb6.size() >= c->cfg.lb_max_entries)
+			return fail(-E2BIG, "lb6 service map full (%u)", c->cfg.lb_max_entries);
+		c->lb6.emplace(m, *val);
+	} else {
+		if (flags == CGPU_NOEXIST)
+			return fail(-EEXIST, "lb6 key exists");
+		it->second = *val;
+	}
+	c->dirty |= 1u << G_LB6;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb6_update(cgpu_ctx *c, const cgpu_lb6_key *key, const cgpu_lb6_service *val,
+				uint64_t flags)
+{
+	if (!c || !key || !val)
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	return lb6_put(c, key, val, flags);
+}
+
+CGPU_EXPORT int cgpu_lb6_update_batch(cgpu_ctx *c, const cgpu_lb6_key *keys,
+				      const cgpu_lb6_service *vals, size_t n, uint64_t flags)
+{
+	if (!c || (n && (!keys || !vals)))
+		return fail(-EINVAL, "null argument");
+	if (int r = check_flags(flags))
+		return r;
+	std::lock_guard<std::mutex> g(c->mu);
+	for (size_t i = 0; i < n; i++)
+		if (int r = lb6_put(c, &keys[i], &vals[i], flags))
+			return r;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb6_delete(cgpu_ctx *c, const cgpu_lb6_key *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	if (!c->lb6.erase(lb6_mkey(key)))
+		return -ENOENT;
+	c->dirty |= 1u << G_LB6;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb6_lookup(cgpu_ctx *c, const cgpu_lb6_key *key, cgpu_lb6_service *out)
+{
+	if (!c || !key || !out)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = c->lb6.find(lb6_mkey(key));
+	if (it == c->lb6.end())
+		return -ENOENT;
+	*out = it->second;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_lb6_get_next_key(cgpu_ctx *c, const cgpu_lb6_key *key, cgpu_lb6_key *next)
+{
+	if (!c || !next)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->mu);
+	auto it = key ? c->lb6.upper_bound(lb6_mkey(key)) : c->lb6.begin();
+	if (it == c->lb6.end())
+		return -ENOENT;
+	*next = lb6_unkey(it->first);
+	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_lb6_count(cgpu_ctx *c)
+{
+	if (!c)
+		return 0;
+	std::lock_guard<std::mutex> g(c->mu);
+	return c->lb6.size();
+}
+
+CGPU_EXPORT uint32_t cgpu_flow_hash6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t sport,
+				     uint16_t dport, uint8_t proto)
+{
+	uint32_t s[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
+	if (saddr16)
+		memcpy(s, saddr16, 16);
+	if (daddr16)
+		memcpy(d, daddr16, 16);
+	return flow_hash(fold6(s[0], s[1], s[2], s[3]), fold6(d[0], d[1], d[2], d[3]), sport, dport, proto);
+}
+
+
 CGPU_EXPORT uint32_t cgpu_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
 				    uint8_t proto)
 {
@@ -2358,6 +2571,7 @@ struct CommitIn {
 	PfIn pf{};
 	std::vector<std::array<uint8_t, 20>> lxc;
 	LbIn lb;
+	Lb6In lb6;
 	std::vector<std::pair<uint32_t, cgpu_lxc_info>> lxcinfo;
 	uint64_t sum_ipc = 0, sum_pol = 0;
 };
@@ -2549,6 +2763,8 @@ static void capture(cgpu_ctx *c, CommitIn &in, const BuildState &b)
 		in.lxc.assign(c->lxc.begin(), c->lxc.end());
 	if (in.dirty & (1u << G_LB))
 		in.lb.assign(c->lb.begin(), c->lb.end());
+	if (in.dirty & (1u << G_LB6))
+		in.lb6.assign(c->lb6.begin(), c->lb6.end());
 	if (in.dirty & (1u << G_LXC))
 		in.lxcinfo.assign(c->lxcinfo.begin(), c->lxcinfo.end());
 	in.sum_ipc = c->sum_ipc;
@@ -2802,6 +3018,27 @@ static int commit_lb(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	return 0;
 }
 
+/* group LB6: cilium_lb6_services frontends + backends */
+static int commit_lb6(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
+{
+	Lb6Build b;
+	if (int r = build_lb6(in.lb6, in.cfg.lb_max_entries, b))
+		return r;
+	Arena ar;
+	const size_t o_f = ar.add(b.fe.data(), b.fe.size() * 32);
+	const size_t o_b = ar.add(b.be.data(), b.be.size() * 32);
+	const size_t o_v = ar.add(b.vip.data(), b.vip.size() * 4);
+	if (int r = upload(c, ar, buf))
+		return r;
+	s.lb6 = lb6_table{at<uint4>(buf, o_f), at<uint4>(buf, o_b), b.mask, (uint32_t)b.be.size(),
+			  at<uint32_t>(buf, o_v), b.vip_mask};
+	uint64_t sum = 0;
+	for (auto &kv : in.lb6)
+		sum += fnv(fnv(31, kv.first.data(), 20), &kv.second, sizeof(kv.second));
+	c->b.sum[G_LB6] = sum;
+	return 0;
+}
+
 /* group LXC: dense per-endpoint lxc identity, 32 B each (absent: verify nothing) */
 static int commit_lxc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 {
@@ -2891,7 +3128,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	}
 	cgpu_snapshot &s = e->snap;
 	int (*const step[G_N])(cgpu_ctx *, CommitIn &, cgpu_snapshot &, DevBufP &) = {
-		commit_ipc, commit_pol, commit_pf, commit_ep, commit_lb, commit_lxc};
+		commit_ipc, commit_pol, commit_pf, commit_ep, commit_lb, commit_lxc, commit_lb6};
 	int rc = 0;
 	for (int k = 0; k < G_N && !rc; k++)
 		if (in.dirty & (1u << k)) {
@@ -3127,6 +3364,35 @@ CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n,
 	HIP_OR_EIO(launch_classify_v6(s, a, (hipStream_t)stream));
 	return 0;
 }
+
+CGPU_EXPORT int cgpu_classify_v6_lb(cgpu_ctx *c, const cgpu_tuples_v6 *t, const uint16_t *sport,
+				    const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+				    uint8_t *stage, void *stream)
+{
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
+		return r;
+	const cgpu_snapshot &s = P.snap();
+	uint64_t *delta = P.delta, *pk = P.pk;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
+			 !t->ep || !verdict || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (((uintptr_t)t->saddr | (uintptr_t)t->daddr) & 15)
+		return fail(-EINVAL, "v6 address columns must be 16-byte aligned");
+	if (n && !hash && !sport)
+		return fail(-EINVAL, "either a hash or an sport column is needed");
+	if (!n)
+		return 0;
+	classify_v6_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
+			   verdict, identity, stage, delta, (uint64_t)n, pk};
+	a.lb = 1;
+	a.sport = sport;
+	a.hash = hash;
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_classify_v6(s, a, (hipStream_t)stream));
+	return 0;
+}
+
 
 static int frames_check(cgpu_ctx *c, const cgpu_frames *f, size_t n)
 {

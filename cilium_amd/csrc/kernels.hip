@@ -415,6 +415,115 @@ __device__ __forceinline__ bool lb_service(const cgpu_snapshot &s, uint32_t addr
 	return false;
 }
 
+/* map_lookup_elem(&cilium_lb6_services, {addr, dport, slave}) (tables.h
+ * lb6_table): tg = target, val = {port | count << 16, rev_nat | weight << 16,
+ * present, 0}; slave 0 carries only the master's count.  f = fold6(addr). */
+__device__ __forceinline__ bool lb6_get(const lb6_table &t, uint4 addr, uint32_t f, uint32_t dport,
+					uint32_t slave, uint4 &tg, uint4 &val)
+{
+	const uint32_t home = lb6_hash(f, dport) & t.fe_mask;
+	uint4 m = t.fe[2u * home + 1u];
+	uint32_t hop = m.z >> POL_HOP_SHIFT;
+	bool found = false;
+	if (hop & 1u) {
+		const uint4 a = t.fe[2u * home];
+		found = a.x == addr.x && a.y == addr.y && a.z == addr.z && a.w == addr.w && (m.x & 0xFFFFu) == dport;
+	}
+	hop &= ~1u;
+	while (hop && !found) {
+		const uint32_t k = (home + (uint32_t)__builtin_ctz(hop)) & t.fe_mask;
+		hop &= hop - 1u;
+		const uint4 a = t.fe[2u * k], mk = t.fe[2u * k + 1u];
+		if (a.x == addr.x && a.y == addr.y && a.z == addr.z && a.w == addr.w && (mk.x & 0xFFFFu) == dport) {
+			m = mk;
+			found = true;
+		}
+	}
+	if (!found || !(m.z & LB_FE_USED))
+		return false;
+	if (slave == 0) {
+		tg = make_uint4(0, 0, 0, 0);
+		val = make_uint4(m.x & 0xFFFF0000u, 0, 1, 0);
+		return true;
+	}
+	if (slave > (m.z & 0xFFFFu))
+		return false;
+	const uint32_t r = m.y + slave - 1u;
+	tg = t.be[2u * r];
+	val = t.be[2u * r + 1u];
+	return val.z != 0;
+}
+
+/* lb6_lookup_service (lb.h:351-380): the L4 key if its count is nonzero,
+ * else *kd = 0 and the L3 key */
+__device__ __forceinline__ bool lb6_service(const cgpu_snapshot &s, uint4 addr, uint32_t f, uint32_t *kd,
+					    uint32_t slave, uint4 &tg, uint4 &val)
+{
+	if ((s.lb_flags & CGPU_LB_L4) && *kd) {
+		if (lb6_get(s.lb6, addr, f, *kd, slave, tg, val) && (val.x >> 16))
+			return true;
+		*kd = 0;
+	}
+	if (s.lb_flags & CGPU_LB_L3)
+		if (lb6_get(s.lb6, addr, f, *kd, slave, tg, val) && (val.x >> 16))
+			return true;
+	return false;
+}
+
+struct lb6_res {
+	int32_t ret; /* 0 not load-balanced, CGPU_LB_XLATED, DROP_NO_SERVICE */
+	uint4 tdaddr;
+	uint32_t dport;
+};
+
+/*
+ * The service step of ipv6_l3_from_lxc (bpf_lxc.c:117-139) with an empty
+ * conntrack table: lb6_extract_key (lb.h:334-349), lb6_lookup_service,
+ * lb6_local (lb.h:426-483).  Raw (network-order) address words in and out;
+ * same decisions as oracle/cgpu_oracle.c lb6_one, which the golden vectors
+ * of the reference pin.  No loopback case on IPv6.
+ */
+__device__ __forceinline__ lb6_res lb6_one(const cgpu_snapshot &s, uint4 da, uint32_t dp, uint32_t proto,
+					   uint32_t hash)
+{
+	lb6_res r{0, da, dp};
+	uint32_t kd = 0;
+	if (s.lb_flags & CGPU_LB_L4) { /* extract_l4_port (lb.h:191-215) */
+		if (proto == 6u || proto == 17u)
+			kd = dp;
+		else if (proto != 1u && proto != 58u)
+			return r;
+	}
+	const uint32_t f = fold6(da.x, da.y, da.z, da.w);
+	/* no frontend has this address (tables.h lb6_table.vip): every key misses */
+	const uint32_t vb = lb6_vip_bit(f) & s.lb6.vip_mask;
+	if (!((s.lb6.vip[vb >> 5] >> (vb & 31u)) & 1u))
+		return r;
+	uint4 tg, val;
+	if (!lb6_service(s, da, f, &kd, 0, tg, val))
+		return r;
+	if (s.ct_proto_gate && proto != 58u && proto != 6u && proto != 17u) {
+		/* lb6_local's CT_SERVICE ct_lookup6: DROP_CT_UNKNOWN_PROTO ->
+		 * DROP_NO_SERVICE (conntrack.h:376-378, lb.h:436-456) */
+		r.ret = DROP_NO_SERVICE;
+		return r;
+	}
+	uint32_t slave = hash % (val.x >> 16) + 1u; /* lb6_select_slave, lb.h:124-156 */
+	if (!lb6_get(s.lb6, da, f, kd, slave, tg, val)) { /* lb6_lookup_slave, lb.h:382-396 */
+		/* lb.h:462-469: the key keeps the slave just tried */
+		if (!lb6_service(s, da, f, &kd, slave, tg, val)) {
+			r.ret = DROP_NO_SERVICE;
+			return r;
+		}
+	}
+	r.ret = CGPU_LB_XLATED;
+	r.tdaddr = tg; /* tuple->daddr = svc->target (lb.h:475) */
+	const uint32_t port = val.x & 0xFFFFu;
+	if ((s.lb_flags & CGPU_LB_L4) && port && kd != port && (proto == 6u || proto == 17u))
+		r.dport = port; /* lb6_xlate (lb.h:410-420); ct_lookup6 reloads it */
+	return r;
+}
+
 struct lb_res {
 	int32_t ret;
 	uint32_t saddr, daddr, tdaddr, dport, rev_nat, slave, probes;
@@ -833,6 +942,24 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		 * tuple.daddr afterwards and policy sees the rewritten dport */
 		bool lbdrop = false;
 		uint32_t eda = 0;
+		uint4 lda6{}; /* v6: the (translated) raw daddr */
+		if (V6 && egress) {
+			lda6 = static_cast<const uint4 *>(a.daddr)[i];
+			if (a.lb) {
+				const uint4 sa6 = static_cast<const uint4 *>(a.saddr)[i];
+				const uint32_t h = a.hash ? a.hash[i]
+							  : flow_hash(fold6(sa6.x, sa6.y, sa6.z, sa6.w),
+								      fold6(lda6.x, lda6.y, lda6.z, lda6.w), a.sport[i],
+								      dport, proto);
+				const lb6_res r = lb6_one(s, lda6, dport, proto, h);
+				if (r.ret == DROP_NO_SERVICE) {
+					lbdrop = true;
+				} else {
+					lda6 = r.tdaddr;
+					dport = r.dport;
+				}
+			}
+		}
 		if (!V6) {
 			eda = static_cast<const uint32_t *>(a.daddr)[i];
 			if (a.lb && egress) {
@@ -866,7 +993,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 			uint32_t sa4 = 0;
 			if (V6) {
 				if (egress)
-					da6 = static_cast<const uint4 *>(a.daddr)[i];
+					da6 = lda6;
 				else
 					sa6 = static_cast<const uint4 *>(a.saddr)[i];
 			} else if (!egress) {
@@ -1042,7 +1169,6 @@ __device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *blo
 template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false>
 __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
 {
-	static_assert(!(LB && V6), "the service step is IPv4");
 	/* per-tuple flag word */
 	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u, F_LBDROP = 32u;
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
@@ -1152,20 +1278,38 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 					da[u] = V6 ? 0u : static_cast<const uint32_t *>(a.daddr)[i];
 				}
 			}
+			uint32_t lbf[Q];
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				lbf[u] = 0;
 			if (V6) {
 				/* the looked-up address only: daddr egress, saddr ingress */
 #pragma unroll
 				for (int u = 0; u < Q; u++) {
 					const uint64_t i = i0 + u < a.n ? i0 + u : i0;
-					ad6[u] = v6_host_words(
-						ld_x4<NTL>(static_cast<const uint4 *>((fl[u] & 1u) ? a.daddr : a.saddr) + i));
+					uint4 raw = ld_x4<NTL>(static_cast<const uint4 *>((fl[u] & 1u) ? a.daddr : a.saddr) + i);
+					if (LB && (fl[u] & 1u) && i0 + u < a.n) {
+						/* egress service step first (bpf_lxc.c:117-149) */
+						uint32_t h;
+						if (a.hash) {
+							h = a.hash[i];
+						} else {
+							const uint4 sr = ld_x4<NTL>(static_cast<const uint4 *>(a.saddr) + i);
+							h = flow_hash(fold6(sr.x, sr.y, sr.z, sr.w), fold6(raw.x, raw.y, raw.z, raw.w),
+								      a.sport[i], dport[u], proto[u]);
+						}
+						const lb6_res r = lb6_one(s, raw, dport[u], proto[u], h);
+						if (r.ret == DROP_NO_SERVICE) {
+							lbf[u] = F_LBDROP;
+						} else {
+							raw = r.tdaddr;
+							dport[u] = r.dport;
+						}
+					}
+					ad6[u] = v6_host_words(raw);
 				}
 			}
-			uint32_t lbf[Q];
-#pragma unroll
-			for (int u = 0; u < Q; u++)
-				lbf[u] = 0;
-			if (LB) {
+			if (LB && !V6) {
 				/* egress service step first (bpf_lxc.c:444-469): the
 				 * translated tuple.daddr and dport feed ipcache / policy */
 				uint32_t hh[QA], sp[QA];
@@ -1223,7 +1367,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 			bool act[Q];
 #pragma unroll
 			for (int u = 0; u < Q; u++)
-				act[u] = (fw[u] & (F_OK | F_GATED)) == F_OK;
+				act[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK;
 			v6_lookup_q<Q>(s.ipc6, ldict, lmasks, nm, ad6, act, e);
 		} else {
 			/* v4: the /16's inline node (x16), then the compressed LPM */
@@ -2289,7 +2433,7 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 	}
 	if (var == 8 && a.pk && x4_aligned(a)) {
 		if (V6)
-			return launch_x4<false, true>(s, a, st);
+			return a.lb ? launch_x4<true, true>(s, a, st) : launch_x4<false, true>(s, a, st);
 		return a.lb ? launch_x4<true, false>(s, a, st) : launch_x4<false, false>(s, a, st);
 	}
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
@@ -2333,8 +2477,8 @@ hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x,
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)
 {
 	return launch_classify<1>(s, cls_args{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len,
-					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, x.pk, 0, nullptr,
-					      nullptr}, st);
+					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, x.pk, x.lb, x.sport,
+					      x.hash}, st);
 }
 
 hipError_t launch_lb4(const cgpu_snapshot &s, const lb4_args &a, hipStream_t st)

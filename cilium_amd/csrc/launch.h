@@ -40,7 +40,12 @@ struct classify_v6_args {
 	uint32_t *identity;
 	uint8_t *stage;
 	uint64_t *delta;
-	uint64_t n;	uint64_t *pk; /* packed cold-slot accumulator (per stream) */
+	uint64_t n;
+	uint64_t *pk; /* packed cold-slot accumulator (per stream) */
+	/* egress service step first (cgpu_classify_v6_lb) */
+	int lb;
+	const uint16_t *sport;
+	const uint32_t *hash; /* NULL: flow_hash(fold6(saddr), fold6(daddr), sport, dport, proto) */
 };
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &a, hipStream_t st);

@@ -310,6 +310,36 @@ static inline __host__ __device__ uint32_t flow_hash(uint32_t saddr, uint32_t da
 	return h;
 }
 
+/* ---- IPv6 service map (cilium_lb6_services, bpf/lib/lb.h:46-52) ----
+ * The lb4 scheme with 32-byte rows: frontend slot = 2 x uint4
+ *   {address (raw words)}, {dport | master_count << 16, base, nslaves | LB_FE_USED | hop << 24, 0}
+ * backend row = 2 x uint4 {target (raw words)}, {port | count << 16, rev_nat | weight << 16, present, 0}.
+ * A service lookup is one 32-byte gather (the home slot), a backend one more. */
+typedef struct lb6_table {
+	const uint4 *fe; /* (fe_mask + 1) x 2 */
+	const uint4 *be; /* n_be x 2 */
+	uint32_t fe_mask;
+	uint32_t n_be;
+	const uint32_t *vip; /* presence bitmap over frontend addresses (lb6_vip_bit) */
+	uint32_t vip_mask;
+} lb6_table;
+
+/* 16 address bytes (as four little-endian words) -> 32 bits */
+static inline __host__ __device__ uint32_t fold6(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
+{
+	return fmix32(w0 ^ fmix32(w1 ^ fmix32(w2 ^ fmix32(w3 ^ 0x6B43A9B5u))));
+}
+
+static inline __host__ __device__ uint32_t lb6_hash(uint32_t f, uint32_t dport)
+{
+	return mix32(f, dport ^ 0x6d5e0000u);
+}
+
+static inline __host__ __device__ uint32_t lb6_vip_bit(uint32_t f)
+{
+	return mix32(f, 0x2f6b1e17u);
+}
+
 /* ---- IPv6 any-match cover (XDP prefilter v6) ----
  * The prefilter only asks "does ANY deny prefix cover saddr" (bpf_xdp.c:
  * 142-152: both the dyn LPM and the fix /128 hash lead to XDP_DROP), so the
@@ -382,6 +412,7 @@ typedef struct cgpu_snapshot {
 	uint32_t hot_slots;      /* counter slots [0, hot_slots) may live in LDS */
 	uint32_t cold_hi;        /* counter slots >= cold_hi are unassigned */
 	lb_table lb;
+	lb6_table lb6;
 	uint32_t lb_flags;       /* CGPU_LB_L3 | CGPU_LB_L4 */
 	uint32_t ipv4_loopback;  /* IPV4_LOOPBACK, network order */
 	/* per-endpoint lxc_config.h identity (cgpu_lxc_info, 32 B = 2 x uint4

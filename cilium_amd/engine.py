@@ -231,6 +231,38 @@ class Engine:
     def lb4_count(self) -> int:
         return self.L.cgpu_lb4_count(self.h)
 
+    # --- cilium_lb6_services ---
+    def lb6_update(self, key, val, flags=BPF_ANY) -> int:
+        return self.L.cgpu_lb6_update(self.h, _buf(key), _buf(val), flags)
+
+    def lb6_update_batch(self, keys, vals, flags=BPF_ANY) -> int:
+        k = np.ascontiguousarray(keys, L.LB6_KEY)
+        v = np.ascontiguousarray(vals, L.LB6_SERVICE)
+        assert len(k) == len(v)
+        return self.L.cgpu_lb6_update_batch(self.h, k.ctypes.data, v.ctypes.data, len(k), flags)
+
+    def lb6_delete(self, key) -> int:
+        return self.L.cgpu_lb6_delete(self.h, _buf(key))
+
+    def lb6_lookup(self, key):
+        out = C.create_string_buffer(24)
+        rc = self.L.cgpu_lb6_lookup(self.h, _buf(key), out)
+        return rc, (np.frombuffer(out.raw, L.LB6_SERVICE)[0] if rc == 0 else None)
+
+    def lb6_keys(self):
+        keys, prev = [], None
+        out = C.create_string_buffer(20)
+        while self.L.cgpu_lb6_get_next_key(self.h, prev, out) == 0:
+            prev = out.raw
+            keys.append(np.frombuffer(prev, L.LB6_KEY)[0])
+        return keys
+
+    def lb6_count(self) -> int:
+        return self.L.cgpu_lb6_count(self.h)
+
+    def flow_hash6(self, saddr16, daddr16, sport, dport, proto) -> int:
+        return self.L.cgpu_flow_hash6(bytes(saddr16), bytes(daddr16), sport, dport, proto)
+
     # --- conntrack map cilium_ct4_global ---
     def ct4_update(self, key, val, flags=BPF_ANY) -> int:
         return self.L.cgpu_ct4_update(self.h, _buf(key), _buf(val), flags)
@@ -405,6 +437,24 @@ class Engine:
         check(self.L.cgpu_classify_v6(self.h, C.byref(tv), n, _ptr(out["verdict"]),
                                       _ptr(out["identity"]), _ptr(out.get("stage")),
                                       _stream(stream)), "cgpu_classify_v6")
+        return out
+
+    def classify_v6_lb(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """classify_v6 with the egress service step of ipv6_l3_from_lxc first;
+        t additionally holds "hash" (int32 view of skb->hash) or "sport"."""
+        import torch
+        n = t["flags"].numel()
+        dev = t["flags"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
+        tv = TuplesV6(*[t[k].data_ptr() for k in
+                        ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")])
+        check(self.L.cgpu_classify_v6_lb(self.h, C.byref(tv), _ptr(t.get("sport")),
+                                         _ptr(t.get("hash")), n, _ptr(out["verdict"]),
+                                         _ptr(out["identity"]), _ptr(out.get("stage")),
+                                         _stream(stream)), "cgpu_classify_v6_lb")
         return out
 
     def prefilter_v4(self, saddr, daddr, flags, out=None, stream=None):

@@ -33,6 +33,30 @@ def flowhash_np(saddr, daddr, sport, dport, proto) -> np.ndarray:
     return h.astype(np.uint32)
 
 
+def _fmix_np(h):
+    h = h & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return h
+
+
+def fold6_np(a16) -> np.ndarray:
+    """tables.h fold6: (n, 16) uint8 addresses -> u32 (four LE words mixed)"""
+    w = np.ascontiguousarray(a16, np.uint8).view("<u4").reshape(-1, 4).astype(np.uint64)
+    h = _fmix_np(w[:, 3] ^ np.uint64(0x6B43A9B5))
+    h = _fmix_np(w[:, 2] ^ h)
+    h = _fmix_np(w[:, 1] ^ h)
+    return _fmix_np(w[:, 0] ^ h).astype(np.uint32)
+
+
+def flowhash6_np(saddr16, daddr16, sport, dport, proto) -> np.ndarray:
+    """cgpu_flow_hash6: flowhash_np over the folded IPv6 addresses"""
+    return flowhash_np(fold6_np(saddr16), fold6_np(daddr16), sport, dport, proto)
+
+
 def shard_of(t: dict, world: int) -> np.ndarray:
     """Owning rank of every tuple: flowhash(5-tuple) % world."""
     sport = t.get("sport", np.zeros_like(t["dport"]))

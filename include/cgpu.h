@@ -294,11 +294,44 @@ int cgpu_lb4_lookup(cgpu_ctx *ctx, const cgpu_lb4_key *key, cgpu_lb4_service *va
 int cgpu_lb4_get_next_key(cgpu_ctx *ctx, const cgpu_lb4_key *key, cgpu_lb4_key *next_out);
 size_t cgpu_lb4_count(cgpu_ctx *ctx);
 
+/* struct lb6_key, bpf/lib/common.h:408-412 (packed, 20 B): address and dport
+ * in network order, slave host order */
+typedef struct cgpu_lb6_key {
+	uint8_t address[16];
+	uint16_t dport;
+	uint16_t slave;
+} cgpu_lb6_key;
+
+/* struct lb6_service, bpf/lib/common.h:414-420 (packed, 24 B) */
+typedef struct cgpu_lb6_service {
+	uint8_t target[16];
+	uint16_t port;
+	uint16_t count;
+	uint16_t rev_nat_index;
+	uint16_t weight;
+} cgpu_lb6_service;
+
+/* cilium_lb6_services (lb.h:46-52), the map lbmap writes for IPv6
+ * frontends (pkg/maps/lbmap/ipv6.go); same semantics as the lb4 calls.
+ * Shares lb_max_entries with the lb4 map as a per-map capacity. */
+int cgpu_lb6_update(cgpu_ctx *ctx, const cgpu_lb6_key *key, const cgpu_lb6_service *val,
+		    uint64_t flags);
+int cgpu_lb6_update_batch(cgpu_ctx *ctx, const cgpu_lb6_key *keys, const cgpu_lb6_service *vals,
+			  size_t n, uint64_t flags);
+int cgpu_lb6_delete(cgpu_ctx *ctx, const cgpu_lb6_key *key);
+int cgpu_lb6_lookup(cgpu_ctx *ctx, const cgpu_lb6_key *key, cgpu_lb6_service *val_out);
+int cgpu_lb6_get_next_key(cgpu_ctx *ctx, const cgpu_lb6_key *key, cgpu_lb6_key *next_out);
+size_t cgpu_lb6_count(cgpu_ctx *ctx);
+
 /* The flow hash the batch entry points use when no hash column is given
  * (skb->hash comes from the kernel's flow dissector, which the reference
  * does not contain: SURVEY §8c).  Over the stored (network-order) fields. */
 uint32_t cgpu_flow_hash(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
 			uint8_t proto);
+/* IPv6: cgpu_flow_hash over the two addresses folded to 32 bits each
+ * (tables.h fold6: the 16 bytes as four little-endian words, murmur3-mixed) */
+uint32_t cgpu_flow_hash6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t sport,
+			 uint16_t dport, uint8_t proto);
 
 /* ------------------------------------------------------------------ */
 /* per-endpoint identity of the endpoint program (lxc_config.h)         */
@@ -408,6 +441,20 @@ int cgpu_classify_v6(cgpu_ctx *ctx, const cgpu_tuples_v6 *t, size_t n, int32_t *
  * given.
  */
 int cgpu_classify_v4_lb(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, const uint16_t *sport,
+			const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+			uint8_t *stage, void *stream);
+
+/*
+ * cgpu_classify_v6 with the egress service step of ipv6_l3_from_lxc in front
+ * (bpf_lxc.c:108-139): lb6_extract_key, lb6_lookup_service and lb6_local
+ * (lb.h:334-483) with an empty conntrack table (CT_NEW); ipcache then
+ * resolves the translated tuple->daddr and policy sees the dport ct_lookup6
+ * reloads from the rewritten packet.  IPv6 has no loopback case.  A
+ * DROP_NO_SERVICE (-158) ends the tuple: identity 0, stage 6, metrics reason
+ * 158 egress.  hash: skb->hash per tuple or NULL for cgpu_flow_hash6 (then
+ * sport is required).
+ */
+int cgpu_classify_v6_lb(cgpu_ctx *ctx, const cgpu_tuples_v6 *t, const uint16_t *sport,
 			const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
 			uint8_t *stage, void *stream);
 

@@ -202,3 +202,104 @@ def test_lb_update_delete_sequences(torch_cuda, cfg_lb):
             np.testing.assert_array_equal(out[k], ref[k], err_msg=f"round {rnd} {k}")
         assert (ref["ret"] == L.DROP_NO_SERVICE).sum() > 0
     e.close()
+
+
+@pytest.mark.parametrize("variant", [3, 8])
+@pytest.mark.parametrize("ci", range(2))
+def test_classify_v6_lb_golden(torch_cuda, golden, ci, variant, monkeypatch):
+    """cgpu_classify_v6_lb against the reference's IPv6 service step
+    (lib/lb.h lb6_local, CT and no-CT builds) composed with its v6 decision
+    (tests/golden/classify_v6_lb.npz), hash injected; on the one-tuple-per-lane
+    kernel (3) and the x4 schedule (8, the default)."""
+    torch = torch_cuda
+    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    g = golden("classify_v6_lb.npz")
+    gate, src = (int(x) for x in g["configs"][ci])
+    e = _engine(ct_proto_gate=gate, ingress_src_identity=src, ipv6_router_ip=g["router_ip"].tobytes())
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert e.ipcache_update(k, v) == 0
+    for k, en, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert e.policy_update(int(ep), k, en) == 0
+    assert e.lb6_update_batch(g["lb_keys"], g["lb_vals"]) == 0
+    assert e.lb6_count() == len({bytes(k) for k in g["lb_keys"]})
+    e.commit()
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    out = e.classify_v6_lb(synth.to_device(t))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["verdict"].cpu().numpy(), g[f"c{ci}_verdict"])
+    np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32), g[f"c{ci}_identity"])
+    np.testing.assert_array_equal(out["stage"].cpu().numpy(), g[f"c{ci}_stage"])
+    for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
+        rc, got = e.policy_lookup(int(ep), k)
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+    np.testing.assert_array_equal(e.metrics(), g[f"c{ci}_metrics"])
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def cfg_lb6():
+    T = synth.make_tables6(n_prefixes=20_000, n_identities=500, n_endpoints=3, keys_per_ep=6000)
+    S = synth.make_services6(T, 20_000)
+    t = synth.add_service_traffic6(synth.make_tuples6(T, 1 << 19), S)
+    return T, S, t
+
+
+@pytest.mark.parametrize("with_hash", [True, False])
+def test_classify_v6_lb_scale_vs_oracle(torch_cuda, cfg_lb6, with_hash):
+    """20k IPv6 services (~70k map entries) + 20k v6 ipcache prefixes, 512k
+    tuples: GPU == restatement, with the hash column and with the in-kernel
+    cgpu_flow_hash6 (sport)."""
+    from oracle import Oracle
+    torch = torch_cuda
+    T, S, t = cfg_lb6
+    if not with_hash:
+        t = {k: v for k, v in t.items() if k != "hash"}
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_services6(o, S)
+    v0, i0, s0, _ = o.classify_v6_lb(t, nthreads=8)
+    e = _engine(**T.engine_config(), lb_max_entries=len(S.keys))
+    synth.load_engine(e, T)
+    synth.load_services6(e, S)
+    e.commit()
+    out = e.classify_v6_lb(synth.to_device(t))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["verdict"].cpu().numpy(), v0)
+    np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
+    np.testing.assert_array_equal(out["stage"].cpu().numpy(), s0)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    eg = (t["flags"] & 1) == 1
+    svc = eg & (t["daddr"][:, :4] == np.array([0xFD, 0, 0, 0x96], np.uint8)).all(1)
+    assert svc.sum() > 10_000 and (s0[svc] != 6).all()  # well-formed services never drop
+    e.close()
+
+
+def test_lb6_map_ops(torch_cuda):
+    """cilium_lb6_services map semantics through the ABI: NOEXIST / EXIST,
+    delete, lookup, GetNextKey over every key, a re-commit after deletes"""
+    from cilium_amd.engine import BPF_EXIST, BPF_NOEXIST
+    e = _engine()
+    k = np.zeros((), L.LB6_KEY)
+    k["address"][:] = np.arange(16, dtype=np.uint8)
+    k["dport"] = L.htons(80)
+    v = np.zeros((), L.LB6_SERVICE)
+    v["count"] = 1
+    assert e.lb6_update(k, v, BPF_EXIST) == -2           # -ENOENT
+    assert e.lb6_update(k, v, BPF_NOEXIST) == 0
+    assert e.lb6_update(k, v, BPF_NOEXIST) == -17        # -EEXIST
+    ks = []
+    for sl in (1, 2, 300):
+        kk = k.copy()
+        kk["slave"] = sl
+        vv = v.copy()
+        vv["target"][:] = 7
+        assert e.lb6_update(kk, vv) == 0
+        ks.append(kk)
+    assert e.lb6_count() == 4
+    assert [int(x["slave"]) for x in e.lb6_keys()] == [0, 1, 2, 300]
+    rc, got = e.lb6_lookup(ks[2])
+    assert rc == 0 and bytes(got["target"]) == bytes([7] * 16)
+    assert e.lb6_delete(ks[1]) == 0 and e.lb6_delete(ks[1]) == -2
+    e.commit()
+    assert e.lb6_count() == 3
+    e.close()

@@ -136,3 +136,22 @@ def test_classify_v6_lb_vs_reference(golden, ci):
         assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
     np.testing.assert_array_equal(o.metrics(), g[f"c{ci}_metrics"])
     assert (st == 6).sum() > 0 and (g[f"c{ci}_tdaddr"] != g["t_daddr"]).any()
+
+
+def test_flow_hash6_three_ways():
+    """cgpu_flow_hash6 (the library, host side), or_flow_hash6 (restatement)
+    and shard.flowhash6_np (sharder / synthetic traffic) agree"""
+    from cilium_amd.engine import Engine
+    from cilium_amd.shard import flowhash6_np
+    rng = np.random.default_rng(6)
+    n = 300
+    s16 = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    d16 = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    sp, dp = rng.integers(0, 65536, (2, n)).astype(np.uint16)
+    pr = rng.integers(0, 256, n).astype(np.uint8)
+    exp = flowhash6_np(s16, d16, sp, dp, pr)
+    e, o = Engine(device=-1), Oracle()
+    for i in range(n):
+        args = (s16[i].tobytes(), d16[i].tobytes(), int(sp[i]), int(dp[i]), int(pr[i]))
+        assert e.flow_hash6(*args) == o.flow_hash6(*args) == int(exp[i])
+    e.close()

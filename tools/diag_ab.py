@@ -41,8 +41,9 @@ def load(name):
     path = _abi.LIB_PATH if name == "product" else os.path.join(DIAG, f"libcgpu_{name}.so")
     L = C.CDLL(path)
     for fn, (res, args) in _abi.PROTOS.items():
-        f = getattr(L, fn)
-        f.restype, f.argtypes = res, args
+        f = getattr(L, fn, None)  # a diag build may predate newer entry points
+        if f is not None:
+            f.restype, f.argtypes = res, args
     _abi._lib = L
 
 
