@@ -820,6 +820,7 @@ struct cls_args {
 	int lb;       /* v4: egress service step first (cgpu_classify_v4_lb) */
 	const uint16_t *sport;
 	const uint32_t *hash;
+	uint32_t cc_n; /* k_classify_x4: cold-slot cache entries in LDS (power of 2, or 0) */
 };
 
 /* The identity resolution and the three-probe policy cascade for one tuple
@@ -1063,6 +1064,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  * two-word path into delta directly.  Each stream has its own pk buffer
  * (host.cpp), so concurrent calls on one context never share the bound. */
 #define PKC_SHIFT 37
+#define CC_PROBE 4 /* linear probes of the LDS cold-slot cache */
 #define PKC_BYTES_MASK ((1ull << PKC_SHIFT) - 1ull)
 #define PKC_MAX_LEN (1u << 11)
 #define PKC_CHUNK (1ull << 26)
@@ -1191,8 +1193,18 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	const uint32_t nbw = V6 && s.ipc6.root ? s.ipc6.bloom_mask + 1u : 0u;
 	const uint32_t nm = V6 ? min(s.ipc6.n_masks, V6_LDS_MASK_ROWS) : 0u;
 	uint4 *lmasks = reinterpret_cast<uint4 *>(ldict + nbw); /* nbw: a multiple of 64 */
+	/* cold-slot cache (x4_lds_layout): cc_n u64 packed counts, then cc_n u32
+	 * tags (slot + 1, 0 = free) */
+	const uint32_t lds_words = V6 ? nbw + 4u * nm : s.ipc4c.n_dict;
+	uint64_t *ccv = lctr + s.hot_slots + ((lds_words + 1u) >> 1);
+	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + a.cc_n);
+	const uint32_t ccm = a.cc_n - 1u;
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
+	for (uint32_t k = threadIdx.x; k < a.cc_n; k += NT) {
+		ccv[k] = 0;
+		cck[k] = 0;
+	}
 	if (threadIdx.x < 16)
 		lmet[threadIdx.x] = 0;
 	if (V6) {
@@ -1549,8 +1561,32 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 						  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
 				} else {
 #ifndef CGPU_DIAG_NO_COLD /* timing-only tool build (tools/diag_ab.py): counters wrong */
-					atomicAdd((unsigned long long *)&pk[c],
-						  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
+					/* the workgroup's cold-slot cache: a global atomic
+					 * executes at the memory side (one 64-B request each,
+					 * MI355X_MICROARCH.md), so hits aggregate in LDS and
+					 * each touched slot costs one atomic at the end; a
+					 * slot that finds no free entry in CC_PROBE goes global */
+					bool done = false;
+					if (a.cc_n) {
+						uint32_t j = (c * 0x9E3779B1u) >> 16;
+#pragma unroll
+						for (int p = 0; p < CC_PROBE && !done; p++, j++) {
+							j &= ccm;
+							uint32_t t = cck[j];
+							if (t == 0u) {
+								const uint32_t o = atomicCAS(&cck[j], 0u, c + 1u);
+								t = o == 0u ? c + 1u : o;
+							}
+							if (t == c + 1u) {
+								atomicAdd((unsigned long long *)&ccv[j],
+									  (1ull << PK_SHIFT) | (unsigned long long)len[u]);
+								done = true;
+							}
+						}
+					}
+					if (!done)
+						atomicAdd((unsigned long long *)&pk[c],
+							  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
 #endif
 				}
 				v[u] = st[u] == 2 ? 0 : (int32_t)(z[u] >> 16);
@@ -1627,6 +1663,13 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		const uint64_t x = lctr[k];
 		if (x)
 			atomicAdd((unsigned long long *)&pk[k],
+				  ((x >> PK_SHIFT) << PKC_SHIFT) | (x & PK_BYTES_MASK));
+	}
+	for (uint32_t k = threadIdx.x; k < a.cc_n; k += NT) {
+		const uint32_t t = cck[k];
+		const uint64_t x = ccv[k];
+		if (t && x)
+			atomicAdd((unsigned long long *)&pk[t - 1u],
 				  ((x >> PK_SHIFT) << PKC_SHIFT) | (x & PK_BYTES_MASK));
 	}
 }
@@ -2366,6 +2409,10 @@ static unsigned resident_blocks(const void *kern, int NT, size_t lds)
 /* x4 schedule: one persistent-size grid (every workgroup resident, so the
  * per-workgroup LDS counter flush is paid once per resident workgroup) per
  * launch of <= PKC_CHUNK tuples, then the unpack of pk into delta. */
+/* dynamic LDS of a k_classify_x4 workgroup: 160 KiB per CU less the static
+ * metrics block and some slack */
+#define X4_LDS_BUDGET (156u * 1024u)
+
 template <bool LB, bool V6>
 static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream_t st)
 {
@@ -2379,6 +2426,15 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 				   : 0u;
 	else
 		lds += (size_t)s.ipc4c.n_dict * 4u;
+	lds = (lds + 7u) & ~(size_t)7u;
+	/* the cold-slot cache takes the LDS one workgroup per CU leaves free
+	 * (the resident grid runs one 1024-thread workgroup per CU) */
+	uint32_t cc_n = 0;
+	if (!getenv("CGPU_NO_CCACHE"))
+		for (uint32_t n = 1u << 14; n >= 512u && !cc_n; n >>= 1)
+			if (lds + (size_t)n * 12u <= X4_LDS_BUDGET)
+				cc_n = n;
+	lds += (size_t)cc_n * 12u;
 #ifdef CGPU_DIAG_LDS_PAD /* timing-only: fewer resident workgroups per CU */
 	lds += CGPU_DIAG_LDS_PAD;
 #endif
@@ -2389,6 +2445,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
 	for (uint64_t off = 0; off < a.n; off += chunk) {
 		cls_args c = a;
+		c.cc_n = cc_n;
 		const uint64_t m = std::min<uint64_t>(a.n - off, chunk);
 		c.n = m;
 		c.verdict += off;
