@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--config", default="gpu", choices=sorted(WORKLOADS))
     ap.add_argument("--tuples", type=int, default=0, help="tuples per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hot-slots", type=int, default=0,
+                    help="cgpu_config.hot_counter_slots (LDS counter slots; 0 = library default)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/*), if present")
@@ -185,6 +187,8 @@ def main():
             f"{', %d service-map entries' % len(S.keys) if S is not None else ''}) "
             f"+ {n} tuples in {time.time() - t0:.1f}s")
         ecfg = T.engine_config()
+        if args.hot_slots:
+            ecfg["hot_counter_slots"] = args.hot_slots
         if S is not None:
             ecfg["lb_max_entries"] = len(S.keys)
         e = Engine(device=local, **ecfg)
