@@ -1514,7 +1514,7 @@ CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
 	c->prefilter_fix4 = c->prefilter_dyn4 = 1; /* bpf/filter_config.h */
 	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
 	c->ingress_src_identity = 0;
-	c->hot_counter_slots = 8192;
+	c->hot_counter_slots = 12288; /* bench --hot-slots 8192 / 12288 / 16384: 1.808 / 1.791 / 1.791 ms (config 2) */
 	c->lb_max_entries = 65536;        /* CILIUM_LB_MAP_MAX_ENTRIES, bpf/node_config.h:60 */
 	c->ipv4_loopback = 0x1ffff50a;    /* IPV4_LOOPBACK, bpf/node_config.h:45 */
 	c->lb_flags = CGPU_LB_L3 | CGPU_LB_L4; /* bpf/lxc_config.h:44-45 */
