@@ -770,6 +770,7 @@ struct Cover6Build {
 	std::vector<std::array<uint32_t, 8>> h64;
 	uint32_t m64 = 0;
 	bool any = false;
+	bool too_big = false; /* node lines past the 25-bit b32 field */
 };
 
 struct P6 {
@@ -793,32 +794,68 @@ template <typename T> std::vector<std::pair<T, T>> merge_iv(std::vector<std::pai
 	return out;
 }
 
-/* /32 node {nb, rest_deep, nd, 0} + nb boundaries + nd deep points: covered
- * iff #(b <= x) is odd.  The deep points are the sorted bits 32..63 of every
- * /64 that has an h64 record, so a reader can tell WHICH uncovered x descend
- * (c6_node32_coop). */
-uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uint32_t>> &iv, bool deep,
-		       const std::vector<uint32_t> &points)
+/* /32 node (tables.h cover6 "node32"): the bits 32..63 range is split into
+ * 2^s equal sub-ranges, s the least that fits every sub-range in one 128-B
+ * line of 32 slots.  The line of sub-range [S, E] holds b - 1 for every
+ * boundary b of the merged covered intervals with S <= b <= E, plus S - 1
+ * when an odd number of boundaries lie below S (it counts for every x of
+ * the sub-range), 0xFFFFFFFF past the last; a boundary at 0 becomes the
+ * entry's flip bit instead.  x is covered iff (flip if x is in sub-range 0)
+ * + #(slot < x) over its line is odd.  Parity needs no length, so the 8
+ * lanes of an octet read the line with one load and treat their units alike
+ * (c6_node32_coop).  Returns the b32 entry NODE << 30 | code << 25 | line,
+ * code = flip | deep << 1 | s << 2 (deep: the /32 has h64 records, so an
+ * uncovered x consults h64); s = 7 (COVER6_LONG) marks a node that even 64
+ * sub-ranges do not fit: one header unit {nb, 0, 0, 0} and all boundaries,
+ * scanned whole by its owner lane. */
+uint32_t cover6_node32(Cover6Build &b, const std::vector<std::pair<uint32_t, uint32_t>> &iv, bool deep)
 {
-	std::vector<uint32_t> bnd;
+	std::vector<uint32_t> bnd; /* boundaries b > 0 */
+	uint32_t flip = 0;
 	for (auto &x : iv) {
-		bnd.push_back(x.first);
+		if (x.first)
+			bnd.push_back(x.first);
+		else
+			flip = 1;
 		if (x.second != 0xFFFFFFFFu)
 			bnd.push_back(x.second + 1u);
 	}
-	const uint32_t nb = (uint32_t)bnd.size();
-	bnd.insert(bnd.end(), points.begin(), points.end());
-	/* a node of <= 8 units (header + 28 entries) never straddles a
-	 * 128-B line: k_prefilter_v6_q reads it with one coalesced octet load */
-	const size_t units = 1 + (bnd.size() + 3) / 4;
-	if (units <= 8 && (b.pool.size() / 4) % 8 + units > 8)
-		b.pool.resize((b.pool.size() / 32 + 1) * 32, 0u);
-	const uint32_t off = (uint32_t)(b.pool.size() / 4);
-	b.pool.insert(b.pool.end(), {nb, deep ? 1u : 0u, (uint32_t)points.size(), 0u});
-	b.pool.insert(b.pool.end(), bnd.begin(), bnd.end());
-	while (b.pool.size() % 4)
-		b.pool.push_back(0);
-	return COVER6_NODE << 30 | off;
+	std::sort(bnd.begin(), bnd.end());
+	b.pool.resize((b.pool.size() + 31) / 32 * 32, 0u);
+	const size_t line = b.pool.size() / 32;
+	uint32_t s = 0;
+	for (; s <= 6; s++) {
+		const uint64_t width = 1ull << (32 - s);
+		std::vector<std::vector<uint32_t>> sub(1u << s);
+		bool fits = true;
+		size_t i = 0;
+		uint32_t below = flip; /* parity of the boundaries below S, flip included */
+		for (uint32_t k = 0; k < (1u << s) && fits; k++) {
+			const uint64_t S = k * width;
+			auto &v = sub[k];
+			if (k && (below & 1u))
+				v.push_back((uint32_t)(S - 1));
+			for (; i < bnd.size() && bnd[i] < S + width; i++, below ^= 1u)
+				v.push_back(bnd[i] - 1u);
+			fits = v.size() <= 32;
+		}
+		if (!fits)
+			continue;
+		for (auto &v : sub) {
+			v.resize(32, 0xFFFFFFFFu);
+			b.pool.insert(b.pool.end(), v.begin(), v.end());
+		}
+		break;
+	}
+	if (s > 6) {
+		s = COVER6_LONG;
+		b.pool.insert(b.pool.end(), {(uint32_t)bnd.size(), 0u, 0u, 0u});
+		for (uint32_t x : bnd)
+			b.pool.push_back(x - 1u);
+		b.pool.resize((b.pool.size() + 31) / 32 * 32, 0xFFFFFFFFu);
+	}
+	b.too_big |= b.pool.size() / 32 > (1u << 25);
+	return COVER6_NODE << 30 | (flip | (deep ? 2u : 0u) | s << 2) << 25 | (uint32_t)line;
 }
 
 uint32_t cover6_node64(Cover6Build &b, const std::vector<std::pair<uint64_t, uint64_t>> &iv)
@@ -880,7 +917,7 @@ uint32_t cover6_group32(Cover6Build &b, const std::vector<P6> &ps, size_t k, siz
 			std::vector<std::array<uint32_t, 8>> &r64)
 {
 	std::vector<std::pair<uint32_t, uint32_t>> s2;
-	std::vector<uint32_t> pts; /* the /64s with an h64 record (sorted by hi) */
+	std::vector<uint32_t> pts; /* bits 32..63 of the /64s with an h64 record */
 	for (size_t q = k; q < l; q++) {
 		const P6 &p = ps[q];
 		if (p.len <= 32)
@@ -924,7 +961,7 @@ uint32_t cover6_group32(Cover6Build &b, const std::vector<P6> &ps, size_t k, siz
 		r64.push_back(r);
 		m = q;
 	}
-	return s2.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s2), !pts.empty(), pts);
+	return s2.empty() ? COVER6_DEEP << 30 : cover6_node32(b, merge_iv(s2), !pts.empty());
 }
 
 /* Any-match cover of (len, address) prefixes, see tables.h cover6: /0../16
@@ -948,6 +985,9 @@ void build_cover6(const std::vector<Rank6> &cand, Cover6Build &b)
 		ps.push_back(P6{hi, lo, c.len});
 	}
 	std::sort(ps.begin(), ps.end());
+	/* line 0: all-ones, the line c6_node32_coop loads for a lane without
+	 * a node line to read */
+	b.pool.assign(32, 0xFFFFFFFFu);
 	const uint32_t FULL = COVER6_FULL << 30, DEEP = COVER6_DEEP << 30;
 	b.root.assign(65536, 0);
 	b.b24.clear();
@@ -2911,6 +2951,8 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	}
 	Cover6Build pf6;
 	build_cover6(pf6_candidates(in.pf), pf6);
+	if (pf6.too_big)
+		return fail(-E2BIG, "prefilter v6 cover exceeds 2^25 node lines");
 	Arena ar;
 	size_t o4[4] = {0, 0, 0, 0}, o6[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	if (have4) {

@@ -2041,98 +2041,84 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilt
  */
 
 /*
- * The /32 interval nodes of Q packets per lane, each node read cooperatively: the 8 lanes of an octet take
- * the octet's Q x 8 nodes in turn, lane j loading 16-B unit j of the node, so
- * one load instruction touches one 128-B line per node instead of one line
- * per lane and unit (the node pass was 8 L2 requests per packet; the kernel is
- * bound by L2 request rate, profiles/r1_pf6).  Lane j counts the boundaries of
- * its unit (4j-4 .. 4j-1) that are <= x, the octet sums them, and the owner
- * keeps the sum; nodes longer than 28 boundaries finish on the owner lane.
- * Every lane of the wave must call this (cross-lane reads).  The pool holds
- * 128 B of padding past its last node (host.cpp cover6 build).
+ * The /32 interval nodes (tables.h cover6 node32) of Q packets per lane, read
+ * cooperatively: each owner lane picks the line of its x's sub-range, the 8
+ * lanes of an octet take the octet's 8 lines in turn, lane j loading 16-B
+ * unit j, so one load instruction touches one 128-B line per node.  A line is
+ * parity-coded, so lane j only counts its 4 slots below x and puts the
+ * count's parity in bit o of a word; three DPP xors over the octet leave all
+ * 8 parities in every lane and owner lane o keeps bit o.  COVER6_LONG nodes
+ * are scanned by their owner.  Every lane of the wave must call this
+ * (cross-lane reads).
  */
+__device__ __forceinline__ uint32_t octet_xor(uint32_t v)
+{
+	v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  /* quad_perm 1,0,3,2 */
+	v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  /* quad_perm 2,3,0,1 */
+	v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false); /* row_half_mirror */
+	return v;
+}
+
+__device__ __forceinline__ uint32_t c6_below4(uint4 q, uint32_t x)
+{
+	return (q.x < x ? 1u : 0u) + (q.y < x ? 1u : 0u) + (q.z < x ? 1u : 0u) + (q.w < x ? 1u : 0u);
+}
+
 template <int Q>
 __device__ __forceinline__ void c6_node32_coop(const uint32_t *pool, const uint32_t (&e)[Q], const uint32_t (&x)[Q],
 					       uint32_t (&tag)[Q], bool (&hit)[Q])
 {
-	const uint4 *P = reinterpret_cast<const uint4 *>(pool);
 	const int lane = (int)__lane_id();
-	const int j = lane & 7, base = lane & ~7;
+	const uint32_t j = (uint32_t)lane & 7u;
+	const int base = lane & ~7;
+	const uint4 *P = reinterpret_cast<const uint4 *>(pool) + j;
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
-		const uint32_t mine = tag[u] == COVER6_NODE ? e[u] & 0x3FFFFFFFu : 0xFFFFFFFFu;
-		uint32_t eo[8], xo[8];
-		uint4 q[8];
+		const bool node = tag[u] == COVER6_NODE;
+		if (!__any(node))
+			continue;
+		const uint32_t split = (e[u] >> 27) & 7u;
+		const uint32_t sub = split == COVER6_LONG ? 0u : (uint32_t)((uint64_t)x[u] >> (32u - split));
+		/* the line to read; 0 (all 0xFFFFFFFF) when none, so the loads
+		 * need no branch */
+		const uint32_t mine = node && split != COVER6_LONG ? (e[u] & 0x1FFFFFFu) + sub : 0u;
+		uint32_t acc = 0;
 #pragma unroll
 		for (int o = 0; o < 8; o++) {
-			eo[o] = __shfl(mine, base | o);
-			xo[o] = __shfl(x[u], base | o);
+			const uint32_t lo = __shfl(mine, base | o), xo = __shfl(x[u], base | o);
+			acc |= (c6_below4(P[lo * 8u], xo) & 1u) << o;
 		}
-#pragma unroll
-		for (int o = 0; o < 8; o++)
-			q[o] = eo[o] != 0xFFFFFFFFu ? P[eo[o] + (uint32_t)j] : make_uint4(0, 0, 0, 0);
-		uint32_t cnt = 0, hdr = 0, nd = 0;
-#pragma unroll
-		for (int o = 0; o < 8; o++) {
-			/* node o's header {nb, rest_deep, nd} sits in lane 0's unit */
-			const uint32_t h = __shfl(q[o].x | (q[o].y ? 0x80000000u : 0u), base);
-			const uint32_t hn = __shfl(q[o].z, base);
-			const uint32_t nb = h & 0x7FFFFFFFu;
-			uint32_t c = 0;
-			if (j) {
-				const uint32_t k0 = 4u * (uint32_t)(j - 1);
-				const uint32_t v[4] = {q[o].x, q[o].y, q[o].z, q[o].w};
-#pragma unroll
-				for (int i = 0; i < 4; i++) {
-					const uint32_t k = k0 + (uint32_t)i;
-					/* boundaries count in bits 0..15, deep points equal to x in 16.. */
-					c += k < nb ? (v[i] <= xo[o] ? 1u : 0u)
-						    : (k < nb + hn && v[i] == xo[o] ? 0x10000u : 0u);
-				}
+		acc = octet_xor(acc);
+		if (node) {
+			uint32_t par = (acc >> j) & 1u;
+			if (split == COVER6_LONG) {
+				const uint4 *n = reinterpret_cast<const uint4 *>(pool) + (size_t)(e[u] & 0x1FFFFFFu) * 8u;
+				const uint32_t nb = n[0].x;
+				par = 0;
+				for (uint32_t k = 1; k <= (nb + 3) / 4; k++)
+					par ^= c6_below4(n[k], x[u]) & 1u;
 			}
-			c += __shfl_xor(c, 1);
-			c += __shfl_xor(c, 2);
-			c += __shfl_xor(c, 4);
-			if (j == o) {
-				cnt = c;
-				hdr = h;
-				nd = hn;
-			}
-		}
-		if (tag[u] == COVER6_NODE) {
-			const uint32_t nb = hdr & 0x7FFFFFFFu;
-			uint32_t par = cnt & 1u, dp = cnt >> 16;
-			for (uint32_t k = 28; k < nb + nd; k += 4) {
-				const uint4 r = P[(e[u] & 0x3FFFFFFFu) + 1 + k / 4];
-				const uint32_t v[4] = {r.x, r.y, r.z, r.w};
-				for (uint32_t i = 0; i < 4; i++) {
-					if (k + i < nb)
-						par ^= v[i] <= x[u] ? 1u : 0u;
-					else if (k + i < nb + nd)
-						dp |= v[i] == x[u] ? 1u : 0u;
-				}
-			}
-			hit[u] = par;
-			/* with deep points: descend only when x's /64 has a record */
-			const bool deep = nd ? dp != 0 : (hdr >> 31) != 0;
-			tag[u] = !hit[u] && deep ? COVER6_DEEP : COVER6_NONE;
+			par ^= sub ? 0u : (e[u] >> 25) & 1u;
+			hit[u] = par != 0u;
+			tag[u] = !par && ((e[u] >> 26) & 1u) ? COVER6_DEEP : COVER6_NONE;
 		}
 	}
 }
 
-/* set16_has whose first bucket is already loaded (tag 0: exact keys) */
-__device__ __forceinline__ bool set16_has_first(const addr_set16 &t, uint4 k0, uint4 m0, uint4 k1, uint4 m1,
+/* set16_has whose first bucket's keys and tag words are already loaded
+ * (tag 0: exact keys); m0 / m1: the first words of the two mask units */
+__device__ __forceinline__ bool set16_has_first(const addr_set16 &t, uint4 k0, uint32_t m0, uint4 k1, uint32_t m1,
 						uint32_t b, uint4 key)
 {
 	bool res = false, done = false;
 	for (uint32_t p = 0; !done;) {
-		if (!(m0.x & 1u)) {
+		if (!(m0 & 1u)) {
 			done = true;
-		} else if (m0.x == 1u && k0.x == key.x && k0.y == key.y && k0.z == key.z && k0.w == key.w) {
+		} else if (m0 == 1u && k0.x == key.x && k0.y == key.y && k0.z == key.z && k0.w == key.w) {
 			res = done = true;
-		} else if (!(m1.x & 1u)) {
+		} else if (!(m1 & 1u)) {
 			done = true;
-		} else if (m1.x == 1u && k1.x == key.x && k1.y == key.y && k1.z == key.z && k1.w == key.w) {
+		} else if (m1 == 1u && k1.x == key.x && k1.y == key.y && k1.z == key.z && k1.w == key.w) {
 			res = done = true;
 		} else if (++p >= t.max_probe) {
 			done = true;
@@ -2140,9 +2126,9 @@ __device__ __forceinline__ bool set16_has_first(const addr_set16 &t, uint4 k0, u
 			b = (b + 1) & t.bucket_mask;
 			const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
 			k0 = bk[0];
-			m0 = bk[1];
+			m0 = bk[1].x;
 			k1 = bk[2];
-			m1 = bk[3];
+			m1 = bk[3].x;
 		}
 	}
 	return res;
@@ -2156,8 +2142,8 @@ __device__ __forceinline__ uint32_t c6_from16(uint32_t r)
 
 /* mode (k_prefilter_v6_q): 0 the root in global memory; 1 lds = root16;
  * 2 lds = rbits then the b24_16 blocks (root and b24 resolved in LDS) */
-template <int Q>
-__device__ __forceinline__ void cover6_any_q(const cover6 &t, int mode, const uint32_t *lds, const uint4 (&a)[Q],
+template <int Q, int mode>
+__device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint32_t *lds, const uint4 (&a)[Q],
 					     const bool (&act)[Q], bool (&hit)[Q])
 {
 	uint32_t w0[Q], w1[Q], w2[Q], w3[Q], e[Q], tag[Q];
@@ -2171,7 +2157,7 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, int mode, const ui
 		if (!act[u] || !t.root)
 			continue;
 		const uint32_t x = w0[u] >> 16;
-		if (mode == 2) {
+		if constexpr (mode == 2) {
 			/* root bitmaps and rank, then the /16's b24 block: all LDS */
 			const uint32_t deep = lds[x >> 5], full = lds[2048u + (x >> 5)];
 			const uint32_t bit = 1u << (x & 31u);
@@ -2183,14 +2169,14 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, int mode, const ui
 				const uint16_t *b24 = reinterpret_cast<const uint16_t *>(lds + COVER6_RBITS_WORDS);
 				e[u] = c6_from16(b24[rank * 256u + ((w0[u] >> 8) & 0xFFu)]);
 			}
-		} else if (mode == 1) {
+		} else if constexpr (mode == 1) {
 			e[u] = c6_from16(reinterpret_cast<const uint16_t *>(lds)[x]);
 		} else {
 			e[u] = t.root[x];
 		}
 	}
 	/* the direct-indexed levels: bits 16..23 (unless resolved in LDS), 24..31 */
-	if (mode != 2) {
+	if constexpr (mode != 2) {
 #pragma unroll
 		for (int u = 0; u < Q; u++)
 			if ((e[u] >> 30) == COVER6_DEEP)
@@ -2205,7 +2191,9 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, int mode, const ui
 		tag[u] = e[u] >> 30;
 		hit[u] = tag[u] == COVER6_FULL;
 	}
+#ifndef CGPU_DIAG_PF6_NO_NODE /* timing-only tool build (tools/diag_ab.py): wrong verdicts */
 	c6_node32_coop<Q>(t.pool, e, w1, tag, hit);
+#endif
 	/* /64 records */
 	uint4 s0[Q], s1[Q];
 	uint32_t home[Q];
@@ -2246,11 +2234,22 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, int mode, const ui
 	}
 }
 
+#ifdef CGPU_DIAG_PF6_PREFETCH /* timing-only tool build (tools/diag_ab.py) */
+#define PF6_PREFETCH true
+#else
+#define PF6_PREFETCH false /* measured slower: the extra registers spill (r2) */
+#endif
+#ifdef CGPU_DIAG_PF6_Q /* timing-only tool build: packets per lane */
+#define PF6_Q CGPU_DIAG_PF6_Q
+#else
+#define PF6_Q 3 /* 3 > 4 > 2 measured (r2, config 3) */
+#endif
+
 /* W: minimum resident waves per SIMD the registers are fitted to.  The /32
  * node reads are octet-cooperative (c6_node32_coop), so the loop trip count
  * is uniform per wave; lanes past the batch end carry inactive packets. */
-template <int Q, int NT>
-__global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a, int mode)
+template <int Q, int NT, int mode>
+__global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a)
 {
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr16);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr16);
@@ -2259,10 +2258,10 @@ __global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilte
 	uint32_t *lc = lbloom + s.ep6_bloom_mask + 1u; /* 16-B aligned: >= 64 words */
 	for (uint32_t k = threadIdx.x; k <= s.ep6_bloom_mask; k += NT)
 		lbloom[k] = s.ep6_bloom[k];
-	if (mode == 1) {
+	if constexpr (mode == 1) {
 		for (uint32_t k = threadIdx.x; k < 65536u * 2u / 16u; k += NT)
 			reinterpret_cast<uint4 *>(lc)[k] = reinterpret_cast<const uint4 *>(s.pf6.root16)[k];
-	} else if (mode == 2) {
+	} else if constexpr (mode == 2) {
 		for (uint32_t k = threadIdx.x; k < COVER6_RBITS_WORDS / 4u; k += NT)
 			reinterpret_cast<uint4 *>(lc)[k] = reinterpret_cast<const uint4 *>(s.pf6.rbits)[k];
 		for (uint32_t k = threadIdx.x; k < s.pf6.n_b24 * 256u * 2u / 16u; k += NT)
@@ -2275,29 +2274,56 @@ __global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilte
 	/* wave-step g covers packets [g * Q, g * Q + 64 Q): packet u of a lane
 	 * is g * Q + 64 u + lane, so each column load of a wave reads 64
 	 * consecutive packets (1 KiB of addresses, 64 B of flags) */
-	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x - lane; g * Q < a.n; g += T) {
+	/* PF6_PREFETCH: the source addresses and flags of the wave's next step
+	 * are loaded while this one resolves */
+	uint4 nsa[Q];
+	uint32_t nf[Q];
+	auto load_src = [&](uint64_t g, uint4 (&sa)[Q], uint32_t (&f)[Q]) {
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = std::min<uint64_t>(g * Q + 64u * u + lane, a.n - 1);
+			const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(sa16 + i));
+			sa[u] = make_uint4(x.x, x.y, x.z, x.w);
+			f[u] = a.flags[i];
+		}
+	};
+	const uint64_t g0 = (uint64_t)blockIdx.x * NT + threadIdx.x - lane;
+	if (PF6_PREFETCH && g0 * Q < a.n)
+		load_src(g0, nsa, nf);
+	for (uint64_t g = g0; g * Q < a.n; g += T) {
 		uint4 sa[Q], da[Q];
 		uint32_t f[Q];
 		uint64_t ix[Q];
 		bool act[Q], hit[Q];
+		if (PF6_PREFETCH) {
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				sa[u] = nsa[u];
+				f[u] = nf[u];
+			}
+			if ((g + T) * Q < a.n)
+				load_src(g + T, nsa, nf);
+		} else {
+			load_src(g, sa, f);
+		}
 #pragma unroll
 		for (int u = 0; u < Q; u++)
 			ix[u] = g * Q + 64u * u + lane;
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = ix[u] < a.n ? ix[u] : a.n - 1;
-			const v4u_t x = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(sa16 + i));
 			const v4u_t y = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(da16 + i));
-			sa[u] = make_uint4(x.x, x.y, x.z, x.w);
 			da[u] = make_uint4(y.x, y.y, y.z, y.w);
-			f[u] = a.flags[i];
 			act[u] = ix[u] < a.n && f[u] == 0u && s.pf6_enabled;
+#ifdef CGPU_DIAG_PF6_NO_COVER /* timing-only tool build: wrong verdicts */
+			act[u] = false;
+#endif
 		}
-		cover6_any_q<Q>(s.pf6, mode, lc, sa, act, hit);
+		cover6_any_q<Q, mode>(s.pf6, lc, sa, act, hit);
 		/* check_v6_endpoint: cilium_lxc on daddr; the LDS bloom filter
 		 * settles most misses, the rest load their first bucket together */
-		uint4 k0[Q], m0[Q], k1[Q], m1[Q];
-		uint32_t b[Q];
+		uint4 k0[Q], k1[Q];
+		uint32_t m0[Q], m1[Q], b[Q];
 		bool need[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
@@ -2306,11 +2332,15 @@ __global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilte
 			b[u] = h & s.ep6.bucket_mask;
 			need[u] = ix[u] < a.n && f[u] == 0u && !hit[u] &&
 				  (lbloom[v6_bloom_word(h, s.ep6_bloom_mask)] & bits) == bits;
+#ifdef CGPU_DIAG_PF6_NO_EP /* timing-only tool build: wrong verdicts */
+			need[u] = false;
+#endif
 			const uint4 *p = reinterpret_cast<const uint4 *>(s.ep6.slots) + (size_t)b[u] * 4u;
+			const uint32_t *pw = reinterpret_cast<const uint32_t *>(p);
 			k0[u] = need[u] ? p[0] : make_uint4(0, 0, 0, 0);
-			m0[u] = need[u] ? p[1] : make_uint4(0, 0, 0, 0);
+			m0[u] = need[u] ? pw[4] : 0u;
 			k1[u] = need[u] ? p[2] : make_uint4(0, 0, 0, 0);
-			m1[u] = need[u] ? p[3] : make_uint4(0, 0, 0, 0);
+			m1[u] = need[u] ? pw[12] : 0u;
 		}
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
@@ -2577,10 +2607,16 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 		mode = 1;
 		lds += 65536u * 2u;
 	}
-	const void *kern = (const void *)k_prefilter_v6_q<4, NT>;
+	const void *kern = mode == 2 ? (const void *)k_prefilter_v6_q<PF6_Q, NT, 2>
+			   : mode == 1 ? (const void *)k_prefilter_v6_q<PF6_Q, NT, 1> : (const void *)k_prefilter_v6_q<PF6_Q, NT, 0>;
 	const unsigned res = resident_blocks(kern, NT, lds);
-	const unsigned g = (unsigned)std::min<uint64_t>((a.n + 4 * NT - 1) / (4 * NT), res);
-	hipLaunchKernelGGL((k_prefilter_v6_q<4, NT>), dim3(g ? g : 1), dim3(NT), lds, st, s, a, mode);
+	const unsigned g = (unsigned)std::min<uint64_t>((a.n + PF6_Q * NT - 1) / (PF6_Q * NT), res);
+	if (mode == 2)
+		hipLaunchKernelGGL((k_prefilter_v6_q<PF6_Q, NT, 2>), dim3(g ? g : 1), dim3(NT), lds, st, s, a);
+	else if (mode == 1)
+		hipLaunchKernelGGL((k_prefilter_v6_q<PF6_Q, NT, 1>), dim3(g ? g : 1), dim3(NT), lds, st, s, a);
+	else
+		hipLaunchKernelGGL((k_prefilter_v6_q<PF6_Q, NT, 0>), dim3(g ? g : 1), dim3(NT), lds, st, s, a);
 	return hipGetLastError();
 }
 

@@ -349,23 +349,29 @@ static inline __host__ __device__ uint32_t lb6_vip_bit(uint32_t f)
  *   bits 24..31]: direct-indexed u32 entries; prefixes of /17../32 are
  *   expanded into the entries they cover (an any-match set has no
  *   priorities, so expansion is exact).  b32 entries of /32s holding
- *   longer prefixes are NODEs: {nb, rest_deep, nd, 0} + nb sorted u32
- *   boundaries of the merged covered intervals of bits 32..63 (covered iff
- *   #(boundaries <= x) is odd) + nd "deep points" (bits 32..63 of every /64
- *   with an h64 record: an uncovered x descends only if it is one of them).
+ *   longer prefixes are NODEs (node32, host.cpp cover6_node32): 2^s
+ *   128-B lines, one per equal sub-range of bits 32..63, each 32 slots of
+ *   b - 1 for the boundaries b of the merged covered intervals in its
+ *   sub-range (plus S - 1 when an odd number lie below its start S),
+ *   0xFFFFFFFF past the last; x is covered iff (flip, in sub-range 0) +
+ *   #(slot < x) over x's line is odd.  The b32 entry carries code << 25 |
+ *   line, code = flip | deep << 1 | s << 2 (s = COVER6_LONG: a header unit
+ *   {nb, 0, 0, 0} + every boundary, scanned whole); deep: the /32 has h64
+ *   records, so an uncovered x consults h64.
  *   h64: hop-hashed 32-B slots {top64.hi, top64.lo, entry, used | hop << 24,
  *        lo.hi, lo.lo, hi.hi, hi.lo} for the /64s holding prefixes longer
  *        than /64 (an INLINE FULL entry covers [lo, hi] of the low 64 bits).
  * entry: tag << 30 | payload, tag COVER6_NONE / _FULL / _DEEP (root, b24:
  * payload = the next level's block; b32: consult h64) / _NODE (payload =
- * offset in 16-B units into `pool`).  Typical config-3 packet: root, b24,
- * b32 (768 KiB together, L2-resident) + one 128-B node + rarely one h64
- * slot. */
+ * code << 25 | 128-B line of `pool`; in h64 records: offset in 16-B units).
+ * Typical config-3 packet: root, b24, b32 (768 KiB together, L2-resident) +
+ * one 128-B node + rarely one h64 slot. */
 #define COVER6_NONE 0u
 #define COVER6_FULL 1u
 #define COVER6_DEEP 2u
 #define COVER6_NODE 3u
 #define COVER6_USED (1u << 16)
+#define COVER6_LONG 7u /* node32 split code: header + boundaries, no split fits */
 #define COVER6_RBITS_WORDS (2048u * 2u + 1024u) /* DEEP, FULL bitmaps + u16 ranks */
 
 typedef struct cover6 {

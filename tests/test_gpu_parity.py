@@ -552,20 +552,39 @@ def test_prefilter6_cover_shapes(torch_cuda, seed, lds_mode, monkeypatch):
     k_prefilter_v6_q (0: root in HBM, 1: u16 root in LDS, 2: root bitmaps +
     u16 b24 blocks in LDS).  Bit-exact against the restatement's kernel-like
     LPM trie."""
-    from oracle import Oracle
-    torch = torch_cuda
     monkeypatch.setenv("CGPU_PF6_LDS", str(lds_mode))
-    rng = np.random.default_rng(100 + seed)
-    roots = rng.integers(0, 256, (6, 2), dtype=np.uint8)
-    lens = [0, 1, 8, 15, 16, 17, 20, 27, 28, 29, 30, 31, 32, 33, 40, 48, 63, 64, 65, 80, 96, 112, 127, 128]
+    _cover6_case(torch_cuda, seed, np.random.default_rng(100 + seed).integers(0, 256, (6, 2), dtype=np.uint8))
+
+
+@pytest.mark.parametrize("n_roots,root_bytes", [(3, 4), (40, 4), (150, 4), (600, 4), (3, 7), (24, 6)])
+def test_prefilter6_dense_nodes(torch_cuda, n_roots, root_bytes):
+    """Thousands of prefixes under a few /32s (root_bytes 4) or packed into a
+    few /56s and /48s (7, 6): /32 nodes of every sub-range split, 0..6 and
+    COVER6_LONG (tables.h cover6 node32), with boundaries at 0 and
+    0xFFFFFFFF (the flip bit, the open last interval)."""
+    rng = np.random.default_rng(7 + n_roots + root_bytes)
+    _cover6_case(torch_cuda, 1, rng.integers(0, 256, (n_roots, root_bytes), dtype=np.uint8), rng=rng,
+                 lens=[0, 0, 0, 0, 0, 33, 40, 48, 56, 63, 64, 64, 65, 80, 96, 112, 127, 128])
+
+
+def _cover6_case(torch, seed, roots, rng=None, lens=None):
+    from oracle import Oracle
+    rng = rng if rng is not None else np.random.default_rng(100 + seed)
+    lens = lens or [0, 1, 8, 15, 16, 17, 20, 27, 28, 29, 30, 31, 32, 33, 40, 48, 63, 64, 65, 80, 96,
+                    112, 127, 128]
     keys = []
     for i in range(3000):
         k = np.zeros((), L.LPM_V6_KEY)
-        ln = int(rng.choice(lens[5:])) if i > 3 else [0, 8, 16, 1][i] if seed == 3 else 17
+        # the first keys: short prefixes over the roots (not in the dense /32 cases)
+        ln = (int(rng.choice(lens[5:])) if i > 3 or roots.shape[1] > 2 else
+              [0, 8, 16, 1][i] if seed == 3 else 17)
         a = rng.integers(0, 256, 16, dtype=np.uint8)
-        a[:2] = roots[rng.integers(0, len(roots))]
-        if rng.random() < 0.2:
+        a[:roots.shape[1]] = roots[rng.integers(0, len(roots))]
+        r = rng.random()
+        if r < 0.2:
             a[2:] = 0xFF
+        elif r < 0.3:
+            a[4:] = 0
         k["prefixlen"] = ln
         k["addr"][:] = a
         keys.append(k)

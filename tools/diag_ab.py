@@ -25,7 +25,13 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "nc_all_l2": ("CGPU_DIAG_NO_COLD", "CGPU_DIAG_P1_SMALL", "CGPU_DIAG_P2_SMALL",
                           "CGPU_DIAG_LPM_SMALL"),
             "one_wg_per_cu": ("CGPU_DIAG_LDS_PAD=65536",),
-            "store_sc1": ("CGPU_DIAG_STORE_SC1",)}
+            "store_sc1": ("CGPU_DIAG_STORE_SC1",),
+            "pf6_no_node": ("CGPU_DIAG_PF6_NO_NODE",), "pf6_no_ep": ("CGPU_DIAG_PF6_NO_EP",),
+            "pf6_no_cover": ("CGPU_DIAG_PF6_NO_COVER",),
+            "pf6_prefetch": ("CGPU_DIAG_PF6_PREFETCH",),
+            "pf6_q4": ("CGPU_DIAG_PF6_Q=4",),
+            "pf6_q2": ("CGPU_DIAG_PF6_Q=2",),
+            "pf6_q2_prefetch": ("CGPU_DIAG_PF6_Q=2", "CGPU_DIAG_PF6_PREFETCH")}
 
 
 def build(names):
