@@ -2843,9 +2843,23 @@ __device__ __forceinline__ int ct_find(const ct_table &T, uint4 k, uint32_t *fre
 	uint32_t h = ct_hash(k.x, k.y, k.z, k.w) & T.mask;
 	uint32_t ff = 0xFFFFFFFFu;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
+#ifdef CGPU_DIAG_CT_COHERENT_PROBE /* timing-only tool build: every slot read at the coherence point */
+		const uint64_t xy0 = __hip_atomic_load(reinterpret_cast<uint64_t *>(T.keys + h), __ATOMIC_RELAXED,
+						       __HIP_MEMORY_SCOPE_AGENT);
+		const uint64_t zw0 = __hip_atomic_load(reinterpret_cast<uint64_t *>(T.keys + h) + 1, __ATOMIC_RELAXED,
+						       __HIP_MEMORY_SCOPE_AGENT);
+		uint4 s = make_uint4((uint32_t)xy0, (uint32_t)(xy0 >> 32), (uint32_t)zw0, (uint32_t)(zw0 >> 32));
+		uint32_t tag = s.w >> 16;
+		if (tag == CT_TAG_EMPTY) {
+			*free_at = ff != 0xFFFFFFFFu ? ff : h;
+			return -1;
+		}
+		if (false) {
+#else
 		uint4 s = ld_x4<true>(T.keys + h);
 		uint32_t tag = s.w >> 16;
 		if (tag == CT_TAG_EMPTY) {
+#endif
 			/* the chain ends only on an EMPTY read at the coherence point:
 			 * the plain load may be a line this XCD's L2 holds from before
 			 * another XCD's lane claimed the slot (a claim's CAS happens at

@@ -3,7 +3,7 @@ product library: these builds drop work and give wrong counters).
 
     python tools/diag_ab.py build            # in the dev container: tools/_diag/*.so
     python tools/diag_ab.py run [variants]   # on the GPU box
-    (CGPU_AB_CONFIG = gpu (config 2, default) / pf6 (config 3) / v6)
+    (CGPU_AB_CONFIG = gpu (config 2, default) / pf6 (config 3) / v6 / ct)
 
 Each variant is cilium_amd/csrc compiled with extra -D flags into
 tools/_diag/libcgpu_<name>.so; `run` loads each in turn into the Engine
@@ -31,7 +31,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "pf6_prefetch": ("CGPU_DIAG_PF6_PREFETCH",),
             "pf6_q4": ("CGPU_DIAG_PF6_Q=4",),
             "pf6_q2": ("CGPU_DIAG_PF6_Q=2",),
-            "pf6_q2_prefetch": ("CGPU_DIAG_PF6_Q=2", "CGPU_DIAG_PF6_PREFETCH")}
+            "pf6_q2_prefetch": ("CGPU_DIAG_PF6_Q=2", "CGPU_DIAG_PF6_PREFETCH"),
+            "ct_coherent_probe": ("CGPU_DIAG_CT_COHERENT_PROBE",)}
 
 
 def build(names):
@@ -69,6 +70,31 @@ def _workload(conf):
             synth.load_prefilter6(e, P)
             return e
         return make, lambda e: e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=v), n
+    if conf == "ct":
+        # bench.py --config ct: 64M packets of 2M connections, every launch
+        # from an empty map (flush + classify, as a bench step)
+        import numpy as np
+        T = synth.make_tables(**synth.CONFIGS["gpu"])
+        n = synth.CONFIGS["gpu"]["n_tuples"]
+        tup, _, seclabels = synth.make_ct_workload(T, n // 32, mean_pkts=32)
+        n = min(n, len(tup["saddr"]))
+        tup = {k: np.ascontiguousarray(v[:n]) for k, v in tup.items()}
+        ct_max = 1 << max(20, int(np.ceil(np.log2(2.5 * n / 32))))
+        d = synth.to_device(tup)
+        out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+               "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None,
+               "ct_ret": torch.empty(n, dtype=torch.uint8, device="cuda")}
+
+        def make():
+            e = Engine(device=0, **T.engine_config(), ct_max=ct_max)
+            synth.load_engine(e, T)
+            synth.load_lxc(e, seclabels)
+            return e
+
+        def step(e):
+            e.ct4_flush()
+            e.classify_v4_ct(d, 1000, out=out)
+        return make, step, n
     v6 = conf == "v6"
     T = (synth.make_tables6 if v6 else synth.make_tables)(**synth.CONFIGS[conf])
     n = synth.CONFIGS[conf]["n_tuples"]
