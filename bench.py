@@ -271,6 +271,9 @@ def main():
         assert int(lo) == int(hi), "replicated tables differ across ranks"
 
     result = None
+    # the CPU baseline is an N=1 figure (rank 0 alone); at N > 1 the
+    # restatement runs once, for the parity check of rank 0's batch only
+    skip_cpu = args.no_cpu_baseline or world > 1
     if rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from oracle import Oracle  # CPU restatement: checker + CPU baseline only
@@ -312,7 +315,7 @@ def main():
             hsh = ((lo * np.uint64(0x9E3779B97F4A7C15)) ^ hi) * np.uint64(0xC2B2AE3D27D4EB4F)
             sub = np.nonzero((hsh >> np.uint64(58)) == 0)[0]
             tsub = {k: v[sub] for k, v in tup.items()}
-        else:
+        elif not skip_cpu:
             cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
         # the median of 3 timed runs (the first also yields the reference result)
         runs = []
@@ -333,7 +336,7 @@ def main():
             runs.append(time.perf_counter() - c0)
             if rep == 0:
                 first = res
-            if ct or args.no_cpu_baseline:
+            if ct or skip_cpu:
                 break  # the sequential conntrack replay mutates its map
         c_el = float(np.median(runs))
         if ct:
@@ -344,14 +347,14 @@ def main():
             v0, i0, _, probes = first
         n_cpu = len(sub) if ct else n
         cpu = None
-        if not args.no_cpu_baseline and ct:
+        if not skip_cpu and ct:
             cpu = {"value": round(n_cpu / c_el / 1e6, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
                    "sample": f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
                              f"pairs from an empty map; oracle/cgpu_oracle.c or_classify_v4_ct "
                              f"(sequential conntrack + LPM trie + open hash), 1 thread, "
                              f"{c_el:.2f}s wall (one run); host: {host_cpu()}"}
-        elif not args.no_cpu_baseline:
+        elif not skip_cpu:
             what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
                     "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash",
                     "v6": "oracle/cgpu_oracle.c IPv6 LPM trie + open hash",
