@@ -910,9 +910,9 @@ void hop_place(std::vector<std::array<uint32_t, W>> &tab, uint32_t &mask,
 uint32_t h64_home(const std::array<uint32_t, 8> &r) { return mix32(r[0], r[1]); }
 
 /* The /32 entry of the prefixes longer than /32 among ps[k, l) (one /32,
- * sorted; shorter ones are skipped): an interval node over bits 32..63 (/33../64) with the
- * deep points of its /64 records, or DEEP when only /65+ prefixes exist;
- * appends the /64 records to r64. */
+ * sorted; shorter ones are skipped): an interval node over bits 32..63
+ * (/33../64) flagged deep when the /32 also has /64 records, or DEEP when only
+ * /65+ prefixes exist; appends the /64 records to r64. */
 uint32_t cover6_group32(Cover6Build &b, const std::vector<P6> &ps, size_t k, size_t l,
 			std::vector<std::array<uint32_t, 8>> &r64)
 {

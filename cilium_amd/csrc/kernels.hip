@@ -2245,9 +2245,10 @@ __device__ __forceinline__ void cover6_any_q(const cover6 &t, const uint32_t *ld
 #define PF6_Q 3 /* 3 > 4 > 2 measured (r2, config 3) */
 #endif
 
-/* W: minimum resident waves per SIMD the registers are fitted to.  The /32
- * node reads are octet-cooperative (c6_node32_coop), so the loop trip count
- * is uniform per wave; lanes past the batch end carry inactive packets. */
+/* Q packets per lane; mode: the LDS staging of the cover's top levels
+ * (cover6_any_q).  The /32 node reads are octet-cooperative
+ * (c6_node32_coop), so the loop trip count is uniform per wave; lanes past
+ * the batch end carry inactive packets. */
 template <int Q, int NT, int mode>
 __global__ __launch_bounds__(NT) void k_prefilter_v6_q(cgpu_snapshot s, prefilter_args a)
 {
