@@ -567,6 +567,69 @@ def test_prefilter6_dense_nodes(torch_cuda, n_roots, root_bytes):
                  lens=[0, 0, 0, 0, 0, 33, 40, 48, 56, 63, 64, 64, 65, 80, 96, 112, 127, 128])
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_prefilter6_split_nodes(torch_cuda, seed):
+    """/32s packed with /60../64 prefixes (and /128s in the same /64s), from
+    8 to 1500 per /32 and clustered into 2^20 / 2^24 windows, so the /32
+    nodes take every sub-range split (tables.h cover6 node32: s = 0..6) and
+    the long-node fallback (COVER6_LONG); boundaries at 0 and 0xFFFFFFFF of
+    bits 32..63 (the flip bit, the open last interval).  Packets sit on, just
+    below and just above every interval edge."""
+    from oracle import Oracle
+    torch = torch_cuda
+    rng = np.random.default_rng(300 + seed)
+    specs = [(8, 32), (20, 32), (40, 32), (60, 32), (150, 32), (250, 32), (400, 32), (1500, 32),
+             (200, 20), (100, 24)]
+    keys, edges = [], []
+    for si, (cnt, wb) in enumerate(specs):
+        top = int(rng.integers(0, 2**32))
+        base = int(rng.integers(0, 2**32 - (1 << wb) + 1)) if wb < 32 else 0
+        xs = base + rng.integers(0, 1 << wb, cnt).astype(np.int64)
+        if si == 0:
+            xs[:2] = [0, 0xFFFFFFFF]
+        for x in xs:
+            ln = int(rng.choice([60, 62, 63, 64, 64, 64]))
+            lo32 = int(x) & ~((1 << (64 - ln)) - 1)
+            keys.append((ln, (top << 32) | lo32, int(rng.integers(0, 2**63))))
+            for e in (lo32 - 1, lo32, lo32 + (1 << (64 - ln)) - 1, lo32 + (1 << (64 - ln))):
+                if 0 <= e < 2**32:
+                    edges.append((top << 32) | e)
+        for x in rng.choice(xs, cnt // 10):
+            keys.append((128, (top << 32) | int(x), int(rng.integers(0, 2**63))))
+    k6 = np.zeros(len(keys), L.LPM_V6_KEY)
+    for i, (ln, hi, lo) in enumerate(keys):
+        a = np.frombuffer(hi.to_bytes(8, "big") + lo.to_bytes(8, "big"), np.uint8)
+        k6[i]["prefixlen"] = ln
+        k6[i]["addr"][:] = a & synth.MASK6[ln]
+    n = 200_000
+    hi = np.array(edges, np.uint64)[rng.integers(0, len(edges), n)]
+    s6 = np.zeros((n, 16), np.uint8)
+    s6[:, :8] = hi.astype(">u8").view(np.uint8).reshape(n, 8)
+    s6[:, 8:] = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+    deep = rng.random(n) < 0.1  # exactly on a /128 key
+    s6[deep] = k6["addr"][rng.integers(0, len(k6), int(deep.sum()))]
+    eps = rng.integers(0, 256, (16, 16), dtype=np.uint8)
+    d6 = eps[rng.integers(0, len(eps), n)]
+    flags = np.zeros(n, np.uint8)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    e = _engine(prefilter_dyn6=1)
+    o = Oracle(dyn6=1)
+    for a in eps:
+        ek = np.zeros((), L.ENDPOINT_KEY)
+        ek["ip"][:] = a
+        ek["family"] = L.ENDPOINT_KEY_IPV6
+        assert e.endpoint_update(ek) == 0 and o.endpoint_update(ek) == 0
+    for k in np.unique(k6):
+        assert e.cidr_update(2, k) == 0 and o.cidr_update(2, k) == 0
+    e.commit()
+    g = e.prefilter_v6(dev(s6), dev(d6), dev(flags))
+    torch.cuda.synchronize()
+    r, _ = o.prefilter_v6(s6, d6, flags, nthreads=8)
+    np.testing.assert_array_equal(_np(g), r)
+    assert 0.2 < (r == L.XDP_DROP).mean() < 0.95
+    e.close()
+
+
 def _cover6_case(torch, seed, roots, rng=None, lens=None):
     from oracle import Oracle
     rng = rng if rng is not None else np.random.default_rng(100 + seed)
