@@ -1,6 +1,6 @@
 """Minimal driver for rocprofv3 PMC passes: one bench workload (CGPU_PMC_CONFIG =
 gpu (config 2, default) / cascade (config 5) / pf6 (config 3) / v6 (IPv6
-classify at config-2 size)), one 64M-tuple
+classify at config-2 size) / ct (conntrack)), one 64M-tuple
 batch resident in HBM, 3 launches (classify variant from CGPU_CLASSIFY_VARIANT)."""
 import os
 import sys
@@ -14,7 +14,7 @@ from cilium_amd import synth  # noqa: E402
 from cilium_amd.engine import Engine  # noqa: E402
 
 name = os.environ.get("CGPU_PMC_CONFIG", "gpu")
-cfg = synth.CONFIGS["gpu" if name == "pf6" else name]
+cfg = synth.CONFIGS["gpu" if name in ("pf6", "ct") else name]
 n = int(os.environ.get("CGPU_PMC_TUPLES", cfg["n_tuples"]))
 if name == "v6":
     T = synth.make_tables6(**cfg)
@@ -27,6 +27,28 @@ if name == "v6":
            "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
     for _ in range(3):
         e.classify_v6(d, out=out)
+    torch.cuda.synchronize()
+    print("ok", name, n)
+    sys.exit(0)
+if name == "ct":
+    # bench.py --config ct: 64M packets of 2M connections from an empty map
+    import numpy as np
+    T = synth.make_tables(**cfg)
+    t, _, seclabels = synth.make_ct_workload(T, n // 32, mean_pkts=32)
+    n = min(n, len(t["saddr"]))
+    t = {k: np.ascontiguousarray(v[:n]) for k, v in t.items()}
+    ct_max = 1 << max(20, int(np.ceil(np.log2(2.5 * n / 32))))
+    e = Engine(device=0, **T.engine_config(), ct_max=ct_max)
+    synth.load_engine(e, T)
+    synth.load_lxc(e, seclabels)
+    e.commit()
+    d = synth.to_device(t)
+    out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+           "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None,
+           "ct_ret": torch.empty(n, dtype=torch.uint8, device="cuda")}
+    for _ in range(3):
+        e.ct4_flush()
+        e.classify_v4_ct(d, 1000, out=out)
     torch.cuda.synchronize()
     print("ok", name, n)
     sys.exit(0)
