@@ -3472,7 +3472,7 @@ CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n
 				     uint32_t *identity, uint8_t *stage, void *stream)
 {
 	Pinned P;
-	if (int r = pin(c, stream, P))
+	if (int r = pin(c, stream, P, true))
 		return r;
 	const cgpu_snapshot &s = P.snap();
 	uint64_t *delta = P.delta;
@@ -3484,7 +3484,7 @@ CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n
 		return 0;
 	frames_args a{f->data, f->len, f->flags, f->ep, f->stride, (uint64_t)n,
 		      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-		      verdict, identity, stage, delta};
+		      verdict, identity, stage, delta, P.pk};
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(launch_classify_frames(s, a, (hipStream_t)stream));
 	return 0;

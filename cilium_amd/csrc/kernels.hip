@@ -1938,6 +1938,10 @@ __global__ __launch_bounds__(NT) void k_frames(cgpu_snapshot s, frames_args a)
 				if (c < s.hot_slots && len < PK_MAX_LEN) {
 					atomicAdd((unsigned long long *)&lctr[c],
 						  (1ull << PK_SHIFT) | (unsigned long long)len);
+				} else if (len < PKC_MAX_LEN) {
+					/* one packed atomic (launch_classify_frames unpacks) */
+					atomicAdd((unsigned long long *)&a.pk[c],
+						  (1ull << PKC_SHIFT) | (unsigned long long)len);
 				} else {
 					atomicAdd((unsigned long long *)&a.delta[2u * c], 1ull);
 					atomicAdd((unsigned long long *)&a.delta[2u * c + 1u], (unsigned long long)len);
@@ -2529,7 +2533,8 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 	constexpr int NT = 1024;
 	const size_t lds = (size_t)s.hot_slots * 8u;
 	const uint64_t cap = 2ull * 256ull;
-	const uint64_t per_launch = cap * (1ull << 22);
+	/* packed cold counters: <= PKC_CHUNK frames between unpacks */
+	const uint64_t per_launch = std::min<uint64_t>(cap * (1ull << 22), PKC_CHUNK);
 	for (uint64_t off = 0; off < a.n; off += per_launch) {
 		cls_args c = a;
 		const uint64_t m = std::min<uint64_t>(a.n - off, per_launch);
@@ -2649,6 +2654,10 @@ hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, 
 			c.stage += off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + NT - 1) / NT, cap);
 		hipLaunchKernelGGL((k_frames<1, NT>), dim3(g), dim3(NT), lds, st, s, c);
+		if (s.cold_hi) {
+			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
+			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
+		}
 	}
 	return hipGetLastError();
 }

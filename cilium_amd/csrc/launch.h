@@ -93,6 +93,7 @@ struct frames_args {
 	uint32_t *identity;
 	uint8_t *stage;
 	uint64_t *delta;
+	uint64_t *pk; /* the stream's packed cold-slot accumulator (classify) */
 };
 
 hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hipStream_t st);
