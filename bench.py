@@ -7,9 +7,13 @@ fraction of the HBM roofline.
 
 A step = one classify pass over one 64M-tuple batch already resident in HBM
 (config 2: 100k IPv4 ipcache prefixes + 64k policy entries), plus the RCCL
-all-reduce of the per-entry/per-reason counter deltas (N > 1) and their fold
-into the totals.  Tables are replicated (same seed on every rank); tuple
-streams are seeded per rank, so per-GPU work is fixed (weak scaling).
+all-reduce of the per-entry/per-reason counter deltas (N > 1: the product's
+cgpu_counters_allreduce, shard.reduce_counters) and their fold into the
+totals.  Tables are replicated (same seed on every rank).  At N > 1 (config
+4) rank r's batch is its flowhash(5-tuple) % N shard of the stream the ranks
+generate together: per-rank seeded tuples whose source port is drawn so the
+tuple hashes to r (shard.assign_shard_sports, asserted), so per-GPU work is
+fixed (weak scaling) and the stream is N x 64M tuples per step.
 Rank 0 prints one JSON line.
 
 Other BASELINE configs (not the headline line; run them explicitly):
@@ -179,6 +183,10 @@ def main():
     else:
         T = synth.make_tables(**cfg)
         tup = synth.make_tuples(T, n, gpu_id=rank)
+        if not cascade and not frames:
+            # config 4: this rank's flowhash % world shard of the stream
+            tup["sport"] = shard.assign_shard_sports(tup, world, rank, seed=synth.SEED + 0x5B0 + rank)
+            assert (shard.shard_of(tup, world) == rank).all()
         if cascade:
             S = synth.make_services(T, cfg["n_services"])
             tup = synth.add_service_traffic(tup, S, gpu_id=rank)
@@ -216,12 +224,18 @@ def main():
     delta = torch.zeros(e.counter_delta_bytes() // 8, dtype=torch.int64, device=dev)
     e.counter_bind(delta)
     stream = torch.cuda.current_stream()
+    if world > 1:
+        # replicas must map every policy key to the same counter slot before
+        # their delta buffers are summed slot by slot
+        lay = torch.tensor([e.counter_layout_checksum() & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64,
+                           device=dev)
+        lo_, hi_ = lay.clone(), lay.clone()
+        dist.all_reduce(lo_, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi_, op=dist.ReduceOp.MAX)
+        assert int(lo_) == int(hi_), "counter slot layouts differ across ranks"
+        shard.init_counter_comm(e, rank, world)
 
-    def step(ev=None):
-        if ct:
-            e.ct4_flush()  # every step starts from an empty conntrack map
-        if ev is not None:
-            ev[0].record(stream)
+    def launch():
         if ct:
             e.classify_v4_ct(d, CT_NOW, out=out, stream=stream)
         elif pf6:
@@ -234,10 +248,16 @@ def main():
             e.classify_frames(d, out=out, stream=stream)
         else:
             e.classify_v4(d, out=out, stream=stream)
+
+    def step(ev=None):
+        if ct:
+            e.ct4_flush()  # every step starts from an empty conntrack map
+        if ev is not None:
+            ev[0].record(stream)
+        launch()
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:
-            shard.allreduce_counters(delta)  # RCCL over xGMI: integer SUM, order-independent
+        shard.reduce_counters(e, world, stream)  # RCCL over xGMI: u64 SUM, order-independent
         e.counter_fold(stream)
 
     for _ in range(args.warmup):
@@ -261,6 +281,25 @@ def main():
         elapsed, kern_ms = float(tt[0]), float(tt[1])
     ms_per_step = 1e3 * elapsed / args.steps
     value = world * n * args.steps / elapsed / 1e6
+
+    allreduce_ok = None
+    if world > 1:
+        # the shipped collective against torch's SUM of the same local deltas
+        # (one untimed step): every rank must hold the sum of all ranks
+        if ct:
+            e.ct4_flush()
+        torch.cuda.synchronize()
+        delta.zero_()
+        launch()
+        torch.cuda.synchronize()
+        local = delta.clone()
+        shard.reduce_counters(e, world, stream)
+        dist.all_reduce(local, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        ok = torch.tensor([int(torch.equal(local, delta))], dtype=torch.int64, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        allreduce_ok = bool(int(ok))
+        e.counter_fold(stream)
 
     # counters replicated across ranks must agree
     if world > 1:
@@ -389,6 +428,9 @@ def main():
                 traffic = None
         conf = {"workload": WORKLOADS[args.config], "tuples_per_gpu": n,
                 "parallelism": f"shard{world}", "kernel_ms": round(kern_ms, 4),
+                "stream_tuples_per_step": world * n, "stream_tuples_timed": world * n * args.steps,
+                "counter_reduce": ("cgpu_counters_allreduce (RCCL u64 SUM)" if world > 1 else "none (1 rank)"),
+                "allreduce_check_vs_torch_sum": allreduce_ok,
                 "probes_per_tuple": round(probes_per, 4), "b_alg_per_tuple": round(b_alg, 2),
                 "parity_vs_oracle": parity}
         if pf6:

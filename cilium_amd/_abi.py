@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libcgpu.so")
 
-CGPU_ABI_VERSION = 1
+CGPU_ABI_VERSION = 2
 
 
 class CgpuConfig(C.Structure):
@@ -33,7 +33,8 @@ class CgpuConfig(C.Structure):
         ("lb_max_entries", C.c_uint32), ("ipv4_loopback", C.c_uint32),
         ("lb_flags", C.c_uint32),
         ("node_mac", C.c_uint8 * 6), ("reserved1", C.c_uint8 * 2),
-        ("ct_max", C.c_uint32), ("reserved", C.c_uint32 * 1),
+        ("ct_max", C.c_uint32), ("schedule", C.c_uint32), ("ct6_max", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -121,6 +122,7 @@ PROTOS = {
     "cgpu_flow_hash": (u32, [u32, u32, C.c_uint16, C.c_uint16, C.c_uint8]),
     "cgpu_commit": (i32, [vp, C.POINTER(u64)]),
     "cgpu_table_checksum": (i32, [vp, C.POINTER(u64)]),
+    "cgpu_counter_layout_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
     "cgpu_classify_v6": (i32, [vp, C.POINTER(TuplesV6), sz, vp, vp, vp, vp]),
     "cgpu_classify_v6_lb": (i32, [vp, C.POINTER(TuplesV6), vp, vp, sz, vp, vp, vp, vp]),
@@ -148,6 +150,7 @@ PROTOS = {
     "cgpu_counter_fold": (i32, [vp, vp]),
     "cgpu_metrics_read": (i32, [vp, vp]),
     "cgpu_counters_reset": (i32, [vp]),
+    "cgpu_stream_release": (i32, [vp, vp]),
     "cgpu_comm_id_create": (i32, [vp]),
     "cgpu_comm_init": (i32, [vp, vp, i32, i32]),
     "cgpu_counters_allreduce": (i32, [vp, vp]),

@@ -24,6 +24,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <set>
 #include <string>
 #include <unordered_map>
@@ -1416,6 +1417,7 @@ struct cgpu_ctx {
 	std::vector<std::pair<uint32_t, uint64_t>> pol_changes; /* (ep, key) */
 	uint64_t captured = 0;          /* id of the newest snapshot whose inputs were captured */
 	uint64_t sum_ipc = 0, sum_pol = 0; /* order-independent content sums */
+	uint64_t sum_slots = 0;            /* (ep, key, counter slot) of every policy key */
 
 	/* ---- device ---- */
 	hipStream_t ustream = nullptr;  /* uploads + counter slot init of commits */
@@ -1425,6 +1427,7 @@ struct cgpu_ctx {
 	std::shared_ptr<Epoch> cur;     /* published snapshot (pub_mu) */
 	uint64_t epoch = 0;             /* id of the published snapshot */
 	uint64_t checksum = 0;
+	uint64_t slot_checksum = 0;     /* sum_slots of the published snapshot */
 	/* snapshots unpublished but maybe still running: (id, done event on
 	 * rstream); alive = ids not known complete (incl. the published one) */
 	std::deque<std::pair<uint64_t, hipEvent_t>> retiring;
@@ -1434,8 +1437,16 @@ struct cgpu_ctx {
 	uint64_t *d_delta_own = nullptr;
 	uint64_t *d_delta = nullptr;  /* own or bound */
 	/* [n_ctr_slots] packed counter accumulator per stream (zero between
-	 * classify calls; one per stream keeps its exactness bound per call) */
-	std::map<void *, uint64_t *> d_pk;
+	 * classify calls; one per stream keeps its exactness bound per call).
+	 * At most kMaxPkStreams buffers: a new stream past that takes the least
+	 * recently used one once that stream's last launch finished (`last`). */
+	struct PkBuf {
+		uint64_t *p = nullptr;
+		hipEvent_t last = nullptr;
+		uint64_t tick = 0;
+	};
+	std::map<void *, PkBuf> d_pk;
+	uint64_t pk_tick = 0;
 
 	/* ---- multi-GPU counter reduction (cgpu_comm_init) ---- */
 	void *comm = nullptr; /* ncclComm_t */
@@ -1508,23 +1519,43 @@ void poll_retired(cgpu_ctx *c)
 	}
 }
 
-/* quarantined counter slots whose snapshots all finished become free
- * (caller holds mu) */
-void release_quarantine(cgpu_ctx *c)
+/* The oldest quarantined counter slot, once every snapshot that may count
+ * into it has finished its launches (caller holds mu).  Slot assignment must
+ * depend only on the sequence of map operations and commits, never on how far
+ * the GPU got: replicas on other ranks apply the same sequence and their
+ * delta buffers are summed slot by slot (cgpu_counters_allreduce).  So the
+ * quarantine is used only after the free lists and the never-used slots, in
+ * deletion order, and is WAITED for (not polled) when its snapshot is still
+ * running.  A slot that the newest captured snapshot may still count into
+ * cannot be reused before the next commit: -E2BIG, as a full map. */
+int take_quarantined(cgpu_ctx *c, uint32_t *slot)
 {
-	if (c->quarantine.empty())
-		return;
-	uint64_t lowest;
-	{
-		std::lock_guard<std::mutex> g(c->retire_mu);
+	if (c->quarantine.empty() || c->quarantine.front().first >= c->captured)
+		return -E2BIG;
+	const uint64_t need = c->quarantine.front().first;
+	for (;;) {
+		std::unique_lock<std::mutex> g(c->retire_mu);
 		poll_retired(c);
-		lowest = c->alive.empty() ? UINT64_MAX : *c->alive.begin();
+		const uint64_t lowest = c->alive.empty() ? UINT64_MAX : *c->alive.begin();
+		if (lowest > need)
+			break;
+		hipEvent_t ev = nullptr;
+		for (auto &r : c->retiring)
+			if (r.first == lowest)
+				ev = r.second;
+		if (ev) {
+			if (hipEventSynchronize(ev) != hipSuccess)
+				return -EIO;
+		} else {
+			/* still published (a commit in another thread is replacing it)
+			 * or being retired right now */
+			g.unlock();
+			std::this_thread::yield();
+		}
 	}
-	while (!c->quarantine.empty() && c->quarantine.front().first < lowest) {
-		const uint32_t slot = c->quarantine.front().second;
-		(slot < c->hot_cap ? c->free_hot : c->free_cold).push_back(slot);
-		c->quarantine.pop_front();
-	}
+	*slot = c->quarantine.front().second;
+	c->quarantine.pop_front();
+	return 0;
 }
 
 } // namespace
@@ -1667,8 +1698,15 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 		comm_destroy(c);
 		(void)hipFree(c->d_totals);
 		(void)hipFree(c->d_delta_own);
-		for (auto &kv : c->d_pk)
-			(void)hipFree(kv.second);
+		{
+			std::lock_guard<std::mutex> g(c->pk_mu);
+			for (auto &kv : c->d_pk) {
+				(void)hipFree(kv.second.p);
+				if (kv.second.last)
+					(void)hipEventDestroy(kv.second.last);
+			}
+			c->d_pk.clear();
+		}
 		(void)hipFree(c->d_ct_keys);
 		(void)hipFree(c->d_ct_vals);
 		(void)hipFree(c->d_ct_count);
@@ -1704,6 +1742,12 @@ static uint64_t pol_hash_sum(uint32_t ep, uint64_t key, const PolEntry &e)
 {
 	const uint64_t h = fnv(1469598103934665603ull ^ ep, &key, 8);
 	return fnv(h, &e.proxy_port, 2);
+}
+
+/* the counter slot a key holds (cgpu_counter_layout_checksum) */
+static uint64_t slot_hash(uint32_t ep, uint64_t key, uint32_t slot)
+{
+	return fnv(fnv(0x51075107ull ^ ep, &key, 8), &slot, 4);
 }
 
 static void ipc_touch(cgpu_ctx *c, const LpmKey<20> &k)
@@ -1851,8 +1895,6 @@ static int pol_update_locked(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *ke
 		/* L3-only {id, 0, 0, dir} and wildcard {0, port, proto, dir} keys
 		 * absorb most hits: give them hot (LDS-accumulated) slots */
 		bool hot = (key->dport == 0 && key->protocol == 0) || key->sec_label == 0;
-		if (c->free_cold.empty() || (hot && c->free_hot.empty()))
-			release_quarantine(c);
 		if (hot && !c->free_hot.empty()) {
 			slot = c->free_hot.back();
 			c->free_hot.pop_back();
@@ -1863,12 +1905,14 @@ static int pol_update_locked(cgpu_ctx *c, uint32_t ep, const cgpu_policy_key *ke
 			c->free_cold.pop_back();
 		} else if (c->next_cold < c->n_ctr_slots) {
 			slot = c->next_cold++;
-		} else {
-			return fail(-E2BIG, "policy device slots exhausted (%u)", c->n_ctr_slots);
+		} else if (int r = take_quarantined(c, &slot)) {
+			return r == -EIO ? fail(-EIO, "waiting for a retired snapshot failed")
+					 : fail(-E2BIG, "policy device slots exhausted (%u)", c->n_ctr_slots);
 		}
 		auto ins = m.emplace(k, PolEntry{e->proxy_port, slot, c->captured + 1}).first;
 		c->pol_total++;
 		c->sum_pol += pol_hash_sum(ep, k, ins->second);
+		c->sum_slots += slot_hash(ep, k, slot);
 	} else {
 		if (flags == CGPU_NOEXIST)
 			return fail(-EEXIST, "policy key exists");
@@ -1905,6 +1949,7 @@ static void pol_erase(cgpu_ctx *c, uint32_t ep, std::map<uint64_t, PolEntry> &m,
 	else
 		(slot < c->hot_cap ? c->free_hot : c->free_cold).push_back(slot);
 	c->sum_pol -= pol_hash_sum(ep, it->first, it->second);
+	c->sum_slots -= slot_hash(ep, it->first, slot);
 	pol_touch(c, ep, it->first);
 	m.erase(it);
 	c->pol_total--;
@@ -2613,7 +2658,7 @@ struct CommitIn {
 	LbIn lb;
 	Lb6In lb6;
 	std::vector<std::pair<uint32_t, cgpu_lxc_info>> lxcinfo;
-	uint64_t sum_ipc = 0, sum_pol = 0;
+	uint64_t sum_ipc = 0, sum_pol = 0, sum_slots = 0;
 };
 
 
@@ -2809,6 +2854,7 @@ static void capture(cgpu_ctx *c, CommitIn &in, const BuildState &b)
 		in.lxcinfo.assign(c->lxcinfo.begin(), c->lxcinfo.end());
 	in.sum_ipc = c->sum_ipc;
 	in.sum_pol = c->sum_pol;
+	in.sum_slots = c->sum_slots;
 	c->dirty = 0;
 	in.id = ++c->captured;
 }
@@ -3222,6 +3268,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	s.ipv4_loopback = cf.ipv4_loopback;
 	memcpy(&s.node_mac_lo, cf.node_mac, 4);
 	s.node_mac_hi = (uint32_t)cf.node_mac[4] | ((uint32_t)cf.node_mac[5] << 8);
+	s.schedule = cf.schedule;
 	s.epoch = e->id;
 	uint64_t sum = 0;
 	for (int k = 0; k < G_N; k++)
@@ -3235,6 +3282,7 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 		c->cur.swap(e); /* e now holds the previous snapshot */
 		c->epoch = s.epoch;
 		c->checksum = sum;
+		c->slot_checksum = in.sum_slots;
 	}
 	e.reset();
 	prev.reset(); /* the last reference retires it (waits + frees on rstream) */
@@ -3254,6 +3302,17 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
 	return 0;
 }
 
+CGPU_EXPORT int cgpu_counter_layout_checksum(cgpu_ctx *c, uint64_t *sum)
+{
+	if (!c || !sum)
+		return fail(-EINVAL, "null argument");
+	std::lock_guard<std::mutex> g(c->pub_mu);
+	if (!c->cur)
+		return fail(-ENOENT, "nothing committed");
+	*sum = c->slot_checksum;
+	return 0;
+}
+
 /* ======================================================================= */
 /* batch entry points                                                        */
 /* ======================================================================= */
@@ -3262,8 +3321,11 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
  * recorded on it tells the snapshot's retirement when these kernels end.
  * Launches never take the mirror lock, so commits (and table updates) do
  * not block them. */
+static const size_t kMaxPkStreams = 16;
+
 struct Pinned {
 	std::shared_ptr<Epoch> ep;
+	cgpu_ctx *c = nullptr;
 	hipStream_t st = nullptr;
 	uint64_t *delta = nullptr, *pk = nullptr;
 	const cgpu_snapshot &snap() const { return ep->snap; }
@@ -3271,6 +3333,12 @@ struct Pinned {
 	{
 		if (!ep)
 			return;
+		if (pk) { /* the stream's packed buffer is free again after this point */
+			std::lock_guard<std::mutex> g(c->pk_mu);
+			auto it = c->d_pk.find((void *)st);
+			if (it != c->d_pk.end() && it->second.p == pk)
+				(void)hipEventRecord(it->second.last, st);
+		}
 		std::lock_guard<std::mutex> g(ep->mu);
 		hipEvent_t ev = nullptr;
 		for (auto &u : ep->used)
@@ -3296,6 +3364,7 @@ static int pin(cgpu_ctx *c, void *stream, Pinned &p, bool want_pk = false)
 	if (!p.ep)
 		return fail(-ENOENT, "no committed snapshot (call cgpu_commit)");
 	p.st = (hipStream_t)stream;
+	p.c = c;
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(hipStreamWaitEvent(p.st, p.ep->ready, 0));
 	std::lock_guard<std::mutex> g(c->pk_mu);
@@ -3303,17 +3372,49 @@ static int pin(cgpu_ctx *c, void *stream, Pinned &p, bool want_pk = false)
 	if (want_pk) {
 		auto it = c->d_pk.find(stream);
 		if (it == c->d_pk.end()) {
-			uint64_t *b = nullptr;
-			const size_t bytes = (size_t)c->n_ctr_slots * 8;
-			HIP_OR_EIO(hipMalloc((void **)&b, bytes));
-			if (hipMemsetAsync(b, 0, bytes, p.st) != hipSuccess) {
-				(void)hipFree(b);
-				return fail(-EIO, "packed counter buffer init failed");
+			cgpu_ctx::PkBuf b;
+			if (c->d_pk.size() >= kMaxPkStreams) {
+				/* recycle the least recently used stream's buffer: zero again
+				 * once that stream's last launch (its unpack) finished */
+				auto lru = c->d_pk.begin();
+				for (auto j = c->d_pk.begin(); j != c->d_pk.end(); ++j)
+					if (j->second.tick < lru->second.tick)
+						lru = j;
+				HIP_OR_EIO(hipEventSynchronize(lru->second.last));
+				b = lru->second;
+				c->d_pk.erase(lru);
+			} else {
+				const size_t bytes = (size_t)c->n_ctr_slots * 8;
+				HIP_OR_EIO(hipMalloc((void **)&b.p, bytes));
+				if (hipMemset(b.p, 0, bytes) != hipSuccess ||
+				    hipEventCreateWithFlags(&b.last, hipEventDisableTiming) != hipSuccess) {
+					(void)hipFree(b.p);
+					return fail(-EIO, "packed counter buffer init failed");
+				}
 			}
 			it = c->d_pk.emplace(stream, b).first;
 		}
-		p.pk = it->second;
+		it->second.tick = ++c->pk_tick;
+		p.pk = it->second.p;
 	}
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_stream_release(cgpu_ctx *c, void *stream)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (c->device < 0)
+		return 0;
+	std::lock_guard<std::mutex> g(c->pk_mu);
+	auto it = c->d_pk.find(stream);
+	if (it == c->d_pk.end())
+		return 0;
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipEventSynchronize(it->second.last));
+	(void)hipFree(it->second.p);
+	(void)hipEventDestroy(it->second.last);
+	c->d_pk.erase(it);
 	return 0;
 }
 
@@ -3587,8 +3688,11 @@ CGPU_EXPORT int cgpu_counters_reset(cgpu_ctx *c)
 	HIP_OR_EIO(hipDeviceSynchronize());
 	HIP_OR_EIO(hipMemset(c->d_totals, 0, bytes));
 	HIP_OR_EIO(hipMemset(c->d_delta, 0, bytes));
-	for (auto &kv : c->d_pk)
-		HIP_OR_EIO(hipMemset(kv.second, 0, (size_t)c->n_ctr_slots * 8));
+	{
+		std::lock_guard<std::mutex> pg(c->pk_mu);
+		for (auto &kv : c->d_pk)
+			HIP_OR_EIO(hipMemset(kv.second.p, 0, (size_t)c->n_ctr_slots * 8));
+	}
 	HIP_OR_EIO(hipDeviceSynchronize());
 	return 0;
 }

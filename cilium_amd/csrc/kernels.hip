@@ -2399,13 +2399,6 @@ unsigned grid_for(uint64_t n)
 
 } // namespace
 
-/* CGPU_CLASSIFY_VARIANT: the classify schedule (see launch_classify). */
-static int classify_variant()
-{
-	const char *v = getenv("CGPU_CLASSIFY_VARIANT");
-	return v ? atoi(v) : 8;
-}
-
 /* k_classify_x4 reads columns as 4/8/16-byte vectors at tuple index
  * multiples of 4: the column base pointers must be aligned to match. */
 static bool x4_aligned(const cls_args &a)
@@ -2465,7 +2458,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 	/* the cold-slot cache takes the LDS one workgroup per CU leaves free
 	 * (the resident grid runs one 1024-thread workgroup per CU) */
 	uint32_t cc_n = 0;
-	if (!getenv("CGPU_NO_CCACHE"))
+	if (!(s.schedule & CGPU_SCHED_NO_CCACHE))
 		for (uint32_t n = 1u << 14; n >= 512u && !cc_n; n >>= 1)
 			if (lds + (size_t)n * 12u <= X4_LDS_BUDGET)
 				cc_n = n;
@@ -2508,22 +2501,21 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
 	return hipGetLastError();
 }
 
-/* CGPU_CLASSIFY_VARIANT selects the schedule (A/B in one process); every
- * variant computes the reference's results (tests/test_gpu_parity.py):
- *   8 (default): k_classify_x4 -- four tuples per lane, vector column
- *      loads, LDS hot counters + one packed atomic per cold hit, resident
- *      grid (needs aligned columns, else 3)
- *   3 (fallback): one tuple per lane, LDS hot counters
- *   0: global atomics for every hit, 256-thread workgroups */
+/* The context's cgpu_config.schedule selects the schedule (every schedule
+ * computes the reference's results, tests/test_gpu_parity.py):
+ *   default: k_classify_x4 -- four tuples per lane, vector column loads, LDS
+ *      hot counters + one packed atomic per cold hit, resident grid (needs
+ *      aligned columns, else the per-lane kernel)
+ *   CGPU_SCHED_PER_LANE: one tuple per lane, LDS hot counters
+ *   CGPU_SCHED_GLOBAL_CTR: global atomics for every hit, 256-thread workgroups */
 template <int V6>
 static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_t st)
 {
-	const int var = classify_variant();
-	if (var == 0) {
+	if (s.schedule & CGPU_SCHED_GLOBAL_CTR) {
 		hipLaunchKernelGGL((k_classify<V6, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
 		return hipGetLastError();
 	}
-	if (var == 8 && a.pk && x4_aligned(a)) {
+	if (!(s.schedule & CGPU_SCHED_PER_LANE) && a.pk && x4_aligned(a)) {
 		if (V6)
 			return a.lb ? launch_x4<true, true>(s, a, st) : launch_x4<false, true>(s, a, st);
 		return a.lb ? launch_x4<true, false>(s, a, st) : launch_x4<false, false>(s, a, st);
@@ -2533,8 +2525,7 @@ static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_
 	constexpr int NT = 1024;
 	const size_t lds = (size_t)s.hot_slots * 8u;
 	const uint64_t cap = 2ull * 256ull;
-	/* packed cold counters: <= PKC_CHUNK frames between unpacks */
-	const uint64_t per_launch = std::min<uint64_t>(cap * (1ull << 22), PKC_CHUNK);
+	const uint64_t per_launch = cap * (1ull << 22); /* k_classify<.., 1, ..> never touches pk */
 	for (uint64_t off = 0; off < a.n; off += per_launch) {
 		cls_args c = a;
 		const uint64_t m = std::min<uint64_t>(a.n - off, per_launch);
@@ -2600,10 +2591,10 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 	/* stage the deepest cover levels that fit next to the bloom filter */
 	const size_t bloom = (size_t)(s.ep6_bloom_mask + 1u) * 4u;
 	const size_t l2 = (size_t)COVER6_RBITS_WORDS * 4u + (size_t)s.pf6.n_b24 * 512u;
-	/* CGPU_PF6_LDS caps the mode (every mode computes the same verdicts;
-	 * tests/test_gpu_parity.py runs each) */
-	const char *cap = getenv("CGPU_PF6_LDS");
-	const int max_mode = cap ? atoi(cap) : 2;
+	/* CGPU_SCHED_PF6_LDS caps the mode (every mode computes the same
+	 * verdicts; tests/test_gpu_parity.py runs each) */
+	const uint32_t cap = (s.schedule >> 4) & 3u;
+	const int max_mode = cap ? (int)cap - 1 : 2;
 	int mode = 0;
 	size_t lds = bloom;
 	if (max_mode >= 2 && s.pf6.rbits && bloom + l2 <= LDS_MAX) {
@@ -2639,7 +2630,10 @@ hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, 
 	constexpr int NT = 1024;
 	const size_t lds = (size_t)s.hot_slots * 8u;
 	const uint64_t cap = 2ull * 256ull;
-	const uint64_t per_launch = cap * (1ull << 22);
+	/* cold-slot hits go to the packed per-stream accumulator pk, exact for
+	 * <= PKC_CHUNK frames between unpacks */
+	const uint64_t per_launch = std::min<uint64_t>(cap * (1ull << 22), PKC_CHUNK);
+	static_assert(PKC_CHUNK <= 512ull * (1ull << 22), "frames chunk within the LDS packing bound");
 	for (uint64_t off = 0; off < a.n; off += per_launch) {
 		frames_args c = a;
 		const uint64_t m = std::min<uint64_t>(a.n - off, per_launch);
@@ -3464,14 +3458,11 @@ template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapsho
 	}
 }
 
-static int ct_sort_bits()
+/* group-key bits the conntrack radix sort orders (CGPU_SCHED_CT_SORT_BITS) */
+static int ct_sort_bits(const cgpu_snapshot &s)
 {
-	static int bits = -1;
-	if (bits < 0) {
-		const char *e = getenv("CGPU_CT_SORT_BITS"); /* diagnostic override */
-		bits = e ? std::max(8, std::min(32, atoi(e))) : 24;
-	}
-	return bits;
+	const int b = (int)((s.schedule >> 8) & 63u);
+	return b ? std::max(8, std::min(32, b)) : 24;
 }
 
 /* hipcub temporary storage for the sort and the head selection of n packets */
@@ -3499,10 +3490,10 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 	/* 24 key bits: three passes; pairs sharing a 24-bit hash merge into
 	 * one group, which only lengthens that lane's walk */
 	hipError_t e = hipcub::DeviceRadixSort::SortPairs(L.temp, tb, L.gkey, L.gkey_sorted, L.idx,
-							   L.idx_sorted, (int)L.n, 0, ct_sort_bits(), st);
+							   L.idx_sorted, (int)L.n, 0, ct_sort_bits(s), st);
 	if (e != hipSuccess)
 		return e;
-	const int bits = ct_sort_bits();
+	const int bits = ct_sort_bits(s);
 	const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
 	hipLaunchKernelGGL(k_ct_heads, dim3(g), dim3(256), 0, st, L.gkey_sorted, L.head, L.n, mask);
 	hipcub::CountingInputIterator<uint32_t> it(0);

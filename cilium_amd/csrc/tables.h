@@ -426,6 +426,7 @@ typedef struct cgpu_snapshot {
 	const uint4 *lxc;
 	uint32_t n_lxc;
 	uint32_t node_mac_lo, node_mac_hi; /* bytes 0-3, 4-5 of NODE_MAC (LE words) */
+	uint32_t schedule;       /* cgpu_config.schedule (CGPU_SCHED_*) */
 	uint64_t epoch;
 } cgpu_snapshot;
 

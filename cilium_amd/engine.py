@@ -343,6 +343,11 @@ class Engine:
         check(self.L.cgpu_table_checksum(self.h, C.byref(s)), "cgpu_table_checksum")
         return s.value
 
+    def counter_layout_checksum(self) -> int:
+        s = C.c_uint64()
+        check(self.L.cgpu_counter_layout_checksum(self.h, C.byref(s)), "cgpu_counter_layout_checksum")
+        return s.value
+
     # -------------------------------------------------------------- batches
     def classify_v4(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
         """t: dict of CUDA tensors saddr/daddr (int32 view of network-order
@@ -553,6 +558,10 @@ class Engine:
         check(self.L.cgpu_metrics_read(self.h, out.ctypes.data_as(C.c_void_p)),
               "cgpu_metrics_read")
         return out
+
+    def stream_release(self, stream) -> None:
+        """cgpu_stream_release: free the stream's packed counter buffer."""
+        check(self.L.cgpu_stream_release(self.h, _stream(stream)), "cgpu_stream_release")
 
     def counters_reset(self) -> None:
         check(self.L.cgpu_counters_reset(self.h), "cgpu_counters_reset")

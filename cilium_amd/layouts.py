@@ -92,6 +92,10 @@ PKT_OK, PKT_TRUNCATED, PKT_NOT_IP = 0, 1, 2
 CT4_TUPLE = np.dtype([("daddr", "<u4"), ("saddr", "<u4"), ("dport", "<u2"), ("sport", "<u2"),
                       ("nexthdr", "u1"), ("flags", "u1")])
 assert CT4_TUPLE.itemsize == 14
+# struct ipv6_ct_tuple (common.h:338-346), packed, 38 B
+CT6_TUPLE = np.dtype([("daddr", "u1", 16), ("saddr", "u1", 16), ("dport", "<u2"), ("sport", "<u2"),
+                      ("nexthdr", "u1"), ("flags", "u1")])
+assert CT6_TUPLE.itemsize == 38
 CT_ENTRY = np.dtype([("rx_packets", "<u8"), ("rx_bytes", "<u8"), ("tx_packets", "<u8"),
                      ("tx_bytes", "<u8"), ("lifetime", "<u4"), ("bits", "<u2"),
                      ("rev_nat_index", "<u2"), ("slave", "<u2"), ("tx_flags_seen", "u1"),
@@ -110,7 +114,7 @@ CT_MAX_GLOBAL = 1000000  # pkg/maps/ctmap/ctmap.go:101 MapNumEntriesGlobal
 
 def ct_sorted(keys: np.ndarray, vals: np.ndarray):
     """Dump of a CT map in a canonical order (key bytes) for comparisons."""
-    kb = np.ascontiguousarray(keys).view(np.uint8).reshape(len(keys), 14)
+    kb = np.ascontiguousarray(keys).view(np.uint8).reshape(len(keys), keys.dtype.itemsize)
     order = np.lexsort(kb.T[::-1])
     return keys[order], vals[order]
 

@@ -17,20 +17,48 @@ import numpy as np
 
 
 def flowhash_np(saddr, daddr, sport, dport, proto) -> np.ndarray:
-    """Deterministic 32-bit flow hash (murmur3 finalizer over the 5-tuple).
-    Direction-sensitive, like skb->hash for the reference's RSS spreading."""
-    h = (saddr.astype(np.uint64) * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
-    h ^= daddr.astype(np.uint64)
-    h = (h * np.uint64(0x85EBCA77)) & np.uint64(0xFFFFFFFF)
-    h ^= (sport.astype(np.uint64) << np.uint64(16)) | dport.astype(np.uint64)
-    h = (h * np.uint64(0xC2B2AE3D)) & np.uint64(0xFFFFFFFF)
-    h ^= proto.astype(np.uint64)
-    h ^= h >> np.uint64(16)
-    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
-    h ^= h >> np.uint64(13)
-    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
-    h ^= h >> np.uint64(16)
-    return h.astype(np.uint32)
+    """Deterministic 32-bit flow hash (murmur3 finalizer over the 5-tuple),
+    cgpu_flow_hash.  Direction-sensitive, like skb->hash for the reference's
+    RSS spreading.  uint32 arithmetic wraps mod 2^32."""
+    with np.errstate(over="ignore"):
+        h = np.asarray(saddr).astype(np.uint32) * np.uint32(0x9E3779B1)
+        h ^= np.asarray(daddr).astype(np.uint32)
+        h *= np.uint32(0x85EBCA77)
+        h ^= (np.asarray(sport).astype(np.uint32) << np.uint32(16)) | np.asarray(dport).astype(np.uint32)
+        h *= np.uint32(0xC2B2AE3D)
+        h ^= np.asarray(proto).astype(np.uint32)
+        h ^= h >> np.uint32(16)
+        h *= np.uint32(0x85EBCA6B)
+        h ^= h >> np.uint32(13)
+        h *= np.uint32(0xC2B2AE35)
+        h ^= h >> np.uint32(16)
+    return h
+
+
+def assign_shard_sports(t: dict, world: int, rank: int, seed: int) -> np.ndarray:
+    """Source ports that put every tuple of `t` on `rank`: the tuple's own
+    sport (or a uniform draw when it has none), redrawn for the tuples whose
+    flowhash(5-tuple) % world != rank.  Rank r's batch is then exactly its
+    flowhash shard of the stream the ranks generate together (config 4: the
+    stream sharded by flowhash % N)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = len(t["saddr"])
+    if "sport" in t:
+        sport = np.array(t["sport"], np.uint16)
+    else:
+        sport = rng.integers(1024, 65536, n).astype(np.uint16)
+    if world == 1:
+        return sport
+    todo = np.arange(n)
+    h = flowhash_np(t["saddr"], t["daddr"], sport, t["dport"], t["proto"])
+    todo = todo[(h % np.uint32(world)) != rank]
+    sport[todo] = rng.integers(1024, 65536, len(todo)).astype(np.uint16)
+    while len(todo):
+        h = flowhash_np(t["saddr"][todo], t["daddr"][todo], sport[todo], t["dport"][todo],
+                        t["proto"][todo])
+        todo = todo[(h % np.uint32(world)) != rank]
+        sport[todo] = rng.integers(1024, 65536, len(todo)).astype(np.uint16)
+    return sport
 
 
 def _fmix_np(h):
@@ -100,10 +128,30 @@ def take(t: dict, idx) -> dict:
     return {k: np.ascontiguousarray(v[idx]) for k, v in t.items()}
 
 
+def init_counter_comm(engine, rank: int, world: int, group=None) -> None:
+    """Join the engine's counter communicator (cgpu_comm_id_create /
+    cgpu_comm_init, RCCL linked into libcgpu.so): rank 0 creates the id and
+    hands it to the other ranks over `group` -- the out-of-band channel the
+    agent would use.  Collective: returns once every rank joined."""
+    import torch.distributed as dist
+    box = [engine.comm_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0, group=group)
+    engine.comm_init(box[0], world, rank)
+
+
+def reduce_counters(engine, world: int, stream=None) -> None:
+    """The per-step counter reduction of the sharded stream: the RCCL u64
+    SUM of every rank's delta buffer (cgpu_counters_allreduce), after which
+    each rank's cgpu_counter_fold adds the same global delta to its totals.
+    Nothing to do for one rank."""
+    if world > 1:
+        engine.counters_allreduce(stream)
+
+
 def allreduce_counters(delta, group=None):
-    """SUM the int64 counter delta across ranks in place (RCCL on GPU
-    tensors, gloo on CPU tensors).  u64 counters travel as their int64 bit
-    pattern: two's-complement addition is the same modulo 2^64."""
+    """The same SUM over torch tensors, for the CPU restatement's counters in
+    the gloo tests (tests/test_multi_gloo.py): u64 counters travel as their
+    int64 bit pattern (two's-complement addition is the same mod 2^64)."""
     import torch.distributed as dist
     dist.all_reduce(delta, op=dist.ReduceOp.SUM, group=group)
     return delta

@@ -777,17 +777,20 @@ def make_ct_stream(rng, n_conn: int, locals_be: np.ndarray, remotes_be: np.ndarr
     with others but stay in order.  Columns as cgpu_classify_v4_ct takes
     them: saddr, daddr, sport, dport (network order), proto, l4b (TCP header
     bytes 12-13 as a little-endian u16, or the ICMP type), flags (CGPU_F_EGRESS | CGPU_F_FRAGMENT), len, ep."""
+    v6 = np.asarray(locals_be).ndim == 2  # (n, 16) uint8 addresses: IPv6 / ICMPv6
+    adt = np.uint8 if v6 else np.uint32
     E = len(locals_be)
     ep = rng.integers(0, E, n_conn)
-    loc = np.asarray(locals_be, np.uint32)[ep]
-    rem = np.asarray(remotes_be, np.uint32)[rng.integers(0, len(remotes_be), n_conn)]
+    loc = np.asarray(locals_be, adt)[ep]
+    rem = np.asarray(remotes_be, adt)[rng.integers(0, len(remotes_be), n_conn)]
     if pair_ok is not None:  # e.g. this rank's conntrack shard: redraw the others
         bad = ~pair_ok(loc, rem)
         while bad.any():
-            rem[bad] = np.asarray(remotes_be, np.uint32)[rng.integers(0, len(remotes_be), int(bad.sum()))]
+            rem[bad] = np.asarray(remotes_be, adt)[rng.integers(0, len(remotes_be), int(bad.sum()))]
             bad[bad] = ~pair_ok(loc[bad], rem[bad])
+    icmp = 58 if v6 else 1
     u = rng.random(n_conn)
-    cproto = np.select([u < 0.70, u < 0.90, u < 1.0 - other_frac], [6, 17, 1], 47).astype(np.uint8)
+    cproto = np.select([u < 0.70, u < 0.90, u < 1.0 - other_frac], [6, 17, icmp], 47).astype(np.uint8)
     init_eg = rng.random(n_conn) < 0.6
     eph = rng.integers(1024, 65536, n_conn)
     well = zipf_ports(rng, n_conn)
@@ -809,23 +812,30 @@ def make_ct_stream(rng, n_conn: int, locals_be: np.ndarray, remotes_be: np.ndarr
     r2 = rng.random(total)
     tcpf = np.where(last & (j > 0) & (r2 < 0.3), L.TCP_FIN | L.TCP_ACK, tcpf)
     tcpf = np.where(last & (j > 0) & (r2 > 0.95), L.TCP_RST, tcpf)
-    # ICMP: echo request (8, some timestamp 13) one way, echo reply (0) back
-    icmpt = np.where(orig, np.where(r < 0.9, 8, 13), 0)
+    # ICMP: echo request (8, some timestamp 13) one way, echo reply (0) back;
+    # ICMPv6: echo request 128 (some 133, a router solicitation), reply 129
+    if v6:
+        icmpt = np.where(orig, np.where(r < 0.9, 128, 133), 129)
+        errt = np.array([1, 2, 3, 4])  # DEST_UNREACH, PKT_TOOBIG, TIME_EXCEED, PARAMPROB
+    else:
+        icmpt = np.where(orig, np.where(r < 0.9, 8, 13), 0)
+        errt = np.array([3, 11, 12])
     # errors related to any connection, in the reply direction
     err = ~orig & (rng.random(total) < icmp_err_frac)
-    proto = np.where(err, 1, proto).astype(np.uint8)
-    icmpt = np.where(err, rng.choice(np.array([3, 11, 12]), total), icmpt)
+    proto = np.where(err, icmp, proto).astype(np.uint8)
+    icmpt = np.where(err, rng.choice(errt, total), icmpt)
     # TCP: header bytes 12-13 as loaded (doff << 4, NS bit sometimes set | flags << 8)
     ns = (rng.random(total) < 0.02).astype(np.int64)
     tcpw = (5 << 4) | ns | (tcpf.astype(np.int64) << 8)
-    l4b = np.where(proto == 6, tcpw, np.where(proto == 1, icmpt, 0)).astype(np.uint16)
+    l4b = np.where(proto == 6, tcpw, np.where(proto == icmp, icmpt, 0)).astype(np.uint16)
     lc, rc = loc[conn], rem[conn]
-    saddr = np.where(egress, lc, rc).astype(np.uint32)
-    daddr = np.where(egress, rc, lc).astype(np.uint32)
+    eg = egress[:, None] if v6 else egress
+    saddr = np.where(eg, lc, rc).astype(adt)
+    daddr = np.where(eg, rc, lc).astype(adt)
     lp, rp = lport[conn].byteswap(), rport[conn].byteswap()
     sport = np.where(egress, lp, rp).astype(np.uint16)
     dport = np.where(egress, rp, lp).astype(np.uint16)
-    frag = (~egress) & (rng.random(total) < frag_frac)
+    frag = (~egress) & (rng.random(total) < frag_frac) & (not v6)
     # interleave: connection start + in-connection gaps, stable by time
     t = rng.random(n_conn)[conn] + span * (j + rng.random(total)) / k[conn]
     order = np.argsort(t, kind="stable")

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CGPU_ABI_VERSION 1u
+#define CGPU_ABI_VERSION 2u
 
 /* bpf(2) update flags (include/uapi/linux/bpf.h) */
 #define CGPU_ANY 0u
@@ -160,8 +160,23 @@ typedef struct cgpu_config {
 	 * holds (MapNumEntriesGlobal 1000000, pkg/maps/ctmap/ctmap.go:101);
 	 * device slots are 2x this, rounded up to a power of two */
 	uint32_t ct_max;
-	uint32_t reserved[1];
+	/* schedule overrides, CGPU_SCHED_* (0 = the tuned default).  Every
+	 * schedule computes the same results; they exist for the parity tests of
+	 * the fallback kernels and for A/B timing, and are fixed per context (no
+	 * behaviour is read from the environment). */
+	uint32_t schedule;
+	/* CT_MAP_SIZE of cilium_ct6_global (0 = ct_max) */
+	uint32_t ct6_max;
+	uint32_t reserved[2];
 } cgpu_config;
+
+#define CGPU_SCHED_PER_LANE 1u   /* classify: one tuple per lane (k_classify) instead of x4 */
+#define CGPU_SCHED_GLOBAL_CTR 2u /* classify: per-lane kernel, one global atomic per hit */
+#define CGPU_SCHED_NO_CCACHE 4u  /* x4 classify without the LDS cold-slot cache */
+/* bits 4-5: v6 prefilter LDS staging mode + 1 (0 = the deepest that fits) */
+#define CGPU_SCHED_PF6_LDS(mode) ((((uint32_t)(mode)) + 1u) << 4)
+/* bits 8-13: conntrack group-key radix sort bits (8..32; 0 = 24) */
+#define CGPU_SCHED_CT_SORT_BITS(b) (((uint32_t)(b)) << 8)
 
 #define CGPU_LB_L3 1u
 #define CGPU_LB_L4 2u
@@ -378,6 +393,12 @@ int cgpu_commit(cgpu_ctx *ctx, uint64_t *epoch_out);
 /* order-independent checksum of the committed table contents; replicas on
  * different GPUs/ranks holding the same tables report the same value */
 int cgpu_table_checksum(cgpu_ctx *ctx, uint64_t *sum_out);
+/* checksum of which counter slot every committed policy key holds.  Slot
+ * assignment is a function of the sequence of map operations and commits
+ * only (never of GPU progress), so replicas that applied the same sequence
+ * agree; ranks compare it before cgpu_counters_allreduce, which sums the
+ * delta buffers slot by slot. */
+int cgpu_counter_layout_checksum(cgpu_ctx *ctx, uint64_t *sum_out);
 
 /* ------------------------------------------------------------------ */
 /* batch classification (device pointers)                              */
@@ -828,6 +849,13 @@ int cgpu_counter_fold(cgpu_ctx *ctx, void *stream);
 /* out: [256][4][2] u64 {count, bytes} (folds and synchronizes first) */
 int cgpu_metrics_read(cgpu_ctx *ctx, uint64_t *out);
 int cgpu_counters_reset(cgpu_ctx *ctx);
+/* Classify launches keep a packed counter accumulator of 8 B per policy
+ * slot (policy_max_total x 8 B of HBM) for each stream they ran on, at most
+ * 16 of them; a 17th stream recycles the least recently used one after that
+ * stream's last launch finished.  A caller that is done with a stream (e.g.
+ * before hipStreamDestroy) releases its buffer here; waits for the stream's
+ * last launch of this context. */
+int cgpu_stream_release(cgpu_ctx *ctx, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* multi-GPU counter reduction (consumer: the agent's      */

@@ -357,6 +357,8 @@ struct or_ctx {
 	uint8_t *lxcinfo;           /* [n_lxcinfo][32] per-endpoint identity */
 	size_t n_lxcinfo;
 	struct ohash ct;            /* ipv4_ct_tuple (14 B) -> ct_entry (56 B) */
+	struct ohash ct6;           /* ipv6_ct_tuple (38 B) -> ct_entry (56 B) */
+	size_t ct6_max;
 	size_t ct_max;              /* CT_MAP_SIZE */
 	uint64_t metrics[N_METRICS];
 };
@@ -400,7 +402,9 @@ or_ctx *or_create(void)
 	oh_init(&c->lb, 8, 12);
 	oh_init(&c->lb6, 20, 24);
 	oh_init(&c->ct, 14, 56);
+	oh_init(&c->ct6, 38, 56);
 	c->ct_max = 1000000; /* ctmap.go:101 MapNumEntriesGlobal */
+	c->ct6_max = 1000000;
 	return c;
 }
 
@@ -416,6 +420,7 @@ void or_destroy(or_ctx *c)
 	oh_destroy(&c->lxc);
 	oh_destroy(&c->lb);
 	oh_destroy(&c->ct);
+	oh_destroy(&c->ct6);
 	for (size_t i = 0; i < c->n_ep; i++)
 		oh_destroy(&c->policy[i]);
 	free(c->policy);
@@ -1977,15 +1982,14 @@ static inline int ct_alive(const struct ct_val *e)
 	return !(e->bits & CTB_RX_CLOSING) || !(e->bits & CTB_TX_CLOSING);
 }
 
-/* __ct_lookup, conntrack.h:198-259: 1 = found (entry updated), 0 = miss */
-static int ct_lookup_one(or_ctx *c, const struct ct_key *k, int action, int dir, int tcp,
-			 uint16_t w, uint32_t len, uint32_t now)
+/* __ct_lookup, conntrack.h:198-259, on the raw key of either map: 1 =
+ * found (entry updated), 0 = miss */
+static int ct_lookup_kb(struct ohash *m, const uint8_t *kb, int action, int dir, int tcp,
+			uint16_t w, uint32_t len, uint32_t now)
 {
-	uint8_t kb[14];
 	uint8_t *p;
 	struct ct_val e;
-	ct_key_bytes(k, kb);
-	p = oh_get(&c->ct, kb);
+	p = oh_get(m, kb);
 	if (!p)
 		return 0;
 	memcpy(&e, p, 56);
@@ -2010,6 +2014,14 @@ static int ct_lookup_one(or_ctx *c, const struct ct_key *k, int action, int dir,
 	}
 	memcpy(p, &e, 56);
 	return 1;
+}
+
+static int ct_lookup_one(or_ctx *c, const struct ct_key *k, int action, int dir, int tcp,
+			 uint16_t w, uint32_t len, uint32_t now)
+{
+	uint8_t kb[14];
+	ct_key_bytes(k, kb);
+	return ct_lookup_kb(&c->ct, kb, action, dir, tcp, w, len, now);
 }
 
 static void ct_reverse(struct ct_key *k)
@@ -2302,5 +2314,270 @@ int or_l3_compile(const void *selectors, const void *reqs, const uint32_t *value
 					  (!(flags & 2u) || dec[1] == 1 ? 2 : 0));
 		}
 	}
+	return 0;
+}
+
+/* ====================================================================== */
+/* IPv6 conntrack (CT_MAP6, bpf_lxc.c:53-63): ct_lookup6 conntrack.h:288-412, */
+/* ct_create6 :588-639, ct_delete6 :564-570, in the order of               */
+/* ipv6_l3_from_lxc (bpf_lxc.c:108-203) and ipv6_policy (:731-800)          */
+/* ====================================================================== */
+#define PROTO_ICMPV6_ 58
+
+/* struct ipv6_ct_tuple, common.h:338-346 (38 B, packed) */
+struct ct6_key {
+	uint8_t daddr[16], saddr[16];
+	uint16_t dport, sport;
+	uint8_t nexthdr, flags;
+} __attribute__((packed));
+_Static_assert(sizeof(struct ct6_key) == 38, "ipv6_ct_tuple layout");
+
+void or_ct6_set_max(or_ctx *c, size_t max_elem) { c->ct6_max = max_elem; }
+size_t or_ct6_count(or_ctx *c) { return c->ct6.n; }
+
+int or_ct6_update(or_ctx *c, const void *key38, const void *val56)
+{
+	if (!oh_get(&c->ct6, key38) && c->ct6.n >= c->ct6_max)
+		return -E2BIG;
+	return oh_update(&c->ct6, key38, val56);
+}
+
+int or_ct6_delete(or_ctx *c, const void *key38) { return oh_delete(&c->ct6, key38); }
+
+int or_ct6_lookup(or_ctx *c, const void *key38, void *val56_out)
+{
+	const uint8_t *v = oh_get(&c->ct6, key38);
+	if (!v)
+		return -ENOENT;
+	memcpy(val56_out, v, 56);
+	return 0;
+}
+
+size_t or_ct6_dump(or_ctx *c, void *keys38, void *vals56, size_t max)
+{
+	size_t k = 0;
+	for (size_t i = 0; i < c->ct6.cap && k < max; i++) {
+		if (!c->ct6.used[i])
+			continue;
+		memcpy((uint8_t *)keys38 + k * 38, c->ct6.keys + i * 38, 38);
+		memcpy((uint8_t *)vals56 + k * 56, c->ct6.vals + i * 56, 56);
+		k++;
+	}
+	return k;
+}
+
+size_t or_ct6_gc(or_ctx *c, uint32_t time)
+{
+	size_t del = 0;
+	for (int again = 1; again;) {
+		again = 0;
+		for (size_t i = 0; i < c->ct6.cap; i++) {
+			struct ct_val v;
+			uint8_t key[38];
+			if (!c->ct6.used[i])
+				continue;
+			memcpy(&v, c->ct6.vals + i * 56, 56);
+			if (v.lifetime < time) {
+				memcpy(key, c->ct6.keys + i * 38, 38);
+				oh_delete(&c->ct6, key);
+				del++;
+				again = 1;
+				break;
+			}
+		}
+	}
+	return del;
+}
+
+/* ipv6_ct_tuple_reverse, conntrack.h:265-285 */
+static void ct6_reverse(struct ct6_key *k)
+{
+	uint8_t a[16];
+	uint16_t p = k->sport;
+	memcpy(a, k->saddr, 16);
+	memcpy(k->saddr, k->daddr, 16);
+	memcpy(k->daddr, a, 16);
+	k->sport = k->dport;
+	k->dport = p;
+	k->flags ^= TUPLE_F_IN;
+}
+
+/* ct_create6, conntrack.h:588-639 (no service: slave 0, no loopback) */
+static int ct6_create(or_ctx *c, const struct ct6_key *k, int dir, uint32_t src_sec_id,
+		      uint16_t rev_nat, uint32_t len, uint32_t now, uint64_t *ops)
+{
+	struct ct_val e;
+	struct ct6_key ik;
+	int tcp = k->nexthdr == PROTO_TCP;
+	memset(&e, 0, sizeof(e));
+	e.rev_nat_index = rev_nat;
+	ct_timeout(&e, now, tcp, dir, tcp ? 1u : 0u); /* seen_flags.syn = is_tcp: bit 0 */
+	if (dir == CT_INGRESS) {
+		e.rx_packets = 1;
+		e.rx_bytes = len;
+	} else {
+		e.tx_packets = 1;
+		e.tx_bytes = len;
+	}
+	e.src_sec_id = src_sec_id;
+	*ops += 1;
+	if (or_ct6_update(c, k, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	memset(&ik, 0, sizeof(ik));
+	memcpy(ik.daddr, k->daddr, 16);
+	memcpy(ik.saddr, k->saddr, 16);
+	ik.nexthdr = PROTO_ICMPV6_;
+	ik.flags = k->flags | TUPLE_F_RELATED;
+	e.bits |= CTB_SEEN_NON_SYN;
+	*ops += 1;
+	if (or_ct6_update(c, &ik, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	return 0;
+}
+
+/*
+ * Stateful IPv6 classification, packets in order; see cgpu.h
+ * cgpu_classify_v6_ct and oracle/ref/harness_ct.c ref_ct_classify_v6.
+ * l4b: TCP header bytes 12-13 or the ICMPv6 type.
+ */
+int or_classify_v6_ct(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+		      const uint16_t *ep, uint32_t now, int32_t *verdict, uint8_t *ct_ret,
+		      uint32_t *identity, uint8_t *stage, uint64_t *probe_sum)
+{
+	const or_config *cfg = &c->cfg;
+	uint64_t ops = 0;
+	for (size_t i = 0; i < n; i++) {
+		int egress = flags[i] & 1;
+		int dir = egress ? CT_EGRESS : CT_INGRESS;
+		int mdir = egress ? METRIC_EGRESS : METRIC_INGRESS;
+		uint8_t pr = proto[i];
+		const uint8_t *sa = saddr16 + 16 * i, *da = daddr16 + 16 * i;
+		struct ohash *h = ep[i] < c->n_ep ? &c->policy[ep[i]] : NULL;
+		struct ct6_key k;
+		int action = ACTION_UNSPEC, tcp = pr == PROTO_TCP, ret;
+		uint16_t w = 0, rev_nat = 0;
+		int32_t v, fin;
+		uint32_t id;
+		struct pol_res r;
+
+		memset(&k, 0, sizeof(k));
+		memcpy(k.daddr, da, 16);
+		memcpy(k.saddr, sa, 16);
+		k.nexthdr = pr;
+		k.flags = egress ? TUPLE_F_IN : TUPLE_F_OUT;
+		if (!egress) { /* ipv6_policy: daddr.s6_addr32[3] & 0xFFFF (bpf_lxc.c:748) */
+			rev_nat = (uint16_t)(da[12] | (da[13] << 8));
+		}
+		if (pr == PROTO_ICMPV6_) {
+			uint8_t type = (uint8_t)l4b[i];
+			if (type >= 1 && type <= 4) { /* DEST_UNREACH, PKT_TOOBIG, TIME_EXCEED, PARAMPROB */
+				k.flags |= TUPLE_F_RELATED;
+			} else if (type == 129) { /* ECHO_REPLY */
+				k.dport = 128;    /* ICMPV6_ECHO_REQUEST */
+			} else {
+				if (type == 128)
+					k.sport = 128;
+				action = ACTION_CREATE;
+			}
+		} else if (pr == PROTO_TCP || pr == PROTO_UDP) {
+			k.dport = sport[i];
+			k.sport = dport[i];
+			if (tcp) {
+				w = l4b[i];
+				action = TF_BIT0(w) ? ACTION_CLOSE : ACTION_CREATE;
+			} else {
+				action = ACTION_CREATE;
+			}
+		} else {
+			verdict[i] = DROP_CT_UNKNOWN_PROTO;
+			ct_ret[i] = 255;
+			if (identity)
+				identity[i] = 0;
+			if (stage)
+				stage[i] = 4;
+			c->metrics[(137 * 4 + mdir) * 2] += 1;
+			c->metrics[(137 * 4 + mdir) * 2 + 1] += len[i];
+			continue;
+		}
+		ops += 1;
+		if (ct_lookup_kb(&c->ct6, (const uint8_t *)&k, action, dir, tcp, w, len[i], now)) {
+			ret = (k.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+		} else {
+			ct6_reverse(&k);
+			ops += 1;
+			ret = ct_lookup_kb(&c->ct6, (const uint8_t *)&k, action, dir, tcp, w, len[i], now)
+				      ? CT_ESTABLISHED : CT_NEW;
+		}
+
+		if (egress) { /* bpf_lxc.c:170-191 */
+			const uint8_t *info = ipcache6(c, da);
+			uint32_t label = 0;
+			if (info)
+				memcpy(&label, info, 4);
+			if (info && label)
+				id = label;
+			else if (!memcmp(da, cfg->router_ip, 8))
+				id = cfg->cluster_id;
+			else
+				id = cfg->world_id;
+			ops += 1;
+			r = policy_access(h, id, k.dport, pr, 1, 0, len[i]);
+		} else { /* bpf_netdev.c:203-211 */
+			uint32_t src = cfg->ingress_src_identity;
+			if (src < cfg->health_id) {
+				const uint8_t *info = ipcache6(c, sa);
+				ops += 1;
+				if (info) {
+					uint32_t label;
+					memcpy(&label, info, 4);
+					if (label && label != cfg->cluster_id)
+						src = label;
+				}
+			}
+			id = src;
+			r = policy_access(h, id, k.dport, pr, 0, 0, len[i]);
+		}
+		ops += (uint64_t)r.probes;
+		v = r.ret >= 0 ? r.ret : DROP_POLICY;
+
+		/* bpf_lxc.c:192-203 (egress), :776-800 (ingress) */
+		if (ret != CT_REPLY && ret != CT_RELATED && v < 0) {
+			if (ret == CT_ESTABLISHED) {
+				ops += 1;
+				oh_delete(&c->ct6, &k);
+			}
+			fin = DROP_POLICY;
+		} else {
+			int cr = 0;
+			if (ret == CT_NEW) {
+				uint32_t sec = 0;
+				if (egress && ep[i] < c->n_lxcinfo)
+					memcpy(&sec, c->lxcinfo + (size_t)ep[i] * 32 + 28, 4); /* SECLABEL */
+				cr = ct6_create(c, &k, dir, egress ? sec : id, egress ? 0 : rev_nat, len[i], now,
+						&ops);
+			}
+			if (cr < 0)
+				fin = cr;
+			else if (v > 0 && (egress || ret == CT_NEW || ret == CT_ESTABLISHED))
+				fin = v;
+			else
+				fin = 0;
+		}
+		verdict[i] = fin;
+		ct_ret[i] = (uint8_t)ret;
+		if (identity)
+			identity[i] = id;
+		if (stage)
+			stage[i] = (uint8_t)r.stage;
+		if (fin <= 0) {
+			uint32_t reason = fin < 0 ? (uint32_t)(-fin) & 0xff : 0;
+			c->metrics[(reason * 4 + mdir) * 2] += 1;
+			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
+		}
+	}
+	if (probe_sum)
+		*probe_sum = ops;
 	return 0;
 }

@@ -187,6 +187,20 @@ size_t or_ct4_count(or_ctx *c);
 size_t or_ct4_dump(or_ctx *c, void *keys14, void *vals56, size_t max);
 /* ctmap.go GC with RemoveExpired: delete entries with lifetime < time */
 size_t or_ct4_gc(or_ctx *c, uint32_t time);
+/* cilium_ct6_global: raw struct ipv6_ct_tuple (38 B) -> struct ct_entry */
+void or_ct6_set_max(or_ctx *c, size_t max_elem);
+int or_ct6_update(or_ctx *c, const void *key38, const void *val56);
+int or_ct6_delete(or_ctx *c, const void *key38);
+int or_ct6_lookup(or_ctx *c, const void *key38, void *val56_out);
+size_t or_ct6_count(or_ctx *c);
+size_t or_ct6_dump(or_ctx *c, void *keys38, void *vals56, size_t max);
+size_t or_ct6_gc(or_ctx *c, uint32_t time);
+/* the IPv6 form of or_classify_v4_ct (ct_lookup6 / ct_create6) */
+int or_classify_v6_ct(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+		      const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+		      const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+		      const uint16_t *ep, uint32_t now, int32_t *verdict, uint8_t *ct_ret,
+		      uint32_t *identity, uint8_t *stage, uint64_t *probe_sum);
 
 /*
  * Stateful IPv4 classification of n packets IN ORDER (the sequence the

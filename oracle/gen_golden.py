@@ -1058,6 +1058,13 @@ def load_ref_ct():
                                        C.c_uint16, C.c_uint8, C.c_uint32, C.c_int, C.c_uint32,
                                        C.c_uint32, C.c_int, ip, u32p, ip]
     lib.ref_ct_constants.argtypes = [u32p, C.c_int]
+    lib.ref_ct6_update.argtypes = [C.c_void_p, C.c_void_p]
+    lib.ref_ct6_delete.argtypes = [C.c_void_p]
+    lib.ref_ct6_count.restype = C.c_size_t
+    lib.ref_ct6_entry.argtypes = [C.c_size_t, C.c_void_p, C.c_void_p]
+    lib.ref_ct_classify_v6.argtypes = [C.c_char_p, C.c_char_p, C.c_uint16, C.c_uint16, C.c_uint8,
+                                       C.c_uint16, C.c_uint8, C.c_uint32, C.c_int, C.c_uint32,
+                                       C.c_uint32, ip, u32p, ip]
     return lib
 
 
@@ -1206,6 +1213,162 @@ def gen_ct_fixture(lib, rng):
                 **{"t2_" + k: v for k, v in t2.items()}, **res)
 
 
+# ------------------------------------------------------- conntrack, IPv6
+def ref_ct6_dump(lib):
+    n = lib.ref_ct6_count()
+    keys = np.zeros(n, L.CT6_TUPLE)
+    vals = np.zeros(n, L.CT_ENTRY)
+    kb, vb = C.create_string_buffer(38), C.create_string_buffer(56)
+    for i in range(n):
+        assert lib.ref_ct6_entry(i, kb, vb) == 0
+        keys[i] = np.frombuffer(kb.raw, L.CT6_TUPLE)[0]
+        vals[i] = np.frombuffer(vb.raw, L.CT_ENTRY)[0]
+    return L.ct_sorted(keys, vals)
+
+
+def ref_ct6_run(lib, t, now, seclabels, src_identity=0):
+    n = len(t["saddr"])
+    out = {"verdict": np.empty(n, np.int32), "ct_ret": np.empty(n, np.uint8),
+           "identity": np.empty(n, np.uint32), "stage": np.empty(n, np.uint8)}
+    cr, idv, st = C.c_int(), C.c_uint32(), C.c_int()
+    lib.ref_ct_set_now(now)
+    for i in range(n):
+        ep = int(t["ep"][i])
+        out["verdict"][i] = lib.ref_ct_classify_v6(
+            t["saddr"][i].tobytes(), t["daddr"][i].tobytes(), int(t["sport"][i]),
+            int(t["dport"][i]), int(t["proto"][i]), int(t["l4b"][i]), int(t["flags"][i]),
+            int(t["len"][i]), ep, int(seclabels[ep]), src_identity, C.byref(cr), C.byref(idv),
+            C.byref(st))
+        out["ct_ret"][i] = cr.value if cr.value >= 0 else L.CT_NONE
+        out["identity"][i], out["stage"][i] = idv.value, st.value
+    return out
+
+
+def gen_ct6_fixture(lib, pol, rng):
+    """IPv6 stateful path (CT_MAP6): as gen_ct_fixture over
+    ct_lookup6 / ct_create6 / ct_delete6 in the v6 endpoint programs' order:
+    ICMPv6 echo / errors, the ingress reverse-NAT index taken from the
+    destination address, ROUTER_IP /64 cluster fallback; 4 batches with
+    pre-installed entries and policy deletions, a small-map run, and a run
+    with a reserved ingress source identity (ipcache-resolved sources)."""
+    router = C.create_string_buffer(16)
+    pol.ref_router_ip(router)
+    router = np.frombuffer(router.raw, np.uint8).copy()
+    ikeys, ivals = gen_ipcache_entries(rng, 0, 260, static=False)
+    keep = ikeys["prefixlen"] > 32 + 4
+    ikeys, ivals = ikeys[keep], ivals[keep]
+    # local endpoints: two inside the router's /64 (cluster), two outside
+    locals6 = np.zeros((4, 16), np.uint8)
+    for i in range(4):
+        a = router.copy() if i < 2 else v6_queries_near(rng, ikeys, 1)[0]
+        a[12:] = rng.integers(0, 256, 4, dtype=np.uint8)
+        if i == 3:
+            a[12:14] = 0  # ingress to it: reverse-NAT index 0
+        locals6[i] = a
+    rem = v6_queries_near(rng, ikeys, 80)
+    inr = np.tile(router, (8, 1))
+    inr[:, 8:] = rng.integers(0, 256, (8, 8), dtype=np.uint8)
+    remotes6 = np.concatenate([rem, inr])
+    labels = np.unique(ivals["sec_label"])
+    labels = labels[(labels != 0) & (labels < 2**24)]
+    pk, pe, pep = [], [], []
+    for ep in range(4):
+        seen = set()
+        for _ in range(160):
+            kind = rng.integers(0, 4)
+            ident = int(rng.choice(labels)) if rng.random() < 0.85 else int(rng.choice([2, 3, 0]))
+            egress = int(rng.integers(0, 2))
+            if kind == 0:  # L3-only
+                port, proto = 0, 0
+            elif kind == 3:  # ICMPv6 echo keys (raw dport 128 or 0)
+                port, proto = int(rng.choice([0, L.ntohs(128)])), 58
+            else:
+                port = int(rng.choice(synth.PORTS64[:12]))
+                proto = int(rng.choice([6, 6, 17]))
+                if kind == 2:
+                    ident = 0
+            k = L.policy_key(ident, port, proto, egress)
+            if b(k) in seen:
+                continue
+            seen.add(b(k))
+            pk.append(k)
+            pe.append(L.policy_entry(int(rng.integers(1, 65536)) if rng.random() < 0.1 else 0))
+            pep.append(ep)
+    pk, pe, pep = (np.array(pk, L.POLICY_KEY), np.array(pe, L.POLICY_ENTRY),
+                   np.array(pep, np.uint16))
+    seclabels = np.array([6000 + 11 * i for i in range(4)], np.uint32)
+    t = synth.make_ct_stream(rng, 700, locals6, remotes6, mean_pkts=6.0, span=0.05)
+    n = len(t["saddr"])
+    cuts = np.array([0, n // 5, n // 2, (3 * n) // 4, n])
+    nows = np.array([100, 103, 250, 40000], np.uint32)
+    pre_i = rng.choice(n, 40, replace=False)
+    pre_k = np.zeros(50, L.CT6_TUPLE)
+    eg = (t["flags"][pre_i] & 1).astype(bool)
+    pre_k["daddr"][:40] = t["saddr"][pre_i]
+    pre_k["saddr"][:40] = t["daddr"][pre_i]
+    pre_k["dport"][:40] = np.where(t["proto"][pre_i] == 58, 0, t["dport"][pre_i])
+    pre_k["sport"][:40] = np.where(t["proto"][pre_i] == 58, 0, t["sport"][pre_i])
+    pre_k["nexthdr"][:40] = t["proto"][pre_i]
+    pre_k["flags"][:40] = np.where(eg, L.TUPLE_F_OUT, L.TUPLE_F_IN)
+    pre_k["daddr"][40:] = rng.integers(0, 256, (10, 16), dtype=np.uint8)
+    pre_k["saddr"][40:] = rng.integers(0, 256, (10, 16), dtype=np.uint8)
+    pre_k["nexthdr"][40:] = 6
+    pre_v = np.zeros(50, L.CT_ENTRY)
+    for f in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
+        pre_v[f] = rng.integers(0, 1000, 50)
+    pre_v["lifetime"] = rng.integers(0, 500, 50)
+    pre_v["bits"] = rng.choice(np.array([0, 1, 2, 3, 16, 19], np.uint16), 50)
+    pre_v["rev_nat_index"] = rng.integers(0, 3, 50)
+    pre_v["tx_flags_seen"] = rng.integers(0, 256, 50)
+    pre_v["rx_flags_seen"] = rng.integers(0, 256, 50)
+    pre_v["src_sec_id"] = rng.integers(0, 70000, 50)
+    pre_v["last_tx_report"] = rng.integers(0, 120, 50)
+    pre_v["last_rx_report"] = rng.integers(0, 120, 50)
+    pol_del = rng.choice(len(pk), len(pk) // 4, replace=False)
+
+    def load(ct_max):
+        lib.ref_ct_reset(ct_max)
+        for k, v in zip(ikeys, ivals):
+            lib.ref_ct_ipcache_update(b(k), b(v))
+        for k, e, ep in zip(pk, pe, pep):
+            lib.ref_ct_policy_update(int(ep), b(k), b(e))
+
+    load(1 << 20)
+    for k, v in zip(pre_k, pre_v):
+        assert lib.ref_ct6_update(b(k), b(v)) == 0
+    outs, dumps = [], []
+    for bi in range(4):
+        if bi == 2:
+            for d in pol_del:
+                assert lib.ref_ct_policy_delete(int(pep[d]), b(pk[d])) == 0
+        tb = {k: v[cuts[bi]:cuts[bi + 1]] for k, v in t.items()}
+        outs.append(ref_ct6_run(lib, tb, int(nows[bi]), seclabels))
+        dumps.append(ref_ct6_dump(lib))
+    res = {f"b_{f}": np.concatenate([o[f] for o in outs]) for f in outs[0]}
+    res["dump_n"] = np.array([len(d[0]) for d in dumps], np.int64)
+    res["dump_keys"] = np.concatenate([d[0] for d in dumps])
+    res["dump_vals"] = np.concatenate([d[1] for d in dumps])
+    final = np.zeros(len(pk), L.POLICY_ENTRY)
+    buf = C.create_string_buffer(24)
+    for i, (k, ep) in enumerate(zip(pk, pep)):
+        if lib.ref_ct_policy_read(int(ep), b(k), buf) == 0:
+            final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+    res["final_entries"] = final
+    # a small CT map (DROP_CT_CREATE_FAILED), with a reserved ingress source
+    # identity: ingress sources resolve through ipcache6 (bpf_netdev.c:203-211)
+    t2 = synth.make_ct_stream(rng, 200, locals6, remotes6, mean_pkts=3.0, span=0.05)
+    load(64)
+    o2 = ref_ct6_run(lib, t2, 500, seclabels, src_identity=2)
+    d2 = ref_ct6_dump(lib)
+    res.update({f"s_{f}": v for f, v in o2.items()})
+    res["s_dump_keys"], res["s_dump_vals"] = d2
+    return dict(ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe, pol_ep=pep,
+                router_ip=router, locals=locals6, seclabels=seclabels, cuts=cuts, nows=nows,
+                pre_keys=pre_k, pre_vals=pre_v, pol_del=np.sort(pol_del),
+                **{"t_" + k: v for k, v in t.items()}, **{"t2_" + k: v for k, v in t2.items()},
+                **res)
+
+
 def save(name, d):
     path = os.path.join(OUT, name)
     np.savez_compressed(path, **d)
@@ -1246,6 +1409,9 @@ def main():
     rng_lb6 = np.random.Generator(np.random.PCG64(SEED + 0x6B))
     manifest["files"]["classify_v6_lb.npz"] = save(
         "classify_v6_lb.npz", gen_classify_v6_lb_fixture(pol, load_ref_lbl6(), rng_lb6))
+    # IPv6 conntrack (CT_MAP6), its own stream
+    rng_ct6 = np.random.Generator(np.random.PCG64(SEED + 0xC6))
+    manifest["files"]["ct6.npz"] = save("ct6.npz", gen_ct6_fixture(load_ref_ct(), pol, rng_ct6))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -91,6 +91,19 @@ def lib():
         L.or_ct4_gc.restype = sz
         L.or_classify_v4_ct.argtypes = [vp, sz] + [vp] * 9 + [C.c_uint32] + [vp] * 4 + [
             C.POINTER(C.c_uint64)]
+        L.or_ct6_set_max.argtypes = [vp, sz]
+        L.or_ct6_set_max.restype = None
+        L.or_ct6_update.argtypes = [vp, vp, vp]
+        L.or_ct6_delete.argtypes = [vp, vp]
+        L.or_ct6_lookup.argtypes = [vp, vp, vp]
+        L.or_ct6_count.argtypes = [vp]
+        L.or_ct6_count.restype = sz
+        L.or_ct6_dump.argtypes = [vp, vp, vp, sz]
+        L.or_ct6_dump.restype = sz
+        L.or_ct6_gc.argtypes = [vp, C.c_uint32]
+        L.or_ct6_gc.restype = sz
+        L.or_classify_v6_ct.argtypes = [vp, sz] + [vp] * 9 + [C.c_uint32] + [vp] * 4 + [
+            C.POINTER(C.c_uint64)]
         u32 = C.c_uint32
         L.or_l3_compile.argtypes = [vp, vp, vp, vp, vp, u32, vp, vp, vp, u32, vp, vp, u32, u32, vp]
         L.or_metrics_read.argtypes = [vp, vp]
@@ -378,6 +391,52 @@ class Oracle:
             ("dport", np.uint16), ("proto", np.uint8), ("l4b", np.uint16), ("flags", np.uint8),
             ("len", np.uint32), ("ep", np.uint16))]
         rc = self.L.or_classify_v4_ct(self.h, n, *[_p(a) for a in arrs], now, _p(verdict),
+                                      _p(ct_ret), _p(identity), _p(stage), C.byref(probes))
+        assert rc == 0, rc
+        return verdict, ct_ret, identity, stage, probes.value
+
+    # --- IPv6 conntrack (cilium_ct6_global) ---
+    def ct6_set_max(self, n):
+        self.L.or_ct6_set_max(self.h, n)
+
+    def ct6_update(self, key, val):
+        return self.L.or_ct6_update(self.h, _b(key), _b(val))
+
+    def ct6_delete(self, key):
+        return self.L.or_ct6_delete(self.h, _b(key))
+
+    def ct6_lookup(self, key):
+        out = C.create_string_buffer(56)
+        r = self.L.or_ct6_lookup(self.h, _b(key), out)
+        return r, out.raw
+
+    def ct6_count(self):
+        return self.L.or_ct6_count(self.h)
+
+    def ct6_dump(self):
+        from cilium_amd import layouts as Ly
+        n = self.ct6_count()
+        keys = np.zeros(n, Ly.CT6_TUPLE)
+        vals = np.zeros(n, Ly.CT_ENTRY)
+        k = self.L.or_ct6_dump(self.h, _p(keys), _p(vals), n)
+        assert k == n
+        return Ly.ct_sorted(keys, vals)
+
+    def ct6_gc(self, time):
+        return self.L.or_ct6_gc(self.h, time)
+
+    def classify_v6_ct(self, t, now):
+        n = len(t["saddr"])
+        verdict = np.empty(n, np.int32)
+        ct_ret = np.empty(n, np.uint8)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint8), ("daddr", np.uint8), ("sport", np.uint16),
+            ("dport", np.uint16), ("proto", np.uint8), ("l4b", np.uint16), ("flags", np.uint8),
+            ("len", np.uint32), ("ep", np.uint16))]
+        rc = self.L.or_classify_v6_ct(self.h, n, *[_p(a) for a in arrs], now, _p(verdict),
                                       _p(ct_ret), _p(identity), _p(stage), C.byref(probes))
         assert rc == 0, rc
         return verdict, ct_ret, identity, stage, probes.value

@@ -25,6 +25,17 @@
  * reported as: the DROP_* it returns, the proxy port it redirects to, or 0
  * (forwarded).
  *
+ * IPv6 (ref_ct_classify_v6): the same for ct_lookup6 / ct_create6 /
+ * ct_delete6 over CT_MAP6 (bpf_lxc.c:53-63), in the order of
+ * ipv6_l3_from_lxc (bpf_lxc.c:108-203: dstID from ipcache6(orig_dip), else
+ * CLUSTER_ID when ipv6_match_prefix_64(daddr, ROUTER_IP), else WORLD_ID) and
+ * ipv6_policy (:731-800: the reverse NAT index of the created entry is
+ * daddr.s6_addr32[3] & 0xFFFF, :748; a hit entry's rev_nat_index sends the
+ * packet through lb6_rev_nat, which is a no-op over the empty
+ * cilium_lb6_reverse_nat map, lib/lb.h:305-317; is_fragment false).  Ingress
+ * identity as bpf_netdev.c:203-211 (no HOST_ID exception on IPv6), the label
+ * the resolved source (FROM_HOST form).
+ *
  * Mocks (writable helper pointers, bpf/include/bpf/api.h:101-118): the CT map
  * is a kernel htab (whole-key memcmp) with max_elem (new keys past it fail as
  * htab_map_update_elem does, -E2BIG); map_delete_elem removes; the policy map
@@ -52,10 +63,10 @@
 
 #define REF_MAX_EP 64
 
-/* stands in for the endpoint's CT_MAP4 (bpf_lxc.c:64-75) */
-static int ct_map4;
-static struct mockmap ct;
-static size_t ct_max = 1u << 20;
+/* stand in for the endpoint's CT_MAP4 (bpf_lxc.c:64-75) and CT_MAP6 (:53-63) */
+static int ct_map4, ct_map6;
+static struct mockmap ct, ct6;
+static size_t ct_max = 1u << 20, ct6_max = 1u << 20;
 static struct mockmap policy_maps[REF_MAX_EP];
 static struct mockmap ipcache;
 static int cur_ep, inited;
@@ -77,25 +88,30 @@ static void *mock_lookup(void *map, const void *key)
 		return mockmap_lookup(&ipcache, key);
 	if (map == &ct_map4)
 		return mockmap_lookup(&ct, key);
+	if (map == &ct_map6)
+		return mockmap_lookup(&ct6, key);
 	fprintf(stderr, "ct harness: lookup on unexpected map %p\n", map);
 	return NULL;
 }
 
 static int mock_update(void *map, const void *key, const void *val, uint32_t flags)
 {
-	if (map != &ct_map4)
+	struct mockmap *m = map == &ct_map4 ? &ct : map == &ct_map6 ? &ct6 : NULL;
+	size_t max = map == &ct_map4 ? ct_max : ct6_max;
+	if (!m)
 		return -1;
-	if (!mockmap_lookup(&ct, key) && ct.n >= ct_max)
+	if (!mockmap_lookup(m, key) && m->n >= max)
 		return -7; /* -E2BIG */
-	mockmap_update(&ct, key, val);
+	mockmap_update(m, key, val);
 	return 0;
 }
 
 static int mock_delete(void *map, const void *key)
 {
-	if (map != &ct_map4)
+	struct mockmap *m = map == &ct_map4 ? &ct : map == &ct_map6 ? &ct6 : NULL;
+	if (!m)
 		return -1;
-	return mockmap_delete(&ct, key) ? 0 : -2;
+	return mockmap_delete(m, key) ? 0 : -2;
 }
 
 static uint64_t mock_ktime(void) { return now_ns; }
@@ -118,6 +134,7 @@ static void ensure_init(void)
 	mockmap_init(&ipcache, MOCK_LPM, sizeof(struct ipcache_key),
 		     sizeof(struct remote_endpoint_info));
 	mockmap_init(&ct, MOCK_HASH, sizeof(struct ipv4_ct_tuple), sizeof(struct ct_entry));
+	mockmap_init(&ct6, MOCK_HASH, sizeof(struct ipv6_ct_tuple), sizeof(struct ct_entry));
 	map_lookup_elem = mock_lookup;
 	map_update_elem = mock_update;
 	map_delete_elem = mock_delete;
@@ -133,13 +150,16 @@ void ref_ct_reset(size_t max_elem)
 		mockmap_clear(&policy_maps[i]);
 	mockmap_clear(&ipcache);
 	mockmap_clear(&ct);
+	mockmap_clear(&ct6);
 	ct_max = max_elem;
+	ct6_max = max_elem;
 }
 
-int ref_ct_sizes(int *tuple_sz, int *entry_sz)
+int ref_ct_sizes(int *tuple_sz, int *entry_sz, int *tuple6_sz)
 {
 	*tuple_sz = sizeof(struct ipv4_ct_tuple);
 	*entry_sz = sizeof(struct ct_entry);
+	*tuple6_sz = sizeof(struct ipv6_ct_tuple);
 	return 0;
 }
 
@@ -190,10 +210,23 @@ int ref_ct_entry(size_t i, void *key_out, void *val_out)
 	return 0;
 }
 
+/* raw 38-byte ipv6_ct_tuple / 56-byte ct_entry of CT_MAP6 */
+int ref_ct6_update(const void *key, const void *val) { ensure_init(); return mock_update(&ct_map6, key, val, 0); }
+int ref_ct6_delete(const void *key) { ensure_init(); return mock_delete(&ct_map6, key); }
+size_t ref_ct6_count(void) { return ct6.n; }
+int ref_ct6_entry(size_t i, void *key_out, void *val_out)
+{
+	if (i >= ct6.n)
+		return -1;
+	memcpy(key_out, ct6.keys + i * ct6.ksz, ct6.ksz);
+	memcpy(val_out, ct6.vals + i * ct6.vsz, ct6.vsz);
+	return 0;
+}
+
 static void l4_header(uint8_t proto, uint16_t sport_be, uint16_t dport_be, uint16_t l4w)
 {
 	memset(l4buf, 0, sizeof(l4buf));
-	if (proto == IPPROTO_ICMP) {
+	if (proto == IPPROTO_ICMP || proto == IPPROTO_ICMPV6) {
 		l4buf[0] = (uint8_t)l4w; /* icmphdr.type */
 	} else {
 		memcpy(l4buf, &sport_be, 2);
@@ -290,6 +323,96 @@ int ref_ct_classify_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t sport_be,
 	}
 	if (verdict > 0 && (egress || ret == CT_NEW || ret == CT_ESTABLISHED))
 		return verdict; /* redirect_to_proxy: the proxy port */
+	return 0;
+}
+
+/*
+ * One IPv6 packet through conntrack + ipcache + policy, in order (the v6
+ * endpoint programs, see the header).  Arguments and outputs as
+ * ref_ct_classify_v4; addresses are 16 network-order bytes.
+ */
+int ref_ct_classify_v6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t sport_be,
+		       uint16_t dport_be, uint8_t proto, uint16_t l4w, uint8_t flags, uint32_t len,
+		       int ep, uint32_t seclabel, uint32_t cfg_src_identity, int *ct_ret,
+		       uint32_t *identity_out, int *stage_out)
+{
+	struct ipv6_ct_tuple tuple = {};
+	struct ct_state ct_state = {}, ct_state_new = {};
+	struct __sk_buff skb;
+	bool monitor = false;
+	int egress = flags & 1;
+	int ret, verdict;
+	uint32_t id;
+	union v6addr sa, da, router_ip;
+	struct remote_endpoint_info *info;
+	BPF_V6(router_ip, ROUTER_IP);
+
+	ensure_init();
+	memset(&skb, 0, sizeof(skb));
+	skb.len = len;
+	cur_ep = ep;
+	pol_probes = pol_hit_probe = 0;
+	*identity_out = 0;
+	*stage_out = 0;
+	l4_header(proto, sport_be, dport_be, l4w);
+	memcpy(&sa, saddr16, 16);
+	memcpy(&da, daddr16, 16);
+
+	tuple.nexthdr = proto;
+	ipv6_addr_copy(&tuple.daddr, &da);
+	ipv6_addr_copy(&tuple.saddr, &sa);
+	if (!egress) {
+		/* ipv6_policy: ct_state_new.rev_nat_index = ip6->daddr.s6_addr32[3] & 0xFFFF */
+		uint32_t w3;
+		memcpy(&w3, daddr16 + 12, 4);
+		ct_state_new.rev_nat_index = w3 & 0xFFFF;
+	}
+	ret = ct_lookup6(&ct_map6, &tuple, &skb, 0, egress ? CT_EGRESS : CT_INGRESS, &ct_state,
+			 &monitor);
+	*ct_ret = ret;
+	if (ret < 0) {
+		*stage_out = ret == DROP_CT_UNKNOWN_PROTO ? 4 : 5;
+		return ret;
+	}
+
+	if (egress) {
+		info = ipcache_lookup6(&cilium_ipcache, &da, V6_CACHE_KEY_LEN);
+		if (info && info->sec_label)
+			id = info->sec_label;
+		else if (ipv6_match_prefix_64(&da, &router_ip))
+			id = CLUSTER_ID;
+		else
+			id = WORLD_ID;
+		verdict = policy_can_egress6(&skb, &tuple, id, ipv6_ct_tuple_get_daddr(&tuple));
+	} else {
+		uint32_t src = cfg_src_identity;
+		if (identity_is_reserved(src)) {
+			info = ipcache_lookup6(&cilium_ipcache, &sa, V6_CACHE_KEY_LEN);
+			if (info && info->sec_label && info->sec_label != CLUSTER_ID)
+				src = info->sec_label;
+		}
+		id = src;
+		verdict = policy_can_access_ingress(&skb, id, tuple.dport, tuple.nexthdr,
+						    sizeof(tuple.saddr), &tuple.saddr, false);
+	}
+	*identity_out = id;
+	*stage_out = pol_hit_probe;
+
+	if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+		if (ret == CT_ESTABLISHED)
+			ct_delete6(&ct_map6, &tuple, &skb);
+		return egress ? verdict : DROP_POLICY;
+	}
+	if (ret == CT_NEW) {
+		ct_state_new.orig_dport = tuple.dport;
+		ct_state_new.src_sec_id = egress ? seclabel : id;
+		ret = ct_create6(&ct_map6, &tuple, &skb, egress ? CT_EGRESS : CT_INGRESS,
+				 &ct_state_new);
+		if (IS_ERR(ret))
+			return ret;
+	}
+	if (verdict > 0 && (egress || ret == CT_NEW || ret == CT_ESTABLISHED))
+		return verdict;
 	return 0;
 }
 

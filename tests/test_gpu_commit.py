@@ -344,3 +344,42 @@ def test_counters_allreduce_one_rank(torch_cuda):
         assert (int(got[i, 0]), int(got[i, 1])) == (int(exp["packets"]), int(exp["bytes"]))
     e.counter_bind(None)
     e.close()
+
+
+def test_counter_slot_layout_deterministic(torch_cuda):
+    """Counter slots are assigned from the sequence of map operations and
+    commits alone: two contexts applying the same delete/insert
+    churn over a small slot space -- one with classify launches in flight
+    between commits, one idle -- report the same counter layout checksum
+    after every commit, so the slot-by-slot RCCL SUM adds like to like."""
+    torch = torch_cuda
+    busy = _engine(policy_max_total=64, hot_counter_slots=8, max_endpoints=2)
+    idle = _engine(policy_max_total=64, hot_counter_slots=8, max_endpoints=2)
+    keys = [L.policy_key(300 + i, 80 if i % 3 else 0, 6 if i % 3 else 0, 1) for i in range(44)]
+    for e in (busy, idle):
+        for k in keys:
+            assert e.policy_update(0, k, L.policy_entry(0)) == 0
+        e.commit()
+    n = 1 << 20
+    rng = np.random.default_rng(7)
+    t = {"saddr": np.zeros(n, np.uint32), "daddr": rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32),
+         "dport": np.full(n, L.htons(80), np.uint16), "proto": np.full(n, 6, np.uint8),
+         "flags": np.ones(n, np.uint8), "len": np.full(n, 100, np.uint32), "ep": np.zeros(n, np.uint16)}
+    d = synth.to_device(t)
+    for rnd in range(40):
+        i = int(rng.integers(0, len(keys)))
+        new = L.policy_key(7000 + rnd, 0 if rnd % 2 else 443, 0 if rnd % 2 else 6, 1)
+        for e in (busy, idle):
+            assert e.policy_delete(0, keys[i]) == 0
+            rc = e.policy_update(0, new, L.policy_entry(0))
+            assert rc == 0, rc
+        keys[i] = new
+        for _ in range(3):
+            busy.classify_v4(d, stage=False)  # launches still running at the commit
+        busy.commit()
+        idle.commit()
+        assert busy.counter_layout_checksum() == idle.counter_layout_checksum(), f"round {rnd}"
+        assert busy.checksum() == idle.checksum()
+    torch.cuda.synchronize()
+    busy.close()
+    idle.close()

@@ -21,9 +21,15 @@ def torch_cuda():
     return torch
 
 
+# cgpu_config defaults of _engine (tests switch the classify schedule through
+# cgpu_config.schedule: the old variant numbers 0 / 3 / 8)
+_DEFAULTS = {}
+SCHED_OF = {0: 2, 3: 1, 8: 0}  # CGPU_SCHED_GLOBAL_CTR, CGPU_SCHED_PER_LANE, default x4
+
+
 def _engine(**kw):
     from cilium_amd.engine import Engine
-    return Engine(device=0, **kw)
+    return Engine(device=0, **{**_DEFAULTS, **kw})
 
 
 def _dev(torch, t):
@@ -212,7 +218,7 @@ def test_classify_v6_lb_golden(torch_cuda, golden, ci, variant, monkeypatch):
     (tests/golden/classify_v6_lb.npz), hash injected; on the one-tuple-per-lane
     kernel (3) and the x4 schedule (8, the default)."""
     torch = torch_cuda
-    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    monkeypatch.setitem(_DEFAULTS, "schedule", SCHED_OF[variant])
     g = golden("classify_v6_lb.npz")
     gate, src = (int(x) for x in g["configs"][ci])
     e = _engine(ct_proto_gate=gate, ingress_src_identity=src, ipv6_router_ip=g["router_ip"].tobytes())

@@ -17,9 +17,15 @@ def torch_cuda():
     return torch
 
 
+# cgpu_config defaults of _engine (tests switch the classify schedule through
+# cgpu_config.schedule: the old variant numbers 0 / 3 / 8)
+_DEFAULTS = {}
+SCHED_OF = {0: 2, 3: 1, 8: 0}  # CGPU_SCHED_GLOBAL_CTR, CGPU_SCHED_PER_LANE, default x4
+
+
 def _engine(**kw):
     from cilium_amd.engine import Engine
-    return Engine(device=0, **kw)
+    return Engine(device=0, **{**_DEFAULTS, **kw})
 
 
 def _np(t, dt=None):
@@ -337,7 +343,7 @@ def test_classify_v6_scale_vs_oracle(torch_cuda, variant, monkeypatch):
     """20k IPv6 ipcache prefixes (lengths 0..128, tombstones, static-part
     entries) + policy, 400k tuples: GPU == restatement, bit-exact, on the
     one-tuple-per-lane kernel (3) and the x4 schedule (8, the default)."""
-    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    monkeypatch.setitem(_DEFAULTS, "schedule", SCHED_OF[variant])
     from oracle import Oracle
     rng = np.random.default_rng(21)
     T = synth.make_tables(n_prefixes=100, n_identities=500, n_endpoints=3, keys_per_ep=6000)
@@ -394,7 +400,7 @@ def test_kernel_variants_exact(torch_cuda, cfg1, variant, monkeypatch):
     """Every classify schedule / counter strategy gives the reference's
     verdicts, identities, stages, per-entry counters and metrics."""
     T, t = cfg1
-    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    monkeypatch.setitem(_DEFAULTS, "schedule", SCHED_OF[variant])
     o, v0, i0, s0, _ = _oracle_run(T, t)
     e = _engine(**T.engine_config())
     synth.load_engine(e, T)
@@ -435,7 +441,7 @@ def test_ragged_batches_long_packets(torch_cuda, cfg1, n, variant, monkeypatch):
     lengths past every packed-counter bound (2^16 cold, 2^18 hot): verdicts,
     identities, stages, per-entry counters and metrics stay exact."""
     T, t_full = cfg1
-    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    monkeypatch.setitem(_DEFAULTS, "schedule", SCHED_OF[variant])
     t = {k: np.ascontiguousarray(v[:n]) for k, v in t_full.items()}
     rng = np.random.default_rng(n)
     t["len"] = rng.choice(np.array([64, 1500, 65535, 65536, 70000, 262143, 262144, 9_000_000],
@@ -461,7 +467,7 @@ def test_unaligned_columns_take_scalar_schedule(torch_cuda, cfg1, monkeypatch):
     """Column views that start off a 16-byte boundary cannot use the vector
     schedule; the launcher picks the per-element one and results stay exact."""
     T, t_full = cfg1
-    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", "8")
+    monkeypatch.setitem(_DEFAULTS, "schedule", 0)
     n = 100_001
     t = {k: np.ascontiguousarray(v[1:n + 1]) for k, v in t_full.items()}
     o, v0, i0, s0, _ = _oracle_run(T, t)
@@ -509,7 +515,7 @@ def test_lpm_shapes_exact(torch_cuda, variant, monkeypatch):
     """Every ipcache LPM table shape resolves the same identity as the
     restatement (egress lookups of daddr; ingress of saddr)."""
     from oracle import Oracle
-    monkeypatch.setenv("CGPU_CLASSIFY_VARIANT", str(variant))
+    monkeypatch.setitem(_DEFAULTS, "schedule", SCHED_OF[variant])
     rng = np.random.default_rng(7)
     keys, vals = _lpm_shapes_tables(rng)
     n = 1 << 18
@@ -552,7 +558,7 @@ def test_prefilter6_cover_shapes(torch_cuda, seed, lds_mode, monkeypatch):
     k_prefilter_v6_q (0: root in HBM, 1: u16 root in LDS, 2: root bitmaps +
     u16 b24 blocks in LDS).  Bit-exact against the restatement's kernel-like
     LPM trie."""
-    monkeypatch.setenv("CGPU_PF6_LDS", str(lds_mode))
+    monkeypatch.setitem(_DEFAULTS, "schedule", (lds_mode + 1) << 4)  # CGPU_SCHED_PF6_LDS
     _cover6_case(torch_cuda, seed, np.random.default_rng(100 + seed).integers(0, 256, (6, 2), dtype=np.uint8))
 
 
