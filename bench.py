@@ -31,6 +31,9 @@ Other BASELINE configs (not the headline line; run them explicitly):
                      updates and reply-skips the same way; parity and the
                      CPU baseline on the packets of 1/64 of the address pairs
                      (pairs are independent conntrack groups)
+  --config ct6       the same over IPv6 (cilium_ct6_global, cgpu_classify_v6_ct):
+                     100k IPv6 ipcache prefixes + 64k policy keys, 64M packets
+                     of 2M connections, parity on 1/64 of the address pairs
   --config mapstate  L3 MapState compilation: the label
                      decision of computeDesiredL3PolicyMapEntries for 100
                      endpoints x 65536 identities over a 1000-rule repository
@@ -56,6 +59,7 @@ B_IN_V6 = 42           # v6 classify: saddr 16 + daddr 16 + dport proto flags le
 FRAME_STRIDE = 64      # --config frames: ring slot bytes (Ethernet + IPv4 + TCP fit)
 B_IN_FRAMES = FRAME_STRIDE + 4 + 1 + 2  # slot + len + flags + ep
 B_IN_CT, B_OUT_CT = 22, 9  # saddr daddr sport dport proto l4(2) flags len ep / verdict identity ct_ret
+B_IN_CT6 = 46              # the same with 16-byte addresses
 CT_PKTS_PER_CONN = 32
 CT_SAMPLE = 64  # parity / CPU baseline on the packets of 1 in CT_SAMPLE address pairs
 
@@ -107,6 +111,10 @@ WORKLOADS = {
           "per GPU of 2M TCP/UDP/ICMP connections (~32 packets each, both directions, ICMP errors), "
           "map emptied each step: ct_lookup4 -> ipcache -> policy -> reply/related skip, "
           "ct_create4 / delete, bit-exact",
+    "ct6": "IPv6 tables at config-2 size (100k IPv6 ipcache prefixes + 64k policy entries) + stateful "
+           "conntrack (cilium_ct6_global): 64M packets per GPU of 2M TCP/UDP/ICMPv6 connections, map "
+           "emptied each step: ct_lookup6 -> ipcache6 -> policy -> reply/related skip, ct_create6 / "
+           "delete, bit-exact",
 }
 
 
@@ -145,9 +153,10 @@ def main():
     pf6 = args.config == "pf6"
     cascade = args.config == "cascade"
     frames = args.config == "frames"
-    ct = args.config == "ct"
+    ct6 = args.config == "ct6"
+    ct = args.config == "ct" or ct6
     v6 = args.config == "v6"
-    cfg = synth.CONFIGS["gpu" if (pf6 or frames or ct) else args.config]
+    cfg = synth.CONFIGS["v6" if ct6 else "gpu" if (pf6 or frames or ct) else args.config]
     n = args.tuples or cfg["n_tuples"]
     t0 = time.time()
     S = None
@@ -159,11 +168,12 @@ def main():
         e = Engine(device=local, **P.engine_config())
         synth.load_prefilter6(e, P)
     elif ct:
-        T = synth.make_tables(**cfg)
+        T = synth.make_tables6(**cfg) if ct6 else synth.make_tables(**cfg)
         # each rank's stream is its conntrack shard (address pairs with
         # pairhash % world == rank): per-rank maps, no shared state
-        tup, _, seclabels = synth.make_ct_workload(T, n // CT_PKTS_PER_CONN, gpu_id=rank,
-                                                   mean_pkts=CT_PKTS_PER_CONN, world=world)
+        mk = synth.make_ct6_workload if ct6 else synth.make_ct_workload
+        tup, _, seclabels = mk(T, n // CT_PKTS_PER_CONN, gpu_id=rank, mean_pkts=CT_PKTS_PER_CONN,
+                               world=world)
         n = min(n, len(tup["saddr"]))
         tup = {k: np.ascontiguousarray(v[:n]) for k, v in tup.items()}
         ct_max = 1 << max(20, int(np.ceil(np.log2(2.5 * n / CT_PKTS_PER_CONN))))
@@ -236,7 +246,9 @@ def main():
         shard.init_counter_comm(e, rank, world)
 
     def launch():
-        if ct:
+        if ct6:
+            e.classify_v6_ct(d, CT_NOW, out=out, stream=stream)
+        elif ct:
             e.classify_v4_ct(d, CT_NOW, out=out, stream=stream)
         elif pf6:
             e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
@@ -249,9 +261,15 @@ def main():
         else:
             e.classify_v4(d, out=out, stream=stream)
 
+    def flush_ct():
+        if ct6:
+            e.ct6_flush()
+        elif ct:
+            e.ct4_flush()
+
     def step(ev=None):
         if ct:
-            e.ct4_flush()  # every step starts from an empty conntrack map
+            flush_ct()  # every step starts from an empty conntrack map
         if ev is not None:
             ev[0].record(stream)
         launch()
@@ -287,7 +305,7 @@ def main():
         # the shipped collective against torch's SUM of the same local deltas
         # (one untimed step): every rank must hold the sum of all ranks
         if ct:
-            e.ct4_flush()
+            flush_ct()
         torch.cuda.synchronize()
         delta.zero_()
         launch()
@@ -327,6 +345,7 @@ def main():
             synth.load_oracle(o, T)
             synth.load_lxc(o, seclabels)
             o.ct_set_max(ct_max)
+            o.ct6_set_max(ct_max)
         else:
             o = Oracle(**T.oracle_config())
             synth.load_oracle(o, T)
@@ -349,10 +368,13 @@ def main():
             # packets of 1 in CT_SAMPLE pairs, in batch order, replayed by the
             # sequential restatement from an empty map are the reference's
             # result for exactly those packets
-            lo = np.minimum(tup["saddr"], tup["daddr"]).astype(np.uint64)
-            hi = np.maximum(tup["saddr"], tup["daddr"]).astype(np.uint64)
-            hsh = ((lo * np.uint64(0x9E3779B97F4A7C15)) ^ hi) * np.uint64(0xC2B2AE3D27D4EB4F)
-            sub = np.nonzero((hsh >> np.uint64(58)) == 0)[0]
+            if ct6:
+                sub = np.nonzero((shard.pairhash6_np(tup["saddr"], tup["daddr"]) >> np.uint32(26)) == 0)[0]
+            else:
+                lo = np.minimum(tup["saddr"], tup["daddr"]).astype(np.uint64)
+                hi = np.maximum(tup["saddr"], tup["daddr"]).astype(np.uint64)
+                hsh = ((lo * np.uint64(0x9E3779B97F4A7C15)) ^ hi) * np.uint64(0xC2B2AE3D27D4EB4F)
+                sub = np.nonzero((hsh >> np.uint64(58)) == 0)[0]
             tsub = {k: v[sub] for k, v in tup.items()}
         elif not skip_cpu:
             cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
@@ -361,7 +383,7 @@ def main():
         for rep in range(3):
             c0 = time.perf_counter()
             if ct:
-                res = o.classify_v4_ct(tsub, CT_NOW)
+                res = (o.classify_v6_ct if ct6 else o.classify_v4_ct)(tsub, CT_NOW)
             elif pf6:
                 res = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
             elif cascade:
@@ -390,7 +412,8 @@ def main():
             cpu = {"value": round(n_cpu / c_el / 1e6, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
                    "sample": f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
-                             f"pairs from an empty map; oracle/cgpu_oracle.c or_classify_v4_ct "
+                             f"pairs from an empty map; oracle/cgpu_oracle.c "
+                             f"or_classify_v{6 if ct6 else 4}_ct "
                              f"(sequential conntrack + LPM trie + open hash), 1 thread, "
                              f"{c_el:.2f}s wall (one run); host: {host_cpu()}"}
         elif not skip_cpu:
@@ -414,7 +437,8 @@ def main():
                 parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
         probes_per = probes / n_cpu
         b_in, b_out = ((B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN_FRAMES, B_OUT) if frames
-                       else (B_IN_CT, B_OUT_CT) if ct else (B_IN_V6, B_OUT) if v6
+                       else (B_IN_CT6, B_OUT_CT) if ct6 else (B_IN_CT, B_OUT_CT) if ct
+                       else (B_IN_V6, B_OUT) if v6
                        else (B_IN + (2 if cascade else 0), B_OUT))
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
@@ -442,7 +466,8 @@ def main():
                 conf.update(services=int(len(S.vip)), lb_map_entries=int(len(S.keys)))
             if ct:
                 ctr = out["ct_ret"].cpu().numpy()
-                conf.update(ct_max=ct_max, ct_entries_after_step=int(e.ct4_count()),
+                conf.update(ct_max=ct_max,
+                            ct_entries_after_step=int(e.ct6_count() if ct6 else e.ct4_count()),
                             parity_sample_packets=int(len(sub)),
                             ct_state_frac={s_: round(float((ctr == c_).mean()), 4) for s_, c_ in
                                            (("new", 0), ("established", 1), ("reply", 2),

@@ -53,6 +53,11 @@ class TuplesV4Ct(C.Structure):
                 ("saddr", "daddr", "sport", "dport", "proto", "l4", "flags", "len", "ep")]
 
 
+class TuplesV6Ct(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ("saddr", "daddr", "sport", "dport", "proto", "l4", "flags", "len", "ep")]
+
+
 class Lb4Tuples(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("saddr", "daddr", "sport", "dport", "proto", "hash")]
 
@@ -143,6 +148,14 @@ PROTOS = {
     "cgpu_ct4_gc": (i32, [vp, u32, C.POINTER(u64)]),
     "cgpu_ct4_flush": (i32, [vp]),
     "cgpu_classify_v4_ct": (i32, [vp, C.POINTER(TuplesV4Ct), sz, u32, vp, vp, vp, vp, vp]),
+    "cgpu_ct6_update": (i32, [vp, vp, vp, u64]),
+    "cgpu_ct6_delete": (i32, [vp, vp]),
+    "cgpu_ct6_lookup": (i32, [vp, vp, vp]),
+    "cgpu_ct6_get_next_key": (i32, [vp, vp, vp]),
+    "cgpu_ct6_count": (sz, [vp]),
+    "cgpu_ct6_gc": (i32, [vp, u32, C.POINTER(u64)]),
+    "cgpu_ct6_flush": (i32, [vp]),
+    "cgpu_classify_v6_ct": (i32, [vp, C.POINTER(TuplesV6Ct), sz, u32, vp, vp, vp, vp, vp]),
     "cgpu_l3_compile": (i32, [vp, vp, vp, vp, u32, vp]),
     "cgpu_mapstate_sync": (i32, [vp, vp, vp, vp, vp, vp]),
     "cgpu_counter_delta_bytes": (sz, [vp]),

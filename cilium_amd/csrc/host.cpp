@@ -1374,6 +1374,21 @@ struct BuildState {
 	uint64_t sum[G_N] = {};
 };
 
+/* One conntrack map (tables.h ct_table layout; CtK4 / CtK6 slots in
+ * kernels.hip).  A host shadow serves the bpf(2)-style map calls; the device
+ * copy is authoritative once a batch ran (dev_newer) and is refreshed from
+ * the shadow before the next batch after host edits (host_newer). */
+struct CtMap {
+	bool v6 = false;
+	uint32_t max = 0;               /* CT_MAP_SIZE */
+	std::vector<uint4> keys, vals;  /* [sw() * nslots], [4 * nslots] */
+	uint32_t mask = 0, live = 0, tombs = 0;
+	bool dev_newer = false, host_newer = false;
+	uint4 *d_keys = nullptr, *d_vals = nullptr;
+	uint32_t *d_count = nullptr;
+	uint32_t sw() const { return v6 ? 4u : 1u; } /* uint4 key words per slot */
+};
+
 } // namespace
 
 struct cgpu_ctx {
@@ -1451,15 +1466,8 @@ struct cgpu_ctx {
 	/* ---- multi-GPU counter reduction (cgpu_comm_init) ---- */
 	void *comm = nullptr; /* ncclComm_t */
 
-	/* ---- conntrack map cilium_ct4_global (tables.h ct_table layout) ----
-	 * A host shadow serves the bpf(2)-style map calls; the device copy is
-	 * authoritative once a batch ran (ct_dev_newer) and is refreshed from
-	 * the shadow before the next batch after host edits (ct_host_newer). */
-	std::vector<uint4> ct_keys, ct_vals; /* [nslots], [4 * nslots] */
-	uint32_t ct_mask = 0, ct_live = 0, ct_tombs = 0;
-	bool ct_dev_newer = false, ct_host_newer = false;
-	uint4 *d_ct_keys = nullptr, *d_ct_vals = nullptr;
-	uint32_t *d_ct_count = nullptr;
+	/* ---- conntrack maps cilium_ct4_global / cilium_ct6_global ---- */
+	CtMap ct4, ct6;
 	void *d_ct_scratch = nullptr;
 	size_t ct_scratch_cap = 0;
 	hipStream_t ct_stream = nullptr; /* the conntrack path's internal stream */
@@ -1612,6 +1620,8 @@ CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **o
 		return fail(-EINVAL, "policy_max_total %u >= 2^24 - 1", cfg->policy_max_total);
 	if (!cfg->ct_max || cfg->ct_max > (1u << 28))
 		return fail(-EINVAL, "ct_max %u out of range (1 .. 2^28)", cfg->ct_max);
+	if (cfg->ct6_max > (1u << 27))
+		return fail(-EINVAL, "ct6_max %u out of range (0 .. 2^27)", cfg->ct6_max);
 	cgpu_ctx *c = new cgpu_ctx();
 	c->cfg = *cfg;
 	c->pol.resize(cfg->max_endpoints);
@@ -1619,6 +1629,9 @@ CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **o
 	c->hot_cap = std::min(cfg->hot_counter_slots, cfg->policy_max_total / 2);
 	c->next_cold = c->hot_cap;
 	c->dirty = (1u << G_N) - 1u; /* the first commit compiles every group */
+	c->ct4.max = cfg->ct_max;
+	c->ct6.v6 = true;
+	c->ct6.max = cfg->ct6_max ? cfg->ct6_max : cfg->ct_max;
 	if (device >= 0) {
 		int ndev = 0, pools = 0;
 		if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
@@ -1707,9 +1720,11 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 			}
 			c->d_pk.clear();
 		}
-		(void)hipFree(c->d_ct_keys);
-		(void)hipFree(c->d_ct_vals);
-		(void)hipFree(c->d_ct_count);
+		for (CtMap *m : {&c->ct4, &c->ct6}) {
+			(void)hipFree(m->d_keys);
+			(void)hipFree(m->d_vals);
+			(void)hipFree(m->d_count);
+		}
 		(void)hipFree(c->d_ct_scratch);
 		(void)hipEventDestroy(c->ct_done);
 		(void)hipStreamDestroy(c->ct_stream);
@@ -3879,295 +3894,461 @@ CGPU_EXPORT int cgpu_counters_allreduce(cgpu_ctx *c, void *stream)
 }
 
 /* ======================================================================= */
-/* conntrack map cilium_ct4_global                        */
+/* conntrack maps cilium_ct4_global / cilium_ct6_global   */
 /* ======================================================================= */
 static_assert(sizeof(cgpu_ct4_tuple) == 14, "ipv4_ct_tuple layout");
+static_assert(sizeof(cgpu_ct6_tuple) == 38, "ipv6_ct_tuple layout");
 static_assert(sizeof(cgpu_ct_entry) == 56, "ct_entry layout");
 
-static inline uint4 ct_key4(const cgpu_ct4_tuple *k)
+/* a key in slot format (CtK4 / CtK6 of kernels.hip), tag bits zero */
+struct CtKey {
+	uint4 w[3];
+};
+
+static inline CtKey ct_key4(const cgpu_ct4_tuple *k)
 {
-	return uint4{k->daddr, k->saddr, (uint32_t)k->dport | ((uint32_t)k->sport << 16),
-		     (uint32_t)k->nexthdr | ((uint32_t)k->flags << 8)};
+	CtKey r{};
+	r.w[0] = uint4{k->daddr, k->saddr, (uint32_t)k->dport | ((uint32_t)k->sport << 16),
+		       (uint32_t)k->nexthdr | ((uint32_t)k->flags << 8)};
+	return r;
 }
 
-static inline cgpu_ct4_tuple ct_unkey(uint4 s)
+static inline CtKey ct_key6(const cgpu_ct6_tuple *k)
 {
-	cgpu_ct4_tuple k;
-	k.daddr = s.x;
-	k.saddr = s.y;
-	k.dport = (uint16_t)s.z;
-	k.sport = (uint16_t)(s.z >> 16);
-	k.nexthdr = (uint8_t)s.w;
-	k.flags = (uint8_t)(s.w >> 8);
+	CtKey r{};
+	r.w[0] = uint4{(uint32_t)k->dport | ((uint32_t)k->sport << 16),
+		       (uint32_t)k->nexthdr | ((uint32_t)k->flags << 8), 0u, 0u};
+	memcpy(&r.w[1], k->daddr, 16);
+	memcpy(&r.w[2], k->saddr, 16);
+	return r;
+}
+
+static inline uint32_t ctm_meta(const CtMap &m, uint32_t h)
+{
+	return m.v6 ? m.keys[4u * h].y : m.keys[h].w;
+}
+
+static inline uint32_t ctm_tag(const CtMap &m, uint32_t h) { return ctm_meta(m, h) >> 16; }
+
+static inline uint32_t ctm_hash(const CtMap &m, const CtKey &k)
+{
+	if (!m.v6)
+		return ct_hash(k.w[0].x, k.w[0].y, k.w[0].z, k.w[0].w);
+	const uint4 d = k.w[1], s = k.w[2];
+	return ct_hash(fold6(d.x, d.y, d.z, d.w), fold6(s.x, s.y, s.z, s.w), k.w[0].x, k.w[0].y);
+}
+
+static inline bool eq4(uint4 a, uint4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
+
+static inline bool ctm_same(const CtMap &m, uint32_t h, const CtKey &k)
+{
+	if (!m.v6) {
+		const uint4 s = m.keys[h];
+		return s.x == k.w[0].x && s.y == k.w[0].y && s.z == k.w[0].z &&
+		       (s.w & 0xFFFFu) == (k.w[0].w & 0xFFFFu);
+	}
+	const uint4 *s = &m.keys[4u * h];
+	return s[0].x == k.w[0].x && (s[0].y & 0xFFFFu) == (k.w[0].y & 0xFFFFu) && eq4(s[1], k.w[1]) &&
+	       eq4(s[2], k.w[2]);
+}
+
+static inline void ctm_set(CtMap &m, uint32_t h, const CtKey &k, uint32_t tag)
+{
+	if (!m.v6) {
+		m.keys[h] = uint4{k.w[0].x, k.w[0].y, k.w[0].z, (k.w[0].w & 0xFFFFu) | (tag << 16)};
+		return;
+	}
+	m.keys[4u * h] = uint4{k.w[0].x, (k.w[0].y & 0xFFFFu) | (tag << 16), 0u, 0u};
+	m.keys[4u * h + 1u] = k.w[1];
+	m.keys[4u * h + 2u] = k.w[2];
+	m.keys[4u * h + 3u] = uint4{0u, 0u, 0u, 0u};
+}
+
+static inline CtKey ctm_key_at(const CtMap &m, uint32_t h)
+{
+	CtKey k{};
+	if (!m.v6) {
+		k.w[0] = m.keys[h];
+		k.w[0].w &= 0xFFFFu;
+	} else {
+		k.w[0] = m.keys[4u * h];
+		k.w[0].y &= 0xFFFFu;
+		k.w[1] = m.keys[4u * h + 1u];
+		k.w[2] = m.keys[4u * h + 2u];
+	}
 	return k;
 }
 
-static void ct_alloc_shadow(cgpu_ctx *c)
+static void ct_alloc_shadow(CtMap &m)
 {
-	if (!c->ct_keys.empty())
+	if (!m.keys.empty())
 		return;
-	const uint32_t nslots = next_pow2((uint64_t)c->cfg.ct_max * 2u);
-	c->ct_mask = nslots - 1u;
-	c->ct_keys.assign(nslots, uint4{0, 0, 0, 0});
-	c->ct_vals.assign((size_t)nslots * 4u, uint4{0, 0, 0, 0});
+	const uint32_t nslots = next_pow2((uint64_t)m.max * 2u);
+	m.mask = nslots - 1u;
+	m.keys.assign((size_t)nslots * m.sw(), uint4{0, 0, 0, 0});
+	m.vals.assign((size_t)nslots * 4u, uint4{0, 0, 0, 0});
 }
 
 /* the probe of k_ct_walk's ct_find, on the shadow */
-static int ct_h_find(const cgpu_ctx *c, uint4 k, uint32_t *free_at)
+static int ct_h_find(const CtMap &m, const CtKey &k, uint32_t *free_at)
 {
-	uint32_t h = ct_hash(k.x, k.y, k.z, k.w) & c->ct_mask;
+	uint32_t h = ctm_hash(m, k) & m.mask;
 	uint32_t ff = UINT32_MAX;
-	for (uint32_t probe = 0; probe <= c->ct_mask; probe++) {
-		const uint4 s = c->ct_keys[h];
-		const uint32_t tag = s.w >> 16;
+	for (uint32_t probe = 0; probe <= m.mask; probe++) {
+		const uint32_t tag = ctm_tag(m, h);
 		if (tag == CT_TAG_EMPTY) {
 			*free_at = ff != UINT32_MAX ? ff : h;
 			return -1;
 		}
-		if (tag == CT_TAG_LIVE && s.x == k.x && s.y == k.y && s.z == k.z &&
-		    (s.w & 0xFFFFu) == (k.w & 0xFFFFu))
+		if (tag == CT_TAG_LIVE && ctm_same(m, h, k))
 			return (int)h;
 		if (tag == CT_TAG_TOMB && ff == UINT32_MAX)
 			ff = h;
-		h = (h + 1u) & c->ct_mask;
+		h = (h + 1u) & m.mask;
 	}
 	*free_at = ff;
 	return -1;
 }
 
 /* re-insert the live entries into clean arrays (drops tombstones) */
-static void ct_rebuild(cgpu_ctx *c)
+static void ct_rebuild(CtMap &m)
 {
-	std::vector<uint4> ok(c->ct_keys.size(), uint4{0, 0, 0, 0}), ov(c->ct_vals.size(), uint4{0, 0, 0, 0});
-	ok.swap(c->ct_keys);
-	ov.swap(c->ct_vals);
-	for (size_t i = 0; i < ok.size(); i++) {
-		if ((ok[i].w >> 16) != CT_TAG_LIVE)
+	std::vector<uint4> ok(m.keys.size(), uint4{0, 0, 0, 0}), ov(m.vals.size(), uint4{0, 0, 0, 0});
+	ok.swap(m.keys);
+	ov.swap(m.vals);
+	CtMap old;
+	old.v6 = m.v6;
+	old.keys.swap(ok);
+	for (uint32_t i = 0; i <= m.mask; i++) {
+		if (ctm_tag(old, i) != CT_TAG_LIVE)
 			continue;
-		uint32_t h = ct_hash(ok[i].x, ok[i].y, ok[i].z, ok[i].w) & c->ct_mask;
-		while ((c->ct_keys[h].w >> 16) != CT_TAG_EMPTY)
-			h = (h + 1u) & c->ct_mask;
-		c->ct_keys[h] = ok[i];
+		const CtKey k = ctm_key_at(old, i);
+		uint32_t h = ctm_hash(m, k) & m.mask;
+		while (ctm_tag(m, h) != CT_TAG_EMPTY)
+			h = (h + 1u) & m.mask;
+		ctm_set(m, h, k, CT_TAG_LIVE);
 		for (int j = 0; j < 4; j++)
-			c->ct_vals[4u * h + j] = ov[4u * i + j];
+			m.vals[4u * h + j] = ov[4u * i + j];
 	}
-	c->ct_tombs = 0;
+	m.tombs = 0;
 }
 
 /* device -> shadow after batches ran */
-static int ct_pull(cgpu_ctx *c)
+static int ct_pull(cgpu_ctx *c, CtMap &m)
 {
-	ct_alloc_shadow(c);
-	if (c->device < 0 || !c->ct_dev_newer)
+	ct_alloc_shadow(m);
+	if (c->device < 0 || !m.dev_newer)
 		return 0;
 	uint32_t cnt[2];
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(hipDeviceSynchronize());
-	HIP_OR_EIO(hipMemcpy(c->ct_keys.data(), c->d_ct_keys, c->ct_keys.size() * 16, hipMemcpyDeviceToHost));
-	HIP_OR_EIO(hipMemcpy(c->ct_vals.data(), c->d_ct_vals, c->ct_vals.size() * 16, hipMemcpyDeviceToHost));
-	HIP_OR_EIO(hipMemcpy(cnt, c->d_ct_count, 8, hipMemcpyDeviceToHost));
-	c->ct_live = cnt[0];
-	c->ct_tombs = cnt[1];
-	c->ct_dev_newer = false;
+	HIP_OR_EIO(hipMemcpy(m.keys.data(), m.d_keys, m.keys.size() * 16, hipMemcpyDeviceToHost));
+	HIP_OR_EIO(hipMemcpy(m.vals.data(), m.d_vals, m.vals.size() * 16, hipMemcpyDeviceToHost));
+	HIP_OR_EIO(hipMemcpy(cnt, m.d_count, 8, hipMemcpyDeviceToHost));
+	m.live = cnt[0];
+	m.tombs = cnt[1];
+	m.dev_newer = false;
 	return 0;
 }
 
 /* shadow -> device before a batch (allocates the device map on first use) */
-static int ct_push(cgpu_ctx *c)
+static int ct_push(CtMap &m)
 {
-	ct_alloc_shadow(c);
-	const size_t nslots = c->ct_keys.size();
-	if (!c->d_ct_keys) {
-		HIP_OR_EIO(hipMalloc((void **)&c->d_ct_keys, nslots * 16));
-		HIP_OR_EIO(hipMalloc((void **)&c->d_ct_vals, nslots * 64));
-		HIP_OR_EIO(hipMalloc((void **)&c->d_ct_count, 8));
-		c->ct_host_newer = true;
+	ct_alloc_shadow(m);
+	if (!m.d_keys) {
+		HIP_OR_EIO(hipMalloc((void **)&m.d_keys, m.keys.size() * 16));
+		HIP_OR_EIO(hipMalloc((void **)&m.d_vals, m.vals.size() * 16));
+		HIP_OR_EIO(hipMalloc((void **)&m.d_count, 8));
+		m.host_newer = true;
 	}
-	if (!c->ct_host_newer)
+	if (!m.host_newer)
 		return 0;
-	const uint32_t cnt[2] = {c->ct_live, c->ct_tombs};
-	HIP_OR_EIO(hipMemcpy(c->d_ct_keys, c->ct_keys.data(), nslots * 16, hipMemcpyHostToDevice));
-	HIP_OR_EIO(hipMemcpy(c->d_ct_vals, c->ct_vals.data(), nslots * 64, hipMemcpyHostToDevice));
-	HIP_OR_EIO(hipMemcpy(c->d_ct_count, cnt, 8, hipMemcpyHostToDevice));
-	c->ct_host_newer = false;
+	const uint32_t cnt[2] = {m.live, m.tombs};
+	HIP_OR_EIO(hipMemcpy(m.d_keys, m.keys.data(), m.keys.size() * 16, hipMemcpyHostToDevice));
+	HIP_OR_EIO(hipMemcpy(m.d_vals, m.vals.data(), m.vals.size() * 16, hipMemcpyHostToDevice));
+	HIP_OR_EIO(hipMemcpy(m.d_count, cnt, 8, hipMemcpyHostToDevice));
+	m.host_newer = false;
 	return 0;
 }
 
-static int ct_check(cgpu_ctx *c, const void *key)
+static int ct_update_l(cgpu_ctx *c, CtMap &m, const CtKey &k, const cgpu_ct_entry *val, uint64_t flags)
 {
-	if (!c || !key)
-		return fail(-EINVAL, "null argument");
-	return 0;
-}
-
-CGPU_EXPORT int cgpu_ct4_update(cgpu_ctx *c, const cgpu_ct4_tuple *key, const cgpu_ct_entry *val,
-				uint64_t flags)
-{
-	if (int r = ct_check(c, key))
-		return r;
 	if (!val)
 		return fail(-EINVAL, "null value");
 	if (int r = check_flags(flags))
 		return r;
 	std::lock_guard<std::mutex> g(c->mu);
-	if (int r = ct_pull(c))
+	if (int r = ct_pull(c, m))
 		return r;
-	const uint4 k = ct_key4(key);
 	uint32_t free_at;
-	int slot = ct_h_find(c, k, &free_at);
+	int slot = ct_h_find(m, k, &free_at);
 	if (slot >= 0 && flags == CGPU_NOEXIST)
 		return fail(-EEXIST, "conntrack entry exists");
 	if (slot < 0) {
 		if (flags == CGPU_EXIST)
 			return fail(-ENOENT, "no such conntrack entry");
-		if (c->ct_live >= c->cfg.ct_max)
-			return fail(-E2BIG, "conntrack map full (%u entries)", c->cfg.ct_max);
+		if (m.live >= m.max)
+			return fail(-E2BIG, "conntrack map full (%u entries)", m.max);
 		if (free_at == UINT32_MAX) {
-			ct_rebuild(c);
-			(void)ct_h_find(c, k, &free_at);
+			ct_rebuild(m);
+			(void)ct_h_find(m, k, &free_at);
 		}
-		if ((c->ct_keys[free_at].w >> 16) == CT_TAG_TOMB)
-			c->ct_tombs--;
+		if (ctm_tag(m, free_at) == CT_TAG_TOMB)
+			m.tombs--;
 		slot = (int)free_at;
-		c->ct_keys[slot] = uint4{k.x, k.y, k.z, k.w | (CT_TAG_LIVE << 16)};
-		c->ct_live++;
+		ctm_set(m, (uint32_t)slot, k, CT_TAG_LIVE);
+		m.live++;
 	}
 	uint4 row[4] = {};
 	memcpy(row, val, sizeof(*val));
 	for (int j = 0; j < 4; j++)
-		c->ct_vals[4u * slot + j] = row[j];
-	c->ct_host_newer = true;
+		m.vals[4u * slot + j] = row[j];
+	m.host_newer = true;
 	return 0;
+}
+
+static int ct_delete_l(cgpu_ctx *c, CtMap &m, const CtKey &k)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c, m))
+		return r;
+	uint32_t free_at;
+	const int slot = ct_h_find(m, k, &free_at);
+	if (slot < 0)
+		return fail(-ENOENT, "no such conntrack entry");
+	ctm_set(m, (uint32_t)slot, CtKey{}, CT_TAG_TOMB);
+	for (int j = 0; j < 4; j++)
+		m.vals[4u * slot + j] = uint4{0, 0, 0, 0};
+	m.live--;
+	m.tombs++;
+	if (m.tombs > (m.mask + 1u) / 4u)
+		ct_rebuild(m);
+	m.host_newer = true;
+	return 0;
+}
+
+static int ct_lookup_l(cgpu_ctx *c, CtMap &m, const CtKey &k, cgpu_ct_entry *val_out)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c, m))
+		return r;
+	uint32_t free_at;
+	const int slot = ct_h_find(m, k, &free_at);
+	if (slot < 0)
+		return fail(-ENOENT, "no such conntrack entry");
+	if (val_out)
+		memcpy(val_out, &m.vals[4u * slot], sizeof(*val_out));
+	return 0;
+}
+
+/* GetNextKey in slot order (a missing key restarts from the first): the
+ * live key after `k` (or the first when k is null), in slot format */
+static int ct_next_l(cgpu_ctx *c, CtMap &m, const CtKey *k, CtKey *next)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c, m))
+		return r;
+	uint32_t from = 0;
+	if (k) {
+		uint32_t free_at;
+		const int slot = ct_h_find(m, *k, &free_at);
+		if (slot >= 0)
+			from = (uint32_t)slot + 1u;
+	}
+	for (uint64_t i = from; i <= m.mask; i++)
+		if (ctm_tag(m, (uint32_t)i) == CT_TAG_LIVE) {
+			*next = ctm_key_at(m, (uint32_t)i);
+			return 0;
+		}
+	return -ENOENT;
+}
+
+static size_t ct_count_l(cgpu_ctx *c, CtMap &m)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	if (ct_pull(c, m))
+		return 0;
+	return m.live;
+}
+
+static int ct_gc_l(cgpu_ctx *c, CtMap &m, uint32_t time, uint64_t *deleted_out)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	if (int r = ct_pull(c, m))
+		return r;
+	uint64_t del = 0;
+	for (uint32_t i = 0; i <= m.mask; i++) {
+		if (ctm_tag(m, i) != CT_TAG_LIVE)
+			continue;
+		const uint32_t lifetime = m.vals[4u * i + 2u].x;
+		if (lifetime < time) { /* doFiltering: RemoveExpired && Lifetime < Time */
+			ctm_set(m, i, CtKey{}, CT_TAG_TOMB);
+			for (int j = 0; j < 4; j++)
+				m.vals[4u * i + j] = uint4{0, 0, 0, 0};
+			m.live--;
+			del++;
+		}
+	}
+	ct_rebuild(m);
+	m.host_newer = true;
+	if (deleted_out)
+		*deleted_out = del;
+	return 0;
+}
+
+static int ct_flush_l(cgpu_ctx *c, CtMap &m)
+{
+	std::lock_guard<std::mutex> g(c->mu);
+	ct_alloc_shadow(m);
+	std::fill(m.keys.begin(), m.keys.end(), uint4{0, 0, 0, 0});
+	std::fill(m.vals.begin(), m.vals.end(), uint4{0, 0, 0, 0});
+	m.live = m.tombs = 0;
+	m.dev_newer = false;
+	m.host_newer = true;
+	if (c->device >= 0 && m.d_keys) {
+		/* empty the device map in place (tags and counts; rows are
+		 * rewritten whole by every insert) instead of re-uploading */
+		HIP_OR_EIO(hipSetDevice(c->device));
+		HIP_OR_EIO(hipDeviceSynchronize());
+		HIP_OR_EIO(hipMemset(m.d_keys, 0, m.keys.size() * 16));
+		HIP_OR_EIO(hipMemset(m.d_count, 0, 8));
+		HIP_OR_EIO(hipDeviceSynchronize());
+		m.host_newer = false;
+	}
+	return 0;
+}
+
+static cgpu_ct4_tuple ct_unkey4(const CtKey &k)
+{
+	cgpu_ct4_tuple t;
+	t.daddr = k.w[0].x;
+	t.saddr = k.w[0].y;
+	t.dport = (uint16_t)k.w[0].z;
+	t.sport = (uint16_t)(k.w[0].z >> 16);
+	t.nexthdr = (uint8_t)k.w[0].w;
+	t.flags = (uint8_t)(k.w[0].w >> 8);
+	return t;
+}
+
+static cgpu_ct6_tuple ct_unkey6(const CtKey &k)
+{
+	cgpu_ct6_tuple t;
+	memcpy(t.daddr, &k.w[1], 16);
+	memcpy(t.saddr, &k.w[2], 16);
+	t.dport = (uint16_t)k.w[0].x;
+	t.sport = (uint16_t)(k.w[0].x >> 16);
+	t.nexthdr = (uint8_t)k.w[0].y;
+	t.flags = (uint8_t)(k.w[0].y >> 8);
+	return t;
+}
+
+/* ---- cilium_ct4_global ---- */
+CGPU_EXPORT int cgpu_ct4_update(cgpu_ctx *c, const cgpu_ct4_tuple *key, const cgpu_ct_entry *val,
+				uint64_t flags)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	return ct_update_l(c, c->ct4, ct_key4(key), val, flags);
 }
 
 CGPU_EXPORT int cgpu_ct4_delete(cgpu_ctx *c, const cgpu_ct4_tuple *key)
 {
-	if (int r = ct_check(c, key))
-		return r;
-	std::lock_guard<std::mutex> g(c->mu);
-	if (int r = ct_pull(c))
-		return r;
-	uint32_t free_at;
-	const int slot = ct_h_find(c, ct_key4(key), &free_at);
-	if (slot < 0)
-		return fail(-ENOENT, "no such conntrack entry");
-	c->ct_keys[slot] = uint4{0, 0, 0, CT_TAG_TOMB << 16};
-	for (int j = 0; j < 4; j++)
-		c->ct_vals[4u * slot + j] = uint4{0, 0, 0, 0};
-	c->ct_live--;
-	c->ct_tombs++;
-	if (c->ct_tombs > (c->ct_mask + 1u) / 4u)
-		ct_rebuild(c);
-	c->ct_host_newer = true;
-	return 0;
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	return ct_delete_l(c, c->ct4, ct_key4(key));
 }
 
 CGPU_EXPORT int cgpu_ct4_lookup(cgpu_ctx *c, const cgpu_ct4_tuple *key, cgpu_ct_entry *val_out)
 {
-	if (int r = ct_check(c, key))
-		return r;
-	std::lock_guard<std::mutex> g(c->mu);
-	if (int r = ct_pull(c))
-		return r;
-	uint32_t free_at;
-	const int slot = ct_h_find(c, ct_key4(key), &free_at);
-	if (slot < 0)
-		return fail(-ENOENT, "no such conntrack entry");
-	if (val_out)
-		memcpy(val_out, &c->ct_vals[4u * slot], sizeof(*val_out));
-	return 0;
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	return ct_lookup_l(c, c->ct4, ct_key4(key), val_out);
 }
 
 CGPU_EXPORT int cgpu_ct4_get_next_key(cgpu_ctx *c, const cgpu_ct4_tuple *key, cgpu_ct4_tuple *next_out)
 {
 	if (!c || !next_out)
 		return fail(-EINVAL, "null argument");
-	std::lock_guard<std::mutex> g(c->mu);
-	if (int r = ct_pull(c))
-		return r;
-	size_t from = 0;
-	if (key) { /* bpf(2) GetNextKey: a missing key restarts from the first */
-		uint32_t free_at;
-		const int slot = ct_h_find(c, ct_key4(key), &free_at);
-		if (slot >= 0)
-			from = (size_t)slot + 1u;
-	}
-	for (size_t i = from; i < c->ct_keys.size(); i++)
-		if ((c->ct_keys[i].w >> 16) == CT_TAG_LIVE) {
-			*next_out = ct_unkey(c->ct_keys[i]);
-			return 0;
-		}
-	return -ENOENT;
+	CtKey k = key ? ct_key4(key) : CtKey{}, nk;
+	const int r = ct_next_l(c, c->ct4, key ? &k : nullptr, &nk);
+	if (!r)
+		*next_out = ct_unkey4(nk);
+	return r;
 }
 
-CGPU_EXPORT size_t cgpu_ct4_count(cgpu_ctx *c)
-{
-	if (!c)
-		return 0;
-	std::lock_guard<std::mutex> g(c->mu);
-	if (ct_pull(c))
-		return 0;
-	return c->ct_live;
-}
+CGPU_EXPORT size_t cgpu_ct4_count(cgpu_ctx *c) { return c ? ct_count_l(c, c->ct4) : 0; }
 
 CGPU_EXPORT int cgpu_ct4_gc(cgpu_ctx *c, uint32_t time, uint64_t *deleted_out)
 {
 	if (!c)
 		return fail(-EINVAL, "null context");
-	std::lock_guard<std::mutex> g(c->mu);
-	if (int r = ct_pull(c))
-		return r;
-	uint64_t del = 0;
-	for (size_t i = 0; i < c->ct_keys.size(); i++) {
-		if ((c->ct_keys[i].w >> 16) != CT_TAG_LIVE)
-			continue;
-		const uint32_t lifetime = c->ct_vals[4u * i + 2u].x;
-		if (lifetime < time) { /* doFiltering: RemoveExpired && Lifetime < Time */
-			c->ct_keys[i] = uint4{0, 0, 0, CT_TAG_TOMB << 16};
-			for (int j = 0; j < 4; j++)
-				c->ct_vals[4u * i + j] = uint4{0, 0, 0, 0};
-			c->ct_live--;
-			del++;
-		}
-	}
-	ct_rebuild(c);
-	c->ct_host_newer = true;
-	if (deleted_out)
-		*deleted_out = del;
-	return 0;
+	return ct_gc_l(c, c->ct4, time, deleted_out);
 }
 
 CGPU_EXPORT int cgpu_ct4_flush(cgpu_ctx *c)
 {
 	if (!c)
 		return fail(-EINVAL, "null context");
-	std::lock_guard<std::mutex> g(c->mu);
-	ct_alloc_shadow(c);
-	std::fill(c->ct_keys.begin(), c->ct_keys.end(), uint4{0, 0, 0, 0});
-	std::fill(c->ct_vals.begin(), c->ct_vals.end(), uint4{0, 0, 0, 0});
-	c->ct_live = c->ct_tombs = 0;
-	c->ct_dev_newer = false;
-	c->ct_host_newer = true;
-	if (c->device >= 0 && c->d_ct_keys) {
-		/* empty the device map in place (tags and counts; rows are
-		 * rewritten whole by every insert) instead of re-uploading */
-		HIP_OR_EIO(hipSetDevice(c->device));
-		HIP_OR_EIO(hipDeviceSynchronize());
-		HIP_OR_EIO(hipMemset(c->d_ct_keys, 0, c->ct_keys.size() * 16));
-		HIP_OR_EIO(hipMemset(c->d_ct_count, 0, 8));
-		HIP_OR_EIO(hipDeviceSynchronize());
-		c->ct_host_newer = false;
-	}
-	return 0;
+	return ct_flush_l(c, c->ct4);
 }
 
-/* scratch of one cgpu_classify_v4_ct launch over n packets */
+/* ---- cilium_ct6_global ---- */
+CGPU_EXPORT int cgpu_ct6_update(cgpu_ctx *c, const cgpu_ct6_tuple *key, const cgpu_ct_entry *val,
+				uint64_t flags)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	return ct_update_l(c, c->ct6, ct_key6(key), val, flags);
+}
+
+CGPU_EXPORT int cgpu_ct6_delete(cgpu_ctx *c, const cgpu_ct6_tuple *key)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	return ct_delete_l(c, c->ct6, ct_key6(key));
+}
+
+CGPU_EXPORT int cgpu_ct6_lookup(cgpu_ctx *c, const cgpu_ct6_tuple *key, cgpu_ct_entry *val_out)
+{
+	if (!c || !key)
+		return fail(-EINVAL, "null argument");
+	return ct_lookup_l(c, c->ct6, ct_key6(key), val_out);
+}
+
+CGPU_EXPORT int cgpu_ct6_get_next_key(cgpu_ctx *c, const cgpu_ct6_tuple *key, cgpu_ct6_tuple *next_out)
+{
+	if (!c || !next_out)
+		return fail(-EINVAL, "null argument");
+	CtKey k = key ? ct_key6(key) : CtKey{}, nk;
+	const int r = ct_next_l(c, c->ct6, key ? &k : nullptr, &nk);
+	if (!r)
+		*next_out = ct_unkey6(nk);
+	return r;
+}
+
+CGPU_EXPORT size_t cgpu_ct6_count(cgpu_ctx *c) { return c ? ct_count_l(c, c->ct6) : 0; }
+
+CGPU_EXPORT int cgpu_ct6_gc(cgpu_ctx *c, uint32_t time, uint64_t *deleted_out)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	return ct_gc_l(c, c->ct6, time, deleted_out);
+}
+
+CGPU_EXPORT int cgpu_ct6_flush(cgpu_ctx *c)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	return ct_flush_l(c, c->ct6);
+}
+
+/* scratch of one cgpu_classify_v{4,6}_ct launch over n packets */
 struct CtScratch {
 	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, heads_pos, head,
 		temp, temp_bytes, total;
 };
 
-static CtScratch ct_scratch_layout(uint64_t n)
+static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes)
 {
 	CtScratch L{};
 	auto take = [&](size_t bytes) {
@@ -4175,7 +4356,7 @@ static CtScratch ct_scratch_layout(uint64_t n)
 		L.total += (bytes + 255) & ~(size_t)255;
 		return off;
 	};
-	L.rec = take(n * 32);
+	L.rec = take(n * rec_bytes);
 	L.gkey = take(n * 4);
 	L.gkey_sorted = take(n * 4);
 	L.idx = take(n * 4);
@@ -4189,22 +4370,10 @@ static CtScratch ct_scratch_layout(uint64_t n)
 	return L;
 }
 
-CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, size_t n, uint32_t now,
-				    int32_t *verdict, uint8_t *ct_ret, uint32_t *identity,
-				    uint8_t *stage, void *stream)
+/* one stateful batch on map m: columns already validated by the caller */
+static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtMap &m, ct_launch a,
+		       void *stream)
 {
-	Pinned P;
-	if (int r = pin(c, stream, P))
-		return r;
-	const cgpu_snapshot &s = P.snap();
-	uint64_t *delta = P.delta;
-	if (!t || (n && (!t->saddr || !t->daddr || !t->sport || !t->dport || !t->proto || !t->l4 ||
-			 !t->flags || !t->len || !t->ep || !verdict || !ct_ret || !identity)))
-		return fail(-EINVAL, "null tuple column or output");
-	if (n > (size_t)INT32_MAX)
-		return fail(-EINVAL, "batch of %zu packets exceeds 2^31 - 1", n);
-	if (!n)
-		return 0;
 	/* One conntrack map, one scratch: every batch runs on the context's
 	 * conntrack stream, after the caller's stream reaches this call (its
 	 * inputs), and the caller's stream then waits for the batch. */
@@ -4213,25 +4382,25 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 	const hipStream_t cs = c->ct_stream;
 	HIP_OR_EIO(hipEventRecord(c->ct_done, (hipStream_t)stream));
 	HIP_OR_EIO(hipStreamWaitEvent(cs, c->ct_done, 0));
-	uint32_t live = c->ct_live;
-	if (c->d_ct_count && !c->ct_host_newer) {
+	uint32_t live = m.live;
+	if (m.d_count && !m.host_newer) {
 		/* tombstones left by the device's deletes: compact before they
 		 * lengthen every probe chain (the host reads the count after the
 		 * previous batch: the one host synchronisation of this call) */
 		uint32_t cnt[2];
-		HIP_OR_EIO(hipMemcpyAsync(cnt, c->d_ct_count, 8, hipMemcpyDeviceToHost, cs));
+		HIP_OR_EIO(hipMemcpyAsync(cnt, m.d_count, 8, hipMemcpyDeviceToHost, cs));
 		HIP_OR_EIO(hipStreamSynchronize(cs));
 		live = cnt[0];
-		if (cnt[1] > (c->ct_mask + 1u) / 4u) {
-			if (int r = ct_pull(c))
+		if (cnt[1] > (m.mask + 1u) / 4u) {
+			if (int r = ct_pull(c, m))
 				return r;
-			ct_rebuild(c);
-			c->ct_host_newer = true;
+			ct_rebuild(m);
+			m.host_newer = true;
 		}
 	}
-	if (int r = ct_push(c))
+	if (int r = ct_push(m))
 		return r;
-	const CtScratch L = ct_scratch_layout(n);
+	const CtScratch L = ct_scratch_layout(a.n, m.v6 ? 64 : 32);
 	if (L.total > c->ct_scratch_cap) {
 		HIP_OR_EIO(hipStreamSynchronize(cs));
 		(void)hipFree(c->d_ct_scratch);
@@ -4243,22 +4412,94 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 	uint8_t *b = static_cast<uint8_t *>(c->d_ct_scratch);
 	/* every walker wave (2048 x 4) holding a chunk stays under a quarter
 	 * of the headroom */
-	const uint32_t headroom = c->cfg.ct_max > live ? c->cfg.ct_max - live : 0u;
+	const uint32_t headroom = m.max > live ? m.max - live : 0u;
 	const uint32_t chunk = std::min<uint32_t>(256u, std::max<uint32_t>(1u, headroom / 32768u));
-	ct_table T{c->d_ct_keys, c->d_ct_vals, c->ct_mask, c->cfg.ct_max, c->d_ct_count, chunk};
-	ct_launch a{t->saddr, t->daddr, t->sport, t->dport, t->proto, t->l4, t->flags, t->len, t->ep,
-		    verdict, ct_ret, identity, stage, delta, (uint64_t)n, now,
-		    reinterpret_cast<uint4 *>(b + L.rec),
-		    reinterpret_cast<uint32_t *>(b + L.gkey),
-		    reinterpret_cast<uint32_t *>(b + L.gkey_sorted), reinterpret_cast<uint32_t *>(b + L.idx),
-		    reinterpret_cast<uint32_t *>(b + L.idx_sorted), b + L.head,
-		    reinterpret_cast<uint32_t *>(b + L.heads), reinterpret_cast<uint32_t *>(b + L.n_heads),
-		    reinterpret_cast<uint32_t *>(b + L.heads_pos), b + L.temp, L.temp_bytes};
-	HIP_OR_EIO(launch_classify_v4_ct(s, T, a, cs));
+	ct_table T{m.d_keys, m.d_vals, m.mask, m.max, m.d_count, chunk};
+	a.delta = delta;
+	a.rec = reinterpret_cast<uint4 *>(b + L.rec);
+	a.gkey = reinterpret_cast<uint32_t *>(b + L.gkey);
+	a.gkey_sorted = reinterpret_cast<uint32_t *>(b + L.gkey_sorted);
+	a.idx = reinterpret_cast<uint32_t *>(b + L.idx);
+	a.idx_sorted = reinterpret_cast<uint32_t *>(b + L.idx_sorted);
+	a.head = b + L.head;
+	a.heads = reinterpret_cast<uint32_t *>(b + L.heads);
+	a.n_heads = reinterpret_cast<uint32_t *>(b + L.n_heads);
+	a.heads_pos = reinterpret_cast<uint32_t *>(b + L.heads_pos);
+	a.temp = b + L.temp;
+	a.temp_bytes = L.temp_bytes;
+	HIP_OR_EIO(m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs));
 	HIP_OR_EIO(hipEventRecord(c->ct_done, cs));
 	HIP_OR_EIO(hipStreamWaitEvent((hipStream_t)stream, c->ct_done, 0));
-	c->ct_dev_newer = true;
+	m.dev_newer = true;
 	return 0;
+}
+
+CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, size_t n, uint32_t now,
+				    int32_t *verdict, uint8_t *ct_ret, uint32_t *identity,
+				    uint8_t *stage, void *stream)
+{
+	Pinned P;
+	if (int r = pin(c, stream, P))
+		return r;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->sport || !t->dport || !t->proto || !t->l4 ||
+			 !t->flags || !t->len || !t->ep || !verdict || !ct_ret || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n > (size_t)INT32_MAX)
+		return fail(-EINVAL, "batch of %zu packets exceeds 2^31 - 1", n);
+	if (!n)
+		return 0;
+	ct_launch a{};
+	a.saddr = t->saddr;
+	a.daddr = t->daddr;
+	a.sport = t->sport;
+	a.dport = t->dport;
+	a.proto = t->proto;
+	a.l4 = t->l4;
+	a.flags = t->flags;
+	a.len = t->len;
+	a.ep = t->ep;
+	a.verdict = verdict;
+	a.ct_ret = ct_ret;
+	a.identity = identity;
+	a.stage = stage;
+	a.n = n;
+	a.now = now;
+	return ct_classify(c, P.snap(), P.delta, c->ct4, a, stream);
+}
+
+CGPU_EXPORT int cgpu_classify_v6_ct(cgpu_ctx *c, const cgpu_tuples_v6_ct *t, size_t n, uint32_t now,
+				    int32_t *verdict, uint8_t *ct_ret, uint32_t *identity,
+				    uint8_t *stage, void *stream)
+{
+	Pinned P;
+	if (int r = pin(c, stream, P))
+		return r;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->sport || !t->dport || !t->proto || !t->l4 ||
+			 !t->flags || !t->len || !t->ep || !verdict || !ct_ret || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n && (((uintptr_t)t->saddr | (uintptr_t)t->daddr) & 15))
+		return fail(-EINVAL, "IPv6 address columns must be 16-byte aligned");
+	if (n > (size_t)INT32_MAX)
+		return fail(-EINVAL, "batch of %zu packets exceeds 2^31 - 1", n);
+	if (!n)
+		return 0;
+	ct_launch a{};
+	a.saddr = t->saddr;
+	a.daddr = t->daddr;
+	a.sport = t->sport;
+	a.dport = t->dport;
+	a.proto = t->proto;
+	a.l4 = t->l4;
+	a.flags = t->flags;
+	a.len = t->len;
+	a.ep = t->ep;
+	a.verdict = verdict;
+	a.ct_ret = ct_ret;
+	a.identity = identity;
+	a.stage = stage;
+	a.n = n;
+	a.now = now;
+	return ct_classify(c, P.snap(), P.delta, c->ct6, a, stream);
 }
 
 /* ======================================================================= */

@@ -2834,34 +2834,146 @@ __device__ __forceinline__ void ct_hit(ct_row &e, uint32_t meta, bool ingress, u
 	}
 }
 
-__device__ __forceinline__ bool ct_same(uint4 s, uint4 k)
+__device__ __forceinline__ uint4 sel4(bool t, uint4 a, uint4 b)
 {
-	return s.x == k.x && s.y == k.y && s.z == k.z && (s.w & 0xFFFFu) == (k.w & 0xFFFFu);
+	return uint4{t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z, t ? a.w : b.w};
 }
 
-/* Probe for k (low 16 bits of .w = nexthdr | flags << 8).  Returns the slot
- * or -1; *free_at = the first tombstone on the chain, else the empty slot
- * that ended it (where an insert of k may start). */
-__device__ __forceinline__ int ct_find(const ct_table &T, uint4 k, uint32_t *free_at)
+/* The two maps' key slots (tables.h ct_table), as traits of one walker:
+ *   CtK4 cilium_ct4_global: keys[h] = {daddr, saddr, dport | sport << 16,
+ *        nexthdr | flags << 8 | tag << 16} (struct ipv4_ct_tuple, 16 B)
+ *   CtK6 cilium_ct6_global: keys[4h .. 4h + 3] = {dport | sport << 16,
+ *        nexthdr | flags << 8 | tag << 16, 0, 0}, {daddr}, {saddr}, {0}
+ *        (struct ipv6_ct_tuple in one 64-B line: a probe is one line)
+ * In a lane's cache the upper half of the meta word (the tag in the map)
+ * holds the CTC_* state instead. */
+struct CtK4 {
+	typedef uint4 key;
+	static constexpr int V6 = 0;
+	__device__ static uint32_t &meta(key &k) { return k.w; }
+	__device__ static uint32_t cmeta(const key &k) { return k.w; }
+	__device__ static uint32_t hash(const key &k) { return ct_hash(k.x, k.y, k.z, k.w); }
+	__device__ static bool same(const key &s, const key &k)
+	{
+		return s.x == k.x && s.y == k.y && s.z == k.z && (s.w & 0xFFFFu) == (k.w & 0xFFFFu);
+	}
+	__device__ static uint32_t *tagp(const ct_table &T, uint32_t h) { return &T.keys[h].w; }
+	__device__ static key load(const ct_table &T, uint32_t h) { return ld_x4<true>(T.keys + h); }
+	/* the key words (not the meta word) again, at the coherence point */
+	__device__ static void reload(const ct_table &T, uint32_t h, key &s)
+	{
+		const uint64_t xy = __hip_atomic_load(reinterpret_cast<uint64_t *>(T.keys + h), __ATOMIC_RELAXED,
+						      __HIP_MEMORY_SCOPE_AGENT);
+		s.x = (uint32_t)xy;
+		s.y = (uint32_t)(xy >> 32);
+		s.z = __hip_atomic_load(&T.keys[h].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+	__device__ static void store(const ct_table &T, uint32_t h, const key &k)
+	{
+		uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + h);
+		st_wt64(p, k.x, k.y);
+		st_wt32(p + 2, k.z);
+	}
+	__device__ static void clear(const ct_table &T, uint32_t h)
+	{
+		uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + h);
+		st_wt64(p, 0u, 0u);
+		st_wt32(p + 2, 0u);
+	}
+	__device__ static key sel(bool t, const key &a, const key &b) { return sel4(t, a, b); }
+	/* ipv4_ct_tuple_reverse, conntrack.h:414-431 */
+	__device__ static key reversed(const key &k)
+	{
+		return uint4{k.y, k.x, (k.z >> 16) | (k.z << 16), k.w ^ (TUPLE_F_IN << 8)};
+	}
+	/* ct_create4's ICMP entry relating errors, conntrack.h:722-733 */
+	__device__ static key related(const key &k)
+	{
+		return uint4{k.x, k.y, 0u, 1u | ((((k.w >> 8) & 0xFFu) | TUPLE_F_RELATED) << 8)};
+	}
+};
+
+struct CtK6 {
+	struct key {
+		uint4 d, s;
+		uint32_t p, m;
+	};
+	static constexpr int V6 = 1;
+	__device__ static uint32_t &meta(key &k) { return k.m; }
+	__device__ static uint32_t cmeta(const key &k) { return k.m; }
+	__device__ static uint32_t hash(const key &k)
+	{
+		return ct_hash(fold6(k.d.x, k.d.y, k.d.z, k.d.w), fold6(k.s.x, k.s.y, k.s.z, k.s.w), k.p, k.m);
+	}
+	__device__ static bool same(const key &a, const key &b)
+	{
+		return a.p == b.p && (a.m & 0xFFFFu) == (b.m & 0xFFFFu) && a.d.x == b.d.x && a.d.y == b.d.y &&
+		       a.d.z == b.d.z && a.d.w == b.d.w && a.s.x == b.s.x && a.s.y == b.s.y && a.s.z == b.s.z &&
+		       a.s.w == b.s.w;
+	}
+	__device__ static uint32_t *tagp(const ct_table &T, uint32_t h) { return &T.keys[4u * h].y; }
+	__device__ static key load(const ct_table &T, uint32_t h)
+	{
+		const uint4 m = ld_x4<true>(T.keys + 4u * h);
+		return key{ld_x4<true>(T.keys + 4u * h + 1u), ld_x4<true>(T.keys + 4u * h + 2u), m.x, m.y};
+	}
+	__device__ static uint4 load_coherent4(const uint4 *q)
+	{
+		const uint64_t lo = __hip_atomic_load(reinterpret_cast<const uint64_t *>(q), __ATOMIC_RELAXED,
+						      __HIP_MEMORY_SCOPE_AGENT);
+		const uint64_t hi = __hip_atomic_load(reinterpret_cast<const uint64_t *>(q) + 1, __ATOMIC_RELAXED,
+						      __HIP_MEMORY_SCOPE_AGENT);
+		return uint4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+	}
+	__device__ static void reload(const ct_table &T, uint32_t h, key &s)
+	{
+		s.p = __hip_atomic_load(&T.keys[4u * h].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		s.d = load_coherent4(T.keys + 4u * h + 1u);
+		s.s = load_coherent4(T.keys + 4u * h + 2u);
+	}
+	__device__ static void store(const ct_table &T, uint32_t h, const key &k)
+	{
+		uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + 4u * h);
+		st_wt32(p, k.p);
+		st_wt64(p + 4, k.d.x, k.d.y);
+		st_wt64(p + 6, k.d.z, k.d.w);
+		st_wt64(p + 8, k.s.x, k.s.y);
+		st_wt64(p + 10, k.s.z, k.s.w);
+	}
+	__device__ static void clear(const ct_table &T, uint32_t h)
+	{
+		store(T, h, key{uint4{0u, 0u, 0u, 0u}, uint4{0u, 0u, 0u, 0u}, 0u, 0u});
+	}
+	__device__ static key sel(bool t, const key &a, const key &b)
+	{
+		return key{sel4(t, a.d, b.d), sel4(t, a.s, b.s), t ? a.p : b.p, t ? a.m : b.m};
+	}
+	/* ipv6_ct_tuple_reverse, conntrack.h:265-285 */
+	__device__ static key reversed(const key &k)
+	{
+		return key{k.s, k.d, (k.p >> 16) | (k.p << 16), k.m ^ (TUPLE_F_IN << 8)};
+	}
+	/* ct_create6's ICMPv6 entry relating errors, conntrack.h:617-629 */
+	__device__ static key related(const key &k)
+	{
+		return key{k.d, k.s, 0u, 58u | ((((k.m >> 8) & 0xFFu) | TUPLE_F_RELATED) << 8)};
+	}
+};
+
+/* Probe for k (low 16 bits of the meta word = nexthdr | flags << 8).
+ * Returns the slot or -1; *free_at = the first tombstone on the chain, else
+ * the empty slot that ended it (where an insert of k may start). */
+template <class K>
+__device__ __forceinline__ int ct_find(const ct_table &T, const typename K::key &k, uint32_t *free_at)
 {
-	uint32_t h = ct_hash(k.x, k.y, k.z, k.w) & T.mask;
+	uint32_t h = K::hash(k) & T.mask;
 	uint32_t ff = 0xFFFFFFFFu;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
+		typename K::key s = K::load(T, h);
+		uint32_t tag = K::meta(s) >> 16;
 #ifdef CGPU_DIAG_CT_COHERENT_PROBE /* timing-only tool build: every slot read at the coherence point */
-		const uint64_t xy0 = __hip_atomic_load(reinterpret_cast<uint64_t *>(T.keys + h), __ATOMIC_RELAXED,
-						       __HIP_MEMORY_SCOPE_AGENT);
-		const uint64_t zw0 = __hip_atomic_load(reinterpret_cast<uint64_t *>(T.keys + h) + 1, __ATOMIC_RELAXED,
-						       __HIP_MEMORY_SCOPE_AGENT);
-		uint4 s = make_uint4((uint32_t)xy0, (uint32_t)(xy0 >> 32), (uint32_t)zw0, (uint32_t)(zw0 >> 32));
-		uint32_t tag = s.w >> 16;
-		if (tag == CT_TAG_EMPTY) {
-			*free_at = ff != 0xFFFFFFFFu ? ff : h;
-			return -1;
-		}
-		if (false) {
+		if (true) {
 #else
-		uint4 s = ld_x4<true>(T.keys + h);
-		uint32_t tag = s.w >> 16;
 		if (tag == CT_TAG_EMPTY) {
 #endif
 			/* the chain ends only on an EMPTY read at the coherence point:
@@ -2871,19 +2983,15 @@ __device__ __forceinline__ int ct_find(const ct_table &T, uint4 k, uint32_t *fre
 			 * lane inserted past it.  Tags never return to EMPTY, so one
 			 * agent-scope re-read settles it; key words written after a
 			 * claim are re-read the same way. */
-			s.w = __hip_atomic_load(&T.keys[h].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			tag = s.w >> 16;
+			K::meta(s) = __hip_atomic_load(K::tagp(T, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			tag = K::meta(s) >> 16;
 			if (tag == CT_TAG_EMPTY) {
 				*free_at = ff != 0xFFFFFFFFu ? ff : h;
 				return -1;
 			}
-			const uint64_t xy = __hip_atomic_load(reinterpret_cast<uint64_t *>(T.keys + h),
-							      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			s.x = (uint32_t)xy;
-			s.y = (uint32_t)(xy >> 32);
-			s.z = __hip_atomic_load(&T.keys[h].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			K::reload(T, h, s);
 		}
-		if (tag == CT_TAG_LIVE && ct_same(s, k))
+		if (tag == CT_TAG_LIVE && K::same(s, k))
 			return (int)h;
 		if (tag == CT_TAG_TOMB && ff == 0xFFFFFFFFu)
 			ff = h;
@@ -2941,25 +3049,26 @@ __device__ __forceinline__ bool ct_take(const ct_table &T, const ct_acct &A)
 	return false;
 }
 
+
 /* Insert absent k at the first free slot from `from` on (htab_map_update_elem
  * of a new key: -E2BIG past max_elem).  Returns the slot or -1. */
-__device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, uint4 k, uint32_t from)
+template <class K>
+__device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, const typename K::key &k,
+					 uint32_t from)
 {
 	if (!ct_take(T, A))
 		return -1;
 	uint32_t h = from & T.mask;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
-		const uint4 s = ld_x4<true>(T.keys + h);
-		const uint32_t tag = s.w >> 16;
+		typename K::key s = K::load(T, h);
+		const uint32_t tag = K::meta(s) >> 16;
 		if (tag == CT_TAG_EMPTY || tag == CT_TAG_TOMB) {
 			const uint32_t expect = tag << 16;
-			const uint32_t want = (k.w & 0xFFFFu) | (CT_TAG_LIVE << 16);
-			if (atomicCAS(&T.keys[h].w, expect, want) == expect) {
+			const uint32_t want = (K::cmeta(k) & 0xFFFFu) | (CT_TAG_LIVE << 16);
+			if (atomicCAS(K::tagp(T, h), expect, want) == expect) {
 				if (tag == CT_TAG_TOMB)
 					atomicSub(A.tombs, 1);
-				uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + h);
-				st_wt64(p, k.x, k.y);
-				st_wt32(p + 2, k.z);
+				K::store(T, h, k);
 				__builtin_amdgcn_s_waitcnt(0);
 				return (int)h;
 			}
@@ -2975,20 +3084,17 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, ui
  * write-through, so draining this lane's outstanding stores (vmcnt 0) is
  * the whole release: no L2 write-back (an agent-scope release fence would
  * write back the XCD's entire L2 for every delete). */
-__device__ __forceinline__ void ct_erase(const ct_table &T, const ct_acct &A, uint32_t slot)
+template <class K> __device__ __forceinline__ void ct_erase(const ct_table &T, const ct_acct &A, uint32_t slot)
 {
-	uint32_t *p = reinterpret_cast<uint32_t *>(T.keys + slot);
-	st_wt64(p, 0u, 0u);
-	st_wt32(p + 2, 0u);
+	K::clear(T, slot);
 	__builtin_amdgcn_s_waitcnt(0);
-	__hip_atomic_exchange(&T.keys[slot].w, CT_TAG_TOMB << 16, __ATOMIC_RELAXED,
-			      __HIP_MEMORY_SCOPE_AGENT);
+	__hip_atomic_exchange(K::tagp(T, slot), CT_TAG_TOMB << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	atomicAdd(A.live, 1);
 	atomicAdd(A.tombs, 1);
 }
 
 struct ct_args {
-	const uint32_t *saddr, *daddr;
+	const uint32_t *saddr, *daddr; /* IPv6: 16 bytes per packet */
 	const uint16_t *sport, *dport;
 	const uint8_t *proto;
 	const uint16_t *l4;
@@ -3003,12 +3109,64 @@ struct ct_args {
 	uint64_t n;
 	uint32_t now;
 	/* scratch */
-	uint4 *rec;                  /* [2n] per packet, batch order */
+	uint4 *rec;                  /* [2n] (IPv4) / [4n] (IPv6) per packet, batch order */
 	uint32_t *gkey, *gkey_sorted; /* [n] */
 	uint32_t *idx, *idx_sorted;   /* [n] */
 	uint8_t *head;               /* [n] */
 	uint32_t *heads, *n_heads;   /* [n], [1] */
 	const uint32_t *gpos, *glen; /* [n_heads] group start / length, longest first */
+};
+
+/* One packet's record, written by k_ct_prep{,6} and read by the walker and
+ * k_ct_finish (batch order):
+ *   IPv4 (2 x 16 B): {daddr, saddr, z, nexthdr | tflags << 8 | meta << 16},
+ *                    {w | port << 16, len, sec, cst}
+ *   IPv6 (4 x 16 B): {daddr}, {saddr}, {z, nexthdr | tflags << 8 | meta << 16,
+ *                    w | port << 16, len}, {sec, cst, rev_nat, 0}
+ * z = the reply-direction tuple's dport | sport << 16 (ct_lookup's first
+ * lookup), w = the L4 word (TCP header bytes 12-13 / ICMP type), port = the
+ * forward decision's proxy port, sec = src_sec_id of a created entry, cst =
+ * counter slot + 1 | stage << 24 of the forward decision, rev_nat = the
+ * reverse NAT index an IPv6 ingress entry is created with. */
+struct ct_pkt {
+	uint32_t meta, w, len, sec, revnat, port, cst, dport, proto;
+	uint32_t sa4, da4;
+	uint4 sa6, da6;
+};
+
+template <class K> struct ct_rec;
+template <> struct ct_rec<CtK4> {
+	static constexpr uint32_t RW = 2;
+	uint4 r0, r1;
+	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
+	{
+		return nt ? ct_rec{ld_x4<true>(rec + 2u * i), ld_x4<true>(rec + 2u * i + 1u)}
+			  : ct_rec{rec[2u * i], rec[2u * i + 1u]};
+	}
+	__device__ CtK4::key key() const { return uint4{r0.x, r0.y, r0.z, r0.w & 0xFFFFu}; }
+	__device__ uint32_t meta() const { return r0.w >> 16; }
+	__device__ ct_pkt pkt() const
+	{
+		return ct_pkt{r0.w >> 16, r1.x & 0xFFFFu, r1.y, r1.z, 0u, r1.x >> 16, r1.w, r0.z & 0xFFFFu,
+			      r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{}};
+	}
+};
+template <> struct ct_rec<CtK6> {
+	static constexpr uint32_t RW = 4;
+	uint4 r0, r1, r2, r3;
+	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
+	{
+		const uint4 *p = rec + 4u * i;
+		return nt ? ct_rec{ld_x4<true>(p), ld_x4<true>(p + 1), ld_x4<true>(p + 2), ld_x4<true>(p + 3)}
+			  : ct_rec{p[0], p[1], p[2], p[3]};
+	}
+	__device__ CtK6::key key() const { return CtK6::key{r0, r1, r2.x, r2.y & 0xFFFFu}; }
+	__device__ uint32_t meta() const { return r2.y >> 16; }
+	__device__ ct_pkt pkt() const
+	{
+		return ct_pkt{r2.y >> 16, r2.z & 0xFFFFu, r2.w, r3.x, r3.z, r2.z >> 16, r3.y, r2.x & 0xFFFFu,
+			      r2.y & 0xFFu, 0u, 0u, r1, r0};
+	}
 };
 
 /* ct_lookup4's tuple setup, conntrack.h:461-528 */
@@ -3091,6 +3249,66 @@ __global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *he
 		head[p] = (p == 0 || ((g[p] ^ g[p - 1]) & mask)) ? 1u : 0u;
 }
 
+/* ct_lookup6's tuple setup (conntrack.h:308-378) and the forward tuple's
+ * decision, as k_ct_prep; IPv6 has no fragment flag (bpf_lxc.c:787-789) and
+ * an ingress entry carries the reverse NAT index ipv6_policy derives from
+ * the destination address, daddr.s6_addr32[3] & 0xFFFF (bpf_lxc.c:748). */
+__global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr);
+	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr);
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t fl = a.flags[i], pr = a.proto[i], w = a.l4[i], len = a.len[i], ep = a.ep[i];
+		const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
+		const bool egress = fl & 1u;
+		uint32_t tfl = egress ? TUPLE_F_IN : 0u, z = 0, meta = egress ? CTM_EGRESS : 0u;
+		if (pr == 58u) {
+			const uint32_t type = w & 0xFFu;
+			if (type >= 1u && type <= 4u) /* DEST_UNREACH, PKT_TOOBIG, TIME_EXCEED, PARAMPROB */
+				tfl |= TUPLE_F_RELATED;
+			else if (type == 129u) /* ECHO_REPLY: tuple->dport = ICMPV6_ECHO_REQUEST */
+				z = 128u;
+			else {
+				if (type == 128u) /* ECHO_REQUEST: tuple->sport = type */
+					z = 128u << 16;
+				meta |= CTM_ACT_CREATE;
+			}
+		} else if (pr == 6u || pr == 17u) {
+			z = (uint32_t)a.sport[i] | ((uint32_t)a.dport[i] << 16);
+			if (pr == 6u)
+				meta |= CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE);
+			else
+				meta |= CTM_ACT_CREATE;
+		} else {
+			meta |= CTM_GATED;
+		}
+		uint32_t sec = 0, port = 0, cst = 0, id = 0;
+		if (!(meta & CTM_GATED)) {
+			const decision d = decide<1>(s, egress, false, 0u, 0u, sa, da, z >> 16, pr, ep);
+			if (d.v >= 0) {
+				meta |= CTM_ALLOWED;
+				port = (uint32_t)d.v;
+			}
+			id = d.id;
+			if (egress)
+				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
+			else
+				sec = d.id;
+			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+		}
+		a.identity[i] = id;
+		uint4 *r = a.rec + 4u * i;
+		r[0] = da;
+		r[1] = sa;
+		r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (port << 16), len};
+		r[3] = uint4{sec, cst, egress ? 0u : (da.w & 0xFFFFu), 0u};
+		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u)
+					       : ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
+		a.idx[i] = (uint32_t)i;
+	}
+}
+
 /* A lane's cache of the map entries its group touched.  The lane owns every
  * key of its group (no other lane inserts, updates or deletes one), so a
  * cached entry - present with its row, or absent with the slot an insert
@@ -3110,22 +3328,23 @@ __global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *he
  * an array, not members of one aggregate) and every access below names
  * them one by one: with an array, instcombine folds the unrolled
  * selects back into a dynamically indexed load and the cache lands in
- * scratch memory. */
-struct ctc_ent {
-	uint4 key; /* .w = nexthdr | flags << 8 | CTC_* */
+ * scratch memory.  The key's meta word carries nexthdr | flags << 8 |
+ * CTC_*. */
+template <class K> struct ctc_ent {
+	typename K::key key;
 	uint32_t pos;
 	ct_row row;
 };
 
-struct ct_cache {
-	ctc_ent &e0, &e1, &e2;
+template <class K> struct ct_cache {
+	ctc_ent<K> &e0, &e1, &e2;
 #if CTC == 4
-	ctc_ent &e3;
+	ctc_ent<K> &e3;
 #endif
 	uint32_t next;
 };
 
-template <typename F> __device__ __forceinline__ void ctc_each(ct_cache &c, F &&f)
+template <class K, typename F> __device__ __forceinline__ void ctc_each(ct_cache<K> &c, F &&f)
 {
 	f(c.e0, 0);
 	f(c.e1, 1);
@@ -3144,35 +3363,30 @@ __device__ __forceinline__ bool ctc_dirty(uint32_t w)
 	return (w & (CTC_VALID | CTC_NEG | CTC_DIRTY)) == (CTC_VALID | CTC_DIRTY);
 }
 
-__device__ __forceinline__ void ctc_flush(const ct_table &T, ct_cache &c)
+template <class K> __device__ __forceinline__ void ctc_flush(const ct_table &T, ct_cache<K> &c)
 {
-	ctc_each(c, [&](ctc_ent &e, int) {
-		const uint32_t w = e.key.w, p = e.pos;
+	ctc_each(c, [&](ctc_ent<K> &e, int) {
+		const uint32_t w = K::meta(e.key), p = e.pos;
 		const ct_row r = e.row;
 		if (ctc_dirty(w))
 			ct_row_store(T, p, r);
-		e.key.w = 0;
+		K::meta(e.key) = 0;
 	});
 	c.next = 0;
 }
 
-__device__ __forceinline__ uint32_t ctc_state(ct_cache &c, int i)
+template <class K> __device__ __forceinline__ uint32_t ctc_state(ct_cache<K> &c, int i)
 {
 	uint32_t w = 0;
-	ctc_each(c, [&](ctc_ent &e, int j) { w = i == j ? e.key.w : w; });
+	ctc_each(c, [&](ctc_ent<K> &e, int j) { w = i == j ? K::meta(e.key) : w; });
 	return w;
 }
 
-__device__ __forceinline__ uint32_t ctc_pos(ct_cache &c, int i)
+template <class K> __device__ __forceinline__ uint32_t ctc_pos(ct_cache<K> &c, int i)
 {
 	uint32_t p = 0;
-	ctc_each(c, [&](ctc_ent &e, int j) { p = i == j ? e.pos : p; });
+	ctc_each(c, [&](ctc_ent<K> &e, int j) { p = i == j ? e.pos : p; });
 	return p;
-}
-
-__device__ __forceinline__ uint4 sel4(bool t, uint4 a, uint4 b)
-{
-	return uint4{t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z, t ? a.w : b.w};
 }
 
 __device__ __forceinline__ ct_row selrow(bool t, const ct_row &a, const ct_row &b)
@@ -3181,40 +3395,41 @@ __device__ __forceinline__ ct_row selrow(bool t, const ct_row &a, const ct_row &
 		      uint2{t ? a.d.x : b.d.x, t ? a.d.y : b.d.y}};
 }
 
-__device__ __forceinline__ ct_row ctc_row(ct_cache &c, int i)
+template <class K> __device__ __forceinline__ ct_row ctc_row(ct_cache<K> &c, int i)
 {
 	ct_row r{};
-	ctc_each(c, [&](ctc_ent &e, int j) { r = selrow(i == j, e.row, r); });
+	ctc_each(c, [&](ctc_ent<K> &e, int j) { r = selrow(i == j, e.row, r); });
 	return r;
 }
 
 /* entry i := present at pos with row r (dirty) */
-__device__ __forceinline__ void ctc_put(ct_cache &c, int i, uint32_t pos, const ct_row &r)
+template <class K> __device__ __forceinline__ void ctc_put(ct_cache<K> &c, int i, uint32_t pos, const ct_row &r)
 {
-	ctc_each(c, [&](ctc_ent &e, int j) {
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
 		const bool t = i == j;
-		e.key.w = t ? (e.key.w & 0xFFFFu) | CTC_VALID | CTC_DIRTY : e.key.w;
+		K::meta(e.key) = t ? (K::meta(e.key) & 0xFFFFu) | CTC_VALID | CTC_DIRTY : K::meta(e.key);
 		e.pos = t ? pos : e.pos;
 		e.row = selrow(t, r, e.row);
 	});
 }
 
 /* entry i := absent, inserts may start at pos */
-__device__ __forceinline__ void ctc_drop(ct_cache &c, int i, uint32_t pos)
+template <class K> __device__ __forceinline__ void ctc_drop(ct_cache<K> &c, int i, uint32_t pos)
 {
-	ctc_each(c, [&](ctc_ent &e, int j) {
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
 		const bool t = i == j;
-		e.key.w = t ? (e.key.w & 0xFFFFu) | CTC_VALID | CTC_NEG : e.key.w;
+		K::meta(e.key) = t ? (K::meta(e.key) & 0xFFFFu) | CTC_VALID | CTC_NEG : K::meta(e.key);
 		e.pos = t ? pos : e.pos;
 	});
 }
 
 /* the cache entry of k, probing the map on a miss */
-__device__ __forceinline__ int ctc_get(const ct_table &T, ct_cache &c, uint4 k)
+template <class K>
+__device__ __forceinline__ int ctc_get(const ct_table &T, ct_cache<K> &c, const typename K::key &k)
 {
 	int hit = -1;
-	ctc_each(c, [&](ctc_ent &e, int j) {
-		hit = ((e.key.w & CTC_VALID) && ct_same(e.key, k)) ? j : hit;
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
+		hit = ((K::meta(e.key) & CTC_VALID) && K::same(e.key, k)) ? j : hit;
 	});
 	if (hit >= 0)
 		return hit;
@@ -3223,37 +3438,39 @@ __device__ __forceinline__ int ctc_get(const ct_table &T, ct_cache &c, uint4 k)
 	/* write back the victim */
 	uint32_t vw = 0, vp = 0;
 	ct_row vr{};
-	ctc_each(c, [&](ctc_ent &e, int j) {
-		vw = j == v ? e.key.w : vw;
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
+		vw = j == v ? K::meta(e.key) : vw;
 		vp = j == v ? e.pos : vp;
 		vr = selrow(j == v, e.row, vr);
 	});
 	if (ctc_dirty(vw))
 		ct_row_store(T, vp, vr);
 	uint32_t from;
-	const int slot = ct_find(T, k, &from);
+	const int slot = ct_find<K>(T, k, &from);
 	ct_row r{};
 	if (slot >= 0)
 		r = ct_row_load(T, (uint32_t)slot);
-	const uint4 nk{k.x, k.y, k.z, (k.w & 0xFFFFu) | CTC_VALID | (slot < 0 ? CTC_NEG : 0u)};
+	typename K::key nk = k;
+	K::meta(nk) = (K::cmeta(k) & 0xFFFFu) | CTC_VALID | (slot < 0 ? CTC_NEG : 0u);
 	const uint32_t np = slot >= 0 ? (uint32_t)slot : from;
-	ctc_each(c, [&](ctc_ent &e, int j) {
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
 		const bool t = j == v;
-		e.key = sel4(t, nk, e.key);
+		e.key = K::sel(t, nk, e.key);
 		e.pos = t ? np : e.pos;
 		e.row = selrow(t, r, e.row);
 	});
 	return v;
 }
 
-/* BPF_ANY update of k (ct_create4's map_update_elem) through the cache */
-__device__ __forceinline__ bool ctc_update(const ct_table &T, const ct_acct &A, ct_cache &c, uint4 k,
-					   const ct_row &e)
+/* BPF_ANY update of k (ct_create's map_update_elem) through the cache */
+template <class K>
+__device__ __forceinline__ bool ctc_update(const ct_table &T, const ct_acct &A, ct_cache<K> &c,
+					   const typename K::key &k, const ct_row &e)
 {
-	const int i = ctc_get(T, c, k);
+	const int i = ctc_get<K>(T, c, k);
 	uint32_t pos = ctc_pos(c, i);
 	if (ctc_state(c, i) & CTC_NEG) {
-		const int slot = pos == 0xFFFFFFFFu ? -1 : ct_insert(T, A, k, pos);
+		const int slot = pos == 0xFFFFFFFFu ? -1 : ct_insert<K>(T, A, k, pos);
 		if (slot < 0)
 			return false;
 		pos = (uint32_t)slot;
@@ -3262,23 +3479,23 @@ __device__ __forceinline__ bool ctc_update(const ct_table &T, const ct_acct &A, 
 	return true;
 }
 
-/* One packet of a group, conntrack.h:441-561 and ct_create4 :653-744, with
- * the policy outcome of bpf_lxc.c:506-537 / :918-937. */
-__device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A, ct_cache &c, uint4 r0,
-					   uint4 r1, uint32_t now)
+/* One packet of a group: ct_lookup4 / ct_lookup6 (conntrack.h:441-561 /
+ * :288-412) and ct_create4 / ct_create6 (:653-744 / :588-639), with the
+ * policy outcome of the endpoint programs (bpf_lxc.c:506-537 / :918-937,
+ * :192-203 / :776-800).  k = the reply-direction tuple of the first lookup. */
+template <class K>
+__device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A, ct_cache<K> &c,
+					   typename K::key k, uint32_t meta, uint32_t w, uint32_t len,
+					   uint32_t sec, uint32_t revnat, uint32_t now)
 {
-	const uint32_t meta = r0.w >> 16;
 	const bool ingress = !(meta & CTM_EGRESS);
-	const uint32_t w = r1.x & 0xFFFFu, len = r1.y;
-	uint4 k{r0.x, r0.y, r0.z, r0.w & 0xFFFFu};
-	int ci = ctc_get(T, c, k);
+	int ci = ctc_get<K>(T, c, k);
 	uint32_t ret;
 	if (!(ctc_state(c, ci) & CTC_NEG)) {
-		ret = ((k.w >> 8) & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+		ret = ((K::cmeta(k) >> 8) & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
 	} else {
-		/* ipv4_ct_tuple_reverse */
-		k = uint4{r0.y, r0.x, (r0.z >> 16) | (r0.z << 16), k.w ^ (TUPLE_F_IN << 8)};
-		ci = ctc_get(T, c, k);
+		k = K::reversed(k);
+		ci = ctc_get<K>(T, c, k);
 		ret = (ctc_state(c, ci) & CTC_NEG) ? CT_NEW : CT_ESTABLISHED;
 	}
 	if (ret != CT_NEW) {
@@ -3287,16 +3504,16 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 		ctc_put(c, ci, ctc_pos(c, ci), e);
 	}
 	if (ret < CT_REPLY && !(meta & CTM_ALLOWED)) {
-		if (ret == CT_ESTABLISHED) { /* ct_delete4 */
+		if (ret == CT_ESTABLISHED) { /* ct_delete4 / ct_delete6 */
 			const uint32_t slot = ctc_pos(c, ci);
-			ct_erase(T, A, slot);
+			ct_erase<K>(T, A, slot);
 			ctc_drop(c, ci, slot);
 		}
 		return ret;
 	}
 	if (ret != CT_NEW)
 		return ret;
-	/* ct_create4: the forward entry, then the ICMP entry relating errors */
+	/* ct_create: the forward entry, then the ICMP entry relating errors */
 	const bool tcp = meta & CTM_TCP;
 	ct_row e{};
 	ct_timeout(e, now, tcp, ingress, tcp ? 1u : 0u); /* seen_flags.syn = is_tcp: bit 0 */
@@ -3304,17 +3521,17 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 		e.a = uint4{1u, 0u, len, 0u};
 	else
 		e.b = uint4{1u, 0u, len, 0u};
-	e.c.w = r1.z; /* src_sec_id */
-	if (!ctc_update(T, A, c, k, e))
+	e.c.y |= revnat << 16; /* rev_nat_index */
+	e.c.w = sec;           /* src_sec_id */
+	if (!ctc_update<K>(T, A, c, k, e))
 		return CT_NEW | CT_FAIL;
 	e.c.y |= CTB_SEEN_NON_SYN;
-	const uint4 ik{k.x, k.y, 0u, 1u | ((((k.w >> 8) & 0xFFu) | TUPLE_F_RELATED) << 8)};
-	if (!ctc_update(T, A, c, ik, e))
+	if (!ctc_update<K>(T, A, c, K::related(k), e))
 		return CT_NEW | CT_FAIL;
 	return CT_NEW;
 }
 
-__global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
+template <class K> __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
 {
 	__shared__ int s_acct[3];
 	if (threadIdx.x < 3)
@@ -3324,11 +3541,11 @@ __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
 	const uint32_t nh = *a.n_heads;
 	const uint32_t stride = gridDim.x * 256u;
 #if CTC == 4
-	ctc_ent e0{}, e1{}, e2{}, e3{};
-	ct_cache c{e0, e1, e2, e3, 0u};
+	ctc_ent<K> e0{}, e1{}, e2{}, e3{};
+	ct_cache<K> c{e0, e1, e2, e3, 0u};
 #else
-	ctc_ent e0{}, e1{}, e2{};
-	ct_cache c{e0, e1, e2, 0u};
+	ctc_ent<K> e0{}, e1{}, e2{};
+	ct_cache<K> c{e0, e1, e2, 0u};
 #endif
 	/* groups longest first (a.glen / a.gpos, sorted by length): the
 	 * elephants start in the first round and the rest fill in behind */
@@ -3340,20 +3557,21 @@ __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
 		 * flight while packet p runs */
 		uint32_t ni = a.idx_sorted[p0];
 		uint32_t nni = p0 + 1u < p1 ? a.idx_sorted[p0 + 1u] : 0u;
-		uint4 n0 = a.rec[2u * ni], n1 = a.rec[2u * ni + 1u];
+		ct_rec<K> nr = ct_rec<K>::load(a.rec, ni, false);
 		for (uint64_t p = p0; p < p1; p++) {
 			const uint32_t i = ni;
-			const uint4 r0 = n0, r1 = n1;
+			const ct_rec<K> r = nr;
 			if (p + 1u < p1) {
 				ni = nni;
-				n0 = a.rec[2u * ni];
-				n1 = a.rec[2u * ni + 1u];
+				nr = ct_rec<K>::load(a.rec, ni, false);
 				if (p + 2u < p1)
 					nni = a.idx_sorted[p + 2u];
 			}
-			if ((r0.w >> 16) & CTM_GATED)
+			const uint32_t meta = r.meta();
+			if (meta & CTM_GATED)
 				continue;
-			a.ct_ret[i] = (uint8_t)ct_step(T, A, c, r0, r1, a.now);
+			const ct_pkt q = r.pkt();
+			a.ct_ret[i] = (uint8_t)ct_step<K>(T, A, c, r.key(), meta, q.w, q.len, q.sec, q.revnat, a.now);
 		}
 		ctc_flush(T, c);
 	}
@@ -3367,11 +3585,11 @@ __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
 	}
 }
 
-/* policy on the tuple ct_lookup4 left, counters, the reply / related skip.
- * CT_NEW / CT_ESTABLISHED packets reuse k_ct_prep's forward decision; only
+/* policy on the tuple ct_lookup left, counters, the reply / related skip.
+ * CT_NEW / CT_ESTABLISHED packets reuse the prep's forward decision; only
  * CT_REPLY / CT_RELATED ones run the cascade again, on the reply tuple.
  * Hot counter slots accumulate in LDS (packed, as k_classify CTR = 1). */
-template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a)
+template <int NT, class K> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* metrics {reason 0 / 133 / 137 / 155} x {ingress, egress} */
@@ -3382,35 +3600,34 @@ template <int NT> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapsho
 	const uint64_t stride = (uint64_t)gridDim.x * NT;
 	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) {
 		/* batch order: records and the walker's results stream in */
-		const uint4 r0 = ld_x4<true>(a.rec + 2u * i);
-		const uint4 r1 = ld_x4<true>(a.rec + 2u * i + 1u);
-		const uint32_t meta = r0.w >> 16;
+		const ct_pkt q = ct_rec<K>::load(a.rec, (uint32_t)i, true).pkt();
+		const uint32_t meta = q.meta;
 		const bool egress = meta & CTM_EGRESS;
-		const uint32_t len = r1.y;
+		const uint32_t len = q.len;
 		int32_t v;
 		uint32_t st = 4, cr = 255u;
 		if (meta & CTM_GATED) {
-			v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup4 default case */
+			v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup default case */
 		} else {
 			const uint32_t c = a.ct_ret[i];
 			cr = c & 3u;
 			int ctr;
 			if (cr >= CT_REPLY) {
 				const bool frag = meta & CTM_FRAG;
-				const decision d = decide<0>(s, egress, frag, r0.y, r0.x, uint4{}, uint4{},
-								    r0.z & 0xFFFFu, r0.w & 0xFFu, a.ep[i]);
+				const decision d = decide<K::V6>(s, egress, frag, q.sa4, q.da4, q.sa6, q.da6, q.dport,
+								 q.proto, a.ep[i]);
 				ctr = d.ctr;
 				st = d.st;
 				v = (egress && d.v > 0) ? d.v : 0;
 			} else {
-				ctr = (int)(r1.w & 0xFFFFFFu) - 1;
-				st = r1.w >> 24;
+				ctr = (int)(q.cst & 0xFFFFFFu) - 1;
+				st = q.cst >> 24;
 				if (!(meta & CTM_ALLOWED))
 					v = DROP_POLICY;
 				else if (c & CT_FAIL)
 					v = DROP_CT_CREATE_FAILED;
 				else
-					v = (int32_t)(r1.x >> 16);
+					v = (int32_t)q.port;
 			}
 			if (ctr >= 0) {
 				const uint32_t cs = (uint32_t)ctr;
@@ -3477,15 +3694,19 @@ size_t ct_temp_bytes(uint64_t n)
 	return std::max(a, b);
 }
 
-hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
-				 hipStream_t st)
+template <class K>
+static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
 {
-	ct_args a{L.saddr, L.daddr, L.sport, L.dport, L.proto, L.l4, L.flags, L.len, L.ep,
+	ct_args a{static_cast<const uint32_t *>(L.saddr), static_cast<const uint32_t *>(L.daddr), L.sport,
+		  L.dport, L.proto, L.l4, L.flags, L.len, L.ep,
 		  L.verdict, L.ct_ret, L.identity, L.stage, L.delta, L.n, L.now,
 		  L.rec, L.gkey, L.gkey_sorted, L.idx, L.idx_sorted, L.head, L.heads,
 		  L.n_heads};
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
-	hipLaunchKernelGGL(k_ct_prep, dim3(g), dim3(256), 0, st, s, a);
+	if (K::V6)
+		hipLaunchKernelGGL(k_ct_prep6, dim3(g), dim3(256), 0, st, s, a);
+	else
+		hipLaunchKernelGGL(k_ct_prep, dim3(g), dim3(256), 0, st, s, a);
 	size_t tb = L.temp_bytes;
 	/* 24 key bits: three passes; pairs sharing a 24-bit hash merge into
 	 * one group, which only lengthens that lane's walk */
@@ -3517,14 +3738,26 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 	a.glen = L.gkey_sorted;
 	a.gpos = L.idx;
 	/* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
-	hipLaunchKernelGGL(k_ct_walk, dim3(2048), dim3(256), 0, st, T, a);
+	hipLaunchKernelGGL(k_ct_walk<K>, dim3(2048), dim3(256), 0, st, T, a);
 	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
 	constexpr int NF = 1024;
 	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((L.n + NF - 1) / NF, 512),
 					       (L.n >> 22) + 1);
-	hipLaunchKernelGGL((k_ct_finish<NF>), dim3((unsigned)gf), dim3(NF), (size_t)s.hot_slots * 8u, st,
+	hipLaunchKernelGGL((k_ct_finish<NF, K>), dim3((unsigned)gf), dim3(NF), (size_t)s.hot_slots * 8u, st,
 			   s, a);
 	return hipGetLastError();
+}
+
+hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				 hipStream_t st)
+{
+	return launch_ct<CtK4>(s, T, L, st);
+}
+
+hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				 hipStream_t st)
+{
+	return launch_ct<CtK6>(s, T, L, st);
 }
 
 /* ======================================================================= */

@@ -102,7 +102,7 @@ hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, 
 /* stateful classification (cgpu_classify_v4_ct): packet columns, outputs,
  * and the caller-allocated scratch (ct_scratch_layout in host.cpp) */
 struct ct_launch {
-	const uint32_t *saddr, *daddr;
+	const void *saddr, *daddr; /* IPv4: u32 per packet; IPv6: 16 bytes (16-byte aligned) */
 	const uint16_t *sport, *dport;
 	const uint8_t *proto;
 	const uint16_t *l4;
@@ -116,7 +116,7 @@ struct ct_launch {
 	uint64_t *delta;
 	uint64_t n;
 	uint32_t now;
-	uint4 *rec;
+	uint4 *rec; /* [2n] IPv4, [4n] IPv6 */
 	uint32_t *gkey, *gkey_sorted, *idx, *idx_sorted;
 	uint8_t *head;
 	uint32_t *heads, *n_heads;
@@ -127,6 +127,9 @@ struct ct_launch {
 
 size_t ct_temp_bytes(uint64_t n);
 hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				 hipStream_t st);
+/* the same over cilium_ct6_global (tables.h CtK6 slots), rec [4n] */
+hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
 				 hipStream_t st);
 
 /* L3 MapState compilation (cgpu_l3_compile): device copies of the program */

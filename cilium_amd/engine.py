@@ -26,7 +26,7 @@ import numpy as np
 
 from . import layouts as L
 from ._abi import (CgpuConfig, CgpuError, FrameTuples, Frames, Lb4Out, Lb4Tuples, TuplesV4,
-                   TuplesV4Ct, TuplesV6, check, lib)
+                   TuplesV4Ct, TuplesV6Ct, TuplesV6, check, lib)
 
 CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX = 0, 1, 2, 3
 BPF_ANY, BPF_NOEXIST, BPF_EXIST = 0, 1, 2
@@ -299,6 +299,40 @@ class Engine:
             vals.append(v)
         return L.ct_sorted(np.array(keys, L.CT4_TUPLE), np.array(vals, L.CT_ENTRY))
 
+    # --- cilium_ct6_global (IPv6 conntrack) ---
+    def ct6_update(self, key, val, flags=BPF_ANY) -> int:
+        return self.L.cgpu_ct6_update(self.h, _buf(key), _buf(val), flags)
+
+    def ct6_delete(self, key) -> int:
+        return self.L.cgpu_ct6_delete(self.h, _buf(key))
+
+    def ct6_lookup(self, key):
+        out = C.create_string_buffer(56)
+        rc = self.L.cgpu_ct6_lookup(self.h, _buf(key), out)
+        return rc, (np.frombuffer(out.raw, L.CT_ENTRY)[0] if rc == 0 else None)
+
+    def ct6_count(self) -> int:
+        return self.L.cgpu_ct6_count(self.h)
+
+    def ct6_gc(self, time: int) -> int:
+        d = C.c_uint64()
+        check(self.L.cgpu_ct6_gc(self.h, time, C.byref(d)), "cgpu_ct6_gc")
+        return d.value
+
+    def ct6_flush(self) -> None:
+        check(self.L.cgpu_ct6_flush(self.h), "cgpu_ct6_flush")
+
+    def ct6_dump(self):
+        keys, vals, prev = [], [], None
+        out = C.create_string_buffer(38)
+        while self.L.cgpu_ct6_get_next_key(self.h, prev, out) == 0:
+            prev = out.raw
+            rc, v = self.ct6_lookup(np.frombuffer(prev, L.CT6_TUPLE)[0])
+            assert rc == 0
+            keys.append(np.frombuffer(prev, L.CT6_TUPLE)[0])
+            vals.append(v)
+        return L.ct_sorted(np.array(keys, L.CT6_TUPLE), np.array(vals, L.CT_ENTRY))
+
     # --- L3 MapState compilation ---
     def l3_compile(self, prog, ep_sets, id_sets, flags: int = 3) -> np.ndarray:
         """cgpu_l3_compile: prog = cilium_amd.policy.L3Program, *_sets =
@@ -386,6 +420,26 @@ class Engine:
                                          _ptr(out["ct_ret"]), _ptr(out["identity"]),
                                          _ptr(out.get("stage")), _stream(stream)),
               "cgpu_classify_v4_ct")
+        return out
+
+    def classify_v6_ct(self, t: dict, now: int, out: dict | None = None, stage: bool = True,
+                       stream=None):
+        """cgpu_classify_v6_ct: as classify_v4_ct with saddr / daddr (n, 16)
+        uint8 tensors (16-byte aligned rows)."""
+        import torch
+        n = t["saddr"].shape[0]
+        dev = t["saddr"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "ct_ret": torch.empty(n, dtype=torch.uint8, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
+        tv = TuplesV6Ct(*[t[k].data_ptr() for k in
+                          ("saddr", "daddr", "sport", "dport", "proto", "l4b", "flags", "len", "ep")])
+        check(self.L.cgpu_classify_v6_ct(self.h, C.byref(tv), n, now, _ptr(out["verdict"]),
+                                         _ptr(out["ct_ret"]), _ptr(out["identity"]),
+                                         _ptr(out.get("stage")), _stream(stream)),
+              "cgpu_classify_v6_ct")
         return out
 
     def classify_v4_lb(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):

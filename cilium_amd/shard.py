@@ -110,6 +110,11 @@ def pairhash_np(saddr, daddr) -> np.ndarray:
     return h.astype(np.uint32)
 
 
+def pairhash6_np(saddr16, daddr16) -> np.ndarray:
+    """pairhash_np over the folded IPv6 addresses (tables.h fold6)."""
+    return pairhash_np(fold6_np(saddr16), fold6_np(daddr16))
+
+
 def ct_shard_of(t: dict, world: int) -> np.ndarray:
     """Owning rank of every packet of the stateful path: pairhash % world.
 
@@ -121,6 +126,8 @@ def ct_shard_of(t: dict, world: int) -> np.ndarray:
     one map, on lane order: cgpu.h), so parity is defined below capacity
     only.  A deployment that wants the aggregate of one map passes
     ct_max // world per rank."""
+    if np.asarray(t["saddr"]).ndim == 2:
+        return (pairhash6_np(t["saddr"], t["daddr"]) % np.uint32(world)).astype(np.int64)
     return (pairhash_np(t["saddr"], t["daddr"]) % np.uint32(world)).astype(np.int64)
 
 

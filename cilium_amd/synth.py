@@ -881,6 +881,39 @@ def make_ct_workload(tables: Tables, n_conn: int, seed=SEED, gpu_id: int = 0, n_
     return t, locals_be, seclabels
 
 
+def ct6_endpoints(tables, n_endpoints: int):
+    """Local IPv6 endpoint addresses (inside ROUTER_IP's /64, the cluster
+    range) and their SECLABELs for the IPv6 stateful workloads."""
+    loc = np.tile(np.frombuffer(tables.router, np.uint8), (n_endpoints, 1))
+    loc[:, 8:12] = [0xC0, 0xA8, 0, 0]
+    loc[:, 12:14] = 0
+    loc[:, 14] = (np.arange(n_endpoints) >> 8) & 0xFF
+    loc[:, 15] = (np.arange(n_endpoints) + 1) & 0xFF
+    seclabels = (np.arange(n_endpoints, dtype=np.uint32) * 7 + 6000).astype(np.uint32)
+    return loc.astype(np.uint8), seclabels
+
+
+def make_ct6_workload(tables, n_conn: int, seed=SEED, gpu_id: int = 0, n_remote=None,
+                      mean_pkts: float = 8.0, span: float = 0.02, world: int = 1):
+    """make_ct_workload over Tables6 (the IPv6 stateful path): remotes 80%
+    inside installed IPv6 ipcache prefixes; with world > 1 every pair belongs
+    to rank gpu_id's shard (shard.pairhash6_np % world)."""
+    rng = np.random.Generator(np.random.PCG64(seed + 0xC6000 + gpu_id))
+    loc, seclabels = ct6_endpoints(tables, tables.n_endpoints)
+    nr = n_remote or max(16, n_conn // 4)
+    pi = rng.integers(0, len(tables.pfx_addr), nr)
+    host = rng.integers(0, 256, (nr, 16), dtype=np.uint8)
+    m = MASK6[tables.pfx_len[pi]]
+    inside = tables.pfx_addr[pi] | (host & ~m)
+    rem = np.where((rng.random(nr) < 0.8)[:, None], inside, host).astype(np.uint8)
+    ok = None
+    if world > 1:
+        from .shard import pairhash6_np
+        ok = lambda a, b: (pairhash6_np(a, b) % np.uint32(world)) == gpu_id  # noqa: E731
+    t = make_ct_stream(rng, n_conn, loc, rem, mean_pkts=mean_pkts, span=span, pair_ok=ok)
+    return t, loc, seclabels
+
+
 def load_lxc(target, seclabels):
     """cgpu_lxc_update / or_lxc_update: the SECLABEL of every endpoint."""
     for ep, sl in enumerate(seclabels):

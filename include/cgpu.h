@@ -696,6 +696,62 @@ int cgpu_classify_v4_ct(cgpu_ctx *ctx, const cgpu_tuples_v4_ct *t, size_t n, uin
 			void *stream);
 
 /* ------------------------------------------------------------------ */
+/* conntrack, IPv6: the map cilium_ct6_global (CT_MAP6, bpf_lxc.c:53-63) */
+/* ------------------------------------------------------------------ */
+/* struct ipv6_ct_tuple (bpf/lib/common.h:338-346), packed, 38 B */
+#pragma pack(push, 1)
+typedef struct cgpu_ct6_tuple {
+	uint8_t daddr[16]; /* network order */
+	uint8_t saddr[16];
+	uint16_t dport;    /* network order */
+	uint16_t sport;
+	uint8_t nexthdr;
+	uint8_t flags;     /* TUPLE_F_OUT 0 / TUPLE_F_IN 1 | TUPLE_F_RELATED 2 */
+} cgpu_ct6_tuple;
+#pragma pack(pop)
+
+/* The cgpu_ct4_* map operations on cilium_ct6_global (capacity
+ * cgpu_config.ct6_max, default ct_max). */
+int cgpu_ct6_update(cgpu_ctx *ctx, const cgpu_ct6_tuple *key, const cgpu_ct_entry *val,
+		    uint64_t flags);
+int cgpu_ct6_delete(cgpu_ctx *ctx, const cgpu_ct6_tuple *key);
+int cgpu_ct6_lookup(cgpu_ctx *ctx, const cgpu_ct6_tuple *key, cgpu_ct_entry *val_out);
+int cgpu_ct6_get_next_key(cgpu_ctx *ctx, const cgpu_ct6_tuple *key, cgpu_ct6_tuple *next_out);
+size_t cgpu_ct6_count(cgpu_ctx *ctx);
+int cgpu_ct6_gc(cgpu_ctx *ctx, uint32_t time, uint64_t *deleted_out);
+int cgpu_ct6_flush(cgpu_ctx *ctx);
+
+/* A batch of IPv6 packets for the stateful path (device pointers). */
+typedef struct cgpu_tuples_v6_ct {
+	const uint8_t *saddr;  /* 16 bytes per packet, network order; 16-byte aligned */
+	const uint8_t *daddr;
+	const uint16_t *sport; /* L4 header ports as on the wire (TCP/UDP) */
+	const uint16_t *dport;
+	const uint8_t *proto;  /* nexthdr after the extension headers */
+	const uint16_t *l4;    /* TCP: header bytes 12-13 as loaded; ICMPv6: the type
+				  in the low byte; else ignored */
+	const uint8_t *flags;  /* CGPU_F_EGRESS (IPv6 has no fragment flag) */
+	const uint32_t *len;
+	const uint16_t *ep;
+} cgpu_tuples_v6_ct;
+
+/*
+ * cgpu_classify_v4_ct for IPv6 over cilium_ct6_global, in the order of
+ * ipv6_l3_from_lxc (egress, bpf_lxc.c:108-203) and ipv6_policy (ingress,
+ * :731-800): ct_lookup6 (conntrack.h:288-412; ICMPv6 errors 1-4 RELATED,
+ * echo request / reply ports 128), identity as cgpu_classify_v6, policy on
+ * the tuple ct_lookup6 left, ct_delete6 of a denied ESTABLISHED entry,
+ * ct_create6 (:588-639, with its ICMPv6 related entry) of an allowed CT_NEW
+ * packet.  An ingress entry is created with rev_nat_index =
+ * daddr.s6_addr32[3] & 0xFFFF (bpf_lxc.c:748); a hit entry's reverse NAT
+ * goes through the empty cilium_lb6_reverse_nat map (a no-op, lib/lb.h:
+ * 305-317).  Outputs, ordering and the capacity caveat as cgpu_classify_v4_ct.
+ */
+int cgpu_classify_v6_ct(cgpu_ctx *ctx, const cgpu_tuples_v6_ct *t, size_t n, uint32_t now,
+			int32_t *verdict, uint8_t *ct_ret, uint32_t *identity, uint8_t *stage,
+			void *stream);
+
+/* ------------------------------------------------------------------ */
 /* L3 MapState compilation                           */
 /* ------------------------------------------------------------------ */
 /* The label decision computeDesiredL3PolicyMapEntries asks of the policy

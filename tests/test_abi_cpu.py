@@ -385,3 +385,41 @@ def test_prefilter_revision_routing_and_undo():
     assert ex.value.errno == errno.EOPNOTSUPP
     PreFilter(e2).Insert(0, ["10.0.0.1/32"])
     e2.close()
+
+
+def _ct6_key(i, flags=0, proto=6):
+    k = np.zeros((), L.CT6_TUPLE)
+    k["daddr"][:] = np.frombuffer(bytes([0xf0, 0x0d] + [0] * 13 + [i]), np.uint8)
+    k["saddr"][:] = np.frombuffer(bytes([0xbe, 0xef] + [0] * 13 + [1]), np.uint8)
+    k["dport"], k["sport"], k["nexthdr"], k["flags"] = 0x5000, 0x3930, proto, flags
+    return k
+
+
+def test_ct6_map_semantics():
+    """cilium_ct6_global through the bpf(2)-style calls: capacity ct6_max,
+    BPF_ANY/NOEXIST/EXIST, the whole 38-byte tuple as the key, get_next_key,
+    GC by lifetime, Flush; independent of cilium_ct4_global."""
+    e = Engine(device=-1, ct_max=100, ct6_max=8)
+    v = np.zeros((), L.CT_ENTRY)
+    for i in range(8):
+        v["lifetime"] = 100 + i
+        v["tx_packets"] = i
+        assert e.ct6_update(_ct6_key(i), v) == 0
+    assert e.ct6_count() == 8 and e.ct4_count() == 0
+    assert e.ct6_update(_ct6_key(8), v) == -errno.E2BIG
+    assert e.ct6_update(_ct6_key(3), v, BPF_NOEXIST) == -errno.EEXIST
+    assert e.ct6_update(_ct6_key(9), v, BPF_EXIST) == -errno.ENOENT
+    rc, got = e.ct6_lookup(_ct6_key(2))
+    assert rc == 0 and got["tx_packets"] == 2 and got["lifetime"] == 102
+    assert e.ct6_lookup(_ct6_key(2, flags=1))[0] == -errno.ENOENT
+    assert e.ct6_lookup(_ct6_key(2, proto=58))[0] == -errno.ENOENT
+    assert e.ct6_delete(_ct6_key(2)) == 0 and e.ct6_delete(_ct6_key(2)) == -errno.ENOENT
+    assert e.ct6_update(_ct6_key(8), v) == 0
+    keys, vals = e.ct6_dump()
+    assert len(keys) == 8 and sorted(keys["daddr"][:, 15].tolist()) == [0, 1, 3, 4, 5, 6, 7, 8]
+    assert (keys["saddr"][:, 0] == 0xbe).all() and (keys["nexthdr"] == 6).all()
+    assert e.ct6_gc(104) == 3
+    assert e.ct6_count() == 5
+    e.ct6_flush()
+    assert e.ct6_count() == 0
+    e.close()
