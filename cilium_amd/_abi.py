@@ -127,6 +127,8 @@ PROTOS = {
     "cgpu_flow_hash": (u32, [u32, u32, C.c_uint16, C.c_uint16, C.c_uint8]),
     "cgpu_commit": (i32, [vp, C.POINTER(u64)]),
     "cgpu_table_checksum": (i32, [vp, C.POINTER(u64)]),
+    "cgpu_table_verify": (i32, [vp]),
+    "cgpu__test_corrupt": (i32, [vp, i32, sz, C.c_uint8]),
     "cgpu_counter_layout_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
     "cgpu_classify_v6": (i32, [vp, C.POINTER(TuplesV6), sz, vp, vp, vp, vp]),

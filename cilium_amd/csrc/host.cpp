@@ -1349,6 +1349,7 @@ struct DevBuf {
 	size_t bytes = 0;
 	int dev = -1;
 	hipStream_t st = nullptr;
+	uint64_t host_sum = 0; /* table_sum_word over the host image (verification) */
 	~DevBuf()
 	{
 		if (p) {
@@ -1451,6 +1452,7 @@ struct cgpu_ctx {
 	uint64_t *d_totals = nullptr; /* [2*slots + METRICS] */
 	uint64_t *d_delta_own = nullptr;
 	uint64_t *d_delta = nullptr;  /* own or bound */
+	uint64_t *d_verify = nullptr; /* [G_N + 1] device-side table sums of a commit / verify */
 	/* [n_ctr_slots] packed counter accumulator per stream (zero between
 	 * classify calls; one per stream keeps its exactness bound per call).
 	 * At most kMaxPkStreams buffers: a new stream past that takes the least
@@ -1662,10 +1664,12 @@ CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **o
 		    hipEventCreateWithFlags(&c->ct_done, hipEventDisableTiming) != hipSuccess ||
 		    hipMalloc((void **)&c->d_totals, words * 8) != hipSuccess ||
 		    hipMalloc((void **)&c->d_delta_own, words * 8) != hipSuccess ||
+		    hipMalloc((void **)&c->d_verify, (G_N + 1) * 8) != hipSuccess ||
 		    hipMemset(c->d_totals, 0, words * 8) != hipSuccess ||
 		    hipMemset(c->d_delta_own, 0, words * 8) != hipSuccess) {
 			(void)hipFree(c->d_totals);
 			(void)hipFree(c->d_delta_own);
+			(void)hipFree(c->d_verify);
 			if (c->ustream)
 				(void)hipStreamDestroy(c->ustream);
 			if (c->rstream)
@@ -1711,6 +1715,7 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 		comm_destroy(c);
 		(void)hipFree(c->d_totals);
 		(void)hipFree(c->d_delta_own);
+		(void)hipFree(c->d_verify);
 		{
 			std::lock_guard<std::mutex> g(c->pk_mu);
 			for (auto &kv : c->d_pk) {
@@ -2889,17 +2894,46 @@ static void uncapture(cgpu_ctx *c, const CommitIn &in)
 	c->slot_inits.insert(c->slot_inits.begin(), in.inits.begin(), in.inits.end());
 }
 
-static int upload(cgpu_ctx *c, const Arena &ar, DevBufP &out)
+/* table_sum_word over the arena's image (parts at their offsets, zero gaps) */
+static uint64_t arena_sum(const Arena &ar)
+{
+	uint64_t sum = 0;
+	for (size_t i = 0; i < ar.parts.size(); i++) {
+		const uint8_t *p = static_cast<const uint8_t *>(ar.parts[i].first);
+		const size_t bytes = ar.parts[i].second, w0 = ar.offs[i] / 8u;
+		const size_t full = bytes / 8u;
+		for (size_t j = 0; j < full; j++) {
+			uint64_t w;
+			memcpy(&w, p + 8u * j, 8);
+			sum += table_sum_word(w, w0 + j);
+		}
+		if (bytes % 8u) {
+			uint64_t w = 0;
+			memcpy(&w, p + 8u * full, bytes % 8u);
+			sum += table_sum_word(w, w0 + full);
+		}
+	}
+	return sum;
+}
+
+/* Upload an arena as one group buffer (stream-ordered on ustream), and queue
+ * the device-side sum of what landed into d_verify[slot]: cgpu_commit
+ * compares it with the host image's sum before publishing (SURVEY §5:
+ * a bad upload or a corrupted buffer is an -EIO, not silent wrong verdicts). */
+static int upload(cgpu_ctx *c, const Arena &ar, DevBufP &out, int slot)
 {
 	auto b = std::make_shared<DevBuf>();
 	b->dev = c->device;
 	b->st = c->rstream;
-	b->bytes = ar.total ? ar.total : 256;
+	b->bytes = (ar.total ? (ar.total + 7u) & ~(size_t)7u : 256);
 	HIP_OR_EIO(hipMallocFromPoolAsync(&b->p, b->bytes, c->pool, c->ustream));
+	HIP_OR_EIO(hipMemsetAsync(b->p, 0, b->bytes, c->ustream));
 	for (size_t i = 0; i < ar.parts.size(); i++)
 		if (ar.parts[i].second)
 			HIP_OR_EIO(hipMemcpyAsync((char *)b->p + ar.offs[i], ar.parts[i].first, ar.parts[i].second,
 						  hipMemcpyHostToDevice, c->ustream));
+	b->host_sum = arena_sum(ar);
+	HIP_OR_EIO(launch_table_sum(b->p, b->bytes, c->d_verify + slot, c->ustream));
 	out = b;
 	return 0;
 }
@@ -2939,7 +2973,7 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		o6[2] = ar.add(b.v6.vals.data(), b.v6.vals.size() * 4);
 		o6[3] = ar.add(b.v6.set.slots.data(), b.v6.set.slots.size() * sizeof(set16_slot));
 	}
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_IPC))
 		return r;
 	s.ipc4c = lpm16c{at<uint32_t>(buf, o_d), at<uint32_t>(buf, o_n), at<uint32_t>(buf, o_v),
 			 at<uint32_t>(buf, o_x), at<uint32_t>(buf, o_c), (uint32_t)b.lc.nodes.size(),
@@ -2986,7 +3020,7 @@ static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	Arena ar;
 	const size_t o_p = ar.add(b.pol.slots.data(), b.pol.slots.size() * sizeof(pol_slot));
 	const size_t o_g = ar.add(b.pg.slots.data(), b.pg.slots.size() * sizeof(uint4));
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_POL))
 		return r;
 	s.pol = pol_table{at<pol_slot>(buf, o_p), b.pol.mask, 0};
 	s.pg = pol_groups{at<uint4>(buf, o_g), b.pg.mask, 0};
@@ -3032,7 +3066,7 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		o6[6] = ar.add(pf6.rbits.data(), pf6.rbits.size() * 4);
 		o6[7] = ar.add(pf6.b24_16.data(), pf6.b24_16.size() * 2);
 	}
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_PF))
 		return r;
 	s.pf4c = lpm16c{};
 	if (have4)
@@ -3090,7 +3124,7 @@ static int commit_ep(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o4 = ar.add(ep4.slots.data(), ep4.slots.size() * sizeof(set4_slot));
 	const size_t o6 = ar.add(ep6.slots.data(), ep6.slots.size() * sizeof(set16_slot));
 	const size_t ob = ar.add(bloom.data(), bloom.size() * 4);
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_EP))
 		return r;
 	s.ep4 = addr_set4{at<set4_slot>(buf, o4), ep4.mask, ep4.max_probe};
 	s.ep6 = addr_set16{at<set16_slot>(buf, o6), ep6.mask, ep6.max_probe};
@@ -3110,7 +3144,7 @@ static int commit_lb(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o_f = ar.add(lbb.fe.data(), lbb.fe.size() * 16);
 	const size_t o_b = ar.add(lbb.be.data(), lbb.be.size() * 16);
 	const size_t o_v = ar.add(lbb.vip.data(), lbb.vip.size() * 4);
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_LB))
 		return r;
 	s.lb = lb_table{at<uint4>(buf, o_f), at<uint4>(buf, o_b), lbb.mask, (uint32_t)lbb.be.size(),
 			at<uint32_t>(buf, o_v), lbb.vip_mask};
@@ -3131,7 +3165,7 @@ static int commit_lb6(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o_f = ar.add(b.fe.data(), b.fe.size() * 32);
 	const size_t o_b = ar.add(b.be.data(), b.be.size() * 32);
 	const size_t o_v = ar.add(b.vip.data(), b.vip.size() * 4);
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_LB6))
 		return r;
 	s.lb6 = lb6_table{at<uint4>(buf, o_f), at<uint4>(buf, o_b), b.mask, (uint32_t)b.be.size(),
 			  at<uint32_t>(buf, o_v), b.vip_mask};
@@ -3157,7 +3191,7 @@ static int commit_lxc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	}
 	Arena ar;
 	const size_t o = ar.add(v.data(), v.size() * sizeof(cgpu_lxc_info));
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_LXC))
 		return r;
 	s.lxc = at<uint4>(buf, o);
 	s.n_lxc = n;
@@ -3188,7 +3222,7 @@ static int commit_inits(cgpu_ctx *c, const CommitIn &in)
 	const size_t o_p = ar.add(pk.data(), pk.size() * 8);
 	const size_t o_b = ar.add(by.data(), by.size() * 8);
 	DevBufP buf;
-	if (int r = upload(c, ar, buf))
+	if (int r = upload(c, ar, buf, G_N))
 		return r;
 	HIP_OR_EIO(launch_slot_init(c->d_totals, c->d_delta, at<uint32_t>(buf, o_s), at<uint64_t>(buf, o_p),
 				    at<uint64_t>(buf, o_b), (uint32_t)slot.size(), c->ustream));
@@ -3232,7 +3266,8 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	cgpu_snapshot &s = e->snap;
 	int (*const step[G_N])(cgpu_ctx *, CommitIn &, cgpu_snapshot &, DevBufP &) = {
 		commit_ipc, commit_pol, commit_pf, commit_ep, commit_lb, commit_lxc, commit_lb6};
-	int rc = 0;
+	int rc = hipMemsetAsync(c->d_verify, 0, (G_N + 1) * 8, c->ustream) == hipSuccess
+			 ? 0 : fail(-EIO, "commit: verify buffer reset failed");
 	for (int k = 0; k < G_N && !rc; k++)
 		if (in.dirty & (1u << k)) {
 			rc = step[k](c, in, s, e->bufs[k]);
@@ -3249,6 +3284,14 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 		    (he = hipEventRecord(e->ready, c->ustream)) != hipSuccess ||
 		    (he = hipEventSynchronize(e->ready)) != hipSuccess))
 		rc = fail(-EIO, "commit upload: %s", hipGetErrorString(he));
+	if (!rc) { /* the device's sums of what it received == the host images' */
+		uint64_t got[G_N + 1];
+		if ((he = hipMemcpy(got, c->d_verify, sizeof(got), hipMemcpyDeviceToHost)) != hipSuccess)
+			rc = fail(-EIO, "commit verify: %s", hipGetErrorString(he));
+		for (int k = 0; k < G_N && !rc; k++)
+			if ((in.dirty & (1u << k)) && e->bufs[k] && got[k] != e->bufs[k]->host_sum)
+				rc = fail(-EIO, "device table group %d differs from the host image after upload", k);
+	}
 	if (rc) {
 		std::string msg = g_last_error;
 		{
@@ -3314,6 +3357,61 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
 	if (!c->cur)
 		return fail(-ENOENT, "nothing committed");
 	*sum = c->checksum;
+	return 0;
+}
+
+/* SURVEY §5 failure detection: recompute every group buffer of the
+ * published snapshot on the device and compare with the host image's sum */
+CGPU_EXPORT int cgpu_table_verify(cgpu_ctx *c)
+{
+	if (!c)
+		return fail(-EINVAL, "null argument");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	std::lock_guard<std::mutex> cg(c->commit_mu);
+	std::shared_ptr<Epoch> e;
+	{
+		std::lock_guard<std::mutex> g(c->pub_mu);
+		e = c->cur;
+	}
+	if (!e)
+		return fail(-ENOENT, "nothing committed");
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipMemsetAsync(c->d_verify, 0, (G_N + 1) * 8, c->ustream));
+	for (int k = 0; k < G_N; k++)
+		if (e->bufs[k])
+			HIP_OR_EIO(launch_table_sum(e->bufs[k]->p, e->bufs[k]->bytes, c->d_verify + k, c->ustream));
+	uint64_t got[G_N + 1];
+	HIP_OR_EIO(hipMemcpyAsync(got, c->d_verify, sizeof(got), hipMemcpyDeviceToHost, c->ustream));
+	HIP_OR_EIO(hipStreamSynchronize(c->ustream));
+	static const char *names[G_N] = {"ipcache", "policy", "prefilter", "endpoints", "lb4", "lxc", "lb6"};
+	for (int k = 0; k < G_N; k++)
+		if (e->bufs[k] && got[k] != e->bufs[k]->host_sum)
+			return fail(-EIO, "device %s tables differ from the host image (sum %016llx, expected %016llx)",
+				    names[k], (unsigned long long)got[k], (unsigned long long)e->bufs[k]->host_sum);
+	return 0;
+}
+
+/* TEST HOOK (not in cgpu.h): xor `mask` into byte `off` of group `group`'s
+ * device buffer of the published snapshot, so that tests can show
+ * cgpu_table_verify catching a corrupted table. */
+CGPU_EXPORT int cgpu__test_corrupt(cgpu_ctx *c, int group, size_t off, uint8_t mask)
+{
+	if (!c || c->device < 0 || group < 0 || group >= G_N)
+		return -EINVAL;
+	std::shared_ptr<Epoch> e;
+	{
+		std::lock_guard<std::mutex> g(c->pub_mu);
+		e = c->cur;
+	}
+	if (!e || !e->bufs[group] || off >= e->bufs[group]->bytes)
+		return -EINVAL;
+	uint8_t b;
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(hipDeviceSynchronize());
+	HIP_OR_EIO(hipMemcpy(&b, (char *)e->bufs[group]->p + off, 1, hipMemcpyDeviceToHost));
+	b ^= mask;
+	HIP_OR_EIO(hipMemcpy((char *)e->bufs[group]->p + off, &b, 1, hipMemcpyHostToDevice));
 	return 0;
 }
 

@@ -2389,6 +2389,18 @@ __global__ void k_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 	}
 }
 
+/* device side of the table verification sum (tables.h table_sum_word) */
+__global__ __launch_bounds__(256) void k_table_sum(const uint64_t *p, uint64_t nwords, uint64_t *out)
+{
+	uint64_t acc = 0;
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < nwords; i += stride)
+		acc += table_sum_word(__builtin_nontemporal_load(p + i), i);
+	acc = wave_sum(acc);
+	if ((threadIdx.x & 63) == 0 && acc)
+		atomicAdd((unsigned long long *)out, (unsigned long long)acc);
+}
+
 unsigned grid_for(uint64_t n)
 {
 	uint64_t blocks = (n + BLOCK - 1) / BLOCK;
@@ -2653,6 +2665,14 @@ hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, 
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
 		}
 	}
+	return hipGetLastError();
+}
+
+hipError_t launch_table_sum(const void *buf, size_t bytes, uint64_t *out, hipStream_t st)
+{
+	const uint64_t nw = bytes / 8u;
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nw + 255) / 256, 4096));
+	hipLaunchKernelGGL(k_table_sum, dim3(g), dim3(256), 0, st, static_cast<const uint64_t *>(buf), nw, out);
 	return hipGetLastError();
 }
 

@@ -488,6 +488,21 @@ CT_HD uint32_t ct_group(uint32_t a, uint32_t b)
 	return ct_fmix(ct_fmix(lo ^ 0x2545f491u) ^ hi);
 }
 
+/* Table verification sum (SURVEY §5 failure detection): over the 8-byte
+ * words of an uploaded group buffer, sum of mix(word, index) for the nonzero
+ * words (the gaps between arena parts are zeroed).  The host computes it over
+ * its image before the upload, the device over the buffer it holds. */
+CT_HD uint64_t table_sum_word(uint64_t w, uint64_t i)
+{
+	if (!w)
+		return 0;
+	uint64_t x = w * 0x9E3779B97F4A7C15ull + (i + 1u) * 0xC2B2AE3D27D4EB4Full;
+	x ^= x >> 31;
+	x *= 0xBF58476D1CE4E5B9ull;
+	x ^= x >> 29;
+	return x;
+}
+
 /* counters: u64 {packets, bytes} per policy slot, then metrics */
 #define CGPU_METRICS_WORDS (256u * 4u * 2u)
 

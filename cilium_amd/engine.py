@@ -377,6 +377,11 @@ class Engine:
         check(self.L.cgpu_table_checksum(self.h, C.byref(s)), "cgpu_table_checksum")
         return s.value
 
+    def verify(self) -> None:
+        """cgpu_table_verify: the device tables still equal the host images
+        (raises CgpuError EIO naming the group otherwise)."""
+        check(self.L.cgpu_table_verify(self.h), "cgpu_table_verify")
+
     def counter_layout_checksum(self) -> int:
         s = C.c_uint64()
         check(self.L.cgpu_counter_layout_checksum(self.h, C.byref(s)), "cgpu_counter_layout_checksum")

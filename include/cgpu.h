@@ -393,6 +393,13 @@ int cgpu_commit(cgpu_ctx *ctx, uint64_t *epoch_out);
 /* order-independent checksum of the committed table contents; replicas on
  * different GPUs/ranks holding the same tables report the same value */
 int cgpu_table_checksum(cgpu_ctx *ctx, uint64_t *sum_out);
+/* Failure detection: every group buffer a commit uploads is
+ * summed on the device and compared with the host image's sum before the
+ * snapshot is published (a mismatch fails the commit with -EIO).  This call
+ * re-sums every buffer of the published snapshot on the device and returns
+ * -EIO (naming the table group) when one no longer matches its host image;
+ * a caller recovers by committing again from the authoritative host mirror. */
+int cgpu_table_verify(cgpu_ctx *ctx);
 /* checksum of which counter slot every committed policy key holds.  Slot
  * assignment is a function of the sequence of map operations and commits
  * only (never of GPU progress), so replicas that applied the same sequence

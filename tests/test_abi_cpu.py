@@ -36,7 +36,9 @@ def test_exports_every_declared_symbol():
     missing = [s for s in syms if not hasattr(L_, s)]
     assert not missing, missing
     # the ctypes table covers the whole header too
-    assert set(syms) == set(PROTOS), set(syms) ^ set(PROTOS)
+    # (cgpu__* are test hooks, exported but deliberately not in the header)
+    protos = {p for p in PROTOS if not p.startswith("cgpu__")}
+    assert set(syms) == protos, set(syms) ^ protos
 
 
 def test_library_is_gfx950():

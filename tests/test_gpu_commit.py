@@ -8,6 +8,7 @@ identity on a one-rank communicator.
 Reference semantics: map writes land per key (pkg/endpoint/endpoint.go:
 2572-2652 syncPolicyMap; pkg/datapath/ipcache/listener.go:78-127) while the
 datapath keeps running (bpf/lib/policy.h:46-110, bpf/lib/eps.h:56-80)."""
+import errno
 import threading
 import time
 
@@ -383,3 +384,36 @@ def test_counter_slot_layout_deterministic(torch_cuda):
     torch.cuda.synchronize()
     busy.close()
     idle.close()
+
+
+def test_table_verify_detects_corruption(torch_cuda):
+    """SURVEY §5 failure detection: every commit checks the device's sum of
+    each uploaded group against the host image; cgpu_table_verify re-checks
+    the published snapshot, and a flipped byte in any group is an EIO that
+    names it; a fresh commit from the host mirror repairs it."""
+    from cilium_amd._abi import CgpuError
+    T = synth.make_tables(n_prefixes=3000, n_identities=200, n_endpoints=2, keys_per_ep=2000)
+    e = _engine(**T.engine_config())
+    synth.load_engine(e, T)
+    e.endpoint_update(L.endpoint_key("10.1.0.1"))
+    e.commit()
+    e.verify()
+    for group, off in ((0, 4096 + 3), (1, 77)):
+        assert e.L.cgpu__test_corrupt(e.h, group, off, 0x10) == 0
+        with pytest.raises(CgpuError) as ex:
+            e.verify()
+        assert ex.value.errno == errno.EIO
+        # the host mirror is authoritative: rewrite the group and commit
+        if group == 0:
+            k, v = T.ipc_keys[0], T.ipc_vals[0]
+            assert e.ipcache_delete(k) == 0
+            e.commit()
+            assert e.ipcache_update(k, v) == 0
+        else:
+            k, en, ep = T.pol_keys[0], T.pol_entries[0], T.pol_ep[0]
+            assert e.policy_delete(int(ep), k) == 0
+            e.commit()
+            assert e.policy_update(int(ep), k, en) == 0
+        e.commit()
+        e.verify()
+    e.close()
