@@ -128,6 +128,8 @@ PROTOS = {
     "cgpu_commit": (i32, [vp, C.POINTER(u64)]),
     "cgpu_table_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_table_verify": (i32, [vp]),
+    "cgpu_mirror_save": (i32, [vp, C.c_char_p]),
+    "cgpu_mirror_restore": (i32, [vp, C.c_char_p]),
     "cgpu__test_corrupt": (i32, [vp, i32, sz, C.c_uint8]),
     "cgpu_counter_layout_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),

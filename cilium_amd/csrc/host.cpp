@@ -4601,6 +4601,318 @@ CGPU_EXPORT int cgpu_classify_v6_ct(cgpu_ctx *c, const cgpu_tuples_v6_ct *t, siz
 }
 
 /* ======================================================================= */
+/* host mirror snapshot / restore (SURVEY §5 checkpoint / resume)            */
+/* ======================================================================= */
+/* The reference keeps its maps pinned in bpffs across agent restarts and
+ * replays the ipcache into new listeners (pkg/ipcache/ipcache.go:328-338
+ * DumpToListenerLocked).  The engine's authoritative state is the host
+ * mirror (plus the device-side counters and conntrack maps), so a checkpoint
+ * is the mirror serialized, and a restore replays it through the same map
+ * calls the agent uses.  File: "CGPUMIR1", u32 version, u32 section count,
+ * sections {u32 tag, u32 record bytes, u64 count, records}, then the FNV-1a
+ * hash of everything before it. */
+enum { MIR_IPC = 1, MIR_POL, MIR_CIDR, MIR_EP, MIR_LB4, MIR_LB6, MIR_LXC, MIR_REV, MIR_CT4, MIR_CT6 };
+
+struct MirOut {
+	std::vector<uint8_t> buf;
+	void put(const void *p, size_t n)
+	{
+		const uint8_t *b = static_cast<const uint8_t *>(p);
+		buf.insert(buf.end(), b, b + n);
+	}
+	template <typename T> void put(const T &v) { put(&v, sizeof(v)); }
+	size_t section(uint32_t tag, uint32_t rec)
+	{
+		put(tag);
+		put(rec);
+		const size_t at = buf.size();
+		put((uint64_t)0);
+		return at;
+	}
+	void count(size_t at, uint64_t n) { memcpy(&buf[at], &n, 8); }
+};
+
+static void mir_ct(MirOut &o, uint32_t tag, const CtMap &m, uint32_t ksz)
+{
+	const size_t at = o.section(tag, ksz + 56);
+	uint64_t n = 0;
+	for (uint32_t h = 0; h <= m.mask && !m.keys.empty(); h++) {
+		if (ctm_tag(m, h) != CT_TAG_LIVE)
+			continue;
+		const CtKey k = ctm_key_at(m, h);
+		if (m.v6) {
+			const cgpu_ct6_tuple t = ct_unkey6(k);
+			o.put(&t, ksz);
+		} else {
+			const cgpu_ct4_tuple t = ct_unkey4(k);
+			o.put(&t, ksz);
+		}
+		o.put(&m.vals[4u * h], 56);
+		n++;
+	}
+	o.count(at, n);
+}
+
+CGPU_EXPORT int cgpu_mirror_save(cgpu_ctx *c, const char *path)
+{
+	if (!c || !path)
+		return fail(-EINVAL, "null argument");
+	MirOut o;
+	o.put("CGPUMIR1", 8);
+	o.put((uint32_t)1);
+	o.put((uint32_t)10);
+	{
+		std::lock_guard<std::mutex> g(c->mu);
+		/* device-side state the mirror does not hold: per-entry counters
+		 * (as cgpu_policy_lookup reports them) and the conntrack maps */
+		std::vector<std::pair<const PolEntry *, size_t>> hit;
+		for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+			for (auto &kv : c->pol[ep])
+				hit.push_back({&kv.second, hit.size()});
+		std::vector<cgpu_policy_entry> ents(hit.size());
+		if (int r = policy_fill(c, hit, ents.data()))
+			return r;
+		if (int r = ct_pull(c, c->ct4))
+			return r;
+		if (int r = ct_pull(c, c->ct6))
+			return r;
+		size_t at = o.section(MIR_IPC, 32);
+		for (auto &kv : c->ipc) {
+			o.put(kv.second.raw);
+			o.put(kv.second.val);
+		}
+		o.count(at, c->ipc.size());
+		at = o.section(MIR_POL, 36);
+		uint64_t n = 0;
+		for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+			for (auto &kv : c->pol[ep]) {
+				o.put(ep);
+				o.put(&kv.first, 8);
+				o.put(ents[n]);
+				n++;
+			}
+		o.count(at, n);
+		at = o.section(MIR_CIDR, 24);
+		n = 0;
+		auto cidr = [&](uint32_t which, const cgpu_cidr_key &k) {
+			o.put(which);
+			o.put(k);
+			n++;
+		};
+		for (auto &kv : c->dyn4)
+			cidr(CGPU_CIDR_V4_DYN, kv.second);
+		for (auto &kv : c->dyn6)
+			cidr(CGPU_CIDR_V6_DYN, kv.second);
+		for (auto &x : c->fix4) {
+			cgpu_cidr_key k{};
+			memcpy(&k, x.data(), x.size());
+			cidr(CGPU_CIDR_V4_FIX, k);
+		}
+		for (auto &x : c->fix6) {
+			cgpu_cidr_key k{};
+			memcpy(&k, x.data(), x.size());
+			cidr(CGPU_CIDR_V6_FIX, k);
+		}
+		o.count(at, n);
+		at = o.section(MIR_EP, 20);
+		for (auto &x : c->lxc)
+			o.put(x.data(), 20);
+		o.count(at, c->lxc.size());
+		at = o.section(MIR_LB4, 20);
+		for (auto &kv : c->lb) {
+			const cgpu_lb4_key k = lb_unkey(kv.first);
+			o.put(k);
+			o.put(kv.second);
+		}
+		o.count(at, c->lb.size());
+		at = o.section(MIR_LB6, 44);
+		for (auto &kv : c->lb6) {
+			const cgpu_lb6_key k = lb6_unkey(kv.first);
+			o.put(k);
+			o.put(kv.second);
+		}
+		o.count(at, c->lb6.size());
+		at = o.section(MIR_LXC, 36);
+		for (auto &kv : c->lxcinfo) {
+			o.put(kv.first);
+			o.put(kv.second);
+		}
+		o.count(at, c->lxcinfo.size());
+		at = o.section(MIR_REV, 8);
+		o.put(c->pf_revision);
+		o.count(at, 1);
+		mir_ct(o, MIR_CT4, c->ct4, 14);
+		mir_ct(o, MIR_CT6, c->ct6, 38);
+	}
+	o.put(fnv(1469598103934665603ull, o.buf.data(), o.buf.size()));
+	const std::string tmp = std::string(path) + ".tmp";
+	FILE *f = fopen(tmp.c_str(), "wb");
+	if (!f)
+		return fail(-errno, "cannot create %s", tmp.c_str());
+	const bool ok = fwrite(o.buf.data(), 1, o.buf.size(), f) == o.buf.size();
+	if (fclose(f) != 0 || !ok || rename(tmp.c_str(), path) != 0) {
+		remove(tmp.c_str());
+		return fail(-EIO, "cannot write %s", path);
+	}
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_mirror_restore(cgpu_ctx *c, const char *path)
+{
+	if (!c || !path)
+		return fail(-EINVAL, "null argument");
+	std::vector<uint8_t> buf;
+	{
+		FILE *f = fopen(path, "rb");
+		if (!f)
+			return fail(-ENOENT, "cannot open %s", path);
+		uint8_t chunk[1 << 16];
+		size_t got;
+		while ((got = fread(chunk, 1, sizeof(chunk), f)) > 0)
+			buf.insert(buf.end(), chunk, chunk + got);
+		fclose(f);
+	}
+	if (buf.size() < 24 || memcmp(buf.data(), "CGPUMIR1", 8))
+		return fail(-EINVAL, "%s is not a cgpu mirror snapshot", path);
+	uint64_t want;
+	memcpy(&want, &buf[buf.size() - 8], 8);
+	if (fnv(1469598103934665603ull, buf.data(), buf.size() - 8) != want)
+		return fail(-EINVAL, "%s: checksum mismatch (truncated or corrupted)", path);
+	uint32_t version, nsec;
+	memcpy(&version, &buf[8], 4);
+	memcpy(&nsec, &buf[12], 4);
+	if (version != 1)
+		return fail(-EINVAL, "%s: snapshot version %u", path, version);
+	{
+		std::lock_guard<std::mutex> g(c->mu);
+		bool empty = c->ipc.empty() && !c->pol_total && c->dyn4.empty() && c->dyn6.empty() &&
+			     c->fix4.empty() && c->fix6.empty() && c->lxc.empty() && c->lb.empty() &&
+			     c->lb6.empty() && c->lxcinfo.empty();
+		for (CtMap *m : {&c->ct4, &c->ct6}) {
+			if (int r = ct_pull(c, *m))
+				return r;
+			empty = empty && !m->live;
+		}
+		if (!empty)
+			return fail(-EEXIST, "restore needs an empty context");
+	}
+	/* validate the section structure before applying anything */
+	struct Sec {
+		uint32_t tag, rec;
+		uint64_t n;
+		size_t off;
+	};
+	std::vector<Sec> secs;
+	size_t off = 16;
+	const size_t end = buf.size() - 8;
+	static const uint32_t recsz[] = {0, 32, 36, 24, 20, 20, 44, 36, 8, 70, 94};
+	for (uint32_t i = 0; i < nsec; i++) {
+		Sec s_;
+		if (off + 16 > end)
+			return fail(-EINVAL, "%s: truncated section header", path);
+		memcpy(&s_.tag, &buf[off], 4);
+		memcpy(&s_.rec, &buf[off + 4], 4);
+		memcpy(&s_.n, &buf[off + 8], 8);
+		s_.off = off + 16;
+		if (s_.tag < MIR_IPC || s_.tag > MIR_CT6 || s_.rec != recsz[s_.tag] ||
+		    s_.n > (end - s_.off) / s_.rec)
+			return fail(-EINVAL, "%s: bad section %u", path, s_.tag);
+		off = s_.off + s_.n * s_.rec;
+		secs.push_back(s_);
+	}
+	if (off != end)
+		return fail(-EINVAL, "%s: trailing bytes", path);
+	/* replay through the map calls (the listeners' path) */
+	for (const Sec &s_ : secs)
+		for (uint64_t i = 0; i < s_.n; i++) {
+			const uint8_t *r = &buf[s_.off + i * s_.rec];
+			int rc = 0;
+			switch (s_.tag) {
+			case MIR_IPC: {
+				cgpu_ipcache_key k;
+				cgpu_remote_endpoint_info v;
+				memcpy(&k, r, 24);
+				memcpy(&v, r + 24, 8);
+				rc = cgpu_ipcache_update(c, &k, &v, CGPU_NOEXIST);
+				break;
+			}
+			case MIR_POL: {
+				uint32_t ep;
+				cgpu_policy_key k;
+				cgpu_policy_entry e;
+				memcpy(&ep, r, 4);
+				memcpy(&k, r + 4, 8);
+				memcpy(&e, r + 12, 24);
+				rc = cgpu_policy_update(c, ep, &k, &e, CGPU_NOEXIST);
+				break;
+			}
+			case MIR_CIDR: {
+				uint32_t which;
+				cgpu_cidr_key k;
+				memcpy(&which, r, 4);
+				memcpy(&k, r + 4, 20);
+				rc = cgpu_cidr_update(c, (int)which, &k, CGPU_NOEXIST);
+				break;
+			}
+			case MIR_EP: {
+				cgpu_endpoint_key k;
+				memcpy(&k, r, 20);
+				rc = cgpu_endpoint_update(c, &k, CGPU_NOEXIST);
+				break;
+			}
+			case MIR_LB4: {
+				cgpu_lb4_key k;
+				cgpu_lb4_service v;
+				memcpy(&k, r, 8);
+				memcpy(&v, r + 8, 12);
+				rc = cgpu_lb4_update(c, &k, &v, CGPU_NOEXIST);
+				break;
+			}
+			case MIR_LB6: {
+				cgpu_lb6_key k;
+				cgpu_lb6_service v;
+				memcpy(&k, r, 20);
+				memcpy(&v, r + 20, 24);
+				rc = cgpu_lb6_update(c, &k, &v, CGPU_NOEXIST);
+				break;
+			}
+			case MIR_LXC: {
+				uint32_t ep;
+				cgpu_lxc_info v;
+				memcpy(&ep, r, 4);
+				memcpy(&v, r + 4, 32);
+				rc = cgpu_lxc_update(c, ep, &v);
+				break;
+			}
+			case MIR_REV: {
+				std::lock_guard<std::mutex> g(c->mu);
+				memcpy(&c->pf_revision, r, 8);
+				break;
+			}
+			case MIR_CT4: {
+				cgpu_ct4_tuple k;
+				cgpu_ct_entry v;
+				memcpy(&k, r, 14);
+				memcpy(&v, r + 14, 56);
+				rc = cgpu_ct4_update(c, &k, &v, CGPU_NOEXIST);
+				break;
+			}
+			case MIR_CT6: {
+				cgpu_ct6_tuple k;
+				cgpu_ct_entry v;
+				memcpy(&k, r, 38);
+				memcpy(&v, r + 38, 56);
+				rc = cgpu_ct6_update(c, &k, &v, CGPU_NOEXIST);
+				break;
+			}
+			}
+			if (rc)
+				return rc;
+		}
+	return 0;
+}
+
+/* ======================================================================= */
 /* L3 MapState compilation                               */
 /* ======================================================================= */
 /* validate a program + label sets (+ a MapState spec), upload them, run

@@ -377,6 +377,14 @@ class Engine:
         check(self.L.cgpu_table_checksum(self.h, C.byref(s)), "cgpu_table_checksum")
         return s.value
 
+    def mirror_save(self, path: str) -> None:
+        """cgpu_mirror_save: checkpoint the host mirror (+ counters, CT maps)."""
+        check(self.L.cgpu_mirror_save(self.h, str(path).encode()), "cgpu_mirror_save")
+
+    def mirror_restore(self, path: str) -> None:
+        """cgpu_mirror_restore into this (empty) context; commit afterwards."""
+        check(self.L.cgpu_mirror_restore(self.h, str(path).encode()), "cgpu_mirror_restore")
+
     def verify(self) -> None:
         """cgpu_table_verify: the device tables still equal the host images
         (raises CgpuError EIO naming the group otherwise)."""

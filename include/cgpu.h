@@ -759,6 +759,24 @@ int cgpu_classify_v6_ct(cgpu_ctx *ctx, const cgpu_tuples_v6_ct *t, size_t n, uin
 			void *stream);
 
 /* ------------------------------------------------------------------ */
+/* checkpoint / resume                                      */
+/* ------------------------------------------------------------------ */
+/* The host mirror is authoritative (the device is rebuilt from it at any
+ * commit), so a checkpoint is the mirror written to a file: every ipcache,
+ * policy (with each entry's packets / bytes counters), prefilter CIDR,
+ * endpoint, lb4 / lb6 and lxc entry, the PreFilter revision, and both
+ * conntrack maps.  The reference's counterpart is its maps pinned in bpffs
+ * plus the ipcache replay into listeners (pkg/ipcache/ipcache.go:328-338).
+ * save: atomic (written to path.tmp, then renamed).  restore: into a context
+ * whose maps are all empty (else -EEXIST); the file is validated whole
+ * (-EINVAL on a bad header, section or checksum) and replayed through the
+ * map calls with BPF_NOEXIST (capacity errors are returned as those calls
+ * return them).  The tables reach the device at the next cgpu_commit.  The
+ * {reason, dir} metrics are not part of a checkpoint (they restart at 0). */
+int cgpu_mirror_save(cgpu_ctx *ctx, const char *path);
+int cgpu_mirror_restore(cgpu_ctx *ctx, const char *path);
+
+/* ------------------------------------------------------------------ */
 /* L3 MapState compilation                           */
 /* ------------------------------------------------------------------ */
 /* The label decision computeDesiredL3PolicyMapEntries asks of the policy

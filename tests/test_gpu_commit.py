@@ -417,3 +417,48 @@ def test_table_verify_detects_corruption(torch_cuda):
         e.commit()
         e.verify()
     e.close()
+
+
+def test_mirror_save_restore_resumes(torch_cuda, tmp_path):
+    """SURVEY §5 checkpoint / resume on the device: after classify and
+    conntrack batches, a checkpoint restored into a fresh context (then
+    committed) holds the same per-entry counters and conntrack map, and the
+    next batches on both contexts produce identical verdicts, counters and
+    maps."""
+    torch = torch_cuda
+    T = synth.make_tables(**synth.CONFIGS["cpu"])
+    T.n_endpoints = 1
+    t = synth.make_tuples(T, 1 << 18)
+    tc, locals_be, seclabels = synth.make_ct_workload(T, 5000, mean_pkts=8.0)
+    e = _engine(**T.engine_config(), ct_max=1 << 16)
+    synth.load_engine(e, T)
+    synth.load_lxc(e, seclabels)
+    e.commit()
+    e.classify_v4(synth.to_device(t), stage=False)
+    half = len(tc["saddr"]) // 2
+    first = {k: v[:half] for k, v in tc.items()}
+    rest = {k: v[half:] for k, v in tc.items()}
+    e.classify_v4_ct(synth.to_device(first), 100)
+    torch.cuda.synchronize()
+    path = str(tmp_path / "ckpt.bin")
+    e.mirror_save(path)
+    f = _engine(**T.engine_config(), ct_max=1 << 16)
+    f.mirror_restore(path)
+    f.commit()
+    np.testing.assert_array_equal(f.policy_counters(T.pol_ep, T.pol_keys),
+                                  e.policy_counters(T.pol_ep, T.pol_keys))
+    for a, b in zip(e.ct4_dump(), f.ct4_dump()):
+        np.testing.assert_array_equal(a, b)
+    outs = []
+    for x in (e, f):
+        o = x.classify_v4_ct(synth.to_device(rest), 104)
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu().numpy() for k, v in o.items() if v is not None})
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+    np.testing.assert_array_equal(f.policy_counters(T.pol_ep, T.pol_keys),
+                                  e.policy_counters(T.pol_ep, T.pol_keys))
+    for a, b in zip(e.ct4_dump(), f.ct4_dump()):
+        np.testing.assert_array_equal(a, b)
+    e.close()
+    f.close()

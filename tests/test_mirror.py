@@ -1,0 +1,129 @@
+"""Checkpoint / resume of the host mirror: cgpu_mirror_save and
+cgpu_mirror_restore on host-only contexts (device = -1).  A context holding
+every map kind (ipcache incl. IPv6 and tombstones, 3 endpoints' policy maps,
+the four prefilter CIDR maps and the PreFilter revision, cilium_lxc, lb4 /
+lb6 services, per-endpoint lxc info, both conntrack maps) is saved and
+restored into a fresh context; every dump, lookup and count is identical.
+Corrupted, truncated and foreign files are -EINVAL, a non-empty target is
+-EEXIST, and nothing is applied from a file that fails validation."""
+import errno
+import os
+
+import numpy as np
+import pytest
+
+from cilium_amd import layouts as L, synth
+from cilium_amd._abi import CgpuError
+from cilium_amd.engine import (CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX, Engine,
+                               PreFilter)
+
+
+def _populated():
+    e = Engine(device=-1, ct_max=4096, lb_max_entries=1 << 16)
+    T = synth.make_tables(n_prefixes=500, n_identities=50, n_endpoints=3, keys_per_ep=300)
+    synth.load_engine(e, T)
+    assert e.ipcache_update(L.ipcache_key("f00d::/64"), L.remote_info(777)) == 0
+    assert e.ipcache_update(L.ipcache_key("f00d::1/128"), L.remote_info(0)) == 0  # tombstone
+    # counters supplied with an entry travel with it
+    assert e.policy_update(1, L.policy_key(4242, 80, 6, 1), L.policy_entry(8080, 12, 3456)) == 0
+    pf = PreFilter(e)
+    pf.Insert(0, ["10.1.0.0/16", "10.2.3.4/32", "2001:db8::/48", "2001:db8::5/128"])
+    assert pf.Revision() == 2
+    for ip in ("10.200.0.1", "10.200.0.2", "f00d::10"):
+        assert e.endpoint_update(L.endpoint_key(ip)) == 0
+    S = synth.make_services(T, 40)
+    assert e.lb4_update_batch(S.keys, S.vals) == 0
+    k6 = np.zeros((), L.LB6_KEY)
+    k6["address"][:] = np.frombuffer(bytes.fromhex("20010db8000000000000000000000099"), np.uint8)
+    k6["dport"] = L.htons(443)
+    v6 = np.zeros((), L.LB6_SERVICE)
+    v6["count"] = 1
+    assert e.lb6_update(k6, v6) == 0
+    k6["slave"] = 1
+    v6["count"] = 0
+    v6["target"][:] = np.frombuffer(bytes.fromhex("20010db8000000000000000000000001"), np.uint8)
+    assert e.lb6_update(k6, v6) == 0
+    synth.load_lxc(e, [5000, 5007, 5014])
+    rng = np.random.default_rng(3)
+    for i in range(50):
+        k = np.zeros((), L.CT4_TUPLE)
+        k["daddr"], k["saddr"], k["dport"], k["nexthdr"] = 0x0A000001 + i, 0x0B000001, 80, 6
+        v = np.zeros((), L.CT_ENTRY)
+        v["lifetime"], v["rx_packets"], v["src_sec_id"] = 100 + i, i, 5000
+        assert e.ct4_update(k, v) == 0
+        k6t = np.zeros((), L.CT6_TUPLE)
+        k6t["daddr"][:] = rng.integers(0, 256, 16, dtype=np.uint8)
+        k6t["saddr"][:] = rng.integers(0, 256, 16, dtype=np.uint8)
+        k6t["nexthdr"], k6t["flags"] = 58, 2
+        v["rev_nat_index"] = i
+        assert e.ct6_update(k6t, v) == 0
+    return e
+
+
+def _state(e):
+    st = {"ipc": sorted(bytes(k) for k in e.ipcache_keys())}
+    st["ipc_vals"] = sorted(bytes(e.ipcache_lookup(np.frombuffer(k, L.IPCACHE_KEY)[0])[1])
+                            for k in st["ipc"])
+    for ep in range(4):
+        k, v = e.policy_dump(ep)
+        st[f"pol{ep}"] = (k.tobytes(), v.tobytes())
+    for w in (CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX):
+        st[f"cidr{w}"] = sorted(bytes(k) for k in e.cidr_keys(w))
+    st["ep"] = [e.endpoint_lookup(L.endpoint_key(ip)) for ip in ("10.200.0.1", "10.200.0.2", "f00d::10",
+                                                                   "10.200.0.3")]
+    st["lb4"] = [(bytes(k), bytes(e.lb4_lookup(k)[1])) for k in e.lb4_keys()]
+    st["lb6"] = [(bytes(k), bytes(e.lb6_lookup(k)[1])) for k in e.lb6_keys()]
+    st["lxc"] = [e.lxc_lookup(ep).tobytes() for ep in range(3)]
+    st["rev"] = PreFilter(e).Revision()
+    st["ct4"] = [a.tobytes() for a in e.ct4_dump()]
+    st["ct6"] = [a.tobytes() for a in e.ct6_dump()]
+    return st
+
+
+def test_mirror_roundtrip(tmp_path):
+    e = _populated()
+    path = str(tmp_path / "mirror.bin")
+    e.mirror_save(path)
+    assert not os.path.exists(path + ".tmp")
+    f = Engine(device=-1, ct_max=4096, lb_max_entries=1 << 16)
+    f.mirror_restore(path)
+    a, b = _state(e), _state(f)
+    assert a.keys() == b.keys()
+    for k in a:
+        assert a[k] == b[k], k
+    assert len(a["ct4"][0]) and len(a["ct6"][0]) and a["rev"] == 2
+    # the entry's supplied counters travel with it
+    k, v = f.policy_dump(1)
+    hit = v[(k["sec_label"] == 4242)]
+    assert int(hit["packets"][0]) == 12 and int(hit["bytes"][0]) == 3456
+    # restore into a non-empty context is refused
+    with pytest.raises(CgpuError) as ex:
+        f.mirror_restore(path)
+    assert ex.value.errno == errno.EEXIST
+    e.close()
+    f.close()
+
+
+@pytest.mark.parametrize("damage", ["flip", "truncate", "foreign", "missing"])
+def test_mirror_rejects_bad_files(tmp_path, damage):
+    e = _populated()
+    path = str(tmp_path / "mirror.bin")
+    e.mirror_save(path)
+    raw = bytearray(open(path, "rb").read())
+    if damage == "flip":
+        raw[len(raw) // 2] ^= 0x40
+    elif damage == "truncate":
+        raw = raw[: len(raw) - 100]
+    elif damage == "foreign":
+        raw[:8] = b"NOTAMIRR"
+    if damage == "missing":
+        path = str(tmp_path / "absent.bin")
+    else:
+        open(path, "wb").write(raw)
+    f = Engine(device=-1, ct_max=4096, lb_max_entries=1 << 16)
+    with pytest.raises(CgpuError) as ex:
+        f.mirror_restore(path)
+    assert ex.value.errno == (errno.ENOENT if damage == "missing" else errno.EINVAL)
+    assert f.ipcache_keys() == [] and f.ct4_count() == 0  # nothing applied
+    e.close()
+    f.close()
