@@ -67,5 +67,59 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str = LIB
     return out
 
 
+SAN_DIR = os.path.join(HERE, "_san")
+SAN_FLAGS = {
+    # each -fsanitize= directly after -Xarch_host: host code only (the
+    # device code is the product's, unchanged)
+    "asan": ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-fno-omit-frame-pointer"],
+    "tsan": ["-Xarch_host", "-fsanitize=thread"],
+}
+
+
+def build_sanitized(kind: str, force: bool = False) -> tuple[str, str]:
+    """SURVEY §5 sanitizers: the library with its host code instrumented
+    (AddressSanitizer + UndefinedBehaviorSanitizer, or ThreadSanitizer) and
+    the host-only ABI driver tests/sanitize/abi_host_driver.cpp linked
+    against it, in cilium_amd/_san/ (development container; never shipped).
+    Returns (library, driver)."""
+    os.makedirs(SAN_DIR, exist_ok=True)
+    lib = os.path.join(SAN_DIR, f"libcgpu_{kind}.so")
+    drv = os.path.join(SAN_DIR, f"abi_host_driver_{kind}")
+    src = os.path.join(ROOT, "tests", "sanitize", "abi_host_driver.cpp")
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [src, os.path.join(ROOT, "include", "cgpu.h")]
+    if not force and os.path.exists(drv) and os.path.exists(lib) and             all(os.path.getmtime(d) < os.path.getmtime(drv) for d in deps):
+        return lib, drv
+    flags = SAN_FLAGS[kind]
+    objs = []
+    for src_ in SOURCES:
+        host = src_.endswith(".cpp")
+        # the device code is not instrumented: one kernels object serves both kinds
+        obj = os.path.join(SAN_DIR, src_.rsplit(".", 1)[0] + (f".{kind}.o" if host else ".plain.o"))
+        if not host and os.path.exists(obj) and all(
+                os.path.getmtime(d) < os.path.getmtime(obj) for d in deps):
+            objs.append(obj)
+            continue
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-O1" if host else "-O3", "-g", "-std=c++17", "-fPIC",
+               "-fvisibility=hidden", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
+               "-c", os.path.join(CSRC, src_), "-o", obj]
+        if host:
+            cmd[1:1] = ["-x", "hip"] + flags
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    link_san = ["-fsanitize=address,undefined"] if kind == "asan" else ["-fsanitize=thread"]
+    subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib,
+                    "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrccl"], check=True)
+    clang = "/opt/rocm/lib/llvm/bin/clang++"
+    subprocess.run([clang, "-O1", "-g", "-std=c++17", *link_san, "-fno-omit-frame-pointer",
+                    "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    "-D__HIP_PLATFORM_AMD__", src, "-o", drv, lib,
+                    f"-Wl,-rpath,{SAN_DIR}", "-Wl,-rpath,/opt/rocm/lib", "-pthread"], check=True)
+    for o in objs:
+        if not o.endswith(".plain.o"):
+            os.remove(o)
+    return lib, drv
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
