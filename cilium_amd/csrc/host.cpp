@@ -683,6 +683,7 @@ struct Rank6 {
 struct V6Build {
 	std::vector<uint32_t> root; /* 2 x 65536: {row, short} */
 	std::vector<uint32_t> masks;
+	std::vector<uint32_t> lens; /* per mask row: tables.h v6_lpm.lens */
 	std::vector<uint32_t> vals;
 	Set16Build set;
 	std::vector<uint32_t> bloom; /* tables.h v6_lpm.bloom */
@@ -745,6 +746,20 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 		}
 		b.root[2 * r] = id;
 		b.root[2 * r + 1] = shortv[r];
+	}
+	/* every row's lengths, longest first: the first 8 as bytes, the count */
+	b.lens.assign(b.masks.size(), 0);
+	for (size_t row = 0; row < b.masks.size() / 4; row++) {
+		uint32_t n = 0;
+		for (int len = 128; len >= 17; len--) {
+			const uint32_t bit = (uint32_t)len - 17u;
+			if (!(b.masks[4 * row + bit / 32] >> (bit % 32) & 1u))
+				continue;
+			if (n < 8)
+				b.lens[4 * row + n / 4] |= (uint32_t)len << (8 * (n % 4));
+			n++;
+		}
+		b.lens[4 * row + 2] = n;
 	}
 	std::vector<std::array<uint32_t, 6>> keys;
 	keys.reserve(longer.size());
@@ -1350,6 +1365,7 @@ struct DevBuf {
 	int dev = -1;
 	hipStream_t st = nullptr;
 	uint64_t host_sum = 0; /* table_sum_word over the host image (verification) */
+	std::vector<std::pair<size_t, size_t>> parts; /* (offset, bytes) summed */
 	~DevBuf()
 	{
 		if (p) {
@@ -2894,24 +2910,46 @@ static void uncapture(cgpu_ctx *c, const CommitIn &in)
 	c->slot_inits.insert(c->slot_inits.begin(), in.inits.begin(), in.inits.end());
 }
 
-/* table_sum_word over the arena's image (parts at their offsets, zero gaps) */
+/* table_sum_word over words [a, b) of one part (its bytes at word w0) */
+static uint64_t part_sum(const uint8_t *p, size_t bytes, size_t w0, size_t a, size_t b)
+{
+	uint64_t sum = 0;
+	const size_t full = std::min(b, bytes / 8u);
+	for (size_t j = a; j < full; j++) {
+		uint64_t w;
+		memcpy(&w, p + 8u * j, 8);
+		sum += table_sum_word(w, w0 + j);
+	}
+	if (b > full && full * 8u < bytes) {
+		uint64_t w = 0;
+		memcpy(&w, p + 8u * full, bytes % 8u);
+		sum += table_sum_word(w, w0 + full);
+	}
+	return sum;
+}
+
+/* table_sum_word over the arena's parts at their offsets (large arenas on
+ * several threads: a commit waits for it) */
 static uint64_t arena_sum(const Arena &ar)
 {
+	const size_t big = (size_t)1 << 20;
 	uint64_t sum = 0;
 	for (size_t i = 0; i < ar.parts.size(); i++) {
 		const uint8_t *p = static_cast<const uint8_t *>(ar.parts[i].first);
-		const size_t bytes = ar.parts[i].second, w0 = ar.offs[i] / 8u;
-		const size_t full = bytes / 8u;
-		for (size_t j = 0; j < full; j++) {
-			uint64_t w;
-			memcpy(&w, p + 8u * j, 8);
-			sum += table_sum_word(w, w0 + j);
+		const size_t bytes = ar.parts[i].second, w0 = ar.offs[i] / 8u, nw = (bytes + 7u) / 8u;
+		if (bytes < 4 * big) {
+			sum += part_sum(p, bytes, w0, 0, nw);
+			continue;
 		}
-		if (bytes % 8u) {
-			uint64_t w = 0;
-			memcpy(&w, p + 8u * full, bytes % 8u);
-			sum += table_sum_word(w, w0 + full);
-		}
+		const size_t nt = std::min<size_t>(8, bytes / big);
+		std::vector<uint64_t> sums(nt, 0);
+		std::vector<std::thread> th;
+		for (size_t t = 0; t < nt; t++)
+			th.emplace_back([&, t] { sums[t] = part_sum(p, bytes, w0, nw * t / nt, nw * (t + 1) / nt); });
+		for (auto &x : th)
+			x.join();
+		for (uint64_t x : sums)
+			sum += x;
 	}
 	return sum;
 }
@@ -2925,15 +2963,17 @@ static int upload(cgpu_ctx *c, const Arena &ar, DevBufP &out, int slot)
 	auto b = std::make_shared<DevBuf>();
 	b->dev = c->device;
 	b->st = c->rstream;
-	b->bytes = (ar.total ? (ar.total + 7u) & ~(size_t)7u : 256);
+	b->bytes = ar.total ? ar.total : 256;
 	HIP_OR_EIO(hipMallocFromPoolAsync(&b->p, b->bytes, c->pool, c->ustream));
-	HIP_OR_EIO(hipMemsetAsync(b->p, 0, b->bytes, c->ustream));
 	for (size_t i = 0; i < ar.parts.size(); i++)
-		if (ar.parts[i].second)
+		if (ar.parts[i].second) {
 			HIP_OR_EIO(hipMemcpyAsync((char *)b->p + ar.offs[i], ar.parts[i].first, ar.parts[i].second,
 						  hipMemcpyHostToDevice, c->ustream));
-	b->host_sum = arena_sum(ar);
-	HIP_OR_EIO(launch_table_sum(b->p, b->bytes, c->d_verify + slot, c->ustream));
+			HIP_OR_EIO(launch_table_sum(b->p, ar.offs[i], ar.parts[i].second, c->d_verify + slot,
+						    c->ustream));
+			b->parts.push_back({ar.offs[i], ar.parts[i].second});
+		}
+	b->host_sum = arena_sum(ar); /* while the device copies and sums */
 	out = b;
 	return 0;
 }
@@ -2965,11 +3005,12 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o_n = ar.add(b.lc.nodes.data(), b.lc.nodes.size() * 4);
 	const size_t o_c = ar.add(b.lc.dict.data(), b.lc.dict.size() * 4);
 	const size_t o_v = ar.add(b.dir.vals.data(), b.dir.vals.size() * 4);
-	size_t o6[5] = {0, 0, 0, 0, 0};
+	size_t o6[6] = {0, 0, 0, 0, 0, 0};
 	if (b.v6.any) {
 		o6[4] = ar.add(b.v6.bloom.data(), b.v6.bloom.size() * 4);
 		o6[0] = ar.add(b.v6.root.data(), b.v6.root.size() * 4);
 		o6[1] = ar.add(b.v6.masks.data(), b.v6.masks.size() * 4);
+		o6[5] = ar.add(b.v6.lens.data(), b.v6.lens.size() * 4);
 		o6[2] = ar.add(b.v6.vals.data(), b.v6.vals.size() * 4);
 		o6[3] = ar.add(b.v6.set.slots.data(), b.v6.set.slots.size() * sizeof(set16_slot));
 	}
@@ -2983,7 +3024,7 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		s.ipc6 = v6_lpm{at<uint2>(buf, o6[0]), at<uint32_t>(buf, o6[1]), at<uint32_t>(buf, o6[2]),
 				addr_set16{at<set16_slot>(buf, o6[3]), b.v6.set.mask, b.v6.set.max_probe},
 				(uint32_t)(b.v6.masks.size() / 4), at<uint32_t>(buf, o6[4]),
-				(uint32_t)b.v6.bloom.size() - 1u};
+				(uint32_t)b.v6.bloom.size() - 1u, at<uint4>(buf, o6[5])};
 	b.sum[G_IPC] = in.sum_ipc;
 	return 0;
 }
@@ -3380,7 +3421,9 @@ CGPU_EXPORT int cgpu_table_verify(cgpu_ctx *c)
 	HIP_OR_EIO(hipMemsetAsync(c->d_verify, 0, (G_N + 1) * 8, c->ustream));
 	for (int k = 0; k < G_N; k++)
 		if (e->bufs[k])
-			HIP_OR_EIO(launch_table_sum(e->bufs[k]->p, e->bufs[k]->bytes, c->d_verify + k, c->ustream));
+			for (auto &pt : e->bufs[k]->parts)
+				HIP_OR_EIO(launch_table_sum(e->bufs[k]->p, pt.first, pt.second, c->d_verify + k,
+							    c->ustream));
 	uint64_t got[G_N + 1];
 	HIP_OR_EIO(hipMemcpyAsync(got, c->d_verify, sizeof(got), hipMemcpyDeviceToHost, c->ustream));
 	HIP_OR_EIO(hipStreamSynchronize(c->ustream));

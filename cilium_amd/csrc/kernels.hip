@@ -241,6 +241,20 @@ __device__ __forceinline__ uint32_t set16_resolve(const addr_set16 &t, uint4 k0,
 	}
 }
 
+/* set16_resolve with only the bucket's first slot loaded (k0, m0): the
+ * second slot is read when the first holds another key */
+__device__ __forceinline__ uint32_t set16_resolve_first(const addr_set16 &t, uint4 k0, uint4 m0, uint32_t b,
+							uint4 key, uint32_t want)
+{
+	if (!(m0.x & 1u))
+		return 0;
+	if (m0.x == want && k0.x == key.x && k0.y == key.y && k0.z == key.z && k0.w == key.w)
+		return m0.y;
+	const uint4 *bk = reinterpret_cast<const uint4 *>(t.slots) + (size_t)b * 4u;
+	return set16_resolve(t, make_uint4(0, 0, 0, 0), make_uint4(1u | (want ^ 0xFF00u), 0, 0, 0), bk[2], bk[3], b,
+			     key, want);
+}
+
 /* The IPv6 address words as stored (network-order bytes, little-endian u32
  * view) -> host-order words (x = address bits 0..31), the prefix-key domain
  * of tables.h pfx6_hash */
@@ -264,6 +278,17 @@ __device__ __forceinline__ uint4 pfx6_key(uint4 w, uint32_t len)
 	const uint32_t m = 0xFFFFFFFFu << (32u - (len - 32u * k));
 	return make_uint4(k == 0 ? w.x & m : w.x, k < 1 ? 0u : (k == 1 ? w.y & m : w.y),
 			  k < 2 ? 0u : (k == 2 ? w.z & m : w.z), k < 3 ? 0u : w.w & m);
+}
+
+/* pfx6_hash of w's prefix key at length len (17..128), P = pfx6_sums(w) */
+__device__ __forceinline__ uint32_t pfx6_hash_at(uint4 w, uint3 P, uint32_t len)
+{
+	const uint32_t k = (len - 1u) >> 5;
+	const uint32_t wk = k == 0 ? w.x : (k == 1 ? w.y : (k == 2 ? w.z : w.w));
+	const uint32_t pk = k == 0 ? 0u : (k == 1 ? P.x : (k == 2 ? P.y : P.z));
+	const uint32_t ck = k == 0 ? PFX6_C0 : (k == 1 ? PFX6_C1 : (k == 2 ? PFX6_C2 : PFX6_C3));
+	const uint32_t mk = wk & (0xFFFFFFFFu << (32u - (len - 32u * k)));
+	return fmix32(pk + mk * ck + len * PFX6_CL);
 }
 
 /* Next candidate length of an IPv6 lookup, longest first: pops lengths off
@@ -1087,70 +1112,155 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 #define DIAG_LPM(b) (b)
 #endif
 
-/* v6_lookup for the Q tuples of a lane (k_classify_x4<.., V6>): root
- * gathers, then mask rows (the first nm rows from LDS), then rounds of one
- * bloom-admitted probe per unresolved tuple, Q bucket loads in flight.  The
- * filter leaves about one probe per tuple (the hit), so a round is usually
- * the last.  w: host-order address words; act[u] false: e[u] = 0 and no
- * memory access. */
+/* Octet-cooperative IPv6 longest-prefix lookup for the x4 schedule
+ * (k_classify_x4<.., V6>; tables.h v6_lpm).
+ * Phase 1, the bloom filter: a wave's tuples are taken 8 at a time; octet o
+ * of the wave (lanes 8o .. 8o + 7) filters one tuple, lane 8o + j its j-th
+ * longest candidate length (the root row's `lens` list): one hash and one
+ * LDS filter test per lane per step, instead of each lane looping over every
+ * length present under its /16 (which ran as long as the wave's slowest
+ * lane, round 2: 1.77 G VALU per 64M tuples).  The admitted lengths return to
+ * the tuple's own lane as an 8-bit mask (bit j: the j-th longest).
+ * Phase 2, per lane: the two longest admitted lengths of every tuple are
+ * probed with all their bucket loads in flight together, the longer hit
+ * wins; a tuple left unresolved by filter false positives takes the next
+ * two.  A row with more than 8 lengths continues below its 8th longest on
+ * the lane's own serial loop (v6_next) when the first 8 miss.
+ * Every lane of the wave must call this together (the octets work for other
+ * lanes' tuples); act[u] false only excludes the lane's own tuple (e = 0). */
 template <int Q>
-__device__ __forceinline__ void v6_lookup_q(const v6_lpm &t, const uint32_t *bloom, const uint4 *lmasks,
-					    uint32_t nm, const uint4 (&w)[Q], const bool (&act)[Q], uint32_t (&e)[Q])
+__device__ __forceinline__ void v6_lookup_coop(const v6_lpm &t, const uint32_t *bloom, const uint4 *llens,
+					       uint32_t nl, const uint4 (&w)[Q], const bool (&act)[Q],
+					       uint32_t (&e)[Q])
 {
+	const uint32_t lane = __lane_id();
+	const uint32_t oct = lane >> 3, j = lane & 7u;
 	uint2 r[Q];
+	uint4 lr[Q];
+	uint32_t pass[Q], res[Q];
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		r[u] = make_uint2(0, 0);
 		if (act[u] && t.root)
 			r[u] = t.root[w[u].x >> 16];
 	}
-	uint64_t hi[Q], lo[Q];
-	uint32_t res[Q];
-	uint3 P[Q];
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
-		uint4 m = make_uint4(0, 0, 0, 0);
+		lr[u] = make_uint4(0, 0, 0, 0);
 		if (r[u].x)
-			m = r[u].x < nm ? lmasks[r[u].x] : reinterpret_cast<const uint4 *>(t.masks)[r[u].x];
-		hi[u] = ((uint64_t)m.w << 32) | m.z;
-		lo[u] = ((uint64_t)m.y << 32) | m.x;
+			lr[u] = r[u].x < nl ? llens[r[u].x] : t.lens[r[u].x];
+		pass[u] = 0;
 		res[u] = 0;
-		P[u] = pfx6_sums(w[u]);
 	}
+	/* phase 1 */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+#pragma unroll
+		for (uint32_t g = 0; g < 8; g++) {
+			const int owner = (int)(8u * g + oct);
+			const uint32_t cnt = __shfl(lr[u].z, owner, 64);
+			/* (a shuffle reads the SOURCE lane's operand: both words travel) */
+			const uint32_t lx = __shfl(lr[u].x, owner, 64), ly = __shfl(lr[u].y, owner, 64);
+			const uint32_t len = j < cnt ? ((j < 4 ? lx : ly) >> (8u * (j & 3u))) & 0xFFu : 0u;
+			const uint4 ow = make_uint4(__shfl(w[u].x, owner, 64), __shfl(w[u].y, owner, 64),
+						    __shfl(w[u].z, owner, 64), __shfl(w[u].w, owner, 64));
+			bool ok = false;
+			if (len) {
+				const uint32_t k = (len - 1u) >> 5;
+				const uint32_t p0 = ow.x * PFX6_C0, p1 = p0 + ow.y * PFX6_C1, p2 = p1 + ow.z * PFX6_C2;
+				const uint32_t wk = k == 0 ? ow.x : (k == 1 ? ow.y : (k == 2 ? ow.z : ow.w));
+				const uint32_t pk = k == 0 ? 0u : (k == 1 ? p0 : (k == 2 ? p1 : p2));
+				const uint32_t ck = k == 0 ? PFX6_C0 : (k == 1 ? PFX6_C1 : (k == 2 ? PFX6_C2 : PFX6_C3));
+				const uint32_t mk = wk & (0xFFFFFFFFu << (32u - (len - 32u * k)));
+				const uint32_t h = fmix32(pk + mk * ck + len * PFX6_CL);
+				const uint32_t bits = v6_bloom_bits(h);
+				ok = (bloom[v6_bloom_word(h, t.bloom_mask)] & bits) == bits;
+			}
+			const uint64_t bal = __ballot(ok);
+			/* lane 8g + o' owns the tuple octet o' filtered in this step */
+			const uint32_t mine = (uint32_t)(bal >> (8u * j)) & 0xFFu;
+			if (oct == g)
+				pass[u] = mine;
+		}
+	}
+	/* phase 2 */
 	for (;;) {
-		uint32_t L[Q], bi[Q];
+		uint32_t L0[Q], L1[Q], b0[Q], b1[Q];
 		bool more = false;
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			L[u] = 0;
-			bi[u] = 0;
-			if (!res[u])
-				L[u] = v6_next(t, bloom, w[u], P[u], hi[u], lo[u], bi[u]);
-			more |= L[u] != 0;
+			L0[u] = L1[u] = 0;
+			b0[u] = b1[u] = 0;
+			if (res[u] || !pass[u])
+				continue;
+			const uint64_t lw = ((uint64_t)lr[u].y << 32) | lr[u].x;
+			const uint32_t s0 = (uint32_t)__ffs(pass[u]) - 1u;
+			pass[u] &= pass[u] - 1u;
+			L0[u] = (uint32_t)(lw >> (8u * s0)) & 0xFFu;
+			if (pass[u]) {
+				const uint32_t s1 = (uint32_t)__ffs(pass[u]) - 1u;
+				pass[u] &= pass[u] - 1u;
+				L1[u] = (uint32_t)(lw >> (8u * s1)) & 0xFFu;
+			}
+			const uint3 P = pfx6_sums(w[u]);
+			b0[u] = pfx6_hash_at(w[u], P, L0[u]) & t.set.bucket_mask;
+			if (L1[u])
+				b1[u] = pfx6_hash_at(w[u], P, L1[u]) & t.set.bucket_mask;
+			more = true;
 		}
 		if (!more)
 			break;
-		uint4 k0[Q], m0[Q], k1[Q], m1[Q];
+		/* the first slot of both buckets of every tuple in flight together */
+		uint4 k0[Q], m0[Q], n0[Q], q0[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[u] * 4u;
-			k0[u] = L[u] ? p[0] : make_uint4(0, 0, 0, 0);
-			m0[u] = L[u] ? p[1] : make_uint4(0, 0, 0, 0);
-			k1[u] = L[u] ? p[2] : make_uint4(0, 0, 0, 0);
-			m1[u] = L[u] ? p[3] : make_uint4(0, 0, 0, 0);
+			const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)b0[u] * 4u;
+			const uint4 *q = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)b1[u] * 4u;
+			k0[u] = L0[u] ? p[0] : make_uint4(0, 0, 0, 0);
+			m0[u] = L0[u] ? p[1] : make_uint4(0, 0, 0, 0);
+			n0[u] = L1[u] ? q[0] : make_uint4(0, 0, 0, 0);
+			q0[u] = L1[u] ? q[1] : make_uint4(0, 0, 0, 0);
 		}
 #pragma unroll
-		for (int u = 0; u < Q; u++)
-			if (L[u])
-				res[u] = set16_resolve(t.set, k0[u], m0[u], k1[u], m1[u], bi[u], pfx6_key(w[u], L[u]),
-						       1u | (L[u] << 8));
+		for (int u = 0; u < Q; u++) {
+			if (L0[u])
+				res[u] = set16_resolve_first(t.set, k0[u], m0[u], b0[u], pfx6_key(w[u], L0[u]),
+							     1u | (L0[u] << 8));
+			if (!res[u] && L1[u])
+				res[u] = set16_resolve_first(t.set, n0[u], q0[u], b1[u], pfx6_key(w[u], L1[u]),
+							     1u | (L1[u] << 8));
+		}
+	}
+	/* rows with more than 8 lengths: the rest, longest first, one at a time */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (res[u] || lr[u].z <= 8u)
+			continue;
+		const uint32_t l7 = (lr[u].y >> 24) & 0xFFu; /* the 8th longest: continue below it */
+		const uint4 m = reinterpret_cast<const uint4 *>(t.masks)[r[u].x];
+		uint64_t hi = ((uint64_t)m.w << 32) | m.z, lo = ((uint64_t)m.y << 32) | m.x;
+		const uint32_t below = l7 - 17u; /* keep bits < below */
+		if (below >= 64u) {
+			hi &= below - 64u >= 64u ? ~0ull : ((1ull << (below - 64u)) - 1ull);
+		} else {
+			hi = 0;
+			lo &= (1ull << below) - 1ull;
+		}
+		const uint3 P = pfx6_sums(w[u]);
+		while (!res[u]) {
+			uint32_t bk = 0;
+			const uint32_t L = v6_next(t, bloom, w[u], P, hi, lo, bk);
+			if (!L)
+				break;
+			const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bk * 4u;
+			res[u] = set16_resolve(t.set, p[0], p[1], p[2], p[3], bk, pfx6_key(w[u], L), 1u | (L << 8));
+		}
 	}
 #pragma unroll
 	for (int u = 0; u < Q; u++)
-		e[u] = res[u] ? res[u] : r[u].y;
+		e[u] = act[u] ? (res[u] ? res[u] : r[u].y) : 0u;
 }
 
-/* mask rows of the v6 ipcache staged in LDS by k_classify_x4<.., V6> */
 #define V6_LDS_MASK_ROWS 256u
 
 /*
@@ -1211,16 +1321,21 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		for (uint32_t k = threadIdx.x; k < nbw; k += NT)
 			ldict[k] = s.ipc6.bloom[k];
 		for (uint32_t k = threadIdx.x; k < nm; k += NT)
-			lmasks[k] = reinterpret_cast<const uint4 *>(s.ipc6.masks)[k];
+			lmasks[k] = s.ipc6.lens[k]; /* the rows' length lists (v6_lookup_coop) */
 	} else {
 		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
 			ldict[k] = s.ipc4c.dict[k];
 	}
 	__syncthreads();
 
-	for (uint64_t g = t0; g * Q < a.n; g += T) {
-		const uint64_t i0 = g * Q;
-		const bool full = i0 + Q <= a.n;
+	/* v6: every lane of a wave runs every iteration (v6_lookup_coop works
+	 * across lanes); a lane past the end runs idle (no F_OK tuple) */
+	for (uint64_t g = t0;; g += T) {
+		const bool live = g * Q < a.n;
+		if (V6 ? !__any(live) : !live)
+			break;
+		const uint64_t i0 = live ? g * Q : 0;
+		const bool full = live && i0 + Q <= a.n;
 		/* decode: hi4 = the policy key's upper word {dport, proto, egress}
 		 * (policy.h:61-64), fw = flag word, ad = the looked-up address */
 		/* QA: the vector-load branches below are written for Q = 4; arrays
@@ -1300,7 +1415,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				for (int u = 0; u < Q; u++) {
 					const uint64_t i = i0 + u < a.n ? i0 + u : i0;
 					uint4 raw = ld_x4<NTL>(static_cast<const uint4 *>((fl[u] & 1u) ? a.daddr : a.saddr) + i);
-					if (LB && (fl[u] & 1u) && i0 + u < a.n) {
+					if (LB && live && (fl[u] & 1u) && i0 + u < a.n) {
 						/* egress service step first (bpf_lxc.c:117-149) */
 						uint32_t h;
 						if (a.hash) {
@@ -1367,7 +1482,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				const bool gated = s.ct_proto_gate && proto[u] != (V6 ? 58u : 1u) && proto[u] != 6u &&
 						   proto[u] != 17u;
 				/* IPv6 passes is_fragment = false (bpf_lxc.c:787-789) */
-				fw[u] = (i0 + u < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) | lbf[u] |
+				fw[u] = (live && i0 + u < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) | lbf[u] |
 					(!V6 && !eg && ((fl[u] >> 1) & 1u) ? F_FRAG : 0u);
 				ad[u] = eg ? da[u] : sa[u];
 				hi4[u] = dport[u] | (proto[u] << 16) | (eg ? (1u << 24) : 0u);
@@ -1380,7 +1495,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 			for (int u = 0; u < Q; u++)
 				act[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK;
-			v6_lookup_q<Q>(s.ipc6, ldict, lmasks, nm, ad6, act, e);
+			v6_lookup_coop<Q>(s.ipc6, ldict, lmasks, nm, ad6, act, e);
 		} else {
 			/* v4: the /16's inline node (x16), then the compressed LPM */
 			{
@@ -2389,13 +2504,21 @@ __global__ void k_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 	}
 }
 
-/* device side of the table verification sum (tables.h table_sum_word) */
-__global__ __launch_bounds__(256) void k_table_sum(const uint64_t *p, uint64_t nwords, uint64_t *out)
+/* device side of the table verification sum (tables.h table_sum_word) over
+ * one part: `bytes` bytes from word w0 of the buffer (a trailing partial
+ * word counts its bytes only) */
+__global__ __launch_bounds__(256) void k_table_sum(const uint64_t *buf, uint64_t w0, uint64_t bytes, uint64_t *out)
 {
 	uint64_t acc = 0;
+	const uint64_t nw = (bytes + 7u) / 8u;
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
-	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < nwords; i += stride)
-		acc += table_sum_word(__builtin_nontemporal_load(p + i), i);
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < nw; i += stride) {
+		uint64_t w = __builtin_nontemporal_load(buf + w0 + i);
+		const uint64_t rem = bytes - 8u * i;
+		if (rem < 8u)
+			w &= (1ull << (8u * rem)) - 1ull;
+		acc += table_sum_word(w, w0 + i);
+	}
 	acc = wave_sum(acc);
 	if ((threadIdx.x & 63) == 0 && acc)
 		atomicAdd((unsigned long long *)out, (unsigned long long)acc);
@@ -2668,11 +2791,14 @@ hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, 
 	return hipGetLastError();
 }
 
-hipError_t launch_table_sum(const void *buf, size_t bytes, uint64_t *out, hipStream_t st)
+hipError_t launch_table_sum(const void *buf, size_t off, size_t bytes, uint64_t *out, hipStream_t st)
 {
-	const uint64_t nw = bytes / 8u;
+	const uint64_t nw = (bytes + 7u) / 8u;
+	if (!nw)
+		return hipSuccess;
 	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nw + 255) / 256, 4096));
-	hipLaunchKernelGGL(k_table_sum, dim3(g), dim3(256), 0, st, static_cast<const uint64_t *>(buf), nw, out);
+	hipLaunchKernelGGL(k_table_sum, dim3(g), dim3(256), 0, st, static_cast<const uint64_t *>(buf), off / 8u,
+			   (uint64_t)bytes, out);
 	return hipGetLastError();
 }
 

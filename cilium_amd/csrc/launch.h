@@ -154,8 +154,9 @@ struct l3_launch {
 
 hipError_t launch_l3_compile(const l3_launch &L, hipStream_t st);
 
-/* *out += sum of table_sum_word over the bytes / 8 words of buf */
-hipError_t launch_table_sum(const void *buf, size_t bytes, uint64_t *out, hipStream_t st);
+/* *out += sum of table_sum_word over `bytes` bytes of buf from byte `off`
+ * (a multiple of 8) */
+hipError_t launch_table_sum(const void *buf, size_t off, size_t bytes, uint64_t *out, hipStream_t st);
 
 /* totals[i] += delta[i]; delta[i] = 0 over n u64 words */
 hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st);

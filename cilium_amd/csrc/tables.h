@@ -239,6 +239,9 @@ typedef struct v6_lpm {
 	 * false negatives, so results never depend on it. */
 	const uint32_t *bloom;
 	uint32_t bloom_mask;   /* n_words - 1 (n_words a power of two <= 2^14) */
+	/* per mask row, its lengths longest first: x, y = the first 8 as bytes
+	 * (byte j of x | y << 32 = the j-th longest), z = how many the row has */
+	const uint4 *lens;
 } v6_lpm;
 
 #define V6_BLOOM_MAX_WORDS 16384u /* 64 KiB: staged in LDS by the x4 kernel */
@@ -489,18 +492,14 @@ CT_HD uint32_t ct_group(uint32_t a, uint32_t b)
 }
 
 /* Table verification sum (SURVEY §5 failure detection): over the 8-byte
- * words of an uploaded group buffer, sum of mix(word, index) for the nonzero
- * words (the gaps between arena parts are zeroed).  The host computes it over
- * its image before the upload, the device over the buffer it holds. */
+ * words of every part of an uploaded group buffer, sum of word x an odd
+ * multiplier that depends on the word's index in the buffer (a changed word
+ * always changes the sum: odd multipliers are invertible mod 2^64).  The
+ * host computes it over its image before the upload, the device over the
+ * buffer it holds. */
 CT_HD uint64_t table_sum_word(uint64_t w, uint64_t i)
 {
-	if (!w)
-		return 0;
-	uint64_t x = w * 0x9E3779B97F4A7C15ull + (i + 1u) * 0xC2B2AE3D27D4EB4Full;
-	x ^= x >> 31;
-	x *= 0xBF58476D1CE4E5B9ull;
-	x ^= x >> 29;
-	return x;
+	return w * ((i * 0x9E3779B97F4A7C15ull) | 1ull);
 }
 
 /* counters: u64 {packets, bytes} per policy slot, then metrics */
