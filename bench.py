@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--hot-slots", type=int, default=0,
                     help="cgpu_config.hot_counter_slots (LDS counter slots; 0 = library default)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-rebalance", action="store_true",
+                    help="keep the class-based counter slots (no cgpu_counters_rebalance after warmup)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/*), if present")
     args = ap.parse_args()
@@ -279,6 +281,14 @@ def main():
         e.counter_fold(stream)
 
     for _ in range(args.warmup):
+        step()
+    # the control plane's periodic slot rebalance (cgpu_counters_rebalance):
+    # after warmup traffic the most-hit keys own the LDS counter slots; every
+    # rank holds the same folded totals, so every rank picks the same layout
+    moved = None
+    if not args.no_rebalance and not pf6 and not ct and args.warmup:
+        torch.cuda.synchronize()
+        moved = e.counters_rebalance()
         step()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -455,6 +465,8 @@ def main():
                 "stream_tuples_per_step": world * n, "stream_tuples_timed": world * n * args.steps,
                 "counter_reduce": ("cgpu_counters_allreduce (RCCL u64 SUM)" if world > 1 else "none (1 rank)"),
                 "allreduce_check_vs_torch_sum": allreduce_ok,
+                "counter_slots": ("class-based" if moved is None else
+                                  f"popularity-rebalanced after warmup ({moved} keys moved)"),
                 "probes_per_tuple": round(probes_per, 4), "b_alg_per_tuple": round(b_alg, 2),
                 "parity_vs_oracle": parity}
         if pf6:

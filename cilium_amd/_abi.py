@@ -168,6 +168,7 @@ PROTOS = {
     "cgpu_metrics_read": (i32, [vp, vp]),
     "cgpu_counters_reset": (i32, [vp]),
     "cgpu_stream_release": (i32, [vp, vp]),
+    "cgpu_counters_rebalance": (i32, [vp, C.POINTER(u64)]),
     "cgpu_comm_id_create": (i32, [vp]),
     "cgpu_comm_init": (i32, [vp, vp, i32, i32]),
     "cgpu_counters_allreduce": (i32, [vp, vp]),

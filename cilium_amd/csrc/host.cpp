@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -3278,6 +3279,8 @@ static int commit_inits(cgpu_ctx *c, const CommitIn &in)
 
 } // namespace
 
+static int commit_locked(cgpu_ctx *c, uint64_t *epoch_out);
+
 CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 {
 	if (!c)
@@ -3285,6 +3288,12 @@ CGPU_EXPORT int cgpu_commit(cgpu_ctx *c, uint64_t *epoch_out)
 	if (c->device < 0)
 		return fail(-ENODEV, "context has no device");
 	std::lock_guard<std::mutex> cg(c->commit_mu);
+	return commit_locked(c, epoch_out);
+}
+
+/* the commit proper; caller holds commit_mu */
+static int commit_locked(cgpu_ctx *c, uint64_t *epoch_out)
+{
 	CommitIn in;
 	{
 		std::lock_guard<std::mutex> g(c->mu);
@@ -3399,6 +3408,152 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
 		return fail(-ENOENT, "nothing committed");
 	*sum = c->checksum;
 	return 0;
+}
+
+/* Popularity-ordered counter slots.  Counter slots [0, hot_cap) accumulate
+ * in LDS per workgroup (one flush per workgroup), the rest cost one global
+ * atomic per hit that the workgroup's small LDS cache misses; slots are first
+ * handed out by key class (L3-only / identity-wildcard keys hot).  This call
+ * re-assigns them by measured traffic: the hot_cap keys with the most
+ * packets so far take the hot slots (ties: hot class first, then endpoint and
+ * key order, so replicas with the same folded totals choose alike), moved
+ * keys carry their counters with them, and the policy tables are republished
+ * (a commit).  Control-plane call: it synchronizes the device, folds the
+ * delta buffer, and needs every map change committed (else -EBUSY); no batch
+ * may be launched on the context while it runs. */
+CGPU_EXPORT int cgpu_counters_rebalance(cgpu_ctx *c, uint64_t *moved_out)
+{
+	if (!c)
+		return fail(-EINVAL, "null argument");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device");
+	std::lock_guard<std::mutex> cg(c->commit_mu);
+	uint64_t moved = 0;
+	{
+		std::lock_guard<std::mutex> g(c->mu);
+		if ((c->dirty & (1u << G_POL)) || !c->slot_inits.empty())
+			return fail(-EBUSY, "uncommitted policy changes: commit first");
+		const size_t words = (size_t)2 * c->n_ctr_slots + CGPU_METRICS_WORDS;
+		uint64_t *delta;
+		{
+			std::lock_guard<std::mutex> pg(c->pk_mu);
+			delta = c->d_delta;
+		}
+		HIP_OR_EIO(hipSetDevice(c->device));
+		HIP_OR_EIO(hipDeviceSynchronize());
+		HIP_OR_EIO(launch_fold(c->d_totals, delta, words, c->ustream));
+		HIP_OR_EIO(hipStreamSynchronize(c->ustream));
+		std::vector<uint64_t> tot(words);
+		HIP_OR_EIO(hipMemcpy(tot.data(), c->d_totals, words * 8, hipMemcpyDeviceToHost));
+		struct K {
+			uint64_t pk;
+			bool cls;
+			uint32_t ep;
+			uint64_t key;
+			PolEntry *e;
+		};
+		std::vector<K> ks;
+		ks.reserve(c->pol_total);
+		for (uint32_t ep = 0; ep < c->pol.size(); ep++)
+			for (auto &kv : c->pol[ep]) {
+				cgpu_policy_key pkey;
+				memcpy(&pkey, &kv.first, 8);
+				const bool cls = (pkey.dport == 0 && pkey.protocol == 0) || pkey.sec_label == 0;
+				ks.push_back(K{tot[2u * kv.second.slot], cls, ep, kv.first, &kv.second});
+			}
+		std::sort(ks.begin(), ks.end(), [](const K &a, const K &b) {
+			if (a.pk != b.pk)
+				return a.pk > b.pk;
+			if (a.cls != b.cls)
+				return a.cls;
+			if (a.ep != b.ep)
+				return a.ep < b.ep;
+			return a.key < b.key;
+		});
+		const size_t H = std::min<size_t>(c->hot_cap, ks.size());
+		std::vector<uint8_t> used(c->n_ctr_slots, 0);
+		for (auto &k : ks)
+			used[k.e->slot] = 1;
+		/* target keys already hot stay; the others' hot slots are released */
+		std::vector<uint8_t> keep(c->hot_cap, 0);
+		for (size_t i = 0; i < H; i++)
+			if (ks[i].e->slot < c->hot_cap)
+				keep[ks[i].e->slot] = 1;
+		std::vector<uint64_t> nt(tot.begin(), tot.begin() + 2 * (size_t)c->n_ctr_slots);
+		std::vector<uint32_t> hot_free, cold_free;
+		for (uint32_t sl = c->hot_cap; sl-- > 0;)
+			if (!keep[sl])
+				hot_free.push_back(sl); /* lowest last: handed out first */
+		uint32_t next_cold = c->next_cold;
+		for (uint32_t sl = c->n_ctr_slots; sl-- > c->hot_cap;)
+			if (sl < next_cold && !used[sl])
+				cold_free.push_back(sl);
+		auto move = [&](PolEntry *e, uint32_t to) {
+			nt[2u * to] = tot[2u * e->slot];
+			nt[2u * to + 1u] = tot[2u * e->slot + 1u];
+			e->slot = to;
+			moved++;
+		};
+		/* evict non-target keys from hot slots first (their slots are in hot_free) */
+		for (size_t i = H; i < ks.size(); i++) {
+			PolEntry *e = ks[i].e;
+			if (e->slot >= c->hot_cap)
+				continue;
+			uint32_t to;
+			if (!cold_free.empty()) {
+				to = cold_free.back();
+				cold_free.pop_back();
+			} else if (next_cold < c->n_ctr_slots) {
+				to = next_cold++;
+			} else {
+				return fail(-E2BIG, "no cold counter slot left to rebalance into");
+			}
+			nt[2u * e->slot] = nt[2u * e->slot + 1u] = 0;
+			move(e, to);
+		}
+		for (size_t i = 0; i < H; i++) {
+			PolEntry *e = ks[i].e;
+			if (e->slot < c->hot_cap)
+				continue;
+			const uint32_t from = e->slot;
+			const uint32_t to = hot_free.back();
+			hot_free.pop_back();
+			move(e, to);
+			nt[2u * from] = nt[2u * from + 1u] = 0;
+			cold_free.push_back(from);
+		}
+		/* counters follow their keys; the layout sum is recomputed */
+		HIP_OR_EIO(hipMemcpy(c->d_totals, nt.data(), nt.size() * 8, hipMemcpyHostToDevice));
+		c->sum_slots = 0;
+		for (auto &k : ks)
+			c->sum_slots += slot_hash(k.ep, k.key, k.e->slot);
+		/* hot slots in use end at next_hot; unused ones below it are free */
+		std::vector<uint8_t> hot_used(c->hot_cap, 0);
+		for (auto &k : ks)
+			if (k.e->slot < c->hot_cap)
+				hot_used[k.e->slot] = 1;
+		uint32_t nh = 0;
+		for (uint32_t sl = 0; sl < c->hot_cap; sl++)
+			if (hot_used[sl])
+				nh = sl + 1u;
+		c->free_hot.clear();
+		for (uint32_t sl = nh; sl-- > 0;)
+			if (!hot_used[sl])
+				c->free_hot.push_back(sl);
+		std::sort(cold_free.begin(), cold_free.end(), std::greater<uint32_t>());
+		c->free_cold.assign(cold_free.begin(), cold_free.end());
+		c->quarantine.clear(); /* the device is idle: no snapshot counts any more */
+		c->next_hot = nh;
+		c->next_cold = next_cold;
+		if (moved) {
+			c->dirty |= 1u << G_POL;
+			c->pol_full = true;
+			c->pol_changes.clear();
+		}
+	}
+	if (moved_out)
+		*moved_out = moved;
+	return moved ? commit_locked(c, nullptr) : 0;
 }
 
 /* SURVEY §5 failure detection: recompute every group buffer of the

@@ -2576,20 +2576,30 @@ static unsigned resident_blocks(const void *kern, int NT, size_t lds)
  * metrics block and some slack */
 #define X4_LDS_BUDGET (156u * 1024u)
 
+/* The snapshot a launch sees with at most `max_hot` LDS counter slots: hits
+ * on slots past it take the kernels' cold path (the counts are the same,
+ * only where they accumulate changes), so LDS never overflows whatever
+ * hot_counter_slots is. */
+static cgpu_snapshot with_lds_hot(const cgpu_snapshot &s, size_t max_hot)
+{
+	cgpu_snapshot r = s;
+	r.hot_slots = (uint32_t)std::min<size_t>(s.hot_slots, max_hot);
+	return r;
+}
+
 template <bool LB, bool V6>
-static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream_t st)
+static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024;
 	/* LDS: hot counters + the ipcache leaf dictionary (v4) / bloom filter
-	 * and mask rows (v6) */
-	size_t lds = (size_t)s.hot_slots * 8u;
-	if (V6)
-		lds += s.ipc6.root ? (size_t)(s.ipc6.bloom_mask + 1u) * 4u +
-					     (size_t)std::min(s.ipc6.n_masks, V6_LDS_MASK_ROWS) * 16u
-				   : 0u;
-	else
-		lds += (size_t)s.ipc4c.n_dict * 4u;
-	lds = (lds + 7u) & ~(size_t)7u;
+	 * and length rows (v6) */
+	size_t fixed = V6 ? (s0.ipc6.root ? (size_t)(s0.ipc6.bloom_mask + 1u) * 4u +
+						  (size_t)std::min(s0.ipc6.n_masks, V6_LDS_MASK_ROWS) * 16u
+					  : 0u)
+			  : (size_t)s0.ipc4c.n_dict * 4u;
+	fixed = (fixed + 7u) & ~(size_t)7u;
+	const cgpu_snapshot s = with_lds_hot(s0, fixed < X4_LDS_BUDGET ? (X4_LDS_BUDGET - fixed) / 8u : 0u);
+	size_t lds = (size_t)s.hot_slots * 8u + fixed;
 	/* the cold-slot cache takes the LDS one workgroup per CU leaves free
 	 * (the resident grid runs one 1024-thread workgroup per CU) */
 	uint32_t cc_n = 0;
@@ -2644,20 +2654,21 @@ static hipError_t launch_x4(const cgpu_snapshot &s, const cls_args &a, hipStream
  *   CGPU_SCHED_PER_LANE: one tuple per lane, LDS hot counters
  *   CGPU_SCHED_GLOBAL_CTR: global atomics for every hit, 256-thread workgroups */
 template <int V6>
-static hipError_t launch_classify(const cgpu_snapshot &s, cls_args a, hipStream_t st)
+static hipError_t launch_classify(const cgpu_snapshot &s0, cls_args a, hipStream_t st)
 {
-	if (s.schedule & CGPU_SCHED_GLOBAL_CTR) {
-		hipLaunchKernelGGL((k_classify<V6, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	if (s0.schedule & CGPU_SCHED_GLOBAL_CTR) {
+		hipLaunchKernelGGL((k_classify<V6, 0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s0, a);
 		return hipGetLastError();
 	}
-	if (!(s.schedule & CGPU_SCHED_PER_LANE) && a.pk && x4_aligned(a)) {
+	if (!(s0.schedule & CGPU_SCHED_PER_LANE) && a.pk && x4_aligned(a)) {
 		if (V6)
-			return a.lb ? launch_x4<true, true>(s, a, st) : launch_x4<false, true>(s, a, st);
-		return a.lb ? launch_x4<true, false>(s, a, st) : launch_x4<false, false>(s, a, st);
+			return a.lb ? launch_x4<true, true>(s0, a, st) : launch_x4<false, true>(s0, a, st);
+		return a.lb ? launch_x4<true, false>(s0, a, st) : launch_x4<false, false>(s0, a, st);
 	}
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
 	constexpr int NT = 1024;
+	const cgpu_snapshot s = with_lds_hot(s0, X4_LDS_BUDGET / 8u);
 	const size_t lds = (size_t)s.hot_slots * 8u;
 	const uint64_t cap = 2ull * 256ull;
 	const uint64_t per_launch = cap * (1ull << 22); /* k_classify<.., 1, ..> never touches pk */
@@ -2760,9 +2771,10 @@ hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hip
 
 /* as the k_classify<.., CTR = 1> launcher: 1024-thread workgroups, <= 2 per
  * CU (LDS), at most 2^22 frames per workgroup (packed LDS counters) */
-hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, hipStream_t st)
+hipError_t launch_classify_frames(const cgpu_snapshot &s0, const frames_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024;
+	const cgpu_snapshot s = with_lds_hot(s0, X4_LDS_BUDGET / 8u);
 	const size_t lds = (size_t)s.hot_slots * 8u;
 	const uint64_t cap = 2ull * 256ull;
 	/* cold-slot hits go to the packed per-stream accumulator pk, exact for
@@ -3889,8 +3901,9 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	constexpr int NF = 1024;
 	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((L.n + NF - 1) / NF, 512),
 					       (L.n >> 22) + 1);
-	hipLaunchKernelGGL((k_ct_finish<NF, K>), dim3((unsigned)gf), dim3(NF), (size_t)s.hot_slots * 8u, st,
-			   s, a);
+	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
+	hipLaunchKernelGGL((k_ct_finish<NF, K>), dim3((unsigned)gf), dim3(NF), (size_t)sf.hot_slots * 8u, st,
+			   sf, a);
 	return hipGetLastError();
 }
 

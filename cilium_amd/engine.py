@@ -626,6 +626,13 @@ class Engine:
               "cgpu_metrics_read")
         return out
 
+    def counters_rebalance(self) -> int:
+        """cgpu_counters_rebalance: hot (LDS) counter slots to the most-hit
+        keys; returns how many keys moved."""
+        m = C.c_uint64()
+        check(self.L.cgpu_counters_rebalance(self.h, C.byref(m)), "cgpu_counters_rebalance")
+        return m.value
+
     def stream_release(self, stream) -> None:
         """cgpu_stream_release: free the stream's packed counter buffer."""
         check(self.L.cgpu_stream_release(self.h, _stream(stream)), "cgpu_stream_release")

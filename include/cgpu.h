@@ -930,6 +930,17 @@ int cgpu_counter_fold(cgpu_ctx *ctx, void *stream);
 /* out: [256][4][2] u64 {count, bytes} (folds and synchronizes first) */
 int cgpu_metrics_read(cgpu_ctx *ctx, uint64_t *out);
 int cgpu_counters_reset(cgpu_ctx *ctx);
+/* Popularity-ordered counter slots: hot slots [0, hot_counter_slots)
+ * accumulate in LDS (one flush per workgroup), the others cost a global
+ * atomic per hit.  Slots start out by key class (L3-only / identity-wildcard
+ * keys hot); this re-assigns them by measured traffic: the keys with the most
+ * packets so far take the hot slots (ties: class, endpoint, key -- replicas
+ * with the same folded totals choose alike), counters move with their keys,
+ * and the policy tables are republished.  A control-plane call: it
+ * synchronizes the device and folds the delta buffer; every map change must be
+ * committed (else -EBUSY) and no batch may run on the context meanwhile.
+ * *moved_out (optional) = keys whose slot changed. */
+int cgpu_counters_rebalance(cgpu_ctx *ctx, uint64_t *moved_out);
 /* Classify launches keep a packed counter accumulator of 8 B per policy
  * slot (policy_max_total x 8 B of HBM) for each stream they ran on, at most
  * 16 of them; a 17th stream recycles the least recently used one after that

@@ -462,3 +462,64 @@ def test_mirror_save_restore_resumes(torch_cuda, tmp_path):
         np.testing.assert_array_equal(a, b)
     e.close()
     f.close()
+
+
+def test_counters_rebalance_popularity(torch_cuda):
+    """cgpu_counters_rebalance: after traffic, the most-hit keys take the hot
+    (LDS) counter slots and carry their counters; every per-entry counter and
+    the metrics stay equal to the restatement's across the move, further
+    batches and later map changes; a second rebalance on the same totals
+    moves nothing; replicas with the same totals choose the same layout."""
+    from oracle import Oracle
+    torch = torch_cuda
+    T = synth.make_tables(**synth.CONFIGS["cpu"])
+    t1 = synth.make_tuples(T, 1 << 20)
+    t2 = synth.make_tuples(T, 1 << 20, gpu_id=5)
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    es = []
+    for _ in range(2):
+        e = _engine(**T.engine_config(), hot_counter_slots=2048)
+        synth.load_engine(e, T)
+        e.commit()
+        es.append(e)
+    e, r = es
+    for x in es:
+        x.classify_v4(synth.to_device(t1), stage=False)
+    o.classify_v4(t1, nthreads=16)
+    lay0 = e.counter_layout_checksum()
+    moved = e.counters_rebalance()
+    assert moved > 0 and r.counters_rebalance() == moved
+    assert e.counter_layout_checksum() != lay0
+    assert e.counter_layout_checksum() == r.counter_layout_checksum()
+    assert e.counters_rebalance() == 0  # stable on the same totals
+
+    def same():
+        torch.cuda.synchronize()
+        got = e.policy_counters(T.pol_ep, T.pol_keys)
+        for i in range(len(T.pol_keys)):
+            _, raw = o.policy_lookup(int(T.pol_ep[i]), T.pol_keys[i])
+            exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+            assert (int(got[i, 0]), int(got[i, 1])) == (int(exp["packets"]), int(exp["bytes"])), i
+        np.testing.assert_array_equal(e.metrics(), o.metrics())
+    same()
+    out = e.classify_v4(synth.to_device(t2))
+    v0, i0, s0, _ = o.classify_v4(t2, nthreads=16)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["verdict"].cpu().numpy(), v0)
+    same()
+    # map changes after the move: deletes, re-adds, new keys
+    for i in range(0, 400, 7):
+        k, ep = T.pol_keys[i], int(T.pol_ep[i])
+        assert e.policy_delete(ep, k) == 0 and o.policy_delete(ep, k) == 0
+    for i in range(0, 400, 14):
+        k, en, ep = T.pol_keys[i], T.pol_entries[i], int(T.pol_ep[i])
+        assert e.policy_update(ep, k, en) == 0 and o.policy_update(ep, k, en) == 0
+    e.commit()
+    out = e.classify_v4(synth.to_device(t1))
+    v0, i0, s0, _ = o.classify_v4(t1, nthreads=16)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["verdict"].cpu().numpy(), v0)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    for x in es:
+        x.close()

@@ -89,10 +89,13 @@ def test_config2_fullsize(torch_cuda, cfg2):
 
 def test_config2_two_context_shard_merge(torch_cuda, cfg2):
     """SURVEY §8e on one device: two engine contexts over the two flow-hash
-    shards, delta buffers bound, summed as int64 exactly as the RCCL SUM of
-    bench.py / cgpu_counters_allreduce does, then counter_fold on both: both
-    contexts report the counters of one context over the whole batch, which
-    equal the restatement's; verdicts of each shard equal the oracle's."""
+    shards, delta buffers bound, summed with the u64 addition of
+    cgpu_counters_allreduce (RCCL refuses two ranks on one GPU: "invalid
+    usage", tools/rccl_two_rank_probe.py, DESIGN §5 -- the ABI collective
+    itself runs in bench.py at N > 1 with its own check), then counter_fold
+    on both: both contexts report the counters of one context over the whole
+    batch, which equal the restatement's; verdicts of each shard equal the
+    oracle's."""
     torch = torch_cuda
     T, t, o, (v0, i0, s0) = cfg2
     world = 2
