@@ -66,6 +66,10 @@ class Lb4Out(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("ret", "saddr", "daddr", "dport", "rev_nat", "slave")]
 
 
+class CtlbOut(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("verdict", "ct_ret", "identity", "stage", "daddr", "dport")]
+
+
 class Frames(C.Structure):
     _fields_ = [("data", C.c_void_p), ("len", C.c_void_p), ("flags", C.c_void_p),
                 ("ep", C.c_void_p), ("stride", C.c_uint32), ("reserved", C.c_uint32)]
@@ -152,6 +156,7 @@ PROTOS = {
     "cgpu_ct4_gc": (i32, [vp, u32, C.POINTER(u64)]),
     "cgpu_ct4_flush": (i32, [vp]),
     "cgpu_classify_v4_ct": (i32, [vp, C.POINTER(TuplesV4Ct), sz, u32, vp, vp, vp, vp, vp]),
+    "cgpu_classify_v4_ctlb": (i32, [vp, C.POINTER(TuplesV4Ct), vp, sz, u32, C.POINTER(CtlbOut), vp]),
     "cgpu_ct6_update": (i32, [vp, vp, vp, u64]),
     "cgpu_ct6_delete": (i32, [vp, vp]),
     "cgpu_ct6_lookup": (i32, [vp, vp, vp]),

@@ -1177,29 +1177,36 @@ int build_lb(const LbIn &lb, uint32_t lb_max_entries, LbBuild &b)
 	for (auto it = lb.begin(); it != lb.end();) {
 		const uint64_t fk = it->first >> 16;
 		uint32_t mcount = 0, maxs = 0;
+		const cgpu_lb4_service *master = nullptr;
 		auto jt = it;
 		for (; jt != lb.end() && (jt->first >> 16) == fk; ++jt) {
 			const uint32_t s = (uint32_t)(jt->first & 0xFFFFu);
-			if (s == 0)
+			if (s == 0) {
 				mcount = jt->second.count;
-			else
+				master = &jt->second;
+			} else {
 				maxs = s; /* ascending: the last is the largest */
+			}
 		}
 		const uint64_t base = b.be.size();
-		if (base + maxs > cap)
+		const uint32_t rows = maxs + (master ? 1u : 0u);
+		if (base + rows > cap)
 			return fail(-E2BIG, "lb4 backend rows exceed %llu (sparse slave numbers)",
 				    (unsigned long long)cap);
-		b.be.resize(base + maxs, std::array<uint32_t, 4>{0, 0, 0, 0});
+		b.be.resize(base + rows, std::array<uint32_t, 4>{0, 0, 0, 0});
+		auto row = [](const cgpu_lb4_service &v) {
+			return std::array<uint32_t, 4>{v.target, (uint32_t)v.port | (uint32_t)v.count << 16,
+						       (uint32_t)v.rev_nat_index | (uint32_t)v.weight << 16, 1u};
+		};
 		for (auto kt = it; kt != jt; ++kt) {
 			const uint32_t s = (uint32_t)(kt->first & 0xFFFFu);
-			if (!s)
-				continue;
-			const cgpu_lb4_service &v = kt->second;
-			b.be[base + s - 1] = {v.target, (uint32_t)v.port | (uint32_t)v.count << 16,
-					      (uint32_t)v.rev_nat_index | (uint32_t)v.weight << 16, 1u};
+			if (s)
+				b.be[base + s - 1] = row(kt->second);
 		}
+		if (master) /* LB_FE_MASTER: the slave-0 row after the slaves */
+			b.be[base + maxs] = row(*master);
 		fes.push_back({(uint32_t)(fk >> 16), (uint32_t)(fk & 0xFFFFu) | mcount << 16, (uint32_t)base,
-			       maxs});
+			       maxs | (master ? LB_FE_MASTER : 0u)});
 		it = jt;
 	}
 	uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * fes.size()));
@@ -4641,10 +4648,10 @@ CGPU_EXPORT int cgpu_ct6_flush(cgpu_ctx *c)
 /* scratch of one cgpu_classify_v{4,6}_ct launch over n packets */
 struct CtScratch {
 	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, heads_pos, head,
-		temp, temp_bytes, total;
+		temp, temp_bytes, svc_out, ctl, flags2, total;
 };
 
-static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes)
+static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc)
 {
 	CtScratch L{};
 	auto take = [&](size_t bytes) {
@@ -4663,12 +4670,17 @@ static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes)
 	L.head = take(n);
 	L.temp_bytes = ct_temp_bytes(n);
 	L.temp = take(L.temp_bytes);
+	if (svc) {
+		L.svc_out = take(n * 16);
+		L.ctl = take(16);
+		L.flags2 = take(2 * n);
+	}
 	return L;
 }
 
 /* one stateful batch on map m: columns already validated by the caller */
 static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtMap &m, ct_launch a,
-		       void *stream)
+		       void *stream, bool svc = false)
 {
 	/* One conntrack map, one scratch: every batch runs on the context's
 	 * conntrack stream, after the caller's stream reaches this call (its
@@ -4696,7 +4708,7 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	}
 	if (int r = ct_push(m))
 		return r;
-	const CtScratch L = ct_scratch_layout(a.n, m.v6 ? 64 : 32);
+	const CtScratch L = ct_scratch_layout(a.n, m.v6 ? 64 : svc ? 48 : 32, svc);
 	if (L.total > c->ct_scratch_cap) {
 		HIP_OR_EIO(hipStreamSynchronize(cs));
 		(void)hipFree(c->d_ct_scratch);
@@ -4723,7 +4735,14 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.heads_pos = reinterpret_cast<uint32_t *>(b + L.heads_pos);
 	a.temp = b + L.temp;
 	a.temp_bytes = L.temp_bytes;
-	HIP_OR_EIO(m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs));
+	if (svc) {
+		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
+		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);
+		a.flags2 = b + L.flags2;
+		HIP_OR_EIO(launch_classify_v4_ctlb(s, T, a, cs));
+	} else {
+		HIP_OR_EIO(m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs));
+	}
 	HIP_OR_EIO(hipEventRecord(c->ct_done, cs));
 	HIP_OR_EIO(hipStreamWaitEvent((hipStream_t)stream, c->ct_done, 0));
 	m.dev_newer = true;
@@ -4761,6 +4780,42 @@ CGPU_EXPORT int cgpu_classify_v4_ct(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, siz
 	a.n = n;
 	a.now = now;
 	return ct_classify(c, P.snap(), P.delta, c->ct4, a, stream);
+}
+
+CGPU_EXPORT int cgpu_classify_v4_ctlb(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, const uint32_t *hash,
+				      size_t n, uint32_t now, const cgpu_ctlb_out *out, void *stream)
+{
+	Pinned P;
+	if (int r = pin(c, stream, P))
+		return r;
+	if (!t || !out || (n && (!t->saddr || !t->daddr || !t->sport || !t->dport || !t->proto || !t->l4 ||
+				 !t->flags || !t->len || !t->ep || !out->verdict || !out->ct_ret ||
+				 !out->identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n > (size_t)INT32_MAX / 2)
+		return fail(-EINVAL, "batch of %zu packets exceeds 2^30 - 1", n);
+	if (!n)
+		return 0;
+	ct_launch a{};
+	a.saddr = t->saddr;
+	a.daddr = t->daddr;
+	a.sport = t->sport;
+	a.dport = t->dport;
+	a.proto = t->proto;
+	a.l4 = t->l4;
+	a.flags = t->flags;
+	a.len = t->len;
+	a.ep = t->ep;
+	a.verdict = out->verdict;
+	a.ct_ret = out->ct_ret;
+	a.identity = out->identity;
+	a.stage = out->stage;
+	a.xdaddr = out->daddr;
+	a.xdport = out->dport;
+	a.hash = hash;
+	a.n = n;
+	a.now = now;
+	return ct_classify(c, P.snap(), P.delta, c->ct4, a, stream, true);
 }
 
 CGPU_EXPORT int cgpu_classify_v6_ct(cgpu_ctx *c, const cgpu_tuples_v6_ct *t, size_t n, uint32_t now,

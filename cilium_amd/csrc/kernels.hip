@@ -418,6 +418,26 @@ __device__ __forceinline__ bool lb_entry(const lb_table &t, uint4 f, uint32_t sl
 	return v->w != 0;
 }
 
+/* map_lookup_elem(&cilium_lb4_services, {addr, dport, slave}) as a full row
+ * (slave 0 included: the LB_FE_MASTER row), for lb4_lookup_slave of the
+ * stateful service step, whose slave comes from a conntrack entry */
+__device__ __forceinline__ bool lb_row(const lb_table &t, uint4 f, uint32_t slave, uint4 *v)
+{
+	if (!f.w)
+		return false;
+	const uint32_t ns = f.w & 0xFFFFu;
+	if (slave == 0) {
+		if (!(f.w & LB_FE_MASTER))
+			return false;
+		*v = t.be[f.z + ns];
+		return true;
+	}
+	if (slave > ns)
+		return false;
+	*v = t.be[f.z + slave - 1u];
+	return v->w != 0;
+}
+
 /* lb4_lookup_service (lb.h:604-635): the L4 key {addr, *kd, slave} if its
  * count is nonzero, else *kd = 0 and the L3 key; *f: the frontend searched
  * last.  *probes counts map lookups as the reference issues them. */
@@ -2882,6 +2902,25 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_GATED 16u
 #define CTM_ALLOWED 32u
 #define CTM_FRAG 64u
+/* the stateful service step (cgpu_classify_v4_ctlb) */
+#define CTM_PHASE2 128u   /* the packet's address pair may hold owed address entries: phase 2 */
+#define CTM_ADDRX 256u    /* its address entry lies in another pair: owed to phase 2 */
+#define CTM_SVCDROP 512u  /* lb4_local returned DROP_NO_SERVICE */
+#define CT_ADDRP 0x40u    /* walker -> phase 2: the address entry of this create is owed */
+#define CTB_LB_LOOPBACK 8u /* struct ct_entry lb_loopback (common.h:389) */
+#define TUPLE_F_SERVICE 4u /* conntrack.h:66 */
+/* rec word 2 .w of the service path: lb_loopback | address-entry mode << 1 */
+#define LBF_LOOPBACK 1u
+#define AM_NONE 0u
+#define AM_INLINE 1u /* same address pair: written by the create itself */
+#define AM_DEFER 2u  /* other pair: capacity reserved, written in phase 2 */
+/* svc_out[i].x: SVC_* | LBS_* << 8 | slave << 16; .y target; .z the dport
+ * rewrite (0 none) | rev_nat_index << 16 */
+#define SVC_NONE 0u
+#define SVC_XLATED 1u
+#define SVC_DROP 2u
+#define LBS_ENTRY 1u /* lb_loopback came from the conntrack entry */
+#define LBS_SNAT 2u  /* saddr == target: loopback source NAT (lb.h:753-767) */
 
 /* 8-byte write-through store (global_store_dwordx2 sc1) */
 __device__ __forceinline__ void st_wt64(void *p, uint32_t lo, uint32_t hi)
@@ -3008,6 +3047,7 @@ __device__ __forceinline__ uint4 sel4(bool t, uint4 a, uint4 b)
 struct CtK4 {
 	typedef uint4 key;
 	static constexpr int V6 = 0;
+	static constexpr bool SVC = false;
 	__device__ static uint32_t &meta(key &k) { return k.w; }
 	__device__ static uint32_t cmeta(const key &k) { return k.w; }
 	__device__ static uint32_t hash(const key &k) { return ct_hash(k.x, k.y, k.z, k.w); }
@@ -3057,6 +3097,7 @@ struct CtK6 {
 		uint32_t p, m;
 	};
 	static constexpr int V6 = 1;
+	static constexpr bool SVC = false;
 	__device__ static uint32_t &meta(key &k) { return k.m; }
 	__device__ static uint32_t cmeta(const key &k) { return k.m; }
 	__device__ static uint32_t hash(const key &k)
@@ -3116,6 +3157,13 @@ struct CtK6 {
 	{
 		return key{k.d, k.s, 0u, 58u | ((((k.m >> 8) & 0xFFu) | TUPLE_F_RELATED) << 8)};
 	}
+};
+
+/* cilium_ct4_global behind the stateful service step: CtK4's key slots,
+ * records of 3 x 16 B (the service's ct_state) and ct_create4's address
+ * entry */
+struct CtK4S : CtK4 {
+	static constexpr bool SVC = true;
 };
 
 /* Probe for k (low 16 bits of the meta word = nexthdr | flags << 8).
@@ -3210,11 +3258,11 @@ __device__ __forceinline__ bool ct_take(const ct_table &T, const ct_acct &A)
 
 /* Insert absent k at the first free slot from `from` on (htab_map_update_elem
  * of a new key: -E2BIG past max_elem).  Returns the slot or -1. */
-template <class K>
+template <class K, bool TAKE = true>
 __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, const typename K::key &k,
 					 uint32_t from)
 {
-	if (!ct_take(T, A))
+	if (TAKE && !ct_take(T, A))
 		return -1;
 	uint32_t h = from & T.mask;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
@@ -3273,6 +3321,13 @@ struct ct_args {
 	uint8_t *head;               /* [n] */
 	uint32_t *heads, *n_heads;   /* [n], [1] */
 	const uint32_t *gpos, *glen; /* [n_heads] group start / length, longest first */
+	/* the stateful service step (cgpu_classify_v4_ctlb) */
+	const uint32_t *hash;        /* skb->hash or NULL (cgpu_flow_hash) */
+	uint4 *svc_out;              /* [n] lb4_local's outcome per packet */
+	uint32_t *ctl;               /* [4] violation, phase-2 packets, owed entries */
+	uint32_t *xdaddr;            /* [n] optional: frame daddr after the service step */
+	uint16_t *xdport;            /* [n] optional: frame dport after it */
+	uint32_t serial;             /* one group for the whole batch (see launch_ctlb) */
 };
 
 /* One packet's record, written by k_ct_prep{,6} and read by the walker and
@@ -3290,6 +3345,9 @@ struct ct_pkt {
 	uint32_t meta, w, len, sec, revnat, port, cst, dport, proto;
 	uint32_t sa4, da4;
 	uint4 sa6, da6;
+	/* the service's ct_state (CtK4S): slave, lb_loopback | mode << 1, addr,
+	 * svc_addr */
+	uint32_t slave, lbf, addr, svc_addr;
 };
 
 template <class K> struct ct_rec;
@@ -3307,6 +3365,26 @@ template <> struct ct_rec<CtK4> {
 	{
 		return ct_pkt{r0.w >> 16, r1.x & 0xFFFFu, r1.y, r1.z, 0u, r1.x >> 16, r1.w, r0.z & 0xFFFFu,
 			      r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{}};
+	}
+};
+/*   IPv4 behind the service step (3 x 16 B): the IPv4 record, then
+ *                    {rev_nat | slave << 16, addr, svc_addr, lbf} */
+template <> struct ct_rec<CtK4S> {
+	static constexpr uint32_t RW = 3;
+	uint4 r0, r1, r2;
+	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
+	{
+		const uint4 *p = rec + 3u * i;
+		return nt ? ct_rec{ld_x4<true>(p), ld_x4<true>(p + 1), ld_x4<true>(p + 2)}
+			  : ct_rec{p[0], p[1], p[2]};
+	}
+	__device__ CtK4::key key() const { return uint4{r0.x, r0.y, r0.z, r0.w & 0xFFFFu}; }
+	__device__ uint32_t meta() const { return r0.w >> 16; }
+	__device__ ct_pkt pkt() const
+	{
+		return ct_pkt{r0.w >> 16, r1.x & 0xFFFFu, r1.y, r1.z, r2.x & 0xFFFFu, r1.x >> 16, r1.w,
+			      r0.z & 0xFFFFu, r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{},
+			      r2.x >> 16, r2.w, r2.y, r2.z};
 	}
 };
 template <> struct ct_rec<CtK6> {
@@ -3327,15 +3405,76 @@ template <> struct ct_rec<CtK6> {
 	}
 };
 
-/* ct_lookup4's tuple setup, conntrack.h:461-528 */
+/* ct_create4's address entry (conntrack.h:697-725) of forward tuple k for
+ * the egress direction: daddr := state->addr; on loopback flags :=
+ * TUPLE_F_IN and saddr := state->svc_addr */
+__device__ __forceinline__ uint4 ct_addr_key(uint4 k, const ct_pkt &q)
+{
+	k.x = q.addr;
+	if (q.lbf & LBF_LOOPBACK) {
+		k.w = (k.w & ~0xFF00u) | (TUPLE_F_IN << 8);
+		k.y = q.svc_addr;
+	}
+	return k;
+}
+
+/* ct_lookup4's tuple setup, conntrack.h:461-528.  SVC (cgpu_classify_v4_ctlb):
+ * egress packets first take lb4_local's outcome (svc_out, the service walk):
+ * the frame's daddr / dport as lb4_xlate left them, tuple.daddr (the service
+ * address is kept on loopback, lb.h:769-770), the ct_state ct_create4 will
+ * store; a packet whose address entry lies in another address pair owes it
+ * to phase 2 (CTM_ADDRX), and a packet whose own pair can receive such
+ * entries runs in phase 2 (CTM_PHASE2).  SERIAL: one group for the batch. */
+template <bool SVC, bool SERIAL>
 __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	constexpr uint32_t RW = SVC ? 3u : 2u;
 	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t fl = a.flags[i], pr = a.proto[i], w = a.l4[i], len = a.len[i];
-		const uint32_t sa = a.saddr[i], da = a.daddr[i], ep = a.ep[i];
+		const uint32_t fl = a.flags[i], pr = a.proto[i], len = a.len[i];
+		const uint32_t sa = a.saddr[i], ep = a.ep[i];
+		uint32_t w = a.l4[i], da = a.daddr[i], dp = a.dport[i];
 		const bool egress = fl & 1u;
 		uint32_t tfl = egress ? TUPLE_F_IN : 0u, z = 0, meta = egress ? CTM_EGRESS : 0u;
+		uint32_t r2x = 0, addr = 0, saddr2 = 0, lbf = 0, xd = da;
+		if constexpr (SVC) {
+			const uint4 so = egress ? a.svc_out[i] : make_uint4(SVC_NONE, 0, 0, 0);
+			if ((so.x & 3u) == SVC_DROP) {
+				a.identity[i] = 0;
+				if (a.xdaddr)
+					a.xdaddr[i] = da;
+				if (a.xdport)
+					a.xdport[i] = (uint16_t)dp;
+				uint4 *r = a.rec + RW * i;
+				r[0] = uint4{da, sa, 0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16)};
+				r[1] = uint4{0u, len, 0u, 0u};
+				r[2] = uint4{0u, 0u, 0u, 0u};
+				a.gkey[i] = SERIAL ? 0u : ct_fmix((uint32_t)i ^ 0x5bd1e995u);
+				a.idx[i] = (uint32_t)i;
+				continue;
+			}
+			if ((so.x & 3u) == SVC_XLATED) {
+				const uint32_t lbs = (so.x >> 8) & 3u, tg = so.y;
+				const bool lb = lbs != 0;
+				xd = tg;
+				if (!lb)
+					da = tg; /* tuple->daddr = svc->target */
+				if (so.z & 0xFFFFu)
+					dp = so.z & 0xFFFFu; /* lb4_xlate's port rewrite */
+				addr = (lbs & LBS_SNAT) ? s.ipv4_loopback : tg;
+				saddr2 = (lbs & LBS_SNAT) ? sa : 0u;
+				/* the address entry's pair {addr, loopback ? svc_addr : daddr}
+				 * against the packet's own {saddr, daddr} */
+				const uint32_t b = lb ? saddr2 : da;
+				const bool same = (addr == sa && b == da) || (addr == da && b == sa);
+				lbf = (lb ? LBF_LOOPBACK : 0u) | ((same || SERIAL ? AM_INLINE : AM_DEFER) << 1);
+				r2x = (so.z >> 16) | (so.x & 0xFFFF0000u);
+			}
+			if (a.xdaddr)
+				a.xdaddr[i] = xd;
+			if (a.xdport)
+				a.xdport[i] = (uint16_t)dp;
+		}
 		if (pr == 1u) {
 			const uint32_t type = w & 0xFFu;
 			if (type == 3u || type == 11u || type == 12u) /* DEST_UNREACH, TIME_EXCEEDED, PARAMETERPROB */
@@ -3349,7 +3488,7 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 			}
 		} else if (pr == 6u || pr == 17u) {
 			/* skb_load_bytes(off, &tuple->dport, 4): dport <- sport, sport <- dport */
-			z = (uint32_t)a.sport[i] | ((uint32_t)a.dport[i] << 16);
+			z = (uint32_t)a.sport[i] | (dp << 16);
 			if (pr == 6u) {
 				meta |= CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE);
 			} else {
@@ -3358,6 +3497,8 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 		} else {
 			meta |= CTM_GATED;
 		}
+		if (pr != 6u)
+			w = 0; /* union tcp_flags stays zero (conntrack.h:448) */
 		uint32_t sec = 0, port = 0, cst = 0, id = 0;
 		if (!(meta & CTM_GATED)) {
 			/* the forward tuple's decision (what CT_NEW / CT_ESTABLISHED
@@ -3366,7 +3507,7 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 			if (frag)
 				meta |= CTM_FRAG;
 			const decision d = decide<0>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
-							    pr, ep);
+						    pr, ep);
 			if (d.v >= 0) {
 				meta |= CTM_ALLOWED;
 				port = (uint32_t)d.v;
@@ -3378,11 +3519,63 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 				sec = d.id;
 			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
 		}
+		uint32_t g = ct_group(sa, da);
+		if constexpr (SVC) {
+			if (!SERIAL && !(meta & CTM_GATED)) {
+				/* pairs an address entry can land in: {T, T}, {IPV4_LOOPBACK,
+				 * x}, {target, 0} (ct_create4's addr / svc_addr rewrites) */
+				const uint32_t lo = s.ipv4_loopback;
+				const bool p2 = sa == da || !sa || !da || sa == lo || da == lo;
+				if ((lbf >> 1) == AM_DEFER) {
+					meta |= CTM_ADDRX;
+					atomicAdd(&a.ctl[2], 1u);
+					if (p2)
+						atomicOr(&a.ctl[0], 1u); /* owes into phase 2 from phase 2 */
+				}
+				if (p2) {
+					meta |= CTM_PHASE2;
+					atomicAdd(&a.ctl[1], 1u);
+					g = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
+				}
+			}
+		}
 		a.identity[i] = id;
-		a.rec[2u * i] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
-		a.rec[2u * i + 1u] = uint4{w | (port << 16), len, sec, cst};
-		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : ct_group(sa, da);
+		uint4 *r = a.rec + RW * i;
+		r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
+		r[1] = uint4{w | (port << 16), len, sec, cst};
+		if constexpr (SVC)
+			r[2] = uint4{r2x, addr, saddr2, lbf};
+		a.gkey[i] = SERIAL ? 0u : (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
 		a.idx[i] = (uint32_t)i;
+	}
+}
+
+/* phase 2 of the service path: candidate 2i = packet i if it runs in phase
+ * 2, 2i + 1 = packet i's owed address entry (kept whatever phase 1 decided:
+ * the walk checks CT_ADDRP) */
+__global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint8_t *f2)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t meta = a.rec[3u * i].w >> 16;
+		const bool live = !(meta & CTM_GATED);
+		f2[2u * i] = live && (meta & CTM_PHASE2) ? 1u : 0u;
+		f2[2u * i + 1u] = live && (meta & CTM_ADDRX) ? 1u : 0u;
+	}
+}
+
+/* group key of each selected candidate: the address pair (packet: its own,
+ * owed entry: the entry's), or, when no packet runs in phase 2, the owed
+ * entry's whole key (blind BPF_ANY writes of different keys commute) */
+__global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args a, uint32_t m, uint32_t by_key)
+{
+	for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) {
+		const uint32_t v = a.idx[j], i = v >> 1;
+		const ct_rec<CtK4S> r = ct_rec<CtK4S>::load(a.rec, i, false);
+		uint4 k = r.key();
+		if (v & 1u)
+			k = ct_addr_key(CtK4::reversed(k), r.pkt());
+		a.gkey[j] = by_key ? ct_hash(k.x, k.y, k.z, k.w) : ct_group(k.x, k.y);
 	}
 }
 
@@ -3637,15 +3830,55 @@ __device__ __forceinline__ bool ctc_update(const ct_table &T, const ct_acct &A, 
 	return true;
 }
 
+/* BPF_ANY update of k whose capacity was reserved earlier (an owed address
+ * entry): an insert consumes the reservation, an existing key returns it */
+template <class K>
+__device__ __forceinline__ void ctc_update_owed(const ct_table &T, const ct_acct &A, ct_cache<K> &c,
+						const typename K::key &k, const ct_row &e)
+{
+	const int i = ctc_get<K>(T, c, k);
+	uint32_t pos = ctc_pos(c, i);
+	if (ctc_state(c, i) & CTC_NEG) {
+		const int slot = pos == 0xFFFFFFFFu ? -1 : ct_insert<K, false>(T, A, k, pos);
+		if (slot < 0)
+			return; /* no free slot on the chain: the slot table is 2x CT_MAP_SIZE */
+		pos = (uint32_t)slot;
+	} else {
+		atomicAdd(A.live, 1);
+	}
+	ctc_put(c, i, pos, e);
+}
+
+/* the entry ct_create4 writes for packet q (before the ICMP entry's
+ * seen_non_syn) */
+template <class K> __device__ __forceinline__ ct_row ct_new_row(const ct_pkt &q, bool ingress, uint32_t now)
+{
+	const bool tcp = q.meta & CTM_TCP;
+	ct_row e{};
+	ct_timeout(e, now, tcp, ingress, tcp ? 1u : 0u); /* seen_flags.syn = is_tcp: bit 0 */
+	if (ingress)
+		e.a = uint4{1u, 0u, q.len, 0u};
+	else
+		e.b = uint4{1u, 0u, q.len, 0u};
+	e.c.y |= q.revnat << 16; /* rev_nat_index */
+	if (K::SVC) {
+		if (q.lbf & LBF_LOOPBACK)
+			e.c.y |= CTB_LB_LOOPBACK;
+		e.c.z |= q.slave;
+	}
+	e.c.w = q.sec; /* src_sec_id */
+	return e;
+}
+
 /* One packet of a group: ct_lookup4 / ct_lookup6 (conntrack.h:441-561 /
  * :288-412) and ct_create4 / ct_create6 (:653-744 / :588-639), with the
  * policy outcome of the endpoint programs (bpf_lxc.c:506-537 / :918-937,
  * :192-203 / :776-800).  k = the reply-direction tuple of the first lookup. */
 template <class K>
 __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A, ct_cache<K> &c,
-					   typename K::key k, uint32_t meta, uint32_t w, uint32_t len,
-					   uint32_t sec, uint32_t revnat, uint32_t now)
+					   typename K::key k, const ct_pkt &q, uint32_t now)
 {
+	const uint32_t meta = q.meta;
 	const bool ingress = !(meta & CTM_EGRESS);
 	int ci = ctc_get<K>(T, c, k);
 	uint32_t ret;
@@ -3658,7 +3891,7 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 	}
 	if (ret != CT_NEW) {
 		ct_row e = ctc_row(c, ci);
-		ct_hit(e, meta, ingress, w, len, now);
+		ct_hit(e, meta, ingress, q.w, q.len, now);
 		ctc_put(c, ci, ctc_pos(c, ci), e);
 	}
 	if (ret < CT_REPLY && !(meta & CTM_ALLOWED)) {
@@ -3671,26 +3904,197 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 	}
 	if (ret != CT_NEW)
 		return ret;
-	/* ct_create: the forward entry, then the ICMP entry relating errors */
-	const bool tcp = meta & CTM_TCP;
-	ct_row e{};
-	ct_timeout(e, now, tcp, ingress, tcp ? 1u : 0u); /* seen_flags.syn = is_tcp: bit 0 */
-	if (ingress)
-		e.a = uint4{1u, 0u, len, 0u};
-	else
-		e.b = uint4{1u, 0u, len, 0u};
-	e.c.y |= revnat << 16; /* rev_nat_index */
-	e.c.w = sec;           /* src_sec_id */
+	/* ct_create: the forward entry, the address entry (service step only),
+	 * then the ICMP entry relating errors */
+	ct_row e = ct_new_row<K>(q, ingress, now);
 	if (!ctc_update<K>(T, A, c, k, e))
 		return CT_NEW | CT_FAIL;
+	uint32_t owed = 0;
+	if constexpr (K::SVC) {
+		const uint32_t am = q.lbf >> 1;
+		if (am == AM_INLINE) {
+			if (!ctc_update<K>(T, A, c, ct_addr_key(k, q), e))
+				return CT_NEW | CT_FAIL;
+		} else if (am == AM_DEFER) {
+			/* the entry lies in another address pair's group: reserve its
+			 * capacity now (the reference's update fails here when the map
+			 * is full), write it in phase 2 */
+			if (!ct_take(T, A))
+				return CT_NEW | CT_FAIL;
+			owed = CT_ADDRP;
+		}
+	}
 	e.c.y |= CTB_SEEN_NON_SYN;
 	if (!ctc_update<K>(T, A, c, K::related(k), e))
-		return CT_NEW | CT_FAIL;
-	return CT_NEW;
+		return CT_NEW | CT_FAIL | owed;
+	return CT_NEW | owed;
 }
 
-template <class K> __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, ct_args a)
+/* ---- the stateful service step: lb4_local with CONNTRACK (lb.h:700-775) ----
+ * Its conntrack keys carry TUPLE_F_SERVICE (4) and nothing else in the
+ * datapath builds such a key (ct_lookup4 sets TUPLE_F_IN / TUPLE_F_OUT |
+ * RELATED for CT_EGRESS / CT_INGRESS; ct_create4's address entry TUPLE_F_IN
+ * or the tuple's flags), so the service keyspace is disjoint from the
+ * endpoint's and the service step of the whole batch runs as its own walk
+ * BEFORE the conntrack walk: packets grouped by the unordered pair {saddr,
+ * service address} (the service entry and its ICMP entry carry it), each
+ * group in batch order.  Its result per packet (the slave, the backend row,
+ * loopback) feeds the conntrack path's prep. */
+
+/* A service packet's record (3 x 16 B, batch order):
+ *   {VIP, saddr, z, nexthdr | (TUPLE_F_SERVICE | RELATED) << 8 | meta << 16},
+ *   {w, len, hash, kd | master count << 16},
+ *   {frontend base, frontend nslaves | flags, dport (the frame's), 0}
+ * z = the service tuple's ports as ct_lookup4 loads them; kd = key.dport
+ * after lb4_lookup_service (0 after an L3 fallback). */
+struct ct_srec {
+	uint4 r0, r1, r2;
+	__device__ static ct_srec load(const uint4 *rec, uint32_t i, bool)
+	{
+		const uint4 *p = rec + 3u * i;
+		return ct_srec{p[0], p[1], p[2]};
+	}
+	__device__ uint32_t meta() const { return r0.w >> 16; }
+};
+
+
+/* lb4_extract_key + lb4_lookup_service (lb.h:590-635) for every egress
+ * packet; service packets get their CT_SERVICE record */
+__global__ __launch_bounds__(256) void k_svc_prep(cgpu_snapshot s, ct_args a)
 {
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	const bool l4 = s.lb_flags & CGPU_LB_L4;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t fl = a.flags[i], pr = a.proto[i];
+		const uint32_t sa = a.saddr[i], da = a.daddr[i], dp = a.dport[i];
+		uint4 out = make_uint4(SVC_NONE, 0, 0, 0);
+		bool svc = false;
+		uint4 f = make_uint4(0, 0, 0, 0), v;
+		uint32_t kd = 0;
+		if (fl & 1u) {
+			bool skip = false;
+			if (l4) { /* extract_l4_port (lb.h:192-216) */
+				if (pr == 6u || pr == 17u)
+					kd = dp;
+				else if (pr != 1u && pr != 58u)
+					skip = true; /* DROP_UNKNOWN_L4: skip_service_lookup */
+			}
+			const uint32_t vb = lb_vip_bit(da) & s.lb.vip_mask;
+			uint32_t probes = 0;
+			if (!skip && ((s.lb.vip[vb >> 5] >> (vb & 31u)) & 1u))
+				svc = lb_service(s, da, &kd, 0, &v, &f, &probes);
+		}
+		uint4 r0 = make_uint4(0, 0, 0, CTM_GATED << 16), r1 = make_uint4(0, 0, 0, 0),
+		      r2 = make_uint4(0, 0, 0, 0);
+		if (svc) {
+			/* ct_lookup4(..., CT_SERVICE, ...)'s tuple (conntrack.h:462-530) */
+			const uint32_t w = a.l4[i];
+			uint32_t tfl = TUPLE_F_SERVICE, z = 0, meta = 0;
+			bool ok = true;
+			if (pr == 1u) {
+				const uint32_t type = w & 0xFFu;
+				if (type == 3u || type == 11u || type == 12u)
+					tfl |= TUPLE_F_RELATED;
+				else if (type == 0u)
+					z = 8u;
+				else {
+					if (type == 8u)
+						z = 8u << 16;
+					meta |= CTM_ACT_CREATE;
+				}
+			} else if (pr == 6u || pr == 17u) {
+				z = (uint32_t)a.sport[i] | (dp << 16);
+				meta |= pr == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
+			} else {
+				ok = false; /* DROP_CT_UNKNOWN_PROTO -> DROP_NO_SERVICE (lb.h:728-730) */
+			}
+			if (ok) {
+				const uint32_t h = a.hash ? a.hash[i] : flow_hash(sa, da, a.sport[i], dp, pr);
+				r0 = make_uint4(da, sa, z, pr | (tfl << 8) | (meta << 16));
+				r1 = make_uint4(pr == 6u ? w : 0u, a.len[i], h, kd | (v.y & 0xFFFF0000u));
+				r2 = make_uint4(f.z, f.w & 0xFFFFFFu, dp, 0u);
+			} else {
+				out.x = SVC_DROP;
+			}
+		}
+		uint4 *r = a.rec + 3u * i;
+		r[0] = r0;
+		r[1] = r1;
+		r[2] = r2;
+		a.svc_out[i] = out;
+		a.gkey[i] = (r0.w >> 16) & CTM_GATED ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : ct_group(sa, da);
+		a.idx[i] = (uint32_t)i;
+	}
+}
+
+/* One service packet of a group: lb4_local (lb.h:700-775) against the map.
+ * k = the CT_SERVICE tuple; no forward lookup for CT_SERVICE (conntrack.h:
+ * 553-558). */
+__device__ __forceinline__ uint4 ct_svc_step(const cgpu_snapshot &s, const ct_table &T, const ct_acct &A,
+					     ct_cache<CtK4> &c, const ct_srec &r, uint32_t now)
+{
+	const uint4 k = uint4{r.r0.x, r.r0.y, r.r0.z, r.r0.w & 0xFFFFu};
+	const uint32_t meta = r.r0.w >> 16, w = r.r1.x, len = r.r1.y, h = r.r1.z;
+	uint32_t kd = r.r1.w & 0xFFFFu;
+	const uint32_t pr = r.r0.w & 0xFFu;
+	uint4 f = uint4{r.r0.x, kd | (r.r1.w & 0xFFFF0000u), r.r2.x, r.r2.y};
+	const uint4 drop = make_uint4(SVC_DROP, 0, 0, 0);
+	uint32_t slave, lbs = 0;
+	int ci = ctc_get<CtK4>(T, c, k);
+	if (!(ctc_state(c, ci) & CTC_NEG)) { /* CT_REPLY / CT_RELATED: the stored state */
+		ct_row e = ctc_row(c, ci);
+		ct_hit(e, meta, false, w, len, now);
+		ctc_put(c, ci, ctc_pos(c, ci), e);
+		if (e.c.y & CTB_LB_LOOPBACK)
+			lbs |= LBS_ENTRY;
+		slave = e.c.z & 0xFFFFu;
+	} else { /* CT_NEW: lb4_select_slave, ct_create4(CT_SERVICE) -- fail closed */
+		slave = h % (r.r1.w >> 16) + 1u;
+		const bool tcp = meta & CTM_TCP;
+		ct_row e{};
+		ct_timeout(e, now, tcp, false, tcp ? 1u : 0u);
+		e.b = uint4{1u, 0u, len, 0u};
+		e.c.z = slave;
+		if (!ctc_update<CtK4>(T, A, c, k, e))
+			return drop;
+		e.c.y |= CTB_SEEN_NON_SYN;
+		if (!ctc_update<CtK4>(T, A, c, CtK4::related(k), e))
+			return drop;
+	}
+	uint4 b;
+	if (!lb_row(s.lb, f, slave, &b)) {
+		/* lb4_lookup_slave missed: lb4_lookup_service with key.slave kept,
+		 * a new slave from its count, ct_update4_slave (lb.h:737-744) */
+		uint32_t probes = 0;
+		if (!lb_service(s, r.r0.x, &kd, slave, &b, &f, &probes))
+			return drop;
+		slave = h % (b.y >> 16) + 1u;
+		ci = ctc_get<CtK4>(T, c, k);
+		if (!(ctc_state(c, ci) & CTC_NEG)) {
+			ct_row e = ctc_row(c, ci);
+			e.c.z = (e.c.z & 0xFFFF0000u) | slave;
+			ctc_put(c, ci, ctc_pos(c, ci), e);
+		}
+	}
+	if (r.r0.y == b.x)
+		lbs |= LBS_SNAT;
+	const uint32_t port = b.y & 0xFFFFu;
+	const uint32_t rw = ((s.lb_flags & CGPU_LB_L4) && port && kd != port && (pr == 6u || pr == 17u)) ? port : 0u;
+	return make_uint4(SVC_XLATED | (lbs << 8) | (slave << 16), b.x, rw | ((b.z & 0xFFFFu) << 16), 0u);
+}
+
+/* walks: WALK_PKT the conntrack path's packets; WALK_SVC the service step
+ * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
+ * service path: candidates c = packet << 1 | kind, kind 0 a packet whose
+ * address pair may hold owed entries, kind 1 an owed address entry */
+#define WALK_PKT 0
+#define WALK_SVC 1
+#define WALK_OWED 2
+
+template <class K, int MODE>
+__global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
+{
+	using R = std::conditional_t<MODE == WALK_SVC, ct_srec, ct_rec<K>>;
 	__shared__ int s_acct[3];
 	if (threadIdx.x < 3)
 		s_acct[threadIdx.x] = 0;
@@ -3705,6 +4109,7 @@ template <class K> __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, 
 	ctc_ent<K> e0{}, e1{}, e2{};
 	ct_cache<K> c{e0, e1, e2, 0u};
 #endif
+	auto pkt_of = [](uint32_t v) { return MODE == WALK_OWED ? v >> 1 : v; };
 	/* groups longest first (a.glen / a.gpos, sorted by length): the
 	 * elephants start in the first round and the rest fill in behind */
 	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {
@@ -3715,21 +4120,39 @@ template <class K> __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, 
 		 * flight while packet p runs */
 		uint32_t ni = a.idx_sorted[p0];
 		uint32_t nni = p0 + 1u < p1 ? a.idx_sorted[p0 + 1u] : 0u;
-		ct_rec<K> nr = ct_rec<K>::load(a.rec, ni, false);
+		R nr = R::load(a.rec, pkt_of(ni), false);
 		for (uint64_t p = p0; p < p1; p++) {
-			const uint32_t i = ni;
-			const ct_rec<K> r = nr;
+			const uint32_t v = ni;
+			const uint32_t i = pkt_of(v);
+			const R r = nr;
 			if (p + 1u < p1) {
 				ni = nni;
-				nr = ct_rec<K>::load(a.rec, ni, false);
+				nr = R::load(a.rec, pkt_of(ni), false);
 				if (p + 2u < p1)
 					nni = a.idx_sorted[p + 2u];
 			}
 			const uint32_t meta = r.meta();
 			if (meta & CTM_GATED)
 				continue;
-			const ct_pkt q = r.pkt();
-			a.ct_ret[i] = (uint8_t)ct_step<K>(T, A, c, r.key(), meta, q.w, q.len, q.sec, q.revnat, a.now);
+			if constexpr (MODE == WALK_SVC) {
+				a.svc_out[i] = ct_svc_step(s, T, A, c, r, a.now);
+			} else {
+				const ct_pkt q = r.pkt();
+				if constexpr (MODE == WALK_OWED) {
+					if (v & 1u) {
+						/* the owed address entry of packet i's create */
+						if (a.ct_ret[i] & CT_ADDRP) {
+							const typename K::key fk = K::reversed(r.key());
+							ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
+									   ct_new_row<K>(q, false, a.now));
+						}
+						continue;
+					}
+				}
+				if (MODE == WALK_PKT && K::SVC && (meta & CTM_PHASE2))
+					continue;
+				a.ct_ret[i] = (uint8_t)ct_step<K>(T, A, c, r.key(), q, a.now);
+			}
 		}
 		ctc_flush(T, c);
 	}
@@ -3750,8 +4173,9 @@ template <class K> __global__ __launch_bounds__(256) void k_ct_walk(ct_table T, 
 template <int NT, class K> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
-	/* metrics {reason 0 / 133 / 137 / 155} x {ingress, egress} */
-	uint64_t mcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mbyt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	/* metrics {reason 0 / 133 / 137 / 155 [/ 158]} x {ingress, egress} */
+	constexpr int NM = K::SVC ? 10 : 8;
+	uint64_t mcnt[NM] = {}, mbyt[NM] = {};
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
 	__syncthreads();
@@ -3766,8 +4190,12 @@ template <int NT, class K> __global__ __launch_bounds__(NT) void k_ct_finish(cgp
 		uint32_t st = 4, cr = 255u;
 		if (meta & CTM_GATED) {
 			v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup default case */
+			if (K::SVC && (meta & CTM_SVCDROP)) {
+				v = DROP_NO_SERVICE; /* lb4_local failed closed (lb.h:715-744) */
+				st = 6;
+			}
 		} else {
-			const uint32_t c = a.ct_ret[i];
+			const uint32_t c = a.ct_ret[i] & ~CT_ADDRP;
 			cr = c & 3u;
 			int ctr;
 			if (cr >= CT_REPLY) {
@@ -3803,18 +4231,18 @@ template <int NT, class K> __global__ __launch_bounds__(NT) void k_ct_finish(cgp
 		if (a.stage)
 			a.stage[i] = (uint8_t)st;
 		/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
-		const uint32_t r = v > 0 ? 4u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : 3u));
+		const uint32_t r = v > 0 ? 5u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : (v == DROP_NO_SERVICE ? 4u : 3u)));
 		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
 #pragma unroll
-		for (int k = 0; k < 8; k++) {
+		for (int k = 0; k < NM; k++) {
 			mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
 			mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
 		}
 	}
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
-	const uint32_t reasons[4] = {0u, 133u, 137u, 155u};
+	const uint32_t reasons[5] = {0u, 133u, 137u, 155u, 158u};
 #pragma unroll
-	for (int k = 0; k < 8; k++) {
+	for (int k = 0; k < NM; k++) {
 		const uint64_t c = wave_sum(mcnt[k]);
 		const uint64_t b = wave_sum(mbyt[k]);
 		if ((threadIdx.x & 63) == 0 && c) {
@@ -3840,7 +4268,8 @@ static int ct_sort_bits(const cgpu_snapshot &s)
 	return b ? std::max(8, std::min(32, b)) : 24;
 }
 
-/* hipcub temporary storage for the sort and the head selection of n packets */
+/* hipcub temporary storage for the sort and the head selection of n packets
+ * (and the selection of the 2n phase-2 candidates of the service path) */
 size_t ct_temp_bytes(uint64_t n)
 {
 	size_t a = 0, b = 0;
@@ -3848,62 +4277,92 @@ size_t ct_temp_bytes(uint64_t n)
 						 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
 	hipcub::CountingInputIterator<uint32_t> it(0);
 	(void)hipcub::DeviceSelect::Flagged(nullptr, b, it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
-					    (uint32_t *)nullptr, (int)n);
+					    (uint32_t *)nullptr, (int)std::min<uint64_t>(2 * n, INT32_MAX));
 	return std::max(a, b);
 }
 
-template <class K>
-static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
+static ct_args ct_args_of(const ct_launch &L)
 {
 	ct_args a{static_cast<const uint32_t *>(L.saddr), static_cast<const uint32_t *>(L.daddr), L.sport,
 		  L.dport, L.proto, L.l4, L.flags, L.len, L.ep,
 		  L.verdict, L.ct_ret, L.identity, L.stage, L.delta, L.n, L.now,
 		  L.rec, L.gkey, L.gkey_sorted, L.idx, L.idx_sorted, L.head, L.heads,
 		  L.n_heads};
-	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
-	if (K::V6)
-		hipLaunchKernelGGL(k_ct_prep6, dim3(g), dim3(256), 0, st, s, a);
-	else
-		hipLaunchKernelGGL(k_ct_prep, dim3(g), dim3(256), 0, st, s, a);
+	a.hash = L.hash;
+	a.svc_out = L.svc_out;
+	a.ctl = L.ctl;
+	a.xdaddr = L.xdaddr;
+	a.xdport = L.xdport;
+	return a;
+}
+
+/* (gkey, idx)[0, m) -> groups in batch order, longest first: a.idx_sorted
+ * the permutation, a.gpos / a.glen per group; *nh (host) the group count */
+static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_args &a, uint64_t m,
+				uint32_t *nh, hipStream_t st)
+{
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m + 255) / 256, 8192));
 	size_t tb = L.temp_bytes;
 	/* 24 key bits: three passes; pairs sharing a 24-bit hash merge into
 	 * one group, which only lengthens that lane's walk */
+	const int bits = ct_sort_bits(s);
 	hipError_t e = hipcub::DeviceRadixSort::SortPairs(L.temp, tb, L.gkey, L.gkey_sorted, L.idx,
-							   L.idx_sorted, (int)L.n, 0, ct_sort_bits(s), st);
+							   L.idx_sorted, (int)m, 0, bits, st);
 	if (e != hipSuccess)
 		return e;
-	const int bits = ct_sort_bits(s);
 	const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
-	hipLaunchKernelGGL(k_ct_heads, dim3(g), dim3(256), 0, st, L.gkey_sorted, L.head, L.n, mask);
+	hipLaunchKernelGGL(k_ct_heads, dim3(g), dim3(256), 0, st, L.gkey_sorted, L.head, m, mask);
 	hipcub::CountingInputIterator<uint32_t> it(0);
 	tb = L.temp_bytes;
-	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.head, L.heads, L.n_heads, (int)L.n, st);
+	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.head, L.heads, L.n_heads, (int)m, st);
 	if (e != hipSuccess)
 		return e;
 	/* groups longest first: gkey / idx are free again and hold (length,
 	 * start) before the sort, gkey_sorted / idx the sorted pairs after */
-	uint32_t nh = 0;
-	e = hipMemcpyAsync(&nh, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+	*nh = 0;
+	e = hipMemcpyAsync(nh, L.n_heads, 4, hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
 		return e;
-	const unsigned gh = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nh + 255) / 256, 8192));
-	hipLaunchKernelGGL(k_ct_lens, dim3(gh), dim3(256), 0, st, L.heads, nh, L.n, L.gkey, L.heads_pos);
+	const unsigned gh = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((*nh + 255) / 256, 8192));
+	hipLaunchKernelGGL(k_ct_lens, dim3(gh), dim3(256), 0, st, L.heads, *nh, m, L.gkey, L.heads_pos);
 	tb = L.temp_bytes;
 	e = hipcub::DeviceRadixSort::SortPairsDescending(L.temp, tb, L.gkey, L.gkey_sorted, L.heads_pos,
-							 L.idx, (int)nh, 0, 32, st);
+							 L.idx, (int)*nh, 0, 32, st);
 	if (e != hipSuccess)
 		return e;
 	a.glen = L.gkey_sorted;
 	a.gpos = L.idx;
-	/* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
-	hipLaunchKernelGGL(k_ct_walk<K>, dim3(2048), dim3(256), 0, st, T, a);
+	return hipSuccess;
+}
+
+/* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
+#define CT_WALK_GRID 2048
+
+template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
+{
 	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
 	constexpr int NF = 1024;
-	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((L.n + NF - 1) / NF, 512),
-					       (L.n >> 22) + 1);
+	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF - 1) / NF, 512), (a.n >> 22) + 1);
 	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
 	hipLaunchKernelGGL((k_ct_finish<NF, K>), dim3((unsigned)gf), dim3(NF), (size_t)sf.hot_slots * 8u, st,
 			   sf, a);
+}
+
+template <class K>
+static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
+{
+	ct_args a = ct_args_of(L);
+	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
+	if (K::V6)
+		hipLaunchKernelGGL(k_ct_prep6, dim3(g), dim3(256), 0, st, s, a);
+	else
+		hipLaunchKernelGGL((k_ct_prep<false, false>), dim3(g), dim3(256), 0, st, s, a);
+	uint32_t nh;
+	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	launch_ct_finish<K>(s, a, st);
 	return hipGetLastError();
 }
 
@@ -3917,6 +4376,75 @@ hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, cons
 				 hipStream_t st)
 {
 	return launch_ct<CtK6>(s, T, L, st);
+}
+
+/*
+ * cgpu_classify_v4_ctlb: the service walk, then the conntrack path.
+ *   1 k_svc_prep + group sort + k_ct_walk<WALK_SVC>: lb4_local for every
+ *     service packet, groups = {saddr, service address}, in batch order.
+ *   2 k_ct_prep<SVC>: the translated tuples (svc_out), their decisions and
+ *     the ct_state their creates store.
+ *   3 group sort + k_ct_walk<WALK_PKT> (phase 1): every packet outside the
+ *     pairs address entries can land in; an address entry of another pair
+ *     is reserved and owed (CT_ADDRP).
+ *   4 phase 2 (only when something is owed or runs in it): the owed
+ *     entries and the phase-2 packets, grouped by address pair (or by the
+ *     owed entry's key when no packet runs in phase 2), in batch order.
+ *   5 k_ct_finish.
+ * A batch where a phase-2 packet itself owes an entry to another pair
+ * (addresses 0 / IPV4_LOOPBACK as endpoints or service backends) runs the
+ * conntrack path as ONE group (exact, serial).
+ */
+hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				   hipStream_t st)
+{
+	ct_args a = ct_args_of(L);
+	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
+	hipLaunchKernelGGL(k_svc_prep, dim3(g), dim3(256), 0, st, s, a);
+	uint32_t nh;
+	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_walk<CtK4, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	e = hipMemsetAsync(a.ctl, 0, 16, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_prep<true, false>), dim3(g), dim3(256), 0, st, s, a);
+	uint32_t ctl[4];
+	e = hipMemcpyAsync(ctl, a.ctl, 16, hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+		return e;
+	const bool serial = ctl[0] != 0;
+	if (serial)
+		hipLaunchKernelGGL((k_ct_prep<true, true>), dim3(g), dim3(256), 0, st, s, a);
+	e = ct_group_sort(s, L, a, L.n, &nh, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	if (!serial && (ctl[1] || ctl[2])) {
+		const unsigned g2 = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
+		hipLaunchKernelGGL(k_ct_owed_flags, dim3(g2), dim3(256), 0, st, a, L.flags2);
+		hipcub::CountingInputIterator<uint32_t> it(0);
+		size_t tb = L.temp_bytes;
+		e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.flags2, L.idx, L.n_heads, (int)(2 * L.n), st);
+		if (e != hipSuccess)
+			return e;
+		uint32_t m = 0;
+		e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+		if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+			return e;
+		if (m) {
+			const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
+			hipLaunchKernelGGL(k_ct_owed_keys, dim3(gm), dim3(256), 0, st, a, m, ctl[1] ? 0u : 1u);
+			e = ct_group_sort(s, L, a, m, &nh, st);
+			if (e != hipSuccess)
+				return e;
+			hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T,
+					   a);
+		}
+	}
+	launch_ct_finish<CtK4S>(s, a, st);
+	return hipGetLastError();
 }
 
 /* ======================================================================= */

@@ -123,6 +123,13 @@ struct ct_launch {
 	uint32_t *heads_pos; /* [n] scratch for the longest-first group sort */
 	void *temp;
 	size_t temp_bytes;
+	/* the stateful service step (cgpu_classify_v4_ctlb); rec is [3n] */
+	const uint32_t *hash; /* NULL: cgpu_flow_hash */
+	uint4 *svc_out;       /* [n] */
+	uint32_t *ctl;        /* [4] */
+	uint8_t *flags2;      /* [2n] */
+	uint32_t *xdaddr;     /* [n] optional */
+	uint16_t *xdport;     /* [n] optional */
 };
 
 size_t ct_temp_bytes(uint64_t n);
@@ -131,6 +138,10 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 /* the same over cilium_ct6_global (tables.h CtK6 slots), rec [4n] */
 hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
 				 hipStream_t st);
+
+/* the same behind the stateful service step (cilium_ct4_global, rec [3n]) */
+hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				   hipStream_t st);
 
 /* L3 MapState compilation (cgpu_l3_compile): device copies of the program */
 struct l3_launch {

@@ -268,6 +268,10 @@ static inline __host__ __device__ uint32_t v6_bloom_bits(uint32_t h)
  * A service lookup is one 16-byte gather (the frontend slot, usually its
  * home slot) and a backend lookup one more, dependent, 16-byte gather. */
 #define LB_FE_USED (1u << 16)
+/* the frontend has a slave-0 (master) entry, stored as a full row at
+ * be[base + nslaves]: read only by the stateful service step, where a stored
+ * CT_SERVICE entry may name slave 0 (lb4_lookup_slave, lb.h:637-651) */
+#define LB_FE_MASTER (1u << 17)
 
 typedef struct lb_table {
 	const uint4 *fe; /* fe_mask + 1 slots, never NULL once committed */

@@ -25,7 +25,7 @@ import ipaddress
 import numpy as np
 
 from . import layouts as L
-from ._abi import (CgpuConfig, CgpuError, FrameTuples, Frames, Lb4Out, Lb4Tuples, TuplesV4,
+from ._abi import (CgpuConfig, CgpuError, CtlbOut, FrameTuples, Frames, Lb4Out, Lb4Tuples, TuplesV4,
                    TuplesV4Ct, TuplesV6Ct, TuplesV6, check, lib)
 
 CIDR_V4_DYN, CIDR_V4_FIX, CIDR_V6_DYN, CIDR_V6_FIX = 0, 1, 2, 3
@@ -433,6 +433,30 @@ class Engine:
                                          _ptr(out["ct_ret"]), _ptr(out["identity"]),
                                          _ptr(out.get("stage")), _stream(stream)),
               "cgpu_classify_v4_ct")
+        return out
+
+    def classify_v4_ctlb(self, t: dict, now: int, out: dict | None = None, stage: bool = True,
+                         xlate: bool = True, stream=None):
+        """cgpu_classify_v4_ctlb: classify_v4_ct with the stateful service
+        step (lb4_local with CONNTRACK) in front; t may carry a "hash" column
+        (skb->hash, int32).  out adds "daddr" / "dport": the frame after the
+        service step (xlate=False: not written)."""
+        import torch
+        n = t["saddr"].numel()
+        dev = t["saddr"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "ct_ret": torch.empty(n, dtype=torch.uint8, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None,
+                   "daddr": torch.empty(n, dtype=torch.int32, device=dev) if xlate else None,
+                   "dport": torch.empty(n, dtype=torch.int16, device=dev) if xlate else None}
+        tv = TuplesV4Ct(*[t[k].data_ptr() for k in
+                          ("saddr", "daddr", "sport", "dport", "proto", "l4b", "flags", "len", "ep")])
+        ov = CtlbOut(*[_ptr(out.get(k)) for k in ("verdict", "ct_ret", "identity", "stage", "daddr",
+                                                   "dport")])
+        check(self.L.cgpu_classify_v4_ctlb(self.h, C.byref(tv), _ptr(t.get("hash")), n, now,
+                                           C.byref(ov), _stream(stream)), "cgpu_classify_v4_ctlb")
         return out
 
     def classify_v6_ct(self, t: dict, now: int, out: dict | None = None, stage: bool = True,

@@ -881,6 +881,73 @@ def make_ct_workload(tables: Tables, n_conn: int, seed=SEED, gpu_id: int = 0, n_
     return t, locals_be, seclabels
 
 
+def make_ctlb_workload(tables: Tables, svcs: Services, n_conn: int, seed=SEED, gpu_id: int = 0,
+                       vip_frac: float = 0.4, mean_pkts: float = 8.0, span: float = 0.02,
+                       loop_frac: float = 0.02, world: int = 1):
+    """The stateful stream behind the service step (cgpu_classify_v4_ctlb):
+    make_ct_workload where `vip_frac` of the connections' remotes are service
+    addresses.  Egress packets to a service carry its port (L4 services);
+    replies come from the service address or, for 2/3 of the connections,
+    from the backend the connection's local port picks (the reverse NAT map
+    is empty, so both occur on the wire).  `loop_frac` of the backends are
+    the endpoints themselves (lb4_local's loopback source NAT).  hash =
+    skb->hash: the flow hash of the connection's egress direction, redrawn
+    for 5 % of the packets.  Returns (t, locals_be, seclabels, services)."""
+    from .shard import flowhash_np, pairhash_np
+    rng = np.random.Generator(np.random.PCG64(seed + 0xCB000 + gpu_id))
+    locals_be, seclabels = ct_endpoints(tables.n_endpoints)
+    ns = len(svcs.vip)
+    vals = svcs.vals.copy()
+    nb = vals["count"][:ns].astype(np.int64)
+    loop = rng.random(len(vals) - ns) < loop_frac
+    vals["target"][ns:] = np.where(loop, locals_be[rng.integers(0, len(locals_be), len(loop))],
+                                   vals["target"][ns:])
+    svcs = Services(svcs.keys, vals, svcs.vip, svcs.port)
+    nr = max(16, n_conn // 4)
+    pi = rng.integers(0, len(tables.pfx_addr), nr)
+    base = tables.pfx_addr[pi].astype(np.uint64)
+    ln = tables.pfx_len[pi].astype(np.uint64)
+    host = rng.integers(0, 2**32, nr, dtype=np.uint64)
+    hmask = (np.uint64(1) << (np.uint64(32) - ln)) - np.uint64(1)
+    rem = np.where(rng.random(nr) < 0.8, base | (host & hmask), host).astype(np.uint32).byteswap()
+    nv = int(nr * vip_frac / (1.0 - vip_frac))
+    rem = np.concatenate([rem, svcs.vip[rng.integers(0, ns, nv)]]).astype(np.uint32)
+    ok = None
+    if world > 1:
+        ok = lambda a, b: (pairhash_np(a, b) % np.uint32(world)) == gpu_id  # noqa: E731
+    t = make_ct_stream(rng, n_conn, locals_be, rem, mean_pkts=mean_pkts, span=span, pair_ok=ok)
+    order = np.argsort(svcs.vip, kind="stable")
+    sv = svcs.vip[order]
+    eg = (t["flags"] & 1).astype(bool)
+    remote = np.where(eg, t["daddr"], t["saddr"])
+    pos = np.minimum(np.searchsorted(sv, remote), ns - 1)
+    isv = sv[pos] == remote
+    si = order[pos]
+    port = svcs.port[si]
+    l4 = np.isin(t["proto"], [6, 17])
+    setp = isv & (port != 0) & l4
+    t["dport"] = np.where(eg & setp, port, t["dport"]).astype(np.uint16)
+    t["sport"] = np.where(~eg & setp, port, t["sport"]).astype(np.uint16)
+    # replies from a backend: the one the connection's local port picks
+    lport = np.where(eg, t["sport"], t["dport"]).astype(np.int64)
+    first = (ns + np.cumsum(nb) - nb)[si]
+    bi = first + lport % np.maximum(nb[si], 1)
+    fromb = ~eg & isv & (nb[si] > 0) & (lport % 3 != 0)
+    bi = np.where(fromb, bi, 0)
+    t["saddr"] = np.where(fromb, vals["target"][bi], t["saddr"]).astype(np.uint32)
+    bport = vals["port"][bi]
+    t["sport"] = np.where(fromb & l4 & (bport != 0), bport, t["sport"]).astype(np.uint16)
+    loc = np.where(eg, t["saddr"], t["daddr"])
+    rmt = np.where(eg, t["daddr"], t["saddr"])
+    lp = np.where(eg, t["sport"], t["dport"])
+    rp = np.where(eg, t["dport"], t["sport"])
+    h = flowhash_np(loc, rmt, lp, rp, t["proto"])
+    redraw = rng.random(len(h)) < 0.05
+    h[redraw] = rng.integers(0, 2**32, int(redraw.sum()), dtype=np.uint64).astype(np.uint32)
+    t["hash"] = h.astype(np.uint32)
+    return t, locals_be, seclabels, svcs
+
+
 def ct6_endpoints(tables, n_endpoints: int):
     """Local IPv6 endpoint addresses (inside ROUTER_IP's /64, the cluster
     range) and their SECLABELs for the IPv6 stateful workloads."""

@@ -702,6 +702,49 @@ int cgpu_classify_v4_ct(cgpu_ctx *ctx, const cgpu_tuples_v4_ct *t, size_t n, uin
 			int32_t *verdict, uint8_t *ct_ret, uint32_t *identity, uint8_t *stage,
 			void *stream);
 
+/* outputs of cgpu_classify_v4_ctlb (device pointers; stage, daddr, dport
+ * may be NULL) */
+typedef struct cgpu_ctlb_out {
+	int32_t *verdict;   /* as cgpu_classify_v4_ct, plus DROP_NO_SERVICE (-158) */
+	uint8_t *ct_ret;    /* the CT_EGRESS / CT_INGRESS lookup; CGPU_CT_NONE for a
+			       service drop or DROP_CT_UNKNOWN_PROTO */
+	uint32_t *identity; /* 0 for a service drop */
+	uint8_t *stage;     /* as cgpu_classify_v4_ct; 6 = service drop */
+	uint32_t *daddr;    /* the frame's daddr after the service step (lb4_xlate) */
+	uint16_t *dport;    /* the frame's dport after it (network order) */
+} cgpu_ctlb_out;
+
+/*
+ * cgpu_classify_v4_ct with the STATEFUL service step of handle_ipv4_from_lxc
+ * in front (bpf_lxc.c:444-469; lb4_local with CONNTRACK, lib/lb.h:700-775),
+ * packets processed in order as the reference's programs would:
+ *   egress packets whose {daddr, dport} (or {daddr, 0}) is a service
+ *   (lb4_extract_key / lb4_lookup_service, lb.h:590-635) look up their
+ *   CT_SERVICE entry (ct_lookup4 with TUPLE_F_SERVICE, no forward lookup):
+ *   CT_NEW selects slave = hash % count + 1 and creates the entry and its
+ *   ICMP entry (src_sec_id 0) -- a failed create drops the packet with
+ *   DROP_NO_SERVICE (fail closed); a hit reuses the stored slave (and
+ *   lb_loopback).  A slave whose backend is gone falls back to
+ *   lb4_lookup_service with key.slave kept, re-selects from that entry's
+ *   count and rewrites the entry's slave (ct_update4_slave); no service ->
+ *   DROP_NO_SERVICE.  Loopback (saddr == target): source NAT to
+ *   IPV4_LOOPBACK and tuple.daddr keeps the service address.
+ *   Then the egress conntrack path of cgpu_classify_v4_ct on the translated
+ *   tuple: ipcache of tuple.daddr, policy on the rewritten dport, and an
+ *   allowed CT_NEW creates its entry with the service's rev_nat_index,
+ *   slave and lb_loopback, the address entry of ct_create4 (tuple->daddr :=
+ *   backend or IPV4_LOOPBACK; conntrack.h:697-725) and the ICMP entry.
+ *   A hit entry's reverse NAT goes through the empty cilium_lb4_reverse_nat
+ *   map (a no-op, lb.h:562-576).  Ingress packets are as cgpu_classify_v4_ct.
+ * hash: skb->hash per packet (NULL: cgpu_flow_hash over the 5-tuple).
+ * Service drops: verdict -158, ct_ret CGPU_CT_NONE, identity 0, stage 6,
+ * metrics reason 158 egress.  Ordering, streams and the capacity caveat as
+ * cgpu_classify_v4_ct (an address entry's capacity is taken when its create
+ * runs).  n < 2^30.
+ */
+int cgpu_classify_v4_ctlb(cgpu_ctx *ctx, const cgpu_tuples_v4_ct *t, const uint32_t *hash, size_t n,
+			  uint32_t now, const cgpu_ctlb_out *out, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* conntrack, IPv6: the map cilium_ct6_global (CT_MAP6, bpf_lxc.c:53-63) */
 /* ------------------------------------------------------------------ */

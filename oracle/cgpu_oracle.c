@@ -2220,6 +2220,336 @@ int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 	return 0;
 }
 
+/* ---------------------------------------------------------------------- */
+/* The stateful service step (lb4_local with CONNTRACK) in front of the    */
+/* egress conntrack path                                                   */
+/* ---------------------------------------------------------------------- */
+#define CT_SERVICE 2            /* common.h:327-329 */
+#define TUPLE_F_SERVICE 4       /* conntrack.h:66 */
+#define CTB_LB_LOOPBACK 8u      /* struct ct_entry lb_loopback (common.h:389) */
+
+/* struct ct_state (common.h:368-378): what lb4_local hands the egress
+ * program's ct_create4 */
+struct ct_st {
+	uint16_t rev_nat, slave;
+	uint8_t loopback;
+	uint32_t addr, svc_addr, src_sec_id;
+};
+
+/* ct_create4 (conntrack.h:663-744) with a full ct_state: the entry carries
+ * rev_nat_index / lb_loopback / slave, and a nonzero state->addr adds the
+ * address entry (tuple->daddr := addr on egress / service, saddr on
+ * ingress; on loopback flags := TUPLE_F_IN and the other address :=
+ * svc_addr) between the forward and the ICMP entries. */
+static int ct_create_st(or_ctx *c, const struct ct_key *k, int dir, const struct ct_st *st,
+			uint32_t len, uint32_t now, uint64_t *ops)
+{
+	struct ct_val e;
+	struct ct_key ik;
+	uint8_t kb[14];
+	int tcp = k->nexthdr == PROTO_TCP;
+	memset(&e, 0, sizeof(e));
+	e.rev_nat_index = st->rev_nat;
+	if (st->loopback)
+		e.bits |= CTB_LB_LOOPBACK;
+	e.slave = st->slave;
+	ct_timeout(&e, now, tcp, dir, tcp ? 1u : 0u);
+	if (dir == CT_INGRESS) {
+		e.rx_packets = 1;
+		e.rx_bytes = len;
+	} else {
+		e.tx_packets = 1;
+		e.tx_bytes = len;
+	}
+	e.src_sec_id = st->src_sec_id;
+	ct_key_bytes(k, kb);
+	*ops += 1;
+	if (or_ct4_update(c, kb, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	if (st->addr) {
+		struct ct_key a = *k;
+		if (dir == CT_INGRESS)
+			a.saddr = st->addr;
+		else
+			a.daddr = st->addr;
+		if (st->loopback) {
+			a.flags = TUPLE_F_IN;
+			if (dir == CT_INGRESS)
+				a.daddr = st->svc_addr;
+			else
+				a.saddr = st->svc_addr;
+		}
+		ct_key_bytes(&a, kb);
+		*ops += 1;
+		if (or_ct4_update(c, kb, &e) < 0)
+			return DROP_CT_CREATE_FAILED;
+	}
+	ik.daddr = k->daddr;
+	ik.saddr = k->saddr;
+	ik.nexthdr = PROTO_ICMP;
+	ik.sport = ik.dport = 0;
+	ik.flags = k->flags | TUPLE_F_RELATED;
+	e.bits |= CTB_SEEN_NON_SYN;
+	ct_key_bytes(&ik, kb);
+	*ops += 1;
+	if (or_ct4_update(c, kb, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	return 0;
+}
+
+/* ct_lookup4's tuple setup (conntrack.h:462-530) for direction flags fl:
+ * ports from the frame (TCP/UDP: tuple->dport <- the L4 sport, tuple->sport
+ * <- the L4 dport), ICMP types.  Returns the action, or -1 for
+ * DROP_CT_UNKNOWN_PROTO. */
+static int ct4_setup(struct ct_key *k, uint8_t fl, uint8_t pr, uint16_t l4b, uint16_t fsport,
+		     uint16_t fdport, uint16_t *w)
+{
+	*w = 0;
+	k->nexthdr = pr;
+	k->flags = fl;
+	if (pr == PROTO_ICMP) {
+		uint8_t type = (uint8_t)l4b;
+		k->sport = k->dport = 0;
+		if (type == 3 || type == 11 || type == 12) {
+			k->flags |= TUPLE_F_RELATED;
+			return ACTION_UNSPEC;
+		}
+		if (type == 0) {
+			k->dport = 8;
+			return ACTION_UNSPEC;
+		}
+		if (type == 8)
+			k->sport = 8;
+		return ACTION_CREATE;
+	}
+	if (pr == PROTO_TCP || pr == PROTO_UDP) {
+		k->dport = fsport;
+		k->sport = fdport;
+		if (pr == PROTO_TCP) {
+			*w = l4b;
+			return TF_BIT0(*w) ? ACTION_CLOSE : ACTION_CREATE;
+		}
+		return ACTION_CREATE;
+	}
+	return -1;
+}
+
+/*
+ * Stateful IPv4 classification with the stateful service step, packets in
+ * order (see cgpu.h cgpu_classify_v4_ctlb and oracle/ref/harness_ctlb.c):
+ * egress packets run lb4_extract_key, lb4_lookup_service and lb4_local
+ * (lb.h:700-775: ct_lookup4 with CT_SERVICE; on CT_NEW the slave is selected
+ * from hash and the service entry created -- DROP_NO_SERVICE when that
+ * fails --, else the stored slave is used; a vanished backend falls back to
+ * lb4_lookup_service with key.slave kept and ct_update4_slave; the loopback
+ * source NAT), then the egress conntrack path of or_classify_v4_ct on the
+ * translated tuple with the service's ct_state.  xdaddr / xdport (optional):
+ * the frame's daddr / L4 dport after the service step (the dport column for
+ * other protocols).
+ */
+int or_classify_v4_ctlb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+			const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+			const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+			const uint16_t *ep, const uint32_t *hash, uint32_t now, int32_t *verdict,
+			uint8_t *ct_ret, uint32_t *identity, uint8_t *stage, uint32_t *xdaddr,
+			uint16_t *xdport, uint64_t *probe_sum)
+{
+	const or_config *cfg = &c->cfg;
+	uint64_t ops = 0;
+	for (size_t i = 0; i < n; i++) {
+		const int egress = flags[i] & 1, frag = (flags[i] >> 1) & 1;
+		const int dir = egress ? CT_EGRESS : CT_INGRESS;
+		const int mdir = egress ? METRIC_EGRESS : METRIC_INGRESS;
+		const uint8_t pr = proto[i];
+		struct ohash *h = ep[i] < c->n_ep ? &c->policy[ep[i]] : NULL;
+		struct ct_st st;
+		struct ct_key k;
+		uint32_t fdaddr = daddr[i], id = 0;
+		uint16_t fdport = dport[i], w;
+		int32_t v, fin = 0;
+		int action, ret = 255, pstage = 0;
+		struct pol_res r;
+
+		memset(&st, 0, sizeof(st));
+		k.daddr = daddr[i];
+		k.saddr = saddr[i];
+		if (egress) {
+			/* lb4_extract_key / extract_l4_port (lb.h:192-216, :590-602) */
+			uint16_t kd = 0;
+			int skip = 0;
+			const uint8_t *svc = NULL;
+			if (cfg->lb_l4) {
+				if (pr == PROTO_TCP || pr == PROTO_UDP)
+					kd = dport[i];
+				else if (pr != PROTO_ICMP && pr != PROTO_ICMPV6)
+					skip = 1; /* DROP_UNKNOWN_L4: skip_service_lookup */
+			}
+			if (!skip)
+				svc = lb_lookup_service(c, daddr[i], &kd, 0, &ops);
+			if (svc) {
+				/* lb4_local (lb.h:700-775) */
+				const uint32_t hh = hash ? hash[i] : or_flow_hash(saddr[i], daddr[i], sport[i],
+										  dport[i], pr);
+				struct ct_key sk = { daddr[i], saddr[i], 0, 0, 0, 0 };
+				uint8_t skb[14];
+				const uint8_t *be;
+				int sret = -1;
+				action = ct4_setup(&sk, TUPLE_F_SERVICE, pr, l4b[i], sport[i], dport[i], &w);
+				if (action >= 0) {
+					ct_key_bytes(&sk, skb);
+					ops += 1;
+					if (ct_lookup_kb(&c->ct, skb, action, CT_SERVICE, pr == PROTO_TCP, w, len[i],
+							 now)) {
+						struct ct_val e;
+						memcpy(&e, oh_get(&c->ct, skb), 56);
+						st.rev_nat = e.rev_nat_index;
+						st.loopback = (e.bits & CTB_LB_LOOPBACK) ? 1 : 0;
+						st.slave = e.slave;
+						sret = 0;
+					} else {
+						st.slave = (uint16_t)(hh % lbv_count(svc) + 1); /* lb4_select_slave */
+						sret = ct_create_st(c, &sk, CT_SERVICE, &st, len[i], now, &ops);
+					}
+				}
+				if (sret < 0) {
+					fin = DROP_NO_SERVICE;
+					goto service_drop;
+				}
+				be = lb_get(c, daddr[i], kd, st.slave, &ops); /* lb4_lookup_slave */
+				if (!be) {
+					be = lb_lookup_service(c, daddr[i], &kd, st.slave, &ops);
+					if (!be) {
+						fin = DROP_NO_SERVICE;
+						goto service_drop;
+					}
+					st.slave = (uint16_t)(hh % lbv_count(be) + 1);
+					{ /* ct_update4_slave (conntrack.h:649-661) */
+						uint8_t *p = oh_get(&c->ct, skb);
+						ops += 1;
+						if (p)
+							memcpy(p + 40, &st.slave, 2); /* ct_entry.slave */
+					}
+				}
+				st.rev_nat = lbv_rev_nat(be);
+				st.addr = lbv_target(be);
+				fdaddr = lbv_target(be);
+				if (saddr[i] == lbv_target(be)) { /* loopback (lb.h:753-767) */
+					st.loopback = 1;
+					st.addr = cfg->ipv4_loopback;
+					st.svc_addr = saddr[i];
+				}
+				if (!st.loopback)
+					k.daddr = lbv_target(be);
+				/* lb4_xlate port rewrite (lb.h:685-694) */
+				if (cfg->lb_l4 && lbv_port(be) && kd != lbv_port(be) &&
+				    (pr == PROTO_TCP || pr == PROTO_UDP))
+					fdport = lbv_port(be);
+			}
+		}
+		/* ct_lookup4 (CT_EGRESS / CT_INGRESS) on the frame as it is now */
+		action = ct4_setup(&k, egress ? TUPLE_F_IN : TUPLE_F_OUT, pr, l4b[i], sport[i], fdport, &w);
+		if (action < 0) {
+			fin = DROP_CT_UNKNOWN_PROTO;
+			pstage = 4;
+			goto out;
+		}
+		{
+			const uint32_t orig_dip = k.daddr;
+			ops += 1;
+			if (ct_lookup_one(c, &k, action, dir, pr == PROTO_TCP, w, len[i], now)) {
+				ret = (k.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+			} else {
+				ct_reverse(&k);
+				ops += 1;
+				ret = ct_lookup_one(c, &k, action, dir, pr == PROTO_TCP, w, len[i], now)
+					      ? CT_ESTABLISHED
+					      : CT_NEW;
+			}
+			if (egress) { /* bpf_lxc.c:484-500 */
+				const uint8_t *info = ipcache4(c, orig_dip);
+				uint32_t label = 0;
+				if (info)
+					memcpy(&label, info, 4);
+				if (info && label)
+					id = label;
+				else if ((orig_dip & cfg->ipv4_cluster_mask) == cfg->ipv4_cluster_range)
+					id = cfg->cluster_id;
+				else
+					id = cfg->world_id;
+				ops += 1;
+				r = policy_access(h, id, k.dport, pr, 1, 0, len[i]);
+			} else { /* bpf_netdev.c:374-404 */
+				uint32_t src = cfg->ingress_src_identity;
+				if (src < cfg->health_id) {
+					const uint8_t *info = ipcache4(c, saddr[i]);
+					ops += 1;
+					if (info) {
+						uint32_t label;
+						memcpy(&label, info, 4);
+						if (label && label != cfg->cluster_id && label != cfg->host_id)
+							src = label;
+					}
+				}
+				id = cfg->ingress_secctx_world ? cfg->world_id : src;
+				r = policy_access(h, id, k.dport, pr, 0, frag, len[i]);
+			}
+		}
+		ops += (uint64_t)r.probes;
+		pstage = r.stage;
+		v = r.ret >= 0 ? r.ret : DROP_POLICY;
+		if (ret != CT_REPLY && ret != CT_RELATED && v < 0) {
+			if (ret == CT_ESTABLISHED) {
+				uint8_t kb[14];
+				ct_key_bytes(&k, kb);
+				ops += 1;
+				oh_delete(&c->ct, kb);
+			}
+			fin = DROP_POLICY;
+		} else {
+			int cr = 0;
+			if (ret == CT_NEW) {
+				uint32_t sec = 0;
+				if (egress && ep[i] < c->n_lxcinfo)
+					memcpy(&sec, c->lxcinfo + (size_t)ep[i] * 32 + 28, 4); /* SECLABEL */
+				st.src_sec_id = egress ? sec : id;
+				cr = ct_create_st(c, &k, dir, &st, len[i], now, &ops);
+			}
+			/* CT_REPLY / CT_RELATED with rev_nat_index: lb4_rev_nat through the
+			 * empty cilium_lb4_reverse_nat map, a no-op (lb.h:562-576) */
+			if (cr < 0)
+				fin = cr;
+			else if (v > 0 && (egress || ret == CT_NEW || ret == CT_ESTABLISHED))
+				fin = v;
+			else
+				fin = 0;
+		}
+		goto out;
+	service_drop:
+		pstage = 6;
+		id = 0;
+		ret = 255;
+	out:
+		verdict[i] = fin;
+		ct_ret[i] = (uint8_t)ret;
+		if (identity)
+			identity[i] = id;
+		if (stage)
+			stage[i] = (uint8_t)pstage;
+		if (xdaddr)
+			xdaddr[i] = fdaddr;
+		if (xdport)
+			xdport[i] = fdport;
+		if (fin <= 0) {
+			uint32_t reason = fin < 0 ? (uint32_t)(-fin) & 0xff : 0;
+			c->metrics[(reason * 4 + mdir) * 2] += 1;
+			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
+		}
+	}
+	if (probe_sum)
+		*probe_sum = ops;
+	return 0;
+}
+
 /* ====================================================================== */
 /* L3 MapState compilation                              */
 /* ====================================================================== */

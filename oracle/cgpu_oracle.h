@@ -219,6 +219,20 @@ int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 		      uint32_t *identity, uint8_t *stage, uint64_t *probe_sum);
 
 /*
+ * or_classify_v4_ct with the stateful service step of handle_ipv4_from_lxc
+ * in front (lb4_local with CONNTRACK, lb.h:700-775; see cgpu.h
+ * cgpu_classify_v4_ctlb).  hash: skb->hash per packet (NULL: or_flow_hash);
+ * xdaddr / xdport (optional): the frame's daddr / dport after the service
+ * step.  Service drops: DROP_NO_SERVICE, ct_ret 255, stage 6, identity 0.
+ */
+int or_classify_v4_ctlb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+			const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+			const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+			const uint16_t *ep, const uint32_t *hash, uint32_t now, int32_t *verdict,
+			uint8_t *ct_ret, uint32_t *identity, uint8_t *stage, uint32_t *xdaddr,
+			uint16_t *xdport, uint64_t *probe_sum);
+
+/*
  * L3 MapState compilation: the tables of cgpu.h
  * cgpu_l3_program / cgpu_label_sets (interned ids, see cilium_amd/policy.py);
  * allow[e * n_id + i] bit 0 = ingress Allowed, bit 1 = egress Allowed.

@@ -178,6 +178,12 @@ int ref_ctlb_policy_read(int ep, const void *key, void *entry_out)
 	memcpy(entry_out, v, sizeof(struct policy_entry));
 	return 0;
 }
+int ref_ctlb_policy_delete(int ep, const void *key)
+{
+	return (ep < 0 || ep >= REF_MAX_EP) ? -1 : (mockmap_delete(&policy_maps[ep], key) ? 0 : -2);
+}
+/* a conntrack entry installed by the agent (bpf(2) BPF_ANY) */
+int ref_ctlb_ct_update(const void *key, const void *val) { ensure_init(); return mock_update(&ct_map4, key, val, 0); }
 int ref_ctlb_ipcache_update(const void *key, const void *info) { ensure_init(); return mockmap_update(&ipcache, key, info); }
 int ref_ctlb_svc_update(const void *key, const void *val) { ensure_init(); return mockmap_update(&svc_m, key, val); }
 int ref_ctlb_svc_delete(const void *key) { ensure_init(); return mockmap_delete(&svc_m, key) ? 0 : -2; }

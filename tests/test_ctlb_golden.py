@@ -1,0 +1,109 @@
+"""Pin the CPU restatement of the stateful service step (oracle/cgpu_oracle.c
+or_classify_v4_ctlb; VERDICT r2 next 7, SURVEY §8f rows 1 + 3) to the
+reference.
+
+tests/golden/ctlb4.npz was produced by the reference's own bpf/lib/lb.h
+(lb4_extract_key, lb4_lookup_service, lb4_local with CONNTRACK),
+conntrack.h, policy.h and eps.h compiled as host C under the endpoint config
+and driven packet by packet in handle_ipv4_from_lxc / ipv4_policy order
+(oracle/ref/harness_ctlb.c).  The stream spans 4 batches: CT entries
+(forward and CT_SERVICE ones, some with slave 0, slaves past the backends or
+the lb_loopback bit) installed beforehand, policy keys and a third of the
+service backends deleted before batch 2, half of those backends re-added
+with new targets before batch 3; a second run uses a 48-entry CT map.
+Bit-exact: verdict, ct_lookup4 result, identity, stage, the frame's
+translated daddr / dport, the whole CT map after every batch (service,
+address and ICMP entries included) and the policy entry counters.
+"""
+import numpy as np
+
+from cilium_amd import layouts as L
+from oracle import Oracle
+
+DROP_NO_SERVICE = -158
+
+
+def ctlb_oracle(g, ct_max=1 << 20):
+    o = Oracle()
+    o.ct_set_max(ct_max)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert o.ipcache_update(k, v) == 0
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert o.policy_update(int(ep), k, e) == 0
+    for ep, sl in enumerate(g["seclabels"]):
+        assert o.lxc_update(ep, L.lxc_info(b"\0" * 6, 0, b"\0" * 16, 0, int(sl))) == 0
+    for k, v in zip(g["lb_keys"], g["lb_vals"]):
+        assert o.lb_update(k, v) == 0
+    return o
+
+
+def stream(g, prefix="t_"):
+    return {k[len(prefix):]: g[k] for k in g.files if k.startswith(prefix)}
+
+
+def check(out, g, p, sl, msg):
+    t = stream(g, "t_" if p == "b_" else "t2_")
+    for f in ("verdict", "ct_ret", "identity", "stage", "xdaddr"):
+        np.testing.assert_array_equal(out[f], g[p + f][sl], err_msg=f"{msg} {f}")
+    # the harness reads the frame's L4 bytes 2-3: the dport only for TCP/UDP
+    # (egress); ingress reports the column unchanged
+    pr = t["proto"][sl]
+    eg = (t["flags"][sl] & 1).astype(bool)
+    m = ~eg | np.isin(pr, [6, 17])
+    np.testing.assert_array_equal(out["xdport"][m], g[p + "xdport"][sl][m], err_msg=f"{msg} xdport")
+
+
+def test_ctlb_stream_vs_reference(golden):
+    g = golden("ctlb4.npz")
+    o = ctlb_oracle(g)
+    for k, v in zip(g["pre_keys"], g["pre_vals"]):
+        assert o.ct4_update(k, v) == 0
+    t = stream(g)
+    cuts, nows = g["cuts"], g["nows"]
+    off = 0
+    for bi in range(4):
+        if bi == 2:
+            for d in g["pol_del"]:
+                assert o.policy_delete(int(g["pol_ep"][d]), g["pol_keys"][d]) == 0
+            for d in g["svc_del"]:
+                assert o.lb_delete(g["lb_keys"][d]) == 0
+        if bi == 3:
+            for d, v in zip(g["svc_readd"], g["readd_vals"]):
+                assert o.lb_update(g["lb_keys"][d], v) == 0
+        sl = slice(int(cuts[bi]), int(cuts[bi + 1]))
+        out = o.classify_v4_ctlb({k: v[sl] for k, v in t.items()}, int(nows[bi]))
+        check(out, g, "b_", sl, f"batch {bi}")
+        n = int(g["dump_n"][bi])
+        keys, vals = o.ct4_dump()
+        np.testing.assert_array_equal(keys, g["dump_keys"][off:off + n], err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(vals, g["dump_vals"][off:off + n], err_msg=f"batch {bi}")
+        off += n
+    for i, (k, ep, fe) in enumerate(zip(g["pol_keys"], g["pol_ep"], g["final_entries"])):
+        rc, raw = o.policy_lookup(int(ep), k)
+        if i in set(g["pol_del"].tolist()):
+            assert rc != 0
+            continue
+        got = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (got["packets"], got["bytes"]) == (fe["packets"], fe["bytes"])
+    # the fixture reaches every branch of lb4_local
+    v, svc = g["b_verdict"], g["b_svc_hit"].astype(bool)
+    assert (svc & (v == DROP_NO_SERVICE)).sum() > 0          # vanished backend, no fallback
+    assert (svc & (g["b_xdaddr"] != t["daddr"])).sum() > 0    # translated
+    keys = g["dump_keys"]
+    assert (keys["flags"] == 4).sum() > 0                    # CT_SERVICE entries
+    assert (keys["flags"] == 6).sum() > 0                    # their ICMP entries
+    vals = g["dump_vals"]
+    assert ((vals["bits"] & 8) != 0).sum() > 0               # lb_loopback entries
+
+
+def test_ctlb_small_map_vs_reference(golden):
+    g = golden("ctlb4.npz")
+    o = ctlb_oracle(g, ct_max=48)
+    out = o.classify_v4_ctlb(stream(g, "t2_"), 500)
+    check(out, g, "s_", slice(None), "small map")
+    keys, vals = o.ct4_dump()
+    np.testing.assert_array_equal(keys, g["s_dump_keys"])
+    np.testing.assert_array_equal(vals, g["s_dump_vals"])
+    assert (g["s_verdict"] == DROP_NO_SERVICE).sum() > 0
+    assert (g["s_verdict"] == L.DROP_CT_CREATE_FAILED).sum() > 0
+    assert o.ct4_count() == 48
