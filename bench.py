@@ -31,6 +31,12 @@ Other BASELINE configs (not the headline line; run them explicitly):
                      updates and reply-skips the same way; parity and the
                      CPU baseline on the packets of 1/64 of the address pairs
                      (pairs are independent conntrack groups)
+  --config ctlb      config 2 tables + 1M services + conntrack behind the
+                     STATEFUL service step (cgpu_classify_v4_ctlb: lb4_local
+                     with CONNTRACK, CT_SERVICE entries, stored slaves,
+                     ct_create4's address entries): 16M packets of 500k
+                     connections (40 % to services), map emptied each step;
+                     parity and the CPU baseline on the whole batch
   --config ct6       the same over IPv6 (cilium_ct6_global, cgpu_classify_v6_ct):
                      100k IPv6 ipcache prefixes + 64k policy keys, 64M packets
                      of 2M connections, parity on 1/64 of the address pairs
@@ -111,6 +117,11 @@ WORKLOADS = {
           "per GPU of 2M TCP/UDP/ICMP connections (~32 packets each, both directions, ICMP errors), "
           "map emptied each step: ct_lookup4 -> ipcache -> policy -> reply/related skip, "
           "ct_create4 / delete, bit-exact",
+    "ctlb": "config2 tables + 1M IPv4 services + stateful conntrack behind the stateful service step "
+            "(cgpu_classify_v4_ctlb, lb4_local with CONNTRACK): 16M packets per GPU of 500k "
+            "connections (~32 packets each, 40 % to services, 2 % loopback backends), map emptied "
+            "each step: CT_SERVICE lookup/create + slave reuse -> ct_lookup4 -> ipcache -> policy -> "
+            "ct_create4 with the service's state and address entry, bit-exact",
     "ct6": "IPv6 tables at config-2 size (100k IPv6 ipcache prefixes + 64k policy entries) + stateful "
            "conntrack (cilium_ct6_global): 64M packets per GPU of 2M TCP/UDP/ICMPv6 connections, map "
            "emptied each step: ct_lookup6 -> ipcache6 -> policy -> reply/related skip, ct_create6 / "
@@ -156,10 +167,11 @@ def main():
     cascade = args.config == "cascade"
     frames = args.config == "frames"
     ct6 = args.config == "ct6"
-    ct = args.config == "ct" or ct6
+    ctlb = args.config == "ctlb"
+    ct = args.config == "ct" or ct6 or ctlb
     v6 = args.config == "v6"
     cfg = synth.CONFIGS["v6" if ct6 else "gpu" if (pf6 or frames or ct) else args.config]
-    n = args.tuples or cfg["n_tuples"]
+    n = args.tuples or (1 << 24 if ctlb else cfg["n_tuples"])
     t0 = time.time()
     S = None
     if pf6:
@@ -173,18 +185,28 @@ def main():
         T = synth.make_tables6(**cfg) if ct6 else synth.make_tables(**cfg)
         # each rank's stream is its conntrack shard (address pairs with
         # pairhash % world == rank): per-rank maps, no shared state
-        mk = synth.make_ct6_workload if ct6 else synth.make_ct_workload
-        tup, _, seclabels = mk(T, n // CT_PKTS_PER_CONN, gpu_id=rank, mean_pkts=CT_PKTS_PER_CONN,
-                               world=world)
+        if ctlb:
+            S = synth.make_services(T, synth.CONFIGS["cascade"]["n_services"])
+            tup, _, seclabels, S = synth.make_ctlb_workload(T, S, n // CT_PKTS_PER_CONN, gpu_id=rank,
+                                                            mean_pkts=CT_PKTS_PER_CONN, world=world)
+        else:
+            mk = synth.make_ct6_workload if ct6 else synth.make_ct_workload
+            tup, _, seclabels = mk(T, n // CT_PKTS_PER_CONN, gpu_id=rank, mean_pkts=CT_PKTS_PER_CONN,
+                                   world=world)
         n = min(n, len(tup["saddr"]))
         tup = {k: np.ascontiguousarray(v[:n]) for k, v in tup.items()}
         ct_max = 1 << max(20, int(np.ceil(np.log2(2.5 * n / CT_PKTS_PER_CONN))))
         log(f"[rank {rank}] synthetic tables ({len(T.ipc_keys)} ipcache, {len(T.pol_keys)} policy) "
             f"+ {n} packets of {n // CT_PKTS_PER_CONN} connections in {time.time() - t0:.1f}s, "
             f"ct_max {ct_max}")
-        e = Engine(device=local, **T.engine_config(), ct_max=ct_max)
+        ecfg = T.engine_config()
+        if S is not None:
+            ecfg["lb_max_entries"] = len(S.keys)
+        e = Engine(device=local, **ecfg, ct_max=ct_max)
         synth.load_engine(e, T)
         synth.load_lxc(e, seclabels)
+        if S is not None:
+            synth.load_services(e, S)
     elif v6:
         T = synth.make_tables6(**cfg)
         tup = synth.make_tuples6(T, n, gpu_id=rank)
@@ -250,6 +272,8 @@ def main():
     def launch():
         if ct6:
             e.classify_v6_ct(d, CT_NOW, out=out, stream=stream)
+        elif ctlb:
+            e.classify_v4_ctlb(d, CT_NOW, out=out, xlate=False, stream=stream)
         elif ct:
             e.classify_v4_ct(d, CT_NOW, out=out, stream=stream)
         elif pf6:
@@ -356,6 +380,8 @@ def main():
             synth.load_lxc(o, seclabels)
             o.ct_set_max(ct_max)
             o.ct6_set_max(ct_max)
+            if S is not None:
+                synth.load_services(o, S)
         else:
             o = Oracle(**T.oracle_config())
             synth.load_oracle(o, T)
@@ -373,7 +399,12 @@ def main():
                 return o.classify_frames({k: v[sl] for k, v in fr.items()}, nthreads=threads)
             return o.classify_v4({k: v[sl] for k, v in tup.items()}, nthreads=threads)
 
-        if ct:
+        if ctlb:
+            # the service step ties pairs together (a service's connections
+            # land on its backends' pairs): the whole batch, sequentially
+            sub = np.arange(n)
+            tsub = tup
+        elif ct:
             # conntrack groups (unordered address pairs) are independent: the
             # packets of 1 in CT_SAMPLE pairs, in batch order, replayed by the
             # sequential restatement from an empty map are the reference's
@@ -392,7 +423,10 @@ def main():
         runs = []
         for rep in range(3):
             c0 = time.perf_counter()
-            if ct:
+            if ctlb:
+                r_ = o.classify_v4_ctlb(tsub, CT_NOW)
+                res = (r_["verdict"], r_["ct_ret"], r_["identity"], r_["stage"], r_["probes"])
+            elif ct:
                 res = (o.classify_v6_ct if ct6 else o.classify_v4_ct)(tsub, CT_NOW)
             elif pf6:
                 res = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
@@ -421,9 +455,11 @@ def main():
         if not skip_cpu and ct:
             cpu = {"value": round(n_cpu / c_el / 1e6, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
-                   "sample": f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
-                             f"pairs from an empty map; oracle/cgpu_oracle.c "
-                             f"or_classify_v{6 if ct6 else 4}_ct "
+                   "sample": (f"rank-0 batch, all {n_cpu} packets from an empty map; "
+                              f"oracle/cgpu_oracle.c or_classify_v4_ctlb " if ctlb else
+                              f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
+                              f"pairs from an empty map; oracle/cgpu_oracle.c "
+                              f"or_classify_v{6 if ct6 else 4}_ct ") +
                              f"(sequential conntrack + LPM trie + open hash), 1 thread, "
                              f"{c_el:.2f}s wall (one run); host: {host_cpu()}"}
         elif not skip_cpu:
@@ -447,7 +483,7 @@ def main():
                 parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
         probes_per = probes / n_cpu
         b_in, b_out = ((B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN_FRAMES, B_OUT) if frames
-                       else (B_IN_CT6, B_OUT_CT) if ct6 else (B_IN_CT, B_OUT_CT) if ct
+                       else (B_IN_CT6, B_OUT_CT) if ct6 else (B_IN_CT + (4 if ctlb else 0), B_OUT_CT) if ct
                        else (B_IN_V6, B_OUT) if v6
                        else (B_IN + (2 if cascade else 0), B_OUT))
         b_alg = b_in + b_out + 64.0 * probes_per

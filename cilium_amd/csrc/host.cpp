@@ -3905,7 +3905,21 @@ CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n
 		      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
 		      verdict, identity, stage, delta, P.pk};
 	HIP_OR_EIO(hipSetDevice(c->device));
-	HIP_OR_EIO(launch_classify_frames(s, a, (hipStream_t)stream));
+	const hipStream_t st = (hipStream_t)stream;
+	const bool x4 = !(s.schedule & (CGPU_SCHED_PER_LANE | CGPU_SCHED_GLOBAL_CTR)) &&
+			!(((uintptr_t)f->len | (uintptr_t)verdict | (uintptr_t)identity) & 15) &&
+			!((uintptr_t)f->ep & 7) && !((uintptr_t)stage & 3);
+	if (!x4) {
+		HIP_OR_EIO(launch_classify_frames(s, a, st));
+		return 0;
+	}
+	/* the parsed columns: stream-ordered scratch from the context's memory
+	 * pool (which keeps freed memory for the next call, cgpu_ctx_create) */
+	void *scr = nullptr;
+	HIP_OR_EIO(hipMallocFromPoolAsync(&scr, frames_x4_bytes(n), c->pool, st));
+	const hipError_t e = launch_classify_frames_x4(s, a, frames_x4_carve(scr, n), st);
+	HIP_OR_EIO(hipFreeAsync(scr, st));
+	HIP_OR_EIO(e);
 	return 0;
 }
 

@@ -866,6 +866,9 @@ struct cls_args {
 	const uint16_t *sport;
 	const uint32_t *hash;
 	uint32_t cc_n; /* k_classify_x4: cold-slot cache entries in LDS (power of 2, or 0) */
+	/* k_classify_x4 FR (frames): the tuple count is *n_dev - n_off, at most n */
+	const uint32_t *n_dev;
+	uint64_t n_off;
 };
 
 /* The identity resolution and the three-probe policy cascade for one tuple
@@ -1298,11 +1301,26 @@ __device__ __forceinline__ void v6_lookup_coop(const v6_lpm &t, const uint32_t *
  * aligned 2-byte columns and 4-byte aligned 1-byte columns; the one partial
  * group at the end of the batch is read element by element.
  */
-template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false>
-__global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a, uint64_t *pk)
+/* frames on the x4 schedule (launch_classify_frames): flag bits of the
+ * parsed columns.  FRF_DEC: the parse ended the frame (daddr column = its
+ * status); FRF_V6: an IPv6 frame, classified by the compacted v6 pass */
+#define FRAME_NOT_CLASSIFIED 1   /* CGPU_FRAME_NOT_CLASSIFIED */
+#define DROP_SNAPLEN (-4096)     /* CGPU_DROP_SNAPLEN */
+#define FRF_DEC 0x80u
+#define FRF_V6 0x40u
+
+template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false,
+	  bool FR = false>
+__global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a0, uint64_t *pk)
 {
+	cls_args a = a0;
+	if (FR && a0.n_dev) {
+		const uint64_t c = *a0.n_dev;
+		a.n = c > a0.n_off ? min(c - a0.n_off, a0.n) : 0;
+	}
 	/* per-tuple flag word */
-	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u, F_LBDROP = 32u;
+	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u, F_LBDROP = 32u,
+			   F_DEC = 64u;
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* drop metrics (send_drop_notify -> update_metrics, drop.h:94-118):
 	 * [reason 133 / 137 / 158][ingress, egress] x {count, bytes} in LDS
@@ -1361,7 +1379,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		/* QA: the vector-load branches below are written for Q = 4; arrays
 		 * they fill are sized for them whatever Q (dead when Q != 4) */
 		constexpr int QA = Q < 4 ? 4 : Q;
-		uint32_t fw[Q], ad[Q], hi4[Q], ep[QA], len[QA];
+		uint32_t fw[Q], ad[Q], hi4[Q], ep[QA], len[QA], dstat[Q];
 		uint4 ad6[Q];
 		{
 			uint32_t fl[QA], proto[QA], dport[QA], sa[QA], da[QA];
@@ -1498,6 +1516,12 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
 				const bool eg = fl[u] & 1u;
+				/* frames: a frame the parse ended runs no lookup (F_GATED
+				 * masks them) and reports its status (dstat) */
+				const bool dec = FR && !V6 && (fl[u] & (FRF_DEC | FRF_V6));
+				dstat[u] = (fl[u] & FRF_V6) ? 0u : da[u];
+				if (dec)
+					lbf[u] |= F_DEC | F_GATED;
 				/* ct_lookup{4,6} protocol gate: ICMP (v4: 1, v6: 58), TCP, UDP */
 				const bool gated = s.ct_proto_gate && proto[u] != (V6 ? 58u : 1u) && proto[u] != 6u &&
 						   proto[u] != 17u;
@@ -1676,8 +1700,29 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 			}
 		/* counters, outputs, metrics */
 		int32_t v[QA];
+		uint64_t *metg = a.delta + 2ull * s.n_ctr_slots;
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
+			if (FR && (fw[u] & F_DEC)) {
+				/* k_frames' rules: NOT_CLASSIFIED counts nothing (stage 7), an
+				 * IPv6 frame's placeholder is overwritten by the v6 pass */
+				id[u] = 0;
+				const int32_t sv = (int32_t)dstat[u];
+				if (sv == 0 || sv == FRAME_NOT_CLASSIFIED) {
+					v[u] = 0;
+					st[u] = sv ? 7u : 0u;
+				} else {
+					v[u] = sv;
+					st[u] = sv == DROP_CT_UNKNOWN_PROTO ? 4u : 5u;
+					if (sv != DROP_SNAPLEN) {
+						const uint32_t reason = (uint32_t)(-sv) & 0xffu;
+						const uint32_t key = (reason * 4u + ((fw[u] & F_EG) ? 2u : 1u)) * 2u;
+						atomicAdd((unsigned long long *)&metg[key], 1ull);
+						atomicAdd((unsigned long long *)&metg[key + 1], (unsigned long long)len[u]);
+					}
+				}
+				continue;
+			}
 			if (fw[u] & F_LBDROP) {
 				v[u] = DROP_NO_SERVICE;
 				id[u] = 0;
@@ -1821,8 +1866,6 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #define DROP_INVALID_EXTHDR (-156)
 #define DROP_FRAG_NOSUPPORT (-157)
 #define EFAULT_LOAD (-14)        /* bpf_skb_load_bytes past skb->len */
-#define FRAME_NOT_CLASSIFIED 1   /* CGPU_FRAME_NOT_CLASSIFIED */
-#define DROP_SNAPLEN (-4096)     /* CGPU_DROP_SNAPLEN */
 
 /* The first 64 bytes of a frame slot as 16 little-endian words: Ethernet,
  * the IPv4 header without options / the IPv6 header, and the L4 type and
@@ -2607,7 +2650,7 @@ static cgpu_snapshot with_lds_hot(const cgpu_snapshot &s, size_t max_hot)
 	return r;
 }
 
-template <bool LB, bool V6>
+template <bool LB, bool V6, bool FR = false>
 static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024;
@@ -2632,7 +2675,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 	lds += CGPU_DIAG_LDS_PAD;
 #endif
 	constexpr int Q = V6 ? 2 : 4; /* v6: Q = 4 spills (16-byte addresses, 64-byte buckets) */
-	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6>;
+	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR>;
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
@@ -2656,8 +2699,9 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 			c.sport += off;
 		if (c.hash)
 			c.hash += off;
+		c.n_off = off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + Q * NT - 1) / (Q * NT), res);
-		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6, FR>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
@@ -2786,6 +2830,131 @@ hipError_t launch_prefilter_v6(const cgpu_snapshot &s, const prefilter_args &a, 
 hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hipStream_t st)
 {
 	hipLaunchKernelGGL((k_frames<0, BLOCK>), dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a);
+	return hipGetLastError();
+}
+
+/* frames -> the x4 schedule: the header parse writes policy-tuple columns
+ * (IPv4 frames in place, frames the parse ended flagged FRF_DEC with their
+ * status, IPv6 frames compacted to their own columns with their index),
+ * then k_classify_x4 runs over the IPv4 columns and, on the device-side
+ * count, over the IPv6 ones, whose results are scattered back */
+__global__ __launch_bounds__(256) void k_frames_cols(cgpu_snapshot s, frames_args a, frames_x4 c)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t len = a.len[i];
+		const bool egress = a.flags[i] & 1u;
+		const uint32_t ep = a.ep[i];
+		const ftuple t = parse_frame(s, a.data + i * (uint64_t)a.stride, len, min(len, a.stride), egress, ep);
+		uint32_t fl = egress ? 1u : 0u, sa = 0, da = 0, dp = 0, pr = 0;
+		const bool v6 = t.status == 0 && t.fam != 4u;
+		if (t.status != 0) {
+			fl |= FRF_DEC;
+			da = (uint32_t)t.status;
+		} else if (!v6) {
+			sa = t.sa.x;
+			da = t.da.x;
+			dp = t.dport;
+			pr = t.proto;
+			fl |= t.frag ? 2u : 0u;
+		} else {
+			fl |= FRF_V6;
+		}
+		/* wave-aggregated slot of the IPv6 frames */
+		const uint64_t m = __ballot(v6);
+		if (m) {
+			const int leader = __ffsll((unsigned long long)m) - 1;
+			uint32_t base = 0;
+			if ((int)__lane_id() == leader)
+				base = atomicAdd(c.n6, (uint32_t)__popcll(m));
+			base = __shfl(base, leader, 64);
+			if (v6) {
+				const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+				c.sa6[j] = t.sa;
+				c.da6[j] = t.da;
+				c.dport6[j] = (uint16_t)t.dport;
+				c.proto6[j] = (uint8_t)t.proto;
+				c.fl6[j] = (uint8_t)(egress ? 1u : 0u);
+				c.len6[j] = len;
+				c.ep6[j] = (uint16_t)ep;
+				c.idx6[j] = (uint32_t)i;
+			}
+		}
+		c.sa4[i] = sa;
+		c.da4[i] = da;
+		c.dport[i] = (uint16_t)dp;
+		c.proto[i] = (uint8_t)pr;
+		c.fl[i] = (uint8_t)fl;
+	}
+}
+
+__global__ __launch_bounds__(256) void k_frames_scatter6(frames_x4 c, int32_t *verdict, uint32_t *identity,
+							 uint8_t *stage)
+{
+	const uint32_t n6 = *c.n6;
+	for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < n6; j += gridDim.x * 256u) {
+		const uint32_t i = c.idx6[j];
+		verdict[i] = c.v6[j];
+		identity[i] = c.id6[j];
+		if (stage)
+			stage[i] = c.st6[j];
+	}
+}
+
+static size_t frames_x4_layout(uint64_t n, size_t *off)
+{
+	/* column element sizes, each column rounded to 256 bytes */
+	static const size_t el[17] = {4, 4, 2, 1, 1, 16, 16, 2, 1, 1, 4, 2, 4, 4, 4, 1, 4};
+	size_t t = 0;
+	for (int k = 0; k < 17; k++) {
+		off[k] = t;
+		t += ((k == 16 ? 1 : n) * el[k] + 255) & ~(size_t)255;
+	}
+	return t;
+}
+
+size_t frames_x4_bytes(uint64_t n)
+{
+	size_t off[17];
+	return frames_x4_layout(n, off);
+}
+
+frames_x4 frames_x4_carve(void *base, uint64_t n)
+{
+	size_t o[17];
+	frames_x4_layout(n, o);
+	char *b = static_cast<char *>(base);
+	return frames_x4{reinterpret_cast<uint32_t *>(b + o[0]), reinterpret_cast<uint32_t *>(b + o[1]),
+			 reinterpret_cast<uint16_t *>(b + o[2]), reinterpret_cast<uint8_t *>(b + o[3]),
+			 reinterpret_cast<uint8_t *>(b + o[4]), reinterpret_cast<uint4 *>(b + o[5]),
+			 reinterpret_cast<uint4 *>(b + o[6]), reinterpret_cast<uint16_t *>(b + o[7]),
+			 reinterpret_cast<uint8_t *>(b + o[8]), reinterpret_cast<uint8_t *>(b + o[9]),
+			 reinterpret_cast<uint32_t *>(b + o[10]), reinterpret_cast<uint16_t *>(b + o[11]),
+			 reinterpret_cast<uint32_t *>(b + o[12]), reinterpret_cast<int32_t *>(b + o[13]),
+			 reinterpret_cast<uint32_t *>(b + o[14]), reinterpret_cast<uint8_t *>(b + o[15]),
+			 reinterpret_cast<uint32_t *>(b + o[16])};
+}
+
+hipError_t launch_classify_frames_x4(const cgpu_snapshot &s, const frames_args &a, const frames_x4 &c,
+				     hipStream_t st)
+{
+	hipError_t e = hipMemsetAsync(c.n6, 0, 4, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_frames_cols, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a, c);
+	cls_args c4{c.sa4, c.da4, c.dport, c.proto, c.fl, a.len, a.ep, a.verdict, a.identity, a.stage,
+		    a.delta, a.n, a.pk, 0, nullptr, nullptr};
+	if (!x4_aligned(c4))
+		return hipErrorInvalidValue;
+	if ((e = launch_x4<false, false, true>(s, c4, st)) != hipSuccess)
+		return e;
+	cls_args c6{c.sa6, c.da6, c.dport6, c.proto6, c.fl6, c.len6, c.ep6, c.v6, c.id6,
+		    a.stage ? c.st6 : nullptr, a.delta, a.n, a.pk, 0, nullptr, nullptr};
+	c6.n_dev = c.n6;
+	if ((e = launch_x4<false, true, true>(s, c6, st)) != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_frames_scatter6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, c, a.verdict, a.identity,
+			   a.stage);
 	return hipGetLastError();
 }
 
@@ -3467,7 +3636,10 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 				 * against the packet's own {saddr, daddr} */
 				const uint32_t b = lb ? saddr2 : da;
 				const bool same = (addr == sa && b == da) || (addr == da && b == sa);
-				lbf = (lb ? LBF_LOOPBACK : 0u) | ((same || SERIAL ? AM_INLINE : AM_DEFER) << 1);
+				/* ct_create4 writes no address entry for addr 0 (a slave-0
+				 * master row carries target 0), conntrack.h:697 */
+				const uint32_t am = !addr ? AM_NONE : (same || SERIAL) ? AM_INLINE : AM_DEFER;
+				lbf = (lb ? LBF_LOOPBACK : 0u) | (am << 1);
 				r2x = (so.z >> 16) | (so.x & 0xFFFF0000u);
 			}
 			if (a.xdaddr)

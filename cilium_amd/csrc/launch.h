@@ -97,6 +97,30 @@ struct frames_args {
 };
 
 hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hipStream_t st);
+
+/* scratch of the frames x4 schedule (launch_classify_frames_x4): the IPv4
+ * policy-tuple columns [n] and the compacted IPv6 ones [n] with their
+ * results; every column 16-byte aligned */
+struct frames_x4 {
+	uint32_t *sa4, *da4;
+	uint16_t *dport;
+	uint8_t *proto, *fl;
+	uint4 *sa6, *da6;
+	uint16_t *dport6;
+	uint8_t *proto6, *fl6;
+	uint32_t *len6;
+	uint16_t *ep6;
+	uint32_t *idx6;
+	int32_t *v6;
+	uint32_t *id6;
+	uint8_t *st6;
+	uint32_t *n6;
+};
+/* bytes of that scratch for n frames, and its carving */
+size_t frames_x4_bytes(uint64_t n);
+frames_x4 frames_x4_carve(void *base, uint64_t n);
+hipError_t launch_classify_frames_x4(const cgpu_snapshot &s, const frames_args &a, const frames_x4 &c,
+				     hipStream_t st);
 hipError_t launch_classify_frames(const cgpu_snapshot &s, const frames_args &a, hipStream_t st);
 
 /* stateful classification (cgpu_classify_v4_ct): packet columns, outputs,
