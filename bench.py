@@ -119,7 +119,7 @@ WORKLOADS = {
           "ct_create4 / delete, bit-exact",
     "ctlb": "config2 tables + 1M IPv4 services + stateful conntrack behind the stateful service step "
             "(cgpu_classify_v4_ctlb, lb4_local with CONNTRACK): 16M packets per GPU of 500k "
-            "connections (~32 packets each, 40 % to services, 2 % loopback backends), map emptied "
+            "connections (~32 packets each, 40 % to services, 0.01 % loopback backends), map emptied "
             "each step: CT_SERVICE lookup/create + slave reuse -> ct_lookup4 -> ipcache -> policy -> "
             "ct_create4 with the service's state and address entry, bit-exact",
     "ct6": "IPv6 tables at config-2 size (100k IPv6 ipcache prefixes + 64k policy entries) + stateful "
@@ -187,8 +187,11 @@ def main():
         # pairhash % world == rank): per-rank maps, no shared state
         if ctlb:
             S = synth.make_services(T, synth.CONFIGS["cascade"]["n_services"])
+            # loopback backends (an endpoint reaching itself through a
+            # service) concentrate on the 4 endpoints' own pairs: a few
             tup, _, seclabels, S = synth.make_ctlb_workload(T, S, n // CT_PKTS_PER_CONN, gpu_id=rank,
-                                                            mean_pkts=CT_PKTS_PER_CONN, world=world)
+                                                            mean_pkts=CT_PKTS_PER_CONN, world=world,
+                                                            loop_frac=1e-4)
         else:
             mk = synth.make_ct6_workload if ct6 else synth.make_ct_workload
             tup, _, seclabels = mk(T, n // CT_PKTS_PER_CONN, gpu_id=rank, mean_pkts=CT_PKTS_PER_CONN,

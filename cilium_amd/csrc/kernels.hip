@@ -1903,8 +1903,27 @@ __device__ __forceinline__ int32_t fchk(uint32_t off, uint32_t sz, uint32_t len,
  * cgpu_frames_parse).  Window reads when the L4 header sits right behind
  * an option-less IPv4 / extension-less IPv6 header, global loads (L2) for
  * IPv4 options and IPv6 extension headers. */
+__device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fwin &W, const uint8_t *f,
+						uint32_t len, uint32_t cap, bool egress, uint32_t ep);
+
 __device__ __forceinline__ ftuple parse_frame(const cgpu_snapshot &s, const uint8_t *f, uint32_t len,
 					      uint32_t cap, bool egress, uint32_t ep)
+{
+	fwin W;
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		const uint4 v = ld_x4<true>(f + 16 * k);
+		W.w[4 * k] = v.x;
+		W.w[4 * k + 1] = v.y;
+		W.w[4 * k + 2] = v.z;
+		W.w[4 * k + 3] = v.w;
+	}
+	return parse_frame_w(s, W, f, len, cap, egress, ep);
+}
+
+/* the same with the frame's first 64 bytes already in W */
+__device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fwin &W, const uint8_t *f,
+						uint32_t len, uint32_t cap, bool egress, uint32_t ep)
 {
 	ftuple t;
 	t.status = 0;
@@ -1914,17 +1933,6 @@ __device__ __forceinline__ ftuple parse_frame(const cgpu_snapshot &s, const uint
 	t.dport = 0;
 	t.proto = 0;
 	t.frag = false;
-	fwin W;
-	{
-#pragma unroll
-		for (int k = 0; k < 4; k++) {
-			const uint4 v = ld_x4<true>(f + 16 * k);
-			W.w[4 * k] = v.x;
-			W.w[4 * k + 1] = v.y;
-			W.w[4 * k + 2] = v.z;
-			W.w[4 * k + 3] = v.w;
-		}
-	}
 	if (len < 14u) { /* no Ethernet header to dispatch on */
 		t.status = DROP_INVALID;
 		return t;
@@ -2840,12 +2848,56 @@ hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hip
  * count, over the IPv6 ones, whose results are scattered back */
 __global__ __launch_bounds__(256) void k_frames_cols(cgpu_snapshot s, frames_args a, frames_x4 c)
 {
+	/* 64-byte slots: a wave reads its 64 frames as four fully coalesced
+	 * 1-KiB loads and hands each lane its frame through LDS (rows of 17
+	 * words: conflict-free reads); per-lane 16-byte loads of 64 separate
+	 * slots cost one address-unit pass per lane and load */
+	__shared__ uint32_t stg[4][64 * 17];
+	const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
-	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t len = a.len[i];
-		const bool egress = a.flags[i] & 1u;
-		const uint32_t ep = a.ep[i];
-		const ftuple t = parse_frame(s, a.data + i * (uint64_t)a.stride, len, min(len, a.stride), egress, ep);
+	for (uint64_t i0 = (uint64_t)blockIdx.x * 256u + wv * 64u; i0 < a.n; i0 += stride) {
+		const uint64_t i = i0 + lane;
+		const bool valid = i < a.n;
+		fwin W;
+		if (a.stride == 64u) {
+			const uint64_t bytes = min((uint64_t)64, a.n - i0) * 64u;
+			const uint8_t *base = a.data + i0 * 64u;
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const uint32_t off = 1024u * k + 16u * lane;
+				if (off < bytes) {
+					const uint4 v = ld_x4<true>(base + off);
+					uint32_t *d = &stg[wv][(off >> 6) * 17u + ((off & 63u) >> 2)];
+					d[0] = v.x;
+					d[1] = v.y;
+					d[2] = v.z;
+					d[3] = v.w;
+				}
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+			for (int j = 0; j < 16; j++)
+				W.w[j] = stg[wv][lane * 17u + j];
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		} else if (valid) {
+			const uint8_t *f = a.data + i * (uint64_t)a.stride;
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const uint4 v = ld_x4<true>(f + 16 * k);
+				W.w[4 * k] = v.x;
+				W.w[4 * k + 1] = v.y;
+				W.w[4 * k + 2] = v.z;
+				W.w[4 * k + 3] = v.w;
+			}
+		}
+		const uint32_t len = valid ? a.len[i] : 0u;
+		const bool egress = valid && (a.flags[i] & 1u);
+		const uint32_t ep = valid ? a.ep[i] : 0u;
+		const ftuple t = parse_frame_w(s, W, a.data + i * (uint64_t)a.stride, len, min(len, a.stride), egress, ep);
 		uint32_t fl = egress ? 1u : 0u, sa = 0, da = 0, dp = 0, pr = 0;
 		const bool v6 = t.status == 0 && t.fam != 4u;
 		if (t.status != 0) {
@@ -2861,14 +2913,14 @@ __global__ __launch_bounds__(256) void k_frames_cols(cgpu_snapshot s, frames_arg
 			fl |= FRF_V6;
 		}
 		/* wave-aggregated slot of the IPv6 frames */
-		const uint64_t m = __ballot(v6);
+		const uint64_t m = __ballot(valid && v6);
 		if (m) {
 			const int leader = __ffsll((unsigned long long)m) - 1;
 			uint32_t base = 0;
 			if ((int)__lane_id() == leader)
 				base = atomicAdd(c.n6, (uint32_t)__popcll(m));
 			base = __shfl(base, leader, 64);
-			if (v6) {
+			if (valid && v6) {
 				const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
 				c.sa6[j] = t.sa;
 				c.da6[j] = t.da;
@@ -2880,6 +2932,8 @@ __global__ __launch_bounds__(256) void k_frames_cols(cgpu_snapshot s, frames_arg
 				c.idx6[j] = (uint32_t)i;
 			}
 		}
+		if (!valid)
+			continue;
 		c.sa4[i] = sa;
 		c.da4[i] = da;
 		c.dport[i] = (uint16_t)dp;
@@ -4263,9 +4317,26 @@ __device__ __forceinline__ uint4 ct_svc_step(const cgpu_snapshot &s, const ct_ta
 #define WALK_SVC 1
 #define WALK_OWED 2
 
+#ifdef CGPU_DIAG_WALK_CLOCK
+/* timing-only tool build (tools/ct_scan.py): per wave of the last walk
+ * {start, end (s_memrealtime, 100 MHz), steps of its busiest lane, steps of
+ * all its lanes} */
+__device__ unsigned long long g_walk_diag[4 * 8192];
+extern "C" __attribute__((visibility("default"))) int cgpu_diag_walk_clock(unsigned long long *out, size_t n)
+{
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_walk_diag), std::min<size_t>(n, 4 * 8192) * 8) == hipSuccess
+		       ? 0
+		       : -5;
+}
+#endif
+
 template <class K, int MODE>
 __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
 {
+#ifdef CGPU_DIAG_WALK_CLOCK
+	const unsigned long long dg_t0 = __builtin_amdgcn_s_memrealtime();
+	uint32_t dg_steps = 0;
+#endif
 	using R = std::conditional_t<MODE == WALK_SVC, ct_srec, ct_rec<K>>;
 	__shared__ int s_acct[3];
 	if (threadIdx.x < 3)
@@ -4306,6 +4377,9 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 			const uint32_t meta = r.meta();
 			if (meta & CTM_GATED)
 				continue;
+#ifdef CGPU_DIAG_WALK_CLOCK
+			dg_steps++;
+#endif
 			if constexpr (MODE == WALK_SVC) {
 				a.svc_out[i] = ct_svc_step(s, T, A, c, r, a.now);
 			} else {
@@ -4328,6 +4402,22 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 		}
 		ctc_flush(T, c);
 	}
+#ifdef CGPU_DIAG_WALK_CLOCK
+	{
+		uint32_t mx = dg_steps;
+		for (int o = 32; o > 0; o >>= 1)
+			mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+		const uint64_t sum = wave_sum((uint64_t)dg_steps);
+		const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+		const uint32_t w = (blockIdx.x * 256u + threadIdx.x) >> 6;
+		if ((threadIdx.x & 63) == 0 && w < 8192u && MODE == WALK_PKT) {
+			g_walk_diag[4u * w] = dg_t0;
+			g_walk_diag[4u * w + 1u] = t1;
+			g_walk_diag[4u * w + 2u] = mx;
+			g_walk_diag[4u * w + 3u] = sum;
+		}
+	}
+#endif
 	__syncthreads();
 	if (threadIdx.x == 0) {
 		const int back = s_acct[0] + s_acct[1]; /* unused reservation + deletes */

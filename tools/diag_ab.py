@@ -32,7 +32,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "pf6_q4": ("CGPU_DIAG_PF6_Q=4",),
             "pf6_q2": ("CGPU_DIAG_PF6_Q=2",),
             "pf6_q2_prefetch": ("CGPU_DIAG_PF6_Q=2", "CGPU_DIAG_PF6_PREFETCH"),
-            "ct_coherent_probe": ("CGPU_DIAG_CT_COHERENT_PROBE",)}
+            "ct_coherent_probe": ("CGPU_DIAG_CT_COHERENT_PROBE",),
+            "walk_clock": ("CGPU_DIAG_WALK_CLOCK",)}
 
 
 def build(names):
