@@ -164,6 +164,7 @@ PROTOS = {
     "cgpu_ct6_count": (sz, [vp]),
     "cgpu_ct6_gc": (i32, [vp, u32, C.POINTER(u64)]),
     "cgpu_ct6_flush": (i32, [vp]),
+    "cgpu_classify_v6_ctlb": (i32, [vp, C.POINTER(TuplesV6Ct), vp, sz, u32, C.POINTER(CtlbOut), vp]),
     "cgpu_classify_v6_ct": (i32, [vp, C.POINTER(TuplesV6Ct), sz, u32, vp, vp, vp, vp, vp]),
     "cgpu_l3_compile": (i32, [vp, vp, vp, vp, u32, vp]),
     "cgpu_mapstate_sync": (i32, [vp, vp, vp, vp, vp, vp]),

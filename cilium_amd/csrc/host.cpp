@@ -1288,29 +1288,36 @@ int build_lb6(const Lb6In &lb, uint32_t lb_max_entries, Lb6Build &b)
 	for (auto it = lb.begin(); it != lb.end();) {
 		auto jt = it;
 		uint32_t mcount = 0, maxs = 0;
+		const cgpu_lb6_service *master = nullptr;
 		for (; jt != lb.end() && !memcmp(jt->first.data(), it->first.data(), 18); ++jt) {
 			const uint32_t sl = (uint32_t)jt->first[18] << 8 | jt->first[19];
-			if (sl == 0)
+			if (sl == 0) {
 				mcount = jt->second.count;
-			else
+				master = &jt->second;
+			} else {
 				maxs = sl; /* ascending */
+			}
 		}
 		const uint64_t base = b.be.size();
-		if (base + maxs > cap)
+		const uint32_t rows = maxs + (master ? 1u : 0u);
+		if (base + rows > cap)
 			return fail(-E2BIG, "lb6 backend rows exceed %llu (sparse slave numbers)",
 				    (unsigned long long)cap);
-		b.be.resize(base + maxs, std::array<uint32_t, 8>{});
-		for (auto kt = it; kt != jt; ++kt) {
-			const uint32_t sl = (uint32_t)kt->first[18] << 8 | kt->first[19];
-			if (!sl)
-				continue;
-			const cgpu_lb6_service &v = kt->second;
-			auto &row = b.be[base + sl - 1];
+		b.be.resize(base + rows, std::array<uint32_t, 8>{});
+		auto put = [&](uint64_t at, const cgpu_lb6_service &v) {
+			auto &row = b.be[at];
 			memcpy(row.data(), v.target, 16);
 			row[4] = (uint32_t)v.port | (uint32_t)v.count << 16;
 			row[5] = (uint32_t)v.rev_nat_index | (uint32_t)v.weight << 16;
 			row[6] = 1u;
+		};
+		for (auto kt = it; kt != jt; ++kt) {
+			const uint32_t sl = (uint32_t)kt->first[18] << 8 | kt->first[19];
+			if (sl)
+				put(base + sl - 1, kt->second);
 		}
+		if (master) /* LB_FE_MASTER: the slave-0 row after the slaves */
+			put(base + maxs, *master);
 		Fe f{};
 		memcpy(f.a, it->first.data(), 16);
 		uint16_t dp;
@@ -1318,7 +1325,7 @@ int build_lb6(const Lb6In &lb, uint32_t lb_max_entries, Lb6Build &b)
 		f.dport = dp;
 		f.mcount = mcount;
 		f.base = (uint32_t)base;
-		f.nslaves = maxs;
+		f.nslaves = maxs | (master ? LB_FE_MASTER : 0u);
 		fes.push_back(f);
 		it = jt;
 	}
@@ -4517,21 +4524,24 @@ static int ct_flush_l(cgpu_ctx *c, CtMap &m)
 {
 	std::lock_guard<std::mutex> g(c->mu);
 	ct_alloc_shadow(m);
+	m.live = m.tombs = 0;
+	if (c->device >= 0 && m.d_keys) {
+		/* empty the device map in place, ordered on the conntrack stream
+		 * behind every batch before it (tags and counts; rows are
+		 * rewritten whole by every insert): no device-wide wait.  The host
+		 * shadow is then stale and re-read before any host access
+		 * (ct_pull), so it is not cleared here either. */
+		HIP_OR_EIO(hipSetDevice(c->device));
+		HIP_OR_EIO(hipMemsetAsync(m.d_keys, 0, m.keys.size() * 16, c->ct_stream));
+		HIP_OR_EIO(hipMemsetAsync(m.d_count, 0, 8, c->ct_stream));
+		m.dev_newer = true;
+		m.host_newer = false;
+		return 0;
+	}
 	std::fill(m.keys.begin(), m.keys.end(), uint4{0, 0, 0, 0});
 	std::fill(m.vals.begin(), m.vals.end(), uint4{0, 0, 0, 0});
-	m.live = m.tombs = 0;
 	m.dev_newer = false;
 	m.host_newer = true;
-	if (c->device >= 0 && m.d_keys) {
-		/* empty the device map in place (tags and counts; rows are
-		 * rewritten whole by every insert) instead of re-uploading */
-		HIP_OR_EIO(hipSetDevice(c->device));
-		HIP_OR_EIO(hipDeviceSynchronize());
-		HIP_OR_EIO(hipMemset(m.d_keys, 0, m.keys.size() * 16));
-		HIP_OR_EIO(hipMemset(m.d_count, 0, 8));
-		HIP_OR_EIO(hipDeviceSynchronize());
-		m.host_newer = false;
-	}
 	return 0;
 }
 
@@ -4665,7 +4675,7 @@ struct CtScratch {
 		temp, temp_bytes, svc_out, ctl, flags2, total;
 };
 
-static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc)
+static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool v6)
 {
 	CtScratch L{};
 	auto take = [&](size_t bytes) {
@@ -4685,7 +4695,7 @@ static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc)
 	L.temp_bytes = ct_temp_bytes(n);
 	L.temp = take(L.temp_bytes);
 	if (svc) {
-		L.svc_out = take(n * 16);
+		L.svc_out = take(n * (v6 ? 32 : 16));
 		L.ctl = take(16);
 		L.flags2 = take(2 * n);
 	}
@@ -4722,7 +4732,7 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	}
 	if (int r = ct_push(m))
 		return r;
-	const CtScratch L = ct_scratch_layout(a.n, m.v6 ? 64 : svc ? 48 : 32, svc);
+	const CtScratch L = ct_scratch_layout(a.n, m.v6 ? 64 : svc ? 48 : 32, svc, m.v6);
 	if (L.total > c->ct_scratch_cap) {
 		HIP_OR_EIO(hipStreamSynchronize(cs));
 		(void)hipFree(c->d_ct_scratch);
@@ -4753,7 +4763,7 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
 		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);
 		a.flags2 = b + L.flags2;
-		HIP_OR_EIO(launch_classify_v4_ctlb(s, T, a, cs));
+		HIP_OR_EIO(m.v6 ? launch_classify_v6_ctlb(s, T, a, cs) : launch_classify_v4_ctlb(s, T, a, cs));
 	} else {
 		HIP_OR_EIO(m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs));
 	}
@@ -4830,6 +4840,44 @@ CGPU_EXPORT int cgpu_classify_v4_ctlb(cgpu_ctx *c, const cgpu_tuples_v4_ct *t, c
 	a.n = n;
 	a.now = now;
 	return ct_classify(c, P.snap(), P.delta, c->ct4, a, stream, true);
+}
+
+CGPU_EXPORT int cgpu_classify_v6_ctlb(cgpu_ctx *c, const cgpu_tuples_v6_ct *t, const uint32_t *hash,
+				      size_t n, uint32_t now, const cgpu_ctlb6_out *out, void *stream)
+{
+	Pinned P;
+	if (int r = pin(c, stream, P))
+		return r;
+	if (!t || !out || (n && (!t->saddr || !t->daddr || !t->sport || !t->dport || !t->proto || !t->l4 ||
+				 !t->flags || !t->len || !t->ep || !out->verdict || !out->ct_ret ||
+				 !out->identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n && (((uintptr_t)t->saddr | (uintptr_t)t->daddr | (uintptr_t)out->daddr) & 15))
+		return fail(-EINVAL, "IPv6 address columns must be 16-byte aligned");
+	if (n > (size_t)INT32_MAX / 2)
+		return fail(-EINVAL, "batch of %zu packets exceeds 2^30 - 1", n);
+	if (!n)
+		return 0;
+	ct_launch a{};
+	a.saddr = t->saddr;
+	a.daddr = t->daddr;
+	a.sport = t->sport;
+	a.dport = t->dport;
+	a.proto = t->proto;
+	a.l4 = t->l4;
+	a.flags = t->flags;
+	a.len = t->len;
+	a.ep = t->ep;
+	a.verdict = out->verdict;
+	a.ct_ret = out->ct_ret;
+	a.identity = out->identity;
+	a.stage = out->stage;
+	a.xdaddr = out->daddr;
+	a.xdport = out->dport;
+	a.hash = hash;
+	a.n = n;
+	a.now = now;
+	return ct_classify(c, P.snap(), P.delta, c->ct6, a, stream, true);
 }
 
 CGPU_EXPORT int cgpu_classify_v6_ct(cgpu_ctx *c, const cgpu_tuples_v6_ct *t, size_t n, uint32_t now,

@@ -462,7 +462,9 @@ __device__ __forceinline__ bool lb_service(const cgpu_snapshot &s, uint32_t addr
 
 /* map_lookup_elem(&cilium_lb6_services, {addr, dport, slave}) (tables.h
  * lb6_table): tg = target, val = {port | count << 16, rev_nat | weight << 16,
- * present, 0}; slave 0 carries only the master's count.  f = fold6(addr). */
+ * present, 0}; slave 0 carries only the master's count, or with FULL0 the
+ * master's stored row (the stateful service step).  f = fold6(addr). */
+template <bool FULL0 = false>
 __device__ __forceinline__ bool lb6_get(const lb6_table &t, uint4 addr, uint32_t f, uint32_t dport,
 					uint32_t slave, uint4 &tg, uint4 &val)
 {
@@ -487,6 +489,14 @@ __device__ __forceinline__ bool lb6_get(const lb6_table &t, uint4 addr, uint32_t
 	if (!found || !(m.z & LB_FE_USED))
 		return false;
 	if (slave == 0) {
+		if (FULL0) { /* the stored master row (LB_FE_MASTER) */
+			if (!(m.z & LB_FE_MASTER))
+				return false;
+			const uint32_t r = m.y + (m.z & 0xFFFFu);
+			tg = t.be[2u * r];
+			val = t.be[2u * r + 1u];
+			return true;
+		}
 		tg = make_uint4(0, 0, 0, 0);
 		val = make_uint4(m.x & 0xFFFF0000u, 0, 1, 0);
 		return true;
@@ -2995,7 +3005,10 @@ hipError_t launch_classify_frames_x4(const cgpu_snapshot &s, const frames_args &
 	hipError_t e = hipMemsetAsync(c.n6, 0, 4, st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL(k_frames_cols, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, s, a, c);
+	/* a streaming pass: up to 8 resident 256-thread blocks per CU (17 KiB
+	 * LDS each) so enough slot loads are in flight */
+	const unsigned gf = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + BLOCK - 1) / BLOCK, 256u * 8u * 4u));
+	hipLaunchKernelGGL(k_frames_cols, dim3(gf), dim3(BLOCK), 0, st, s, a, c);
 	cls_args c4{c.sa4, c.da4, c.dport, c.proto, c.fl, a.len, a.ep, a.verdict, a.identity, a.stage,
 		    a.delta, a.n, a.pk, 0, nullptr, nullptr};
 	if (!x4_aligned(c4))
@@ -3174,8 +3187,13 @@ __device__ __forceinline__ ct_row ct_row_load(const ct_table &T, uint32_t slot)
 
 /* Write-through stores complete asynchronously: a later load of the same
  * bytes by this lane (after the entry was evicted from its cache and is
- * probed again) could be served from memory before the store lands.  Every
- * store burst to the map therefore ends with a wait for its completion. */
+ * probed again) could be served from memory before the store lands.  The
+ * lane's cache therefore marks stores pending (ct_cache.pend) and the next
+ * probe of the map first waits for them (ct_pend_wait): a store burst never
+ * stalls the walk itself, only a later cache miss does, which reads the
+ * map anyway.  Other lanes never read this lane's keys or rows (a slot's
+ * tag changes by atomics only; a deleted slot is retired with a wait,
+ * ct_erase). */
 __device__ __forceinline__ void ct_row_store(const ct_table &T, uint32_t slot, const ct_row &e)
 {
 	uint32_t *p = reinterpret_cast<uint32_t *>(T.vals + 4u * slot);
@@ -3186,7 +3204,14 @@ __device__ __forceinline__ void ct_row_store(const ct_table &T, uint32_t slot, c
 	st_wt64(p + 8, e.c.x, e.c.y);
 	st_wt64(p + 10, e.c.z, e.c.w);
 	st_wt64(p + 12, e.d.x, e.d.y);
-	__builtin_amdgcn_s_waitcnt(0);
+}
+
+__device__ __forceinline__ void ct_pend_wait(uint32_t &pend)
+{
+	if (pend) {
+		__builtin_amdgcn_s_waitcnt(0);
+		pend = 0;
+	}
 }
 
 __device__ __forceinline__ void add64(uint32_t &lo, uint32_t &hi, uint32_t v)
@@ -3270,7 +3295,8 @@ __device__ __forceinline__ uint4 sel4(bool t, uint4 a, uint4 b)
 struct CtK4 {
 	typedef uint4 key;
 	static constexpr int V6 = 0;
-	static constexpr bool SVC = false;
+	static constexpr bool SVC = false;  /* entries carry the service's slave / lb_loopback */
+	static constexpr bool ADDR = false; /* creates write ct_create4's address entry */
 	__device__ static uint32_t &meta(key &k) { return k.w; }
 	__device__ static uint32_t cmeta(const key &k) { return k.w; }
 	__device__ static uint32_t hash(const key &k) { return ct_hash(k.x, k.y, k.z, k.w); }
@@ -3321,6 +3347,7 @@ struct CtK6 {
 	};
 	static constexpr int V6 = 1;
 	static constexpr bool SVC = false;
+	static constexpr bool ADDR = false;
 	__device__ static uint32_t &meta(key &k) { return k.m; }
 	__device__ static uint32_t cmeta(const key &k) { return k.m; }
 	__device__ static uint32_t hash(const key &k)
@@ -3387,14 +3414,22 @@ struct CtK6 {
  * entry */
 struct CtK4S : CtK4 {
 	static constexpr bool SVC = true;
+	static constexpr bool ADDR = true;
+};
+/* cilium_ct6_global behind the IPv6 service step (ct_create6 writes no
+ * address entry) */
+struct CtK6S : CtK6 {
+	static constexpr bool SVC = true;
 };
 
 /* Probe for k (low 16 bits of the meta word = nexthdr | flags << 8).
  * Returns the slot or -1; *free_at = the first tombstone on the chain, else
  * the empty slot that ended it (where an insert of k may start). */
 template <class K>
-__device__ __forceinline__ int ct_find(const ct_table &T, const typename K::key &k, uint32_t *free_at)
+__device__ __forceinline__ int ct_find(const ct_table &T, const typename K::key &k, uint32_t *free_at,
+				       uint32_t &pend)
 {
+	ct_pend_wait(pend);
 	uint32_t h = K::hash(k) & T.mask;
 	uint32_t ff = 0xFFFFFFFFu;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
@@ -3497,8 +3532,7 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, co
 			if (atomicCAS(K::tagp(T, h), expect, want) == expect) {
 				if (tag == CT_TAG_TOMB)
 					atomicSub(A.tombs, 1);
-				K::store(T, h, k);
-				__builtin_amdgcn_s_waitcnt(0);
+				K::store(T, h, k); /* pending: the caller marks it (ctc_update) */
 				return (int)h;
 			}
 		}
@@ -3640,6 +3674,26 @@ __device__ __forceinline__ uint4 ct_addr_key(uint4 k, const ct_pkt &q)
 	}
 	return k;
 }
+
+/*   IPv6 behind the service step: the IPv6 record with {sec, cst, rev_nat,
+ *                    slave | lbf << 16} as its last word */
+template <> struct ct_rec<CtK6S> {
+	static constexpr uint32_t RW = 4;
+	uint4 r0, r1, r2, r3;
+	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
+	{
+		const uint4 *p = rec + 4u * i;
+		return nt ? ct_rec{ld_x4<true>(p), ld_x4<true>(p + 1), ld_x4<true>(p + 2), ld_x4<true>(p + 3)}
+			  : ct_rec{p[0], p[1], p[2], p[3]};
+	}
+	__device__ CtK6::key key() const { return CtK6::key{r0, r1, r2.x, r2.y & 0xFFFFu}; }
+	__device__ uint32_t meta() const { return r2.y >> 16; }
+	__device__ ct_pkt pkt() const
+	{
+		return ct_pkt{r2.y >> 16, r2.z & 0xFFFFu, r2.w, r3.x, r3.z, r2.z >> 16, r3.y, r2.x & 0xFFFFu,
+			      r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
+	}
+};
 
 /* ct_lookup4's tuple setup, conntrack.h:461-528.  SVC (cgpu_classify_v4_ctlb):
  * egress packets first take lb4_local's outcome (svc_out, the service walk):
@@ -3830,16 +3884,51 @@ __global__ __launch_bounds__(256) void k_ct_heads(const uint32_t *g, uint8_t *he
  * decision, as k_ct_prep; IPv6 has no fragment flag (bpf_lxc.c:787-789) and
  * an ingress entry carries the reverse NAT index ipv6_policy derives from
  * the destination address, daddr.s6_addr32[3] & 0xFFFF (bpf_lxc.c:748). */
+template <bool SVC>
 __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr);
 	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t fl = a.flags[i], pr = a.proto[i], w = a.l4[i], len = a.len[i], ep = a.ep[i];
-		const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
+		const uint32_t fl = a.flags[i], pr = a.proto[i], len = a.len[i], ep = a.ep[i];
+		uint32_t w = a.l4[i], dp = a.dport[i];
+		const uint4 sa = ld_x4<true>(sa16 + i);
+		uint4 da = ld_x4<true>(da16 + i);
 		const bool egress = fl & 1u;
 		uint32_t tfl = egress ? TUPLE_F_IN : 0u, z = 0, meta = egress ? CTM_EGRESS : 0u;
+		uint32_t svcw = 0; /* slave | lbf << 16 */
+		uint32_t rev = egress ? 0u : (da.w & 0xFFFFu);
+		if constexpr (SVC) {
+			/* lb6_local's outcome (svc_out[2i], target svc_out[2i + 1]) */
+			const uint4 so = egress ? a.svc_out[2u * i] : make_uint4(SVC_NONE, 0, 0, 0);
+			if ((so.x & 3u) == SVC_DROP) {
+				a.identity[i] = 0;
+				if (a.xdaddr)
+					reinterpret_cast<uint4 *>(a.xdaddr)[i] = da;
+				if (a.xdport)
+					a.xdport[i] = (uint16_t)dp;
+				uint4 *r = a.rec + 4u * i;
+				r[0] = da;
+				r[1] = sa;
+				r[2] = uint4{0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16), 0u, len};
+				r[3] = uint4{0u, 0u, 0u, 0u};
+				a.gkey[i] = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
+				a.idx[i] = (uint32_t)i;
+				continue;
+			}
+			if ((so.x & 3u) == SVC_XLATED) {
+				da = a.svc_out[2u * i + 1u]; /* tuple->daddr = svc->target (lb.h:475) */
+				if (so.y & 0xFFFFu)
+					dp = so.y & 0xFFFFu; /* lb6_xlate's port rewrite */
+				rev = so.y >> 16;
+				svcw = (so.x >> 16) | ((((so.x >> 8) & LBS_ENTRY) ? LBF_LOOPBACK : 0u) << 16);
+			}
+			if (a.xdaddr)
+				reinterpret_cast<uint4 *>(a.xdaddr)[i] = da;
+			if (a.xdport)
+				a.xdport[i] = (uint16_t)dp;
+		}
 		if (pr == 58u) {
 			const uint32_t type = w & 0xFFu;
 			if (type >= 1u && type <= 4u) /* DEST_UNREACH, PKT_TOOBIG, TIME_EXCEED, PARAMPROB */
@@ -3852,7 +3941,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 				meta |= CTM_ACT_CREATE;
 			}
 		} else if (pr == 6u || pr == 17u) {
-			z = (uint32_t)a.sport[i] | ((uint32_t)a.dport[i] << 16);
+			z = (uint32_t)a.sport[i] | (dp << 16);
 			if (pr == 6u)
 				meta |= CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE);
 			else
@@ -3860,6 +3949,8 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 		} else {
 			meta |= CTM_GATED;
 		}
+		if (pr != 6u)
+			w = 0; /* union tcp_flags stays zero (conntrack.h:294) */
 		uint32_t sec = 0, port = 0, cst = 0, id = 0;
 		if (!(meta & CTM_GATED)) {
 			const decision d = decide<1>(s, egress, false, 0u, 0u, sa, da, z >> 16, pr, ep);
@@ -3879,7 +3970,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 		r[0] = da;
 		r[1] = sa;
 		r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (port << 16), len};
-		r[3] = uint4{sec, cst, egress ? 0u : (da.w & 0xFFFFu), 0u};
+		r[3] = uint4{sec, cst, rev, svcw};
 		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u)
 					       : ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
 		a.idx[i] = (uint32_t)i;
@@ -3919,6 +4010,7 @@ template <class K> struct ct_cache {
 	ctc_ent<K> &e3;
 #endif
 	uint32_t next;
+	uint32_t pend; /* map stores of this lane not yet waited for */
 };
 
 template <class K, typename F> __device__ __forceinline__ void ctc_each(ct_cache<K> &c, F &&f)
@@ -3945,8 +4037,10 @@ template <class K> __device__ __forceinline__ void ctc_flush(const ct_table &T, 
 	ctc_each(c, [&](ctc_ent<K> &e, int) {
 		const uint32_t w = K::meta(e.key), p = e.pos;
 		const ct_row r = e.row;
-		if (ctc_dirty(w))
+		if (ctc_dirty(w)) {
 			ct_row_store(T, p, r);
+			c.pend = 1;
+		}
 		K::meta(e.key) = 0;
 	});
 	c.next = 0;
@@ -4012,7 +4106,13 @@ __device__ __forceinline__ int ctc_get(const ct_table &T, ct_cache<K> &c, const 
 		return hit;
 	const int v = (int)c.next;
 	c.next = v + 1 == CTC ? 0u : (uint32_t)v + 1u;
-	/* write back the victim */
+	uint32_t from;
+	const int slot = ct_find<K>(T, k, &from, c.pend);
+	ct_row r{};
+	if (slot >= 0)
+		r = ct_row_load(T, (uint32_t)slot);
+	/* write back the victim (a different key: the probe above cannot have
+	 * read its row) */
 	uint32_t vw = 0, vp = 0;
 	ct_row vr{};
 	ctc_each(c, [&](ctc_ent<K> &e, int j) {
@@ -4020,13 +4120,10 @@ __device__ __forceinline__ int ctc_get(const ct_table &T, ct_cache<K> &c, const 
 		vp = j == v ? e.pos : vp;
 		vr = selrow(j == v, e.row, vr);
 	});
-	if (ctc_dirty(vw))
+	if (ctc_dirty(vw)) {
 		ct_row_store(T, vp, vr);
-	uint32_t from;
-	const int slot = ct_find<K>(T, k, &from);
-	ct_row r{};
-	if (slot >= 0)
-		r = ct_row_load(T, (uint32_t)slot);
+		c.pend = 1;
+	}
 	typename K::key nk = k;
 	K::meta(nk) = (K::cmeta(k) & 0xFFFFu) | CTC_VALID | (slot < 0 ? CTC_NEG : 0u);
 	const uint32_t np = slot >= 0 ? (uint32_t)slot : from;
@@ -4037,6 +4134,160 @@ __device__ __forceinline__ int ctc_get(const ct_table &T, ct_cache<K> &c, const 
 		e.row = selrow(t, r, e.row);
 	});
 	return v;
+}
+
+/* the cache entry of k, or -1 (no probe) */
+template <class K> __device__ __forceinline__ int ctc_find(ct_cache<K> &c, const typename K::key &k)
+{
+	int hit = -1;
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
+		hit = ((K::meta(e.key) & CTC_VALID) && K::same(e.key, k)) ? j : hit;
+	});
+	return hit;
+}
+
+/* One probe chain of ct_find, advanced a slot per round so that the chains
+ * of several keys have their loads in flight together.  slot: -3 not
+ * probed, -2 running, -1 absent (inserts may start at ff), else found. */
+struct ct_chain {
+	uint32_t h, ff, n;
+	int slot;
+};
+
+/* s = the slot as loaded; cm = its meta word re-read at the coherence point
+ * when the plain read was EMPTY (ct_find's rule) */
+template <class K>
+__device__ __forceinline__ void ct_chain_eval(const ct_table &T, const typename K::key &k, typename K::key s,
+					      uint32_t cm, ct_chain &ch)
+{
+	if (ch.slot != -2)
+		return;
+	uint32_t tag = K::meta(s) >> 16;
+	if (tag == CT_TAG_EMPTY) {
+		K::meta(s) = cm;
+		tag = cm >> 16;
+		if (tag == CT_TAG_EMPTY) {
+			ch.slot = -1;
+			if (ch.ff == 0xFFFFFFFFu)
+				ch.ff = ch.h;
+			return;
+		}
+		K::reload(T, ch.h, s);
+	}
+	if (tag == CT_TAG_LIVE && K::same(s, k)) {
+		ch.slot = (int)ch.h;
+		return;
+	}
+	if (tag == CT_TAG_TOMB && ch.ff == 0xFFFFFFFFu)
+		ch.ff = ch.h;
+	ch.h = (ch.h + 1u) & T.mask;
+	if (++ch.n > T.mask)
+		ch.slot = -1;
+}
+
+template <class K>
+__device__ __forceinline__ void ct_find3(const ct_table &T, const typename K::key &k0, const typename K::key &k1,
+					 const typename K::key &k2, ct_chain &c0, ct_chain &c1, ct_chain &c2,
+					 uint32_t &pend)
+{
+	ct_pend_wait(pend);
+	c0.h = K::hash(k0) & T.mask;
+	c1.h = K::hash(k1) & T.mask;
+	c2.h = K::hash(k2) & T.mask;
+	while (c0.slot == -2 || c1.slot == -2 || c2.slot == -2) {
+		typename K::key s0 = k0, s1 = k1, s2 = k2;
+		if (c0.slot == -2)
+			s0 = K::load(T, c0.h);
+		if (c1.slot == -2)
+			s1 = K::load(T, c1.h);
+		if (c2.slot == -2)
+			s2 = K::load(T, c2.h);
+		uint32_t m0 = 0, m1 = 0, m2 = 0;
+		if (c0.slot == -2 && (K::meta(s0) >> 16) == CT_TAG_EMPTY)
+			m0 = __hip_atomic_load(K::tagp(T, c0.h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (c1.slot == -2 && (K::meta(s1) >> 16) == CT_TAG_EMPTY)
+			m1 = __hip_atomic_load(K::tagp(T, c1.h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (c2.slot == -2 && (K::meta(s2) >> 16) == CT_TAG_EMPTY)
+			m2 = __hip_atomic_load(K::tagp(T, c2.h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		ct_chain_eval<K>(T, k0, s0, m0, c0);
+		ct_chain_eval<K>(T, k1, s1, m1, c1);
+		ct_chain_eval<K>(T, k2, s2, m2, c2);
+	}
+}
+
+/* put probed key k (chain ch, row r) into the cache, in the next entry
+ * round-robin that holds none of the wanted keys k0..k2 */
+template <class K>
+__device__ __forceinline__ void ctc_install(const ct_table &T, ct_cache<K> &c, const typename K::key &k,
+					    const ct_chain &ch, const ct_row &r, const typename K::key &k0,
+					    const typename K::key &k1, const typename K::key &k2)
+{
+	if (ch.slot == -3)
+		return;
+	uint32_t keep = 0;
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
+		const bool v = K::meta(e.key) & CTC_VALID;
+		if (v && (K::same(e.key, k0) || K::same(e.key, k1) || K::same(e.key, k2)))
+			keep |= 1u << j;
+	});
+	int v = -1;
+#pragma unroll
+	for (int t = 0; t < CTC; t++) {
+		int j = (int)c.next + t;
+		j = j >= CTC ? j - CTC : j;
+		v = (v < 0 && !((keep >> j) & 1u)) ? j : v;
+	}
+	c.next = v + 1 == CTC ? 0u : (uint32_t)v + 1u;
+	uint32_t vw = 0, vp = 0;
+	ct_row vr{};
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
+		vw = j == v ? K::meta(e.key) : vw;
+		vp = j == v ? e.pos : vp;
+		vr = selrow(j == v, e.row, vr);
+	});
+	if (ctc_dirty(vw)) {
+		ct_row_store(T, vp, vr);
+		c.pend = 1;
+	}
+	typename K::key nk = k;
+	K::meta(nk) = (K::cmeta(k) & 0xFFFFu) | CTC_VALID | (ch.slot < 0 ? CTC_NEG : 0u);
+	const uint32_t np = ch.slot >= 0 ? (uint32_t)ch.slot : ch.ff;
+	ctc_each(c, [&](ctc_ent<K> &e, int j) {
+		const bool t = j == v;
+		e.key = K::sel(t, nk, e.key);
+		e.pos = t ? np : e.pos;
+		e.row = selrow(t, r, e.row);
+	});
+}
+
+/* The keys a step will need (w0..w2 select them), probed together when
+ * the cache lacks them: a new connection's reply key, forward key and ICMP
+ * key cost one round of loads instead of three dependent probes */
+template <class K>
+__device__ __forceinline__ void ctc_prefetch(const ct_table &T, ct_cache<K> &c, const typename K::key &k0,
+					     const typename K::key &k1, const typename K::key &k2, bool w0, bool w1,
+					     bool w2)
+{
+	ct_chain c0{0, 0xFFFFFFFFu, 0, -3}, c1 = c0, c2 = c0;
+	if (w0 && ctc_find<K>(c, k0) < 0)
+		c0.slot = -2;
+	if (w1 && ctc_find<K>(c, k1) < 0)
+		c1.slot = -2;
+	if (w2 && ctc_find<K>(c, k2) < 0)
+		c2.slot = -2;
+	if (c0.slot == -3 && c1.slot == -3 && c2.slot == -3)
+		return;
+	ct_find3<K>(T, k0, k1, k2, c0, c1, c2, c.pend);
+	ct_row r0{}, r1{}, r2{};
+	if (c0.slot >= 0)
+		r0 = ct_row_load(T, (uint32_t)c0.slot);
+	if (c1.slot >= 0)
+		r1 = ct_row_load(T, (uint32_t)c1.slot);
+	if (c2.slot >= 0)
+		r2 = ct_row_load(T, (uint32_t)c2.slot);
+	ctc_install<K>(T, c, k0, c0, r0, k0, k1, k2);
+	ctc_install<K>(T, c, k1, c1, r1, k0, k1, k2);
+	ctc_install<K>(T, c, k2, c2, r2, k0, k1, k2);
 }
 
 /* BPF_ANY update of k (ct_create's map_update_elem) through the cache */
@@ -4051,6 +4302,7 @@ __device__ __forceinline__ bool ctc_update(const ct_table &T, const ct_acct &A, 
 		if (slot < 0)
 			return false;
 		pos = (uint32_t)slot;
+		c.pend = 1;
 	}
 	ctc_put(c, i, pos, e);
 	return true;
@@ -4069,6 +4321,7 @@ __device__ __forceinline__ void ctc_update_owed(const ct_table &T, const ct_acct
 		if (slot < 0)
 			return; /* no free slot on the chain: the slot table is 2x CT_MAP_SIZE */
 		pos = (uint32_t)slot;
+		c.pend = 1;
 	} else {
 		atomicAdd(A.live, 1);
 	}
@@ -4106,6 +4359,15 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 {
 	const uint32_t meta = q.meta;
 	const bool ingress = !(meta & CTM_EGRESS);
+	{
+		/* reply key not cached, or cached absent: fetch it, the forward key
+		 * and (when the packet may create) the ICMP key in one round */
+		const int c1 = ctc_find<K>(c, k);
+		if (c1 < 0 || (ctc_state(c, c1) & CTC_NEG)) {
+			const typename K::key fk = K::reversed(k);
+			ctc_prefetch<K>(T, c, k, fk, K::related(fk), c1 < 0, true, (meta & CTM_ALLOWED) != 0);
+		}
+	}
 	int ci = ctc_get<K>(T, c, k);
 	uint32_t ret;
 	if (!(ctc_state(c, ci) & CTC_NEG)) {
@@ -4136,7 +4398,7 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 	if (!ctc_update<K>(T, A, c, k, e))
 		return CT_NEW | CT_FAIL;
 	uint32_t owed = 0;
-	if constexpr (K::SVC) {
+	if constexpr (K::ADDR) {
 		const uint32_t am = q.lbf >> 1;
 		if (am == AM_INLINE) {
 			if (!ctc_update<K>(T, A, c, ct_addr_key(k, q), e))
@@ -4266,6 +4528,8 @@ __device__ __forceinline__ uint4 ct_svc_step(const cgpu_snapshot &s, const ct_ta
 	uint4 f = uint4{r.r0.x, kd | (r.r1.w & 0xFFFF0000u), r.r2.x, r.r2.y};
 	const uint4 drop = make_uint4(SVC_DROP, 0, 0, 0);
 	uint32_t slave, lbs = 0;
+	if (ctc_find<CtK4>(c, k) < 0) /* the service key and its ICMP key in one round */
+		ctc_prefetch<CtK4>(T, c, k, CtK4::related(k), k, true, true, false);
 	int ci = ctc_get<CtK4>(T, c, k);
 	if (!(ctc_state(c, ci) & CTC_NEG)) { /* CT_REPLY / CT_RELATED: the stored state */
 		ct_row e = ctc_row(c, ci);
@@ -4309,6 +4573,143 @@ __device__ __forceinline__ uint4 ct_svc_step(const cgpu_snapshot &s, const ct_ta
 	return make_uint4(SVC_XLATED | (lbs << 8) | (slave << 16), b.x, rw | ((b.z & 0xFFFFu) << 16), 0u);
 }
 
+/* The IPv6 service step: lb6_local with CONNTRACK (lb.h:426-483) over
+ * cilium_ct6_global.  A service packet's record (4 x 16 B):
+ *   {VIP}, {saddr}, {z, nexthdr | (TUPLE_F_SERVICE | RELATED) << 8 | meta << 16,
+ *   w, len}, {hash, kd | master count << 16, fold6(VIP), dport}
+ * Result: svc_out[2i] = {SVC_* | LBS_* << 8 | slave << 16, the dport rewrite
+ * | rev_nat << 16, 0, 0}, svc_out[2i + 1] = the target. */
+struct ct_srec6 {
+	uint4 r0, r1, r2, r3;
+	__device__ static ct_srec6 load(const uint4 *rec, uint32_t i, bool)
+	{
+		const uint4 *p = rec + 4u * i;
+		return ct_srec6{p[0], p[1], p[2], p[3]};
+	}
+	__device__ uint32_t meta() const { return r2.y >> 16; }
+};
+
+__global__ __launch_bounds__(256) void k_svc_prep6(cgpu_snapshot s, ct_args a)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	const bool l4 = s.lb_flags & CGPU_LB_L4;
+	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr);
+	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr);
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
+		const uint32_t fl = a.flags[i], pr = a.proto[i], dp = a.dport[i];
+		const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
+		uint4 out = make_uint4(SVC_NONE, 0, 0, 0);
+		bool svc = false;
+		uint4 tg, val;
+		uint32_t kd = 0, f = 0;
+		if (fl & 1u) {
+			bool skip = false;
+			if (l4) { /* extract_l4_port (lb.h:192-216) */
+				if (pr == 6u || pr == 17u)
+					kd = dp;
+				else if (pr != 1u && pr != 58u)
+					skip = true;
+			}
+			f = fold6(da.x, da.y, da.z, da.w);
+			const uint32_t vb = lb6_vip_bit(f) & s.lb6.vip_mask;
+			if (!skip && ((s.lb6.vip[vb >> 5] >> (vb & 31u)) & 1u))
+				svc = lb6_service(s, da, f, &kd, 0, tg, val);
+		}
+		uint4 *r = a.rec + 4u * i;
+		uint4 r2 = make_uint4(0, CTM_GATED << 16, 0, 0), r3 = make_uint4(0, 0, 0, 0);
+		if (svc) {
+			/* ct_lookup6(..., CT_SERVICE, ...)'s tuple (conntrack.h:308-378) */
+			const uint32_t w = a.l4[i];
+			uint32_t tfl = TUPLE_F_SERVICE, z = 0, meta = 0;
+			bool ok = true;
+			if (pr == 58u) {
+				const uint32_t type = w & 0xFFu;
+				if (type >= 1u && type <= 4u)
+					tfl |= TUPLE_F_RELATED;
+				else if (type == 129u)
+					z = 128u;
+				else {
+					if (type == 128u)
+						z = 128u << 16;
+					meta |= CTM_ACT_CREATE;
+				}
+			} else if (pr == 6u || pr == 17u) {
+				z = (uint32_t)a.sport[i] | (dp << 16);
+				meta |= pr == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
+			} else {
+				ok = false; /* DROP_CT_UNKNOWN_PROTO -> DROP_NO_SERVICE (lb.h:453-455) */
+			}
+			if (ok) {
+				const uint32_t h = a.hash ? a.hash[i]
+							  : flow_hash(fold6(sa.x, sa.y, sa.z, sa.w), f, a.sport[i], dp, pr);
+				r2 = make_uint4(z, pr | (tfl << 8) | (meta << 16), pr == 6u ? w : 0u, a.len[i]);
+				r3 = make_uint4(h, kd | (val.x & 0xFFFF0000u), f, dp);
+			} else {
+				out.x = SVC_DROP;
+			}
+		}
+		r[0] = da;
+		r[1] = sa;
+		r[2] = r2;
+		r[3] = r3;
+		a.svc_out[2u * i] = out;
+		a.gkey[i] = (r2.y >> 16) & CTM_GATED ? ct_fmix((uint32_t)i ^ 0x5bd1e995u)
+						      : ct_group(fold6(sa.x, sa.y, sa.z, sa.w), f);
+		a.idx[i] = (uint32_t)i;
+	}
+}
+
+__device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_table &T, const ct_acct &A,
+					      ct_cache<CtK6> &c, const ct_srec6 &r, uint32_t now, uint4 &tg)
+{
+	const CtK6::key k{r.r0, r.r1, r.r2.x, r.r2.y & 0xFFFFu};
+	const uint32_t meta = r.r2.y >> 16, w = r.r2.z, len = r.r2.w, h = r.r3.x, f = r.r3.z;
+	uint32_t kd = r.r3.y & 0xFFFFu;
+	const uint32_t pr = r.r2.y & 0xFFu;
+	const uint4 drop = make_uint4(SVC_DROP, 0, 0, 0);
+	uint32_t slave, lbs = 0;
+	if (ctc_find<CtK6>(c, k) < 0)
+		ctc_prefetch<CtK6>(T, c, k, CtK6::related(k), k, true, true, false);
+	int ci = ctc_get<CtK6>(T, c, k);
+	if (!(ctc_state(c, ci) & CTC_NEG)) {
+		ct_row e = ctc_row(c, ci);
+		ct_hit(e, meta, false, w, len, now);
+		ctc_put(c, ci, ctc_pos(c, ci), e);
+		if (e.c.y & CTB_LB_LOOPBACK)
+			lbs |= LBS_ENTRY;
+		slave = e.c.z & 0xFFFFu;
+	} else { /* CT_NEW: lb6_select_slave, ct_create6(CT_SERVICE) -- fail closed */
+		slave = h % (r.r3.y >> 16) + 1u;
+		const bool tcp = meta & CTM_TCP;
+		ct_row e{};
+		ct_timeout(e, now, tcp, false, tcp ? 1u : 0u);
+		e.b = uint4{1u, 0u, len, 0u};
+		e.c.z = slave;
+		if (!ctc_update<CtK6>(T, A, c, k, e))
+			return drop;
+		e.c.y |= CTB_SEEN_NON_SYN;
+		if (!ctc_update<CtK6>(T, A, c, CtK6::related(k), e))
+			return drop;
+	}
+	uint4 val;
+	if (!lb6_get<true>(s.lb6, r.r0, f, kd, slave, tg, val)) {
+		/* lb6_lookup_slave missed: lb6_lookup_service with key.slave kept,
+		 * a new slave from its count, ct_update6_slave (lb.h:462-469) */
+		if (!lb6_service(s, r.r0, f, &kd, slave, tg, val))
+			return drop;
+		slave = h % (val.x >> 16) + 1u;
+		ci = ctc_get<CtK6>(T, c, k);
+		if (!(ctc_state(c, ci) & CTC_NEG)) {
+			ct_row e = ctc_row(c, ci);
+			e.c.z = (e.c.z & 0xFFFF0000u) | slave;
+			ctc_put(c, ci, ctc_pos(c, ci), e);
+		}
+	}
+	const uint32_t port = val.x & 0xFFFFu;
+	const uint32_t rw = ((s.lb_flags & CGPU_LB_L4) && port && kd != port && (pr == 6u || pr == 17u)) ? port : 0u;
+	return make_uint4(SVC_XLATED | (lbs << 8) | (slave << 16), rw | ((val.y & 0xFFFFu) << 16), 0u, 0u);
+}
+
 /* walks: WALK_PKT the conntrack path's packets; WALK_SVC the service step
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
  * service path: candidates c = packet << 1 | kind, kind 0 a packet whose
@@ -4337,7 +4738,8 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 	const unsigned long long dg_t0 = __builtin_amdgcn_s_memrealtime();
 	uint32_t dg_steps = 0;
 #endif
-	using R = std::conditional_t<MODE == WALK_SVC, ct_srec, ct_rec<K>>;
+	using R = std::conditional_t<MODE == WALK_SVC, std::conditional_t<K::V6 != 0, ct_srec6, ct_srec>,
+				     ct_rec<K>>;
 	__shared__ int s_acct[3];
 	if (threadIdx.x < 3)
 		s_acct[threadIdx.x] = 0;
@@ -4347,10 +4749,10 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 	const uint32_t stride = gridDim.x * 256u;
 #if CTC == 4
 	ctc_ent<K> e0{}, e1{}, e2{}, e3{};
-	ct_cache<K> c{e0, e1, e2, e3, 0u};
+	ct_cache<K> c{e0, e1, e2, e3, 0u, 0u};
 #else
 	ctc_ent<K> e0{}, e1{}, e2{};
-	ct_cache<K> c{e0, e1, e2, 0u};
+	ct_cache<K> c{e0, e1, e2, 0u, 0u};
 #endif
 	auto pkt_of = [](uint32_t v) { return MODE == WALK_OWED ? v >> 1 : v; };
 	/* groups longest first (a.glen / a.gpos, sorted by length): the
@@ -4361,18 +4763,24 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 		/* packets in batch order through the sort permutation, software-
 		 * pipelined: the record of p + 1 and the index of p + 2 are in
 		 * flight while packet p runs */
-		uint32_t ni = a.idx_sorted[p0];
-		uint32_t nni = p0 + 1u < p1 ? a.idx_sorted[p0 + 1u] : 0u;
-		R nr = R::load(a.rec, pkt_of(ni), false);
+		uint32_t n1 = a.idx_sorted[p0];
+		uint32_t n2 = p0 + 1u < p1 ? a.idx_sorted[p0 + 1u] : n1;
+		uint32_t n3 = p0 + 2u < p1 ? a.idx_sorted[p0 + 2u] : n1;
+		R r1 = R::load(a.rec, pkt_of(n1), false);
+		R r2 = p0 + 1u < p1 ? R::load(a.rec, pkt_of(n2), false) : r1;
 		for (uint64_t p = p0; p < p1; p++) {
-			const uint32_t v = ni;
+			/* records two packets ahead and the index three ahead are in
+			 * flight while packet p runs */
+			const uint32_t v = n1;
 			const uint32_t i = pkt_of(v);
-			const R r = nr;
-			if (p + 1u < p1) {
-				ni = nni;
-				nr = R::load(a.rec, pkt_of(ni), false);
-				if (p + 2u < p1)
-					nni = a.idx_sorted[p + 2u];
+			const R r = r1;
+			n1 = n2;
+			r1 = r2;
+			if (p + 2u < p1) {
+				n2 = n3;
+				r2 = R::load(a.rec, pkt_of(n2), false);
+				if (p + 3u < p1)
+					n3 = a.idx_sorted[p + 3u];
 			}
 			const uint32_t meta = r.meta();
 			if (meta & CTM_GATED)
@@ -4381,7 +4789,14 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 			dg_steps++;
 #endif
 			if constexpr (MODE == WALK_SVC) {
-				a.svc_out[i] = ct_svc_step(s, T, A, c, r, a.now);
+				if constexpr (K::V6 != 0) {
+					uint4 tg = make_uint4(0, 0, 0, 0);
+					const uint4 o = ct_svc_step6(s, T, A, c, r, a.now, tg);
+					a.svc_out[2u * i] = o;
+					a.svc_out[2u * i + 1u] = tg;
+				} else {
+					a.svc_out[i] = ct_svc_step(s, T, A, c, r, a.now);
+				}
 			} else {
 				const ct_pkt q = r.pkt();
 				if constexpr (MODE == WALK_OWED) {
@@ -4553,7 +4968,7 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.hash = L.hash;
 	a.svc_out = L.svc_out;
 	a.ctl = L.ctl;
-	a.xdaddr = L.xdaddr;
+	a.xdaddr = static_cast<uint32_t *>(L.xdaddr);
 	a.xdport = L.xdport;
 	return a;
 }
@@ -4616,7 +5031,7 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	ct_args a = ct_args_of(L);
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	if (K::V6)
-		hipLaunchKernelGGL(k_ct_prep6, dim3(g), dim3(256), 0, st, s, a);
+		hipLaunchKernelGGL(k_ct_prep6<false>, dim3(g), dim3(256), 0, st, s, a);
 	else
 		hipLaunchKernelGGL((k_ct_prep<false, false>), dim3(g), dim3(256), 0, st, s, a);
 	uint32_t nh;
@@ -4638,6 +5053,29 @@ hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, cons
 				 hipStream_t st)
 {
 	return launch_ct<CtK6>(s, T, L, st);
+}
+
+/* cgpu_classify_v6_ctlb: the IPv6 service walk (k_svc_prep6, WALK_SVC over
+ * CtK6), then the IPv6 conntrack path with the service's state; ct_create6
+ * writes no address entry, so there is no phase 2 */
+hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				   hipStream_t st)
+{
+	ct_args a = ct_args_of(L);
+	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
+	hipLaunchKernelGGL(k_svc_prep6, dim3(g), dim3(256), 0, st, s, a);
+	uint32_t nh;
+	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_walk<CtK6, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
+	e = ct_group_sort(s, L, a, L.n, &nh, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_walk<CtK6S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	launch_ct_finish<CtK6S>(s, a, st);
+	return hipGetLastError();
 }
 
 /*

@@ -152,7 +152,7 @@ struct ct_launch {
 	uint4 *svc_out;       /* [n] */
 	uint32_t *ctl;        /* [4] */
 	uint8_t *flags2;      /* [2n] */
-	uint32_t *xdaddr;     /* [n] optional */
+	void *xdaddr;         /* [n] optional (IPv6: 16 bytes each) */
 	uint16_t *xdport;     /* [n] optional */
 };
 
@@ -163,6 +163,10 @@ hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, cons
 hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
 				 hipStream_t st);
 
+/* behind the IPv6 stateful service step (cilium_ct6_global, rec [4n],
+ * svc_out [2n], xdaddr 16 bytes per packet) */
+hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
+				   hipStream_t st);
 /* the same behind the stateful service step (cilium_ct4_global, rec [3n]) */
 hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
 				   hipStream_t st);

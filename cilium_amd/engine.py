@@ -479,6 +479,29 @@ class Engine:
               "cgpu_classify_v6_ct")
         return out
 
+    def classify_v6_ctlb(self, t: dict, now: int, out: dict | None = None, stage: bool = True,
+                         xlate: bool = True, stream=None):
+        """cgpu_classify_v6_ctlb: classify_v6_ct with the stateful service
+        step (lb6_local with CONNTRACK) in front; out "daddr" is (n, 16)
+        uint8."""
+        import torch
+        n = t["saddr"].shape[0]
+        dev = t["saddr"].device
+        if out is None:
+            out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+                   "ct_ret": torch.empty(n, dtype=torch.uint8, device=dev),
+                   "identity": torch.empty(n, dtype=torch.int32, device=dev),
+                   "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None,
+                   "daddr": torch.empty((n, 16), dtype=torch.uint8, device=dev) if xlate else None,
+                   "dport": torch.empty(n, dtype=torch.int16, device=dev) if xlate else None}
+        tv = TuplesV6Ct(*[t[k].data_ptr() for k in
+                          ("saddr", "daddr", "sport", "dport", "proto", "l4b", "flags", "len", "ep")])
+        ov = CtlbOut(*[_ptr(out.get(k)) for k in ("verdict", "ct_ret", "identity", "stage", "daddr",
+                                                   "dport")])
+        check(self.L.cgpu_classify_v6_ctlb(self.h, C.byref(tv), _ptr(t.get("hash")), n, now,
+                                           C.byref(ov), _stream(stream)), "cgpu_classify_v6_ctlb")
+        return out
+
     def classify_v4_lb(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
         """classify_v4 with the egress service step first (BASELINE config 5).
         t additionally holds "hash" (int32 view of skb->hash) or "sport"."""

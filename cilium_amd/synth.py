@@ -981,6 +981,67 @@ def make_ct6_workload(tables, n_conn: int, seed=SEED, gpu_id: int = 0, n_remote=
     return t, loc, seclabels
 
 
+def make_ctlb6_workload(tables, svcs: Services, n_conn: int, seed=SEED, gpu_id: int = 0,
+                        vip_frac: float = 0.4, mean_pkts: float = 8.0, span: float = 0.02,
+                        loop_frac: float = 0.02, world: int = 1):
+    """make_ctlb_workload for IPv6 (cgpu_classify_v6_ctlb) over Tables6 and
+    make_services6: `vip_frac` of the remotes are service addresses, replies
+    from the service address or (2/3 of the connections) the backend,
+    `loop_frac` of the backends are the endpoints themselves, hash = the
+    egress direction's cgpu_flow_hash6, redrawn for 5 % of the packets.
+    Returns (t, locals, seclabels, services)."""
+    from .shard import flowhash6_np, pairhash6_np
+    rng = np.random.Generator(np.random.PCG64(seed + 0xCB600 + gpu_id))
+    loc, seclabels = ct6_endpoints(tables, tables.n_endpoints)
+    ns = len(svcs.vip)
+    vals = svcs.vals.copy()
+    nb = vals["count"][:ns].astype(np.int64)
+    loop = rng.random(len(vals) - ns) < loop_frac
+    vals["target"][ns:] = np.where(loop[:, None], loc[rng.integers(0, len(loc), len(loop))],
+                                   vals["target"][ns:])
+    svcs = Services(svcs.keys, vals, svcs.vip, svcs.port)
+    nr = max(16, n_conn // 4)
+    pi = rng.integers(0, len(tables.pfx_addr), nr)
+    host = rng.integers(0, 256, (nr, 16), dtype=np.uint8)
+    m = MASK6[tables.pfx_len[pi]]
+    rem = np.where((rng.random(nr) < 0.8)[:, None], tables.pfx_addr[pi] | (host & ~m), host)
+    nv = int(nr * vip_frac / (1.0 - vip_frac))
+    rem = np.concatenate([rem, svcs.vip[rng.integers(0, ns, nv)]]).astype(np.uint8)
+    ok = None
+    if world > 1:
+        ok = lambda a, b: (pairhash6_np(a, b) % np.uint32(world)) == gpu_id  # noqa: E731
+    t = make_ct_stream(rng, n_conn, loc, rem, mean_pkts=mean_pkts, span=span, pair_ok=ok)
+    eg = (t["flags"] & 1).astype(bool)
+    remote = np.where(eg[:, None], t["daddr"], t["saddr"])
+    # make_services6 VIPs: fd00:96:<index>:...; match the index, then the row
+    si = np.ascontiguousarray(remote[:, 4:8]).view(np.uint32)[:, 0].astype(np.int64)
+    isv = (remote[:, :4] == [0xFD, 0x00, 0x00, 0x96]).all(axis=1) & (si < ns)
+    si = np.where(isv, si, 0)
+    isv &= (svcs.vip[si] == remote).all(axis=1)
+    port = svcs.port[si]
+    l4 = np.isin(t["proto"], [6, 17])
+    setp = isv & (port != 0) & l4
+    t["dport"] = np.where(eg & setp, port, t["dport"]).astype(np.uint16)
+    t["sport"] = np.where(~eg & setp, port, t["sport"]).astype(np.uint16)
+    lport = np.where(eg, t["sport"], t["dport"]).astype(np.int64)
+    first = (ns + np.cumsum(nb) - nb)[si]
+    bi = first + lport % np.maximum(nb[si], 1)
+    fromb = ~eg & isv & (nb[si] > 0) & (lport % 3 != 0)
+    bi = np.where(fromb, bi, 0)
+    t["saddr"] = np.where(fromb[:, None], vals["target"][bi], t["saddr"]).astype(np.uint8)
+    bport = vals["port"][bi]
+    t["sport"] = np.where(fromb & l4 & (bport != 0), bport, t["sport"]).astype(np.uint16)
+    lo = np.where(eg[:, None], t["saddr"], t["daddr"])
+    rm = np.where(eg[:, None], t["daddr"], t["saddr"])
+    lp = np.where(eg, t["sport"], t["dport"])
+    rp = np.where(eg, t["dport"], t["sport"])
+    h = flowhash6_np(lo, rm, lp, rp, t["proto"])
+    redraw = rng.random(len(h)) < 0.05
+    h[redraw] = rng.integers(0, 2**32, int(redraw.sum()), dtype=np.uint64).astype(np.uint32)
+    t["hash"] = h.astype(np.uint32)
+    return t, loc, seclabels, svcs
+
+
 def load_lxc(target, seclabels):
     """cgpu_lxc_update / or_lxc_update: the SECLABEL of every endpoint."""
     for ep, sl in enumerate(seclabels):

@@ -801,6 +801,37 @@ int cgpu_classify_v6_ct(cgpu_ctx *ctx, const cgpu_tuples_v6_ct *t, size_t n, uin
 			int32_t *verdict, uint8_t *ct_ret, uint32_t *identity, uint8_t *stage,
 			void *stream);
 
+/* cgpu_classify_v6_ctlb's outputs: as cgpu_ctlb_out with the frame's daddr
+ * 16 bytes per packet (16-byte aligned) */
+typedef struct cgpu_ctlb6_out {
+	int32_t *verdict;
+	uint8_t *ct_ret;
+	uint32_t *identity;
+	uint8_t *stage;
+	uint8_t *daddr;     /* [n][16]: the frame's daddr after lb6_xlate */
+	uint16_t *dport;
+} cgpu_ctlb6_out;
+
+/*
+ * cgpu_classify_v6_ct with the stateful service step of ipv6_l3_from_lxc in
+ * front (bpf_lxc.c:122-146; lb6_local with CONNTRACK, lib/lb.h:426-483):
+ * egress packets whose {daddr, dport} (or {daddr, 0}) is an IPv6 service
+ * (lb6_extract_key / lb6_lookup_service, lb.h:327-365) look up their
+ * CT_SERVICE entry in cilium_ct6_global; CT_NEW selects slave = hash % count
+ * + 1 and creates it (ct_create6 with its ICMPv6 entry; a failed create
+ * drops with DROP_NO_SERVICE), a hit reuses the stored slave; a slave whose
+ * backend is gone falls back to lb6_lookup_service with key.slave kept and
+ * ct_update6_slave; no service -> DROP_NO_SERVICE.  lb6_xlate rewrites the
+ * frame's daddr (and the dport for TCP / UDP under CGPU_LB_L4); the tuple's
+ * daddr becomes the backend, its dport the rewritten one.  Then the egress
+ * conntrack path of cgpu_classify_v6_ct on that tuple, identity from the
+ * ipcache of the backend, CT_NEW creates the entry with the service's
+ * rev_nat_index and slave (ct_create6 writes no address entry).  Outputs as
+ * cgpu_classify_v4_ctlb.  n < 2^30; address columns 16-byte aligned.
+ */
+int cgpu_classify_v6_ctlb(cgpu_ctx *ctx, const cgpu_tuples_v6_ct *t, const uint32_t *hash, size_t n,
+			  uint32_t now, const cgpu_ctlb6_out *out, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* checkpoint / resume                                      */
 /* ------------------------------------------------------------------ */

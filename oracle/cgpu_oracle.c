@@ -2911,3 +2911,280 @@ int or_classify_v6_ct(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t
 		*probe_sum = ops;
 	return 0;
 }
+
+/* ct_create6 (conntrack.h:588-639) with the service's ct_state: the entry
+ * carries rev_nat_index, lb_loopback and slave (IPv6 writes no address
+ * entry) */
+static int ct6_create_st(or_ctx *c, const struct ct6_key *k, int dir, const struct ct_st *st, uint32_t len,
+			 uint32_t now, uint64_t *ops)
+{
+	struct ct_val e;
+	struct ct6_key ik;
+	int tcp = k->nexthdr == PROTO_TCP;
+	memset(&e, 0, sizeof(e));
+	e.rev_nat_index = st->rev_nat;
+	if (st->loopback)
+		e.bits |= CTB_LB_LOOPBACK;
+	e.slave = st->slave;
+	ct_timeout(&e, now, tcp, dir, tcp ? 1u : 0u);
+	if (dir == CT_INGRESS) {
+		e.rx_packets = 1;
+		e.rx_bytes = len;
+	} else {
+		e.tx_packets = 1;
+		e.tx_bytes = len;
+	}
+	e.src_sec_id = st->src_sec_id;
+	*ops += 1;
+	if (or_ct6_update(c, k, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	memset(&ik, 0, sizeof(ik));
+	memcpy(ik.daddr, k->daddr, 16);
+	memcpy(ik.saddr, k->saddr, 16);
+	ik.nexthdr = PROTO_ICMPV6_;
+	ik.flags = k->flags | TUPLE_F_RELATED;
+	e.bits |= CTB_SEEN_NON_SYN;
+	*ops += 1;
+	if (or_ct6_update(c, &ik, &e) < 0)
+		return DROP_CT_CREATE_FAILED;
+	return 0;
+}
+
+/* ct_lookup6's tuple setup (conntrack.h:308-378) for direction flags fl;
+ * returns the action or -1 (DROP_CT_UNKNOWN_PROTO) */
+static int ct6_setup(struct ct6_key *k, uint8_t fl, uint8_t pr, uint16_t l4b, uint16_t fsport, uint16_t fdport,
+		     uint16_t *w)
+{
+	*w = 0;
+	k->nexthdr = pr;
+	k->flags = fl;
+	k->sport = k->dport = 0;
+	if (pr == PROTO_ICMPV6_) {
+		uint8_t type = (uint8_t)l4b;
+		if (type >= 1 && type <= 4) {
+			k->flags |= TUPLE_F_RELATED;
+			return ACTION_UNSPEC;
+		}
+		if (type == 129) {
+			k->dport = 128;
+			return ACTION_UNSPEC;
+		}
+		if (type == 128)
+			k->sport = 128;
+		return ACTION_CREATE;
+	}
+	if (pr == PROTO_TCP || pr == PROTO_UDP) {
+		k->dport = fsport;
+		k->sport = fdport;
+		if (pr == PROTO_TCP) {
+			*w = l4b;
+			return TF_BIT0(*w) ? ACTION_CLOSE : ACTION_CREATE;
+		}
+		return ACTION_CREATE;
+	}
+	return -1;
+}
+
+/*
+ * or_classify_v6_ct with the stateful service step of ipv6_l3_from_lxc in
+ * front (lb6_local with CONNTRACK, lb.h:426-483; see cgpu.h
+ * cgpu_classify_v6_ctlb and oracle/ref/harness_ctlb.c
+ * ref_ctlb_classify_v6).  hash NULL: or_flow_hash6.  xdaddr16 / xdport
+ * (optional): the frame's daddr / dport after the service step.
+ */
+int or_classify_v6_ctlb(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+			const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+			const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+			const uint16_t *ep, const uint32_t *hash, uint32_t now, int32_t *verdict,
+			uint8_t *ct_ret, uint32_t *identity, uint8_t *stage, uint8_t *xdaddr16,
+			uint16_t *xdport, uint64_t *probe_sum)
+{
+	const or_config *cfg = &c->cfg;
+	uint64_t ops = 0;
+	for (size_t i = 0; i < n; i++) {
+		const int egress = flags[i] & 1;
+		const int dir = egress ? CT_EGRESS : CT_INGRESS;
+		const int mdir = egress ? METRIC_EGRESS : METRIC_INGRESS;
+		const uint8_t pr = proto[i];
+		const uint8_t *sa = saddr16 + 16 * i, *da = daddr16 + 16 * i;
+		struct ohash *h = ep[i] < c->n_ep ? &c->policy[ep[i]] : NULL;
+		struct ct_st st;
+		struct ct6_key k;
+		uint8_t fdaddr[16];
+		uint32_t id = 0;
+		uint16_t fdport = dport[i], w;
+		int32_t v, fin = 0;
+		int action, ret = 255, pstage = 0;
+		struct pol_res r;
+
+		memset(&st, 0, sizeof(st));
+		memset(&k, 0, sizeof(k));
+		memcpy(k.daddr, da, 16);
+		memcpy(k.saddr, sa, 16);
+		memcpy(fdaddr, da, 16);
+		if (egress) {
+			uint16_t kd = 0;
+			int skip = 0;
+			const uint8_t *svc = NULL;
+			if (cfg->lb_l4) { /* extract_l4_port (lb.h:192-216) */
+				if (pr == PROTO_TCP || pr == PROTO_UDP)
+					kd = dport[i];
+				else if (pr != PROTO_ICMP && pr != PROTO_ICMPV6)
+					skip = 1;
+			}
+			if (!skip)
+				svc = lb6_lookup_service(c, da, &kd, 0, &ops);
+			if (svc) {
+				/* lb6_local (lb.h:426-483) */
+				const uint32_t hh = hash ? hash[i] : or_flow_hash6(sa, da, sport[i], dport[i], pr);
+				struct ct6_key sk;
+				const uint8_t *be;
+				int sret = -1;
+				memset(&sk, 0, sizeof(sk));
+				memcpy(sk.daddr, da, 16);
+				memcpy(sk.saddr, sa, 16);
+				action = ct6_setup(&sk, TUPLE_F_SERVICE, pr, l4b[i], sport[i], dport[i], &w);
+				if (action >= 0) {
+					ops += 1;
+					if (ct_lookup_kb(&c->ct6, (const uint8_t *)&sk, action, CT_SERVICE, pr == PROTO_TCP, w,
+							 len[i], now)) {
+						struct ct_val e;
+						memcpy(&e, oh_get(&c->ct6, &sk), 56);
+						st.loopback = (e.bits & CTB_LB_LOOPBACK) ? 1 : 0;
+						st.slave = e.slave;
+						sret = 0;
+					} else {
+						st.slave = (uint16_t)(hh % lb6v_count(svc) + 1); /* lb6_select_slave */
+						sret = ct6_create_st(c, &sk, CT_SERVICE, &st, len[i], now, &ops);
+					}
+				}
+				if (sret < 0) {
+					fin = DROP_NO_SERVICE;
+					goto service_drop;
+				}
+				be = lb6_get(c, da, kd, st.slave, &ops); /* lb6_lookup_slave */
+				if (!be) {
+					be = lb6_lookup_service(c, da, &kd, st.slave, &ops);
+					if (!be) {
+						fin = DROP_NO_SERVICE;
+						goto service_drop;
+					}
+					st.slave = (uint16_t)(hh % lb6v_count(be) + 1);
+					{ /* ct_update6_slave (conntrack.h:572-584) */
+						uint8_t *p = oh_get(&c->ct6, &sk);
+						ops += 1;
+						if (p)
+							memcpy(p + 40, &st.slave, 2); /* ct_entry.slave */
+					}
+				}
+				st.rev_nat = lb6v_rev_nat(be);
+				memcpy(k.daddr, be, 16); /* tuple->daddr = svc->target */
+				memcpy(fdaddr, be, 16);
+				if (cfg->lb_l4 && lb6v_port(be) && kd != lb6v_port(be) &&
+				    (pr == PROTO_TCP || pr == PROTO_UDP))
+					fdport = lb6v_port(be);
+			}
+		} else {
+			/* ipv6_policy: daddr.s6_addr32[3] & 0xFFFF (bpf_lxc.c:748) */
+			st.rev_nat = (uint16_t)(da[12] | (da[13] << 8));
+		}
+		action = ct6_setup(&k, egress ? TUPLE_F_IN : TUPLE_F_OUT, pr, l4b[i], sport[i], fdport, &w);
+		if (action < 0) {
+			fin = DROP_CT_UNKNOWN_PROTO;
+			pstage = 4;
+			goto out;
+		}
+		{
+			uint8_t orig_dip[16];
+			memcpy(orig_dip, k.daddr, 16);
+			ops += 1;
+			if (ct_lookup_kb(&c->ct6, (const uint8_t *)&k, action, dir, pr == PROTO_TCP, w, len[i], now)) {
+				ret = (k.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+			} else {
+				ct6_reverse(&k);
+				ops += 1;
+				ret = ct_lookup_kb(&c->ct6, (const uint8_t *)&k, action, dir, pr == PROTO_TCP, w, len[i],
+						   now)
+					      ? CT_ESTABLISHED
+					      : CT_NEW;
+			}
+			if (egress) { /* bpf_lxc.c:172-189: ipcache6(orig_dip), the frame's daddr /64 */
+				const uint8_t *info = ipcache6(c, orig_dip);
+				uint32_t label = 0;
+				if (info)
+					memcpy(&label, info, 4);
+				if (info && label)
+					id = label;
+				else if (!memcmp(fdaddr, cfg->router_ip, 8))
+					id = cfg->cluster_id;
+				else
+					id = cfg->world_id;
+				ops += 1;
+				r = policy_access(h, id, k.dport, pr, 1, 0, len[i]);
+			} else { /* bpf_netdev.c:203-211 */
+				uint32_t src = cfg->ingress_src_identity;
+				if (src < cfg->health_id) {
+					const uint8_t *info = ipcache6(c, sa);
+					ops += 1;
+					if (info) {
+						uint32_t label;
+						memcpy(&label, info, 4);
+						if (label && label != cfg->cluster_id)
+							src = label;
+					}
+				}
+				id = src;
+				r = policy_access(h, id, k.dport, pr, 0, 0, len[i]);
+			}
+		}
+		ops += (uint64_t)r.probes;
+		pstage = r.stage;
+		v = r.ret >= 0 ? r.ret : DROP_POLICY;
+		if (ret != CT_REPLY && ret != CT_RELATED && v < 0) {
+			if (ret == CT_ESTABLISHED) {
+				ops += 1;
+				oh_delete(&c->ct6, &k);
+			}
+			fin = DROP_POLICY;
+		} else {
+			int cr = 0;
+			if (ret == CT_NEW) {
+				uint32_t sec = 0;
+				if (egress && ep[i] < c->n_lxcinfo)
+					memcpy(&sec, c->lxcinfo + (size_t)ep[i] * 32 + 28, 4); /* SECLABEL */
+				st.src_sec_id = egress ? sec : id;
+				cr = ct6_create_st(c, &k, dir, &st, len[i], now, &ops);
+			}
+			if (cr < 0)
+				fin = cr;
+			else if (v > 0 && (egress || ret == CT_NEW || ret == CT_ESTABLISHED))
+				fin = v;
+			else
+				fin = 0;
+		}
+		goto out;
+	service_drop:
+		pstage = 6;
+		id = 0;
+		ret = 255;
+	out:
+		verdict[i] = fin;
+		ct_ret[i] = (uint8_t)ret;
+		if (identity)
+			identity[i] = id;
+		if (stage)
+			stage[i] = (uint8_t)pstage;
+		if (xdaddr16)
+			memcpy(xdaddr16 + 16 * i, fdaddr, 16);
+		if (xdport)
+			xdport[i] = fdport;
+		if (fin <= 0) {
+			uint32_t reason = fin < 0 ? (uint32_t)(-fin) & 0xff : 0;
+			c->metrics[(reason * 4 + mdir) * 2] += 1;
+			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
+		}
+	}
+	if (probe_sum)
+		*probe_sum = ops;
+	return 0;
+}

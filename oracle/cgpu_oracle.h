@@ -232,6 +232,14 @@ int or_classify_v4_ctlb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32
 			uint8_t *ct_ret, uint32_t *identity, uint8_t *stage, uint32_t *xdaddr,
 			uint16_t *xdport, uint64_t *probe_sum);
 
+/* the IPv6 form of or_classify_v4_ctlb (lb6_local with CONNTRACK, lb.h:426-483) */
+int or_classify_v6_ctlb(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t *daddr16,
+			const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+			const uint16_t *l4b, const uint8_t *flags, const uint32_t *len,
+			const uint16_t *ep, const uint32_t *hash, uint32_t now, int32_t *verdict,
+			uint8_t *ct_ret, uint32_t *identity, uint8_t *stage, uint8_t *xdaddr16,
+			uint16_t *xdport, uint64_t *probe_sum);
+
 /*
  * L3 MapState compilation: the tables of cgpu.h
  * cgpu_l3_program / cgpu_label_sets (interned ids, see cilium_amd/policy.py);

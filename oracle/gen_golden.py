@@ -1245,13 +1245,9 @@ def ref_ct6_run(lib, t, now, seclabels, src_identity=0):
     return out
 
 
-def gen_ct6_fixture(lib, pol, rng):
-    """IPv6 stateful path (SURVEY §8f row 3, CT_MAP6): as gen_ct_fixture over
-    ct_lookup6 / ct_create6 / ct_delete6 in the v6 endpoint programs' order:
-    ICMPv6 echo / errors, the ingress reverse-NAT index taken from the
-    destination address, ROUTER_IP /64 cluster fallback; 4 batches with
-    pre-installed entries and policy deletions, a small-map run, and a run
-    with a reserved ingress source identity (ipcache-resolved sources)."""
+def ct6_tables(pol, rng):
+    """The IPv6 stateful fixtures' tables: ipcache6 prefixes, 4 local
+    endpoints (two inside ROUTER_IP's /64), remotes, per-endpoint policy."""
     router = C.create_string_buffer(16)
     pol.ref_router_ip(router)
     router = np.frombuffer(router.raw, np.uint8).copy()
@@ -1297,6 +1293,17 @@ def gen_ct6_fixture(lib, pol, rng):
             pep.append(ep)
     pk, pe, pep = (np.array(pk, L.POLICY_KEY), np.array(pe, L.POLICY_ENTRY),
                    np.array(pep, np.uint16))
+    return router, ikeys, ivals, locals6, remotes6, pk, pe, pep
+
+
+def gen_ct6_fixture(lib, pol, rng):
+    """IPv6 stateful path (SURVEY §8f row 3, CT_MAP6): as gen_ct_fixture over
+    ct_lookup6 / ct_create6 / ct_delete6 in the v6 endpoint programs' order:
+    ICMPv6 echo / errors, the ingress reverse-NAT index taken from the
+    destination address, ROUTER_IP /64 cluster fallback; 4 batches with
+    pre-installed entries and policy deletions, a small-map run, and a run
+    with a reserved ingress source identity (ipcache-resolved sources)."""
+    router, ikeys, ivals, locals6, remotes6, pk, pe, pep = ct6_tables(pol, rng)
     seclabels = np.array([6000 + 11 * i for i in range(4)], np.uint32)
     t = synth.make_ct_stream(rng, 700, locals6, remotes6, mean_pkts=6.0, span=0.05)
     n = len(t["saddr"])
@@ -1385,6 +1392,16 @@ def load_ref_ctlb():
     lib.ref_ctlb_svc_delete.argtypes = [C.c_void_p]
     lib.ref_ctlb_policy_delete.argtypes = [C.c_int, C.c_void_p]
     lib.ref_ctlb_ct_update.argtypes = [C.c_void_p, C.c_void_p]
+    lib.ref_ctlb_svc6_update.argtypes = [C.c_void_p, C.c_void_p]
+    lib.ref_ctlb_svc6_delete.argtypes = [C.c_void_p]
+    lib.ref_ctlb_ct6_update.argtypes = [C.c_void_p, C.c_void_p]
+    lib.ref_ctlb6_count.restype = C.c_size_t
+    lib.ref_ctlb6_entry.argtypes = [C.c_size_t, C.c_void_p, C.c_void_p]
+    lib.ref_ctlb_classify_v6.argtypes = [C.c_char_p, C.c_char_p, C.c_uint16, C.c_uint16, C.c_uint8,
+                                         C.c_uint16, C.c_uint8, C.c_uint32, C.c_int, C.c_uint32,
+                                         C.c_uint32, C.c_uint32, C.POINTER(C.c_int),
+                                         C.POINTER(C.c_uint32), C.POINTER(C.c_int), C.c_char_p,
+                                         C.POINTER(C.c_uint16), C.POINTER(C.c_int)]
     lib.ref_ctlb_count.restype = C.c_size_t
     lib.ref_ctlb_entry.argtypes = [C.c_size_t, C.c_void_p, C.c_void_p]
     lib.ref_ctlb_classify_v4.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_uint8,
@@ -1585,6 +1602,189 @@ def gen_ctlb_fixture(lib, rng):
                 **{"t2_" + k: v for k, v in t2.items()}, **res)
 
 
+def ref_ctlb6_dump(lib):
+    n = lib.ref_ctlb6_count()
+    keys = np.zeros(n, L.CT6_TUPLE)
+    vals = np.zeros(n, L.CT_ENTRY)
+    kb, vb = C.create_string_buffer(38), C.create_string_buffer(56)
+    for i in range(n):
+        assert lib.ref_ctlb6_entry(i, kb, vb) == 0
+        keys[i] = np.frombuffer(kb.raw, L.CT6_TUPLE)[0]
+        vals[i] = np.frombuffer(vb.raw, L.CT_ENTRY)[0]
+    return L.ct_sorted(keys, vals)
+
+
+def ref_ctlb6_run(lib, t, now, seclabels):
+    n = len(t["saddr"])
+    out = {"verdict": np.empty(n, np.int32), "ct_ret": np.empty(n, np.uint8),
+           "identity": np.empty(n, np.uint32), "stage": np.empty(n, np.uint8),
+           "xdaddr": np.empty((n, 16), np.uint8), "xdport": np.empty(n, np.uint16),
+           "svc_hit": np.empty(n, np.uint8)}
+    cr, idv, st, xp, sh = C.c_int(), C.c_uint32(), C.c_int(), C.c_uint16(), C.c_int()
+    xd = C.create_string_buffer(16)
+    lib.ref_ctlb_set_now(now)
+    for i in range(n):
+        ep = int(t["ep"][i])
+        out["verdict"][i] = lib.ref_ctlb_classify_v6(
+            t["saddr"][i].tobytes(), t["daddr"][i].tobytes(), int(t["sport"][i]), int(t["dport"][i]),
+            int(t["proto"][i]), int(t["l4b"][i]), int(t["flags"][i]), int(t["len"][i]), ep,
+            int(seclabels[ep]), int(t["hash"][i]), 0, C.byref(cr), C.byref(idv), C.byref(st), xd,
+            C.byref(xp), C.byref(sh))
+        out["ct_ret"][i] = cr.value if 0 <= cr.value < 255 else L.CT_NONE
+        out["identity"][i], out["stage"][i] = idv.value, st.value
+        out["xdaddr"][i] = np.frombuffer(xd.raw, np.uint8)
+        out["xdport"][i], out["svc_hit"][i] = xp.value, sh.value
+    return out
+
+
+def ctlb6_stream(rng, n_conn, locals6, remotes6, lb_keys, lb_vals, vips):
+    """ctlb_stream over IPv6 addresses ((n, 16) uint8)."""
+    rem = np.concatenate([remotes6, np.repeat(vips, 4, axis=0)]).astype(np.uint8)
+    t = synth.make_ct_stream(rng, n_conn, locals6, rem, mean_pkts=6.0, span=0.05)
+    ports, backs = {}, {}
+    for k, v in zip(lb_keys, lb_vals):
+        a = k["address"].tobytes()
+        if int(k["dport"]):
+            ports.setdefault(a, set()).add(int(k["dport"]))
+        if int(k["slave"]) and v["target"].any():
+            backs.setdefault(a, []).append((v["target"].copy(), int(v["port"])))
+    vipset = set(v.tobytes() for v in vips)
+    eg = (t["flags"] & 1).astype(bool)
+    for i in range(len(t["saddr"])):
+        vip = (t["daddr"][i] if eg[i] else t["saddr"][i]).tobytes()
+        if vip not in vipset:
+            continue
+        rp = int(t["dport"][i]) if eg[i] else int(t["sport"][i])
+        ps = sorted(ports.get(vip, ()))
+        if ps and (rp * 2654435761) % 7 != 0:
+            rp = ps[(rp * 40503) % len(ps)]
+        if eg[i]:
+            t["dport"][i] = rp
+        else:
+            t["sport"][i] = rp
+            bl = backs.get(vip, [])
+            if bl and (int(t["dport"][i]) * 2246822519) % 3 != 0:
+                tg, tp = bl[int(t["dport"][i]) % len(bl)]
+                t["saddr"][i] = tg
+                if tp and t["proto"][i] in (6, 17):
+                    t["sport"][i] = tp
+    loc = np.where(eg[:, None], t["saddr"], t["daddr"])
+    rmt = np.where(eg[:, None], t["daddr"], t["saddr"])
+    lp = np.where(eg, t["sport"], t["dport"])
+    rp = np.where(eg, t["dport"], t["sport"])
+    h = shard.flowhash_np(shard.fold6_np(loc), shard.fold6_np(rmt), lp, rp, t["proto"])
+    redraw = rng.random(len(h)) < 0.1
+    h[redraw] = rng.integers(0, 2**32, int(redraw.sum()), dtype=np.uint64).astype(np.uint32)
+    h[:6] = [0, 1, 0xFFFFFFFF, 0x7FFFFFFF, 65536, 0x80000000]
+    t["hash"] = h.astype(np.uint32)
+    return t
+
+
+def gen_ctlb6_fixture(lib, pol, rng):
+    """The IPv6 stateful service step (lb6_local with CONNTRACK, lb.h:426-483)
+    composed with the v6 egress conntrack path in ipv6_l3_from_lxc order, as
+    gen_ctlb_fixture: 4 batches with backends deleted / re-added and policy
+    keys deleted, CT_SERVICE entries installed beforehand (slave 0 / past the
+    backends / lb_loopback), a small-map run."""
+    router, ikeys, ivals, locals6, remotes6, pk, pe, pep = ct6_tables(pol, rng)
+    seclabels = np.array([8000 + 17 * i for i in range(4)], np.uint32)
+    targets = np.concatenate([remotes6[:40], locals6]).astype(np.uint8)
+    keys, vals, vips = gen_lb6_services(rng, 24, targets)
+    t = ctlb6_stream(rng, 700, locals6, remotes6, keys, vals, vips)
+    n = len(t["saddr"])
+    cuts = np.array([0, n // 5, n // 2, (3 * n) // 4, n])
+    nows = np.array([100, 103, 250, 40000], np.uint32)
+    eg = (t["flags"] & 1).astype(bool)
+    pre_i = rng.choice(n, 30, replace=False)
+    vipset = set(v.tobytes() for v in vips)
+    tovip = np.flatnonzero(eg & np.array([d.tobytes() in vipset for d in t["daddr"]]) &
+                           np.isin(t["proto"], [6, 17]))
+    svc_i = rng.choice(tovip, min(20, len(tovip)), replace=False)
+    pre_k = np.zeros(30 + len(svc_i), L.CT6_TUPLE)
+    pe_ = eg[pre_i]
+    pre_k["daddr"][:30] = t["saddr"][pre_i]
+    pre_k["saddr"][:30] = t["daddr"][pre_i]
+    pre_k["dport"][:30] = np.where(t["proto"][pre_i] == 58, 0, t["dport"][pre_i])
+    pre_k["sport"][:30] = np.where(t["proto"][pre_i] == 58, 0, t["sport"][pre_i])
+    pre_k["nexthdr"][:30] = t["proto"][pre_i]
+    pre_k["flags"][:30] = np.where(pe_, L.TUPLE_F_OUT, L.TUPLE_F_IN)
+    pre_k["daddr"][30:] = t["daddr"][svc_i]
+    pre_k["saddr"][30:] = t["saddr"][svc_i]
+    pre_k["dport"][30:] = t["sport"][svc_i]
+    pre_k["sport"][30:] = t["dport"][svc_i]
+    pre_k["nexthdr"][30:] = t["proto"][svc_i]
+    pre_k["flags"][30:] = 4  # TUPLE_F_SERVICE
+    m = len(pre_k)
+    pre_v = np.zeros(m, L.CT_ENTRY)
+    for f in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
+        pre_v[f] = rng.integers(0, 1000, m)
+    pre_v["lifetime"] = rng.integers(0, 500, m)
+    pre_v["bits"] = rng.choice(np.array([0, 1, 2, 3, 8, 16, 19, 24], np.uint16), m)
+    pre_v["rev_nat_index"] = rng.integers(0, 3, m)
+    pre_v["slave"] = rng.choice(np.array([0, 1, 2, 3, 7, 40], np.uint16), m)
+    pre_v["tx_flags_seen"] = rng.integers(0, 256, m)
+    pre_v["rx_flags_seen"] = rng.integers(0, 256, m)
+    pre_v["src_sec_id"] = rng.integers(0, 70000, m)
+    pre_v["last_tx_report"] = rng.integers(0, 120, m)
+    pre_v["last_rx_report"] = rng.integers(0, 120, m)
+    pol_del = rng.choice(len(pk), len(pk) // 4, replace=False)
+    slaves = np.flatnonzero(keys["slave"] != 0)
+    svc_del = rng.choice(slaves, len(slaves) // 3, replace=False)
+    svc_readd = svc_del[: len(svc_del) // 2]
+    readd_vals = vals[svc_readd].copy()
+    readd_vals["target"] = targets[rng.integers(0, len(targets), len(svc_readd))]
+    readd_vals["port"] = np.where(rng.random(len(svc_readd)) < 0.5, 0,
+                                  rng.integers(1, 65536, len(svc_readd)))
+
+    def load(ct_max):
+        lib.ref_ctlb_reset(ct_max)
+        for k, v in zip(ikeys, ivals):
+            lib.ref_ctlb_ipcache_update(b(k), b(v))
+        for k, e, ep in zip(pk, pe, pep):
+            lib.ref_ctlb_policy_update(int(ep), b(k), b(e))
+        for k, v in zip(keys, vals):
+            lib.ref_ctlb_svc6_update(b(k), b(v))
+
+    load(1 << 20)
+    for k, v in zip(pre_k, pre_v):
+        assert lib.ref_ctlb_ct6_update(b(k), b(v)) == 0
+    outs, dumps = [], []
+    for bi in range(4):
+        if bi == 2:
+            for d in pol_del:
+                assert lib.ref_ctlb_policy_delete(int(pep[d]), b(pk[d])) == 0
+            for d in svc_del:
+                assert lib.ref_ctlb_svc6_delete(b(keys[d])) == 0
+        if bi == 3:
+            for d, v in zip(svc_readd, readd_vals):
+                lib.ref_ctlb_svc6_update(b(keys[d]), b(v))
+        tb = {k: v[cuts[bi]:cuts[bi + 1]] for k, v in t.items()}
+        outs.append(ref_ctlb6_run(lib, tb, int(nows[bi]), seclabels))
+        dumps.append(ref_ctlb6_dump(lib))
+    res = {f"b_{f}": np.concatenate([o[f] for o in outs]) for f in outs[0]}
+    res["dump_n"] = np.array([len(d[0]) for d in dumps], np.int64)
+    res["dump_keys"] = np.concatenate([d[0] for d in dumps])
+    res["dump_vals"] = np.concatenate([d[1] for d in dumps])
+    final = np.zeros(len(pk), L.POLICY_ENTRY)
+    buf = C.create_string_buffer(24)
+    for i, (k, ep) in enumerate(zip(pk, pep)):
+        if lib.ref_ctlb_policy_read(int(ep), b(k), buf) == 0:
+            final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+    res["final_entries"] = final
+    t2 = ctlb6_stream(rng, 200, locals6, remotes6, keys, vals, vips)
+    load(48)
+    o2 = ref_ctlb6_run(lib, t2, 500, seclabels)
+    d2 = ref_ctlb6_dump(lib)
+    res.update({f"s_{f}": v for f, v in o2.items()})
+    res["s_dump_keys"], res["s_dump_vals"] = d2
+    return dict(ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe, pol_ep=pep,
+                router_ip=router, locals=locals6, lb_keys=keys, lb_vals=vals, vips=vips,
+                svc_del=svc_del, svc_readd=svc_readd, readd_vals=readd_vals,
+                seclabels=seclabels, cuts=cuts, nows=nows, pre_keys=pre_k, pre_vals=pre_v,
+                pol_del=np.sort(pol_del), **{"t_" + k: v for k, v in t.items()},
+                **{"t2_" + k: v for k, v in t2.items()}, **res)
+
+
 def save(name, d):
     path = os.path.join(OUT, name)
     np.savez_compressed(path, **d)
@@ -1631,6 +1831,9 @@ def main():
     # the stateful service step (lb4_local with CONNTRACK), its own stream
     rng_ctlb = np.random.Generator(np.random.PCG64(SEED + 0xCB))
     manifest["files"]["ctlb4.npz"] = save("ctlb4.npz", gen_ctlb_fixture(load_ref_ctlb(), rng_ctlb))
+    # the IPv6 stateful service step (lb6_local with CONNTRACK), its own stream
+    rng_ctlb6 = np.random.Generator(np.random.PCG64(SEED + 0xCC))
+    manifest["files"]["ctlb6.npz"] = save("ctlb6.npz", gen_ctlb6_fixture(load_ref_ctlb(), pol, rng_ctlb6))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -104,6 +104,8 @@ def lib():
         L.or_ct6_gc.restype = sz
         L.or_classify_v4_ctlb.argtypes = [vp, sz] + [vp] * 10 + [C.c_uint32] + [vp] * 6 + [
             C.POINTER(C.c_uint64)]
+        L.or_classify_v6_ctlb.argtypes = [vp, sz] + [vp] * 10 + [C.c_uint32] + [vp] * 6 + [
+            C.POINTER(C.c_uint64)]
         L.or_classify_v6_ct.argtypes = [vp, sz] + [vp] * 9 + [C.c_uint32] + [vp] * 4 + [
             C.POINTER(C.c_uint64)]
         u32 = C.c_uint32
@@ -464,6 +466,28 @@ class Oracle:
                                       _p(ct_ret), _p(identity), _p(stage), C.byref(probes))
         assert rc == 0, rc
         return verdict, ct_ret, identity, stage, probes.value
+
+    def classify_v6_ctlb(self, t, now):
+        """or_classify_v6_ctlb: classify_v6_ct with the stateful service
+        step; t may carry a "hash" column.  xdaddr is (n, 16) uint8."""
+        n = len(t["saddr"])
+        out = {"verdict": np.empty(n, np.int32), "ct_ret": np.empty(n, np.uint8),
+               "identity": np.empty(n, np.uint32), "stage": np.empty(n, np.uint8),
+               "xdaddr": np.empty((n, 16), np.uint8), "xdport": np.empty(n, np.uint16)}
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint8), ("daddr", np.uint8), ("sport", np.uint16),
+            ("dport", np.uint16), ("proto", np.uint8), ("l4b", np.uint16), ("flags", np.uint8),
+            ("len", np.uint32), ("ep", np.uint16))]
+        h = np.ascontiguousarray(t["hash"], np.uint32) if t.get("hash") is not None else None
+        rc = self.L.or_classify_v6_ctlb(self.h, n, *[_p(a) for a in arrs],
+                                        None if h is None else _p(h), now,
+                                        *[_p(out[k]) for k in ("verdict", "ct_ret", "identity",
+                                                               "stage", "xdaddr", "xdport")],
+                                        C.byref(probes))
+        assert rc == 0, rc
+        out["probes"] = probes.value
+        return out
 
     # --- L3 MapState compilation (SURVEY §8f row 4) ---
     @staticmethod

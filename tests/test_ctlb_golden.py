@@ -107,3 +107,78 @@ def test_ctlb_small_map_vs_reference(golden):
     assert (g["s_verdict"] == DROP_NO_SERVICE).sum() > 0
     assert (g["s_verdict"] == L.DROP_CT_CREATE_FAILED).sum() > 0
     assert o.ct4_count() == 48
+
+
+# ---------------------------------------------------------------- IPv6
+def ctlb6_oracle(g, ct_max=1 << 20):
+    o = Oracle(router_ip=bytes(g["router_ip"]))
+    o.ct6_set_max(ct_max)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert o.ipcache_update(k, v) == 0
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert o.policy_update(int(ep), k, e) == 0
+    for ep, sl in enumerate(g["seclabels"]):
+        assert o.lxc_update(ep, L.lxc_info(b"\0" * 6, 0, b"\0" * 16, 0, int(sl))) == 0
+    for k, v in zip(g["lb_keys"], g["lb_vals"]):
+        assert o.lb6_update(k, v) == 0
+    return o
+
+
+def check6(out, g, p, sl, msg):
+    t = stream(g, "t_" if p == "b_" else "t2_")
+    for f in ("verdict", "ct_ret", "identity", "stage", "xdaddr"):
+        np.testing.assert_array_equal(out[f], g[p + f][sl], err_msg=f"{msg} {f}")
+    pr = t["proto"][sl]
+    eg = (t["flags"][sl] & 1).astype(bool)
+    m = ~eg | np.isin(pr, [6, 17])
+    np.testing.assert_array_equal(out["xdport"][m], g[p + "xdport"][sl][m], err_msg=f"{msg} xdport")
+
+
+def test_ctlb6_stream_vs_reference(golden):
+    g = golden("ctlb6.npz")
+    o = ctlb6_oracle(g)
+    for k, v in zip(g["pre_keys"], g["pre_vals"]):
+        assert o.ct6_update(k, v) == 0
+    t = stream(g)
+    cuts, nows = g["cuts"], g["nows"]
+    off = 0
+    for bi in range(4):
+        if bi == 2:
+            for d in g["pol_del"]:
+                assert o.policy_delete(int(g["pol_ep"][d]), g["pol_keys"][d]) == 0
+            for d in g["svc_del"]:
+                assert o.lb6_delete(g["lb_keys"][d]) == 0
+        if bi == 3:
+            for d, v in zip(g["svc_readd"], g["readd_vals"]):
+                assert o.lb6_update(g["lb_keys"][d], v) == 0
+        sl = slice(int(cuts[bi]), int(cuts[bi + 1]))
+        out = o.classify_v6_ctlb({k: v[sl] for k, v in t.items()}, int(nows[bi]))
+        check6(out, g, "b_", sl, f"batch {bi}")
+        n = int(g["dump_n"][bi])
+        keys, vals = o.ct6_dump()
+        np.testing.assert_array_equal(keys, g["dump_keys"][off:off + n], err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(vals, g["dump_vals"][off:off + n], err_msg=f"batch {bi}")
+        off += n
+    for i, (k, ep, fe) in enumerate(zip(g["pol_keys"], g["pol_ep"], g["final_entries"])):
+        rc, raw = o.policy_lookup(int(ep), k)
+        if i in set(g["pol_del"].tolist()):
+            assert rc != 0
+            continue
+        got = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (got["packets"], got["bytes"]) == (fe["packets"], fe["bytes"])
+    v, svc = g["b_verdict"], g["b_svc_hit"].astype(bool)
+    assert (svc & (v == DROP_NO_SERVICE)).sum() > 0
+    assert (svc & (g["b_xdaddr"] != t["daddr"]).any(axis=1)).sum() > 0
+    assert (g["dump_keys"]["flags"] == 4).sum() > 0
+
+
+def test_ctlb6_small_map_vs_reference(golden):
+    g = golden("ctlb6.npz")
+    o = ctlb6_oracle(g, ct_max=48)
+    out = o.classify_v6_ctlb(stream(g, "t2_"), 500)
+    check6(out, g, "s_", slice(None), "small map")
+    keys, vals = o.ct6_dump()
+    np.testing.assert_array_equal(keys, g["s_dump_keys"])
+    np.testing.assert_array_equal(vals, g["s_dump_vals"])
+    assert (g["s_verdict"] == DROP_NO_SERVICE).sum() > 0
+    assert o.ct6_count() == 48

@@ -82,6 +82,13 @@ else:
     d = synth.to_device(t)
     out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
            "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
+    # as bench.py: warm traffic, then the popularity rebalance of the
+    # counter slots (cgpu_counters_rebalance), then the measured launches
+    (e.classify_v4_lb if S is not None else e.classify_v4)(d, out=out)
+    torch.cuda.synchronize()
+    e.counter_fold()
+    torch.cuda.synchronize()
+    e.counters_rebalance()
     for _ in range(3):
         (e.classify_v4_lb if S is not None else e.classify_v4)(d, out=out)
 torch.cuda.synchronize()
