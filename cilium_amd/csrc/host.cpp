@@ -682,13 +682,12 @@ struct Rank6 {
 };
 
 struct V6Build {
-	std::vector<uint32_t> root; /* 2 x 65536: {row, short} */
-	std::vector<uint32_t> masks;
-	std::vector<uint32_t> lens; /* per mask row: tables.h v6_lpm.lens */
-	std::vector<uint32_t> vals;
-	Set16Build set;
-	std::vector<uint32_t> bloom; /* tables.h v6_lpm.bloom */
+	std::vector<uint32_t> root, b24, b32, pool, vals, rbits;
+	std::vector<uint16_t> b24_16; /* empty: not representable */
+	std::vector<std::array<uint32_t, 8>> h64;
+	uint32_t m64 = 0;
 	bool any = false;
+	bool too_big = false; /* node lines past V6T_LINE_MASK */
 };
 
 uint32_t v6_encode(std::vector<uint32_t> &vals, uint32_t label)
@@ -699,84 +698,406 @@ uint32_t v6_encode(std::vector<uint32_t> &vals, uint32_t label)
 	return DIR_TAG_INDIRECT | (uint32_t)(vals.size() - 1);
 }
 
-/* Longest-prefix table over (len, address) candidates; see tables.h v6_lpm. */
+/* a prefix of the v6 trie: address as two host-order halves, the rank it
+ * applies in (tables.h v6_lpm: later ranks paint over earlier ones) */
+struct T6 {
+	uint64_t hi, lo;
+	uint32_t len, rank, enc;
+};
+
+/* Piecewise-constant labels over [0, end): start -> label.  Painting the
+ * prefixes of one range in rank order leaves the highest-ranked cover of
+ * every point (prefix intervals nest or are disjoint). */
+typedef unsigned __int128 u128;
+struct Runs {
+	std::map<u128, uint32_t> m;
+	u128 end;
+	Runs(u128 e, uint32_t base) : end(e) { m[0] = base; }
+	uint32_t at(u128 x) const { return std::prev(m.upper_bound(x))->second; }
+	void paint(u128 a, u128 b, uint32_t lab) /* [a, b) */
+	{
+		const uint32_t after = b < end ? at(b) : 0u;
+		m.erase(m.lower_bound(a), m.lower_bound(b));
+		m[a] = lab;
+		if (b < end)
+			m[b] = after;
+	}
+	/* boundaries (points > 0 where the label changes) and the label from each */
+	void cuts(std::vector<std::pair<u128, uint32_t>> &out, uint32_t &first) const
+	{
+		out.clear();
+		first = m.begin()->second;
+		uint32_t cur = first;
+		for (auto it = std::next(m.begin()); it != m.end(); ++it)
+			if (it->second != cur) {
+				out.push_back({it->first, it->second});
+				cur = it->second;
+			}
+	}
+};
+
+/* the /32 node over bits 32..63 (tables.h v6_lpm): returns the b32 entry */
+static uint2 v6t_node32(V6Build &b, const std::vector<const T6 *> &ps, uint32_t l32, bool deep)
+{
+	Runs r((u128)1 << 32, l32);
+	for (const T6 *p : ps) /* rank order */
+		if (p->len > 32 && p->len <= 64) {
+			const uint64_t st = (uint32_t)p->hi;
+			r.paint(st, st + (1ull << (64 - p->len)), p->enc);
+		}
+	std::vector<std::pair<u128, uint32_t>> cut;
+	uint32_t first;
+	r.cuts(cut, first);
+	if (cut.empty() && !deep)
+		return make_uint2(first, 0u);
+	const uint32_t last = cut.empty() ? first : cut.back().second;
+	/* the window: least aligned [base, base + 2^w), w >= 9, holding every
+	 * boundary, whose outside (below: first, above: last) has one label */
+	uint32_t w = 9, base = 0, outer = first;
+	for (;; w++) {
+		if (w == 32) {
+			base = 0;
+			outer = first;
+			break;
+		}
+		const uint64_t lo = cut.empty() ? 0 : (uint64_t)cut.front().first;
+		const uint64_t hi = cut.empty() ? 0 : (uint64_t)cut.back().first;
+		base = (uint32_t)(lo & ~((1ull << w) - 1));
+		const uint64_t top = (uint64_t)base + (1ull << w);
+		if (hi > top)
+			continue;
+		const bool below = base > 0, above = top < (1ull << 32);
+		if (below && above && first != last)
+			continue;
+		outer = below ? first : last;
+		break;
+	}
+	b.pool.resize((b.pool.size() + 31) / 32 * 32, 0u);
+	const size_t line = b.pool.size() / 32;
+	uint32_t s = 0;
+	for (; s <= 6 && s <= w; s++) {
+		const uint64_t width = 1ull << (w - s);
+		std::vector<std::array<uint32_t, 32>> lines(1u << s);
+		bool fits = true;
+		size_t i = 0;
+		uint32_t cur = first;
+		for (uint32_t k = 0; k < (1u << s) && fits; k++) {
+			const uint64_t S = (uint64_t)base + k * width;
+			auto &L = lines[k];
+			L.fill(0xFFFFFFFFu);
+			for (; i < cut.size() && (uint64_t)cut[i].first <= S; i++)
+				cur = cut[i].second;
+			L[15] = outer;
+			L[16] = cur;
+			uint32_t n = 0;
+			for (; i < cut.size() && (uint64_t)cut[i].first < S + width; i++) {
+				if (n == 15) {
+					fits = false;
+					break;
+				}
+				L[n] = (uint32_t)cut[i].first - 1u;
+				cur = cut[i].second;
+				L[16 + ++n] = cur;
+			}
+			for (uint32_t j = n + 1; j < 16; j++)
+				L[16 + j] = cur;
+		}
+		if (!fits)
+			continue;
+		for (auto &L : lines)
+			b.pool.insert(b.pool.end(), L.begin(), L.end());
+		break;
+	}
+	if (s > 6 || s > w) {
+		s = V6T_LONG;
+		w = 32;
+		base = 0;
+		std::array<uint32_t, 32> h;
+		h.fill(0u);
+		h[0] = (uint32_t)cut.size();
+		h[15] = first;
+		b.pool.insert(b.pool.end(), h.begin(), h.end());
+		for (auto &c : cut)
+			b.pool.push_back((uint32_t)c.first - 1u);
+		b.pool.push_back(first);
+		for (auto &c : cut)
+			b.pool.push_back(c.second);
+		b.pool.resize((b.pool.size() + 31) / 32 * 32, 0u);
+	}
+	b.too_big |= line > V6T_LINE_MASK;
+	return make_uint2(DIR_TAG_GROUP | (deep ? V6T_DEEP : 0u) | (uint32_t)line, base | (w - 9u) | s << 5);
+}
+
+/* the /64 record of prefixes longer than /64 (ps: one /64, rank order) */
+static std::array<uint32_t, 8> v6t_rec64(V6Build &b, uint64_t top, const std::vector<const T6 *> &ps)
+{
+	Runs r((u128)1 << 64, V6T_FALL);
+	for (const T6 *p : ps)
+		r.paint(p->lo, (u128)p->lo + ((u128)1 << (128 - p->len)), p->enc);
+	std::vector<std::pair<u128, uint32_t>> cut;
+	uint32_t first;
+	r.cuts(cut, first);
+	std::array<uint32_t, 8> rec{(uint32_t)(top >> 32), (uint32_t)top, 0u, 0u, 0u, 0u, 0u, 0u};
+	const bool inline1 = first == V6T_FALL && !cut.empty() && cut.size() <= 2 &&
+			     (cut.size() == 1 || cut[1].second == V6T_FALL);
+	if (inline1) {
+		const uint64_t lo = (uint64_t)cut[0].first;
+		const uint64_t hi = cut.size() == 2 ? (uint64_t)(cut[1].first - 1) : ~0ull;
+		rec[2] = cut[0].second;
+		rec[4] = (uint32_t)(lo >> 32);
+		rec[5] = (uint32_t)lo;
+		rec[6] = (uint32_t)(hi >> 32);
+		rec[7] = (uint32_t)hi;
+		return rec;
+	}
+	const uint32_t off = (uint32_t)(b.pool.size() / 4);
+	b.pool.insert(b.pool.end(), {(uint32_t)cut.size(), 0u, 0u, 0u});
+	for (auto &c : cut) {
+		b.pool.push_back((uint32_t)((uint64_t)c.first >> 32));
+		b.pool.push_back((uint32_t)(uint64_t)c.first);
+	}
+	b.pool.push_back(first);
+	for (auto &c : cut)
+		b.pool.push_back(c.second);
+	while (b.pool.size() % 4)
+		b.pool.push_back(0u);
+	rec[2] = DIR_TAG_GROUP | off;
+	return rec;
+}
+
+uint32_t h64_home(const std::array<uint32_t, 8> &r) { return mix32(r[0], r[1]); }
+
+template <size_t W>
+void hop_place(std::vector<std::array<uint32_t, W>> &tab, uint32_t &mask,
+	       const std::vector<std::array<uint32_t, W>> &recs, uint32_t (*home_of)(const std::array<uint32_t, W> &));
+
+/* Longest-prefix trie over (rank, len, address) candidates; see tables.h v6_lpm. */
 void build_v6(std::vector<Rank6> cand, V6Build &b)
 {
 	b.any = !cand.empty();
 	if (!b.any)
 		return;
-	std::stable_sort(cand.begin(), cand.end(),
-			 [](const Rank6 &x, const Rank6 &y) { return x.rank < y.rank; });
-	std::vector<uint32_t> shortv(65536, 0);
-	std::vector<std::array<uint32_t, 4>> rootmask(65536, std::array<uint32_t, 4>{0, 0, 0, 0});
-	std::map<std::pair<uint32_t, std::array<uint32_t, 4>>, uint32_t> longer; /* (len, masked) */
 	b.vals.clear();
+	std::vector<T6> ps;
+	ps.reserve(cand.size());
 	for (auto &c : cand) {
-		uint32_t enc = v6_encode(b.vals, c.label);
-		uint32_t top = (uint32_t)c.addr[0] << 8 | c.addr[1];
-		if (c.len <= 16) {
-			uint32_t cnt = 1u << (16 - c.len);
-			uint32_t base = c.len == 0 ? 0 : (top & ~(cnt - 1));
-			std::fill(shortv.begin() + base, shortv.begin() + base + cnt, enc);
+		uint64_t hi = 0, lo = 0;
+		for (int i = 0; i < 8; i++) {
+			hi = hi << 8 | c.addr[i];
+			lo = lo << 8 | c.addr[8 + i];
+		}
+		ps.push_back(T6{hi, lo, c.len, c.rank, 0u});
+	}
+	/* address order, ties by rank: every range's prefixes are contiguous */
+	std::vector<uint32_t> ord(ps.size());
+	for (uint32_t i = 0; i < ord.size(); i++)
+		ord[i] = i;
+	std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return cand[x].rank < cand[y].rank; });
+	for (uint32_t i : ord) /* vals in rank order (as the DIR builds) */
+		ps[i].enc = v6_encode(b.vals, cand[i].label);
+	std::vector<T6> srt(ps);
+	std::stable_sort(srt.begin(), srt.end(), [](const T6 &x, const T6 &y) {
+		return x.hi != y.hi ? x.hi < y.hi : (x.lo != y.lo ? x.lo < y.lo : x.rank < y.rank);
+	});
+	auto by_rank = [](std::vector<const T6 *> &v) {
+		std::stable_sort(v.begin(), v.end(), [](const T6 *x, const T6 *y) { return x->rank < y->rank; });
+	};
+	/* /0../16 */
+	std::vector<const T6 *> shortp;
+	for (auto &p : srt)
+		if (p.len <= 16)
+			shortp.push_back(&p);
+	by_rank(shortp);
+	b.root.assign(65536, 0u);
+	for (const T6 *p : shortp) {
+		const uint32_t cnt = 1u << (16 - p->len);
+		const uint32_t base = p->len == 0 ? 0 : ((uint32_t)(p->hi >> 48) & ~(cnt - 1));
+		std::fill(b.root.begin() + base, b.root.begin() + base + cnt, p->enc);
+	}
+	b.pool.assign(32, 0xFFFFFFFFu); /* line 0 unused */
+	b.b24.clear();
+	b.b32.clear();
+	std::vector<std::array<uint32_t, 8>> r64;
+	size_t i = 0;
+	while (i < srt.size()) {
+		const uint32_t top16 = (uint32_t)(srt[i].hi >> 48);
+		size_t j = i;
+		while (j < srt.size() && (uint32_t)(srt[j].hi >> 48) == top16)
+			j++;
+		std::vector<const T6 *> g16;
+		for (size_t k = i; k < j; k++)
+			if (srt[k].len > 16)
+				g16.push_back(&srt[k]);
+		if (g16.empty()) {
+			i = j;
 			continue;
 		}
-		uint32_t bit = c.len - 17;
-		rootmask[top][bit / 32] |= 1u << (bit % 32);
-		std::array<uint32_t, 4> w; /* the prefix key: host-order words, masked */
-		for (uint32_t i = 0; i < 4; i++) {
-			const uint32_t x = (uint32_t)c.addr[4 * i] << 24 | (uint32_t)c.addr[4 * i + 1] << 16 |
-					   (uint32_t)c.addr[4 * i + 2] << 8 | c.addr[4 * i + 3];
-			const uint32_t keep = c.len > 32 * i ? std::min(32u, c.len - 32 * i) : 0u;
-			w[i] = keep == 0 ? 0u : x & (0xFFFFFFFFu << (32 - keep));
+		std::array<uint32_t, 256> e24;
+		e24.fill(b.root[top16]);
+		{
+			std::vector<const T6 *> v;
+			for (const T6 *p : g16)
+				if (p->len <= 24)
+					v.push_back(p);
+			by_rank(v);
+			for (const T6 *p : v) {
+				const uint32_t cnt = 1u << (24 - p->len);
+				const uint32_t base = (uint32_t)(p->hi >> 40) & 0xFFu & ~(cnt - 1);
+				std::fill(e24.begin() + base, e24.begin() + base + cnt, p->enc);
+			}
 		}
-		longer[{c.len, w}] = enc; /* canonical keys are unique; later rank wins */
-	}
-	std::map<std::array<uint32_t, 4>, uint32_t> ids;
-	b.masks.assign(4, 0); /* row 0: no lengths */
-	ids[{0, 0, 0, 0}] = 0;
-	b.root.assign(2 * 65536, 0);
-	for (uint32_t r = 0; r < 65536; r++) {
-		auto it = ids.find(rootmask[r]);
-		uint32_t id;
-		if (it == ids.end()) {
-			id = (uint32_t)(b.masks.size() / 4);
-			ids[rootmask[r]] = id;
-			b.masks.insert(b.masks.end(), rootmask[r].begin(), rootmask[r].end());
-		} else {
-			id = it->second;
-		}
-		b.root[2 * r] = id;
-		b.root[2 * r + 1] = shortv[r];
-	}
-	/* every row's lengths, longest first: the first 8 as bytes, the count */
-	b.lens.assign(b.masks.size(), 0);
-	for (size_t row = 0; row < b.masks.size() / 4; row++) {
-		uint32_t n = 0;
-		for (int len = 128; len >= 17; len--) {
-			const uint32_t bit = (uint32_t)len - 17u;
-			if (!(b.masks[4 * row + bit / 32] >> (bit % 32) & 1u))
+		size_t k = 0;
+		while (k < g16.size()) {
+			const uint32_t x24 = (uint32_t)(g16[k]->hi >> 40) & 0xFFu;
+			size_t l = k;
+			std::vector<const T6 *> g24;
+			for (; l < g16.size() && ((uint32_t)(g16[l]->hi >> 40) & 0xFFu) == x24; l++)
+				if (g16[l]->len > 24)
+					g24.push_back(g16[l]);
+			if (g24.empty()) {
+				k = l;
 				continue;
-			if (n < 8)
-				b.lens[4 * row + n / 4] |= (uint32_t)len << (8 * (n % 4));
-			n++;
+			}
+			std::array<uint32_t, 256> e32;
+			e32.fill(e24[x24]);
+			{
+				std::vector<const T6 *> v;
+				for (const T6 *p : g24)
+					if (p->len <= 32)
+						v.push_back(p);
+				by_rank(v);
+				for (const T6 *p : v) {
+					const uint32_t cnt = 1u << (32 - p->len);
+					const uint32_t base = (uint32_t)(p->hi >> 32) & 0xFFu & ~(cnt - 1);
+					std::fill(e32.begin() + base, e32.begin() + base + cnt, p->enc);
+				}
+			}
+			std::array<uint2, 256> n32;
+			for (uint32_t x = 0; x < 256; x++)
+				n32[x] = make_uint2(e32[x], 0u);
+			size_t q = 0;
+			while (q < g24.size()) {
+				const uint32_t x32 = (uint32_t)(g24[q]->hi >> 32) & 0xFFu;
+				size_t r = q;
+				std::vector<const T6 *> g32, g64;
+				for (; r < g24.size() && ((uint32_t)(g24[r]->hi >> 32) & 0xFFu) == x32; r++)
+					if (g24[r]->len > 32)
+						(g24[r]->len <= 64 ? g32 : g64).push_back(g24[r]);
+				if (!g32.empty() || !g64.empty()) {
+					by_rank(g32);
+					n32[x32] = v6t_node32(b, g32, e32[x32], !g64.empty());
+					/* /64 groups (address order within the /32) */
+					size_t m = 0;
+					while (m < g64.size()) {
+						const uint64_t top = g64[m]->hi;
+						std::vector<const T6 *> v;
+						for (; m < g64.size() && g64[m]->hi == top; m++)
+							v.push_back(g64[m]);
+						by_rank(v);
+						r64.push_back(v6t_rec64(b, top, v));
+					}
+				}
+				q = r;
+			}
+			e24[x24] = DIR_TAG_GROUP | (uint32_t)(b.b32.size() / 2 / 256);
+			for (auto &e : n32) {
+				b.b32.push_back(e.x);
+				b.b32.push_back(e.y);
+			}
+			k = l;
 		}
-		b.lens[4 * row + 2] = n;
+		b.root[top16] = DIR_TAG_GROUP | (uint32_t)(b.b24.size() / 256);
+		b.b24.insert(b.b24.end(), e24.begin(), e24.end());
+		i = j;
 	}
-	std::vector<std::array<uint32_t, 6>> keys;
-	keys.reserve(longer.size());
-	for (auto &kv : longer) {
-		auto &w = kv.first.second;
-		keys.push_back({w[0], w[1], w[2], w[3], kv.first.first, kv.second});
+	hop_place<8>(b.h64, b.m64, r64, h64_home);
+	/* 32 words past the last line: a lane reads a whole line */
+	b.pool.insert(b.pool.end(), 32, 0xFFFFFFFFu);
+	/* LDS-staged forms */
+	const uint32_t nb24 = (uint32_t)(b.b24.size() / 256), nb32 = (uint32_t)(b.b32.size() / 512);
+	b.rbits.assign(V6T_RBITS_WORDS, 0u);
+	uint32_t rank = 0;
+	for (uint32_t wd = 0; wd < 2048; wd++) {
+		b.rbits[2048 + wd / 2] |= rank << (16 * (wd & 1));
+		for (uint32_t k = 0; k < 32; k++)
+			if ((b.root[32 * wd + k] & DIR_TAG_MASK) == DIR_TAG_GROUP) {
+				b.rbits[wd] |= 1u << k;
+				rank++;
+			}
 	}
-	build_set16(keys, b.set, true);
-	/* ~12 bits per key, at most V6_BLOOM_MAX_WORDS words */
-	const uint32_t nw = (uint32_t)std::min<uint64_t>(
-		V6_BLOOM_MAX_WORDS, next_pow2(std::max<uint64_t>(64, keys.size() * 12 / 32 + 1)));
-	b.bloom.assign(nw, 0);
-	for (auto &k : keys) {
-		const uint32_t h = pfx6_hash(k[0], k[1], k[2], k[3], k[4]);
-		b.bloom[v6_bloom_word(h, nw - 1)] |= v6_bloom_bits(h);
+	b.b24_16.clear();
+	if (nb32 <= 0x7FFFu) {
+		b.b24_16.resize(b.b24.size());
+		for (size_t x = 0; x < b.b24.size(); x++)
+			b.b24_16[x] = (b.b24[x] & DIR_TAG_MASK) == DIR_TAG_GROUP
+					      ? (uint16_t)(0x8000u | (b.b24[x] & DIR_PAYLOAD_MASK))
+					      : (uint16_t)0u;
 	}
+	(void)nb24;
+}
+
+/* The device lookup (kernels.hip v6_lookup) restated over a V6Build on the
+ * host: the trie builder's CPU test hook (cgpu_diag_ipc6_trie) */
+static uint32_t v6t_host_lookup(const V6Build &b, const uint8_t *a)
+{
+	uint32_t w[4];
+	for (int i = 0; i < 4; i++)
+		w[i] = (uint32_t)a[4 * i] << 24 | (uint32_t)a[4 * i + 1] << 16 | (uint32_t)a[4 * i + 2] << 8 | a[4 * i + 3];
+	auto grp = [](uint32_t e) { return (e & DIR_TAG_MASK) == DIR_TAG_GROUP; };
+	uint32_t e = b.root[w[0] >> 16];
+	if (grp(e))
+		e = b.b24[(size_t)(e & DIR_PAYLOAD_MASK) * 256 + ((w[0] >> 8) & 0xFFu)];
+	if (!grp(e))
+		return e;
+	const size_t bi = (size_t)(e & DIR_PAYLOAD_MASK) * 256 + (w[0] & 0xFFu);
+	const uint32_t nx = b.b32[2 * bi], ny = b.b32[2 * bi + 1];
+	if (!grp(nx))
+		return nx;
+	const uint32_t x = w[1], wb = (ny & 31u) + 9u, sc = (ny >> 5) & 7u, rel = x - (ny & ~511u);
+	size_t line = nx & V6T_LINE_MASK;
+	uint32_t lab;
+	if (sc == V6T_LONG) {
+		const uint32_t n = b.pool[32 * line];
+		uint32_t c = 0;
+		for (uint32_t i = 0; i < n; i++)
+			c += b.pool[32 * (line + 1) + i] < x;
+		lab = b.pool[32 * (line + 1) + n + c];
+	} else {
+		const bool out = wb < 32 && (rel >> wb) != 0;
+		const uint32_t sh = wb - sc;
+		line += out || sh >= 32 ? 0 : rel >> sh;
+		uint32_t c = 0;
+		for (int i = 0; i < 15; i++)
+			c += b.pool[32 * line + i] < x;
+		lab = out ? b.pool[32 * line + 15] : b.pool[32 * line + 16 + c];
+	}
+	if (nx & V6T_DEEP) {
+		const uint32_t home = mix32(w[0], w[1]) & b.m64;
+		const uint32_t hop = b.h64[home][3] >> POL_HOP_SHIFT;
+		for (uint32_t d = 0; d < POL_HOP; d++) {
+			if (!(hop >> d & 1u))
+				continue;
+			const auto &r = b.h64[(home + d) & b.m64];
+			if (r[0] != w[0] || r[1] != w[1])
+				continue;
+			const uint64_t xl = (uint64_t)w[2] << 32 | w[3];
+			uint32_t v;
+			if (grp(r[2])) {
+				const uint32_t *p = &b.pool[4 * (size_t)(r[2] & DIR_PAYLOAD_MASK)];
+				uint32_t c = 0;
+				for (uint32_t i = 0; i < p[0]; i++)
+					c += ((uint64_t)p[4 + 2 * i] << 32 | p[5 + 2 * i]) <= xl;
+				v = p[4 + 2 * p[0] + c];
+			} else {
+				const uint64_t lo = (uint64_t)r[4] << 32 | r[5], hi = (uint64_t)r[6] << 32 | r[7];
+				v = lo <= xl && xl <= hi ? r[2] : V6T_FALL;
+			}
+			if (v != V6T_FALL)
+				lab = v;
+			break;
+		}
+	}
+	return lab;
 }
 
 /* ---- IPv6 any-match cover (tables.h cover6) ---- */
@@ -923,8 +1244,6 @@ void hop_place(std::vector<std::array<uint32_t, W>> &tab, uint32_t &mask,
 		nb *= 2;
 	}
 }
-
-uint32_t h64_home(const std::array<uint32_t, 8> &r) { return mix32(r[0], r[1]); }
 
 /* The /32 entry of the prefixes longer than /32 among ps[k, l) (one /32,
  * sorted; shorter ones are skipped): an interval node over bits 32..63
@@ -1158,6 +1477,57 @@ bool ipc6_candidate(const cgpu_ipcache_key &raw, const uint8_t *canon, uint32_t 
 	}
 	return true;
 }
+
+} // namespace
+
+/* Test hook (not part of the drop-in boundary, no header): build the IPv6
+ * ipcache trie of n ipcache keys / labels exactly as a commit does and look
+ * up m addresses on the host.  out[j] = the matched sec_label, 0xFFFFFFFF
+ * for no match; stats (8 words): /32 nodes, V6T_LONG nodes, h64 records, /64
+ * lists, pool words, b24 blocks, b32 blocks, h64 slots. */
+CGPU_EXPORT int cgpu_diag_ipc6_trie(const cgpu_ipcache_key *keys, const uint32_t *labels, size_t n,
+				    const uint8_t *addrs, size_t m, uint32_t *out, uint32_t *stats)
+{
+	std::vector<Rank6> cand;
+	for (size_t i = 0; i < n; i++) {
+		uint8_t canon[20];
+		memcpy(canon, (const uint8_t *)&keys[i] + 4, 20);
+		const uint32_t p = std::min<uint32_t>(keys[i].prefixlen, 160);
+		for (uint32_t bit = p; bit < 160; bit++)
+			canon[bit / 8] &= (uint8_t) ~(0x80u >> (bit % 8));
+		Rank6 r;
+		if (ipc6_candidate(keys[i], canon, labels[i], &r))
+			cand.push_back(r);
+	}
+	V6Build b;
+	build_v6(cand, b);
+	for (size_t j = 0; j < m; j++) {
+		const uint32_t e = b.any ? v6t_host_lookup(b, addrs + 16 * j) : 0u;
+		out[j] = !e ? 0xFFFFFFFFu
+			    : ((e & DIR_TAG_MASK) == DIR_TAG_INDIRECT ? b.vals[e & DIR_PAYLOAD_MASK] : e & DIR_PAYLOAD_MASK);
+	}
+	if (stats) {
+		uint32_t st[8] = {};
+		for (size_t i = 0; i + 1 < b.b32.size(); i += 2)
+			if ((b.b32[i] & DIR_TAG_MASK) == DIR_TAG_GROUP) {
+				st[0]++;
+				st[1] += ((b.b32[i + 1] >> 5) & 7u) == V6T_LONG;
+			}
+		for (auto &r : b.h64)
+			if (r[3] & COVER6_USED) {
+				st[2]++;
+				st[3] += (r[2] & DIR_TAG_MASK) == DIR_TAG_GROUP;
+			}
+		st[4] = (uint32_t)b.pool.size();
+		st[5] = (uint32_t)(b.b24.size() / 256);
+		st[6] = (uint32_t)(b.b32.size() / 512);
+		st[7] = (uint32_t)b.h64.size();
+		memcpy(stats, st, sizeof(st));
+	}
+	return b.too_big ? -E2BIG : 0;
+}
+
+namespace {
 
 /* Service map -> frontend hash + dense backend rows (tables.h lb_table).
  * Returns -E2BIG when sparse slave numbers would need more than
@@ -3020,14 +3390,18 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o_n = ar.add(b.lc.nodes.data(), b.lc.nodes.size() * 4);
 	const size_t o_c = ar.add(b.lc.dict.data(), b.lc.dict.size() * 4);
 	const size_t o_v = ar.add(b.dir.vals.data(), b.dir.vals.size() * 4);
-	size_t o6[6] = {0, 0, 0, 0, 0, 0};
+	if (b.v6.too_big)
+		return fail(-E2BIG, "ipcache v6 trie exceeds 2^29 node lines");
+	size_t o6[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	if (b.v6.any) {
-		o6[4] = ar.add(b.v6.bloom.data(), b.v6.bloom.size() * 4);
 		o6[0] = ar.add(b.v6.root.data(), b.v6.root.size() * 4);
-		o6[1] = ar.add(b.v6.masks.data(), b.v6.masks.size() * 4);
-		o6[5] = ar.add(b.v6.lens.data(), b.v6.lens.size() * 4);
-		o6[2] = ar.add(b.v6.vals.data(), b.v6.vals.size() * 4);
-		o6[3] = ar.add(b.v6.set.slots.data(), b.v6.set.slots.size() * sizeof(set16_slot));
+		o6[1] = ar.add(b.v6.b24.data(), b.v6.b24.size() * 4);
+		o6[2] = ar.add(b.v6.b32.data(), b.v6.b32.size() * 4);
+		o6[3] = ar.add(b.v6.pool.data(), b.v6.pool.size() * 4);
+		o6[4] = ar.add(b.v6.vals.data(), b.v6.vals.size() * 4);
+		o6[5] = ar.add(b.v6.h64.data(), b.v6.h64.size() * 32);
+		o6[6] = ar.add(b.v6.rbits.data(), b.v6.rbits.size() * 4);
+		o6[7] = ar.add(b.v6.b24_16.data(), b.v6.b24_16.size() * 2);
 	}
 	if (int r = upload(c, ar, buf, G_IPC))
 		return r;
@@ -3036,10 +3410,11 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 			 (uint32_t)b.lc.dict.size()};
 	s.ipc6 = v6_lpm{};
 	if (b.v6.any)
-		s.ipc6 = v6_lpm{at<uint2>(buf, o6[0]), at<uint32_t>(buf, o6[1]), at<uint32_t>(buf, o6[2]),
-				addr_set16{at<set16_slot>(buf, o6[3]), b.v6.set.mask, b.v6.set.max_probe},
-				(uint32_t)(b.v6.masks.size() / 4), at<uint32_t>(buf, o6[4]),
-				(uint32_t)b.v6.bloom.size() - 1u, at<uint4>(buf, o6[5])};
+		s.ipc6 = v6_lpm{at<uint32_t>(buf, o6[0]), at<uint32_t>(buf, o6[1]), at<uint2>(buf, o6[2]),
+				at<uint32_t>(buf, o6[3]), at<uint32_t>(buf, o6[4]), at<uint4>(buf, o6[5]), b.v6.m64,
+				at<uint32_t>(buf, o6[6]),
+				b.v6.b24_16.empty() ? nullptr : at<uint16_t>(buf, o6[7]),
+				(uint32_t)(b.v6.b24.size() / 256)};
 	b.sum[G_IPC] = in.sum_ipc;
 	return 0;
 }

@@ -263,114 +263,116 @@ __device__ __forceinline__ uint4 v6_host_words(uint4 a)
 	return make_uint4(bswap32(a.x), bswap32(a.y), bswap32(a.z), bswap32(a.w));
 }
 
-/* Running sums of pfx6_hash's word products: P.x = w0 C0, P.y = P.x + w1 C1,
- * P.z = P.y + w2 C2 (a prefix cut in word k adds P_k + masked w_k C_k) */
-__device__ __forceinline__ uint3 pfx6_sums(uint4 w)
+/* ---- IPv6 ipcache trie (tables.h v6_lpm) ---- */
+
+/* (ah, al) <= (bh, bl) as 64-bit values */
+__device__ __forceinline__ bool le64(uint32_t ah, uint32_t al, uint32_t bh, uint32_t bl)
 {
-	const uint32_t p0 = w.x * PFX6_C0, p1 = p0 + w.y * PFX6_C1;
-	return make_uint3(p0, p1, p1 + w.z * PFX6_C2);
+	return ah < bh || (ah == bh && al <= bl);
 }
 
-/* the prefix key of w at length len (17..128): words past the cut are 0 */
-__device__ __forceinline__ uint4 pfx6_key(uint4 w, uint32_t len)
+/* the line of x (= address bits 32..63) in the /32 node {ex, ey}; outside:
+ * x lies outside the node's window (its label is the line's outer slot) */
+__device__ __forceinline__ uint32_t v6t_line(uint32_t ex, uint32_t ey, uint32_t x, bool &outside)
 {
-	const uint32_t k = (len - 1u) >> 5;
-	const uint32_t m = 0xFFFFFFFFu << (32u - (len - 32u * k));
-	return make_uint4(k == 0 ? w.x & m : w.x, k < 1 ? 0u : (k == 1 ? w.y & m : w.y),
-			  k < 2 ? 0u : (k == 2 ? w.z & m : w.z), k < 3 ? 0u : w.w & m);
+	const uint32_t w = (ey & 31u) + 9u, s = (ey >> 5) & 7u;
+	const uint32_t rel = x - (ey & ~511u);
+	outside = w < 32u ? (rel >> w) != 0u : false;
+	const uint32_t sh = w - (s == V6T_LONG ? 0u : s);
+	const uint32_t k = outside || sh >= 32u ? 0u : rel >> sh;
+	return (ex & V6T_LINE_MASK) + (s == V6T_LONG ? 0u : k);
 }
 
-/* pfx6_hash of w's prefix key at length len (17..128), P = pfx6_sums(w) */
-__device__ __forceinline__ uint32_t pfx6_hash_at(uint4 w, uint3 P, uint32_t len)
+/* region of x in a line: #{slot i < x, i < 15} over its boundary units */
+__device__ __forceinline__ uint32_t v6t_count(uint4 q0, uint4 q1, uint4 q2, uint4 q3, uint32_t x)
 {
-	const uint32_t k = (len - 1u) >> 5;
-	const uint32_t wk = k == 0 ? w.x : (k == 1 ? w.y : (k == 2 ? w.z : w.w));
-	const uint32_t pk = k == 0 ? 0u : (k == 1 ? P.x : (k == 2 ? P.y : P.z));
-	const uint32_t ck = k == 0 ? PFX6_C0 : (k == 1 ? PFX6_C1 : (k == 2 ? PFX6_C2 : PFX6_C3));
-	const uint32_t mk = wk & (0xFFFFFFFFu << (32u - (len - 32u * k)));
-	return fmix32(pk + mk * ck + len * PFX6_CL);
+	return (q0.x < x) + (q0.y < x) + (q0.z < x) + (q0.w < x) + (q1.x < x) + (q1.y < x) + (q1.z < x) +
+	       (q1.w < x) + (q2.x < x) + (q2.y < x) + (q2.z < x) + (q2.w < x) + (q3.x < x) + (q3.y < x) +
+	       (q3.z < x);
 }
 
-/* Next candidate length of an IPv6 lookup, longest first: pops lengths off
- * the root's mask (hi: 81..128, lo: 17..80) until one passes the bloom
- * filter (tables.h v6_lpm) and returns it with its set bucket (0: none
- * left).  w: host-order address words, P: pfx6_sums(w); bloom: the filter
- * words (LDS or global).  Per length: one masked word, one multiply-add and
- * the finalizer. */
-__device__ __forceinline__ uint32_t v6_next(const v6_lpm &t, const uint32_t *bloom, uint4 w, uint3 P,
-					    uint64_t &hi, uint64_t &lo, uint32_t &bucket)
+/* a V6T_LONG node: n boundaries (b - 1) and n + 1 labels from line + 1 on,
+ * binary-searched */
+__device__ __forceinline__ uint32_t v6t_long(const uint32_t *pool, uint32_t line, uint32_t n, uint32_t x)
 {
-	while (hi | lo) {
-		uint32_t len;
-		if (hi) {
-			const int bit = 63 - __clzll(hi);
-			hi &= ~(1ull << bit);
-			len = 17u + 64u + (uint32_t)bit;
-		} else {
-			const int bit = 63 - __clzll(lo);
-			lo &= ~(1ull << bit);
-			len = 17u + (uint32_t)bit;
-		}
-		const uint32_t k = (len - 1u) >> 5;
-		const uint32_t wk = k == 0 ? w.x : (k == 1 ? w.y : (k == 2 ? w.z : w.w));
-		const uint32_t pk = k == 0 ? 0u : (k == 1 ? P.x : (k == 2 ? P.y : P.z));
-		const uint32_t ck = k == 0 ? PFX6_C0 : (k == 1 ? PFX6_C1 : (k == 2 ? PFX6_C2 : PFX6_C3));
-		const uint32_t mk = wk & (0xFFFFFFFFu << (32u - (len - 32u * k)));
-		const uint32_t h = fmix32(pk + mk * ck + len * PFX6_CL);
-		const uint32_t bits = v6_bloom_bits(h);
-		if ((bloom[v6_bloom_word(h, t.bloom_mask)] & bits) == bits) {
-			bucket = h & t.set.bucket_mask;
-			return len;
+	const uint32_t *b = pool + 32u * (line + 1u);
+	uint32_t lo = 0, hi = n; /* count of b[i] < x */
+	while (lo < hi) {
+		const uint32_t m = (lo + hi) >> 1;
+		if (b[m] < x)
+			lo = m + 1u;
+		else
+			hi = m;
+	}
+	return b[n + lo];
+}
+
+/* a /64 list (tables.h v6_lpm h64): label of the low 64 bits (xh, xl) */
+__device__ __forceinline__ uint32_t v6t_list64(const uint32_t *pool, uint32_t off, uint32_t xh, uint32_t xl)
+{
+	const uint32_t *p = pool + 4u * off;
+	const uint32_t n = p[0];
+	uint32_t c = 0;
+	for (uint32_t i = 0; i < n; i++)
+		c += le64(p[4u + 2u * i], p[5u + 2u * i], xh, xl) ? 1u : 0u;
+	return p[4u + 2u * n + c];
+}
+
+/* the /64 record of w's /64 (or V6T_FALL): home slot s0 / s1 loaded */
+__device__ __forceinline__ uint32_t v6t_rec(const v6_lpm &t, uint4 w, uint32_t home, uint4 s0, uint4 s1)
+{
+	uint32_t hop = s0.w >> POL_HOP_SHIFT;
+	bool found = (hop & 1u) && s0.x == w.x && s0.y == w.y;
+	hop &= ~1u;
+	while (hop && !found) {
+		const uint32_t k = (home + (uint32_t)__builtin_ctz(hop)) & t.m64;
+		hop &= hop - 1u;
+		const uint4 x = t.h64[2u * k];
+		if (x.x == w.x && x.y == w.y) {
+			s0 = x;
+			s1 = t.h64[2u * k + 1u];
+			found = true;
 		}
 	}
-	return 0;
+	if (!found)
+		return V6T_FALL;
+	if ((s0.z & DIR_TAG_MASK) == DIR_TAG_GROUP)
+		return v6t_list64(t.pool, s0.z & DIR_PAYLOAD_MASK, w.z, w.w);
+	return le64(s1.x, s1.y, w.z, w.w) && le64(w.z, w.w, s1.z, s1.w) ? s0.z : V6T_FALL;
 }
 
-/* IPv6 longest-prefix lookup (tables.h v6_lpm): the prefix lengths present
- * under the address's /16 are tried longest first; lengths the bloom filter
- * rules out cost no memory access, the others are probed four at a time
- * (independent bucket loads in flight); the first hit is the longest match.
- * a: the address as stored.  Returns the DIR-encoded entry (0 = no match). */
+/* IPv6 longest-prefix lookup (tables.h v6_lpm), one lane, every level from
+ * global memory.  a: the address as stored.  Returns the DIR-encoded entry
+ * (0 = no match). */
 __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 {
 	if (!t.root)
 		return 0;
 	const uint4 w = v6_host_words(a);
-	const uint2 r = t.root[w.x >> 16];
-	uint32_t res = 0;
-	if (r.x) {
-		const uint3 P = pfx6_sums(w);
-		const uint4 m = reinterpret_cast<const uint4 *>(t.masks)[r.x];
-		uint64_t hi = ((uint64_t)m.w << 32) | m.z, lo = ((uint64_t)m.y << 32) | m.x;
-		/* NB: the result is carried, never returned from inside the
-		 * unrolled loop: a divergent early return there miscompiled on
-		 * gfx950 / ROCm 7.2 (round 1, reproduced in isolation). */
-		while ((hi | lo) && !res) {
-			uint32_t L[4], bi[4];
-			uint4 k0[4], m0[4], k1[4], m1[4];
-#pragma unroll
-			for (int j = 0; j < 4; j++) {
-				bi[j] = 0;
-				L[j] = v6_next(t, t.bloom, w, P, hi, lo, bi[j]);
-			}
-			/* issue every probe's bucket load before resolving any */
-#pragma unroll
-			for (int j = 0; j < 4; j++) {
-				const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bi[j] * 4u;
-				k0[j] = L[j] ? p[0] : make_uint4(0, 0, 0, 0);
-				m0[j] = L[j] ? p[1] : make_uint4(0, 0, 0, 0);
-				k1[j] = L[j] ? p[2] : make_uint4(0, 0, 0, 0);
-				m1[j] = L[j] ? p[3] : make_uint4(0, 0, 0, 0);
-			}
-			/* longest first: the first hit is the longest match */
-#pragma unroll
-			for (int j = 0; j < 4; j++)
-				if (!res && L[j])
-					res = set16_resolve(t.set, k0[j], m0[j], k1[j], m1[j], bi[j], pfx6_key(w, L[j]),
-							    1u | (L[j] << 8));
-		}
+	uint32_t e = t.root[w.x >> 16];
+	if ((e & DIR_TAG_MASK) == DIR_TAG_GROUP)
+		e = t.b24[(e & DIR_PAYLOAD_MASK) * 256u + ((w.x >> 8) & 0xFFu)];
+	if ((e & DIR_TAG_MASK) != DIR_TAG_GROUP)
+		return e;
+	const uint2 n = t.b32[(e & DIR_PAYLOAD_MASK) * 256u + (w.x & 0xFFu)];
+	if ((n.x & DIR_TAG_MASK) != DIR_TAG_GROUP)
+		return n.x;
+	bool out;
+	const uint32_t line = v6t_line(n.x, n.y, w.y, out);
+	const uint4 *q = reinterpret_cast<const uint4 *>(t.pool) + 8u * line;
+	const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+	uint32_t lab;
+	if (((n.y >> 5) & 7u) == V6T_LONG)
+		lab = v6t_long(t.pool, line, q0.x, w.y);
+	else
+		lab = out ? q3.w : t.pool[32u * line + 16u + v6t_count(q0, q1, q2, q3, w.y)];
+	if (n.x & V6T_DEEP) {
+		const uint32_t home = mix32(w.x, w.y) & t.m64;
+		const uint32_t r = v6t_rec(t, w, home, t.h64[2u * home], t.h64[2u * home + 1u]);
+		if (r != V6T_FALL)
+			lab = r;
 	}
-	return res ? res : r.y;
+	return lab;
 }
 
 /* ---- service load balancer (bpf/lib/lb.h, bpf/bpf_lb.c) ---- */
@@ -806,11 +808,6 @@ template <int MODE> __global__ __launch_bounds__(BLOCK) void k_lb4(cgpu_snapshot
 
 /* ---- IPv6 any-match cover (tables.h cover6) ---- */
 
-__device__ __forceinline__ bool le64(uint32_t ah, uint32_t al, uint32_t bh, uint32_t bl)
-{
-	return ah < bh || (ah == bh && al <= bl);
-}
-
 __device__ __forceinline__ bool c6_node64(const uint32_t *pool, uint32_t off, uint32_t xh, uint32_t xl)
 {
 	const uint4 *nd = reinterpret_cast<const uint4 *>(pool) + off;
@@ -1145,156 +1142,139 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 #define DIAG_LPM(b) (b)
 #endif
 
-/* Octet-cooperative IPv6 longest-prefix lookup for the x4 schedule
- * (k_classify_x4<.., V6>; tables.h v6_lpm).
- * Phase 1, the bloom filter: a wave's tuples are taken 8 at a time; octet o
- * of the wave (lanes 8o .. 8o + 7) filters one tuple, lane 8o + j its j-th
- * longest candidate length (the root row's `lens` list): one hash and one
- * LDS filter test per lane per step, instead of each lane looping over every
- * length present under its /16 (which ran as long as the wave's slowest
- * lane, round 2: 1.77 G VALU per 64M tuples).  The admitted lengths return to
- * the tuple's own lane as an 8-bit mask (bit j: the j-th longest).
- * Phase 2, per lane: the two longest admitted lengths of every tuple are
- * probed with all their bucket loads in flight together, the longer hit
- * wins; a tuple left unresolved by filter false positives takes the next
- * two.  A row with more than 8 lengths continues below its 8th longest on
- * the lane's own serial loop (v6_next) when the first 8 miss.
- * Every lane of the wave must call this together (the octets work for other
- * lanes' tuples); act[u] false only excludes the lane's own tuple (e = 0). */
-template <int Q>
-__device__ __forceinline__ void v6_lookup_coop(const v6_lpm &t, const uint32_t *bloom, const uint4 *llens,
-					       uint32_t nl, const uint4 (&w)[Q], const bool (&act)[Q],
-					       uint32_t (&e)[Q])
+/* IPv6 ipcache lookups of Q tuples per lane for the x4 schedule
+ * (k_classify_x4<.., V6>; tables.h v6_lpm), level by level with the Q
+ * tuples' loads of a level in flight together:
+ *   root: the GROUP bitmap and ranks in LDS (lds; a leaf root reads its
+ *         entry from global memory at the next level);
+ *   b24:  the u16 blocks in LDS when staged (lds24), else global;
+ *   b32:  one 8-byte gather;
+ *   node: the line's four boundary units (64 B) and, for a /32 with /65+
+ *         prefixes, the /64's h64 home slot, together; then the label word.
+ * w: host-order address words; act false: e = 0. */
+#define V6T_LDS_B24 96u /* b24 blocks staged in LDS at most (48 KiB) */
+
+/* b24 blocks the x4 kernel stages in LDS (0: b24 read from global memory) */
+__host__ __device__ __forceinline__ uint32_t v6t_lds_b24(const v6_lpm &t)
 {
-	const uint32_t lane = __lane_id();
-	const uint32_t oct = lane >> 3, j = lane & 7u;
-	uint2 r[Q];
-	uint4 lr[Q];
-	uint32_t pass[Q], res[Q];
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		r[u] = make_uint2(0, 0);
-		if (act[u] && t.root)
-			r[u] = t.root[w[u].x >> 16];
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		lr[u] = make_uint4(0, 0, 0, 0);
-		if (r[u].x)
-			lr[u] = r[u].x < nl ? llens[r[u].x] : t.lens[r[u].x];
-		pass[u] = 0;
-		res[u] = 0;
-	}
-	/* phase 1 */
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-#pragma unroll
-		for (uint32_t g = 0; g < 8; g++) {
-			const int owner = (int)(8u * g + oct);
-			const uint32_t cnt = __shfl(lr[u].z, owner, 64);
-			/* (a shuffle reads the SOURCE lane's operand: both words travel) */
-			const uint32_t lx = __shfl(lr[u].x, owner, 64), ly = __shfl(lr[u].y, owner, 64);
-			const uint32_t len = j < cnt ? ((j < 4 ? lx : ly) >> (8u * (j & 3u))) & 0xFFu : 0u;
-			const uint4 ow = make_uint4(__shfl(w[u].x, owner, 64), __shfl(w[u].y, owner, 64),
-						    __shfl(w[u].z, owner, 64), __shfl(w[u].w, owner, 64));
-			bool ok = false;
-			if (len) {
-				const uint32_t k = (len - 1u) >> 5;
-				const uint32_t p0 = ow.x * PFX6_C0, p1 = p0 + ow.y * PFX6_C1, p2 = p1 + ow.z * PFX6_C2;
-				const uint32_t wk = k == 0 ? ow.x : (k == 1 ? ow.y : (k == 2 ? ow.z : ow.w));
-				const uint32_t pk = k == 0 ? 0u : (k == 1 ? p0 : (k == 2 ? p1 : p2));
-				const uint32_t ck = k == 0 ? PFX6_C0 : (k == 1 ? PFX6_C1 : (k == 2 ? PFX6_C2 : PFX6_C3));
-				const uint32_t mk = wk & (0xFFFFFFFFu << (32u - (len - 32u * k)));
-				const uint32_t h = fmix32(pk + mk * ck + len * PFX6_CL);
-				const uint32_t bits = v6_bloom_bits(h);
-				ok = (bloom[v6_bloom_word(h, t.bloom_mask)] & bits) == bits;
-			}
-			const uint64_t bal = __ballot(ok);
-			/* lane 8g + o' owns the tuple octet o' filtered in this step */
-			const uint32_t mine = (uint32_t)(bal >> (8u * j)) & 0xFFu;
-			if (oct == g)
-				pass[u] = mine;
-		}
-	}
-	/* phase 2 */
-	for (;;) {
-		uint32_t L0[Q], L1[Q], b0[Q], b1[Q];
-		bool more = false;
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			L0[u] = L1[u] = 0;
-			b0[u] = b1[u] = 0;
-			if (res[u] || !pass[u])
-				continue;
-			const uint64_t lw = ((uint64_t)lr[u].y << 32) | lr[u].x;
-			const uint32_t s0 = (uint32_t)__ffs(pass[u]) - 1u;
-			pass[u] &= pass[u] - 1u;
-			L0[u] = (uint32_t)(lw >> (8u * s0)) & 0xFFu;
-			if (pass[u]) {
-				const uint32_t s1 = (uint32_t)__ffs(pass[u]) - 1u;
-				pass[u] &= pass[u] - 1u;
-				L1[u] = (uint32_t)(lw >> (8u * s1)) & 0xFFu;
-			}
-			const uint3 P = pfx6_sums(w[u]);
-			b0[u] = pfx6_hash_at(w[u], P, L0[u]) & t.set.bucket_mask;
-			if (L1[u])
-				b1[u] = pfx6_hash_at(w[u], P, L1[u]) & t.set.bucket_mask;
-			more = true;
-		}
-		if (!more)
-			break;
-		/* the first slot of both buckets of every tuple in flight together */
-		uint4 k0[Q], m0[Q], n0[Q], q0[Q];
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)b0[u] * 4u;
-			const uint4 *q = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)b1[u] * 4u;
-			k0[u] = L0[u] ? p[0] : make_uint4(0, 0, 0, 0);
-			m0[u] = L0[u] ? p[1] : make_uint4(0, 0, 0, 0);
-			n0[u] = L1[u] ? q[0] : make_uint4(0, 0, 0, 0);
-			q0[u] = L1[u] ? q[1] : make_uint4(0, 0, 0, 0);
-		}
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			if (L0[u])
-				res[u] = set16_resolve_first(t.set, k0[u], m0[u], b0[u], pfx6_key(w[u], L0[u]),
-							     1u | (L0[u] << 8));
-			if (!res[u] && L1[u])
-				res[u] = set16_resolve_first(t.set, n0[u], q0[u], b1[u], pfx6_key(w[u], L1[u]),
-							     1u | (L1[u] << 8));
-		}
-	}
-	/* rows with more than 8 lengths: the rest, longest first, one at a time */
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (res[u] || lr[u].z <= 8u)
-			continue;
-		const uint32_t l7 = (lr[u].y >> 24) & 0xFFu; /* the 8th longest: continue below it */
-		const uint4 m = reinterpret_cast<const uint4 *>(t.masks)[r[u].x];
-		uint64_t hi = ((uint64_t)m.w << 32) | m.z, lo = ((uint64_t)m.y << 32) | m.x;
-		const uint32_t below = l7 - 17u; /* keep bits < below */
-		if (below >= 64u) {
-			hi &= below - 64u >= 64u ? ~0ull : ((1ull << (below - 64u)) - 1ull);
-		} else {
-			hi = 0;
-			lo &= (1ull << below) - 1ull;
-		}
-		const uint3 P = pfx6_sums(w[u]);
-		while (!res[u]) {
-			uint32_t bk = 0;
-			const uint32_t L = v6_next(t, bloom, w[u], P, hi, lo, bk);
-			if (!L)
-				break;
-			const uint4 *p = reinterpret_cast<const uint4 *>(t.set.slots) + (size_t)bk * 4u;
-			res[u] = set16_resolve(t.set, p[0], p[1], p[2], p[3], bk, pfx6_key(w[u], L), 1u | (L << 8));
-		}
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++)
-		e[u] = act[u] ? (res[u] ? res[u] : r[u].y) : 0u;
+	return t.root && t.b24_16 && t.n_b24 <= V6T_LDS_B24 ? t.n_b24 : 0u;
 }
 
-#define V6_LDS_MASK_ROWS 256u
+/* LDS words of the x4 kernel's staged trie levels */
+__host__ __device__ __forceinline__ uint32_t v6t_lds_words(const v6_lpm &t)
+{
+	return t.root ? V6T_RBITS_WORDS + v6t_lds_b24(t) * 128u : 0u;
+}
+
+template <int Q>
+__device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *lds, bool lds24,
+					     const uint4 (&w)[Q], const bool (&act)[Q], uint32_t (&e)[Q])
+{
+	const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + 2048u);
+	const uint16_t *b16 = reinterpret_cast<const uint16_t *>(lds + V6T_RBITS_WORDS);
+	const uint32_t *src[Q];
+	bool leaf[Q];
+	uint32_t b32i[Q];
+	/* root and (staged) b24 in LDS: each tuple ends with the global word it
+	 * needs (a leaf of root / b24, or an unstaged b24 entry) or a b32 block */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		src[u] = nullptr;
+		leaf[u] = false;
+		b32i[u] = 0xFFFFFFFFu;
+		e[u] = 0;
+		if (!act[u] || !t.root)
+			continue;
+		const uint32_t r = w[u].x >> 16, wd = lds[r >> 5], bit = 1u << (r & 31u);
+		if (!(wd & bit)) {
+			src[u] = t.root + r;
+			leaf[u] = true;
+			continue;
+		}
+		const uint32_t blk = rank[r >> 5] + __popc(wd & (bit - 1u));
+		const uint32_t x24 = blk * 256u + ((w[u].x >> 8) & 0xFFu);
+		if (lds24) {
+			const uint32_t c = b16[x24];
+			if (c & 0x8000u) {
+				b32i[u] = c & 0x7FFFu;
+			} else {
+				src[u] = t.b24 + x24;
+				leaf[u] = true;
+			}
+		} else {
+			src[u] = t.b24 + x24;
+		}
+	}
+	uint32_t g[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		g[u] = src[u] ? *src[u] : 0u;
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (!src[u])
+			continue;
+		if (!leaf[u] && (g[u] & DIR_TAG_MASK) == DIR_TAG_GROUP)
+			b32i[u] = g[u] & DIR_PAYLOAD_MASK; /* an unstaged b24 GROUP */
+		else
+			e[u] = g[u];
+	}
+	/* b32 */
+	uint2 n[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		n[u] = b32i[u] != 0xFFFFFFFFu ? t.b32[b32i[u] * 256u + (w[u].x & 0xFFu)] : make_uint2(0, 0);
+	bool node[Q], deep[Q], out[Q];
+	uint32_t line[Q], home[Q];
+	uint4 q0[Q], q1[Q], q2[Q], q3[Q], h0[Q], h1[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		node[u] = b32i[u] != 0xFFFFFFFFu && (n[u].x & DIR_TAG_MASK) == DIR_TAG_GROUP;
+		if (b32i[u] != 0xFFFFFFFFu && !node[u])
+			e[u] = n[u].x;
+		deep[u] = node[u] && (n[u].x & V6T_DEEP);
+		out[u] = false;
+		line[u] = node[u] ? v6t_line(n[u].x, n[u].y, w[u].y, out[u]) : 0u;
+		home[u] = mix32(w[u].x, w[u].y) & t.m64;
+	}
+	/* the node line and the /64 home slot together */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		q0[u] = q1[u] = q2[u] = q3[u] = h0[u] = h1[u] = make_uint4(0, 0, 0, 0);
+		if (node[u]) {
+			const uint4 *q = reinterpret_cast<const uint4 *>(t.pool) + 8u * line[u];
+			q0[u] = q[0];
+			q1[u] = q[1];
+			q2[u] = q[2];
+			q3[u] = q[3];
+		}
+		if (deep[u]) {
+			h0[u] = t.h64[2u * home[u]];
+			h1[u] = t.h64[2u * home[u] + 1u];
+		}
+	}
+	uint32_t lab[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		lab[u] = 0;
+		if (!node[u])
+			continue;
+		if (((n[u].y >> 5) & 7u) == V6T_LONG)
+			lab[u] = v6t_long(t.pool, line[u], q0[u].x, w[u].y);
+		else
+			lab[u] = out[u] ? q3[u].w
+					: t.pool[32u * line[u] + 16u + v6t_count(q0[u], q1[u], q2[u], q3[u], w[u].y)];
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (!node[u])
+			continue;
+		uint32_t r = V6T_FALL;
+		if (deep[u])
+			r = v6t_rec(t, w[u], home[u], h0[u], h1[u]);
+		e[u] = r != V6T_FALL ? r : lab[u];
+	}
+}
+
 
 /*
  * IPv4 classification, four consecutive tuples per lane per step.
@@ -1345,15 +1325,13 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	uint64_t *pctr = a.delta;
 	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
 	const uint32_t pmask = s.pol.bucket_mask;
-	/* after the hot counters: v4 the LPM leaf dictionary; v6 the bloom
-	 * filter and the first mask rows of the ipcache */
+	/* after the hot counters: v4 the LPM leaf dictionary; v6 the ipcache
+	 * trie's root bitmap and ranks, then its b24 blocks as u16 (if staged) */
 	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots);
-	const uint32_t nbw = V6 && s.ipc6.root ? s.ipc6.bloom_mask + 1u : 0u;
-	const uint32_t nm = V6 ? min(s.ipc6.n_masks, V6_LDS_MASK_ROWS) : 0u;
-	uint4 *lmasks = reinterpret_cast<uint4 *>(ldict + nbw); /* nbw: a multiple of 64 */
+	const uint32_t n24 = V6 ? v6t_lds_b24(s.ipc6) : 0u;
 	/* cold-slot cache (x4_lds_layout): cc_n u64 packed counts, then cc_n u32
 	 * tags (slot + 1, 0 = free) */
-	const uint32_t lds_words = V6 ? nbw + 4u * nm : s.ipc4c.n_dict;
+	const uint32_t lds_words = V6 ? v6t_lds_words(s.ipc6) : s.ipc4c.n_dict;
 	uint64_t *ccv = lctr + s.hot_slots + ((lds_words + 1u) >> 1);
 	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + a.cc_n);
 	const uint32_t ccm = a.cc_n - 1u;
@@ -1366,21 +1344,22 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	if (threadIdx.x < 16)
 		lmet[threadIdx.x] = 0;
 	if (V6) {
-		for (uint32_t k = threadIdx.x; k < nbw; k += NT)
-			ldict[k] = s.ipc6.bloom[k];
-		for (uint32_t k = threadIdx.x; k < nm; k += NT)
-			lmasks[k] = s.ipc6.lens[k]; /* the rows' length lists (v6_lookup_coop) */
+		if (s.ipc6.root) {
+			for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += NT)
+				ldict[k] = s.ipc6.rbits[k];
+			const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
+			for (uint32_t k = threadIdx.x; k < n24 * 128u; k += NT)
+				ldict[V6T_RBITS_WORDS + k] = b16[k];
+		}
 	} else {
 		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
 			ldict[k] = s.ipc4c.dict[k];
 	}
 	__syncthreads();
 
-	/* v6: every lane of a wave runs every iteration (v6_lookup_coop works
-	 * across lanes); a lane past the end runs idle (no F_OK tuple) */
 	for (uint64_t g = t0;; g += T) {
 		const bool live = g * Q < a.n;
-		if (V6 ? !__any(live) : !live)
+		if (!live)
 			break;
 		const uint64_t i0 = live ? g * Q : 0;
 		const bool full = live && i0 + Q <= a.n;
@@ -1549,7 +1528,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 			for (int u = 0; u < Q; u++)
 				act[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK;
-			v6_lookup_coop<Q>(s.ipc6, ldict, lmasks, nm, ad6, act, e);
+			v6t_lookup_q<Q>(s.ipc6, ldict, n24 != 0u, ad6, act, e);
 		} else {
 			/* v4: the /16's inline node (x16), then the compressed LPM */
 			{
@@ -2672,12 +2651,9 @@ template <bool LB, bool V6, bool FR = false>
 static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024;
-	/* LDS: hot counters + the ipcache leaf dictionary (v4) / bloom filter
-	 * and length rows (v6) */
-	size_t fixed = V6 ? (s0.ipc6.root ? (size_t)(s0.ipc6.bloom_mask + 1u) * 4u +
-						  (size_t)std::min(s0.ipc6.n_masks, V6_LDS_MASK_ROWS) * 16u
-					  : 0u)
-			  : (size_t)s0.ipc4c.n_dict * 4u;
+	/* LDS: hot counters + the ipcache leaf dictionary (v4) / the staged trie
+	 * levels (v6) */
+	size_t fixed = V6 ? (size_t)v6t_lds_words(s0.ipc6) * 4u : (size_t)s0.ipc4c.n_dict * 4u;
 	fixed = (fixed + 7u) & ~(size_t)7u;
 	const cgpu_snapshot s = with_lds_hot(s0, fixed < X4_LDS_BUDGET ? (X4_LDS_BUDGET - fixed) / 8u : 0u);
 	size_t lds = (size_t)s.hot_slots * 8u + fixed;
@@ -4222,7 +4198,7 @@ __device__ __forceinline__ void ctc_install(const ct_table &T, ct_cache<K> &c, c
 					    const ct_chain &ch, const ct_row &r, const typename K::key &k0,
 					    const typename K::key &k1, const typename K::key &k2)
 {
-	if (ch.slot == -3)
+	if (ch.slot == -3 || ctc_find<K>(c, k) >= 0)
 		return;
 	uint32_t keep = 0;
 	ctc_each(c, [&](ctc_ent<K> &e, int j) {
@@ -4269,6 +4245,11 @@ __device__ __forceinline__ void ctc_prefetch(const ct_table &T, ct_cache<K> &c, 
 					     bool w2)
 {
 	ct_chain c0{0, 0xFFFFFFFFu, 0, -3}, c1 = c0, c2 = c0;
+	/* one probe per distinct key: an ICMP error's forward key IS its
+	 * related key (ports 0, RELATED set), and two cache entries of one key
+	 * would lose updates and insert it twice */
+	w1 = w1 && !(w0 && K::same(k1, k0));
+	w2 = w2 && !(w0 && K::same(k2, k0)) && !(w1 && K::same(k2, k1));
 	if (w0 && ctc_find<K>(c, k0) < 0)
 		c0.slot = -2;
 	if (w1 && ctc_find<K>(c, k1) < 0)

@@ -216,35 +216,58 @@ static inline __host__ __device__ uint32_t pfx6_hash(uint32_t w0, uint32_t w1, u
 	return fmix32(w0 * PFX6_C0 + w1 * PFX6_C1 + w2 * PFX6_C2 + w3 * PFX6_C3 + len * PFX6_CL);
 }
 
-/* ---- IPv6 longest-prefix table (ipcache v6) ----
- * root[addr >> 112] (65536 x {row, short}): `short` is the longest entry of
- * length <= 16 covering that /16 (DIR-24-8 entry encoding, 0 = none) and
- * `row` selects a 128-bit row of `masks`: the prefix lengths 17..128 present
- * under that /16 (bit L-17).  Each present length L is ONE probe of `set`,
- * keyed by the prefix key (host-order words masked to L, L; bucket =
- * pfx6_hash & bucket_mask); a slot's pad[0] holds the entry.  A bloom
- * filter over the same keys rules most lengths out without a memory access;
- * the probes left do not depend on each other and are issued together,
- * longest first; the first hit in descending length order is the longest
- * match, else `short`. */
+/* ---- IPv6 longest-prefix trie (ipcache v6, ipcache_lookup6 eps.h:56-66) ----
+ * Strides 16 / 8 / 8 over address bits 0..31, labelled interval lines over
+ * bits 32..63, hashed /64 records for the prefixes longer than /64.  The
+ * entries use the DIR encoding: a leaf (0 / DIRECT / INDIRECT) is the
+ * highest-ranked prefix covering the entry's whole range, by controlled prefix
+ * expansion in rank order; GROUP descends.
+ *   root[bits 0..15], b24[blk * 256 + bits 16..23]: u32, leaf or GROUP | blk;
+ *   b32[blk * 256 + bits 24..31]: uint2, {leaf, 0} or the /32's node
+ *     {GROUP | deep << 29 | line, base | (w - 9) | s << 5}.
+ * A node is the /32's labelled intervals over x = bits 32..63 (prefixes /33..
+ * /64, the /32's own leaf where none covers x): every boundary (a point where
+ * the label changes) lies in the window [base, base + 2^w), w >= 9, outside
+ * of which the label is the line's `outer`; the window is cut into 2^s equal
+ * sub-ranges (the least s that fits), one 128-B line each:
+ *   slots 0..14  b - 1 for each boundary b inside the sub-range (not at its
+ *                start), ascending, 0xFFFFFFFF past the last
+ *   slot 15      outer
+ *   slots 16..31 label of region r = #{slot i < x, i < 15}
+ * so a lookup reads one line: four 16-B loads and one label word.
+ * s = 7 (V6T_LONG: even 64 sub-ranges do not fit): line {n, .., slot 15 =
+ * outer} then n boundaries (b - 1) and n + 1 labels from the next line on,
+ * binary-searched (no window).
+ * deep: the /32 holds prefixes longer than /64, in h64, a hop hash over the
+ * /64 (home = mix32(w0, w1), 32-B slots {w0, w1, lbl, used | hop << 24, lo.hi,
+ * lo.lo, hi.hi, hi.lo}): lbl a leaf = the label of low-64 x in [lo, hi];
+ * lbl = GROUP | off: a list at pool[4 * off] {n, 0, 0, 0}, n boundaries (hi,
+ * lo words), n + 1 labels.  V6T_FALL where no /65+ prefix covers x: the node's
+ * label stands. */
+#define V6T_LONG 7u
+#define V6T_FALL DIR_TAG_GROUP
+#define V6T_RBITS_WORDS (2048u + 1024u) /* GROUP bitmap of the root, u16 ranks */
+#define V6T_DEEP (1u << 29)
+#define V6T_LINE_MASK (V6T_DEEP - 1u)
+
 typedef struct v6_lpm {
-	const uint2 *root;     /* 65536 x {row, short entry}; NULL = empty table */
-	const uint32_t *masks; /* n_masks x 4 u32 (row 0 = no lengths) */
+	const uint32_t *root;  /* 65536 entries; NULL = empty table */
+	const uint32_t *b24;
+	const uint2 *b32;
+	const uint32_t *pool;  /* 128-B lines (node32) and 16-B units (lists) */
 	const uint32_t *vals;  /* indirect labels (>= 2^30) */
-	addr_set16 set;        /* used: bit0 used, bits 8..15 length; pad[0] entry */
-	uint32_t n_masks;
-	/* blocked bloom filter over the set's prefix keys: one 32-bit word per
-	 * key (bits 16.. of its pfx6_hash), three bits in it (v6_bloom_bits).
-	 * A probe whose bits are not all set cannot hit and is not issued; no
-	 * false negatives, so results never depend on it. */
-	const uint32_t *bloom;
-	uint32_t bloom_mask;   /* n_words - 1 (n_words a power of two <= 2^14) */
-	/* per mask row, its lengths longest first: x, y = the first 8 as bytes
-	 * (byte j of x | y << 32 = the j-th longest), z = how many the row has */
-	const uint4 *lens;
+	const uint4 *h64;      /* (m64 + 1) x 2 uint4 */
+	uint32_t m64;
+	/* LDS-staged forms (k_classify_x4): rbits = the root's GROUP bitmap
+	 * (2048 words) and u16 ranks (GROUP entries before word k: the b24
+	 * block, blocks being appended in root order); b24_16 = every b24 entry
+	 * as u16: 0x8000 | b32 block for GROUP, 0 for a leaf (read b24);
+	 * NULL when not representable */
+	const uint32_t *rbits;
+	const uint16_t *b24_16;
+	uint32_t n_b24;        /* b24 blocks */
 } v6_lpm;
 
-#define V6_BLOOM_MAX_WORDS 16384u /* 64 KiB: staged in LDS by the x4 kernel */
 #define EP6_BLOOM_MAX_WORDS 8192u /* 32 KiB: staged in LDS by k_prefilter_v6_q */
 
 static inline __host__ __device__ uint32_t v6_bloom_word(uint32_t h, uint32_t mask) { return (h >> 16) & mask; }

@@ -291,7 +291,11 @@ class Engine:
         canonically (layouts.ct_sorted)."""
         keys, vals, prev = [], [], None
         out = C.create_string_buffer(14)
+        cap = self.ct4_count()
         while self.L.cgpu_ct4_get_next_key(self.h, prev, out) == 0:
+            # a key stored twice would restart the walk forever
+            if len(keys) > cap:
+                raise AssertionError("cilium_ct4_global holds a key twice")
             prev = out.raw
             rc, v = self.ct4_lookup(np.frombuffer(prev, L.CT4_TUPLE)[0])
             assert rc == 0
@@ -325,7 +329,11 @@ class Engine:
     def ct6_dump(self):
         keys, vals, prev = [], [], None
         out = C.create_string_buffer(38)
+        cap = self.ct6_count()
         while self.L.cgpu_ct6_get_next_key(self.h, prev, out) == 0:
+            # a key stored twice would restart the walk forever
+            if len(keys) > cap:
+                raise AssertionError("cilium_ct6_global holds a key twice")
             prev = out.raw
             rc, v = self.ct6_lookup(np.frombuffer(prev, L.CT6_TUPLE)[0])
             assert rc == 0
