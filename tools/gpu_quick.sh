@@ -9,7 +9,7 @@ TAG=$1; TESTS=$2; CONFS=$3; TRACE=$4
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v --tb=short --timeout 150 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest.log
   [ $rc -le 1 ] || exit $rc
 fi
