@@ -37,7 +37,8 @@ Other BASELINE configs (not the headline line; run them explicitly):
                      ct_create4's address entries): 16M packets of 500k
                      connections (40 % to services), map emptied each step;
                      parity and the CPU baseline on the whole batch
-  --config ct6       the same over IPv6 (cilium_ct6_global, cgpu_classify_v6_ct):
+  --config ctlb6     ctlb over IPv6 (cgpu_classify_v6_ctlb, 100k IPv6 services)
+  --config ct6       ct over IPv6 (cilium_ct6_global, cgpu_classify_v6_ct):
                      100k IPv6 ipcache prefixes + 64k policy keys, 64M packets
                      of 2M connections, parity on 1/64 of the address pairs
   --config mapstate  L3 MapState compilation: the label
@@ -122,6 +123,11 @@ WORKLOADS = {
             "connections (~32 packets each, 40 % to services, 0.01 % loopback backends), map emptied "
             "each step: CT_SERVICE lookup/create + slave reuse -> ct_lookup4 -> ipcache -> policy -> "
             "ct_create4 with the service's state and address entry, bit-exact",
+    "ctlb6": "IPv6 tables at config-2 size + 100k IPv6 services + stateful conntrack behind the IPv6 "
+             "stateful service step (cgpu_classify_v6_ctlb, lb6_local with CONNTRACK over "
+             "cilium_ct6_global): 16M packets per GPU of 500k connections (~32 packets each, 40 % to "
+             "services), map emptied each step: CT_SERVICE lookup/create + slave reuse -> lb6_xlate -> "
+             "ct_lookup6 -> ipcache6 -> policy -> ct_create6 with the service's state, bit-exact",
     "ct6": "IPv6 tables at config-2 size (100k IPv6 ipcache prefixes + 64k policy entries) + stateful "
            "conntrack (cilium_ct6_global): 64M packets per GPU of 2M TCP/UDP/ICMPv6 connections, map "
            "emptied each step: ct_lookup6 -> ipcache6 -> policy -> reply/related skip, ct_create6 / "
@@ -166,8 +172,8 @@ def main():
     pf6 = args.config == "pf6"
     cascade = args.config == "cascade"
     frames = args.config == "frames"
-    ct6 = args.config == "ct6"
-    ctlb = args.config == "ctlb"
+    ct6 = args.config in ("ct6", "ctlb6")
+    ctlb = args.config in ("ctlb", "ctlb6")
     ct = args.config == "ct" or ct6 or ctlb
     v6 = args.config == "v6"
     cfg = synth.CONFIGS["v6" if ct6 else "gpu" if (pf6 or frames or ct) else args.config]
@@ -185,7 +191,12 @@ def main():
         T = synth.make_tables6(**cfg) if ct6 else synth.make_tables(**cfg)
         # each rank's stream is its conntrack shard (address pairs with
         # pairhash % world == rank): per-rank maps, no shared state
-        if ctlb:
+        if ctlb and ct6:
+            S = synth.make_services6(T, 100_000)
+            tup, _, seclabels, S = synth.make_ctlb6_workload(T, S, n // CT_PKTS_PER_CONN, gpu_id=rank,
+                                                             mean_pkts=CT_PKTS_PER_CONN, world=world,
+                                                             loop_frac=1e-4)
+        elif ctlb:
             S = synth.make_services(T, synth.CONFIGS["cascade"]["n_services"])
             # loopback backends (an endpoint reaching itself through a
             # service) concentrate on the 4 endpoints' own pairs: a few
@@ -209,7 +220,7 @@ def main():
         synth.load_engine(e, T)
         synth.load_lxc(e, seclabels)
         if S is not None:
-            synth.load_services(e, S)
+            (synth.load_services6 if ct6 else synth.load_services)(e, S)
     elif v6:
         T = synth.make_tables6(**cfg)
         tup = synth.make_tuples6(T, n, gpu_id=rank)
@@ -273,7 +284,9 @@ def main():
         shard.init_counter_comm(e, rank, world)
 
     def launch():
-        if ct6:
+        if ctlb and ct6:
+            e.classify_v6_ctlb(d, CT_NOW, out=out, xlate=False, stream=stream)
+        elif ct6:
             e.classify_v6_ct(d, CT_NOW, out=out, stream=stream)
         elif ctlb:
             e.classify_v4_ctlb(d, CT_NOW, out=out, xlate=False, stream=stream)
@@ -384,7 +397,7 @@ def main():
             o.ct_set_max(ct_max)
             o.ct6_set_max(ct_max)
             if S is not None:
-                synth.load_services(o, S)
+                (synth.load_services6 if ct6 else synth.load_services)(o, S)
         else:
             o = Oracle(**T.oracle_config())
             synth.load_oracle(o, T)
@@ -427,7 +440,7 @@ def main():
         for rep in range(3):
             c0 = time.perf_counter()
             if ctlb:
-                r_ = o.classify_v4_ctlb(tsub, CT_NOW)
+                r_ = (o.classify_v6_ctlb if ct6 else o.classify_v4_ctlb)(tsub, CT_NOW)
                 res = (r_["verdict"], r_["ct_ret"], r_["identity"], r_["stage"], r_["probes"])
             elif ct:
                 res = (o.classify_v6_ct if ct6 else o.classify_v4_ct)(tsub, CT_NOW)
@@ -459,7 +472,7 @@ def main():
             cpu = {"value": round(n_cpu / c_el / 1e6, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
                    "sample": (f"rank-0 batch, all {n_cpu} packets from an empty map; "
-                              f"oracle/cgpu_oracle.c or_classify_v4_ctlb " if ctlb else
+                              f"oracle/cgpu_oracle.c or_classify_v{6 if ct6 else 4}_ctlb " if ctlb else
                               f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
                               f"pairs from an empty map; oracle/cgpu_oracle.c "
                               f"or_classify_v{6 if ct6 else 4}_ct ") +
@@ -486,7 +499,7 @@ def main():
                 parity = parity and np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
         probes_per = probes / n_cpu
         b_in, b_out = ((B_IN_PF6, B_OUT_PF6) if pf6 else (B_IN_FRAMES, B_OUT) if frames
-                       else (B_IN_CT6, B_OUT_CT) if ct6 else (B_IN_CT + (4 if ctlb else 0), B_OUT_CT) if ct
+                       else (B_IN_CT6 + (4 if ctlb else 0), B_OUT_CT) if ct6 else (B_IN_CT + (4 if ctlb else 0), B_OUT_CT) if ct
                        else (B_IN_V6, B_OUT) if v6
                        else (B_IN + (2 if cascade else 0), B_OUT))
         b_alg = b_in + b_out + 64.0 * probes_per

@@ -772,35 +772,35 @@ static uint2 v6t_node32(V6Build &b, const std::vector<const T6 *> &ps, uint32_t 
 		outer = below ? first : last;
 		break;
 	}
-	b.pool.resize((b.pool.size() + 31) / 32 * 32, 0u);
-	const size_t line = b.pool.size() / 32;
+	b.pool.resize((b.pool.size() + V6T_LW - 1) / V6T_LW * V6T_LW, 0u);
+	const size_t line = b.pool.size() / V6T_LW;
 	uint32_t s = 0;
 	for (; s <= 6 && s <= w; s++) {
 		const uint64_t width = 1ull << (w - s);
-		std::vector<std::array<uint32_t, 32>> lines(1u << s);
+		std::vector<std::vector<uint32_t>> lines(1u << s);
 		bool fits = true;
 		size_t i = 0;
 		uint32_t cur = first;
 		for (uint32_t k = 0; k < (1u << s) && fits; k++) {
 			const uint64_t S = (uint64_t)base + k * width;
 			auto &L = lines[k];
-			L.fill(0xFFFFFFFFu);
+			L.assign(V6T_LW, 0xFFFFFFFFu);
 			for (; i < cut.size() && (uint64_t)cut[i].first <= S; i++)
 				cur = cut[i].second;
-			L[15] = outer;
-			L[16] = cur;
+			L[V6T_NB] = outer;
+			L[V6T_NB + 1] = cur;
 			uint32_t n = 0;
 			for (; i < cut.size() && (uint64_t)cut[i].first < S + width; i++) {
-				if (n == 15) {
+				if (n == V6T_NB) {
 					fits = false;
 					break;
 				}
 				L[n] = (uint32_t)cut[i].first - 1u;
 				cur = cut[i].second;
-				L[16 + ++n] = cur;
+				L[V6T_NB + 1 + ++n] = cur;
 			}
-			for (uint32_t j = n + 1; j < 16; j++)
-				L[16 + j] = cur;
+			for (uint32_t j = n + 1; j <= V6T_NB; j++)
+				L[V6T_NB + 1 + j] = cur;
 		}
 		if (!fits)
 			continue;
@@ -812,17 +812,16 @@ static uint2 v6t_node32(V6Build &b, const std::vector<const T6 *> &ps, uint32_t 
 		s = V6T_LONG;
 		w = 32;
 		base = 0;
-		std::array<uint32_t, 32> h;
-		h.fill(0u);
+		std::vector<uint32_t> h(V6T_LW, 0u);
 		h[0] = (uint32_t)cut.size();
-		h[15] = first;
+		h[V6T_NB] = first;
 		b.pool.insert(b.pool.end(), h.begin(), h.end());
 		for (auto &c : cut)
 			b.pool.push_back((uint32_t)c.first - 1u);
 		b.pool.push_back(first);
 		for (auto &c : cut)
 			b.pool.push_back(c.second);
-		b.pool.resize((b.pool.size() + 31) / 32 * 32, 0u);
+		b.pool.resize((b.pool.size() + V6T_LW - 1) / V6T_LW * V6T_LW, 0u);
 	}
 	b.too_big |= line > V6T_LINE_MASK;
 	return make_uint2(DIR_TAG_GROUP | (deep ? V6T_DEEP : 0u) | (uint32_t)line, base | (w - 9u) | s << 5);
@@ -914,7 +913,7 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 		const uint32_t base = p->len == 0 ? 0 : ((uint32_t)(p->hi >> 48) & ~(cnt - 1));
 		std::fill(b.root.begin() + base, b.root.begin() + base + cnt, p->enc);
 	}
-	b.pool.assign(32, 0xFFFFFFFFu); /* line 0 unused */
+	b.pool.assign(V6T_LW, 0xFFFFFFFFu); /* line 0 unused */
 	b.b24.clear();
 	b.b32.clear();
 	std::vector<std::array<uint32_t, 8>> r64;
@@ -1011,8 +1010,8 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 		i = j;
 	}
 	hop_place<8>(b.h64, b.m64, r64, h64_home);
-	/* 32 words past the last line: a lane reads a whole line */
-	b.pool.insert(b.pool.end(), 32, 0xFFFFFFFFu);
+	/* a line past the last: a lane reads a whole line */
+	b.pool.insert(b.pool.end(), V6T_LW, 0xFFFFFFFFu);
 	/* LDS-staged forms */
 	const uint32_t nb24 = (uint32_t)(b.b24.size() / 256), nb32 = (uint32_t)(b.b32.size() / 512);
 	b.rbits.assign(V6T_RBITS_WORDS, 0u);
@@ -1057,19 +1056,19 @@ static uint32_t v6t_host_lookup(const V6Build &b, const uint8_t *a)
 	size_t line = nx & V6T_LINE_MASK;
 	uint32_t lab;
 	if (sc == V6T_LONG) {
-		const uint32_t n = b.pool[32 * line];
+		const uint32_t n = b.pool[V6T_LW * line];
 		uint32_t c = 0;
 		for (uint32_t i = 0; i < n; i++)
-			c += b.pool[32 * (line + 1) + i] < x;
-		lab = b.pool[32 * (line + 1) + n + c];
+			c += b.pool[V6T_LW * (line + 1) + i] < x;
+		lab = b.pool[V6T_LW * (line + 1) + n + c];
 	} else {
 		const bool out = wb < 32 && (rel >> wb) != 0;
 		const uint32_t sh = wb - sc;
 		line += out || sh >= 32 ? 0 : rel >> sh;
 		uint32_t c = 0;
-		for (int i = 0; i < 15; i++)
-			c += b.pool[32 * line + i] < x;
-		lab = out ? b.pool[32 * line + 15] : b.pool[32 * line + 16 + c];
+		for (uint32_t i = 0; i < V6T_NB; i++)
+			c += b.pool[V6T_LW * line + i] < x;
+		lab = out ? b.pool[V6T_LW * line + V6T_NB] : b.pool[V6T_LW * line + V6T_NB + 1 + c];
 	}
 	if (nx & V6T_DEEP) {
 		const uint32_t home = mix32(w[0], w[1]) & b.m64;

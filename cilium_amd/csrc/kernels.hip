@@ -283,19 +283,32 @@ __device__ __forceinline__ uint32_t v6t_line(uint32_t ex, uint32_t ey, uint32_t 
 	return (ex & V6T_LINE_MASK) + (s == V6T_LONG ? 0u : k);
 }
 
-/* region of x in a line: #{slot i < x, i < 15} over its boundary units */
-__device__ __forceinline__ uint32_t v6t_count(uint4 q0, uint4 q1, uint4 q2, uint4 q3, uint32_t x)
+/* The label of x in a node line whose first four 16-B units are q0..q3
+ * (tables.h v6_lpm): the region r = #{slot i < x, i < V6T_NB}; 128-B lines
+ * read label r as one more word of the line, 64-B lines hold it in q2, q3. */
+__device__ __forceinline__ uint32_t v6t_label(const uint32_t *pool, uint32_t line, bool out, uint4 q0, uint4 q1,
+					      uint4 q2, uint4 q3, uint32_t x)
 {
-	return (q0.x < x) + (q0.y < x) + (q0.z < x) + (q0.w < x) + (q1.x < x) + (q1.y < x) + (q1.z < x) +
-	       (q1.w < x) + (q2.x < x) + (q2.y < x) + (q2.z < x) + (q2.w < x) + (q3.x < x) + (q3.y < x) +
-	       (q3.z < x);
+	static_assert(V6T_NB == 15u || V6T_NB == 7u, "node lines of 15 or 7 boundaries");
+	if constexpr (V6T_NB == 15u) {
+		const uint32_t c = (q0.x < x) + (q0.y < x) + (q0.z < x) + (q0.w < x) + (q1.x < x) + (q1.y < x) +
+				   (q1.z < x) + (q1.w < x) + (q2.x < x) + (q2.y < x) + (q2.z < x) + (q2.w < x) +
+				   (q3.x < x) + (q3.y < x) + (q3.z < x);
+		return out ? q3.w : pool[V6T_LW * line + 16u + c];
+	} else {
+		const uint32_t c = (q0.x < x) + (q0.y < x) + (q0.z < x) + (q0.w < x) + (q1.x < x) + (q1.y < x) +
+				   (q1.z < x);
+		const uint32_t lo = c & 1u ? (c & 2u ? q2.w : q2.y) : (c & 2u ? q2.z : q2.x);
+		const uint32_t hi = c & 1u ? (c & 2u ? q3.w : q3.y) : (c & 2u ? q3.z : q3.x);
+		return out ? q1.w : (c & 4u ? hi : lo);
+	}
 }
 
 /* a V6T_LONG node: n boundaries (b - 1) and n + 1 labels from line + 1 on,
  * binary-searched */
 __device__ __forceinline__ uint32_t v6t_long(const uint32_t *pool, uint32_t line, uint32_t n, uint32_t x)
 {
-	const uint32_t *b = pool + 32u * (line + 1u);
+	const uint32_t *b = pool + V6T_LW * (line + 1u);
 	uint32_t lo = 0, hi = n; /* count of b[i] < x */
 	while (lo < hi) {
 		const uint32_t m = (lo + hi) >> 1;
@@ -359,13 +372,13 @@ __device__ __forceinline__ uint32_t v6_lookup(const v6_lpm &t, uint4 a)
 		return n.x;
 	bool out;
 	const uint32_t line = v6t_line(n.x, n.y, w.y, out);
-	const uint4 *q = reinterpret_cast<const uint4 *>(t.pool) + 8u * line;
+	const uint4 *q = reinterpret_cast<const uint4 *>(t.pool) + (V6T_LW / 4u) * line;
 	const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
 	uint32_t lab;
 	if (((n.y >> 5) & 7u) == V6T_LONG)
 		lab = v6t_long(t.pool, line, q0.x, w.y);
 	else
-		lab = out ? q3.w : t.pool[32u * line + 16u + v6t_count(q0, q1, q2, q3, w.y)];
+		lab = v6t_label(t.pool, line, out, q0, q1, q2, q3, w.y);
 	if (n.x & V6T_DEEP) {
 		const uint32_t home = mix32(w.x, w.y) & t.m64;
 		const uint32_t r = v6t_rec(t, w, home, t.h64[2u * home], t.h64[2u * home + 1u]);
@@ -1241,7 +1254,7 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 	for (int u = 0; u < Q; u++) {
 		q0[u] = q1[u] = q2[u] = q3[u] = h0[u] = h1[u] = make_uint4(0, 0, 0, 0);
 		if (node[u]) {
-			const uint4 *q = reinterpret_cast<const uint4 *>(t.pool) + 8u * line[u];
+			const uint4 *q = reinterpret_cast<const uint4 *>(t.pool) + (V6T_LW / 4u) * line[u];
 			q0[u] = q[0];
 			q1[u] = q[1];
 			q2[u] = q[2];
@@ -1261,8 +1274,7 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 		if (((n[u].y >> 5) & 7u) == V6T_LONG)
 			lab[u] = v6t_long(t.pool, line[u], q0[u].x, w[u].y);
 		else
-			lab[u] = out[u] ? q3[u].w
-					: t.pool[32u * line[u] + 16u + v6t_count(q0[u], q1[u], q2[u], q3[u], w[u].y)];
+			lab[u] = v6t_label(t.pool, line[u], out[u], q0[u], q1[u], q2[u], q3[u], w[u].y);
 	}
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
@@ -1528,7 +1540,13 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 			for (int u = 0; u < Q; u++)
 				act[u] = (fw[u] & (F_OK | F_GATED | F_LBDROP)) == F_OK;
+#ifdef CGPU_DIAG_V6_NO_TRIE /* timing-only tool build: wrong identities */
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				e[u] = act[u] ? (DIR_TAG_DIRECT | 2u) : 0u;
+#else
 			v6t_lookup_q<Q>(s.ipc6, ldict, n24 != 0u, ad6, act, e);
+#endif
 		} else {
 			/* v4: the /16's inline node (x16), then the compressed LPM */
 			{
@@ -2668,7 +2686,11 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 #ifdef CGPU_DIAG_LDS_PAD /* timing-only: fewer resident workgroups per CU */
 	lds += CGPU_DIAG_LDS_PAD;
 #endif
-	constexpr int Q = V6 ? 2 : 4; /* v6: Q = 4 spills (16-byte addresses, 64-byte buckets) */
+#ifdef CGPU_DIAG_V6_Q /* timing-only tool build (tools/diag_ab.py): v6 tuples per lane */
+	constexpr int Q = V6 ? CGPU_DIAG_V6_Q : 4;
+#else
+	constexpr int Q = V6 ? 2 : 4; /* v6: 16-byte addresses and the trie's line registers */
+#endif
 	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR>;
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
@@ -4244,6 +4266,9 @@ __device__ __forceinline__ void ctc_prefetch(const ct_table &T, ct_cache<K> &c, 
 					     const typename K::key &k1, const typename K::key &k2, bool w0, bool w1,
 					     bool w2)
 {
+#ifdef CGPU_DIAG_CT_NO_PREFETCH /* timing-only tool build: keys probed one by one */
+	return;
+#endif
 	ct_chain c0{0, 0xFFFFFFFFu, 0, -3}, c1 = c0, c2 = c0;
 	/* one probe per distinct key: an ICMP error's forward key IS its
 	 * related key (ports 0, RELATED set), and two cache entries of one key

@@ -245,6 +245,14 @@ static inline __host__ __device__ uint32_t pfx6_hash(uint32_t w0, uint32_t w1, u
  * lo words), n + 1 labels.  V6T_FALL where no /65+ prefix covers x: the node's
  * label stands. */
 #define V6T_LONG 7u
+#ifndef CGPU_V6T_NB
+#define CGPU_V6T_NB 15
+#endif
+/* boundaries per node line (15: 128-B lines as above; 7: 64-B lines of 7
+ * boundaries, outer, 8 labels: the label is in the registers the count
+ * read) */
+#define V6T_NB ((uint32_t)CGPU_V6T_NB)
+#define V6T_LW (2u * (V6T_NB + 1u)) /* line words */
 #define V6T_FALL DIR_TAG_GROUP
 #define V6T_RBITS_WORDS (2048u + 1024u) /* GROUP bitmap of the root, u16 ranks */
 #define V6T_DEEP (1u << 29)

@@ -33,7 +33,11 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "pf6_q2": ("CGPU_DIAG_PF6_Q=2",),
             "pf6_q2_prefetch": ("CGPU_DIAG_PF6_Q=2", "CGPU_DIAG_PF6_PREFETCH"),
             "ct_coherent_probe": ("CGPU_DIAG_CT_COHERENT_PROBE",),
-            "walk_clock": ("CGPU_DIAG_WALK_CLOCK",)}
+            "walk_clock": ("CGPU_DIAG_WALK_CLOCK",),
+            "v6_q3": ("CGPU_DIAG_V6_Q=3",), "v6_q4": ("CGPU_DIAG_V6_Q=4",),
+            "v6_no_trie": ("CGPU_DIAG_V6_NO_TRIE",), "v6_l64": ("CGPU_V6T_NB=7",),
+            "v6_l64_q3": ("CGPU_V6T_NB=7", "CGPU_DIAG_V6_Q=3"),
+            "ct_no_prefetch": ("CGPU_DIAG_CT_NO_PREFETCH",)}
 
 
 def build(names):
