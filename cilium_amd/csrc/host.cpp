@@ -4203,7 +4203,16 @@ CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n,
 	classify_v6_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
 			   verdict, identity, stage, delta, (uint64_t)n, pk};
 	HIP_OR_EIO(hipSetDevice(c->device));
-	HIP_OR_EIO(launch_classify_v6(s, a, (hipStream_t)stream));
+	/* the x4 schedule's ipcache pre-pass: n entries of stream-ordered pool
+	 * scratch */
+	void *scr = nullptr;
+	if (s.ipc6.root && !(s.schedule & (CGPU_SCHED_PER_LANE | CGPU_SCHED_GLOBAL_CTR)))
+		HIP_OR_EIO(hipMallocFromPoolAsync(&scr, (size_t)n * 4u, c->pool, (hipStream_t)stream));
+	a.ipc_e = static_cast<uint32_t *>(scr);
+	const hipError_t le = launch_classify_v6(s, a, (hipStream_t)stream);
+	if (scr)
+		HIP_OR_EIO(hipFreeAsync(scr, (hipStream_t)stream));
+	HIP_OR_EIO(le);
 	return 0;
 }
 

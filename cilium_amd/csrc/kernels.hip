@@ -889,6 +889,8 @@ struct cls_args {
 	/* k_classify_x4 FR (frames): the tuple count is *n_dev - n_off, at most n */
 	const uint32_t *n_dev;
 	uint64_t n_off;
+	/* k_classify_x4 IPCE: the ipcache entries k_ipc6_pre wrote, [n] */
+	uint32_t *ipc_e;
 };
 
 /* The identity resolution and the three-probe policy cascade for one tuple
@@ -1312,7 +1314,7 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 #define FRF_V6 0x40u
 
 template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false,
-	  bool FR = false>
+	  bool FR = false, bool IPCE = false>
 __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a0, uint64_t *pk)
 {
 	cls_args a = a0;
@@ -1340,10 +1342,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	/* after the hot counters: v4 the LPM leaf dictionary; v6 the ipcache
 	 * trie's root bitmap and ranks, then its b24 blocks as u16 (if staged) */
 	uint32_t *ldict = reinterpret_cast<uint32_t *>(lctr + s.hot_slots);
-	const uint32_t n24 = V6 ? v6t_lds_b24(s.ipc6) : 0u;
+	const uint32_t n24 = V6 && !IPCE ? v6t_lds_b24(s.ipc6) : 0u;
 	/* cold-slot cache (x4_lds_layout): cc_n u64 packed counts, then cc_n u32
 	 * tags (slot + 1, 0 = free) */
-	const uint32_t lds_words = V6 ? v6t_lds_words(s.ipc6) : s.ipc4c.n_dict;
+	const uint32_t lds_words = V6 ? (IPCE ? 0u : v6t_lds_words(s.ipc6)) : s.ipc4c.n_dict;
 	uint64_t *ccv = lctr + s.hot_slots + ((lds_words + 1u) >> 1);
 	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + a.cc_n);
 	const uint32_t ccm = a.cc_n - 1u;
@@ -1356,7 +1358,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	if (threadIdx.x < 16)
 		lmet[threadIdx.x] = 0;
 	if (V6) {
-		if (s.ipc6.root) {
+		if (s.ipc6.root && !IPCE) {
 			for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += NT)
 				ldict[k] = s.ipc6.rbits[k];
 			const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
@@ -1453,6 +1455,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 				for (int u = 0; u < Q; u++) {
 					const uint64_t i = i0 + u < a.n ? i0 + u : i0;
+					if constexpr (IPCE) { /* the pre-pass looked the address up */
+						ad6[u] = make_uint4(0, 0, 0, 0);
+						continue;
+					}
 					uint4 raw = ld_x4<NTL>(static_cast<const uint4 *>((fl[u] & 1u) ? a.daddr : a.saddr) + i);
 					if (LB && live && (fl[u] & 1u) && i0 + u < a.n) {
 						/* egress service step first (bpf_lxc.c:117-149) */
@@ -1545,7 +1551,25 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 			for (int u = 0; u < Q; u++)
 				e[u] = act[u] ? (DIR_TAG_DIRECT | 2u) : 0u;
 #else
-			v6t_lookup_q<Q>(s.ipc6, ldict, n24 != 0u, ad6, act, e);
+			if constexpr (IPCE) {
+				uint32_t pe[QA];
+				if (full && Q == 4) {
+					const uint4 v = ld_x4<NTL>(a.ipc_e + i0);
+					pe[0] = v.x, pe[1] = v.y, pe[2] = v.z, pe[3] = v.w;
+				} else if (full && Q == 2) {
+					const uint2 v = ld_x2<NTL>(a.ipc_e + i0);
+					pe[0] = v.x, pe[1] = v.y;
+				} else {
+#pragma unroll
+					for (int u = 0; u < Q; u++)
+						pe[u] = a.ipc_e[i0 + u < a.n ? i0 + u : i0];
+				}
+#pragma unroll
+				for (int u = 0; u < Q; u++)
+					e[u] = act[u] ? pe[u] : 0u;
+			} else {
+				v6t_lookup_q<Q>(s.ipc6, ldict, n24 != 0u, ad6, act, e);
+			}
 #endif
 		} else {
 			/* v4: the /16's inline node (x16), then the compressed LPM */
@@ -2665,13 +2689,76 @@ static cgpu_snapshot with_lds_hot(const cgpu_snapshot &s, size_t max_hot)
 	return r;
 }
 
-template <bool LB, bool V6, bool FR = false>
+/* cgpu_classify_v6's ipcache pass on the x4 schedule: every tuple's
+ * looked-up address (daddr egress, saddr ingress, bpf_lxc.c:170-187 /
+ * bpf_netdev.c:203-211) through the trie (v6t_lookup_q), its DIR entry to
+ * e[i].  Kept out of k_classify_x4 so that the trie walk's dependent loads
+ * run at this kernel's occupancy (few registers, no counter LDS) instead of
+ * the classify kernel's; the classify kernel then reads 4 bytes per tuple
+ * instead of the address.  Lane-interleaved: load instruction u of a wave
+ * covers 64 consecutive tuples. */
+template <int Q, int NT>
+__global__ __launch_bounds__(NT) void k_ipc6_pre(cgpu_snapshot s, const uint4 *sa, const uint4 *da,
+						 const uint8_t *flags, uint32_t *e_out, uint64_t n)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t lt[];
+	const uint32_t n24 = v6t_lds_b24(s.ipc6);
+	if (s.ipc6.root) {
+		for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += NT)
+			lt[k] = s.ipc6.rbits[k];
+		const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
+		for (uint32_t k = threadIdx.x; k < n24 * 128u; k += NT)
+			lt[V6T_RBITS_WORDS + k] = b16[k];
+	}
+	__syncthreads();
+	const uint64_t T = (uint64_t)gridDim.x * NT;
+	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < n; g += T * Q) {
+		uint4 w[Q];
+		bool act[Q];
+		uint32_t e[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = i < n;
+			w[u] = make_uint4(0, 0, 0, 0);
+			if (act[u])
+				w[u] = v6_host_words(ld_x4<true>(((flags[i] & 1u) ? da : sa) + i));
+		}
+		v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w, act, e);
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (act[u])
+				e_out[g + (uint64_t)u * T] = e[u];
+	}
+}
+
+#ifndef CGPU_DIAG_IPC6_PRE_Q
+#define CGPU_DIAG_IPC6_PRE_Q 2
+#endif
+
+static hipError_t launch_ipc6_pre(const cgpu_snapshot &s, const cls_args &a, hipStream_t st)
+{
+	constexpr int NT = 1024, Q = CGPU_DIAG_IPC6_PRE_Q;
+	const size_t lds = (size_t)v6t_lds_words(s.ipc6) * 4u;
+	const unsigned res = resident_blocks((const void *)k_ipc6_pre<Q, NT>, NT, lds);
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + Q * NT - 1) / (Q * NT), res));
+	hipLaunchKernelGGL((k_ipc6_pre<Q, NT>), dim3(g), dim3(NT), lds, st, s, static_cast<const uint4 *>(a.saddr),
+			   static_cast<const uint4 *>(a.daddr), a.flags, a.ipc_e, a.n);
+	return hipGetLastError();
+}
+
+template <bool LB, bool V6, bool FR = false, bool IPCE = false>
 static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024;
+	if constexpr (IPCE) {
+		hipError_t e = launch_ipc6_pre(s0, a, st);
+		if (e != hipSuccess)
+			return e;
+	}
 	/* LDS: hot counters + the ipcache leaf dictionary (v4) / the staged trie
-	 * levels (v6) */
-	size_t fixed = V6 ? (size_t)v6t_lds_words(s0.ipc6) * 4u : (size_t)s0.ipc4c.n_dict * 4u;
+	 * levels (v6 without the pre-pass) */
+	size_t fixed = V6 ? (IPCE ? 0u : (size_t)v6t_lds_words(s0.ipc6) * 4u) : (size_t)s0.ipc4c.n_dict * 4u;
 	fixed = (fixed + 7u) & ~(size_t)7u;
 	const cgpu_snapshot s = with_lds_hot(s0, fixed < X4_LDS_BUDGET ? (X4_LDS_BUDGET - fixed) / 8u : 0u);
 	size_t lds = (size_t)s.hot_slots * 8u + fixed;
@@ -2687,11 +2774,11 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 	lds += CGPU_DIAG_LDS_PAD;
 #endif
 #ifdef CGPU_DIAG_V6_Q /* timing-only tool build (tools/diag_ab.py): v6 tuples per lane */
-	constexpr int Q = V6 ? CGPU_DIAG_V6_Q : 4;
+	constexpr int Q = V6 && !IPCE ? CGPU_DIAG_V6_Q : 4;
 #else
-	constexpr int Q = V6 ? 2 : 4; /* v6: 16-byte addresses and the trie's line registers */
+	constexpr int Q = V6 && !IPCE ? 2 : 4; /* in-kernel v6 lookups: the trie's line registers */
 #endif
-	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR>;
+	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE>;
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
@@ -2715,9 +2802,12 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 			c.sport += off;
 		if (c.hash)
 			c.hash += off;
+		if (c.ipc_e)
+			c.ipc_e += off;
 		c.n_off = off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + Q * NT - 1) / (Q * NT), res);
-		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6, FR>), dim3(g), dim3(NT), lds, st, s, c, a.pk);
+		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE>), dim3(g), dim3(NT), lds, st, s, c,
+				   a.pk);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
@@ -2742,7 +2832,8 @@ static hipError_t launch_classify(const cgpu_snapshot &s0, cls_args a, hipStream
 	}
 	if (!(s0.schedule & CGPU_SCHED_PER_LANE) && a.pk && x4_aligned(a)) {
 		if (V6)
-			return a.lb ? launch_x4<true, true>(s0, a, st) : launch_x4<false, true>(s0, a, st);
+			return a.lb ? launch_x4<true, true>(s0, a, st)
+				    : (a.ipc_e ? launch_x4<false, true, false, true>(s0, a, st) : launch_x4<false, true>(s0, a, st));
 		return a.lb ? launch_x4<true, false>(s0, a, st) : launch_x4<false, false>(s0, a, st);
 	}
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
@@ -2786,9 +2877,10 @@ hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x,
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)
 {
-	return launch_classify<1>(s, cls_args{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len,
-					      x.ep, x.verdict, x.identity, x.stage, x.delta, x.n, x.pk, x.lb, x.sport,
-					      x.hash}, st);
+	cls_args c{x.saddr16, x.daddr16, x.dport, x.proto, x.flags, x.len, x.ep, x.verdict, x.identity,
+		   x.stage, x.delta, x.n, x.pk, x.lb, x.sport, x.hash};
+	c.ipc_e = x.ipc_e;
+	return launch_classify<1>(s, c, st);
 }
 
 hipError_t launch_lb4(const cgpu_snapshot &s, const lb4_args &a, hipStream_t st)
@@ -4266,7 +4358,11 @@ __device__ __forceinline__ void ctc_prefetch(const ct_table &T, ct_cache<K> &c, 
 					     const typename K::key &k1, const typename K::key &k2, bool w0, bool w1,
 					     bool w2)
 {
-#ifdef CGPU_DIAG_CT_NO_PREFETCH /* timing-only tool build: keys probed one by one */
+#ifndef CGPU_CT_PREFETCH
+	/* off: probing the step's keys together measured slower than probing
+	 * them as the step needs them (ct config 21.9 -> 18.5 ms per 64M-packet
+	 * batch, profiles/r3_ct_ab): the extra chains cost more than the latency
+	 * they overlap, and most packets need only the reply key */
 	return;
 #endif
 	ct_chain c0{0, 0xFFFFFFFFu, 0, -3}, c1 = c0, c2 = c0;

@@ -46,6 +46,9 @@ struct classify_v6_args {
 	int lb;
 	const uint16_t *sport;
 	const uint32_t *hash; /* NULL: flow_hash(fold6(saddr), fold6(daddr), sport, dport, proto) */
+	/* scratch of n u32 (optional): the x4 schedule's ipcache pre-pass
+	 * (k_ipc6_pre) writes every tuple's trie entry there */
+	uint32_t *ipc_e;
 };
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &a, hipStream_t st);
