@@ -5077,10 +5077,10 @@ static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool 
 	L.head = take(n);
 	L.temp_bytes = ct_temp_bytes(n);
 	L.temp = take(L.temp_bytes);
+	L.flags2 = take(2 * n); /* phase-2 candidates */
 	if (svc) {
 		L.svc_out = take(n * (v6 ? 32 : 16));
 		L.ctl = take(16);
-		L.flags2 = take(2 * n);
 	}
 	return L;
 }
@@ -5142,10 +5142,10 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.heads_pos = reinterpret_cast<uint32_t *>(b + L.heads_pos);
 	a.temp = b + L.temp;
 	a.temp_bytes = L.temp_bytes;
+	a.flags2 = b + L.flags2;
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
 		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);
-		a.flags2 = b + L.flags2;
 		HIP_OR_EIO(m.v6 ? launch_classify_v6_ctlb(s, T, a, cs) : launch_classify_v4_ctlb(s, T, a, cs));
 	} else {
 		HIP_OR_EIO(m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs));

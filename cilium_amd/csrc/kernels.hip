@@ -1935,7 +1935,8 @@ __device__ __forceinline__ int32_t fchk(uint32_t off, uint32_t sz, uint32_t len,
  * an option-less IPv4 / extension-less IPv6 header, global loads (L2) for
  * IPv4 options and IPv6 extension headers. */
 __device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fwin &W, const uint8_t *f,
-						uint32_t len, uint32_t cap, bool egress, uint32_t ep);
+						uint32_t len, uint32_t cap, bool egress, uint32_t ep,
+						const uint4 *lxc);
 
 __device__ __forceinline__ ftuple parse_frame(const cgpu_snapshot &s, const uint8_t *f, uint32_t len,
 					      uint32_t cap, bool egress, uint32_t ep)
@@ -1949,12 +1950,14 @@ __device__ __forceinline__ ftuple parse_frame(const cgpu_snapshot &s, const uint
 		W.w[4 * k + 2] = v.z;
 		W.w[4 * k + 3] = v.w;
 	}
-	return parse_frame_w(s, W, f, len, cap, egress, ep);
+	return parse_frame_w(s, W, f, len, cap, egress, ep, s.lxc);
 }
 
-/* the same with the frame's first 64 bytes already in W */
+/* the same with the frame's first 64 bytes already in W; lxc = the
+ * endpoints' rows (s.lxc, or a copy in LDS) */
 __device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fwin &W, const uint8_t *f,
-						uint32_t len, uint32_t cap, bool egress, uint32_t ep)
+						uint32_t len, uint32_t cap, bool egress, uint32_t ep,
+						const uint4 *lxc)
 {
 	ftuple t;
 	t.status = 0;
@@ -1996,7 +1999,7 @@ __device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fw
 	if (egress && ep < s.n_lxc) {
 		/* SMAC / DMAC / SIP checks of the endpoint (bpf_lxc.c:431-437,
 		 * :100-105; lib/lxc.h:31-89) */
-		const uint4 i0 = s.lxc[2u * ep];
+		const uint4 i0 = lxc[2u * ep];
 		const uint32_t verify = (i0.y >> 16) & 0xffu;
 		if ((verify & CGPU_VERIFY_SMAC) && (W.d(6) != i0.x || W.h(10) != (i0.y & 0xffffu))) {
 			t.status = DROP_INVALID_SMAC;
@@ -2011,7 +2014,7 @@ __device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fw
 			if (v4) {
 				ok = t.sa.x == i0.z;
 			} else {
-				const uint4 i1 = s.lxc[2u * ep + 1u];
+				const uint4 i1 = lxc[2u * ep + 1u];
 				ok = t.sa.x == i0.w && t.sa.y == i1.x && t.sa.z == i1.y && t.sa.w == i1.z;
 			}
 			if (!ok) {
@@ -2946,44 +2949,143 @@ hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hip
  * status, IPv6 frames compacted to their own columns with their index),
  * then k_classify_x4 runs over the IPv4 columns and, on the device-side
  * count, over the IPv6 ones, whose results are scattered back */
+/* endpoints whose rows k_frames_cols stages in LDS (8 KiB): the egress
+ * SMAC / DMAC / SIP checks then read LDS, not a global load that would wait
+ * behind the next tile's slot loads */
+#define FR_LXC_LDS 256u
+
+/* one tile of 64 frames in 64-byte slots: the wave's four coalesced 1-KiB
+ * loads (lane l holds bytes [1024 k + 16 l, +16) of the tile) and the
+ * lane's own len / flags / ep */
+struct fr_tile {
+	uint4 v[4];
+	uint32_t len, fl, ep;
+};
+
+__device__ __forceinline__ void fr_fetch(const frames_args &a, uint64_t i0, uint32_t lane, fr_tile &t)
+{
+	const uint64_t i = i0 + lane;
+	const uint64_t bytes = i0 < a.n ? min((uint64_t)64, a.n - i0) * 64u : 0u;
+	const uint8_t *base = a.data + i0 * 64u;
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		const uint32_t off = 1024u * k + 16u * lane;
+		t.v[k] = off < bytes ? ld_x4<true>(base + off) : make_uint4(0, 0, 0, 0);
+	}
+	const bool valid = i < a.n;
+	t.len = valid ? a.len[i] : 0u;
+	t.fl = valid ? a.flags[i] : 0u;
+	t.ep = valid ? a.ep[i] : 0u;
+}
+
+/* frame i's policy-tuple columns (or its FRF_DEC status / its compacted
+ * IPv6 row) from its parse */
+__device__ __forceinline__ void fr_emit(const cgpu_snapshot &s, const frames_args &a, const frames_x4 &c,
+					const uint4 *lxc, const fwin &W, uint64_t i, uint32_t len, uint32_t flv,
+					uint32_t ep)
+{
+	const bool valid = i < a.n;
+	const bool egress = valid && (flv & 1u);
+	const ftuple t = parse_frame_w(s, W, a.data + i * (uint64_t)a.stride, len, min(len, a.stride), egress, ep, lxc);
+	uint32_t fl = egress ? 1u : 0u, sa = 0, da = 0, dp = 0, pr = 0;
+	const bool v6 = t.status == 0 && t.fam != 4u;
+	if (t.status != 0) {
+		fl |= FRF_DEC;
+		da = (uint32_t)t.status;
+	} else if (!v6) {
+		sa = t.sa.x;
+		da = t.da.x;
+		dp = t.dport;
+		pr = t.proto;
+		fl |= t.frag ? 2u : 0u;
+	} else {
+		fl |= FRF_V6;
+	}
+	/* wave-aggregated slot of the IPv6 frames */
+	const uint64_t m = __ballot(valid && v6);
+	if (m) {
+		const int leader = __ffsll((unsigned long long)m) - 1;
+		uint32_t base = 0;
+		if ((int)__lane_id() == leader)
+			base = atomicAdd(c.n6, (uint32_t)__popcll(m));
+		base = __shfl(base, leader, 64);
+		if (valid && v6) {
+			const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+			c.sa6[j] = t.sa;
+			c.da6[j] = t.da;
+			c.dport6[j] = (uint16_t)t.dport;
+			c.proto6[j] = (uint8_t)t.proto;
+			c.fl6[j] = (uint8_t)(egress ? 1u : 0u);
+			c.len6[j] = len;
+			c.ep6[j] = (uint16_t)ep;
+			c.idx6[j] = (uint32_t)i;
+		}
+	}
+	if (!valid)
+		return;
+	c.sa4[i] = sa;
+	c.da4[i] = da;
+	c.dport[i] = (uint16_t)dp;
+	c.proto[i] = (uint8_t)pr;
+	c.fl[i] = (uint8_t)fl;
+}
+
+template <bool LXL>
 __global__ __launch_bounds__(256) void k_frames_cols(cgpu_snapshot s, frames_args a, frames_x4 c)
 {
 	/* 64-byte slots: a wave reads its 64 frames as four fully coalesced
 	 * 1-KiB loads and hands each lane its frame through LDS (rows of 17
 	 * words: conflict-free reads); per-lane 16-byte loads of 64 separate
-	 * slots cost one address-unit pass per lane and load */
+	 * slots cost one address-unit pass per lane and load.  Software-
+	 * pipelined: the next tile's slots and len / flags / ep are in flight
+	 * while this tile is parsed, and the endpoint rows come from LDS, so a
+	 * tile costs one memory round trip, not three. */
 	__shared__ uint32_t stg[4][64 * 17];
+	__shared__ uint4 lxl[LXL ? 2u * FR_LXC_LDS : 1u];
+	if constexpr (LXL) {
+		for (uint32_t k = threadIdx.x; k < 2u * s.n_lxc; k += 256u)
+			lxl[k] = s.lxc[k];
+		__syncthreads();
+	}
+	const uint4 *lxc = LXL ? static_cast<const uint4 *>(lxl) : s.lxc;
 	const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
-	for (uint64_t i0 = (uint64_t)blockIdx.x * 256u + wv * 64u; i0 < a.n; i0 += stride) {
-		const uint64_t i = i0 + lane;
-		const bool valid = i < a.n;
-		fwin W;
-		if (a.stride == 64u) {
-			const uint64_t bytes = min((uint64_t)64, a.n - i0) * 64u;
-			const uint8_t *base = a.data + i0 * 64u;
+	uint64_t i0 = (uint64_t)blockIdx.x * 256u + wv * 64u;
+	if (a.stride == 64u) {
+		fr_tile cur;
+		fr_fetch(a, i0, lane, cur);
+		for (; i0 < a.n; i0 += stride) {
+			fr_tile nxt;
+			fr_fetch(a, i0 + stride, lane, nxt);
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				const uint32_t off = 1024u * k + 16u * lane;
-				if (off < bytes) {
-					const uint4 v = ld_x4<true>(base + off);
-					uint32_t *d = &stg[wv][(off >> 6) * 17u + ((off & 63u) >> 2)];
-					d[0] = v.x;
-					d[1] = v.y;
-					d[2] = v.z;
-					d[3] = v.w;
-				}
+				uint32_t *d = &stg[wv][(off >> 6) * 17u + ((off & 63u) >> 2)];
+				d[0] = cur.v[k].x;
+				d[1] = cur.v[k].y;
+				d[2] = cur.v[k].z;
+				d[3] = cur.v[k].w;
 			}
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 			__builtin_amdgcn_wave_barrier();
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			fwin W;
 #pragma unroll
 			for (int j = 0; j < 16; j++)
 				W.w[j] = stg[wv][lane * 17u + j];
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 			__builtin_amdgcn_wave_barrier();
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-		} else if (valid) {
+			fr_emit(s, a, c, lxc, W, i0 + lane, cur.len, cur.fl, cur.ep);
+			cur = nxt;
+		}
+		return;
+	}
+	for (; i0 < a.n; i0 += stride) {
+		const uint64_t i = i0 + lane;
+		const bool valid = i < a.n;
+		fwin W;
+		if (valid) {
 			const uint8_t *f = a.data + i * (uint64_t)a.stride;
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
@@ -2994,51 +3096,7 @@ __global__ __launch_bounds__(256) void k_frames_cols(cgpu_snapshot s, frames_arg
 				W.w[4 * k + 3] = v.w;
 			}
 		}
-		const uint32_t len = valid ? a.len[i] : 0u;
-		const bool egress = valid && (a.flags[i] & 1u);
-		const uint32_t ep = valid ? a.ep[i] : 0u;
-		const ftuple t = parse_frame_w(s, W, a.data + i * (uint64_t)a.stride, len, min(len, a.stride), egress, ep);
-		uint32_t fl = egress ? 1u : 0u, sa = 0, da = 0, dp = 0, pr = 0;
-		const bool v6 = t.status == 0 && t.fam != 4u;
-		if (t.status != 0) {
-			fl |= FRF_DEC;
-			da = (uint32_t)t.status;
-		} else if (!v6) {
-			sa = t.sa.x;
-			da = t.da.x;
-			dp = t.dport;
-			pr = t.proto;
-			fl |= t.frag ? 2u : 0u;
-		} else {
-			fl |= FRF_V6;
-		}
-		/* wave-aggregated slot of the IPv6 frames */
-		const uint64_t m = __ballot(valid && v6);
-		if (m) {
-			const int leader = __ffsll((unsigned long long)m) - 1;
-			uint32_t base = 0;
-			if ((int)__lane_id() == leader)
-				base = atomicAdd(c.n6, (uint32_t)__popcll(m));
-			base = __shfl(base, leader, 64);
-			if (valid && v6) {
-				const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
-				c.sa6[j] = t.sa;
-				c.da6[j] = t.da;
-				c.dport6[j] = (uint16_t)t.dport;
-				c.proto6[j] = (uint8_t)t.proto;
-				c.fl6[j] = (uint8_t)(egress ? 1u : 0u);
-				c.len6[j] = len;
-				c.ep6[j] = (uint16_t)ep;
-				c.idx6[j] = (uint32_t)i;
-			}
-		}
-		if (!valid)
-			continue;
-		c.sa4[i] = sa;
-		c.da4[i] = da;
-		c.dport[i] = (uint16_t)dp;
-		c.proto[i] = (uint8_t)pr;
-		c.fl[i] = (uint8_t)fl;
+		fr_emit(s, a, c, lxc, W, i, valid ? a.len[i] : 0u, valid ? a.flags[i] : 0u, valid ? a.ep[i] : 0u);
 	}
 }
 
@@ -3095,10 +3153,13 @@ hipError_t launch_classify_frames_x4(const cgpu_snapshot &s, const frames_args &
 	hipError_t e = hipMemsetAsync(c.n6, 0, 4, st);
 	if (e != hipSuccess)
 		return e;
-	/* a streaming pass: up to 8 resident 256-thread blocks per CU (17 KiB
+	/* a streaming pass: up to 8 resident 256-thread blocks per CU (25 KiB
 	 * LDS each) so enough slot loads are in flight */
 	const unsigned gf = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + BLOCK - 1) / BLOCK, 256u * 8u * 4u));
-	hipLaunchKernelGGL(k_frames_cols, dim3(gf), dim3(BLOCK), 0, st, s, a, c);
+	if (s.n_lxc <= FR_LXC_LDS)
+		hipLaunchKernelGGL(k_frames_cols<true>, dim3(gf), dim3(BLOCK), 0, st, s, a, c);
+	else
+		hipLaunchKernelGGL(k_frames_cols<false>, dim3(gf), dim3(BLOCK), 0, st, s, a, c);
 	cls_args c4{c.sa4, c.da4, c.dport, c.proto, c.fl, a.len, a.ep, a.verdict, a.identity, a.stage,
 		    a.delta, a.n, a.pk, 0, nullptr, nullptr};
 	if (!x4_aligned(c4))
@@ -3232,7 +3293,10 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_PHASE2 128u   /* the packet's address pair may hold owed address entries: phase 2 */
 #define CTM_ADDRX 256u    /* its address entry lies in another pair: owed to phase 2 */
 #define CTM_SVCDROP 512u  /* lb4_local returned DROP_NO_SERVICE */
-#define CT_ADDRP 0x40u    /* walker -> phase 2: the address entry of this create is owed */
+#define CT_ADDRP 0x40u    /* walker -> phase 2: the address entry of this create is owed
+			   * (service path) / its ICMP entry (plain path, CTM_RELX) */
+#define CTM_RELX 1024u    /* plain path, TCP / UDP: grouped by connection in phase 1, the
+			   * ICMP entry a create writes is reserved and owed to phase 2 */
 #define CTB_LB_LOOPBACK 8u /* struct ct_entry lb_loopback (common.h:389) */
 #define TUPLE_F_SERVICE 4u /* conntrack.h:66 */
 /* rec word 2 .w of the service path: lb_loopback | address-entry mode << 1 */
@@ -3890,6 +3954,19 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
 		}
 		uint32_t g = ct_group(sa, da);
+		if constexpr (!SVC) {
+			/* phase 1 by connection: only the ICMP entries of creates
+			 * (owed) and the ICMP packets (phase 2) share an address pair's
+			 * keys across connections */
+			if (!(meta & CTM_GATED)) {
+				if (pr == 1u) {
+					meta |= CTM_PHASE2;
+				} else {
+					meta |= CTM_RELX;
+					g = ct_conn_group(g, z, pr);
+				}
+			}
+		}
 		if constexpr (SVC) {
 			if (!SERIAL && !(meta & CTM_GATED)) {
 				/* pairs an address entry can land in: {T, T}, {IPV4_LOOPBACK,
@@ -3920,32 +3997,47 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 	}
 }
 
-/* phase 2 of the service path: candidate 2i = packet i if it runs in phase
- * 2, 2i + 1 = packet i's owed address entry (kept whatever phase 1 decided:
- * the walk checks CT_ADDRP) */
-__global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint8_t *f2)
+/* phase 2: candidate 2i = packet i if it runs in phase 2, 2i + 1 = packet
+ * i's owed entry.  Service path: the address entry of every packet that may
+ * owe one (kept whatever phase 1 decided: the walk checks CT_ADDRP); plain
+ * path: the ICMP entry of every create phase 1 owed (CT_ADDRP). */
+template <class K> __global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint8_t *f2)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
 	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t meta = a.rec[3u * i].w >> 16;
+		const uint32_t meta = ct_rec<K>::load(a.rec, (uint32_t)i, true).meta();
 		const bool live = !(meta & CTM_GATED);
 		f2[2u * i] = live && (meta & CTM_PHASE2) ? 1u : 0u;
-		f2[2u * i + 1u] = live && (meta & CTM_ADDRX) ? 1u : 0u;
+		bool owes;
+		if constexpr (K::ADDR)
+			owes = meta & CTM_ADDRX;
+		else
+			owes = (meta & CTM_RELX) && (a.ct_ret[i] & CT_ADDRP);
+		f2[2u * i + 1u] = live && owes ? 1u : 0u;
 	}
 }
 
 /* group key of each selected candidate: the address pair (packet: its own,
  * owed entry: the entry's), or, when no packet runs in phase 2, the owed
  * entry's whole key (blind BPF_ANY writes of different keys commute) */
-__global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args a, uint32_t m, uint32_t by_key)
+template <class K> __global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args a, uint32_t m, uint32_t by_key)
 {
 	for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) {
 		const uint32_t v = a.idx[j], i = v >> 1;
-		const ct_rec<CtK4S> r = ct_rec<CtK4S>::load(a.rec, i, false);
-		uint4 k = r.key();
-		if (v & 1u)
-			k = ct_addr_key(CtK4::reversed(k), r.pkt());
-		a.gkey[j] = by_key ? ct_hash(k.x, k.y, k.z, k.w) : ct_group(k.x, k.y);
+		const ct_rec<K> r = ct_rec<K>::load(a.rec, i, false);
+		if constexpr (K::ADDR) {
+			uint4 k = r.key();
+			if (v & 1u)
+				k = ct_addr_key(CtK4::reversed(k), r.pkt());
+			a.gkey[j] = by_key ? ct_hash(k.x, k.y, k.z, k.w) : ct_group(k.x, k.y);
+		} else if constexpr (K::V6 != 0) {
+			/* an ICMP entry carries its packet's pair */
+			const typename K::key k = r.key();
+			a.gkey[j] = ct_group(fold6(k.d.x, k.d.y, k.d.z, k.d.w), fold6(k.s.x, k.s.y, k.s.z, k.s.w));
+		} else {
+			const uint4 k = r.key();
+			a.gkey[j] = ct_group(k.x, k.y);
+		}
 	}
 }
 
@@ -4055,14 +4147,24 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 				sec = d.id;
 			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
 		}
+		uint32_t g = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
+		if constexpr (!SVC) { /* phase 1 by connection, as k_ct_prep */
+			if (!(meta & CTM_GATED)) {
+				if (pr == 58u) {
+					meta |= CTM_PHASE2;
+				} else {
+					meta |= CTM_RELX;
+					g = ct_conn_group(g, z, pr);
+				}
+			}
+		}
 		a.identity[i] = id;
 		uint4 *r = a.rec + 4u * i;
 		r[0] = da;
 		r[1] = sa;
 		r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (port << 16), len};
 		r[3] = uint4{sec, cst, rev, svcw};
-		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u)
-					       : ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
+		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
 		a.idx[i] = (uint32_t)i;
 	}
 }
@@ -4515,6 +4617,14 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 		}
 	}
 	e.c.y |= CTB_SEEN_NON_SYN;
+	if (meta & CTM_RELX) {
+		/* the ICMP entry lies in the address pair's phase-2 group: reserve
+		 * its capacity now (where the reference's update would fail), write
+		 * it in phase 2 in batch order */
+		if (!ct_take(T, A))
+			return CT_NEW | CT_FAIL;
+		return CT_NEW | CT_ADDRP;
+	}
 	if (!ctc_update<K>(T, A, c, K::related(k), e))
 		return CT_NEW | CT_FAIL | owed;
 	return CT_NEW | owed;
@@ -4903,16 +5013,23 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 				const ct_pkt q = r.pkt();
 				if constexpr (MODE == WALK_OWED) {
 					if (v & 1u) {
-						/* the owed address entry of packet i's create */
+						/* the owed address entry (service path) / ICMP
+						 * entry (plain path) of packet i's create */
 						if (a.ct_ret[i] & CT_ADDRP) {
 							const typename K::key fk = K::reversed(r.key());
-							ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
-									   ct_new_row<K>(q, false, a.now));
+							if constexpr (K::ADDR) {
+								ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
+										   ct_new_row<K>(q, false, a.now));
+							} else {
+								ct_row e = ct_new_row<K>(q, !(q.meta & CTM_EGRESS), a.now);
+								e.c.y |= CTB_SEEN_NON_SYN;
+								ctc_update_owed<K>(T, A, c, K::related(fk), e);
+							}
 						}
 						continue;
 					}
 				}
-				if (MODE == WALK_PKT && K::SVC && (meta & CTM_PHASE2))
+				if (MODE == WALK_PKT && (meta & CTM_PHASE2))
 					continue;
 				a.ct_ret[i] = (uint8_t)ct_step<K>(T, A, c, r.key(), q, a.now);
 			}
@@ -5141,6 +5258,26 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	/* phase 2: the ICMP packets and the owed ICMP entries of the creates,
+	 * grouped by address pair, in batch order */
+	hipLaunchKernelGGL(k_ct_owed_flags<K>, dim3(g), dim3(256), 0, st, a, L.flags2);
+	hipcub::CountingInputIterator<uint32_t> it(0);
+	size_t tb = L.temp_bytes;
+	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.flags2, L.idx, L.n_heads, (int)(2 * L.n), st);
+	if (e != hipSuccess)
+		return e;
+	uint32_t m = 0;
+	e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+		return e;
+	if (m) {
+		const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
+		hipLaunchKernelGGL(k_ct_owed_keys<K>, dim3(gm), dim3(256), 0, st, a, m, 0u);
+		e = ct_group_sort(s, L, a, m, &nh, st);
+		if (e != hipSuccess)
+			return e;
+		hipLaunchKernelGGL((k_ct_walk<K, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	}
 	launch_ct_finish<K>(s, a, st);
 	return hipGetLastError();
 }
@@ -5225,7 +5362,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if (!serial && (ctl[1] || ctl[2])) {
 		const unsigned g2 = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
-		hipLaunchKernelGGL(k_ct_owed_flags, dim3(g2), dim3(256), 0, st, a, L.flags2);
+		hipLaunchKernelGGL(k_ct_owed_flags<CtK4S>, dim3(g2), dim3(256), 0, st, a, L.flags2);
 		hipcub::CountingInputIterator<uint32_t> it(0);
 		size_t tb = L.temp_bytes;
 		e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.flags2, L.idx, L.n_heads, (int)(2 * L.n), st);
@@ -5237,7 +5374,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 			return e;
 		if (m) {
 			const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
-			hipLaunchKernelGGL(k_ct_owed_keys, dim3(gm), dim3(256), 0, st, a, m, ctl[1] ? 0u : 1u);
+			hipLaunchKernelGGL(k_ct_owed_keys<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, ctl[1] ? 0u : 1u);
 			e = ct_group_sort(s, L, a, m, &nh, st);
 			if (e != hipSuccess)
 				return e;

@@ -526,6 +526,18 @@ CT_HD uint32_t ct_group(uint32_t a, uint32_t b)
 	return ct_fmix(ct_fmix(lo ^ 0x2545f491u) ^ hi);
 }
 
+/* the phase-1 conntrack group of a TCP / UDP packet on the plain path: its
+ * connection (unordered address pair, unordered ports, protocol).  Every
+ * key its ct_lookup / ct_create / ct_delete touch but the ICMP entry of
+ * ct_create carries the connection; that entry is owed to phase 2, which
+ * groups by address pair.  z = sport | dport << 16 of either direction. */
+CT_HD uint32_t ct_conn_group(uint32_t pair_group, uint32_t z, uint32_t proto)
+{
+	const uint32_t a = z & 0xFFFFu, b = z >> 16;
+	const uint32_t ports = a < b ? (a | b << 16) : (b | a << 16);
+	return ct_fmix(pair_group ^ ct_fmix(ports ^ (proto << 24) ^ 0x68e31da4u));
+}
+
 /* Table verification sum (SURVEY §5 failure detection): over the 8-byte
  * words of every part of an uploaded group buffer, sum of word x an odd
  * multiplier that depends on the word's index in the buffer (a changed word
