@@ -3739,6 +3739,7 @@ struct ct_args {
 	uint32_t *xdaddr;            /* [n] optional: frame daddr after the service step */
 	uint16_t *xdport;            /* [n] optional: frame dport after it */
 	uint32_t serial;             /* one group for the whole batch (see launch_ctlb) */
+	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
 };
 
 /* One packet's record, written by k_ct_prep{,6} and read by the walker and
@@ -3955,17 +3956,23 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 		}
 		uint32_t g = ct_group(sa, da);
 		if constexpr (!SVC) {
-			/* phase 1 by connection: only the ICMP entries of creates
-			 * (owed) and the ICMP packets (phase 2) share an address pair's
-			 * keys across connections */
+			/* phase 1 by connection (TCP / UDP ports, ICMP echo ids): only
+			 * the ICMP entries of creates (owed) and the ICMP errors that
+			 * read them (phase 2) share an address pair's keys across
+			 * connections */
+			bool p2 = false;
 			if (!(meta & CTM_GATED)) {
-				if (pr == 1u) {
+				if (pr == 1u && (tfl & TUPLE_F_RELATED)) {
 					meta |= CTM_PHASE2;
+					p2 = true;
 				} else {
 					meta |= CTM_RELX;
 					g = ct_conn_group(g, z, pr);
 				}
 			}
+			/* phase-2 candidates 2i (the packet) and 2i + 1 (its owed ICMP
+			 * entry, set by the walker) */
+			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
 		}
 		if constexpr (SVC) {
 			if (!SERIAL && !(meta & CTM_GATED)) {
@@ -3997,23 +4004,18 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 	}
 }
 
-/* phase 2: candidate 2i = packet i if it runs in phase 2, 2i + 1 = packet
- * i's owed entry.  Service path: the address entry of every packet that may
- * owe one (kept whatever phase 1 decided: the walk checks CT_ADDRP); plain
- * path: the ICMP entry of every create phase 1 owed (CT_ADDRP). */
-template <class K> __global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint8_t *f2)
+/* phase 2 of the service path: candidate 2i = packet i if it runs in phase
+ * 2, 2i + 1 = packet i's owed address entry (kept whatever phase 1 decided:
+ * the walk checks CT_ADDRP).  The plain path's flags come from its prep and
+ * walk (ct_args.f2). */
+__global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint8_t *f2)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
 	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t meta = ct_rec<K>::load(a.rec, (uint32_t)i, true).meta();
+		const uint32_t meta = a.rec[3u * i].w >> 16;
 		const bool live = !(meta & CTM_GATED);
 		f2[2u * i] = live && (meta & CTM_PHASE2) ? 1u : 0u;
-		bool owes;
-		if constexpr (K::ADDR)
-			owes = meta & CTM_ADDRX;
-		else
-			owes = (meta & CTM_RELX) && (a.ct_ret[i] & CT_ADDRP);
-		f2[2u * i + 1u] = live && owes ? 1u : 0u;
+		f2[2u * i + 1u] = live && (meta & CTM_ADDRX) ? 1u : 0u;
 	}
 }
 
@@ -4149,14 +4151,17 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 		}
 		uint32_t g = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
 		if constexpr (!SVC) { /* phase 1 by connection, as k_ct_prep */
+			bool p2 = false;
 			if (!(meta & CTM_GATED)) {
-				if (pr == 58u) {
+				if (pr == 58u && (tfl & TUPLE_F_RELATED)) {
 					meta |= CTM_PHASE2;
+					p2 = true;
 				} else {
 					meta |= CTM_RELX;
 					g = ct_conn_group(g, z, pr);
 				}
 			}
+			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
 		}
 		a.identity[i] = id;
 		uint4 *r = a.rec + 4u * i;
@@ -5031,7 +5036,10 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 				}
 				if (MODE == WALK_PKT && (meta & CTM_PHASE2))
 					continue;
-				a.ct_ret[i] = (uint8_t)ct_step<K>(T, A, c, r.key(), q, a.now);
+				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now);
+				a.ct_ret[i] = (uint8_t)ret;
+				if (!K::ADDR && MODE == WALK_PKT && (ret & CT_ADDRP))
+					a.f2[2u * i + 1u] = 1u; /* its ICMP entry is owed to phase 2 */
 			}
 		}
 		ctc_flush(T, c);
@@ -5164,17 +5172,123 @@ static int ct_sort_bits(const cgpu_snapshot &s)
 	return b ? std::max(8, std::min(32, b)) : 24;
 }
 
-/* hipcub temporary storage for the sort and the head selection of n packets
- * (and the selection of the 2n phase-2 candidates of the service path) */
+/* Ordered stream compaction of byte flags (the group heads, the phase-2
+ * candidates): the indices of the set flags, in index order.  Three small
+ * launches, count per 4096-flag block -> one-block scan of the counts ->
+ * emit, read the flags twice at streaming rate; hipcub's DeviceSelect over
+ * a counting iterator took 0.77 ms per 64M flags and 1.43 ms per 128M
+ * (profiles/r3_ct). */
+#define SEL_T 16u            /* flags per thread: one 16-byte load */
+#define SEL_B (256u * SEL_T) /* flags per block */
+
+__device__ __forceinline__ uint32_t sel_bits(const uint8_t *f, uint64_t n, uint64_t i0)
+{
+	uint32_t bits = 0;
+	if (i0 + SEL_T <= n) {
+		const uint4 v = *reinterpret_cast<const uint4 *>(f + i0);
+		const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+		for (int k = 0; k < 4; k++)
+#pragma unroll
+			for (int b = 0; b < 4; b++)
+				bits |= ((w[k] >> (8 * b)) & 0xFFu) ? 1u << (4 * k + b) : 0u;
+	} else {
+		for (uint32_t j = 0; j < SEL_T; j++)
+			bits |= (i0 + j < n && f[i0 + j]) ? 1u << j : 0u;
+	}
+	return bits;
+}
+
+__global__ __launch_bounds__(256) void k_sel_count(const uint8_t *f, uint64_t n, uint32_t *bc)
+{
+	__shared__ uint32_t ws[4];
+	const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * SEL_T;
+	const uint32_t c = wave_sum((uint32_t)__popc(sel_bits(f, n, i0)));
+	if ((threadIdx.x & 63u) == 0)
+		ws[threadIdx.x >> 6] = c;
+	__syncthreads();
+	if (threadIdx.x == 0)
+		bc[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+/* one workgroup: exclusive scan of the nb block counts in place, the total
+ * to *count */
+__global__ __launch_bounds__(1024) void k_sel_scan(uint32_t *bc, uint32_t nb, uint32_t *count)
+{
+	__shared__ uint32_t sc[1024];
+	uint32_t carry = 0;
+	for (uint32_t base = 0; base < nb; base += 1024u) {
+		const uint32_t k = base + threadIdx.x;
+		const uint32_t v = k < nb ? bc[k] : 0u;
+		sc[threadIdx.x] = v;
+		__syncthreads();
+		for (uint32_t o = 1; o < 1024u; o <<= 1) {
+			const uint32_t t = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
+			__syncthreads();
+			sc[threadIdx.x] += t;
+			__syncthreads();
+		}
+		if (k < nb)
+			bc[k] = carry + sc[threadIdx.x] - v;
+		carry += sc[1023];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0)
+		*count = carry;
+}
+
+__global__ __launch_bounds__(256) void k_sel_emit(const uint8_t *f, uint64_t n, const uint32_t *bc, uint32_t *out)
+{
+	__shared__ uint32_t ws[4];
+	const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+	const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * SEL_T;
+	uint32_t bits = sel_bits(f, n, i0);
+	const uint32_t c = (uint32_t)__popc(bits);
+	uint32_t x = c; /* inclusive scan over the wave */
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+		x += lane >= (uint32_t)o ? y : 0u;
+	}
+	if (lane == 63u)
+		ws[wv] = x;
+	__syncthreads();
+	uint32_t pos = bc[blockIdx.x] + x - c;
+	for (uint32_t w = 0; w < wv; w++)
+		pos += ws[w];
+	while (bits) {
+		const uint32_t j = (uint32_t)__ffs(bits) - 1u;
+		bits &= bits - 1u;
+		out[pos++] = (uint32_t)(i0 + j);
+	}
+}
+
+static uint64_t sel_blocks(uint64_t n)
+{
+	return (n + SEL_B - 1) / SEL_B;
+}
+
+/* out[0, *count) = the indices i < n with f[i] != 0, ascending; bc = nb
+ * words of scratch */
+static hipError_t ct_select(const uint8_t *f, uint64_t n, uint32_t *out, uint32_t *count, uint32_t *bc,
+			    hipStream_t st)
+{
+	const uint64_t nb = sel_blocks(n);
+	if (!nb)
+		return hipMemsetAsync(count, 0, 4, st);
+	hipLaunchKernelGGL(k_sel_count, dim3((unsigned)nb), dim3(256), 0, st, f, n, bc);
+	hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, bc, (uint32_t)nb, count);
+	hipLaunchKernelGGL(k_sel_emit, dim3((unsigned)nb), dim3(256), 0, st, f, n, bc, out);
+	return hipGetLastError();
+}
+
+/* scratch for the sort of n packets (hipcub) and for the block counts of the
+ * selections (the 2n phase-2 candidates of the service path at most) */
 size_t ct_temp_bytes(uint64_t n)
 {
-	size_t a = 0, b = 0;
+	size_t a = 0;
 	(void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
 						 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
-	hipcub::CountingInputIterator<uint32_t> it(0);
-	(void)hipcub::DeviceSelect::Flagged(nullptr, b, it, (const uint8_t *)nullptr, (uint32_t *)nullptr,
-					    (uint32_t *)nullptr, (int)std::min<uint64_t>(2 * n, INT32_MAX));
-	return std::max(a, b);
+	return std::max<size_t>(a, sel_blocks(2 * n) * 4u + 4u);
 }
 
 static ct_args ct_args_of(const ct_launch &L)
@@ -5189,6 +5303,7 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.ctl = L.ctl;
 	a.xdaddr = static_cast<uint32_t *>(L.xdaddr);
 	a.xdport = L.xdport;
+	a.f2 = L.flags2;
 	return a;
 }
 
@@ -5208,9 +5323,7 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 		return e;
 	const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
 	hipLaunchKernelGGL(k_ct_heads, dim3(g), dim3(256), 0, st, L.gkey_sorted, L.head, m, mask);
-	hipcub::CountingInputIterator<uint32_t> it(0);
-	tb = L.temp_bytes;
-	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.head, L.heads, L.n_heads, (int)m, st);
+	e = ct_select(L.head, m, L.heads, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 	if (e != hipSuccess)
 		return e;
 	/* groups longest first: gkey / idx are free again and hold (length,
@@ -5258,12 +5371,10 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
-	/* phase 2: the ICMP packets and the owed ICMP entries of the creates,
-	 * grouped by address pair, in batch order */
-	hipLaunchKernelGGL(k_ct_owed_flags<K>, dim3(g), dim3(256), 0, st, a, L.flags2);
-	hipcub::CountingInputIterator<uint32_t> it(0);
-	size_t tb = L.temp_bytes;
-	e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.flags2, L.idx, L.n_heads, (int)(2 * L.n), st);
+	/* phase 2: the ICMP errors and the owed ICMP entries of the creates,
+	 * grouped by address pair, in batch order (the prep and the walk set
+	 * the candidate flags) */
+	e = ct_select(L.flags2, 2 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 	if (e != hipSuccess)
 		return e;
 	uint32_t m = 0;
@@ -5362,10 +5473,8 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if (!serial && (ctl[1] || ctl[2])) {
 		const unsigned g2 = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
-		hipLaunchKernelGGL(k_ct_owed_flags<CtK4S>, dim3(g2), dim3(256), 0, st, a, L.flags2);
-		hipcub::CountingInputIterator<uint32_t> it(0);
-		size_t tb = L.temp_bytes;
-		e = hipcub::DeviceSelect::Flagged(L.temp, tb, it, L.flags2, L.idx, L.n_heads, (int)(2 * L.n), st);
+		hipLaunchKernelGGL(k_ct_owed_flags, dim3(g2), dim3(256), 0, st, a, L.flags2);
+		e = ct_select(L.flags2, 2 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 		if (e != hipSuccess)
 			return e;
 		uint32_t m = 0;
