@@ -4206,7 +4206,10 @@ CGPU_EXPORT int cgpu_classify_v6(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n,
 	/* the x4 schedule's ipcache pre-pass: n entries of stream-ordered pool
 	 * scratch */
 	void *scr = nullptr;
-	if (s.ipc6.root && !(s.schedule & (CGPU_SCHED_PER_LANE | CGPU_SCHED_GLOBAL_CTR)))
+	/* (the pre-pass folds the egress fallback identity into a DIRECT entry
+	 * of cluster_id: its payload must hold it) */
+	if (s.ipc6.root && !(s.schedule & (CGPU_SCHED_PER_LANE | CGPU_SCHED_GLOBAL_CTR)) &&
+	    s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK)
 		HIP_OR_EIO(hipMallocFromPoolAsync(&scr, (size_t)n * 4u, c->pool, (hipStream_t)stream));
 	a.ipc_e = static_cast<uint32_t *>(scr);
 	const hipError_t le = launch_classify_v6(s, a, (hipStream_t)stream);

@@ -971,6 +971,122 @@ __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, 
 	return d;
 }
 
+/* The policy cascade of decide<> (probe 1 {id, dport, proto, dir} unless a
+ * fragment, probe 2 {id, any port, dir}, probe 3 {any identity, dport,
+ * proto, dir} unless a fragment) for Q tuples whose identity d[u].id is
+ * set, each probe's Q gathers issued together. */
+template <int Q>
+__device__ __forceinline__ void policy_q(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&eg)[Q],
+					 const bool (&frag)[Q], const uint32_t (&dport)[Q], const uint32_t (&proto)[Q],
+					 const uint32_t (&ep)[Q], decision (&d)[Q])
+{
+	uint32_t hi4[Q], egw[Q], z[Q];
+	int ctr[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		egw[u] = eg[u] ? (1u << 24) : 0u;
+		hi4[u] = dport[u] | (proto[u] << 16) | egw[u];
+		z[u] = 0;
+		ctr[u] = -1;
+		d[u].st = 0;
+	}
+	/* probe 1: {id, dport, proto, dir} (not for fragments) */
+	uint32_t b[Q];
+	uint4 sl[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		b[u] = pol_hash(d[u].id, hi4[u], ep[u]) & s.pol.bucket_mask;
+		sl[u] = (act[u] && !frag[u]) ? reinterpret_cast<const uint4 *>(s.pol.slots)[b[u]] : make_uint4(0, 0, 0, 0);
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		if (act[u] && !frag[u]) {
+			ctr[u] = pol_resolve1(s.pol, sl[u], b[u], d[u].id, hi4[u], ep[u], &z[u]);
+			d[u].st = 1;
+		}
+	/* probe 2: {id, any port, dir} */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		b[u] = pol_hash(d[u].id, egw[u], ep[u]) & s.pol.bucket_mask;
+		sl[u] = (act[u] && ctr[u] < 0) ? reinterpret_cast<const uint4 *>(s.pol.slots)[b[u]] : make_uint4(0, 0, 0, 0);
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		if (act[u] && ctr[u] < 0) {
+			ctr[u] = pol_resolve1(s.pol, sl[u], b[u], d[u].id, egw[u], ep[u], &z[u]);
+			d[u].st = 2;
+		}
+	/* probe 3: {any identity, dport, proto, dir} (not for fragments) */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		b[u] = pol_hash(0u, hi4[u], ep[u]) & s.pol.bucket_mask;
+		sl[u] = (act[u] && ctr[u] < 0 && !frag[u]) ? reinterpret_cast<const uint4 *>(s.pol.slots)[b[u]]
+							   : make_uint4(0, 0, 0, 0);
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (act[u] && ctr[u] < 0 && !frag[u]) {
+			ctr[u] = pol_resolve1(s.pol, sl[u], b[u], 0u, hi4[u], ep[u], &z[u]);
+			d[u].st = 3;
+		}
+		if (ctr[u] >= 0) {
+			d[u].v = d[u].st == 2 ? 0 : (int32_t)(z[u] >> 16);
+		} else {
+			d[u].st = 0;
+			d[u].v = DROP_POLICY;
+		}
+		d[u].ctr = ctr[u];
+	}
+}
+
+/* decide<0> for Q tuples of one lane, stage by stage: each stage (the /16
+ * run node, the leaf, policy probe 1, 2, 3) issues the Q tuples' gathers
+ * together, so a wave has Q x 64 independent loads in flight where decide
+ * has 64.  Same results as decide<0> tuple by tuple (the stateful path's
+ * prep and finish passes; the dictionary is read from global memory). */
+template <int Q>
+__device__ __forceinline__ void decide4_q(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&eg)[Q],
+					  const bool (&frag)[Q], const uint32_t (&sa)[Q], const uint32_t (&da)[Q],
+					  const uint32_t (&dport)[Q], const uint32_t (&proto)[Q],
+					  const uint32_t (&ep)[Q], decision (&d)[Q])
+{
+	const lpm16c &t = s.ipc4c;
+	uint32_t h[Q], e[Q];
+	uint4 q[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		h[u] = bswap32(eg[u] ? da[u] : sa[u]);
+		q[u] = act[u] ? reinterpret_cast<const uint4 *>(t.x16)[h[u] >> 16] : make_uint4(0, 0, 0, 0);
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (!(q[u].w & LPMC_OVERFLOW)) {
+			const uint32_t x = h[u] & 0xFFFFu;
+			const uint32_t cnt = (x >= (q[u].x & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].x >> 16) ? 1u : 0u) +
+					     (x >= (q[u].y & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].y >> 16) ? 1u : 0u);
+			const uint64_t v = ((uint64_t)q[u].w << 32) | q[u].z;
+			e[u] = act[u] ? t.dict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
+		} else {
+			e[u] = lpmc_lookup(t, t.dict, eg[u] ? da[u] : sa[u]);
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		const uint32_t label = entry_label(t.vals, e[u]);
+		const uint32_t ad = eg[u] ? da[u] : sa[u];
+		const bool in_cluster = (ad & s.ipv4_cluster_mask) == s.ipv4_cluster_range;
+		if (eg[u]) {
+			d[u].id = (e[u] && label) ? label : (in_cluster ? s.cluster_id : s.world_id);
+		} else {
+			uint32_t src = s.ingress_src_identity;
+			if (src < s.health_id && e[u] && label && label != s.cluster_id && label != s.host_id)
+				src = label;
+			d[u].id = s.ingress_secctx_world ? s.world_id : src;
+		}
+	}
+	policy_q<Q>(s, act, eg, frag, dport, proto, ep, d);
+}
+
 /* Packed per-workgroup counter: packets in bits 41..63, bytes in 0..40.
  * Exact while a workgroup adds < 2^23 hits of < 2^18 bytes to one slot
  * (the launcher bounds tuples per workgroup; longer packets take the
@@ -2729,9 +2845,23 @@ __global__ __launch_bounds__(NT) void k_ipc6_pre(cgpu_snapshot s, const uint4 *s
 		}
 		v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w, act, e);
 #pragma unroll
-		for (int u = 0; u < Q; u++)
-			if (act[u])
-				e_out[g + (uint64_t)u * T] = e[u];
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			if (!act[u])
+				continue;
+			/* the classify kernel reads no address: an egress tuple's
+			 * fallback identity (no match or a label-0 match) is folded in
+			 * here, as a DIRECT entry of cluster_id when the address lies in
+			 * ROUTER_IP's /64 (ipv6_match_prefix_64, bpf/lib/ipv6.h:166-175;
+			 * bpf_lxc.c:170-187), else no match (WORLD_ID) */
+			uint32_t ev = e[u];
+			if ((flags[i] & 1u) && !(ev && entry_label(s.ipc6.vals, ev))) {
+				const bool in_cluster = w[u].x == bswap32(s.router_ip64[0]) &&
+							w[u].y == bswap32(s.router_ip64[1]);
+				ev = in_cluster ? (DIR_TAG_DIRECT | s.cluster_id) : 0u;
+			}
+			e_out[i] = ev;
+		}
 	}
 }
 
@@ -4004,6 +4134,201 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 	}
 }
 
+/* k_ct_prep<false, false> (the plain IPv4 path) with Q packets per lane:
+ * the forward decisions through decide4_q; packet i = g + u * (threads),
+ * so every column load of a wave covers 64 consecutive packets */
+template <int Q>
+__global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
+{
+	const uint64_t T = (uint64_t)gridDim.x * 256u;
+	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+		bool act[Q], dec[Q], eg[Q], frag[Q];
+		uint32_t sa[Q], da[Q], fdp[Q], pr[Q], ep[Q], meta[Q], tfl[Q], z[Q], w[Q], len[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = i < a.n;
+			const uint64_t j = act[u] ? i : 0u;
+			const uint32_t fl = a.flags[j];
+			pr[u] = a.proto[j];
+			len[u] = a.len[j];
+			sa[u] = a.saddr[j];
+			da[u] = a.daddr[j];
+			ep[u] = a.ep[j];
+			w[u] = a.l4[j];
+			const uint32_t dp = a.dport[j], sp = a.sport[j];
+			eg[u] = fl & 1u;
+			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
+			meta[u] = eg[u] ? CTM_EGRESS : 0u;
+			z[u] = 0;
+			if (pr[u] == 1u) { /* as k_ct_prep */
+				const uint32_t type = w[u] & 0xFFu;
+				if (type == 3u || type == 11u || type == 12u)
+					tfl[u] |= TUPLE_F_RELATED;
+				else if (type == 0u)
+					z[u] = 8u;
+				else {
+					if (type == 8u)
+						z[u] = 8u << 16;
+					meta[u] |= CTM_ACT_CREATE;
+				}
+			} else if (pr[u] == 6u || pr[u] == 17u) {
+				z[u] = sp | (dp << 16);
+				meta[u] |= pr[u] == 6u ? (CTM_TCP | ((w[u] & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE))
+						       : CTM_ACT_CREATE;
+			} else {
+				meta[u] |= CTM_GATED;
+			}
+			if (pr[u] != 6u)
+				w[u] = 0;
+			frag[u] = !eg[u] && ((fl >> 1) & 1u);
+			if (frag[u] && !(meta[u] & CTM_GATED))
+				meta[u] |= CTM_FRAG;
+			dec[u] = act[u] && !(meta[u] & CTM_GATED);
+			fdp[u] = z[u] >> 16;
+		}
+		decision d[Q];
+		decide4_q<Q>(s, dec, eg, frag, sa, da, fdp, pr, ep, d);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (!act[u])
+				continue;
+			const uint64_t i = g + (uint64_t)u * T;
+			uint32_t sec = 0, port = 0, cst = 0, id = 0, m = meta[u];
+			if (dec[u]) {
+				if (d[u].v >= 0) {
+					m |= CTM_ALLOWED;
+					port = (uint32_t)d[u].v;
+				}
+				id = d[u].id;
+				sec = eg[u] ? (ep[u] < s.n_lxc ? s.lxc[2u * ep[u] + 1u].w : 0u) : d[u].id;
+				cst = (uint32_t)(d[u].ctr + 1) | (d[u].st << 24);
+			}
+			uint32_t gk = ct_group(sa[u], da[u]);
+			bool p2 = false;
+			if (dec[u]) {
+				if (pr[u] == 1u && (tfl[u] & TUPLE_F_RELATED)) {
+					m |= CTM_PHASE2;
+					p2 = true;
+				} else {
+					m |= CTM_RELX;
+					gk = ct_conn_group(gk, z[u], pr[u]);
+				}
+			}
+			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
+			a.identity[i] = id;
+			uint4 *r = a.rec + 2u * i;
+			r[0] = uint4{da[u], sa[u], z[u], pr[u] | (tfl[u] << 8) | (m << 16)};
+			r[1] = uint4{w[u] | (port << 16), len[u], sec, cst};
+			a.gkey[i] = (m & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
+			a.idx[i] = (uint32_t)i;
+		}
+	}
+}
+
+/* k_ct_prep6<false> (the plain IPv6 path) with Q packets per lane, the
+ * ipcache entries from the pre-pass (k_ipc6_pre, egress fallback folded in)
+ * and the policy cascades through policy_q */
+template <int Q>
+__global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, const uint32_t *ipc_e)
+{
+	const uint64_t T = (uint64_t)gridDim.x * 256u;
+	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr);
+	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr);
+	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+		bool act[Q], dec[Q], eg[Q], frag[Q];
+		uint32_t fdp[Q], pr[Q], ep[Q], meta[Q], tfl[Q], z[Q], w[Q], len[Q];
+		decision d[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = i < a.n;
+			const uint64_t j = act[u] ? i : 0u;
+			const uint32_t fl = a.flags[j], dp = a.dport[j], sp = a.sport[j];
+			pr[u] = a.proto[j];
+			len[u] = a.len[j];
+			ep[u] = a.ep[j];
+			w[u] = a.l4[j];
+			eg[u] = fl & 1u;
+			frag[u] = false; /* no fragment flag on IPv6 (bpf_lxc.c:787-789) */
+			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
+			meta[u] = eg[u] ? CTM_EGRESS : 0u;
+			z[u] = 0;
+			if (pr[u] == 58u) { /* as k_ct_prep6 */
+				const uint32_t type = w[u] & 0xFFu;
+				if (type >= 1u && type <= 4u)
+					tfl[u] |= TUPLE_F_RELATED;
+				else if (type == 129u)
+					z[u] = 128u;
+				else {
+					if (type == 128u)
+						z[u] = 128u << 16;
+					meta[u] |= CTM_ACT_CREATE;
+				}
+			} else if (pr[u] == 6u || pr[u] == 17u) {
+				z[u] = sp | (dp << 16);
+				meta[u] |= pr[u] == 6u ? (CTM_TCP | ((w[u] & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE))
+						       : CTM_ACT_CREATE;
+			} else {
+				meta[u] |= CTM_GATED;
+			}
+			if (pr[u] != 6u)
+				w[u] = 0;
+			dec[u] = act[u] && !(meta[u] & CTM_GATED);
+			fdp[u] = z[u] >> 16;
+			/* decide<1>'s identity from the pre-pass entry */
+			const uint32_t e = ipc_e[j];
+			const uint32_t label = entry_label(s.ipc6.vals, e);
+			if (eg[u]) {
+				d[u].id = (e && label) ? label : s.world_id; /* cluster fallback folded into e */
+			} else {
+				uint32_t src = s.ingress_src_identity;
+				if (src < s.health_id && e && label && label != s.cluster_id)
+					src = label;
+				d[u].id = src;
+			}
+		}
+		policy_q<Q>(s, dec, eg, frag, fdp, pr, ep, d);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (!act[u])
+				continue;
+			const uint64_t i = g + (uint64_t)u * T;
+			const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
+			uint32_t sec = 0, port = 0, cst = 0, id = 0, m = meta[u];
+			if (dec[u]) {
+				if (d[u].v >= 0) {
+					m |= CTM_ALLOWED;
+					port = (uint32_t)d[u].v;
+				}
+				id = d[u].id;
+				sec = eg[u] ? (ep[u] < s.n_lxc ? s.lxc[2u * ep[u] + 1u].w : 0u) : d[u].id;
+				cst = (uint32_t)(d[u].ctr + 1) | (d[u].st << 24);
+			}
+			uint32_t gk = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
+			bool p2 = false;
+			if (dec[u]) {
+				if (pr[u] == 58u && (tfl[u] & TUPLE_F_RELATED)) {
+					m |= CTM_PHASE2;
+					p2 = true;
+				} else {
+					m |= CTM_RELX;
+					gk = ct_conn_group(gk, z[u], pr[u]);
+				}
+			}
+			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
+			a.identity[i] = id;
+			uint4 *r = a.rec + 4u * i;
+			r[0] = da;
+			r[1] = sa;
+			r[2] = uint4{z[u], pr[u] | (tfl[u] << 8) | (m << 16), w[u] | (port << 16), len[u]};
+			r[3] = uint4{sec, cst, eg[u] ? 0u : (da.w & 0xFFFFu), 0u};
+			a.gkey[i] = (m & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
+			a.idx[i] = (uint32_t)i;
+		}
+	}
+}
+
 /* phase 2 of the service path: candidate 2i = packet i if it runs in phase
  * 2, 2i + 1 = packet i's owed address entry (kept whatever phase 1 decided:
  * the walk checks CT_ADDRP).  The plain path's flags come from its prep and
@@ -5074,7 +5399,7 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
  * CT_NEW / CT_ESTABLISHED packets reuse the prep's forward decision; only
  * CT_REPLY / CT_RELATED ones run the cascade again, on the reply tuple.
  * Hot counter slots accumulate in LDS (packed, as k_classify CTR = 1). */
-template <int NT, class K> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a)
+template <int NT, class K, int Q> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* metrics {reason 0 / 133 / 137 / 155 [/ 158]} x {ingress, egress} */
@@ -5083,76 +5408,102 @@ template <int NT, class K> __global__ __launch_bounds__(NT) void k_ct_finish(cgp
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
 	__syncthreads();
-	const uint64_t stride = (uint64_t)gridDim.x * NT;
-	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) {
-		/* batch order: records and the walker's results stream in */
-		const ct_pkt q = ct_rec<K>::load(a.rec, (uint32_t)i, true).pkt();
-		const uint32_t meta = q.meta;
-		const bool egress = meta & CTM_EGRESS;
-		const uint32_t len = q.len;
-		int32_t v;
-		uint32_t st = 4, cr = 255u;
-		if (meta & CTM_GATED) {
-			v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup default case */
-			if (K::SVC && (meta & CTM_SVCDROP)) {
-				v = DROP_NO_SERVICE; /* lb4_local failed closed (lb.h:715-744) */
-				st = 6;
-			}
-		} else {
-			const uint32_t c = a.ct_ret[i] & ~CT_ADDRP;
-			cr = c & 3u;
-			int ctr;
-			if (cr >= CT_REPLY) {
-				const bool frag = meta & CTM_FRAG;
-				const decision d = decide<K::V6>(s, egress, frag, q.sa4, q.da4, q.sa6, q.da6, q.dport,
-								 q.proto, a.ep[i]);
-				ctr = d.ctr;
-				st = d.st;
-				v = (egress && d.v > 0) ? d.v : 0;
+	/* Q packets per lane (packet g + u * threads): the CT_REPLY / CT_RELATED
+	 * packets' policy cascades run stage-interleaved (policy_q) */
+	const uint64_t T = (uint64_t)gridDim.x * NT;
+	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < a.n; g += T * Q) {
+		ct_pkt q[Q];
+		uint32_t c[Q], ep[Q], dp[Q], pr[Q];
+		bool act[Q], rep[Q], eg[Q], frag[Q];
+		decision d[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = i < a.n;
+			const uint64_t j = act[u] ? i : 0u;
+			/* batch order: records and the walker's results stream in */
+			q[u] = ct_rec<K>::load(a.rec, (uint32_t)j, true).pkt();
+			c[u] = a.ct_ret[j] & ~CT_ADDRP;
+			ep[u] = a.ep[j];
+			eg[u] = q[u].meta & CTM_EGRESS;
+			frag[u] = q[u].meta & CTM_FRAG;
+			rep[u] = act[u] && !(q[u].meta & CTM_GATED) && (c[u] & 3u) >= CT_REPLY;
+			dp[u] = q[u].dport;
+			pr[u] = q[u].proto;
+			/* the reply tuple keeps the packet's addresses and direction, so
+			 * its identity is the one the prep resolved (decide<>'s identity
+			 * depends on neither port nor protocol) */
+			d[u].id = rep[u] ? a.identity[j] : 0u;
+		}
+		policy_q<Q>(s, rep, eg, frag, dp, pr, ep, d);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (!act[u])
+				continue;
+			const uint64_t i = g + (uint64_t)u * T;
+			const uint32_t meta = q[u].meta;
+			const bool egress = eg[u];
+			const uint32_t len = q[u].len;
+			int32_t v;
+			uint32_t st = 4, cr = 255u;
+			if (meta & CTM_GATED) {
+				v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup default case */
+				if (K::SVC && (meta & CTM_SVCDROP)) {
+					v = DROP_NO_SERVICE; /* lb4_local failed closed (lb.h:715-744) */
+					st = 6;
+				}
 			} else {
-				ctr = (int)(q.cst & 0xFFFFFFu) - 1;
-				st = q.cst >> 24;
-				if (!(meta & CTM_ALLOWED))
-					v = DROP_POLICY;
-				else if (c & CT_FAIL)
-					v = DROP_CT_CREATE_FAILED;
-				else
-					v = (int32_t)q.port;
-			}
-			if (ctr >= 0) {
-				const uint32_t cs = (uint32_t)ctr;
-				if (cs < s.hot_slots && len < PK_MAX_LEN) {
-					atomicAdd((unsigned long long *)&lctr[cs],
-						  (1ull << PK_SHIFT) | (unsigned long long)len);
+				cr = c[u] & 3u;
+				int ctr;
+				if (cr >= CT_REPLY) {
+					ctr = d[u].ctr;
+					st = d[u].st;
+					v = (egress && d[u].v > 0) ? d[u].v : 0;
 				} else {
-					atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
-					atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u], (unsigned long long)len);
+					ctr = (int)(q[u].cst & 0xFFFFFFu) - 1;
+					st = q[u].cst >> 24;
+					if (!(meta & CTM_ALLOWED))
+						v = DROP_POLICY;
+					else if (c[u] & CT_FAIL)
+						v = DROP_CT_CREATE_FAILED;
+					else
+						v = (int32_t)q[u].port;
+				}
+				if (ctr >= 0) {
+					const uint32_t cs = (uint32_t)ctr;
+					if (cs < s.hot_slots && len < PK_MAX_LEN) {
+						atomicAdd((unsigned long long *)&lctr[cs],
+							  (1ull << PK_SHIFT) | (unsigned long long)len);
+					} else {
+						atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
+						atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u], (unsigned long long)len);
+					}
 				}
 			}
-		}
-		a.verdict[i] = v;
-		a.ct_ret[i] = (uint8_t)cr;
-		if (a.stage)
-			a.stage[i] = (uint8_t)st;
-		/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
-		const uint32_t r = v > 0 ? 5u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : (v == DROP_NO_SERVICE ? 4u : 3u)));
-		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
+			a.verdict[i] = v;
+			a.ct_ret[i] = (uint8_t)cr;
+			if (a.stage)
+				a.stage[i] = (uint8_t)st;
+			/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
+			const uint32_t r = v > 0 ? 5u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : (v == DROP_NO_SERVICE ? 4u : 3u)));
+			const uint32_t idx = r * 2u + (egress ? 1u : 0u);
 #pragma unroll
-		for (int k = 0; k < NM; k++) {
-			mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
-			mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
+			for (int k = 0; k < NM; k++) {
+				mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
+				mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
+			}
 		}
 	}
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
 	const uint32_t reasons[5] = {0u, 133u, 137u, 155u, 158u};
 #pragma unroll
 	for (int k = 0; k < NM; k++) {
-		const uint64_t c = wave_sum(mcnt[k]);
-		const uint64_t b = wave_sum(mbyt[k]);
-		if ((threadIdx.x & 63) == 0 && c) {
+		const uint64_t cn = wave_sum(mcnt[k]);
+		const uint64_t by = wave_sum(mbyt[k]);
+		if ((threadIdx.x & 63) == 0 && cn) {
 			const uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
-			atomicAdd((unsigned long long *)&met[key], (unsigned long long)c);
-			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)b);
+			atomicAdd((unsigned long long *)&met[key], (unsigned long long)cn);
+			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)by);
 		}
 	}
 	__syncthreads();
@@ -5350,10 +5701,10 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
 	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
-	constexpr int NF = 1024;
-	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF - 1) / NF, 512), (a.n >> 22) + 1);
+	constexpr int NF = 1024, Q = 4;
+	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF * Q - 1) / (NF * Q), 512), (a.n >> 22) + 1);
 	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
-	hipLaunchKernelGGL((k_ct_finish<NF, K>), dim3((unsigned)gf), dim3(NF), (size_t)sf.hot_slots * 8u, st,
+	hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), (size_t)sf.hot_slots * 8u, st,
 			   sf, a);
 }
 
@@ -5362,10 +5713,28 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 {
 	ct_args a = ct_args_of(L);
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
-	if (K::V6)
-		hipLaunchKernelGGL(k_ct_prep6<false>, dim3(g), dim3(256), 0, st, s, a);
-	else
-		hipLaunchKernelGGL((k_ct_prep<false, false>), dim3(g), dim3(256), 0, st, s, a);
+	if (K::V6) {
+		/* the ipcache lookups through the trie pre-pass (its entries into
+		 * idx_sorted, free until the group sort) when it can fold the
+		 * egress fallback identity */
+		if (s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK) {
+			constexpr int NT = 1024, QP = CGPU_DIAG_IPC6_PRE_Q, Q = 4;
+			const size_t lds = (size_t)v6t_lds_words(s.ipc6) * 4u;
+			const unsigned res = resident_blocks((const void *)k_ipc6_pre<QP, NT>, NT, lds);
+			const unsigned gp = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + QP * NT - 1) / (QP * NT), res));
+			hipLaunchKernelGGL((k_ipc6_pre<QP, NT>), dim3(gp), dim3(NT), lds, st, s,
+					   static_cast<const uint4 *>(L.saddr), static_cast<const uint4 *>(L.daddr), L.flags,
+					   L.idx_sorted, L.n);
+			const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+			hipLaunchKernelGGL((k_ct_prep6_q<Q>), dim3(gq), dim3(256), 0, st, s, a, L.idx_sorted);
+		} else {
+			hipLaunchKernelGGL(k_ct_prep6<false>, dim3(g), dim3(256), 0, st, s, a);
+		}
+	} else {
+		constexpr int Q = 4;
+		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
+	}
 	uint32_t nh;
 	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
