@@ -3865,7 +3865,7 @@ struct ct_args {
 	/* the stateful service step (cgpu_classify_v4_ctlb) */
 	const uint32_t *hash;        /* skb->hash or NULL (cgpu_flow_hash) */
 	uint4 *svc_out;              /* [n] lb4_local's outcome per packet */
-	uint32_t *ctl;               /* [4] violation, phase-2 packets, owed entries */
+	uint32_t *ctl;               /* [4] flags: violation, phase-2 packets, owed entries */
 	uint32_t *xdaddr;            /* [n] optional: frame daddr after the service step */
 	uint16_t *xdport;            /* [n] optional: frame dport after it */
 	uint32_t serial;             /* one group for the whole batch (see launch_ctlb) */
@@ -3979,6 +3979,18 @@ template <> struct ct_rec<CtK6S> {
 			      r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
 	}
 };
+
+/* set a batch-wide flag word (0 -> 1): the launcher only asks whether any
+ * packet set it.  One plain store per wave that needs it (performed in the
+ * XCD's L2; every writer writes the same value): an atomic per packet (or
+ * per wave) on one word serialises at the memory side (~88 per us,
+ * MI355X_MICROARCH.md), 3 ms per 16M packets of the service path. */
+__device__ __forceinline__ void ct_flag(uint32_t *w)
+{
+	const uint64_t m = __ballot(1);
+	if ((int)__lane_id() == __ffsll((unsigned long long)m) - 1)
+		*w = 1u;
+}
 
 /* ct_lookup4's tuple setup, conntrack.h:461-528.  SVC (cgpu_classify_v4_ctlb):
  * egress packets first take lb4_local's outcome (svc_out, the service walk):
@@ -4112,13 +4124,13 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 				const bool p2 = sa == da || !sa || !da || sa == lo || da == lo;
 				if ((lbf >> 1) == AM_DEFER) {
 					meta |= CTM_ADDRX;
-					atomicAdd(&a.ctl[2], 1u);
+					ct_flag(&a.ctl[2]);
 					if (p2)
-						atomicOr(&a.ctl[0], 1u); /* owes into phase 2 from phase 2 */
+						ct_flag(&a.ctl[0]); /* owes into phase 2 from phase 2 */
 				}
 				if (p2) {
 					meta |= CTM_PHASE2;
-					atomicAdd(&a.ctl[1], 1u);
+					ct_flag(&a.ctl[1]);
 					g = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
 				}
 			}
@@ -5399,14 +5411,25 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
  * CT_NEW / CT_ESTABLISHED packets reuse the prep's forward decision; only
  * CT_REPLY / CT_RELATED ones run the cascade again, on the reply tuple.
  * Hot counter slots accumulate in LDS (packed, as k_classify CTR = 1). */
-template <int NT, class K, int Q> __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a)
+template <int NT, class K, int Q>
+__global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, uint32_t cc_n)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* metrics {reason 0 / 133 / 137 / 155 [/ 158]} x {ingress, egress} */
 	constexpr int NM = K::SVC ? 10 : 8;
 	uint64_t mcnt[NM] = {}, mbyt[NM] = {};
+	/* LDS: the hot counter slots, then the cold-slot cache (as k_classify_x4:
+	 * cc_n packed counts, cc_n tags = slot + 1): each touched cold slot costs
+	 * one pair of memory-side atomics per workgroup instead of one per hit */
+	uint64_t *ccv = lctr + s.hot_slots;
+	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + cc_n);
+	const uint32_t ccm = cc_n - 1u;
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
+	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
+		ccv[k] = 0;
+		cck[k] = 0;
+	}
 	__syncthreads();
 	/* Q packets per lane (packet g + u * threads): the CT_REPLY / CT_RELATED
 	 * packets' policy cascades run stage-interleaved (policy_q) */
@@ -5471,10 +5494,31 @@ template <int NT, class K, int Q> __global__ __launch_bounds__(NT) void k_ct_fin
 				}
 				if (ctr >= 0) {
 					const uint32_t cs = (uint32_t)ctr;
-					if (cs < s.hot_slots && len < PK_MAX_LEN) {
-						atomicAdd((unsigned long long *)&lctr[cs],
-							  (1ull << PK_SHIFT) | (unsigned long long)len);
-					} else {
+					bool done = false;
+					if (len < PK_MAX_LEN) {
+						if (cs < s.hot_slots) {
+							atomicAdd((unsigned long long *)&lctr[cs],
+								  (1ull << PK_SHIFT) | (unsigned long long)len);
+							done = true;
+						} else if (cc_n) {
+							uint32_t j = (cs * 0x9E3779B1u) >> 16;
+#pragma unroll
+							for (int p = 0; p < CC_PROBE && !done; p++, j++) {
+								j &= ccm;
+								uint32_t t = cck[j];
+								if (t == 0u) {
+									const uint32_t o = atomicCAS(&cck[j], 0u, cs + 1u);
+									t = o == 0u ? cs + 1u : o;
+								}
+								if (t == cs + 1u) {
+									atomicAdd((unsigned long long *)&ccv[j],
+										  (1ull << PK_SHIFT) | (unsigned long long)len);
+									done = true;
+								}
+							}
+						}
+					}
+					if (!done) {
 						atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
 						atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u], (unsigned long long)len);
 					}
@@ -5512,6 +5556,14 @@ template <int NT, class K, int Q> __global__ __launch_bounds__(NT) void k_ct_fin
 		if (x) {
 			atomicAdd((unsigned long long *)&a.delta[2u * k], x >> PK_SHIFT);
 			atomicAdd((unsigned long long *)&a.delta[2u * k + 1u], x & PK_BYTES_MASK);
+		}
+	}
+	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
+		const uint32_t t = cck[k];
+		const uint64_t x = ccv[k];
+		if (t && x) {
+			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u)], x >> PK_SHIFT);
+			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u) + 1u], x & PK_BYTES_MASK);
 		}
 	}
 }
@@ -5704,8 +5756,15 @@ template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct
 	constexpr int NF = 1024, Q = 4;
 	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF * Q - 1) / (NF * Q), 512), (a.n >> 22) + 1);
 	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
-	hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), (size_t)sf.hot_slots * 8u, st,
-			   sf, a);
+	/* the cold-slot cache in the LDS the hot slots leave */
+	const size_t hot = (size_t)sf.hot_slots * 8u;
+	uint32_t cc_n = 0;
+	if (!(s.schedule & CGPU_SCHED_NO_CCACHE))
+		for (uint32_t c = 1u << 14; c >= 512u && !cc_n; c >>= 1)
+			if (hot + (size_t)c * 12u <= X4_LDS_BUDGET)
+				cc_n = c;
+	hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), hot + (size_t)cc_n * 12u, st, sf,
+			   a, cc_n);
 }
 
 template <class K>
