@@ -5080,7 +5080,7 @@ static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool 
 	L.head = take(n);
 	L.temp_bytes = ct_temp_bytes(n);
 	L.temp = take(L.temp_bytes);
-	L.flags2 = take(2 * n); /* phase-2 candidates */
+	L.flags2 = take((svc ? 4 : 2) * n); /* phase-2 candidates */
 	if (svc) {
 		L.svc_out = take(n * (v6 ? 32 : 16));
 		L.ctl = take(16);

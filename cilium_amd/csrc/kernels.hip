@@ -36,6 +36,12 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
  * hint (`nt`), so the 26 B/tuple stream does not evict table lines. */
 typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u_t __attribute__((ext_vector_type(2)));
+/* one column element, nontemporal (streams past the table lines in L2) */
+template <typename T> __device__ __forceinline__ uint32_t ntl(const T *p)
+{
+	return (uint32_t)__builtin_nontemporal_load(p);
+}
+
 template <bool NTL> __device__ __forceinline__ uint4 ld_x4(const void *p)
 {
 	if (NTL) {
@@ -3423,10 +3429,10 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_PHASE2 128u   /* the packet's address pair may hold owed address entries: phase 2 */
 #define CTM_ADDRX 256u    /* its address entry lies in another pair: owed to phase 2 */
 #define CTM_SVCDROP 512u  /* lb4_local returned DROP_NO_SERVICE */
-#define CT_ADDRP 0x40u    /* walker -> phase 2: the address entry of this create is owed
-			   * (service path) / its ICMP entry (plain path, CTM_RELX) */
-#define CTM_RELX 1024u    /* plain path, TCP / UDP: grouped by connection in phase 1, the
-			   * ICMP entry a create writes is reserved and owed to phase 2 */
+#define CT_ADDRP 0x40u    /* walker -> phase 2: the address entry of this create is owed */
+#define CTM_RELX 1024u    /* grouped by connection in phase 1: the ICMP entry a create
+			   * writes is reserved and owed to phase 2 */
+#define CT_RELP 0x20u     /* walker -> phase 2: the ICMP entry of this create is owed */
 #define CTB_LB_LOOPBACK 8u /* struct ct_entry lb_loopback (common.h:389) */
 #define TUPLE_F_SERVICE 4u /* conntrack.h:66 */
 /* rec word 2 .w of the service path: lb_loopback | address-entry mode << 1 */
@@ -4000,7 +4006,7 @@ __device__ __forceinline__ void ct_flag(uint32_t *w)
  * to phase 2 (CTM_ADDRX), and a packet whose own pair can receive such
  * entries runs in phase 2 (CTM_PHASE2).  SERIAL: one group for the batch. */
 template <bool SVC, bool SERIAL>
-__global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
+__global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, bool conn = false)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
 	constexpr uint32_t RW = SVC ? 3u : 2u;
@@ -4121,17 +4127,28 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a)
 				/* pairs an address entry can land in: {T, T}, {IPV4_LOOPBACK,
 				 * x}, {target, 0} (ct_create4's addr / svc_addr rewrites) */
 				const uint32_t lo = s.ipv4_loopback;
-				const bool p2 = sa == da || !sa || !da || sa == lo || da == lo;
+				/* ... and, grouping by connection (conn), ICMP errors, which
+				 * read the ICMP entries the creates of every connection of
+				 * their pair owe */
+				const bool special = sa == da || !sa || !da || sa == lo || da == lo;
+				const bool p2 = special || (conn && pr == 1u && (tfl & TUPLE_F_RELATED));
 				if ((lbf >> 1) == AM_DEFER) {
 					meta |= CTM_ADDRX;
 					ct_flag(&a.ctl[2]);
-					if (p2)
-						ct_flag(&a.ctl[0]); /* owes into phase 2 from phase 2 */
+					if (special)
+						ct_flag(&a.ctl[0]); /* owes into phase 2b from phase 2b */
 				}
 				if (p2) {
 					meta |= CTM_PHASE2;
 					ct_flag(&a.ctl[1]);
 					g = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
+				} else if (conn) {
+					/* phase 1 by connection (an address entry of the same
+					 * pair is the forward key itself: tuple.daddr is the
+					 * target already), the ICMP entry owed */
+					meta |= CTM_RELX;
+					ct_flag(&a.ctl[2]);
+					g = ct_conn_group(g, z, pr);
 				}
 			}
 		}
@@ -4161,14 +4178,16 @@ __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 			const uint64_t i = g + (uint64_t)u * T;
 			act[u] = i < a.n;
 			const uint64_t j = act[u] ? i : 0u;
-			const uint32_t fl = a.flags[j];
-			pr[u] = a.proto[j];
-			len[u] = a.len[j];
-			sa[u] = a.saddr[j];
-			da[u] = a.daddr[j];
-			ep[u] = a.ep[j];
-			w[u] = a.l4[j];
-			const uint32_t dp = a.dport[j], sp = a.sport[j];
+			/* columns stream past the tables: nontemporal, so they do not
+			 * evict the LPM / policy lines from L2 */
+			const uint32_t fl = ntl(a.flags + j);
+			pr[u] = ntl(a.proto + j);
+			len[u] = ntl(a.len + j);
+			sa[u] = ntl(a.saddr + j);
+			da[u] = ntl(a.daddr + j);
+			ep[u] = ntl(a.ep + j);
+			w[u] = ntl(a.l4 + j);
+			const uint32_t dp = ntl(a.dport + j), sp = ntl(a.sport + j);
 			eg[u] = fl & 1u;
 			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
 			meta[u] = eg[u] ? CTM_EGRESS : 0u;
@@ -4256,11 +4275,11 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 			const uint64_t i = g + (uint64_t)u * T;
 			act[u] = i < a.n;
 			const uint64_t j = act[u] ? i : 0u;
-			const uint32_t fl = a.flags[j], dp = a.dport[j], sp = a.sport[j];
-			pr[u] = a.proto[j];
-			len[u] = a.len[j];
-			ep[u] = a.ep[j];
-			w[u] = a.l4[j];
+			const uint32_t fl = ntl(a.flags + j), dp = ntl(a.dport + j), sp = ntl(a.sport + j);
+			pr[u] = ntl(a.proto + j);
+			len[u] = ntl(a.len + j);
+			ep[u] = ntl(a.ep + j);
+			w[u] = ntl(a.l4 + j);
 			eg[u] = fl & 1u;
 			frag[u] = false; /* no fragment flag on IPv6 (bpf_lxc.c:787-789) */
 			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
@@ -4289,7 +4308,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 			dec[u] = act[u] && !(meta[u] & CTM_GATED);
 			fdp[u] = z[u] >> 16;
 			/* decide<1>'s identity from the pre-pass entry */
-			const uint32_t e = ipc_e[j];
+			const uint32_t e = ntl(ipc_e + j);
 			const uint32_t label = entry_label(s.ipc6.vals, e);
 			if (eg[u]) {
 				d[u].id = (e && label) ? label : s.world_id; /* cluster fallback folded into e */
@@ -4341,18 +4360,33 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 	}
 }
 
-/* phase 2 of the service path: candidate 2i = packet i if it runs in phase
- * 2, 2i + 1 = packet i's owed address entry (kept whatever phase 1 decided:
- * the walk checks CT_ADDRP).  The plain path's flags come from its prep and
- * walk (ct_args.f2). */
-__global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint8_t *f2)
+/* phase 2 of the service path, in two sub-phases: candidate 4i = packet i
+ * if it runs in phase 2, 4i + 1 = packet i's owed address entry (kept
+ * whatever phase 1 decided: the walk checks CT_ADDRP), 4i + 2 = the ICMP
+ * entry phase 1 owed (CT_RELP).  Phase 2a: the ICMP errors of ordinary
+ * pairs and the ICMP entries (all in ordinary pairs); phase 2b: the special
+ * pairs ({a, a}, 0, IPV4_LOOPBACK) - their packets and the address entries,
+ * which only land there.  2a writes and reads ordinary pairs only and may
+ * owe into 2b, 2b runs after it; a 2b packet that owes runs the batch
+ * serially.  The plain path's flags come from its prep and walk (ct_args.f2,
+ * two per packet). */
+__global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint32_t *f4, uint32_t lo, uint32_t phase)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
 	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t meta = a.rec[3u * i].w >> 16;
+		const uint4 r0 = a.rec[3u * i];
+		const uint32_t meta = r0.w >> 16, da = r0.x, sa = r0.y;
 		const bool live = !(meta & CTM_GATED);
-		f2[2u * i] = live && (meta & CTM_PHASE2) ? 1u : 0u;
-		f2[2u * i + 1u] = live && (meta & CTM_ADDRX) ? 1u : 0u;
+		const bool special = sa == da || !sa || !da || sa == lo || da == lo;
+		const bool p2 = live && (meta & CTM_PHASE2);
+		uint32_t f;
+		if (phase == 0u) {
+			const bool rel = live && (meta & CTM_RELX) && (a.ct_ret[i] & CT_RELP);
+			f = (p2 && !special ? 1u : 0u) | (rel ? 1u << 16 : 0u);
+		} else {
+			f = (p2 && special ? 1u : 0u) | (live && (meta & CTM_ADDRX) ? 1u << 8 : 0u);
+		}
+		f4[i] = f;
 	}
 }
 
@@ -4362,12 +4396,14 @@ __global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint8_t *f2)
 template <class K> __global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args a, uint32_t m, uint32_t by_key)
 {
 	for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) {
-		const uint32_t v = a.idx[j], i = v >> 1;
+		const uint32_t v = a.idx[j], i = K::ADDR ? v >> 2 : v >> 1;
 		const ct_rec<K> r = ct_rec<K>::load(a.rec, i, false);
 		if constexpr (K::ADDR) {
 			uint4 k = r.key();
-			if (v & 1u)
+			if ((v & 3u) == 1u)
 				k = ct_addr_key(CtK4::reversed(k), r.pkt());
+			else if ((v & 3u) == 2u)
+				k = CtK4::related(CtK4::reversed(k));
 			a.gkey[j] = by_key ? ct_hash(k.x, k.y, k.z, k.w) : ct_group(k.x, k.y);
 		} else if constexpr (K::V6 != 0) {
 			/* an ICMP entry carries its packet's pair */
@@ -4964,8 +5000,8 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 		 * its capacity now (where the reference's update would fail), write
 		 * it in phase 2 in batch order */
 		if (!ct_take(T, A))
-			return CT_NEW | CT_FAIL;
-		return CT_NEW | CT_ADDRP;
+			return CT_NEW | CT_FAIL | owed;
+		return CT_NEW | CT_RELP | owed;
 	}
 	if (!ctc_update<K>(T, A, c, K::related(k), e))
 		return CT_NEW | CT_FAIL | owed;
@@ -5308,7 +5344,10 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 	ctc_ent<K> e0{}, e1{}, e2{};
 	ct_cache<K> c{e0, e1, e2, 0u, 0u};
 #endif
-	auto pkt_of = [](uint32_t v) { return MODE == WALK_OWED ? v >> 1 : v; };
+	/* phase-2 candidates: v = packet << 1 | kind (plain path: kind 1 = the
+	 * ICMP entry), v = packet << 2 | kind (service path: kind 1 = the address
+	 * entry, 2 = the ICMP entry) */
+	auto pkt_of = [](uint32_t v) { return MODE == WALK_OWED ? (K::ADDR ? v >> 2 : v >> 1) : v; };
 	/* groups longest first (a.glen / a.gpos, sorted by length): the
 	 * elephants start in the first round and the rest fill in behind */
 	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {
@@ -5354,19 +5393,23 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 			} else {
 				const ct_pkt q = r.pkt();
 				if constexpr (MODE == WALK_OWED) {
-					if (v & 1u) {
-						/* the owed address entry (service path) / ICMP
-						 * entry (plain path) of packet i's create */
-						if (a.ct_ret[i] & CT_ADDRP) {
-							const typename K::key fk = K::reversed(r.key());
-							if constexpr (K::ADDR) {
+					const uint32_t kind = K::ADDR ? (v & 3u) : (v & 1u) << 1;
+					const typename K::key fk = K::reversed(r.key());
+					if (kind == 1u) {
+						/* the owed address entry of packet i's create */
+						if constexpr (K::ADDR) {
+							if (a.ct_ret[i] & CT_ADDRP)
 								ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
 										   ct_new_row<K>(q, false, a.now));
-							} else {
-								ct_row e = ct_new_row<K>(q, !(q.meta & CTM_EGRESS), a.now);
-								e.c.y |= CTB_SEEN_NON_SYN;
-								ctc_update_owed<K>(T, A, c, K::related(fk), e);
-							}
+						}
+						continue;
+					}
+					if (kind == 2u) {
+						/* the owed ICMP entry of packet i's create */
+						if (a.ct_ret[i] & CT_RELP) {
+							ct_row e = ct_new_row<K>(q, !(q.meta & CTM_EGRESS), a.now);
+							e.c.y |= CTB_SEEN_NON_SYN;
+							ctc_update_owed<K>(T, A, c, K::related(fk), e);
 						}
 						continue;
 					}
@@ -5375,7 +5418,7 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 					continue;
 				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now);
 				a.ct_ret[i] = (uint8_t)ret;
-				if (!K::ADDR && MODE == WALK_PKT && (ret & CT_ADDRP))
+				if (!K::ADDR && MODE == WALK_PKT && (ret & CT_RELP))
 					a.f2[2u * i + 1u] = 1u; /* its ICMP entry is owed to phase 2 */
 			}
 		}
@@ -5446,8 +5489,8 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 			const uint64_t j = act[u] ? i : 0u;
 			/* batch order: records and the walker's results stream in */
 			q[u] = ct_rec<K>::load(a.rec, (uint32_t)j, true).pkt();
-			c[u] = a.ct_ret[j] & ~CT_ADDRP;
-			ep[u] = a.ep[j];
+			c[u] = ntl(a.ct_ret + j) & ~(CT_ADDRP | CT_RELP);
+			ep[u] = ntl(a.ep + j);
 			eg[u] = q[u].meta & CTM_EGRESS;
 			frag[u] = q[u].meta & CTM_FRAG;
 			rep[u] = act[u] && !(q[u].meta & CTM_GATED) && (c[u] & 3u) >= CT_REPLY;
@@ -5456,7 +5499,7 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 			/* the reply tuple keeps the packet's addresses and direction, so
 			 * its identity is the one the prep resolved (decide<>'s identity
 			 * depends on neither port nor protocol) */
-			d[u].id = rep[u] ? a.identity[j] : 0u;
+			d[u].id = rep[u] ? ntl(a.identity + j) : 0u;
 		}
 		policy_q<Q>(s, rep, eg, frag, dp, pr, ep, d);
 #pragma unroll
@@ -5685,13 +5728,13 @@ static hipError_t ct_select(const uint8_t *f, uint64_t n, uint32_t *out, uint32_
 }
 
 /* scratch for the sort of n packets (hipcub) and for the block counts of the
- * selections (the 2n phase-2 candidates of the service path at most) */
+ * selections (the 4n phase-2 candidates of the service path at most) */
 size_t ct_temp_bytes(uint64_t n)
 {
 	size_t a = 0;
 	(void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
 						 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
-	return std::max<size_t>(a, sel_blocks(2 * n) * 4u + 4u);
+	return std::max<size_t>(a, sel_blocks(4 * n) * 4u + 4u);
 }
 
 static ct_args ct_args_of(const ct_launch &L)
@@ -5747,13 +5790,19 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 	return hipSuccess;
 }
 
+/* packets per lane of the conntrack prep / finish passes (timing-only tool
+ * builds vary it, tools/diag_ab.py) */
+#ifndef CGPU_CT_Q
+#define CGPU_CT_Q 4
+#endif
+
 /* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
 #define CT_WALK_GRID 2048
 
 template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
 	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
-	constexpr int NF = 1024, Q = 4;
+	constexpr int NF = 1024, Q = CGPU_CT_Q;
 	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF * Q - 1) / (NF * Q), 512), (a.n >> 22) + 1);
 	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
 	/* the cold-slot cache in the LDS the hot slots leave */
@@ -5790,7 +5839,7 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 			hipLaunchKernelGGL(k_ct_prep6<false>, dim3(g), dim3(256), 0, st, s, a);
 		}
 	} else {
-		constexpr int Q = 4;
+		constexpr int Q = CGPU_CT_Q;
 		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
 		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
 	}
@@ -5863,14 +5912,17 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
  *   2 k_ct_prep<SVC>: the translated tuples (svc_out), their decisions and
  *     the ct_state their creates store.
  *   3 group sort + k_ct_walk<WALK_PKT> (phase 1): every packet outside the
- *     pairs address entries can land in; an address entry of another pair
- *     is reserved and owed (CT_ADDRP).
+ *     pairs address entries can land in and but ICMP errors, grouped by
+ *     connection; an address entry of another pair and the ICMP entry of
+ *     every create are reserved and owed (CT_ADDRP, CT_RELP).
  *   4 phase 2 (only when something is owed or runs in it): the owed
- *     entries and the phase-2 packets, grouped by address pair (or by the
- *     owed entry's key when no packet runs in phase 2), in batch order.
+ *     entries and the phase-2 packets, grouped by address pair, in batch
+ *     order: 2a the ordinary pairs (ICMP errors, owed ICMP entries), then 2b
+ *     the special pairs (their packets, the owed address entries, which
+ *     land only there; see k_ct_owed_flags).
  *   5 k_ct_finish.
- * A batch where a phase-2 packet itself owes an entry to another pair
- * (addresses 0 / IPV4_LOOPBACK as endpoints or service backends) runs the
+ * A batch where a packet of the special pairs (addresses 0 / IPV4_LOOPBACK
+ * as endpoints or service backends) itself owes an address entry runs the
  * conntrack path as ONE group (exact, serial).
  */
 hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
@@ -5887,7 +5939,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	e = hipMemsetAsync(a.ctl, 0, 16, st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL((k_ct_prep<true, false>), dim3(g), dim3(256), 0, st, s, a);
+	hipLaunchKernelGGL((k_ct_prep<true, false>), dim3(g), dim3(256), 0, st, s, a, true);
 	uint32_t ctl[4];
 	e = hipMemcpyAsync(ctl, a.ctl, 16, hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
@@ -5901,22 +5953,24 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if (!serial && (ctl[1] || ctl[2])) {
 		const unsigned g2 = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
-		hipLaunchKernelGGL(k_ct_owed_flags, dim3(g2), dim3(256), 0, st, a, L.flags2);
-		e = ct_select(L.flags2, 2 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
-		if (e != hipSuccess)
-			return e;
-		uint32_t m = 0;
-		e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
-		if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
-			return e;
-		if (m) {
+		for (uint32_t ph = 0; ph < 2u; ph++) {
+			hipLaunchKernelGGL(k_ct_owed_flags, dim3(g2), dim3(256), 0, st, a,
+					   reinterpret_cast<uint32_t *>(L.flags2), s.ipv4_loopback, ph);
+			e = ct_select(L.flags2, 4 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
+			if (e != hipSuccess)
+				return e;
+			uint32_t m = 0;
+			e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+			if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+				return e;
+			if (!m)
+				continue;
 			const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
-			hipLaunchKernelGGL(k_ct_owed_keys<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, ctl[1] ? 0u : 1u);
+			hipLaunchKernelGGL(k_ct_owed_keys<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, 0u);
 			e = ct_group_sort(s, L, a, m, &nh, st);
 			if (e != hipSuccess)
 				return e;
-			hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T,
-					   a);
+			hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 		}
 	}
 	launch_ct_finish<CtK4S>(s, a, st);

@@ -154,7 +154,7 @@ struct ct_launch {
 	const uint32_t *hash; /* NULL: cgpu_flow_hash */
 	uint4 *svc_out;       /* [n] */
 	uint32_t *ctl;        /* [4] */
-	uint8_t *flags2;      /* [2n] */
+	uint8_t *flags2;      /* [2n] plain path, [4n] service path: phase-2 candidates */
 	void *xdaddr;         /* [n] optional (IPv6: 16 bytes each) */
 	uint16_t *xdport;     /* [n] optional */
 };
