@@ -4461,6 +4461,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 			const uint4 so = egress ? a.svc_out[2u * i] : make_uint4(SVC_NONE, 0, 0, 0);
 			if ((so.x & 3u) == SVC_DROP) {
 				a.identity[i] = 0;
+				reinterpret_cast<uint16_t *>(a.f2)[i] = 0u;
 				if (a.xdaddr)
 					reinterpret_cast<uint4 *>(a.xdaddr)[i] = da;
 				if (a.xdport)
@@ -4523,7 +4524,8 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
 		}
 		uint32_t g = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
-		if constexpr (!SVC) { /* phase 1 by connection, as k_ct_prep */
+		{ /* phase 1 by connection, as k_ct_prep (ct_create6 writes no address
+		   * entry, so the service path groups the same way) */
 			bool p2 = false;
 			if (!(meta & CTM_GATED)) {
 				if (pr == 58u && (tfl & TUPLE_F_RELATED)) {
@@ -4575,7 +4577,10 @@ template <class K> struct ctc_ent {
 };
 
 template <class K> struct ct_cache {
-	ctc_ent<K> &e0, &e1, &e2;
+	ctc_ent<K> &e0, &e1;
+#if CTC >= 3
+	ctc_ent<K> &e2;
+#endif
 #if CTC == 4
 	ctc_ent<K> &e3;
 #endif
@@ -4587,7 +4592,9 @@ template <class K, typename F> __device__ __forceinline__ void ctc_each(ct_cache
 {
 	f(c.e0, 0);
 	f(c.e1, 1);
+#if CTC >= 3
 	f(c.e2, 2);
+#endif
 #if CTC == 4
 	f(c.e3, 3);
 #endif
@@ -5340,9 +5347,12 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 #if CTC == 4
 	ctc_ent<K> e0{}, e1{}, e2{}, e3{};
 	ct_cache<K> c{e0, e1, e2, e3, 0u, 0u};
-#else
+#elif CTC == 3
 	ctc_ent<K> e0{}, e1{}, e2{};
 	ct_cache<K> c{e0, e1, e2, 0u, 0u};
+#else
+	ctc_ent<K> e0{}, e1{};
+	ct_cache<K> c{e0, e1, 0u, 0u};
 #endif
 	/* phase-2 candidates: v = packet << 1 | kind (plain path: kind 1 = the
 	 * ICMP entry), v = packet << 2 | kind (service path: kind 1 = the address
@@ -5816,6 +5826,31 @@ template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct
 			   a, cc_n);
 }
 
+/* phase 2 of the plain paths (and of the IPv6 service path): the ICMP
+ * errors and the owed ICMP entries of the creates, grouped by address pair,
+ * in batch order (the prep and the walk set the candidate flags) */
+template <class K>
+static hipError_t ct_phase2(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, ct_args &a,
+			    hipStream_t st)
+{
+	hipError_t e = ct_select(L.flags2, 2 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
+	if (e != hipSuccess)
+		return e;
+	uint32_t m = 0, nh = 0;
+	e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+		return e;
+	if (!m)
+		return hipSuccess;
+	const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
+	hipLaunchKernelGGL(k_ct_owed_keys<K>, dim3(gm), dim3(256), 0, st, a, m, 0u);
+	e = ct_group_sort(s, L, a, m, &nh, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_walk<K, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	return hipGetLastError();
+}
+
 template <class K>
 static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
 {
@@ -5848,24 +5883,8 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
-	/* phase 2: the ICMP errors and the owed ICMP entries of the creates,
-	 * grouped by address pair, in batch order (the prep and the walk set
-	 * the candidate flags) */
-	e = ct_select(L.flags2, 2 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
-	if (e != hipSuccess)
+	if ((e = ct_phase2<K>(s, T, L, a, st)) != hipSuccess)
 		return e;
-	uint32_t m = 0;
-	e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
-	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
-		return e;
-	if (m) {
-		const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
-		hipLaunchKernelGGL(k_ct_owed_keys<K>, dim3(gm), dim3(256), 0, st, a, m, 0u);
-		e = ct_group_sort(s, L, a, m, &nh, st);
-		if (e != hipSuccess)
-			return e;
-		hipLaunchKernelGGL((k_ct_walk<K, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
-	}
 	launch_ct_finish<K>(s, a, st);
 	return hipGetLastError();
 }
@@ -5883,8 +5902,9 @@ hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, cons
 }
 
 /* cgpu_classify_v6_ctlb: the IPv6 service walk (k_svc_prep6, WALK_SVC over
- * CtK6), then the IPv6 conntrack path with the service's state; ct_create6
- * writes no address entry, so there is no phase 2 */
+ * CtK6), then the IPv6 conntrack path with the service's state: phase 1 by
+ * connection, phase 2 the ICMPv6 errors and owed ICMPv6 entries by address
+ * pair, as the plain path (ct_create6 writes no address entry) */
 hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
 				   hipStream_t st)
 {
@@ -5901,6 +5921,8 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK6S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	if ((e = ct_phase2<CtK6S>(s, T, L, a, st)) != hipSuccess)
+		return e;
 	launch_ct_finish<CtK6S>(s, a, st);
 	return hipGetLastError();
 }
