@@ -549,7 +549,15 @@ def main():
             "config": conf,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic},
+                         "traffic": traffic,
+                         # achieved counts ALGORITHMIC bytes (64 B per reference map
+                         # lookup); the HBM-side rate from the PMC traffic says how
+                         # much of the 8 TB/s the kernel really moves: the tables
+                         # are mostly L2 / MALL hits, so the kernel is bound by
+                         # gather latency and memory-side atomics, not bandwidth
+                         "basis": "B_alg (columns + 64 B per reference map lookup)",
+                         "hbm_side_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                           if traffic else None)},
             "cpu_baseline": cpu,
         }
         if not parity:

@@ -2822,8 +2822,11 @@ static cgpu_snapshot with_lds_hot(const cgpu_snapshot &s, size_t max_hot)
  * the classify kernel's; the classify kernel then reads 4 bytes per tuple
  * instead of the address.  Lane-interleaved: load instruction u of a wave
  * covers 64 consecutive tuples. */
+#ifndef CGPU_IPC6_MINW
+#define CGPU_IPC6_MINW 1 /* workgroups per CU the register budget aims at */
+#endif
 template <int Q, int NT>
-__global__ __launch_bounds__(NT) void k_ipc6_pre(cgpu_snapshot s, const uint4 *sa, const uint4 *da,
+__global__ __launch_bounds__(NT, CGPU_IPC6_MINW) void k_ipc6_pre(cgpu_snapshot s, const uint4 *sa, const uint4 *da,
 						 const uint8_t *flags, uint32_t *e_out, uint64_t n)
 {
 	extern __shared__ __attribute__((aligned(16))) uint32_t lt[];

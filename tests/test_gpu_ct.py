@@ -235,3 +235,24 @@ def test_ct_crowded_map_no_duplicates(torch_cuda, cfg_ct):
     _assert_same_map(e, o)
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     e.close()
+
+
+def test_ct_many_connections_per_pair(torch_cuda, cfg_ct):
+    """Phase 1 groups by connection, phase 2 by address pair: 3,000
+    overlapping connections over FOUR address pairs (one endpoint, four
+    remotes), so every pair's creates owe hundreds of ICMP entries to phase 2
+    and its ICMP errors must see exactly the entries created before them in
+    batch order; ICMP echo connections of a pair share their ids.  Two
+    batches, map, verdicts, ct results and counters bit-exact against the
+    restatement."""
+    T, _, _, _ = cfg_ct
+    t, locals_be, seclabels = synth.make_ct_workload(T, 3_000, seed=91, n_remote=4, mean_pkts=12.0,
+                                                     span=0.6)
+    err = (t["proto"] == 1) & np.isin(t["l4b"], [3, 11, 12])
+    lo, hi = np.minimum(t["saddr"], t["daddr"]), np.maximum(t["saddr"], t["daddr"])
+    pairs = np.unique(lo.astype(np.uint64) << np.uint64(32) | hi.astype(np.uint64))
+    assert err.sum() > 100 and len(pairs) <= 4
+    e, o = _pair(torch_cuda, T, t, locals_be, seclabels, 2, [3000, 3002])
+    _assert_same_map(e, o)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
