@@ -686,6 +686,7 @@ struct V6Build {
 	std::vector<uint16_t> b24_16; /* empty: not representable */
 	std::vector<std::array<uint32_t, 8>> h64;
 	uint32_t m64 = 0;
+	std::vector<uint32_t> bl64; /* bloom of the /64s with records (tables.h v6_lpm) */
 	bool any = false;
 	bool too_big = false; /* node lines past V6T_LINE_MASK */
 };
@@ -1010,6 +1011,18 @@ void build_v6(std::vector<Rank6> cand, V6Build &b)
 		i = j;
 	}
 	hop_place<8>(b.h64, b.m64, r64, h64_home);
+	/* the bloom of the /64s with records: ~2 records per 32-bit word (3
+	 * bits each) keeps false positives near 1 % */
+	{
+		uint32_t nw = 16;
+		while (nw < V6T_BLOOM_MAX_WORDS && nw * 2u < r64.size())
+			nw <<= 1;
+		b.bl64.assign(nw, 0u);
+		for (const auto &r : r64) {
+			const uint32_t h = mix32(r[0], r[1]);
+			b.bl64[v6_bloom_word(h, nw - 1u)] |= v6_bloom_bits(h);
+		}
+	}
 	/* a line past the last: a lane reads a whole line */
 	b.pool.insert(b.pool.end(), V6T_LW, 0xFFFFFFFFu);
 	/* LDS-staged forms */
@@ -3391,7 +3404,7 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o_v = ar.add(b.dir.vals.data(), b.dir.vals.size() * 4);
 	if (b.v6.too_big)
 		return fail(-E2BIG, "ipcache v6 trie exceeds 2^29 node lines");
-	size_t o6[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	size_t o6[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 	if (b.v6.any) {
 		o6[0] = ar.add(b.v6.root.data(), b.v6.root.size() * 4);
 		o6[1] = ar.add(b.v6.b24.data(), b.v6.b24.size() * 4);
@@ -3401,6 +3414,7 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 		o6[5] = ar.add(b.v6.h64.data(), b.v6.h64.size() * 32);
 		o6[6] = ar.add(b.v6.rbits.data(), b.v6.rbits.size() * 4);
 		o6[7] = ar.add(b.v6.b24_16.data(), b.v6.b24_16.size() * 2);
+		o6[8] = ar.add(b.v6.bl64.data(), b.v6.bl64.size() * 4);
 	}
 	if (int r = upload(c, ar, buf, G_IPC))
 		return r;
@@ -3413,7 +3427,8 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 				at<uint32_t>(buf, o6[3]), at<uint32_t>(buf, o6[4]), at<uint4>(buf, o6[5]), b.v6.m64,
 				at<uint32_t>(buf, o6[6]),
 				b.v6.b24_16.empty() ? nullptr : at<uint16_t>(buf, o6[7]),
-				(uint32_t)(b.v6.b24.size() / 256)};
+				(uint32_t)(b.v6.b24.size() / 256), at<uint32_t>(buf, o6[8]),
+				(uint32_t)b.v6.bl64.size() - 1u};
 	b.sum[G_IPC] = in.sum_ipc;
 	return 0;
 }

@@ -1303,9 +1303,18 @@ __host__ __device__ __forceinline__ uint32_t v6t_lds_words(const v6_lpm &t)
 	return t.root ? V6T_RBITS_WORDS + v6t_lds_b24(t) * 128u : 0u;
 }
 
+/* bloom words the lookup pre-pass stages behind them (0: none) */
+__host__ __device__ __forceinline__ uint32_t v6t_lds_bloom(const v6_lpm &t)
+{
+	return t.root && t.bl64 && t.bl64_mask < V6T_BLOOM_MAX_WORDS ? t.bl64_mask + 1u : 0u;
+}
+
+/* bl: the /64 bloom staged in LDS (v6_lpm.bl64), or NULL: probe h64 for
+ * every tuple under a deep /32 */
 template <int Q>
 __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *lds, bool lds24,
-					     const uint4 (&w)[Q], const bool (&act)[Q], uint32_t (&e)[Q])
+					     const uint4 (&w)[Q], const bool (&act)[Q], uint32_t (&e)[Q],
+					     const uint32_t *bl = nullptr)
 {
 	const uint16_t *rank = reinterpret_cast<const uint16_t *>(lds + 2048u);
 	const uint16_t *b16 = reinterpret_cast<const uint16_t *>(lds + V6T_RBITS_WORDS);
@@ -1368,7 +1377,15 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 		node[u] = b32i[u] != 0xFFFFFFFFu && (n[u].x & DIR_TAG_MASK) == DIR_TAG_GROUP;
 		if (b32i[u] != 0xFFFFFFFFu && !node[u])
 			e[u] = n[u].x;
+#ifdef CGPU_DIAG_V6_NO_H64 /* timing-only tool build: the /64 records never read (wrong results) */
+		deep[u] = false;
+#else
 		deep[u] = node[u] && (n[u].x & V6T_DEEP);
+		if (bl && deep[u]) {
+			const uint32_t h = mix32(w[u].x, w[u].y), m = v6_bloom_bits(h);
+			deep[u] = (bl[v6_bloom_word(h, t.bl64_mask)] & m) == m;
+		}
+#endif
 		out[u] = false;
 		line[u] = node[u] ? v6t_line(n[u].x, n[u].y, w[u].y, out[u]) : 0u;
 		home[u] = mix32(w[u].x, w[u].y) & t.m64;
@@ -2831,12 +2848,16 @@ __global__ __launch_bounds__(NT, CGPU_IPC6_MINW) void k_ipc6_pre(cgpu_snapshot s
 {
 	extern __shared__ __attribute__((aligned(16))) uint32_t lt[];
 	const uint32_t n24 = v6t_lds_b24(s.ipc6);
+	const uint32_t nbl = v6t_lds_bloom(s.ipc6);
+	uint32_t *lbl = lt + v6t_lds_words(s.ipc6);
 	if (s.ipc6.root) {
 		for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += NT)
 			lt[k] = s.ipc6.rbits[k];
 		const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
 		for (uint32_t k = threadIdx.x; k < n24 * 128u; k += NT)
 			lt[V6T_RBITS_WORDS + k] = b16[k];
+		for (uint32_t k = threadIdx.x; k < nbl; k += NT)
+			lbl[k] = s.ipc6.bl64[k];
 	}
 	__syncthreads();
 	const uint64_t T = (uint64_t)gridDim.x * NT;
@@ -2852,7 +2873,7 @@ __global__ __launch_bounds__(NT, CGPU_IPC6_MINW) void k_ipc6_pre(cgpu_snapshot s
 			if (act[u])
 				w[u] = v6_host_words(ld_x4<true>(((flags[i] & 1u) ? da : sa) + i));
 		}
-		v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w, act, e);
+		v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w, act, e, nbl ? lbl : nullptr);
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
@@ -2881,7 +2902,7 @@ __global__ __launch_bounds__(NT, CGPU_IPC6_MINW) void k_ipc6_pre(cgpu_snapshot s
 static hipError_t launch_ipc6_pre(const cgpu_snapshot &s, const cls_args &a, hipStream_t st)
 {
 	constexpr int NT = 1024, Q = CGPU_DIAG_IPC6_PRE_Q;
-	const size_t lds = (size_t)v6t_lds_words(s.ipc6) * 4u;
+	const size_t lds = (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u;
 	const unsigned res = resident_blocks((const void *)k_ipc6_pre<Q, NT>, NT, lds);
 	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + Q * NT - 1) / (Q * NT), res));
 	hipLaunchKernelGGL((k_ipc6_pre<Q, NT>), dim3(g), dim3(NT), lds, st, s, static_cast<const uint4 *>(a.saddr),
@@ -5865,7 +5886,7 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 		 * egress fallback identity */
 		if (s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK) {
 			constexpr int NT = 1024, QP = CGPU_DIAG_IPC6_PRE_Q, Q = 4;
-			const size_t lds = (size_t)v6t_lds_words(s.ipc6) * 4u;
+			const size_t lds = (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u;
 			const unsigned res = resident_blocks((const void *)k_ipc6_pre<QP, NT>, NT, lds);
 			const unsigned gp = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + QP * NT - 1) / (QP * NT), res));
 			hipLaunchKernelGGL((k_ipc6_pre<QP, NT>), dim3(gp), dim3(NT), lds, st, s,

@@ -274,7 +274,14 @@ typedef struct v6_lpm {
 	const uint32_t *rbits;
 	const uint16_t *b24_16;
 	uint32_t n_b24;        /* b24 blocks */
+	/* blocked bloom filter of the /64s that hold h64 records (v6_bloom_word /
+	 * v6_bloom_bits over mix32 of the /64's words), staged in LDS by the
+	 * lookup pre-pass: a lookup whose /64 misses it skips the h64 probe */
+	const uint32_t *bl64;
+	uint32_t bl64_mask;    /* words - 1 */
 } v6_lpm;
+
+#define V6T_BLOOM_MAX_WORDS 16384u /* 64 KiB */
 
 #define EP6_BLOOM_MAX_WORDS 8192u /* 32 KiB: staged in LDS by k_prefilter_v6_q */
 
