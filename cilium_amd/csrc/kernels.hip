@@ -5331,6 +5331,10 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
 	return make_uint4(SVC_XLATED | (lbs << 8) | (slave << 16), rw | ((val.y & 0xFFFFu) << 16), 0u, 0u);
 }
 
+#ifndef CT_RETB
+#define CT_RETB 16 /* results a walker lane buffers before storing them */
+#endif
+
 /* walks: WALK_PKT the conntrack path's packets; WALK_SVC the service step
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
  * service path: candidates c = packet << 1 | kind, kind 0 a packet whose
@@ -5362,6 +5366,24 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 	using R = std::conditional_t<MODE == WALK_SVC, std::conditional_t<K::V6 != 0, ct_srec6, ct_srec>,
 				     ct_rec<K>>;
 	__shared__ int s_acct[3];
+	/* each lane's last CT_RETB results (packet index, ct result), stored
+	 * together: a scattered 1-byte store is a memory-side write whose
+	 * completion every later load wait of the lane also waits for (vmcnt
+	 * counts stores), so storing per packet put one write latency into every
+	 * step (1.4 ms of a 12.3 ms step, profiles/r3_session_h/ab_ct_ret.log);
+	 * CT_RETB stores issued back to back cost about one */
+	__shared__ uint32_t s_ri[CT_RETB][256];
+	__shared__ uint8_t s_rr[CT_RETB][256];
+	uint32_t nret = 0;
+	auto ret_flush = [&]() {
+		for (uint32_t k = 0; k < nret; k++) {
+			const uint32_t i = s_ri[k][threadIdx.x], ret = s_rr[k][threadIdx.x];
+			a.ct_ret[i] = (uint8_t)ret;
+			if (!K::ADDR && MODE == WALK_PKT && (ret & CT_RELP))
+				a.f2[2u * i + 1u] = 1u; /* its ICMP entry is owed to phase 2 */
+		}
+		nret = 0;
+	};
 	if (threadIdx.x < 3)
 		s_acct[threadIdx.x] = 0;
 	__syncthreads();
@@ -5451,13 +5473,15 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 				if (MODE == WALK_PKT && (meta & CTM_PHASE2))
 					continue;
 				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now);
-				a.ct_ret[i] = (uint8_t)ret;
-				if (!K::ADDR && MODE == WALK_PKT && (ret & CT_RELP))
-					a.f2[2u * i + 1u] = 1u; /* its ICMP entry is owed to phase 2 */
+				s_ri[nret][threadIdx.x] = i;
+				s_rr[nret][threadIdx.x] = (uint8_t)ret;
+				if (++nret == CT_RETB)
+					ret_flush();
 			}
 		}
 		ctc_flush(T, c);
 	}
+	ret_flush();
 #ifdef CGPU_DIAG_WALK_CLOCK
 	{
 		uint32_t mx = dg_steps;
