@@ -1521,7 +1521,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		/* QA: the vector-load branches below are written for Q = 4; arrays
 		 * they fill are sized for them whatever Q (dead when Q != 4) */
 		constexpr int QA = Q < 4 ? 4 : Q;
-		uint32_t fw[Q], ad[Q], hi4[Q], ep[QA], len[QA], dstat[Q];
+		uint32_t fw[Q], ad[Q], hi4[Q], ep[QA], len[QA];
 		uint4 ad6[Q];
 		{
 			uint32_t fl[QA], proto[QA], dport[QA], sa[QA], da[QA];
@@ -1663,9 +1663,9 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 			for (int u = 0; u < Q; u++) {
 				const bool eg = fl[u] & 1u;
 				/* frames: a frame the parse ended runs no lookup (F_GATED
-				 * masks them) and reports its status (dstat) */
+				 * masks them) and reports its status (its daddr column,
+				 * re-read at the output: 0 for an IPv6 frame's placeholder) */
 				const bool dec = FR && !V6 && (fl[u] & (FRF_DEC | FRF_V6));
-				dstat[u] = (fl[u] & FRF_V6) ? 0u : da[u];
 				if (dec)
 					lbf[u] |= F_DEC | F_GATED;
 				/* ct_lookup{4,6} protocol gate: ICMP (v4: 1, v6: 58), TCP, UDP */
@@ -1877,7 +1877,11 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				/* k_frames' rules: NOT_CLASSIFIED counts nothing (stage 7), an
 				 * IPv6 frame's placeholder is overwritten by the v6 pass */
 				id[u] = 0;
-				const int32_t sv = (int32_t)dstat[u];
+				v[u] = 0;
+				st[u] = 0;
+				if (!(fw[u] & F_OK))
+					continue; /* a tail lane repeating tuple i0: no status, no metrics */
+				const int32_t sv = (int32_t)static_cast<const uint32_t *>(a.daddr)[i0 + u];
 				if (sv == 0 || sv == FRAME_NOT_CLASSIFIED) {
 					v[u] = 0;
 					st[u] = sv ? 7u : 0u;

@@ -112,6 +112,32 @@ def test_classify_frames_vs_restatement(torch_cuda, gate, verify):
     e.close()
 
 
+@pytest.mark.parametrize("tail", [1, 2, 3])
+def test_classify_frames_ragged_tail(torch_cuda, tail):
+    """Batches of 4k + tail frames whose last partial quad starts with a frame
+    the parse drops: the x4 schedule's tail lanes repeat that frame's columns
+    and must count nothing (verdicts, stages and metrics equal the
+    restatement's)."""
+    T = synth.make_tables(n_prefixes=2000, n_identities=100, n_endpoints=5, keys_per_ep=500)
+    rng = np.random.Generator(np.random.PCG64(0x7A11 + tail))
+    pool = T.pfx_addr.astype(np.uint32).byteswap()
+    n = 4 * 5000 + tail
+    f = synth.make_frames(rng, n, width=128, addr4=pool)
+    f["len"][n - tail] = 10  # a runt: DROP_INVALID, counted in the metrics
+    e = _engine(1, 7, **T.engine_config())
+    synth.load_engine(e, T)
+    e.commit()
+    o = frame_oracle(1, 7, **T.oracle_config())
+    synth.load_oracle(o, T)
+    v, idt, st = _classify_frames(torch_cuda, e, f)
+    ov, oi, ost, _ = o.classify_frames(f, nthreads=4)
+    assert ov[n - tail] == L.DROP_INVALID
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(st, ost)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
+
+
 def test_classify_frames_equals_classify_v4(torch_cuda):
     """Config-2 style tuples serialized as frames (64-byte slots) classify
     exactly as the tuples themselves do through cgpu_classify_v4."""
