@@ -28,19 +28,22 @@ Other BASELINE configs (not the headline line; run them explicitly):
                      cgpu_classify_v4_ct over 64M packets of 2M connections,
                      the cilium_ct4_global map emptied at the start of every
                      step (cgpu_ct4_flush, timed), so each step creates,
-                     updates and reply-skips the same way; parity and the
-                     CPU baseline on the packets of 1/64 of the address pairs
-                     (pairs are independent conntrack groups)
+                     updates and reply-skips the same way; parity on the
+                     whole batch and the CPU baseline from the restatement
+                     threaded over address-pair shards (pairs are independent
+                     conntrack groups, so the threaded run is exact)
   --config ctlb      config 2 tables + 1M services + conntrack behind the
                      STATEFUL service step (cgpu_classify_v4_ctlb: lb4_local
                      with CONNTRACK, CT_SERVICE entries, stored slaves,
-                     ct_create4's address entries): 16M packets of 500k
-                     connections (40 % to services), map emptied each step;
-                     parity and the CPU baseline on the whole batch
+                     ct_create4's address entries): 64M packets of 2M
+                     connections (40 % to services), map emptied each step,
+                     the translated daddr / dport written; parity against the
+                     sequential restatement over the whole batch, the CPU
+                     baseline threaded by connection
   --config ctlb6     ctlb over IPv6 (cgpu_classify_v6_ctlb, 100k IPv6 services)
   --config ct6       ct over IPv6 (cilium_ct6_global, cgpu_classify_v6_ct):
                      100k IPv6 ipcache prefixes + 64k policy keys, 64M packets
-                     of 2M connections, parity on 1/64 of the address pairs
+                     of 2M connections, parity on the whole batch
   --config mapstate  L3 MapState compilation: the label
                      decision of computeDesiredL3PolicyMapEntries for 100
                      endpoints x 65536 identities over a 1000-rule repository
@@ -68,7 +71,6 @@ B_IN_FRAMES = FRAME_STRIDE + 4 + 1 + 2  # slot + len + flags + ep
 B_IN_CT, B_OUT_CT = 22, 9  # saddr daddr sport dport proto l4(2) flags len ep / verdict identity ct_ret
 B_IN_CT6 = 46              # the same with 16-byte addresses
 CT_PKTS_PER_CONN = 32
-CT_SAMPLE = 64  # parity / CPU baseline on the packets of 1 in CT_SAMPLE address pairs
 
 
 def log(*a):
@@ -119,13 +121,13 @@ WORKLOADS = {
           "map emptied each step: ct_lookup4 -> ipcache -> policy -> reply/related skip, "
           "ct_create4 / delete, bit-exact",
     "ctlb": "config2 tables + 1M IPv4 services + stateful conntrack behind the stateful service step "
-            "(cgpu_classify_v4_ctlb, lb4_local with CONNTRACK): 16M packets per GPU of 500k "
+            "(cgpu_classify_v4_ctlb, lb4_local with CONNTRACK): 64M packets per GPU of 2M "
             "connections (~32 packets each, 40 % to services, 0.01 % loopback backends), map emptied "
             "each step: CT_SERVICE lookup/create + slave reuse -> ct_lookup4 -> ipcache -> policy -> "
             "ct_create4 with the service's state and address entry, bit-exact",
     "ctlb6": "IPv6 tables at config-2 size + 100k IPv6 services + stateful conntrack behind the IPv6 "
              "stateful service step (cgpu_classify_v6_ctlb, lb6_local with CONNTRACK over "
-             "cilium_ct6_global): 16M packets per GPU of 500k connections (~32 packets each, 40 % to "
+             "cilium_ct6_global): 64M packets per GPU of 2M connections (~32 packets each, 40 % to "
              "services), map emptied each step: CT_SERVICE lookup/create + slave reuse -> lb6_xlate -> "
              "ct_lookup6 -> ipcache6 -> policy -> ct_create6 with the service's state, bit-exact",
     "ct6": "IPv6 tables at config-2 size (100k IPv6 ipcache prefixes + 64k policy entries) + stateful "
@@ -133,6 +135,34 @@ WORKLOADS = {
            "emptied each step: ct_lookup6 -> ipcache6 -> policy -> reply/related skip, ct_create6 / "
            "delete, bit-exact",
 }
+
+
+def pmc_traffic(args):
+    """roofline.traffic: the HBM-side bytes per step from a PMC profile of
+    the kernels this process actually ran.  profiles/traffic_<config>.json
+    (written by tools/pmc_summary.py, copied in from a profile run) carries
+    the identity of the library it measured; a profile of another build
+    (other sources) is stale and reported as null."""
+    from cilium_amd.build import lib_identity
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if not os.path.exists(tj):
+        return None, f"no PMC profile ({os.path.relpath(tj, ROOT)} absent)", None
+    try:
+        t = json.load(open(tj))
+    except (OSError, ValueError):
+        return None, f"unreadable {os.path.relpath(tj, ROOT)}", None
+    have = lib_identity()
+    was = t.get("library") or {}
+    same = ((was.get("lib_sha256") and was.get("lib_sha256") == have["lib_sha256"]) or
+            (was.get("src_sha256") and was.get("src_sha256") == have.get("src_sha256")))
+    if not same or t.get("config") != args.config:
+        return None, (f"stale: {os.path.relpath(tj, ROOT)} measured sources "
+                      f"{str(was.get('src_sha256'))[:12]} (config {t.get('config')}), this library's "
+                      f"sources {str(have.get('src_sha256'))[:12]}"), None
+    return (t.get("hbm_bytes_per_step"),
+            f"{os.path.relpath(tj, ROOT)}: {t.get('source')}; sources {str(was.get('src_sha256'))[:12]}, "
+            f"built at {str(was.get('git_head'))[:12]}",
+            {"name": t.get("dominant_kernel"), "hbm_bytes_per_launch": t.get("hbm_bytes_per_launch")})
 
 
 def main():
@@ -143,13 +173,17 @@ def main():
     ap.add_argument("--config", default="gpu", choices=sorted(WORKLOADS))
     ap.add_argument("--tuples", type=int, default=0, help="tuples per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the restatement entirely (profiling passes: tools/profile.sh)")
     ap.add_argument("--hot-slots", type=int, default=0,
                     help="cgpu_config.hot_counter_slots (LDS counter slots; 0 = library default)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-rebalance", action="store_true",
                     help="keep the class-based counter slots (no cgpu_counters_rebalance after warmup)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (profiles/*), if present")
+    ap.add_argument("--traffic-json", default="",
+                    help="PMC summary (tools/pmc_summary.py traffic.json) to report as roofline.traffic; "
+                         "default profiles/traffic_<config>.json.  Printed only when it was measured "
+                         "on the library this process loaded")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -177,7 +211,7 @@ def main():
     ct = args.config == "ct" or ct6 or ctlb
     v6 = args.config == "v6"
     cfg = synth.CONFIGS["v6" if ct6 else "gpu" if (pf6 or frames or ct) else args.config]
-    n = args.tuples or (1 << 24 if ctlb else cfg["n_tuples"])
+    n = args.tuples or cfg["n_tuples"]
     t0 = time.time()
     S = None
     if pf6:
@@ -209,7 +243,10 @@ def main():
                                    world=world)
         n = min(n, len(tup["saddr"]))
         tup = {k: np.ascontiguousarray(v[:n]) for k, v in tup.items()}
-        ct_max = 1 << max(20, int(np.ceil(np.log2(2.5 * n / CT_PKTS_PER_CONN))))
+        # entries per connection: ~1.9 plain (forward + ICMP), ~3.4 behind the
+        # service step (+ CT_SERVICE + address entries); the map stays under
+        # half full so no create meets the capacity edge
+        ct_max = 1 << max(20, int(np.ceil(np.log2((4.5 if ctlb else 2.5) * n / CT_PKTS_PER_CONN))))
         log(f"[rank {rank}] synthetic tables ({len(T.ipc_keys)} ipcache, {len(T.pol_keys)} policy) "
             f"+ {n} packets of {n // CT_PKTS_PER_CONN} connections in {time.time() - t0:.1f}s, "
             f"ct_max {ct_max}")
@@ -268,11 +305,17 @@ def main():
                "identity": torch.empty(n, dtype=torch.int32, device=dev), "stage": None}
         if ct:
             out["ct_ret"] = torch.empty(n, dtype=torch.uint8, device=dev)
+        if ctlb:
+            # the frame after the service step (lb4_xlate / lb6_xlate,
+            # lb.h:700-775): part of the reference's result, written every step
+            out["daddr"] = (torch.empty((n, 16), dtype=torch.uint8, device=dev) if ct6 else
+                            torch.empty(n, dtype=torch.int32, device=dev))
+            out["dport"] = torch.empty(n, dtype=torch.int16, device=dev)
     CT_NOW = 1000
     delta = torch.zeros(e.counter_delta_bytes() // 8, dtype=torch.int64, device=dev)
     e.counter_bind(delta)
     stream = torch.cuda.current_stream()
-    if world > 1:
+    def check_layout(when):
         # replicas must map every policy key to the same counter slot before
         # their delta buffers are summed slot by slot
         lay = torch.tensor([e.counter_layout_checksum() & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64,
@@ -280,16 +323,19 @@ def main():
         lo_, hi_ = lay.clone(), lay.clone()
         dist.all_reduce(lo_, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi_, op=dist.ReduceOp.MAX)
-        assert int(lo_) == int(hi_), "counter slot layouts differ across ranks"
+        assert int(lo_) == int(hi_), f"counter slot layouts differ across ranks ({when})"
+
+    if world > 1:
+        check_layout("before warmup")
         shard.init_counter_comm(e, rank, world)
 
     def launch():
         if ctlb and ct6:
-            e.classify_v6_ctlb(d, CT_NOW, out=out, xlate=False, stream=stream)
+            e.classify_v6_ctlb(d, CT_NOW, out=out, stream=stream)
         elif ct6:
             e.classify_v6_ct(d, CT_NOW, out=out, stream=stream)
         elif ctlb:
-            e.classify_v4_ctlb(d, CT_NOW, out=out, xlate=False, stream=stream)
+            e.classify_v4_ctlb(d, CT_NOW, out=out, stream=stream)
         elif ct:
             e.classify_v4_ct(d, CT_NOW, out=out, stream=stream)
         elif pf6:
@@ -329,6 +375,10 @@ def main():
     if not args.no_rebalance and not pf6 and not ct and args.warmup:
         torch.cuda.synchronize()
         moved = e.counters_rebalance()
+        if world > 1:
+            # the rebalance moved slots again: every rank must have moved them
+            # the same way before the timed steps' slot-wise sums
+            check_layout("after counters_rebalance")
         step()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -369,8 +419,10 @@ def main():
         allreduce_ok = bool(int(ok))
         e.counter_fold(stream)
 
-    # counters replicated across ranks must agree
+    # the replicated map contents (cgpu_table_checksum) must agree across
+    # ranks, and so must the counter slot layout the timed sums relied on
     if world > 1:
+        check_layout("after the timed steps")
         cs = torch.tensor([e.checksum() & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64, device=dev)
         lo, hi = cs.clone(), cs.clone()
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
@@ -381,7 +433,12 @@ def main():
     # the CPU baseline is an N=1 figure (rank 0 alone); at N > 1 the
     # restatement runs once, for the parity check of rank 0's batch only
     skip_cpu = args.no_cpu_baseline or world > 1
-    if rank == 0:
+    if rank == 0 and args.no_parity:
+        result = {"metric": METRIC, "value": round(value, 2), "unit": "Mpps", "n_gpus": world,
+                  "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+                  "config": {"workload": WORKLOADS[args.config], "kernel_ms": round(kern_ms, 4),
+                             "parity_vs_oracle": None, "note": "--no-parity profiling pass"}}
+    elif rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from oracle import Oracle  # CPU restatement: checker + CPU baseline only
 
@@ -415,36 +472,64 @@ def main():
                 return o.classify_frames({k: v[sl] for k, v in fr.items()}, nthreads=threads)
             return o.classify_v4({k: v[sl] for k, v in tup.items()}, nthreads=threads)
 
-        if ctlb:
-            # the service step ties pairs together (a service's connections
-            # land on its backends' pairs): the whole batch, sequentially
+        cpu = None
+        if ct:
+            # the stateful restatement (oracle/cgpu_oracle.c or_classify_v{4,6}_ct{,lb}),
+            # threaded over shards with a conntrack map per shard (Oracle.sharded)
+            meth = f"classify_v{6 if ct6 else 4}_ct{'lb' if ctlb else ''}"
             sub = np.arange(n)
-            tsub = tup
-        elif ct:
-            # conntrack groups (unordered address pairs) are independent: the
-            # packets of 1 in CT_SAMPLE pairs, in batch order, replayed by the
-            # sequential restatement from an empty map are the reference's
-            # result for exactly those packets
-            if ct6:
-                sub = np.nonzero((shard.pairhash6_np(tup["saddr"], tup["daddr"]) >> np.uint32(26)) == 0)[0]
+            if ctlb:
+                # parity: the sequential restatement over the whole batch (a
+                # service's connections are tied to its backends' pairs, so no
+                # pair partition is exact); the CPU baseline: the same code
+                # threaded RSS-style by connection (shard.conn_shard_of),
+                # checked against the sequential result
+                c0 = time.perf_counter()
+                r_ = getattr(o, meth)(tup, CT_NOW)
+                seq_s = time.perf_counter() - c0
+                first = (r_["verdict"], r_["ct_ret"], r_["identity"], r_["stage"], r_["probes"])
+                x0 = (r_["xdaddr"], r_["xdport"])
+                if not skip_cpu:
+                    o2 = Oracle(**T.oracle_config())
+                    synth.load_oracle(o2, T)
+                    synth.load_lxc(o2, seclabels)
+                    o2.ct_set_max(ct_max)
+                    o2.ct6_set_max(ct_max)
+                    (synth.load_services6 if ct6 else synth.load_services)(o2, S)
+                    rs, c_el = o2.sharded(meth, tup, CT_NOW, shard.conn_shard_of(tup, 4 * threads),
+                                          threads)
+                    same = float(np.mean((rs["verdict"] == r_["verdict"]) & (rs["ct_ret"] == r_["ct_ret"])))
+                    cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
+                           "kind": "port",
+                           "sample": (f"rank-0 batch, all {n} packets from an empty map; "
+                                      f"oracle/cgpu_oracle.c or_{meth} threaded RSS-style by connection "
+                                      f"(shard.conn_shard_of, {4 * threads} shards, a conntrack map per "
+                                      f"shard) on {threads} threads, {c_el:.2f}s wall of the parallel "
+                                      f"section; {100 * same:.3f} % of its verdicts + ct results equal "
+                                      f"the sequential run's ({seq_s:.1f}s on 1 thread, the parity "
+                                      f"reference); host: {host_cpu()}")}
             else:
-                lo = np.minimum(tup["saddr"], tup["daddr"]).astype(np.uint64)
-                hi = np.maximum(tup["saddr"], tup["daddr"]).astype(np.uint64)
-                hsh = ((lo * np.uint64(0x9E3779B97F4A7C15)) ^ hi) * np.uint64(0xC2B2AE3D27D4EB4F)
-                sub = np.nonzero((hsh >> np.uint64(58)) == 0)[0]
-            tsub = {k: v[sub] for k, v in tup.items()}
+                # address pairs are independent conntrack groups (every key a
+                # packet touches carries its pair): the pair-sharded run is
+                # exactly the sequential result for the whole batch
+                first, c_el = o.sharded(meth, tup, CT_NOW, shard.ct_shard_of(tup, 4 * threads),
+                                        threads)
+                if not skip_cpu:
+                    cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
+                           "kind": "port",
+                           "sample": (f"rank-0 batch, all {n} packets from an empty map; "
+                                      f"oracle/cgpu_oracle.c or_{meth} (sequential conntrack + LPM "
+                                      f"trie + open hash per address-pair shard: "
+                                      f"shard.ct_shard_of, {4 * threads} shards, a conntrack map per "
+                                      f"shard) on {threads} threads, {c_el:.2f}s wall of the parallel "
+                                      f"section; host: {host_cpu()}")}
         elif not skip_cpu:
             cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
         # the median of 3 timed runs (the first also yields the reference result)
         runs = []
-        for rep in range(3):
+        for rep in range(0 if ct else 3):
             c0 = time.perf_counter()
-            if ctlb:
-                r_ = (o.classify_v6_ctlb if ct6 else o.classify_v4_ctlb)(tsub, CT_NOW)
-                res = (r_["verdict"], r_["ct_ret"], r_["identity"], r_["stage"], r_["probes"])
-            elif ct:
-                res = (o.classify_v6_ct if ct6 else o.classify_v4_ct)(tsub, CT_NOW)
-            elif pf6:
+            if pf6:
                 res = o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
             elif cascade:
                 res = o.classify_v4_lb(tup, nthreads=threads)
@@ -457,28 +542,18 @@ def main():
             runs.append(time.perf_counter() - c0)
             if rep == 0:
                 first = res
-            if ct or skip_cpu:
-                break  # the sequential conntrack replay mutates its map
-        c_el = float(np.median(runs))
+            if skip_cpu:
+                break
         if ct:
             v0, cr0, i0, _, probes = first
         elif pf6:
+            c_el = float(np.median(runs))
             v0, probes = first
         else:
+            c_el = float(np.median(runs))
             v0, i0, _, probes = first
-        n_cpu = len(sub) if ct else n
-        cpu = None
-        if not skip_cpu and ct:
-            cpu = {"value": round(n_cpu / c_el / 1e6, 3), "unit": "Mpps", "cores": 1,
-                   "kind": "port",
-                   "sample": (f"rank-0 batch, all {n_cpu} packets from an empty map; "
-                              f"oracle/cgpu_oracle.c or_classify_v{6 if ct6 else 4}_ctlb " if ctlb else
-                              f"rank-0 batch, the {n_cpu} packets of 1/{CT_SAMPLE} of the address "
-                              f"pairs from an empty map; oracle/cgpu_oracle.c "
-                              f"or_classify_v{6 if ct6 else 4}_ct ") +
-                             f"(sequential conntrack + LPM trie + open hash), 1 thread, "
-                             f"{c_el:.2f}s wall (one run); host: {host_cpu()}"}
-        elif not skip_cpu:
+        n_cpu = n
+        if not skip_cpu and not ct:
             what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
                     "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash",
                     "v6": "oracle/cgpu_oracle.c IPv6 LPM trie + open hash",
@@ -490,9 +565,13 @@ def main():
                              f"{threads} threads, median of {len(runs)} runs "
                              f"{'/'.join(f'{x:.2f}' for x in runs)} s; host: {host_cpu()}"}
         if ct:
-            parity = bool(np.array_equal(out["verdict"].cpu().numpy()[sub], v0) and
-                          np.array_equal(out["ct_ret"].cpu().numpy()[sub], cr0) and
-                          np.array_equal(out["identity"].cpu().numpy().view(np.uint32)[sub], i0))
+            parity = bool(np.array_equal(out["verdict"].cpu().numpy(), v0) and
+                          np.array_equal(out["ct_ret"].cpu().numpy(), cr0) and
+                          np.array_equal(out["identity"].cpu().numpy().view(np.uint32), i0))
+            if ctlb:
+                xd = out["daddr"].cpu().numpy()
+                parity = parity and np.array_equal(xd if ct6 else xd.view(np.uint32), x0[0]) and \
+                    np.array_equal(out["dport"].cpu().numpy().view(np.uint16), x0[1])
         else:
             parity = bool(np.array_equal(out["verdict"].cpu().numpy(), v0))
             if not pf6:
@@ -504,14 +583,7 @@ def main():
                        else (B_IN + (2 if cascade else 0), B_OUT))
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        tj = (args.traffic_json if args.config == "gpu"
-              else os.path.join(ROOT, "profiles", f"traffic_{args.config}.json"))
-        if os.path.exists(tj):
-            try:
-                traffic = json.load(open(tj)).get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        traffic, traffic_note, traffic_dom = pmc_traffic(args)
         conf = {"workload": WORKLOADS[args.config], "tuples_per_gpu": n,
                 "parallelism": f"shard{world}", "kernel_ms": round(kern_ms, 4),
                 "stream_tuples_per_step": world * n, "stream_tuples_timed": world * n * args.steps,
@@ -532,13 +604,14 @@ def main():
                 ctr = out["ct_ret"].cpu().numpy()
                 conf.update(ct_max=ct_max,
                             ct_entries_after_step=int(e.ct6_count() if ct6 else e.ct4_count()),
-                            parity_sample_packets=int(len(sub)),
+                            parity_packets=int(len(sub)),
                             ct_state_frac={s_: round(float((ctr == c_).mean()), 4) for s_, c_ in
                                            (("new", 0), ("established", 1), ("reply", 2),
                                             ("related", 3), ("none", 255))},
                             ops_per_packet_note="probes = ipcache + policy probes + CT map "
-                                                "lookups/updates/deletes of the reference, "
-                                                "counted on the parity sample")
+                                                "lookups/updates/deletes of the reference "
+                                                "(+ service lookups), counted by the restatement "
+                                                "over the whole batch")
         result = {
             "metric": METRIC if not pf6 else "Mpps XDP IPv6 prefilter verdicts; % HBM roofline",
             "value": round(value, 2), "unit": "Mpps", "n_gpus": world,
@@ -550,6 +623,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "traffic_source": traffic_note,
+                         "traffic_dominant_kernel": traffic_dom,
                          # achieved counts ALGORITHMIC bytes (64 B per reference map
                          # lookup); the HBM-side rate from the PMC traffic says how
                          # much of the 8 TB/s the kernel really moves: the tables

@@ -7,6 +7,7 @@ GPU box with the repository snapshot; it is git-ignored.
 """
 from __future__ import annotations
 
+import json
 import os
 import subprocess
 import sys
@@ -30,10 +31,72 @@ def hipcc() -> str:
 def stale() -> bool:
     if not os.path.exists(LIB):
         return True
+    if not os.path.exists(BUILD_JSON):
+        _write_build_json()
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(ROOT, "include", "cgpu.h"))
     return any(os.path.getmtime(d) > t for d in deps)
+
+
+BUILD_JSON = os.path.join(HERE, "libcgpu.build.json")
+
+
+def _sha256(path: str) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def src_sha256() -> str:
+    """Hash of the library's sources (csrc + include/cgpu.h): what a build
+    of them contains, independent of where and when it was compiled."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted([os.path.join(CSRC, f) for f in SOURCES + HEADERS] +
+                    [os.path.join(ROOT, "include", "cgpu.h")]):
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def lib_identity(path: str = LIB) -> dict:
+    """The identity of the library file at `path` (the one a process loads):
+    its own sha256 and, from libcgpu.build.json when that describes this very
+    file, the sources it was built from and the git HEAD at build time.
+    Profile summaries (tools/pmc_summary.py) are stamped with it and
+    bench.py prints a PMC traffic figure only for the identity it loaded."""
+    ident = {"lib_sha256": _sha256(path) if os.path.exists(path) else None,
+             "src_sha256": None, "git_head": None}
+    try:
+        b = json.load(open(BUILD_JSON))
+        if b.get("lib_sha256") == ident["lib_sha256"]:
+            ident.update(src_sha256=b.get("src_sha256"), git_head=b.get("git_head"),
+                         git_dirty=b.get("git_dirty"))
+    except (OSError, ValueError):
+        pass
+    return ident
+
+
+def _write_build_json() -> None:
+    head, dirty = None, None
+    try:
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "HEAD"], capture_output=True,
+                              text=True, check=True).stdout.strip()
+        dirty = bool(subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--",
+                                     "cilium_amd/csrc", "include"], capture_output=True, text=True,
+                                    check=True).stdout.strip())
+    except (OSError, subprocess.CalledProcessError):
+        pass
+    rec = {"lib_sha256": _sha256(LIB), "src_sha256": src_sha256(), "git_head": head,
+           "git_dirty": dirty, "arch": ARCH}
+    with open(BUILD_JSON + ".tmp", "w") as f:
+        json.dump(rec, f, indent=1)
+    os.replace(BUILD_JSON + ".tmp", BUILD_JSON)
 
 
 def build(force: bool = False, verbose: bool = False, defines=(), out: str = LIB) -> str:
@@ -64,6 +127,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str = LIB
     os.replace(tmp, out)
     for o in objs:
         os.remove(o)
+    if out == LIB:
+        _write_build_json()
     return out
 
 

@@ -5473,6 +5473,102 @@ CGPU_EXPORT int cgpu_mirror_save(cgpu_ctx *c, const char *path)
 	return 0;
 }
 
+struct MirSec {
+	uint32_t tag, rec;
+	uint64_t n;
+	size_t off;
+};
+
+struct CgpuConfigCaps {
+	uint64_t ipcache, policy_per_ep, endpoints, lb, ct4, ct6;
+};
+
+static CgpuConfigCaps config_caps(const cgpu_ctx *c)
+{
+	return CgpuConfigCaps{c->cfg.ipcache_max, c->cfg.policy_max_per_ep, c->cfg.endpoints_max,
+			      c->cfg.lb_max_entries, c->ct4.max, c->ct6.max};
+}
+
+/* undo a partial replay: delete, newest first, every record of sections
+ * [0, si) and records [0, upto) of section si (each was a NOEXIST insert
+ * into the empty context), and put the prefilter revision back */
+static void mirror_rollback(cgpu_ctx *c, const std::vector<uint8_t> &buf, const std::vector<MirSec> &secs,
+			    size_t si, uint64_t upto, int64_t rev0)
+{
+	for (size_t k = si + 1; k-- > 0;) {
+		const MirSec &s_ = secs[k];
+		const uint64_t n = k == si ? upto : s_.n;
+		for (uint64_t i = n; i-- > 0;) {
+			const uint8_t *r = &buf[s_.off + i * s_.rec];
+			switch (s_.tag) {
+			case MIR_IPC: {
+				cgpu_ipcache_key key;
+				memcpy(&key, r, 24);
+				cgpu_ipcache_delete(c, &key);
+				break;
+			}
+			case MIR_POL: {
+				uint32_t ep;
+				cgpu_policy_key key;
+				memcpy(&ep, r, 4);
+				memcpy(&key, r + 4, 8);
+				cgpu_policy_delete(c, ep, &key);
+				break;
+			}
+			case MIR_CIDR: {
+				uint32_t which;
+				cgpu_cidr_key key;
+				memcpy(&which, r, 4);
+				memcpy(&key, r + 4, 20);
+				cgpu_cidr_delete(c, (int)which, &key);
+				break;
+			}
+			case MIR_EP: {
+				cgpu_endpoint_key key;
+				memcpy(&key, r, 20);
+				cgpu_endpoint_delete(c, &key);
+				break;
+			}
+			case MIR_LB4: {
+				cgpu_lb4_key key;
+				memcpy(&key, r, 8);
+				cgpu_lb4_delete(c, &key);
+				break;
+			}
+			case MIR_LB6: {
+				cgpu_lb6_key key;
+				memcpy(&key, r, 20);
+				cgpu_lb6_delete(c, &key);
+				break;
+			}
+			case MIR_LXC: {
+				uint32_t ep;
+				memcpy(&ep, r, 4);
+				cgpu_lxc_delete(c, ep);
+				break;
+			}
+			case MIR_REV: {
+				std::lock_guard<std::mutex> g(c->mu);
+				c->pf_revision = rev0;
+				break;
+			}
+			case MIR_CT4: {
+				cgpu_ct4_tuple key;
+				memcpy(&key, r, 14);
+				cgpu_ct4_delete(c, &key);
+				break;
+			}
+			case MIR_CT6: {
+				cgpu_ct6_tuple key;
+				memcpy(&key, r, 38);
+				cgpu_ct6_delete(c, &key);
+				break;
+			}
+			}
+		}
+	}
+}
+
 CGPU_EXPORT int cgpu_mirror_restore(cgpu_ctx *c, const char *path)
 {
 	if (!c || !path)
@@ -5513,11 +5609,7 @@ CGPU_EXPORT int cgpu_mirror_restore(cgpu_ctx *c, const char *path)
 			return fail(-EEXIST, "restore needs an empty context");
 	}
 	/* validate the section structure before applying anything */
-	struct Sec {
-		uint32_t tag, rec;
-		uint64_t n;
-		size_t off;
-	};
+	typedef MirSec Sec;
 	std::vector<Sec> secs;
 	size_t off = 16;
 	const size_t end = buf.size() - 8;
@@ -5538,8 +5630,49 @@ CGPU_EXPORT int cgpu_mirror_restore(cgpu_ctx *c, const char *path)
 	}
 	if (off != end)
 		return fail(-EINVAL, "%s: trailing bytes", path);
-	/* replay through the map calls (the listeners' path) */
-	for (const Sec &s_ : secs)
+	/* capacities of this context against the snapshot's record counts: a
+	 * context configured smaller than the one that saved the file is refused
+	 * before anything is applied */
+	{
+		uint64_t cnt[MIR_CT6 + 1] = {};
+		std::map<uint32_t, uint64_t> per_ep;
+		for (const Sec &s_ : secs) {
+			cnt[s_.tag] += s_.n;
+			if (s_.tag == MIR_POL)
+				for (uint64_t i = 0; i < s_.n; i++) {
+					uint32_t ep;
+					memcpy(&ep, &buf[s_.off + i * s_.rec], 4);
+					per_ep[ep]++;
+				}
+		}
+		const CgpuConfigCaps cap = config_caps(c);
+		const struct {
+			int tag;
+			uint64_t max;
+			const char *what;
+		} lim[] = {{MIR_IPC, cap.ipcache, "ipcache_max"},   {MIR_EP, cap.endpoints, "endpoints_max"},
+			   {MIR_LB4, cap.lb, "lb_max_entries (lb4)"}, {MIR_LB6, cap.lb, "lb_max_entries (lb6)"},
+			   {MIR_CT4, cap.ct4, "ct_max"},              {MIR_CT6, cap.ct6, "ct6_max"}};
+		for (const auto &l : lim)
+			if (cnt[l.tag] > l.max)
+				return fail(-E2BIG, "%s: %llu records exceed this context's %s (%llu)", path,
+					    (unsigned long long)cnt[l.tag], l.what, (unsigned long long)l.max);
+		for (const auto &kv : per_ep)
+			if (kv.second > cap.policy_per_ep)
+				return fail(-E2BIG, "%s: %llu policy keys of endpoint %u exceed policy_max_per_ep (%llu)",
+					    path, (unsigned long long)kv.second, kv.first,
+					    (unsigned long long)cap.policy_per_ep);
+	}
+	/* replay through the map calls (the listeners' path); a record that
+	 * still fails (a per-family limit, a bad key) rolls every applied record
+	 * back, so the context is empty again and the restore can be retried */
+	int64_t rev0;
+	{
+		std::lock_guard<std::mutex> g(c->mu);
+		rev0 = c->pf_revision;
+	}
+	for (size_t si = 0; si < secs.size(); si++) {
+		const Sec &s_ = secs[si];
 		for (uint64_t i = 0; i < s_.n; i++) {
 			const uint8_t *r = &buf[s_.off + i * s_.rec];
 			int rc = 0;
@@ -5622,9 +5755,12 @@ CGPU_EXPORT int cgpu_mirror_restore(cgpu_ctx *c, const char *path)
 				break;
 			}
 			}
-			if (rc)
+			if (rc) {
+				mirror_rollback(c, buf, secs, si, i, rev0);
 				return rc;
+			}
 		}
+	}
 	return 0;
 }
 

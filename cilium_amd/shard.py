@@ -131,6 +131,25 @@ def ct_shard_of(t: dict, world: int) -> np.ndarray:
     return (pairhash_np(t["saddr"], t["daddr"]) % np.uint32(world)).astype(np.int64)
 
 
+def conn_shard_of(t: dict, world: int) -> np.ndarray:
+    """RSS-style owner of every packet of the service path: a hash of the
+    local side of its connection (the endpoint address and port, the
+    protocol), the same for both directions whatever address the remote side
+    shows (service VIP or backend).  Used to thread the CPU restatement of
+    cgpu_classify_v{4,6}_ctlb (bench.py cpu_baseline); unlike ct_shard_of
+    it is not a partition into independent conntrack groups (ICMP-related and
+    address entries cross connections), so bench.py compares its result with
+    the sequential run."""
+    eg = (np.asarray(t["flags"]) & 1).astype(bool)
+    sa, da = np.asarray(t["saddr"]), np.asarray(t["daddr"])
+    if sa.ndim == 2:
+        sa, da = fold6_np(sa), fold6_np(da)
+    loc = np.where(eg, sa, da).astype(np.uint32)
+    lport = np.where(eg, t["sport"], t["dport"]).astype(np.uint32)
+    return (flowhash_np(loc, np.zeros_like(loc), lport, np.zeros_like(lport), t["proto"]) %
+            np.uint32(world)).astype(np.int64)
+
+
 def take(t: dict, idx) -> dict:
     return {k: np.ascontiguousarray(v[idx]) for k, v in t.items()}
 

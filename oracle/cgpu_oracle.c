@@ -428,6 +428,48 @@ void or_destroy(or_ctx *c)
 	free(c);
 }
 
+/* Shard views for the threaded stateful runs (bench.py cpu_baseline and the
+ * full-batch parity of the conntrack paths): a view shares every table of
+ * `base` (ipcache, endpoint policy maps with their atomic counters,
+ * services, lxc info) and owns an empty pair of conntrack maps (sized as the
+ * base's) and its own metrics.  Packets of independent conntrack groups run
+ * in separate views on separate threads, as the reference's datapath runs
+ * them on separate CPUs; or_view_merge folds a finished view back. */
+or_ctx *or_view_create(or_ctx *base)
+{
+	or_ctx *v = malloc(sizeof(*v));
+	*v = *base;
+	oh_init(&v->ct, 14, 56);
+	oh_init(&v->ct6, 38, 56);
+	memset(v->metrics, 0, sizeof(v->metrics));
+	return v;
+}
+
+/* metrics summed into base, every conntrack entry of the view written into
+ * base's maps (BPF_ANY); the view's maps are freed (the view stays usable) */
+void or_view_merge(or_ctx *base, or_ctx *v)
+{
+	for (size_t i = 0; i < N_METRICS; i++)
+		base->metrics[i] += v->metrics[i];
+	for (size_t i = 0; i < v->ct.cap; i++)
+		if (v->ct.used[i])
+			oh_update(&base->ct, v->ct.keys + i * 14, v->ct.vals + i * 56);
+	for (size_t i = 0; i < v->ct6.cap; i++)
+		if (v->ct6.used[i])
+			oh_update(&base->ct6, v->ct6.keys + i * 38, v->ct6.vals + i * 56);
+	oh_destroy(&v->ct);
+	oh_destroy(&v->ct6);
+}
+
+void or_view_destroy(or_ctx *v)
+{
+	if (!v)
+		return;
+	oh_destroy(&v->ct);
+	oh_destroy(&v->ct6);
+	free(v);
+}
+
 void or_set_config(or_ctx *c, const or_config *cfg)
 {
 	c->cfg = *cfg;

@@ -251,6 +251,12 @@ int or_l3_compile(const void *selectors, const void *reqs, const uint32_t *value
 		  const uint32_t *id_off, const void *id_labels, uint32_t n_id, uint32_t flags,
 		  uint8_t *allow);
 
+/* shard views (threaded stateful runs): share base's tables, own empty
+ * conntrack maps and metrics; merge folds a finished view into base */
+or_ctx *or_view_create(or_ctx *base);
+void or_view_merge(or_ctx *base, or_ctx *v);
+void or_view_destroy(or_ctx *v);
+
 /* metrics {reason, dir} -> {count, bytes}; out is [256][4][2] u64 */
 void or_metrics_read(or_ctx *c, uint64_t *out);
 void or_counters_reset(or_ctx *c);

@@ -110,6 +110,12 @@ def lib():
             C.POINTER(C.c_uint64)]
         u32 = C.c_uint32
         L.or_l3_compile.argtypes = [vp, vp, vp, vp, vp, u32, vp, vp, vp, u32, vp, vp, u32, u32, vp]
+        L.or_view_create.argtypes = [vp]
+        L.or_view_create.restype = vp
+        L.or_view_merge.argtypes = [vp, vp]
+        L.or_view_merge.restype = None
+        L.or_view_destroy.argtypes = [vp]
+        L.or_view_destroy.restype = None
         L.or_metrics_read.argtypes = [vp, vp]
         L.or_counters_reset.argtypes = [vp]
         _lib = L
@@ -488,6 +494,79 @@ class Oracle:
         assert rc == 0, rc
         out["probes"] = probes.value
         return out
+
+    # --- threaded stateful runs over independent shards ---
+    def sharded(self, method, t, now, shard, nthreads):
+        """Run the stateful `method` ("classify_v4_ct", "classify_v6_ct",
+        "classify_v4_ctlb", "classify_v6_ctlb") over the packets of `t`
+        split by `shard` (one id per packet), each shard on its own thread
+        in a view with its own conntrack maps starting EMPTY (this context's
+        maps must be empty), packets of a shard in batch order.  For shards
+        that share no conntrack key (shard.ct_shard_of: every key a packet
+        touches carries its address pair) this is exactly the sequential
+        result.  Returns (results in batch order as `method` returns them,
+        the wall seconds of the parallel section alone).  Afterwards this
+        context holds the union of the shard maps and the summed metrics."""
+        import threading
+        import time as _time
+        assert self.ct4_count() == 0 and self.ct6_count() == 0, "sharded run needs empty CT maps"
+        shard = np.asarray(shard)
+        ids = np.unique(shard)
+        order = np.argsort(shard, kind="stable")
+        bounds = np.searchsorted(shard[order], ids, side="left").tolist() + [len(order)]
+        parts = [order[bounds[k]:bounds[k + 1]] for k in range(len(ids))]
+        subs = [{k: (None if v is None else np.ascontiguousarray(v[p])) for k, v in t.items()}
+                for p in parts]
+        views = [Oracle.__new__(Oracle) for _ in parts]
+        for v in views:
+            v.L, v.cfg = self.L, self.cfg
+            v.h = self.L.or_view_create(self.h)
+        res = [None] * len(parts)
+        nxt = [0]
+        lock = threading.Lock()
+
+        def run():
+            while True:
+                with lock:
+                    k = nxt[0]
+                    nxt[0] += 1
+                if k >= len(parts):
+                    return
+                res[k] = getattr(views[k], method)(subs[k], now)
+
+        th = [threading.Thread(target=run) for _ in range(max(1, min(nthreads, len(parts))))]
+        c0 = _time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        wall = _time.perf_counter() - c0
+        for v in views:
+            self.L.or_view_merge(self.h, v.h)
+            self.L.or_view_destroy(v.h)
+            v.h = None
+        n = len(t["saddr"])
+        if isinstance(res[0], dict):
+            out = {}
+            for key, val in res[0].items():
+                if key == "probes":
+                    out[key] = sum(r[key] for r in res)
+                    continue
+                a = np.empty((n,) + val.shape[1:], val.dtype)
+                for p, r in zip(parts, res):
+                    a[p] = r[key]
+                out[key] = a
+            return out, wall
+        outs = []
+        for j, val in enumerate(res[0]):
+            if not isinstance(val, np.ndarray):
+                outs.append(sum(r[j] for r in res))
+                continue
+            a = np.empty((n,) + val.shape[1:], val.dtype)
+            for p, r in zip(parts, res):
+                a[p] = r[j]
+            outs.append(a)
+        return tuple(outs), wall
 
     # --- L3 MapState compilation (SURVEY §8f row 4) ---
     @staticmethod

@@ -112,27 +112,44 @@ def test_classify_frames_vs_restatement(torch_cuda, gate, verify):
     e.close()
 
 
+@pytest.mark.parametrize("kind", ["runt", "v6", "not_classified"])
 @pytest.mark.parametrize("tail", [1, 2, 3])
-def test_classify_frames_ragged_tail(torch_cuda, tail):
+def test_classify_frames_ragged_tail(torch_cuda, tail, kind):
     """Batches of 4k + tail frames whose last partial quad starts with a frame
-    the parse drops: the x4 schedule's tail lanes repeat that frame's columns
-    and must count nothing (verdicts, stages and metrics equal the
-    restatement's)."""
+    the x4 schedule does not carry through its cascade: a runt the parse
+    drops (DROP_INVALID, counted in the metrics), an IPv6 frame (its v4
+    columns are placeholders until the v6 pass scatters its result back) or
+    an egress ARP frame (FRAME_NOT_CLASSIFIED: stage 7, no metrics).  The
+    tail lanes repeat that frame's columns and must count nothing: verdicts,
+    identities, stages and metrics equal the restatement's."""
     T = synth.make_tables(n_prefixes=2000, n_identities=100, n_endpoints=5, keys_per_ep=500)
     rng = np.random.Generator(np.random.PCG64(0x7A11 + tail))
     pool = T.pfx_addr.astype(np.uint32).byteswap()
     n = 4 * 5000 + tail
     f = synth.make_frames(rng, n, width=128, addr4=pool)
-    f["len"][n - tail] = 10  # a runt: DROP_INVALID, counted in the metrics
+    o = frame_oracle(1, 7, **T.oracle_config())
+    synth.load_oracle(o, T)
+    at = n - tail
+    if kind == "runt":
+        f["len"][at] = 10
+    else:
+        p = o.frames_parse(f)
+        want = (p["status"] == 0) & (p["family"] == 6) if kind == "v6" else \
+            p["status"] == L.FRAME_NOT_CLASSIFIED
+        j = int(np.flatnonzero(want[:at])[0])
+        for k in ("data", "len", "flags", "ep"):
+            f[k][at] = f[k][j]
     e = _engine(1, 7, **T.engine_config())
     synth.load_engine(e, T)
     e.commit()
-    o = frame_oracle(1, 7, **T.oracle_config())
-    synth.load_oracle(o, T)
     v, idt, st = _classify_frames(torch_cuda, e, f)
     ov, oi, ost, _ = o.classify_frames(f, nthreads=4)
-    assert ov[n - tail] == L.DROP_INVALID
+    if kind == "runt":
+        assert ov[at] == L.DROP_INVALID
+    elif kind == "not_classified":
+        assert ost[at] == 7
     np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(idt, oi)
     np.testing.assert_array_equal(st, ost)
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     e.close()

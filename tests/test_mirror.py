@@ -127,3 +127,50 @@ def test_mirror_rejects_bad_files(tmp_path, damage):
     assert f.ipcache_keys() == [] and f.ct4_count() == 0  # nothing applied
     e.close()
     f.close()
+
+
+def _empty(f):
+    return (f.ipcache_keys() == [] and f.ct4_count() == 0 and f.ct6_count() == 0 and
+            all(len(f.policy_dump(ep)[0]) == 0 for ep in range(4)) and f.lb4_keys() == [] and
+            PreFilter(f).Revision() == 1)
+
+
+@pytest.mark.parametrize("cap", [{"ct_max": 16}, {"ct6_max": 16}, {"ipcache_max": 100},
+                                 {"policy_max_per_ep": 64}, {"lb_max_entries": 8}])
+def test_mirror_restore_refuses_smaller_context(tmp_path, cap):
+    """a target configured smaller than the saver is refused with
+    -E2BIG before any record is applied."""
+    e = _populated()
+    path = str(tmp_path / "mirror.bin")
+    e.mirror_save(path)
+    kw = {"ct_max": 4096, "lb_max_entries": 1 << 16}
+    kw.update(cap)
+    f = Engine(device=-1, **kw)
+    with pytest.raises(CgpuError) as ex:
+        f.mirror_restore(path)
+    assert ex.value.errno == errno.E2BIG
+    assert _empty(f)
+    e.close()
+    f.close()
+
+
+def test_mirror_restore_rolls_back_partial_replay(tmp_path):
+    """A record that fails during the replay itself (here the total policy
+    capacity, which the per-section precheck does not cover) rolls back
+    every record already applied: the context is empty again, and a retry
+    fails the same way rather than with -EEXIST."""
+    e = _populated()
+    path = str(tmp_path / "mirror.bin")
+    e.mirror_save(path)
+    f = Engine(device=-1, ct_max=4096, lb_max_entries=1 << 16, policy_max_total=400)
+    for _ in range(2):
+        with pytest.raises(CgpuError) as ex:
+            f.mirror_restore(path)
+        assert ex.value.errno in (errno.E2BIG, errno.ENOSPC)
+        assert _empty(f)
+    # a context of the saver's size takes the same file
+    g = Engine(device=-1, ct_max=4096, lb_max_entries=1 << 16)
+    g.mirror_restore(path)
+    assert _state(g) == _state(e)
+    for x in (e, f, g):
+        x.close()

@@ -180,3 +180,29 @@ def test_ct_workload_rank_streams_are_pair_shards():
     for r in range(3):
         t, _, _ = synth.make_ct_workload(T, 2000, gpu_id=r, world=3)
         assert (shard.ct_shard_of(t, 3) == r).all()
+
+
+def test_config4_rank_streams_partition_by_shard_of():
+    """bench.py config 4 at world 8: every rank draws its own seeded tuples
+    and redraws source ports (shard.assign_shard_sports) until each tuple
+    hashes to that rank.  The union of the 8 rank streams is then exactly
+    partitioned by shard_of: every tuple is owned by the rank that holds it,
+    no rank's stream is empty, and the redraw leaves the tuples' other
+    fields as generated."""
+    T = synth.make_tables(n_prefixes=500, n_identities=50, keys_per_ep=300)
+    world, n = 8, 20_000
+    streams = []
+    for r in range(world):
+        t = synth.make_tuples(T, n, gpu_id=r)
+        before = {k: v.copy() for k, v in t.items() if k != "sport"}
+        t["sport"] = shard.assign_shard_sports(t, world, r, seed=synth.SEED + 0x5B0 + r)
+        assert (shard.shard_of(t, world) == r).all()
+        for k, v in before.items():
+            np.testing.assert_array_equal(t[k], v)
+        streams.append(t)
+    union = {k: np.concatenate([s[k] for s in streams]) for k in streams[0]}
+    owner = shard.shard_of(union, world)
+    np.testing.assert_array_equal(owner, np.repeat(np.arange(world), n))
+    assert np.bincount(owner, minlength=world).tolist() == [n] * world
+    # the ranks' streams differ (per-rank seeds), so the stream is world x n tuples
+    assert not np.array_equal(streams[0]["saddr"], streams[1]["saddr"])

@@ -11,7 +11,7 @@ mkdir -p $OUT
 if [ -n "$TESTS" ]; then
   timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v --tb=short --timeout 150 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest.log
-  [ $rc -le 1 ] || exit $rc
+  [ $rc -eq 0 ] || { echo FAILED > $OUT/FAILED; exit $rc; }
 fi
 for C in $CONFS; do
   NAME=${C%%:*}; EXTRA=${C#*:}; [ "$EXTRA" = "$C" ] && EXTRA=""

@@ -12,11 +12,11 @@ mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
-[ $rc -le 1 ] || exit $rc
+[ $rc -eq 0 ] || { echo FAILED > $OUT/FAILED; exit $rc; }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 rc=$?
 echo "smoke rc=$rc"; tail -1 $OUT/smoke.log
-[ $rc -le 1 ] || exit $rc
+[ $rc -eq 0 ] || { echo FAILED > $OUT/FAILED; exit $rc; }
 [ $# -gt 0 ] || set -- gpu
 for C in "$@"; do
   NAME=${C%%:*}; EXTRA=${C#*:}; [ "$EXTRA" = "$C" ] && EXTRA=""
