@@ -137,6 +137,25 @@ WORKLOADS = {
 }
 
 
+def link_rates(torch, dev, nbytes=1 << 30):
+    """Host <-> device copy rates over page-locked memory (GB/s), each
+    direction alone, best of 3: the link the host-resident line rides on."""
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    g = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    out = {}
+    for name, dst, src in (("h2d", g, h), ("d2h", h, g)):
+        best = 0.0
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            best = max(best, nbytes / (time.perf_counter() - t0) / 1e9)
+        out[name] = round(best, 2)
+    del h, g
+    return out
+
+
 def pmc_traffic(args):
     """roofline.traffic: the HBM-side bytes per step from a PMC profile of
     the kernels this process actually ran.  profiles/traffic_<config>.json
@@ -144,6 +163,8 @@ def pmc_traffic(args):
     the identity of the library it measured; a profile of another build
     (other sources) is stale and reported as null."""
     from cilium_amd.build import lib_identity
+    if getattr(args, "host_tuples", False):
+        return None, "not profiled: the host-resident line is bound by the host link", None
     tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if not os.path.exists(tj):
         return None, f"no PMC profile ({os.path.relpath(tj, ROOT)} absent)", None
@@ -173,6 +194,9 @@ def main():
     ap.add_argument("--config", default="gpu", choices=sorted(WORKLOADS))
     ap.add_argument("--tuples", type=int, default=0, help="tuples per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-tuples", action="store_true",
+                    help="config 2 with the batch in page-locked host memory (cgpu_classify_v4_host): "
+                         "the PCIe-inclusive rate, reported beside the link's ingest bound")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the restatement entirely (profiling passes: tools/profile.sh)")
     ap.add_argument("--hot-slots", type=int, default=0,
@@ -203,6 +227,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    if args.host_tuples and args.config != "gpu":
+        raise SystemExit("--host-tuples measures config 2 (--config gpu) only")
     pf6 = args.config == "pf6"
     cascade = args.config == "cascade"
     frames = args.config == "frames"
@@ -299,6 +325,15 @@ def main():
         d = synth.frames_to_device(fr, dev)
         out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
                "identity": torch.empty(n, dtype=torch.int32, device=dev), "stage": None}
+    elif args.host_tuples:
+        # the batch in page-locked HOST memory, outputs back into it: every
+        # step uploads the columns and downloads the verdicts through
+        # cgpu_classify_v4_host (PCIe-inclusive)
+        view = {np.uint32: np.int32, np.uint16: np.int16, np.uint8: np.uint8}
+        d = {k: torch.from_numpy(np.ascontiguousarray(tup[k], dt).view(view[dt])).pin_memory()
+             for k, dt in synth.TUPLE_DTYPES.items() if k in tup}
+        out = {"verdict": torch.empty(n, dtype=torch.int32).pin_memory(),
+               "identity": torch.empty(n, dtype=torch.int32).pin_memory(), "stage": None}
     else:
         d = synth.to_device(tup, dev)
         out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
@@ -346,6 +381,8 @@ def main():
             e.classify_v6(d, out=out, stream=stream)
         elif frames:
             e.classify_frames(d, out=out, stream=stream)
+        elif args.host_tuples:
+            e.classify_v4_host(d, out=out, stream=stream)
         else:
             e.classify_v4(d, out=out, stream=stream)
 
@@ -593,6 +630,16 @@ def main():
                                   f"popularity-rebalanced after warmup ({moved} keys moved)"),
                 "probes_per_tuple": round(probes_per, 4), "b_alg_per_tuple": round(b_alg, 2),
                 "parity_vs_oracle": parity}
+        if args.host_tuples:
+            bw = link_rates(torch, dev)
+            per_in, per_out = B_IN, B_OUT  # bytes up / down per tuple
+            conf.update(host_tuples=True,
+                        pcie_measured_gbs=bw,
+                        ingest_bound_mpps=round(min(bw["h2d"] * 1e3 / per_in, bw["d2h"] * 1e3 / per_out), 1),
+                        note=("PCIe-inclusive: the columns (18 B/tuple) go up and the verdict + identity "
+                              "(8 B) come down every step through double-buffered 4M-tuple chunks; "
+                              "ingest_bound_mpps = the measured link rate over those bytes. The "
+                              "HBM-resident rate is the default line (no --host-tuples)"))
         if pf6:
             conf.update(dyn6_prefixes=len(P.dyn6), fix6_prefixes=len(P.fix6),
                         endpoints=len(P.ep6))
@@ -613,7 +660,8 @@ def main():
                                                 "(+ service lookups), counted by the restatement "
                                                 "over the whole batch")
         result = {
-            "metric": METRIC if not pf6 else "Mpps XDP IPv6 prefilter verdicts; % HBM roofline",
+            "metric": ("Mpps classified from host-resident batches (PCIe-inclusive)" if args.host_tuples
+                       else METRIC if not pf6 else "Mpps XDP IPv6 prefilter verdicts; % HBM roofline"),
             "value": round(value, 2), "unit": "Mpps", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

@@ -137,6 +137,7 @@ PROTOS = {
     "cgpu__test_corrupt": (i32, [vp, i32, sz, C.c_uint8]),
     "cgpu_counter_layout_checksum": (i32, [vp, C.POINTER(u64)]),
     "cgpu_classify_v4": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
+    "cgpu_classify_v4_host": (i32, [vp, C.POINTER(TuplesV4), sz, vp, vp, vp, vp]),
     "cgpu_classify_v6": (i32, [vp, C.POINTER(TuplesV6), sz, vp, vp, vp, vp]),
     "cgpu_classify_v6_lb": (i32, [vp, C.POINTER(TuplesV6), vp, vp, sz, vp, vp, vp, vp]),
     "cgpu_classify_v4_lb": (i32, [vp, C.POINTER(TuplesV4), vp, vp, sz, vp, vp, vp, vp]),

@@ -1884,6 +1884,15 @@ struct cgpu_ctx {
 	/* ---- conntrack maps cilium_ct4_global / cilium_ct6_global ---- */
 	CtMap ct4, ct6;
 	void *d_ct_scratch = nullptr;
+	/* host-resident batches (cgpu_classify_v4_host): double-buffered device
+	 * staging, one copy stream per direction */
+	std::mutex host_mu;
+	struct {
+		size_t chunk = 0;
+		void *d_in[2] = {}, *d_out[2] = {};
+		hipStream_t h2d = nullptr, d2h = nullptr;
+		hipEvent_t ev_in[2] = {}, ev_cls[2] = {}, ev_out[2] = {};
+	} hs;
 	size_t ct_scratch_cap = 0;
 	hipStream_t ct_stream = nullptr; /* the conntrack path's internal stream */
 	hipEvent_t ct_done = nullptr;
@@ -2144,6 +2153,19 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 			(void)hipFree(m->d_count);
 		}
 		(void)hipFree(c->d_ct_scratch);
+		if (c->hs.chunk) {
+			(void)hipStreamSynchronize(c->hs.h2d);
+			(void)hipStreamSynchronize(c->hs.d2h);
+			for (int b = 0; b < 2; b++) {
+				(void)hipFree(c->hs.d_in[b]);
+				(void)hipFree(c->hs.d_out[b]);
+				(void)hipEventDestroy(c->hs.ev_in[b]);
+				(void)hipEventDestroy(c->hs.ev_cls[b]);
+				(void)hipEventDestroy(c->hs.ev_out[b]);
+			}
+			(void)hipStreamDestroy(c->hs.h2d);
+			(void)hipStreamDestroy(c->hs.d2h);
+		}
 		(void)hipEventDestroy(c->ct_done);
 		(void)hipStreamDestroy(c->ct_stream);
 		(void)hipStreamDestroy(c->ustream);
@@ -4152,6 +4174,114 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
 	return 0;
 }
 
+/* ---- host-resident batches (host or device pointers) ----
+ * The batch streams through two device staging buffers of HS_CHUNK tuples:
+ * chunk k's columns go up on the h2d stream, its classify runs on the
+ * caller's stream, its outputs come back on the d2h stream, so chunk k + 1's
+ * upload and chunk k - 1's download overlap chunk k's classify. */
+#define HS_CHUNK (1u << 22)
+
+static size_t hs_in_off(size_t m, int col)
+{
+	/* saddr, daddr, dport, proto, flags, len, ep; each column 256-aligned */
+	static const size_t el[7] = {4, 4, 2, 1, 1, 4, 2};
+	size_t o = 0;
+	for (int k = 0; k < col; k++)
+		o += (m * el[k] + 255) & ~(size_t)255;
+	return o;
+}
+
+static size_t hs_out_off(size_t m, int col)
+{
+	static const size_t el[3] = {4, 4, 1}; /* verdict, identity, stage */
+	size_t o = 0;
+	for (int k = 0; k < col; k++)
+		o += (m * el[k] + 255) & ~(size_t)255;
+	return o;
+}
+
+static int host_stage_init(cgpu_ctx *c)
+{
+	auto &H = c->hs;
+	if (H.chunk)
+		return 0;
+	for (int b = 0; b < 2; b++) {
+		HIP_OR_EIO(hipMalloc(&H.d_in[b], hs_in_off(HS_CHUNK, 7)));
+		HIP_OR_EIO(hipMalloc(&H.d_out[b], hs_out_off(HS_CHUNK, 3)));
+		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_in[b], hipEventDisableTiming));
+		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_cls[b], hipEventDisableTiming));
+		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_out[b], hipEventDisableTiming));
+	}
+	HIP_OR_EIO(hipStreamCreateWithFlags(&H.h2d, hipStreamNonBlocking));
+	HIP_OR_EIO(hipStreamCreateWithFlags(&H.d2h, hipStreamNonBlocking));
+	H.chunk = HS_CHUNK;
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
+				      uint32_t *identity, uint8_t *stage, void *stream)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
+			 !t->ep || !verdict || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device (host-only); no CPU path");
+	if (!n)
+		return 0;
+	std::lock_guard<std::mutex> g(c->host_mu);
+	HIP_OR_EIO(hipSetDevice(c->device));
+	if (int r = host_stage_init(c))
+		return r;
+	auto &H = c->hs;
+	const hipStream_t cs = (hipStream_t)stream;
+	bool used[2] = {false, false};
+	for (size_t off = 0, k = 0; off < n; off += H.chunk, k++) {
+		const size_t m = std::min<size_t>(H.chunk, n - off);
+		const int b = (int)(k & 1u);
+		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]), *out = static_cast<uint8_t *>(H.d_out[b]);
+		/* the input buffer is free once chunk k - 2's classify ran */
+		if (used[b])
+			HIP_OR_EIO(hipStreamWaitEvent(H.h2d, H.ev_cls[b], 0));
+		const void *src[7] = {t->saddr + off, t->daddr + off, t->dport + off, t->proto + off,
+				      t->flags + off, t->len + off, t->ep + off};
+		static const size_t el[7] = {4, 4, 2, 1, 1, 4, 2};
+		for (int col = 0; col < 7; col++)
+			HIP_OR_EIO(hipMemcpyAsync(in + hs_in_off(m, col), src[col], m * el[col], hipMemcpyHostToDevice,
+						  H.h2d));
+		HIP_OR_EIO(hipEventRecord(H.ev_in[b], H.h2d));
+		/* classify on the caller's stream once the columns landed and the
+		 * output buffer drained (chunk k - 2's download) */
+		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_in[b], 0));
+		if (used[b])
+			HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
+		const cgpu_tuples_v4 dt{reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 0)),
+					reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 1)),
+					reinterpret_cast<const uint16_t *>(in + hs_in_off(m, 2)), in + hs_in_off(m, 3),
+					in + hs_in_off(m, 4), reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 5)),
+					reinterpret_cast<const uint16_t *>(in + hs_in_off(m, 6))};
+		int32_t *dv = reinterpret_cast<int32_t *>(out + hs_out_off(m, 0));
+		uint32_t *di = reinterpret_cast<uint32_t *>(out + hs_out_off(m, 1));
+		uint8_t *ds = stage ? out + hs_out_off(m, 2) : nullptr;
+		if (int r = cgpu_classify_v4(c, &dt, m, dv, di, ds, stream))
+			return r;
+		HIP_OR_EIO(hipEventRecord(H.ev_cls[b], cs));
+		HIP_OR_EIO(hipStreamWaitEvent(H.d2h, H.ev_cls[b], 0));
+		HIP_OR_EIO(hipMemcpyAsync(verdict + off, dv, m * 4, hipMemcpyDeviceToHost, H.d2h));
+		HIP_OR_EIO(hipMemcpyAsync(identity + off, di, m * 4, hipMemcpyDeviceToHost, H.d2h));
+		if (stage)
+			HIP_OR_EIO(hipMemcpyAsync(stage + off, ds, m, hipMemcpyDeviceToHost, H.d2h));
+		HIP_OR_EIO(hipEventRecord(H.ev_out[b], H.d2h));
+		used[b] = true;
+	}
+	/* the caller's stream completes once the last outputs are in host memory */
+	for (int b = 0; b < 2; b++)
+		if (used[b])
+			HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
+	return 0;
+}
+
 CGPU_EXPORT int cgpu_classify_v4_lb(cgpu_ctx *c, const cgpu_tuples_v4 *t, const uint16_t *sport,
 				    const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
 				    uint8_t *stage, void *stream)
@@ -5072,8 +5202,8 @@ CGPU_EXPORT int cgpu_ct6_flush(cgpu_ctx *c)
 
 /* scratch of one cgpu_classify_v{4,6}_ct launch over n packets */
 struct CtScratch {
-	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, heads_pos, head,
-		temp, temp_bytes, svc_out, ctl, flags2, total;
+	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, head,
+		temp, temp_bytes, svc_out, ctl, flags2, res, total;
 };
 
 static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool v6)
@@ -5091,11 +5221,11 @@ static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool 
 	L.idx_sorted = take(n * 4);
 	L.heads = take(n * 4);
 	L.n_heads = take(4);
-	L.heads_pos = take(n * 4);
 	L.head = take(n);
 	L.temp_bytes = ct_temp_bytes(n);
 	L.temp = take(L.temp_bytes);
 	L.flags2 = take((svc ? 4 : 2) * n); /* phase-2 candidates */
+	L.res = take(n * 8);                /* packed outcome per packet */
 	if (svc) {
 		L.svc_out = take(n * (v6 ? 32 : 16));
 		L.ctl = take(16);
@@ -5157,10 +5287,10 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.head = b + L.head;
 	a.heads = reinterpret_cast<uint32_t *>(b + L.heads);
 	a.n_heads = reinterpret_cast<uint32_t *>(b + L.n_heads);
-	a.heads_pos = reinterpret_cast<uint32_t *>(b + L.heads_pos);
 	a.temp = b + L.temp;
 	a.temp_bytes = L.temp_bytes;
 	a.flags2 = b + L.flags2;
+	a.res = reinterpret_cast<uint2 *>(b + L.res);
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
 		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);

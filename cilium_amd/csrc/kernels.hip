@@ -3904,19 +3904,33 @@ struct ct_args {
 	uint16_t *xdport;            /* [n] optional: frame dport after it */
 	uint32_t serial;             /* one group for the whole batch (see launch_ctlb) */
 	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
+	/* [n] every packet's outcome, batch order, written by the walks (the
+	 * prep for packets no walk replays): x = verdict (17 bits, signed) |
+	 * ct result with the walker's CT_* flags << 17 | stage << 25, y = the
+	 * identity; k_ct_out unpacks it into the caller's columns */
+	uint2 *res;
 };
 
-/* One packet's record, written by k_ct_prep{,6} and read by the walker and
- * k_ct_finish (batch order):
+/* the packed per-packet outcome (ct_args.res) */
+#define CTR_NONE 0xFFu /* ct_lookup never ran (gated packets): ct_ret 255 */
+__device__ __forceinline__ uint2 ct_res(int32_t v, uint32_t ret, uint32_t st, uint32_t id)
+{
+	return make_uint2(((uint32_t)v & 0x1FFFFu) | ((ret & 0xFFu) << 17) | ((st & 7u) << 25), id);
+}
+__device__ __forceinline__ int32_t ct_res_verdict(uint32_t x) { return (int32_t)(x << 15) >> 15; }
+__device__ __forceinline__ uint32_t ct_res_ret(uint32_t x) { return (x >> 17) & 0xFFu; }
+
+/* One packet's record, written by k_ct_prep{,6} and read by the walks
+ * (batch order):
  *   IPv4 (2 x 16 B): {daddr, saddr, z, nexthdr | tflags << 8 | meta << 16},
- *                    {w | port << 16, len, sec, cst}
+ *                    {w | ep << 16, len, 0, 0}
  *   IPv6 (4 x 16 B): {daddr}, {saddr}, {z, nexthdr | tflags << 8 | meta << 16,
- *                    w | port << 16, len}, {sec, cst, rev_nat, 0}
+ *                    w | ep << 16, len}, {0, 0, rev_nat, 0}
  * z = the reply-direction tuple's dport | sport << 16 (ct_lookup's first
- * lookup), w = the L4 word (TCP header bytes 12-13 / ICMP type), port = the
- * forward decision's proxy port, sec = src_sec_id of a created entry, cst =
- * counter slot + 1 | stage << 24 of the forward decision, rev_nat = the
- * reverse NAT index an IPv6 ingress entry is created with. */
+ * lookup), w = the L4 word (TCP header bytes 12-13 / ICMP type), ep = the
+ * endpoint, rev_nat = the reverse NAT index an IPv6 ingress entry is created
+ * with.  The policy decision is not in the record: the walker takes it when
+ * the ct result says which tuple policy sees (ct_pol). */
 struct ct_pkt {
 	uint32_t meta, w, len, sec, revnat, port, cst, dport, proto;
 	uint32_t sa4, da4;
@@ -3924,6 +3938,9 @@ struct ct_pkt {
 	/* the service's ct_state (CtK4S): slave, lb_loopback | mode << 1, addr,
 	 * svc_addr */
 	uint32_t slave, lbf, addr, svc_addr;
+	/* the endpoint index, and z (the reply tuple's dport | sport << 16: the
+	 * forward tuple's dport is z >> 16) */
+	uint32_t ep, z;
 };
 
 template <class K> struct ct_rec;
@@ -3939,8 +3956,11 @@ template <> struct ct_rec<CtK4> {
 	__device__ uint32_t meta() const { return r0.w >> 16; }
 	__device__ ct_pkt pkt() const
 	{
-		return ct_pkt{r0.w >> 16, r1.x & 0xFFFFu, r1.y, r1.z, 0u, r1.x >> 16, r1.w, r0.z & 0xFFFFu,
-			      r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{}};
+		ct_pkt q{r0.w >> 16, r1.x & 0xFFFFu, r1.y, 0u, 0u, 0u, 0u, r0.z & 0xFFFFu,
+			 r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{}};
+		q.ep = r1.x >> 16;
+		q.z = r0.z;
+		return q;
 	}
 };
 /*   IPv4 behind the service step (3 x 16 B): the IPv4 record, then
@@ -3958,9 +3978,12 @@ template <> struct ct_rec<CtK4S> {
 	__device__ uint32_t meta() const { return r0.w >> 16; }
 	__device__ ct_pkt pkt() const
 	{
-		return ct_pkt{r0.w >> 16, r1.x & 0xFFFFu, r1.y, r1.z, r2.x & 0xFFFFu, r1.x >> 16, r1.w,
-			      r0.z & 0xFFFFu, r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{},
-			      r2.x >> 16, r2.w, r2.y, r2.z};
+		ct_pkt q{r0.w >> 16, r1.x & 0xFFFFu, r1.y, 0u, r2.x & 0xFFFFu, 0u, 0u,
+			 r0.z & 0xFFFFu, r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{},
+			 r2.x >> 16, r2.w, r2.y, r2.z};
+		q.ep = r1.x >> 16;
+		q.z = r0.z;
+		return q;
 	}
 };
 template <> struct ct_rec<CtK6> {
@@ -3976,8 +3999,11 @@ template <> struct ct_rec<CtK6> {
 	__device__ uint32_t meta() const { return r2.y >> 16; }
 	__device__ ct_pkt pkt() const
 	{
-		return ct_pkt{r2.y >> 16, r2.z & 0xFFFFu, r2.w, r3.x, r3.z, r2.z >> 16, r3.y, r2.x & 0xFFFFu,
-			      r2.y & 0xFFu, 0u, 0u, r1, r0};
+		ct_pkt q{r2.y >> 16, r2.z & 0xFFFFu, r2.w, 0u, r3.z, 0u, 0u, r2.x & 0xFFFFu,
+			 r2.y & 0xFFu, 0u, 0u, r1, r0};
+		q.ep = r2.z >> 16;
+		q.z = r2.x;
+		return q;
 	}
 };
 
@@ -3994,7 +4020,7 @@ __device__ __forceinline__ uint4 ct_addr_key(uint4 k, const ct_pkt &q)
 	return k;
 }
 
-/*   IPv6 behind the service step: the IPv6 record with {sec, cst, rev_nat,
+/*   IPv6 behind the service step: the IPv6 record with {0, 0, rev_nat,
  *                    slave | lbf << 16} as its last word */
 template <> struct ct_rec<CtK6S> {
 	static constexpr uint32_t RW = 4;
@@ -4009,8 +4035,11 @@ template <> struct ct_rec<CtK6S> {
 	__device__ uint32_t meta() const { return r2.y >> 16; }
 	__device__ ct_pkt pkt() const
 	{
-		return ct_pkt{r2.y >> 16, r2.z & 0xFFFFu, r2.w, r3.x, r3.z, r2.z >> 16, r3.y, r2.x & 0xFFFFu,
-			      r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
+		ct_pkt q{r2.y >> 16, r2.z & 0xFFFFu, r2.w, 0u, r3.z, 0u, 0u, r2.x & 0xFFFFu,
+			 r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
+		q.ep = r2.z >> 16;
+		q.z = r2.x;
+		return q;
 	}
 };
 
@@ -4048,14 +4077,15 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 		if constexpr (SVC) {
 			const uint4 so = egress ? a.svc_out[i] : make_uint4(SVC_NONE, 0, 0, 0);
 			if ((so.x & 3u) == SVC_DROP) {
-				a.identity[i] = 0;
+				/* lb4_local failed closed (lb.h:715-744) */
+				a.res[i] = ct_res(DROP_NO_SERVICE, CTR_NONE, 6u, 0u);
 				if (a.xdaddr)
 					a.xdaddr[i] = da;
 				if (a.xdport)
 					a.xdport[i] = (uint16_t)dp;
 				uint4 *r = a.rec + RW * i;
 				r[0] = uint4{da, sa, 0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16)};
-				r[1] = uint4{0u, len, 0u, 0u};
+				r[1] = uint4{ep << 16, len, 0u, 0u};
 				r[2] = uint4{0u, 0u, 0u, 0u};
 				a.gkey[i] = SERIAL ? 0u : ct_fmix((uint32_t)i ^ 0x5bd1e995u);
 				a.idx[i] = (uint32_t)i;
@@ -4110,25 +4140,13 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 		}
 		if (pr != 6u)
 			w = 0; /* union tcp_flags stays zero (conntrack.h:448) */
-		uint32_t sec = 0, port = 0, cst = 0, id = 0;
 		if (!(meta & CTM_GATED)) {
-			/* the forward tuple's decision (what CT_NEW / CT_ESTABLISHED
-			 * packets see); k_ct_finish bumps its counter */
-			const bool frag = !egress && ((fl >> 1) & 1u);
-			if (frag)
+			/* the policy decision is the walker's (ct_pol): it knows which
+			 * tuple policy sees */
+			if (!egress && ((fl >> 1) & 1u))
 				meta |= CTM_FRAG;
-			const decision d = decide<0>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
-						    pr, ep);
-			if (d.v >= 0) {
-				meta |= CTM_ALLOWED;
-				port = (uint32_t)d.v;
-			}
-			id = d.id;
-			if (egress)
-				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
-			else
-				sec = d.id;
-			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+		} else {
+			a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u); /* ct_lookup4's default */
 		}
 		uint32_t g = ct_group(sa, da);
 		if constexpr (!SVC) {
@@ -4180,10 +4198,9 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 				}
 			}
 		}
-		a.identity[i] = id;
 		uint4 *r = a.rec + RW * i;
 		r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
-		r[1] = uint4{w | (port << 16), len, sec, cst};
+		r[1] = uint4{w | (ep << 16), len, 0u, 0u};
 		if constexpr (SVC)
 			r[2] = uint4{r2x, addr, saddr2, lbf};
 		a.gkey[i] = SERIAL ? 0u : (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
@@ -4192,197 +4209,130 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 }
 
 /* k_ct_prep<false, false> (the plain IPv4 path) with Q packets per lane:
- * the forward decisions through decide4_q; packet i = g + u * (threads),
- * so every column load of a wave covers 64 consecutive packets */
+ * packet i = g + u * (threads), so every column load of a wave covers 64
+ * consecutive packets.  A streaming pass: the tuple ct_lookup4 builds, the
+ * group key and the record; no table is read (the policy step is the
+ * walker's) */
 template <int Q>
 __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 {
 	const uint64_t T = (uint64_t)gridDim.x * 256u;
 	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
-		bool act[Q], dec[Q], eg[Q], frag[Q];
-		uint32_t sa[Q], da[Q], fdp[Q], pr[Q], ep[Q], meta[Q], tfl[Q], z[Q], w[Q], len[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
-			act[u] = i < a.n;
-			const uint64_t j = act[u] ? i : 0u;
-			/* columns stream past the tables: nontemporal, so they do not
-			 * evict the LPM / policy lines from L2 */
-			const uint32_t fl = ntl(a.flags + j);
-			pr[u] = ntl(a.proto + j);
-			len[u] = ntl(a.len + j);
-			sa[u] = ntl(a.saddr + j);
-			da[u] = ntl(a.daddr + j);
-			ep[u] = ntl(a.ep + j);
-			w[u] = ntl(a.l4 + j);
-			const uint32_t dp = ntl(a.dport + j), sp = ntl(a.sport + j);
-			eg[u] = fl & 1u;
-			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
-			meta[u] = eg[u] ? CTM_EGRESS : 0u;
-			z[u] = 0;
-			if (pr[u] == 1u) { /* as k_ct_prep */
-				const uint32_t type = w[u] & 0xFFu;
+			if (i >= a.n)
+				continue;
+			/* columns stream past the map: nontemporal */
+			const uint32_t fl = ntl(a.flags + i), pr = ntl(a.proto + i), len = ntl(a.len + i);
+			const uint32_t sa = ntl(a.saddr + i), da = ntl(a.daddr + i), ep = ntl(a.ep + i);
+			const uint32_t dp = ntl(a.dport + i), sp = ntl(a.sport + i);
+			uint32_t w = ntl(a.l4 + i);
+			const bool eg = fl & 1u;
+			uint32_t tfl = eg ? TUPLE_F_IN : 0u, meta = eg ? CTM_EGRESS : 0u, z = 0;
+			if (pr == 1u) { /* as k_ct_prep */
+				const uint32_t type = w & 0xFFu;
 				if (type == 3u || type == 11u || type == 12u)
-					tfl[u] |= TUPLE_F_RELATED;
+					tfl |= TUPLE_F_RELATED;
 				else if (type == 0u)
-					z[u] = 8u;
+					z = 8u;
 				else {
 					if (type == 8u)
-						z[u] = 8u << 16;
-					meta[u] |= CTM_ACT_CREATE;
+						z = 8u << 16;
+					meta |= CTM_ACT_CREATE;
 				}
-			} else if (pr[u] == 6u || pr[u] == 17u) {
-				z[u] = sp | (dp << 16);
-				meta[u] |= pr[u] == 6u ? (CTM_TCP | ((w[u] & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE))
-						       : CTM_ACT_CREATE;
+			} else if (pr == 6u || pr == 17u) {
+				z = sp | (dp << 16);
+				meta |= pr == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
 			} else {
-				meta[u] |= CTM_GATED;
+				meta |= CTM_GATED;
 			}
-			if (pr[u] != 6u)
-				w[u] = 0;
-			frag[u] = !eg[u] && ((fl >> 1) & 1u);
-			if (frag[u] && !(meta[u] & CTM_GATED))
-				meta[u] |= CTM_FRAG;
-			dec[u] = act[u] && !(meta[u] & CTM_GATED);
-			fdp[u] = z[u] >> 16;
-		}
-		decision d[Q];
-		decide4_q<Q>(s, dec, eg, frag, sa, da, fdp, pr, ep, d);
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			if (!act[u])
-				continue;
-			const uint64_t i = g + (uint64_t)u * T;
-			uint32_t sec = 0, port = 0, cst = 0, id = 0, m = meta[u];
-			if (dec[u]) {
-				if (d[u].v >= 0) {
-					m |= CTM_ALLOWED;
-					port = (uint32_t)d[u].v;
-				}
-				id = d[u].id;
-				sec = eg[u] ? (ep[u] < s.n_lxc ? s.lxc[2u * ep[u] + 1u].w : 0u) : d[u].id;
-				cst = (uint32_t)(d[u].ctr + 1) | (d[u].st << 24);
-			}
-			uint32_t gk = ct_group(sa[u], da[u]);
+			if (pr != 6u)
+				w = 0;
+			uint32_t gk = ct_group(sa, da);
 			bool p2 = false;
-			if (dec[u]) {
-				if (pr[u] == 1u && (tfl[u] & TUPLE_F_RELATED)) {
-					m |= CTM_PHASE2;
+			if (!(meta & CTM_GATED)) {
+				if (!eg && ((fl >> 1) & 1u))
+					meta |= CTM_FRAG;
+				if (pr == 1u && (tfl & TUPLE_F_RELATED)) {
+					meta |= CTM_PHASE2;
 					p2 = true;
 				} else {
-					m |= CTM_RELX;
-					gk = ct_conn_group(gk, z[u], pr[u]);
+					meta |= CTM_RELX;
+					gk = ct_conn_group(gk, z, pr);
 				}
+			} else {
+				a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u);
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
-			a.identity[i] = id;
 			uint4 *r = a.rec + 2u * i;
-			r[0] = uint4{da[u], sa[u], z[u], pr[u] | (tfl[u] << 8) | (m << 16)};
-			r[1] = uint4{w[u] | (port << 16), len[u], sec, cst};
-			a.gkey[i] = (m & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
+			r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
+			r[1] = uint4{w | (ep << 16), len, 0u, 0u};
+			a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
 			a.idx[i] = (uint32_t)i;
 		}
 	}
 }
 
-/* k_ct_prep6<false> (the plain IPv6 path) with Q packets per lane, the
- * ipcache entries from the pre-pass (k_ipc6_pre, egress fallback folded in)
- * and the policy cascades through policy_q */
+/* k_ct_prep6<false> (the plain IPv6 path) with Q packets per lane: a
+ * streaming pass as k_ct_prep_q */
 template <int Q>
-__global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, const uint32_t *ipc_e)
+__global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a)
 {
 	const uint64_t T = (uint64_t)gridDim.x * 256u;
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr);
 	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
-		bool act[Q], dec[Q], eg[Q], frag[Q];
-		uint32_t fdp[Q], pr[Q], ep[Q], meta[Q], tfl[Q], z[Q], w[Q], len[Q];
-		decision d[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
-			act[u] = i < a.n;
-			const uint64_t j = act[u] ? i : 0u;
-			const uint32_t fl = ntl(a.flags + j), dp = ntl(a.dport + j), sp = ntl(a.sport + j);
-			pr[u] = ntl(a.proto + j);
-			len[u] = ntl(a.len + j);
-			ep[u] = ntl(a.ep + j);
-			w[u] = ntl(a.l4 + j);
-			eg[u] = fl & 1u;
-			frag[u] = false; /* no fragment flag on IPv6 (bpf_lxc.c:787-789) */
-			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
-			meta[u] = eg[u] ? CTM_EGRESS : 0u;
-			z[u] = 0;
-			if (pr[u] == 58u) { /* as k_ct_prep6 */
-				const uint32_t type = w[u] & 0xFFu;
+			if (i >= a.n)
+				continue;
+			const uint32_t fl = ntl(a.flags + i), dp = ntl(a.dport + i), sp = ntl(a.sport + i);
+			const uint32_t pr = ntl(a.proto + i), len = ntl(a.len + i), ep = ntl(a.ep + i);
+			uint32_t w = ntl(a.l4 + i);
+			const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
+			const bool eg = fl & 1u; /* no fragment flag on IPv6 (bpf_lxc.c:787-789) */
+			uint32_t tfl = eg ? TUPLE_F_IN : 0u, meta = eg ? CTM_EGRESS : 0u, z = 0;
+			if (pr == 58u) { /* as k_ct_prep6 */
+				const uint32_t type = w & 0xFFu;
 				if (type >= 1u && type <= 4u)
-					tfl[u] |= TUPLE_F_RELATED;
+					tfl |= TUPLE_F_RELATED;
 				else if (type == 129u)
-					z[u] = 128u;
+					z = 128u;
 				else {
 					if (type == 128u)
-						z[u] = 128u << 16;
-					meta[u] |= CTM_ACT_CREATE;
+						z = 128u << 16;
+					meta |= CTM_ACT_CREATE;
 				}
-			} else if (pr[u] == 6u || pr[u] == 17u) {
-				z[u] = sp | (dp << 16);
-				meta[u] |= pr[u] == 6u ? (CTM_TCP | ((w[u] & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE))
-						       : CTM_ACT_CREATE;
+			} else if (pr == 6u || pr == 17u) {
+				z = sp | (dp << 16);
+				meta |= pr == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
 			} else {
-				meta[u] |= CTM_GATED;
+				meta |= CTM_GATED;
 			}
-			if (pr[u] != 6u)
-				w[u] = 0;
-			dec[u] = act[u] && !(meta[u] & CTM_GATED);
-			fdp[u] = z[u] >> 16;
-			/* decide<1>'s identity from the pre-pass entry */
-			const uint32_t e = ntl(ipc_e + j);
-			const uint32_t label = entry_label(s.ipc6.vals, e);
-			if (eg[u]) {
-				d[u].id = (e && label) ? label : s.world_id; /* cluster fallback folded into e */
-			} else {
-				uint32_t src = s.ingress_src_identity;
-				if (src < s.health_id && e && label && label != s.cluster_id)
-					src = label;
-				d[u].id = src;
-			}
-		}
-		policy_q<Q>(s, dec, eg, frag, fdp, pr, ep, d);
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			if (!act[u])
-				continue;
-			const uint64_t i = g + (uint64_t)u * T;
-			const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
-			uint32_t sec = 0, port = 0, cst = 0, id = 0, m = meta[u];
-			if (dec[u]) {
-				if (d[u].v >= 0) {
-					m |= CTM_ALLOWED;
-					port = (uint32_t)d[u].v;
-				}
-				id = d[u].id;
-				sec = eg[u] ? (ep[u] < s.n_lxc ? s.lxc[2u * ep[u] + 1u].w : 0u) : d[u].id;
-				cst = (uint32_t)(d[u].ctr + 1) | (d[u].st << 24);
-			}
+			if (pr != 6u)
+				w = 0;
 			uint32_t gk = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
 			bool p2 = false;
-			if (dec[u]) {
-				if (pr[u] == 58u && (tfl[u] & TUPLE_F_RELATED)) {
-					m |= CTM_PHASE2;
+			if (!(meta & CTM_GATED)) {
+				if (pr == 58u && (tfl & TUPLE_F_RELATED)) {
+					meta |= CTM_PHASE2;
 					p2 = true;
 				} else {
-					m |= CTM_RELX;
-					gk = ct_conn_group(gk, z[u], pr[u]);
+					meta |= CTM_RELX;
+					gk = ct_conn_group(gk, z, pr);
 				}
+			} else {
+				a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u);
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
-			a.identity[i] = id;
 			uint4 *r = a.rec + 4u * i;
 			r[0] = da;
 			r[1] = sa;
-			r[2] = uint4{z[u], pr[u] | (tfl[u] << 8) | (m << 16), w[u] | (port << 16), len[u]};
-			r[3] = uint4{sec, cst, eg[u] ? 0u : (da.w & 0xFFFFu), 0u};
-			a.gkey[i] = (m & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
+			r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (ep << 16), len};
+			r[3] = uint4{0u, 0u, eg ? 0u : (da.w & 0xFFFFu), 0u};
+			a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
 			a.idx[i] = (uint32_t)i;
 		}
 	}
@@ -4409,7 +4359,7 @@ __global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint32_t *f4, 
 		const bool p2 = live && (meta & CTM_PHASE2);
 		uint32_t f;
 		if (phase == 0u) {
-			const bool rel = live && (meta & CTM_RELX) && (a.ct_ret[i] & CT_RELP);
+			const bool rel = live && (meta & CTM_RELX) && (ct_res_ret(a.res[i].x) & CT_RELP);
 			f = (p2 && !special ? 1u : 0u) | (rel ? 1u << 16 : 0u);
 		} else {
 			f = (p2 && special ? 1u : 0u) | (live && (meta & CTM_ADDRX) ? 1u << 8 : 0u);
@@ -4441,18 +4391,6 @@ template <class K> __global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args
 			const uint4 k = r.key();
 			a.gkey[j] = ct_group(k.x, k.y);
 		}
-	}
-}
-
-/* length of every group (keys) and its start (values), for the longest-
- * first sort */
-__global__ __launch_bounds__(256) void k_ct_lens(const uint32_t *heads, uint32_t nh, uint64_t n,
-						 uint32_t *len, uint32_t *pos)
-{
-	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += gridDim.x * 256u) {
-		const uint32_t p0 = heads[h];
-		len[h] = (uint32_t)((h + 1u < nh ? (uint64_t)heads[h + 1u] : n) - p0);
-		pos[h] = p0;
 	}
 }
 
@@ -4488,7 +4426,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 			/* lb6_local's outcome (svc_out[2i], target svc_out[2i + 1]) */
 			const uint4 so = egress ? a.svc_out[2u * i] : make_uint4(SVC_NONE, 0, 0, 0);
 			if ((so.x & 3u) == SVC_DROP) {
-				a.identity[i] = 0;
+				a.res[i] = ct_res(DROP_NO_SERVICE, CTR_NONE, 6u, 0u);
 				reinterpret_cast<uint16_t *>(a.f2)[i] = 0u;
 				if (a.xdaddr)
 					reinterpret_cast<uint4 *>(a.xdaddr)[i] = da;
@@ -4497,7 +4435,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 				uint4 *r = a.rec + 4u * i;
 				r[0] = da;
 				r[1] = sa;
-				r[2] = uint4{0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16), 0u, len};
+				r[2] = uint4{0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16), ep << 16, len};
 				r[3] = uint4{0u, 0u, 0u, 0u};
 				a.gkey[i] = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
 				a.idx[i] = (uint32_t)i;
@@ -4537,20 +4475,8 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 		}
 		if (pr != 6u)
 			w = 0; /* union tcp_flags stays zero (conntrack.h:294) */
-		uint32_t sec = 0, port = 0, cst = 0, id = 0;
-		if (!(meta & CTM_GATED)) {
-			const decision d = decide<1>(s, egress, false, 0u, 0u, sa, da, z >> 16, pr, ep);
-			if (d.v >= 0) {
-				meta |= CTM_ALLOWED;
-				port = (uint32_t)d.v;
-			}
-			id = d.id;
-			if (egress)
-				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
-			else
-				sec = d.id;
-			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
-		}
+		if (meta & CTM_GATED)
+			a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u);
 		uint32_t g = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
 		{ /* phase 1 by connection, as k_ct_prep (ct_create6 writes no address
 		   * entry, so the service path groups the same way) */
@@ -4566,12 +4492,11 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
 		}
-		a.identity[i] = id;
 		uint4 *r = a.rec + 4u * i;
 		r[0] = da;
 		r[1] = sa;
-		r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (port << 16), len};
-		r[3] = uint4{sec, cst, rev, svcw};
+		r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (ep << 16), len};
+		r[3] = uint4{0u, 0u, rev, svcw};
 		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
 		a.idx[i] = (uint32_t)i;
 	}
@@ -4970,19 +4895,19 @@ template <class K> __device__ __forceinline__ ct_row ct_new_row(const ct_pkt &q,
  * :288-412) and ct_create4 / ct_create6 (:653-744 / :588-639), with the
  * policy outcome of the endpoint programs (bpf_lxc.c:506-537 / :918-937,
  * :192-203 / :776-800).  k = the reply-direction tuple of the first lookup. */
-template <class K>
+template <class K, class DF>
 __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A, ct_cache<K> &c,
-					   typename K::key k, const ct_pkt &q, uint32_t now)
+					   typename K::key k, ct_pkt &q, uint32_t now, DF &&policy, decision &d)
 {
 	const uint32_t meta = q.meta;
 	const bool ingress = !(meta & CTM_EGRESS);
 	{
 		/* reply key not cached, or cached absent: fetch it, the forward key
-		 * and (when the packet may create) the ICMP key in one round */
+		 * and the ICMP key in one round */
 		const int c1 = ctc_find<K>(c, k);
 		if (c1 < 0 || (ctc_state(c, c1) & CTC_NEG)) {
 			const typename K::key fk = K::reversed(k);
-			ctc_prefetch<K>(T, c, k, fk, K::related(fk), c1 < 0, true, (meta & CTM_ALLOWED) != 0);
+			ctc_prefetch<K>(T, c, k, fk, K::related(fk), c1 < 0, true, true);
 		}
 	}
 	int ci = ctc_get<K>(T, c, k);
@@ -4994,12 +4919,16 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 		ci = ctc_get<K>(T, c, k);
 		ret = (ctc_state(c, ci) & CTC_NEG) ? CT_NEW : CT_ESTABLISHED;
 	}
+	/* the endpoint program's policy step on the tuple ct_lookup left: the
+	 * reply tuple for CT_REPLY / CT_RELATED, the forward one otherwise */
+	d = policy(ret >= CT_REPLY);
+	const bool allowed = d.v >= 0;
 	if (ret != CT_NEW) {
 		ct_row e = ctc_row(c, ci);
 		ct_hit(e, meta, ingress, q.w, q.len, now);
 		ctc_put(c, ci, ctc_pos(c, ci), e);
 	}
-	if (ret < CT_REPLY && !(meta & CTM_ALLOWED)) {
+	if (ret < CT_REPLY && !allowed) {
 		if (ret == CT_ESTABLISHED) { /* ct_delete4 / ct_delete6 */
 			const uint32_t slot = ctc_pos(c, ci);
 			ct_erase<K>(T, A, slot);
@@ -5010,7 +4939,9 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 	if (ret != CT_NEW)
 		return ret;
 	/* ct_create: the forward entry, the address entry (service step only),
-	 * then the ICMP entry relating errors */
+	 * then the ICMP entry relating errors; src_sec_id = SECLABEL (egress) or
+	 * the source identity (ingress) */
+	q.sec = ingress ? d.id : q.sec;
 	ct_row e = ct_new_row<K>(q, ingress, now);
 	if (!ctc_update<K>(T, A, c, k, e))
 		return CT_NEW | CT_FAIL;
@@ -5336,8 +5267,130 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
 }
 
 #ifndef CT_RETB
-#define CT_RETB 16 /* results a walker lane buffers before storing them */
+#define CT_RETB 6 /* results a walker lane buffers before storing them (12 B each in LDS) */
 #endif
+
+/* ---- the endpoint programs' policy step inside the walker ----
+ * decide<> for the packet a lane replays: the ipcache identity and the
+ * three-probe cascade (bpf_lxc.c:484-537 / :876-950, bpf_netdev.c:374-404)
+ * of the tuple policy sees - the forward tuple's dport for CT_NEW /
+ * CT_ESTABLISHED, the reply tuple's for CT_REPLY / CT_RELATED (left
+ * unreversed, policy.h:98-99).  Inside one connection the decision varies
+ * only with that dport, the direction, the fragment bit and the endpoint,
+ * so a lane keeps the last two decisions of its group's address pair keyed
+ * by those: a connection costs a couple of cascades instead of one per
+ * packet.  The hit entries' counters accumulate per slot in two register
+ * sets, flushed (two memory-side atomics) when a third slot needs one and
+ * at the lane's end: one flush per slot per lane instead of an atomic per
+ * packet.  Scalar members only, so the cache stays in VGPRs. */
+struct ct_pol {
+	uint32_t k0, e0, v0, i0, c0; /* key word (0: empty), ep, verdict, identity, ctr + 1 | st << 24 */
+	uint32_t k1, e1, v1, i1, c1;
+	uint32_t nxt;
+	uint32_t s0, n0, b0, h0; /* counter slot + 1 (0: none), packets, bytes lo / hi */
+	uint32_t s1, n1, b1, h1;
+	uint32_t nc;
+};
+
+__device__ __forceinline__ void ct_pol_flush1(uint64_t *delta, uint32_t sl, uint32_t n, uint32_t b, uint32_t h)
+{
+	if (sl) {
+		atomicAdd((unsigned long long *)&delta[2u * (sl - 1u)], (unsigned long long)n);
+		atomicAdd((unsigned long long *)&delta[2u * (sl - 1u) + 1u], ((unsigned long long)h << 32) | b);
+	}
+}
+
+/* packets / bytes of counter slot ctr (>= 0) */
+__device__ __forceinline__ void ct_pol_count(ct_pol &p, uint64_t *delta, int ctr, uint32_t len)
+{
+	const uint32_t sl = (uint32_t)ctr + 1u;
+	if (p.s0 == sl) {
+		p.n0++;
+		add64(p.b0, p.h0, len);
+	} else if (p.s1 == sl) {
+		p.n1++;
+		add64(p.b1, p.h1, len);
+	} else if (p.nc == 0u) {
+		ct_pol_flush1(delta, p.s0, p.n0, p.b0, p.h0);
+		p.s0 = sl;
+		p.n0 = 1u;
+		p.b0 = len;
+		p.h0 = 0u;
+		p.nc = 1u;
+	} else {
+		ct_pol_flush1(delta, p.s1, p.n1, p.b1, p.h1);
+		p.s1 = sl;
+		p.n1 = 1u;
+		p.b1 = len;
+		p.h1 = 0u;
+		p.nc = 0u;
+	}
+}
+
+template <class K>
+__device__ __forceinline__ decision ct_pol_decide(const cgpu_snapshot &s, ct_pol &p, bool cacheable, bool orient,
+						  const ct_pkt &q, bool reply)
+{
+	const bool egress = q.meta & CTM_EGRESS, frag = q.meta & CTM_FRAG;
+	const uint32_t dport = reply ? (q.z & 0xFFFFu) : (q.z >> 16);
+	/* orient: the packet's saddr is the group pair's first address (the
+	 * identity is looked up on daddr for egress, saddr for ingress) */
+	const uint32_t kw = dport | (q.proto << 16) | (egress ? 1u << 24 : 0u) | (frag ? 1u << 25 : 0u) |
+			    (orient ? 1u << 26 : 0u) | (1u << 31);
+	decision d;
+	if (cacheable && p.k0 == kw && p.e0 == q.ep) {
+		d.v = (int32_t)p.v0;
+		d.id = p.i0;
+		d.ctr = (int)(p.c0 & 0xFFFFFFu) - 1;
+		d.st = p.c0 >> 24;
+		return d;
+	}
+	if (cacheable && p.k1 == kw && p.e1 == q.ep) {
+		d.v = (int32_t)p.v1;
+		d.id = p.i1;
+		d.ctr = (int)(p.c1 & 0xFFFFFFu) - 1;
+		d.st = p.c1 >> 24;
+		return d;
+	}
+	d = decide<K::V6>(s, egress, frag, q.sa4, q.da4, q.sa6, q.da6, dport, q.proto, q.ep);
+	if (cacheable) {
+		const uint32_t c = (uint32_t)(d.ctr + 1) | (d.st << 24);
+		if (p.nxt == 0u) {
+			p.k0 = kw;
+			p.e0 = q.ep;
+			p.v0 = (uint32_t)d.v;
+			p.i0 = d.id;
+			p.c0 = c;
+			p.nxt = 1u;
+		} else {
+			p.k1 = kw;
+			p.e1 = q.ep;
+			p.v1 = (uint32_t)d.v;
+			p.i1 = d.id;
+			p.c1 = c;
+			p.nxt = 0u;
+		}
+	}
+	return d;
+}
+
+/* the outcome k_ct_finish used to compute: verdict, stage and the counter
+ * bump of a replayed packet (bpf_lxc.c:506-537 / :918-950: CT_REPLY /
+ * CT_RELATED skip the drop; an egress proxy redirect keeps its port) */
+__device__ __forceinline__ uint2 ct_outcome(const decision &d, uint32_t ret, const ct_pkt &q)
+{
+	const bool egress = q.meta & CTM_EGRESS;
+	int32_t v;
+	if ((ret & 3u) >= CT_REPLY)
+		v = (egress && d.v > 0) ? d.v : 0;
+	else if (d.v < 0)
+		v = DROP_POLICY;
+	else if (ret & CT_FAIL)
+		v = DROP_CT_CREATE_FAILED;
+	else
+		v = d.v;
+	return ct_res(v, ret, d.st, d.id);
+}
 
 /* walks: WALK_PKT the conntrack path's packets; WALK_SVC the service step
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
@@ -5377,17 +5430,19 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 	 * step (1.4 ms of a 12.3 ms step, profiles/r3_session_h/ab_ct_ret.log);
 	 * CT_RETB stores issued back to back cost about one */
 	__shared__ uint32_t s_ri[CT_RETB][256];
-	__shared__ uint8_t s_rr[CT_RETB][256];
+	__shared__ uint2 s_rr[CT_RETB][256];
 	uint32_t nret = 0;
 	auto ret_flush = [&]() {
 		for (uint32_t k = 0; k < nret; k++) {
-			const uint32_t i = s_ri[k][threadIdx.x], ret = s_rr[k][threadIdx.x];
-			a.ct_ret[i] = (uint8_t)ret;
-			if (!K::ADDR && MODE == WALK_PKT && (ret & CT_RELP))
+			const uint32_t i = s_ri[k][threadIdx.x];
+			const uint2 r = s_rr[k][threadIdx.x];
+			a.res[i] = r;
+			if (!K::ADDR && MODE == WALK_PKT && (ct_res_ret(r.x) & CT_RELP))
 				a.f2[2u * i + 1u] = 1u; /* its ICMP entry is owed to phase 2 */
 		}
 		nret = 0;
 	};
+	ct_pol pc{};
 	if (threadIdx.x < 3)
 		s_acct[threadIdx.x] = 0;
 	__syncthreads();
@@ -5421,6 +5476,15 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 		uint32_t n3 = p0 + 2u < p1 ? a.idx_sorted[p0 + 2u] : n1;
 		R r1 = R::load(a.rec, pkt_of(n1), false);
 		R r2 = p0 + 1u < p1 ? R::load(a.rec, pkt_of(n2), false) : r1;
+		/* the group's address pair (its first packet's): decisions of other
+		 * pairs (a hash collision of two groups) are not cached */
+		uint4 ga{}, gb{};
+		if constexpr (MODE != WALK_SVC) {
+			const ct_pkt g0 = r1.pkt();
+			ga = K::V6 ? g0.sa6 : make_uint4(g0.sa4, 0u, 0u, 0u);
+			gb = K::V6 ? g0.da6 : make_uint4(g0.da4, 0u, 0u, 0u);
+			pc.k0 = pc.k1 = 0u;
+		}
 		for (uint64_t p = p0; p < p1; p++) {
 			/* records two packets ahead and the index three ahead are in
 			 * flight while packet p runs */
@@ -5451,23 +5515,30 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 					a.svc_out[i] = ct_svc_step(s, T, A, c, r, a.now);
 				}
 			} else {
-				const ct_pkt q = r.pkt();
+				ct_pkt q = r.pkt();
+				const bool egress = q.meta & CTM_EGRESS;
+				/* src_sec_id of an egress create: the endpoint's SECLABEL */
+				q.sec = egress && q.ep < s.n_lxc ? s.lxc[2u * q.ep + 1u].w : 0u;
 				if constexpr (MODE == WALK_OWED) {
 					const uint32_t kind = K::ADDR ? (v & 3u) : (v & 1u) << 1;
-					const typename K::key fk = K::reversed(r.key());
-					if (kind == 1u) {
-						/* the owed address entry of packet i's create */
-						if constexpr (K::ADDR) {
-							if (a.ct_ret[i] & CT_ADDRP)
-								ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
-										   ct_new_row<K>(q, false, a.now));
+					if (kind != 0u) {
+						const typename K::key fk = K::reversed(r.key());
+						/* the owed entries carry the create's ct_state: its
+						 * src_sec_id is the identity the create stored */
+						const uint2 pr = a.res[i];
+						q.sec = egress ? q.sec : pr.y;
+						if (kind == 1u) {
+							/* the owed address entry of packet i's create */
+							if constexpr (K::ADDR) {
+								if (ct_res_ret(pr.x) & CT_ADDRP)
+									ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
+											   ct_new_row<K>(q, false, a.now));
+							}
+							continue;
 						}
-						continue;
-					}
-					if (kind == 2u) {
 						/* the owed ICMP entry of packet i's create */
-						if (a.ct_ret[i] & CT_RELP) {
-							ct_row e = ct_new_row<K>(q, !(q.meta & CTM_EGRESS), a.now);
+						if (ct_res_ret(pr.x) & CT_RELP) {
+							ct_row e = ct_new_row<K>(q, !egress, a.now);
 							e.c.y |= CTB_SEEN_NON_SYN;
 							ctc_update_owed<K>(T, A, c, K::related(fk), e);
 						}
@@ -5476,9 +5547,30 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 				}
 				if (MODE == WALK_PKT && (meta & CTM_PHASE2))
 					continue;
-				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now);
+				bool inpair, orient;
+				if constexpr (K::V6 != 0) {
+					const bool f = q.sa6.x == ga.x && q.sa6.y == ga.y && q.sa6.z == ga.z && q.sa6.w == ga.w &&
+						       q.da6.x == gb.x && q.da6.y == gb.y && q.da6.z == gb.z && q.da6.w == gb.w;
+					const bool b = q.sa6.x == gb.x && q.sa6.y == gb.y && q.sa6.z == gb.z && q.sa6.w == gb.w &&
+						       q.da6.x == ga.x && q.da6.y == ga.y && q.da6.z == ga.z && q.da6.w == ga.w;
+					inpair = f || b;
+					orient = f;
+				} else {
+					const bool f = q.sa4 == ga.x && q.da4 == gb.x, b = q.sa4 == gb.x && q.da4 == ga.x;
+					inpair = f || b;
+					orient = f;
+				}
+				decision d;
+				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now,
+								[&](bool reply) {
+									return ct_pol_decide<K>(s, pc, inpair, orient, q,
+												reply);
+								},
+								d);
+				if (d.ctr >= 0)
+					ct_pol_count(pc, a.delta, d.ctr, q.len);
 				s_ri[nret][threadIdx.x] = i;
-				s_rr[nret][threadIdx.x] = (uint8_t)ret;
+				s_rr[nret][threadIdx.x] = ct_outcome(d, ret, q);
 				if (++nret == CT_RETB)
 					ret_flush();
 			}
@@ -5486,6 +5578,10 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 		ctc_flush(T, c);
 	}
 	ret_flush();
+	if constexpr (MODE != WALK_SVC) {
+		ct_pol_flush1(a.delta, pc.s0, pc.n0, pc.b0, pc.h0);
+		ct_pol_flush1(a.delta, pc.s1, pc.n1, pc.b1, pc.h1);
+	}
 #ifdef CGPU_DIAG_WALK_CLOCK
 	{
 		uint32_t mx = dg_steps;
@@ -5512,163 +5608,46 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 	}
 }
 
-/* policy on the tuple ct_lookup left, counters, the reply / related skip.
- * CT_NEW / CT_ESTABLISHED packets reuse the prep's forward decision; only
- * CT_REPLY / CT_RELATED ones run the cascade again, on the reply tuple.
- * Hot counter slots accumulate in LDS (packed, as k_classify CTR = 1). */
-template <int NT, class K, int Q>
-__global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, uint32_t cc_n)
+/* The batch's outcome into the caller's columns, in batch order (the walks
+ * wrote every packet's packed result, ct_args.res, the prep the gated
+ * ones), and the {reason, dir} metrics of the verdicts (drop.h:94-118 /
+ * metrics.h:41-59; a proxy redirect traces TRACE_TO_PROXY and counts none).
+ * A streaming pass: 13 bytes in, 10 out per packet. */
+template <int NT>
+__global__ __launch_bounds__(NT) void k_ct_out(cgpu_snapshot s, ct_args a)
 {
-	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
-	/* metrics {reason 0 / 133 / 137 / 155 [/ 158]} x {ingress, egress} */
-	constexpr int NM = K::SVC ? 10 : 8;
-	uint64_t mcnt[NM] = {}, mbyt[NM] = {};
-	/* LDS: the hot counter slots, then the cold-slot cache (as k_classify_x4:
-	 * cc_n packed counts, cc_n tags = slot + 1): each touched cold slot costs
-	 * one pair of memory-side atomics per workgroup instead of one per hit */
-	uint64_t *ccv = lctr + s.hot_slots;
-	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + cc_n);
-	const uint32_t ccm = cc_n - 1u;
-	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
-		lctr[k] = 0;
-	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
-		ccv[k] = 0;
-		cck[k] = 0;
-	}
-	__syncthreads();
-	/* Q packets per lane (packet g + u * threads): the CT_REPLY / CT_RELATED
-	 * packets' policy cascades run stage-interleaved (policy_q) */
+	/* metrics {reason 0 / 133 / 137 / 155 / 158} x {ingress, egress} */
+	uint64_t mcnt[10] = {}, mbyt[10] = {};
 	const uint64_t T = (uint64_t)gridDim.x * NT;
-	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < a.n; g += T * Q) {
-		ct_pkt q[Q];
-		uint32_t c[Q], ep[Q], dp[Q], pr[Q];
-		bool act[Q], rep[Q], eg[Q], frag[Q];
-		decision d[Q];
+	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += T) {
+		const uint2 r = ld_x2<true>(a.res + i);
+		const uint32_t fl = ntl(a.flags + i), len = ntl(a.len + i);
+		const int32_t v = ct_res_verdict(r.x);
+		const uint32_t cr = ct_res_ret(r.x);
+		a.verdict[i] = v;
+		a.ct_ret[i] = (uint8_t)(cr == CTR_NONE ? 255u : cr & 3u);
+		a.identity[i] = r.y;
+		if (a.stage)
+			a.stage[i] = (uint8_t)((r.x >> 25) & 7u);
+		const uint32_t rr = v > 0 ? 5u : v == 0 ? 0u : v == DROP_POLICY ? 1u : v == DROP_CT_UNKNOWN_PROTO ? 2u
+				 : v == DROP_NO_SERVICE ? 4u : 3u;
+		const uint32_t idx = rr * 2u + (fl & 1u);
 #pragma unroll
-		for (int u = 0; u < Q; u++) {
-			const uint64_t i = g + (uint64_t)u * T;
-			act[u] = i < a.n;
-			const uint64_t j = act[u] ? i : 0u;
-			/* batch order: records and the walker's results stream in */
-			q[u] = ct_rec<K>::load(a.rec, (uint32_t)j, true).pkt();
-			c[u] = ntl(a.ct_ret + j) & ~(CT_ADDRP | CT_RELP);
-			ep[u] = ntl(a.ep + j);
-			eg[u] = q[u].meta & CTM_EGRESS;
-			frag[u] = q[u].meta & CTM_FRAG;
-			rep[u] = act[u] && !(q[u].meta & CTM_GATED) && (c[u] & 3u) >= CT_REPLY;
-			dp[u] = q[u].dport;
-			pr[u] = q[u].proto;
-			/* the reply tuple keeps the packet's addresses and direction, so
-			 * its identity is the one the prep resolved (decide<>'s identity
-			 * depends on neither port nor protocol) */
-			d[u].id = rep[u] ? ntl(a.identity + j) : 0u;
-		}
-		policy_q<Q>(s, rep, eg, frag, dp, pr, ep, d);
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			if (!act[u])
-				continue;
-			const uint64_t i = g + (uint64_t)u * T;
-			const uint32_t meta = q[u].meta;
-			const bool egress = eg[u];
-			const uint32_t len = q[u].len;
-			int32_t v;
-			uint32_t st = 4, cr = 255u;
-			if (meta & CTM_GATED) {
-				v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup default case */
-				if (K::SVC && (meta & CTM_SVCDROP)) {
-					v = DROP_NO_SERVICE; /* lb4_local failed closed (lb.h:715-744) */
-					st = 6;
-				}
-			} else {
-				cr = c[u] & 3u;
-				int ctr;
-				if (cr >= CT_REPLY) {
-					ctr = d[u].ctr;
-					st = d[u].st;
-					v = (egress && d[u].v > 0) ? d[u].v : 0;
-				} else {
-					ctr = (int)(q[u].cst & 0xFFFFFFu) - 1;
-					st = q[u].cst >> 24;
-					if (!(meta & CTM_ALLOWED))
-						v = DROP_POLICY;
-					else if (c[u] & CT_FAIL)
-						v = DROP_CT_CREATE_FAILED;
-					else
-						v = (int32_t)q[u].port;
-				}
-				if (ctr >= 0) {
-					const uint32_t cs = (uint32_t)ctr;
-					bool done = false;
-					if (len < PK_MAX_LEN) {
-						if (cs < s.hot_slots) {
-							atomicAdd((unsigned long long *)&lctr[cs],
-								  (1ull << PK_SHIFT) | (unsigned long long)len);
-							done = true;
-						} else if (cc_n) {
-							uint32_t j = (cs * 0x9E3779B1u) >> 16;
-#pragma unroll
-							for (int p = 0; p < CC_PROBE && !done; p++, j++) {
-								j &= ccm;
-								uint32_t t = cck[j];
-								if (t == 0u) {
-									const uint32_t o = atomicCAS(&cck[j], 0u, cs + 1u);
-									t = o == 0u ? cs + 1u : o;
-								}
-								if (t == cs + 1u) {
-									atomicAdd((unsigned long long *)&ccv[j],
-										  (1ull << PK_SHIFT) | (unsigned long long)len);
-									done = true;
-								}
-							}
-						}
-					}
-					if (!done) {
-						atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
-						atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u], (unsigned long long)len);
-					}
-				}
-			}
-			a.verdict[i] = v;
-			a.ct_ret[i] = (uint8_t)cr;
-			if (a.stage)
-				a.stage[i] = (uint8_t)st;
-			/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
-			const uint32_t r = v > 0 ? 5u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : (v == DROP_NO_SERVICE ? 4u : 3u)));
-			const uint32_t idx = r * 2u + (egress ? 1u : 0u);
-#pragma unroll
-			for (int k = 0; k < NM; k++) {
-				mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
-				mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
-			}
+		for (int k = 0; k < 10; k++) {
+			mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
+			mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
 		}
 	}
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
 	const uint32_t reasons[5] = {0u, 133u, 137u, 155u, 158u};
 #pragma unroll
-	for (int k = 0; k < NM; k++) {
+	for (int k = 0; k < 10; k++) {
 		const uint64_t cn = wave_sum(mcnt[k]);
 		const uint64_t by = wave_sum(mbyt[k]);
 		if ((threadIdx.x & 63) == 0 && cn) {
 			const uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
 			atomicAdd((unsigned long long *)&met[key], (unsigned long long)cn);
 			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)by);
-		}
-	}
-	__syncthreads();
-	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
-		const uint64_t x = lctr[k];
-		if (x) {
-			atomicAdd((unsigned long long *)&a.delta[2u * k], x >> PK_SHIFT);
-			atomicAdd((unsigned long long *)&a.delta[2u * k + 1u], x & PK_BYTES_MASK);
-		}
-	}
-	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
-		const uint32_t t = cck[k];
-		const uint64_t x = ccv[k];
-		if (t && x) {
-			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u)], x >> PK_SHIFT);
-			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u) + 1u], x & PK_BYTES_MASK);
 		}
 	}
 }
@@ -5687,6 +5666,7 @@ static int ct_sort_bits(const cgpu_snapshot &s)
  * a counting iterator took 0.77 ms per 64M flags and 1.43 ms per 128M
  * (profiles/r3_ct). */
 #define SEL_T 16u            /* flags per thread: one 16-byte load */
+#define LH_B 256u            /* head ranges of the longest-first ordering (k_ct_lhist) */
 #define SEL_B (256u * SEL_T) /* flags per block */
 
 __device__ __forceinline__ uint32_t sel_bits(const uint8_t *f, uint64_t n, uint64_t i0)
@@ -5796,7 +5776,8 @@ size_t ct_temp_bytes(uint64_t n)
 	size_t a = 0;
 	(void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
 						 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
-	return std::max<size_t>(a, sel_blocks(4 * n) * 4u + 4u);
+	/* ... and the range counts of the longest-first ordering (k_ct_lhist) */
+	return std::max<size_t>(std::max<size_t>(a, sel_blocks(4 * n) * 4u + 4u), (size_t)LH_B * 32u * 4u);
 }
 
 static ct_args ct_args_of(const ct_launch &L)
@@ -5812,13 +5793,124 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.xdaddr = static_cast<uint32_t *>(L.xdaddr);
 	a.xdport = L.xdport;
 	a.f2 = L.flags2;
+	a.res = L.res;
 	return a;
 }
 
+/* Groups longest first, ordered on the device (the group count stays in
+ * device memory: no host round trip between the sort and the walk).  A
+ * group's bucket is the highest set bit of its length; the buckets are laid
+ * out longest first, so the elephants start in the walker's first round.
+ * LH_B workgroups each own a contiguous range of the group heads: count the
+ * range's buckets (k_ct_lhist), one workgroup turns the LH_B x 32 counts
+ * into offsets (k_ct_lscan), and each range places its groups in head order
+ * inside every bucket (k_ct_lplace: ranks from wave ballots, so the layout
+ * is deterministic). */
+__device__ __forceinline__ void lh_range(uint32_t nh, uint32_t b, uint32_t &lo, uint32_t &hi)
+{
+	lo = (uint32_t)((uint64_t)nh * b / LH_B);
+	hi = (uint32_t)((uint64_t)nh * (b + 1u) / LH_B);
+}
+
+__device__ __forceinline__ uint32_t lh_len(const uint32_t *heads, uint32_t k, uint32_t nh, uint64_t n)
+{
+	return (uint32_t)((k + 1u < nh ? (uint64_t)heads[k + 1u] : n) - heads[k]);
+}
+
+__global__ __launch_bounds__(256) void k_ct_lhist(const uint32_t *heads, const uint32_t *n_heads, uint64_t n,
+						  uint32_t *bh)
+{
+	__shared__ uint32_t h[32];
+	if (threadIdx.x < 32)
+		h[threadIdx.x] = 0;
+	__syncthreads();
+	uint32_t lo, hi;
+	lh_range(*n_heads, blockIdx.x, lo, hi);
+	const uint32_t nh = *n_heads;
+	for (uint32_t k = lo + threadIdx.x; k < hi; k += 256u)
+		atomicAdd(&h[31 - __clz(lh_len(heads, k, nh, n))], 1u);
+	__syncthreads();
+	if (threadIdx.x < 32)
+		bh[blockIdx.x * 32u + threadIdx.x] = h[threadIdx.x];
+}
+
+/* one workgroup: bh[b][bucket] := where range b's groups of that bucket
+ * start, buckets longest first, ranges in order inside a bucket */
+__global__ __launch_bounds__(256) void k_ct_lscan(uint32_t *bh)
+{
+	__shared__ uint32_t c[LH_B * 32u];
+	__shared__ uint32_t base[32];
+	for (uint32_t k = threadIdx.x; k < LH_B * 32u; k += 256u)
+		c[k] = bh[k];
+	__syncthreads();
+	if (threadIdx.x < 32) { /* per bucket: ranges' exclusive prefix, the total */
+		uint32_t run = 0;
+		for (uint32_t b = 0; b < LH_B; b++) {
+			const uint32_t x = c[b * 32u + threadIdx.x];
+			c[b * 32u + threadIdx.x] = run;
+			run += x;
+		}
+		base[threadIdx.x] = run;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint32_t o = 0;
+		for (int k = 31; k >= 0; k--) {
+			const uint32_t t = base[k];
+			base[k] = o;
+			o += t;
+		}
+	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < LH_B * 32u; k += 256u)
+		bh[k] = c[k] + base[k & 31u];
+}
+
+__global__ __launch_bounds__(256) void k_ct_lplace(const uint32_t *heads, const uint32_t *n_heads, uint64_t n,
+						   const uint32_t *bh, uint32_t *glen, uint32_t *gpos)
+{
+	__shared__ uint32_t off[32];
+	__shared__ uint32_t wc[4][32];
+	const uint32_t nh = *n_heads, lane = __lane_id(), wv = threadIdx.x >> 6;
+	uint32_t lo, hi;
+	lh_range(nh, blockIdx.x, lo, hi);
+	if (threadIdx.x < 32)
+		off[threadIdx.x] = bh[blockIdx.x * 32u + threadIdx.x];
+	__syncthreads();
+	for (uint32_t t0 = lo; t0 < hi; t0 += 256u) {
+		const uint32_t k = t0 + threadIdx.x;
+		const bool act = k < hi;
+		const uint32_t len = act ? lh_len(heads, k, nh, n) : 1u;
+		const uint32_t bk = act ? 31u - (uint32_t)__clz(len) : 32u;
+		uint32_t rank = 0;
+		const uint64_t below = (1ull << lane) - 1ull;
+		for (uint32_t b = 0; b < 32u; b++) {
+			const uint64_t m = __ballot(bk == b);
+			if (bk == b)
+				rank = (uint32_t)__popcll(m & below);
+			if (lane == 0)
+				wc[wv][b] = (uint32_t)__popcll(m);
+		}
+		__syncthreads();
+		if (act) {
+			uint32_t at = off[bk] + rank;
+			for (uint32_t w = 0; w < wv; w++)
+				at += wc[w][bk];
+			glen[at] = len;
+			gpos[at] = heads[k];
+		}
+		__syncthreads();
+		if (threadIdx.x < 32)
+			off[threadIdx.x] += wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] + wc[3][threadIdx.x];
+		__syncthreads();
+	}
+}
+
 /* (gkey, idx)[0, m) -> groups in batch order, longest first: a.idx_sorted
- * the permutation, a.gpos / a.glen per group; *nh (host) the group count */
+ * the permutation, a.gpos / a.glen per group, *L.n_heads (device) the group
+ * count */
 static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_args &a, uint64_t m,
-				uint32_t *nh, hipStream_t st)
+				hipStream_t st)
 {
 	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m + 255) / 256, 8192));
 	size_t tb = L.temp_bytes;
@@ -5834,22 +5926,16 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 	e = ct_select(L.head, m, L.heads, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 	if (e != hipSuccess)
 		return e;
-	/* groups longest first: gkey / idx are free again and hold (length,
-	 * start) before the sort, gkey_sorted / idx the sorted pairs after */
-	*nh = 0;
-	e = hipMemcpyAsync(nh, L.n_heads, 4, hipMemcpyDeviceToHost, st);
-	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
-		return e;
-	const unsigned gh = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((*nh + 255) / 256, 8192));
-	hipLaunchKernelGGL(k_ct_lens, dim3(gh), dim3(256), 0, st, L.heads, *nh, m, L.gkey, L.heads_pos);
-	tb = L.temp_bytes;
-	e = hipcub::DeviceRadixSort::SortPairsDescending(L.temp, tb, L.gkey, L.gkey_sorted, L.heads_pos,
-							 L.idx, (int)*nh, 0, 32, st);
-	if (e != hipSuccess)
-		return e;
-	a.glen = L.gkey_sorted;
+	/* gkey / idx are free again: (length, start) of the groups, longest
+	 * first; temp holds the range counts */
+	uint32_t *bh = static_cast<uint32_t *>(L.temp);
+	hipLaunchKernelGGL(k_ct_lhist, dim3(LH_B), dim3(256), 0, st, L.heads, L.n_heads, (uint64_t)m, bh);
+	hipLaunchKernelGGL(k_ct_lscan, dim3(1), dim3(256), 0, st, bh);
+	hipLaunchKernelGGL(k_ct_lplace, dim3(LH_B), dim3(256), 0, st, L.heads, L.n_heads, (uint64_t)m,
+			   (const uint32_t *)bh, L.gkey, L.idx);
+	a.glen = L.gkey;
 	a.gpos = L.idx;
-	return hipSuccess;
+	return hipGetLastError();
 }
 
 /* packets per lane of the conntrack prep / finish passes (timing-only tool
@@ -5861,21 +5947,11 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 /* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
 #define CT_WALK_GRID 2048
 
-template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
+static void launch_ct_out(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
-	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
-	constexpr int NF = 1024, Q = CGPU_CT_Q;
-	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF * Q - 1) / (NF * Q), 512), (a.n >> 22) + 1);
-	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
-	/* the cold-slot cache in the LDS the hot slots leave */
-	const size_t hot = (size_t)sf.hot_slots * 8u;
-	uint32_t cc_n = 0;
-	if (!(s.schedule & CGPU_SCHED_NO_CCACHE))
-		for (uint32_t c = 1u << 14; c >= 512u && !cc_n; c >>= 1)
-			if (hot + (size_t)c * 12u <= X4_LDS_BUDGET)
-				cc_n = c;
-	hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), hot + (size_t)cc_n * 12u, st, sf,
-			   a, cc_n);
+	constexpr int NT = 256;
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + NT - 1) / NT, 256u * 16u));
+	hipLaunchKernelGGL((k_ct_out<NT>), dim3(g), dim3(NT), 0, st, s, a);
 }
 
 /* phase 2 of the plain paths (and of the IPv6 service path): the ICMP
@@ -5888,7 +5964,9 @@ static hipError_t ct_phase2(const cgpu_snapshot &s, const ct_table &T, const ct_
 	hipError_t e = ct_select(L.flags2, 2 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 	if (e != hipSuccess)
 		return e;
-	uint32_t m = 0, nh = 0;
+	/* the candidate count sizes the radix sort: the one host read of the
+	 * plain path */
+	uint32_t m = 0;
 	e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
 		return e;
@@ -5896,7 +5974,7 @@ static hipError_t ct_phase2(const cgpu_snapshot &s, const ct_table &T, const ct_
 		return hipSuccess;
 	const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_ct_owed_keys<K>, dim3(gm), dim3(256), 0, st, a, m, 0u);
-	e = ct_group_sort(s, L, a, m, &nh, st);
+	e = ct_group_sort(s, L, a, m, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
@@ -5907,37 +5985,19 @@ template <class K>
 static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
 {
 	ct_args a = ct_args_of(L);
-	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
-	if (K::V6) {
-		/* the ipcache lookups through the trie pre-pass (its entries into
-		 * idx_sorted, free until the group sort) when it can fold the
-		 * egress fallback identity */
-		if (s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK) {
-			constexpr int NT = 1024, QP = CGPU_DIAG_IPC6_PRE_Q, Q = 4;
-			const size_t lds = (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u;
-			const unsigned res = resident_blocks((const void *)k_ipc6_pre<QP, NT>, NT, lds);
-			const unsigned gp = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + QP * NT - 1) / (QP * NT), res));
-			hipLaunchKernelGGL((k_ipc6_pre<QP, NT>), dim3(gp), dim3(NT), lds, st, s,
-					   static_cast<const uint4 *>(L.saddr), static_cast<const uint4 *>(L.daddr), L.flags,
-					   L.idx_sorted, L.n);
-			const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
-			hipLaunchKernelGGL((k_ct_prep6_q<Q>), dim3(gq), dim3(256), 0, st, s, a, L.idx_sorted);
-		} else {
-			hipLaunchKernelGGL(k_ct_prep6<false>, dim3(g), dim3(256), 0, st, s, a);
-		}
-	} else {
-		constexpr int Q = CGPU_CT_Q;
-		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+	constexpr int Q = CGPU_CT_Q;
+	const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+	if (K::V6)
+		hipLaunchKernelGGL((k_ct_prep6_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
+	else
 		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
-	}
-	uint32_t nh;
-	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	hipError_t e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<K>(s, T, L, a, st)) != hipSuccess)
 		return e;
-	launch_ct_finish<K>(s, a, st);
+	launch_ct_out(s, a, st);
 	return hipGetLastError();
 }
 
@@ -5963,19 +6023,18 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	ct_args a = ct_args_of(L);
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_svc_prep6, dim3(g), dim3(256), 0, st, s, a);
-	uint32_t nh;
-	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	hipError_t e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK6, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
-	e = ct_group_sort(s, L, a, L.n, &nh, st);
+	e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK6S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<CtK6S>(s, T, L, a, st)) != hipSuccess)
 		return e;
-	launch_ct_finish<CtK6S>(s, a, st);
+	launch_ct_out(s, a, st);
 	return hipGetLastError();
 }
 
@@ -6005,8 +6064,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	ct_args a = ct_args_of(L);
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_svc_prep, dim3(g), dim3(256), 0, st, s, a);
-	uint32_t nh;
-	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	hipError_t e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK4, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
@@ -6021,7 +6079,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	const bool serial = ctl[0] != 0;
 	if (serial)
 		hipLaunchKernelGGL((k_ct_prep<true, true>), dim3(g), dim3(256), 0, st, s, a);
-	e = ct_group_sort(s, L, a, L.n, &nh, st);
+	e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
@@ -6041,13 +6099,13 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 				continue;
 			const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
 			hipLaunchKernelGGL(k_ct_owed_keys<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, 0u);
-			e = ct_group_sort(s, L, a, m, &nh, st);
+			e = ct_group_sort(s, L, a, m, st);
 			if (e != hipSuccess)
 				return e;
 			hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 		}
 	}
-	launch_ct_finish<CtK4S>(s, a, st);
+	launch_ct_out(s, a, st);
 	return hipGetLastError();
 }
 

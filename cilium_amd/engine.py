@@ -421,6 +421,33 @@ class Engine:
                                       _stream(stream)), "cgpu_classify_v4")
         return out
 
+    def classify_v4_host(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """cgpu_classify_v4_host: t holds HOST arrays (numpy, or CPU tensors
+        -- page-locked ones overlap the copies with the classify) with the
+        dtypes of classify_v4; outputs are host numpy arrays, complete when
+        `stream` is (the call synchronizes it before returning unless
+        out is given)."""
+        import numpy as np
+        n = len(t["saddr"])
+
+        def ptr(x):
+            if x is None:
+                return None
+            return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else x.ctypes.data)
+        given = out is not None
+        if out is None:
+            out = {"verdict": np.empty(n, np.int32), "identity": np.empty(n, np.uint32),
+                   "stage": np.empty(n, np.uint8) if stage else None}
+        cols = [t[k] for k in ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")]
+        tv = TuplesV4(*[ptr(x).value for x in cols])
+        check(self.L.cgpu_classify_v4_host(self.h, C.byref(tv), n, ptr(out["verdict"]),
+                                           ptr(out["identity"]), ptr(out.get("stage")),
+                                           _stream(stream)), "cgpu_classify_v4_host")
+        if not given:
+            import torch
+            (stream or torch.cuda.current_stream()).synchronize()
+        return out
+
     def classify_v4_ct(self, t: dict, now: int, out: dict | None = None, stage: bool = True,
                        stream=None):
         """Stateful classification (cgpu_classify_v4_ct): t holds CUDA tensors

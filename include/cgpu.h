@@ -437,6 +437,22 @@ typedef struct cgpu_tuples_v4 {
 int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
 		     uint32_t *identity, uint8_t *stage, void *stream);
 
+/*
+ * cgpu_classify_v4 over a HOST-resident batch (the reference
+ * classifies each packet as the NIC hands it over, bpf_xdp.c:181-184 /
+ * bpf_netdev.c:470; the engine takes batches that arrive in host memory
+ * too): every column of t and the outputs are host pointers.  The batch
+ * streams through double-buffered device staging in chunks of 4M tuples:
+ * chunk k + 1 uploads and chunk k - 1 downloads while chunk k classifies on
+ * `stream`.  Returns once enqueued; the outputs are complete when `stream`
+ * is (page-locked buffers overlap the copies with the classify, pageable
+ * ones are staged by the runtime and serialise).  Same results, counters
+ * and metrics as cgpu_classify_v4 of the same tuples.  -ENODEV on a
+ * host-only context, -EINVAL for a null column or output.
+ */
+int cgpu_classify_v4_host(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
+			  uint32_t *identity, uint8_t *stage, void *stream);
+
 typedef struct cgpu_tuples_v6 {
 	const uint8_t *saddr;  /* 16 bytes per tuple, network order */
 	const uint8_t *daddr;  /* 16 bytes per tuple */

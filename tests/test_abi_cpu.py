@@ -425,3 +425,29 @@ def test_ct6_map_semantics():
     e.ct6_flush()
     assert e.ct6_count() == 0
     e.close()
+
+
+def test_host_batch_entry_errors():
+    """cgpu_classify_v4_host (host-resident batches): a null
+    column or output is -EINVAL, a host-only context -ENODEV (no CPU path),
+    an empty batch is a no-op."""
+    e = Engine(device=-1)
+    L_ = lib()
+    n = 8
+    cols = [np.zeros(n, dt) for dt in (np.uint32, np.uint32, np.uint16, np.uint8, np.uint8,
+                                        np.uint32, np.uint16)]
+    v = np.zeros(n, np.int32)
+    i = np.zeros(n, np.uint32)
+    tv = TuplesV4(*[c.ctypes.data for c in cols])
+    assert L_.cgpu_classify_v4_host(e.h, C.byref(tv), n, v.ctypes.data, i.ctypes.data, None,
+                                    None) == -errno.ENODEV
+    assert L_.cgpu_classify_v4_host(e.h, C.byref(tv), n, None, i.ctypes.data, None,
+                                    None) == -errno.EINVAL
+    bad = TuplesV4(*([c.ctypes.data for c in cols[:3]] + [0] + [c.ctypes.data for c in cols[4:]]))
+    assert L_.cgpu_classify_v4_host(e.h, C.byref(bad), n, v.ctypes.data, i.ctypes.data, None,
+                                    None) == -errno.EINVAL
+    assert L_.cgpu_classify_v4_host(e.h, None, n, v.ctypes.data, i.ctypes.data, None,
+                                    None) == -errno.EINVAL
+    assert L_.cgpu_classify_v4_host(None, C.byref(tv), n, v.ctypes.data, i.ctypes.data, None,
+                                    None) == -errno.EINVAL
+    e.close()

@@ -1,0 +1,164 @@
+"""The composition of the endpoint program, compiled from the reference
+instead of restated.
+
+tests/golden/ct4.npz and ctlb4.npz were produced by oracle/ref/harness_ct.c
+and harness_ctlb.c, which call the reference's lib/ functions in the order
+bpf_lxc.c does, that order written out by hand.  oracle/ref/harness_lxc.c
+compiles bpf/bpf_lxc.c itself and runs its entry points tail_handle_ipv4
+(egress: handle_ipv4_from_lxc, bpf_lxc.c:408-669) and tail_ipv4_policy
+(ingress: ipv4_policy, :862-964).  Replaying each fixture's batches through
+it must reproduce the fixture: every packet's verdict, ct_lookup4 result,
+identity, policy stage, the frame after the service step, the conntrack map
+after every batch and the policy entries' counters.  Two known differences,
+both from the reference's build, not its logic:
+  * SECLABEL is node_config.h's compile-time 2 in the compiled program (the
+    agent generates it per endpoint), so an egress create's src_sec_id reads
+    2 where the fixture holds the endpoint's label;
+  * a proxy-redirected frame has its daddr / dport rewritten to the proxy
+    (lib/lxc.h:97-140), so the post-service frame is compared for the others.
+The ingress source identity is computed as bpf_netdev.c:374-404 does
+(restated: bpf_netdev.c is a separate program).
+
+Development container only: skipped where the reference harness was not
+built (it compiles /root/reference, which never reaches the GPU box)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from cilium_amd import layouts as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "_ref", "libref_lxc.so")
+pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason="reference harness not built (oracle/_ref)")
+
+SECLABEL_BUILD = 2  # bpf/node_config.h
+
+
+def _lib():
+    lib = C.CDLL(LIB)
+    vp, ip, u32p = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_uint32)
+    lib.ref_lxc_reset.argtypes = [C.c_size_t]
+    lib.ref_lxc_reset.restype = None
+    lib.ref_lxc_set_now.argtypes = [C.c_uint32]
+    lib.ref_lxc_set_now.restype = None
+    for f in ("ref_lxc_policy_update", "ref_lxc_policy_read"):
+        getattr(lib, f).argtypes = [C.c_int, vp, vp]
+    lib.ref_lxc_policy_delete.argtypes = [C.c_int, vp]
+    for f in ("ref_lxc_ipcache_update", "ref_lxc_svc_update", "ref_lxc_ct_update"):
+        getattr(lib, f).argtypes = [vp, vp]
+    lib.ref_lxc_svc_delete.argtypes = [vp]
+    lib.ref_lxc_ct_count.restype = C.c_size_t
+    lib.ref_lxc_ct_entry.argtypes = [C.c_size_t, vp, vp]
+    lib.ref_lxc_src_identity.argtypes = [C.c_uint32, C.c_uint32]
+    lib.ref_lxc_src_identity.restype = C.c_uint32
+    lib.ref_lxc_metrics.argtypes = [vp]
+    lib.ref_lxc_metrics.restype = None
+    lib.ref_lxc_v4.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_uint8, C.c_uint16,
+                               C.c_uint8, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, ip, u32p, ip, ip,
+                               u32p, C.POINTER(C.c_uint16)]
+    return lib
+
+
+def _b(x):
+    return np.ascontiguousarray(x).tobytes()
+
+
+def _dump(lib):
+    n = lib.ref_lxc_ct_count()
+    keys = np.zeros(n, L.CT4_TUPLE)
+    vals = np.zeros(n, L.CT_ENTRY)
+    kb, vb = C.create_string_buffer(14), C.create_string_buffer(56)
+    for i in range(n):
+        assert lib.ref_lxc_ct_entry(i, kb, vb) == 0
+        keys[i] = np.frombuffer(kb.raw, L.CT4_TUPLE)[0]
+        vals[i] = np.frombuffer(vb.raw, L.CT_ENTRY)[0]
+    return L.ct_sorted(keys, vals)
+
+
+def _run(lib, t, now, hashes=None):
+    n = len(t["saddr"])
+    out = {k: np.zeros(n, dt) for k, dt in (("verdict", np.int32), ("ct_ret", np.uint8),
+                                             ("identity", np.uint32), ("stage", np.uint8),
+                                             ("xdaddr", np.uint32), ("xdport", np.uint16))}
+    v, cr, st = C.c_int(), C.c_int(), C.c_int()
+    idv, xd = C.c_uint32(), C.c_uint32()
+    xp = C.c_uint16()
+    lib.ref_lxc_set_now(now)
+    for i in range(n):
+        eg = int(t["flags"][i]) & 1
+        src = 0 if eg else lib.ref_lxc_src_identity(int(t["saddr"][i]), 0)
+        lib.ref_lxc_v4(int(t["saddr"][i]), int(t["daddr"][i]), int(t["sport"][i]), int(t["dport"][i]),
+                       int(t["proto"][i]), int(t["l4b"][i]), int(t["flags"][i]), int(t["len"][i]),
+                       int(t["ep"][i]), int(hashes[i]) if hashes is not None else 0, src, C.byref(v),
+                       C.byref(idv), C.byref(cr), C.byref(st), C.byref(xd), C.byref(xp))
+        out["verdict"][i], out["ct_ret"][i], out["identity"][i] = v.value, cr.value, idv.value
+        out["stage"][i], out["xdaddr"][i], out["xdport"][i] = st.value, xd.value, xp.value
+    return out
+
+
+def _cmp_dump(got, want, seclabels):
+    (gk, gv), (wk, wv) = got, want
+    np.testing.assert_array_equal(gk, wk)
+    rest = [f for f in L.CT_ENTRY.names if f != "src_sec_id"]
+    for f in rest:
+        np.testing.assert_array_equal(gv[f], wv[f], err_msg=f)
+    same = gv["src_sec_id"] == wv["src_sec_id"]
+    built = (gv["src_sec_id"] == SECLABEL_BUILD) & np.isin(wv["src_sec_id"], seclabels)
+    assert (same | built).all()
+
+
+@pytest.mark.parametrize("fixture", ["ct4.npz", "ctlb4.npz"])
+def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
+    g = golden(fixture)
+    lib = _lib()
+    svc = "lb_keys" in g.files
+    lib.ref_lxc_reset(1 << 20)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        lib.ref_lxc_ipcache_update(_b(k), _b(v))
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert lib.ref_lxc_policy_update(int(ep), _b(k), _b(e)) == 0
+    if svc:
+        for k, v in zip(g["lb_keys"], g["lb_vals"]):
+            lib.ref_lxc_svc_update(_b(k), _b(v))
+    for k, v in zip(g["pre_keys"], g["pre_vals"]):
+        assert lib.ref_lxc_ct_update(_b(k), _b(v)) == 0
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    cuts, nows = g["cuts"], g["nows"]
+    off = 0
+    for bi in range(4):
+        if bi == 2:
+            for d in g["pol_del"]:
+                assert lib.ref_lxc_policy_delete(int(g["pol_ep"][d]), _b(g["pol_keys"][d])) == 0
+            if svc:
+                for d in g["svc_del"]:
+                    assert lib.ref_lxc_svc_delete(_b(g["lb_keys"][d])) == 0
+        if bi == 3 and svc:
+            for d, v in zip(g["svc_readd"], g["readd_vals"]):
+                lib.ref_lxc_svc_update(_b(g["lb_keys"][d]), _b(v))
+        sl = slice(int(cuts[bi]), int(cuts[bi + 1]))
+        tb = {k: x[sl] for k, x in t.items()}
+        o = _run(lib, tb, int(nows[bi]), tb.get("hash"))
+        msg = f"{fixture} batch {bi}"
+        np.testing.assert_array_equal(o["verdict"], g["b_verdict"][sl], err_msg=msg)
+        np.testing.assert_array_equal(o["ct_ret"], g["b_ct_ret"][sl], err_msg=msg)
+        np.testing.assert_array_equal(o["identity"], g["b_identity"][sl], err_msg=msg)
+        probed = g["b_stage"][sl] <= 3
+        np.testing.assert_array_equal(o["stage"][probed], g["b_stage"][sl][probed], err_msg=msg)
+        if svc:
+            eg = (tb["flags"] & 1).astype(bool) & (o["verdict"] <= 0)
+            np.testing.assert_array_equal(o["xdaddr"][eg], g["b_xdaddr"][sl][eg], err_msg=msg)
+            np.testing.assert_array_equal(o["xdport"][eg], g["b_xdport"][sl][eg], err_msg=msg)
+        n = int(g["dump_n"][bi])
+        _cmp_dump(_dump(lib), (g["dump_keys"][off:off + n], g["dump_vals"][off:off + n]),
+                  g["seclabels"])
+        off += n
+    deleted = set(g["pol_del"].tolist())
+    buf = C.create_string_buffer(24)
+    for i, (k, ep, fe) in enumerate(zip(g["pol_keys"], g["pol_ep"], g["final_entries"])):
+        if i in deleted:
+            continue
+        assert lib.ref_lxc_policy_read(int(ep), _b(k), buf) == 0
+        got = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
