@@ -55,7 +55,7 @@
 
 #define REF_MAX_EP 64
 
-static struct mockmap ct, svc_m, ipcache, metrics_m, policy_maps[REF_MAX_EP];
+static struct mockmap ct, ct6, svc_m, svc6_m, ipcache, metrics_m, policy_maps[REF_MAX_EP];
 static size_t ct_max = 1u << 20;
 static int cur_ep, inited;
 static uint64_t now_ns;
@@ -106,6 +106,18 @@ static void *mock_lookup(void *map, const void *key)
 		}
 		return v;
 	}
+	if (map == &CT_MAP6) {
+		const struct ipv6_ct_tuple *k = key;
+		void *v = mockmap_lookup(&ct6, key);
+		if (!(k->flags & TUPLE_F_SERVICE) && n_ct_lookups < 2) {
+			ct_hit[n_ct_lookups] = v != NULL;
+			ct_rel[n_ct_lookups] = (k->flags & TUPLE_F_RELATED) != 0;
+			n_ct_lookups++;
+		}
+		return v;
+	}
+	if (map == &cilium_lb6_services)
+		return mockmap_lookup(&svc6_m, key);
 	if (map == &cilium_ipcache)
 		return mockmap_lookup(&ipcache, key);
 	if (map == &cilium_lb4_services)
@@ -125,8 +137,16 @@ static int mock_update(void *map, const void *key, const void *val, uint32_t fla
 		mockmap_update(&ct, key, val);
 		return 0;
 	}
+	if (map == &CT_MAP6) {
+		if (!mockmap_lookup(&ct6, key) && ct6.n >= ct_max)
+			return -7;
+		mockmap_update(&ct6, key, val);
+		return 0;
+	}
 	if (map == &cilium_metrics)
 		return mockmap_update(&metrics_m, key, val) < 0 ? -1 : 0;
+	if (map == &cilium_proxy6)
+		proxied = 1; /* ipv6_redirect_to_host_port's proxy6 entry */
 	if (map == &cilium_proxy4)
 		proxied = 1; /* ipv4_redirect_to_host_port's proxy4 entry (lib/lxc.h:141) */
 	return 0; /* the proxy map: accepted, not read back */
@@ -136,6 +156,8 @@ static int mock_delete(void *map, const void *key)
 {
 	if (map == &CT_MAP4)
 		return mockmap_delete(&ct, key) ? 0 : -2;
+	if (map == &CT_MAP6)
+		return mockmap_delete(&ct6, key) ? 0 : -2;
 	return -2;
 }
 
@@ -196,6 +218,8 @@ static int ensure_init(void)
 	mockmap_init(&ipcache, MOCK_LPM, sizeof(struct ipcache_key), sizeof(struct remote_endpoint_info));
 	mockmap_init(&ct, MOCK_HASH, sizeof(struct ipv4_ct_tuple), sizeof(struct ct_entry));
 	mockmap_init(&svc_m, MOCK_HASH, sizeof(struct lb4_key), sizeof(struct lb4_service));
+	mockmap_init(&ct6, MOCK_HASH, sizeof(struct ipv6_ct_tuple), sizeof(struct ct_entry));
+	mockmap_init(&svc6_m, MOCK_HASH, sizeof(struct lb6_key), sizeof(struct lb6_service));
 	mockmap_init(&metrics_m, MOCK_HASH, sizeof(struct metrics_key), sizeof(struct metrics_value));
 	frame_buf = mmap(NULL, 1 << 12, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_32BIT, -1, 0);
 	if (frame_buf == MAP_FAILED)
@@ -228,6 +252,8 @@ void ref_lxc_reset(size_t max_elem)
 	mockmap_clear(&ipcache);
 	mockmap_clear(&ct);
 	mockmap_clear(&svc_m);
+	mockmap_clear(&ct6);
+	mockmap_clear(&svc6_m);
 	mockmap_clear(&metrics_m);
 	ct_max = max_elem;
 }
@@ -254,6 +280,18 @@ int ref_lxc_ipcache_update(const void *key, const void *info) { ensure_init(); r
 int ref_lxc_svc_update(const void *key, const void *val) { ensure_init(); return mockmap_update(&svc_m, key, val); }
 int ref_lxc_svc_delete(const void *key) { ensure_init(); return mockmap_delete(&svc_m, key) ? 0 : -2; }
 int ref_lxc_ct_update(const void *key, const void *val) { ensure_init(); return mock_update(&CT_MAP4, key, val, 0); }
+int ref_lxc_svc6_update(const void *key, const void *val) { ensure_init(); return mockmap_update(&svc6_m, key, val); }
+int ref_lxc_svc6_delete(const void *key) { ensure_init(); return mockmap_delete(&svc6_m, key) ? 0 : -2; }
+int ref_lxc_ct6_update(const void *key, const void *val) { ensure_init(); return mock_update(&CT_MAP6, key, val, 0); }
+size_t ref_lxc_ct6_count(void) { return ct6.n; }
+int ref_lxc_ct6_entry(size_t i, void *key_out, void *val_out)
+{
+	if (i >= ct6.n)
+		return -1;
+	memcpy(key_out, ct6.keys + i * ct6.ksz, ct6.ksz);
+	memcpy(val_out, ct6.vals + i * ct6.vsz, ct6.vsz);
+	return 0;
+}
 size_t ref_lxc_ct_count(void) { return ct.n; }
 int ref_lxc_ct_entry(size_t i, void *key_out, void *val_out)
 {
@@ -279,6 +317,20 @@ uint32_t ref_lxc_src_identity(uint32_t saddr_be, uint32_t src)
 	return src;
 }
 
+/* the same for IPv6 (bpf_netdev.c:203-211: no HOST_ID exception) */
+uint32_t ref_lxc_src_identity6(const uint8_t *saddr16, uint32_t src)
+{
+	struct remote_endpoint_info *info;
+	union v6addr sa;
+	memcpy(&sa, saddr16, 16);
+	if (identity_is_reserved(src)) {
+		info = ipcache_lookup6(&cilium_ipcache, &sa, V6_CACHE_KEY_LEN);
+		if (info && info->sec_label && info->sec_label != CLUSTER_ID)
+			src = info->sec_label;
+	}
+	return src;
+}
+
 /* cilium_metrics as [256 reasons][4 dirs][count, bytes] */
 void ref_lxc_metrics(uint64_t *out)
 {
@@ -290,6 +342,9 @@ void ref_lxc_metrics(uint64_t *out)
 		out[(k->reason * 4u + k->dir) * 2u + 1u] = v->bytes;
 	}
 }
+
+static void reset_obs(void);
+static void outcome(uint8_t flags, uint32_t l4_off, int *verdict, uint32_t *identity, int *ct_ret, int *stage);
 
 /* Ethernet + IPv4 (ihl 5, ttl 64) + a 20-byte L4 header from the tuple
  * columns, the stream harnesses' frame */
@@ -345,10 +400,7 @@ int ref_lxc_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t sport_be, uint16_t
 	skb.protocol = bpf_htons(ETH_P_IP);
 	inj_hash = hash;
 	cur_ep = ep;
-	n_ct_lookups = n_probes = probe_hit_at = 0;
-	ct_hit[0] = ct_hit[1] = ct_rel[0] = ct_rel[1] = 0;
-	probe_label = 0;
-	drop_reason = proxied = 0;
+	reset_obs();
 	if (flags & 1) {
 		ret = tail_handle_ipv4(&skb);
 		memcpy(xdaddr, frame_buf + ETH_HLEN + 16, 4);
@@ -359,11 +411,25 @@ int ref_lxc_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t sport_be, uint16_t
 		*xdaddr = daddr_be;
 		*xdport = dport_be;
 	}
+	outcome(flags, ETH_HLEN + 20, verdict, identity, ct_ret, stage);
+	return ret;
+}
+
+static void reset_obs(void)
+{
+	n_ct_lookups = n_probes = probe_hit_at = 0;
+	ct_hit[0] = ct_hit[1] = ct_rel[0] = ct_rel[1] = 0;
+	probe_label = 0;
+	drop_reason = proxied = 0;
+}
+
+static void outcome(uint8_t flags, uint32_t l4_off, int *verdict, uint32_t *identity, int *ct_ret, int *stage)
+{
 	if (drop_reason) {
 		*verdict = -drop_reason;
 	} else if (proxied) {
 		uint16_t p;
-		memcpy(&p, frame_buf + ETH_HLEN + 20 + 2, 2); /* l4_modify_port's new_port */
+		memcpy(&p, frame_buf + l4_off + 2, 2); /* l4_modify_port's new_port */
 		*verdict = p;
 	} else {
 		*verdict = 0;
@@ -380,5 +446,67 @@ int ref_lxc_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t sport_be, uint16_t
 		*ct_ret = CT_ESTABLISHED;
 	else
 		*ct_ret = CT_NEW;
+}
+
+/* Ethernet + IPv6 (no extension headers, hop limit 64) + a 20-byte L4
+ * header */
+static void build_frame6(const uint8_t *sa16, const uint8_t *da16, uint16_t sport, uint16_t dport,
+			 uint8_t proto, uint16_t l4w)
+{
+	memset(frame_buf, 0, 96);
+	frame_buf[12] = 0x86;
+	frame_buf[13] = 0xDD;
+	struct ipv6hdr *ip6 = (struct ipv6hdr *)(frame_buf + ETH_HLEN);
+	ip6->version = 6;
+	ip6->nexthdr = proto;
+	ip6->payload_len = bpf_htons(20);
+	ip6->hop_limit = 64;
+	memcpy(&ip6->saddr, sa16, 16);
+	memcpy(&ip6->daddr, da16, 16);
+	uint8_t *l4 = frame_buf + ETH_HLEN + 40;
+	if (proto == IPPROTO_ICMPV6) {
+		l4[0] = (uint8_t)l4w;
+	} else {
+		memcpy(l4, &sport, 2);
+		memcpy(l4 + 2, &dport, 2);
+		if (proto == IPPROTO_TCP) {
+			l4[12] = (uint8_t)l4w;
+			l4[13] = (uint8_t)(l4w >> 8);
+		}
+	}
+	frame_len = ETH_HLEN + 60;
+}
+
+/* One IPv6 packet: tail_handle_ipv6 (bpf_lxc.c:365-403) or tail_ipv6_policy
+ * (:718-860); outputs as ref_lxc_v4, xdaddr 16 bytes */
+int ref_lxc_v6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t sport_be, uint16_t dport_be,
+	       uint8_t proto, uint16_t l4w, uint8_t flags, uint32_t len, int ep, uint32_t hash, uint32_t src_label,
+	       int *verdict, uint32_t *identity, int *ct_ret, int *stage, uint8_t *xdaddr16, uint16_t *xdport)
+{
+	struct __sk_buff skb;
+	int ret;
+
+	if (ensure_init() || ep < 0 || ep >= REF_MAX_EP)
+		return -1;
+	build_frame6(saddr16, daddr16, sport_be, dport_be, proto, l4w);
+	memset(&skb, 0, sizeof(skb));
+	skb.data = (uint32_t)(unsigned long)frame_buf;
+	skb.data_end = (uint32_t)(unsigned long)(frame_buf + frame_len);
+	skb.len = len;
+	skb.protocol = bpf_htons(ETH_P_IPV6);
+	inj_hash = hash;
+	cur_ep = ep;
+	reset_obs();
+	if (flags & 1) {
+		ret = tail_handle_ipv6(&skb);
+		memcpy(xdaddr16, frame_buf + ETH_HLEN + 24, 16);
+		memcpy(xdport, frame_buf + ETH_HLEN + 40 + 2, 2);
+	} else {
+		skb.cb[CB_SRC_LABEL] = src_label;
+		ret = tail_ipv6_policy(&skb);
+		memcpy(xdaddr16, daddr16, 16);
+		*xdport = dport_be;
+	}
+	outcome(flags & 1, ETH_HLEN + 40, verdict, identity, ct_ret, stage);
 	return ret;
 }

@@ -1,12 +1,14 @@
 """The composition of the endpoint program, compiled from the reference
 instead of restated.
 
-tests/golden/ct4.npz and ctlb4.npz were produced by oracle/ref/harness_ct.c
-and harness_ctlb.c, which call the reference's lib/ functions in the order
-bpf_lxc.c does, that order written out by hand.  oracle/ref/harness_lxc.c
-compiles bpf/bpf_lxc.c itself and runs its entry points tail_handle_ipv4
-(egress: handle_ipv4_from_lxc, bpf_lxc.c:408-669) and tail_ipv4_policy
-(ingress: ipv4_policy, :862-964).  Replaying each fixture's batches through
+tests/golden/ct4.npz, ctlb4.npz, ct6.npz and ctlb6.npz were produced by
+oracle/ref/harness_ct.c and harness_ctlb.c, which call the reference's lib/
+functions in the order bpf_lxc.c does, that order written out by hand.
+oracle/ref/harness_lxc.c compiles bpf/bpf_lxc.c itself and runs its entry
+points tail_handle_ipv4 / tail_handle_ipv6 (egress: handle_ipv4_from_lxc,
+bpf_lxc.c:408-669; handle_ipv6 -> ipv6_l3_from_lxc, :82-403) and
+tail_ipv4_policy / tail_ipv6_policy (ingress: ipv4_policy, :862-964;
+ipv6_policy, :718-860).  Replaying each fixture's batches through
 it must reproduce the fixture: every packet's verdict, ct_lookup4 result,
 identity, policy stage, the frame after the service step, the conntrack map
 after every batch and the policy entries' counters.  Two known differences,
@@ -16,8 +18,9 @@ both from the reference's build, not its logic:
     2 where the fixture holds the endpoint's label;
   * a proxy-redirected frame has its daddr / dport rewritten to the proxy
     (lib/lxc.h:97-140), so the post-service frame is compared for the others.
-The ingress source identity is computed as bpf_netdev.c:374-404 does
-(restated: bpf_netdev.c is a separate program).
+The ingress source identity is computed as bpf_netdev.c:374-404 / :203-211
+do (restated: bpf_netdev.c is a separate program), through the harness's
+own ipcache_lookup4 / ipcache_lookup6.
 
 Development container only: skipped where the reference harness was not
 built (it compiles /root/reference, which never reaches the GPU box)."""
@@ -58,6 +61,16 @@ def _lib():
     lib.ref_lxc_v4.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_uint8, C.c_uint16,
                                C.c_uint8, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, ip, u32p, ip, ip,
                                u32p, C.POINTER(C.c_uint16)]
+    lib.ref_lxc_v6.argtypes = [C.c_char_p, C.c_char_p, C.c_uint16, C.c_uint16, C.c_uint8, C.c_uint16,
+                               C.c_uint8, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, ip, u32p, ip, ip,
+                               C.c_char_p, C.POINTER(C.c_uint16)]
+    lib.ref_lxc_src_identity6.argtypes = [C.c_char_p, C.c_uint32]
+    lib.ref_lxc_src_identity6.restype = C.c_uint32
+    for f in ("ref_lxc_svc6_update", "ref_lxc_ct6_update"):
+        getattr(lib, f).argtypes = [vp, vp]
+    lib.ref_lxc_svc6_delete.argtypes = [vp]
+    lib.ref_lxc_ct6_count.restype = C.c_size_t
+    lib.ref_lxc_ct6_entry.argtypes = [C.c_size_t, vp, vp]
     return lib
 
 
@@ -65,36 +78,49 @@ def _b(x):
     return np.ascontiguousarray(x).tobytes()
 
 
-def _dump(lib):
-    n = lib.ref_lxc_ct_count()
-    keys = np.zeros(n, L.CT4_TUPLE)
+def _dump(lib, v6):
+    n = (lib.ref_lxc_ct6_count if v6 else lib.ref_lxc_ct_count)()
+    kt = L.CT6_TUPLE if v6 else L.CT4_TUPLE
+    keys = np.zeros(n, kt)
     vals = np.zeros(n, L.CT_ENTRY)
-    kb, vb = C.create_string_buffer(14), C.create_string_buffer(56)
+    kb, vb = C.create_string_buffer(kt.itemsize), C.create_string_buffer(56)
     for i in range(n):
-        assert lib.ref_lxc_ct_entry(i, kb, vb) == 0
-        keys[i] = np.frombuffer(kb.raw, L.CT4_TUPLE)[0]
+        assert (lib.ref_lxc_ct6_entry if v6 else lib.ref_lxc_ct_entry)(i, kb, vb) == 0
+        keys[i] = np.frombuffer(kb.raw, kt)[0]
         vals[i] = np.frombuffer(vb.raw, L.CT_ENTRY)[0]
     return L.ct_sorted(keys, vals)
 
 
 def _run(lib, t, now, hashes=None):
     n = len(t["saddr"])
+    v6 = np.asarray(t["saddr"]).ndim == 2
     out = {k: np.zeros(n, dt) for k, dt in (("verdict", np.int32), ("ct_ret", np.uint8),
                                              ("identity", np.uint32), ("stage", np.uint8),
-                                             ("xdaddr", np.uint32), ("xdport", np.uint16))}
+                                             ("xdport", np.uint16))}
+    out["xdaddr"] = np.zeros((n, 16), np.uint8) if v6 else np.zeros(n, np.uint32)
     v, cr, st = C.c_int(), C.c_int(), C.c_int()
     idv, xd = C.c_uint32(), C.c_uint32()
+    xd6 = C.create_string_buffer(16)
     xp = C.c_uint16()
     lib.ref_lxc_set_now(now)
     for i in range(n):
         eg = int(t["flags"][i]) & 1
-        src = 0 if eg else lib.ref_lxc_src_identity(int(t["saddr"][i]), 0)
-        lib.ref_lxc_v4(int(t["saddr"][i]), int(t["daddr"][i]), int(t["sport"][i]), int(t["dport"][i]),
-                       int(t["proto"][i]), int(t["l4b"][i]), int(t["flags"][i]), int(t["len"][i]),
-                       int(t["ep"][i]), int(hashes[i]) if hashes is not None else 0, src, C.byref(v),
-                       C.byref(idv), C.byref(cr), C.byref(st), C.byref(xd), C.byref(xp))
+        h = int(hashes[i]) if hashes is not None else 0
+        cols = (int(t["sport"][i]), int(t["dport"][i]), int(t["proto"][i]), int(t["l4b"][i]),
+                int(t["flags"][i]), int(t["len"][i]), int(t["ep"][i]), h)
+        if v6:
+            sa, da = t["saddr"][i].tobytes(), t["daddr"][i].tobytes()
+            src = 0 if eg else lib.ref_lxc_src_identity6(sa, 0)
+            lib.ref_lxc_v6(sa, da, *cols, src, C.byref(v), C.byref(idv), C.byref(cr), C.byref(st), xd6,
+                           C.byref(xp))
+            out["xdaddr"][i] = np.frombuffer(xd6.raw, np.uint8)
+        else:
+            src = 0 if eg else lib.ref_lxc_src_identity(int(t["saddr"][i]), 0)
+            lib.ref_lxc_v4(int(t["saddr"][i]), int(t["daddr"][i]), *cols, src, C.byref(v), C.byref(idv),
+                           C.byref(cr), C.byref(st), C.byref(xd), C.byref(xp))
+            out["xdaddr"][i] = xd.value
         out["verdict"][i], out["ct_ret"][i], out["identity"][i] = v.value, cr.value, idv.value
-        out["stage"][i], out["xdaddr"][i], out["xdport"][i] = st.value, xd.value, xp.value
+        out["stage"][i], out["xdport"][i] = st.value, xp.value
     return out
 
 
@@ -109,11 +135,14 @@ def _cmp_dump(got, want, seclabels):
     assert (same | built).all()
 
 
-@pytest.mark.parametrize("fixture", ["ct4.npz", "ctlb4.npz"])
+@pytest.mark.parametrize("fixture", ["ct4.npz", "ctlb4.npz", "ct6.npz", "ctlb6.npz"])
 def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
     g = golden(fixture)
     lib = _lib()
     svc = "lb_keys" in g.files
+    v6 = "6" in fixture
+    svc_update = lib.ref_lxc_svc6_update if v6 else lib.ref_lxc_svc_update
+    svc_delete = lib.ref_lxc_svc6_delete if v6 else lib.ref_lxc_svc_delete
     lib.ref_lxc_reset(1 << 20)
     for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
         lib.ref_lxc_ipcache_update(_b(k), _b(v))
@@ -121,9 +150,9 @@ def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
         assert lib.ref_lxc_policy_update(int(ep), _b(k), _b(e)) == 0
     if svc:
         for k, v in zip(g["lb_keys"], g["lb_vals"]):
-            lib.ref_lxc_svc_update(_b(k), _b(v))
+            svc_update(_b(k), _b(v))
     for k, v in zip(g["pre_keys"], g["pre_vals"]):
-        assert lib.ref_lxc_ct_update(_b(k), _b(v)) == 0
+        assert (lib.ref_lxc_ct6_update if v6 else lib.ref_lxc_ct_update)(_b(k), _b(v)) == 0
     t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
     cuts, nows = g["cuts"], g["nows"]
     off = 0
@@ -133,10 +162,10 @@ def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
                 assert lib.ref_lxc_policy_delete(int(g["pol_ep"][d]), _b(g["pol_keys"][d])) == 0
             if svc:
                 for d in g["svc_del"]:
-                    assert lib.ref_lxc_svc_delete(_b(g["lb_keys"][d])) == 0
+                    assert svc_delete(_b(g["lb_keys"][d])) == 0
         if bi == 3 and svc:
             for d, v in zip(g["svc_readd"], g["readd_vals"]):
-                lib.ref_lxc_svc_update(_b(g["lb_keys"][d]), _b(v))
+                svc_update(_b(g["lb_keys"][d]), _b(v))
         sl = slice(int(cuts[bi]), int(cuts[bi + 1]))
         tb = {k: x[sl] for k, x in t.items()}
         o = _run(lib, tb, int(nows[bi]), tb.get("hash"))
@@ -151,7 +180,7 @@ def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
             np.testing.assert_array_equal(o["xdaddr"][eg], g["b_xdaddr"][sl][eg], err_msg=msg)
             np.testing.assert_array_equal(o["xdport"][eg], g["b_xdport"][sl][eg], err_msg=msg)
         n = int(g["dump_n"][bi])
-        _cmp_dump(_dump(lib), (g["dump_keys"][off:off + n], g["dump_vals"][off:off + n]),
+        _cmp_dump(_dump(lib, v6), (g["dump_keys"][off:off + n], g["dump_vals"][off:off + n]),
                   g["seclabels"])
         off += n
     deleted = set(g["pol_del"].tolist())
