@@ -259,6 +259,13 @@ void ref_lxc_reset(size_t max_elem)
 }
 
 void ref_lxc_set_now(uint32_t sec) { now_ns = (uint64_t)sec * NSEC_PER_SEC; }
+/* empty conntrack maps: the stateless decision (every packet CT_NEW) */
+void ref_lxc_ct_clear(void)
+{
+	ensure_init();
+	mockmap_clear(&ct);
+	mockmap_clear(&ct6);
+}
 int ref_lxc_policy_update(int ep, const void *key, const void *entry)
 {
 	ensure_init();

@@ -46,6 +46,7 @@ def _lib():
     lib.ref_lxc_reset.restype = None
     lib.ref_lxc_set_now.argtypes = [C.c_uint32]
     lib.ref_lxc_set_now.restype = None
+    lib.ref_lxc_ct_clear.restype = None
     for f in ("ref_lxc_policy_update", "ref_lxc_policy_read"):
         getattr(lib, f).argtypes = [C.c_int, vp, vp]
     lib.ref_lxc_policy_delete.argtypes = [C.c_int, vp]
@@ -191,3 +192,44 @@ def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
         assert lib.ref_lxc_policy_read(int(ep), _b(k), buf) == 0
         got = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
         assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+
+
+@pytest.mark.parametrize("cfg", [0, 2, 3, 4])
+def test_compiled_endpoint_program_reproduces_stateless_fixture(golden, cfg):
+    """tests/golden/classify_v4.npz (harness_policy.c: the stateless
+    decision, every packet CT_NEW) under its CONNTRACK configurations: the
+    compiled program with an empty conntrack map before every packet gives
+    the fixture's verdict, identity and stage for every TCP / UDP tuple
+    (ICMP tuples carry a policy port the frame's type does not; the other
+    protocols are the gate's, compared too)."""
+    g = golden("classify_v4.npz")
+    gate, src_cfg, secctx_world = (int(x) for x in g["configs"][cfg])
+    assert gate == 1
+    lib = _lib()
+    lib.ref_lxc_reset(1 << 20)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        lib.ref_lxc_ipcache_update(_b(k), _b(v))
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert lib.ref_lxc_policy_update(int(ep), _b(k), _b(e)) == 0
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    n = len(t["saddr"])
+    v, cr, st = C.c_int(), C.c_int(), C.c_int()
+    idv, xd = C.c_uint32(), C.c_uint32()
+    xp = C.c_uint16()
+    got = np.zeros((n, 3), np.int64)
+    for i in range(n):
+        lib.ref_lxc_ct_clear()
+        eg = int(t["flags"][i]) & 1
+        src = 0
+        if not eg:
+            src = 2 if secctx_world else lib.ref_lxc_src_identity(int(t["saddr"][i]), src_cfg)
+        lib.ref_lxc_v4(int(t["saddr"][i]), int(t["daddr"][i]), 0, int(t["dport"][i]), int(t["proto"][i]),
+                       0, int(t["flags"][i]), int(t["len"][i]), int(t["ep"][i]), 0, src, C.byref(v),
+                       C.byref(idv), C.byref(cr), C.byref(st), C.byref(xd), C.byref(xp))
+        got[i] = v.value, idv.value, st.value
+    keep = t["proto"] != 1
+    gated = ~np.isin(t["proto"], [1, 6, 17])
+    assert keep.sum() > 4000 and gated.sum() > 0
+    np.testing.assert_array_equal(got[keep, 0], g[f"c{cfg}_verdict"][keep])
+    np.testing.assert_array_equal(got[keep & ~gated, 1], g[f"c{cfg}_identity"][keep & ~gated])
+    np.testing.assert_array_equal(got[keep & ~gated, 2], g[f"c{cfg}_stage"][keep & ~gated])
