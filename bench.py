@@ -201,6 +201,9 @@ def main():
                     help="skip the restatement entirely (profiling passes: tools/profile.sh)")
     ap.add_argument("--hot-slots", type=int, default=0,
                     help="cgpu_config.hot_counter_slots (LDS counter slots; 0 = library default)")
+    ap.add_argument("--schedule", type=int, default=0,
+                    help="cgpu_config.schedule (CGPU_SCHED_*, A/B timing of the fallback schedules; "
+                         "0 = the tuned default)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-rebalance", action="store_true",
                     help="keep the class-based counter slots (no cgpu_counters_rebalance after warmup)")
@@ -310,7 +313,7 @@ def main():
             ecfg["hot_counter_slots"] = args.hot_slots
         if S is not None:
             ecfg["lb_max_entries"] = len(S.keys)
-        e = Engine(device=local, **ecfg)
+        e = Engine(device=local, **ecfg, schedule=args.schedule)
         synth.load_engine(e, T)
         if S is not None:
             synth.load_services(e, S)
@@ -630,6 +633,8 @@ def main():
                                   f"popularity-rebalanced after warmup ({moved} keys moved)"),
                 "probes_per_tuple": round(probes_per, 4), "b_alg_per_tuple": round(b_alg, 2),
                 "parity_vs_oracle": parity}
+        if args.schedule:
+            conf["schedule"] = args.schedule
         if args.host_tuples:
             bw = link_rates(torch, dev)
             per_in, per_out = B_IN, B_OUT  # bytes up / down per tuple

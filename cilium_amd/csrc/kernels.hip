@@ -1051,10 +1051,9 @@ __device__ __forceinline__ void policy_q(const cgpu_snapshot &s, const bool (&ac
  * has 64.  Same results as decide<0> tuple by tuple (the stateful path's
  * prep and finish passes; the dictionary is read from global memory). */
 template <int Q>
-__device__ __forceinline__ void decide4_q(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&eg)[Q],
-					  const bool (&frag)[Q], const uint32_t (&sa)[Q], const uint32_t (&da)[Q],
-					  const uint32_t (&dport)[Q], const uint32_t (&proto)[Q],
-					  const uint32_t (&ep)[Q], decision (&d)[Q])
+__device__ __forceinline__ void ident4_q(const cgpu_snapshot &s, const uint32_t *dict, const bool (&act)[Q],
+					 const bool (&eg)[Q], const uint32_t (&sa)[Q], const uint32_t (&da)[Q],
+					 decision (&d)[Q])
 {
 	const lpm16c &t = s.ipc4c;
 	uint32_t h[Q], e[Q];
@@ -1071,7 +1070,7 @@ __device__ __forceinline__ void decide4_q(const cgpu_snapshot &s, const bool (&a
 			const uint32_t cnt = (x >= (q[u].x & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].x >> 16) ? 1u : 0u) +
 					     (x >= (q[u].y & 0xFFFFu) ? 1u : 0u) + (x >= (q[u].y >> 16) ? 1u : 0u);
 			const uint64_t v = ((uint64_t)q[u].w << 32) | q[u].z;
-			e[u] = act[u] ? t.dict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
+			e[u] = act[u] ? dict[(uint32_t)(v >> (12u * cnt)) & 0xFFFu] : 0u;
 		} else {
 			e[u] = lpmc_lookup(t, t.dict, eg[u] ? da[u] : sa[u]);
 		}
@@ -1090,7 +1089,135 @@ __device__ __forceinline__ void decide4_q(const cgpu_snapshot &s, const bool (&a
 			d[u].id = s.ingress_secctx_world ? s.world_id : src;
 		}
 	}
+}
+
+template <int Q>
+__device__ __forceinline__ void decide4_q(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&eg)[Q],
+					  const bool (&frag)[Q], const uint32_t (&sa)[Q], const uint32_t (&da)[Q],
+					  const uint32_t (&dport)[Q], const uint32_t (&proto)[Q],
+					  const uint32_t (&ep)[Q], decision (&d)[Q])
+{
+	ident4_q<Q>(s, s.ipc4c.dict, act, eg, sa, da, d);
 	policy_q<Q>(s, act, eg, frag, dport, proto, ep, d);
+}
+
+/* policy_q's cascade for the two dports one conntrack packet's policy step
+ * can see (k_ct_decide: the forward tuple's, dpf, and the reply tuple's,
+ * dpr, where act2), for Q tuples whose identity d[u].id is set, through the
+ * group table as k_classify_x4 (tables.h pol_groups): one gather of the
+ * {identity, endpoint, direction} group slot serves both - probe 2 is its
+ * L3 key, and its bloom over the group's (dport, proto) admits probe 1 only
+ * where an exact key can exist; probe 3 gathers directly.  Both tuples'
+ * probes of a stage are in flight together.  Results as policy_q. */
+template <int Q>
+__device__ __forceinline__ void policy2_qg(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&act2)[Q],
+					   const bool (&eg)[Q], const bool (&frag)[Q], const uint32_t (&dpf)[Q],
+					   const uint32_t (&dpr)[Q], const uint32_t (&proto)[Q],
+					   const uint32_t (&ep)[Q], decision (&d)[Q], decision (&d2)[Q])
+{
+	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
+	const uint32_t pm = s.pol.bucket_mask;
+	uint4 grp[Q], sf[Q], sr[Q];
+	uint32_t bg[Q], hf[Q], hr[Q], zf[Q], zr[Q], bf[Q], br[Q];
+	int cf[Q], cr[Q];
+	bool n1f[Q], n1r[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		grp[u] = make_uint4(0, 0, POL_CTR_EMPTY, 0);
+		bg[u] = pg_hash(d[u].id, ep[u] | (eg[u] ? 1u << 16 : 0u)) & s.pg.mask;
+		if (act[u])
+			grp[u] = s.pg.slots[bg[u]];
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (act[u])
+			grp[u] = pg_resolve(s.pg, grp[u], bg[u], d[u].id, ep[u] | (eg[u] ? 1u << 16 : 0u));
+		const uint32_t egw = eg[u] ? (1u << 24) : 0u;
+		hf[u] = dpf[u] | (proto[u] << 16) | egw;
+		hr[u] = dpr[u] | (proto[u] << 16) | egw;
+		cf[u] = cr[u] = -1;
+		zf[u] = zr[u] = 0;
+		d[u].st = d2[u].st = 0;
+		const uint32_t blf = pg_bloom(dpf[u], proto[u]), blr = pg_bloom(dpr[u], proto[u]);
+		n1f[u] = act[u] && !frag[u] && (grp[u].w & blf) == blf;
+		n1r[u] = act2[u] && !frag[u] && (grp[u].w & blr) == blr;
+	}
+	/* probe 1: {id, dport, proto, dir} (policy.h:61-72) */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (n1f[u]) {
+			bf[u] = pol_hash(d[u].id, hf[u], ep[u]) & pm;
+			sf[u] = ptab[bf[u]];
+		}
+		if (n1r[u]) {
+			br[u] = pol_hash(d[u].id, hr[u], ep[u]) & pm;
+			sr[u] = ptab[br[u]];
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (n1f[u]) {
+			cf[u] = pol_resolve1(s.pol, sf[u], bf[u], d[u].id, hf[u], ep[u], &zf[u]);
+			d[u].st = 1;
+		}
+		if (n1r[u]) {
+			cr[u] = pol_resolve1(s.pol, sr[u], br[u], d[u].id, hr[u], ep[u], &zr[u]);
+			d2[u].st = 1;
+		}
+		/* probe 2: {id, any port, dir} (policy.h:74-83), the group's */
+		const bool l3 = (grp[u].z & POL_CTR_MASK) != POL_CTR_EMPTY;
+		if (act[u] && cf[u] < 0) {
+			d[u].st = 2;
+			if (l3) {
+				cf[u] = (int)(grp[u].z & POL_CTR_MASK);
+				zf[u] = 0;
+			}
+		}
+		if (act2[u] && cr[u] < 0) {
+			d2[u].st = 2;
+			if (l3) {
+				cr[u] = (int)(grp[u].z & POL_CTR_MASK);
+				zr[u] = 0;
+			}
+		}
+	}
+	/* probe 3: {any identity, dport, proto, dir} (policy.h:85-96) */
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (act[u] && cf[u] < 0 && !frag[u]) {
+			bf[u] = pol_hash(0u, hf[u], ep[u]) & pm;
+			sf[u] = ptab[bf[u]];
+		}
+		if (act2[u] && cr[u] < 0 && !frag[u]) {
+			br[u] = pol_hash(0u, hr[u], ep[u]) & pm;
+			sr[u] = ptab[br[u]];
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (act[u] && cf[u] < 0 && !frag[u]) {
+			cf[u] = pol_resolve1(s.pol, sf[u], bf[u], 0u, hf[u], ep[u], &zf[u]);
+			d[u].st = 3;
+		}
+		if (act2[u] && cr[u] < 0 && !frag[u]) {
+			cr[u] = pol_resolve1(s.pol, sr[u], br[u], 0u, hr[u], ep[u], &zr[u]);
+			d2[u].st = 3;
+		}
+		if (cf[u] >= 0) {
+			d[u].v = d[u].st == 2 ? 0 : (int32_t)(zf[u] >> 16);
+		} else {
+			d[u].st = 0;
+			d[u].v = DROP_POLICY;
+		}
+		d[u].ctr = cf[u];
+		if (cr[u] >= 0) {
+			d2[u].v = d2[u].st == 2 ? 0 : (int32_t)(zr[u] >> 16);
+		} else {
+			d2[u].st = 0;
+			d2[u].v = DROP_POLICY;
+		}
+		d2[u].ctr = cr[u];
+	}
 }
 
 /* Packed per-workgroup counter: packets in bits 41..63, bytes in 0..40.
@@ -1451,11 +1578,63 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 #define DROP_SNAPLEN (-4096)     /* CGPU_DROP_SNAPLEN */
 #define FRF_DEC 0x80u
 #define FRF_V6 0x40u
+/* The first 64 bytes of a frame slot as 16 little-endian words: Ethernet,
+ * the IPv4 header without options / the IPv6 header, and the L4 type and
+ * ports right behind them.  Offsets are compile-time constants after
+ * inlining, so the words stay in VGPRs. */
+struct fwin {
+	uint32_t w[16];
+	__device__ __forceinline__ uint32_t b(int o) const { return (w[o >> 2] >> ((o & 3) * 8)) & 0xffu; }
+	/* raw (memory-order) u16 at an even offset */
+	__device__ __forceinline__ uint32_t h(int o) const { return (w[o >> 2] >> ((o & 2) * 8)) & 0xffffu; }
+	/* raw u32 at an even offset */
+	__device__ __forceinline__ uint32_t d(int o) const
+	{
+		return (o & 2) ? ((w[o >> 2] >> 16) | (w[(o >> 2) + 1] << 16)) : w[o >> 2];
+	}
+};
 
-template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false,
-	  bool FR = false, bool IPCE = false>
-__global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a0, uint64_t *pk)
+struct ftuple {
+	int32_t status; /* 0 reached policy, FRAME_NOT_CLASSIFIED, or a drop */
+	uint32_t fam;   /* 4 / 6 / 0 */
+	uint4 sa, da;   /* IPv4 in .x */
+	uint32_t dport, proto;
+	bool frag;
+};
+
+/* endpoints whose rows the frame parse stages in LDS (8 KiB): the egress
+ * SMAC / DMAC / SIP checks then read LDS, not a global load that would wait
+ * behind the frame loads */
+#define FR_LXC_LDS 256u
+#ifndef CGPU_FF_H
+#define CGPU_FF_H 2 /* fused frames: slots loaded together (1, 2, 4) */
+#endif
+#define FF_H CGPU_FF_H
+
+__device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fwin &W, const uint8_t *f,
+						uint32_t len, uint32_t cap, bool egress, uint32_t ep,
+						const uint4 *lxc);
+
+/* a wave-uniform 64-bit value into scalar registers */
+__device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
 {
+	const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+	const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+	return ((uint64_t)hi << 32) | lo;
+}
+
+/* FR: 0 tuple columns; 1 the columns k_frames_cols parsed (a parse-ended
+ * frame's status in its daddr column); 2 fused frames: the kernel parses
+ * the 64-byte frame slots itself (a.saddr = the slots; lane l of a wave
+ * handles frames i0 + 64 u + l, so each load instruction covers 64
+ * consecutive slots and each output store 64 consecutive frames), IPv6
+ * frames compacted to fx for the v6 pass */
+template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false,
+	  int FR = 0, bool IPCE = false>
+__global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a0, uint64_t *pk, frames_x4 fx)
+{
+	constexpr bool FF = FR == 2;
+	static_assert(!FF || (Q == 4 && !V6 && !LB), "fused frames: the v4 x4 schedule");
 	cls_args a = a0;
 	if (FR && a0.n_dev) {
 		const uint64_t c = *a0.n_dev;
@@ -1488,6 +1667,14 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	uint64_t *ccv = lctr + s.hot_slots + ((lds_words + 1u) >> 1);
 	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + a.cc_n);
 	const uint32_t ccm = a.cc_n - 1u;
+	/* fused frames: the endpoints' rows (16-byte aligned) and each lane's
+	 * four parse statuses, after the cold-slot cache (launch_x4's LDS) */
+	uint4 *lxl = reinterpret_cast<uint4 *>((reinterpret_cast<uintptr_t>(cck + a.cc_n) + 15u) & ~(uintptr_t)15u);
+	int16_t *fst = reinterpret_cast<int16_t *>(lxl + (FF ? 2u * FR_LXC_LDS : 0u));
+	if constexpr (FF) {
+		for (uint32_t k = threadIdx.x; k < 2u * s.n_lxc; k += NT)
+			lxl[k] = s.lxc[k];
+	}
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
 	for (uint32_t k = threadIdx.x; k < a.cc_n; k += NT) {
@@ -1510,12 +1697,16 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	}
 	__syncthreads();
 
+	const uint32_t lane = threadIdx.x & 63u;
 	for (uint64_t g = t0;; g += T) {
-		const bool live = g * Q < a.n;
+		/* FF: i0 = the wave's first frame, frame u of the lane at iu(u) */
+		const uint64_t i0 = FF ? wave_uniform64((g - lane) * Q) : g * Q;
+		const bool live = FF ? i0 + lane < a.n : i0 < a.n;
 		if (!live)
 			break;
-		const uint64_t i0 = live ? g * Q : 0;
-		const bool full = live && i0 + Q <= a.n;
+		const bool full = FF ? false : i0 + Q <= a.n;
+		/* FF: a scalar base (i0 + 64 u) plus the lane */
+		auto iu = [&](int u) -> uint64_t { return FF ? (i0 + 64u * (uint32_t)u) + lane : i0 + (uint64_t)u; };
 		/* decode: hi4 = the policy key's upper word {dport, proto, egress}
 		 * (policy.h:61-64), fw = flag word, ad = the looked-up address */
 		/* QA: the vector-load branches below are written for Q = 4; arrays
@@ -1525,7 +1716,85 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		uint4 ad6[Q];
 		{
 			uint32_t fl[QA], proto[QA], dport[QA], sa[QA], da[QA];
-			if (full && Q == 4) {
+			if constexpr (FF) {
+				/* the frames' 64-byte slots and len / flags / ep, all in
+				 * flight together, then the parse (parse_frame_w) of each */
+				const uint8_t *fd = static_cast<const uint8_t *>(a.saddr);
+				uint4 raw[FF_H][4];
+				uint32_t flv[Q];
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					const bool ok = iu(u) < a.n;
+					const uint64_t i = ok ? iu(u) : i0 + lane;
+					len[u] = a.len[i];
+					flv[u] = a.flags[i];
+					ep[u] = a.ep[i];
+				}
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
+					const bool ok = iu(u) < a.n;
+					const uint64_t i = ok ? iu(u) : i0 + lane;
+					/* FF_H frames' slots in flight at a time (registers) */
+					if (u % FF_H == 0) {
+#pragma unroll
+						for (int h = 0; h < FF_H; h++) {
+							const bool okh = iu(u + h) < a.n;
+							const uint64_t ih = okh ? iu(u + h) : i0 + lane;
+#pragma unroll
+							for (int k = 0; k < 4; k++)
+								raw[h][k] = okh ? ld_x4<NTL>(fd + ih * 64u + 16u * k) : make_uint4(0, 0, 0, 0);
+						}
+					}
+					fwin W;
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						W.w[4 * k] = raw[u % FF_H][k].x;
+						W.w[4 * k + 1] = raw[u % FF_H][k].y;
+						W.w[4 * k + 2] = raw[u % FF_H][k].z;
+						W.w[4 * k + 3] = raw[u % FF_H][k].w;
+					}
+					const bool egress = flv[u] & 1u;
+					const ftuple t = parse_frame_w(s, W, fd + i * 64u, len[u], min(len[u], 64u), egress, ep[u], lxl);
+					const bool v6 = t.status == 0 && t.fam != 4u;
+					fl[u] = egress ? 1u : 0u;
+					sa[u] = da[u] = dport[u] = proto[u] = 0u;
+					/* the status the output reports (0 for an IPv6 frame's
+					 * placeholder, which the v6 pass overwrites) */
+					fst[threadIdx.x * Q + u] = (int16_t)t.status;
+					if (t.status != 0) {
+						fl[u] |= FRF_DEC;
+					} else if (!v6) {
+						sa[u] = t.sa.x;
+						da[u] = t.da.x;
+						dport[u] = t.dport;
+						proto[u] = t.proto;
+						fl[u] |= t.frag ? 2u : 0u;
+					} else {
+						fl[u] |= FRF_V6;
+					}
+					/* wave-aggregated rows of the IPv6 frames (fr_emit) */
+					const bool m6 = ok && v6;
+					const uint64_t m = __ballot(m6);
+					if (m) {
+						const int leader = __ffsll((unsigned long long)m) - 1;
+						uint32_t base = 0;
+						if ((int)lane == leader)
+							base = atomicAdd(fx.n6, (uint32_t)__popcll(m));
+						base = __shfl(base, leader, 64);
+						if (m6) {
+							const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+							fx.sa6[j] = t.sa;
+							fx.da6[j] = t.da;
+							fx.dport6[j] = (uint16_t)t.dport;
+							fx.proto6[j] = (uint8_t)t.proto;
+							fx.fl6[j] = (uint8_t)(egress ? 1u : 0u);
+							fx.len6[j] = len[u];
+							fx.ep6[j] = (uint16_t)ep[u];
+							fx.idx6[j] = (uint32_t)(a.n_off + i);
+						}
+					}
+				}
+			} else if (full && Q == 4) {
 				const uint32_t f4 = ld_x1<NTL>(a.flags + i0);
 				const uint32_t p4 = ld_x1<NTL>(a.proto + i0);
 				const uint2 d4 = ld_x2<NTL>(a.dport + i0);
@@ -1672,7 +1941,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				const bool gated = s.ct_proto_gate && proto[u] != (V6 ? 58u : 1u) && proto[u] != 6u &&
 						   proto[u] != 17u;
 				/* IPv6 passes is_fragment = false (bpf_lxc.c:787-789) */
-				fw[u] = (live && i0 + u < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) | lbf[u] |
+				fw[u] = (live && iu(u) < a.n ? F_OK : 0u) | (eg ? F_EG : 0u) | (gated ? F_GATED : 0u) | lbf[u] |
 					(!V6 && !eg && ((fl[u] >> 1) & 1u) ? F_FRAG : 0u);
 				ad[u] = eg ? da[u] : sa[u];
 				hi4[u] = dport[u] | (proto[u] << 16) | (eg ? (1u << 24) : 0u);
@@ -1881,7 +2150,8 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				st[u] = 0;
 				if (!(fw[u] & F_OK))
 					continue; /* a tail lane repeating tuple i0: no status, no metrics */
-				const int32_t sv = (int32_t)static_cast<const uint32_t *>(a.daddr)[i0 + u];
+				const int32_t sv = FF ? (int32_t)fst[threadIdx.x * Q + u]
+						      : (int32_t)static_cast<const uint32_t *>(a.daddr)[i0 + u];
 				if (sv == 0 || sv == FRAME_NOT_CLASSIFIED) {
 					v[u] = 0;
 					st[u] = sv ? 7u : 0u;
@@ -1960,7 +2230,22 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				atomicAdd(&lmet[mi + 1u], (unsigned long long)len[u]);
 			}
 		}
-		if (full && Q == 4) {
+		if constexpr (FF) {
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				if (fw[u] & F_OK) {
+					const uint64_t i = iu(u);
+					if (NTL) {
+						__builtin_nontemporal_store(v[u], a.verdict + i);
+						__builtin_nontemporal_store(id[u], a.identity + i);
+					} else {
+						a.verdict[i] = v[u];
+						a.identity[i] = id[u];
+					}
+					if (a.stage)
+						a.stage[i] = (uint8_t)st[u];
+				}
+		} else if (full && Q == 4) {
 #ifdef CGPU_DIAG_STORE_SC1 /* write-through stores that leave the XCD's L2 */
 			{
 				const auto rv = __builtin_amdgcn_make_buffer_rsrc(a.verdict, 0, (int)(a.n * 4u), 0x00020000);
@@ -2041,29 +2326,6 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #define DROP_FRAG_NOSUPPORT (-157)
 #define EFAULT_LOAD (-14)        /* bpf_skb_load_bytes past skb->len */
 
-/* The first 64 bytes of a frame slot as 16 little-endian words: Ethernet,
- * the IPv4 header without options / the IPv6 header, and the L4 type and
- * ports right behind them.  Offsets are compile-time constants after
- * inlining, so the words stay in VGPRs. */
-struct fwin {
-	uint32_t w[16];
-	__device__ __forceinline__ uint32_t b(int o) const { return (w[o >> 2] >> ((o & 3) * 8)) & 0xffu; }
-	/* raw (memory-order) u16 at an even offset */
-	__device__ __forceinline__ uint32_t h(int o) const { return (w[o >> 2] >> ((o & 2) * 8)) & 0xffffu; }
-	/* raw u32 at an even offset */
-	__device__ __forceinline__ uint32_t d(int o) const
-	{
-		return (o & 2) ? ((w[o >> 2] >> 16) | (w[(o >> 2) + 1] << 16)) : w[o >> 2];
-	}
-};
-
-struct ftuple {
-	int32_t status; /* 0 reached policy, FRAME_NOT_CLASSIFIED, or a drop */
-	uint32_t fam;   /* 4 / 6 / 0 */
-	uint4 sa, da;   /* IPv4 in .x */
-	uint32_t dport, proto;
-	bool frag;
-};
 
 /* A header read of [off, off + sz): the reference bounds it by skb->len
  * (revalidate_data / skb_load_bytes) and returns `err` past it; within len
@@ -2914,9 +3176,11 @@ static hipError_t launch_ipc6_pre(const cgpu_snapshot &s, const cls_args &a, hip
 	return hipGetLastError();
 }
 
-template <bool LB, bool V6, bool FR = false, bool IPCE = false>
-static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st)
+template <bool LB, bool V6, int FR = 0, bool IPCE = false>
+static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st,
+			    const frames_x4 &fx = frames_x4{})
 {
+	constexpr bool FF = FR == 2;
 	constexpr int NT = 1024;
 	if constexpr (IPCE) {
 		hipError_t e = launch_ipc6_pre(s0, a, st);
@@ -2927,6 +3191,9 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 	 * levels (v6 without the pre-pass) */
 	size_t fixed = V6 ? (IPCE ? 0u : (size_t)v6t_lds_words(s0.ipc6) * 4u) : (size_t)s0.ipc4c.n_dict * 4u;
 	fixed = (fixed + 7u) & ~(size_t)7u;
+	/* fused frames: the endpoint rows (+ alignment) and 4 statuses per lane */
+	const size_t ff = FF ? 16u + 2u * FR_LXC_LDS * 16u + (size_t)NT * 4u * 2u : 0u;
+	fixed += ff;
 	const cgpu_snapshot s = with_lds_hot(s0, fixed < X4_LDS_BUDGET ? (X4_LDS_BUDGET - fixed) / 8u : 0u);
 	size_t lds = (size_t)s.hot_slots * 8u + fixed;
 	/* the cold-slot cache takes the LDS one workgroup per CU leaves free
@@ -2946,6 +3213,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 	constexpr int Q = V6 && !IPCE ? 2 : 4; /* in-kernel v6 lookups: the trie's line registers */
 #endif
 	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE>;
+	static_assert(!FF || Q == 4, "fused frames: Q = 4");
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
 	const uint64_t chunk = std::min<uint64_t>(PKC_CHUNK, (uint64_t)res << 22);
@@ -2958,13 +3226,17 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 		c.identity += off;
 		if (c.stage)
 			c.stage += off;
-		c.dport += off;
-		c.proto += off;
 		c.flags += off;
 		c.len += off;
 		c.ep += off;
-		c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
-		c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
+		if (FF) { /* a.saddr = the 64-byte frame slots */
+			c.saddr = static_cast<const char *>(a.saddr) + off * 64u;
+		} else {
+			c.dport += off;
+			c.proto += off;
+			c.saddr = static_cast<const char *>(a.saddr) + off * (V6 ? 16 : 4);
+			c.daddr = static_cast<const char *>(a.daddr) + off * (V6 ? 16 : 4);
+		}
 		if (c.sport)
 			c.sport += off;
 		if (c.hash)
@@ -2974,7 +3246,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 		c.n_off = off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + Q * NT - 1) / (Q * NT), res);
 		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE>), dim3(g), dim3(NT), lds, st, s, c,
-				   a.pk);
+				   a.pk, fx);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
@@ -3113,10 +3385,6 @@ hipError_t launch_frames_parse(const cgpu_snapshot &s, const frames_args &a, hip
  * status, IPv6 frames compacted to their own columns with their index),
  * then k_classify_x4 runs over the IPv4 columns and, on the device-side
  * count, over the IPv6 ones, whose results are scattered back */
-/* endpoints whose rows k_frames_cols stages in LDS (8 KiB): the egress
- * SMAC / DMAC / SIP checks then read LDS, not a global load that would wait
- * behind the next tile's slot loads */
-#define FR_LXC_LDS 256u
 
 /* one tile of 64 frames in 64-byte slots: the wave's four coalesced 1-KiB
  * loads (lane l holds bytes [1024 k + 16 l, +16) of the tile) and the
@@ -3317,6 +3585,27 @@ hipError_t launch_classify_frames_x4(const cgpu_snapshot &s, const frames_args &
 	hipError_t e = hipMemsetAsync(c.n6, 0, 4, st);
 	if (e != hipSuccess)
 		return e;
+	if (a.stride == 64u && s.n_lxc <= FR_LXC_LDS && !((uintptr_t)a.data & 15u) &&
+	    (s.schedule & CGPU_SCHED_FRAMES_FUSED)) {
+		/* fused: the classify kernel parses the slots itself (no tuple
+		 * columns written and re-read), the IPv6 frames as below.  Not the
+		 * default: each lane's 16-byte slot loads touch 4x the cache lines
+		 * of k_frames_cols' coalesced tile loads and the kernel spills at
+		 * 128 VGPRs, 2.98 against 2.74 ms per 64M frames
+		 * (profiles/r4_f/) */
+		cls_args f4{a.data, nullptr, nullptr, nullptr, a.flags, a.len, a.ep, a.verdict, a.identity, a.stage,
+			    a.delta, a.n, a.pk, 0, nullptr, nullptr};
+		if ((e = launch_x4<false, false, 2>(s, f4, st, c)) != hipSuccess)
+			return e;
+		cls_args c6{c.sa6, c.da6, c.dport6, c.proto6, c.fl6, c.len6, c.ep6, c.v6, c.id6,
+			    a.stage ? c.st6 : nullptr, a.delta, a.n, a.pk, 0, nullptr, nullptr};
+		c6.n_dev = c.n6;
+		if ((e = launch_x4<false, true, 1>(s, c6, st)) != hipSuccess)
+			return e;
+		hipLaunchKernelGGL(k_frames_scatter6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, c, a.verdict,
+				   a.identity, a.stage);
+		return hipGetLastError();
+	}
 	/* a streaming pass: up to 8 resident 256-thread blocks per CU (25 KiB
 	 * LDS each) so enough slot loads are in flight */
 	const unsigned gf = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + BLOCK - 1) / BLOCK, 256u * 8u * 4u));
@@ -3328,12 +3617,12 @@ hipError_t launch_classify_frames_x4(const cgpu_snapshot &s, const frames_args &
 		    a.delta, a.n, a.pk, 0, nullptr, nullptr};
 	if (!x4_aligned(c4))
 		return hipErrorInvalidValue;
-	if ((e = launch_x4<false, false, true>(s, c4, st)) != hipSuccess)
+	if ((e = launch_x4<false, false, 1>(s, c4, st)) != hipSuccess)
 		return e;
 	cls_args c6{c.sa6, c.da6, c.dport6, c.proto6, c.fl6, c.len6, c.ep6, c.v6, c.id6,
 		    a.stage ? c.st6 : nullptr, a.delta, a.n, a.pk, 0, nullptr, nullptr};
 	c6.n_dev = c.n6;
-	if ((e = launch_x4<false, true, true>(s, c6, st)) != hipSuccess)
+	if ((e = launch_x4<false, true, 1>(s, c6, st)) != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(k_frames_scatter6, dim3(grid_for(a.n)), dim3(BLOCK), 0, st, c, a.verdict, a.identity,
 			   a.stage);
@@ -3909,6 +4198,8 @@ struct ct_args {
 	 * ct result with the walker's CT_* flags << 17 | stage << 25, y = the
 	 * identity; k_ct_out unpacks it into the caller's columns */
 	uint2 *res;
+	/* [n] both tuples' policy decisions (k_ct_decide), batch order */
+	uint4 *dec;
 };
 
 /* the packed per-packet outcome (ct_args.res) */
@@ -3920,6 +4211,24 @@ __device__ __forceinline__ uint2 ct_res(int32_t v, uint32_t ret, uint32_t st, ui
 __device__ __forceinline__ int32_t ct_res_verdict(uint32_t x) { return (int32_t)(x << 15) >> 15; }
 __device__ __forceinline__ uint32_t ct_res_ret(uint32_t x) { return (x >> 17) & 0xFFu; }
 
+/* ct_args.dec words (k_ct_decide) */
+__device__ __forceinline__ uint32_t ct_dec_pack(const decision &d)
+{
+	return (uint32_t)(d.ctr + 1) | (d.st << 24) | (d.v < 0 ? 1u << 26 : 0u);
+}
+
+__device__ __forceinline__ decision ct_dec_of(const uint4 &D, bool reply)
+{
+	const uint32_t x = reply ? D.y : D.x;
+	decision d;
+	d.ctr = (int)(x & 0xFFFFFFu) - 1;
+	d.st = (x >> 24) & 3u;
+	d.v = (x & (1u << 26)) ? DROP_POLICY : (int32_t)((reply ? D.w >> 16 : D.w) & 0xFFFFu);
+	d.id = D.z;
+	return d;
+}
+
+
 /* One packet's record, written by k_ct_prep{,6} and read by the walks
  * (batch order):
  *   IPv4 (2 x 16 B): {daddr, saddr, z, nexthdr | tflags << 8 | meta << 16},
@@ -3929,8 +4238,10 @@ __device__ __forceinline__ uint32_t ct_res_ret(uint32_t x) { return (x >> 17) & 
  * z = the reply-direction tuple's dport | sport << 16 (ct_lookup's first
  * lookup), w = the L4 word (TCP header bytes 12-13 / ICMP type), ep = the
  * endpoint, rev_nat = the reverse NAT index an IPv6 ingress entry is created
- * with.  The policy decision is not in the record: the walker takes it when
- * the ct result says which tuple policy sees (ct_pol). */
+ * with.  The policy decisions are k_ct_decide's (ct_args.dec); it also fills
+ * the record's words DW, DW + 1 (IPv4: r1.z, r1.w; IPv6: r3.x, r3.y) with
+ * what the walk needs of them: the identity and whether the forward tuple's
+ * verdict allows (creates / deletes). */
 struct ct_pkt {
 	uint32_t meta, w, len, sec, revnat, port, cst, dport, proto;
 	uint32_t sa4, da4;
@@ -3941,6 +4252,9 @@ struct ct_pkt {
 	/* the endpoint index, and z (the reply tuple's dport | sport << 16: the
 	 * forward tuple's dport is z >> 16) */
 	uint32_t ep, z;
+	/* k_ct_decide's words in the record: the identity, and bit 0 = the
+	 * forward tuple's verdict is not a drop */
+	uint32_t pid, pok;
 };
 
 template <class K> struct ct_rec;
@@ -3954,19 +4268,22 @@ template <> struct ct_rec<CtK4> {
 	}
 	__device__ CtK4::key key() const { return uint4{r0.x, r0.y, r0.z, r0.w & 0xFFFFu}; }
 	__device__ uint32_t meta() const { return r0.w >> 16; }
+	static constexpr uint32_t DW = 6;
 	__device__ ct_pkt pkt() const
 	{
 		ct_pkt q{r0.w >> 16, r1.x & 0xFFFFu, r1.y, 0u, 0u, 0u, 0u, r0.z & 0xFFFFu,
 			 r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{}};
 		q.ep = r1.x >> 16;
 		q.z = r0.z;
+		q.pid = r1.z;
+		q.pok = r1.w;
 		return q;
 	}
 };
 /*   IPv4 behind the service step (3 x 16 B): the IPv4 record, then
  *                    {rev_nat | slave << 16, addr, svc_addr, lbf} */
 template <> struct ct_rec<CtK4S> {
-	static constexpr uint32_t RW = 3;
+	static constexpr uint32_t RW = 3, DW = 6;
 	uint4 r0, r1, r2;
 	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
 	{
@@ -3983,11 +4300,13 @@ template <> struct ct_rec<CtK4S> {
 			 r2.x >> 16, r2.w, r2.y, r2.z};
 		q.ep = r1.x >> 16;
 		q.z = r0.z;
+		q.pid = r1.z;
+		q.pok = r1.w;
 		return q;
 	}
 };
 template <> struct ct_rec<CtK6> {
-	static constexpr uint32_t RW = 4;
+	static constexpr uint32_t RW = 4, DW = 12;
 	uint4 r0, r1, r2, r3;
 	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
 	{
@@ -4003,6 +4322,8 @@ template <> struct ct_rec<CtK6> {
 			 r2.y & 0xFFu, 0u, 0u, r1, r0};
 		q.ep = r2.z >> 16;
 		q.z = r2.x;
+		q.pid = r3.x;
+		q.pok = r3.y;
 		return q;
 	}
 };
@@ -4023,7 +4344,7 @@ __device__ __forceinline__ uint4 ct_addr_key(uint4 k, const ct_pkt &q)
 /*   IPv6 behind the service step: the IPv6 record with {0, 0, rev_nat,
  *                    slave | lbf << 16} as its last word */
 template <> struct ct_rec<CtK6S> {
-	static constexpr uint32_t RW = 4;
+	static constexpr uint32_t RW = 4, DW = 12;
 	uint4 r0, r1, r2, r3;
 	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
 	{
@@ -4039,6 +4360,8 @@ template <> struct ct_rec<CtK6S> {
 			 r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
 		q.ep = r2.z >> 16;
 		q.z = r2.x;
+		q.pid = r3.x;
+		q.pok = r3.y;
 		return q;
 	}
 };
@@ -4141,8 +4464,6 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 		if (pr != 6u)
 			w = 0; /* union tcp_flags stays zero (conntrack.h:448) */
 		if (!(meta & CTM_GATED)) {
-			/* the policy decision is the walker's (ct_pol): it knows which
-			 * tuple policy sees */
 			if (!egress && ((fl >> 1) & 1u))
 				meta |= CTM_FRAG;
 		} else {
@@ -4210,27 +4531,48 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 
 /* k_ct_prep<false, false> (the plain IPv4 path) with Q packets per lane:
  * packet i = g + u * (threads), so every column load of a wave covers 64
- * consecutive packets.  A streaming pass: the tuple ct_lookup4 builds, the
- * group key and the record; no table is read (the policy step is the
- * walker's) */
+ * consecutive packets: the tuple ct_lookup4 builds, the group key and the
+ * record, then k_ct_decide's two decisions (the other paths run it as its
+ * own pass) with every lookup stage's gathers in flight together */
+#ifndef CGPU_CT_FUSED_DECIDE
+#define CGPU_CT_FUSED_DECIDE 1 /* 0: the IPv4 prep leaves the decisions to k_ct_decide (A/B) */
+#endif
+
 template <int Q>
 __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 {
+	constexpr bool FD = CGPU_CT_FUSED_DECIDE;
+	/* the LPM leaf dictionary in LDS, as k_classify_x4 */
+	extern __shared__ __attribute__((aligned(16))) uint32_t ldict[];
+	if (FD) {
+		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += 256u)
+			ldict[k] = s.ipc4c.dict[k];
+		__syncthreads();
+	}
 	const uint64_t T = (uint64_t)gridDim.x * 256u;
 	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+		bool act[Q], eg[Q], frag[Q], act2[Q];
+		uint32_t sa[Q], da[Q], dpf[Q], dpr[Q], pr[Q], ep[Q], w1[Q], len[Q];
+		decision d[Q], d2[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = eg[u] = frag[u] = false;
+			sa[u] = da[u] = dpf[u] = dpr[u] = pr[u] = ep[u] = w1[u] = len[u] = 0u;
 			if (i >= a.n)
 				continue;
 			/* columns stream past the map: nontemporal */
-			const uint32_t fl = ntl(a.flags + i), pr = ntl(a.proto + i), len = ntl(a.len + i);
-			const uint32_t sa = ntl(a.saddr + i), da = ntl(a.daddr + i), ep = ntl(a.ep + i);
+			const uint32_t fl = ntl(a.flags + i);
+			len[u] = ntl(a.len + i);
+			pr[u] = ntl(a.proto + i);
+			sa[u] = ntl(a.saddr + i);
+			da[u] = ntl(a.daddr + i);
+			ep[u] = ntl(a.ep + i);
 			const uint32_t dp = ntl(a.dport + i), sp = ntl(a.sport + i);
 			uint32_t w = ntl(a.l4 + i);
-			const bool eg = fl & 1u;
-			uint32_t tfl = eg ? TUPLE_F_IN : 0u, meta = eg ? CTM_EGRESS : 0u, z = 0;
-			if (pr == 1u) { /* as k_ct_prep */
+			eg[u] = fl & 1u;
+			uint32_t tfl = eg[u] ? TUPLE_F_IN : 0u, meta = eg[u] ? CTM_EGRESS : 0u, z = 0;
+			if (pr[u] == 1u) { /* as k_ct_prep */
 				const uint32_t type = w & 0xFFu;
 				if (type == 3u || type == 11u || type == 12u)
 					tfl |= TUPLE_F_RELATED;
@@ -4241,35 +4583,69 @@ __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 						z = 8u << 16;
 					meta |= CTM_ACT_CREATE;
 				}
-			} else if (pr == 6u || pr == 17u) {
+			} else if (pr[u] == 6u || pr[u] == 17u) {
 				z = sp | (dp << 16);
-				meta |= pr == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
+				meta |= pr[u] == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
 			} else {
 				meta |= CTM_GATED;
 			}
-			if (pr != 6u)
+			if (pr[u] != 6u)
 				w = 0;
-			uint32_t gk = ct_group(sa, da);
+			w1[u] = w | (ep[u] << 16);
+			uint32_t gk = ct_group(sa[u], da[u]);
 			bool p2 = false;
 			if (!(meta & CTM_GATED)) {
-				if (!eg && ((fl >> 1) & 1u))
+				if (!eg[u] && ((fl >> 1) & 1u))
 					meta |= CTM_FRAG;
-				if (pr == 1u && (tfl & TUPLE_F_RELATED)) {
+				if (pr[u] == 1u && (tfl & TUPLE_F_RELATED)) {
 					meta |= CTM_PHASE2;
 					p2 = true;
 				} else {
 					meta |= CTM_RELX;
-					gk = ct_conn_group(gk, z, pr);
+					gk = ct_conn_group(gk, z, pr[u]);
 				}
+				act[u] = FD;
 			} else {
 				a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u);
 			}
+			frag[u] = meta & CTM_FRAG;
+			dpf[u] = z >> 16;
+			dpr[u] = z & 0xFFFFu;
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
-			uint4 *r = a.rec + 2u * i;
-			r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
-			r[1] = uint4{w | (ep << 16), len, 0u, 0u};
+			a.rec[2u * i] = uint4{da[u], sa[u], z, pr[u] | (tfl << 8) | (meta << 16)};
 			a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
 			a.idx[i] = (uint32_t)i;
+		}
+		/* the policy step of both tuples (k_ct_decide) */
+		if (FD) {
+			ident4_q<Q>(s, ldict, act, eg, sa, da, d);
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				act2[u] = act[u] && dpr[u] != dpf[u];
+				d2[u].id = d[u].id;
+			}
+			policy2_qg<Q>(s, act, act2, eg, frag, dpf, dpr, pr, ep, d, d2);
+		} else {
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				act2[u] = false;
+				d[u].v = -1;
+				d[u].id = 0;
+				d[u].ctr = -1;
+				d[u].st = 0;
+				d2[u] = d[u];
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			if (i >= a.n)
+				continue;
+			const decision &rp = act2[u] ? d2[u] : d[u];
+			const uint32_t pf = d[u].v > 0 ? (uint32_t)d[u].v : 0u, prt = rp.v > 0 ? (uint32_t)rp.v : 0u;
+			if (act[u])
+				a.dec[i] = make_uint4(ct_dec_pack(d[u]), ct_dec_pack(rp), d[u].id, pf | (prt << 16));
+			a.rec[2u * i + 1u] = uint4{w1[u], len[u], act[u] ? d[u].id : 0u, (act[u] && d[u].v >= 0) ? 1u : 0u};
 		}
 	}
 }
@@ -5270,116 +5646,121 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
 #define CT_RETB 6 /* results a walker lane buffers before storing them (12 B each in LDS) */
 #endif
 
-/* ---- the endpoint programs' policy step inside the walker ----
- * decide<> for the packet a lane replays: the ipcache identity and the
- * three-probe cascade (bpf_lxc.c:484-537 / :876-950, bpf_netdev.c:374-404)
- * of the tuple policy sees - the forward tuple's dport for CT_NEW /
- * CT_ESTABLISHED, the reply tuple's for CT_REPLY / CT_RELATED (left
- * unreversed, policy.h:98-99).  Inside one connection the decision varies
- * only with that dport, the direction, the fragment bit and the endpoint,
- * so a lane keeps the last two decisions of its group's address pair keyed
- * by those: a connection costs a couple of cascades instead of one per
- * packet.  The hit entries' counters accumulate per slot in two register
- * sets, flushed (two memory-side atomics) when a third slot needs one and
- * at the lane's end: one flush per slot per lane instead of an atomic per
- * packet.  Scalar members only, so the cache stays in VGPRs. */
-struct ct_pol {
-	uint32_t k0, e0, v0, i0, c0; /* key word (0: empty), ep, verdict, identity, ctr + 1 | st << 24 */
-	uint32_t k1, e1, v1, i1, c1;
-	uint32_t nxt;
-	uint32_t s0, n0, b0, h0; /* counter slot + 1 (0: none), packets, bytes lo / hi */
-	uint32_t s1, n1, b1, h1;
-	uint32_t nc;
-};
-
-__device__ __forceinline__ void ct_pol_flush1(uint64_t *delta, uint32_t sl, uint32_t n, uint32_t b, uint32_t h)
+/* ---- the endpoint programs' policy step (k_ct_decide) ----
+ * decide<> for both tuples policy can see (bpf_lxc.c:484-537 / :876-950,
+ * bpf_netdev.c:374-404): the forward tuple's dport (CT_NEW / CT_ESTABLISHED)
+ * and the reply tuple's (CT_REPLY / CT_RELATED, left unreversed,
+ * policy.h:98-99); the identity is the same for both (the addresses are).
+ * A pass over the batch before the walk, Q packets per lane with every
+ * lookup stage's gathers in flight together, so the walker's dependent
+ * chain holds only conntrack: it reads the packet's decisions with its
+ * record.  dec[i] = {fwd, rep, identity, fwd port | rep port << 16},
+ * fwd / rep = counter slot + 1 | stage << 24 | deny << 26 (port = the
+ * proxy port of an allowed verdict). */
+template <class K, int Q>
+__global__ __launch_bounds__(256) void k_ct_decide(cgpu_snapshot s, ct_args a)
 {
-	if (sl) {
-		atomicAdd((unsigned long long *)&delta[2u * (sl - 1u)], (unsigned long long)n);
-		atomicAdd((unsigned long long *)&delta[2u * (sl - 1u) + 1u], ((unsigned long long)h << 32) | b);
+	using R = ct_rec<K>;
+	constexpr bool V6 = K::V6 != 0;
+	/* v6: the trie's root bitmap, b24 blocks and /64 bloom in LDS, as
+	 * k_ipc6_pre */
+	extern __shared__ __attribute__((aligned(16))) uint32_t lt[];
+	uint32_t n24 = 0, nbl = 0;
+	uint32_t *lbl = lt;
+	if constexpr (!V6) { /* the LPM leaf dictionary */
+		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += 256u)
+			lt[k] = s.ipc4c.dict[k];
+		__syncthreads();
 	}
-}
-
-/* packets / bytes of counter slot ctr (>= 0) */
-__device__ __forceinline__ void ct_pol_count(ct_pol &p, uint64_t *delta, int ctr, uint32_t len)
-{
-	const uint32_t sl = (uint32_t)ctr + 1u;
-	if (p.s0 == sl) {
-		p.n0++;
-		add64(p.b0, p.h0, len);
-	} else if (p.s1 == sl) {
-		p.n1++;
-		add64(p.b1, p.h1, len);
-	} else if (p.nc == 0u) {
-		ct_pol_flush1(delta, p.s0, p.n0, p.b0, p.h0);
-		p.s0 = sl;
-		p.n0 = 1u;
-		p.b0 = len;
-		p.h0 = 0u;
-		p.nc = 1u;
-	} else {
-		ct_pol_flush1(delta, p.s1, p.n1, p.b1, p.h1);
-		p.s1 = sl;
-		p.n1 = 1u;
-		p.b1 = len;
-		p.h1 = 0u;
-		p.nc = 0u;
+	if constexpr (V6) {
+		n24 = v6t_lds_b24(s.ipc6);
+		nbl = v6t_lds_bloom(s.ipc6);
+		lbl = lt + v6t_lds_words(s.ipc6);
+		if (s.ipc6.root) {
+			for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += 256u)
+				lt[k] = s.ipc6.rbits[k];
+			const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
+			for (uint32_t k = threadIdx.x; k < n24 * 128u; k += 256u)
+				lt[V6T_RBITS_WORDS + k] = b16[k];
+			for (uint32_t k = threadIdx.x; k < nbl; k += 256u)
+				lbl[k] = s.ipc6.bl64[k];
+		}
+		__syncthreads();
 	}
-}
-
-template <class K>
-__device__ __forceinline__ decision ct_pol_decide(const cgpu_snapshot &s, ct_pol &p, bool cacheable, bool orient,
-						  const ct_pkt &q, bool reply)
-{
-	const bool egress = q.meta & CTM_EGRESS, frag = q.meta & CTM_FRAG;
-	const uint32_t dport = reply ? (q.z & 0xFFFFu) : (q.z >> 16);
-	/* orient: the packet's saddr is the group pair's first address (the
-	 * identity is looked up on daddr for egress, saddr for ingress) */
-	const uint32_t kw = dport | (q.proto << 16) | (egress ? 1u << 24 : 0u) | (frag ? 1u << 25 : 0u) |
-			    (orient ? 1u << 26 : 0u) | (1u << 31);
-	decision d;
-	if (cacheable && p.k0 == kw && p.e0 == q.ep) {
-		d.v = (int32_t)p.v0;
-		d.id = p.i0;
-		d.ctr = (int)(p.c0 & 0xFFFFFFu) - 1;
-		d.st = p.c0 >> 24;
-		return d;
-	}
-	if (cacheable && p.k1 == kw && p.e1 == q.ep) {
-		d.v = (int32_t)p.v1;
-		d.id = p.i1;
-		d.ctr = (int)(p.c1 & 0xFFFFFFu) - 1;
-		d.st = p.c1 >> 24;
-		return d;
-	}
-	d = decide<K::V6>(s, egress, frag, q.sa4, q.da4, q.sa6, q.da6, dport, q.proto, q.ep);
-	if (cacheable) {
-		const uint32_t c = (uint32_t)(d.ctr + 1) | (d.st << 24);
-		if (p.nxt == 0u) {
-			p.k0 = kw;
-			p.e0 = q.ep;
-			p.v0 = (uint32_t)d.v;
-			p.i0 = d.id;
-			p.c0 = c;
-			p.nxt = 1u;
+	const uint64_t T = (uint64_t)gridDim.x * 256u;
+	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+		bool act[Q], eg[Q], frag[Q], act2[Q];
+		uint32_t dpf[Q], dpr[Q], pr[Q], ep[Q], sa[Q], da[Q];
+		uint4 w6[Q];
+		decision d[Q], d2[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = i < a.n;
+			const R r = R::load(a.rec, act[u] ? (uint32_t)i : 0u, true);
+			const ct_pkt q = r.pkt();
+			act[u] = act[u] && !(q.meta & CTM_GATED);
+			eg[u] = q.meta & CTM_EGRESS;
+			frag[u] = q.meta & CTM_FRAG;
+			dpf[u] = q.z >> 16;
+			dpr[u] = q.z & 0xFFFFu;
+			pr[u] = q.proto;
+			ep[u] = q.ep;
+			sa[u] = q.sa4;
+			da[u] = q.da4;
+			w6[u] = V6 ? v6_host_words(eg[u] ? q.da6 : q.sa6) : make_uint4(0, 0, 0, 0);
+		}
+		if constexpr (V6) {
+			/* decide<1>'s identity (bpf_lxc.c:170-187 / bpf_netdev.c:203-211) */
+			uint32_t e[Q];
+			v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w6, act, e, nbl ? lbl : nullptr);
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				const uint32_t label = entry_label(s.ipc6.vals, e[u]);
+				const bool in_cluster = w6[u].x == bswap32(s.router_ip64[0]) &&
+							w6[u].y == bswap32(s.router_ip64[1]);
+				if (eg[u]) {
+					d[u].id = (e[u] && label) ? label : (in_cluster ? s.cluster_id : s.world_id);
+				} else {
+					uint32_t src = s.ingress_src_identity;
+					if (src < s.health_id && e[u] && label && label != s.cluster_id)
+						src = label;
+					d[u].id = src;
+				}
+			}
 		} else {
-			p.k1 = kw;
-			p.e1 = q.ep;
-			p.v1 = (uint32_t)d.v;
-			p.i1 = d.id;
-			p.c1 = c;
-			p.nxt = 0u;
+			ident4_q<Q>(s, lt, act, eg, sa, da, d);
+		}
+		/* both tuples' cascades (the reply tuple's where its dport differs) */
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			act2[u] = act[u] && dpr[u] != dpf[u];
+			d2[u].id = d[u].id;
+		}
+		policy2_qg<Q>(s, act, act2, eg, frag, dpf, dpr, pr, ep, d, d2);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			if (!act[u])
+				continue;
+			const decision &rp = act2[u] ? d2[u] : d[u];
+			const uint32_t pf = d[u].v > 0 ? (uint32_t)d[u].v : 0u, prt = rp.v > 0 ? (uint32_t)rp.v : 0u;
+			a.dec[i] = make_uint4(ct_dec_pack(d[u]), ct_dec_pack(rp), d[u].id, pf | (prt << 16));
+			*reinterpret_cast<uint2 *>(reinterpret_cast<uint32_t *>(a.rec) + (uint64_t)R::RW * 4u * i + R::DW) =
+				make_uint2(d[u].id, d[u].v >= 0 ? 1u : 0u);
 		}
 	}
-	return d;
 }
 
-/* the outcome k_ct_finish used to compute: verdict, stage and the counter
- * bump of a replayed packet (bpf_lxc.c:506-537 / :918-950: CT_REPLY /
- * CT_RELATED skip the drop; an egress proxy redirect keeps its port) */
-__device__ __forceinline__ uint2 ct_outcome(const decision &d, uint32_t ret, const ct_pkt &q)
+static size_t ct_decide_lds(const cgpu_snapshot &s, bool v6)
 {
-	const bool egress = q.meta & CTM_EGRESS;
+	return v6 ? (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u : (size_t)s.ipc4c.n_dict * 4u;
+}
+
+/* the verdict of a replayed packet (bpf_lxc.c:506-537 / :918-950: CT_REPLY /
+ * CT_RELATED skip the drop; an egress proxy redirect keeps its port) */
+__device__ __forceinline__ int32_t ct_verdict(const decision &d, uint32_t ret, bool egress)
+{
 	int32_t v;
 	if ((ret & 3u) >= CT_REPLY)
 		v = (egress && d.v > 0) ? d.v : 0;
@@ -5389,13 +5770,20 @@ __device__ __forceinline__ uint2 ct_outcome(const decision &d, uint32_t ret, con
 		v = DROP_CT_CREATE_FAILED;
 	else
 		v = d.v;
-	return ct_res(v, ret, d.st, d.id);
+	return v;
 }
 
 /* walks: WALK_PKT the conntrack path's packets; WALK_SVC the service step
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
  * service path: candidates c = packet << 1 | kind, kind 0 a packet whose
  * address pair may hold owed entries, kind 1 an owed address entry */
+/* workgroups per CU the service-path walker (CtK4S: ~280 registers) is
+ * compiled for: 2 spills a few registers to scratch to double its
+ * occupancy */
+#ifndef CGPU_WALK_MINB_SVC
+#define CGPU_WALK_MINB_SVC 2
+#endif
+
 #define WALK_PKT 0
 #define WALK_SVC 1
 #define WALK_OWED 2
@@ -5414,7 +5802,7 @@ extern "C" __attribute__((visibility("default"))) int cgpu_diag_walk_clock(unsig
 #endif
 
 template <class K, int MODE>
-__global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
+__global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
 {
 #ifdef CGPU_DIAG_WALK_CLOCK
 	const unsigned long long dg_t0 = __builtin_amdgcn_s_memrealtime();
@@ -5442,7 +5830,6 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 		}
 		nret = 0;
 	};
-	ct_pol pc{};
 	if (threadIdx.x < 3)
 		s_acct[threadIdx.x] = 0;
 	__syncthreads();
@@ -5476,15 +5863,6 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 		uint32_t n3 = p0 + 2u < p1 ? a.idx_sorted[p0 + 2u] : n1;
 		R r1 = R::load(a.rec, pkt_of(n1), false);
 		R r2 = p0 + 1u < p1 ? R::load(a.rec, pkt_of(n2), false) : r1;
-		/* the group's address pair (its first packet's): decisions of other
-		 * pairs (a hash collision of two groups) are not cached */
-		uint4 ga{}, gb{};
-		if constexpr (MODE != WALK_SVC) {
-			const ct_pkt g0 = r1.pkt();
-			ga = K::V6 ? g0.sa6 : make_uint4(g0.sa4, 0u, 0u, 0u);
-			gb = K::V6 ? g0.da6 : make_uint4(g0.da4, 0u, 0u, 0u);
-			pc.k0 = pc.k1 = 0u;
-		}
 		for (uint64_t p = p0; p < p1; p++) {
 			/* records two packets ahead and the index three ahead are in
 			 * flight while packet p runs */
@@ -5547,30 +5925,22 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 				}
 				if (MODE == WALK_PKT && (meta & CTM_PHASE2))
 					continue;
-				bool inpair, orient;
-				if constexpr (K::V6 != 0) {
-					const bool f = q.sa6.x == ga.x && q.sa6.y == ga.y && q.sa6.z == ga.z && q.sa6.w == ga.w &&
-						       q.da6.x == gb.x && q.da6.y == gb.y && q.da6.z == gb.z && q.da6.w == gb.w;
-					const bool b = q.sa6.x == gb.x && q.sa6.y == gb.y && q.sa6.z == gb.z && q.sa6.w == gb.w &&
-						       q.da6.x == ga.x && q.da6.y == ga.y && q.da6.z == ga.z && q.da6.w == ga.w;
-					inpair = f || b;
-					orient = f;
-				} else {
-					const bool f = q.sa4 == ga.x && q.da4 == gb.x, b = q.sa4 == gb.x && q.da4 == ga.x;
-					inpair = f || b;
-					orient = f;
-				}
+				/* what the walk needs of the decisions (k_ct_decide): the
+				 * identity and whether the forward tuple is allowed; the
+				 * verdict, stage and counters are k_ct_out's */
 				decision d;
 				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now,
-								[&](bool reply) {
-									return ct_pol_decide<K>(s, pc, inpair, orient, q,
-												reply);
+								[&](bool) {
+									decision x;
+									x.v = (q.pok & 1u) ? 0 : DROP_POLICY;
+									x.id = q.pid;
+									x.st = 0;
+									x.ctr = -1;
+									return x;
 								},
 								d);
-				if (d.ctr >= 0)
-					ct_pol_count(pc, a.delta, d.ctr, q.len);
 				s_ri[nret][threadIdx.x] = i;
-				s_rr[nret][threadIdx.x] = ct_outcome(d, ret, q);
+				s_rr[nret][threadIdx.x] = ct_res(0, ret, 0u, q.pid);
 				if (++nret == CT_RETB)
 					ret_flush();
 			}
@@ -5578,10 +5948,6 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 		ctc_flush(T, c);
 	}
 	ret_flush();
-	if constexpr (MODE != WALK_SVC) {
-		ct_pol_flush1(a.delta, pc.s0, pc.n0, pc.b0, pc.h0);
-		ct_pol_flush1(a.delta, pc.s1, pc.n1, pc.b1, pc.h1);
-	}
 #ifdef CGPU_DIAG_WALK_CLOCK
 	{
 		uint32_t mx = dg_steps;
@@ -5608,27 +5974,86 @@ __global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct
 	}
 }
 
-/* The batch's outcome into the caller's columns, in batch order (the walks
- * wrote every packet's packed result, ct_args.res, the prep the gated
- * ones), and the {reason, dir} metrics of the verdicts (drop.h:94-118 /
- * metrics.h:41-59; a proxy redirect traces TRACE_TO_PROXY and counts none).
- * A streaming pass: 13 bytes in, 10 out per packet. */
+/* The batch's outcome into the caller's columns, in batch order: the walks
+ * wrote every replayed packet's ct result (ct_args.res), the prep the
+ * gated ones' final outcome; the decision of the tuple policy saw (the
+ * reply tuple's for CT_REPLY / CT_RELATED, k_ct_decide) gives the verdict,
+ * stage and identity (bpf_lxc.c:506-537 / :918-950), and the hit entry's
+ * counter (policy.h:68-93) its packet and bytes: hot slots in LDS, the
+ * others through an LDS cold-slot cache (as k_classify_x4), one global
+ * atomic pair per touched slot per workgroup at the end.  The {reason,
+ * dir} metrics of the verdicts (drop.h:94-118 / metrics.h:41-59; a proxy
+ * redirect traces TRACE_TO_PROXY and counts none).  A streaming pass over
+ * the resident grid. */
 template <int NT>
-__global__ __launch_bounds__(NT) void k_ct_out(cgpu_snapshot s, ct_args a)
+__global__ __launch_bounds__(NT) void k_ct_out(cgpu_snapshot s, ct_args a, uint32_t cc_n)
 {
+	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
+	uint64_t *ccv = lctr + s.hot_slots;
+	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + cc_n);
+	const uint32_t ccm = cc_n - 1u;
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
+		lctr[k] = 0;
+	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
+		ccv[k] = 0;
+		cck[k] = 0;
+	}
+	__syncthreads();
 	/* metrics {reason 0 / 133 / 137 / 155 / 158} x {ingress, egress} */
 	uint64_t mcnt[10] = {}, mbyt[10] = {};
 	const uint64_t T = (uint64_t)gridDim.x * NT;
 	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += T) {
 		const uint2 r = ld_x2<true>(a.res + i);
 		const uint32_t fl = ntl(a.flags + i), len = ntl(a.len + i);
-		const int32_t v = ct_res_verdict(r.x);
 		const uint32_t cr = ct_res_ret(r.x);
+		int32_t v;
+		uint32_t id, st;
+		if (cr == CTR_NONE) {
+			v = ct_res_verdict(r.x);
+			id = r.y;
+			st = (r.x >> 25) & 7u;
+		} else {
+			const uint4 D = ld_x4<true>(a.dec + i);
+			const decision d = ct_dec_of(D, (cr & 3u) >= CT_REPLY);
+			v = ct_verdict(d, cr, fl & 1u);
+			id = d.id;
+			st = d.st;
+			if (d.ctr >= 0) {
+				const uint32_t c = (uint32_t)d.ctr;
+				bool done = false;
+				if (len < PK_MAX_LEN) {
+					if (c < s.hot_slots) {
+						atomicAdd((unsigned long long *)&lctr[c], (1ull << PK_SHIFT) | (unsigned long long)len);
+						done = true;
+					} else if (cc_n) {
+						uint32_t j = (c * 0x9E3779B1u) >> 16;
+#pragma unroll
+						for (int p = 0; p < CC_PROBE && !done; p++, j++) {
+							j &= ccm;
+							uint32_t t = cck[j];
+							if (t == 0u) {
+								const uint32_t o = atomicCAS(&cck[j], 0u, c + 1u);
+								t = o == 0u ? c + 1u : o;
+							}
+							if (t == c + 1u) {
+								atomicAdd((unsigned long long *)&ccv[j],
+									  (1ull << PK_SHIFT) | (unsigned long long)len);
+								done = true;
+							}
+						}
+					}
+				}
+				if (!done) {
+					atomicAdd((unsigned long long *)&a.delta[2u * c], 1ull);
+					atomicAdd((unsigned long long *)&a.delta[2u * c + 1u], (unsigned long long)len);
+				}
+			}
+		}
 		a.verdict[i] = v;
 		a.ct_ret[i] = (uint8_t)(cr == CTR_NONE ? 255u : cr & 3u);
-		a.identity[i] = r.y;
+		a.identity[i] = id;
 		if (a.stage)
-			a.stage[i] = (uint8_t)((r.x >> 25) & 7u);
+			a.stage[i] = (uint8_t)st;
 		const uint32_t rr = v > 0 ? 5u : v == 0 ? 0u : v == DROP_POLICY ? 1u : v == DROP_CT_UNKNOWN_PROTO ? 2u
 				 : v == DROP_NO_SERVICE ? 4u : 3u;
 		const uint32_t idx = rr * 2u + (fl & 1u);
@@ -5648,6 +6073,24 @@ __global__ __launch_bounds__(NT) void k_ct_out(cgpu_snapshot s, ct_args a)
 			const uint32_t key = (reasons[k >> 1] * 4u + ((k & 1) ? 2u : 1u)) * 2u;
 			atomicAdd((unsigned long long *)&met[key], (unsigned long long)cn);
 			atomicAdd((unsigned long long *)&met[key + 1], (unsigned long long)by);
+		}
+	}
+	__syncthreads();
+	/* the workgroup's slots: one atomic pair per touched slot */
+	for (uint32_t k = threadIdx.x; k < s.hot_slots + cc_n; k += NT) {
+		uint32_t c;
+		uint64_t x;
+		if (k < s.hot_slots) {
+			c = k;
+			x = lctr[k];
+		} else {
+			const uint32_t t = cck[k - s.hot_slots];
+			x = t ? ccv[k - s.hot_slots] : 0u;
+			c = t - 1u;
+		}
+		if (x) {
+			atomicAdd((unsigned long long *)&a.delta[2u * c], (unsigned long long)(x >> PK_SHIFT));
+			atomicAdd((unsigned long long *)&a.delta[2u * c + 1u], (unsigned long long)(x & PK_BYTES_MASK));
 		}
 	}
 }
@@ -5794,6 +6237,7 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.xdport = L.xdport;
 	a.f2 = L.flags2;
 	a.res = L.res;
+	a.dec = L.dec;
 	return a;
 }
 
@@ -5947,11 +6391,31 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 /* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
 #define CT_WALK_GRID 2048
 
-static void launch_ct_out(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
+template <class K> static void launch_ct_decide(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
-	constexpr int NT = 256;
-	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + NT - 1) / NT, 256u * 16u));
-	hipLaunchKernelGGL((k_ct_out<NT>), dim3(g), dim3(NT), 0, st, s, a);
+	constexpr int Q = K::V6 ? 2 : CGPU_CT_Q; /* v6: the trie walk's registers */
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + 256 * Q - 1) / (256 * Q), 8192));
+	hipLaunchKernelGGL((k_ct_decide<K, Q>), dim3(g), dim3(256), ct_decide_lds(s, K::V6 != 0), st, s, a);
+}
+
+/* k_ct_out: 1024-thread workgroups, one per CU (LDS: hot counter slots and
+ * the cold-slot cache), at most 2^22 packets per workgroup (the LDS packing,
+ * PK_SHIFT) */
+static void launch_ct_out(const cgpu_snapshot &s0, const ct_args &a, hipStream_t st)
+{
+	constexpr int NT = 1024;
+	const cgpu_snapshot s = with_lds_hot(s0, X4_LDS_BUDGET / 16u);
+	size_t lds = (size_t)s.hot_slots * 8u;
+	uint32_t cc_n = 0;
+	if (!(s.schedule & CGPU_SCHED_NO_CCACHE))
+		for (uint32_t n = 1u << 14; n >= 512u && !cc_n; n >>= 1)
+			if (lds + (size_t)n * 12u <= X4_LDS_BUDGET)
+				cc_n = n;
+	lds += (size_t)cc_n * 12u;
+	const uint64_t per_wg = 1ull << 22;
+	const uint64_t want = std::max<uint64_t>(256u, (a.n + per_wg - 1) / per_wg);
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + NT - 1) / NT, want));
+	hipLaunchKernelGGL((k_ct_out<NT>), dim3(g), dim3(NT), lds, st, s, a, cc_n);
 }
 
 /* phase 2 of the plain paths (and of the IPv6 service path): the ICMP
@@ -5990,7 +6454,10 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	if (K::V6)
 		hipLaunchKernelGGL((k_ct_prep6_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
 	else
-		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
+		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), CGPU_CT_FUSED_DECIDE ? s.ipc4c.n_dict * 4u : 0u, st,
+				   s, a);
+	if (K::V6 || !CGPU_CT_FUSED_DECIDE) /* the IPv4 prep decides itself */
+		launch_ct_decide<K>(s, a, st);
 	hipError_t e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;
@@ -6028,6 +6495,7 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK6, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
+	launch_ct_decide<CtK6S>(s, a, st);
 	e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;
@@ -6079,6 +6547,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	const bool serial = ctl[0] != 0;
 	if (serial)
 		hipLaunchKernelGGL((k_ct_prep<true, true>), dim3(g), dim3(256), 0, st, s, a);
+	launch_ct_decide<CtK4S>(s, a, st);
 	e = ct_group_sort(s, L, a, L.n, st);
 	if (e != hipSuccess)
 		return e;

@@ -157,6 +157,7 @@ struct ct_launch {
 	void *xdaddr;         /* [n] optional (IPv6: 16 bytes each) */
 	uint16_t *xdport;     /* [n] optional */
 	uint2 *res;           /* [n] packed per-packet outcome (kernels.hip ct_res) */
+	uint4 *dec;           /* [n] both tuples' policy decisions (kernels.hip k_ct_decide) */
 };
 
 size_t ct_temp_bytes(uint64_t n);

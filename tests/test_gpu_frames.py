@@ -82,15 +82,22 @@ def _classify_frames(torch, e, f):
             out["stage"].cpu().numpy())
 
 
+SCHED_FRAMES_FUSED = 8  # CGPU_SCHED_FRAMES_FUSED: the classify kernel parses the slots
+
+
 @pytest.mark.parametrize("gate,verify", [(1, 7), (0, 7), (1, 0)])
-def test_classify_frames_vs_restatement(torch_cuda, gate, verify):
+@pytest.mark.parametrize("stride,sched", [(128, 0), (64, 0), (64, SCHED_FRAMES_FUSED)])
+def test_classify_frames_vs_restatement(torch_cuda, gate, verify, stride, sched):
     """Mixed v4 / v6 frames through the whole decision: verdicts, identities,
-    stages, per-entry counters and metrics equal the restatement's."""
+    stages, per-entry counters and metrics equal the restatement's: the
+    parse pass + classify pass, and with 64-byte slots the fused kernel (the
+    classify kernel parses the slots itself) the schedule can select."""
     T = synth.make_tables(n_prefixes=5000, n_identities=300, n_endpoints=5, keys_per_ep=3000)
     rng = np.random.Generator(np.random.PCG64(0xC1A55 + gate + verify))
     pool = T.pfx_addr.astype(np.uint32).byteswap()
     f = synth.make_frames(rng, 300_000, width=128, addr4=pool)
-    e = _engine(gate, verify, **T.engine_config())
+    f["data"] = np.ascontiguousarray(f["data"][:, :stride])
+    e = _engine(gate, verify, **T.engine_config(), schedule=sched)
     synth.load_engine(e, T)
     e.commit()
     o = frame_oracle(gate, verify, **T.oracle_config())
@@ -112,9 +119,10 @@ def test_classify_frames_vs_restatement(torch_cuda, gate, verify):
     e.close()
 
 
+@pytest.mark.parametrize("stride,sched", [(128, 0), (64, 0), (64, SCHED_FRAMES_FUSED)])
 @pytest.mark.parametrize("kind", ["runt", "v6", "not_classified"])
-@pytest.mark.parametrize("tail", [1, 2, 3])
-def test_classify_frames_ragged_tail(torch_cuda, tail, kind):
+@pytest.mark.parametrize("tail", [1, 2, 3, 63, 65])
+def test_classify_frames_ragged_tail(torch_cuda, tail, kind, stride, sched):
     """Batches of 4k + tail frames whose last partial quad starts with a frame
     the x4 schedule does not carry through its cascade: a runt the parse
     drops (DROP_INVALID, counted in the metrics), an IPv6 frame (its v4
@@ -127,6 +135,7 @@ def test_classify_frames_ragged_tail(torch_cuda, tail, kind):
     pool = T.pfx_addr.astype(np.uint32).byteswap()
     n = 4 * 5000 + tail
     f = synth.make_frames(rng, n, width=128, addr4=pool)
+    f["data"] = np.ascontiguousarray(f["data"][:, :stride])
     o = frame_oracle(1, 7, **T.oracle_config())
     synth.load_oracle(o, T)
     at = n - tail
@@ -139,7 +148,7 @@ def test_classify_frames_ragged_tail(torch_cuda, tail, kind):
         j = int(np.flatnonzero(want[:at])[0])
         for k in ("data", "len", "flags", "ep"):
             f[k][at] = f[k][j]
-    e = _engine(1, 7, **T.engine_config())
+    e = _engine(1, 7, **T.engine_config(), schedule=sched)
     synth.load_engine(e, T)
     e.commit()
     v, idt, st = _classify_frames(torch_cuda, e, f)
