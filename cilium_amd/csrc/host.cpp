@@ -5202,8 +5202,8 @@ CGPU_EXPORT int cgpu_ct6_flush(cgpu_ctx *c)
 
 /* scratch of one cgpu_classify_v{4,6}_ct launch over n packets */
 struct CtScratch {
-	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, head,
-		temp, temp_bytes, svc_out, ctl, flags2, res, dec, total;
+	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, heads_pos, head,
+		temp, temp_bytes, svc_out, ctl, flags2, total;
 };
 
 static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool v6)
@@ -5221,12 +5221,11 @@ static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool 
 	L.idx_sorted = take(n * 4);
 	L.heads = take(n * 4);
 	L.n_heads = take(4);
+	L.heads_pos = take(n * 4);
 	L.head = take(n);
 	L.temp_bytes = ct_temp_bytes(n);
 	L.temp = take(L.temp_bytes);
 	L.flags2 = take((svc ? 4 : 2) * n); /* phase-2 candidates */
-	L.res = take(n * 8);                /* packed outcome per packet */
-	L.dec = take(n * 16);               /* policy decisions per packet */
 	if (svc) {
 		L.svc_out = take(n * (v6 ? 32 : 16));
 		L.ctl = take(16);
@@ -5288,11 +5287,10 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.head = b + L.head;
 	a.heads = reinterpret_cast<uint32_t *>(b + L.heads);
 	a.n_heads = reinterpret_cast<uint32_t *>(b + L.n_heads);
+	a.heads_pos = reinterpret_cast<uint32_t *>(b + L.heads_pos);
 	a.temp = b + L.temp;
 	a.temp_bytes = L.temp_bytes;
 	a.flags2 = b + L.flags2;
-	a.res = reinterpret_cast<uint2 *>(b + L.res);
-	a.dec = reinterpret_cast<uint4 *>(b + L.dec);
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
 		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);

@@ -4193,55 +4193,19 @@ struct ct_args {
 	uint16_t *xdport;            /* [n] optional: frame dport after it */
 	uint32_t serial;             /* one group for the whole batch (see launch_ctlb) */
 	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
-	/* [n] every packet's outcome, batch order, written by the walks (the
-	 * prep for packets no walk replays): x = verdict (17 bits, signed) |
-	 * ct result with the walker's CT_* flags << 17 | stage << 25, y = the
-	 * identity; k_ct_out unpacks it into the caller's columns */
-	uint2 *res;
-	/* [n] both tuples' policy decisions (k_ct_decide), batch order */
-	uint4 *dec;
 };
 
-/* the packed per-packet outcome (ct_args.res) */
-#define CTR_NONE 0xFFu /* ct_lookup never ran (gated packets): ct_ret 255 */
-__device__ __forceinline__ uint2 ct_res(int32_t v, uint32_t ret, uint32_t st, uint32_t id)
-{
-	return make_uint2(((uint32_t)v & 0x1FFFFu) | ((ret & 0xFFu) << 17) | ((st & 7u) << 25), id);
-}
-__device__ __forceinline__ int32_t ct_res_verdict(uint32_t x) { return (int32_t)(x << 15) >> 15; }
-__device__ __forceinline__ uint32_t ct_res_ret(uint32_t x) { return (x >> 17) & 0xFFu; }
-
-/* ct_args.dec words (k_ct_decide) */
-__device__ __forceinline__ uint32_t ct_dec_pack(const decision &d)
-{
-	return (uint32_t)(d.ctr + 1) | (d.st << 24) | (d.v < 0 ? 1u << 26 : 0u);
-}
-
-__device__ __forceinline__ decision ct_dec_of(const uint4 &D, bool reply)
-{
-	const uint32_t x = reply ? D.y : D.x;
-	decision d;
-	d.ctr = (int)(x & 0xFFFFFFu) - 1;
-	d.st = (x >> 24) & 3u;
-	d.v = (x & (1u << 26)) ? DROP_POLICY : (int32_t)((reply ? D.w >> 16 : D.w) & 0xFFFFu);
-	d.id = D.z;
-	return d;
-}
-
-
-/* One packet's record, written by k_ct_prep{,6} and read by the walks
- * (batch order):
+/* One packet's record, written by k_ct_prep{,6} and read by the walker and
+ * k_ct_finish (batch order):
  *   IPv4 (2 x 16 B): {daddr, saddr, z, nexthdr | tflags << 8 | meta << 16},
- *                    {w | ep << 16, len, 0, 0}
+ *                    {w | port << 16, len, sec, cst}
  *   IPv6 (4 x 16 B): {daddr}, {saddr}, {z, nexthdr | tflags << 8 | meta << 16,
- *                    w | ep << 16, len}, {0, 0, rev_nat, 0}
+ *                    w | port << 16, len}, {sec, cst, rev_nat, 0}
  * z = the reply-direction tuple's dport | sport << 16 (ct_lookup's first
- * lookup), w = the L4 word (TCP header bytes 12-13 / ICMP type), ep = the
- * endpoint, rev_nat = the reverse NAT index an IPv6 ingress entry is created
- * with.  The policy decisions are k_ct_decide's (ct_args.dec); it also fills
- * the record's words DW, DW + 1 (IPv4: r1.z, r1.w; IPv6: r3.x, r3.y) with
- * what the walk needs of them: the identity and whether the forward tuple's
- * verdict allows (creates / deletes). */
+ * lookup), w = the L4 word (TCP header bytes 12-13 / ICMP type), port = the
+ * forward decision's proxy port, sec = src_sec_id of a created entry, cst =
+ * counter slot + 1 | stage << 24 of the forward decision, rev_nat = the
+ * reverse NAT index an IPv6 ingress entry is created with. */
 struct ct_pkt {
 	uint32_t meta, w, len, sec, revnat, port, cst, dport, proto;
 	uint32_t sa4, da4;
@@ -4249,12 +4213,6 @@ struct ct_pkt {
 	/* the service's ct_state (CtK4S): slave, lb_loopback | mode << 1, addr,
 	 * svc_addr */
 	uint32_t slave, lbf, addr, svc_addr;
-	/* the endpoint index, and z (the reply tuple's dport | sport << 16: the
-	 * forward tuple's dport is z >> 16) */
-	uint32_t ep, z;
-	/* k_ct_decide's words in the record: the identity, and bit 0 = the
-	 * forward tuple's verdict is not a drop */
-	uint32_t pid, pok;
 };
 
 template <class K> struct ct_rec;
@@ -4268,22 +4226,16 @@ template <> struct ct_rec<CtK4> {
 	}
 	__device__ CtK4::key key() const { return uint4{r0.x, r0.y, r0.z, r0.w & 0xFFFFu}; }
 	__device__ uint32_t meta() const { return r0.w >> 16; }
-	static constexpr uint32_t DW = 6;
 	__device__ ct_pkt pkt() const
 	{
-		ct_pkt q{r0.w >> 16, r1.x & 0xFFFFu, r1.y, 0u, 0u, 0u, 0u, r0.z & 0xFFFFu,
-			 r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{}};
-		q.ep = r1.x >> 16;
-		q.z = r0.z;
-		q.pid = r1.z;
-		q.pok = r1.w;
-		return q;
+		return ct_pkt{r0.w >> 16, r1.x & 0xFFFFu, r1.y, r1.z, 0u, r1.x >> 16, r1.w, r0.z & 0xFFFFu,
+			      r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{}};
 	}
 };
 /*   IPv4 behind the service step (3 x 16 B): the IPv4 record, then
  *                    {rev_nat | slave << 16, addr, svc_addr, lbf} */
 template <> struct ct_rec<CtK4S> {
-	static constexpr uint32_t RW = 3, DW = 6;
+	static constexpr uint32_t RW = 3;
 	uint4 r0, r1, r2;
 	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
 	{
@@ -4295,18 +4247,13 @@ template <> struct ct_rec<CtK4S> {
 	__device__ uint32_t meta() const { return r0.w >> 16; }
 	__device__ ct_pkt pkt() const
 	{
-		ct_pkt q{r0.w >> 16, r1.x & 0xFFFFu, r1.y, 0u, r2.x & 0xFFFFu, 0u, 0u,
-			 r0.z & 0xFFFFu, r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{},
-			 r2.x >> 16, r2.w, r2.y, r2.z};
-		q.ep = r1.x >> 16;
-		q.z = r0.z;
-		q.pid = r1.z;
-		q.pok = r1.w;
-		return q;
+		return ct_pkt{r0.w >> 16, r1.x & 0xFFFFu, r1.y, r1.z, r2.x & 0xFFFFu, r1.x >> 16, r1.w,
+			      r0.z & 0xFFFFu, r0.w & 0xFFu, r0.y, r0.x, uint4{}, uint4{},
+			      r2.x >> 16, r2.w, r2.y, r2.z};
 	}
 };
 template <> struct ct_rec<CtK6> {
-	static constexpr uint32_t RW = 4, DW = 12;
+	static constexpr uint32_t RW = 4;
 	uint4 r0, r1, r2, r3;
 	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
 	{
@@ -4318,13 +4265,8 @@ template <> struct ct_rec<CtK6> {
 	__device__ uint32_t meta() const { return r2.y >> 16; }
 	__device__ ct_pkt pkt() const
 	{
-		ct_pkt q{r2.y >> 16, r2.z & 0xFFFFu, r2.w, 0u, r3.z, 0u, 0u, r2.x & 0xFFFFu,
-			 r2.y & 0xFFu, 0u, 0u, r1, r0};
-		q.ep = r2.z >> 16;
-		q.z = r2.x;
-		q.pid = r3.x;
-		q.pok = r3.y;
-		return q;
+		return ct_pkt{r2.y >> 16, r2.z & 0xFFFFu, r2.w, r3.x, r3.z, r2.z >> 16, r3.y, r2.x & 0xFFFFu,
+			      r2.y & 0xFFu, 0u, 0u, r1, r0};
 	}
 };
 
@@ -4341,10 +4283,10 @@ __device__ __forceinline__ uint4 ct_addr_key(uint4 k, const ct_pkt &q)
 	return k;
 }
 
-/*   IPv6 behind the service step: the IPv6 record with {0, 0, rev_nat,
+/*   IPv6 behind the service step: the IPv6 record with {sec, cst, rev_nat,
  *                    slave | lbf << 16} as its last word */
 template <> struct ct_rec<CtK6S> {
-	static constexpr uint32_t RW = 4, DW = 12;
+	static constexpr uint32_t RW = 4;
 	uint4 r0, r1, r2, r3;
 	__device__ static ct_rec load(const uint4 *rec, uint32_t i, bool nt)
 	{
@@ -4356,13 +4298,8 @@ template <> struct ct_rec<CtK6S> {
 	__device__ uint32_t meta() const { return r2.y >> 16; }
 	__device__ ct_pkt pkt() const
 	{
-		ct_pkt q{r2.y >> 16, r2.z & 0xFFFFu, r2.w, 0u, r3.z, 0u, 0u, r2.x & 0xFFFFu,
-			 r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
-		q.ep = r2.z >> 16;
-		q.z = r2.x;
-		q.pid = r3.x;
-		q.pok = r3.y;
-		return q;
+		return ct_pkt{r2.y >> 16, r2.z & 0xFFFFu, r2.w, r3.x, r3.z, r2.z >> 16, r3.y, r2.x & 0xFFFFu,
+			      r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
 	}
 };
 
@@ -4400,15 +4337,14 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 		if constexpr (SVC) {
 			const uint4 so = egress ? a.svc_out[i] : make_uint4(SVC_NONE, 0, 0, 0);
 			if ((so.x & 3u) == SVC_DROP) {
-				/* lb4_local failed closed (lb.h:715-744) */
-				a.res[i] = ct_res(DROP_NO_SERVICE, CTR_NONE, 6u, 0u);
+				a.identity[i] = 0;
 				if (a.xdaddr)
 					a.xdaddr[i] = da;
 				if (a.xdport)
 					a.xdport[i] = (uint16_t)dp;
 				uint4 *r = a.rec + RW * i;
 				r[0] = uint4{da, sa, 0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16)};
-				r[1] = uint4{ep << 16, len, 0u, 0u};
+				r[1] = uint4{0u, len, 0u, 0u};
 				r[2] = uint4{0u, 0u, 0u, 0u};
 				a.gkey[i] = SERIAL ? 0u : ct_fmix((uint32_t)i ^ 0x5bd1e995u);
 				a.idx[i] = (uint32_t)i;
@@ -4463,11 +4399,25 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 		}
 		if (pr != 6u)
 			w = 0; /* union tcp_flags stays zero (conntrack.h:448) */
+		uint32_t sec = 0, port = 0, cst = 0, id = 0;
 		if (!(meta & CTM_GATED)) {
-			if (!egress && ((fl >> 1) & 1u))
+			/* the forward tuple's decision (what CT_NEW / CT_ESTABLISHED
+			 * packets see); k_ct_finish bumps its counter */
+			const bool frag = !egress && ((fl >> 1) & 1u);
+			if (frag)
 				meta |= CTM_FRAG;
-		} else {
-			a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u); /* ct_lookup4's default */
+			const decision d = decide<0>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
+						    pr, ep);
+			if (d.v >= 0) {
+				meta |= CTM_ALLOWED;
+				port = (uint32_t)d.v;
+			}
+			id = d.id;
+			if (egress)
+				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
+			else
+				sec = d.id;
+			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
 		}
 		uint32_t g = ct_group(sa, da);
 		if constexpr (!SVC) {
@@ -4519,9 +4469,10 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 				}
 			}
 		}
+		a.identity[i] = id;
 		uint4 *r = a.rec + RW * i;
 		r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
-		r[1] = uint4{w | (ep << 16), len, 0u, 0u};
+		r[1] = uint4{w | (port << 16), len, sec, cst};
 		if constexpr (SVC)
 			r[2] = uint4{r2x, addr, saddr2, lbf};
 		a.gkey[i] = SERIAL ? 0u : (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
@@ -4530,185 +4481,197 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 }
 
 /* k_ct_prep<false, false> (the plain IPv4 path) with Q packets per lane:
- * packet i = g + u * (threads), so every column load of a wave covers 64
- * consecutive packets: the tuple ct_lookup4 builds, the group key and the
- * record, then k_ct_decide's two decisions (the other paths run it as its
- * own pass) with every lookup stage's gathers in flight together */
-#ifndef CGPU_CT_FUSED_DECIDE
-#define CGPU_CT_FUSED_DECIDE 1 /* 0: the IPv4 prep leaves the decisions to k_ct_decide (A/B) */
-#endif
-
+ * the forward decisions through decide4_q; packet i = g + u * (threads),
+ * so every column load of a wave covers 64 consecutive packets */
 template <int Q>
 __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 {
-	constexpr bool FD = CGPU_CT_FUSED_DECIDE;
-	/* the LPM leaf dictionary in LDS, as k_classify_x4 */
-	extern __shared__ __attribute__((aligned(16))) uint32_t ldict[];
-	if (FD) {
-		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += 256u)
-			ldict[k] = s.ipc4c.dict[k];
-		__syncthreads();
-	}
 	const uint64_t T = (uint64_t)gridDim.x * 256u;
 	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
-		bool act[Q], eg[Q], frag[Q], act2[Q];
-		uint32_t sa[Q], da[Q], dpf[Q], dpr[Q], pr[Q], ep[Q], w1[Q], len[Q];
-		decision d[Q], d2[Q];
+		bool act[Q], dec[Q], eg[Q], frag[Q];
+		uint32_t sa[Q], da[Q], fdp[Q], pr[Q], ep[Q], meta[Q], tfl[Q], z[Q], w[Q], len[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
-			act[u] = eg[u] = frag[u] = false;
-			sa[u] = da[u] = dpf[u] = dpr[u] = pr[u] = ep[u] = w1[u] = len[u] = 0u;
-			if (i >= a.n)
-				continue;
-			/* columns stream past the map: nontemporal */
-			const uint32_t fl = ntl(a.flags + i);
-			len[u] = ntl(a.len + i);
-			pr[u] = ntl(a.proto + i);
-			sa[u] = ntl(a.saddr + i);
-			da[u] = ntl(a.daddr + i);
-			ep[u] = ntl(a.ep + i);
-			const uint32_t dp = ntl(a.dport + i), sp = ntl(a.sport + i);
-			uint32_t w = ntl(a.l4 + i);
+			act[u] = i < a.n;
+			const uint64_t j = act[u] ? i : 0u;
+			/* columns stream past the tables: nontemporal, so they do not
+			 * evict the LPM / policy lines from L2 */
+			const uint32_t fl = ntl(a.flags + j);
+			pr[u] = ntl(a.proto + j);
+			len[u] = ntl(a.len + j);
+			sa[u] = ntl(a.saddr + j);
+			da[u] = ntl(a.daddr + j);
+			ep[u] = ntl(a.ep + j);
+			w[u] = ntl(a.l4 + j);
+			const uint32_t dp = ntl(a.dport + j), sp = ntl(a.sport + j);
 			eg[u] = fl & 1u;
-			uint32_t tfl = eg[u] ? TUPLE_F_IN : 0u, meta = eg[u] ? CTM_EGRESS : 0u, z = 0;
+			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
+			meta[u] = eg[u] ? CTM_EGRESS : 0u;
+			z[u] = 0;
 			if (pr[u] == 1u) { /* as k_ct_prep */
-				const uint32_t type = w & 0xFFu;
+				const uint32_t type = w[u] & 0xFFu;
 				if (type == 3u || type == 11u || type == 12u)
-					tfl |= TUPLE_F_RELATED;
+					tfl[u] |= TUPLE_F_RELATED;
 				else if (type == 0u)
-					z = 8u;
+					z[u] = 8u;
 				else {
 					if (type == 8u)
-						z = 8u << 16;
-					meta |= CTM_ACT_CREATE;
+						z[u] = 8u << 16;
+					meta[u] |= CTM_ACT_CREATE;
 				}
 			} else if (pr[u] == 6u || pr[u] == 17u) {
-				z = sp | (dp << 16);
-				meta |= pr[u] == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
+				z[u] = sp | (dp << 16);
+				meta[u] |= pr[u] == 6u ? (CTM_TCP | ((w[u] & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE))
+						       : CTM_ACT_CREATE;
 			} else {
-				meta |= CTM_GATED;
+				meta[u] |= CTM_GATED;
 			}
 			if (pr[u] != 6u)
-				w = 0;
-			w1[u] = w | (ep[u] << 16);
-			uint32_t gk = ct_group(sa[u], da[u]);
-			bool p2 = false;
-			if (!(meta & CTM_GATED)) {
-				if (!eg[u] && ((fl >> 1) & 1u))
-					meta |= CTM_FRAG;
-				if (pr[u] == 1u && (tfl & TUPLE_F_RELATED)) {
-					meta |= CTM_PHASE2;
-					p2 = true;
-				} else {
-					meta |= CTM_RELX;
-					gk = ct_conn_group(gk, z, pr[u]);
-				}
-				act[u] = FD;
-			} else {
-				a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u);
-			}
-			frag[u] = meta & CTM_FRAG;
-			dpf[u] = z >> 16;
-			dpr[u] = z & 0xFFFFu;
-			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
-			a.rec[2u * i] = uint4{da[u], sa[u], z, pr[u] | (tfl << 8) | (meta << 16)};
-			a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
-			a.idx[i] = (uint32_t)i;
+				w[u] = 0;
+			frag[u] = !eg[u] && ((fl >> 1) & 1u);
+			if (frag[u] && !(meta[u] & CTM_GATED))
+				meta[u] |= CTM_FRAG;
+			dec[u] = act[u] && !(meta[u] & CTM_GATED);
+			fdp[u] = z[u] >> 16;
 		}
-		/* the policy step of both tuples (k_ct_decide) */
-		if (FD) {
-			ident4_q<Q>(s, ldict, act, eg, sa, da, d);
-#pragma unroll
-			for (int u = 0; u < Q; u++) {
-				act2[u] = act[u] && dpr[u] != dpf[u];
-				d2[u].id = d[u].id;
-			}
-			policy2_qg<Q>(s, act, act2, eg, frag, dpf, dpr, pr, ep, d, d2);
-		} else {
-#pragma unroll
-			for (int u = 0; u < Q; u++) {
-				act2[u] = false;
-				d[u].v = -1;
-				d[u].id = 0;
-				d[u].ctr = -1;
-				d[u].st = 0;
-				d2[u] = d[u];
-			}
-		}
+		decision d[Q];
+		decide4_q<Q>(s, dec, eg, frag, sa, da, fdp, pr, ep, d);
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
-			const uint64_t i = g + (uint64_t)u * T;
-			if (i >= a.n)
+			if (!act[u])
 				continue;
-			const decision &rp = act2[u] ? d2[u] : d[u];
-			const uint32_t pf = d[u].v > 0 ? (uint32_t)d[u].v : 0u, prt = rp.v > 0 ? (uint32_t)rp.v : 0u;
-			if (act[u])
-				a.dec[i] = make_uint4(ct_dec_pack(d[u]), ct_dec_pack(rp), d[u].id, pf | (prt << 16));
-			a.rec[2u * i + 1u] = uint4{w1[u], len[u], act[u] ? d[u].id : 0u, (act[u] && d[u].v >= 0) ? 1u : 0u};
+			const uint64_t i = g + (uint64_t)u * T;
+			uint32_t sec = 0, port = 0, cst = 0, id = 0, m = meta[u];
+			if (dec[u]) {
+				if (d[u].v >= 0) {
+					m |= CTM_ALLOWED;
+					port = (uint32_t)d[u].v;
+				}
+				id = d[u].id;
+				sec = eg[u] ? (ep[u] < s.n_lxc ? s.lxc[2u * ep[u] + 1u].w : 0u) : d[u].id;
+				cst = (uint32_t)(d[u].ctr + 1) | (d[u].st << 24);
+			}
+			uint32_t gk = ct_group(sa[u], da[u]);
+			bool p2 = false;
+			if (dec[u]) {
+				if (pr[u] == 1u && (tfl[u] & TUPLE_F_RELATED)) {
+					m |= CTM_PHASE2;
+					p2 = true;
+				} else {
+					m |= CTM_RELX;
+					gk = ct_conn_group(gk, z[u], pr[u]);
+				}
+			}
+			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
+			a.identity[i] = id;
+			uint4 *r = a.rec + 2u * i;
+			r[0] = uint4{da[u], sa[u], z[u], pr[u] | (tfl[u] << 8) | (m << 16)};
+			r[1] = uint4{w[u] | (port << 16), len[u], sec, cst};
+			a.gkey[i] = (m & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
+			a.idx[i] = (uint32_t)i;
 		}
 	}
 }
 
-/* k_ct_prep6<false> (the plain IPv6 path) with Q packets per lane: a
- * streaming pass as k_ct_prep_q */
+/* k_ct_prep6<false> (the plain IPv6 path) with Q packets per lane, the
+ * ipcache entries from the pre-pass (k_ipc6_pre, egress fallback folded in)
+ * and the policy cascades through policy_q */
 template <int Q>
-__global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a)
+__global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, const uint32_t *ipc_e)
 {
 	const uint64_t T = (uint64_t)gridDim.x * 256u;
 	const uint4 *sa16 = reinterpret_cast<const uint4 *>(a.saddr);
 	const uint4 *da16 = reinterpret_cast<const uint4 *>(a.daddr);
 	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+		bool act[Q], dec[Q], eg[Q], frag[Q];
+		uint32_t fdp[Q], pr[Q], ep[Q], meta[Q], tfl[Q], z[Q], w[Q], len[Q];
+		decision d[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
-			if (i >= a.n)
-				continue;
-			const uint32_t fl = ntl(a.flags + i), dp = ntl(a.dport + i), sp = ntl(a.sport + i);
-			const uint32_t pr = ntl(a.proto + i), len = ntl(a.len + i), ep = ntl(a.ep + i);
-			uint32_t w = ntl(a.l4 + i);
-			const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
-			const bool eg = fl & 1u; /* no fragment flag on IPv6 (bpf_lxc.c:787-789) */
-			uint32_t tfl = eg ? TUPLE_F_IN : 0u, meta = eg ? CTM_EGRESS : 0u, z = 0;
-			if (pr == 58u) { /* as k_ct_prep6 */
-				const uint32_t type = w & 0xFFu;
+			act[u] = i < a.n;
+			const uint64_t j = act[u] ? i : 0u;
+			const uint32_t fl = ntl(a.flags + j), dp = ntl(a.dport + j), sp = ntl(a.sport + j);
+			pr[u] = ntl(a.proto + j);
+			len[u] = ntl(a.len + j);
+			ep[u] = ntl(a.ep + j);
+			w[u] = ntl(a.l4 + j);
+			eg[u] = fl & 1u;
+			frag[u] = false; /* no fragment flag on IPv6 (bpf_lxc.c:787-789) */
+			tfl[u] = eg[u] ? TUPLE_F_IN : 0u;
+			meta[u] = eg[u] ? CTM_EGRESS : 0u;
+			z[u] = 0;
+			if (pr[u] == 58u) { /* as k_ct_prep6 */
+				const uint32_t type = w[u] & 0xFFu;
 				if (type >= 1u && type <= 4u)
-					tfl |= TUPLE_F_RELATED;
+					tfl[u] |= TUPLE_F_RELATED;
 				else if (type == 129u)
-					z = 128u;
+					z[u] = 128u;
 				else {
 					if (type == 128u)
-						z = 128u << 16;
-					meta |= CTM_ACT_CREATE;
+						z[u] = 128u << 16;
+					meta[u] |= CTM_ACT_CREATE;
 				}
-			} else if (pr == 6u || pr == 17u) {
-				z = sp | (dp << 16);
-				meta |= pr == 6u ? (CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE)) : CTM_ACT_CREATE;
+			} else if (pr[u] == 6u || pr[u] == 17u) {
+				z[u] = sp | (dp << 16);
+				meta[u] |= pr[u] == 6u ? (CTM_TCP | ((w[u] & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE))
+						       : CTM_ACT_CREATE;
 			} else {
-				meta |= CTM_GATED;
+				meta[u] |= CTM_GATED;
 			}
-			if (pr != 6u)
-				w = 0;
+			if (pr[u] != 6u)
+				w[u] = 0;
+			dec[u] = act[u] && !(meta[u] & CTM_GATED);
+			fdp[u] = z[u] >> 16;
+			/* decide<1>'s identity from the pre-pass entry */
+			const uint32_t e = ntl(ipc_e + j);
+			const uint32_t label = entry_label(s.ipc6.vals, e);
+			if (eg[u]) {
+				d[u].id = (e && label) ? label : s.world_id; /* cluster fallback folded into e */
+			} else {
+				uint32_t src = s.ingress_src_identity;
+				if (src < s.health_id && e && label && label != s.cluster_id)
+					src = label;
+				d[u].id = src;
+			}
+		}
+		policy_q<Q>(s, dec, eg, frag, fdp, pr, ep, d);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (!act[u])
+				continue;
+			const uint64_t i = g + (uint64_t)u * T;
+			const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
+			uint32_t sec = 0, port = 0, cst = 0, id = 0, m = meta[u];
+			if (dec[u]) {
+				if (d[u].v >= 0) {
+					m |= CTM_ALLOWED;
+					port = (uint32_t)d[u].v;
+				}
+				id = d[u].id;
+				sec = eg[u] ? (ep[u] < s.n_lxc ? s.lxc[2u * ep[u] + 1u].w : 0u) : d[u].id;
+				cst = (uint32_t)(d[u].ctr + 1) | (d[u].st << 24);
+			}
 			uint32_t gk = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
 			bool p2 = false;
-			if (!(meta & CTM_GATED)) {
-				if (pr == 58u && (tfl & TUPLE_F_RELATED)) {
-					meta |= CTM_PHASE2;
+			if (dec[u]) {
+				if (pr[u] == 58u && (tfl[u] & TUPLE_F_RELATED)) {
+					m |= CTM_PHASE2;
 					p2 = true;
 				} else {
-					meta |= CTM_RELX;
-					gk = ct_conn_group(gk, z, pr);
+					m |= CTM_RELX;
+					gk = ct_conn_group(gk, z[u], pr[u]);
 				}
-			} else {
-				a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u);
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
+			a.identity[i] = id;
 			uint4 *r = a.rec + 4u * i;
 			r[0] = da;
 			r[1] = sa;
-			r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (ep << 16), len};
-			r[3] = uint4{0u, 0u, eg ? 0u : (da.w & 0xFFFFu), 0u};
-			a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
+			r[2] = uint4{z[u], pr[u] | (tfl[u] << 8) | (m << 16), w[u] | (port << 16), len[u]};
+			r[3] = uint4{sec, cst, eg[u] ? 0u : (da.w & 0xFFFFu), 0u};
+			a.gkey[i] = (m & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
 			a.idx[i] = (uint32_t)i;
 		}
 	}
@@ -4735,7 +4698,7 @@ __global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint32_t *f4, 
 		const bool p2 = live && (meta & CTM_PHASE2);
 		uint32_t f;
 		if (phase == 0u) {
-			const bool rel = live && (meta & CTM_RELX) && (ct_res_ret(a.res[i].x) & CT_RELP);
+			const bool rel = live && (meta & CTM_RELX) && (a.ct_ret[i] & CT_RELP);
 			f = (p2 && !special ? 1u : 0u) | (rel ? 1u << 16 : 0u);
 		} else {
 			f = (p2 && special ? 1u : 0u) | (live && (meta & CTM_ADDRX) ? 1u << 8 : 0u);
@@ -4767,6 +4730,18 @@ template <class K> __global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args
 			const uint4 k = r.key();
 			a.gkey[j] = ct_group(k.x, k.y);
 		}
+	}
+}
+
+/* length of every group (keys) and its start (values), for the longest-
+ * first sort */
+__global__ __launch_bounds__(256) void k_ct_lens(const uint32_t *heads, uint32_t nh, uint64_t n,
+						 uint32_t *len, uint32_t *pos)
+{
+	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += gridDim.x * 256u) {
+		const uint32_t p0 = heads[h];
+		len[h] = (uint32_t)((h + 1u < nh ? (uint64_t)heads[h + 1u] : n) - p0);
+		pos[h] = p0;
 	}
 }
 
@@ -4802,7 +4777,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 			/* lb6_local's outcome (svc_out[2i], target svc_out[2i + 1]) */
 			const uint4 so = egress ? a.svc_out[2u * i] : make_uint4(SVC_NONE, 0, 0, 0);
 			if ((so.x & 3u) == SVC_DROP) {
-				a.res[i] = ct_res(DROP_NO_SERVICE, CTR_NONE, 6u, 0u);
+				a.identity[i] = 0;
 				reinterpret_cast<uint16_t *>(a.f2)[i] = 0u;
 				if (a.xdaddr)
 					reinterpret_cast<uint4 *>(a.xdaddr)[i] = da;
@@ -4811,7 +4786,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 				uint4 *r = a.rec + 4u * i;
 				r[0] = da;
 				r[1] = sa;
-				r[2] = uint4{0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16), ep << 16, len};
+				r[2] = uint4{0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16), 0u, len};
 				r[3] = uint4{0u, 0u, 0u, 0u};
 				a.gkey[i] = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
 				a.idx[i] = (uint32_t)i;
@@ -4851,8 +4826,20 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 		}
 		if (pr != 6u)
 			w = 0; /* union tcp_flags stays zero (conntrack.h:294) */
-		if (meta & CTM_GATED)
-			a.res[i] = ct_res(DROP_CT_UNKNOWN_PROTO, CTR_NONE, 4u, 0u);
+		uint32_t sec = 0, port = 0, cst = 0, id = 0;
+		if (!(meta & CTM_GATED)) {
+			const decision d = decide<1>(s, egress, false, 0u, 0u, sa, da, z >> 16, pr, ep);
+			if (d.v >= 0) {
+				meta |= CTM_ALLOWED;
+				port = (uint32_t)d.v;
+			}
+			id = d.id;
+			if (egress)
+				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
+			else
+				sec = d.id;
+			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+		}
 		uint32_t g = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
 		{ /* phase 1 by connection, as k_ct_prep (ct_create6 writes no address
 		   * entry, so the service path groups the same way) */
@@ -4868,11 +4855,12 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
 		}
+		a.identity[i] = id;
 		uint4 *r = a.rec + 4u * i;
 		r[0] = da;
 		r[1] = sa;
-		r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (ep << 16), len};
-		r[3] = uint4{0u, 0u, rev, svcw};
+		r[2] = uint4{z, pr | (tfl << 8) | (meta << 16), w | (port << 16), len};
+		r[3] = uint4{sec, cst, rev, svcw};
 		a.gkey[i] = (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
 		a.idx[i] = (uint32_t)i;
 	}
@@ -5271,19 +5259,19 @@ template <class K> __device__ __forceinline__ ct_row ct_new_row(const ct_pkt &q,
  * :288-412) and ct_create4 / ct_create6 (:653-744 / :588-639), with the
  * policy outcome of the endpoint programs (bpf_lxc.c:506-537 / :918-937,
  * :192-203 / :776-800).  k = the reply-direction tuple of the first lookup. */
-template <class K, class DF>
+template <class K>
 __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A, ct_cache<K> &c,
-					   typename K::key k, ct_pkt &q, uint32_t now, DF &&policy, decision &d)
+					   typename K::key k, const ct_pkt &q, uint32_t now)
 {
 	const uint32_t meta = q.meta;
 	const bool ingress = !(meta & CTM_EGRESS);
 	{
 		/* reply key not cached, or cached absent: fetch it, the forward key
-		 * and the ICMP key in one round */
+		 * and (when the packet may create) the ICMP key in one round */
 		const int c1 = ctc_find<K>(c, k);
 		if (c1 < 0 || (ctc_state(c, c1) & CTC_NEG)) {
 			const typename K::key fk = K::reversed(k);
-			ctc_prefetch<K>(T, c, k, fk, K::related(fk), c1 < 0, true, true);
+			ctc_prefetch<K>(T, c, k, fk, K::related(fk), c1 < 0, true, (meta & CTM_ALLOWED) != 0);
 		}
 	}
 	int ci = ctc_get<K>(T, c, k);
@@ -5295,16 +5283,12 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 		ci = ctc_get<K>(T, c, k);
 		ret = (ctc_state(c, ci) & CTC_NEG) ? CT_NEW : CT_ESTABLISHED;
 	}
-	/* the endpoint program's policy step on the tuple ct_lookup left: the
-	 * reply tuple for CT_REPLY / CT_RELATED, the forward one otherwise */
-	d = policy(ret >= CT_REPLY);
-	const bool allowed = d.v >= 0;
 	if (ret != CT_NEW) {
 		ct_row e = ctc_row(c, ci);
 		ct_hit(e, meta, ingress, q.w, q.len, now);
 		ctc_put(c, ci, ctc_pos(c, ci), e);
 	}
-	if (ret < CT_REPLY && !allowed) {
+	if (ret < CT_REPLY && !(meta & CTM_ALLOWED)) {
 		if (ret == CT_ESTABLISHED) { /* ct_delete4 / ct_delete6 */
 			const uint32_t slot = ctc_pos(c, ci);
 			ct_erase<K>(T, A, slot);
@@ -5315,9 +5299,7 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 	if (ret != CT_NEW)
 		return ret;
 	/* ct_create: the forward entry, the address entry (service step only),
-	 * then the ICMP entry relating errors; src_sec_id = SECLABEL (egress) or
-	 * the source identity (ingress) */
-	q.sec = ingress ? d.id : q.sec;
+	 * then the ICMP entry relating errors */
 	ct_row e = ct_new_row<K>(q, ingress, now);
 	if (!ctc_update<K>(T, A, c, k, e))
 		return CT_NEW | CT_FAIL;
@@ -5643,147 +5625,13 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
 }
 
 #ifndef CT_RETB
-#define CT_RETB 6 /* results a walker lane buffers before storing them (12 B each in LDS) */
+#define CT_RETB 16 /* results a walker lane buffers before storing them */
 #endif
-
-/* ---- the endpoint programs' policy step (k_ct_decide) ----
- * decide<> for both tuples policy can see (bpf_lxc.c:484-537 / :876-950,
- * bpf_netdev.c:374-404): the forward tuple's dport (CT_NEW / CT_ESTABLISHED)
- * and the reply tuple's (CT_REPLY / CT_RELATED, left unreversed,
- * policy.h:98-99); the identity is the same for both (the addresses are).
- * A pass over the batch before the walk, Q packets per lane with every
- * lookup stage's gathers in flight together, so the walker's dependent
- * chain holds only conntrack: it reads the packet's decisions with its
- * record.  dec[i] = {fwd, rep, identity, fwd port | rep port << 16},
- * fwd / rep = counter slot + 1 | stage << 24 | deny << 26 (port = the
- * proxy port of an allowed verdict). */
-template <class K, int Q>
-__global__ __launch_bounds__(256) void k_ct_decide(cgpu_snapshot s, ct_args a)
-{
-	using R = ct_rec<K>;
-	constexpr bool V6 = K::V6 != 0;
-	/* v6: the trie's root bitmap, b24 blocks and /64 bloom in LDS, as
-	 * k_ipc6_pre */
-	extern __shared__ __attribute__((aligned(16))) uint32_t lt[];
-	uint32_t n24 = 0, nbl = 0;
-	uint32_t *lbl = lt;
-	if constexpr (!V6) { /* the LPM leaf dictionary */
-		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += 256u)
-			lt[k] = s.ipc4c.dict[k];
-		__syncthreads();
-	}
-	if constexpr (V6) {
-		n24 = v6t_lds_b24(s.ipc6);
-		nbl = v6t_lds_bloom(s.ipc6);
-		lbl = lt + v6t_lds_words(s.ipc6);
-		if (s.ipc6.root) {
-			for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += 256u)
-				lt[k] = s.ipc6.rbits[k];
-			const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
-			for (uint32_t k = threadIdx.x; k < n24 * 128u; k += 256u)
-				lt[V6T_RBITS_WORDS + k] = b16[k];
-			for (uint32_t k = threadIdx.x; k < nbl; k += 256u)
-				lbl[k] = s.ipc6.bl64[k];
-		}
-		__syncthreads();
-	}
-	const uint64_t T = (uint64_t)gridDim.x * 256u;
-	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
-		bool act[Q], eg[Q], frag[Q], act2[Q];
-		uint32_t dpf[Q], dpr[Q], pr[Q], ep[Q], sa[Q], da[Q];
-		uint4 w6[Q];
-		decision d[Q], d2[Q];
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			const uint64_t i = g + (uint64_t)u * T;
-			act[u] = i < a.n;
-			const R r = R::load(a.rec, act[u] ? (uint32_t)i : 0u, true);
-			const ct_pkt q = r.pkt();
-			act[u] = act[u] && !(q.meta & CTM_GATED);
-			eg[u] = q.meta & CTM_EGRESS;
-			frag[u] = q.meta & CTM_FRAG;
-			dpf[u] = q.z >> 16;
-			dpr[u] = q.z & 0xFFFFu;
-			pr[u] = q.proto;
-			ep[u] = q.ep;
-			sa[u] = q.sa4;
-			da[u] = q.da4;
-			w6[u] = V6 ? v6_host_words(eg[u] ? q.da6 : q.sa6) : make_uint4(0, 0, 0, 0);
-		}
-		if constexpr (V6) {
-			/* decide<1>'s identity (bpf_lxc.c:170-187 / bpf_netdev.c:203-211) */
-			uint32_t e[Q];
-			v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w6, act, e, nbl ? lbl : nullptr);
-#pragma unroll
-			for (int u = 0; u < Q; u++) {
-				const uint32_t label = entry_label(s.ipc6.vals, e[u]);
-				const bool in_cluster = w6[u].x == bswap32(s.router_ip64[0]) &&
-							w6[u].y == bswap32(s.router_ip64[1]);
-				if (eg[u]) {
-					d[u].id = (e[u] && label) ? label : (in_cluster ? s.cluster_id : s.world_id);
-				} else {
-					uint32_t src = s.ingress_src_identity;
-					if (src < s.health_id && e[u] && label && label != s.cluster_id)
-						src = label;
-					d[u].id = src;
-				}
-			}
-		} else {
-			ident4_q<Q>(s, lt, act, eg, sa, da, d);
-		}
-		/* both tuples' cascades (the reply tuple's where its dport differs) */
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			act2[u] = act[u] && dpr[u] != dpf[u];
-			d2[u].id = d[u].id;
-		}
-		policy2_qg<Q>(s, act, act2, eg, frag, dpf, dpr, pr, ep, d, d2);
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			const uint64_t i = g + (uint64_t)u * T;
-			if (!act[u])
-				continue;
-			const decision &rp = act2[u] ? d2[u] : d[u];
-			const uint32_t pf = d[u].v > 0 ? (uint32_t)d[u].v : 0u, prt = rp.v > 0 ? (uint32_t)rp.v : 0u;
-			a.dec[i] = make_uint4(ct_dec_pack(d[u]), ct_dec_pack(rp), d[u].id, pf | (prt << 16));
-			*reinterpret_cast<uint2 *>(reinterpret_cast<uint32_t *>(a.rec) + (uint64_t)R::RW * 4u * i + R::DW) =
-				make_uint2(d[u].id, d[u].v >= 0 ? 1u : 0u);
-		}
-	}
-}
-
-static size_t ct_decide_lds(const cgpu_snapshot &s, bool v6)
-{
-	return v6 ? (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u : (size_t)s.ipc4c.n_dict * 4u;
-}
-
-/* the verdict of a replayed packet (bpf_lxc.c:506-537 / :918-950: CT_REPLY /
- * CT_RELATED skip the drop; an egress proxy redirect keeps its port) */
-__device__ __forceinline__ int32_t ct_verdict(const decision &d, uint32_t ret, bool egress)
-{
-	int32_t v;
-	if ((ret & 3u) >= CT_REPLY)
-		v = (egress && d.v > 0) ? d.v : 0;
-	else if (d.v < 0)
-		v = DROP_POLICY;
-	else if (ret & CT_FAIL)
-		v = DROP_CT_CREATE_FAILED;
-	else
-		v = d.v;
-	return v;
-}
 
 /* walks: WALK_PKT the conntrack path's packets; WALK_SVC the service step
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
  * service path: candidates c = packet << 1 | kind, kind 0 a packet whose
  * address pair may hold owed entries, kind 1 an owed address entry */
-/* workgroups per CU the service-path walker (CtK4S: ~280 registers) is
- * compiled for: 2 spills a few registers to scratch to double its
- * occupancy */
-#ifndef CGPU_WALK_MINB_SVC
-#define CGPU_WALK_MINB_SVC 2
-#endif
-
 #define WALK_PKT 0
 #define WALK_SVC 1
 #define WALK_OWED 2
@@ -5802,7 +5650,7 @@ extern "C" __attribute__((visibility("default"))) int cgpu_diag_walk_clock(unsig
 #endif
 
 template <class K, int MODE>
-__global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
+__global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
 {
 #ifdef CGPU_DIAG_WALK_CLOCK
 	const unsigned long long dg_t0 = __builtin_amdgcn_s_memrealtime();
@@ -5818,14 +5666,13 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_wa
 	 * step (1.4 ms of a 12.3 ms step, profiles/r3_session_h/ab_ct_ret.log);
 	 * CT_RETB stores issued back to back cost about one */
 	__shared__ uint32_t s_ri[CT_RETB][256];
-	__shared__ uint2 s_rr[CT_RETB][256];
+	__shared__ uint8_t s_rr[CT_RETB][256];
 	uint32_t nret = 0;
 	auto ret_flush = [&]() {
 		for (uint32_t k = 0; k < nret; k++) {
-			const uint32_t i = s_ri[k][threadIdx.x];
-			const uint2 r = s_rr[k][threadIdx.x];
-			a.res[i] = r;
-			if (!K::ADDR && MODE == WALK_PKT && (ct_res_ret(r.x) & CT_RELP))
+			const uint32_t i = s_ri[k][threadIdx.x], ret = s_rr[k][threadIdx.x];
+			a.ct_ret[i] = (uint8_t)ret;
+			if (!K::ADDR && MODE == WALK_PKT && (ret & CT_RELP))
 				a.f2[2u * i + 1u] = 1u; /* its ICMP entry is owed to phase 2 */
 		}
 		nret = 0;
@@ -5893,30 +5740,23 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_wa
 					a.svc_out[i] = ct_svc_step(s, T, A, c, r, a.now);
 				}
 			} else {
-				ct_pkt q = r.pkt();
-				const bool egress = q.meta & CTM_EGRESS;
-				/* src_sec_id of an egress create: the endpoint's SECLABEL */
-				q.sec = egress && q.ep < s.n_lxc ? s.lxc[2u * q.ep + 1u].w : 0u;
+				const ct_pkt q = r.pkt();
 				if constexpr (MODE == WALK_OWED) {
 					const uint32_t kind = K::ADDR ? (v & 3u) : (v & 1u) << 1;
-					if (kind != 0u) {
-						const typename K::key fk = K::reversed(r.key());
-						/* the owed entries carry the create's ct_state: its
-						 * src_sec_id is the identity the create stored */
-						const uint2 pr = a.res[i];
-						q.sec = egress ? q.sec : pr.y;
-						if (kind == 1u) {
-							/* the owed address entry of packet i's create */
-							if constexpr (K::ADDR) {
-								if (ct_res_ret(pr.x) & CT_ADDRP)
-									ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
-											   ct_new_row<K>(q, false, a.now));
-							}
-							continue;
+					const typename K::key fk = K::reversed(r.key());
+					if (kind == 1u) {
+						/* the owed address entry of packet i's create */
+						if constexpr (K::ADDR) {
+							if (a.ct_ret[i] & CT_ADDRP)
+								ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
+										   ct_new_row<K>(q, false, a.now));
 						}
+						continue;
+					}
+					if (kind == 2u) {
 						/* the owed ICMP entry of packet i's create */
-						if (ct_res_ret(pr.x) & CT_RELP) {
-							ct_row e = ct_new_row<K>(q, !egress, a.now);
+						if (a.ct_ret[i] & CT_RELP) {
+							ct_row e = ct_new_row<K>(q, !(q.meta & CTM_EGRESS), a.now);
 							e.c.y |= CTB_SEEN_NON_SYN;
 							ctc_update_owed<K>(T, A, c, K::related(fk), e);
 						}
@@ -5925,22 +5765,9 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_wa
 				}
 				if (MODE == WALK_PKT && (meta & CTM_PHASE2))
 					continue;
-				/* what the walk needs of the decisions (k_ct_decide): the
-				 * identity and whether the forward tuple is allowed; the
-				 * verdict, stage and counters are k_ct_out's */
-				decision d;
-				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now,
-								[&](bool) {
-									decision x;
-									x.v = (q.pok & 1u) ? 0 : DROP_POLICY;
-									x.id = q.pid;
-									x.st = 0;
-									x.ctr = -1;
-									return x;
-								},
-								d);
+				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now);
 				s_ri[nret][threadIdx.x] = i;
-				s_rr[nret][threadIdx.x] = ct_res(0, ret, 0u, q.pid);
+				s_rr[nret][threadIdx.x] = (uint8_t)ret;
 				if (++nret == CT_RETB)
 					ret_flush();
 			}
@@ -5974,21 +5801,20 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_wa
 	}
 }
 
-/* The batch's outcome into the caller's columns, in batch order: the walks
- * wrote every replayed packet's ct result (ct_args.res), the prep the
- * gated ones' final outcome; the decision of the tuple policy saw (the
- * reply tuple's for CT_REPLY / CT_RELATED, k_ct_decide) gives the verdict,
- * stage and identity (bpf_lxc.c:506-537 / :918-950), and the hit entry's
- * counter (policy.h:68-93) its packet and bytes: hot slots in LDS, the
- * others through an LDS cold-slot cache (as k_classify_x4), one global
- * atomic pair per touched slot per workgroup at the end.  The {reason,
- * dir} metrics of the verdicts (drop.h:94-118 / metrics.h:41-59; a proxy
- * redirect traces TRACE_TO_PROXY and counts none).  A streaming pass over
- * the resident grid. */
-template <int NT>
-__global__ __launch_bounds__(NT) void k_ct_out(cgpu_snapshot s, ct_args a, uint32_t cc_n)
+/* policy on the tuple ct_lookup left, counters, the reply / related skip.
+ * CT_NEW / CT_ESTABLISHED packets reuse the prep's forward decision; only
+ * CT_REPLY / CT_RELATED ones run the cascade again, on the reply tuple.
+ * Hot counter slots accumulate in LDS (packed, as k_classify CTR = 1). */
+template <int NT, class K, int Q>
+__global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, uint32_t cc_n)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
+	/* metrics {reason 0 / 133 / 137 / 155 [/ 158]} x {ingress, egress} */
+	constexpr int NM = K::SVC ? 10 : 8;
+	uint64_t mcnt[NM] = {}, mbyt[NM] = {};
+	/* LDS: the hot counter slots, then the cold-slot cache (as k_classify_x4:
+	 * cc_n packed counts, cc_n tags = slot + 1): each touched cold slot costs
+	 * one pair of memory-side atomics per workgroup instead of one per hit */
 	uint64_t *ccv = lctr + s.hot_slots;
 	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + cc_n);
 	const uint32_t ccm = cc_n - 1u;
@@ -5999,74 +5825,117 @@ __global__ __launch_bounds__(NT) void k_ct_out(cgpu_snapshot s, ct_args a, uint3
 		cck[k] = 0;
 	}
 	__syncthreads();
-	/* metrics {reason 0 / 133 / 137 / 155 / 158} x {ingress, egress} */
-	uint64_t mcnt[10] = {}, mbyt[10] = {};
+	/* Q packets per lane (packet g + u * threads): the CT_REPLY / CT_RELATED
+	 * packets' policy cascades run stage-interleaved (policy_q) */
 	const uint64_t T = (uint64_t)gridDim.x * NT;
-	for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += T) {
-		const uint2 r = ld_x2<true>(a.res + i);
-		const uint32_t fl = ntl(a.flags + i), len = ntl(a.len + i);
-		const uint32_t cr = ct_res_ret(r.x);
-		int32_t v;
-		uint32_t id, st;
-		if (cr == CTR_NONE) {
-			v = ct_res_verdict(r.x);
-			id = r.y;
-			st = (r.x >> 25) & 7u;
-		} else {
-			const uint4 D = ld_x4<true>(a.dec + i);
-			const decision d = ct_dec_of(D, (cr & 3u) >= CT_REPLY);
-			v = ct_verdict(d, cr, fl & 1u);
-			id = d.id;
-			st = d.st;
-			if (d.ctr >= 0) {
-				const uint32_t c = (uint32_t)d.ctr;
-				bool done = false;
-				if (len < PK_MAX_LEN) {
-					if (c < s.hot_slots) {
-						atomicAdd((unsigned long long *)&lctr[c], (1ull << PK_SHIFT) | (unsigned long long)len);
-						done = true;
-					} else if (cc_n) {
-						uint32_t j = (c * 0x9E3779B1u) >> 16;
+	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < a.n; g += T * Q) {
+		ct_pkt q[Q];
+		uint32_t c[Q], ep[Q], dp[Q], pr[Q];
+		bool act[Q], rep[Q], eg[Q], frag[Q];
+		decision d[Q];
 #pragma unroll
-						for (int p = 0; p < CC_PROBE && !done; p++, j++) {
-							j &= ccm;
-							uint32_t t = cck[j];
-							if (t == 0u) {
-								const uint32_t o = atomicCAS(&cck[j], 0u, c + 1u);
-								t = o == 0u ? c + 1u : o;
-							}
-							if (t == c + 1u) {
-								atomicAdd((unsigned long long *)&ccv[j],
-									  (1ull << PK_SHIFT) | (unsigned long long)len);
-								done = true;
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = i < a.n;
+			const uint64_t j = act[u] ? i : 0u;
+			/* batch order: records and the walker's results stream in */
+			q[u] = ct_rec<K>::load(a.rec, (uint32_t)j, true).pkt();
+			c[u] = ntl(a.ct_ret + j) & ~(CT_ADDRP | CT_RELP);
+			ep[u] = ntl(a.ep + j);
+			eg[u] = q[u].meta & CTM_EGRESS;
+			frag[u] = q[u].meta & CTM_FRAG;
+			rep[u] = act[u] && !(q[u].meta & CTM_GATED) && (c[u] & 3u) >= CT_REPLY;
+			dp[u] = q[u].dport;
+			pr[u] = q[u].proto;
+			/* the reply tuple keeps the packet's addresses and direction, so
+			 * its identity is the one the prep resolved (decide<>'s identity
+			 * depends on neither port nor protocol) */
+			d[u].id = rep[u] ? ntl(a.identity + j) : 0u;
+		}
+		policy_q<Q>(s, rep, eg, frag, dp, pr, ep, d);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (!act[u])
+				continue;
+			const uint64_t i = g + (uint64_t)u * T;
+			const uint32_t meta = q[u].meta;
+			const bool egress = eg[u];
+			const uint32_t len = q[u].len;
+			int32_t v;
+			uint32_t st = 4, cr = 255u;
+			if (meta & CTM_GATED) {
+				v = DROP_CT_UNKNOWN_PROTO; /* ct_lookup default case */
+				if (K::SVC && (meta & CTM_SVCDROP)) {
+					v = DROP_NO_SERVICE; /* lb4_local failed closed (lb.h:715-744) */
+					st = 6;
+				}
+			} else {
+				cr = c[u] & 3u;
+				int ctr;
+				if (cr >= CT_REPLY) {
+					ctr = d[u].ctr;
+					st = d[u].st;
+					v = (egress && d[u].v > 0) ? d[u].v : 0;
+				} else {
+					ctr = (int)(q[u].cst & 0xFFFFFFu) - 1;
+					st = q[u].cst >> 24;
+					if (!(meta & CTM_ALLOWED))
+						v = DROP_POLICY;
+					else if (c[u] & CT_FAIL)
+						v = DROP_CT_CREATE_FAILED;
+					else
+						v = (int32_t)q[u].port;
+				}
+				if (ctr >= 0) {
+					const uint32_t cs = (uint32_t)ctr;
+					bool done = false;
+					if (len < PK_MAX_LEN) {
+						if (cs < s.hot_slots) {
+							atomicAdd((unsigned long long *)&lctr[cs],
+								  (1ull << PK_SHIFT) | (unsigned long long)len);
+							done = true;
+						} else if (cc_n) {
+							uint32_t j = (cs * 0x9E3779B1u) >> 16;
+#pragma unroll
+							for (int p = 0; p < CC_PROBE && !done; p++, j++) {
+								j &= ccm;
+								uint32_t t = cck[j];
+								if (t == 0u) {
+									const uint32_t o = atomicCAS(&cck[j], 0u, cs + 1u);
+									t = o == 0u ? cs + 1u : o;
+								}
+								if (t == cs + 1u) {
+									atomicAdd((unsigned long long *)&ccv[j],
+										  (1ull << PK_SHIFT) | (unsigned long long)len);
+									done = true;
+								}
 							}
 						}
 					}
-				}
-				if (!done) {
-					atomicAdd((unsigned long long *)&a.delta[2u * c], 1ull);
-					atomicAdd((unsigned long long *)&a.delta[2u * c + 1u], (unsigned long long)len);
+					if (!done) {
+						atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
+						atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u], (unsigned long long)len);
+					}
 				}
 			}
-		}
-		a.verdict[i] = v;
-		a.ct_ret[i] = (uint8_t)(cr == CTR_NONE ? 255u : cr & 3u);
-		a.identity[i] = id;
-		if (a.stage)
-			a.stage[i] = (uint8_t)st;
-		const uint32_t rr = v > 0 ? 5u : v == 0 ? 0u : v == DROP_POLICY ? 1u : v == DROP_CT_UNKNOWN_PROTO ? 2u
-				 : v == DROP_NO_SERVICE ? 4u : 3u;
-		const uint32_t idx = rr * 2u + (fl & 1u);
+			a.verdict[i] = v;
+			a.ct_ret[i] = (uint8_t)cr;
+			if (a.stage)
+				a.stage[i] = (uint8_t)st;
+			/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
+			const uint32_t r = v > 0 ? 5u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_CT_UNKNOWN_PROTO ? 2u : (v == DROP_NO_SERVICE ? 4u : 3u)));
+			const uint32_t idx = r * 2u + (egress ? 1u : 0u);
 #pragma unroll
-		for (int k = 0; k < 10; k++) {
-			mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
-			mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
+			for (int k = 0; k < NM; k++) {
+				mcnt[k] += (idx == (uint32_t)k) ? 1u : 0u;
+				mbyt[k] += (idx == (uint32_t)k) ? len : 0u;
+			}
 		}
 	}
 	uint64_t *met = a.delta + 2ull * s.n_ctr_slots;
 	const uint32_t reasons[5] = {0u, 133u, 137u, 155u, 158u};
 #pragma unroll
-	for (int k = 0; k < 10; k++) {
+	for (int k = 0; k < NM; k++) {
 		const uint64_t cn = wave_sum(mcnt[k]);
 		const uint64_t by = wave_sum(mbyt[k]);
 		if ((threadIdx.x & 63) == 0 && cn) {
@@ -6076,21 +5945,19 @@ __global__ __launch_bounds__(NT) void k_ct_out(cgpu_snapshot s, ct_args a, uint3
 		}
 	}
 	__syncthreads();
-	/* the workgroup's slots: one atomic pair per touched slot */
-	for (uint32_t k = threadIdx.x; k < s.hot_slots + cc_n; k += NT) {
-		uint32_t c;
-		uint64_t x;
-		if (k < s.hot_slots) {
-			c = k;
-			x = lctr[k];
-		} else {
-			const uint32_t t = cck[k - s.hot_slots];
-			x = t ? ccv[k - s.hot_slots] : 0u;
-			c = t - 1u;
-		}
+	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
+		const uint64_t x = lctr[k];
 		if (x) {
-			atomicAdd((unsigned long long *)&a.delta[2u * c], (unsigned long long)(x >> PK_SHIFT));
-			atomicAdd((unsigned long long *)&a.delta[2u * c + 1u], (unsigned long long)(x & PK_BYTES_MASK));
+			atomicAdd((unsigned long long *)&a.delta[2u * k], x >> PK_SHIFT);
+			atomicAdd((unsigned long long *)&a.delta[2u * k + 1u], x & PK_BYTES_MASK);
+		}
+	}
+	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
+		const uint32_t t = cck[k];
+		const uint64_t x = ccv[k];
+		if (t && x) {
+			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u)], x >> PK_SHIFT);
+			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u) + 1u], x & PK_BYTES_MASK);
 		}
 	}
 }
@@ -6109,7 +5976,6 @@ static int ct_sort_bits(const cgpu_snapshot &s)
  * a counting iterator took 0.77 ms per 64M flags and 1.43 ms per 128M
  * (profiles/r3_ct). */
 #define SEL_T 16u            /* flags per thread: one 16-byte load */
-#define LH_B 256u            /* head ranges of the longest-first ordering (k_ct_lhist) */
 #define SEL_B (256u * SEL_T) /* flags per block */
 
 __device__ __forceinline__ uint32_t sel_bits(const uint8_t *f, uint64_t n, uint64_t i0)
@@ -6219,8 +6085,7 @@ size_t ct_temp_bytes(uint64_t n)
 	size_t a = 0;
 	(void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
 						 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
-	/* ... and the range counts of the longest-first ordering (k_ct_lhist) */
-	return std::max<size_t>(std::max<size_t>(a, sel_blocks(4 * n) * 4u + 4u), (size_t)LH_B * 32u * 4u);
+	return std::max<size_t>(a, sel_blocks(4 * n) * 4u + 4u);
 }
 
 static ct_args ct_args_of(const ct_launch &L)
@@ -6236,125 +6101,13 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.xdaddr = static_cast<uint32_t *>(L.xdaddr);
 	a.xdport = L.xdport;
 	a.f2 = L.flags2;
-	a.res = L.res;
-	a.dec = L.dec;
 	return a;
 }
 
-/* Groups longest first, ordered on the device (the group count stays in
- * device memory: no host round trip between the sort and the walk).  A
- * group's bucket is the highest set bit of its length; the buckets are laid
- * out longest first, so the elephants start in the walker's first round.
- * LH_B workgroups each own a contiguous range of the group heads: count the
- * range's buckets (k_ct_lhist), one workgroup turns the LH_B x 32 counts
- * into offsets (k_ct_lscan), and each range places its groups in head order
- * inside every bucket (k_ct_lplace: ranks from wave ballots, so the layout
- * is deterministic). */
-__device__ __forceinline__ void lh_range(uint32_t nh, uint32_t b, uint32_t &lo, uint32_t &hi)
-{
-	lo = (uint32_t)((uint64_t)nh * b / LH_B);
-	hi = (uint32_t)((uint64_t)nh * (b + 1u) / LH_B);
-}
-
-__device__ __forceinline__ uint32_t lh_len(const uint32_t *heads, uint32_t k, uint32_t nh, uint64_t n)
-{
-	return (uint32_t)((k + 1u < nh ? (uint64_t)heads[k + 1u] : n) - heads[k]);
-}
-
-__global__ __launch_bounds__(256) void k_ct_lhist(const uint32_t *heads, const uint32_t *n_heads, uint64_t n,
-						  uint32_t *bh)
-{
-	__shared__ uint32_t h[32];
-	if (threadIdx.x < 32)
-		h[threadIdx.x] = 0;
-	__syncthreads();
-	uint32_t lo, hi;
-	lh_range(*n_heads, blockIdx.x, lo, hi);
-	const uint32_t nh = *n_heads;
-	for (uint32_t k = lo + threadIdx.x; k < hi; k += 256u)
-		atomicAdd(&h[31 - __clz(lh_len(heads, k, nh, n))], 1u);
-	__syncthreads();
-	if (threadIdx.x < 32)
-		bh[blockIdx.x * 32u + threadIdx.x] = h[threadIdx.x];
-}
-
-/* one workgroup: bh[b][bucket] := where range b's groups of that bucket
- * start, buckets longest first, ranges in order inside a bucket */
-__global__ __launch_bounds__(256) void k_ct_lscan(uint32_t *bh)
-{
-	__shared__ uint32_t c[LH_B * 32u];
-	__shared__ uint32_t base[32];
-	for (uint32_t k = threadIdx.x; k < LH_B * 32u; k += 256u)
-		c[k] = bh[k];
-	__syncthreads();
-	if (threadIdx.x < 32) { /* per bucket: ranges' exclusive prefix, the total */
-		uint32_t run = 0;
-		for (uint32_t b = 0; b < LH_B; b++) {
-			const uint32_t x = c[b * 32u + threadIdx.x];
-			c[b * 32u + threadIdx.x] = run;
-			run += x;
-		}
-		base[threadIdx.x] = run;
-	}
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		uint32_t o = 0;
-		for (int k = 31; k >= 0; k--) {
-			const uint32_t t = base[k];
-			base[k] = o;
-			o += t;
-		}
-	}
-	__syncthreads();
-	for (uint32_t k = threadIdx.x; k < LH_B * 32u; k += 256u)
-		bh[k] = c[k] + base[k & 31u];
-}
-
-__global__ __launch_bounds__(256) void k_ct_lplace(const uint32_t *heads, const uint32_t *n_heads, uint64_t n,
-						   const uint32_t *bh, uint32_t *glen, uint32_t *gpos)
-{
-	__shared__ uint32_t off[32];
-	__shared__ uint32_t wc[4][32];
-	const uint32_t nh = *n_heads, lane = __lane_id(), wv = threadIdx.x >> 6;
-	uint32_t lo, hi;
-	lh_range(nh, blockIdx.x, lo, hi);
-	if (threadIdx.x < 32)
-		off[threadIdx.x] = bh[blockIdx.x * 32u + threadIdx.x];
-	__syncthreads();
-	for (uint32_t t0 = lo; t0 < hi; t0 += 256u) {
-		const uint32_t k = t0 + threadIdx.x;
-		const bool act = k < hi;
-		const uint32_t len = act ? lh_len(heads, k, nh, n) : 1u;
-		const uint32_t bk = act ? 31u - (uint32_t)__clz(len) : 32u;
-		uint32_t rank = 0;
-		const uint64_t below = (1ull << lane) - 1ull;
-		for (uint32_t b = 0; b < 32u; b++) {
-			const uint64_t m = __ballot(bk == b);
-			if (bk == b)
-				rank = (uint32_t)__popcll(m & below);
-			if (lane == 0)
-				wc[wv][b] = (uint32_t)__popcll(m);
-		}
-		__syncthreads();
-		if (act) {
-			uint32_t at = off[bk] + rank;
-			for (uint32_t w = 0; w < wv; w++)
-				at += wc[w][bk];
-			glen[at] = len;
-			gpos[at] = heads[k];
-		}
-		__syncthreads();
-		if (threadIdx.x < 32)
-			off[threadIdx.x] += wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] + wc[3][threadIdx.x];
-		__syncthreads();
-	}
-}
-
 /* (gkey, idx)[0, m) -> groups in batch order, longest first: a.idx_sorted
- * the permutation, a.gpos / a.glen per group, *L.n_heads (device) the group
- * count */
+ * the permutation, a.gpos / a.glen per group; *nh (host) the group count */
 static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_args &a, uint64_t m,
-				hipStream_t st)
+				uint32_t *nh, hipStream_t st)
 {
 	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m + 255) / 256, 8192));
 	size_t tb = L.temp_bytes;
@@ -6370,16 +6123,22 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 	e = ct_select(L.head, m, L.heads, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 	if (e != hipSuccess)
 		return e;
-	/* gkey / idx are free again: (length, start) of the groups, longest
-	 * first; temp holds the range counts */
-	uint32_t *bh = static_cast<uint32_t *>(L.temp);
-	hipLaunchKernelGGL(k_ct_lhist, dim3(LH_B), dim3(256), 0, st, L.heads, L.n_heads, (uint64_t)m, bh);
-	hipLaunchKernelGGL(k_ct_lscan, dim3(1), dim3(256), 0, st, bh);
-	hipLaunchKernelGGL(k_ct_lplace, dim3(LH_B), dim3(256), 0, st, L.heads, L.n_heads, (uint64_t)m,
-			   (const uint32_t *)bh, L.gkey, L.idx);
-	a.glen = L.gkey;
+	/* groups longest first: gkey / idx are free again and hold (length,
+	 * start) before the sort, gkey_sorted / idx the sorted pairs after */
+	*nh = 0;
+	e = hipMemcpyAsync(nh, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+		return e;
+	const unsigned gh = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((*nh + 255) / 256, 8192));
+	hipLaunchKernelGGL(k_ct_lens, dim3(gh), dim3(256), 0, st, L.heads, *nh, m, L.gkey, L.heads_pos);
+	tb = L.temp_bytes;
+	e = hipcub::DeviceRadixSort::SortPairsDescending(L.temp, tb, L.gkey, L.gkey_sorted, L.heads_pos,
+							 L.idx, (int)*nh, 0, 32, st);
+	if (e != hipSuccess)
+		return e;
+	a.glen = L.gkey_sorted;
 	a.gpos = L.idx;
-	return hipGetLastError();
+	return hipSuccess;
 }
 
 /* packets per lane of the conntrack prep / finish passes (timing-only tool
@@ -6391,31 +6150,21 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 /* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
 #define CT_WALK_GRID 2048
 
-template <class K> static void launch_ct_decide(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
+template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
-	constexpr int Q = K::V6 ? 2 : CGPU_CT_Q; /* v6: the trie walk's registers */
-	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + 256 * Q - 1) / (256 * Q), 8192));
-	hipLaunchKernelGGL((k_ct_decide<K, Q>), dim3(g), dim3(256), ct_decide_lds(s, K::V6 != 0), st, s, a);
-}
-
-/* k_ct_out: 1024-thread workgroups, one per CU (LDS: hot counter slots and
- * the cold-slot cache), at most 2^22 packets per workgroup (the LDS packing,
- * PK_SHIFT) */
-static void launch_ct_out(const cgpu_snapshot &s0, const ct_args &a, hipStream_t st)
-{
-	constexpr int NT = 1024;
-	const cgpu_snapshot s = with_lds_hot(s0, X4_LDS_BUDGET / 16u);
-	size_t lds = (size_t)s.hot_slots * 8u;
+	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
+	constexpr int NF = 1024, Q = CGPU_CT_Q;
+	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF * Q - 1) / (NF * Q), 512), (a.n >> 22) + 1);
+	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
+	/* the cold-slot cache in the LDS the hot slots leave */
+	const size_t hot = (size_t)sf.hot_slots * 8u;
 	uint32_t cc_n = 0;
 	if (!(s.schedule & CGPU_SCHED_NO_CCACHE))
-		for (uint32_t n = 1u << 14; n >= 512u && !cc_n; n >>= 1)
-			if (lds + (size_t)n * 12u <= X4_LDS_BUDGET)
-				cc_n = n;
-	lds += (size_t)cc_n * 12u;
-	const uint64_t per_wg = 1ull << 22;
-	const uint64_t want = std::max<uint64_t>(256u, (a.n + per_wg - 1) / per_wg);
-	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + NT - 1) / NT, want));
-	hipLaunchKernelGGL((k_ct_out<NT>), dim3(g), dim3(NT), lds, st, s, a, cc_n);
+		for (uint32_t c = 1u << 14; c >= 512u && !cc_n; c >>= 1)
+			if (hot + (size_t)c * 12u <= X4_LDS_BUDGET)
+				cc_n = c;
+	hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), hot + (size_t)cc_n * 12u, st, sf,
+			   a, cc_n);
 }
 
 /* phase 2 of the plain paths (and of the IPv6 service path): the ICMP
@@ -6428,9 +6177,7 @@ static hipError_t ct_phase2(const cgpu_snapshot &s, const ct_table &T, const ct_
 	hipError_t e = ct_select(L.flags2, 2 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 	if (e != hipSuccess)
 		return e;
-	/* the candidate count sizes the radix sort: the one host read of the
-	 * plain path */
-	uint32_t m = 0;
+	uint32_t m = 0, nh = 0;
 	e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
 		return e;
@@ -6438,7 +6185,7 @@ static hipError_t ct_phase2(const cgpu_snapshot &s, const ct_table &T, const ct_
 		return hipSuccess;
 	const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_ct_owed_keys<K>, dim3(gm), dim3(256), 0, st, a, m, 0u);
-	e = ct_group_sort(s, L, a, m, st);
+	e = ct_group_sort(s, L, a, m, &nh, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
@@ -6449,22 +6196,37 @@ template <class K>
 static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
 {
 	ct_args a = ct_args_of(L);
-	constexpr int Q = CGPU_CT_Q;
-	const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
-	if (K::V6)
-		hipLaunchKernelGGL((k_ct_prep6_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
-	else
-		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), CGPU_CT_FUSED_DECIDE ? s.ipc4c.n_dict * 4u : 0u, st,
-				   s, a);
-	if (K::V6 || !CGPU_CT_FUSED_DECIDE) /* the IPv4 prep decides itself */
-		launch_ct_decide<K>(s, a, st);
-	hipError_t e = ct_group_sort(s, L, a, L.n, st);
+	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
+	if (K::V6) {
+		/* the ipcache lookups through the trie pre-pass (its entries into
+		 * idx_sorted, free until the group sort) when it can fold the
+		 * egress fallback identity */
+		if (s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK) {
+			constexpr int NT = 1024, QP = CGPU_DIAG_IPC6_PRE_Q, Q = 4;
+			const size_t lds = (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u;
+			const unsigned res = resident_blocks((const void *)k_ipc6_pre<QP, NT>, NT, lds);
+			const unsigned gp = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + QP * NT - 1) / (QP * NT), res));
+			hipLaunchKernelGGL((k_ipc6_pre<QP, NT>), dim3(gp), dim3(NT), lds, st, s,
+					   static_cast<const uint4 *>(L.saddr), static_cast<const uint4 *>(L.daddr), L.flags,
+					   L.idx_sorted, L.n);
+			const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+			hipLaunchKernelGGL((k_ct_prep6_q<Q>), dim3(gq), dim3(256), 0, st, s, a, L.idx_sorted);
+		} else {
+			hipLaunchKernelGGL(k_ct_prep6<false>, dim3(g), dim3(256), 0, st, s, a);
+		}
+	} else {
+		constexpr int Q = CGPU_CT_Q;
+		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
+	}
+	uint32_t nh;
+	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<K>(s, T, L, a, st)) != hipSuccess)
 		return e;
-	launch_ct_out(s, a, st);
+	launch_ct_finish<K>(s, a, st);
 	return hipGetLastError();
 }
 
@@ -6490,19 +6252,19 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	ct_args a = ct_args_of(L);
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_svc_prep6, dim3(g), dim3(256), 0, st, s, a);
-	hipError_t e = ct_group_sort(s, L, a, L.n, st);
+	uint32_t nh;
+	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK6, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
-	launch_ct_decide<CtK6S>(s, a, st);
-	e = ct_group_sort(s, L, a, L.n, st);
+	e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK6S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<CtK6S>(s, T, L, a, st)) != hipSuccess)
 		return e;
-	launch_ct_out(s, a, st);
+	launch_ct_finish<CtK6S>(s, a, st);
 	return hipGetLastError();
 }
 
@@ -6532,7 +6294,8 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	ct_args a = ct_args_of(L);
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_svc_prep, dim3(g), dim3(256), 0, st, s, a);
-	hipError_t e = ct_group_sort(s, L, a, L.n, st);
+	uint32_t nh;
+	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK4, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
@@ -6547,8 +6310,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	const bool serial = ctl[0] != 0;
 	if (serial)
 		hipLaunchKernelGGL((k_ct_prep<true, true>), dim3(g), dim3(256), 0, st, s, a);
-	launch_ct_decide<CtK4S>(s, a, st);
-	e = ct_group_sort(s, L, a, L.n, st);
+	e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
@@ -6568,13 +6330,13 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 				continue;
 			const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
 			hipLaunchKernelGGL(k_ct_owed_keys<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, 0u);
-			e = ct_group_sort(s, L, a, m, st);
+			e = ct_group_sort(s, L, a, m, &nh, st);
 			if (e != hipSuccess)
 				return e;
 			hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 		}
 	}
-	launch_ct_out(s, a, st);
+	launch_ct_finish<CtK4S>(s, a, st);
 	return hipGetLastError();
 }
 

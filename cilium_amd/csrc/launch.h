@@ -147,6 +147,7 @@ struct ct_launch {
 	uint32_t *gkey, *gkey_sorted, *idx, *idx_sorted;
 	uint8_t *head;
 	uint32_t *heads, *n_heads;
+	uint32_t *heads_pos; /* [n] scratch for the longest-first group sort */
 	void *temp;
 	size_t temp_bytes;
 	/* the stateful service step (cgpu_classify_v4_ctlb); rec is [3n] */
@@ -156,8 +157,6 @@ struct ct_launch {
 	uint8_t *flags2;      /* [2n] plain path, [4n] service path: phase-2 candidates */
 	void *xdaddr;         /* [n] optional (IPv6: 16 bytes each) */
 	uint16_t *xdport;     /* [n] optional */
-	uint2 *res;           /* [n] packed per-packet outcome (kernels.hip ct_res) */
-	uint4 *dec;           /* [n] both tuples' policy decisions (kernels.hip k_ct_decide) */
 };
 
 size_t ct_temp_bytes(uint64_t n);
