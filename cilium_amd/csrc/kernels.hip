@@ -980,14 +980,27 @@ __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, 
 /* The policy cascade of decide<> (probe 1 {id, dport, proto, dir} unless a
  * fragment, probe 2 {id, any port, dir}, probe 3 {any identity, dport,
  * proto, dir} unless a fragment) for Q tuples whose identity d[u].id is
- * set, each probe's Q gathers issued together. */
-template <int Q>
+ * set, each stage's Q gathers issued together, through the group table as
+ * k_classify_x4 (tables.h pol_groups): one gather of the {identity,
+ * endpoint, direction} group slot gives probe 2 (its L3 key) and a bloom
+ * over the group's (dport, proto) that admits probe 1 only where an exact
+ * key can exist; probe 3 gathers directly.  Same results as the three
+ * probes in order (GROUP false: the probes themselves, for kernels at their
+ * register limit - the group slots' registers spill k_ct_finish, 2.18 ->
+ * 2.36 ms, profiles/r4_i/; CGPU_POLICY_Q_PROBES: every caller, A/B). */
+#ifndef CGPU_POLICY_Q_PROBES
+#define CGPU_POLICY_Q_PROBES 0
+#endif
+template <int Q, bool GROUP = true>
 __device__ __forceinline__ void policy_q(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&eg)[Q],
 					 const bool (&frag)[Q], const uint32_t (&dport)[Q], const uint32_t (&proto)[Q],
 					 const uint32_t (&ep)[Q], decision (&d)[Q])
 {
-	uint32_t hi4[Q], egw[Q], z[Q];
+	uint32_t hi4[Q], egw[Q], z[Q], b[Q];
 	int ctr[Q];
+	uint4 sl[Q];
+	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
+	const uint32_t pm = s.pol.bucket_mask;
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		egw[u] = eg[u] ? (1u << 24) : 0u;
@@ -996,38 +1009,78 @@ __device__ __forceinline__ void policy_q(const cgpu_snapshot &s, const bool (&ac
 		ctr[u] = -1;
 		d[u].st = 0;
 	}
-	/* probe 1: {id, dport, proto, dir} (not for fragments) */
-	uint32_t b[Q];
-	uint4 sl[Q];
+	if (CGPU_POLICY_Q_PROBES || !GROUP) {
+		/* probe 1: {id, dport, proto, dir} (not for fragments) */
 #pragma unroll
-	for (int u = 0; u < Q; u++) {
-		b[u] = pol_hash(d[u].id, hi4[u], ep[u]) & s.pol.bucket_mask;
-		sl[u] = (act[u] && !frag[u]) ? reinterpret_cast<const uint4 *>(s.pol.slots)[b[u]] : make_uint4(0, 0, 0, 0);
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++)
-		if (act[u] && !frag[u]) {
-			ctr[u] = pol_resolve1(s.pol, sl[u], b[u], d[u].id, hi4[u], ep[u], &z[u]);
-			d[u].st = 1;
+		for (int u = 0; u < Q; u++) {
+			b[u] = pol_hash(d[u].id, hi4[u], ep[u]) & pm;
+			sl[u] = (act[u] && !frag[u]) ? ptab[b[u]] : make_uint4(0, 0, 0, 0);
 		}
-	/* probe 2: {id, any port, dir} */
 #pragma unroll
-	for (int u = 0; u < Q; u++) {
-		b[u] = pol_hash(d[u].id, egw[u], ep[u]) & s.pol.bucket_mask;
-		sl[u] = (act[u] && ctr[u] < 0) ? reinterpret_cast<const uint4 *>(s.pol.slots)[b[u]] : make_uint4(0, 0, 0, 0);
-	}
+		for (int u = 0; u < Q; u++)
+			if (act[u] && !frag[u]) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], b[u], d[u].id, hi4[u], ep[u], &z[u]);
+				d[u].st = 1;
+			}
+		/* probe 2: {id, any port, dir} */
 #pragma unroll
-	for (int u = 0; u < Q; u++)
-		if (act[u] && ctr[u] < 0) {
-			ctr[u] = pol_resolve1(s.pol, sl[u], b[u], d[u].id, egw[u], ep[u], &z[u]);
-			d[u].st = 2;
+		for (int u = 0; u < Q; u++) {
+			b[u] = pol_hash(d[u].id, egw[u], ep[u]) & pm;
+			sl[u] = (act[u] && ctr[u] < 0) ? ptab[b[u]] : make_uint4(0, 0, 0, 0);
 		}
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (act[u] && ctr[u] < 0) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], b[u], d[u].id, egw[u], ep[u], &z[u]);
+				d[u].st = 2;
+			}
+	} else {
+		/* the group slot: probe 2 and the bloom that gates probe 1 */
+		uint4 grp[Q];
+		bool need[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			grp[u] = make_uint4(0, 0, POL_CTR_EMPTY, 0);
+			b[u] = pg_hash(d[u].id, ep[u] | (eg[u] ? 1u << 16 : 0u)) & s.pg.mask;
+			if (act[u])
+				grp[u] = s.pg.slots[b[u]];
+		}
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			need[u] = false;
+			if (!act[u])
+				continue;
+			grp[u] = pg_resolve(s.pg, grp[u], b[u], d[u].id, ep[u] | (eg[u] ? 1u << 16 : 0u));
+			const uint32_t bl = pg_bloom(dport[u], proto[u]);
+			need[u] = !frag[u] && (grp[u].w & bl) == bl;
+		}
+		/* probe 1: {id, dport, proto, dir} (policy.h:61-72), if the bloom admits it */
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			b[u] = pol_hash(d[u].id, hi4[u], ep[u]) & pm;
+			sl[u] = need[u] ? ptab[b[u]] : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			if (need[u]) {
+				ctr[u] = pol_resolve1(s.pol, sl[u], b[u], d[u].id, hi4[u], ep[u], &z[u]);
+				d[u].st = 1;
+			}
+			/* probe 2: {id, any port, dir} (policy.h:74-83), the group's L3 key */
+			if (act[u] && ctr[u] < 0) {
+				d[u].st = 2;
+				if ((grp[u].z & POL_CTR_MASK) != POL_CTR_EMPTY) {
+					ctr[u] = (int)(grp[u].z & POL_CTR_MASK);
+					z[u] = 0;
+				}
+			}
+		}
+	}
 	/* probe 3: {any identity, dport, proto, dir} (not for fragments) */
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
-		b[u] = pol_hash(0u, hi4[u], ep[u]) & s.pol.bucket_mask;
-		sl[u] = (act[u] && ctr[u] < 0 && !frag[u]) ? reinterpret_cast<const uint4 *>(s.pol.slots)[b[u]]
-							   : make_uint4(0, 0, 0, 0);
+		b[u] = pol_hash(0u, hi4[u], ep[u]) & pm;
+		sl[u] = (act[u] && ctr[u] < 0 && !frag[u]) ? ptab[b[u]] : make_uint4(0, 0, 0, 0);
 	}
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
@@ -1099,125 +1152,6 @@ __device__ __forceinline__ void decide4_q(const cgpu_snapshot &s, const bool (&a
 {
 	ident4_q<Q>(s, s.ipc4c.dict, act, eg, sa, da, d);
 	policy_q<Q>(s, act, eg, frag, dport, proto, ep, d);
-}
-
-/* policy_q's cascade for the two dports one conntrack packet's policy step
- * can see (k_ct_decide: the forward tuple's, dpf, and the reply tuple's,
- * dpr, where act2), for Q tuples whose identity d[u].id is set, through the
- * group table as k_classify_x4 (tables.h pol_groups): one gather of the
- * {identity, endpoint, direction} group slot serves both - probe 2 is its
- * L3 key, and its bloom over the group's (dport, proto) admits probe 1 only
- * where an exact key can exist; probe 3 gathers directly.  Both tuples'
- * probes of a stage are in flight together.  Results as policy_q. */
-template <int Q>
-__device__ __forceinline__ void policy2_qg(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&act2)[Q],
-					   const bool (&eg)[Q], const bool (&frag)[Q], const uint32_t (&dpf)[Q],
-					   const uint32_t (&dpr)[Q], const uint32_t (&proto)[Q],
-					   const uint32_t (&ep)[Q], decision (&d)[Q], decision (&d2)[Q])
-{
-	const uint4 *ptab = reinterpret_cast<const uint4 *>(s.pol.slots);
-	const uint32_t pm = s.pol.bucket_mask;
-	uint4 grp[Q], sf[Q], sr[Q];
-	uint32_t bg[Q], hf[Q], hr[Q], zf[Q], zr[Q], bf[Q], br[Q];
-	int cf[Q], cr[Q];
-	bool n1f[Q], n1r[Q];
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		grp[u] = make_uint4(0, 0, POL_CTR_EMPTY, 0);
-		bg[u] = pg_hash(d[u].id, ep[u] | (eg[u] ? 1u << 16 : 0u)) & s.pg.mask;
-		if (act[u])
-			grp[u] = s.pg.slots[bg[u]];
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (act[u])
-			grp[u] = pg_resolve(s.pg, grp[u], bg[u], d[u].id, ep[u] | (eg[u] ? 1u << 16 : 0u));
-		const uint32_t egw = eg[u] ? (1u << 24) : 0u;
-		hf[u] = dpf[u] | (proto[u] << 16) | egw;
-		hr[u] = dpr[u] | (proto[u] << 16) | egw;
-		cf[u] = cr[u] = -1;
-		zf[u] = zr[u] = 0;
-		d[u].st = d2[u].st = 0;
-		const uint32_t blf = pg_bloom(dpf[u], proto[u]), blr = pg_bloom(dpr[u], proto[u]);
-		n1f[u] = act[u] && !frag[u] && (grp[u].w & blf) == blf;
-		n1r[u] = act2[u] && !frag[u] && (grp[u].w & blr) == blr;
-	}
-	/* probe 1: {id, dport, proto, dir} (policy.h:61-72) */
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (n1f[u]) {
-			bf[u] = pol_hash(d[u].id, hf[u], ep[u]) & pm;
-			sf[u] = ptab[bf[u]];
-		}
-		if (n1r[u]) {
-			br[u] = pol_hash(d[u].id, hr[u], ep[u]) & pm;
-			sr[u] = ptab[br[u]];
-		}
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (n1f[u]) {
-			cf[u] = pol_resolve1(s.pol, sf[u], bf[u], d[u].id, hf[u], ep[u], &zf[u]);
-			d[u].st = 1;
-		}
-		if (n1r[u]) {
-			cr[u] = pol_resolve1(s.pol, sr[u], br[u], d[u].id, hr[u], ep[u], &zr[u]);
-			d2[u].st = 1;
-		}
-		/* probe 2: {id, any port, dir} (policy.h:74-83), the group's */
-		const bool l3 = (grp[u].z & POL_CTR_MASK) != POL_CTR_EMPTY;
-		if (act[u] && cf[u] < 0) {
-			d[u].st = 2;
-			if (l3) {
-				cf[u] = (int)(grp[u].z & POL_CTR_MASK);
-				zf[u] = 0;
-			}
-		}
-		if (act2[u] && cr[u] < 0) {
-			d2[u].st = 2;
-			if (l3) {
-				cr[u] = (int)(grp[u].z & POL_CTR_MASK);
-				zr[u] = 0;
-			}
-		}
-	}
-	/* probe 3: {any identity, dport, proto, dir} (policy.h:85-96) */
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (act[u] && cf[u] < 0 && !frag[u]) {
-			bf[u] = pol_hash(0u, hf[u], ep[u]) & pm;
-			sf[u] = ptab[bf[u]];
-		}
-		if (act2[u] && cr[u] < 0 && !frag[u]) {
-			br[u] = pol_hash(0u, hr[u], ep[u]) & pm;
-			sr[u] = ptab[br[u]];
-		}
-	}
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (act[u] && cf[u] < 0 && !frag[u]) {
-			cf[u] = pol_resolve1(s.pol, sf[u], bf[u], 0u, hf[u], ep[u], &zf[u]);
-			d[u].st = 3;
-		}
-		if (act2[u] && cr[u] < 0 && !frag[u]) {
-			cr[u] = pol_resolve1(s.pol, sr[u], br[u], 0u, hr[u], ep[u], &zr[u]);
-			d2[u].st = 3;
-		}
-		if (cf[u] >= 0) {
-			d[u].v = d[u].st == 2 ? 0 : (int32_t)(zf[u] >> 16);
-		} else {
-			d[u].st = 0;
-			d[u].v = DROP_POLICY;
-		}
-		d[u].ctr = cf[u];
-		if (cr[u] >= 0) {
-			d2[u].v = d2[u].st == 2 ? 0 : (int32_t)(zr[u] >> 16);
-		} else {
-			d2[u].st = 0;
-			d2[u].v = DROP_POLICY;
-		}
-		d2[u].ctr = cr[u];
-	}
 }
 
 /* Packed per-workgroup counter: packets in bits 41..63, bytes in 0..40.
@@ -5852,7 +5786,7 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 			 * depends on neither port nor protocol) */
 			d[u].id = rep[u] ? ntl(a.identity + j) : 0u;
 		}
-		policy_q<Q>(s, rep, eg, frag, dp, pr, ep, d);
+		policy_q<Q, false>(s, rep, eg, frag, dp, pr, ep, d);
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			if (!act[u])

@@ -41,7 +41,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "ct_prefetch": ("CGPU_CT_PREFETCH",),
             "ctc3": ("CTC=3",), "ctc2": ("CTC=2",),
             "v6_no_h64": ("CGPU_DIAG_V6_NO_H64",), "v6_pre_w2": ("CGPU_IPC6_MINW=2",), "v6_pre_q1_w2": ("CGPU_IPC6_MINW=2", "CGPU_DIAG_IPC6_PRE_Q=1"),
-            "v6_pre_q4_w2": ("CGPU_IPC6_MINW=2", "CGPU_DIAG_IPC6_PRE_Q=4"), "ct_q2": ("CGPU_CT_Q=2",), "ct_q1": ("CGPU_CT_Q=1",)}
+            "v6_pre_q4_w2": ("CGPU_IPC6_MINW=2", "CGPU_DIAG_IPC6_PRE_Q=4"), "ct_q2": ("CGPU_CT_Q=2",), "ct_q1": ("CGPU_CT_Q=1",),
+            "policy_probes": ("CGPU_POLICY_Q_PROBES=1",)}
 
 
 def build(names):
