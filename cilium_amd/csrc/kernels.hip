@@ -5295,7 +5295,9 @@ struct ct_srec {
 
 
 /* lb4_extract_key + lb4_lookup_service (lb.h:590-635) for every egress
- * packet; service packets get their CT_SERVICE record */
+ * packet; service packets get their CT_SERVICE record, their group key (in
+ * gkey_sorted, batch order) and a set f2 flag: only they are compacted,
+ * sorted and walked (about a fifth of the bench's packets) */
 __global__ __launch_bounds__(256) void k_svc_prep(cgpu_snapshot s, ct_args a)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
@@ -5353,14 +5355,25 @@ __global__ __launch_bounds__(256) void k_svc_prep(cgpu_snapshot s, ct_args a)
 				out.x = SVC_DROP;
 			}
 		}
-		uint4 *r = a.rec + 3u * i;
-		r[0] = r0;
-		r[1] = r1;
-		r[2] = r2;
+		const bool walk = !((r0.w >> 16) & CTM_GATED);
+		if (walk) {
+			uint4 *r = a.rec + 3u * i;
+			r[0] = r0;
+			r[1] = r1;
+			r[2] = r2;
+			a.gkey_sorted[i] = ct_group(sa, da);
+		}
+		a.f2[i] = walk ? 1u : 0u;
 		a.svc_out[i] = out;
-		a.gkey[i] = (r0.w >> 16) & CTM_GATED ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : ct_group(sa, da);
-		a.idx[i] = (uint32_t)i;
 	}
+}
+
+/* dst[j] = src[idx[j]], j < m (the compacted service packets' group keys) */
+__global__ __launch_bounds__(256) void k_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t *dst,
+						    uint32_t m)
+{
+	for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u)
+		dst[j] = src[idx[j]];
 }
 
 /* One service packet of a group: lb4_local (lb.h:700-775) against the map.
@@ -5496,14 +5509,16 @@ __global__ __launch_bounds__(256) void k_svc_prep6(cgpu_snapshot s, ct_args a)
 				out.x = SVC_DROP;
 			}
 		}
-		r[0] = da;
-		r[1] = sa;
-		r[2] = r2;
-		r[3] = r3;
+		const bool walk = !((r2.y >> 16) & CTM_GATED);
+		if (walk) { /* as k_svc_prep: only service packets are walked */
+			r[0] = da;
+			r[1] = sa;
+			r[2] = r2;
+			r[3] = r3;
+			a.gkey_sorted[i] = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), f);
+		}
+		a.f2[i] = walk ? 1u : 0u;
 		a.svc_out[2u * i] = out;
-		a.gkey[i] = (r2.y >> 16) & CTM_GATED ? ct_fmix((uint32_t)i ^ 0x5bd1e995u)
-						      : ct_group(fold6(sa.x, sa.y, sa.z, sa.w), f);
-		a.idx[i] = (uint32_t)i;
 	}
 }
 
@@ -6176,6 +6191,32 @@ hipError_t launch_classify_v6_ct(const cgpu_snapshot &s, const ct_table &T, cons
 	return launch_ct<CtK6>(s, T, L, st);
 }
 
+/* the service walk over the packets k_svc_prep{,6} flagged: compacted (the
+ * count sizes the radix sort: a host read), their keys gathered, grouped,
+ * walked */
+template <class K>
+static hipError_t ct_svc_walk(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, ct_args &a,
+			      hipStream_t st)
+{
+	hipError_t e = ct_select(L.flags2, L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
+	if (e != hipSuccess)
+		return e;
+	uint32_t m = 0;
+	e = hipMemcpyAsync(&m, L.n_heads, 4, hipMemcpyDeviceToHost, st);
+	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
+		return e;
+	if (!m)
+		return hipSuccess;
+	const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
+	hipLaunchKernelGGL(k_gather_u32, dim3(gm), dim3(256), 0, st, (const uint32_t *)L.gkey_sorted,
+			   (const uint32_t *)L.idx, L.gkey, m);
+	uint32_t nh;
+	if ((e = ct_group_sort(s, L, a, m, &nh, st)) != hipSuccess)
+		return e;
+	hipLaunchKernelGGL((k_ct_walk<K, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
+	return hipGetLastError();
+}
+
 /* cgpu_classify_v6_ctlb: the IPv6 service walk (k_svc_prep6, WALK_SVC over
  * CtK6), then the IPv6 conntrack path with the service's state: phase 1 by
  * connection, phase 2 the ICMPv6 errors and owed ICMPv6 entries by address
@@ -6187,10 +6228,9 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_svc_prep6, dim3(g), dim3(256), 0, st, s, a);
 	uint32_t nh;
-	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	hipError_t e = ct_svc_walk<CtK6>(s, T, L, a, st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL((k_ct_walk<CtK6, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
 	e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
@@ -6229,10 +6269,9 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	hipLaunchKernelGGL(k_svc_prep, dim3(g), dim3(256), 0, st, s, a);
 	uint32_t nh;
-	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st);
+	hipError_t e = ct_svc_walk<CtK4>(s, T, L, a, st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL((k_ct_walk<CtK4, WALK_SVC>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	e = hipMemsetAsync(a.ctl, 0, 16, st);
 	if (e != hipSuccess)
 		return e;
