@@ -3676,6 +3676,18 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_GATED 16u
 #define CTM_ALLOWED 32u
 #define CTM_FRAG 64u
+/* packets per lane of the conntrack prep / finish passes (timing-only tool
+ * builds vary it, tools/diag_ab.py) */
+#ifndef CGPU_CT_Q
+#define CGPU_CT_Q 4
+#endif
+/* the service paths' forward decisions: 0 inside the per-packet prep, 1 a
+ * k_ct_decq pass after it (Q packets per lane).  Measured slower (ctlb
+ * 25.19 -> 25.53 ms, ctlb6 24.13 -> 26.93: the v6 pass stages the trie
+ * levels in LDS per 256-thread workgroup, profiles/r4_o/): kept for A/B */
+#ifndef CGPU_CT_SVC_DECQ
+#define CGPU_CT_SVC_DECQ 0
+#endif
 /* the stateful service step (cgpu_classify_v4_ctlb) */
 #define CTM_PHASE2 128u   /* the packet's address pair may hold owed address entries: phase 2 */
 #define CTM_ADDRX 256u    /* its address entry lies in another pair: owed to phase 2 */
@@ -4340,18 +4352,20 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 			const bool frag = !egress && ((fl >> 1) & 1u);
 			if (frag)
 				meta |= CTM_FRAG;
-			const decision d = decide<0>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
-						    pr, ep);
-			if (d.v >= 0) {
-				meta |= CTM_ALLOWED;
-				port = (uint32_t)d.v;
-			}
-			id = d.id;
 			if (egress)
 				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
-			else
-				sec = d.id;
-			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+			if constexpr (!SVC || !CGPU_CT_SVC_DECQ) {
+				const decision d = decide<0>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
+							    pr, ep);
+				if (d.v >= 0) {
+					meta |= CTM_ALLOWED;
+					port = (uint32_t)d.v;
+				}
+				id = d.id;
+				if (!egress)
+					sec = d.id;
+				cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+			} /* SVC: k_ct_decq, Q packets per lane */
 		}
 		uint32_t g = ct_group(sa, da);
 		if constexpr (!SVC) {
@@ -4611,6 +4625,122 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 	}
 }
 
+/* The forward tuple's decision for the service paths' records (k_ct_prep /
+ * k_ct_prep6 with SVC leave it out of their per-packet lanes): Q packets per
+ * lane, packet i = g + u * (threads), every lookup stage's gathers in flight
+ * together (decide4_q; v6 the trie walk with its levels in LDS as
+ * k_ipc6_pre, then policy_q).  Patches the record as the per-packet prep
+ * writes it: CTM_ALLOWED, the proxy port, src_sec_id (ingress: the source
+ * identity), the counter slot | stage, and the identity column. */
+template <class K, int Q>
+__global__ __launch_bounds__(256) void k_ct_decq(cgpu_snapshot s, ct_args a)
+{
+	constexpr bool V6 = K::V6 != 0;
+	constexpr uint32_t RW = ct_rec<K>::RW;
+	extern __shared__ __attribute__((aligned(16))) uint32_t lt[];
+	uint32_t n24 = 0, nbl = 0;
+	uint32_t *lbl = lt;
+	if constexpr (V6) {
+		n24 = v6t_lds_b24(s.ipc6);
+		nbl = v6t_lds_bloom(s.ipc6);
+		lbl = lt + v6t_lds_words(s.ipc6);
+		if (s.ipc6.root) {
+			for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += 256u)
+				lt[k] = s.ipc6.rbits[k];
+			const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
+			for (uint32_t k = threadIdx.x; k < n24 * 128u; k += 256u)
+				lt[V6T_RBITS_WORDS + k] = b16[k];
+			for (uint32_t k = threadIdx.x; k < nbl; k += 256u)
+				lbl[k] = s.ipc6.bl64[k];
+		}
+	} else {
+		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += 256u)
+			lt[k] = s.ipc4c.dict[k];
+	}
+	__syncthreads();
+	const uint64_t T = (uint64_t)gridDim.x * 256u;
+	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+		bool act[Q], eg[Q], frag[Q];
+		uint32_t sa[Q], da[Q], dp[Q], pr[Q], ep[Q];
+		uint4 w6[Q], rm[Q], rd[Q];
+		decision d[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			const uint64_t j = i < a.n ? i : 0u;
+			const uint4 *r = a.rec + RW * j;
+			/* v4: r0 = {daddr, saddr, z, proto | meta}, r1 = {w | port, len,
+			 * sec, cst}; v6: r2 = {z, proto | meta, w | port, len}, r3 =
+			 * {sec, cst, rev_nat, svcw} */
+			rm[u] = V6 ? r[2] : r[0];
+			rd[u] = V6 ? r[3] : r[1];
+			const uint32_t meta = (V6 ? rm[u].y : rm[u].w) >> 16;
+			act[u] = i < a.n && !(meta & CTM_GATED);
+			eg[u] = meta & CTM_EGRESS;
+			frag[u] = meta & CTM_FRAG;
+			dp[u] = V6 ? rm[u].x >> 16 : rm[u].z >> 16;
+			pr[u] = (V6 ? rm[u].y : rm[u].w) & 0xFFu;
+			ep[u] = a.ep[j];
+			sa[u] = V6 ? 0u : rm[u].y;
+			da[u] = V6 ? 0u : rm[u].x;
+			w6[u] = make_uint4(0, 0, 0, 0);
+			if (V6)
+				w6[u] = v6_host_words(eg[u] ? r[0] : r[1]);
+		}
+		if constexpr (V6) {
+			/* decide<1>'s identity (bpf_lxc.c:170-187 / bpf_netdev.c:203-211) */
+			uint32_t e[Q];
+			v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w6, act, e, nbl ? lbl : nullptr);
+#pragma unroll
+			for (int u = 0; u < Q; u++) {
+				const uint32_t label = entry_label(s.ipc6.vals, e[u]);
+				const bool in_cluster = w6[u].x == bswap32(s.router_ip64[0]) &&
+							w6[u].y == bswap32(s.router_ip64[1]);
+				if (eg[u]) {
+					d[u].id = (e[u] && label) ? label : (in_cluster ? s.cluster_id : s.world_id);
+				} else {
+					uint32_t src = s.ingress_src_identity;
+					if (src < s.health_id && e[u] && label && label != s.cluster_id)
+						src = label;
+					d[u].id = src;
+				}
+			}
+		} else {
+			ident4_q<Q>(s, lt, act, eg, sa, da, d);
+		}
+		policy_q<Q>(s, act, eg, frag, dp, pr, ep, d);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			if (!act[u])
+				continue;
+			const uint32_t allowed = d[u].v >= 0 ? (CTM_ALLOWED << 16) : 0u;
+			const uint32_t port = d[u].v >= 0 ? (uint32_t)d[u].v << 16 : 0u;
+			const uint32_t cst = (uint32_t)(d[u].ctr + 1) | (d[u].st << 24);
+			uint4 *r = a.rec + RW * i;
+			if (V6) {
+				r[2] = make_uint4(rm[u].x, rm[u].y | allowed, rm[u].z | port, rm[u].w);
+				r[3] = make_uint4(eg[u] ? rd[u].x : d[u].id, cst, rd[u].z, rd[u].w);
+			} else {
+				r[0] = make_uint4(rm[u].x, rm[u].y, rm[u].z, rm[u].w | allowed);
+				r[1] = make_uint4(rd[u].x | port, rd[u].y, eg[u] ? rd[u].z : d[u].id, cst);
+			}
+			a.identity[i] = d[u].id;
+		}
+	}
+}
+
+template <class K> static void launch_ct_decq(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
+{
+	if (!CGPU_CT_SVC_DECQ)
+		return;
+	constexpr int Q = K::V6 ? 2 : CGPU_CT_Q;
+	const size_t lds = K::V6 ? (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u
+				 : (size_t)s.ipc4c.n_dict * 4u;
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + 256 * Q - 1) / (256 * Q), 8192));
+	hipLaunchKernelGGL((k_ct_decq<K, Q>), dim3(g), dim3(256), lds, st, s, a);
+}
+
 /* phase 2 of the service path, in two sub-phases: candidate 4i = packet i
  * if it runs in phase 2, 4i + 1 = packet i's owed address entry (kept
  * whatever phase 1 decided: the walk checks CT_ADDRP), 4i + 2 = the ICMP
@@ -4762,17 +4892,19 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 			w = 0; /* union tcp_flags stays zero (conntrack.h:294) */
 		uint32_t sec = 0, port = 0, cst = 0, id = 0;
 		if (!(meta & CTM_GATED)) {
-			const decision d = decide<1>(s, egress, false, 0u, 0u, sa, da, z >> 16, pr, ep);
-			if (d.v >= 0) {
-				meta |= CTM_ALLOWED;
-				port = (uint32_t)d.v;
-			}
-			id = d.id;
 			if (egress)
 				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
-			else
-				sec = d.id;
-			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+			if constexpr (!SVC || !CGPU_CT_SVC_DECQ) {
+				const decision d = decide<1>(s, egress, false, 0u, 0u, sa, da, z >> 16, pr, ep);
+				if (d.v >= 0) {
+					meta |= CTM_ALLOWED;
+					port = (uint32_t)d.v;
+				}
+				id = d.id;
+				if (!egress)
+					sec = d.id;
+				cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+			} /* SVC: k_ct_decq, Q packets per lane */
 		}
 		uint32_t g = ct_group(fold6(sa.x, sa.y, sa.z, sa.w), fold6(da.x, da.y, da.z, da.w));
 		{ /* phase 1 by connection, as k_ct_prep (ct_create6 writes no address
@@ -5581,6 +5713,13 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
  * service path: candidates c = packet << 1 | kind, kind 0 a packet whose
  * address pair may hold owed entries, kind 1 an owed address entry */
+/* workgroups per CU the service-path walker (CtK4S: ~280 registers) is
+ * compiled for: 2 spills a few registers to scratch and doubles its
+ * occupancy (profiles/r4_f/ab_ctlb_walker_occupancy.log) */
+#ifndef CGPU_WALK_MINB_SVC
+#define CGPU_WALK_MINB_SVC 2
+#endif
+
 #define WALK_PKT 0
 #define WALK_SVC 1
 #define WALK_OWED 2
@@ -5599,7 +5738,7 @@ extern "C" __attribute__((visibility("default"))) int cgpu_diag_walk_clock(unsig
 #endif
 
 template <class K, int MODE>
-__global__ __launch_bounds__(256) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
+__global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
 {
 #ifdef CGPU_DIAG_WALK_CLOCK
 	const unsigned long long dg_t0 = __builtin_amdgcn_s_memrealtime();
@@ -6090,11 +6229,6 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 	return hipSuccess;
 }
 
-/* packets per lane of the conntrack prep / finish passes (timing-only tool
- * builds vary it, tools/diag_ab.py) */
-#ifndef CGPU_CT_Q
-#define CGPU_CT_Q 4
-#endif
 
 /* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
 #define CT_WALK_GRID 2048
@@ -6232,6 +6366,7 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
+	launch_ct_decq<CtK6S>(s, a, st);
 	e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
 		return e;
@@ -6283,6 +6418,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	const bool serial = ctl[0] != 0;
 	if (serial)
 		hipLaunchKernelGGL((k_ct_prep<true, true>), dim3(g), dim3(256), 0, st, s, a);
+	launch_ct_decq<CtK4S>(s, a, st);
 	e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)
 		return e;

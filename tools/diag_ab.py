@@ -3,7 +3,7 @@ product library: these builds drop work and give wrong counters).
 
     python tools/diag_ab.py build            # in the dev container: tools/_diag/*.so
     python tools/diag_ab.py run [variants]   # on the GPU box
-    (CGPU_AB_CONFIG = gpu (config 2, default) / pf6 (config 3) / v6 / ct / ct6 / ctlb)
+    (CGPU_AB_CONFIG = gpu (config 2, default) / pf6 (config 3) / v6 / ct / ct6 / ctlb / ctlb6)
 
 Each variant is cilium_amd/csrc compiled with extra -D flags into
 tools/_diag/libcgpu_<name>.so; `run` loads each in turn into the Engine
@@ -42,7 +42,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "ctc3": ("CTC=3",), "ctc2": ("CTC=2",),
             "v6_no_h64": ("CGPU_DIAG_V6_NO_H64",), "v6_pre_w2": ("CGPU_IPC6_MINW=2",), "v6_pre_q1_w2": ("CGPU_IPC6_MINW=2", "CGPU_DIAG_IPC6_PRE_Q=1"),
             "v6_pre_q4_w2": ("CGPU_IPC6_MINW=2", "CGPU_DIAG_IPC6_PRE_Q=4"), "ct_q2": ("CGPU_CT_Q=2",), "ct_q1": ("CGPU_CT_Q=1",),
-            "policy_probes": ("CGPU_POLICY_Q_PROBES=1",)}
+            "policy_probes": ("CGPU_POLICY_Q_PROBES=1",), "walk_svc_minb1": ("CGPU_WALK_MINB_SVC=1",),
+            "svc_decq": ("CGPU_CT_SVC_DECQ=1",)}
 
 
 def build(names):
@@ -109,6 +110,34 @@ def _workload(conf):
             else:
                 e.ct4_flush()
                 e.classify_v4_ct(d, 1000, out=out)
+        return make, step, n
+    if conf == "ctlb6":
+        # bench.py --config ctlb6
+        import numpy as np
+        T = synth.make_tables6(**synth.CONFIGS["v6"])
+        S = synth.make_services6(T, 100_000)
+        n = synth.CONFIGS["v6"]["n_tuples"]
+        tup, _, seclabels, S = synth.make_ctlb6_workload(T, S, n // 32, mean_pkts=32, loop_frac=1e-4)
+        n = min(n, len(tup["saddr"]))
+        tup = {k: np.ascontiguousarray(v[:n]) for k, v in tup.items()}
+        ct_max = 1 << max(20, int(np.ceil(np.log2(4.5 * n / 32))))
+        d = synth.to_device(tup)
+        out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+               "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None,
+               "ct_ret": torch.empty(n, dtype=torch.uint8, device="cuda"),
+               "daddr": torch.empty((n, 16), dtype=torch.uint8, device="cuda"),
+               "dport": torch.empty(n, dtype=torch.int16, device="cuda")}
+
+        def make():
+            e = Engine(device=0, **T.engine_config(), lb_max_entries=len(S.keys), ct_max=ct_max)
+            synth.load_engine(e, T)
+            synth.load_lxc(e, seclabels)
+            synth.load_services6(e, S)
+            return e
+
+        def step(e):
+            e.ct6_flush()
+            e.classify_v6_ctlb(d, 1000, out=out)
         return make, step, n
     if conf == "ctlb":
         # bench.py --config ctlb: 64M packets behind the service step, every
