@@ -5719,6 +5719,10 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
 #ifndef CGPU_WALK_MINB_SVC
 #define CGPU_WALK_MINB_SVC 2
 #endif
+/* ... and the other walkers (1: the compiler's choice, A/B) */
+#ifndef CGPU_WALK_W
+#define CGPU_WALK_W 1
+#endif
 
 #define WALK_PKT 0
 #define WALK_SVC 1
@@ -5738,7 +5742,7 @@ extern "C" __attribute__((visibility("default"))) int cgpu_diag_walk_clock(unsig
 #endif
 
 template <class K, int MODE>
-__global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : 1) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
+__global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) void k_ct_walk(cgpu_snapshot s, ct_table T, ct_args a)
 {
 #ifdef CGPU_DIAG_WALK_CLOCK
 	const unsigned long long dg_t0 = __builtin_amdgcn_s_memrealtime();
