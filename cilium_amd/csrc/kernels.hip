@@ -3688,6 +3688,14 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #ifndef CGPU_CT_SVC_DECQ
 #define CGPU_CT_SVC_DECQ 0
 #endif
+/* ... IPv6 (k_ct_prep6's per-lane decide<1> walks the trie from global
+ * memory: 32 GB of HBM traffic per 64M packets, profiles/r4_prof/ctlb6):
+ * 1 = k_ct_decq on a resident grid of 1024-thread workgroups, the trie
+ * levels staged in LDS once per CU as k_ipc6_pre.  Measured slower too,
+ * 24.10 -> 24.75 ms (profiles/r4_s/): off */
+#ifndef CGPU_CT_SVC_DECQ6
+#define CGPU_CT_SVC_DECQ6 0
+#endif
 /* the stateful service step (cgpu_classify_v4_ctlb) */
 #define CTM_PHASE2 128u   /* the packet's address pair may hold owed address entries: phase 2 */
 #define CTM_ADDRX 256u    /* its address entry lies in another pair: owed to phase 2 */
@@ -4632,8 +4640,8 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
  * k_ipc6_pre, then policy_q).  Patches the record as the per-packet prep
  * writes it: CTM_ALLOWED, the proxy port, src_sec_id (ingress: the source
  * identity), the counter slot | stage, and the identity column. */
-template <class K, int Q>
-__global__ __launch_bounds__(256) void k_ct_decq(cgpu_snapshot s, ct_args a)
+template <class K, int Q, int NT>
+__global__ __launch_bounds__(NT) void k_ct_decq(cgpu_snapshot s, ct_args a)
 {
 	constexpr bool V6 = K::V6 != 0;
 	constexpr uint32_t RW = ct_rec<K>::RW;
@@ -4645,21 +4653,21 @@ __global__ __launch_bounds__(256) void k_ct_decq(cgpu_snapshot s, ct_args a)
 		nbl = v6t_lds_bloom(s.ipc6);
 		lbl = lt + v6t_lds_words(s.ipc6);
 		if (s.ipc6.root) {
-			for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += 256u)
+			for (uint32_t k = threadIdx.x; k < V6T_RBITS_WORDS; k += NT)
 				lt[k] = s.ipc6.rbits[k];
 			const uint32_t *b16 = reinterpret_cast<const uint32_t *>(s.ipc6.b24_16);
-			for (uint32_t k = threadIdx.x; k < n24 * 128u; k += 256u)
+			for (uint32_t k = threadIdx.x; k < n24 * 128u; k += NT)
 				lt[V6T_RBITS_WORDS + k] = b16[k];
-			for (uint32_t k = threadIdx.x; k < nbl; k += 256u)
+			for (uint32_t k = threadIdx.x; k < nbl; k += NT)
 				lbl[k] = s.ipc6.bl64[k];
 		}
 	} else {
-		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += 256u)
+		for (uint32_t k = threadIdx.x; k < s.ipc4c.n_dict; k += NT)
 			lt[k] = s.ipc4c.dict[k];
 	}
 	__syncthreads();
-	const uint64_t T = (uint64_t)gridDim.x * 256u;
-	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+	const uint64_t T = (uint64_t)gridDim.x * NT;
+	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < a.n; g += T * Q) {
 		bool act[Q], eg[Q], frag[Q];
 		uint32_t sa[Q], da[Q], dp[Q], pr[Q], ep[Q];
 		uint4 w6[Q], rm[Q], rd[Q];
@@ -4732,13 +4740,21 @@ __global__ __launch_bounds__(256) void k_ct_decq(cgpu_snapshot s, ct_args a)
 
 template <class K> static void launch_ct_decq(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
-	if (!CGPU_CT_SVC_DECQ)
+	if (!(K::V6 ? CGPU_CT_SVC_DECQ6 : CGPU_CT_SVC_DECQ))
 		return;
-	constexpr int Q = K::V6 ? 2 : CGPU_CT_Q;
-	const size_t lds = K::V6 ? (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u
-				 : (size_t)s.ipc4c.n_dict * 4u;
-	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + 256 * Q - 1) / (256 * Q), 8192));
-	hipLaunchKernelGGL((k_ct_decq<K, Q>), dim3(g), dim3(256), lds, st, s, a);
+	if constexpr (K::V6 != 0) {
+		/* as k_ipc6_pre: the staged levels once per CU */
+		constexpr int Q = 2, NT = 1024;
+		const size_t lds = (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u;
+		const unsigned res = resident_blocks((const void *)k_ct_decq<K, Q, NT>, NT, lds);
+		const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + Q * NT - 1) / (Q * NT), res));
+		hipLaunchKernelGGL((k_ct_decq<K, Q, NT>), dim3(g), dim3(NT), lds, st, s, a);
+	} else {
+		constexpr int Q = CGPU_CT_Q;
+		const size_t lds = (size_t)s.ipc4c.n_dict * 4u;
+		const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + 256 * Q - 1) / (256 * Q), 8192));
+		hipLaunchKernelGGL((k_ct_decq<K, Q, 256>), dim3(g), dim3(256), lds, st, s, a);
+	}
 }
 
 /* phase 2 of the service path, in two sub-phases: candidate 4i = packet i
@@ -4894,7 +4910,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 		if (!(meta & CTM_GATED)) {
 			if (egress)
 				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
-			if constexpr (!SVC || !CGPU_CT_SVC_DECQ) {
+			if constexpr (!SVC || !CGPU_CT_SVC_DECQ6) {
 				const decision d = decide<1>(s, egress, false, 0u, 0u, sa, da, z >> 16, pr, ep);
 				if (d.v >= 0) {
 					meta |= CTM_ALLOWED;
