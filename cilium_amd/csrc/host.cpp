@@ -5203,7 +5203,7 @@ CGPU_EXPORT int cgpu_ct6_flush(cgpu_ctx *c)
 /* scratch of one cgpu_classify_v{4,6}_ct launch over n packets */
 struct CtScratch {
 	size_t rec, gkey, gkey_sorted, idx, idx_sorted, heads, n_heads, heads_pos, head,
-		temp, temp_bytes, svc_out, ctl, flags2, total;
+		temp, temp_bytes, svc_out, ctl, flags2, pcls, total;
 };
 
 static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool v6)
@@ -5229,6 +5229,7 @@ static CtScratch ct_scratch_layout(uint64_t n, size_t rec_bytes, bool svc, bool 
 	if (svc) {
 		L.svc_out = take(n * (v6 ? 32 : 16));
 		L.ctl = take(16);
+		L.pcls = take(n);
 	}
 	return L;
 }
@@ -5294,6 +5295,7 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
 		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);
+		a.pcls = b + L.pcls;
 		HIP_OR_EIO(m.v6 ? launch_classify_v6_ctlb(s, T, a, cs) : launch_classify_v4_ctlb(s, T, a, cs));
 	} else {
 		HIP_OR_EIO(m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs));

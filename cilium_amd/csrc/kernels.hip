@@ -3676,6 +3676,11 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_GATED 16u
 #define CTM_ALLOWED 32u
 #define CTM_FRAG 64u
+/* ct_args.pcls: a service-path packet's phase-2 class */
+#define PCL_P2A 1u   /* runs in phase 2a (an ordinary pair) */
+#define PCL_P2B 2u   /* runs in phase 2b (a special pair) */
+#define PCL_ADDRX 4u /* owes an address entry to another pair */
+#define PCL_RELX 8u  /* a create may owe its ICMP entry */
 /* packets per lane of the conntrack prep / finish passes (timing-only tool
  * builds vary it, tools/diag_ab.py) */
 #ifndef CGPU_CT_Q
@@ -4147,6 +4152,7 @@ struct ct_args {
 	uint16_t *xdport;            /* [n] optional: frame dport after it */
 	uint32_t serial;             /* one group for the whole batch (see launch_ctlb) */
 	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
+	uint8_t *pcls;               /* [n] service path: phase-2 class, PCL_* (k_ct_prep) */
 };
 
 /* One packet's record, written by k_ct_prep{,6} and read by the walker and
@@ -4433,6 +4439,17 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 			r[2] = uint4{r2x, addr, saddr2, lbf};
 		a.gkey[i] = SERIAL ? 0u : (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
 		a.idx[i] = (uint32_t)i;
+		if constexpr (SVC && !SERIAL) {
+			/* what k_ct_owed_flags selects by, in one byte instead of the
+			 * record's first line */
+			const bool live = !(meta & CTM_GATED);
+			const uint32_t lo = s.ipv4_loopback;
+			const bool special = sa == da || !sa || !da || sa == lo || da == lo;
+			const bool p2 = live && (meta & CTM_PHASE2);
+			a.pcls[i] = (uint8_t)((p2 && !special ? PCL_P2A : 0u) | (p2 && special ? PCL_P2B : 0u) |
+					      (live && (meta & CTM_ADDRX) ? PCL_ADDRX : 0u) |
+					      (live && (meta & CTM_RELX) ? PCL_RELX : 0u));
+		}
 	}
 }
 
@@ -4767,21 +4784,19 @@ template <class K> static void launch_ct_decq(const cgpu_snapshot &s, const ct_a
  * owe into 2b, 2b runs after it; a 2b packet that owes runs the batch
  * serially.  The plain path's flags come from its prep and walk (ct_args.f2,
  * two per packet). */
-__global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint32_t *f4, uint32_t lo, uint32_t phase)
+__global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint32_t *f4, uint32_t phase)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
 	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint4 r0 = a.rec[3u * i];
-		const uint32_t meta = r0.w >> 16, da = r0.x, sa = r0.y;
-		const bool live = !(meta & CTM_GATED);
-		const bool special = sa == da || !sa || !da || sa == lo || da == lo;
-		const bool p2 = live && (meta & CTM_PHASE2);
+		/* the packet's class (k_ct_prep: phase-2 packet of an ordinary /
+		 * special pair, owes an address entry, owes its ICMP entry) */
+		const uint32_t c = a.pcls[i];
 		uint32_t f;
 		if (phase == 0u) {
-			const bool rel = live && (meta & CTM_RELX) && (a.ct_ret[i] & CT_RELP);
-			f = (p2 && !special ? 1u : 0u) | (rel ? 1u << 16 : 0u);
+			const bool rel = (c & PCL_RELX) && (a.ct_ret[i] & CT_RELP);
+			f = (c & PCL_P2A ? 1u : 0u) | (rel ? 1u << 16 : 0u);
 		} else {
-			f = (p2 && special ? 1u : 0u) | (live && (meta & CTM_ADDRX) ? 1u << 8 : 0u);
+			f = (c & PCL_P2B ? 1u : 0u) | (c & PCL_ADDRX ? 1u << 8 : 0u);
 		}
 		f4[i] = f;
 	}
@@ -6209,6 +6224,7 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.xdaddr = static_cast<uint32_t *>(L.xdaddr);
 	a.xdport = L.xdport;
 	a.f2 = L.flags2;
+	a.pcls = L.pcls;
 	return a;
 }
 
@@ -6447,7 +6463,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 		const unsigned g2 = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 		for (uint32_t ph = 0; ph < 2u; ph++) {
 			hipLaunchKernelGGL(k_ct_owed_flags, dim3(g2), dim3(256), 0, st, a,
-					   reinterpret_cast<uint32_t *>(L.flags2), s.ipv4_loopback, ph);
+					   reinterpret_cast<uint32_t *>(L.flags2), ph);
 			e = ct_select(L.flags2, 4 * L.n, L.idx, L.n_heads, static_cast<uint32_t *>(L.temp), st);
 			if (e != hipSuccess)
 				return e;
