@@ -909,6 +909,10 @@ struct cls_args {
  *   policy : policy.h:46-110, negative collapsed to DROP_POLICY
  * v: verdict; id: label given to policy; st: 1 exact, 2 L3-only, 3 wildcard,
  * 0 miss; ctr: the hit entry's counter slot or -1. */
+#ifndef CGPU_POLICY_Q_PROBES
+#define CGPU_POLICY_Q_PROBES 0
+#endif
+
 struct decision {
 	int32_t v;
 	uint32_t id, st;
@@ -955,13 +959,33 @@ __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, 
 	uint32_t z = 0;
 	int ctr = -1;
 	d.st = 0;
-	if (!frag) {
-		ctr = pol_lookup(s.pol, d.id, hi4, ep, &z);
-		d.st = 1;
-	}
-	if (ctr < 0) {
-		ctr = pol_lookup(s.pol, d.id, eg, ep, &z);
-		d.st = 2;
+	if (CGPU_POLICY_Q_PROBES) {
+		if (!frag) {
+			ctr = pol_lookup(s.pol, d.id, hi4, ep, &z);
+			d.st = 1;
+		}
+		if (ctr < 0) {
+			ctr = pol_lookup(s.pol, d.id, eg, ep, &z);
+			d.st = 2;
+		}
+	} else {
+		/* as policy_q: the {identity, endpoint, direction} group slot gives
+		 * probe 2 and the bloom that gates probe 1 */
+		const uint32_t ed = ep | (egress ? 1u << 16 : 0u);
+		const uint32_t bg = pg_hash(d.id, ed) & s.pg.mask;
+		const uint4 grp = pg_resolve(s.pg, s.pg.slots[bg], bg, d.id, ed);
+		const uint32_t bl = pg_bloom(dport, proto);
+		if (!frag && (grp.w & bl) == bl) {
+			ctr = pol_lookup(s.pol, d.id, hi4, ep, &z);
+			d.st = 1;
+		}
+		if (ctr < 0) {
+			d.st = 2;
+			if ((grp.z & POL_CTR_MASK) != POL_CTR_EMPTY) {
+				ctr = (int)(grp.z & POL_CTR_MASK);
+				z = 0;
+			}
+		}
 	}
 	if (ctr < 0 && !frag) {
 		ctr = pol_lookup(s.pol, 0u, hi4, ep, &z);
@@ -988,9 +1012,6 @@ __device__ __forceinline__ decision decide(const cgpu_snapshot &s, bool egress, 
  * probes in order (GROUP false: the probes themselves, for kernels at their
  * register limit - the group slots' registers spill k_ct_finish, 2.18 ->
  * 2.36 ms, profiles/r4_i/; CGPU_POLICY_Q_PROBES: every caller, A/B). */
-#ifndef CGPU_POLICY_Q_PROBES
-#define CGPU_POLICY_Q_PROBES 0
-#endif
 template <int Q, bool GROUP = true>
 __device__ __forceinline__ void policy_q(const cgpu_snapshot &s, const bool (&act)[Q], const bool (&eg)[Q],
 					 const bool (&frag)[Q], const uint32_t (&dport)[Q], const uint32_t (&proto)[Q],
