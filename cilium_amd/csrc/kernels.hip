@@ -891,7 +891,7 @@ struct cls_args {
 	int lb;       /* v4: egress service step first (cgpu_classify_v4_lb) */
 	const uint16_t *sport;
 	const uint32_t *hash;
-	uint32_t cc_n; /* k_classify_x4: cold-slot cache entries in LDS (power of 2, or 0) */
+	uint32_t cc_n; /* k_classify_x4: cold-slot cache entries in LDS (cc_entries, or 0) */
 	/* k_classify_x4 FR (frames): the tuple count is *n_dev - n_off, at most n */
 	const uint32_t *n_dev;
 	uint64_t n_off;
@@ -1621,7 +1621,6 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	const uint32_t lds_words = V6 ? (IPCE ? 0u : v6t_lds_words(s.ipc6)) : s.ipc4c.n_dict;
 	uint64_t *ccv = lctr + s.hot_slots + ((lds_words + 1u) >> 1);
 	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + a.cc_n);
-	const uint32_t ccm = a.cc_n - 1u;
 	/* fused frames: the endpoints' rows (16-byte aligned) and each lane's
 	 * four parse statuses, after the cold-slot cache (launch_x4's LDS) */
 	uint4 *lxl = reinterpret_cast<uint4 *>((reinterpret_cast<uintptr_t>(cck + a.cc_n) + 15u) & ~(uintptr_t)15u);
@@ -2147,10 +2146,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 					 * slot that finds no free entry in CC_PROBE goes global */
 					bool done = false;
 					if (a.cc_n) {
-						uint32_t j = (c * 0x9E3779B1u) >> 16;
+						uint32_t j = __umulhi(c * 0x9E3779B1u, a.cc_n);
 #pragma unroll
 						for (int p = 0; p < CC_PROBE && !done; p++, j++) {
-							j &= ccm;
+							j = j == a.cc_n ? 0u : j;
 							uint32_t t = cck[j];
 							if (t == 0u) {
 								const uint32_t o = atomicCAS(&cck[j], 0u, c + 1u);
@@ -3041,6 +3040,18 @@ static unsigned resident_blocks(const void *kern, int NT, size_t lds)
  * metrics block and some slack */
 #define X4_LDS_BUDGET (156u * 1024u)
 
+/* cold-slot cache entries (12 B each: packed count + tag) in the LDS left
+ * under X4_LDS_BUDGET by `used` bytes: a multiple of 64, at most 16384,
+ * none below 512 (any count: the probe start is a multiply-high of the slot
+ * hash, the probe wraps at the end) */
+static uint32_t cc_entries(size_t used)
+{
+	if (used >= X4_LDS_BUDGET)
+		return 0u;
+	const size_t n = std::min<size_t>((X4_LDS_BUDGET - used) / 12u, 16384u) & ~(size_t)63u;
+	return n >= 512u ? (uint32_t)n : 0u;
+}
+
 /* The snapshot a launch sees with at most `max_hot` LDS counter slots: hits
  * on slots past it take the kernels' cold path (the counts are the same,
  * only where they accumulate changes), so LDS never overflows whatever
@@ -3153,11 +3164,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 	size_t lds = (size_t)s.hot_slots * 8u + fixed;
 	/* the cold-slot cache takes the LDS one workgroup per CU leaves free
 	 * (the resident grid runs one 1024-thread workgroup per CU) */
-	uint32_t cc_n = 0;
-	if (!(s.schedule & CGPU_SCHED_NO_CCACHE))
-		for (uint32_t n = 1u << 14; n >= 512u && !cc_n; n >>= 1)
-			if (lds + (size_t)n * 12u <= X4_LDS_BUDGET)
-				cc_n = n;
+	const uint32_t cc_n = (s.schedule & CGPU_SCHED_NO_CCACHE) ? 0u : cc_entries(lds);
 	lds += (size_t)cc_n * 12u;
 #ifdef CGPU_DIAG_LDS_PAD /* timing-only: fewer resident workgroups per CU */
 	lds += CGPU_DIAG_LDS_PAD;
@@ -5961,7 +5968,6 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 	 * one pair of memory-side atomics per workgroup instead of one per hit */
 	uint64_t *ccv = lctr + s.hot_slots;
 	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + cc_n);
-	const uint32_t ccm = cc_n - 1u;
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
 		lctr[k] = 0;
 	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
@@ -6039,10 +6045,10 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 								  (1ull << PK_SHIFT) | (unsigned long long)len);
 							done = true;
 						} else if (cc_n) {
-							uint32_t j = (cs * 0x9E3779B1u) >> 16;
+							uint32_t j = __umulhi(cs * 0x9E3779B1u, cc_n);
 #pragma unroll
 							for (int p = 0; p < CC_PROBE && !done; p++, j++) {
-								j &= ccm;
+								j = j == cc_n ? 0u : j;
 								uint32_t t = cck[j];
 								if (t == 0u) {
 									const uint32_t o = atomicCAS(&cck[j], 0u, cs + 1u);
@@ -6298,11 +6304,7 @@ template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct
 	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
 	/* the cold-slot cache in the LDS the hot slots leave */
 	const size_t hot = (size_t)sf.hot_slots * 8u;
-	uint32_t cc_n = 0;
-	if (!(s.schedule & CGPU_SCHED_NO_CCACHE))
-		for (uint32_t c = 1u << 14; c >= 512u && !cc_n; c >>= 1)
-			if (hot + (size_t)c * 12u <= X4_LDS_BUDGET)
-				cc_n = c;
+	const uint32_t cc_n = (s.schedule & CGPU_SCHED_NO_CCACHE) ? 0u : cc_entries(hot);
 	hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), hot + (size_t)cc_n * 12u, st, sf,
 			   a, cc_n);
 }
