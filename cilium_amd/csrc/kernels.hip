@@ -1338,7 +1338,13 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  * two-word path into delta directly.  Each stream has its own pk buffer
  * (host.cpp), so concurrent calls on one context never share the bound. */
 #define PKC_SHIFT 37
-#define CC_PROBE 4 /* linear probes of the LDS cold-slot cache */
+#ifndef CC_PROBE
+/* linear probes of the LDS cold-slot cache: 1 (direct-mapped) measured
+ * fastest, config 2 1.771 / 1.734 / 1.752 / 1.763 ms at 4 / 1 / 2 / 3
+ * (profiles/r4_x/): a second probe rarely finds room the first did not
+ * and costs an LDS round trip on every miss */
+#define CC_PROBE 1
+#endif
 #define PKC_BYTES_MASK ((1ull << PKC_SHIFT) - 1ull)
 #define PKC_MAX_LEN (1u << 11)
 #define PKC_CHUNK (1ull << 26)

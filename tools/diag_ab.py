@@ -44,7 +44,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "v6_pre_q4_w2": ("CGPU_IPC6_MINW=2", "CGPU_DIAG_IPC6_PRE_Q=4"), "ct_q2": ("CGPU_CT_Q=2",), "ct_q1": ("CGPU_CT_Q=1",),
             "policy_probes": ("CGPU_POLICY_Q_PROBES=1",), "walk_svc_minb1": ("CGPU_WALK_MINB_SVC=1",),
             "svc_decq": ("CGPU_CT_SVC_DECQ=1",), "svc_decq6": ("CGPU_CT_SVC_DECQ6=1",),
-            "walk_w4": ("CGPU_WALK_W=4",), "walk_w3": ("CGPU_WALK_W=3",)}
+            "walk_w4": ("CGPU_WALK_W=4",), "walk_w3": ("CGPU_WALK_W=3",),
+            "cc_probe2": ("CC_PROBE=2",), "cc_probe4": ("CC_PROBE=4",)}
 
 
 def build(names):
