@@ -2017,7 +2017,11 @@ CGPU_EXPORT void cgpu_config_default(cgpu_config *c)
 	c->prefilter_fix4 = c->prefilter_dyn4 = 1; /* bpf/filter_config.h */
 	c->prefilter_fix6 = c->prefilter_dyn6 = 1;
 	c->ingress_src_identity = 0;
-	c->hot_counter_slots = 12288; /* bench --hot-slots 8192 / 12288 / 16384: 1.808 / 1.791 / 1.791 ms (config 2) */
+	/* as many as a kernel's LDS holds (each launcher caps it): with the
+	 * popularity rebalance, config 2 1.692 / 1.657 / 1.645 ms at 12288 /
+	 * 16384 / 17920 (the x4 kernel's cap), v6 2.805 / 2.759 / 2.725 at
+	 * 12288 / 16384 / 24576 (profiles/r4_z/) */
+	c->hot_counter_slots = 24576;
 	c->lb_max_entries = 65536;        /* CILIUM_LB_MAP_MAX_ENTRIES, bpf/node_config.h:60 */
 	c->ipv4_loopback = 0x1ffff50a;    /* IPV4_LOOPBACK, bpf/node_config.h:45 */
 	c->lb_flags = CGPU_LB_L3 | CGPU_LB_L4; /* bpf/lxc_config.h:44-45 */

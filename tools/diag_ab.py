@@ -178,7 +178,10 @@ def _workload(conf):
            "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
 
     def make():
-        e = Engine(device=0, **T.engine_config())
+        cfg = T.engine_config()
+        if os.environ.get("CGPU_AB_HOT"):  # LDS hot counter slots (bench.py --hot-slots)
+            cfg["hot_counter_slots"] = int(os.environ["CGPU_AB_HOT"])
+        e = Engine(device=0, **cfg)
         synth.load_engine(e, T)
         return e
     return make, lambda e: (e.classify_v6 if v6 else e.classify_v4)(d, out=out), n
@@ -193,6 +196,9 @@ def run(names):
         e.commit()
         for _ in range(3):
             launch(e)
+        if os.environ.get("CGPU_AB_REBALANCE"):  # as bench.py after its warmup
+            torch.cuda.synchronize()
+            e.counters_rebalance()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
         for a, b in ev:
             a.record()
