@@ -100,7 +100,10 @@ def _workload(conf):
                "ct_ret": torch.empty(n, dtype=torch.uint8, device="cuda")}
 
         def make():
-            e = Engine(device=0, **T.engine_config(), ct_max=ct_max)
+            cfg = T.engine_config()
+            if os.environ.get("CGPU_AB_HOT"):
+                cfg["hot_counter_slots"] = int(os.environ["CGPU_AB_HOT"])
+            e = Engine(device=0, **cfg, ct_max=ct_max)
             synth.load_engine(e, T)
             synth.load_lxc(e, seclabels)
             return e
