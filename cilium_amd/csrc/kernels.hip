@@ -1377,7 +1377,9 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
  *   node: the line's four boundary units (64 B) and, for a /32 with /65+
  *         prefixes, the /64's h64 home slot, together; then the label word.
  * w: host-order address words; act false: e = 0. */
+#ifndef V6T_LDS_B24
 #define V6T_LDS_B24 96u /* b24 blocks staged in LDS at most (48 KiB) */
+#endif
 
 /* b24 blocks the x4 kernel stages in LDS (0: b24 read from global memory) */
 __host__ __device__ __forceinline__ uint32_t v6t_lds_b24(const v6_lpm &t)
