@@ -3722,6 +3722,11 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #ifndef CGPU_CT_Q
 #define CGPU_CT_Q 4
 #endif
+/* phase 2b groups an address entry no phase-2 packet can read by its whole
+ * key (k_ct_owed_bloom); 0: by its pair (A/B) */
+#ifndef CGPU_OWED_BY_KEY
+#define CGPU_OWED_BY_KEY 1
+#endif
 /* the service paths' forward decisions: 0 inside the per-packet prep, 1 a
  * k_ct_decq pass after it (Q packets per lane).  Measured slower (ctlb
  * 25.19 -> 25.53 ms, ctlb6 24.13 -> 26.93: the v6 pass stages the trie
@@ -4841,7 +4846,28 @@ __global__ __launch_bounds__(256) void k_ct_owed_flags(ct_args a, uint32_t *f4, 
 /* group key of each selected candidate: the address pair (packet: its own,
  * owed entry: the entry's), or, when no packet runs in phase 2, the owed
  * entry's whole key (blind BPF_ANY writes of different keys commute) */
-template <class K> __global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args a, uint32_t m, uint32_t by_key)
+/* Phase 2b of the service path: the pairs its PACKETS run in (candidates
+ * of kind 0), as a bloom filter over their pair hashes: an owed address
+ * entry whose pair has no such packet is a blind BPF_ANY write that no
+ * phase-2 read sees, so k_ct_owed_keys groups it by its whole key (entries
+ * of one key stay in batch order) instead of serialising the pair's */
+#define OWED_BLOOM_WORDS (1u << 15) /* 2^20 bits */
+template <class K> __global__ __launch_bounds__(256) void k_ct_owed_bloom(ct_args a, uint32_t m, uint32_t *bl)
+{
+	for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) {
+		const uint32_t v = a.idx[j];
+		if ((v & 3u) != 0u)
+			continue;
+		const uint4 k = ct_rec<K>::load(a.rec, v >> 2, false).key();
+		const uint32_t h = ct_group(k.x, k.y);
+		atomicOr(&bl[(h >> 5) & (OWED_BLOOM_WORDS - 1u)], 1u << (h & 31u));
+	}
+}
+
+/* bl (the service path's phase 2b): k_ct_owed_bloom's filter, or nullptr */
+template <class K>
+__global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args a, uint32_t m, uint32_t by_key,
+						     const uint32_t *bl = nullptr)
 {
 	for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < m; j += gridDim.x * 256u) {
 		const uint32_t v = a.idx[j], i = K::ADDR ? v >> 2 : v >> 1;
@@ -4852,7 +4878,10 @@ template <class K> __global__ __launch_bounds__(256) void k_ct_owed_keys(ct_args
 				k = ct_addr_key(CtK4::reversed(k), r.pkt());
 			else if ((v & 3u) == 2u)
 				k = CtK4::related(CtK4::reversed(k));
-			a.gkey[j] = by_key ? ct_hash(k.x, k.y, k.z, k.w) : ct_group(k.x, k.y);
+			const uint32_t h = ct_group(k.x, k.y);
+			const bool alone = bl && (v & 3u) == 1u &&
+					   !((bl[(h >> 5) & (OWED_BLOOM_WORDS - 1u)] >> (h & 31u)) & 1u);
+			a.gkey[j] = (by_key || alone) ? ct_hash(k.x, k.y, k.z, k.w) : h;
 		} else if constexpr (K::V6 != 0) {
 			/* an ICMP entry carries its packet's pair */
 			const typename K::key k = r.key();
@@ -6243,7 +6272,8 @@ size_t ct_temp_bytes(uint64_t n)
 	size_t a = 0;
 	(void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
 						 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
-	return std::max<size_t>(a, sel_blocks(4 * n) * 4u + 4u);
+	/* ... and phase 2b's bloom filter (k_ct_owed_bloom) */
+	return std::max<size_t>(std::max<size_t>(a, sel_blocks(4 * n) * 4u + 4u), (size_t)OWED_BLOOM_WORDS * 4u);
 }
 
 static ct_args ct_args_of(const ct_launch &L)
@@ -6505,7 +6535,18 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 			if (!m)
 				continue;
 			const unsigned gm = (unsigned)std::min<uint64_t>((m + 255) / 256, 8192);
-			hipLaunchKernelGGL(k_ct_owed_keys<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, 0u);
+			/* 2b: the address entries of pairs no phase-2 packet reads go by
+			 * key (the filter in temp, free between the selection and the
+			 * sort) */
+			uint32_t *bl = nullptr;
+			if (ph == 1u && CGPU_OWED_BY_KEY) {
+				bl = static_cast<uint32_t *>(L.temp);
+				if ((e = hipMemsetAsync(bl, 0, OWED_BLOOM_WORDS * 4u, st)) != hipSuccess)
+					return e;
+				hipLaunchKernelGGL(k_ct_owed_bloom<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, bl);
+			}
+			hipLaunchKernelGGL(k_ct_owed_keys<CtK4S>, dim3(gm), dim3(256), 0, st, a, m, 0u,
+					   (const uint32_t *)bl);
 			e = ct_group_sort(s, L, a, m, &nh, st);
 			if (e != hipSuccess)
 				return e;

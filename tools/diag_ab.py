@@ -45,7 +45,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "policy_probes": ("CGPU_POLICY_Q_PROBES=1",), "walk_svc_minb1": ("CGPU_WALK_MINB_SVC=1",),
             "svc_decq": ("CGPU_CT_SVC_DECQ=1",), "svc_decq6": ("CGPU_CT_SVC_DECQ6=1",),
             "walk_w4": ("CGPU_WALK_W=4",), "walk_w3": ("CGPU_WALK_W=3",),
-            "cc_probe2": ("CC_PROBE=2",), "cc_probe4": ("CC_PROBE=4",)}
+            "cc_probe2": ("CC_PROBE=2",), "cc_probe4": ("CC_PROBE=4",),
+            "owed_by_pair": ("CGPU_OWED_BY_KEY=0",)}
 
 
 def build(names):
