@@ -156,6 +156,33 @@ def link_rates(torch, dev, nbytes=1 << 30):
     return out
 
 
+def numa_nodes(t, samples=64):
+    """NUMA node of a host tensor's pages (move_pages(2) query, sampled):
+    where the host-resident line's buffers landed relative to the GPU."""
+    import ctypes
+    from collections import Counter
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        base, nbytes = t.data_ptr(), t.numel() * t.element_size()
+        step = max(4096, (nbytes // samples) & ~4095)
+        pages = (ctypes.c_void_p * samples)(*[(base + i * step) & ~4095 for i in range(samples)])
+        status = (ctypes.c_int * samples)()
+        if libc.syscall(279, 0, samples, pages, None, status, 0) != 0:  # SYS_move_pages
+            return None
+        return dict(Counter(int(x) for x in status))
+    except (OSError, AttributeError):
+        return None
+
+
+def gpu_numa_node(torch, dev):
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        return int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
 def pmc_traffic(args):
     """roofline.traffic: the HBM-side bytes per step from a PMC profile of
     the kernels this process actually ran.  profiles/traffic_<config>.json
@@ -640,6 +667,9 @@ def main():
             per_in, per_out = B_IN, B_OUT  # bytes up / down per tuple
             conf.update(host_tuples=True,
                         pcie_measured_gbs=bw,
+                        numa={"gpu": gpu_numa_node(torch, dev),
+                              "inputs": numa_nodes(d["saddr"]), "verdict": numa_nodes(out["verdict"]),
+                              "identity": numa_nodes(out["identity"])},
                         ingest_bound_mpps=round(min(bw["h2d"] * 1e3 / per_in, bw["d2h"] * 1e3 / per_out), 1),
                         note=("PCIe-inclusive: the columns (18 B/tuple) go up and the verdict + identity "
                               "(8 B) come down every step through double-buffered 4M-tuple chunks; "

@@ -1884,14 +1884,16 @@ struct cgpu_ctx {
 	/* ---- conntrack maps cilium_ct4_global / cilium_ct6_global ---- */
 	CtMap ct4, ct6;
 	void *d_ct_scratch = nullptr;
-	/* host-resident batches (cgpu_classify_v4_host): double-buffered device
-	 * staging, one copy stream per direction */
+	/* host-resident batches (cgpu_classify_v4_host): device staging for up
+	 * to HS_NBUF chunks (grown to the largest batch seen), one stream per
+	 * direction */
 	std::mutex host_mu;
 	struct {
 		size_t chunk = 0;
-		void *d_in[2] = {}, *d_out[2] = {};
+		int nb = 0;
+		void *d_in[16] = {}, *d_out[16] = {};
 		hipStream_t h2d = nullptr, d2h = nullptr;
-		hipEvent_t ev_in[2] = {}, ev_cls[2] = {}, ev_out[2] = {};
+		hipEvent_t ev_in[16] = {}, ev_cls[16] = {}, ev_out[16] = {};
 	} hs;
 	size_t ct_scratch_cap = 0;
 	hipStream_t ct_stream = nullptr; /* the conntrack path's internal stream */
@@ -2160,7 +2162,7 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 		if (c->hs.chunk) {
 			(void)hipStreamSynchronize(c->hs.h2d);
 			(void)hipStreamSynchronize(c->hs.d2h);
-			for (int b = 0; b < 2; b++) {
+			for (int b = 0; b < c->hs.nb; b++) {
 				(void)hipFree(c->hs.d_in[b]);
 				(void)hipFree(c->hs.d_out[b]);
 				(void)hipEventDestroy(c->hs.ev_in[b]);
@@ -4184,6 +4186,10 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
  * caller's stream, its outputs come back on the d2h stream, so chunk k + 1's
  * upload and chunk k - 1's download overlap chunk k's classify. */
 #define HS_CHUNK (1u << 22)
+#define HS_NBUF 16
+#ifndef CGPU_HS_STORE
+#define CGPU_HS_STORE 1
+#endif
 
 static size_t hs_in_off(size_t m, int col)
 {
@@ -4204,22 +4210,50 @@ static size_t hs_out_off(size_t m, int col)
 	return o;
 }
 
-static int host_stage_init(cgpu_ctx *c)
+static int host_stage_init(cgpu_ctx *c, size_t nch)
 {
 	auto &H = c->hs;
-	if (H.chunk)
-		return 0;
-	for (int b = 0; b < 2; b++) {
+	if (!H.chunk) {
+		/* the copy streams in priority classes of their own, non-blocking:
+		 * the runtime spreads plain streams over the process's few hardware
+		 * queues round robin, and an upload stream that landed on the
+		 * caller's queue serialised every chunk's classify behind all queued
+		 * uploads (profiles/r4_ah); queues are pooled per priority */
+		int least = 0, greatest = 0;
+		HIP_OR_EIO(hipDeviceGetStreamPriorityRange(&least, &greatest));
+		HIP_OR_EIO(hipStreamCreateWithPriority(&H.h2d, hipStreamNonBlocking, greatest));
+		HIP_OR_EIO(hipStreamCreateWithPriority(&H.d2h, hipStreamNonBlocking, least));
+		H.chunk = HS_CHUNK;
+	}
+	const int want = (int)std::min<size_t>(nch, HS_NBUF);
+	for (; H.nb < want; H.nb++) {
+		const int b = H.nb;
 		HIP_OR_EIO(hipMalloc(&H.d_in[b], hs_in_off(HS_CHUNK, 7)));
 		HIP_OR_EIO(hipMalloc(&H.d_out[b], hs_out_off(HS_CHUNK, 3)));
 		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_in[b], hipEventDisableTiming));
 		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_cls[b], hipEventDisableTiming));
 		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_out[b], hipEventDisableTiming));
 	}
-	HIP_OR_EIO(hipStreamCreateWithFlags(&H.h2d, hipStreamNonBlocking));
-	HIP_OR_EIO(hipStreamCreateWithFlags(&H.d2h, hipStreamNonBlocking));
-	H.chunk = HS_CHUNK;
 	return 0;
+}
+
+/* the device address of a page-locked host range [p, p + bytes), or null
+ * when the range is not page-locked host memory the device maps (both ends
+ * checked) */
+static void *host_mapped(void *p, size_t bytes)
+{
+	if (!p || !bytes)
+		return nullptr;
+	hipPointerAttribute_t a0{}, a1{};
+	char *last = static_cast<char *>(p) + bytes - 1;
+	if (hipPointerGetAttributes(&a0, p) != hipSuccess || hipPointerGetAttributes(&a1, last) != hipSuccess) {
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	if (a0.type != hipMemoryTypeHost || a1.type != hipMemoryTypeHost || !a0.devicePointer ||
+	    static_cast<char *>(a1.devicePointer) != static_cast<char *>(a0.devicePointer) + bytes - 1)
+		return nullptr;
+	return a0.devicePointer;
 }
 
 CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
@@ -4236,30 +4270,72 @@ CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size
 		return 0;
 	std::lock_guard<std::mutex> g(c->host_mu);
 	HIP_OR_EIO(hipSetDevice(c->device));
-	if (int r = host_stage_init(c))
+	const size_t nch = (n + HS_CHUNK - 1) / HS_CHUNK;
+	if (int r = host_stage_init(c, nch))
 		return r;
 	auto &H = c->hs;
 	const hipStream_t cs = (hipStream_t)stream;
-	bool used[2] = {false, false};
-	for (size_t off = 0, k = 0; off < n; off += H.chunk, k++) {
-		const size_t m = std::min<size_t>(H.chunk, n - off);
-		const int b = (int)(k & 1u);
-		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]), *out = static_cast<uint8_t *>(H.d_out[b]);
-		/* the input buffer is free once chunk k - 2's classify ran */
-		if (used[b])
-			HIP_OR_EIO(hipStreamWaitEvent(H.h2d, H.ev_cls[b], 0));
+	const size_t nb = (size_t)H.nb;
+	static const size_t el[7] = {4, 4, 2, 1, 1, 4, 2};
+	/* the columns read by the CUs when page-locked and mapped (a DMA copy's
+	 * wait on another stream's event, and in this runtime the copy itself,
+	 * held the issuing thread, profiles/r4_ah), else copied */
+	const void *const cols[7] = {t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep};
+	const uint8_t *src_dev[7];
+	for (int col = 0; col < 7; col++)
+		src_dev[col] = static_cast<const uint8_t *>(host_mapped(const_cast<void *>(cols[col]), n * el[col]));
+	/* chunk k's columns up on the h2d stream into buffer k % nb, free once
+	 * that buffer's last classify ran (in this call or an earlier one; an
+	 * event never recorded is no wait) */
+	auto upload = [&](size_t k) -> int {
+		const size_t off = k * H.chunk, m = std::min<size_t>(H.chunk, n - off);
+		const size_t b = k % nb;
+		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]);
+		HIP_OR_EIO(hipStreamWaitEvent(H.h2d, H.ev_cls[b], 0));
 		const void *src[7] = {t->saddr + off, t->daddr + off, t->dport + off, t->proto + off,
 				      t->flags + off, t->len + off, t->ep + off};
-		static const size_t el[7] = {4, 4, 2, 1, 1, 4, 2};
-		for (int col = 0; col < 7; col++)
+		for (int col = 0; col < 7; col++) {
+			if (src_dev[col] && CGPU_HS_STORE &&
+			    launch_copy_host(in + hs_in_off(m, col), src_dev[col] + off * el[col], m * el[col], H.h2d) ==
+				    hipSuccess)
+				continue;
+			(void)hipGetLastError();
 			HIP_OR_EIO(hipMemcpyAsync(in + hs_in_off(m, col), src[col], m * el[col], hipMemcpyHostToDevice,
 						  H.h2d));
+		}
 		HIP_OR_EIO(hipEventRecord(H.ev_in[b], H.h2d));
+		return 0;
+	};
+	/* outputs: stored by the CUs into the caller's buffers when they are
+	 * page-locked and mapped (a DMA download ran at a quarter of the link
+	 * rate beside the uploads, profiles/r4_ah), else downloaded */
+	int32_t *v_dev = static_cast<int32_t *>(host_mapped(verdict, n * 4));
+	uint32_t *i_dev = static_cast<uint32_t *>(host_mapped(identity, n * 4));
+	uint8_t *s_dev = stage ? static_cast<uint8_t *>(host_mapped(stage, n)) : nullptr;
+	auto download = [&](void *dst_host, void *dst_dev, const void *src, size_t bytes) -> int {
+		if (dst_dev && CGPU_HS_STORE && launch_copy_host(dst_dev, src, bytes, H.d2h) == hipSuccess)
+			return 0;
+		(void)hipGetLastError();
+		HIP_OR_EIO(hipMemcpyAsync(dst_host, src, bytes, hipMemcpyDeviceToHost, H.d2h));
+		return 0;
+	};
+	/* every upload that has a buffer of its own is queued first, so the
+	 * h2d stream runs back to back (the runtime resolves a copy's wait on
+	 * another stream's event on the issuing thread: an upload queued behind
+	 * a download's wait on a classify stalled until that classify ended,
+	 * profiles/r4_ah); past HS_NBUF chunks, chunk k + nb goes up once chunk
+	 * k's classify is queued */
+	for (size_t k = 0; k < std::min(nch, nb); k++)
+		if (int r = upload(k))
+			return r;
+	for (size_t k = 0; k < nch; k++) {
+		const size_t off = k * H.chunk, m = std::min<size_t>(H.chunk, n - off);
+		const size_t b = k % nb;
+		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]), *out = static_cast<uint8_t *>(H.d_out[b]);
 		/* classify on the caller's stream once the columns landed and the
-		 * output buffer drained (chunk k - 2's download) */
+		 * output buffer drained (its last download) */
 		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_in[b], 0));
-		if (used[b])
-			HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
+		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
 		const cgpu_tuples_v4 dt{reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 0)),
 					reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 1)),
 					reinterpret_cast<const uint16_t *>(in + hs_in_off(m, 2)), in + hs_in_off(m, 3),
@@ -4271,18 +4347,22 @@ CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size
 		if (int r = cgpu_classify_v4(c, &dt, m, dv, di, ds, stream))
 			return r;
 		HIP_OR_EIO(hipEventRecord(H.ev_cls[b], cs));
+		if (k + nb < nch)
+			if (int r = upload(k + nb))
+				return r;
 		HIP_OR_EIO(hipStreamWaitEvent(H.d2h, H.ev_cls[b], 0));
-		HIP_OR_EIO(hipMemcpyAsync(verdict + off, dv, m * 4, hipMemcpyDeviceToHost, H.d2h));
-		HIP_OR_EIO(hipMemcpyAsync(identity + off, di, m * 4, hipMemcpyDeviceToHost, H.d2h));
+		if (int r = download(verdict + off, v_dev ? v_dev + off : nullptr, dv, m * 4))
+			return r;
+		if (int r = download(identity + off, i_dev ? i_dev + off : nullptr, di, m * 4))
+			return r;
 		if (stage)
-			HIP_OR_EIO(hipMemcpyAsync(stage + off, ds, m, hipMemcpyDeviceToHost, H.d2h));
+			if (int r = download(stage + off, s_dev ? s_dev + off : nullptr, ds, m))
+				return r;
 		HIP_OR_EIO(hipEventRecord(H.ev_out[b], H.d2h));
-		used[b] = true;
 	}
 	/* the caller's stream completes once the last outputs are in host memory */
-	for (int b = 0; b < 2; b++)
-		if (used[b])
-			HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
+	for (size_t b = 0; b < nb && b < nch; b++)
+		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
 	return 0;
 }
 

@@ -3651,6 +3651,43 @@ hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_
 	return hipGetLastError();
 }
 
+/* host-resident batches (host.cpp cgpu_classify_v4_host): a chunk's columns
+ * read from, and its outputs stored into, the caller's page-locked host
+ * buffers by the CUs (16 B per lane, four in flight per lane, coalesced
+ * PCIe requests) in place of DMA copies, so every step of the pipeline is a
+ * kernel the queues order on the device */
+__global__ __launch_bounds__(256) void k_copy_host(uint4 *dst, const uint4 *src, uint64_t n16, uint8_t *dtail,
+						   const uint8_t *stail, uint32_t ntail)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	for (; i + 3 * stride < n16; i += 4 * stride) {
+		const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+		dst[i] = a;
+		dst[i + stride] = b;
+		dst[i + 2 * stride] = c;
+		dst[i + 3 * stride] = d;
+	}
+	for (; i < n16; i += stride)
+		dst[i] = src[i];
+	if (blockIdx.x == 0 && threadIdx.x < ntail)
+		dtail[threadIdx.x] = stail[threadIdx.x];
+}
+
+hipError_t launch_copy_host(void *dst, const void *src, uint64_t bytes, hipStream_t st)
+{
+	if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15u)
+		return hipErrorInvalidValue;
+	if (!bytes)
+		return hipSuccess;
+	const uint64_t n16 = bytes >> 4;
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n16 + 1023) / 1024, 128));
+	hipLaunchKernelGGL(k_copy_host, dim3(g), dim3(256), 0, st, static_cast<uint4 *>(dst),
+			   static_cast<const uint4 *>(src), n16, static_cast<uint8_t *>(dst) + (n16 << 4),
+			   static_cast<const uint8_t *>(src) + (n16 << 4), (uint32_t)(bytes & 15u));
+	return hipGetLastError();
+}
+
 hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *slot,
 			    const uint64_t *pk, const uint64_t *by, uint32_t n, hipStream_t st)
 {

@@ -203,6 +203,10 @@ hipError_t launch_table_sum(const void *buf, size_t off, size_t bytes, uint64_t 
 
 /* totals[i] += delta[i]; delta[i] = 0 over n u64 words */
 hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_t st);
+/* a copy by the CUs between device memory and a device-visible page-locked
+ * host range (either way); hipErrorInvalidValue unless dst and src are
+ * 16-byte aligned */
+hipError_t launch_copy_host(void *dst, const void *src, uint64_t bytes, hipStream_t st);
 /* totals[2*slot[i]] = pk[i]; totals[2*slot[i]+1] = by[i]; delta[..] = 0 */
 hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *slot,
 			    const uint64_t *pk, const uint64_t *by, uint32_t n, hipStream_t st);
