@@ -443,11 +443,11 @@ int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *
  * classifies each packet as the NIC hands it over, bpf_xdp.c:181-184 /
  * bpf_netdev.c:470; the engine takes batches that arrive in host memory
  * too): every column of t and the outputs are host pointers.  The batch
- * streams through double-buffered device staging in chunks of 4M tuples:
- * chunk k + 1 uploads and chunk k - 1 downloads while chunk k classifies on
- * `stream`.  Returns once enqueued; the outputs are complete when `stream`
- * is (page-locked buffers overlap the copies with the classify, pageable
- * ones are staged by the runtime and serialise).  Same results, counters
+ * streams through device staging (up to 16 chunks of 4M tuples): uploads,
+ * the classify of each chunk on `stream` and the stores of its outputs
+ * overlap on queues of their own.  Returns once enqueued; the outputs are
+ * complete when `stream` is (page-locked buffers are read and written by
+ * the CUs; pageable ones are copied by the runtime and serialise).  Same results, counters
  * and metrics as cgpu_classify_v4 of the same tuples.  -ENODEV on a
  * host-only context, -EINVAL for a null column or output.
  */
