@@ -210,7 +210,98 @@ def pmc_traffic(args):
     return (t.get("hbm_bytes_per_step"),
             f"{os.path.relpath(tj, ROOT)}: {t.get('source')}; sources {str(was.get('src_sha256'))[:12]}, "
             f"built at {str(was.get('git_head'))[:12]}",
-            {"name": t.get("dominant_kernel"), "hbm_bytes_per_launch": t.get("hbm_bytes_per_launch")})
+            {"name": t.get("dominant_kernel"), "hbm_bytes_per_launch": t.get("hbm_bytes_per_launch"),
+             "memory_side_atomics_per_step": t.get("memory_side_atomics_per_step",
+                                                   t.get("memory_side_atomics_dominant")),
+             "l2_requests_per_step": t.get("l2_requests_per_step")})
+
+
+CEILINGS = os.path.join(ROOT, "profiles", "ceilings.json")
+# reference map -> the engine table its lookups gather from (cgpu_table_bytes)
+MAP_TABLE = {"ipcache": "ipcache", "policy": "policy", "lb": "lb4", "prefilter": "prefilter",
+             "endpoint": "endpoint", "ct": "ct4"}
+
+
+def tier_rate(ceil, nbytes):
+    """Measured random-gather ceiling (G/s) of a table of nbytes: the rate of
+    the largest measured table no larger than it (rates fall with size, so
+    this never understates what the tier can serve)."""
+    g = ceil["gather"]
+    floor = g[0][0]
+    for s_, _ in g:
+        if s_ <= nbytes:
+            floor = s_
+    # the envelope: no table of at least `floor` bytes measured faster
+    return max(r for s_, r in g if s_ >= floor)
+
+
+def roofline(n, kern_ms, b_in, b_out, probes_total, split, tbytes, v6, dom):
+    """The roofline a lookup-bound step cannot beat: three time
+    floors from measured ceilings (profiles/ceilings.json), the largest
+    bounds the step.
+      gather  every reference map lookup (counted per map by the restatement)
+              at the random-gather ceiling of the tier its table lives in
+              (tier by the table's device bytes): the lookups into tables of
+              at least theta bytes take at least their count / R(theta), for
+              every theta (the measured tier mixes in ceilings.json obey it)
+      atomic  the memory-side atomics the step's kernels issued (PMC,
+              stamped profile of this library) at the measured atomic rate
+      stream  the tuple columns in and out at the measured stream rates
+    frac = floor / measured kernel time of the step."""
+    if not os.path.exists(CEILINGS):
+        return None
+    ceil = json.load(open(CEILINGS))
+    t_s = kern_ms * 1e-3
+    counts = dict(split)
+    counts["ct"] = max(0, int(probes_total) - sum(split.values()))
+    per_map = {}
+    for m, c in counts.items():
+        if not c:
+            continue
+        tab = MAP_TABLE[m]
+        if v6 and tab in ("lb4", "ct4"):
+            tab = tab[:-1] + "6"
+        nb = int(tbytes.get(tab, 0))
+        per_map[m] = {"lookups_per_tuple": round(c / n, 4), "table": tab, "table_bytes": nb,
+                      "tier_g_per_s": tier_rate(ceil, nb), "_n": c}
+    # every gather into a table of at least theta bytes is served no faster
+    # than the measured tier of a theta-byte table, whatever else runs beside
+    # it: T >= max over theta of (lookups into tables >= theta) / R(theta)
+    # (ceilings.json "mix": measured two-tier mixes stay within this)
+    t_gather, theta = 0.0, None
+    for m, x in per_map.items():
+        t = sum(y["_n"] for y in per_map.values() if y["table_bytes"] >= x["table_bytes"]) / (
+            x["tier_g_per_s"] * 1e9)
+        if t > t_gather:
+            t_gather, theta = t, x["table_bytes"]
+    for x in per_map.values():
+        del x["_n"]
+    look = sum(counts.values())
+    comp = {"gather": {"achieved": round(look / t_s / 1e9, 2),
+                       "peak": round(look / t_gather / 1e9, 2) if t_gather else None,
+                       "unit": "G lookups/s", "frac": round(t_gather / t_s, 4),
+                       "binding_table_bytes": theta, "maps": per_map}}
+    rd, wr = ceil["stream"]["read_gbs"], ceil["stream"]["write_gbs"]
+    t_stream = n * (b_in / (rd * 1e9) + b_out / (wr * 1e9))
+    comp["stream"] = {"achieved": round(n * (b_in + b_out) / t_s / 1e9, 1),
+                      "peak": round(n * (b_in + b_out) / t_stream / 1e9, 1), "unit": "GB/s",
+                      "frac": round(t_stream / t_s, 4), "bytes_in_per_tuple": b_in,
+                      "bytes_out_per_tuple": b_out, "read_gbs": rd, "write_gbs": wr}
+    at = (dom or {}).get("memory_side_atomics_per_step")
+    t_atomic = None
+    if at is not None and ceil.get("atomic_g_per_s"):
+        t_atomic = at / (ceil["atomic_g_per_s"] * 1e9)
+        comp["atomic"] = {"achieved": round(at / t_s / 1e9, 3), "peak": ceil["atomic_g_per_s"],
+                          "unit": "G atomics/s", "frac": round(t_atomic / t_s, 4),
+                          "atomics_per_step": at, "source": "stamped PMC profile (TCC_EA0_ATOMIC)"}
+    else:
+        comp["atomic"] = None
+    floors = {"gather": t_gather, "stream": t_stream, "atomic": t_atomic or 0.0}
+    bound = max(floors, key=floors.get)
+    c = comp[bound]
+    return {"bound": bound, "achieved": c["achieved"], "peak": c["peak"], "unit": c["unit"],
+            "frac": c["frac"], "components": comp,
+            "ceilings": f"{os.path.relpath(CEILINGS, ROOT)}: {ceil.get('source')}"}
 
 
 def main():
@@ -551,9 +642,11 @@ def main():
                 # pair partition is exact); the CPU baseline: the same code
                 # threaded RSS-style by connection (shard.conn_shard_of),
                 # checked against the sequential result
+                o.probe_split()
                 c0 = time.perf_counter()
                 r_ = getattr(o, meth)(tup, CT_NOW)
                 seq_s = time.perf_counter() - c0
+                split = o.probe_split()
                 first = (r_["verdict"], r_["ct_ret"], r_["identity"], r_["stage"], r_["probes"])
                 x0 = (r_["xdaddr"], r_["xdport"])
                 if not skip_cpu:
@@ -579,8 +672,10 @@ def main():
                 # address pairs are independent conntrack groups (every key a
                 # packet touches carries its pair): the pair-sharded run is
                 # exactly the sequential result for the whole batch
+                o.probe_split()
                 first, c_el = o.sharded(meth, tup, CT_NOW, shard.ct_shard_of(tup, 4 * threads),
                                         threads)
+                split = o.probe_split()
                 if not skip_cpu:
                     cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
                            "kind": "port",
@@ -594,6 +689,8 @@ def main():
             cpu_run(slice(0, min(n, 1 << 20)))  # warm the tables' pages before timing
         # the median of 3 timed runs (the first also yields the reference result)
         runs = []
+        if not ct:
+            o.probe_split()
         for rep in range(0 if ct else 3):
             c0 = time.perf_counter()
             if pf6:
@@ -609,6 +706,7 @@ def main():
             runs.append(time.perf_counter() - c0)
             if rep == 0:
                 first = res
+                split = o.probe_split()
             if skip_cpu:
                 break
         if ct:
@@ -651,6 +749,8 @@ def main():
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
         traffic, traffic_note, traffic_dom = pmc_traffic(args)
+        roof = roofline(n_cpu, kern_ms, b_in, b_out, probes, split, e.table_bytes(), ct6 or v6 or pf6,
+                        traffic_dom)
         conf = {"workload": WORKLOADS[args.config], "tuples_per_gpu": n,
                 "parallelism": f"shard{world}", "kernel_ms": round(kern_ms, 4),
                 "stream_tuples_per_step": world * n, "stream_tuples_timed": world * n * args.steps,
@@ -671,10 +771,20 @@ def main():
                               "inputs": numa_nodes(d["saddr"]), "verdict": numa_nodes(out["verdict"]),
                               "identity": numa_nodes(out["identity"])},
                         ingest_bound_mpps=round(min(bw["h2d"] * 1e3 / per_in, bw["d2h"] * 1e3 / per_out), 1),
+                        hbm_resident_roofline=roof,
                         note=("PCIe-inclusive: the columns (18 B/tuple) go up and the verdict + identity "
                               "(8 B) come down every step through double-buffered 4M-tuple chunks; "
                               "ingest_bound_mpps = the measured link rate over those bytes. The "
                               "HBM-resident rate is the default line (no --host-tuples)"))
+            # the host line is bound by the link, both directions at once: the
+            # floor is the slower direction's bytes at its measured rate
+            t_s = ms_per_step * 1e-3
+            t_up, t_down = n * per_in / (bw["h2d"] * 1e9), n * per_out / (bw["d2h"] * 1e9)
+            roof = {"bound": "link", "achieved": round(n * (per_in + per_out) / t_s / 1e9, 2),
+                    "peak": round(n * (per_in + per_out) / max(t_up, t_down) / 1e9, 2), "unit": "GB/s",
+                    "frac": round(max(t_up, t_down) / t_s, 4),
+                    "components": {"h2d": {"gbs": bw["h2d"], "frac": round(t_up / t_s, 4)},
+                                   "d2h": {"gbs": bw["d2h"], "frac": round(t_down / t_s, 4)}}}
         if pf6:
             conf.update(dyn6_prefixes=len(P.dyn6), fix6_prefixes=len(P.fix6),
                         endpoints=len(P.ep6))
@@ -703,19 +813,18 @@ def main():
             "dtype": "u8" if pf6 else "u32",
             "data": "synthetic (seeded PCG64 tables + tuples, SURVEY §8d)",
             "config": conf,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "traffic_source": traffic_note,
-                         "traffic_dominant_kernel": traffic_dom,
-                         # achieved counts ALGORITHMIC bytes (64 B per reference map
-                         # lookup); the HBM-side rate from the PMC traffic says how
-                         # much of the 8 TB/s the kernel really moves: the tables
-                         # are mostly L2 / MALL hits, so the kernel is bound by
-                         # gather latency and memory-side atomics, not bandwidth
-                         "basis": "B_alg (columns + 64 B per reference map lookup)",
-                         "hbm_side_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                           if traffic else None)},
+            "roofline": dict(roof or {"bound": None, "note": "profiles/ceilings.json absent"},
+                             traffic=traffic, traffic_source=traffic_note,
+                             traffic_dominant_kernel=traffic_dom,
+                             hbm_side_frac=(round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                            if traffic else None),
+                             # the round-1..4 model, kept for comparison: 64 B per
+                             # reference lookup against the 8 TB/s HBM peak; it is
+                             # not a bound (the tables are L2 / MALL hits), so
+                             # it can exceed 1
+                             b_alg={"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                    "basis": "B_alg (columns + 64 B per reference map lookup)"}),
             "cpu_baseline": cpu,
         }
         if not parity:

@@ -149,6 +149,7 @@ PROTOS = {
     "cgpu_lxc_lookup": (i32, [vp, u32, vp]),
     "cgpu_frames_parse": (i32, [vp, C.POINTER(Frames), sz, C.POINTER(FrameTuples), vp]),
     "cgpu_classify_frames": (i32, [vp, C.POINTER(Frames), sz, vp, vp, vp, vp]),
+    "cgpu_classify_frames_host": (i32, [vp, C.POINTER(Frames), sz, vp, vp, vp, vp]),
     "cgpu_ct4_update": (i32, [vp, vp, vp, u64]),
     "cgpu_ct4_delete": (i32, [vp, vp]),
     "cgpu_ct4_lookup": (i32, [vp, vp, vp]),
@@ -175,6 +176,9 @@ PROTOS = {
     "cgpu_metrics_read": (i32, [vp, vp]),
     "cgpu_counters_reset": (i32, [vp]),
     "cgpu_stream_release": (i32, [vp, vp]),
+    "cgpu_host_stage_release": (i32, [vp]),
+    "cgpu_table_bytes": (i32, [vp, vp]),
+    "cgpu_host_stage_bytes": (sz, [vp]),
     "cgpu_counters_rebalance": (i32, [vp, C.POINTER(u64)]),
     "cgpu_comm_id_create": (i32, [vp]),
     "cgpu_comm_init": (i32, [vp, vp, i32, i32]),

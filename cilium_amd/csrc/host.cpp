@@ -1884,12 +1884,11 @@ struct cgpu_ctx {
 	/* ---- conntrack maps cilium_ct4_global / cilium_ct6_global ---- */
 	CtMap ct4, ct6;
 	void *d_ct_scratch = nullptr;
-	/* host-resident batches (cgpu_classify_v4_host): device staging for up
-	 * to HS_NBUF chunks (grown to the largest batch seen), one stream per
-	 * direction */
+	/* host-resident batches (cgpu_classify_v4_host / _frames_host): device
+	 * staging for up to HS_NBUF chunks (grown to the largest batch seen,
+	 * freed by cgpu_host_stage_release), one stream per direction */
 	std::mutex host_mu;
 	struct {
-		size_t chunk = 0;
 		int nb = 0;
 		void *d_in[16] = {}, *d_out[16] = {};
 		hipStream_t h2d = nullptr, d2h = nullptr;
@@ -2119,6 +2118,34 @@ CGPU_EXPORT int cgpu_ctx_create(const cgpu_config *cfg, int device, cgpu_ctx **o
 
 static void comm_destroy(cgpu_ctx *c);
 
+/* the host-batch staging (cgpu_classify_v4_host / _frames_host): waits for
+ * every upload, classify and store queued on it, then frees it (the next host
+ * call allocates again) */
+static void host_stage_free(cgpu_ctx *c)
+{
+	auto &H = c->hs;
+	if (H.h2d)
+		(void)hipStreamSynchronize(H.h2d);
+	if (H.d2h)
+		(void)hipStreamSynchronize(H.d2h);
+	for (int b = 0; b < H.nb; b++) {
+		(void)hipEventSynchronize(H.ev_cls[b]);
+		(void)hipFree(H.d_in[b]);
+		(void)hipFree(H.d_out[b]);
+		(void)hipEventDestroy(H.ev_in[b]);
+		(void)hipEventDestroy(H.ev_cls[b]);
+		(void)hipEventDestroy(H.ev_out[b]);
+		H.d_in[b] = H.d_out[b] = nullptr;
+		H.ev_in[b] = H.ev_cls[b] = H.ev_out[b] = nullptr;
+	}
+	H.nb = 0;
+	if (H.h2d)
+		(void)hipStreamDestroy(H.h2d);
+	if (H.d2h)
+		(void)hipStreamDestroy(H.d2h);
+	H.h2d = H.d2h = nullptr;
+}
+
 CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 {
 	if (!c)
@@ -2159,19 +2186,7 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 			(void)hipFree(m->d_count);
 		}
 		(void)hipFree(c->d_ct_scratch);
-		if (c->hs.chunk) {
-			(void)hipStreamSynchronize(c->hs.h2d);
-			(void)hipStreamSynchronize(c->hs.d2h);
-			for (int b = 0; b < c->hs.nb; b++) {
-				(void)hipFree(c->hs.d_in[b]);
-				(void)hipFree(c->hs.d_out[b]);
-				(void)hipEventDestroy(c->hs.ev_in[b]);
-				(void)hipEventDestroy(c->hs.ev_cls[b]);
-				(void)hipEventDestroy(c->hs.ev_out[b]);
-			}
-			(void)hipStreamDestroy(c->hs.h2d);
-			(void)hipStreamDestroy(c->hs.d2h);
-		}
+		host_stage_free(c);
 		(void)hipEventDestroy(c->ct_done);
 		(void)hipStreamDestroy(c->ct_stream);
 		(void)hipStreamDestroy(c->ustream);
@@ -3841,6 +3856,23 @@ CGPU_EXPORT int cgpu_table_checksum(cgpu_ctx *c, uint64_t *sum)
 	return 0;
 }
 
+CGPU_EXPORT int cgpu_table_bytes(cgpu_ctx *c, uint64_t *out)
+{
+	if (!c || !out)
+		return fail(-EINVAL, "null argument");
+	static_assert(G_N == CGPU_TBL_CT4, "table groups of cgpu.h");
+	std::shared_ptr<Epoch> ep;
+	{
+		std::lock_guard<std::mutex> g(c->pub_mu);
+		ep = c->cur;
+	}
+	for (int k = 0; k < G_N; k++)
+		out[k] = ep && ep->bufs[k] ? (uint64_t)ep->bufs[k]->bytes : 0u;
+	out[CGPU_TBL_CT4] = (uint64_t)(c->ct4.keys.size() + c->ct4.vals.size()) * 16u;
+	out[CGPU_TBL_CT6] = (uint64_t)(c->ct6.keys.size() + c->ct6.vals.size()) * 16u;
+	return 0;
+}
+
 /* Popularity-ordered counter slots.  Counter slots [0, hot_cap) accumulate
  * in LDS per workgroup (one flush per workgroup), the rest cost one global
  * atomic per hit that the workgroup's small LDS cache misses; slots are first
@@ -4181,39 +4213,60 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
 }
 
 /* ---- host-resident batches (host or device pointers) ----
- * The batch streams through two device staging buffers of HS_CHUNK tuples:
+ * The batch streams through device staging buffers of one chunk each:
  * chunk k's columns go up on the h2d stream, its classify runs on the
  * caller's stream, its outputs come back on the d2h stream, so chunk k + 1's
  * upload and chunk k - 1's download overlap chunk k's classify. */
 #define HS_CHUNK (1u << 22)
 #define HS_NBUF 16
+/* one staging pair holds HS_CHUNK v4 tuples (18 B in, 9 B out) in
+ * 256-aligned columns; a wider tuple (frames) takes fewer per chunk */
+#define HS_IN_BYTES ((size_t)HS_CHUNK * 18 + 8 * 256)
+#define HS_OUT_BYTES ((size_t)HS_CHUNK * 9 + 4 * 256)
 #ifndef CGPU_HS_STORE
 #define CGPU_HS_STORE 1
 #endif
 
-static size_t hs_in_off(size_t m, int col)
+/* a host batch: its input and output columns and their bytes per tuple */
+struct hs_cols {
+	int nin = 0, nout = 0;
+	const uint8_t *in[8] = {};
+	size_t in_el[8] = {};
+	uint8_t *out[8] = {}; /* null: output not requested */
+	size_t out_el[8] = {};
+};
+
+static size_t hs_off(const size_t *el, size_t m, int col)
 {
-	/* saddr, daddr, dport, proto, flags, len, ep; each column 256-aligned */
-	static const size_t el[7] = {4, 4, 2, 1, 1, 4, 2};
 	size_t o = 0;
 	for (int k = 0; k < col; k++)
 		o += (m * el[k] + 255) & ~(size_t)255;
 	return o;
 }
 
-static size_t hs_out_off(size_t m, int col)
+/* tuples per chunk: what one staging pair holds, a multiple of 4096 (so
+ * every column of chunk k starts 16-byte aligned in the caller's buffers
+ * whenever the column does) */
+static size_t hs_chunk(const hs_cols &C)
 {
-	static const size_t el[3] = {4, 4, 1}; /* verdict, identity, stage */
-	size_t o = 0;
-	for (int k = 0; k < col; k++)
-		o += (m * el[k] + 255) & ~(size_t)255;
-	return o;
+	size_t pin = 0, pout = 0;
+	for (int k = 0; k < C.nin; k++)
+		pin += C.in_el[k];
+	for (int k = 0; k < C.nout; k++)
+		pout += C.out_el[k];
+	size_t m = HS_CHUNK;
+	m = std::min(m, (HS_IN_BYTES - (size_t)256 * C.nin) / std::max<size_t>(pin, 1));
+	m = std::min(m, (HS_OUT_BYTES - (size_t)256 * C.nout) / std::max<size_t>(pout, 1));
+	return m & ~(size_t)4095;
 }
 
+/* grow the staging to min(nch, HS_NBUF) buffers.  A failed allocation rolls
+ * back that buffer; the call then runs on the buffers it has (any number >= 1
+ * is correct: chunk k uses buffer k % nb). */
 static int host_stage_init(cgpu_ctx *c, size_t nch)
 {
 	auto &H = c->hs;
-	if (!H.chunk) {
+	if (!H.h2d) {
 		/* the copy streams in priority classes of their own, non-blocking:
 		 * the runtime spreads plain streams over the process's few hardware
 		 * queues round robin, and an upload stream that landed on the
@@ -4222,17 +4275,37 @@ static int host_stage_init(cgpu_ctx *c, size_t nch)
 		int least = 0, greatest = 0;
 		HIP_OR_EIO(hipDeviceGetStreamPriorityRange(&least, &greatest));
 		HIP_OR_EIO(hipStreamCreateWithPriority(&H.h2d, hipStreamNonBlocking, greatest));
-		HIP_OR_EIO(hipStreamCreateWithPriority(&H.d2h, hipStreamNonBlocking, least));
-		H.chunk = HS_CHUNK;
+		if (hipStreamCreateWithPriority(&H.d2h, hipStreamNonBlocking, least) != hipSuccess) {
+			(void)hipGetLastError();
+			(void)hipStreamDestroy(H.h2d);
+			H.h2d = nullptr;
+			return fail(-EIO, "host staging stream creation failed");
+		}
 	}
 	const int want = (int)std::min<size_t>(nch, HS_NBUF);
-	for (; H.nb < want; H.nb++) {
-		const int b = H.nb;
-		HIP_OR_EIO(hipMalloc(&H.d_in[b], hs_in_off(HS_CHUNK, 7)));
-		HIP_OR_EIO(hipMalloc(&H.d_out[b], hs_out_off(HS_CHUNK, 3)));
-		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_in[b], hipEventDisableTiming));
-		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_cls[b], hipEventDisableTiming));
-		HIP_OR_EIO(hipEventCreateWithFlags(&H.ev_out[b], hipEventDisableTiming));
+	while (H.nb < want) {
+		void *in = nullptr, *out = nullptr;
+		hipEvent_t ev[3] = {};
+		bool ok = hipMalloc(&in, HS_IN_BYTES) == hipSuccess && hipMalloc(&out, HS_OUT_BYTES) == hipSuccess;
+		for (int k = 0; ok && k < 3; k++)
+			ok = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) == hipSuccess;
+		if (!ok) {
+			(void)hipGetLastError();
+			(void)hipFree(in);
+			(void)hipFree(out);
+			for (hipEvent_t e : ev)
+				if (e)
+					(void)hipEventDestroy(e);
+			if (H.nb)
+				break;
+			return fail(-ENOMEM, "host staging allocation failed");
+		}
+		const int b = H.nb++;
+		H.d_in[b] = in;
+		H.d_out[b] = out;
+		H.ev_in[b] = ev[0];
+		H.ev_cls[b] = ev[1];
+		H.ev_out[b] = ev[2];
 	}
 	return 0;
 }
@@ -4240,12 +4313,12 @@ static int host_stage_init(cgpu_ctx *c, size_t nch)
 /* the device address of a page-locked host range [p, p + bytes), or null
  * when the range is not page-locked host memory the device maps (both ends
  * checked) */
-static void *host_mapped(void *p, size_t bytes)
+static void *host_mapped(const void *p, size_t bytes)
 {
 	if (!p || !bytes)
 		return nullptr;
 	hipPointerAttribute_t a0{}, a1{};
-	char *last = static_cast<char *>(p) + bytes - 1;
+	const char *last = static_cast<const char *>(p) + bytes - 1;
 	if (hipPointerGetAttributes(&a0, p) != hipSuccess || hipPointerGetAttributes(&a1, last) != hipSuccess) {
 		(void)hipGetLastError();
 		return nullptr;
@@ -4254,6 +4327,139 @@ static void *host_mapped(void *p, size_t bytes)
 	    static_cast<char *>(a1.devicePointer) != static_cast<char *>(a0.devicePointer) + bytes - 1)
 		return nullptr;
 	return a0.devicePointer;
+}
+
+/* The pipeline of a host batch.  classify(m, din, dout) enqueues one chunk's
+ * work on cs over device columns.  Page-locked, mapped columns are read and
+ * written by the CUs, all columns of a chunk in one launch (a DMA copy's wait
+ * on another stream's event, and in this runtime the copy itself, held the
+ * issuing thread; a DMA download ran at a quarter of the link rate beside the
+ * uploads, profiles/r4_ah); other columns are copied by the runtime.
+ * Called with host_mu held. */
+template <typename F>
+static int host_pipeline(cgpu_ctx *c, size_t n, const hs_cols &C, hipStream_t cs, F &&classify)
+{
+	auto &H = c->hs;
+	const size_t chunk = hs_chunk(C);
+	if (!chunk)
+		return fail(-EINVAL, "tuple too wide for the host staging");
+	const size_t nch = (n + chunk - 1) / chunk;
+	if (int r = host_stage_init(c, nch))
+		return r;
+	const size_t nb = (size_t)H.nb;
+	/* after an error past the first enqueue, every copy already queued still
+	 * reads or writes the caller's buffers: wait for them before returning */
+	struct Drain {
+		cgpu_ctx *c;
+		bool armed = false;
+		~Drain()
+		{
+			if (armed) {
+				(void)hipStreamSynchronize(c->hs.h2d);
+				(void)hipStreamSynchronize(c->hs.d2h);
+			}
+		}
+	} drain{c};
+	const uint8_t *src_dev[8] = {};
+	uint8_t *dst_dev[8] = {};
+	for (int k = 0; k < C.nin; k++)
+		src_dev[k] = static_cast<const uint8_t *>(host_mapped(C.in[k], n * C.in_el[k]));
+	for (int k = 0; k < C.nout; k++)
+		dst_dev[k] = C.out[k] ? static_cast<uint8_t *>(host_mapped(C.out[k], n * C.out_el[k])) : nullptr;
+	auto aligned = [](const void *p) { return !(reinterpret_cast<uintptr_t>(p) & 15u); };
+	/* one launch for the mapped columns; the others (and, should the launch
+	 * fail, those too) by the runtime's copy on the same stream */
+	auto move = [&](hipStream_t st, hipMemcpyKind kind, int ncol, void *const *dst, const void *const *src,
+			void *const *dst_mapped, const void *const *src_mapped, const size_t *bytes) -> int {
+		copy_segs d{};
+		int which[8];
+		for (int col = 0; col < ncol; col++) {
+			if (!bytes[col])
+				continue;
+			void *dd = dst_mapped ? dst_mapped[col] : dst[col];
+			const void *ss = src_mapped ? src_mapped[col] : src[col];
+			if (CGPU_HS_STORE && dd && ss && aligned(dd) && aligned(ss)) {
+				which[d.n] = col;
+				d.seg[d.n++] = copy_seg{dd, ss, bytes[col]};
+				continue;
+			}
+			HIP_OR_EIO(hipMemcpyAsync(dst[col], src[col], bytes[col], kind, st));
+		}
+		if (d.n && launch_copy_host_multi(d, st) != hipSuccess) {
+			(void)hipGetLastError();
+			for (uint32_t j = 0; j < d.n; j++)
+				HIP_OR_EIO(hipMemcpyAsync(dst[which[j]], src[which[j]], bytes[which[j]], kind, st));
+		}
+		return 0;
+	};
+	/* chunk k's columns up on the h2d stream into buffer k % nb, free once
+	 * that buffer's last classify ran (in this call or an earlier one; an
+	 * event never recorded is no wait) */
+	auto upload = [&](size_t k) -> int {
+		const size_t off = k * chunk, m = std::min(chunk, n - off), b = k % nb;
+		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]);
+		HIP_OR_EIO(hipStreamWaitEvent(H.h2d, H.ev_cls[b], 0));
+		void *dst[8];
+		const void *src[8], *src_m[8];
+		size_t bytes[8];
+		for (int col = 0; col < C.nin; col++) {
+			dst[col] = in + hs_off(C.in_el, m, col);
+			src[col] = C.in[col] + off * C.in_el[col];
+			src_m[col] = src_dev[col] ? src_dev[col] + off * C.in_el[col] : nullptr;
+			bytes[col] = m * C.in_el[col];
+		}
+		drain.armed = true;
+		if (int r = move(H.h2d, hipMemcpyHostToDevice, C.nin, dst, src, nullptr, src_m, bytes))
+			return r;
+		HIP_OR_EIO(hipEventRecord(H.ev_in[b], H.h2d));
+		return 0;
+	};
+	/* every upload that has a buffer of its own is queued first, so the
+	 * h2d stream runs back to back (the runtime resolves a copy's wait on
+	 * another stream's event on the issuing thread: an upload queued behind
+	 * a download's wait on a classify stalled until that classify ended,
+	 * profiles/r4_ah); past nb chunks, chunk k + nb goes up once chunk k's
+	 * classify is queued */
+	for (size_t k = 0; k < std::min(nch, nb); k++)
+		if (int r = upload(k))
+			return r;
+	for (size_t k = 0; k < nch; k++) {
+		const size_t off = k * chunk, m = std::min(chunk, n - off), b = k % nb;
+		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]), *out = static_cast<uint8_t *>(H.d_out[b]);
+		/* classify on the caller's stream once the columns landed and the
+		 * output buffer drained (its last download) */
+		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_in[b], 0));
+		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
+		uint8_t *din[8], *dout[8];
+		for (int col = 0; col < C.nin; col++)
+			din[col] = in + hs_off(C.in_el, m, col);
+		for (int col = 0; col < C.nout; col++)
+			dout[col] = C.out[col] ? out + hs_off(C.out_el, m, col) : nullptr;
+		if (int r = classify(m, din, dout))
+			return r;
+		HIP_OR_EIO(hipEventRecord(H.ev_cls[b], cs));
+		if (k + nb < nch)
+			if (int r = upload(k + nb))
+				return r;
+		HIP_OR_EIO(hipStreamWaitEvent(H.d2h, H.ev_cls[b], 0));
+		void *dst[8], *dst_m[8];
+		const void *src[8];
+		size_t bytes[8];
+		for (int col = 0; col < C.nout; col++) {
+			dst[col] = C.out[col] ? C.out[col] + off * C.out_el[col] : nullptr;
+			dst_m[col] = dst_dev[col] ? dst_dev[col] + off * C.out_el[col] : nullptr;
+			src[col] = dout[col];
+			bytes[col] = C.out[col] ? m * C.out_el[col] : 0;
+		}
+		if (int r = move(H.d2h, hipMemcpyDeviceToHost, C.nout, dst, src, dst_m, nullptr, bytes))
+			return r;
+		HIP_OR_EIO(hipEventRecord(H.ev_out[b], H.d2h));
+	}
+	/* the caller's stream completes once the last outputs are in host memory */
+	for (size_t b = 0; b < nb && b < nch; b++)
+		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
+	drain.armed = false;
+	return 0;
 }
 
 CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
@@ -4269,101 +4475,56 @@ CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size
 	if (!n)
 		return 0;
 	std::lock_guard<std::mutex> g(c->host_mu);
-	HIP_OR_EIO(hipSetDevice(c->device));
-	const size_t nch = (n + HS_CHUNK - 1) / HS_CHUNK;
-	if (int r = host_stage_init(c, nch))
+	/* ONE snapshot and one packed-counter buffer for the whole batch: a
+	 * commit from another thread between chunks cannot split it */
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
 		return r;
-	auto &H = c->hs;
+	const cgpu_snapshot &s = P.snap();
 	const hipStream_t cs = (hipStream_t)stream;
-	const size_t nb = (size_t)H.nb;
+	hs_cols C;
+	C.nin = 7;
+	const void *cols[7] = {t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep};
 	static const size_t el[7] = {4, 4, 2, 1, 1, 4, 2};
-	/* the columns read by the CUs when page-locked and mapped (a DMA copy's
-	 * wait on another stream's event, and in this runtime the copy itself,
-	 * held the issuing thread, profiles/r4_ah), else copied */
-	const void *const cols[7] = {t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep};
-	const uint8_t *src_dev[7];
-	for (int col = 0; col < 7; col++)
-		src_dev[col] = static_cast<const uint8_t *>(host_mapped(const_cast<void *>(cols[col]), n * el[col]));
-	/* chunk k's columns up on the h2d stream into buffer k % nb, free once
-	 * that buffer's last classify ran (in this call or an earlier one; an
-	 * event never recorded is no wait) */
-	auto upload = [&](size_t k) -> int {
-		const size_t off = k * H.chunk, m = std::min<size_t>(H.chunk, n - off);
-		const size_t b = k % nb;
-		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]);
-		HIP_OR_EIO(hipStreamWaitEvent(H.h2d, H.ev_cls[b], 0));
-		const void *src[7] = {t->saddr + off, t->daddr + off, t->dport + off, t->proto + off,
-				      t->flags + off, t->len + off, t->ep + off};
-		for (int col = 0; col < 7; col++) {
-			if (src_dev[col] && CGPU_HS_STORE &&
-			    launch_copy_host(in + hs_in_off(m, col), src_dev[col] + off * el[col], m * el[col], H.h2d) ==
-				    hipSuccess)
-				continue;
-			(void)hipGetLastError();
-			HIP_OR_EIO(hipMemcpyAsync(in + hs_in_off(m, col), src[col], m * el[col], hipMemcpyHostToDevice,
-						  H.h2d));
-		}
-		HIP_OR_EIO(hipEventRecord(H.ev_in[b], H.h2d));
-		return 0;
-	};
-	/* outputs: stored by the CUs into the caller's buffers when they are
-	 * page-locked and mapped (a DMA download ran at a quarter of the link
-	 * rate beside the uploads, profiles/r4_ah), else downloaded */
-	int32_t *v_dev = static_cast<int32_t *>(host_mapped(verdict, n * 4));
-	uint32_t *i_dev = static_cast<uint32_t *>(host_mapped(identity, n * 4));
-	uint8_t *s_dev = stage ? static_cast<uint8_t *>(host_mapped(stage, n)) : nullptr;
-	auto download = [&](void *dst_host, void *dst_dev, const void *src, size_t bytes) -> int {
-		if (dst_dev && CGPU_HS_STORE && launch_copy_host(dst_dev, src, bytes, H.d2h) == hipSuccess)
-			return 0;
-		(void)hipGetLastError();
-		HIP_OR_EIO(hipMemcpyAsync(dst_host, src, bytes, hipMemcpyDeviceToHost, H.d2h));
-		return 0;
-	};
-	/* every upload that has a buffer of its own is queued first, so the
-	 * h2d stream runs back to back (the runtime resolves a copy's wait on
-	 * another stream's event on the issuing thread: an upload queued behind
-	 * a download's wait on a classify stalled until that classify ended,
-	 * profiles/r4_ah); past HS_NBUF chunks, chunk k + nb goes up once chunk
-	 * k's classify is queued */
-	for (size_t k = 0; k < std::min(nch, nb); k++)
-		if (int r = upload(k))
-			return r;
-	for (size_t k = 0; k < nch; k++) {
-		const size_t off = k * H.chunk, m = std::min<size_t>(H.chunk, n - off);
-		const size_t b = k % nb;
-		uint8_t *in = static_cast<uint8_t *>(H.d_in[b]), *out = static_cast<uint8_t *>(H.d_out[b]);
-		/* classify on the caller's stream once the columns landed and the
-		 * output buffer drained (its last download) */
-		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_in[b], 0));
-		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
-		const cgpu_tuples_v4 dt{reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 0)),
-					reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 1)),
-					reinterpret_cast<const uint16_t *>(in + hs_in_off(m, 2)), in + hs_in_off(m, 3),
-					in + hs_in_off(m, 4), reinterpret_cast<const uint32_t *>(in + hs_in_off(m, 5)),
-					reinterpret_cast<const uint16_t *>(in + hs_in_off(m, 6))};
-		int32_t *dv = reinterpret_cast<int32_t *>(out + hs_out_off(m, 0));
-		uint32_t *di = reinterpret_cast<uint32_t *>(out + hs_out_off(m, 1));
-		uint8_t *ds = stage ? out + hs_out_off(m, 2) : nullptr;
-		if (int r = cgpu_classify_v4(c, &dt, m, dv, di, ds, stream))
-			return r;
-		HIP_OR_EIO(hipEventRecord(H.ev_cls[b], cs));
-		if (k + nb < nch)
-			if (int r = upload(k + nb))
-				return r;
-		HIP_OR_EIO(hipStreamWaitEvent(H.d2h, H.ev_cls[b], 0));
-		if (int r = download(verdict + off, v_dev ? v_dev + off : nullptr, dv, m * 4))
-			return r;
-		if (int r = download(identity + off, i_dev ? i_dev + off : nullptr, di, m * 4))
-			return r;
-		if (stage)
-			if (int r = download(stage + off, s_dev ? s_dev + off : nullptr, ds, m))
-				return r;
-		HIP_OR_EIO(hipEventRecord(H.ev_out[b], H.d2h));
+	for (int k = 0; k < 7; k++) {
+		C.in[k] = static_cast<const uint8_t *>(cols[k]);
+		C.in_el[k] = el[k];
 	}
-	/* the caller's stream completes once the last outputs are in host memory */
-	for (size_t b = 0; b < nb && b < nch; b++)
-		HIP_OR_EIO(hipStreamWaitEvent(cs, H.ev_out[b], 0));
+	C.nout = 3;
+	C.out[0] = reinterpret_cast<uint8_t *>(verdict);
+	C.out[1] = reinterpret_cast<uint8_t *>(identity);
+	C.out[2] = stage;
+	C.out_el[0] = C.out_el[1] = 4;
+	C.out_el[2] = 1;
+	return host_pipeline(c, n, C, cs, [&](size_t m, uint8_t *const *di, uint8_t *const *dout) -> int {
+		classify_v4_args a{reinterpret_cast<const uint32_t *>(di[0]), reinterpret_cast<const uint32_t *>(di[1]),
+				   reinterpret_cast<const uint16_t *>(di[2]), di[3], di[4],
+				   reinterpret_cast<const uint32_t *>(di[5]), reinterpret_cast<const uint16_t *>(di[6]),
+				   reinterpret_cast<int32_t *>(dout[0]), reinterpret_cast<uint32_t *>(dout[1]), dout[2],
+				   P.delta, (uint64_t)m, P.pk, 0, nullptr, nullptr};
+		HIP_OR_EIO(launch_classify_v4(s, a, cs));
+		return 0;
+	});
+}
+
+CGPU_EXPORT int cgpu_host_stage_release(cgpu_ctx *c)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (c->device < 0)
+		return 0;
+	std::lock_guard<std::mutex> g(c->host_mu);
+	HIP_OR_EIO(hipSetDevice(c->device));
+	host_stage_free(c);
 	return 0;
+}
+
+CGPU_EXPORT size_t cgpu_host_stage_bytes(cgpu_ctx *c)
+{
+	if (!c)
+		return 0;
+	std::lock_guard<std::mutex> g(c->host_mu);
+	return (size_t)c->hs.nb * (HS_IN_BYTES + HS_OUT_BYTES);
 }
 
 CGPU_EXPORT int cgpu_classify_v4_lb(cgpu_ctx *c, const cgpu_tuples_v4 *t, const uint16_t *sport,
@@ -4509,25 +4670,14 @@ CGPU_EXPORT int cgpu_frames_parse(cgpu_ctx *c, const cgpu_frames *f, size_t n,
 	return 0;
 }
 
-CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n, int32_t *verdict,
-				     uint32_t *identity, uint8_t *stage, void *stream)
+/* cgpu_classify_frames' launches on a pinned snapshot (device columns) */
+static int frames_enqueue(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, uint64_t *pk,
+			  const cgpu_frames *f, size_t n, int32_t *verdict, uint32_t *identity, uint8_t *stage,
+			  hipStream_t st)
 {
-	Pinned P;
-	if (int r = pin(c, stream, P, true))
-		return r;
-	const cgpu_snapshot &s = P.snap();
-	uint64_t *delta = P.delta;
-	if (int r = frames_check(c, f, n))
-		return r;
-	if (n && (!verdict || !identity))
-		return fail(-EINVAL, "null output");
-	if (!n)
-		return 0;
 	frames_args a{f->data, f->len, f->flags, f->ep, f->stride, (uint64_t)n,
 		      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-		      verdict, identity, stage, delta, P.pk};
-	HIP_OR_EIO(hipSetDevice(c->device));
-	const hipStream_t st = (hipStream_t)stream;
+		      verdict, identity, stage, delta, pk};
 	const bool x4 = !(s.schedule & (CGPU_SCHED_PER_LANE | CGPU_SCHED_GLOBAL_CTR)) &&
 			!(((uintptr_t)f->len | (uintptr_t)verdict | (uintptr_t)identity) & 15) &&
 			!((uintptr_t)f->ep & 7) && !((uintptr_t)stage & 3);
@@ -4543,6 +4693,65 @@ CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n
 	HIP_OR_EIO(hipFreeAsync(scr, st));
 	HIP_OR_EIO(e);
 	return 0;
+}
+
+CGPU_EXPORT int cgpu_classify_frames(cgpu_ctx *c, const cgpu_frames *f, size_t n, int32_t *verdict,
+				     uint32_t *identity, uint8_t *stage, void *stream)
+{
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
+		return r;
+	if (int r = frames_check(c, f, n))
+		return r;
+	if (n && (!verdict || !identity))
+		return fail(-EINVAL, "null output");
+	if (!n)
+		return 0;
+	HIP_OR_EIO(hipSetDevice(c->device));
+	return frames_enqueue(c, P.snap(), P.delta, P.pk, f, n, verdict, identity, stage, (hipStream_t)stream);
+}
+
+CGPU_EXPORT int cgpu_classify_frames_host(cgpu_ctx *c, const cgpu_frames *f, size_t n, int32_t *verdict,
+					  uint32_t *identity, uint8_t *stage, void *stream)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (int r = frames_check(c, f, n))
+		return r;
+	if (n && (!verdict || !identity))
+		return fail(-EINVAL, "null output");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device (host-only); no CPU path");
+	if (!n)
+		return 0;
+	std::lock_guard<std::mutex> g(c->host_mu);
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
+		return r;
+	const cgpu_snapshot &s = P.snap();
+	const hipStream_t cs = (hipStream_t)stream;
+	hs_cols C;
+	C.nin = 4;
+	C.in[0] = f->data;
+	C.in_el[0] = f->stride;
+	C.in[1] = reinterpret_cast<const uint8_t *>(f->len);
+	C.in_el[1] = 4;
+	C.in[2] = f->flags;
+	C.in_el[2] = 1;
+	C.in[3] = reinterpret_cast<const uint8_t *>(f->ep);
+	C.in_el[3] = 2;
+	C.nout = 3;
+	C.out[0] = reinterpret_cast<uint8_t *>(verdict);
+	C.out[1] = reinterpret_cast<uint8_t *>(identity);
+	C.out[2] = stage;
+	C.out_el[0] = C.out_el[1] = 4;
+	C.out_el[2] = 1;
+	return host_pipeline(c, n, C, cs, [&](size_t m, uint8_t *const *di, uint8_t *const *dout) -> int {
+		const cgpu_frames df{di[0], reinterpret_cast<const uint32_t *>(di[1]), di[2],
+				     reinterpret_cast<const uint16_t *>(di[3]), f->stride, 0};
+		return frames_enqueue(c, s, P.delta, P.pk, &df, m, reinterpret_cast<int32_t *>(dout[0]),
+				      reinterpret_cast<uint32_t *>(dout[1]), dout[2], cs);
+	});
 }
 
 CGPU_EXPORT int cgpu_prefilter_v4(cgpu_ctx *c, const uint32_t *saddr, const uint32_t *daddr,

@@ -3688,6 +3688,48 @@ hipError_t launch_copy_host(void *dst, const void *src, uint64_t bytes, hipStrea
 	return hipGetLastError();
 }
 
+/* every column of a chunk in ONE launch: segment blockIdx.y, the blocks of
+ * a row grid-stride over it (a launch per column left ~10 us gaps between
+ * seven small kernels per chunk, profiles/r4_ah) */
+__global__ __launch_bounds__(256) void k_copy_host_multi(copy_segs d)
+{
+	const copy_seg g = d.seg[blockIdx.y];
+	const uint64_t n16 = g.bytes >> 4;
+	uint4 *dst = static_cast<uint4 *>(g.dst);
+	const uint4 *src = static_cast<const uint4 *>(g.src);
+	const uint64_t stride = (uint64_t)gridDim.x * 256u;
+	uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	for (; i + 3 * stride < n16; i += 4 * stride) {
+		const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], e = src[i + 3 * stride];
+		dst[i] = a;
+		dst[i + stride] = b;
+		dst[i + 2 * stride] = c;
+		dst[i + 3 * stride] = e;
+	}
+	for (; i < n16; i += stride)
+		dst[i] = src[i];
+	const uint32_t tail = (uint32_t)(g.bytes & 15u);
+	if (blockIdx.x == 0 && threadIdx.x < tail)
+		static_cast<uint8_t *>(g.dst)[(n16 << 4) + threadIdx.x] =
+			static_cast<const uint8_t *>(g.src)[(n16 << 4) + threadIdx.x];
+}
+
+hipError_t launch_copy_host_multi(const copy_segs &d, hipStream_t st)
+{
+	uint64_t most = 0;
+	for (uint32_t k = 0; k < d.n; k++) {
+		if ((reinterpret_cast<uintptr_t>(d.seg[k].dst) | reinterpret_cast<uintptr_t>(d.seg[k].src)) & 15u)
+			return hipErrorInvalidValue;
+		most = std::max(most, d.seg[k].bytes);
+	}
+	if (!d.n || !most)
+		return hipSuccess;
+	/* the longest segment sets the row width; shorter rows' spare blocks exit */
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((most >> 4) + 1023) / 1024, 128));
+	hipLaunchKernelGGL(k_copy_host_multi, dim3(g, d.n), dim3(256), 0, st, d);
+	return hipGetLastError();
+}
+
 hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *slot,
 			    const uint64_t *pk, const uint64_t *by, uint32_t n, hipStream_t st)
 {
@@ -4386,6 +4428,8 @@ __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, boo
 				r[2] = uint4{0u, 0u, 0u, 0u};
 				a.gkey[i] = SERIAL ? 0u : ct_fmix((uint32_t)i ^ 0x5bd1e995u);
 				a.idx[i] = (uint32_t)i;
+				if constexpr (!SERIAL)
+					a.pcls[i] = 0u; /* dropped: no phase-2 class (the scratch is reused) */
 				continue;
 			}
 			if ((so.x & 3u) == SVC_XLATED) {

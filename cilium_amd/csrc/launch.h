@@ -207,6 +207,17 @@ hipError_t launch_fold(uint64_t *totals, uint64_t *delta, uint64_t n, hipStream_
  * host range (either way); hipErrorInvalidValue unless dst and src are
  * 16-byte aligned */
 hipError_t launch_copy_host(void *dst, const void *src, uint64_t bytes, hipStream_t st);
+/* up to 8 such copies in one launch (every segment 16-byte aligned) */
+struct copy_seg {
+	void *dst;
+	const void *src;
+	uint64_t bytes;
+};
+struct copy_segs {
+	copy_seg seg[8];
+	uint32_t n;
+};
+hipError_t launch_copy_host_multi(const copy_segs &d, hipStream_t st);
 /* totals[2*slot[i]] = pk[i]; totals[2*slot[i]+1] = by[i]; delta[..] = 0 */
 hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *slot,
 			    const uint64_t *pk, const uint64_t *by, uint32_t n, hipStream_t st);

@@ -398,6 +398,15 @@ class Engine:
         (raises CgpuError EIO naming the group otherwise)."""
         check(self.L.cgpu_table_verify(self.h), "cgpu_table_verify")
 
+    TABLES = ("ipcache", "policy", "prefilter", "endpoint", "lb4", "lxc", "lb6", "ct4", "ct6")
+
+    def table_bytes(self) -> dict:
+        """cgpu_table_bytes: device bytes of each table group of the published
+        snapshot and of the conntrack maps."""
+        out = np.zeros(len(self.TABLES), np.uint64)
+        check(self.L.cgpu_table_bytes(self.h, out.ctypes.data_as(C.c_void_p)), "cgpu_table_bytes")
+        return {k: int(v) for k, v in zip(self.TABLES, out)}
+
     def counter_layout_checksum(self) -> int:
         s = C.c_uint64()
         check(self.L.cgpu_counter_layout_checksum(self.h, C.byref(s)), "cgpu_counter_layout_checksum")
@@ -684,6 +693,42 @@ class Engine:
                                           _ptr(out["identity"]), _ptr(out.get("stage")),
                                           _stream(stream)), "cgpu_classify_frames")
         return out
+
+    def classify_frames_host(self, f: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """cgpu_classify_frames_host: f holds HOST arrays (numpy, or CPU
+        tensors -- page-locked ones are read by the CUs) data (n, stride)
+        uint8, len, flags, ep; outputs are host arrays, complete when
+        `stream` is (synchronized here unless out is given)."""
+        import numpy as np
+        n = len(f["len"])
+
+        def ptr(x):
+            if x is None:
+                return None
+            return x.data_ptr() if hasattr(x, "data_ptr") else x.ctypes.data
+        data = f["data"]
+        assert data.ndim == 2 if hasattr(data, "ndim") else data.dim() == 2
+        given = out is not None
+        if out is None:
+            out = {"verdict": np.empty(n, np.int32), "identity": np.empty(n, np.uint32),
+                   "stage": np.empty(n, np.uint8) if stage else None}
+        fr = Frames(ptr(data), ptr(f["len"]), ptr(f["flags"]), ptr(f["ep"]), data.shape[1], 0)
+        check(self.L.cgpu_classify_frames_host(self.h, C.byref(fr), n, C.c_void_p(ptr(out["verdict"])),
+                                               C.c_void_p(ptr(out["identity"])),
+                                               C.c_void_p(ptr(out.get("stage"))), _stream(stream)),
+              "cgpu_classify_frames_host")
+        if not given:
+            import torch
+            (stream or torch.cuda.current_stream()).synchronize()
+        return out
+
+    def host_stage_release(self) -> None:
+        """cgpu_host_stage_release: free the host-batch device staging."""
+        check(self.L.cgpu_host_stage_release(self.h), "cgpu_host_stage_release")
+
+    def host_stage_bytes(self) -> int:
+        """cgpu_host_stage_bytes: device bytes the host-batch staging holds."""
+        return int(self.L.cgpu_host_stage_bytes(self.h))
 
     # ------------------------------------------------------------- counters
     def counter_delta_bytes(self) -> int:

@@ -394,6 +394,15 @@ int cgpu_commit(cgpu_ctx *ctx, uint64_t *epoch_out);
 /* order-independent checksum of the committed table contents; replicas on
  * different GPUs/ranks holding the same tables report the same value */
 int cgpu_table_checksum(cgpu_ctx *ctx, uint64_t *sum_out);
+/* Device bytes of every table group of the published snapshot (0 for a
+ * group never committed) and of the conntrack maps: what a lookup into each
+ * map gathers from (bench.py prices each map's lookups at the measured
+ * gather ceiling of the cache tier a table of that size lives in). */
+enum {
+	CGPU_TBL_IPCACHE = 0, CGPU_TBL_POLICY, CGPU_TBL_PREFILTER, CGPU_TBL_ENDPOINT, CGPU_TBL_LB4,
+	CGPU_TBL_LXC, CGPU_TBL_LB6, CGPU_TBL_CT4, CGPU_TBL_CT6, CGPU_TBL_N
+};
+int cgpu_table_bytes(cgpu_ctx *ctx, uint64_t *bytes_out /* [CGPU_TBL_N] */);
 /* Failure detection: every group buffer a commit uploads is
  * summed on the device and compared with the host image's sum before the
  * snapshot is published (a mismatch fails the commit with -EIO).  This call
@@ -453,6 +462,18 @@ int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *
  */
 int cgpu_classify_v4_host(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
 			  uint32_t *identity, uint8_t *stage, void *stream);
+/*
+ * A host call pins ONE snapshot for its whole batch: a cgpu_commit from
+ * another thread while the chunks are queued does not split the batch.  On
+ * an error after the first chunk was queued, the call waits for every copy
+ * it queued (they read and write the caller's buffers) before returning.
+ * The staging (up to 16 x ~109 MB of device memory) stays allocated for the
+ * next host call: cgpu_host_stage_bytes reports it, cgpu_host_stage_release
+ * waits for the host calls queued on it and frees it (cgpu_ctx_destroy does
+ * too).
+ */
+int cgpu_host_stage_release(cgpu_ctx *ctx);
+size_t cgpu_host_stage_bytes(cgpu_ctx *ctx);
 
 typedef struct cgpu_tuples_v6 {
 	const uint8_t *saddr;  /* 16 bytes per tuple, network order */
@@ -615,6 +636,17 @@ int cgpu_frames_parse(cgpu_ctx *ctx, const cgpu_frames *f, size_t n,
  */
 int cgpu_classify_frames(cgpu_ctx *ctx, const cgpu_frames *f, size_t n, int32_t *verdict,
 			 uint32_t *identity, uint8_t *stage, void *stream);
+
+/*
+ * cgpu_classify_frames over a HOST-resident batch (the frames as the NIC's
+ * receive ring holds them, bpf_xdp.c:181-184 / bpf_netdev.c:470): f's data,
+ * len, flags and ep and the outputs are host pointers; the batch streams
+ * through the staging of cgpu_classify_v4_host (~1M 64-byte slots per
+ * chunk), with its snapshot, error and completion rules.  Same results,
+ * counters and metrics as cgpu_classify_frames of the same frames.
+ */
+int cgpu_classify_frames_host(cgpu_ctx *ctx, const cgpu_frames *f, size_t n, int32_t *verdict,
+			      uint32_t *identity, uint8_t *stage, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* conntrack: the map cilium_ct4_global               */

@@ -361,7 +361,32 @@ struct or_ctx {
 	size_t ct6_max;
 	size_t ct_max;              /* CT_MAP_SIZE */
 	uint64_t metrics[N_METRICS];
+	uint64_t cls[OR_CLS_N];     /* reference map lookups by map since or_probe_split */
 };
+
+/* Reference map lookups counted per map (the roofline prices each map's
+ * lookups at the gather ceiling of the tier that holds it, bench.py):
+ * counted per thread where the lookup happens, moved into the context by
+ * cls_flush when a worker or a batch call ends.  Conntrack operations are
+ * the batch's probe_sum minus these. */
+static __thread uint64_t tl_cls[OR_CLS_N];
+
+static void cls_flush(or_ctx *c)
+{
+	for (int k = 0; k < OR_CLS_N; k++) {
+		if (tl_cls[k])
+			__atomic_fetch_add(&c->cls[k], tl_cls[k], __ATOMIC_RELAXED);
+		tl_cls[k] = 0;
+	}
+}
+
+void or_probe_split(or_ctx *c, uint64_t *out)
+{
+	cls_flush(c);
+	for (int k = 0; k < OR_CLS_N; k++) {
+		out[k] = __atomic_exchange_n(&c->cls[k], 0, __ATOMIC_RELAXED);
+	}
+}
 
 void or_default_config(or_config *cfg)
 {
@@ -442,6 +467,7 @@ or_ctx *or_view_create(or_ctx *base)
 	oh_init(&v->ct, 14, 56);
 	oh_init(&v->ct6, 38, 56);
 	memset(v->metrics, 0, sizeof(v->metrics));
+	memset(v->cls, 0, sizeof(v->cls));
 	return v;
 }
 
@@ -451,6 +477,10 @@ void or_view_merge(or_ctx *base, or_ctx *v)
 {
 	for (size_t i = 0; i < N_METRICS; i++)
 		base->metrics[i] += v->metrics[i];
+	for (int k = 0; k < OR_CLS_N; k++) {
+		base->cls[k] += v->cls[k];
+		v->cls[k] = 0;
+	}
 	for (size_t i = 0; i < v->ct.cap; i++)
 		if (v->ct.used[i])
 			oh_update(&base->ct, v->ct.keys + i * 14, v->ct.vals + i * 56);
@@ -577,6 +607,7 @@ int or_endpoint_delete(or_ctx *c, const void *key20)
  * key {prefixlen = 32 static + 32, pad = 0, family = ENDPOINT_KEY_IPV4, ip4}. */
 static const uint8_t *ipcache4(const or_ctx *c, uint32_t addr_be)
 {
+	tl_cls[OR_CLS_IPCACHE]++;
 	uint8_t key[24];
 	uint32_t plen = 64;
 	memset(key, 0, sizeof(key));
@@ -589,6 +620,7 @@ static const uint8_t *ipcache4(const or_ctx *c, uint32_t addr_be)
 /* ipcache_lookup6 (bpf/lib/eps.h:56-66): {prefixlen 32 + 128, family 2, ip6} */
 static const uint8_t *ipcache6(const or_ctx *c, const uint8_t *addr16)
 {
+	tl_cls[OR_CLS_IPCACHE]++;
 	uint8_t key[24];
 	uint32_t plen = 160;
 	memset(key, 0, sizeof(key));
@@ -622,6 +654,7 @@ static struct pol_res policy_access(struct ohash *h, uint32_t identity, uint16_t
 
 	if (!frag) { /* policy.h:61-72, exact L4 */
 		r.probes++;
+		tl_cls[OR_CLS_POLICY]++;
 		if (h && (e = oh_get(h, key))) {
 			__atomic_fetch_add((uint64_t *)(e + 8), 1, __ATOMIC_RELAXED);
 			__atomic_fetch_add((uint64_t *)(e + 16), (uint64_t)len, __ATOMIC_RELAXED);
@@ -634,6 +667,7 @@ static struct pol_res policy_access(struct ohash *h, uint32_t identity, uint16_t
 	/* policy.h:74-83, L3-only {id, 0, 0, dir} */
 	memset(key + 4, 0, 3);
 	r.probes++;
+	tl_cls[OR_CLS_POLICY]++;
 	if (h && (e = oh_get(h, key))) {
 		__atomic_fetch_add((uint64_t *)(e + 8), 1, __ATOMIC_RELAXED);
 		__atomic_fetch_add((uint64_t *)(e + 16), (uint64_t)len, __ATOMIC_RELAXED);
@@ -646,6 +680,7 @@ static struct pol_res policy_access(struct ohash *h, uint32_t identity, uint16_t
 		memcpy(key + 4, &dport, 2);
 		key[6] = proto;
 		r.probes++;
+		tl_cls[OR_CLS_POLICY]++;
 		if (h && (e = oh_get(h, key))) {
 			__atomic_fetch_add((uint64_t *)(e + 8), 1, __ATOMIC_RELAXED);
 			__atomic_fetch_add((uint64_t *)(e + 16), (uint64_t)len, __ATOMIC_RELAXED);
@@ -715,6 +750,7 @@ static const uint8_t *lb_get(const or_ctx *c, uint32_t addr, uint16_t dport, uin
 	memcpy(key + 4, &dport, 2);
 	memcpy(key + 6, &slave, 2);
 	(*probes)++;
+	tl_cls[OR_CLS_LB]++;
 	return oh_get(&c->lb, key);
 }
 
@@ -864,6 +900,7 @@ static const uint8_t *lb6_get(const or_ctx *c, const uint8_t *addr, uint16_t dpo
 	memcpy(key + 16, &dport, 2);
 	memcpy(key + 18, &slave, 2);
 	(*probes)++;
+	tl_cls[OR_CLS_LB]++;
 	return oh_get(&c->lb6, key);
 }
 
@@ -976,6 +1013,7 @@ static void *lb_worker(void *arg)
 		if (j->slave_out)
 			j->slave_out[i] = r.slave;
 	}
+	cls_flush((or_ctx *)j->c);
 	return NULL;
 }
 
@@ -1027,6 +1065,7 @@ int or_lb4(or_ctx *c, int mode, size_t n, const uint32_t *saddr, const uint32_t 
 			pthread_join(th[t], NULL);
 		probes += jobs[t].probes;
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = probes;
 	free(jobs);
@@ -1155,6 +1194,7 @@ static void *cls_worker(void *arg)
 			m[1] += j->len[i];
 		}
 	}
+	cls_flush((or_ctx *)j->c);
 	return NULL;
 }
 
@@ -1203,6 +1243,7 @@ static int classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_
 		for (int k = 0; k < N_METRICS; k++)
 			c->metrics[k] += jobs[t].metrics[k];
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = probes;
 	free(jobs);
@@ -1342,6 +1383,7 @@ static void *cls6_worker(void *arg)
 			m[1] += j->len[i];
 		}
 	}
+	cls_flush((or_ctx *)j->c);
 	return NULL;
 }
 
@@ -1390,6 +1432,7 @@ static int classify_v6(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_
 		for (int k = 0; k < N_METRICS; k++)
 			c->metrics[k] += jobs[t].metrics[k];
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = probes;
 	free(jobs);
@@ -1466,21 +1509,25 @@ static void *pf_worker(void *arg)
 		if (fix) { /* CIDR{4,6}_FILTER */
 			if (dyn) { /* CIDR{4,6}_LPM_PREFILTER */
 				j->probes++;
+				tl_cls[OR_CLS_PREFILTER]++;
 				if (lpm_lookup(j->v6 ? &c->dyn6 : &c->dyn4, pfx))
 					v = XDP_DROP;
 			}
 			if (!v) {
 				j->probes++;
+				tl_cls[OR_CLS_PREFILTER]++;
 				if (oh_get(j->v6 ? &c->fix6 : &c->fix4, pfx))
 					v = XDP_DROP;
 			}
 		}
 		if (!v) { /* check_v{4,6}_endpoint (bpf_xdp.c:88-95, :123-130) */
 			j->probes++;
+			tl_cls[OR_CLS_ENDPOINT]++;
 			v = oh_get(&c->lxc, ek) ? XDP_PASS : XDP_DROP;
 		}
 		j->verdict[i] = v;
 	}
+	cls_flush((or_ctx *)j->c);
 	return NULL;
 }
 
@@ -1519,6 +1566,7 @@ static int prefilter(or_ctx *c, int v6, size_t n, const uint32_t *s4, const uint
 			pthread_join(th[t], NULL);
 		probes += jobs[t].probes;
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = probes;
 	free(jobs);
@@ -1765,6 +1813,7 @@ static void *fp_worker(void *arg)
 	or_frames_parse(j->c, m, j->data + lo * j->stride, j->stride, j->len + lo, j->flags + lo,
 			j->ep + lo, j->st + lo, j->fam + lo, j->sa + 16 * lo, j->da + 16 * lo, j->dp + lo,
 			j->pr + lo, j->tf + lo);
+	cls_flush((or_ctx *)j->c);
 	return NULL;
 }
 
@@ -1860,6 +1909,7 @@ int or_classify_frames(or_ctx *c, size_t n, const uint8_t *data, uint32_t stride
 		c->metrics[(reason * 4 + dir) * 2] += 1;
 		c->metrics[(reason * 4 + dir) * 2 + 1] += len[i];
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = ps;
 	free(st); free(fam); free(sa); free(da); free(pr); free(tf); free(dp); free(idx);
@@ -2257,6 +2307,7 @@ int or_classify_v4_ct(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
 		}
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = ops;
 	return 0;
@@ -2587,6 +2638,7 @@ int or_classify_v4_ctlb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32
 			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
 		}
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = ops;
 	return 0;
@@ -2949,6 +3001,7 @@ int or_classify_v6_ct(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8_t
 			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
 		}
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = ops;
 	return 0;
@@ -3226,6 +3279,7 @@ int or_classify_v6_ctlb(or_ctx *c, size_t n, const uint8_t *saddr16, const uint8
 			c->metrics[(reason * 4 + mdir) * 2 + 1] += len[i];
 		}
 	}
+	cls_flush(c);
 	if (probe_sum)
 		*probe_sum = ops;
 	return 0;

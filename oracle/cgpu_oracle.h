@@ -42,6 +42,12 @@ void or_destroy(or_ctx *c);
 void or_set_config(or_ctx *c, const or_config *cfg);
 void or_default_config(or_config *cfg);
 
+/* reference map lookups of the batch calls since the last call, by map
+ * (bench.py's roofline prices each at its tier's gather ceiling); the
+ * conntrack operations are a call's probe_sum minus these.  Read and reset. */
+enum { OR_CLS_IPCACHE = 0, OR_CLS_POLICY, OR_CLS_LB, OR_CLS_PREFILTER, OR_CLS_ENDPOINT, OR_CLS_N };
+void or_probe_split(or_ctx *c, uint64_t *out /* [OR_CLS_N] */);
+
 /* table ops: 0 on success, -errno (bpf(2) convention) on failure */
 int or_ipcache_update(or_ctx *c, const void *key24, const void *val8);
 int or_ipcache_delete(or_ctx *c, const void *key24);

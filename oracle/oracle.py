@@ -117,6 +117,8 @@ def lib():
         L.or_view_destroy.argtypes = [vp]
         L.or_view_destroy.restype = None
         L.or_metrics_read.argtypes = [vp, vp]
+        L.or_probe_split.argtypes = [vp, vp]
+        L.or_probe_split.restype = None
         L.or_counters_reset.argtypes = [vp]
         _lib = L
     return _lib
@@ -583,6 +585,18 @@ class Oracle:
                             p(prog.rule_clauses), len(prog.rule_subject), p(prog.clauses), p(eo),
                             p(el), len(ep_sets), p(io), p(il), len(id_sets), flags, p(allow))
         return allow
+
+    PROBE_MAPS = ("ipcache", "policy", "lb", "prefilter", "endpoint")
+
+    def probe_split(self):
+        """Reference map lookups since the last call, by map (or_probe_split,
+        read and reset; after `sharded` the views' lookups are included):
+        the roofline prices each at the gather ceiling of its tier.  A
+        stateful call's conntrack operations are its probe count minus the
+        sum of these."""
+        out = np.zeros(len(self.PROBE_MAPS), np.uint64)
+        self.L.or_probe_split(self.h, _p(out))
+        return {k: int(v) for k, v in zip(self.PROBE_MAPS, out)}
 
     def metrics(self):
         out = np.zeros((256, 4, 2), np.uint64)

@@ -451,3 +451,35 @@ def test_host_batch_entry_errors():
     assert L_.cgpu_classify_v4_host(None, C.byref(tv), n, v.ctypes.data, i.ctypes.data, None,
                                     None) == -errno.EINVAL
     e.close()
+
+
+def test_frames_host_and_staging_entry_errors():
+    """cgpu_classify_frames_host: bad frame columns / stride / output are
+    -EINVAL, a host-only context -ENODEV; cgpu_host_stage_release and
+    cgpu_host_stage_bytes on a context that never staged anything; and
+    cgpu_table_bytes reports zeros before the first commit."""
+    from cilium_amd._abi import Frames
+    e = Engine(device=-1)
+    L_ = lib()
+    n = 4
+    data = np.zeros((n, 64), np.uint8)
+    ln = np.full(n, 60, np.uint32)
+    fl = np.zeros(n, np.uint8)
+    ep = np.zeros(n, np.uint16)
+    v = np.zeros(n, np.int32)
+    i = np.zeros(n, np.uint32)
+    fr = Frames(data.ctypes.data, ln.ctypes.data, fl.ctypes.data, ep.ctypes.data, 64, 0)
+    assert L_.cgpu_classify_frames_host(e.h, C.byref(fr), n, v.ctypes.data, i.ctypes.data, None,
+                                        None) == -errno.ENODEV
+    assert L_.cgpu_classify_frames_host(e.h, C.byref(fr), n, None, i.ctypes.data, None,
+                                        None) == -errno.EINVAL
+    bad = Frames(data.ctypes.data, ln.ctypes.data, fl.ctypes.data, ep.ctypes.data, 40, 0)
+    assert L_.cgpu_classify_frames_host(e.h, C.byref(bad), n, v.ctypes.data, i.ctypes.data, None,
+                                        None) == -errno.EINVAL
+    assert L_.cgpu_classify_frames_host(None, C.byref(fr), n, v.ctypes.data, i.ctypes.data, None,
+                                        None) == -errno.EINVAL
+    assert L_.cgpu_host_stage_release(e.h) == 0
+    assert L_.cgpu_host_stage_bytes(e.h) == 0
+    assert L_.cgpu_host_stage_release(None) == -errno.EINVAL
+    assert set(e.table_bytes().values()) == {0}
+    e.close()

@@ -235,6 +235,54 @@ def test_ctlb_phase2_and_serial(torch_cuda, cfg_ctlb):
     e.close()
 
 
+def test_ctlb_dropped_service_packets_after_phase2_batch(torch_cuda, cfg_ctlb):
+    """DROP_NO_SERVICE packets (services whose every backend was deleted,
+    lb.h:745-751) at the very indices where the previous batch on the same
+    context carried phase-2 packets (self-addressed, loopback and 0.0.0.0
+    pairs): the per-packet phase-2 class scratch is reused across batches,
+    so a dropped packet must not inherit the stale class.  Bit-exact."""
+    T, svcs, t, seclabels = cfg_ctlb
+    lo = 0x1ffff50a  # IPV4_LOOPBACK (node_config.h:45, raw network-order word)
+    rng = np.random.Generator(np.random.PCG64(41))
+    a = {k: x[:30_000].copy() for k, x in t.items()}
+    pick = rng.choice(np.flatnonzero((a["flags"] & 1) == 1), 600, replace=False)
+    tg = svcs.vals["target"][len(svcs.vip):]
+    a["saddr"][pick[:300]] = tg[pick[:300] % len(tg)]
+    a["daddr"][pick[:300]] = a["saddr"][pick[:300]]
+    a["daddr"][pick[300:450]] = lo
+    a["saddr"][pick[450:]] = 0
+    b = {k: x[30_000:60_000].copy() for k, x in t.items()}
+    dead = np.arange(20)  # services whose backends all go before batch b
+    b["flags"][pick] |= 1
+    b["proto"][pick] = 6
+    b["daddr"][pick] = svcs.vip[dead[np.arange(len(pick)) % len(dead)]]
+    b["dport"][pick] = np.where(svcs.port[dead[np.arange(len(pick)) % len(dead)]] != 0,
+                                svcs.port[dead[np.arange(len(pick)) % len(dead)]], b["dport"][pick])
+    gone = np.flatnonzero(np.isin(svcs.keys["address"], svcs.vip[dead]) & (svcs.keys["slave"] > 0))
+    from oracle import Oracle
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_services(o, svcs)
+    synth.load_lxc(o, seclabels)
+    o.ct_set_max(1 << 20)
+    e = _engine(**T.engine_config(), ct_max=1 << 20)
+    synth.load_engine(e, T)
+    synth.load_services(e, svcs)
+    synth.load_lxc(e, seclabels)
+    e.commit()
+    _check(_run(torch_cuda, e, a, 2000), o.classify_v4_ctlb(a, 2000), a, "phase-2 batch")
+    for d in gone:
+        assert e.lb4_delete(svcs.keys[d]) == 0 and o.lb_delete(svcs.keys[d]) == 0
+    e.commit()
+    out = _run(torch_cuda, e, b, 2001)
+    exp = o.classify_v4_ctlb(b, 2001)
+    _check(out, exp, b, "drop batch")
+    assert (out["verdict"][pick] == DROP_NO_SERVICE).sum() > 300
+    _assert_same_map(e, o)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
+
+
 def test_ctlb_empty_and_plain(torch_cuda, cfg_ctlb):
     """An empty batch; a batch without any service traffic equals
     cgpu_classify_v4_ct on a second context."""

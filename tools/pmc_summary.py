@@ -106,5 +106,14 @@ if complete and per_kernel:
         t["l2_hit_rate_dominant"] = round(c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
     if "TCC_EA0_ATOMIC_sum" in c:
         t["memory_side_atomics_dominant"] = round(c["TCC_EA0_ATOMIC_sum"])
+    # whole-step sums over every kernel of a step (bench.py's atomic floor)
+    def step_sum(name):
+        vals = [v["dispatches_per_step"] * v["counters"][name] for v in per_kernel.values()
+                if name in v["counters"]]
+        return round(sum(vals)) if vals else None
+    t["memory_side_atomics_per_step"] = step_sum("TCC_EA0_ATOMIC_sum")
+    hits, miss = step_sum("TCC_HIT_sum"), step_sum("TCC_MISS_sum")
+    t["l2_requests_per_step"] = hits + miss if hits is not None and miss is not None else None
+    t["l2_misses_per_step"] = miss
     json.dump(t, open(os.path.join(d, "traffic.json"), "w"), indent=1)
 print(json.dumps({k: v["dispatches_per_step"] for k, v in per_kernel.items()}, indent=1))
