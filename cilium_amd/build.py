@@ -31,8 +31,6 @@ def hipcc() -> str:
 def stale() -> bool:
     if not os.path.exists(LIB):
         return True
-    if not os.path.exists(BUILD_JSON):
-        _write_build_json()
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(ROOT, "include", "cgpu.h"))
@@ -67,7 +65,9 @@ def src_sha256() -> str:
 def lib_identity(path: str = LIB) -> dict:
     """The identity of the library file at `path` (the one a process loads):
     its own sha256 and, from libcgpu.build.json when that describes this very
-    file, the sources it was built from and the git HEAD at build time.
+    file, the sources it was built from and the git HEAD at build time
+    (written only by build(); without it, or for another file, the sources
+    and HEAD are reported unknown, never guessed).
     Profile summaries (tools/pmc_summary.py) are stamped with it and
     bench.py prints a PMC traffic figure only for the identity it loaded."""
     ident = {"lib_sha256": _sha256(path) if os.path.exists(path) else None,
