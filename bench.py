@@ -530,7 +530,7 @@ def main():
     # after warmup traffic the most-hit keys own the LDS counter slots; every
     # rank holds the same folded totals, so every rank picks the same layout
     moved = None
-    if not args.no_rebalance and not pf6 and not ct and args.warmup:
+    if not args.no_rebalance and not pf6 and args.warmup:
         torch.cuda.synchronize()
         moved = e.counters_rebalance()
         if world > 1:

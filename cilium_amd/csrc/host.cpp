@@ -1762,6 +1762,8 @@ struct DevBuf {
 	int dev = -1;
 	hipStream_t st = nullptr;
 	uint64_t host_sum = 0; /* table_sum_word over the host image (verification) */
+	size_t gather = 0;     /* bytes of the parts lookups gather from device memory
+				  (not LDS-staged, not fallback-only); 0 = all (cgpu_table_bytes) */
 	std::vector<std::pair<size_t, size_t>> parts; /* (offset, bytes) summed */
 	~DevBuf()
 	{
@@ -1884,6 +1886,7 @@ struct cgpu_ctx {
 	/* ---- conntrack maps cilium_ct4_global / cilium_ct6_global ---- */
 	CtMap ct4, ct6;
 	void *d_ct_scratch = nullptr;
+	uint64_t *d_ct_pk = nullptr; /* the conntrack finish's packed counters (k_unpack re-zeroes) */
 	/* host-resident batches (cgpu_classify_v4_host / _frames_host): device
 	 * staging for up to HS_NBUF chunks (grown to the largest batch seen,
 	 * freed by cgpu_host_stage_release), one stream per direction */
@@ -2186,6 +2189,7 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 			(void)hipFree(m->d_count);
 		}
 		(void)hipFree(c->d_ct_scratch);
+		(void)hipFree(c->d_ct_pk);
 		host_stage_free(c);
 		(void)hipEventDestroy(c->ct_done);
 		(void)hipStreamDestroy(c->ct_stream);
@@ -3461,6 +3465,13 @@ static int commit_ipc(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	}
 	if (int r = upload(c, ar, buf, G_IPC))
 		return r;
+	/* the x4 kernels read x16 and the overflow nodes (the leaf dictionary in
+	 * LDS); the v6 pre-pass b32, the node lines, labels and h64 records (root
+	 * and b24 LDS-staged when representable) */
+	buf->gather = (b.lc.x16.size() + b.lc.nodes.size()) * 4;
+	if (b.v6.any)
+		buf->gather += (b.v6.b32.size() + b.v6.pool.size() + b.v6.vals.size()) * 4 + b.v6.h64.size() * 32 +
+			       (b.v6.b24_16.empty() ? b.v6.b24.size() * 4 + b.v6.root.size() * 4 : 0);
 	s.ipc4c = lpm16c{at<uint32_t>(buf, o_d), at<uint32_t>(buf, o_n), at<uint32_t>(buf, o_v),
 			 at<uint32_t>(buf, o_x), at<uint32_t>(buf, o_c), (uint32_t)b.lc.nodes.size(),
 			 (uint32_t)b.lc.dict.size()};
@@ -3510,6 +3521,7 @@ static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const size_t o_g = ar.add(b.pg.slots.data(), b.pg.slots.size() * sizeof(uint4));
 	if (int r = upload(c, ar, buf, G_POL))
 		return r;
+	buf->gather = b.pol.slots.size() * sizeof(pol_slot) + b.pg.slots.size() * sizeof(uint4);
 	s.pol = pol_table{at<pol_slot>(buf, o_p), b.pol.mask, 0};
 	s.pg = pol_groups{at<uint4>(buf, o_g), b.pg.mask, 0};
 	b.sum[G_POL] = in.sum_pol;
@@ -3556,6 +3568,11 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	}
 	if (int r = upload(c, ar, buf, G_PF))
 		return r;
+	buf->gather = have4 ? (lc.x16.size() + lc.nodes.size()) * 4 : 0;
+	if (pf6.any)
+		buf->gather += (pf6.b32.size() + pf6.pool.size()) * 4 + pf6.h64.size() * 32 +
+			       (pf6.b24_16.empty() ? pf6.b24.size() * 4 : 0) +
+			       (pf6.root16.empty() && pf6.rbits.empty() ? pf6.root.size() * 4 : 0);
 	s.pf4c = lpm16c{};
 	if (have4)
 		s.pf4c = lpm16c{at<uint32_t>(buf, o4[1]), at<uint32_t>(buf, o4[2]), nullptr, at<uint32_t>(buf, o4[0]),
@@ -3804,6 +3821,7 @@ static int commit_locked(cgpu_ctx *c, uint64_t *epoch_out)
 	}
 	const cgpu_config &cf = in.cfg;
 	memcpy(s.router_ip64, cf.ipv6_router_ip, 8);
+	memcpy(s.router_ip, cf.ipv6_router_ip, 16);
 	s.pf4_enabled = cf.prefilter_fix4;
 	s.pf6_enabled = cf.prefilter_fix6;
 	s.world_id = cf.world_id;
@@ -3866,8 +3884,10 @@ CGPU_EXPORT int cgpu_table_bytes(cgpu_ctx *c, uint64_t *out)
 		std::lock_guard<std::mutex> g(c->pub_mu);
 		ep = c->cur;
 	}
-	for (int k = 0; k < G_N; k++)
-		out[k] = ep && ep->bufs[k] ? (uint64_t)ep->bufs[k]->bytes : 0u;
+	for (int k = 0; k < G_N; k++) {
+		const DevBuf *b = ep ? ep->bufs[k].get() : nullptr;
+		out[k] = !b ? 0u : b->gather ? (uint64_t)b->gather : (uint64_t)b->bytes;
+	}
 	out[CGPU_TBL_CT4] = (uint64_t)(c->ct4.keys.size() + c->ct4.vals.size()) * 16u;
 	out[CGPU_TBL_CT6] = (uint64_t)(c->ct6.keys.size() + c->ct6.vals.size()) * 16u;
 	return 0;
@@ -5566,6 +5586,10 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 		HIP_OR_EIO(hipMalloc(&c->d_ct_scratch, L.total));
 		c->ct_scratch_cap = L.total;
 	}
+	if (!c->d_ct_pk) {
+		HIP_OR_EIO(hipMalloc((void **)&c->d_ct_pk, (size_t)c->n_ctr_slots * 8u));
+		HIP_OR_EIO(hipMemsetAsync(c->d_ct_pk, 0, (size_t)c->n_ctr_slots * 8u, cs));
+	}
 	uint8_t *b = static_cast<uint8_t *>(c->d_ct_scratch);
 	/* every walker wave (2048 x 4) holding a chunk stays under a quarter
 	 * of the headroom */
@@ -5585,6 +5609,7 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.temp = b + L.temp;
 	a.temp_bytes = L.temp_bytes;
 	a.flags2 = b + L.flags2;
+	a.pk = c->d_ct_pk;
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
 		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);

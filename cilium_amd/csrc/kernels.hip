@@ -2284,6 +2284,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #define DROP_INVALID (-134)
 #define DROP_CT_INVALID_HDR (-135)
 #define DROP_UNKNOWN_L3 (-139)
+#define DROP_UNKNOWN_TARGET (-150)
 #define DROP_INVALID_EXTHDR (-156)
 #define DROP_FRAG_NOSUPPORT (-157)
 #define EFAULT_LOAD (-14)        /* bpf_skb_load_bytes past skb->len */
@@ -2362,6 +2363,43 @@ __device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fw
 		t.sa = uint4{W.d(22), W.d(26), W.d(30), W.d(34)};
 		t.da = uint4{W.d(38), W.d(42), W.d(46), W.d(50)};
 		t.proto = W.b(20);
+	}
+	if (egress && !v4 && t.proto == 58u) {
+		/* handle_ipv6 (bpf_lxc.c:364-389), before ipv6_l3_from_lxc and its
+		 * endpoint checks: an ICMPv6 frame needs its icmp6hdr (DROP_INVALID),
+		 * then icmp6_handle (lib/icmp6.h:390-412) hands a neighbour
+		 * solicitation and an echo request to ROUTER_IP to the responders
+		 * (tail calls: the frame leaves classification, as ARP does).  The
+		 * NS responder drops an unknown target (ACTION_UNKNOWN_ICMP6_NS,
+		 * DROP_UNKNOWN_TARGET) and reads the ND option at 78 (icmp6.h:
+		 * 148-204).  The ND target lies past the window: byte loads (rare). */
+		int32_t r = len < 62u ? DROP_INVALID : 0;
+		if (!r) {
+			const uint32_t type = W.b(54);
+			if (type == 135u) {
+				r = fchk(62u, 16u, len, cap, DROP_INVALID);
+				if (!r) {
+					uint32_t diff = 0;
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						const uint32_t w = (uint32_t)f[62 + 4 * k] | (uint32_t)f[63 + 4 * k] << 8 |
+								   (uint32_t)f[64 + 4 * k] << 16 |
+								   (uint32_t)f[65 + 4 * k] << 24;
+						diff |= w ^ s.router_ip[k];
+					}
+					r = diff ? DROP_UNKNOWN_TARGET : fchk(78u, 8u, len, cap, DROP_INVALID);
+					if (!r)
+						r = FRAME_NOT_CLASSIFIED;
+				}
+			} else if (type == 128u && t.da.x == s.router_ip[0] && t.da.y == s.router_ip[1] &&
+				   t.da.z == s.router_ip[2] && t.da.w == s.router_ip[3]) {
+				r = FRAME_NOT_CLASSIFIED;
+			}
+		}
+		if (r) {
+			t.status = r;
+			return t;
+		}
 	}
 	if (egress && ep < s.n_lxc) {
 		/* SMAC / DMAC / SIP checks of the endpoint (bpf_lxc.c:431-437,
@@ -4273,6 +4311,7 @@ struct ct_args {
 	uint32_t serial;             /* one group for the whole batch (see launch_ctlb) */
 	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
 	uint8_t *pcls;               /* [n] service path: phase-2 class, PCL_* (k_ct_prep) */
+	uint64_t *pk;                /* packed per-slot counters (k_ct_finish, k_unpack) */
 };
 
 /* One packet's record, written by k_ct_prep{,6} and read by the walker and
@@ -6076,7 +6115,8 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
  * CT_REPLY / CT_RELATED ones run the cascade again, on the reply tuple.
  * Hot counter slots accumulate in LDS (packed, as k_classify CTR = 1). */
 template <int NT, class K, int Q>
-__global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, uint32_t cc_n)
+__global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, uint32_t cc_n, uint64_t lo,
+						   uint64_t hi)
 {
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* metrics {reason 0 / 133 / 137 / 155 [/ 158]} x {ingress, egress} */
@@ -6084,7 +6124,11 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 	uint64_t mcnt[NM] = {}, mbyt[NM] = {};
 	/* LDS: the hot counter slots, then the cold-slot cache (as k_classify_x4:
 	 * cc_n packed counts, cc_n tags = slot + 1): each touched cold slot costs
-	 * one pair of memory-side atomics per workgroup instead of one per hit */
+	 * one packed memory-side atomic per workgroup instead of one per hit; a
+	 * hit the cache cannot take is one packed atomic into pk (PKC format;
+	 * the launcher unpacks pk into delta after every PKC_CHUNK packets), as
+	 * k_classify_x4 does: two unpacked atomics per hit made this kernel issue
+	 * 30M memory-side atomics per 64M packets (profiles/r4_prof/ct) */
 	uint64_t *ccv = lctr + s.hot_slots;
 	uint32_t *cck = reinterpret_cast<uint32_t *>(ccv + cc_n);
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT)
@@ -6097,7 +6141,7 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 	/* Q packets per lane (packet g + u * threads): the CT_REPLY / CT_RELATED
 	 * packets' policy cascades run stage-interleaved (policy_q) */
 	const uint64_t T = (uint64_t)gridDim.x * NT;
-	for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < a.n; g += T * Q) {
+	for (uint64_t g = lo + (uint64_t)blockIdx.x * NT + threadIdx.x; g < hi; g += T * Q) {
 		ct_pkt q[Q];
 		uint32_t c[Q], ep[Q], dp[Q], pr[Q];
 		bool act[Q], rep[Q], eg[Q], frag[Q];
@@ -6105,7 +6149,7 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
-			act[u] = i < a.n;
+			act[u] = i < hi;
 			const uint64_t j = act[u] ? i : 0u;
 			/* batch order: records and the walker's results stream in */
 			q[u] = ct_rec<K>::load(a.rec, (uint32_t)j, true).pkt();
@@ -6182,8 +6226,14 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 						}
 					}
 					if (!done) {
-						atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
-						atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u], (unsigned long long)len);
+						if (len < PKC_MAX_LEN) {
+							atomicAdd((unsigned long long *)&a.pk[cs],
+								  (1ull << PKC_SHIFT) | (unsigned long long)len);
+						} else {
+							atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
+							atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u],
+								  (unsigned long long)len);
+						}
 					}
 				}
 			}
@@ -6214,20 +6264,20 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 		}
 	}
 	__syncthreads();
+	/* one packed atomic per touched slot: PK (LDS) -> PKC (pk) format; a
+	 * workgroup's bytes per slot stay < 2^37 (< 2^26 packets of < 2^11, the
+	 * larger ones went to delta directly) */
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
 		const uint64_t x = lctr[k];
-		if (x) {
-			atomicAdd((unsigned long long *)&a.delta[2u * k], x >> PK_SHIFT);
-			atomicAdd((unsigned long long *)&a.delta[2u * k + 1u], x & PK_BYTES_MASK);
-		}
+		if (x)
+			atomicAdd((unsigned long long *)&a.pk[k], ((x >> PK_SHIFT) << PKC_SHIFT) | (x & PK_BYTES_MASK));
 	}
 	for (uint32_t k = threadIdx.x; k < cc_n; k += NT) {
 		const uint32_t t = cck[k];
 		const uint64_t x = ccv[k];
-		if (t && x) {
-			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u)], x >> PK_SHIFT);
-			atomicAdd((unsigned long long *)&a.delta[2u * (t - 1u) + 1u], x & PK_BYTES_MASK);
-		}
+		if (t && x)
+			atomicAdd((unsigned long long *)&a.pk[t - 1u],
+				  ((x >> PK_SHIFT) << PKC_SHIFT) | (x & PK_BYTES_MASK));
 	}
 }
 
@@ -6373,6 +6423,7 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.xdport = L.xdport;
 	a.f2 = L.flags2;
 	a.pcls = L.pcls;
+	a.pk = L.pk;
 	return a;
 }
 
@@ -6557,8 +6608,16 @@ template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct
 	/* the cold-slot cache in the LDS the hot slots leave */
 	const size_t hot = (size_t)sf.hot_slots * 8u;
 	const uint32_t cc_n = (s.schedule & CGPU_SCHED_NO_CCACHE) ? 0u : cc_entries(hot);
-	hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), hot + (size_t)cc_n * 12u, st, sf,
-			   a, cc_n);
+	/* pk stays exact for PKC_CHUNK packets per slot: unpack after each chunk */
+	for (uint64_t lo = 0; lo < a.n; lo += PKC_CHUNK) {
+		const uint64_t hi = std::min<uint64_t>(a.n, lo + PKC_CHUNK);
+		hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), hot + (size_t)cc_n * 12u, st,
+				   sf, a, cc_n, lo, hi);
+		if (s.cold_hi) {
+			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
+			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
+		}
+	}
 }
 
 /* phase 2 of the plain paths (and of the IPv6 service path): the ICMP

@@ -156,6 +156,7 @@ struct ct_launch {
 	uint32_t *ctl;        /* [4] */
 	uint8_t *flags2;      /* [2n] plain path, [4n] service path: phase-2 candidates */
 	uint8_t *pcls;        /* [n] service path: each packet's phase-2 class (k_ct_prep) */
+	uint64_t *pk;         /* [n_ctr_slots] packed counters, zero between calls */
 	void *xdaddr;         /* [n] optional (IPv6: 16 bytes each) */
 	uint16_t *xdport;     /* [n] optional */
 };

@@ -458,6 +458,7 @@ typedef struct cgpu_snapshot {
 	uint32_t world_id, cluster_id, host_id, health_id;
 	uint32_t ipv4_cluster_mask, ipv4_cluster_range;
 	uint32_t router_ip64[2]; /* first 8 bytes of ROUTER_IP (ipv6_match_prefix_64) */
+	uint32_t router_ip[4];   /* ROUTER_IP whole (handle_ipv6's ICMPv6 responders) */
 	uint32_t ct_proto_gate, ingress_secctx_world, ingress_src_identity;
 	uint32_t n_ctr_slots;
 	uint32_t hot_slots;      /* counter slots [0, hot_slots) may live in LDS */

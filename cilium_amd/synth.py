@@ -612,6 +612,11 @@ def _be16(x):
     return np.stack([x >> 8, x & 0xff], 1).astype(np.uint8)
 
 
+# ROUTER_IP of the endpoint programs' build (bpf/node_config.h:30), the
+# engine's and the restatement's default
+ROUTER_IP6 = bytes([0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 0])
+
+
 def make_frames(rng, n: int, width: int = 256, n_ep: int = 5, addr4=None, edge: bool = True):
     """Diverse Ethernet frames for the frame-path parity tests (vectorized).
 
@@ -721,8 +726,25 @@ def make_frames(rng, n: int, width: int = 256, n_ep: int = 5, addr4=None, edge: 
     trunc = rng.random(n) < 0.2
     lo = np.where(edge, 0, 14)
     lens[trunc] = rng.integers(lo, np.maximum(full[trunc], lo + 1))
-    return {"data": D, "len": lens.astype(np.uint32), "flags": egress.astype(np.uint8),
-            "ep": rng.integers(0, n_ep, n).astype(np.uint16)}
+    ep = rng.integers(0, n_ep, n).astype(np.uint16)
+    # handle_ipv6's ICMPv6 responders (bpf_lxc.c:364-389, lib/icmp6.h):
+    # neighbour solicitations for the router and for other targets, echo
+    # requests to the router, at lengths around the responders' reads
+    # (icmp6hdr 62, ND target 78, ND option 86); drawn last, so the frames
+    # above stay as they were
+    icmp6 = r6[(next_chain == 0) & (proto == 58)]
+    pick = icmp6[rng.random(len(icmp6)) < 0.5]
+    m = len(pick)
+    ns = rng.random(m) < 0.6
+    D[pick[ns], 54] = 135
+    tgt = rng.integers(0, 256, (int(ns.sum()), 16), dtype=np.uint8)
+    tgt[rng.random(int(ns.sum())) < 0.5] = np.frombuffer(ROUTER_IP6, np.uint8)
+    if width >= 78:
+        D[pick[ns], 62:78] = tgt
+    D[pick[~ns], 54] = 128
+    D[pick[~ns], 38:54] = np.frombuffer(ROUTER_IP6, np.uint8)
+    lens[pick] = rng.integers(56, 100, m)
+    return {"data": D, "len": lens.astype(np.uint32), "flags": egress.astype(np.uint8), "ep": ep}
 
 
 def frames_from_tuples(t: dict, stride: int = 64, seed=SEED):

@@ -394,10 +394,11 @@ int cgpu_commit(cgpu_ctx *ctx, uint64_t *epoch_out);
 /* order-independent checksum of the committed table contents; replicas on
  * different GPUs/ranks holding the same tables report the same value */
 int cgpu_table_checksum(cgpu_ctx *ctx, uint64_t *sum_out);
-/* Device bytes of every table group of the published snapshot (0 for a
- * group never committed) and of the conntrack maps: what a lookup into each
- * map gathers from (bench.py prices each map's lookups at the measured
- * gather ceiling of the cache tier a table of that size lives in). */
+/* Device bytes a lookup into each table group of the published snapshot
+ * gathers from (0 for a group never committed; parts staged in LDS or read
+ * only by fallback schedules excluded), and of the conntrack maps: bench.py
+ * prices each map's lookups at the measured gather ceiling of the cache tier
+ * a table of that size lives in. */
 enum {
 	CGPU_TBL_IPCACHE = 0, CGPU_TBL_POLICY, CGPU_TBL_PREFILTER, CGPU_TBL_ENDPOINT, CGPU_TBL_LB4,
 	CGPU_TBL_LXC, CGPU_TBL_LB6, CGPU_TBL_CT4, CGPU_TBL_CT6, CGPU_TBL_N
@@ -588,8 +589,10 @@ typedef struct cgpu_frames {
 
 /* frame status / verdict values beyond the reference's DROP_* codes */
 #define CGPU_FRAME_NOT_CLASSIFIED 1 /* egress ARP (tail call to the ARP responder,
-				       bpf_lxc.c:703-706) or ingress non-IP (passed
-				       to the stack, bpf_netdev.c:518-520) */
+				       bpf_lxc.c:703-706), an egress ICMPv6 frame the
+				       ICMPv6 responders take (bpf_lxc.c:377-386) or
+				       ingress non-IP (passed to the stack,
+				       bpf_netdev.c:518-520) */
 #define CGPU_DROP_SNAPLEN (-4096)   /* a header the reference would read lies past
 				       the stored slot (stride < len): re-submit
 				       with a larger stride */
@@ -611,7 +614,12 @@ typedef struct cgpu_frame_tuples {
  * Per frame, the steps of the endpoint programs before the ipcache lookup
  * (stateless: conntrack empty, every packet CT_NEW):
  *   egress : skb->protocol dispatch (bpf_lxc.c:683-711; other than IPv4,
- *            IPv6, ARP -> DROP_UNKNOWN_L3 -139), revalidate_data (-134), the
+ *            IPv6, ARP -> DROP_UNKNOWN_L3 -139), revalidate_data (-134),
+ *            handle_ipv6's ICMPv6 responders (bpf_lxc.c:364-389: an ICMPv6
+ *            frame shorter than its icmp6hdr -134; a neighbour solicitation
+ *            for another target DROP_UNKNOWN_TARGET -150, for ROUTER_IP -134
+ *            without its ND option, else -- and an echo request to ROUTER_IP
+ *            -- handed to the responder: CGPU_FRAME_NOT_CLASSIFIED), the
  *            SMAC / DMAC / SIP checks (-130 / -131 / -132), ipv6_hdrlen
  *            (-156, -157, -134), extract_l4_port of lb{4,6}_extract_key
  *            (TCP/UDP dport past len -> -14, -EFAULT of skb_load_bytes),

@@ -1612,6 +1612,7 @@ void or_counters_reset(or_ctx *c)
 #define DROP_INVALID (-134)
 #define DROP_CT_INVALID_HDR (-135)
 #define DROP_UNKNOWN_L3 (-139)
+#define DROP_UNKNOWN_TARGET (-150)
 #define DROP_INVALID_EXTHDR (-156)
 #define EFAULT_LOAD (-14)      /* bpf_skb_load_bytes past skb->len */
 #define FRAME_NOT_CLASSIFIED 1
@@ -1692,6 +1693,7 @@ static int ipv6_hdrlen_r(const struct frame *f, uint8_t *nexthdr)
  * One frame (cgpu.h cgpu_frames_parse):
  *  dispatch   bpf_lxc.c:683-711 (egress) / bpf_netdev.c:494-521 (ingress)
  *  revalidate bpf/lib/common.h:71-91
+ *  ICMPv6     egress: handle_ipv6's responders, bpf_lxc.c:364-389, icmp6.h
  *  SMAC/DMAC/SIP bpf_lxc.c:431-437, :100-105; bpf/lib/lxc.h:31-89
  *  hdrlen     ipv4.h:45-48 / ipv6.h:61-98; fragment ipv4.h:50-61 (ingress v4)
  *  LB_L4 port lb.h:192-215 via lb{4,6}_extract_key (egress)
@@ -1724,6 +1726,29 @@ static int frame_parse_one(const or_ctx *c, const struct frame *f, int egress, u
 		memcpy(t->sa, f->p + 22, 16);
 		memcpy(t->da, f->p + 38, 16);
 		t->proto = f->p[20];
+	}
+	if (egress && !v4 && t->proto == PROTO_ICMPV6) {
+		/* handle_ipv6 (bpf_lxc.c:364-389), before ipv6_l3_from_lxc's
+		 * endpoint checks: the icmp6hdr must be there, then icmp6_handle
+		 * (lib/icmp6.h:390-412) sends a neighbour solicitation and an echo
+		 * request to ROUTER_IP to the responders (tail calls that end the
+		 * program): an unknown ND target is DROP_UNKNOWN_TARGET
+		 * (ACTION_UNKNOWN_ICMP6_NS), the router's needs the ND option the
+		 * advertisement rewrites (icmp6.h:148-204) */
+		uint8_t tg[16], opt[8];
+		if (f->len < 62)
+			return DROP_INVALID;
+		if (f->p[54] == 135) {
+			if ((r = fr_ld(f, 62, 16, tg, DROP_INVALID)))
+				return r;
+			if (memcmp(tg, cfg->router_ip, 16))
+				return DROP_UNKNOWN_TARGET;
+			if ((r = fr_ld(f, 78, 8, opt, DROP_INVALID)))
+				return r;
+			return FRAME_NOT_CLASSIFIED;
+		}
+		if (f->p[54] == 128 && !memcmp(t->da, cfg->router_ip, 16))
+			return FRAME_NOT_CLASSIFIED;
 	}
 	if (info) {
 		uint8_t verify = info[6];

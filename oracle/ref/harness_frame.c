@@ -9,8 +9,9 @@
  * LXC_IP, LXC_IPV4) and runs, per Ethernet frame, the steps of the endpoint
  * programs that come BEFORE the ipcache / policy decision:
  *   egress  (from-container): handle_ingress dispatch (bpf_lxc.c:683-711),
- *           handle_ipv4_from_lxc (bpf_lxc.c:426-481) / ipv6_l3_from_lxc
- *           (bpf_lxc.c:82-163): revalidate_data, SMAC / DMAC / SIP checks,
+ *           handle_ipv4_from_lxc (bpf_lxc.c:426-481) / handle_ipv6's
+ *           ICMPv6 responders (bpf_lxc.c:364-389, lib/icmp6.h) and
+ *           ipv6_l3_from_lxc (bpf_lxc.c:82-163): revalidate_data, SMAC / DMAC / SIP checks,
  *           ipv{4,6}_hdrlen, lb{4,6}_extract_key + lb{4,6}_lookup_service
  *           over an EMPTY service map, ct_lookup{4,6}(CT_EGRESS)
  *   ingress (to-container): bpf_netdev.c handle_netdev dispatch (:494-521,
@@ -29,6 +30,7 @@
  * lookup misses; skb_load_bytes reads the frame buffer bounded by skb->len
  * (-EFAULT past it, as the kernel helper); debug helpers are inert.
  */
+#include <setjmp.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -50,6 +52,7 @@
 #include "lib/l4.h"
 #include "lib/lb.h"
 #include "lib/lxc.h"
+#include "lib/icmp6.h"
 
 /* stand in for the endpoint's CT_MAP4 / CT_MAP6 (bpf_lxc.c:53-75) */
 static int ct_map4, ct_map6;
@@ -57,6 +60,28 @@ static int ct_map4, ct_map6;
 static int inited;
 static unsigned char *frame_buf;
 static uint32_t frame_len;
+
+/* BPF_LD_ABS (api.h:228-235: load_byte / load_half / load_word are these
+ * LLVM BPF intrinsics), used by icmp6_load_type */
+unsigned long long harness_fr_ld_abs_b(void *skb, unsigned long long off) __asm__("llvm.bpf.load.byte");
+unsigned long long harness_fr_ld_abs_b(void *skb, unsigned long long off) { return frame_buf[off]; }
+unsigned long long harness_fr_ld_abs_h(void *skb, unsigned long long off) __asm__("llvm.bpf.load.half");
+unsigned long long harness_fr_ld_abs_h(void *skb, unsigned long long off)
+{
+	return (unsigned long long)frame_buf[off] << 8 | frame_buf[off + 1];
+}
+unsigned long long harness_fr_ld_abs_w(void *skb, unsigned long long off) __asm__("llvm.bpf.load.word");
+unsigned long long harness_fr_ld_abs_w(void *skb, unsigned long long off)
+{
+	return (unsigned long long)frame_buf[off] << 24 | (unsigned long long)frame_buf[off + 1] << 16 |
+	       (unsigned long long)frame_buf[off + 2] << 8 | frame_buf[off + 3];
+}
+
+/* the ICMPv6 responders of handle_ipv6 (bpf_lxc.c:377-386) are tail calls
+ * that end the program: the mocked tail call runs the responder's body and
+ * returns its outcome to frame_v6 */
+static jmp_buf icmp6_env;
+static int icmp6_ret;
 
 static void *mock_lookup(void *map, const void *key) { return NULL; }
 static int mock_update(void *map, const void *key, const void *val, uint32_t flags) { return 0; }
@@ -69,6 +94,36 @@ static int mock_load(struct __sk_buff *skb, uint32_t off, void *to, uint32_t len
 		return -14; /* -EFAULT, bpf_skb_load_bytes */
 	memcpy(to, frame_buf + off, len);
 	return 0;
+}
+
+static int mock_store(struct __sk_buff *skb, uint32_t off, const void *from, uint32_t len, uint32_t flags)
+{
+	if ((uint64_t)off + len > frame_len)
+		return -14;
+	memcpy(frame_buf + off, from, len);
+	return 0;
+}
+
+static int mock_csum_diff(void *from, uint32_t fs, void *to, uint32_t ts, uint32_t seed) { return 0; }
+static int mock_csum_replace(struct __sk_buff *skb, uint32_t off, uint32_t from, uint32_t to, uint32_t flags)
+{
+	return 0;
+}
+static int mock_redirect(int ifindex, uint32_t flags) { return TC_ACT_REDIRECT; }
+
+/* a responder's outcome: its drop, or 1 (the frame left the classification
+ * path, as an ARP request does) */
+static void mock_tail_call(struct __sk_buff *skb, void *map, uint32_t index)
+{
+	int r;
+	if (index == CILIUM_CALL_HANDLE_ICMP6_NS)
+		r = __icmp6_handle_ns(skb, skb->cb[0]);
+	else if (index == CILIUM_CALL_SEND_ICMP6_ECHO_REPLY)
+		r = __icmp6_send_echo_reply(skb, skb->cb[0]);
+	else
+		return;
+	icmp6_ret = IS_ERR(r) ? r : 1;
+	longjmp(icmp6_env, 1);
 }
 
 static int ensure_init(void)
@@ -84,6 +139,12 @@ static int ensure_init(void)
 	map_delete_elem = mock_delete;
 	ktime_get_ns = mock_ktime;
 	skb_load_bytes = mock_load;
+	skb_store_bytes = mock_store;
+	csum_diff = mock_csum_diff;
+	l3_csum_replace = mock_csum_replace;
+	l4_csum_replace = mock_csum_replace;
+	redirect = mock_redirect;
+	tail_call = mock_tail_call;
 	inited = 1;
 	return 0;
 }
@@ -160,6 +221,19 @@ static int frame_v6(struct __sk_buff *skb, int egress, struct frame_out *o)
 
 	if (!revalidate_data(skb, &data, &data_end, &ip6))
 		return DROP_INVALID;
+	if (egress && ip6->nexthdr == IPPROTO_ICMPV6) {
+		/* handle_ipv6 (bpf_lxc.c:364-389): special ICMPv6 messages before
+		 * ipv6_l3_from_lxc -- neighbour solicitations and echo requests
+		 * to the router go to the responders (icmp6_handle,
+		 * lib/icmp6.h:390-412) */
+		if (data + sizeof(*ip6) + ETH_HLEN + sizeof(struct icmp6hdr) > data_end)
+			return DROP_INVALID;
+		if (setjmp(icmp6_env))
+			return icmp6_ret;
+		ret = icmp6_handle(skb, ETH_HLEN, ip6, METRIC_EGRESS);
+		if (IS_ERR(ret))
+			return ret;
+	}
 	tuple.nexthdr = ip6->nexthdr;
 	if (egress) {
 		struct ethhdr *eth = data;

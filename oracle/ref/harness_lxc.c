@@ -44,6 +44,7 @@
  * skb_load_bytes / skb_store_bytes act on a MAP_32BIT frame buffer;
  * checksum helpers return 0; get_hash_recalc the injected skb->hash.
  */
+#include <setjmp.h>
 #include <stdio.h>
 #include <string.h>
 #include <stdint.h>
@@ -66,6 +67,13 @@ static uint32_t frame_len;
 static int n_ct_lookups, ct_hit[2], ct_rel[2];
 static int n_probes;
 static uint32_t probe_label;
+static uint16_t probe_dport;
+static uint8_t probe_proto;
+static uint8_t ct_key0[40];
+/* ref_lxc_frame: the from-container program's tail calls run the callee and
+ * return to the harness (a BPF tail call does not come back) */
+static int dispatching, tail_arp;
+static jmp_buf tail_env;
 static int drop_reason, proxied, probe_hit_at;
 
 /* BPF_LD_ABS (api.h:228-235 binds load_byte / load_half / load_word to
@@ -90,8 +98,11 @@ static void *mock_lookup(void *map, const void *key)
 	if (map == &POLICY_MAP) {
 		const struct policy_key *k = key;
 		void *v = mockmap_lookup(&policy_maps[cur_ep], key);
-		if (n_probes++ == 0)
+		if (n_probes++ == 0) {
 			probe_label = k->sec_label;
+			probe_dport = k->dport;
+			probe_proto = k->protocol;
+		}
 		if (v && !probe_hit_at)
 			probe_hit_at = n_probes;
 		return v;
@@ -100,6 +111,8 @@ static void *mock_lookup(void *map, const void *key)
 		const struct ipv4_ct_tuple *k = key;
 		void *v = mockmap_lookup(&ct, key);
 		if (!(k->flags & TUPLE_F_SERVICE) && n_ct_lookups < 2) {
+			if (!n_ct_lookups)
+				memcpy(ct_key0, k, sizeof(*k));
 			ct_hit[n_ct_lookups] = v != NULL;
 			ct_rel[n_ct_lookups] = (k->flags & TUPLE_F_RELATED) != 0;
 			n_ct_lookups++;
@@ -110,6 +123,8 @@ static void *mock_lookup(void *map, const void *key)
 		const struct ipv6_ct_tuple *k = key;
 		void *v = mockmap_lookup(&ct6, key);
 		if (!(k->flags & TUPLE_F_SERVICE) && n_ct_lookups < 2) {
+			if (!n_ct_lookups)
+				memcpy(ct_key0, k, sizeof(*k));
 			ct_hit[n_ct_lookups] = v != NULL;
 			ct_rel[n_ct_lookups] = (k->flags & TUPLE_F_RELATED) != 0;
 			n_ct_lookups++;
@@ -195,8 +210,27 @@ static int mock_tunnel_key(struct __sk_buff *skb, const struct bpf_tunnel_key *f
 
 static void mock_tail_call(struct __sk_buff *skb, void *map, uint32_t index)
 {
-	if (index == CILIUM_CALL_DROP_NOTIFY)
+	if (index == CILIUM_CALL_DROP_NOTIFY) {
 		__send_drop_notify(skb);
+		return;
+	}
+	if (!dispatching)
+		return;
+	if (index == CILIUM_CALL_IPV4_FROM_LXC)
+		tail_handle_ipv4(skb);
+	else if (index == CILIUM_CALL_IPV6_FROM_LXC)
+		tail_handle_ipv6(skb);
+	else if (index == CILIUM_CALL_ARP)
+		tail_arp = 1; /* tail_handle_arp: the ARP responder, not classified */
+	else if (index == CILIUM_CALL_HANDLE_ICMP6_NS) {
+		tail_arp = 2; /* icmp6_handle_ns: the neighbour-solicitation responder */
+		tail_icmp6_handle_ns(skb);
+	} else if (index == CILIUM_CALL_SEND_ICMP6_ECHO_REPLY) {
+		tail_arp = 3; /* echo request to the router: the echo responder */
+		tail_icmp6_send_echo_reply(skb);
+	} else
+		return;
+	longjmp(tail_env, 1);
 }
 
 static int mock_event_output(struct __sk_buff *skb, void *map, uint64_t index, const void *data, uint32_t size)
@@ -424,6 +458,10 @@ int ref_lxc_v4(uint32_t saddr_be, uint32_t daddr_be, uint16_t sport_be, uint16_t
 
 static void reset_obs(void)
 {
+	tail_arp = 0;
+	probe_dport = 0;
+	probe_proto = 0;
+	memset(ct_key0, 0, sizeof(ct_key0));
 	n_ct_lookups = n_probes = probe_hit_at = 0;
 	ct_hit[0] = ct_hit[1] = ct_rel[0] = ct_rel[1] = 0;
 	probe_label = 0;
@@ -516,4 +554,73 @@ int ref_lxc_v6(const uint8_t *saddr16, const uint8_t *daddr16, uint16_t sport_be
 	}
 	outcome(flags & 1, ETH_HLEN + 40, verdict, identity, ct_ret, stage);
 	return ret;
+}
+
+/*
+ * A raw Ethernet frame through the compiled program with empty policy and
+ * conntrack maps: egress (flags bit 0) from the from-container entry
+ * handle_ingress (bpf_lxc.c:682-711: the protocol dispatch, its tail calls
+ * into tail_handle_ipv4 / tail_handle_ipv6 / the ARP responder); ingress by
+ * ethertype into tail_ipv4_policy / tail_ipv6_policy (the host device's
+ * dispatch, bpf_netdev.c:494-521, passes anything else to the stack).
+ * Reports what reached the policy step: *status 0 when a policy probe ran
+ * (then *proto / *dport from the first probe's key, the tuple's addresses
+ * from the first conntrack lookup's key in key order), 1 for a frame the
+ * program did not classify (ARP, ingress non-IP), else -(drop reason).
+ * *family 4 / 6 / 0.  data holds stored = min(len, slot) bytes.
+ */
+int ref_lxc_frame(const uint8_t *data, uint32_t stored, uint32_t len, uint8_t flags, int ep, int *status,
+		  int *family, uint8_t *key_daddr16, uint8_t *key_saddr16, uint16_t *dport, uint8_t *proto)
+{
+	struct __sk_buff skb;
+	uint16_t et;
+
+	if (ensure_init() || ep < 0 || ep >= REF_MAX_EP || stored > 4096)
+		return -1;
+	mockmap_clear(&ct);
+	mockmap_clear(&ct6);
+	memset(frame_buf, 0, 4096);
+	memcpy(frame_buf, data, stored);
+	frame_len = stored < len ? stored : len;
+	memset(&skb, 0, sizeof(skb));
+	skb.data = (uint32_t)(unsigned long)frame_buf;
+	skb.data_end = (uint32_t)(unsigned long)(frame_buf + frame_len);
+	skb.len = len;
+	et = frame_len >= 14 ? (uint16_t)(frame_buf[12] | frame_buf[13] << 8) : 0;
+	skb.protocol = et;
+	cur_ep = ep;
+	reset_obs();
+	*family = et == bpf_htons(ETH_P_IP) ? 4 : et == bpf_htons(ETH_P_IPV6) ? 6 : 0;
+	if (flags & 1) {
+		dispatching = 1;
+		if (!setjmp(tail_env))
+			handle_ingress(&skb);
+		dispatching = 0;
+	} else if (*family == 4) {
+		tail_ipv4_policy(&skb);
+	} else if (*family == 6) {
+		tail_ipv6_policy(&skb);
+	} else {
+		*status = 1;
+		return 0;
+	}
+	memset(key_daddr16, 0, 16);
+	memset(key_saddr16, 0, 16);
+	if (n_probes) {
+		*status = 0;
+		*dport = probe_dport;
+		*proto = probe_proto;
+		if (*family == 6) {
+			memcpy(key_daddr16, ct_key0, 16);
+			memcpy(key_saddr16, ct_key0 + 16, 16);
+		} else {
+			memcpy(key_daddr16, ct_key0, 4);
+			memcpy(key_saddr16, ct_key0 + 4, 4);
+		}
+	} else if (tail_arp && !drop_reason) {
+		*status = 1;
+	} else {
+		*status = drop_reason ? -drop_reason : 0x7fffffff;
+	}
+	return 0;
 }

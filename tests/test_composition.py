@@ -18,9 +18,14 @@ both from the reference's build, not its logic:
     2 where the fixture holds the endpoint's label;
   * a proxy-redirected frame has its daddr / dport rewritten to the proxy
     (lib/lxc.h:97-140), so the post-service frame is compared for the others.
-The ingress source identity is computed as bpf_netdev.c:374-404 / :203-211
-do (restated: bpf_netdev.c is a separate program), through the harness's
-own ipcache_lookup4 / ipcache_lookup6.
+The ingress source identity comes from the reference's host-device program
+compiled whole as well (oracle/ref/harness_netdev.c: bpf_netdev.c under its
+node_config.h / netdev_config.h, the cilium_host build; handle_ipv4 /
+handle_ipv6 run to the tail call into the endpoint's policy program, whose
+skb->cb[CB_SRC_LABEL] is the identity ipv4_policy / ipv6_policy receive).
+Only the stateless fixture's ingress_secctx_world form (the cilium_net
+build, where derive_ipv4_sec_ctx gives WORLD_ID, bpf_netdev.c:45-62) is a
+constant here: netdev_config.h compiles the FROM_HOST form.
 
 Development container only: skipped where the reference harness was not
 built (it compiles /root/reference, which never reaches the GPU box)."""
@@ -34,6 +39,7 @@ from cilium_amd import layouts as L
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "_ref", "libref_lxc.so")
+NETDEV = os.path.join(ROOT, "oracle", "_ref", "libref_netdev.so")
 pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason="reference harness not built (oracle/_ref)")
 
 SECLABEL_BUILD = 2  # bpf/node_config.h
@@ -75,6 +81,35 @@ def _lib():
     return lib
 
 
+def _nd():
+    nd = C.CDLL(NETDEV)
+    u32p = C.POINTER(C.c_uint32)
+    nd.ref_netdev_reset.restype = None
+    nd.ref_netdev_ipcache_update.argtypes = [C.c_void_p, C.c_void_p]
+    nd.ref_netdev_v4.argtypes = [C.c_uint32, C.c_uint32, C.c_uint8, C.c_uint32, u32p]
+    nd.ref_netdev_v6.argtypes = [C.c_char_p, C.c_char_p, C.c_uint8, C.c_uint32, u32p]
+    return nd
+
+
+class _Netdev:
+    """The source identity bpf_netdev.c hands the endpoint's policy program."""
+
+    def __init__(self, ipc_keys, ipc_vals):
+        self.nd = _nd()
+        self.nd.ref_netdev_reset()
+        for k, v in zip(ipc_keys, ipc_vals):
+            assert self.nd.ref_netdev_ipcache_update(_b(k), _b(v)) >= 0
+        self.lab = C.c_uint32()
+
+    def src4(self, saddr, daddr, proto, src):
+        assert self.nd.ref_netdev_v4(int(saddr), int(daddr), int(proto), int(src), C.byref(self.lab)) == 0
+        return self.lab.value
+
+    def src6(self, saddr, daddr, proto, src):
+        assert self.nd.ref_netdev_v6(bytes(saddr), bytes(daddr), int(proto), int(src), C.byref(self.lab)) == 0
+        return self.lab.value
+
+
 def _b(x):
     return np.ascontiguousarray(x).tobytes()
 
@@ -92,7 +127,7 @@ def _dump(lib, v6):
     return L.ct_sorted(keys, vals)
 
 
-def _run(lib, t, now, hashes=None):
+def _run(lib, t, now, hashes=None, nd=None):
     n = len(t["saddr"])
     v6 = np.asarray(t["saddr"]).ndim == 2
     out = {k: np.zeros(n, dt) for k, dt in (("verdict", np.int32), ("ct_ret", np.uint8),
@@ -111,12 +146,12 @@ def _run(lib, t, now, hashes=None):
                 int(t["flags"][i]), int(t["len"][i]), int(t["ep"][i]), h)
         if v6:
             sa, da = t["saddr"][i].tobytes(), t["daddr"][i].tobytes()
-            src = 0 if eg else lib.ref_lxc_src_identity6(sa, 0)
+            src = 0 if eg else nd.src6(sa, da, int(t["proto"][i]), 0)
             lib.ref_lxc_v6(sa, da, *cols, src, C.byref(v), C.byref(idv), C.byref(cr), C.byref(st), xd6,
                            C.byref(xp))
             out["xdaddr"][i] = np.frombuffer(xd6.raw, np.uint8)
         else:
-            src = 0 if eg else lib.ref_lxc_src_identity(int(t["saddr"][i]), 0)
+            src = 0 if eg else nd.src4(t["saddr"][i], t["daddr"][i], t["proto"][i], 0)
             lib.ref_lxc_v4(int(t["saddr"][i]), int(t["daddr"][i]), *cols, src, C.byref(v), C.byref(idv),
                            C.byref(cr), C.byref(st), C.byref(xd), C.byref(xp))
             out["xdaddr"][i] = xd.value
@@ -147,6 +182,7 @@ def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
     lib.ref_lxc_reset(1 << 20)
     for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
         lib.ref_lxc_ipcache_update(_b(k), _b(v))
+    nd = _Netdev(g["ipc_keys"], g["ipc_vals"])
     for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
         assert lib.ref_lxc_policy_update(int(ep), _b(k), _b(e)) == 0
     if svc:
@@ -169,7 +205,7 @@ def test_compiled_endpoint_program_reproduces_fixture(golden, fixture):
                 svc_update(_b(g["lb_keys"][d]), _b(v))
         sl = slice(int(cuts[bi]), int(cuts[bi + 1]))
         tb = {k: x[sl] for k, x in t.items()}
-        o = _run(lib, tb, int(nows[bi]), tb.get("hash"))
+        o = _run(lib, tb, int(nows[bi]), tb.get("hash"), nd)
         msg = f"{fixture} batch {bi}"
         np.testing.assert_array_equal(o["verdict"], g["b_verdict"][sl], err_msg=msg)
         np.testing.assert_array_equal(o["ct_ret"], g["b_ct_ret"][sl], err_msg=msg)
@@ -209,6 +245,7 @@ def test_compiled_endpoint_program_reproduces_stateless_fixture(golden, cfg):
     lib.ref_lxc_reset(1 << 20)
     for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
         lib.ref_lxc_ipcache_update(_b(k), _b(v))
+    nd = _Netdev(g["ipc_keys"], g["ipc_vals"])
     for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
         assert lib.ref_lxc_policy_update(int(ep), _b(k), _b(e)) == 0
     t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
@@ -222,7 +259,8 @@ def test_compiled_endpoint_program_reproduces_stateless_fixture(golden, cfg):
         eg = int(t["flags"][i]) & 1
         src = 0
         if not eg:
-            src = 2 if secctx_world else lib.ref_lxc_src_identity(int(t["saddr"][i]), src_cfg)
+            # WORLD_ID: the cilium_net form (derive_ipv4_sec_ctx)
+            src = 2 if secctx_world else nd.src4(t["saddr"][i], t["daddr"][i], t["proto"][i], src_cfg)
         lib.ref_lxc_v4(int(t["saddr"][i]), int(t["daddr"][i]), 0, int(t["dport"][i]), int(t["proto"][i]),
                        0, int(t["flags"][i]), int(t["len"][i]), int(t["ep"][i]), 0, src, C.byref(v),
                        C.byref(idv), C.byref(cr), C.byref(st), C.byref(xd), C.byref(xp))
@@ -233,3 +271,132 @@ def test_compiled_endpoint_program_reproduces_stateless_fixture(golden, cfg):
     np.testing.assert_array_equal(got[keep, 0], g[f"c{cfg}_verdict"][keep])
     np.testing.assert_array_equal(got[keep & ~gated, 1], g[f"c{cfg}_identity"][keep & ~gated])
     np.testing.assert_array_equal(got[keep & ~gated, 2], g[f"c{cfg}_stage"][keep & ~gated])
+
+
+# IPv6 extension-header numbers (ipv6_hdrlen walks them, lib/ipv6.h:61-98):
+# a tuple's nexthdr is the final protocol after them, so a tuple naming one
+# has no frame of that form (the v6 fixtures' gated tuples include 0)
+V6_EXT = (0, 43, 44, 50, 51, 59, 60)
+
+
+def _stateless_replay(g, gate_src, v6, lib, nd, src_cfg):
+    """Every tuple of a stateless fixture through the compiled endpoint
+    program with an empty conntrack map (the fixture's every-packet-CT_NEW
+    scope); ingress tuples carry the identity the compiled bpf_netdev.c hands
+    over.  Returns (verdict, identity, stage) per tuple."""
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
+    n = len(t["proto"])
+    v, cr, st = C.c_int(), C.c_int(), C.c_int()
+    idv, xd = C.c_uint32(), C.c_uint32()
+    xd6 = C.create_string_buffer(16)
+    xp = C.c_uint16()
+    got = np.zeros((n, 3), np.int64)
+    sport = t.get("sport", np.zeros(n, np.uint16))
+    hashes = t.get("hash", np.zeros(n, np.uint32))
+    for i in range(n):
+        if v6 and int(t["proto"][i]) in V6_EXT:
+            continue
+        lib.ref_lxc_ct_clear()
+        eg = int(t["flags"][i]) & 1
+        cols = (int(sport[i]), int(t["dport"][i]), int(t["proto"][i]), 0, int(t["flags"][i]),
+                int(t["len"][i]), int(t["ep"][i]), int(hashes[i]))
+        if v6:
+            sa, da = t["saddr"][i].tobytes(), t["daddr"][i].tobytes()
+            src = 0 if eg else nd.src6(sa, da, t["proto"][i], src_cfg)
+            lib.ref_lxc_v6(sa, da, *cols, src, C.byref(v), C.byref(idv), C.byref(cr), C.byref(st), xd6,
+                           C.byref(xp))
+        else:
+            src = 0 if eg else nd.src4(t["saddr"][i], t["daddr"][i], t["proto"][i], src_cfg)
+            lib.ref_lxc_v4(int(t["saddr"][i]), int(t["daddr"][i]), *cols, src, C.byref(v), C.byref(idv),
+                           C.byref(cr), C.byref(st), C.byref(xd), C.byref(xp))
+        got[i] = v.value, idv.value, st.value
+    return t, got
+
+
+@pytest.mark.parametrize("fixture,cfg", [("classify_v4_lb.npz", 0), ("classify_v6.npz", 0),
+                                         ("classify_v6.npz", 2), ("classify_v6.npz", 3),
+                                         ("classify_v6_lb.npz", 0)])
+def test_compiled_endpoint_program_reproduces_restated_orders(golden, fixture, cfg):
+    """The fixtures whose endpoint-program order the harnesses restate step by
+    step -- config 5's egress service step before ipcache and policy
+    (classify_v4_lb.npz: lb4_local, then ipcache on tuple.daddr and policy on
+    the rewritten dport, bpf_lxc.c:444-505), the IPv6 decision (classify_v6.npz:
+    ipv6_l3_from_lxc / ipv6_policy with the ROUTER_IP /64 fallback,
+    bpf_lxc.c:158-203, :731-800) and the IPv6 service step
+    (classify_v6_lb.npz, bpf_lxc.c:108-139) -- replayed through the compiled
+    bpf_lxc.c: verdict of every TCP / UDP / gated tuple, and identity and
+    stage of every tuple that reached a policy probe (ICMP tuples carry a
+    policy port the frame's type does not; the CONNTRACK builds only)."""
+    g = golden(fixture)
+    v6 = "v6" in fixture
+    row = [int(x) for x in g["configs"][cfg]]
+    gate, src_cfg = row[0], row[1]
+    assert gate == 1
+    lib = _lib()
+    lib.ref_lxc_reset(1 << 20)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        lib.ref_lxc_ipcache_update(_b(k), _b(v))
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert lib.ref_lxc_policy_update(int(ep), _b(k), _b(e)) == 0
+    if "lb_keys" in g.files:
+        upd = lib.ref_lxc_svc6_update if v6 else lib.ref_lxc_svc_update
+        for k, v in zip(g["lb_keys"], g["lb_vals"]):
+            upd(_b(k), _b(v))
+    nd = _Netdev(g["ipc_keys"], g["ipc_vals"])
+    t, got = _stateless_replay(g, row, v6, lib, nd, src_cfg)
+    icmp = np.isin(t["proto"], [1, 58])
+    gated = ~np.isin(t["proto"], [1, 6, 17, 58])
+    keep = ~icmp & ~(np.isin(t["proto"], V6_EXT) & v6)
+    assert keep.sum() > 3000 and gated.sum() > 0
+    np.testing.assert_array_equal(got[keep, 0], g[f"c{cfg}_verdict"][keep])
+    probed = keep & (g[f"c{cfg}_stage"] <= 3) & ~gated
+    assert probed.sum() > 2000
+    np.testing.assert_array_equal(got[probed, 1], g[f"c{cfg}_identity"][probed])
+    np.testing.assert_array_equal(got[probed, 2], g[f"c{cfg}_stage"][probed])
+    if "lb_keys" in g.files:
+        # the service step's drops are the compiled program's too
+        drop = keep & (g[f"c{cfg}_verdict"] == -158)
+        assert drop.sum() > 0 and (got[drop, 0] == -158).all()
+
+
+def test_compiled_endpoint_program_reproduces_frame_parse(golden):
+    """tests/golden/frames.npz (harness_frame.c: the header steps before
+    policy, bpf_lxc.c's dispatch and handlers restated in order) against the
+    compiled program on the raw frames, in the build the compiled harness
+    has (CONNTRACK, the SMAC / DMAC / SIP checks disabled: the fixture's
+    "nover" variant): every frame's status -- reached policy, not
+    classified, or the drop before policy -- and, for frames that reached
+    policy, the protocol and the port the policy step sees and the
+    addresses (the first conntrack key's, in either order)."""
+    g = golden("frames.npz")
+    lib = _lib()
+    lib.ref_lxc_frame.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_int,
+                                  C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_char_p,
+                                  C.POINTER(C.c_uint16), C.POINTER(C.c_uint8)]
+    lib.ref_lxc_reset(1 << 20)
+    data, ln, fl, ep = g["data"], g["len"], g["flags"], g["ep"]
+    n, width = data.shape
+    st, fam = C.c_int(), C.c_int()
+    kd, ks = C.create_string_buffer(16), C.create_string_buffer(16)
+    dp, pr = C.c_uint16(), C.c_uint8()
+    status = np.zeros(n, np.int64)
+    family = np.zeros(n, np.int64)
+    port = np.zeros(n, np.uint16)
+    proto = np.zeros(n, np.uint8)
+    addrs = [None] * n
+    for i in range(n):
+        stored = min(int(ln[i]), width)
+        assert lib.ref_lxc_frame(data[i].tobytes(), stored, int(ln[i]), int(fl[i]), int(ep[i]),
+                                 C.byref(st), C.byref(fam), kd, ks, C.byref(dp), C.byref(pr)) == 0
+        status[i], family[i], port[i], proto[i] = st.value, fam.value, dp.value, pr.value
+        addrs[i] = {kd.raw, ks.raw}
+    want = g["nover_status"].astype(np.int64)
+    np.testing.assert_array_equal(status, want)
+    ok = want == 0
+    assert ok.sum() > 1000 and len(np.unique(want)) >= 6
+    np.testing.assert_array_equal(family[ok], g["nover_family"][ok])
+    nofrag = ok & (g["nover_frag"] == 0)
+    np.testing.assert_array_equal(proto[nofrag], g["nover_proto"][nofrag])
+    np.testing.assert_array_equal(port[nofrag], g["nover_dport"][nofrag])
+    for i in np.flatnonzero(ok):
+        assert addrs[i] == {g["nover_saddr"][i].tobytes(), g["nover_daddr"][i].tobytes()}, i
