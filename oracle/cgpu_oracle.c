@@ -339,6 +339,8 @@ static inline uint8_t *oh_get(const struct ohash *h, const void *key)
 	return i < 0 ? NULL : h->vals + i * h->vsz;
 }
 
+#include "fast_lpm.h"
+
 /* ====================================================================== */
 /* Context                                                                 */
 /* ====================================================================== */
@@ -362,6 +364,9 @@ struct or_ctx {
 	size_t ct_max;              /* CT_MAP_SIZE */
 	uint64_t metrics[N_METRICS];
 	uint64_t cls[OR_CLS_N];     /* reference map lookups by map since or_probe_split */
+	struct fast_lpm *fast;      /* or_set_fast: DIR-24-8 / multibit ipcache lookups */
+	struct fast_lpm *fpf4, *fpf6; /* ... and the prefilter's dyn4 / dyn6 */
+	int view;                   /* a shard view: shares the base's tables */
 };
 
 /* Reference map lookups counted per map (the roofline prices each map's
@@ -437,6 +442,9 @@ void or_destroy(or_ctx *c)
 {
 	if (!c)
 		return;
+	fl_free(c->fast);
+	fl_free(c->fpf4);
+	fl_free(c->fpf6);
 	lpm_destroy(&c->ipcache);
 	lpm_destroy(&c->dyn4);
 	lpm_destroy(&c->dyn6);
@@ -468,6 +476,7 @@ or_ctx *or_view_create(or_ctx *base)
 	oh_init(&v->ct6, 38, 56);
 	memset(v->metrics, 0, sizeof(v->metrics));
 	memset(v->cls, 0, sizeof(v->cls));
+	v->view = 1; /* the fast tables stay the base's */
 	return v;
 }
 
@@ -505,14 +514,42 @@ void or_set_config(or_ctx *c, const or_config *cfg)
 	c->cfg = *cfg;
 }
 
+/* the optimized lookups answer for the ipcache they were built from: any
+ * change drops them (or_set_fast builds them again) */
+static void fast_drop(or_ctx *c)
+{
+	fl_free(c->fast);
+	fl_free(c->fpf4);
+	fl_free(c->fpf6);
+	c->fast = c->fpf4 = c->fpf6 = NULL;
+}
+
 int or_ipcache_update(or_ctx *c, const void *key24, const void *val8)
 {
+	fast_drop(c);
 	return lpm_update(&c->ipcache, key24, val8);
 }
 
 int or_ipcache_delete(or_ctx *c, const void *key24)
 {
+	fast_drop(c);
 	return lpm_delete(&c->ipcache, key24);
+}
+
+/* 1: ipcache lookups through a DIR-24-8 (IPv4) and a multibit trie with
+ * per-/64 lists (IPv6) built from the current ipcache (fast_lpm.h); 0: the
+ * kernel-like trie.  Same answers either way. */
+int or_set_fast(or_ctx *c, int on)
+{
+	if (c->view)
+		return -EINVAL;
+	fast_drop(c);
+	if (on) {
+		c->fast = fl_build(&c->ipcache, 1);
+		c->fpf4 = fl_build(&c->dyn4, 0);
+		c->fpf6 = fl_build(&c->dyn6, 0);
+	}
+	return 0;
 }
 
 int or_ipcache_lookup(or_ctx *c, const void *key24, void *val8_out)
@@ -568,6 +605,7 @@ int or_policy_lookup(or_ctx *c, uint32_t ep, const void *key8, void *entry24_out
 int or_cidr_update(or_ctx *c, int which, const void *key)
 {
 	uint8_t one = 0;
+	fast_drop(c);
 	switch (which) {
 	case 0: return lpm_update(&c->dyn4, key, &one);
 	case 1: return oh_update(&c->fix4, key, &one);
@@ -579,6 +617,7 @@ int or_cidr_update(or_ctx *c, int which, const void *key)
 
 int or_cidr_delete(or_ctx *c, int which, const void *key)
 {
+	fast_drop(c);
 	switch (which) {
 	case 0: return lpm_delete(&c->dyn4, key);
 	case 1: return oh_delete(&c->fix4, key);
@@ -608,6 +647,8 @@ int or_endpoint_delete(or_ctx *c, const void *key20)
 static const uint8_t *ipcache4(const or_ctx *c, uint32_t addr_be)
 {
 	tl_cls[OR_CLS_IPCACHE]++;
+	if (c->fast)
+		return fl_lookup4(c->fast, addr_be);
 	uint8_t key[24];
 	uint32_t plen = 64;
 	memset(key, 0, sizeof(key));
@@ -621,6 +662,8 @@ static const uint8_t *ipcache4(const or_ctx *c, uint32_t addr_be)
 static const uint8_t *ipcache6(const or_ctx *c, const uint8_t *addr16)
 {
 	tl_cls[OR_CLS_IPCACHE]++;
+	if (c->fast)
+		return fl_lookup6(c->fast, addr16);
 	uint8_t key[24];
 	uint32_t plen = 160;
 	memset(key, 0, sizeof(key));
@@ -628,6 +671,26 @@ static const uint8_t *ipcache6(const or_ctx *c, const uint8_t *addr16)
 	key[7] = 2; /* ENDPOINT_KEY_IPV6 */
 	memcpy(key + 8, addr16, 16);
 	return lpm_lookup(&c->ipcache, key);
+}
+
+/* the batch paths' lookups (ipcache4 / ipcache6, through the fast tables
+ * when or_set_fast is on): value bytes or -ENOENT */
+int or_ipcache_lookup4(or_ctx *c, uint32_t addr_be, void *val8_out)
+{
+	const uint8_t *v = ipcache4(c, addr_be);
+	if (!v)
+		return -ENOENT;
+	memcpy(val8_out, v, 8);
+	return 0;
+}
+
+int or_ipcache_lookup6(or_ctx *c, const uint8_t *addr16, void *val8_out)
+{
+	const uint8_t *v = ipcache6(c, addr16);
+	if (!v)
+		return -ENOENT;
+	memcpy(val8_out, v, 8);
+	return 0;
 }
 
 struct pol_res {
@@ -1510,7 +1573,11 @@ static void *pf_worker(void *arg)
 			if (dyn) { /* CIDR{4,6}_LPM_PREFILTER */
 				j->probes++;
 				tl_cls[OR_CLS_PREFILTER]++;
-				if (lpm_lookup(j->v6 ? &c->dyn6 : &c->dyn4, pfx))
+				const struct fast_lpm *fp = j->v6 ? c->fpf6 : c->fpf4;
+				uint32_t a4;
+				memcpy(&a4, pfx + 4, 4);
+				if (fp ? (j->v6 ? fl_lookup6(fp, pfx + 4) : fl_lookup4(fp, a4)) != NULL
+				       : lpm_lookup(j->v6 ? &c->dyn6 : &c->dyn4, pfx) != NULL)
 					v = XDP_DROP;
 			}
 			if (!v) {

@@ -47,6 +47,14 @@ void or_default_config(or_config *cfg);
  * conntrack operations are a call's probe_sum minus these.  Read and reset. */
 enum { OR_CLS_IPCACHE = 0, OR_CLS_POLICY, OR_CLS_LB, OR_CLS_PREFILTER, OR_CLS_ENDPOINT, OR_CLS_N };
 void or_probe_split(or_ctx *c, uint64_t *out /* [OR_CLS_N] */);
+/* ipcache lookups through a DIR-24-8 (IPv4) and a multibit trie (IPv6)
+ * built from the current ipcache (1), or the kernel-like trie (0): the
+ * "optimized CPU" baseline of BASELINE.md §2, same answers.  An ipcache
+ * change drops the fast tables; -EINVAL on a shard view. */
+int or_set_fast(or_ctx *c, int on);
+/* the batch paths' ipcache lookups (fast or trie): value or -ENOENT */
+int or_ipcache_lookup4(or_ctx *c, uint32_t addr_be, void *val8_out);
+int or_ipcache_lookup6(or_ctx *c, const uint8_t *addr16, void *val8_out);
 
 /* table ops: 0 on success, -errno (bpf(2) convention) on failure */
 int or_ipcache_update(or_ctx *c, const void *key24, const void *val8);

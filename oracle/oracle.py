@@ -119,6 +119,9 @@ def lib():
         L.or_metrics_read.argtypes = [vp, vp]
         L.or_probe_split.argtypes = [vp, vp]
         L.or_probe_split.restype = None
+        L.or_set_fast.argtypes = [vp, C.c_int]
+        L.or_ipcache_lookup4.argtypes = [vp, C.c_uint32, vp]
+        L.or_ipcache_lookup6.argtypes = [vp, C.c_char_p, vp]
         L.or_counters_reset.argtypes = [vp]
         _lib = L
     return _lib
@@ -585,6 +588,24 @@ class Oracle:
                             p(prog.rule_clauses), len(prog.rule_subject), p(prog.clauses), p(eo),
                             p(el), len(ep_sets), p(io), p(il), len(id_sets), flags, p(allow))
         return allow
+
+    def ipcache_lookup_addr(self, addr):
+        """The batch paths' ipcache lookup of one address (network-order u32
+        for IPv4, 16 bytes for IPv6): (rc, 8 value bytes)."""
+        buf = C.create_string_buffer(8)
+        if isinstance(addr, (bytes, bytearray, np.ndarray)) and len(bytes(addr)) == 16:
+            rc = self.L.or_ipcache_lookup6(self.h, bytes(addr), buf)
+        else:
+            rc = self.L.or_ipcache_lookup4(self.h, int(addr), buf)
+        return rc, buf.raw
+
+    def set_fast(self, on=True):
+        """or_set_fast: the optimized CPU ipcache (DIR-24-8 for IPv4, a
+        multibit trie for IPv6, oracle/fast_lpm.h) built from the current
+        ipcache, or back to the kernel-like trie.  Same answers; an ipcache
+        change drops it."""
+        rc = self.L.or_set_fast(self.h, 1 if on else 0)
+        assert rc == 0, rc
 
     PROBE_MAPS = ("ipcache", "policy", "lb", "prefilter", "endpoint")
 

@@ -89,8 +89,11 @@ def test_policy_raw_codes(golden):
     assert (g["ret"][fr] == L.DROP_FRAG_NOSUPPORT).all() and fr.sum() > 0
 
 
-def test_ipcache_lpm_vs_reference(golden):
-    """ipcache_lookup4/6 (bpf/lib/eps.h:56-80) over kernel LPM semantics."""
+@pytest.mark.parametrize("fast", [False, True])
+def test_ipcache_lpm_vs_reference(golden, fast):
+    """ipcache_lookup4/6 (bpf/lib/eps.h:56-80) over kernel LPM semantics:
+    the kernel-like trie, and the optimized CPU lookups of the batch paths
+    (DIR-24-8 / multibit trie, or_set_fast) on the same ipcache."""
     g = golden("ipcache_lpm.npz")
     keys, vals = g["keys"], g["vals"]
     n_static = int(g["n_static"])
@@ -98,6 +101,8 @@ def test_ipcache_lpm_vs_reference(golden):
         o = Oracle()
         for k, v in zip(keys[:upto], vals[:upto]):
             assert o.ipcache_update(k, v) == 0
+        if fast:
+            o.set_fast(True)
         for fam, q, r in ((4, g["q4"], g["r4" + phase]), (6, g["q6"], g["r6" + phase])):
             for i in range(len(q)):
                 key = np.zeros((), L.IPCACHE_KEY)
@@ -108,7 +113,10 @@ def test_ipcache_lpm_vs_reference(golden):
                 else:
                     key["prefixlen"] = 160
                     key["ip"][:] = q[i]
-                rc, val = o.ipcache_lookup(key)
+                if fast:
+                    rc, val = o.ipcache_lookup_addr(int(q[i]) if fam == 4 else bytes(q[i]))
+                else:
+                    rc, val = o.ipcache_lookup(key)
                 found = rc == 0
                 assert found == bool(r[i][0]), (phase, fam, i)
                 if found:
@@ -116,9 +124,12 @@ def test_ipcache_lpm_vs_reference(golden):
                     assert (lab, tun) == (r[i][1], r[i][2]), (phase, fam, i)
 
 
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("ci", range(5))
-def test_classify_v4_vs_reference(golden, ci):
-    """Full stateless tuple decision: verdict, identity, stage, probes, counters."""
+def test_classify_v4_vs_reference(golden, ci, fast):
+    """Full stateless tuple decision: verdict, identity, stage, probes,
+    counters; with the kernel-like trie and with the optimized CPU ipcache
+    (DIR-24-8, the cpu_baseline's "optimized" figure)."""
     g = golden("classify_v4.npz")
     gate, src, sw = (int(x) for x in g["configs"][ci])
     o = Oracle(ct_proto_gate=gate, ingress_src_identity=src, ingress_secctx_world=sw)
@@ -126,6 +137,8 @@ def test_classify_v4_vs_reference(golden, ci):
         assert o.ipcache_update(k, v) == 0
     for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
         assert o.policy_update(int(ep), k, e) == 0
+    if fast:
+        o.set_fast(True)
     t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
     for nthreads in (1, 4):
         o.counters_reset()
@@ -181,7 +194,10 @@ def parse_frames(g):
     return fam, flags, s4, d4, s6, d6
 
 
-def test_xdp_prefilter_vs_reference(golden):
+@pytest.mark.parametrize("fast", [False, True])
+def test_xdp_prefilter_vs_reference(golden, fast):
+    """check_v4 / check_v6 (bpf_xdp.c:88-184); fast: the deny LPMs through
+    the optimized CPU structures (DIR-24-8 / multibit trie)."""
     g = golden("xdp_prefilter.npz")
     o = Oracle()
     for w, name in enumerate(("dyn4", "fix4", "dyn6", "fix6")):
@@ -189,6 +205,8 @@ def test_xdp_prefilter_vs_reference(golden):
             assert o.cidr_update(w, k) == 0
     for k in g["endpoints"]:
         assert o.endpoint_update(k) == 0
+    if fast:
+        o.set_fast(True)
     fam, flags, s4, d4, s6, d6 = parse_frames(g)
     v4 = fam == 4
     out4, p4 = o.prefilter_v4(s4[v4], d4[v4], flags[v4])
@@ -247,8 +265,9 @@ def test_oracle_table_ops_errno():
     assert o.ipcache_delete(L.ipcache_key("10.0.0.0/8")) == -2
 
 
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("ci", range(4))
-def test_classify_v6_vs_reference(golden, ci):
+def test_classify_v6_vs_reference(golden, ci, fast):
     g = golden("classify_v6.npz")
     gate, src = (int(x) for x in g["configs"][ci])
     o = Oracle(ct_proto_gate=gate, ingress_src_identity=src, router_ip=g["router_ip"].tobytes())
@@ -256,6 +275,8 @@ def test_classify_v6_vs_reference(golden, ci):
         assert o.ipcache_update(k, v) == 0
     for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
         assert o.policy_update(int(ep), k, e) == 0
+    if fast:
+        o.set_fast(True)  # the multibit trie of the optimized CPU baseline
     t = {k[2:]: g[k] for k in g.files if k.startswith("t_")}
     v, idt, st, probes = o.classify_v6(t, nthreads=3)
     np.testing.assert_array_equal(o.metrics(), g[f"c{ci}_metrics"])
