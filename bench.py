@@ -348,8 +348,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    if args.host_tuples and args.config != "gpu":
-        raise SystemExit("--host-tuples measures config 2 (--config gpu) only")
+    if args.host_tuples and args.config not in ("gpu", "frames"):
+        raise SystemExit("--host-tuples measures config 2 (--config gpu) and its raw frames (--config frames)")
     pf6 = args.config == "pf6"
     cascade = args.config == "cascade"
     frames = args.config == "frames"
@@ -441,6 +441,16 @@ def main():
     if pf6:
         d = synth.packets6_to_device(tup, dev)
         out = {"verdict": torch.empty(n, dtype=torch.uint8, device=dev)}
+    elif frames and args.host_tuples:
+        # the frames in page-locked HOST memory (a receive ring), outputs
+        # back into it: cgpu_classify_frames_host (PCIe-inclusive)
+        fr = synth.frames_from_tuples(tup, stride=FRAME_STRIDE)
+        d = {"data": torch.from_numpy(np.ascontiguousarray(fr["data"])).pin_memory(),
+             "len": torch.from_numpy(np.ascontiguousarray(fr["len"], np.uint32).view(np.int32)).pin_memory(),
+             "flags": torch.from_numpy(np.ascontiguousarray(fr["flags"], np.uint8)).pin_memory(),
+             "ep": torch.from_numpy(np.ascontiguousarray(fr["ep"], np.uint16).view(np.int16)).pin_memory()}
+        out = {"verdict": torch.empty(n, dtype=torch.int32).pin_memory(),
+               "identity": torch.empty(n, dtype=torch.int32).pin_memory(), "stage": None}
     elif frames:
         fr = synth.frames_from_tuples(tup, stride=FRAME_STRIDE)
         d = synth.frames_to_device(fr, dev)
@@ -500,6 +510,8 @@ def main():
             e.classify_v4_lb(d, out=out, stream=stream)
         elif v6:
             e.classify_v6(d, out=out, stream=stream)
+        elif frames and args.host_tuples:
+            e.classify_frames_host(d, out=out, stream=stream)
         elif frames:
             e.classify_frames(d, out=out, stream=stream)
         elif args.host_tuples:
@@ -790,18 +802,20 @@ def main():
             conf["schedule"] = args.schedule
         if args.host_tuples:
             bw = link_rates(torch, dev)
-            per_in, per_out = B_IN, B_OUT  # bytes up / down per tuple
+            # bytes up / down per tuple (frames: the 64-byte slot + len, flags, ep)
+            per_in, per_out = (B_IN_FRAMES if frames else B_IN), B_OUT
             conf.update(host_tuples=True,
                         pcie_measured_gbs=bw,
                         numa={"gpu": gpu_numa_node(torch, dev),
-                              "inputs": numa_nodes(d["saddr"]), "verdict": numa_nodes(out["verdict"]),
+                              "inputs": numa_nodes(d["data" if frames else "saddr"]),
+                              "verdict": numa_nodes(out["verdict"]),
                               "identity": numa_nodes(out["identity"])},
                         ingest_bound_mpps=round(min(bw["h2d"] * 1e3 / per_in, bw["d2h"] * 1e3 / per_out), 1),
                         hbm_resident_roofline=roof,
-                        note=("PCIe-inclusive: the columns (18 B/tuple) go up and the verdict + identity "
-                              "(8 B) come down every step through double-buffered 4M-tuple chunks; "
-                              "ingest_bound_mpps = the measured link rate over those bytes. The "
-                              "HBM-resident rate is the default line (no --host-tuples)"))
+                        note=(f"PCIe-inclusive: the {'frames (64-B slots + len, flags, ep: 71 B' if frames else 'columns (18 B'}"
+                              "/tuple) go up and the verdict + identity (8 B) come down every step through "
+                              "the device staging chunks; ingest_bound_mpps = the measured link rate over "
+                              "those bytes. The HBM-resident rate is the default line (no --host-tuples)"))
             # the host line is bound by the link, both directions at once: the
             # floor is the slower direction's bytes at its measured rate
             t_s = ms_per_step * 1e-3
@@ -831,7 +845,8 @@ def main():
                                                 "(+ service lookups), counted by the restatement "
                                                 "over the whole batch")
         result = {
-            "metric": ("Mpps classified from host-resident batches (PCIe-inclusive)" if args.host_tuples
+            "metric": (f"Mpps classified from host-resident {'raw frames' if frames else 'batches'} (PCIe-inclusive)"
+                       if args.host_tuples
                        else METRIC if not pf6 else "Mpps XDP IPv6 prefilter verdicts; % HBM roofline"),
             "value": round(value, 2), "unit": "Mpps", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),

@@ -1399,6 +1399,21 @@ __host__ __device__ __forceinline__ uint32_t v6t_lds_bloom(const v6_lpm &t)
 	return t.root && t.bl64 && t.bl64_mask < V6T_BLOOM_MAX_WORDS ? t.bl64_mask + 1u : 0u;
 }
 
+/* 1: the x4 lookups read a node's whole 128-B line (boundaries, outer AND
+ * the 16 region labels) in one go and select the label in registers, so a
+ * lookup has no dependent label load; 0: the 64-B
+ * boundary half, then the label word */
+#ifndef CGPU_V6T_FULL_LINE
+#define CGPU_V6T_FULL_LINE 0
+#endif
+
+__device__ __forceinline__ uint32_t sel16(const uint4 &a, const uint4 &b, const uint4 &c, const uint4 &d, uint32_t i)
+{
+	const uint4 v = (i & 8u) ? ((i & 4u) ? d : c) : ((i & 4u) ? b : a);
+	const uint32_t lo = (i & 1u) ? v.y : v.x, hi = (i & 1u) ? v.w : v.z;
+	return (i & 2u) ? hi : lo;
+}
+
 /* bl: the /64 bloom staged in LDS (v6_lpm.bl64), or NULL: probe h64 for
  * every tuple under a deep /32 */
 template <int Q>
@@ -1462,6 +1477,8 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 	bool node[Q], deep[Q], out[Q];
 	uint32_t line[Q], home[Q];
 	uint4 q0[Q], q1[Q], q2[Q], q3[Q], h0[Q], h1[Q];
+	constexpr bool FULL = CGPU_V6T_FULL_LINE && V6T_NB == 15u;
+	uint4 q4[FULL ? Q : 1], q5[FULL ? Q : 1], q6[FULL ? Q : 1], q7[FULL ? Q : 1];
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		node[u] = b32i[u] != 0xFFFFFFFFu && (n[u].x & DIR_TAG_MASK) == DIR_TAG_GROUP;
@@ -1484,12 +1501,20 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		q0[u] = q1[u] = q2[u] = q3[u] = h0[u] = h1[u] = make_uint4(0, 0, 0, 0);
+		if constexpr (FULL)
+			q4[u] = q5[u] = q6[u] = q7[u] = make_uint4(0, 0, 0, 0);
 		if (node[u]) {
 			const uint4 *q = reinterpret_cast<const uint4 *>(t.pool) + (V6T_LW / 4u) * line[u];
 			q0[u] = q[0];
 			q1[u] = q[1];
 			q2[u] = q[2];
 			q3[u] = q[3];
+			if constexpr (FULL) {
+				q4[u] = q[4];
+				q5[u] = q[5];
+				q6[u] = q[6];
+				q7[u] = q[7];
+			}
 		}
 		if (deep[u]) {
 			h0[u] = t.h64[2u * home[u]];
@@ -1502,10 +1527,18 @@ __device__ __forceinline__ void v6t_lookup_q(const v6_lpm &t, const uint32_t *ld
 		lab[u] = 0;
 		if (!node[u])
 			continue;
-		if (((n[u].y >> 5) & 7u) == V6T_LONG)
+		if (((n[u].y >> 5) & 7u) == V6T_LONG) {
 			lab[u] = v6t_long(t.pool, line[u], q0[u].x, w[u].y);
-		else
+		} else if constexpr (FULL) {
+			const uint32_t x = w[u].y;
+			const uint32_t c = (q0[u].x < x) + (q0[u].y < x) + (q0[u].z < x) + (q0[u].w < x) +
+					   (q1[u].x < x) + (q1[u].y < x) + (q1[u].z < x) + (q1[u].w < x) +
+					   (q2[u].x < x) + (q2[u].y < x) + (q2[u].z < x) + (q2[u].w < x) +
+					   (q3[u].x < x) + (q3[u].y < x) + (q3[u].z < x);
+			lab[u] = out[u] ? q3[u].w : sel16(q4[u], q5[u], q6[u], q7[u], c);
+		} else {
 			lab[u] = v6t_label(t.pool, line[u], out[u], q0[u], q1[u], q2[u], q3[u], w[u].y);
+		}
 	}
 #pragma unroll
 	for (int u = 0; u < Q; u++) {

@@ -46,7 +46,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "svc_decq": ("CGPU_CT_SVC_DECQ=1",), "svc_decq6": ("CGPU_CT_SVC_DECQ6=1",),
             "walk_w4": ("CGPU_WALK_W=4",), "walk_w3": ("CGPU_WALK_W=3",),
             "cc_probe2": ("CC_PROBE=2",), "cc_probe4": ("CC_PROBE=4",),
-            "owed_by_pair": ("CGPU_OWED_BY_KEY=0",), "ct_len_sort": ("CGPU_CT_LH=0",)}
+            "owed_by_pair": ("CGPU_OWED_BY_KEY=0",), "ct_len_sort": ("CGPU_CT_LH=0",),
+            "v6_half_line": ("CGPU_V6T_FULL_LINE=0",)}
 
 
 def build(names):
