@@ -4237,7 +4237,10 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
  * chunk k's columns go up on the h2d stream, its classify runs on the
  * caller's stream, its outputs come back on the d2h stream, so chunk k + 1's
  * upload and chunk k - 1's download overlap chunk k's classify. */
-#define HS_CHUNK (1u << 22)
+#ifndef CGPU_HS_CHUNK_LOG2 /* tuples per staging chunk (timing-only A/B builds vary it) */
+#define CGPU_HS_CHUNK_LOG2 22
+#endif
+#define HS_CHUNK (1u << CGPU_HS_CHUNK_LOG2)
 #define HS_NBUF 16
 /* one staging pair holds HS_CHUNK v4 tuples (18 B in, 9 B out) in
  * 256-aligned columns; a wider tuple (frames) takes fewer per chunk */

@@ -3759,6 +3759,12 @@ hipError_t launch_copy_host(void *dst, const void *src, uint64_t bytes, hipStrea
 	return hipGetLastError();
 }
 
+/* blocks per segment row of the host copies (timing-only A/B builds vary it,
+ * tools/host_ab.py) */
+#ifndef CGPU_HS_COPY_G
+#define CGPU_HS_COPY_G 128
+#endif
+
 /* every column of a chunk in ONE launch: segment blockIdx.y, the blocks of
  * a row grid-stride over it (a launch per column left ~10 us gaps between
  * seven small kernels per chunk, profiles/r4_ah) */
@@ -3796,7 +3802,8 @@ hipError_t launch_copy_host_multi(const copy_segs &d, hipStream_t st)
 	if (!d.n || !most)
 		return hipSuccess;
 	/* the longest segment sets the row width; shorter rows' spare blocks exit */
-	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((most >> 4) + 1023) / 1024, 128));
+	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(((most >> 4) + 1023) / 1024,
+									     CGPU_HS_COPY_G));
 	hipLaunchKernelGGL(k_copy_host_multi, dim3(g, d.n), dim3(256), 0, st, d);
 	return hipGetLastError();
 }

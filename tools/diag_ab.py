@@ -47,7 +47,10 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "walk_w4": ("CGPU_WALK_W=4",), "walk_w3": ("CGPU_WALK_W=3",),
             "cc_probe2": ("CC_PROBE=2",), "cc_probe4": ("CC_PROBE=4",),
             "owed_by_pair": ("CGPU_OWED_BY_KEY=0",), "ct_len_sort": ("CGPU_CT_LH=0",),
-            "v6_half_line": ("CGPU_V6T_FULL_LINE=0",)}
+            "v6_full_line": ("CGPU_V6T_FULL_LINE=1",),
+            "hs_g256": ("CGPU_HS_COPY_G=256",), "hs_g512": ("CGPU_HS_COPY_G=512",),
+            "hs_g64": ("CGPU_HS_COPY_G=64",), "hs_chunk23": ("CGPU_HS_CHUNK_LOG2=23",),
+            "hs_chunk21": ("CGPU_HS_CHUNK_LOG2=21",)}
 
 
 def build(names):
