@@ -6020,7 +6020,14 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 	auto ret_flush = [&]() {
 		for (uint32_t k = 0; k < nret; k++) {
 			const uint32_t i = s_ri[k][threadIdx.x], ret = s_rr[k][threadIdx.x];
+#if defined(CGPU_DIAG_NO_RET) /* timing only: the walk without its result stores */
+#elif defined(CGPU_DIAG_RET_SMALL) /* timing only: the stores into 1 MiB */
+			a.ct_ret[i & 0xFFFFFu] = (uint8_t)ret;
+#elif defined(CGPU_DIAG_RET_NT)
+			__builtin_nontemporal_store((uint8_t)ret, a.ct_ret + i);
+#else
 			a.ct_ret[i] = (uint8_t)ret;
+#endif
 			if (!K::ADDR && MODE == WALK_PKT && (ret & CT_RELP))
 				a.f2[2u * i + 1u] = 1u; /* its ICMP entry is owed to phase 2 */
 		}
@@ -6636,8 +6643,12 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 }
 
 
-/* resident walker grid: 256 CUs x 8 workgroups of 4 waves */
-#define CT_WALK_GRID 2048
+/* walker grid: 8192 workgroups of 4 waves, ~4 rounds of the resident
+ * ~2300: a lane takes fewer groups, so the walk's tail is shorter (2048:
+ * +0.35 ms on --config ct, +0.44 ms on ctlb, profiles/r5_i/ab_grid_*.log) */
+#ifndef CT_WALK_GRID
+#define CT_WALK_GRID 8192
+#endif
 
 template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
