@@ -1606,6 +1606,11 @@ struct ftuple {
 #define CGPU_FF_H 2 /* fused frames: slots loaded together (1, 2, 4) */
 #endif
 #define FF_H CGPU_FF_H
+#ifndef CGPU_FF_STAGE
+#define CGPU_FF_STAGE 1 /* fused frames: coalesced tile loads handed out through LDS */
+#endif
+/* fused frames' LDS rows per wave: 64 slots x 80 B */
+#define FF_STG_U4 320u
 
 __device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fwin &W, const uint8_t *f,
 						uint32_t len, uint32_t cap, bool egress, uint32_t ep,
@@ -1666,6 +1671,8 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	 * four parse statuses, after the cold-slot cache (launch_x4's LDS) */
 	uint4 *lxl = reinterpret_cast<uint4 *>((reinterpret_cast<uintptr_t>(cck + a.cc_n) + 15u) & ~(uintptr_t)15u);
 	int16_t *fst = reinterpret_cast<int16_t *>(lxl + (FF ? 2u * FR_LXC_LDS : 0u));
+	/* fused frames: this wave's staging rows, after the statuses */
+	uint4 *stg = reinterpret_cast<uint4 *>(fst + (FF ? NT * Q : 0)) + (threadIdx.x >> 6) * FF_STG_U4;
 	if constexpr (FF) {
 		for (uint32_t k = threadIdx.x; k < 2u * s.n_lxc; k += NT)
 			lxl[k] = s.lxc[k];
@@ -1696,7 +1703,9 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	for (uint64_t g = t0;; g += T) {
 		/* FF: i0 = the wave's first frame, frame u of the lane at iu(u) */
 		const uint64_t i0 = FF ? wave_uniform64((g - lane) * Q) : g * Q;
-		const bool live = FF ? i0 + lane < a.n : i0 < a.n;
+		/* FF: wave-uniform, every lane of the wave stages its part of the
+		 * tile; a lane past the batch carries no tuple (F_OK clear) */
+		const bool live = i0 < a.n;
 		if (!live)
 			break;
 		const bool full = FF ? false : i0 + Q <= a.n;
@@ -1720,7 +1729,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 				for (int u = 0; u < Q; u++) {
 					const bool ok = iu(u) < a.n;
-					const uint64_t i = ok ? iu(u) : i0 + lane;
+					const uint64_t i = ok ? iu(u) : i0;
 					len[u] = a.len[i];
 					flv[u] = a.flags[i];
 					ep[u] = a.ep[i];
@@ -1728,19 +1737,48 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 #pragma unroll
 				for (int u = 0; u < Q; u++) {
 					const bool ok = iu(u) < a.n;
-					const uint64_t i = ok ? iu(u) : i0 + lane;
+					const uint64_t i = ok ? iu(u) : i0;
 					/* FF_H frames' slots in flight at a time (registers) */
 					if (u % FF_H == 0) {
 #pragma unroll
 						for (int h = 0; h < FF_H; h++) {
+#if CGPU_FF_STAGE
+							/* the wave's tile of 64 slots as four coalesced
+							 * 1-KiB loads: load k, lane l = slot 16 k + l / 4,
+							 * quarter l % 4 */
+							const uint64_t t = i0 + 64u * (uint32_t)(u + h);
+#pragma unroll
+							for (int k = 0; k < 4; k++)
+								raw[h][k] = t + 16u * k + (lane >> 2) < a.n
+										    ? ld_x4<NTL>(fd + t * 64u + 1024u * k + 16u * lane)
+										    : make_uint4(0, 0, 0, 0);
+#else
 							const bool okh = iu(u + h) < a.n;
-							const uint64_t ih = okh ? iu(u + h) : i0 + lane;
+							const uint64_t ih = okh ? iu(u + h) : i0;
 #pragma unroll
 							for (int k = 0; k < 4; k++)
 								raw[h][k] = okh ? ld_x4<NTL>(fd + ih * 64u + 16u * k) : make_uint4(0, 0, 0, 0);
+#endif
 						}
 					}
 					fwin W;
+#if CGPU_FF_STAGE
+					/* each lane's slot through the wave's LDS rows (64 slots of
+					 * 80 B: conflict-free 16-B reads) */
+#pragma unroll
+					for (int k = 0; k < 4; k++)
+						stg[(16u * k + (lane >> 2)) * 5u + (lane & 3u)] = raw[u % FF_H][k];
+					__builtin_amdgcn_wave_barrier();
+#pragma unroll
+					for (int q = 0; q < 4; q++) {
+						const uint4 v = stg[lane * 5u + q];
+						W.w[4 * q] = v.x;
+						W.w[4 * q + 1] = v.y;
+						W.w[4 * q + 2] = v.z;
+						W.w[4 * q + 3] = v.w;
+					}
+					__builtin_amdgcn_wave_barrier();
+#else
 #pragma unroll
 					for (int k = 0; k < 4; k++) {
 						W.w[4 * k] = raw[u % FF_H][k].x;
@@ -1748,6 +1786,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 						W.w[4 * k + 2] = raw[u % FF_H][k].z;
 						W.w[4 * k + 3] = raw[u % FF_H][k].w;
 					}
+#endif
 					const bool egress = flv[u] & 1u;
 					const ftuple t = parse_frame_w(s, W, fd + i * 64u, len[u], min(len[u], 64u), egress, ep[u], lxl);
 					const bool v6 = t.status == 0 && t.fam != 4u;
@@ -3237,7 +3276,9 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 	size_t fixed = V6 ? (IPCE ? 0u : (size_t)v6t_lds_words(s0.ipc6) * 4u) : (size_t)s0.ipc4c.n_dict * 4u;
 	fixed = (fixed + 7u) & ~(size_t)7u;
 	/* fused frames: the endpoint rows (+ alignment) and 4 statuses per lane */
-	const size_t ff = FF ? 16u + 2u * FR_LXC_LDS * 16u + (size_t)NT * 4u * 2u : 0u;
+	const size_t ff = FF ? 16u + 2u * FR_LXC_LDS * 16u + (size_t)NT * 4u * 2u +
+				       (CGPU_FF_STAGE ? (size_t)(NT / 64) * FF_STG_U4 * 16u : 0u)
+			     : 0u;
 	fixed += ff;
 	const cgpu_snapshot s = with_lds_hot(s0, fixed < X4_LDS_BUDGET ? (X4_LDS_BUDGET - fixed) / 8u : 0u);
 	size_t lds = (size_t)s.hot_slots * 8u + fixed;
@@ -3627,13 +3668,13 @@ hipError_t launch_classify_frames_x4(const cgpu_snapshot &s, const frames_args &
 	if (e != hipSuccess)
 		return e;
 	if (a.stride == 64u && s.n_lxc <= FR_LXC_LDS && !((uintptr_t)a.data & 15u) &&
-	    (s.schedule & CGPU_SCHED_FRAMES_FUSED)) {
+	    !(s.schedule & CGPU_SCHED_FRAMES_SPLIT)) {
 		/* fused: the classify kernel parses the slots itself (no tuple
-		 * columns written and re-read), the IPv6 frames as below.  Not the
-		 * default: each lane's 16-byte slot loads touch 4x the cache lines
-		 * of k_frames_cols' coalesced tile loads and the kernel spills at
-		 * 128 VGPRs, 2.98 against 2.74 ms per 64M frames
-		 * (profiles/r4_f/) */
+		 * columns written and re-read), the IPv6 frames as below.  Each
+		 * wave reads its 64-slot tile as four coalesced 1-KiB loads and
+		 * hands the slots out through LDS (CGPU_FF_STAGE): 2.64 against
+		 * 2.81 ms per 64M frames for the two passes, 2.96 with per-lane
+		 * slot loads (profiles/r5_j/) */
 		cls_args f4{a.data, nullptr, nullptr, nullptr, a.flags, a.len, a.ep, a.verdict, a.identity, a.stage,
 			    a.delta, a.n, a.pk, 0, nullptr, nullptr};
 		if ((e = launch_x4<false, false, 2>(s, f4, st, c)) != hipSuccess)

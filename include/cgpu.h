@@ -173,7 +173,7 @@ typedef struct cgpu_config {
 #define CGPU_SCHED_PER_LANE 1u   /* classify: one tuple per lane (k_classify) instead of x4 */
 #define CGPU_SCHED_GLOBAL_CTR 2u /* classify: per-lane kernel, one global atomic per hit */
 #define CGPU_SCHED_NO_CCACHE 4u  /* x4 classify without the LDS cold-slot cache */
-#define CGPU_SCHED_FRAMES_FUSED 8u /* classify_frames, 64-byte slots: the classify kernel parses the slots itself */
+#define CGPU_SCHED_FRAMES_SPLIT 8u /* classify_frames, 64-byte slots: a header pass writes tuple columns, then the classify pass (default: one fused kernel) */
 /* bits 4-5: v6 prefilter LDS staging mode + 1 (0 = the deepest that fits) */
 #define CGPU_SCHED_PF6_LDS(mode) ((((uint32_t)(mode)) + 1u) << 4)
 /* bits 8-13: conntrack group-key radix sort bits (8..32; 0 = 24) */

@@ -82,16 +82,17 @@ def _classify_frames(torch, e, f):
             out["stage"].cpu().numpy())
 
 
-SCHED_FRAMES_FUSED = 8  # CGPU_SCHED_FRAMES_FUSED: the classify kernel parses the slots
+SCHED_FRAMES_SPLIT = 8  # CGPU_SCHED_FRAMES_SPLIT: header pass + classify pass instead of the fused kernel
 
 
 @pytest.mark.parametrize("gate,verify", [(1, 7), (0, 7), (1, 0)])
-@pytest.mark.parametrize("stride,sched", [(128, 0), (64, 0), (64, SCHED_FRAMES_FUSED)])
+@pytest.mark.parametrize("stride,sched", [(128, 0), (64, 0), (64, SCHED_FRAMES_SPLIT)])
 def test_classify_frames_vs_restatement(torch_cuda, gate, verify, stride, sched):
     """Mixed v4 / v6 frames through the whole decision: verdicts, identities,
     stages, per-entry counters and metrics equal the restatement's: the
-    parse pass + classify pass, and with 64-byte slots the fused kernel (the
-    classify kernel parses the slots itself) the schedule can select."""
+    parse pass + classify pass (128-byte slots, or the split schedule), and
+    with 64-byte slots the default fused kernel (the classify kernel parses
+    the slots itself, staged through LDS)."""
     T = synth.make_tables(n_prefixes=5000, n_identities=300, n_endpoints=5, keys_per_ep=3000)
     rng = np.random.Generator(np.random.PCG64(0xC1A55 + gate + verify))
     pool = T.pfx_addr.astype(np.uint32).byteswap()
@@ -119,7 +120,7 @@ def test_classify_frames_vs_restatement(torch_cuda, gate, verify, stride, sched)
     e.close()
 
 
-@pytest.mark.parametrize("stride,sched", [(128, 0), (64, 0), (64, SCHED_FRAMES_FUSED)])
+@pytest.mark.parametrize("stride,sched", [(128, 0), (64, 0), (64, SCHED_FRAMES_SPLIT)])
 @pytest.mark.parametrize("kind", ["runt", "v6", "not_classified"])
 @pytest.mark.parametrize("tail", [1, 2, 3, 63, 65])
 def test_classify_frames_ragged_tail(torch_cuda, tail, kind, stride, sched):

@@ -56,7 +56,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "walk_grid1024": ("CT_WALK_GRID=1024",), "walk_grid2048": ("CT_WALK_GRID=2048",), "walk_grid4096": ("CT_WALK_GRID=4096",),
             "walk_grid8192": ("CT_WALK_GRID=8192",), "retb32": ("CT_RETB=32",),
             "g4096_retb32": ("CT_WALK_GRID=4096", "CT_RETB=32"), "g8192_retb32": ("CT_WALK_GRID=8192", "CT_RETB=32"),
-            "walk_grid16384": ("CT_WALK_GRID=16384",), "walk_grid32768": ("CT_WALK_GRID=32768",)}
+            "walk_grid16384": ("CT_WALK_GRID=16384",), "walk_grid32768": ("CT_WALK_GRID=32768",),
+            "ff_nostage": ("CGPU_FF_STAGE=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
 
 
 def build(names):
@@ -184,6 +185,21 @@ def _workload(conf):
             e.ct4_flush()
             e.classify_v4_ctlb(d, 1000, out=out)
         return make, step, n
+    if conf == "frames":
+        # bench.py --config frames: config-2 tuples as 64-byte frame slots;
+        # CGPU_AB_SCHED = cgpu_config.schedule (8: the fused kernel)
+        T = synth.make_tables(**synth.CONFIGS["gpu"])
+        n = synth.CONFIGS["gpu"]["n_tuples"]
+        d = synth.frames_to_device(synth.frames_from_tuples(synth.make_tuples(T, n), stride=64), "cuda")
+        out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+               "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
+        sched = int(os.environ.get("CGPU_AB_SCHED", "0"))
+
+        def make():
+            e = Engine(device=0, **T.engine_config(), schedule=sched)
+            synth.load_engine(e, T)
+            return e
+        return make, lambda e: e.classify_frames(d, out=out), n
     v6 = conf == "v6"
     T = (synth.make_tables6 if v6 else synth.make_tables)(**synth.CONFIGS[conf])
     n = synth.CONFIGS[conf]["n_tuples"]
