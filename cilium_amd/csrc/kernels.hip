@@ -6140,22 +6140,23 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 				const ct_pkt q = r.pkt();
 				if constexpr (MODE == WALK_OWED) {
 					const uint32_t kind = K::ADDR ? (v & 3u) : (v & 1u) << 1;
-					const typename K::key fk = K::reversed(r.key());
-					if (kind == 1u) {
-						/* the owed address entry of packet i's create */
-						if constexpr (K::ADDR) {
-							if (a.ct_ret[i] & CT_ADDRP)
-								ctc_update_owed<K>(T, A, c, ct_addr_key(fk, q),
-										   ct_new_row<K>(q, false, a.now));
-						}
-						continue;
-					}
-					if (kind == 2u) {
-						/* the owed ICMP entry of packet i's create */
-						if (a.ct_ret[i] & CT_RELP) {
-							ct_row e = ct_new_row<K>(q, !(q.meta & CTM_EGRESS), a.now);
-							e.c.y |= CTB_SEEN_NON_SYN;
-							ctc_update_owed<K>(T, A, c, K::related(fk), e);
+					if (kind != 0u) {
+						/* an owed entry of packet i's create: kind 1 its
+						 * address entry, kind 2 its ICMP entry.  One update
+						 * call site for both (each inlined copy of the map
+						 * update costs the walker registers) */
+						const typename K::key fk = K::reversed(r.key());
+						const bool addr = K::ADDR && kind == 1u;
+						if (a.ct_ret[i] & (addr ? CT_ADDRP : CT_RELP)) {
+							ct_row e = ct_new_row<K>(q, !addr && !(q.meta & CTM_EGRESS), a.now);
+							if (!addr)
+								e.c.y |= CTB_SEEN_NON_SYN;
+							typename K::key k = K::related(fk);
+							if constexpr (K::ADDR) {
+								if (addr)
+									k = ct_addr_key(fk, q);
+							}
+							ctc_update_owed<K>(T, A, c, k, e);
 						}
 						continue;
 					}
