@@ -5241,6 +5241,9 @@ __global__ __launch_bounds__(256) void k_ct_prep6(cgpu_snapshot s, ct_args a)
 #ifndef CTC
 #define CTC 4 /* 3 ways measured 14 % slower (more re-probes) */
 #endif
+#ifndef CGPU_CT_CREATE_LOOP
+#define CGPU_CT_CREATE_LOOP 1 /* the service step's creates through one update call site */
+#endif
 #define CTC_VALID 0x10000u
 #define CTC_NEG 0x20000u
 #define CTC_DIRTY 0x40000u
@@ -5664,34 +5667,76 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 		return ret;
 	/* ct_create: the forward entry, the address entry (service step only),
 	 * then the ICMP entry relating errors */
-	ct_row e = ct_new_row<K>(q, ingress, now);
+	const ct_row e = ct_new_row<K>(q, ingress, now);
+	uint32_t owed = 0;
+	if (K::ADDR && CGPU_CT_CREATE_LOOP) {
+	/* the service step's creates in order, t = 0 the forward entry, 1 the
+	 * address entry, 2 the ICMP entry, through ONE map-update call site:
+	 * three inlined copies took the CtK4S walker to 256 VGPRs with spills,
+	 * one 186 (the plain walkers keep the straight line, which fits their
+	 * occupancy budget) */
+#pragma unroll 1
+	for (int t = 0; t < 3; t++) {
+		typename K::key kt = k;
+		ct_row et = e;
+		if (t == 1) {
+			if constexpr (!K::ADDR) {
+				continue;
+			} else {
+				const uint32_t am = q.lbf >> 1;
+				if (am == AM_INLINE) {
+					kt = ct_addr_key(k, q);
+				} else {
+					/* AM_DEFER: the entry lies in another address pair's
+					 * group: reserve its capacity now (the reference's
+					 * update fails here when the map is full), write it
+					 * in phase 2 */
+					if (am == AM_DEFER) {
+						if (!ct_take(T, A))
+							return CT_NEW | CT_FAIL;
+						owed = CT_ADDRP;
+					}
+					continue;
+				}
+			}
+		} else if (t == 2) {
+			et.c.y |= CTB_SEEN_NON_SYN;
+			if (meta & CTM_RELX) {
+				/* the ICMP entry lies in the address pair's phase-2 group:
+				 * reserve its capacity now (where the reference's update
+				 * would fail), write it in phase 2 in batch order */
+				if (!ct_take(T, A))
+					return CT_NEW | CT_FAIL | owed;
+				return CT_NEW | CT_RELP | owed;
+			}
+			kt = K::related(k);
+		}
+		if (!ctc_update<K>(T, A, c, kt, et))
+			return CT_NEW | CT_FAIL | owed;
+	}
+	return CT_NEW | owed;
+	}
 	if (!ctc_update<K>(T, A, c, k, e))
 		return CT_NEW | CT_FAIL;
-	uint32_t owed = 0;
 	if constexpr (K::ADDR) {
 		const uint32_t am = q.lbf >> 1;
 		if (am == AM_INLINE) {
 			if (!ctc_update<K>(T, A, c, ct_addr_key(k, q), e))
 				return CT_NEW | CT_FAIL;
 		} else if (am == AM_DEFER) {
-			/* the entry lies in another address pair's group: reserve its
-			 * capacity now (the reference's update fails here when the map
-			 * is full), write it in phase 2 */
 			if (!ct_take(T, A))
 				return CT_NEW | CT_FAIL;
 			owed = CT_ADDRP;
 		}
 	}
-	e.c.y |= CTB_SEEN_NON_SYN;
+	ct_row e2 = e;
+	e2.c.y |= CTB_SEEN_NON_SYN;
 	if (meta & CTM_RELX) {
-		/* the ICMP entry lies in the address pair's phase-2 group: reserve
-		 * its capacity now (where the reference's update would fail), write
-		 * it in phase 2 in batch order */
 		if (!ct_take(T, A))
 			return CT_NEW | CT_FAIL | owed;
 		return CT_NEW | CT_RELP | owed;
 	}
-	if (!ctc_update<K>(T, A, c, K::related(k), e))
+	if (!ctc_update<K>(T, A, c, K::related(k), e2))
 		return CT_NEW | CT_FAIL | owed;
 	return CT_NEW | owed;
 }
@@ -6011,11 +6056,12 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
  * service path: candidates c = packet << 1 | kind, kind 0 a packet whose
  * address pair may hold owed entries, kind 1 an owed address entry */
-/* workgroups per CU the service-path walker (CtK4S: ~280 registers) is
- * compiled for: 2 spills a few registers to scratch and doubles its
- * occupancy (profiles/r4_f/ab_ctlb_walker_occupancy.log) */
+/* workgroups per CU the service-path walker (CtK4S) is compiled for: its
+ * creates through one update call site need 186 VGPRs (2 waves per SIMD);
+ * 3 caps it at 168 with ~10 spilled: ctlb 20.83 -> 20.64 ms
+ * (profiles/r5_k/ab_ctlb_minb.log; round 4: 1 -> 2, r4_f) */
 #ifndef CGPU_WALK_MINB_SVC
-#define CGPU_WALK_MINB_SVC 2
+#define CGPU_WALK_MINB_SVC 3
 #endif
 /* ... and the other walkers (1: the compiler's choice, A/B) */
 #ifndef CGPU_WALK_W

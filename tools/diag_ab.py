@@ -57,7 +57,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "walk_grid8192": ("CT_WALK_GRID=8192",), "retb32": ("CT_RETB=32",),
             "g4096_retb32": ("CT_WALK_GRID=4096", "CT_RETB=32"), "g8192_retb32": ("CT_WALK_GRID=8192", "CT_RETB=32"),
             "walk_grid16384": ("CT_WALK_GRID=16384",), "walk_grid32768": ("CT_WALK_GRID=32768",),
-            "ff_nostage": ("CGPU_FF_STAGE=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
+            "ff_nostage": ("CGPU_FF_STAGE=0",), "walk_svc_minb3": ("CGPU_WALK_MINB_SVC=3",),
+            "ct_create_noloop": ("CGPU_CT_CREATE_LOOP=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
 
 
 def build(names):
