@@ -3192,10 +3192,19 @@ static cgpu_snapshot with_lds_hot(const cgpu_snapshot &s, size_t max_hot)
 #ifndef CGPU_IPC6_MINW
 #define CGPU_IPC6_MINW 1 /* workgroups per CU the register budget aims at */
 #endif
+/* svc_out[i].x: SVC_* | LBS_* << 8 | slave << 16; .y target; .z the dport
+ * rewrite (0 none) | rev_nat_index << 16 */
+#define SVC_NONE 0u
+#define SVC_XLATED 1u
+#define SVC_DROP 2u
+
 template <int Q, int NT>
 __global__ __launch_bounds__(NT, CGPU_IPC6_MINW) void k_ipc6_pre(cgpu_snapshot s, const uint4 *sa, const uint4 *da,
-						 const uint8_t *flags, uint32_t *e_out, uint64_t n)
+						 const uint8_t *flags, uint32_t *e_out, uint64_t n,
+						 const uint4 *svc)
 {
+	/* svc (the IPv6 service path, or NULL): an egress packet lb6_local
+	 * translated is looked up on its target (svc[2i + 1]) */
 	extern __shared__ __attribute__((aligned(16))) uint32_t lt[];
 	const uint32_t n24 = v6t_lds_b24(s.ipc6);
 	const uint32_t nbl = v6t_lds_bloom(s.ipc6);
@@ -3220,8 +3229,13 @@ __global__ __launch_bounds__(NT, CGPU_IPC6_MINW) void k_ipc6_pre(cgpu_snapshot s
 			const uint64_t i = g + (uint64_t)u * T;
 			act[u] = i < n;
 			w[u] = make_uint4(0, 0, 0, 0);
-			if (act[u])
-				w[u] = v6_host_words(ld_x4<true>(((flags[i] & 1u) ? da : sa) + i));
+			if (act[u]) {
+				const bool eg = flags[i] & 1u;
+				uint4 x = ld_x4<true>((eg ? da : sa) + i);
+				if (svc && eg && (svc[2u * i].x & 3u) == SVC_XLATED)
+					x = svc[2u * i + 1u];
+				w[u] = v6_host_words(x);
+			}
 		}
 		v6t_lookup_q<Q>(s.ipc6, lt, n24 != 0u, w, act, e, nbl ? lbl : nullptr);
 #pragma unroll
@@ -3256,7 +3270,7 @@ static hipError_t launch_ipc6_pre(const cgpu_snapshot &s, const cls_args &a, hip
 	const unsigned res = resident_blocks((const void *)k_ipc6_pre<Q, NT>, NT, lds);
 	const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.n + Q * NT - 1) / (Q * NT), res));
 	hipLaunchKernelGGL((k_ipc6_pre<Q, NT>), dim3(g), dim3(NT), lds, st, s, static_cast<const uint4 *>(a.saddr),
-			   static_cast<const uint4 *>(a.daddr), a.flags, a.ipc_e, a.n);
+			   static_cast<const uint4 *>(a.daddr), a.flags, a.ipc_e, a.n, nullptr);
 	return hipGetLastError();
 }
 
@@ -3932,6 +3946,11 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #ifndef CGPU_CT_SVC_DECQ
 #define CGPU_CT_SVC_DECQ 0
 #endif
+/* the service path's prep: Q packets per lane (k_ct_prep_svc_q), 1 = the
+ * per-lane k_ct_prep */
+#ifndef CGPU_CT_SVC_Q
+#define CGPU_CT_SVC_Q 2
+#endif
 /* ... IPv6 (k_ct_prep6's per-lane decide<1> walks the trie from global
  * memory: 32 GB of HBM traffic per 64M packets, profiles/r4_prof/ctlb6):
  * 1 = k_ct_decq on a resident grid of 1024-thread workgroups, the trie
@@ -3939,6 +3958,11 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
  * 24.10 -> 24.75 ms (profiles/r4_s/): off */
 #ifndef CGPU_CT_SVC_DECQ6
 #define CGPU_CT_SVC_DECQ6 0
+#endif
+/* ... IPv6: 1 = the trie pre-pass on the translated addresses, then
+ * k_ct_prep6_q<SVC> (as the plain IPv6 path) */
+#ifndef CGPU_CT_SVC_PRE6
+#define CGPU_CT_SVC_PRE6 1
 #endif
 /* the stateful service step (cgpu_classify_v4_ctlb) */
 #define CTM_PHASE2 128u   /* the packet's address pair may hold owed address entries: phase 2 */
@@ -3955,11 +3979,6 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define AM_NONE 0u
 #define AM_INLINE 1u /* same address pair: written by the create itself */
 #define AM_DEFER 2u  /* other pair: capacity reserved, written in phase 2 */
-/* svc_out[i].x: SVC_* | LBS_* << 8 | slave << 16; .y target; .z the dport
- * rewrite (0 none) | rev_nat_index << 16 */
-#define SVC_NONE 0u
-#define SVC_XLATED 1u
-#define SVC_DROP 2u
 #define LBS_ENTRY 1u /* lb_loopback came from the conntrack entry */
 #define LBS_SNAT 2u  /* saddr == target: loopback source NAT (lb.h:753-767) */
 
@@ -4522,176 +4541,251 @@ __device__ __forceinline__ void ct_flag(uint32_t *w)
  * store; a packet whose address entry lies in another address pair owes it
  * to phase 2 (CTM_ADDRX), and a packet whose own pair can receive such
  * entries runs in phase 2 (CTM_PHASE2).  SERIAL: one group for the batch. */
+/* one packet of k_ct_prep before and after its forward decision (the
+ * per-lane kernel and the Q-interleaved service prep share them) */
+struct prep4 {
+	uint32_t fl, pr, len, sa, ep, w, da, dp, tfl, z, meta, r2x, addr, saddr2, lbf;
+	bool egress, frag, dec; /* dec: the packet takes the forward decision */
+};
+
+template <bool SVC, bool SERIAL>
+__device__ __forceinline__ bool prep4_pre(const cgpu_snapshot &s, const ct_args &a, uint64_t i, prep4 &p)
+{
+	constexpr uint32_t RW = SVC ? 3u : 2u;
+	p.fl = a.flags[i];
+	p.pr = a.proto[i];
+	p.len = a.len[i];
+	p.sa = a.saddr[i];
+	p.ep = a.ep[i];
+	p.w = a.l4[i];
+	p.da = a.daddr[i];
+	p.dp = a.dport[i];
+	p.egress = p.fl & 1u;
+	p.tfl = p.egress ? TUPLE_F_IN : 0u;
+	p.z = 0;
+	p.meta = p.egress ? CTM_EGRESS : 0u;
+	p.r2x = p.addr = p.saddr2 = p.lbf = 0;
+	const uint32_t &fl = p.fl, &pr = p.pr, &len = p.len, &sa = p.sa;
+	uint32_t &w = p.w, &da = p.da, &dp = p.dp, &tfl = p.tfl, &z = p.z, &meta = p.meta, &r2x = p.r2x,
+		 &addr = p.addr, &saddr2 = p.saddr2, &lbf = p.lbf;
+	const bool egress = p.egress;
+	uint32_t xd = da;
+	if constexpr (SVC) {
+		const uint4 so = egress ? a.svc_out[i] : make_uint4(SVC_NONE, 0, 0, 0);
+		if ((so.x & 3u) == SVC_DROP) {
+			a.identity[i] = 0;
+			if (a.xdaddr)
+				a.xdaddr[i] = da;
+			if (a.xdport)
+				a.xdport[i] = (uint16_t)dp;
+			uint4 *r = a.rec + RW * i;
+			r[0] = uint4{da, sa, 0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16)};
+			r[1] = uint4{0u, len, 0u, 0u};
+			r[2] = uint4{0u, 0u, 0u, 0u};
+			a.gkey[i] = SERIAL ? 0u : ct_fmix((uint32_t)i ^ 0x5bd1e995u);
+			a.idx[i] = (uint32_t)i;
+			if constexpr (!SERIAL)
+				a.pcls[i] = 0u; /* dropped: no phase-2 class (the scratch is reused) */
+			return false;
+		}
+		if ((so.x & 3u) == SVC_XLATED) {
+			const uint32_t lbs = (so.x >> 8) & 3u, tg = so.y;
+			const bool lb = lbs != 0;
+			xd = tg;
+			if (!lb)
+				da = tg; /* tuple->daddr = svc->target */
+			if (so.z & 0xFFFFu)
+				dp = so.z & 0xFFFFu; /* lb4_xlate's port rewrite */
+			addr = (lbs & LBS_SNAT) ? s.ipv4_loopback : tg;
+			saddr2 = (lbs & LBS_SNAT) ? sa : 0u;
+			/* the address entry's pair {addr, loopback ? svc_addr : daddr}
+			 * against the packet's own {saddr, daddr} */
+			const uint32_t b = lb ? saddr2 : da;
+			const bool same = (addr == sa && b == da) || (addr == da && b == sa);
+			/* ct_create4 writes no address entry for addr 0 (a slave-0
+			 * master row carries target 0), conntrack.h:697 */
+			const uint32_t am = !addr ? AM_NONE : (same || SERIAL) ? AM_INLINE : AM_DEFER;
+			lbf = (lb ? LBF_LOOPBACK : 0u) | (am << 1);
+			r2x = (so.z >> 16) | (so.x & 0xFFFF0000u);
+		}
+		if (a.xdaddr)
+			a.xdaddr[i] = xd;
+		if (a.xdport)
+			a.xdport[i] = (uint16_t)dp;
+	}
+	if (pr == 1u) {
+		const uint32_t type = w & 0xFFu;
+		if (type == 3u || type == 11u || type == 12u) /* DEST_UNREACH, TIME_EXCEEDED, PARAMETERPROB */
+			tfl |= TUPLE_F_RELATED;
+		else if (type == 0u) /* ECHOREPLY: tuple->dport = ICMP_ECHO */
+			z = 8u;
+		else {
+			if (type == 8u) /* ECHO: tuple->sport = type */
+				z = 8u << 16;
+			meta |= CTM_ACT_CREATE;
+		}
+	} else if (pr == 6u || pr == 17u) {
+		/* skb_load_bytes(off, &tuple->dport, 4): dport <- sport, sport <- dport */
+		z = (uint32_t)a.sport[i] | (dp << 16);
+		if (pr == 6u) {
+			meta |= CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE);
+		} else {
+			meta |= CTM_ACT_CREATE;
+		}
+	} else {
+		meta |= CTM_GATED;
+	}
+	if (pr != 6u)
+		w = 0; /* union tcp_flags stays zero (conntrack.h:448) */
+	p.frag = !egress && ((fl >> 1) & 1u);
+	p.dec = !(meta & CTM_GATED);
+	return true;
+}
+
+template <bool SVC, bool SERIAL>
+__device__ __forceinline__ void prep4_post(const cgpu_snapshot &s, const ct_args &a, uint64_t i, const prep4 &p,
+					   const decision &d, bool conn)
+{
+	constexpr uint32_t RW = SVC ? 3u : 2u;
+	const uint32_t &pr = p.pr, &len = p.len, &sa = p.sa, &ep = p.ep, &w = p.w, &da = p.da, &tfl = p.tfl, &z = p.z,
+		       &r2x = p.r2x, &addr = p.addr, &saddr2 = p.saddr2, &lbf = p.lbf;
+	uint32_t meta = p.meta;
+	const bool egress = p.egress;
+	uint32_t sec = 0, port = 0, cst = 0, id = 0;
+	if (p.dec) {
+		/* the forward tuple's decision (what CT_NEW / CT_ESTABLISHED packets
+		 * see); k_ct_finish bumps its counter */
+		if (p.frag)
+			meta |= CTM_FRAG;
+		if (egress)
+			sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
+		if constexpr (!SVC || !CGPU_CT_SVC_DECQ) {
+			if (d.v >= 0) {
+				meta |= CTM_ALLOWED;
+				port = (uint32_t)d.v;
+			}
+			id = d.id;
+			if (!egress)
+				sec = d.id;
+			cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
+		} /* SVC: k_ct_decq, Q packets per lane */
+	}
+	uint32_t g = ct_group(sa, da);
+	if constexpr (!SVC) {
+		/* phase 1 by connection (TCP / UDP ports, ICMP echo ids): only
+		 * the ICMP entries of creates (owed) and the ICMP errors that
+		 * read them (phase 2) share an address pair's keys across
+		 * connections */
+		bool p2 = false;
+		if (!(meta & CTM_GATED)) {
+			if (pr == 1u && (tfl & TUPLE_F_RELATED)) {
+				meta |= CTM_PHASE2;
+				p2 = true;
+			} else {
+				meta |= CTM_RELX;
+				g = ct_conn_group(g, z, pr);
+			}
+		}
+		/* phase-2 candidates 2i (the packet) and 2i + 1 (its owed ICMP
+		 * entry, set by the walker) */
+		reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
+	}
+	if constexpr (SVC) {
+		if (!SERIAL && !(meta & CTM_GATED)) {
+			/* pairs an address entry can land in: {T, T}, {IPV4_LOOPBACK,
+			 * x}, {target, 0} (ct_create4's addr / svc_addr rewrites) */
+			const uint32_t lo = s.ipv4_loopback;
+			/* ... and, grouping by connection (conn), ICMP errors, which
+			 * read the ICMP entries the creates of every connection of
+			 * their pair owe */
+			const bool special = sa == da || !sa || !da || sa == lo || da == lo;
+			const bool p2 = special || (conn && pr == 1u && (tfl & TUPLE_F_RELATED));
+			if ((lbf >> 1) == AM_DEFER) {
+				meta |= CTM_ADDRX;
+				ct_flag(&a.ctl[2]);
+				if (special)
+					ct_flag(&a.ctl[0]); /* owes into phase 2b from phase 2b */
+			}
+			if (p2) {
+				meta |= CTM_PHASE2;
+				ct_flag(&a.ctl[1]);
+				g = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
+			} else if (conn) {
+				/* phase 1 by connection (an address entry of the same
+				 * pair is the forward key itself: tuple.daddr is the
+				 * target already), the ICMP entry owed */
+				meta |= CTM_RELX;
+				ct_flag(&a.ctl[2]);
+				g = ct_conn_group(g, z, pr);
+			}
+		}
+	}
+	a.identity[i] = id;
+	uint4 *r = a.rec + RW * i;
+	r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
+	r[1] = uint4{w | (port << 16), len, sec, cst};
+	if constexpr (SVC)
+		r[2] = uint4{r2x, addr, saddr2, lbf};
+	a.gkey[i] = SERIAL ? 0u : (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
+	a.idx[i] = (uint32_t)i;
+	if constexpr (SVC && !SERIAL) {
+		/* what k_ct_owed_flags selects by, in one byte instead of the
+		 * record's first line */
+		const bool live = !(meta & CTM_GATED);
+		const uint32_t lo = s.ipv4_loopback;
+		const bool special = sa == da || !sa || !da || sa == lo || da == lo;
+		const bool p2 = live && (meta & CTM_PHASE2);
+		a.pcls[i] = (uint8_t)((p2 && !special ? PCL_P2A : 0u) | (p2 && special ? PCL_P2B : 0u) |
+				      (live && (meta & CTM_ADDRX) ? PCL_ADDRX : 0u) |
+				      (live && (meta & CTM_RELX) ? PCL_RELX : 0u));
+	}
+}
+
 template <bool SVC, bool SERIAL>
 __global__ __launch_bounds__(256) void k_ct_prep(cgpu_snapshot s, ct_args a, bool conn = false)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * 256u;
-	constexpr uint32_t RW = SVC ? 3u : 2u;
 	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += stride) {
-		const uint32_t fl = a.flags[i], pr = a.proto[i], len = a.len[i];
-		const uint32_t sa = a.saddr[i], ep = a.ep[i];
-		uint32_t w = a.l4[i], da = a.daddr[i], dp = a.dport[i];
-		const bool egress = fl & 1u;
-		uint32_t tfl = egress ? TUPLE_F_IN : 0u, z = 0, meta = egress ? CTM_EGRESS : 0u;
-		uint32_t r2x = 0, addr = 0, saddr2 = 0, lbf = 0, xd = da;
-		if constexpr (SVC) {
-			const uint4 so = egress ? a.svc_out[i] : make_uint4(SVC_NONE, 0, 0, 0);
-			if ((so.x & 3u) == SVC_DROP) {
-				a.identity[i] = 0;
-				if (a.xdaddr)
-					a.xdaddr[i] = da;
-				if (a.xdport)
-					a.xdport[i] = (uint16_t)dp;
-				uint4 *r = a.rec + RW * i;
-				r[0] = uint4{da, sa, 0u, pr | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16)};
-				r[1] = uint4{0u, len, 0u, 0u};
-				r[2] = uint4{0u, 0u, 0u, 0u};
-				a.gkey[i] = SERIAL ? 0u : ct_fmix((uint32_t)i ^ 0x5bd1e995u);
-				a.idx[i] = (uint32_t)i;
-				if constexpr (!SERIAL)
-					a.pcls[i] = 0u; /* dropped: no phase-2 class (the scratch is reused) */
-				continue;
-			}
-			if ((so.x & 3u) == SVC_XLATED) {
-				const uint32_t lbs = (so.x >> 8) & 3u, tg = so.y;
-				const bool lb = lbs != 0;
-				xd = tg;
-				if (!lb)
-					da = tg; /* tuple->daddr = svc->target */
-				if (so.z & 0xFFFFu)
-					dp = so.z & 0xFFFFu; /* lb4_xlate's port rewrite */
-				addr = (lbs & LBS_SNAT) ? s.ipv4_loopback : tg;
-				saddr2 = (lbs & LBS_SNAT) ? sa : 0u;
-				/* the address entry's pair {addr, loopback ? svc_addr : daddr}
-				 * against the packet's own {saddr, daddr} */
-				const uint32_t b = lb ? saddr2 : da;
-				const bool same = (addr == sa && b == da) || (addr == da && b == sa);
-				/* ct_create4 writes no address entry for addr 0 (a slave-0
-				 * master row carries target 0), conntrack.h:697 */
-				const uint32_t am = !addr ? AM_NONE : (same || SERIAL) ? AM_INLINE : AM_DEFER;
-				lbf = (lb ? LBF_LOOPBACK : 0u) | (am << 1);
-				r2x = (so.z >> 16) | (so.x & 0xFFFF0000u);
-			}
-			if (a.xdaddr)
-				a.xdaddr[i] = xd;
-			if (a.xdport)
-				a.xdport[i] = (uint16_t)dp;
+		prep4 p;
+		if (!prep4_pre<SVC, SERIAL>(s, a, i, p))
+			continue;
+		decision d{};
+		if (p.dec && (!SVC || !CGPU_CT_SVC_DECQ))
+			d = decide<0>(s, p.egress, p.frag, p.sa, p.da, uint4{}, uint4{}, p.z >> 16, p.pr, p.ep);
+		prep4_post<SVC, SERIAL>(s, a, i, p, d, conn);
+	}
+}
+
+/* k_ct_prep<true, false> (the service path) with Q packets per lane: the
+ * forward decisions through decide4_q, every lookup stage's gathers of the
+ * lane's packets in flight together */
+template <int Q>
+__global__ __launch_bounds__(256) void k_ct_prep_svc_q(cgpu_snapshot s, ct_args a, bool conn)
+{
+	const uint64_t T = (uint64_t)gridDim.x * 256u;
+	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
+		prep4 p[Q];
+		bool act[Q], dec[Q], eg[Q], frag[Q];
+		uint32_t sa[Q], da[Q], fdp[Q], pr[Q], ep[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint64_t i = g + (uint64_t)u * T;
+			act[u] = i < a.n && prep4_pre<true, false>(s, a, i, p[u]);
+			dec[u] = act[u] && p[u].dec;
+			eg[u] = act[u] && p[u].egress;
+			frag[u] = act[u] && p[u].frag;
+			sa[u] = act[u] ? p[u].sa : 0u;
+			da[u] = act[u] ? p[u].da : 0u;
+			fdp[u] = act[u] ? p[u].z >> 16 : 0u;
+			pr[u] = act[u] ? p[u].pr : 0u;
+			ep[u] = act[u] ? p[u].ep : 0u;
 		}
-		if (pr == 1u) {
-			const uint32_t type = w & 0xFFu;
-			if (type == 3u || type == 11u || type == 12u) /* DEST_UNREACH, TIME_EXCEEDED, PARAMETERPROB */
-				tfl |= TUPLE_F_RELATED;
-			else if (type == 0u) /* ECHOREPLY: tuple->dport = ICMP_ECHO */
-				z = 8u;
-			else {
-				if (type == 8u) /* ECHO: tuple->sport = type */
-					z = 8u << 16;
-				meta |= CTM_ACT_CREATE;
-			}
-		} else if (pr == 6u || pr == 17u) {
-			/* skb_load_bytes(off, &tuple->dport, 4): dport <- sport, sport <- dport */
-			z = (uint32_t)a.sport[i] | (dp << 16);
-			if (pr == 6u) {
-				meta |= CTM_TCP | ((w & 1u) ? CTM_ACT_CLOSE : CTM_ACT_CREATE);
-			} else {
-				meta |= CTM_ACT_CREATE;
-			}
-		} else {
-			meta |= CTM_GATED;
-		}
-		if (pr != 6u)
-			w = 0; /* union tcp_flags stays zero (conntrack.h:448) */
-		uint32_t sec = 0, port = 0, cst = 0, id = 0;
-		if (!(meta & CTM_GATED)) {
-			/* the forward tuple's decision (what CT_NEW / CT_ESTABLISHED
-			 * packets see); k_ct_finish bumps its counter */
-			const bool frag = !egress && ((fl >> 1) & 1u);
-			if (frag)
-				meta |= CTM_FRAG;
-			if (egress)
-				sec = ep < s.n_lxc ? s.lxc[2u * ep + 1u].w : 0u; /* SECLABEL */
-			if constexpr (!SVC || !CGPU_CT_SVC_DECQ) {
-				const decision d = decide<0>(s, egress, frag, sa, da, uint4{}, uint4{}, z >> 16,
-							    pr, ep);
-				if (d.v >= 0) {
-					meta |= CTM_ALLOWED;
-					port = (uint32_t)d.v;
-				}
-				id = d.id;
-				if (!egress)
-					sec = d.id;
-				cst = (uint32_t)(d.ctr + 1) | (d.st << 24);
-			} /* SVC: k_ct_decq, Q packets per lane */
-		}
-		uint32_t g = ct_group(sa, da);
-		if constexpr (!SVC) {
-			/* phase 1 by connection (TCP / UDP ports, ICMP echo ids): only
-			 * the ICMP entries of creates (owed) and the ICMP errors that
-			 * read them (phase 2) share an address pair's keys across
-			 * connections */
-			bool p2 = false;
-			if (!(meta & CTM_GATED)) {
-				if (pr == 1u && (tfl & TUPLE_F_RELATED)) {
-					meta |= CTM_PHASE2;
-					p2 = true;
-				} else {
-					meta |= CTM_RELX;
-					g = ct_conn_group(g, z, pr);
-				}
-			}
-			/* phase-2 candidates 2i (the packet) and 2i + 1 (its owed ICMP
-			 * entry, set by the walker) */
-			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
-		}
-		if constexpr (SVC) {
-			if (!SERIAL && !(meta & CTM_GATED)) {
-				/* pairs an address entry can land in: {T, T}, {IPV4_LOOPBACK,
-				 * x}, {target, 0} (ct_create4's addr / svc_addr rewrites) */
-				const uint32_t lo = s.ipv4_loopback;
-				/* ... and, grouping by connection (conn), ICMP errors, which
-				 * read the ICMP entries the creates of every connection of
-				 * their pair owe */
-				const bool special = sa == da || !sa || !da || sa == lo || da == lo;
-				const bool p2 = special || (conn && pr == 1u && (tfl & TUPLE_F_RELATED));
-				if ((lbf >> 1) == AM_DEFER) {
-					meta |= CTM_ADDRX;
-					ct_flag(&a.ctl[2]);
-					if (special)
-						ct_flag(&a.ctl[0]); /* owes into phase 2b from phase 2b */
-				}
-				if (p2) {
-					meta |= CTM_PHASE2;
-					ct_flag(&a.ctl[1]);
-					g = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
-				} else if (conn) {
-					/* phase 1 by connection (an address entry of the same
-					 * pair is the forward key itself: tuple.daddr is the
-					 * target already), the ICMP entry owed */
-					meta |= CTM_RELX;
-					ct_flag(&a.ctl[2]);
-					g = ct_conn_group(g, z, pr);
-				}
-			}
-		}
-		a.identity[i] = id;
-		uint4 *r = a.rec + RW * i;
-		r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
-		r[1] = uint4{w | (port << 16), len, sec, cst};
-		if constexpr (SVC)
-			r[2] = uint4{r2x, addr, saddr2, lbf};
-		a.gkey[i] = SERIAL ? 0u : (meta & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : g;
-		a.idx[i] = (uint32_t)i;
-		if constexpr (SVC && !SERIAL) {
-			/* what k_ct_owed_flags selects by, in one byte instead of the
-			 * record's first line */
-			const bool live = !(meta & CTM_GATED);
-			const uint32_t lo = s.ipv4_loopback;
-			const bool special = sa == da || !sa || !da || sa == lo || da == lo;
-			const bool p2 = live && (meta & CTM_PHASE2);
-			a.pcls[i] = (uint8_t)((p2 && !special ? PCL_P2A : 0u) | (p2 && special ? PCL_P2B : 0u) |
-					      (live && (meta & CTM_ADDRX) ? PCL_ADDRX : 0u) |
-					      (live && (meta & CTM_RELX) ? PCL_RELX : 0u));
-		}
+		decision d[Q];
+		decide4_q<Q>(s, dec, eg, frag, sa, da, fdp, pr, ep, d);
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			if (act[u])
+				prep4_post<true, false>(s, a, g + (uint64_t)u * T, p[u], d[u], conn);
 	}
 }
 
@@ -4792,7 +4886,7 @@ __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 /* k_ct_prep6<false> (the plain IPv6 path) with Q packets per lane, the
  * ipcache entries from the pre-pass (k_ipc6_pre, egress fallback folded in)
  * and the policy cascades through policy_q */
-template <int Q>
+template <int Q, bool SVC = false>
 __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, const uint32_t *ipc_e)
 {
 	const uint64_t T = (uint64_t)gridDim.x * 256u;
@@ -4801,13 +4895,29 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 	for (uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x; g < a.n; g += T * Q) {
 		bool act[Q], dec[Q], eg[Q], frag[Q];
 		uint32_t fdp[Q], pr[Q], ep[Q], meta[Q], tfl[Q], z[Q], w[Q], len[Q];
+		/* SVC: lb6_local's outcome (svc_out[2i], target svc_out[2i + 1]):
+		 * drop, translated, and the dport as lb6_xlate left it */
+		bool drop[Q], xl[Q];
+		uint32_t dpx[Q];
 		decision d[Q];
 #pragma unroll
 		for (int u = 0; u < Q; u++) {
 			const uint64_t i = g + (uint64_t)u * T;
 			act[u] = i < a.n;
 			const uint64_t j = act[u] ? i : 0u;
-			const uint32_t fl = ntl(a.flags + j), dp = ntl(a.dport + j), sp = ntl(a.sport + j);
+			const uint32_t fl = ntl(a.flags + j), sp = ntl(a.sport + j);
+			uint32_t dp = ntl(a.dport + j);
+			drop[u] = xl[u] = false;
+			if constexpr (SVC) {
+				if (fl & 1u) {
+					const uint4 so = a.svc_out[2u * j];
+					drop[u] = (so.x & 3u) == SVC_DROP;
+					xl[u] = (so.x & 3u) == SVC_XLATED;
+					if (xl[u] && (so.y & 0xFFFFu))
+						dp = so.y & 0xFFFFu; /* lb6_xlate's port rewrite */
+				}
+			}
+			dpx[u] = dp;
 			pr[u] = ntl(a.proto + j);
 			len[u] = ntl(a.len + j);
 			ep[u] = ntl(a.ep + j);
@@ -4837,9 +4947,10 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 			}
 			if (pr[u] != 6u)
 				w[u] = 0;
-			dec[u] = act[u] && !(meta[u] & CTM_GATED);
+			dec[u] = act[u] && !drop[u] && !(meta[u] & CTM_GATED);
 			fdp[u] = z[u] >> 16;
-			/* decide<1>'s identity from the pre-pass entry */
+			/* decide<1>'s identity from the pre-pass entry (SVC: looked up
+			 * on the translated daddr) */
 			const uint32_t e = ntl(ipc_e + j);
 			const uint32_t label = entry_label(s.ipc6.vals, e);
 			if (eg[u]) {
@@ -4857,7 +4968,37 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 			if (!act[u])
 				continue;
 			const uint64_t i = g + (uint64_t)u * T;
-			const uint4 sa = ld_x4<true>(sa16 + i), da = ld_x4<true>(da16 + i);
+			const uint4 sa = ld_x4<true>(sa16 + i);
+			uint4 da = ld_x4<true>(da16 + i);
+			uint32_t rev = eg[u] ? 0u : (da.w & 0xFFFFu), svcw = 0; /* svcw: slave | lbf << 16 */
+			if constexpr (SVC) {
+				if (drop[u]) { /* as k_ct_prep6<true> */
+					a.identity[i] = 0;
+					reinterpret_cast<uint16_t *>(a.f2)[i] = 0u;
+					if (a.xdaddr)
+						reinterpret_cast<uint4 *>(a.xdaddr)[i] = da;
+					if (a.xdport)
+						a.xdport[i] = (uint16_t)dpx[u];
+					uint4 *r = a.rec + 4u * i;
+					r[0] = da;
+					r[1] = sa;
+					r[2] = uint4{0u, pr[u] | ((CTM_EGRESS | CTM_GATED | CTM_SVCDROP) << 16), 0u, len[u]};
+					r[3] = uint4{0u, 0u, 0u, 0u};
+					a.gkey[i] = ct_fmix((uint32_t)i ^ 0x5bd1e995u);
+					a.idx[i] = (uint32_t)i;
+					continue;
+				}
+				if (xl[u]) {
+					const uint4 so = a.svc_out[2u * i];
+					da = a.svc_out[2u * i + 1u]; /* tuple->daddr = svc->target (lb.h:475) */
+					rev = so.y >> 16;
+					svcw = (so.x >> 16) | ((((so.x >> 8) & LBS_ENTRY) ? LBF_LOOPBACK : 0u) << 16);
+				}
+				if (a.xdaddr)
+					reinterpret_cast<uint4 *>(a.xdaddr)[i] = da;
+				if (a.xdport)
+					a.xdport[i] = (uint16_t)dpx[u];
+			}
 			uint32_t sec = 0, port = 0, cst = 0, id = 0, m = meta[u];
 			if (dec[u]) {
 				if (d[u].v >= 0) {
@@ -4885,7 +5026,7 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 			r[0] = da;
 			r[1] = sa;
 			r[2] = uint4{z[u], pr[u] | (tfl[u] << 8) | (m << 16), w[u] | (port << 16), len[u]};
-			r[3] = uint4{sec, cst, eg[u] ? 0u : (da.w & 0xFFFFu), 0u};
+			r[3] = uint4{sec, cst, rev, svcw};
 			a.gkey[i] = (m & CTM_GATED) ? ct_fmix((uint32_t)i ^ 0x5bd1e995u) : gk;
 			a.idx[i] = (uint32_t)i;
 		}
@@ -6800,7 +6941,7 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 			const unsigned gp = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + QP * NT - 1) / (QP * NT), res));
 			hipLaunchKernelGGL((k_ipc6_pre<QP, NT>), dim3(gp), dim3(NT), lds, st, s,
 					   static_cast<const uint4 *>(L.saddr), static_cast<const uint4 *>(L.daddr), L.flags,
-					   L.idx_sorted, L.n);
+					   L.idx_sorted, L.n, nullptr);
 			const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
 			hipLaunchKernelGGL((k_ct_prep6_q<Q>), dim3(gq), dim3(256), 0, st, s, a, L.idx_sorted);
 		} else {
@@ -6874,8 +7015,23 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	hipError_t e = ct_svc_walk<CtK6>(s, T, L, a, st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
-	launch_ct_decq<CtK6S>(s, a, st);
+	if (CGPU_CT_SVC_PRE6 && s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK && !CGPU_CT_SVC_DECQ6) {
+		/* as the plain IPv6 path: the ipcache lookups (on the translated
+		 * daddr) through the trie pre-pass into idx_sorted (free between
+		 * the service walk and the group sort), then Q packets per lane */
+		constexpr int NT = 1024, QP = CGPU_DIAG_IPC6_PRE_Q, Q = 4;
+		const size_t lds = (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u;
+		const unsigned res = resident_blocks((const void *)k_ipc6_pre<QP, NT>, NT, lds);
+		const unsigned gp = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + QP * NT - 1) / (QP * NT), res));
+		hipLaunchKernelGGL((k_ipc6_pre<QP, NT>), dim3(gp), dim3(NT), lds, st, s,
+				   static_cast<const uint4 *>(L.saddr), static_cast<const uint4 *>(L.daddr), L.flags,
+				   L.idx_sorted, L.n, static_cast<const uint4 *>(a.svc_out));
+		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+		hipLaunchKernelGGL((k_ct_prep6_q<Q, true>), dim3(gq), dim3(256), 0, st, s, a, L.idx_sorted);
+	} else {
+		hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
+		launch_ct_decq<CtK6S>(s, a, st);
+	}
 	e = ct_group_sort(s, L, a, L.n, &nh, st, true);
 	if (e != hipSuccess)
 		return e;
@@ -6919,7 +7075,13 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	e = hipMemsetAsync(a.ctl, 0, 16, st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL((k_ct_prep<true, false>), dim3(g), dim3(256), 0, st, s, a, true);
+	if (CGPU_CT_SVC_Q > 1) {
+		constexpr int Q = CGPU_CT_SVC_Q > 1 ? CGPU_CT_SVC_Q : 2;
+		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
+		hipLaunchKernelGGL((k_ct_prep_svc_q<Q>), dim3(gq), dim3(256), 0, st, s, a, true);
+	} else {
+		hipLaunchKernelGGL((k_ct_prep<true, false>), dim3(g), dim3(256), 0, st, s, a, true);
+	}
 	uint32_t ctl[4];
 	e = hipMemcpyAsync(ctl, a.ctl, 16, hipMemcpyDeviceToHost, st);
 	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)

@@ -58,7 +58,9 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "g4096_retb32": ("CT_WALK_GRID=4096", "CT_RETB=32"), "g8192_retb32": ("CT_WALK_GRID=8192", "CT_RETB=32"),
             "walk_grid16384": ("CT_WALK_GRID=16384",), "walk_grid32768": ("CT_WALK_GRID=32768",),
             "ff_nostage": ("CGPU_FF_STAGE=0",), "walk_svc_minb3": ("CGPU_WALK_MINB_SVC=3",),
-            "ct_create_noloop": ("CGPU_CT_CREATE_LOOP=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
+            "ct_create_noloop": ("CGPU_CT_CREATE_LOOP=0",),
+            "svc_q1": ("CGPU_CT_SVC_Q=1",), "svc_q2": ("CGPU_CT_SVC_Q=2",), "svc_q4": ("CGPU_CT_SVC_Q=4",),
+            "svc_pre6_off": ("CGPU_CT_SVC_PRE6=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
 
 
 def build(names):
