@@ -13,7 +13,8 @@ W=1; K=2
 for CONF in "$@"; do
   OUT=gpurun_out/prof_$TAG/$CONF
   mkdir -p $OUT
-  case $CONF in gpu|cascade|v6|frames) SKIP=$((W + 1));; *) SKIP=$W;; esac
+  # every config but pf6 runs one more step after the counter rebalance
+  case $CONF in pf6) SKIP=$W;; *) SKIP=$((W + 1));; esac
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --config $CONF --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/bench.err
   rc=$?; echo "$CONF trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
   i=0
