@@ -57,7 +57,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "walk_grid8192": ("CT_WALK_GRID=8192",), "retb32": ("CT_RETB=32",),
             "g4096_retb32": ("CT_WALK_GRID=4096", "CT_RETB=32"), "g8192_retb32": ("CT_WALK_GRID=8192", "CT_RETB=32"),
             "walk_grid16384": ("CT_WALK_GRID=16384",), "walk_grid32768": ("CT_WALK_GRID=32768",),
-            "ff_nostage": ("CGPU_FF_STAGE=0",), "walk_svc_minb3": ("CGPU_WALK_MINB_SVC=3",),
+            "ff_nostage": ("CGPU_FF_STAGE=0",), "ff_pool0": ("CGPU_FF_POOL=0",), "ff_pool8": ("CGPU_FF_POOL=8",),
+            "ff_pool2": ("CGPU_FF_POOL=2",), "walk_svc_minb3": ("CGPU_WALK_MINB_SVC=3",),
             "ct_create_noloop": ("CGPU_CT_CREATE_LOOP=0",),
             "svc_q1": ("CGPU_CT_SVC_Q=1",), "svc_q2": ("CGPU_CT_SVC_Q=2",), "svc_q4": ("CGPU_CT_SVC_Q=4",),
             "svc_pre6_off": ("CGPU_CT_SVC_PRE6=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
@@ -199,7 +200,10 @@ def _workload(conf):
         sched = int(os.environ.get("CGPU_AB_SCHED", "0"))
 
         def make():
-            e = Engine(device=0, **T.engine_config(), schedule=sched)
+            cfg = T.engine_config()
+            if os.environ.get("CGPU_AB_HOT"):
+                cfg["hot_counter_slots"] = int(os.environ["CGPU_AB_HOT"])
+            e = Engine(device=0, **cfg, schedule=sched)
             synth.load_engine(e, T)
             return e
         return make, lambda e: e.classify_frames(d, out=out), n
