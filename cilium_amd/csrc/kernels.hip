@@ -1611,6 +1611,11 @@ struct ftuple {
 #endif
 /* fused frames' LDS rows per wave: 64 slots x 80 B */
 #define FF_STG_U4 320u
+/* fused frames: staging buffers shared by a workgroup's 16 waves (0: one
+ * per wave) */
+#ifndef CGPU_FF_POOL
+#define CGPU_FF_POOL 4
+#endif
 
 __device__ __forceinline__ ftuple parse_frame_w(const cgpu_snapshot &s, const fwin &W, const uint8_t *f,
 						uint32_t len, uint32_t cap, bool egress, uint32_t ep,
@@ -1672,7 +1677,18 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	uint4 *lxl = reinterpret_cast<uint4 *>((reinterpret_cast<uintptr_t>(cck + a.cc_n) + 15u) & ~(uintptr_t)15u);
 	int16_t *fst = reinterpret_cast<int16_t *>(lxl + (FF ? 2u * FR_LXC_LDS : 0u));
 	/* fused frames: this wave's staging rows, after the statuses */
-	uint4 *stg = reinterpret_cast<uint4 *>(fst + (FF ? NT * Q : 0)) + (threadIdx.x >> 6) * FF_STG_U4;
+	uint4 *stg0 = reinterpret_cast<uint4 *>(fst + (FF ? NT * Q : 0));
+#if CGPU_FF_POOL
+	/* CGPU_FF_POOL staging buffers shared by the workgroup's waves (a wave
+	 * holds one only between its tile's LDS write and read), then their
+	 * busy flags: the LDS the per-wave rows took goes to hot counter slots */
+	uint32_t *pool_busy = reinterpret_cast<uint32_t *>(stg0 + CGPU_FF_POOL * FF_STG_U4);
+	if (FF && threadIdx.x < CGPU_FF_POOL)
+		pool_busy[threadIdx.x] = 0u;
+	uint4 *stg = stg0;
+#else
+	uint4 *stg = stg0 + (threadIdx.x >> 6) * FF_STG_U4;
+#endif
 	if constexpr (FF) {
 		for (uint32_t k = threadIdx.x; k < 2u * s.n_lxc; k += NT)
 			lxl[k] = s.lxc[k];
@@ -1763,6 +1779,30 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 					}
 					fwin W;
 #if CGPU_FF_STAGE
+#if CGPU_FF_POOL
+					/* take a free staging buffer (lane 0 for the wave) */
+					uint32_t pb = 0;
+					if (lane == 0) {
+						const uint32_t w0 = (threadIdx.x >> 6) % CGPU_FF_POOL;
+						for (bool got = false; !got;) {
+#pragma unroll 1
+							for (uint32_t t = 0; t < CGPU_FF_POOL && !got; t++) {
+								const uint32_t b = (w0 + t) % CGPU_FF_POOL;
+								uint32_t z0 = 0u;
+								if (__hip_atomic_compare_exchange_strong(&pool_busy[b], &z0, 1u, __ATOMIC_ACQUIRE,
+													 __ATOMIC_RELAXED,
+													 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+									pb = b;
+									got = true;
+								}
+							}
+							if (!got)
+								__builtin_amdgcn_s_sleep(1);
+						}
+					}
+					pb = (uint32_t)__shfl((int)pb, 0, 64);
+					stg = stg0 + pb * FF_STG_U4;
+#endif
 					/* each lane's slot through the wave's LDS rows (64 slots of
 					 * 80 B: conflict-free 16-B reads) */
 #pragma unroll
@@ -1778,6 +1818,11 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 						W.w[4 * q + 3] = v.w;
 					}
 					__builtin_amdgcn_wave_barrier();
+#if CGPU_FF_POOL
+					/* the reads above are done before the buffer is free */
+					if (lane == 0)
+						__hip_atomic_store(&pool_busy[pb], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
 #else
 #pragma unroll
 					for (int k = 0; k < 4; k++) {
@@ -3291,7 +3336,8 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 	fixed = (fixed + 7u) & ~(size_t)7u;
 	/* fused frames: the endpoint rows (+ alignment) and 4 statuses per lane */
 	const size_t ff = FF ? 16u + 2u * FR_LXC_LDS * 16u + (size_t)NT * 4u * 2u +
-				       (CGPU_FF_STAGE ? (size_t)(NT / 64) * FF_STG_U4 * 16u : 0u)
+				       (CGPU_FF_STAGE ? (size_t)(CGPU_FF_POOL ? CGPU_FF_POOL : NT / 64) * FF_STG_U4 * 16u + 64u
+						      : 0u)
 			     : 0u;
 	fixed += ff;
 	const cgpu_snapshot s = with_lds_hot(s0, fixed < X4_LDS_BUDGET ? (X4_LDS_BUDGET - fixed) / 8u : 0u);
