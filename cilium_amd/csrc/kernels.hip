@@ -3980,6 +3980,16 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #ifndef CGPU_CT_Q
 #define CGPU_CT_Q 4
 #endif
+/* ... of the finish pass alone (3: its 1024-thread workgroups spill 33-54
+ * VGPRs at Q = 4; ct 11.70 -> 11.12 ms, ct6 15.19 -> 14.50, ctlb 20.38 ->
+ * 19.65, ctlb6 22.16 -> 21.28, profiles/r5_m/ab_fin_*.log), and its
+ * workgroup size */
+#ifndef CGPU_CT_FQ
+#define CGPU_CT_FQ 3
+#endif
+#ifndef CGPU_CT_FNT
+#define CGPU_CT_FNT 1024
+#endif
 /* phase 2b groups an address entry no phase-2 packet can read by its whole
  * key (k_ct_owed_bloom); 0: by its pair (A/B) */
 #ifndef CGPU_OWED_BY_KEY
@@ -6928,7 +6938,7 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
 	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
-	constexpr int NF = 1024, Q = CGPU_CT_Q;
+	constexpr int NF = CGPU_CT_FNT, Q = CGPU_CT_FQ;
 	const uint64_t gf = std::max<uint64_t>(std::min<uint64_t>((a.n + NF * Q - 1) / (NF * Q), 512), (a.n >> 22) + 1);
 	const cgpu_snapshot sf = with_lds_hot(s, X4_LDS_BUDGET / 8u);
 	/* the cold-slot cache in the LDS the hot slots leave */

@@ -58,7 +58,10 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "g4096_retb32": ("CT_WALK_GRID=4096", "CT_RETB=32"), "g8192_retb32": ("CT_WALK_GRID=8192", "CT_RETB=32"),
             "walk_grid16384": ("CT_WALK_GRID=16384",), "walk_grid32768": ("CT_WALK_GRID=32768",),
             "ff_nostage": ("CGPU_FF_STAGE=0",), "ff_pool0": ("CGPU_FF_POOL=0",), "ff_pool8": ("CGPU_FF_POOL=8",),
-            "ff_pool2": ("CGPU_FF_POOL=2",), "walk_svc_minb3": ("CGPU_WALK_MINB_SVC=3",),
+            "ff_pool2": ("CGPU_FF_POOL=2",), "fin_q2": ("CGPU_CT_FQ=2",), "fin_q3": ("CGPU_CT_FQ=3",), "fin_q4": ("CGPU_CT_FQ=4",),
+            "prep_q3": ("CGPU_CT_Q=3",), "prep_q2": ("CGPU_CT_Q=2",),
+            "fin_nt512": ("CGPU_CT_FNT=512",), "fin_q3_nt512": ("CGPU_CT_FQ=3", "CGPU_CT_FNT=512"),
+            "fin_q2_nt512": ("CGPU_CT_FQ=2", "CGPU_CT_FNT=512"), "walk_svc_minb3": ("CGPU_WALK_MINB_SVC=3",),
             "ct_create_noloop": ("CGPU_CT_CREATE_LOOP=0",),
             "svc_q1": ("CGPU_CT_SVC_Q=1",), "svc_q2": ("CGPU_CT_SVC_Q=2",), "svc_q4": ("CGPU_CT_SVC_Q=4",),
             "svc_pre6_off": ("CGPU_CT_SVC_PRE6=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
