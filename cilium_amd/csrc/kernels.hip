@@ -6407,6 +6407,10 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 				if (MODE == WALK_PKT && (meta & CTM_PHASE2))
 					continue;
 				const uint32_t ret = ct_step<K>(T, A, c, r.key(), q, a.now);
+#ifdef CGPU_DIAG_RET_DEFAULT /* timing only: no store where the result is the direction's default */
+				if (ret == ((meta & CTM_EGRESS) ? CT_ESTABLISHED : CT_REPLY))
+					continue;
+#endif
 				s_ri[nret][threadIdx.x] = i;
 				s_rr[nret][threadIdx.x] = (uint8_t)ret;
 				if (++nret == CT_RETB)

@@ -51,7 +51,7 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "hs_g256": ("CGPU_HS_COPY_G=256",), "hs_g512": ("CGPU_HS_COPY_G=512",),
             "hs_g64": ("CGPU_HS_COPY_G=64",), "hs_chunk23": ("CGPU_HS_CHUNK_LOG2=23",),
             "hs_chunk21": ("CGPU_HS_CHUNK_LOG2=21",),
-            "ct_noret": ("CGPU_DIAG_NO_RET",),
+            "ct_noret": ("CGPU_DIAG_NO_RET",), "ret_default": ("CGPU_DIAG_RET_DEFAULT",),
             "ct_ret_small": ("CGPU_DIAG_RET_SMALL",), "ct_ret_nt": ("CGPU_DIAG_RET_NT",),
             "walk_grid1024": ("CT_WALK_GRID=1024",), "walk_grid2048": ("CT_WALK_GRID=2048",), "walk_grid4096": ("CT_WALK_GRID=4096",),
             "walk_grid8192": ("CT_WALK_GRID=8192",), "retb32": ("CT_RETB=32",),
