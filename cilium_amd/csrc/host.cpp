@@ -3888,8 +3888,12 @@ CGPU_EXPORT int cgpu_table_bytes(cgpu_ctx *c, uint64_t *out)
 		const DevBuf *b = ep ? ep->bufs[k].get() : nullptr;
 		out[k] = !b ? 0u : b->gather ? (uint64_t)b->gather : (uint64_t)b->bytes;
 	}
-	out[CGPU_TBL_CT4] = (uint64_t)(c->ct4.keys.size() + c->ct4.vals.size()) * 16u;
-	out[CGPU_TBL_CT6] = (uint64_t)(c->ct6.keys.size() + c->ct6.vals.size()) * 16u;
+	{
+		/* ct_classify resizes the mirrors under mu */
+		std::lock_guard<std::mutex> g(c->mu);
+		out[CGPU_TBL_CT4] = (uint64_t)(c->ct4.keys.size() + c->ct4.vals.size()) * 16u;
+		out[CGPU_TBL_CT6] = (uint64_t)(c->ct6.keys.size() + c->ct6.vals.size()) * 16u;
+	}
 	return 0;
 }
 
@@ -5613,13 +5617,20 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.temp_bytes = L.temp_bytes;
 	a.flags2 = b + L.flags2;
 	a.pk = c->d_ct_pk;
+	hipError_t le;
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);
 		a.ctl = reinterpret_cast<uint32_t *>(b + L.ctl);
 		a.pcls = b + L.pcls;
-		HIP_OR_EIO(m.v6 ? launch_classify_v6_ctlb(s, T, a, cs) : launch_classify_v4_ctlb(s, T, a, cs));
+		le = m.v6 ? launch_classify_v6_ctlb(s, T, a, cs) : launch_classify_v4_ctlb(s, T, a, cs);
 	} else {
-		HIP_OR_EIO(m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs));
+		le = m.v6 ? launch_classify_v6_ct(s, T, a, cs) : launch_classify_v4_ct(s, T, a, cs);
+	}
+	if (le != hipSuccess) {
+		/* pk is shared by every conntrack call and only k_unpack zeroes it:
+		 * a finish whose unpack never ran must not leak into the next call */
+		(void)hipMemsetAsync(c->d_ct_pk, 0, (size_t)c->n_ctr_slots * 8u, cs);
+		return fail(-EIO, "conntrack launch: %s", hipGetErrorString(le));
 	}
 	HIP_OR_EIO(hipEventRecord(c->ct_done, cs));
 	HIP_OR_EIO(hipStreamWaitEvent((hipStream_t)stream, c->ct_done, 0));

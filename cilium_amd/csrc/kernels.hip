@@ -6538,7 +6538,10 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 				if (ctr >= 0) {
 					const uint32_t cs = (uint32_t)ctr;
 					bool done = false;
-					if (len < PK_MAX_LEN) {
+					/* only packets of < PKC_MAX_LEN bytes may enter the LDS
+					 * sums: they are flushed into pk, whose byte field holds
+					 * PKC_CHUNK packets of < 2^11 bytes (as k_classify_x4) */
+					if (len < PKC_MAX_LEN) {
 						if (cs < s.hot_slots) {
 							atomicAdd((unsigned long long *)&lctr[cs],
 								  (1ull << PK_SHIFT) | (unsigned long long)len);
@@ -6565,7 +6568,7 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 						if (len < PKC_MAX_LEN) {
 							atomicAdd((unsigned long long *)&a.pk[cs],
 								  (1ull << PKC_SHIFT) | (unsigned long long)len);
-						} else {
+						} else { /* exact two-word path, never packed */
 							atomicAdd((unsigned long long *)&a.delta[2u * cs], 1ull);
 							atomicAdd((unsigned long long *)&a.delta[2u * cs + 1u],
 								  (unsigned long long)len);
@@ -6601,8 +6604,9 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 	}
 	__syncthreads();
 	/* one packed atomic per touched slot: PK (LDS) -> PKC (pk) format; a
-	 * workgroup's bytes per slot stay < 2^37 (< 2^26 packets of < 2^11, the
-	 * larger ones went to delta directly) */
+	 * workgroup's bytes per slot stay < 2^37 (< 2^26 packets of < 2^11 =
+	 * PKC_MAX_LEN; every packet of PKC_MAX_LEN bytes or more went to delta
+	 * directly above) */
 	for (uint32_t k = threadIdx.x; k < s.hot_slots; k += NT) {
 		const uint64_t x = lctr[k];
 		if (x)
@@ -6939,7 +6943,7 @@ static hipError_t ct_group_sort(const cgpu_snapshot &s, const ct_launch &L, ct_a
 #define CT_WALK_GRID 8192
 #endif
 
-template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
+template <class K> static hipError_t launch_ct_finish(const cgpu_snapshot &s, const ct_args &a, hipStream_t st)
 {
 	/* <= 2^23 packets per workgroup keeps the packed LDS counters exact */
 	constexpr int NF = CGPU_CT_FNT, Q = CGPU_CT_FQ;
@@ -6953,11 +6957,17 @@ template <class K> static void launch_ct_finish(const cgpu_snapshot &s, const ct
 		const uint64_t hi = std::min<uint64_t>(a.n, lo + PKC_CHUNK);
 		hipLaunchKernelGGL((k_ct_finish<NF, K, Q>), dim3((unsigned)gf), dim3(NF), hot + (size_t)cc_n * 12u, st,
 				   sf, a, cc_n, lo, hi);
+		hipError_t e = hipGetLastError();
+		if (e != hipSuccess)
+			return e;
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
 			hipLaunchKernelGGL(k_unpack, dim3(ug), dim3(256), 0, st, a.delta, a.pk, 0u, s.cold_hi);
+			if ((e = hipGetLastError()) != hipSuccess)
+				return e;
 		}
 	}
+	return hipSuccess;
 }
 
 /* phase 2 of the plain paths (and of the IPv6 service path): the ICMP
@@ -7019,8 +7029,7 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<K>(s, T, L, a, st)) != hipSuccess)
 		return e;
-	launch_ct_finish<K>(s, a, st);
-	return hipGetLastError();
+	return launch_ct_finish<K>(s, a, st);
 }
 
 hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
@@ -7098,8 +7107,7 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	hipLaunchKernelGGL((k_ct_walk<CtK6S, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<CtK6S>(s, T, L, a, st)) != hipSuccess)
 		return e;
-	launch_ct_finish<CtK6S>(s, a, st);
-	return hipGetLastError();
+	return launch_ct_finish<CtK6S>(s, a, st);
 }
 
 /*
@@ -7187,8 +7195,7 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 			hipLaunchKernelGGL((k_ct_walk<CtK4S, WALK_OWED>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 		}
 	}
-	launch_ct_finish<CtK4S>(s, a, st);
-	return hipGetLastError();
+	return launch_ct_finish<CtK4S>(s, a, st);
 }
 
 /* ======================================================================= */

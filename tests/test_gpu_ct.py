@@ -256,3 +256,56 @@ def test_ct_many_connections_per_pair(torch_cuda, cfg_ct):
     _assert_same_map(e, o)
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     e.close()
+
+
+def test_ct_jumbo_counters_one_slot(torch_cuda, cfg_ct):
+    """~2.2M packets of 65,535 bytes hit ONE policy slot in
+    one batch, 2^37.07 bytes, past the 37-bit byte field of the packed
+    per-slot accumulator that the finish sums over a whole PKC_CHUNK.  Every
+    packet of >= 2^11 bytes must take the exact two-word path: the slot's
+    packet and byte counters, every other slot's, and the metrics equal the
+    restatement's."""
+    from oracle import Oracle
+    T, t, locals_be, seclabels = cfg_ct
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_lxc(o, seclabels)
+    o.ct_set_max(1 << 18)
+    probe = {k: x[:20_000] for k, x in t.items()}
+    v0, cr0, _, _, _ = o.classify_v4_ct(probe, 10)
+    cand = np.flatnonzero((v0 == 0) & (probe["flags"] & 1 == 1) & (probe["proto"] == 6))
+    assert len(cand), "no allowed egress TCP packet to replicate"
+    j = int(cand[0])
+    n, n_conn = 2_200_000, 20_000
+    rng = np.random.Generator(np.random.PCG64(23))
+    conn = rng.integers(0, n_conn, n)
+    jumbo = {
+        "saddr": np.full(n, probe["saddr"][j], np.uint32), "daddr": np.full(n, probe["daddr"][j], np.uint32),
+        "sport": (1024 + conn).astype(np.uint16), "dport": np.full(n, probe["dport"][j], np.uint16),
+        "proto": np.full(n, 6, np.uint8), "l4b": np.full(n, (5 << 4) | (16 << 8), np.uint16),
+        "flags": np.full(n, probe["flags"][j], np.uint8), "len": np.full(n, 65535, np.uint32),
+        "ep": np.full(n, probe["ep"][j], np.uint16),
+    }
+    o2 = Oracle(**T.oracle_config())
+    synth.load_oracle(o2, T)
+    synth.load_lxc(o2, seclabels)
+    o2.ct_set_max(1 << 18)
+    e = _engine(**T.engine_config(), ct_max=1 << 18)
+    synth.load_engine(e, T)
+    synth.load_lxc(e, seclabels)
+    e.commit()
+    v, cr, idt, st = _run(torch_cuda, e, jumbo, 20)
+    ve, cre, ie, se, _ = o2.classify_v4_ct(jumbo, 20)
+    np.testing.assert_array_equal(v, ve)
+    np.testing.assert_array_equal(cr, cre)
+    assert (v == 0).sum() > (1 << 21), "the jumbo packets must be allowed to count"
+    np.testing.assert_array_equal(e.metrics(), o2.metrics())
+    big = 0
+    for k, ep in zip(T.pol_keys, T.pol_ep):
+        rc, got = e.policy_lookup(int(ep), k)
+        _, raw = o2.policy_lookup(int(ep), k)
+        exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(exp["packets"]), int(exp["bytes"]))
+        big = max(big, int(exp["bytes"]))
+    assert big >= 1 << 37, "one slot must pass the packed byte field"
+    e.close()

@@ -194,7 +194,7 @@ def _workload(conf):
         return make, step, n
     if conf == "frames":
         # bench.py --config frames: config-2 tuples as 64-byte frame slots;
-        # CGPU_AB_SCHED = cgpu_config.schedule (8: the fused kernel)
+        # CGPU_AB_SCHED = cgpu_config.schedule (8: the split header + classify passes; 0: the fused default)
         T = synth.make_tables(**synth.CONFIGS["gpu"])
         n = synth.CONFIGS["gpu"]["n_tuples"]
         d = synth.frames_to_device(synth.frames_from_tuples(synth.make_tuples(T, n), stride=64), "cuda")
