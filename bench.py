@@ -17,9 +17,13 @@ fixed (weak scaling) and the stream is N x 64M tuples per step.
 Rank 0 prints one JSON line.
 
 Other BASELINE configs (not the headline line; run them explicitly):
-  --config cascade   config 5: 1M IPv4 services in front of config 2 (the
-                     egress service step of bpf_lxc.c:444-469 fused into the
-                     classify kernel, cgpu_classify_v4_lb)
+  --config cascade   config 5 whole, "prefilter -> ipcache -> policy -> LB":
+                     the netdev's XDP prefilter (bpf_xdp.c check_v4: 16k dyn4
+                     prefixes + 200k fix4 /32s, then the local-endpoint check)
+                     in front of every ingress tuple and the egress service
+                     step over 1M services (bpf_lxc.c:444-469) in front of
+                     every egress tuple, both fused into the classify kernel
+                     (cgpu_classify_v4_cascade)
   --config pf6       config 3: XDP IPv6 prefilter over 1M deny prefixes
   --config frames    config 2 tables, the batch as raw Ethernet frames in
                      64-byte ring slots (cgpu_classify_frames: header parse
@@ -105,9 +109,11 @@ WORKLOADS = {
     "v6": "IPv6 classify at config-2 size: 100k IPv6 ipcache prefixes (1024 /48 sites under 64 "
           "/16 roots; /128 40%, /64 30%, /56 10%, /48 7%, /96 5%, /112 5%, /32 3%) + 64k policy "
           "entries (4 ep x 16k), 64M-tuple batches per GPU, bit-exact verdicts",
-    "cascade": "config5: 1M IPv4 services (lb4_local, backends ~Geom(0.3) cap 16, 30% of egress "
-               "tuples to a service) -> ipcache(post-DNAT) -> policy over config-2 tables, "
-               "64M-tuple batches per GPU, bit-exact verdicts",
+    "cascade": "config5: XDP prefilter on ingress (bpf_xdp.c check_v4: 16k dyn4 LPM prefixes + 200k fix4 "
+               "/32s on saddr, then daddr in the 4 local endpoints; ~5% of ingress tuples from the deny "
+               "set, 1% to no endpoint) | 1M IPv4 services on egress (lb4_local, backends ~Geom(0.3) cap "
+               "16, 30% of egress tuples to a service) -> ipcache(post-DNAT) -> policy over config-2 "
+               "tables, 64M-tuple batches per GPU, bit-exact verdicts",
     "pf6": "config3: XDP IPv6 prefilter, 1M deny prefixes (/32..../128, /128 in fix) under 256 "
            "/24 roots + 4k endpoints, 64M packets per GPU",
     "frames": "config2 tables, 64M raw Ethernet/IPv4/TCP|UDP frames per GPU in 64-byte slots: "
@@ -421,7 +427,9 @@ def main():
             assert (shard.shard_of(tup, world) == rank).all()
         if cascade:
             S = synth.make_services(T, cfg["n_services"])
-            tup = synth.add_service_traffic(tup, S, gpu_id=rank)
+            P4 = synth.make_prefilter4(T)
+            tup = synth.add_prefilter_traffic(synth.add_service_traffic(tup, S, gpu_id=rank), P4,
+                                              gpu_id=rank)
             del tup["hash"]  # skb->hash stand-in computed in the kernel from sport
         log(f"[rank {rank}] synthetic tables ({len(T.ipc_keys)} ipcache, {len(T.pol_keys)} policy"
             f"{', %d service-map entries' % len(S.keys) if S is not None else ''}) "
@@ -435,6 +443,8 @@ def main():
         synth.load_engine(e, T)
         if S is not None:
             synth.load_services(e, S)
+        if cascade:
+            synth.load_prefilter4(e, P4)
     t0 = time.time()
     e.commit()
     log(f"[rank {rank}] commit {time.time() - t0:.2f}s, checksum {e.checksum():#x}")
@@ -507,7 +517,7 @@ def main():
         elif pf6:
             e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
         elif cascade:
-            e.classify_v4_lb(d, out=out, stream=stream)
+            e.classify_v4_cascade(d, out=out, stream=stream)
         elif v6:
             e.classify_v6(d, out=out, stream=stream)
         elif frames and args.host_tuples:
@@ -630,12 +640,14 @@ def main():
             synth.load_oracle(o, T)
             if S is not None:
                 synth.load_services(o, S)
+            if cascade:
+                synth.load_prefilter4(o, P4)
         def cpu_run(sl):
             if pf6:
                 return o.prefilter_v6(tup["saddr"][sl], tup["daddr"][sl], tup["flags"][sl],
                                       nthreads=threads)
             if cascade:
-                return o.classify_v4_lb({k: v[sl] for k, v in tup.items()}, nthreads=threads)
+                return o.classify_v4_cascade({k: v[sl] for k, v in tup.items()}, nthreads=threads)
             if v6:
                 return o.classify_v6({k: v[sl] for k, v in tup.items()}, nthreads=threads)
             if frames:
@@ -715,7 +727,7 @@ def main():
             if pf6:
                 return o.prefilter_v6(tup["saddr"], tup["daddr"], tup["flags"], nthreads=threads)
             if cascade:
-                return o.classify_v4_lb(tup, nthreads=threads)
+                return o.classify_v4_cascade(tup, nthreads=threads)
             if v6:
                 return o.classify_v6(tup, nthreads=threads)
             if frames:
@@ -742,7 +754,8 @@ def main():
         n_cpu = n
         if not skip_cpu and not ct:
             what = {"pf6": "oracle/cgpu_oracle.c prefilter (kernel-like LPM trie + hash)",
-                    "cascade": "oracle/cgpu_oracle.c lb4_local + LPM trie + open hash",
+                    "cascade": ("oracle/cgpu_oracle.c or_classify_v4_cascade: XDP check_v4 (LPM trie + "
+                                "hash + endpoint hash) | lb4_local, then LPM trie + open hash"),
                     "v6": "oracle/cgpu_oracle.c IPv6 LPM trie + open hash",
                     "frames": "oracle/cgpu_oracle.c frame parse + LPM trie + open hash"}.get(
                 args.config, "oracle/cgpu_oracle.c (kernel-like LPM trie + open hash)")
@@ -840,6 +853,11 @@ def main():
             conf.update(ipcache_prefixes=int(len(T.ipc_keys)), policy_entries=int(len(T.pol_keys)))
             if S is not None:
                 conf.update(services=int(len(S.vip)), lb_map_entries=int(len(S.keys)))
+            if cascade:
+                conf.update(prefilter_dyn4=int(len(P4.dyn4)), prefilter_fix4=int(len(P4.fix4)),
+                            local_endpoints=int(len(P4.ep_keys)),
+                            xdp_drop_frac_of_ingress=round(float(
+                                (v0 == -4097).sum() / max(1, int(((tup["flags"] & 1) == 0).sum()))), 4))
             if ct:
                 ctr = out["ct_ret"].cpu().numpy()
                 conf.update(ct_max=ct_max,

@@ -3528,6 +3528,50 @@ static int commit_pol(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	return 0;
 }
 
+/* the any-match DIR-24-8 image of the v4 deny set as one boundary node per
+ * /16 (tables.h PF4X_*) */
+static void build_pf4x(const Dir248 &d, std::vector<uint4> &x)
+{
+	x.assign((size_t)65536 * 2, uint4{0, 0, 0, 0});
+	std::vector<uint32_t> b;
+	for (uint32_t p = 0; p < 65536; p++) {
+		b.clear();
+		bool cur = false, flip = false;
+		for (uint32_t j = 0; j < 256 && b.size() <= 15; j++) {
+			const uint32_t e = d.tbl24[(size_t)p * 256 + j];
+			const bool grp = (e & DIR_TAG_MASK) == DIR_TAG_GROUP;
+			for (uint32_t k = 0; k < (grp ? 256u : 1u); k++) {
+				const bool v = (grp ? d.tbl8[(size_t)(e & DIR_PAYLOAD_MASK) * 256 + k] : e) != 0u;
+				const uint32_t at = (j << 8) | k;
+				if (at == 0)
+					flip = cur = v;
+				else if (v != cur) {
+					b.push_back(at);
+					cur = v;
+				}
+			}
+		}
+		uint16_t w[16];
+		for (int i = 0; i < 16; i++)
+			w[i] = 0xFFFFu;
+		uint16_t h = flip ? 1u : 0u;
+		if (b.size() > 15) {
+			h |= PF4X_OVF;
+		} else {
+			if (b.size() > 7)
+				h |= PF4X_TWO;
+			for (size_t i = 0; i < b.size(); i++)
+				w[1 + i] = (uint16_t)(b[i] - 1u);
+		}
+		w[0] = h;
+		uint32_t u[8];
+		for (int i = 0; i < 8; i++)
+			u[i] = (uint32_t)w[2 * i] | ((uint32_t)w[2 * i + 1] << 16);
+		x[2 * p] = uint4{u[0], u[1], u[2], u[3]};
+		x[2 * p + 1] = uint4{u[4], u[5], u[6], u[7]};
+	}
+}
+
 /* group PF: XDP prefilter any-match tables (v4 compressed like the ipcache,
  * v6 interval cover) */
 static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
@@ -3536,9 +3580,11 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	const bool have4 = !c4.empty();
 	Dir248 d;
 	Lpm16cBuild lc;
+	std::vector<uint4> x4;
 	if (have4) {
 		build_dir(std::move(c4), d, true);
 		lc.build(d.tbl24, d.tbl8);
+		build_pf4x(d, x4);
 		d.tbl24.clear();
 		d.tbl24.shrink_to_fit();
 		d.tbl8.clear();
@@ -3549,8 +3595,9 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	if (pf6.too_big)
 		return fail(-E2BIG, "prefilter v6 cover exceeds 2^25 node lines");
 	Arena ar;
-	size_t o4[4] = {0, 0, 0, 0}, o6[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	size_t o4[5] = {0, 0, 0, 0, 0}, o6[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	if (have4) {
+		o4[4] = ar.add(x4.data(), x4.size() * sizeof(uint4));
 		o4[0] = ar.add(lc.x16.data(), lc.x16.size() * 4);
 		o4[1] = ar.add(lc.d16.data(), lc.d16.size() * 4);
 		o4[2] = ar.add(lc.nodes.data(), lc.nodes.size() * 4);
@@ -3568,12 +3615,14 @@ static int commit_pf(cgpu_ctx *c, CommitIn &in, cgpu_snapshot &s, DevBufP &buf)
 	}
 	if (int r = upload(c, ar, buf, G_PF))
 		return r;
-	buf->gather = have4 ? (lc.x16.size() + lc.nodes.size()) * 4 : 0;
+	/* the cascade's lookups gather pf4x (and the nodes of overflowing /16s) */
+	buf->gather = have4 ? x4.size() * sizeof(uint4) + lc.nodes.size() * 4 : 0;
 	if (pf6.any)
 		buf->gather += (pf6.b32.size() + pf6.pool.size()) * 4 + pf6.h64.size() * 32 +
 			       (pf6.b24_16.empty() ? pf6.b24.size() * 4 : 0) +
 			       (pf6.root16.empty() && pf6.rbits.empty() ? pf6.root.size() * 4 : 0);
 	s.pf4c = lpm16c{};
+	s.pf4x = have4 ? at<uint4>(buf, o4[4]) : nullptr;
 	if (have4)
 		s.pf4c = lpm16c{at<uint32_t>(buf, o4[1]), at<uint32_t>(buf, o4[2]), nullptr, at<uint32_t>(buf, o4[0]),
 				at<uint32_t>(buf, o4[3]), (uint32_t)lc.nodes.size(), (uint32_t)lc.dict.size()};
@@ -4573,6 +4622,33 @@ CGPU_EXPORT int cgpu_classify_v4_lb(cgpu_ctx *c, const cgpu_tuples_v4 *t, const 
 	classify_v4_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
 			   verdict, identity, stage, delta, (uint64_t)n, pk};
 	a.lb = 1;
+	a.sport = sport;
+	a.hash = hash;
+	HIP_OR_EIO(hipSetDevice(c->device));
+	HIP_OR_EIO(launch_classify_v4(s, a, (hipStream_t)stream));
+	return 0;
+}
+
+CGPU_EXPORT int cgpu_classify_v4_cascade(cgpu_ctx *c, const cgpu_tuples_v4 *t, const uint16_t *sport,
+					 const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+					 uint8_t *stage, void *stream)
+{
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
+		return r;
+	const cgpu_snapshot &s = P.snap();
+	uint64_t *delta = P.delta, *pk = P.pk;
+	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
+			 !t->ep || !verdict || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (n && !hash && !sport)
+		return fail(-EINVAL, "either a hash or an sport column is needed");
+	if (!n)
+		return 0;
+	classify_v4_args a{t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep,
+			   verdict, identity, stage, delta, (uint64_t)n, pk};
+	a.lb = 1;
+	a.xdp = 1;
 	a.sport = sport;
 	a.hash = hash;
 	HIP_OR_EIO(hipSetDevice(c->device));

@@ -23,6 +23,9 @@
 #define DROP_NO_SERVICE (-158)      /* bpf/lib/common.h:265 */
 #define XDP_DROP 1
 #define XDP_PASS 2
+/* CGPU_VERDICT_XDP_DROP: an ingress tuple the netdev's XDP prefilter dropped
+ * (cgpu_classify_v4_cascade; stage 8) */
+#define VERDICT_XDP_DROP (-4097)
 #define TC_ACT_OK 0
 #define TC_ACT_REDIRECT 7
 
@@ -220,6 +223,95 @@ __device__ __forceinline__ bool set4_has(const addr_set4 &t, uint32_t a)
 		b = (b + 1) & t.bucket_mask;
 	}
 	return false;
+}
+
+/* check_v4 of the netdev's XDP program for a pre-parsed IPv4 packet
+ * (bpf_xdp.c:97-121): saddr covered by the dyn LPM or a fix /32
+ * (CIDR4_FILTER; pf4c is their any-match union) -> XDP_DROP, else daddr must
+ * be a local endpoint (check_v4_endpoint :88-95).  true = XDP_PASS. */
+/* slots of a pf4x half-node below x: u16 lanes k0.. of the four words */
+__device__ __forceinline__ uint32_t pf4x_below(uint4 q, uint32_t x, bool skip_header)
+{
+	return (!skip_header && (q.x & 0xFFFFu) < x ? 1u : 0u) + ((q.x >> 16) < x ? 1u : 0u) +
+	       ((q.y & 0xFFFFu) < x ? 1u : 0u) + ((q.y >> 16) < x ? 1u : 0u) + ((q.z & 0xFFFFu) < x ? 1u : 0u) +
+	       ((q.z >> 16) < x ? 1u : 0u) + ((q.w & 0xFFFFu) < x ? 1u : 0u) + ((q.w >> 16) < x ? 1u : 0u);
+}
+
+/* the deny set covers saddr (network order): pf4x (tables.h PF4X_*), with
+ * pf4c for the /16s of more than 15 boundaries */
+__device__ __forceinline__ bool pf4_covered(const cgpu_snapshot &s, uint32_t sa)
+{
+	const uint32_t h = bswap32(sa), x = h & 0xFFFFu;
+	const uint4 q = s.pf4x[2u * (h >> 16)];
+	if (q.x & PF4X_OVF)
+		return lpmc_lookup(s.pf4c, s.pf4c.dict, sa) != 0;
+	uint32_t c = pf4x_below(q, x, true) + (q.x & 1u);
+	if (q.x & PF4X_TWO)
+		c += pf4x_below(s.pf4x[2u * (h >> 16) + 1u], x, false);
+	return c & 1u;
+}
+
+__device__ __forceinline__ bool xdp_pass4(const cgpu_snapshot &s, uint32_t sa, uint32_t da)
+{
+	if (s.pf4_enabled && s.pf4x && pf4_covered(s, sa))
+		return false;
+	return set4_has(s.ep4, da);
+}
+
+/* xdp_pass4 for Q packets of one lane, stage by stage: the Q deny-set
+ * gathers (the /16's pf4x half-nodes) together, then, for the packets the
+ * deny set passed, the Q endpoint buckets' first 16 bytes (slots 0 and 1)
+ * together; a /16 of more than 15 boundaries and a bucket the first two
+ * slots do not decide take the per-packet path.  act false: pass[u] = true. */
+template <int Q>
+__device__ __forceinline__ void xdp4_q(const cgpu_snapshot &s, const bool (&act)[Q], const uint32_t (&sa)[Q],
+				       const uint32_t (&da)[Q], bool (&pass)[Q])
+{
+	const bool pf = s.pf4_enabled && s.pf4x;
+	bool chk[Q];
+	{
+		/* the /16's first half-node for every packet, then the second half
+		 * for the /16s of 8..15 boundaries (the same line) */
+		uint4 q[Q];
+		uint32_t c[Q];
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			q[u] = (act[u] && pf) ? s.pf4x[2u * (bswap32(sa[u]) >> 16)] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+		for (int u = 0; u < Q; u++)
+			c[u] = pf4x_below(q[u], bswap32(sa[u]) & 0xFFFFu, true) + (q[u].x & 1u);
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			const uint4 q2 = (q[u].x & PF4X_TWO) ? s.pf4x[2u * (bswap32(sa[u]) >> 16) + 1u] : make_uint4(0, 0, 0, 0);
+			if (q[u].x & PF4X_TWO)
+				c[u] += pf4x_below(q2, bswap32(sa[u]) & 0xFFFFu, false);
+		}
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			bool deny = false;
+			if (act[u] && pf)
+				deny = (q[u].x & PF4X_OVF) ? lpmc_lookup(s.pf4c, s.pf4c.dict, sa[u]) != 0u : (c[u] & 1u) != 0u;
+			pass[u] = !deny;
+			chk[u] = act[u] && !deny;
+		}
+	}
+	uint4 b[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++)
+		b[u] = chk[u] ? reinterpret_cast<const uint4 *>(s.ep4.slots)[(size_t)(mix32(da[u], 0x5e7) & s.ep4.bucket_mask) * 4u]
+			      : make_uint4(0, 0, 0, 0);
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		if (!chk[u])
+			continue;
+		/* slots 0 / 1 of the home bucket decide unless both are used and
+		 * neither holds da */
+		const uint4 w = b[u];
+		if (!w.y || w.x == da[u] || !w.w || w.z == da[u])
+			pass[u] = w.y && (w.x == da[u] || (w.w && w.z == da[u]));
+		else
+			pass[u] = set4_has(s.ep4, da[u]);
+	}
 }
 
 /* Resolve a 16-byte-key probe whose first bucket is loaded: returns the
@@ -897,6 +989,7 @@ struct cls_args {
 	uint64_t n_off;
 	/* k_classify_x4 IPCE: the ipcache entries k_ipc6_pre wrote, [n] */
 	uint32_t *ipc_e;
+	int xdp; /* v4 with lb: the XDP prefilter before every ingress tuple (cgpu_classify_v4_cascade) */
 };
 
 /* The identity resolution and the three-probe policy cascade for one tuple
@@ -1235,8 +1328,13 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 				}
 			}
 		}
+		/* config 5 whole: the netdev's XDP prefilter before an ingress
+		 * tuple reaches from_netdev (bpf_xdp.c:180-184) */
+		bool xdpdrop = false;
 		if (!V6) {
 			eda = static_cast<const uint32_t *>(a.daddr)[i];
+			if (a.xdp && !egress)
+				xdpdrop = !xdp_pass4(s, static_cast<const uint32_t *>(a.saddr)[i], eda);
 			if (a.lb && egress) {
 				const uint32_t sa = static_cast<const uint32_t *>(a.saddr)[i];
 				const uint32_t h = a.hash ? a.hash[i] : flow_hash(sa, eda, a.sport[i], dport, proto);
@@ -1253,7 +1351,12 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		const bool gated = s.ct_proto_gate && proto != (V6 ? 58u : 1u) && proto != 6u &&
 				   proto != 17u;
 
-		if (lbdrop) {
+		if (xdpdrop) {
+			/* XDP_DROP: nothing counted, nothing notified */
+			v = VERDICT_XDP_DROP;
+			id = 0;
+			st = 8;
+		} else if (lbdrop) {
 			v = DROP_NO_SERVICE;
 			id = 0;
 			st = 6;
@@ -1295,7 +1398,7 @@ __global__ __launch_bounds__(NT) void k_classify(cgpu_snapshot s, cls_args a)
 		if (a.stage)
 			a.stage[i] = (uint8_t)st;
 		/* a proxy redirect (v > 0) traces TRACE_TO_PROXY: no metrics */
-		const uint32_t r = v > 0 ? 4u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_NO_SERVICE ? 3u : 2u));
+		const uint32_t r = (v > 0 || xdpdrop) ? 4u : v == 0 ? 0u : (v == DROP_POLICY ? 1u : (v == DROP_NO_SERVICE ? 3u : 2u));
 		const uint32_t idx = r * 2u + (egress ? 1u : 0u);
 #pragma unroll
 		for (int k = 0; k < 8; k++) {
@@ -1636,10 +1739,11 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t x)
  * consecutive slots and each output store 64 consecutive frames), IPv6
  * frames compacted to fx for the v6 pass */
 template <int NT, bool NTL = false, int Q = 4, int MINW = 1, bool LB = false, bool V6 = false,
-	  int FR = 0, bool IPCE = false>
+	  int FR = 0, bool IPCE = false, bool XDP = false>
 __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_args a0, uint64_t *pk, frames_x4 fx)
 {
 	constexpr bool FF = FR == 2;
+	static_assert(!XDP || (LB && !V6), "the XDP prefilter: the IPv4 cascade");
 	static_assert(!FF || (Q == 4 && !V6 && !LB), "fused frames: the v4 x4 schedule");
 	cls_args a = a0;
 	if (FR && a0.n_dev) {
@@ -1647,8 +1751,10 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 		a.n = c > a0.n_off ? min(c - a0.n_off, a0.n) : 0;
 	}
 	/* per-tuple flag word */
+	/* F_XDP (with F_LBDROP, which ends the tuple's lookups): the XDP
+	 * prefilter dropped an ingress tuple (cgpu_classify_v4_cascade) */
 	constexpr uint32_t F_OK = 1u, F_EG = 2u, F_GATED = 4u, F_FRAG = 8u, F_LVL8 = 16u, F_LBDROP = 32u,
-			   F_DEC = 64u;
+			   F_DEC = 64u, F_XDP = 128u;
 	extern __shared__ __attribute__((aligned(16))) uint64_t lctr[];
 	/* drop metrics (send_drop_notify -> update_metrics, drop.h:94-118):
 	 * [reason 133 / 137 / 158][ingress, egress] x {count, bytes} in LDS
@@ -2006,6 +2112,21 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				for (int u = 0; u < Q; u++)
 					if (drop[u])
 						lbf[u] = F_LBDROP;
+				if constexpr (XDP) {
+					/* config 5 whole: the netdev's XDP prefilter (bpf_xdp.c
+					 * check_v4) before an ingress tuple reaches from_netdev
+					 * (bpf_netdev.c:470); the egress tuples took the service
+					 * step above */
+					bool in[QA], pass[QA];
+#pragma unroll
+					for (int u = 0; u < QA; u++)
+						in[u] = u < Q && !(fl[u] & 1u) && i0 + u < a.n;
+					xdp4_q<QA>(s, in, sa, da, pass);
+#pragma unroll
+					for (int u = 0; u < Q; u++)
+						if (!pass[u])
+							lbf[u] = F_LBDROP | F_XDP;
+				}
 			}
 #pragma unroll
 			for (int u = 0; u < Q; u++) {
@@ -2246,7 +2367,12 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				}
 				continue;
 			}
-			if (fw[u] & F_LBDROP) {
+			if (XDP && (fw[u] & F_XDP)) {
+				/* XDP_DROP: nothing counted, nothing notified */
+				v[u] = VERDICT_XDP_DROP;
+				id[u] = 0;
+				st[u] = 8;
+			} else if (fw[u] & F_LBDROP) {
 				v[u] = DROP_NO_SERVICE;
 				id[u] = 0;
 				st[u] = 6;
@@ -2302,7 +2428,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 				fwd_n[e] += 1u;
 				fwd_b[e] += len[u];
 			}
-			if ((fw[u] & F_OK) && v[u] < 0) {
+			if ((fw[u] & (F_OK | (XDP ? F_XDP : 0u))) == F_OK && v[u] < 0) {
 				const uint32_t mr = v[u] == DROP_POLICY ? 1u : (v[u] == DROP_NO_SERVICE ? 3u : 2u);
 				const uint32_t mi = (mr * 2u + ((fw[u] & F_EG) ? 1u : 0u)) * 2u;
 				atomicAdd(&lmet[mi], 1ull);
@@ -2771,8 +2897,7 @@ __global__ __launch_bounds__(BLOCK) void k_prefilter_v4(cgpu_snapshot s, prefilt
 		} else if (f != 0u) {
 			v = XDP_DROP;
 		} else {
-			const bool drop = s.pf4_enabled && s.pf4c.x16 && lpmc_lookup(s.pf4c, s.pf4c.dict, sa) != 0;
-			v = drop ? XDP_DROP : (set4_has(s.ep4, da) ? XDP_PASS : XDP_DROP);
+			v = xdp_pass4(s, sa, da) ? XDP_PASS : XDP_DROP;
 		}
 		a.verdict[i] = v;
 	}
@@ -3319,7 +3444,7 @@ static hipError_t launch_ipc6_pre(const cgpu_snapshot &s, const cls_args &a, hip
 	return hipGetLastError();
 }
 
-template <bool LB, bool V6, int FR = 0, bool IPCE = false>
+template <bool LB, bool V6, int FR = 0, bool IPCE = false, bool XDP = false>
 static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st,
 			    const frames_x4 &fx = frames_x4{})
 {
@@ -3354,7 +3479,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 #else
 	constexpr int Q = V6 && !IPCE ? 2 : 4; /* in-kernel v6 lookups: the trie's line registers */
 #endif
-	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE>;
+	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE, XDP>;
 	static_assert(!FF || Q == 4, "fused frames: Q = 4");
 	const unsigned res = resident_blocks(kern, NT, lds);
 	/* LDS packed counters: <= 2^22 tuples per workgroup (PK_SHIFT) */
@@ -3387,7 +3512,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 			c.ipc_e += off;
 		c.n_off = off;
 		const unsigned g = (unsigned)std::min<uint64_t>((m + Q * NT - 1) / (Q * NT), res);
-		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE>), dim3(g), dim3(NT), lds, st, s, c,
+		hipLaunchKernelGGL((k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE, XDP>), dim3(g), dim3(NT), lds, st, s, c,
 				   a.pk, fx);
 		if (s.cold_hi) {
 			const unsigned ug = std::min<unsigned>((s.cold_hi + 255) / 256, 1024);
@@ -3415,7 +3540,9 @@ static hipError_t launch_classify(const cgpu_snapshot &s0, cls_args a, hipStream
 		if (V6)
 			return a.lb ? launch_x4<true, true>(s0, a, st)
 				    : (a.ipc_e ? launch_x4<false, true, false, true>(s0, a, st) : launch_x4<false, true>(s0, a, st));
-		return a.lb ? launch_x4<true, false>(s0, a, st) : launch_x4<false, false>(s0, a, st);
+		if (a.lb)
+			return a.xdp ? launch_x4<true, false, 0, false, true>(s0, a, st) : launch_x4<true, false>(s0, a, st);
+		return launch_x4<false, false>(s0, a, st);
 	}
 	/* LDS counters: 1024-thread workgroups, <= 2 per CU (LDS), and at most
 	 * 2^22 tuples per workgroup (packed-counter exactness) */
@@ -3451,9 +3578,10 @@ static hipError_t launch_classify(const cgpu_snapshot &s0, cls_args a, hipStream
 
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &x, hipStream_t st)
 {
-	return launch_classify<0>(s, cls_args{x.saddr, x.daddr, x.dport, x.proto, x.flags, x.len, x.ep,
-					      x.verdict, x.identity, x.stage, x.delta, x.n, x.pk, x.lb, x.sport,
-					      x.hash}, st);
+	cls_args c{x.saddr, x.daddr, x.dport, x.proto, x.flags, x.len, x.ep, x.verdict, x.identity,
+		   x.stage, x.delta, x.n, x.pk, x.lb, x.sport, x.hash};
+	c.xdp = x.lb ? x.xdp : 0;
+	return launch_classify<0>(s, c, st);
 }
 
 hipError_t launch_classify_v6(const cgpu_snapshot &s, const classify_v6_args &x, hipStream_t st)

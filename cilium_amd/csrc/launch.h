@@ -26,6 +26,8 @@ struct classify_v4_args {
 	int lb;
 	const uint16_t *sport;
 	const uint32_t *hash; /* NULL: flow_hash(saddr, daddr, sport, dport, proto) */
+	/* with lb: the XDP prefilter before every ingress tuple (cgpu_classify_v4_cascade) */
+	int xdp;
 };
 
 hipError_t launch_classify_v4(const cgpu_snapshot &s, const classify_v4_args &a, hipStream_t st);

@@ -437,12 +437,26 @@ typedef struct cover6 {
 	uint32_t m64;
 } cover6;
 
+/* ---- IPv4 any-match /16 nodes (the XDP deny set, cgpu_classify_v4_cascade) ----
+ * pf4x[2 p], pf4x[2 p + 1]: the /16 p as the addresses x (its low 16 bits)
+ * where coverage changes, b_1 < .. < b_k in [1, 0xFFFF], stored as b_i - 1
+ * (u16, pad 0xFFFF): x is covered iff flip + #{i : b_i - 1 < x} is odd.
+ *   u16 0 of the first uint4: header (PF4X_OVF: more than 15 boundaries,
+ *         look the address up in pf4c; PF4X_TWO: slots 7..14 are used;
+ *         bit 0: flip = coverage at x = 0)
+ *   u16 1..7: slots 0..6;  the second uint4: slots 7..14.
+ * A lookup is one 16-byte gather for a /16 of <= 7 boundaries (three /32s),
+ * a second in the same line for <= 15. */
+#define PF4X_OVF 0x8000u
+#define PF4X_TWO 0x4000u
+
 /* ---- one committed snapshot ---- */
 typedef struct cgpu_snapshot {
 	lpm16c ipc4c;    /* ipcache, IPv4 lookups (compiled from a host DIR-24-8) */
 	pol_table pol;   /* every policy key (probe 1 / 3 gathers) */
 	pol_groups pg;   /* per (ep, identity, dir): probe 2 + probe 1 filter */
 	lpm16c pf4c;     /* any-match: dyn4 (if enabled) + fix4 /32; leaves 0 / 1 */
+	const uint4 *pf4x; /* the same set as one 32-byte boundary node per /16 (PF4X_*), or NULL */
 	addr_set4 ep4;   /* cilium_lxc IPv4 keys */
 	addr_set16 ep6;  /* cilium_lxc IPv6 keys (bucket: pfx6_hash(raw words, 0)) */
 	/* bloom filter over ep6 keys (v6_bloom_word / v6_bloom_bits of the same

@@ -546,9 +546,12 @@ class Engine:
                                            C.byref(ov), _stream(stream)), "cgpu_classify_v6_ctlb")
         return out
 
-    def classify_v4_lb(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+    def classify_v4_lb(self, t: dict, out: dict | None = None, stage: bool = True, stream=None,
+                       xdp: bool = False):
         """classify_v4 with the egress service step first (BASELINE config 5).
-        t additionally holds "hash" (int32 view of skb->hash) or "sport"."""
+        t additionally holds "hash" (int32 view of skb->hash) or "sport".
+        xdp=True: cgpu_classify_v4_cascade, the netdev's XDP prefilter before
+        every ingress tuple too (the full config-5 cascade)."""
         import torch
         n = t["saddr"].numel()
         dev = t["saddr"].device
@@ -558,11 +561,17 @@ class Engine:
                    "stage": torch.empty(n, dtype=torch.uint8, device=dev) if stage else None}
         tv = TuplesV4(*[t[k].data_ptr() for k in
                         ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")])
-        check(self.L.cgpu_classify_v4_lb(self.h, C.byref(tv), _ptr(t.get("sport")),
-                                         _ptr(t.get("hash")), n, _ptr(out["verdict"]),
-                                         _ptr(out["identity"]), _ptr(out.get("stage")),
-                                         _stream(stream)), "cgpu_classify_v4_lb")
+        fn = "cgpu_classify_v4_cascade" if xdp else "cgpu_classify_v4_lb"
+        check(getattr(self.L, fn)(self.h, C.byref(tv), _ptr(t.get("sport")), _ptr(t.get("hash")), n,
+                                  _ptr(out["verdict"]), _ptr(out["identity"]), _ptr(out.get("stage")),
+                                  _stream(stream)), fn)
         return out
+
+    def classify_v4_cascade(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """BASELINE config 5 whole (cgpu_classify_v4_cascade): XDP prefilter
+        -> ipcache -> policy for ingress tuples, service step -> ipcache ->
+        policy for egress ones."""
+        return self.classify_v4_lb(t, out=out, stage=stage, stream=stream, xdp=True)
 
     def lb4_select(self, t: dict, mode: int, out: dict | None = None, stream=None):
         """Service translation alone: t holds saddr/daddr (int32 views),

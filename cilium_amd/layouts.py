@@ -66,6 +66,11 @@ DROP_POLICY = -133
 DROP_CT_UNKNOWN_PROTO = -137
 DROP_FRAG_NOSUPPORT = -157
 XDP_DROP, XDP_PASS = 1, 2
+# cgpu_classify_v4_cascade (config 5 whole): an ingress tuple the netdev's XDP
+# prefilter dropped (bpf_xdp.c:97-121) -- the engine's own code, like
+# DROP_SNAPLEN: the XDP program returns XDP_DROP and records no drop reason
+VERDICT_XDP_DROP = -4097
+STAGE_XDP_DROP = 8
 METRIC_INGRESS, METRIC_EGRESS = 1, 2
 # CT direction (bpf/lib/common.h:327-328); policy_key.egress = !dir
 CT_EGRESS, CT_INGRESS = 0, 1

@@ -308,6 +308,113 @@ def load_services(target, svcs: Services):
     assert rc == 0, rc
 
 
+# ---------------------------------------------------------------------------
+# config 5's first stage (BASELINE "prefilter -> ipcache -> policy -> LB"):
+# the netdev's XDP CIDR prefilter (bpf_xdp.c check_v4) over an IPv4 deny set
+# -- dyn4 LPM prefixes /16../28 (pkg/policy/prefilter.go maxLKeys 64k: 16k
+# here) and fix4 /32s (maxHKeys 20M: 200k here), 5 % of each drawn inside
+# installed ipcache prefixes (part of a remote identity's range denied), the
+# rest uniform -- and the node's local endpoints in cilium_lxc (one IPv4 address
+# per endpoint id, in the cluster range 10.0.0.0/8), which check_v4_endpoint
+# requires of every ingress daddr.
+# ---------------------------------------------------------------------------
+@dataclass
+class Prefilter4:
+    dyn4: np.ndarray     # LPM_V4_KEY
+    fix4: np.ndarray     # LPM_V4_KEY, prefixlen 32
+    ep_addr: np.ndarray  # network-order u32 per endpoint id
+    ep_keys: np.ndarray  # ENDPOINT_KEY (cilium_lxc)
+
+
+def _lpm4_keys(addr_host, plen):
+    k = np.zeros(len(addr_host), L.LPM_V4_KEY)
+    k["prefixlen"] = plen
+    k["addr"] = addr_host.astype(">u4").view(np.uint8).reshape(-1, 4)
+    return k
+
+
+def make_prefilter4(tables: Tables, n_dyn=16_000, n_fix=200_000, seed=SEED) -> Prefilter4:
+    rng = np.random.Generator(np.random.PCG64(seed + 0x9F4))
+    npfx = len(tables.pfx_addr)
+
+    def draw(n, lens):
+        # a deny prefix inside an installed ipcache prefix is no wider than
+        # it (lens raised in place), so it blocks part of one identity's range
+        inside = rng.random(n) < 0.05
+        pi = rng.integers(0, npfx, n)
+        ln = tables.pfx_len[pi].astype(np.uint64)
+        hmask = (np.uint64(1) << (np.uint64(32) - ln)) - np.uint64(1)
+        a = np.where(inside, tables.pfx_addr[pi].astype(np.uint64) |
+                     (rng.integers(0, 2**32, n, dtype=np.uint64) & hmask),
+                     rng.integers(0, 2**32, n, dtype=np.uint64))
+        lens[:] = np.where(inside, np.maximum(lens, ln.astype(lens.dtype)), lens)
+        m = ((np.uint64(0xFFFFFFFF) << (np.uint64(32) - lens.astype(np.uint64))) & np.uint64(0xFFFFFFFF))
+        return (a & m).astype(np.uint32)
+
+    # keep the cluster /8 (the endpoints' range) out of the deny set
+    lens = rng.choice(np.array([16, 20, 24, 28]), int(n_dyn * 1.2) + 16, p=[0.05, 0.15, 0.6, 0.2])
+    da = draw(len(lens), lens)
+    ok = (da >> 24) != (CLUSTER_V4 >> 24)
+    key = (lens.astype(np.uint64) << np.uint64(32)) | da.astype(np.uint64)
+    _, first = np.unique(key, return_index=True)
+    first = np.sort(first[ok[first]])[:n_dyn]
+    dyn = _lpm4_keys(da[first], lens[first])
+    fa = draw(int(n_fix * 1.2) + 16, np.full(int(n_fix * 1.2) + 16, 32))
+    fa = fa[(fa >> 24) != (CLUSTER_V4 >> 24)]
+    _, first = np.unique(fa, return_index=True)
+    fa = fa[np.sort(first)][:n_fix]
+    fix = _lpm4_keys(fa, 32)
+    ep_host = (CLUSTER_V4 | (0x42 << 16) | (np.arange(max(tables.n_endpoints, 1)) + 2)).astype(np.uint32)
+    ep_keys = np.zeros(len(ep_host), L.ENDPOINT_KEY)
+    ep_keys["ip"][:, :4] = ep_host.astype(">u4").view(np.uint8).reshape(-1, 4)
+    ep_keys["family"] = L.ENDPOINT_KEY_IPV4
+    return Prefilter4(dyn, fix, ep_host.byteswap(), ep_keys)
+
+
+def add_prefilter_traffic(t: dict, P: Prefilter4, seed=SEED, gpu_id: int = 0, deny_frac=0.05,
+                          stray_frac=0.01):
+    """Ingress tuples as the netdev hands them to XDP: daddr = the address
+    of the endpoint whose policy map (ep) classifies them, except
+    `stray_frac` aimed at no local endpoint (check_v4_endpoint drops them);
+    `deny_frac` of them come from a deny-set address (half a dyn4 prefix,
+    half a fix4 /32).  Egress tuples are left as they are."""
+    rng = np.random.Generator(np.random.PCG64(seed + 0xD4 + gpu_id))
+    n = len(t["saddr"])
+    t = dict(t)
+    ing = (t["flags"] & 1) == 0
+    stray = rng.random(n) < stray_frac
+    t["daddr"] = np.where(ing & ~stray, P.ep_addr[t["ep"] % len(P.ep_addr)], t["daddr"]).astype(np.uint32)
+    deny = ing & (rng.random(n) < deny_frac)
+    use_dyn = rng.random(n) < 0.5
+    di = rng.integers(0, len(P.dyn4), n)
+    dbase = P.dyn4["addr"][di].copy().view(">u4").ravel().astype(np.uint64)
+    dlen = P.dyn4["prefixlen"][di].astype(np.uint64)
+    dhost = rng.integers(0, 2**32, n, dtype=np.uint64) & ((np.uint64(1) << (np.uint64(32) - dlen)) - np.uint64(1))
+    fi = rng.integers(0, len(P.fix4), n)
+    fbase = P.fix4["addr"][fi].copy().view(">u4").ravel().astype(np.uint64)
+    src = np.where(use_dyn, dbase | dhost, fbase).astype(np.uint32).byteswap()
+    t["saddr"] = np.where(deny, src, t["saddr"]).astype(np.uint32)
+    if "hash" in t:
+        from .shard import flowhash_np
+        t["hash"] = flowhash_np(t["saddr"], t["daddr"], t["sport"], t["dport"], t["proto"])
+    return t
+
+
+def load_prefilter4(target, P: Prefilter4):
+    """Engine or Oracle: dyn4 / fix4 CIDR maps (pkg/maps/cidrmap) + cilium_lxc."""
+    for which, keys in ((0, P.dyn4), (1, P.fix4)):
+        if hasattr(target, "cidr_update_batch"):
+            rc = target.cidr_update_batch(which, keys)
+            assert rc == 0, rc
+            continue
+        for k in keys:
+            rc = target.cidr_update(which, k)
+            assert rc == 0, rc
+    for k in P.ep_keys:
+        rc = target.endpoint_update(k)
+        assert rc == 0, rc
+
+
 def make_services6(tables, n_services: int, seed=SEED, max_backends=16, p=0.3, l3_frac=0.1):
     """make_services for cilium_lb6_services: VIPs in fd00:96::/32, backend
     targets inside the installed IPv6 ipcache prefixes (tables: Tables6).

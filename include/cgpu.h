@@ -512,6 +512,27 @@ int cgpu_classify_v4_lb(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, const uint16_t *
 			uint8_t *stage, void *stream);
 
 /*
+ * BASELINE config 5 whole ("prefilter -> ipcache identity -> policy verdict ->
+ * LB"): cgpu_classify_v4_lb with the netdev's XDP prefilter in front of every
+ * INGRESS tuple, as a packet meets xdp_start -> check_filters -> check_v4
+ * (bpf_xdp.c:97-121, :158-184) before from_netdev (bpf_netdev.c:470):
+ *   saddr in the dyn4 LPM (CIDR4_LPM_PREFILTER) or a fix4 /32 (CIDR4_FILTER;
+ *   both per cgpu_config.prefilter_*) -> XDP_DROP; else daddr must be a key
+ *   of the endpoint map (check_v4_endpoint :88-95) -> XDP_PASS, else XDP_DROP.
+ * An XDP_DROP ends the tuple: verdict CGPU_VERDICT_XDP_DROP, identity 0,
+ * stage 8, no policy counters and no metrics (the XDP program notifies
+ * nothing).  A passed ingress tuple and every egress tuple are classified
+ * exactly as cgpu_classify_v4_lb (egress: lb4_local, then ipcache / policy).
+ * Replaces, for a pre-parsed batch, the XDP program + bpf_netdev.c +
+ * bpf_lxc.c sequence the kernel runs per packet.
+ */
+#define CGPU_VERDICT_XDP_DROP (-4097)
+#define CGPU_STAGE_XDP_DROP 8
+int cgpu_classify_v4_cascade(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, const uint16_t *sport,
+			     const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+			     uint8_t *stage, void *stream);
+
+/*
  * cgpu_classify_v6 with the egress service step of ipv6_l3_from_lxc in front
  * (bpf_lxc.c:108-139): lb6_extract_key, lb6_lookup_service and lb6_local
  * (lb.h:334-483) with an empty conntrack table (CT_NEW); ipcache then

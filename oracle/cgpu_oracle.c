@@ -1136,6 +1136,63 @@ int or_lb4(or_ctx *c, int mode, size_t n, const uint32_t *saddr, const uint32_t 
 	return 0;
 }
 
+/* check_filters of one pre-parsed packet (bpf_xdp.c:158-178): flags 2 = not
+ * IP (XDP_PASS), 1 = truncated (xdp_no_room, XDP_DROP); else check_v4 /
+ * check_v6 (:97-121, :132-156): with CIDR{4,6}_FILTER the dyn LPM (when
+ * CIDR{4,6}_LPM_PREFILTER) then the fix hash on saddr, then
+ * check_v{4,6}_endpoint (:88-95, :123-130) on daddr.  Counts its lookups. */
+static uint8_t pf_one(const or_ctx *c, int v6, uint8_t f, uint32_t s4, uint32_t d4, const uint8_t *s6,
+		      const uint8_t *d6, uint64_t *probes)
+{
+	const or_config *cfg = &c->cfg;
+	uint8_t pfx[20], ek[20], v;
+	int fix = v6 ? cfg->fix6 : cfg->fix4, dyn = v6 ? cfg->dyn6 : cfg->dyn4;
+	if (f == 2)
+		return XDP_PASS;
+	if (f == 1)
+		return XDP_DROP;
+	memset(pfx, 0, sizeof(pfx));
+	memset(ek, 0, sizeof(ek));
+	if (!v6) {
+		uint32_t plen = 32;
+		memcpy(pfx, &plen, 4);
+		memcpy(pfx + 4, &s4, 4);
+		memcpy(ek, &d4, 4);
+		ek[16] = 1; /* ENDPOINT_KEY_IPV4 */
+	} else {
+		uint32_t plen = 128;
+		memcpy(pfx, &plen, 4);
+		memcpy(pfx + 4, s6, 16);
+		memcpy(ek, d6, 16);
+		ek[16] = 2; /* ENDPOINT_KEY_IPV6 */
+	}
+	v = 0;
+	if (fix) { /* CIDR{4,6}_FILTER */
+		if (dyn) { /* CIDR{4,6}_LPM_PREFILTER */
+			(*probes)++;
+			tl_cls[OR_CLS_PREFILTER]++;
+			const struct fast_lpm *fp = v6 ? c->fpf6 : c->fpf4;
+			uint32_t a4;
+			memcpy(&a4, pfx + 4, 4);
+			if (fp ? (v6 ? fl_lookup6(fp, pfx + 4) : fl_lookup4(fp, a4)) != NULL
+			       : lpm_lookup(v6 ? &c->dyn6 : &c->dyn4, pfx) != NULL)
+				v = XDP_DROP;
+		}
+		if (!v) {
+			(*probes)++;
+			tl_cls[OR_CLS_PREFILTER]++;
+			if (oh_get(v6 ? &c->fix6 : &c->fix4, pfx))
+				v = XDP_DROP;
+		}
+	}
+	if (!v) {
+		(*probes)++;
+		tl_cls[OR_CLS_ENDPOINT]++;
+		v = oh_get(&c->lxc, ek) ? XDP_PASS : XDP_DROP;
+	}
+	return v;
+}
+
 struct cls_job {
 	or_ctx *c;
 	size_t lo, hi;
@@ -1143,6 +1200,7 @@ struct cls_job {
 	const uint16_t *dport, *ep;
 	const uint8_t *proto, *flags;
 	int lb;                  /* egress service step first (or_classify_v4_lb) */
+	int xdp;                 /* XDP prefilter before every ingress tuple (or_classify_v4_cascade) */
 	const uint16_t *sport;
 	const uint32_t *hash;
 	int32_t *verdict;
@@ -1169,6 +1227,17 @@ static void *cls_worker(void *arg)
 		uint16_t dport = j->dport[i];
 		int lbdrop = 0;
 
+		if (j->xdp && !egress &&
+		    pf_one(c, 0, 0, j->saddr[i], daddr, NULL, NULL, &j->probes) == XDP_DROP) {
+			/* the netdev's XDP program dropped it: from_netdev never runs,
+			 * nothing is counted or notified (bpf_xdp.c:180-184) */
+			j->verdict[i] = OR_VERDICT_XDP_DROP;
+			if (j->identity)
+				j->identity[i] = 0;
+			if (j->stage)
+				j->stage[i] = 8;
+			continue;
+		}
 		if (j->lb && egress) {
 			/* service translation before conntrack and policy
 			 * (bpf_lxc.c:444-469): ipcache resolves tuple.daddr
@@ -1265,7 +1334,7 @@ static int classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_
 		       const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
 		       const uint32_t *len, const uint16_t *ep, int32_t *verdict,
 		       uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum,
-		       int lb, const uint16_t *sport, const uint32_t *hash)
+		       int lb, const uint16_t *sport, const uint32_t *hash, int xdp)
 {
 	struct cls_job *jobs;
 	pthread_t *th;
@@ -1292,6 +1361,7 @@ static int classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_
 		j->identity = identity;
 		j->stage = stage;
 		j->lb = lb;
+		j->xdp = xdp;
 		j->sport = sport;
 		j->hash = hash;
 		if (nthreads == 1)
@@ -1320,7 +1390,7 @@ int or_classify_v4(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *d
 		   uint32_t *identity, uint8_t *stage, int nthreads, uint64_t *probe_sum)
 {
 	return classify_v4(c, n, saddr, daddr, dport, proto, flags, len, ep, verdict, identity,
-			   stage, nthreads, probe_sum, 0, NULL, NULL);
+			   stage, nthreads, probe_sum, 0, NULL, NULL, 0);
 }
 
 int or_classify_v4_lb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
@@ -1332,7 +1402,19 @@ int or_classify_v4_lb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 	if (!hash && !sport && n)
 		return -EINVAL;
 	return classify_v4(c, n, saddr, daddr, dport, proto, flags, len, ep, verdict, identity,
-			   stage, nthreads, probe_sum, 1, sport, hash);
+			   stage, nthreads, probe_sum, 1, sport, hash, 0);
+}
+
+int or_classify_v4_cascade(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+			   const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+			   const uint8_t *flags, const uint32_t *len, const uint16_t *ep,
+			   const uint32_t *hash, int32_t *verdict, uint32_t *identity, uint8_t *stage,
+			   int nthreads, uint64_t *probe_sum)
+{
+	if (!hash && !sport && n)
+		return -EINVAL;
+	return classify_v4(c, n, saddr, daddr, dport, proto, flags, len, ep, verdict, identity,
+			   stage, nthreads, probe_sum, 1, sport, hash, 1);
 }
 
 struct cls6_job {
@@ -1539,61 +1621,9 @@ struct pf_job {
 static void *pf_worker(void *arg)
 {
 	struct pf_job *j = arg;
-	const or_ctx *c = j->c;
-	const or_config *cfg = &c->cfg;
-	for (size_t i = j->lo; i < j->hi; i++) {
-		uint8_t f = j->flags[i], v;
-		uint8_t pfx[20], ek[20];
-		int fix = j->v6 ? cfg->fix6 : cfg->fix4, dyn = j->v6 ? cfg->dyn6 : cfg->dyn4;
-		if (f == 2) { /* check_filters: other ethertypes pass (bpf_xdp.c:173-177) */
-			j->verdict[i] = XDP_PASS;
-			continue;
-		}
-		if (f == 1) { /* xdp_no_room (bpf_xdp.c:104-105, :139-140, :165-166) */
-			j->verdict[i] = XDP_DROP;
-			continue;
-		}
-		memset(pfx, 0, sizeof(pfx));
-		memset(ek, 0, sizeof(ek));
-		if (!j->v6) {
-			uint32_t plen = 32;
-			memcpy(pfx, &plen, 4);
-			memcpy(pfx + 4, &j->s4[i], 4);
-			memcpy(ek, &j->d4[i], 4);
-			ek[16] = 1; /* ENDPOINT_KEY_IPV4 */
-		} else {
-			uint32_t plen = 128;
-			memcpy(pfx, &plen, 4);
-			memcpy(pfx + 4, j->s6 + 16 * i, 16);
-			memcpy(ek, j->d6 + 16 * i, 16);
-			ek[16] = 2; /* ENDPOINT_KEY_IPV6 */
-		}
-		v = 0;
-		if (fix) { /* CIDR{4,6}_FILTER */
-			if (dyn) { /* CIDR{4,6}_LPM_PREFILTER */
-				j->probes++;
-				tl_cls[OR_CLS_PREFILTER]++;
-				const struct fast_lpm *fp = j->v6 ? c->fpf6 : c->fpf4;
-				uint32_t a4;
-				memcpy(&a4, pfx + 4, 4);
-				if (fp ? (j->v6 ? fl_lookup6(fp, pfx + 4) : fl_lookup4(fp, a4)) != NULL
-				       : lpm_lookup(j->v6 ? &c->dyn6 : &c->dyn4, pfx) != NULL)
-					v = XDP_DROP;
-			}
-			if (!v) {
-				j->probes++;
-				tl_cls[OR_CLS_PREFILTER]++;
-				if (oh_get(j->v6 ? &c->fix6 : &c->fix4, pfx))
-					v = XDP_DROP;
-			}
-		}
-		if (!v) { /* check_v{4,6}_endpoint (bpf_xdp.c:88-95, :123-130) */
-			j->probes++;
-			tl_cls[OR_CLS_ENDPOINT]++;
-			v = oh_get(&c->lxc, ek) ? XDP_PASS : XDP_DROP;
-		}
-		j->verdict[i] = v;
-	}
+	for (size_t i = j->lo; i < j->hi; i++)
+		j->verdict[i] = j->v6 ? pf_one(j->c, 1, j->flags[i], 0, 0, j->s6 + 16 * i, j->d6 + 16 * i, &j->probes)
+				      : pf_one(j->c, 0, j->flags[i], j->s4[i], j->d4[i], NULL, NULL, &j->probes);
 	cls_flush((or_ctx *)j->c);
 	return NULL;
 }

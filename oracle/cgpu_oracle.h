@@ -161,6 +161,24 @@ int or_classify_v4_lb(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t
 		      int nthreads, uint64_t *probe_sum);
 
 /*
+ * BASELINE config 5, the full cascade: or_classify_v4_lb with the XDP
+ * prefilter of the netdev in front of every INGRESS tuple (bpf_xdp.c:97-121,
+ * xdp_start -> check_filters -> check_v4: saddr in the dyn LPM or the fix
+ * /32 hash -> XDP_DROP, else daddr must be a local endpoint,
+ * check_v4_endpoint :88-95).  An XDP_DROP ends the tuple before
+ * from_netdev (bpf_netdev.c:470) ever sees it: verdict OR_VERDICT_XDP_DROP,
+ * identity 0, stage 8, no counters and no metrics (bpf_xdp.c notifies
+ * nothing).  Egress tuples take the service step as or_classify_v4_lb.
+ * *probe_sum adds the prefilter and endpoint lookups.
+ */
+#define OR_VERDICT_XDP_DROP (-4097)
+int or_classify_v4_cascade(or_ctx *c, size_t n, const uint32_t *saddr, const uint32_t *daddr,
+			   const uint16_t *sport, const uint16_t *dport, const uint8_t *proto,
+			   const uint8_t *flags, const uint32_t *len, const uint16_t *ep,
+			   const uint32_t *hash, int32_t *verdict, uint32_t *identity, uint8_t *stage,
+			   int nthreads, uint64_t *probe_sum);
+
+/*
  * Raw Ethernet frames.  Per-endpoint identity of the
  * endpoint program (lxc_config.h LXC_MAC / LXC_IPV4 / LXC_IP and which of
  * the SMAC / DMAC / SIP checks are compiled in), 32 bytes in the layout of

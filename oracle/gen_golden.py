@@ -819,6 +819,142 @@ def gen_classify_lb_fixture(pol, lbls, rng):
                 **{"t_" + k: v for k, v in t.items()}, **out)
 
 
+def gen_cascade_fixture(pol, xdp, lbls, rng):
+    """BASELINE config 5 whole, composed from the reference's own programs in
+    the order a packet meets them: an INGRESS packet first runs the netdev's
+    XDP program (libref_xdp = bpf_xdp.c xdp_start, :180-184, over a frame
+    built from the tuple: check_v4's dyn LPM / fix hash on saddr, then
+    check_v4_endpoint on daddr); XDP_DROP ends it (no counter, no metric:
+    the XDP program notifies nothing), XDP_PASS hands it to the ingress
+    identity + policy (libref_policy ref_classify_v4 = bpf_netdev.c +
+    ipv4_policy).  An EGRESS packet takes the service step (libref_lbl)
+    then ipcache / policy, as classify_v4_lb.npz."""
+    base = gen_classify_fixture(pol, rng)
+    ikeys, ivals = base["ipc_keys"], base["ipc_vals"]
+    pk, pe, pep = base["pol_keys"], base["pol_entries"], base["pol_ep"]
+    v4 = ikeys["prefixlen"] >= 32
+    pfx = ikeys[v4]["ip"][:, :4].copy().view("<u4").ravel()
+    targets = pfx[rng.integers(0, len(pfx), 200)]
+    clients = rng.integers(0, 2**32, 4, dtype=np.uint64).astype(np.uint32)
+    keys, vals, vips = gen_lb_services(rng, 60, targets, clients)
+    # the deny set: dyn4 prefixes of every length class, fix4 /32s (and a few
+    # prefixlen-24 hash keys, which a /32 lookup key never matches), many of
+    # them over installed ipcache ranges; the local endpoints (a few keys
+    # with a nonzero pad, which no lookup key matches)
+    dyn4, fix4, eps = [], [], []
+    a4, l4 = rand_v4_prefixes(rng, 120, [8, 12, 16, 20, 24, 28, 31, 32], [1, 2, 4, 5, 10, 3, 1, 2])
+    for i, (a, ln) in enumerate(zip(a4, l4)):
+        if i % 3 == 0:
+            a = int(pfx[rng.integers(0, len(pfx))].byteswap())
+        k = np.zeros((), L.LPM_V4_KEY)
+        k["prefixlen"] = ln
+        m = (0xFFFFFFFF << (32 - int(ln))) & 0xFFFFFFFF
+        k["addr"][:] = np.frombuffer((int(a) & m).to_bytes(4, "big"), np.uint8)
+        dyn4.append(k)
+    a4f, _ = rand_v4_prefixes(rng, 150, [32], [1])
+    for i, a in enumerate(a4f):
+        if i % 2 == 0:
+            a = int(pfx[rng.integers(0, len(pfx))].byteswap()) ^ int(rng.integers(0, 256))
+        k = np.zeros((), L.LPM_V4_KEY)
+        k["prefixlen"] = 32 if i % 25 else 24
+        k["addr"][:] = np.frombuffer(int(a).to_bytes(4, "big"), np.uint8)
+        fix4.append(k)
+    ep4 = rng.integers(0, 2**32, 24, dtype=np.uint64).astype(np.uint32)
+    for i in range(24):
+        k = np.zeros((), L.ENDPOINT_KEY)
+        k["ip"][:4] = np.frombuffer(int(ep4[i]).to_bytes(4, "little"), np.uint8)
+        k["family"] = L.ENDPOINT_KEY_IPV4
+        if i % 12 == 11:
+            k["pad4"] = 1
+        eps.append(k)
+    dyn4, fix4, eps = (np.array(dyn4, L.LPM_V4_KEY), np.array(fix4, L.LPM_V4_KEY),
+                       np.array(eps, L.ENDPOINT_KEY))
+    xdp.ref_xdp_reset()
+    for w, arr in ((0, dyn4), (1, fix4)):
+        for k in arr:
+            xdp.ref_xdp_cidr_update(w, b(k))
+    for k in eps:
+        xdp.ref_xdp_endpoint_update(b(k))
+    n = 6000
+    lt = lb_tuples(rng, n, keys, vips, clients)
+    eg = (rng.random(n) < 0.5).astype(np.uint8)
+    # ingress: daddr a local endpoint (or a stray address); saddr from the
+    # deny set (inside a dyn prefix, on or next to a fix /32) or anywhere
+    daddr = np.where(rng.random(n) < 0.8, ep4[rng.integers(0, 24, n)],
+                     rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)).astype(np.uint32)
+    dsrc = []
+    for i in range(n):
+        r = rng.random()
+        if r < 0.2:
+            k = dyn4[rng.integers(0, len(dyn4))]
+            base_ = int.from_bytes(bytes(k["addr"]), "big")
+            host = int(rng.integers(0, 2**32)) & ((1 << (32 - int(k["prefixlen"]))) - 1)
+            dsrc.append(L.ip4_be(base_ | host))
+        elif r < 0.35:
+            base_ = int.from_bytes(bytes(fix4[rng.integers(0, len(fix4))]["addr"]), "big")
+            dsrc.append(L.ip4_be(base_ ^ (int(rng.integers(0, 4)) if rng.random() < 0.3 else 0)))
+        else:
+            dsrc.append(int(lt["saddr"][i]))
+    dsrc = np.array(dsrc, np.uint32)
+    t = {"saddr": np.where(eg == 1, lt["saddr"], dsrc).astype(np.uint32),
+         "daddr": np.where(eg == 1, lt["daddr"], daddr).astype(np.uint32),
+         "sport": lt["sport"], "dport": lt["dport"], "proto": lt["proto"], "hash": lt["hash"],
+         "flags": (eg | (((rng.random(n) < 0.05) & (eg == 0)).astype(np.uint8) << 1)).astype(np.uint8),
+         "len": rng.integers(0, 70000, n).astype(np.uint32),
+         "ep": rng.integers(0, 5, n).astype(np.uint16), "opts": lt["opts"]}
+    xv = np.zeros(n, np.uint8)
+    xp = np.zeros(n, np.uint64)
+    pc = C.c_uint64()
+    for i in range(n):
+        if eg[i]:
+            continue
+        fr = eth(0x0800, ip4hdr(t["saddr"][i], t["daddr"][i]))
+        xv[i] = xdp.ref_xdp_run(fr, len(fr), C.byref(pc))
+        xp[i] = pc.value
+    out = {"xdp_verdict": xv, "xdp_probes": xp}
+    idv, st, npb, na = C.c_uint32(), C.c_int(), C.c_int(), C.c_int()
+    for ci, (gate, src, sw) in enumerate(CONFIGS[:2]):
+        lx = run_lb_lxc(lbls[gate], keys, vals, t)
+        pol.ref_reset()
+        for k, v in zip(ikeys, ivals):
+            pol.ref_ipcache_update(b(k), b(v))
+        for k, e, ep in zip(pk, pe, pep):
+            pol.ref_policy_update(int(ep), b(k), b(e))
+        verdict = np.empty(n, np.int32)
+        ident = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        nprobes = np.empty(n, np.int64)
+        for i in range(n):
+            if not eg[i] and xv[i] == L.XDP_DROP:
+                verdict[i], ident[i], stage[i], nprobes[i] = L.VERDICT_XDP_DROP, 0, L.STAGE_XDP_DROP, xp[i]
+                continue
+            if eg[i] and lx["ret"][i] < 0:
+                verdict[i], ident[i], stage[i], nprobes[i] = lx["ret"][i], 0, 6, lx["lookups"][i]
+                pol.ref_metrics_packet(int(lx["ret"][i]), int(t["len"][i]), 1)
+                continue
+            da = int(lx["tdaddr"][i]) if eg[i] else int(t["daddr"][i])
+            dp = int(lx["dport"][i]) if eg[i] else int(t["dport"][i])
+            verdict[i] = pol.ref_classify_v4(
+                int(t["saddr"][i]), da, dp, int(t["proto"][i]), int(t["flags"][i]),
+                int(t["len"][i]), int(t["ep"][i]), gate, src, sw,
+                C.byref(idv), C.byref(st), C.byref(npb), C.byref(na))
+            ident[i], stage[i] = idv.value, st.value
+            nprobes[i] = npb.value + na.value + (int(lx["lookups"][i]) if eg[i] else int(xp[i]))
+        final = np.zeros(len(pk), L.POLICY_ENTRY)
+        for i, (k, ep) in enumerate(zip(pk, pep)):
+            buf = C.create_string_buffer(24)
+            assert pol.ref_policy_read(int(ep), b(k), buf) == 0
+            final[i] = np.frombuffer(buf.raw, L.POLICY_ENTRY)[0]
+        out[f"c{ci}_verdict"], out[f"c{ci}_identity"] = verdict, ident
+        out[f"c{ci}_stage"], out[f"c{ci}_nprobes"] = stage, nprobes
+        out[f"c{ci}_final_entries"] = final
+        out[f"c{ci}_metrics"] = ref_metrics(pol)
+    return dict(ipc_keys=ikeys, ipc_vals=ivals, pol_keys=pk, pol_entries=pe, pol_ep=pep,
+                lb_keys=keys, lb_vals=vals, dyn4=dyn4, fix4=fix4, endpoints=eps,
+                configs=np.array(CONFIGS[:2], np.int64),
+                **{"t_" + k: v for k, v in t.items()}, **out)
+
+
 # ------------------------------------------------ IPv6 service translation
 def load_ref_lbl6():
     libs = {}
@@ -1834,6 +1970,9 @@ def main():
     # the IPv6 stateful service step (lb6_local with CONNTRACK), its own stream
     rng_ctlb6 = np.random.Generator(np.random.PCG64(SEED + 0xCC))
     manifest["files"]["ctlb6.npz"] = save("ctlb6.npz", gen_ctlb6_fixture(load_ref_ctlb(), pol, rng_ctlb6))
+    # config 5 whole (the XDP prefilter in front of the ingress tuples), its own stream
+    rng_cas = np.random.Generator(np.random.PCG64(SEED + 0xCA))
+    manifest["files"]["cascade_v4.npz"] = save("cascade_v4.npz", gen_cascade_fixture(pol, xdp, lbls, rng_cas))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -70,6 +70,7 @@ def lib():
         L.or_lb4.argtypes = [vp, C.c_int, sz] + [vp] * 13 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_classify_v4_lb.argtypes = [vp, sz] + [vp] * 12 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_classify_v6_lb.argtypes = [vp, sz] + [vp] * 12 + [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_classify_v4_cascade.argtypes = [vp, sz] + [vp] * 12 + [C.c_int, C.POINTER(C.c_uint64)]
         L.or_lb6_update.argtypes = [vp, vp, vp]
         L.or_lb6_delete.argtypes = [vp, vp]
         L.or_flow_hash6.argtypes = [vp, vp, C.c_uint16, C.c_uint16, C.c_uint8]
@@ -292,6 +293,26 @@ class Oracle:
         h = None if t.get("hash") is None else np.ascontiguousarray(t["hash"], np.uint32)
         rc = self.L.or_classify_v4_lb(self.h, n, *[_p(a) for a in arrs], _p(h), _p(verdict),
                                       _p(identity), _p(stage), nthreads, C.byref(probes))
+        assert rc == 0, rc
+        return verdict, identity, stage, probes.value
+
+    def classify_v4_cascade(self, t, nthreads=1):
+        """BASELINE config 5 whole: the XDP prefilter (bpf_xdp.c check_v4)
+        before every ingress tuple, the service step before every egress one,
+        then ipcache -> policy (or_classify_v4_cascade).  An XDP drop: verdict
+        XDP_DROP_VERDICT, identity 0, stage 8, nothing counted."""
+        n = len(t["saddr"])
+        verdict = np.empty(n, np.int32)
+        identity = np.empty(n, np.uint32)
+        stage = np.empty(n, np.uint8)
+        probes = C.c_uint64(0)
+        arrs = [np.ascontiguousarray(t[k], dt) for k, dt in (
+            ("saddr", np.uint32), ("daddr", np.uint32), ("sport", np.uint16),
+            ("dport", np.uint16), ("proto", np.uint8), ("flags", np.uint8), ("len", np.uint32),
+            ("ep", np.uint16))]
+        h = None if t.get("hash") is None else np.ascontiguousarray(t["hash"], np.uint32)
+        rc = self.L.or_classify_v4_cascade(self.h, n, *[_p(a) for a in arrs], _p(h), _p(verdict),
+                                           _p(identity), _p(stage), nthreads, C.byref(probes))
         assert rc == 0, rc
         return verdict, identity, stage, probes.value
 

@@ -40,6 +40,7 @@ from cilium_amd import layouts as L
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "_ref", "libref_lxc.so")
 NETDEV = os.path.join(ROOT, "oracle", "_ref", "libref_netdev.so")
+XDP = os.path.join(ROOT, "oracle", "_ref", "libref_xdp.so")
 pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason="reference harness not built (oracle/_ref)")
 
 SECLABEL_BUILD = 2  # bpf/node_config.h
@@ -400,3 +401,69 @@ def test_compiled_endpoint_program_reproduces_frame_parse(golden):
     np.testing.assert_array_equal(port[nofrag], g["nover_dport"][nofrag])
     for i in np.flatnonzero(ok):
         assert addrs[i] == {g["nover_saddr"][i].tobytes(), g["nover_daddr"][i].tobytes()}, i
+
+
+def _xdp_frame(saddr, daddr):
+    """Ethernet + a 20-byte IPv4 header carrying the tuple's addresses
+    (network-order u32 as stored): what check_v4 reads."""
+    h = bytearray(20)
+    h[0], h[9] = 0x45, 6
+    h[12:16] = int(saddr).to_bytes(4, "little")
+    h[16:20] = int(daddr).to_bytes(4, "little")
+    return bytes(6) + bytes([2, 0, 0, 0, 0, 1]) + (0x0800).to_bytes(2, "big") + bytes(h)
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+def test_compiled_programs_reproduce_cascade(golden, cfg):
+    """tests/golden/cascade_v4.npz (BASELINE config 5 whole) replayed through
+    the reference's programs compiled whole, in the order a packet meets
+    them: an ingress packet through bpf_xdp.c (libref_xdp, xdp_start on its
+    frame) and, if XDP_PASS, bpf_netdev.c's identity into bpf_lxc.c's
+    ipv4_policy; an egress packet through bpf_lxc.c's handle_ipv4_from_lxc
+    (service step, ipcache, policy).  Verdict of every TCP / UDP / gated
+    packet and every XDP drop, identity and stage of every packet that
+    reached a policy probe."""
+    g = golden("cascade_v4.npz")
+    row = [int(x) for x in g["configs"][cfg]]
+    gate, src_cfg = row[0], row[1]
+    if not gate:
+        pytest.skip("the compiled endpoint program is the CONNTRACK build")
+    lib = _lib()
+    lib.ref_lxc_reset(1 << 20)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        lib.ref_lxc_ipcache_update(_b(k), _b(v))
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert lib.ref_lxc_policy_update(int(ep), _b(k), _b(e)) == 0
+    for k, v in zip(g["lb_keys"], g["lb_vals"]):
+        lib.ref_lxc_svc_update(_b(k), _b(v))
+    x = C.CDLL(XDP)
+    x.ref_xdp_reset.restype = None
+    x.ref_xdp_cidr_update.argtypes = [C.c_int, C.c_void_p]
+    x.ref_xdp_endpoint_update.argtypes = [C.c_void_p]
+    x.ref_xdp_run.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint64)]
+    x.ref_xdp_reset()
+    for w, name in ((0, "dyn4"), (1, "fix4")):
+        for k in g[name]:
+            assert x.ref_xdp_cidr_update(w, _b(k)) >= 0
+    for k in g["endpoints"]:
+        assert x.ref_xdp_endpoint_update(_b(k)) >= 0
+    nd = _Netdev(g["ipc_keys"], g["ipc_vals"])
+    t, got = _stateless_replay(g, row, False, lib, nd, src_cfg)
+    ing = (t["flags"] & 1) == 0
+    pc = C.c_uint64()
+    xv = np.zeros(len(ing), np.int64)
+    for i in np.flatnonzero(ing):
+        fr = _xdp_frame(t["saddr"][i], t["daddr"][i])
+        xv[i] = x.ref_xdp_run(fr, len(fr), C.byref(pc))
+    drop = ing & (xv == L.XDP_DROP)
+    got[drop] = L.VERDICT_XDP_DROP, 0, L.STAGE_XDP_DROP
+    want = g[f"c{cfg}_verdict"]
+    np.testing.assert_array_equal(drop, want == L.VERDICT_XDP_DROP)
+    icmp = t["proto"] == 1
+    gated = ~np.isin(t["proto"], [1, 6, 17])
+    keep = ~icmp | drop
+    assert drop.sum() > 500 and (ing & ~drop & keep).sum() > 500
+    np.testing.assert_array_equal(got[keep, 0], want[keep])
+    probed = keep & (g[f"c{cfg}_stage"] <= 3) & ~gated
+    np.testing.assert_array_equal(got[probed, 1], g[f"c{cfg}_identity"][probed])
+    np.testing.assert_array_equal(got[probed, 2], g[f"c{cfg}_stage"][probed])

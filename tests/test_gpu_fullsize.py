@@ -166,6 +166,49 @@ def test_config5_fullsize(torch_cuda):
     e.close()
 
 
+def test_config5_cascade_fullsize(torch_cuda):
+    """Config 5 as BASELINE names it, "prefilter -> ipcache identity ->
+    policy verdict -> LB": every ingress tuple first meets the netdev's XDP
+    prefilter (bpf_xdp.c:97-121 check_v4 over a 16k-prefix dyn4 LPM + 200k
+    fix4 /32s, then check_v4_endpoint on daddr), every egress tuple the
+    service step over 1M services; then ipcache -> policy
+    (cgpu_classify_v4_cascade).  Verdict, identity, stage, every entry's
+    counters and the metrics equal the restatement's composition
+    (or_classify_v4_cascade)."""
+    from oracle import Oracle
+    torch = torch_cuda
+    cfg = synth.CONFIGS["cascade"]
+    T = synth.make_tables(**cfg)
+    S = synth.make_services(T, cfg["n_services"])
+    P = synth.make_prefilter4(T)
+    t = synth.add_prefilter_traffic(synth.add_service_traffic(synth.make_tuples(T, N_SLICE), S), P)
+    del t["hash"]
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_services(o, S)
+    synth.load_prefilter4(o, P)
+    v0, i0, s0, _ = o.classify_v4_cascade(t, nthreads=16)
+    ing = (t["flags"] & 1) == 0
+    xd = v0 == L.VERDICT_XDP_DROP
+    assert xd.sum() > 0.03 * ing.sum() and not xd[~ing].any()
+    e = _engine(**T.engine_config(), lb_max_entries=len(S.keys))
+    synth.load_engine(e, T)
+    synth.load_services(e, S)
+    synth.load_prefilter4(e, P)
+    e.commit()
+    out = e.classify_v4_cascade(synth.to_device(t))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(out["verdict"]), v0)
+    np.testing.assert_array_equal(_np(out["identity"], np.uint32), i0)
+    np.testing.assert_array_equal(_np(out["stage"]), s0)
+    gp, gb = _entry_counters(e, T)
+    op, ob = _oracle_counters(o, T)
+    np.testing.assert_array_equal(gp, op)
+    np.testing.assert_array_equal(gb, ob)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    e.close()
+
+
 def test_config3_fullsize(torch_cuda):
     """Config 3: the XDP IPv6 prefilter over the 1M-prefix deny set (dyn6 +
     /128 fix6 under 256 /24 roots, bpf/bpf_xdp.c:132-156) and 4k endpoints,

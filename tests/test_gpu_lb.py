@@ -114,6 +114,81 @@ def test_classify_v4_lb_golden(torch_cuda, golden, ci):
     e.close()
 
 
+@pytest.mark.parametrize("variant", [0, 3, 8])
+@pytest.mark.parametrize("ci", range(2))
+def test_classify_v4_cascade_golden(torch_cuda, golden, ci, variant, monkeypatch):
+    """BASELINE config 5 whole (cgpu_classify_v4_cascade) against the
+    reference's XDP program + ingress decision and service step + egress
+    decision (tests/golden/cascade_v4.npz), on every classify schedule: the
+    x4 kernel's XDP stage and the per-lane kernels' must agree."""
+    torch = torch_cuda
+    monkeypatch.setitem(_DEFAULTS, "schedule", SCHED_OF[variant])
+    g = golden("cascade_v4.npz")
+    gate, src, sw = (int(x) for x in g["configs"][ci])
+    e = _engine(ct_proto_gate=gate, ingress_src_identity=src, ingress_secctx_world=sw)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert e.ipcache_update(k, v) == 0
+    for k, en, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert e.policy_update(int(ep), k, en) == 0
+    assert e.lb4_update_batch(g["lb_keys"], g["lb_vals"]) == 0
+    for w, name in ((0, "dyn4"), (1, "fix4")):
+        for k in g[name]:
+            assert e.cidr_update(w, k) == 0
+    for k in g["endpoints"]:
+        assert e.endpoint_update(k) == 0
+    e.commit()
+    t = {k[2:]: g[k] for k in g.files if k.startswith("t_") and k != "t_opts"}
+    out = e.classify_v4_cascade(synth.to_device(t))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["verdict"].cpu().numpy(), g[f"c{ci}_verdict"])
+    np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32),
+                                  g[f"c{ci}_identity"])
+    np.testing.assert_array_equal(out["stage"].cpu().numpy(), g[f"c{ci}_stage"])
+    for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
+        rc, got = e.policy_lookup(int(ep), k)
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+    np.testing.assert_array_equal(e.metrics(), g[f"c{ci}_metrics"])
+    e.close()
+
+
+@pytest.mark.parametrize("variant", [0, 3, 8])
+def test_classify_v4_cascade_scale_vs_oracle(torch_cuda, variant, monkeypatch):
+    """Config-1 tables + 50k services + the config-5 deny set (16k dyn4,
+    200k fix4) and endpoints, 1M tuples plus a ragged tail, every schedule,
+    against the restatement (or_classify_v4_cascade)."""
+    from oracle import Oracle
+    torch = torch_cuda
+    monkeypatch.setitem(_DEFAULTS, "schedule", SCHED_OF[variant])
+    T = synth.make_tables(**synth.CONFIGS["cpu"])
+    T.n_endpoints = 1
+    S = synth.make_services(T, 50_000)
+    P = synth.make_prefilter4(T)
+    t = synth.add_prefilter_traffic(synth.add_service_traffic(synth.make_tuples(T, (1 << 20) + 3), S), P)
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_services(o, S)
+    synth.load_prefilter4(o, P)
+    v0, i0, s0, _ = o.classify_v4_cascade(t, nthreads=8)
+    e = _engine(**T.engine_config(), lb_max_entries=len(S.keys))
+    synth.load_engine(e, T)
+    synth.load_services(e, S)
+    synth.load_prefilter4(e, P)
+    e.commit()
+    out = e.classify_v4_cascade(synth.to_device(t))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["verdict"].cpu().numpy(), v0)
+    np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
+    np.testing.assert_array_equal(out["stage"].cpu().numpy(), s0)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    for k, ep in zip(T.pol_keys[:4000], T.pol_ep[:4000]):
+        rc, got = e.policy_lookup(int(ep), k)
+        _, raw = o.policy_lookup(int(ep), k)
+        exp = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(exp["packets"]), int(exp["bytes"]))
+    assert (v0 == L.VERDICT_XDP_DROP).sum() > 10_000
+    e.close()
+
+
 @pytest.fixture(scope="module")
 def cfg_lb():
     T = synth.make_tables(**synth.CONFIGS["cpu"])

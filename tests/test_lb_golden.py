@@ -110,6 +110,56 @@ def test_classify_v4_lb_vs_reference(golden, ci):
     assert (st == 6).sum() > 0
 
 
+def _cascade_oracle(g, ci, **extra):
+    gate, src, sw = (int(x) for x in g["configs"][ci])
+    o = Oracle(ct_proto_gate=gate, ingress_src_identity=src, ingress_secctx_world=sw, **extra)
+    for k, v in zip(g["ipc_keys"], g["ipc_vals"]):
+        assert o.ipcache_update(k, v) == 0
+    for k, e, ep in zip(g["pol_keys"], g["pol_entries"], g["pol_ep"]):
+        assert o.policy_update(int(ep), k, e) == 0
+    for k, v in zip(g["lb_keys"], g["lb_vals"]):
+        assert o.lb_update(k, v) == 0
+    for w, name in ((0, "dyn4"), (1, "fix4")):
+        for k in g[name]:
+            assert o.cidr_update(w, k) == 0
+    for k in g["endpoints"]:
+        assert o.endpoint_update(k) == 0
+    return o
+
+
+@pytest.mark.parametrize("ci", range(2))
+def test_classify_v4_cascade_vs_reference(golden, ci):
+    """BASELINE config 5 whole: tests/golden/cascade_v4.npz composes the
+    reference's XDP program (libref_xdp: bpf_xdp.c check_v4 on the ingress
+    packets' frames) with its ingress decision (libref_policy) and, for
+    egress packets, its service step (libref_lbl) and egress decision.  The
+    restatement or_classify_v4_cascade reproduces every verdict (an XDP drop:
+    CGPU_VERDICT_XDP_DROP, stage 8), identity, stage, lookup count, counter
+    and metric."""
+    g = golden("cascade_v4.npz")
+    o = _cascade_oracle(g, ci)
+    t = _tuples(g)
+    v, idt, st, probes = o.classify_v4_cascade(t)
+    np.testing.assert_array_equal(v, g[f"c{ci}_verdict"])
+    np.testing.assert_array_equal(idt, g[f"c{ci}_identity"])
+    np.testing.assert_array_equal(st, g[f"c{ci}_stage"])
+    assert probes == int(g[f"c{ci}_nprobes"].sum())
+    for k, ep, fe in zip(g["pol_keys"], g["pol_ep"], g[f"c{ci}_final_entries"]):
+        rc, raw = o.policy_lookup(int(ep), k)
+        got = np.frombuffer(raw, L.POLICY_ENTRY)[0]
+        assert (int(got["packets"]), int(got["bytes"])) == (int(fe["packets"]), int(fe["bytes"]))
+    np.testing.assert_array_equal(o.metrics(), g[f"c{ci}_metrics"])
+    xd = v == L.VERDICT_XDP_DROP
+    ing = (t["flags"] & 1) == 0
+    # both XDP outcomes, both deny maps and the endpoint check all decide some packets
+    assert xd.sum() > 500 and (ing & ~xd).sum() > 500 and not xd[~ing].any()
+    assert set(np.unique(g["xdp_probes"][ing & xd]).tolist()) >= {1, 2, 3}
+    # the fast LPM of the optimized CPU baseline gives the same answers
+    o.set_fast(True)
+    v2, _, _, _ = o.classify_v4_cascade(t, nthreads=3)
+    np.testing.assert_array_equal(v2, g[f"c{ci}_verdict"])
+
+
 @pytest.mark.parametrize("ci", range(2))
 def test_classify_v6_lb_vs_reference(golden, ci):
     """the IPv6 egress path with lb6_local in front (bpf_lxc.c:108-203):
