@@ -808,8 +808,30 @@ def main():
         b_alg = b_in + b_out + 64.0 * probes_per
         achieved = b_alg * n / (kern_ms * 1e-3) / 1e9
         traffic, traffic_note, traffic_dom = pmc_traffic(args)
-        roof = roofline(n_cpu, kern_ms, b_in, b_out, probes, split, e.table_bytes(), ct6 or v6 or pf6,
-                        traffic_dom)
+        tb = e.table_bytes()
+        roof = roofline(n_cpu, kern_ms, b_in, b_out, probes, split, tb, ct6 or v6 or pf6, traffic_dom)
+        # the same floor with every table at the REFERENCE's own map footprint
+        # (entries x (key + value) bytes of the BPF map): a larger engine
+        # layout moves its lookups to a slower tier and so raises the floor;
+        # priced at the reference's bytes the floor is the lower of the two
+        ref_tb = dict(tb)
+        if not pf6:
+            ref_tb.update(ipcache=len(T.ipc_keys) * (24 + 8), policy=len(T.pol_keys) * (8 + 24))
+            if S is not None:
+                ref_tb.update(lb4=len(S.keys) * (8 + 12), lb6=len(S.keys) * (20 + 24))
+            if cascade:
+                ref_tb.update(prefilter=(len(P4.dyn4) + len(P4.fix4)) * (8 + 4),
+                              endpoint=len(P4.ep_keys) * (20 + 24))
+            if ct:
+                ce = int(e.ct6_count() if ct6 else e.ct4_count())
+                ref_tb.update(ct4=ce * (14 + 56), ct6=ce * (38 + 56))
+        roof_ref = roofline(n_cpu, kern_ms, b_in, b_out, probes, split, ref_tb, ct6 or v6 or pf6, traffic_dom)
+        if roof is not None and roof_ref is not None:
+            roof["frac_at_reference_footprint"] = roof_ref["frac"]
+            roof["bound_at_reference_footprint"] = roof_ref["bound"]
+            roof["reference_footprint_bytes"] = {k: ref_tb[k] for k in ("ipcache", "policy", "lb4", "lb6",
+                                                                       "prefilter", "endpoint", "ct4", "ct6")
+                                                 if k in ref_tb and ref_tb[k] != tb.get(k)}
         conf = {"workload": WORKLOADS[args.config], "tuples_per_gpu": n,
                 "parallelism": f"shard{world}", "kernel_ms": round(kern_ms, 4),
                 "stream_tuples_per_step": world * n, "stream_tuples_timed": world * n * args.steps,

@@ -468,19 +468,59 @@ struct PolKey {
 	uint32_t lo, hi, z, slot; /* key words, ep | proxy << 16, counter slot */
 };
 
+/* policy table slots per key at a full build (power-of-two rounded) */
+#ifndef CGPU_POL_SLOTS_PER_KEY
+#define CGPU_POL_SLOTS_PER_KEY 8
+#endif
+
 struct PolBuild {
 	std::vector<pol_slot> slots;
 	uint32_t mask = 0;
 	size_t count = 0;
-	/* place one key; false when its neighbourhood is full */
+	bool used(uint32_t i) const { return (slots[i & mask].ctr & POL_CTR_MASK) != POL_CTR_EMPTY; }
+	/* place one key; false when no free slot can be brought into its
+	 * neighbourhood.  Hopscotch insertion: the nearest free slot past the
+	 * neighbourhood is moved towards the home slot by relocating keys whose
+	 * own neighbourhood still covers it (a key's hop bit lives in ITS home
+	 * slot; a slot's own hop bits stay where they are), so the table holds
+	 * its keys at up to 50 % load (first-fit needed 512k slots for config 2's
+	 * 64k keys even at 2 slots per key) */
 	bool insert(const PolKey &k)
 	{
 		const uint32_t home = pol_hash(k.lo, k.hi, k.z & 0xFFFFu) & mask;
 		uint32_t d = 0;
-		while (d < POL_HOP && (slots[(home + d) & mask].ctr & POL_CTR_MASK) != POL_CTR_EMPTY)
+		const uint32_t limit = std::min<uint32_t>(mask + 1u, 4096u);
+		while (d < limit && used(home + d))
 			d++;
-		if (d == POL_HOP)
+		if (d == limit)
 			return false;
+		while (d >= POL_HOP) {
+			/* free slot f = home + d: move a key of home h2 = f - j (j < HOP)
+			 * that sits at h2 + o, o < j, into f */
+			const uint32_t f = (home + d) & mask;
+			bool moved = false;
+			for (uint32_t j = POL_HOP - 1; j >= 1 && !moved; j--) {
+				const uint32_t h2 = (f - j) & mask;
+				const uint32_t hop2 = slots[h2].ctr >> POL_HOP_SHIFT;
+				for (uint32_t o = 0; o < j; o++) {
+					if (!((hop2 >> o) & 1u))
+						continue;
+					pol_slot &src = slots[(h2 + o) & mask], &dst = slots[f];
+					dst.key_lo = src.key_lo;
+					dst.key_hi = src.key_hi;
+					dst.ep_proxy = src.ep_proxy;
+					dst.ctr = (dst.ctr & ~POL_CTR_MASK) | (src.ctr & POL_CTR_MASK);
+					src.key_lo = src.key_hi = src.ep_proxy = 0;
+					src.ctr = (src.ctr & ~POL_CTR_MASK) | POL_CTR_EMPTY;
+					slots[h2].ctr = (slots[h2].ctr & ~(1u << (POL_HOP_SHIFT + o))) | (1u << (POL_HOP_SHIFT + j));
+					d -= j - o;
+					moved = true;
+					break;
+				}
+			}
+			if (!moved)
+				return false;
+		}
 		pol_slot &sl = slots[(home + d) & mask];
 		sl.key_lo = k.lo;
 		sl.key_hi = k.hi;
@@ -509,10 +549,14 @@ struct PolBuild {
 		}
 		return false;
 	}
-	/* <= 50 % load: a lookup almost always finds its key in the home slot */
+	/* CGPU_POL_SLOTS_PER_KEY slots per key: at 8 (<= 12.5 % load) nearly
+	 * every key sits in its home slot, one gather per probe.  Denser tables
+	 * measured slower although smaller (config 2, one session, no rebalance:
+	 * 2 MiB 1.80 ms, 4 MiB 1.75, 8 MiB 1.72; profiles/r6_d/ab.log): a key
+	 * displaced from its home slot costs a dependent second gather */
 	void build(const std::vector<PolKey> &keys)
 	{
-		uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * keys.size() + 2));
+		uint32_t nb = next_pow2(std::max<uint64_t>(64, (uint64_t)CGPU_POL_SLOTS_PER_KEY * keys.size() + 2));
 		for (;;) {
 			slots.assign(nb, pol_slot{0, 0, 0, POL_CTR_EMPTY});
 			mask = nb - 1;

@@ -64,7 +64,11 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "fin_q2_nt512": ("CGPU_CT_FQ=2", "CGPU_CT_FNT=512"), "walk_svc_minb3": ("CGPU_WALK_MINB_SVC=3",),
             "ct_create_noloop": ("CGPU_CT_CREATE_LOOP=0",),
             "svc_q1": ("CGPU_CT_SVC_Q=1",), "svc_q2": ("CGPU_CT_SVC_Q=2",), "svc_q4": ("CGPU_CT_SVC_Q=4",),
-            "svc_pre6_off": ("CGPU_CT_SVC_PRE6=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",)}
+            "svc_pre6_off": ("CGPU_CT_SVC_PRE6=0",), "ff_h1": ("CGPU_FF_H=1",), "ff_h4": ("CGPU_FF_H=4",),
+            # policy table slots per key (hopscotch, round 6): 2 = 2 MiB at config 2
+            # (the product), 4 = 4 MiB, 8 = 8 MiB (round 5's footprint)
+            "pol_spk4": ("CGPU_POL_SLOTS_PER_KEY=4",), "pol_spk8": ("CGPU_POL_SLOTS_PER_KEY=8",),
+            "pol_spk2": ("CGPU_POL_SLOTS_PER_KEY=2",)}
 
 
 def build(names):
