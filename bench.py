@@ -329,6 +329,11 @@ def main():
                     help="cgpu_config.schedule (CGPU_SCHED_*, A/B timing of the fallback schedules; "
                          "0 = the tuned default)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--ct-persist", type=int, default=0, metavar="K",
+                    help="--config ct / ct6 in steady state: the conntrack map is carried across "
+                         "steps (no flush), each step 30 s after the last, and cgpu_ct{4,6}_gc "
+                         "(ctmap.GC RemoveExpired) runs before every K-th step on the device map; "
+                         "parity against the restatement carried the same way")
     ap.add_argument("--no-rebalance", action="store_true",
                     help="keep the class-based counter slots (no cgpu_counters_rebalance after warmup)")
     ap.add_argument("--traffic-json", default="",
@@ -346,7 +351,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from cilium_amd import shard, synth
+    from cilium_amd import layouts as L, shard, synth
     from cilium_amd.engine import Engine
 
     torch.cuda.set_device(local)
@@ -488,6 +493,13 @@ def main():
                             torch.empty(n, dtype=torch.int32, device=dev))
             out["dport"] = torch.empty(n, dtype=torch.int16, device=dev)
     CT_NOW = 1000
+    persist = args.ct_persist if (ct and not ctlb) else 0
+    if args.ct_persist and not persist:
+        raise SystemExit("--ct-persist applies to --config ct / ct6")
+    CT_DT = 30  # seconds between steps in steady state (UDP / ICMP entries live 60 s)
+    ct_k = [0]          # classify calls so far
+    ct_ops = []         # ("cls", now) / ("gc", time), in order, for the restatement
+    gc_log = []         # (entries deleted, host ms) per GC call
     delta = torch.zeros(e.counter_delta_bytes() // 8, dtype=torch.int64, device=dev)
     e.counter_bind(delta)
     stream = torch.cuda.current_stream()
@@ -506,14 +518,18 @@ def main():
         shard.init_counter_comm(e, rank, world)
 
     def launch():
+        now = CT_NOW + CT_DT * ct_k[0] if persist else CT_NOW
+        if ct:
+            ct_ops.append(("cls", now))
+            ct_k[0] += 1
         if ctlb and ct6:
-            e.classify_v6_ctlb(d, CT_NOW, out=out, stream=stream)
+            e.classify_v6_ctlb(d, now, out=out, stream=stream)
         elif ct6:
-            e.classify_v6_ct(d, CT_NOW, out=out, stream=stream)
+            e.classify_v6_ct(d, now, out=out, stream=stream)
         elif ctlb:
-            e.classify_v4_ctlb(d, CT_NOW, out=out, stream=stream)
+            e.classify_v4_ctlb(d, now, out=out, stream=stream)
         elif ct:
-            e.classify_v4_ct(d, CT_NOW, out=out, stream=stream)
+            e.classify_v4_ct(d, now, out=out, stream=stream)
         elif pf6:
             e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
         elif cascade:
@@ -535,8 +551,19 @@ def main():
         elif ct:
             e.ct4_flush()
 
+    def gc_ct():
+        # ctmap.GC RemoveExpired at the coming step's time, on the device map
+        tm = CT_NOW + CT_DT * ct_k[0]
+        g0 = time.perf_counter()
+        dl = e.ct6_gc(tm) if ct6 else e.ct4_gc(tm)
+        gc_log.append((dl, 1e3 * (time.perf_counter() - g0)))
+        ct_ops.append(("gc", tm))
+
     def step(ev=None):
-        if ct:
+        if persist:
+            if ct_k[0] and ct_k[0] % persist == 0:
+                gc_ct()
+        elif ct:
             flush_ct()  # every step starts from an empty conntrack map
         if ev is not None:
             ev[0].record(stream)
@@ -584,7 +611,7 @@ def main():
     if world > 1:
         # the shipped collective against torch's SUM of the same local deltas
         # (one untimed step): every rank must hold the sum of all ranks
-        if ct:
+        if ct and not persist:
             flush_ct()
         torch.cuda.synchronize()
         delta.zero_()
@@ -681,25 +708,52 @@ def main():
                     o2.ct_set_max(ct_max)
                     o2.ct6_set_max(ct_max)
                     (synth.load_services6 if ct6 else synth.load_services)(o2, S)
-                    rs, c_el = o2.sharded(meth, tup, CT_NOW, shard.conn_shard_of(tup, 4 * threads),
-                                          threads)
-                    same = float(np.mean((rs["verdict"] == r_["verdict"]) & (rs["ct_ret"] == r_["ct_ret"])))
-                    # the baseline is the exact computation: the sequential
-                    # restatement (one thread, the whole batch); the threaded
-                    # run is reported beside it, with how much of it agrees
-                    cpu = {"value": round(n / seq_s / 1e6, 3), "unit": "Mpps", "cores": 1,
+                    # threaded over an EXACT partition: the connected components
+                    # of the address pairs a packet can touch through any
+                    # backend of its service (shard.svc_component_shard_of)
+                    p0 = time.perf_counter()
+                    comp = shard.svc_component_shard_of(tup, S.keys, S.vals, 4 * threads,
+                                                        0 if ct6 else L.IPV4_LOOPBACK)
+                    part_s = time.perf_counter() - p0
+                    rs, c_el = o2.sharded(meth, tup, CT_NOW, comp, threads)
+                    same = all(np.array_equal(rs[k], r_[k]) for k in
+                               ("verdict", "ct_ret", "identity", "stage", "xdaddr", "xdport"))
+                    cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
                            "kind": "port",
                            "sample": (f"rank-0 batch, all {n} packets from an empty map; "
-                                      f"oracle/cgpu_oracle.c or_{meth}, sequential (the parity "
-                                      f"reference: no partition of a service's connections is exact), "
-                                      f"{seq_s:.1f}s on 1 thread; host: {host_cpu()}")}
-                    cpu_thr = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
-                               "kind": "port, approximate",
-                               "sample": (f"the same code threaded RSS-style by connection "
-                                          f"(shard.conn_shard_of, {4 * threads} shards, a conntrack map "
-                                          f"per shard) on {threads} threads, {c_el:.2f}s wall of the "
-                                          f"parallel section; {100 * same:.3f} % of its verdicts + ct "
-                                          f"results equal the sequential run's")}
+                                      f"oracle/cgpu_oracle.c or_{meth} threaded over {4 * threads} "
+                                      f"shards of an exact partition (shard.svc_component_shard_of: "
+                                      f"connected components of the address pairs reachable through "
+                                      f"any backend, {part_s:.1f}s to compute, untimed), a conntrack "
+                                      f"map per shard, on {threads} threads, {c_el:.2f}s wall of the "
+                                      f"parallel section; results equal to the sequential run's: "
+                                      f"{same}; host: {host_cpu()}")}
+                    cpu_thr = {"value": round(n / seq_s / 1e6, 3), "unit": "Mpps", "cores": 1,
+                               "kind": "port, sequential",
+                               "sample": (f"the same code on 1 thread over the whole batch in order "
+                                          f"(the parity reference), {seq_s:.1f}s")}
+            elif persist:
+                # steady state: the same batch replayed in the same order of
+                # steps and GCs (ct_ops) over pair-shard views whose maps
+                # persist; the last step's results are the parity reference
+                o.probe_split()
+                first, walls, odels = o.sharded_steps(meth, tup, shard.ct_shard_of(tup, 4 * threads),
+                                                      threads, ct_ops)
+                split = o.probe_split()
+                cls_w = [w for (op_, _), w in zip(ct_ops, walls) if op_ == "cls"]
+                c_el = float(np.median(cls_w))
+                gc_same = odels == [dl for dl, _ in gc_log]
+                # probes of the last batch only (probe_split counted all of them)
+                n_cls = len(cls_w)
+                split = {k_: v_ // n_cls for k_, v_ in split.items()}
+                if not skip_cpu:
+                    cpu = {"value": round(n / c_el / 1e6, 3), "unit": "Mpps", "cores": threads,
+                           "kind": "port",
+                           "sample": (f"rank-0 batch, all {n} packets per step, {n_cls} steps replayed "
+                                      f"with the same times and {len(odels)} GCs over persistent "
+                                      f"conntrack maps per address-pair shard (Oracle.sharded_steps, "
+                                      f"{4 * threads} shards) on {threads} threads; median "
+                                      f"{c_el:.2f}s wall per batch; host: {host_cpu()}")}
             else:
                 # address pairs are independent conntrack groups (every key a
                 # packet touches carries its pair): the pair-sharded run is
@@ -745,6 +799,8 @@ def main():
                 break
         if ct:
             v0, cr0, i0, _, probes = first
+            if persist:
+                probes = sum(split.values())
         elif pf6:
             c_el = float(np.median(runs))
             v0, probes = first
@@ -892,6 +948,20 @@ def main():
                                                 "lookups/updates/deletes of the reference "
                                                 "(+ service lookups), counted by the restatement "
                                                 "over the whole batch")
+                if persist:
+                    timed_gc = gc_log[-(args.steps // persist + 1):]
+                    conf.update(ct_persist={
+                        "gc_every_steps": persist, "seconds_per_step": CT_DT,
+                        "steps_total": ct_k[0], "gc_calls": len(gc_log),
+                        "gc_deleted": [dl for dl, _ in gc_log],
+                        "gc_deleted_equal_restatement": gc_same,
+                        "gc_ms_per_call": round(float(np.median([ms for _, ms in gc_log])), 3) if gc_log else None,
+                        "gc_ms_in_timed_steps": round(sum(ms for _, ms in timed_gc), 3),
+                        "ct_stats_after": e.ct_stats(ct6),
+                        "note": ("the same 64M-packet batch every step, 30 s apart, so UDP / ICMP / "
+                                 "SYN-only entries (60 s) expire and are re-created while TCP "
+                                 "connections stay established; kernel_ms is the classify alone, "
+                                 "ms_per_step includes the GC calls (device GC, one host read)")})
         result = {
             "metric": (f"Mpps classified from host-resident {'raw frames' if frames else 'batches'} (PCIe-inclusive)"
                        if args.host_tuples
@@ -918,7 +988,7 @@ def main():
             "cpu_baseline_optimized": cpu_opt,
         }
         if cpu_thr is not None:
-            result["cpu_baseline_threaded"] = cpu_thr
+            result["cpu_baseline_sequential"] = cpu_thr
         if not parity:
             log("WARNING: GPU verdicts differ from the restatement")
     if world > 1:

@@ -157,6 +157,7 @@ PROTOS = {
     "cgpu_ct4_get_next_key": (i32, [vp, vp, vp]),
     "cgpu_ct4_count": (sz, [vp]),
     "cgpu_ct4_gc": (i32, [vp, u32, C.POINTER(u64)]),
+    "cgpu_ct_stats": (i32, [vp, C.c_int, vp]),
     "cgpu_ct4_flush": (i32, [vp]),
     "cgpu_classify_v4_ct": (i32, [vp, C.POINTER(TuplesV4Ct), sz, u32, vp, vp, vp, vp, vp]),
     "cgpu_classify_v4_ctlb": (i32, [vp, C.POINTER(TuplesV4Ct), vp, sz, u32, C.POINTER(CtlbOut), vp]),

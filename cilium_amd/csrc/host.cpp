@@ -1846,6 +1846,11 @@ struct CtMap {
 	bool dev_newer = false, host_newer = false;
 	uint4 *d_keys = nullptr, *d_vals = nullptr;
 	uint32_t *d_count = nullptr;
+	/* the device compaction's second table (allocated at its first use) and
+	 * the device GC's result word */
+	uint4 *d_keys2 = nullptr, *d_vals2 = nullptr;
+	uint32_t *d_gc = nullptr;
+	uint64_t compactions = 0;
 	uint32_t sw() const { return v6 ? 4u : 1u; } /* uint4 key words per slot */
 };
 
@@ -2231,6 +2236,9 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 			(void)hipFree(m->d_keys);
 			(void)hipFree(m->d_vals);
 			(void)hipFree(m->d_count);
+			(void)hipFree(m->d_keys2);
+			(void)hipFree(m->d_vals2);
+			(void)hipFree(m->d_gc);
 		}
 		(void)hipFree(c->d_ct_scratch);
 		(void)hipFree(c->d_ct_pk);
@@ -5466,9 +5474,53 @@ static size_t ct_count_l(cgpu_ctx *c, CtMap &m)
 	return m.live;
 }
 
+/* compaction on the device (caller holds mu; the map is current on the
+ * device): every live entry re-inserted into the second table on the
+ * conntrack stream, then the two swap */
+static int ct_rehash_dev(cgpu_ctx *c, CtMap &m, hipStream_t cs)
+{
+	const size_t kb = m.keys.size() * 16, vb = m.vals.size() * 16;
+	if (!m.d_keys2) {
+		HIP_OR_EIO(hipMalloc((void **)&m.d_keys2, kb));
+		HIP_OR_EIO(hipMalloc((void **)&m.d_vals2, vb));
+	}
+	HIP_OR_EIO(hipMemsetAsync(m.d_keys2, 0, kb, cs));
+	const ct_table src{m.d_keys, m.d_vals, m.mask, m.max, m.d_count, 1u};
+	const ct_table dst{m.d_keys2, m.d_vals2, m.mask, m.max, m.d_count, 1u};
+	HIP_OR_EIO(launch_ct_rehash(src, dst, m.v6, cs));
+	HIP_OR_EIO(hipMemsetAsync(m.d_count + 1, 0, 4, cs));
+	std::swap(m.d_keys, m.d_keys2);
+	std::swap(m.d_vals, m.d_vals2);
+	m.tombs = 0;
+	m.compactions++;
+	(void)c;
+	return 0;
+}
+
 static int ct_gc_l(cgpu_ctx *c, CtMap &m, uint32_t time, uint64_t *deleted_out)
 {
 	std::lock_guard<std::mutex> g(c->mu);
+	if (c->device >= 0 && m.d_keys && !m.host_newer) {
+		/* the device map is current: filter it in place, ordered behind
+		 * the batches on the conntrack stream; one read of the result */
+		HIP_OR_EIO(hipSetDevice(c->device));
+		const hipStream_t cs = c->ct_stream;
+		if (!m.d_gc)
+			HIP_OR_EIO(hipMalloc((void **)&m.d_gc, 4));
+		HIP_OR_EIO(hipMemsetAsync(m.d_gc, 0, 4, cs));
+		const ct_table T{m.d_keys, m.d_vals, m.mask, m.max, m.d_count, 1u};
+		HIP_OR_EIO(launch_ct_gc(T, m.v6, time, m.d_gc, cs));
+		uint32_t r[3];
+		HIP_OR_EIO(hipMemcpyAsync(r, m.d_gc, 4, hipMemcpyDeviceToHost, cs));
+		HIP_OR_EIO(hipMemcpyAsync(r + 1, m.d_count, 8, hipMemcpyDeviceToHost, cs));
+		HIP_OR_EIO(hipStreamSynchronize(cs));
+		m.live = r[1];
+		m.tombs = r[2];
+		m.dev_newer = true;
+		if (deleted_out)
+			*deleted_out = r[0];
+		return 0;
+	}
 	if (int r = ct_pull(c, m))
 		return r;
 	uint64_t del = 0;
@@ -5581,6 +5633,27 @@ CGPU_EXPORT int cgpu_ct4_gc(cgpu_ctx *c, uint32_t time, uint64_t *deleted_out)
 	if (!c)
 		return fail(-EINVAL, "null context");
 	return ct_gc_l(c, c->ct4, time, deleted_out);
+}
+
+CGPU_EXPORT int cgpu_ct_stats(cgpu_ctx *c, int v6, uint64_t *out)
+{
+	if (!c || !out)
+		return fail(-EINVAL, "null argument");
+	CtMap &m = v6 ? c->ct6 : c->ct4;
+	std::lock_guard<std::mutex> g(c->mu);
+	uint32_t live = m.live, tombs = m.tombs;
+	if (c->device >= 0 && m.d_count && m.dev_newer) {
+		uint32_t cnt[2];
+		HIP_OR_EIO(hipSetDevice(c->device));
+		HIP_OR_EIO(hipMemcpyAsync(cnt, m.d_count, 8, hipMemcpyDeviceToHost, c->ct_stream));
+		HIP_OR_EIO(hipStreamSynchronize(c->ct_stream));
+		live = cnt[0];
+		tombs = cnt[1];
+	}
+	out[0] = live;
+	out[1] = tombs;
+	out[2] = m.compactions;
+	return 0;
 }
 
 CGPU_EXPORT int cgpu_ct4_flush(cgpu_ctx *c)
@@ -5696,10 +5769,8 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 		HIP_OR_EIO(hipStreamSynchronize(cs));
 		live = cnt[0];
 		if (cnt[1] > (m.mask + 1u) / 4u) {
-			if (int r = ct_pull(c, m))
+			if (int r = ct_rehash_dev(c, m, cs))
 				return r;
-			ct_rebuild(m);
-			m.host_newer = true;
 		}
 	}
 	if (int r = ct_push(m))

@@ -6749,6 +6749,82 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 	}
 }
 
+/* ctmap.GC's RemoveExpired filter (pkg/maps/ctmap/ctmap.go:273-367,
+ * doFiltering: an entry whose lifetime < time is deleted) over the device
+ * map, one lane per slot: the map stays on the device (the host path pulls
+ * and pushes both arrays, ~0.7 GB each way at config-2 sizes).  The slot
+ * turns into a tombstone as a batch's delete does; the live / tombstone
+ * counts and the number deleted are netted per workgroup. */
+template <class K> __global__ __launch_bounds__(256) void k_ct_gc(ct_table T, uint32_t time, uint32_t *deleted)
+{
+	__shared__ uint32_t s_del;
+	if (threadIdx.x == 0)
+		s_del = 0;
+	__syncthreads();
+	uint32_t del = 0;
+	for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i <= T.mask; i += gridDim.x * 256u) {
+		const uint32_t tag = *K::tagp(T, i) >> 16;
+		if (tag != CT_TAG_LIVE || T.vals[4u * i + 2u].x >= time)
+			continue;
+		K::clear(T, i);
+		*K::tagp(T, i) = CT_TAG_TOMB << 16;
+		del++;
+	}
+	del = (uint32_t)wave_sum((uint64_t)del);
+	if ((threadIdx.x & 63u) == 0 && del)
+		atomicAdd(&s_del, del);
+	__syncthreads();
+	if (threadIdx.x == 0 && s_del) {
+		atomicAdd(deleted, s_del);
+		atomicSub(&T.count[0], s_del);
+		atomicAdd(&T.count[1], s_del);
+	}
+}
+
+/* Compaction of a map whose tombstones lengthen the probe chains: every
+ * live slot of src re-inserted into the empty table dst (same size), its
+ * row with it; dst's tombstone count is 0, its live count src's. */
+template <class K> __global__ __launch_bounds__(256) void k_ct_rehash(ct_table src, ct_table dst)
+{
+	for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i <= src.mask; i += gridDim.x * 256u) {
+		if ((*K::tagp(src, i) >> 16) != CT_TAG_LIVE)
+			continue;
+		typename K::key k = K::load(src, i);
+		const uint32_t want = (K::cmeta(k) & 0xFFFFu) | (CT_TAG_LIVE << 16);
+		uint32_t h = K::hash(k) & dst.mask;
+		while (atomicCAS(K::tagp(dst, h), CT_TAG_EMPTY, want) != CT_TAG_EMPTY)
+			h = (h + 1u) & dst.mask;
+		K::store(dst, h, k);
+		const uint4 *sv = src.vals + 4u * i;
+		uint4 *dv = dst.vals + 4u * h;
+		dv[0] = sv[0];
+		dv[1] = sv[1];
+		dv[2] = sv[2];
+		dv[3] = sv[3];
+	}
+}
+
+hipError_t launch_ct_gc(const ct_table &T, bool v6, uint32_t time, uint32_t *deleted, hipStream_t st)
+{
+	const unsigned g = (unsigned)std::min<uint64_t>(((uint64_t)T.mask + 256u) / 256u, 8192);
+	if (v6)
+		hipLaunchKernelGGL(k_ct_gc<CtK6>, dim3(g), dim3(256), 0, st, T, time, deleted);
+	else
+		hipLaunchKernelGGL(k_ct_gc<CtK4>, dim3(g), dim3(256), 0, st, T, time, deleted);
+	return hipGetLastError();
+}
+
+/* dst: zeroed keys (tags EMPTY), vals and count set by the caller */
+hipError_t launch_ct_rehash(const ct_table &src, const ct_table &dst, bool v6, hipStream_t st)
+{
+	const unsigned g = (unsigned)std::min<uint64_t>(((uint64_t)src.mask + 256u) / 256u, 8192);
+	if (v6)
+		hipLaunchKernelGGL(k_ct_rehash<CtK6>, dim3(g), dim3(256), 0, st, src, dst);
+	else
+		hipLaunchKernelGGL(k_ct_rehash<CtK4>, dim3(g), dim3(256), 0, st, src, dst);
+	return hipGetLastError();
+}
+
 /* group-key bits the conntrack radix sort orders (CGPU_SCHED_CT_SORT_BITS) */
 static int ct_sort_bits(const cgpu_snapshot &s)
 {

@@ -164,6 +164,10 @@ struct ct_launch {
 };
 
 size_t ct_temp_bytes(uint64_t n);
+/* ctmap.GC RemoveExpired on the device map; compaction into an empty table */
+hipError_t launch_ct_gc(const ct_table &T, bool v6, uint32_t time, uint32_t *deleted, hipStream_t st);
+hipError_t launch_ct_rehash(const ct_table &src, const ct_table &dst, bool v6, hipStream_t st);
+
 hipError_t launch_classify_v4_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L,
 				 hipStream_t st);
 /* the same over cilium_ct6_global (tables.h CtK6 slots), rec [4n] */

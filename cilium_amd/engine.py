@@ -283,6 +283,12 @@ class Engine:
         check(self.L.cgpu_ct4_gc(self.h, time, C.byref(d)), "cgpu_ct4_gc")
         return d.value
 
+    def ct_stats(self, v6: bool = False) -> dict:
+        """cgpu_ct_stats: live entries, tombstones and compactions of the map."""
+        out = np.zeros(3, np.uint64)
+        check(self.L.cgpu_ct_stats(self.h, int(v6), out.ctypes.data_as(C.c_void_p)), "cgpu_ct_stats")
+        return {"live": int(out[0]), "tombstones": int(out[1]), "compactions": int(out[2])}
+
     def ct4_flush(self) -> None:
         check(self.L.cgpu_ct4_flush(self.h), "cgpu_ct4_flush")
 

@@ -150,6 +150,81 @@ def conn_shard_of(t: dict, world: int) -> np.ndarray:
             np.uint32(world)).astype(np.int64)
 
 
+def _addr_ids(a) -> np.ndarray:
+    a = np.asarray(a)
+    return (fold6_np(a) if a.ndim == 2 else a).astype(np.uint64)
+
+
+def _pairkey(a, b) -> np.ndarray:
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    return (lo << np.uint64(32)) | hi
+
+
+def svc_component_shard_of(t: dict, svc_keys, svc_vals, world: int, loopback: int = 0) -> np.ndarray:
+    """An EXACT partition of the service path (cgpu_classify_v{4,6}_ctlb) into
+    independent conntrack groups, for threading its CPU restatement and for
+    sharding it across GPUs.  ct_shard_of is not one: a service packet's
+    keys live in its own address pair {client, VIP} (the CT_SERVICE entry,
+    lb.h:700-775), in the pair of the backend it is translated to {client,
+    backend} (the conntrack entries, conntrack.h:649-744) and, through
+    ct_create4's address entry, in {backend, backend} or, on loopback, in
+    {IPV4_LOOPBACK, client} / {backend, 0}.  Every packet is a node's member
+    (its own pair); a packet that may be a service packet (egress to an
+    address the service map holds) links its pair with every pair it could
+    reach through ANY backend of that address (the selection itself depends
+    on state, so all of them), and the connected components of those links
+    are closed under every key any of their packets touches: each component
+    runs alone and the union of the runs is the sequential result.  IPv6
+    addresses enter as their 32-bit folds (a collision only merges
+    components).  Returns a shard id per packet: component hash % world."""
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+    sa, da = _addr_ids(t["saddr"]), _addr_ids(t["daddr"])
+    node = _pairkey(sa, da)
+    k = np.asarray(svc_keys)
+    v = np.asarray(svc_vals)
+    vip = _addr_ids(k["address"])
+    back = k["slave"] != 0
+    bvip, btgt = vip[back], _addr_ids(v["target"][back])
+    order = np.argsort(bvip, kind="stable")
+    bvip, btgt = bvip[order], btgt[order]
+    uvip, first, cnt = np.unique(bvip, return_index=True, return_counts=True)
+    eg = (np.asarray(t["flags"]) & 1).astype(bool)
+    cand = eg & np.isin(da, np.unique(vip))
+    # distinct (client, address) pairs of the candidates, each with every
+    # backend row of that address
+    cv = np.unique(np.stack([sa[cand], da[cand]], 1), axis=0) if cand.any() else np.zeros((0, 2), np.uint64)
+    vi = np.searchsorted(uvip, cv[:, 1])
+    has = (vi < len(uvip))
+    has[has] &= uvip[vi[has]] == cv[has, 1]
+    cv, vi = cv[has], vi[has]
+    rep = cnt[vi]
+    c_rep = np.repeat(cv[:, 0], rep)
+    v_rep = np.repeat(cv[:, 1], rep)
+    off = np.arange(rep.sum()) - np.repeat(np.cumsum(rep) - rep, rep)
+    b_rep = btgt[np.repeat(first[vi], rep) + off]
+    src = _pairkey(c_rep, v_rep)
+    lb = np.uint64(loopback)
+    loop = b_rep == c_rep
+    ends = [(src, _pairkey(c_rep, b_rep)), (_pairkey(c_rep, b_rep), _pairkey(b_rep, b_rep)),
+            (src[loop], _pairkey(np.full(int(loop.sum()), lb, np.uint64), c_rep[loop])),
+            (src[loop], _pairkey(b_rep[loop], np.zeros(int(loop.sum()), np.uint64)))]
+    keys = np.concatenate([node] + [x for e in ends for x in e])
+    uk, inv = np.unique(keys, return_inverse=True)
+    n = len(node)
+    ei, pos = [], n
+    for a_, b_ in ends:
+        m = len(a_)
+        ei.append((inv[pos:pos + m], inv[pos + m:pos + 2 * m]))
+        pos += 2 * m
+    r = np.concatenate([x for x, _ in ei]) if ei else np.zeros(0, np.int64)
+    c = np.concatenate([y for _, y in ei]) if ei else np.zeros(0, np.int64)
+    g = coo_matrix((np.ones(len(r), np.int8), (r, c)), shape=(len(uk), len(uk)))
+    _, lab = connected_components(g, directed=False)
+    comp = lab[inv[:n]].astype(np.uint64)
+    return (_fmix_np(comp ^ np.uint64(0x5BD1E995)) % np.uint64(world)).astype(np.int64)
+
+
 def take(t: dict, idx) -> dict:
     return {k: np.ascontiguousarray(v[idx]) for k, v in t.items()}
 

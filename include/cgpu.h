@@ -723,6 +723,11 @@ size_t cgpu_ct4_count(cgpu_ctx *ctx);
 int cgpu_ct4_gc(cgpu_ctx *ctx, uint32_t time, uint64_t *deleted_out);
 /* ctmap Flush (ctmap.go:361-367): delete every entry */
 int cgpu_ct4_flush(cgpu_ctx *ctx);
+/* (new, diagnostic) the map's slot statistics after everything queued on it:
+ * out[0] live entries, out[1] tombstones, out[2] compactions so far (a batch
+ * that finds more than a quarter of the slots tombstones first re-inserts the
+ * live entries into a clean table, on the device).  v6: cilium_ct6_global. */
+int cgpu_ct_stats(cgpu_ctx *ctx, int v6, uint64_t *out);
 
 /* A batch of IPv4 packets for the stateful path (device pointers). */
 typedef struct cgpu_tuples_v4_ct {

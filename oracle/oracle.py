@@ -594,6 +594,72 @@ class Oracle:
             outs.append(a)
         return tuple(outs), wall
 
+    def sharded_steps(self, method, t, shard, nthreads, ops):
+        """The steady-state form of `sharded`: one view per shard whose
+        conntrack maps PERSIST across `ops`, a list of ("cls", now) -- the
+        whole batch `t` again at time now -- and ("gc", time) -- ctmap.GC
+        RemoveExpired on every view (a shard's entries carry its address
+        pairs, so GC per shard = GC of the union).  Returns (the results of
+        the last "cls" as `method` returns them, in batch order; the wall
+        seconds of every op; the entries every "gc" deleted)."""
+        import threading
+        import time as _time
+        assert self.ct4_count() == 0 and self.ct6_count() == 0, "sharded run needs empty CT maps"
+        v6 = "v6" in method
+        shard = np.asarray(shard)
+        ids = np.unique(shard)
+        order = np.argsort(shard, kind="stable")
+        bounds = np.searchsorted(shard[order], ids, side="left").tolist() + [len(order)]
+        parts = [order[bounds[k]:bounds[k + 1]] for k in range(len(ids))]
+        subs = [{k: (None if v is None else np.ascontiguousarray(v[p])) for k, v in t.items()}
+                for p in parts]
+        views = [Oracle.__new__(Oracle) for _ in parts]
+        for v in views:
+            v.L, v.cfg = self.L, self.cfg
+            v.h = self.L.or_view_create(self.h)
+        walls, dels, res = [], [], [None] * len(parts)
+        for op, tm in ops:
+            nxt = [0]
+            lock = threading.Lock()
+            got = [0] * len(parts)
+
+            def run():
+                while True:
+                    with lock:
+                        k = nxt[0]
+                        nxt[0] += 1
+                    if k >= len(parts):
+                        return
+                    if op == "cls":
+                        res[k] = getattr(views[k], method)(subs[k], tm)
+                    else:
+                        got[k] = (views[k].ct6_gc if v6 else views[k].ct4_gc)(tm)
+
+            th = [threading.Thread(target=run) for _ in range(max(1, min(nthreads, len(parts))))]
+            c0 = _time.perf_counter()
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            walls.append(_time.perf_counter() - c0)
+            if op == "gc":
+                dels.append(int(sum(got)))
+        for v in views:
+            self.L.or_view_merge(self.h, v.h)
+            self.L.or_view_destroy(v.h)
+            v.h = None
+        n = len(t["saddr"])
+        outs = []
+        for j, val in enumerate(res[0]):
+            if not isinstance(val, np.ndarray):
+                outs.append(sum(r[j] for r in res))
+                continue
+            a = np.empty((n,) + val.shape[1:], val.dtype)
+            for p, r in zip(parts, res):
+                a[p] = r[j]
+            outs.append(a)
+        return tuple(outs), walls, dels
+
     # --- L3 MapState compilation (SURVEY §8f row 4) ---
     @staticmethod
     def l3_compile(prog, ep_sets, id_sets, flags=3):

@@ -309,3 +309,63 @@ def test_ct_jumbo_counters_one_slot(torch_cuda, cfg_ct):
         big = max(big, int(exp["bytes"]))
     assert big >= 1 << 37, "one slot must pass the packed byte field"
     e.close()
+
+
+@pytest.mark.parametrize("v6", [False, True])
+def test_ct_device_gc_and_compaction(torch_cuda, cfg_ct, v6):
+    """ctmap.GC (RemoveExpired) and the tombstone compaction run on the device
+    map (k_ct_gc, k_ct_rehash) with the map never leaving the device between
+    batches: 6 rounds of {batch, GC} over a CT_MAP_SIZE-4096 map (8192
+    slots) whose UDP / ICMP / SYN-only entries (60 s lifetime) expire
+    between rounds, so every GC turns about 2,000 slots into tombstones and
+    a later batch finds more than a quarter of the slots tombstones and
+    compacts the table first.  Verdicts, ct results, the GC's deleted counts,
+    the live counts and the whole map equal the restatement's carried the
+    same way; the live connections' TCP entries survive the compactions."""
+    from oracle import Oracle
+    T, _, _, _ = cfg_ct
+    if v6:
+        T = synth.make_tables6(n_prefixes=5000, n_identities=200, n_endpoints=1, keys_per_ep=4000)
+        t, _, seclabels = synth.make_ct6_workload(T, 1_800, seed=33, mean_pkts=6.0, span=0.9)
+    else:
+        t, _, seclabels = synth.make_ct_workload(T, 1_800, seed=33, mean_pkts=6.0, span=0.9)
+    ct_max = 1 << 12
+    o = Oracle(**T.oracle_config())
+    synth.load_oracle(o, T)
+    synth.load_lxc(o, seclabels)
+    o.ct_set_max(ct_max)
+    o.ct6_set_max(ct_max)
+    e = _engine(**T.engine_config(), ct_max=ct_max)
+    synth.load_engine(e, T)
+    synth.load_lxc(e, seclabels)
+    e.commit()
+    run_o = o.classify_v6_ct if v6 else o.classify_v4_ct
+    run_e = e.classify_v6_ct if v6 else e.classify_v4_ct
+    gc_o = o.ct6_gc if v6 else o.ct4_gc
+    gc_e = e.ct6_gc if v6 else e.ct4_gc
+    n = len(t["proto"])
+    rng = np.random.Generator(np.random.PCG64(8))
+    deleted = 0
+    for rnd in range(6):
+        # each round a different window of the stream, 120 s later
+        lo = int(rng.integers(0, n // 2))
+        tb = {k: x[lo:lo + n // 2] for k, x in t.items()}
+        now = 1000 + 120 * rnd
+        out = run_e(synth.to_device(tb), now)
+        torch_cuda.cuda.synchronize()
+        v0, cr0, i0, _, _ = run_o(tb, now)
+        np.testing.assert_array_equal(out["verdict"].cpu().numpy(), v0, err_msg=f"round {rnd}")
+        np.testing.assert_array_equal(out["ct_ret"].cpu().numpy(), cr0, err_msg=f"round {rnd}")
+        np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
+        assert not (out["verdict"].cpu().numpy() == L.DROP_CT_CREATE_FAILED).any()
+        d_e, d_o = gc_e(now + 100), gc_o(now + 100)
+        assert d_e == d_o, f"round {rnd}: GC deleted {d_e} vs {d_o}"
+        deleted += d_o
+        assert (e.ct6_count() if v6 else e.ct4_count()) == (o.ct6_count() if v6 else o.ct4_count())
+    st = e.ct_stats(v6)
+    assert deleted > 4 * ct_max and st["compactions"] >= 1, (deleted, st)
+    ek, ev = (e.ct6_dump() if v6 else e.ct4_dump())
+    ok, ov = (o.ct6_dump() if v6 else o.ct4_dump())
+    np.testing.assert_array_equal(ek, ok)
+    np.testing.assert_array_equal(ev, ov)
+    e.close()

@@ -64,3 +64,66 @@ def test_conn_sharded_ctlb_close_to_sequential():
     got1, _ = one.sharded("classify_v4_ctlb", t, 1000, np.zeros(len(t["saddr"]), np.int64), nthreads=4)
     for k in ("verdict", "ct_ret", "identity", "stage", "xdaddr", "xdport"):
         np.testing.assert_array_equal(got1[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("v6", [False, True])
+def test_component_sharded_ctlb_equals_sequential(v6):
+    """The service path threaded over shard.svc_component_shard_of (bench.py's
+    ctlb / ctlb6 cpu_baseline): the connected components
+    of the address pairs a packet can touch through any backend of its
+    service are independent conntrack groups, so the threaded run equals the
+    sequential one exactly -- every output, the metrics and the whole map --
+    with loopback backends (1 % of the connections) in the stream."""
+    from cilium_amd import layouts as L
+    if v6:
+        T = synth.make_tables6(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+        S = synth.make_services6(T, 3000)
+        t, _, sl, S = synth.make_ctlb6_workload(T, S, 20_000, mean_pkts=8.0, loop_frac=1e-2)
+    else:
+        T = synth.make_tables(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+        S = synth.make_services(T, 3000)
+        t, _, sl, S = synth.make_ctlb_workload(T, S, 20_000, mean_pkts=8.0, loop_frac=1e-2)
+    meth = "classify_v6_ctlb" if v6 else "classify_v4_ctlb"
+    seq = _oracle(T, sl, S, v6)
+    ref = getattr(seq, meth)(t, 1000)
+    par = _oracle(T, sl, S, v6)
+    comp = shard.svc_component_shard_of(t, S.keys, S.vals, 16, 0 if v6 else L.IPV4_LOOPBACK)
+    assert len(np.unique(comp)) == 16
+    got, _ = par.sharded(meth, t, 1000, comp, nthreads=4)
+    for k in ("verdict", "ct_ret", "identity", "stage", "xdaddr", "xdport"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    np.testing.assert_array_equal(par.metrics(), seq.metrics())
+    dump = "ct6_dump" if v6 else "ct4_dump"
+    for a, b in zip(getattr(par, dump)(), getattr(seq, dump)()):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("v6", [False, True])
+def test_sharded_steps_equals_sequential_with_gc(v6):
+    """Oracle.sharded_steps (bench.py --ct-persist): pair-shard views whose
+    maps persist over batches at advancing times with ctmap.GC between them
+    give the sequential restatement's results, GC counts and map."""
+    if v6:
+        T = synth.make_tables6(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+        t, _, sl = synth.make_ct6_workload(T, 10_000, mean_pkts=6.0, span=0.05)
+    else:
+        T = synth.make_tables(n_prefixes=3000, n_identities=300, n_endpoints=2, keys_per_ep=2000)
+        t, _, sl = synth.make_ct_workload(T, 10_000, mean_pkts=6.0, span=0.05)
+    meth = "classify_v6_ct" if v6 else "classify_v4_ct"
+    ops = [("cls", 1000), ("cls", 1030), ("gc", 1065), ("cls", 1070), ("cls", 1100), ("gc", 1200),
+           ("cls", 1201)]
+    seq = _oracle(T, sl)
+    dels = []
+    for op, tm in ops:
+        if op == "gc":
+            dels.append((seq.ct6_gc if v6 else seq.ct4_gc)(tm))
+        else:
+            ref = getattr(seq, meth)(t, tm)
+    par = _oracle(T, sl)
+    got, walls, gdels = par.sharded_steps(meth, t, shard.ct_shard_of(t, 7), 4, ops)
+    assert len(walls) == len(ops) and gdels == dels and dels[0] > 0
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
+    dump = "ct6_dump" if v6 else "ct4_dump"
+    for a, b in zip(getattr(par, dump)(), getattr(seq, dump)()):
+        np.testing.assert_array_equal(a, b)
