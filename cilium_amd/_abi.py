@@ -34,7 +34,7 @@ class CgpuConfig(C.Structure):
         ("lb_flags", C.c_uint32),
         ("node_mac", C.c_uint8 * 6), ("reserved1", C.c_uint8 * 2),
         ("ct_max", C.c_uint32), ("schedule", C.c_uint32), ("ct6_max", C.c_uint32),
-        ("reserved", C.c_uint32 * 2),
+        ("ct_lru", C.c_uint32), ("reserved", C.c_uint32 * 1),
     ]
 
 

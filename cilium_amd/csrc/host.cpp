@@ -1838,6 +1838,9 @@ struct BuildState {
  * kernels.hip).  A host shadow serves the bpf(2)-style map calls; the device
  * copy is authoritative once a batch ran (dev_newer) and is refreshed from
  * the shadow before the next batch after host edits (host_newer). */
+/* LRU mode's bloom filter of a batch's conntrack keys: 2^22 words (2^27 bits) */
+#define CT_BLOOM_WORDS (1u << 22)
+
 struct CtMap {
 	bool v6 = false;
 	uint32_t max = 0;               /* CT_MAP_SIZE */
@@ -1850,6 +1853,7 @@ struct CtMap {
 	 * the device GC's result word */
 	uint4 *d_keys2 = nullptr, *d_vals2 = nullptr;
 	uint32_t *d_gc = nullptr;
+	uint32_t *d_bloom = nullptr; /* LRU mode: the batch's key filter */
 	uint64_t compactions = 0;
 	uint32_t sw() const { return v6 ? 4u : 1u; } /* uint4 key words per slot */
 };
@@ -2239,6 +2243,7 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 			(void)hipFree(m->d_keys2);
 			(void)hipFree(m->d_vals2);
 			(void)hipFree(m->d_gc);
+			(void)hipFree(m->d_bloom);
 		}
 		(void)hipFree(c->d_ct_scratch);
 		(void)hipFree(c->d_ct_pk);
@@ -5794,6 +5799,15 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	const uint32_t headroom = m.max > live ? m.max - live : 0u;
 	const uint32_t chunk = std::min<uint32_t>(256u, std::max<uint32_t>(1u, headroom / 32768u));
 	ct_table T{m.d_keys, m.d_vals, m.mask, m.max, m.d_count, chunk};
+	/* LRU mode (the plain paths; the service paths keep failing creates
+	 * closed): the batch's key filter, 16 MiB */
+	if (c->cfg.ct_lru && !svc) {
+		if (!m.d_bloom)
+			HIP_OR_EIO(hipMalloc((void **)&m.d_bloom, (size_t)CT_BLOOM_WORDS * 4u));
+		T.bloom = m.d_bloom;
+		T.bloom_mask = CT_BLOOM_WORDS - 1u;
+		T.lru = 1;
+	}
 	a.delta = delta;
 	a.rec = reinterpret_cast<uint4 *>(b + L.rec);
 	a.gkey = reinterpret_cast<uint32_t *>(b + L.gkey);

@@ -4522,13 +4522,84 @@ __device__ __forceinline__ bool ct_take(const ct_table &T, const ct_acct &A)
 }
 
 
+/* ---- LRU mode (cgpu_config.ct_lru) ----
+ * The reference declares CT_MAP4 / CT_MAP6 as BPF_MAP_TYPE_LRU_HASH on every
+ * kernel with LRU maps (bpf/bpf_lxc.c:53-75, probe bpf/probes/raw_lru_map.t),
+ * so a full map evicts instead of failing ct_create.  Its victim is the
+ * kernel's per-CPU LRU list's; ours is an entry none of this batch's
+ * packets can touch: every key a packet of the batch may look up or create
+ * (reply, forward and ICMP tuples; the service path's service, address and
+ * ICMP tuples) is marked in a bloom filter before the walks, and a create
+ * that finds the map full scans the slots from a hashed start for a live
+ * entry outside the filter.  So every packet of the batch gets the result
+ * the map it started from gives it, whatever was evicted; across batches an
+ * entry idle in one batch may be gone in the next, as an LRU-evicted one. */
+#ifndef CT_EVICT_SCAN
+#define CT_EVICT_SCAN 4096u
+#endif
+
+template <class K> __device__ __forceinline__ uint32_t ct_bbit(const typename K::key &k)
+{
+	return ct_fmix(K::hash(k) ^ 0x2545F491u);
+}
+
+template <class K> __device__ __forceinline__ bool ct_in_batch(const ct_table &T, const typename K::key &k)
+{
+	const uint32_t b = ct_bbit<K>(k);
+	return (T.bloom[(b >> 5) & T.bloom_mask] >> (b & 31u)) & 1u;
+}
+
+template <class K> __device__ __forceinline__ void ct_mark(uint32_t *bloom, uint32_t mask, const typename K::key &k)
+{
+	const uint32_t b = ct_bbit<K>(k);
+	uint32_t *w = bloom + ((b >> 5) & mask);
+	const uint32_t m = 1u << (b & 31u);
+	if (!(*w & m)) /* most marks repeat a connection's: read before the atomic */
+		atomicOr(w, m);
+}
+
+/* evict one live entry outside the batch's filter: its capacity passes to
+ * the caller's create (the live count does not change), the slot becomes a
+ * tombstone as a delete leaves it (claimed first, so no prober compares
+ * and no insert reuses it while its words are cleared) */
+template <class K> __device__ __forceinline__ bool ct_evict(const ct_table &T, const ct_acct &A, uint32_t start)
+{
+	uint32_t h = start & T.mask;
+	for (uint32_t probe = 0; probe < CT_EVICT_SCAN; probe++, h = (h + 1u) & T.mask) {
+		const uint32_t tw = __hip_atomic_load(K::tagp(T, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if ((tw >> 16) != CT_TAG_LIVE)
+			continue;
+		typename K::key s{};
+		K::reload(T, h, s);
+		K::meta(s) = tw;
+		if (ct_in_batch<K>(T, s))
+			continue;
+		if (atomicCAS(K::tagp(T, h), tw, (CT_TAG_CLAIM << 16) | (tw & 0xFFFFu)) != tw)
+			continue;
+		K::clear(T, h);
+		__builtin_amdgcn_s_waitcnt(0);
+		__hip_atomic_exchange(K::tagp(T, h), CT_TAG_TOMB << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		atomicAdd(A.tombs, 1);
+		return true;
+	}
+	return false;
+}
+
+/* ct_take, and in LRU mode an eviction when the map is full */
+template <class K> __device__ __forceinline__ bool ct_take_k(const ct_table &T, const ct_acct &A, uint32_t seed)
+{
+	if (ct_take(T, A))
+		return true;
+	return T.lru && ct_evict<K>(T, A, ct_fmix(seed ^ (blockIdx.x * 256u + threadIdx.x) * 0x9E3779B1u));
+}
+
 /* Insert absent k at the first free slot from `from` on (htab_map_update_elem
  * of a new key: -E2BIG past max_elem).  Returns the slot or -1. */
 template <class K, bool TAKE = true>
 __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, const typename K::key &k,
 					 uint32_t from)
 {
-	if (TAKE && !ct_take(T, A))
+	if (TAKE && !ct_take_k<K>(T, A, K::hash(k)))
 		return -1;
 	uint32_t h = from & T.mask;
 	for (uint32_t probe = 0; probe <= T.mask; probe++) {
@@ -4537,10 +4608,18 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, co
 		if (tag == CT_TAG_EMPTY || tag == CT_TAG_TOMB) {
 			const uint32_t expect = tag << 16;
 			const uint32_t want = (K::cmeta(k) & 0xFFFFu) | (CT_TAG_LIVE << 16);
-			if (atomicCAS(K::tagp(T, h), expect, want) == expect) {
+			/* LRU mode: the slot turns LIVE only once its key words are
+			 * written (claimed first), so an eviction never judges a key it
+			 * reads half-written */
+			const uint32_t first = T.lru ? (K::cmeta(k) & 0xFFFFu) | (CT_TAG_CLAIM << 16) : want;
+			if (atomicCAS(K::tagp(T, h), expect, first) == expect) {
 				if (tag == CT_TAG_TOMB)
 					atomicSub(A.tombs, 1);
 				K::store(T, h, k); /* pending: the caller marks it (ctc_update) */
+				if (T.lru) {
+					__builtin_amdgcn_s_waitcnt(0);
+					__hip_atomic_exchange(K::tagp(T, h), want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				}
 				return (int)h;
 			}
 		}
@@ -4557,6 +4636,8 @@ __device__ __forceinline__ int ct_insert(const ct_table &T, const ct_acct &A, co
  * write back the XCD's entire L2 for every delete). */
 template <class K> __device__ __forceinline__ void ct_erase(const ct_table &T, const ct_acct &A, uint32_t slot)
 {
+	if (T.lru) /* claimed first: an eviction's CAS of the LIVE tag then fails */
+		__hip_atomic_exchange(K::tagp(T, slot), CT_TAG_CLAIM << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	K::clear(T, slot);
 	__builtin_amdgcn_s_waitcnt(0);
 	__hip_atomic_exchange(K::tagp(T, slot), CT_TAG_TOMB << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -6017,7 +6098,7 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 					 * update fails here when the map is full), write it
 					 * in phase 2 */
 					if (am == AM_DEFER) {
-						if (!ct_take(T, A))
+						if (!ct_take_k<K>(T, A, K::hash(k)))
 							return CT_NEW | CT_FAIL;
 						owed = CT_ADDRP;
 					}
@@ -6030,7 +6111,7 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 				/* the ICMP entry lies in the address pair's phase-2 group:
 				 * reserve its capacity now (where the reference's update
 				 * would fail), write it in phase 2 in batch order */
-				if (!ct_take(T, A))
+				if (!ct_take_k<K>(T, A, K::hash(k)))
 					return CT_NEW | CT_FAIL | owed;
 				return CT_NEW | CT_RELP | owed;
 			}
@@ -6049,7 +6130,7 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 			if (!ctc_update<K>(T, A, c, ct_addr_key(k, q), e))
 				return CT_NEW | CT_FAIL;
 		} else if (am == AM_DEFER) {
-			if (!ct_take(T, A))
+			if (!ct_take_k<K>(T, A, K::hash(k)))
 				return CT_NEW | CT_FAIL;
 			owed = CT_ADDRP;
 		}
@@ -6057,7 +6138,7 @@ __device__ __forceinline__ uint32_t ct_step(const ct_table &T, const ct_acct &A,
 	ct_row e2 = e;
 	e2.c.y |= CTB_SEEN_NON_SYN;
 	if (meta & CTM_RELX) {
-		if (!ct_take(T, A))
+		if (!ct_take_k<K>(T, A, K::hash(k)))
 			return CT_NEW | CT_FAIL | owed;
 		return CT_NEW | CT_RELP | owed;
 	}
@@ -6376,6 +6457,22 @@ __device__ __forceinline__ uint4 ct_svc_step6(const cgpu_snapshot &s, const ct_t
 #ifndef CT_RETB
 #define CT_RETB 16 /* results a walker lane buffers before storing them */
 #endif
+
+/* LRU mode: the keys packet i's conntrack step can look up or create (the
+ * reply tuple, the forward tuple, its ICMP tuple) into the batch's filter */
+template <class K> __global__ __launch_bounds__(256) void k_ct_mark(ct_args a, uint32_t *bloom, uint32_t mask)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256u) {
+		const ct_rec<K> r = ct_rec<K>::load(a.rec, (uint32_t)i, true);
+		if (r.meta() & CTM_GATED)
+			continue;
+		const typename K::key k = r.key();
+		const typename K::key fk = K::reversed(k);
+		ct_mark<K>(bloom, mask, k);
+		ct_mark<K>(bloom, mask, fk);
+		ct_mark<K>(bloom, mask, K::related(fk));
+	}
+}
 
 /* walks: WALK_PKT the conntrack path's packets; WALK_SVC the service step
  * (K = CtK4, ct_srec records, result into svc_out); WALK_OWED phase 2 of the
@@ -7225,6 +7322,15 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 		constexpr int Q = CGPU_CT_Q;
 		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
 		hipLaunchKernelGGL((k_ct_prep_q<Q>), dim3(gq), dim3(256), 0, st, s, a);
+	}
+	if (T.lru) {
+		/* LRU mode: every key the batch can touch into the filter the
+		 * evictions avoid (the prep's records are complete) */
+		hipError_t e0 = hipMemsetAsync(const_cast<uint32_t *>(T.bloom), 0, ((size_t)T.bloom_mask + 1u) * 4u, st);
+		if (e0 != hipSuccess)
+			return e0;
+		hipLaunchKernelGGL(k_ct_mark<K>, dim3(g), dim3(256), 0, st, a, const_cast<uint32_t *>(T.bloom),
+				   T.bloom_mask);
 	}
 	uint32_t nh;
 	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st, K::V6 != 0);

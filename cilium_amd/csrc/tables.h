@@ -513,6 +513,12 @@ typedef struct ct_table {
 	uint32_t max;       /* CT_MAP_SIZE: live entries allowed */
 	uint32_t *count;    /* [0] live entries, [1] tombstones */
 	uint32_t res_chunk; /* capacity a workgroup reserves at a time (headroom-sized) */
+	/* LRU mode (cgpu_config.ct_lru): a create that finds the map full evicts
+	 * an entry none of the batch's packets can touch -- the batch's keys are
+	 * in this bloom filter (bloom_mask + 1 words) -- instead of failing */
+	const uint32_t *bloom;
+	uint32_t bloom_mask;
+	uint32_t lru;
 } ct_table;
 
 #if defined(__HIPCC__)

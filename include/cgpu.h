@@ -167,7 +167,19 @@ typedef struct cgpu_config {
 	uint32_t schedule;
 	/* CT_MAP_SIZE of cilium_ct6_global (0 = ct_max) */
 	uint32_t ct6_max;
-	uint32_t reserved[2];
+	/* 1: the conntrack maps behave as BPF_MAP_TYPE_LRU_HASH, which the
+	 * reference builds CT_MAP4 / CT_MAP6 as on every kernel with LRU maps
+	 * (bpf/bpf_lxc.c:53-75, probe bpf/probes/raw_lru_map.t): a create that
+	 * finds the map full evicts an entry instead of failing.  The victim is
+	 * the engine's own choice, not the kernel's per-CPU LRU list: a live
+	 * entry none of the batch's packets can look up or create (a key filter
+	 * built before the walk; the scan covers CT_EVICT_SCAN = 4096 slots from
+	 * a hashed start), so every packet of a batch gets the result the map it
+	 * started from gives it.  cgpu_classify_v{4,6}_ct only: the service paths
+	 * keep failing the create (DROP_NO_SERVICE / DROP_CT_CREATE_FAILED).
+	 * 0 (default): the non-LRU build, CT_MAP_SIZE enforced as -E2BIG. */
+	uint32_t ct_lru;
+	uint32_t reserved[1];
 } cgpu_config;
 
 #define CGPU_SCHED_PER_LANE 1u   /* classify: one tuple per lane (k_classify) instead of x4 */

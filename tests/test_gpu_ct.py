@@ -372,3 +372,64 @@ def test_ct_device_gc_and_compaction(torch_cuda, cfg_ct, v6):
     np.testing.assert_array_equal(ek, ok)
     np.testing.assert_array_equal(ev, ov)
     e.close()
+
+
+@pytest.mark.parametrize("v6", [False, True])
+def test_ct_lru_evicts_instead_of_failing(torch_cuda, cfg_ct, v6):
+    """LRU mode (cgpu_config.ct_lru; the reference's CT_MAP4 / CT_MAP6 are
+    BPF_MAP_TYPE_LRU_HASH, bpf/bpf_lxc.c:53-75): a CT_MAP_SIZE-4096 map is
+    filled by one stream, then a stream of other connections needs ~3,000
+    more entries.  Properties (the victim choice is the engine's own):
+    no DROP_CT_CREATE_FAILED, the live count never exceeds the map size,
+    every packet of the second batch gets exactly what the restatement gives
+    it starting from the map the batch found (no key the batch touches is
+    evicted), and the map afterwards is the restatement's minus evicted
+    entries of the first stream that the second batch never touched."""
+    from oracle import Oracle
+    T, _, _, _ = cfg_ct
+    if v6:
+        T = synth.make_tables6(n_prefixes=5000, n_identities=200, n_endpoints=1, keys_per_ep=4000)
+        mk, run, dump, upd = synth.make_ct6_workload, "classify_v6_ct", "ct6_dump", "ct6_update"
+    else:
+        mk, run, dump, upd = synth.make_ct_workload, "classify_v4_ct", "ct4_dump", "ct4_update"
+    ta, _, seclabels = mk(T, 1_400, seed=41, mean_pkts=5.0, span=0.9)
+    tb, _, _ = mk(T, 1_400, seed=42, mean_pkts=5.0, span=0.9)
+    ct_max = 1 << 12
+    e = _engine(**T.engine_config(), ct_max=ct_max, ct_lru=1)
+    synth.load_engine(e, T)
+    synth.load_lxc(e, seclabels)
+    e.commit()
+    count = e.ct6_count if v6 else e.ct4_count
+    for bi, (tt, now) in enumerate(((ta, 1000), (tb, 1010))):
+        pre_k, pre_v = getattr(e, dump)()
+        o = Oracle(**T.oracle_config())
+        synth.load_oracle(o, T)
+        synth.load_lxc(o, seclabels)
+        o.ct_set_max(1 << 20)
+        o.ct6_set_max(1 << 20)
+        for k, v in zip(pre_k, pre_v):
+            assert getattr(o, upd)(k, v) == 0
+        out = getattr(e, run)(synth.to_device(tt), now)
+        torch_cuda.cuda.synchronize()
+        v0, cr0, i0, _, _ = getattr(o, run)(tt, now)
+        v = out["verdict"].cpu().numpy()
+        assert not (v == L.DROP_CT_CREATE_FAILED).any(), f"batch {bi}"
+        np.testing.assert_array_equal(v, v0, err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(out["ct_ret"].cpu().numpy(), cr0, err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
+        assert count() <= ct_max
+        gk, gv = getattr(e, dump)()
+        ok_, ov = getattr(o, dump)()
+        gb = {a.tobytes(): b.tobytes() for a, b in zip(gk, gv)}
+        ob = {a.tobytes(): b.tobytes() for a, b in zip(ok_, ov)}
+        pre = {a.tobytes(): b.tobytes() for a, b in zip(pre_k, pre_v)}
+        for kk, vv in gb.items():
+            assert ob.get(kk) == vv
+        gone = set(ob) - set(gb)
+        # only untouched entries of the map the batch found were evicted
+        assert all(kk in pre and ob[kk] == pre[kk] for kk in gone)
+        if bi == 1:
+            # (capacity reserved by other workgroups counts as taken while a
+            # batch runs, so evictions start a little before the map is full)
+            assert len(gone) > 300
+    e.close()
