@@ -68,7 +68,10 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             # policy table slots per key (hopscotch, round 6): 2 = 2 MiB at config 2
             # (the product), 4 = 4 MiB, 8 = 8 MiB (round 5's footprint)
             "pol_spk4": ("CGPU_POL_SLOTS_PER_KEY=4",), "pol_spk8": ("CGPU_POL_SLOTS_PER_KEY=8",),
-            "pol_spk2": ("CGPU_POL_SLOTS_PER_KEY=2",)}
+            "pol_spk2": ("CGPU_POL_SLOTS_PER_KEY=2",),
+            # the v6 pre-pass: addresses behind the direction flag (round 5's form)
+            "v6_pre_nospec": ("CGPU_IPC6_SPEC=0",),
+            "v6_pre_q3": ("CGPU_DIAG_IPC6_PRE_Q=3",), "v6_pre_q4b": ("CGPU_DIAG_IPC6_PRE_Q=4",)}
 
 
 def build(names):
