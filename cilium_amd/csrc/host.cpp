@@ -468,6 +468,10 @@ struct PolKey {
 	uint32_t lo, hi, z, slot; /* key words, ep | proxy << 16, counter slot */
 };
 
+#ifndef CGPU_LB_SLOTS_PER_FE
+#define CGPU_LB_SLOTS_PER_FE 2
+#endif
+
 /* policy table slots per key at a full build (power-of-two rounded) */
 #ifndef CGPU_POL_SLOTS_PER_KEY
 #define CGPU_POL_SLOTS_PER_KEY 8
@@ -1635,17 +1639,47 @@ int build_lb(const LbIn &lb, uint32_t lb_max_entries, LbBuild &b)
 			       maxs | (master ? LB_FE_MASTER : 0u)});
 		it = jt;
 	}
-	uint32_t nb = next_pow2(std::max<uint64_t>(64, 2 * fes.size()));
+	/* frontend slots per frontend (power-of-two rounded); hopscotch insertion
+	 * as the policy table's (PolBuild::insert): first-fit needed 16 slots per
+	 * frontend for config 5's 1M frontends (a 256-MiB table, past the
+	 * Infinity Cache) */
+	uint32_t nb = next_pow2(std::max<uint64_t>(64, (uint64_t)CGPU_LB_SLOTS_PER_FE * fes.size()));
 	for (;;) {
 		b.fe.assign(nb, std::array<uint32_t, 4>{0, 0, 0, 0});
 		b.mask = nb - 1;
 		bool ok = true;
+		auto used = [&](uint32_t i) { return (b.fe[i & b.mask][3] & LB_FE_USED) != 0u; };
 		for (auto &f : fes) {
 			const uint32_t home = lb_hash(f[0], f[1] & 0xFFFFu) & b.mask;
 			uint32_t d = 0;
-			while (d < POL_HOP && (b.fe[(home + d) & b.mask][3] & LB_FE_USED))
+			const uint32_t limit = std::min<uint32_t>(b.mask + 1u, 4096u);
+			while (d < limit && used(home + d))
 				d++;
-			if (d == POL_HOP) {
+			while (ok && d < limit && d >= POL_HOP) {
+				const uint32_t fr = (home + d) & b.mask;
+				bool moved = false;
+				for (uint32_t j = POL_HOP - 1; j >= 1 && !moved; j--) {
+					const uint32_t h2 = (fr - j) & b.mask;
+					const uint32_t hop2 = b.fe[h2][3] >> POL_HOP_SHIFT;
+					for (uint32_t o = 0; o < j; o++) {
+						if (!((hop2 >> o) & 1u))
+							continue;
+						auto &src = b.fe[(h2 + o) & b.mask], &dst = b.fe[fr];
+						dst[0] = src[0];
+						dst[1] = src[1];
+						dst[2] = src[2];
+						dst[3] = (dst[3] & 0xFF000000u) | (src[3] & 0xFFFFFFu);
+						src[0] = src[1] = src[2] = 0;
+						src[3] &= 0xFF000000u;
+						b.fe[h2][3] = (b.fe[h2][3] & ~(1u << (POL_HOP_SHIFT + o))) | (1u << (POL_HOP_SHIFT + j));
+						d -= j - o;
+						moved = true;
+						break;
+					}
+				}
+				ok = moved;
+			}
+			if (!ok || d >= POL_HOP) {
 				ok = false;
 				break;
 			}

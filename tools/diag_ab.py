@@ -71,7 +71,10 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "pol_spk2": ("CGPU_POL_SLOTS_PER_KEY=2",),
             # the v6 pre-pass: addresses behind the direction flag (round 5's form)
             "v6_pre_nospec": ("CGPU_IPC6_SPEC=0",),
-            "v6_pre_q3": ("CGPU_DIAG_IPC6_PRE_Q=3",), "v6_pre_q4b": ("CGPU_DIAG_IPC6_PRE_Q=4",)}
+            "v6_pre_q3": ("CGPU_DIAG_IPC6_PRE_Q=3",), "v6_pre_q4b": ("CGPU_DIAG_IPC6_PRE_Q=4",),
+            # LB frontend slots per frontend (hopscotch, round 6): 2 = 32 MiB at config 5
+            "lb_fe4": ("CGPU_LB_SLOTS_PER_FE=4",), "lb_fe8": ("CGPU_LB_SLOTS_PER_FE=8",),
+            "lb_fe16": ("CGPU_LB_SLOTS_PER_FE=16",)}
 
 
 def build(names):
@@ -199,6 +202,26 @@ def _workload(conf):
             e.ct4_flush()
             e.classify_v4_ctlb(d, 1000, out=out)
         return make, step, n
+    if conf == "cascade":
+        # bench.py --config cascade: config 5 whole (XDP prefilter | 1M services)
+        cfg = synth.CONFIGS["cascade"]
+        T = synth.make_tables(**cfg)
+        S = synth.make_services(T, cfg["n_services"])
+        P = synth.make_prefilter4(T)
+        n = cfg["n_tuples"]
+        t = synth.add_prefilter_traffic(synth.add_service_traffic(synth.make_tuples(T, n), S), P)
+        del t["hash"]
+        d = synth.to_device(t, "cuda")
+        out = {"verdict": torch.empty(n, dtype=torch.int32, device="cuda"),
+               "identity": torch.empty(n, dtype=torch.int32, device="cuda"), "stage": None}
+
+        def make():
+            e = Engine(device=0, **T.engine_config(), lb_max_entries=len(S.keys))
+            synth.load_engine(e, T)
+            synth.load_services(e, S)
+            synth.load_prefilter4(e, P)
+            return e
+        return make, lambda e: e.classify_v4_cascade(d, out=out), n
     if conf == "frames":
         # bench.py --config frames: config-2 tuples as 64-byte frame slots;
         # CGPU_AB_SCHED = cgpu_config.schedule (8: the split header + classify passes; 0: the fused default)
