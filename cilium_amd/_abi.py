@@ -142,9 +142,15 @@ PROTOS = {
     "cgpu_classify_v6_lb": (i32, [vp, C.POINTER(TuplesV6), vp, vp, sz, vp, vp, vp, vp]),
     "cgpu_classify_v4_lb": (i32, [vp, C.POINTER(TuplesV4), vp, vp, sz, vp, vp, vp, vp]),
     "cgpu_classify_v4_cascade": (i32, [vp, C.POINTER(TuplesV4), vp, vp, sz, vp, vp, vp, vp]),
+    "cgpu_classify_v4_lb_host": (i32, [vp, C.POINTER(TuplesV4), vp, vp, sz, vp, vp, vp, vp]),
+    "cgpu_classify_v4_cascade_host": (i32, [vp, C.POINTER(TuplesV4), vp, vp, sz, vp, vp, vp, vp]),
+    "cgpu_classify_v6_host": (i32, [vp, C.POINTER(TuplesV6), sz, vp, vp, vp, vp]),
+    "cgpu_classify_v6_lb_host": (i32, [vp, C.POINTER(TuplesV6), vp, vp, sz, vp, vp, vp, vp]),
     "cgpu_lb4_select": (i32, [vp, i32, C.POINTER(Lb4Tuples), sz, C.POINTER(Lb4Out), vp]),
     "cgpu_prefilter_v4": (i32, [vp, vp, vp, vp, sz, vp, vp]),
     "cgpu_prefilter_v6": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+    "cgpu_prefilter_v4_host": (i32, [vp, vp, vp, vp, sz, vp, vp]),
+    "cgpu_prefilter_v6_host": (i32, [vp, vp, vp, vp, sz, vp, vp]),
     "cgpu_lxc_update": (i32, [vp, u32, vp]),
     "cgpu_lxc_delete": (i32, [vp, u32]),
     "cgpu_lxc_lookup": (i32, [vp, u32, vp]),

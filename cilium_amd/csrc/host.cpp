@@ -4629,14 +4629,19 @@ static int host_pipeline(cgpu_ctx *c, size_t n, const hs_cols &C, hipStream_t cs
 	return 0;
 }
 
-CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
-				      uint32_t *identity, uint8_t *stage, void *stream)
+/* the host-resident v4 paths: plain (lb 0), service-translated (lb 1) and
+ * the XDP prefilter cascade (lb 1, xdp 1); the service paths upload the hash
+ * column when there is one (it wins over sport in the kernel), else sport */
+static int v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, const uint16_t *sport, const uint32_t *hash, size_t n,
+		   int32_t *verdict, uint32_t *identity, uint8_t *stage, void *stream, int lb, int xdp)
 {
 	if (!c)
 		return fail(-EINVAL, "null context");
 	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
 			 !t->ep || !verdict || !identity)))
 		return fail(-EINVAL, "null tuple column or output");
+	if (lb && n && !hash && !sport)
+		return fail(-EINVAL, "either a hash or an sport column is needed");
 	if (c->device < 0)
 		return fail(-ENODEV, "context has no device (host-only); no CPU path");
 	if (!n)
@@ -4657,6 +4662,11 @@ CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size
 		C.in[k] = static_cast<const uint8_t *>(cols[k]);
 		C.in_el[k] = el[k];
 	}
+	if (lb) {
+		C.in[7] = hash ? reinterpret_cast<const uint8_t *>(hash) : reinterpret_cast<const uint8_t *>(sport);
+		C.in_el[7] = hash ? 4 : 2;
+		C.nin = 8;
+	}
 	C.nout = 3;
 	C.out[0] = reinterpret_cast<uint8_t *>(verdict);
 	C.out[1] = reinterpret_cast<uint8_t *>(identity);
@@ -4669,9 +4679,37 @@ CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size
 				   reinterpret_cast<const uint32_t *>(di[5]), reinterpret_cast<const uint16_t *>(di[6]),
 				   reinterpret_cast<int32_t *>(dout[0]), reinterpret_cast<uint32_t *>(dout[1]), dout[2],
 				   P.delta, (uint64_t)m, P.pk, 0, nullptr, nullptr};
+		if (lb) {
+			a.lb = 1;
+			a.xdp = xdp;
+			if (hash)
+				a.hash = reinterpret_cast<const uint32_t *>(di[7]);
+			else
+				a.sport = reinterpret_cast<const uint16_t *>(di[7]);
+		}
 		HIP_OR_EIO(launch_classify_v4(s, a, cs));
 		return 0;
 	});
+}
+
+CGPU_EXPORT int cgpu_classify_v4_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n, int32_t *verdict,
+				      uint32_t *identity, uint8_t *stage, void *stream)
+{
+	return v4_host(c, t, nullptr, nullptr, n, verdict, identity, stage, stream, 0, 0);
+}
+
+CGPU_EXPORT int cgpu_classify_v4_lb_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, const uint16_t *sport,
+					 const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+					 uint8_t *stage, void *stream)
+{
+	return v4_host(c, t, sport, hash, n, verdict, identity, stage, stream, 1, 0);
+}
+
+CGPU_EXPORT int cgpu_classify_v4_cascade_host(cgpu_ctx *c, const cgpu_tuples_v4 *t, const uint16_t *sport,
+					      const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+					      uint8_t *stage, void *stream)
+{
+	return v4_host(c, t, sport, hash, n, verdict, identity, stage, stream, 1, 1);
 }
 
 CGPU_EXPORT int cgpu_host_stage_release(cgpu_ctx *c)
@@ -4832,6 +4870,87 @@ CGPU_EXPORT int cgpu_classify_v6_lb(cgpu_ctx *c, const cgpu_tuples_v6 *t, const 
 }
 
 
+/* the host-resident v6 paths (plain and service-translated): 42 B of
+ * columns per tuple in, the x4 pre-pass scratch per chunk from the pool */
+static int v6_host(cgpu_ctx *c, const cgpu_tuples_v6 *t, const uint16_t *sport, const uint32_t *hash, size_t n,
+		   int32_t *verdict, uint32_t *identity, uint8_t *stage, void *stream, int lb)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (!t || (n && (!t->saddr || !t->daddr || !t->dport || !t->proto || !t->flags || !t->len ||
+			 !t->ep || !verdict || !identity)))
+		return fail(-EINVAL, "null tuple column or output");
+	if (lb && n && !hash && !sport)
+		return fail(-EINVAL, "either a hash or an sport column is needed");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device (host-only); no CPU path");
+	if (!n)
+		return 0;
+	std::lock_guard<std::mutex> g(c->host_mu);
+	Pinned P;
+	if (int r = pin(c, stream, P, true))
+		return r;
+	const cgpu_snapshot &s = P.snap();
+	const hipStream_t cs = (hipStream_t)stream;
+	hs_cols C;
+	C.nin = 7;
+	const void *cols[7] = {t->saddr, t->daddr, t->dport, t->proto, t->flags, t->len, t->ep};
+	static const size_t el[7] = {16, 16, 2, 1, 1, 4, 2};
+	for (int k = 0; k < 7; k++) {
+		C.in[k] = static_cast<const uint8_t *>(cols[k]);
+		C.in_el[k] = el[k];
+	}
+	if (lb) {
+		C.in[7] = hash ? reinterpret_cast<const uint8_t *>(hash) : reinterpret_cast<const uint8_t *>(sport);
+		C.in_el[7] = hash ? 4 : 2;
+		C.nin = 8;
+	}
+	C.nout = 3;
+	C.out[0] = reinterpret_cast<uint8_t *>(verdict);
+	C.out[1] = reinterpret_cast<uint8_t *>(identity);
+	C.out[2] = stage;
+	C.out_el[0] = C.out_el[1] = 4;
+	C.out_el[2] = 1;
+	const bool pre = !lb && s.ipc6.root && !(s.schedule & (CGPU_SCHED_PER_LANE | CGPU_SCHED_GLOBAL_CTR)) &&
+			 s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK;
+	return host_pipeline(c, n, C, cs, [&](size_t m, uint8_t *const *di, uint8_t *const *dout) -> int {
+		classify_v6_args a{di[0], di[1], reinterpret_cast<const uint16_t *>(di[2]), di[3], di[4],
+				   reinterpret_cast<const uint32_t *>(di[5]), reinterpret_cast<const uint16_t *>(di[6]),
+				   reinterpret_cast<int32_t *>(dout[0]), reinterpret_cast<uint32_t *>(dout[1]), dout[2],
+				   P.delta, (uint64_t)m, P.pk};
+		if (lb) {
+			a.lb = 1;
+			if (hash)
+				a.hash = reinterpret_cast<const uint32_t *>(di[7]);
+			else
+				a.sport = reinterpret_cast<const uint16_t *>(di[7]);
+		}
+		void *scr = nullptr;
+		if (pre)
+			HIP_OR_EIO(hipMallocFromPoolAsync(&scr, m * 4u, c->pool, cs));
+		a.ipc_e = static_cast<uint32_t *>(scr);
+		const hipError_t le = launch_classify_v6(s, a, cs);
+		if (scr)
+			HIP_OR_EIO(hipFreeAsync(scr, cs));
+		HIP_OR_EIO(le);
+		return 0;
+	});
+}
+
+CGPU_EXPORT int cgpu_classify_v6_host(cgpu_ctx *c, const cgpu_tuples_v6 *t, size_t n, int32_t *verdict,
+				      uint32_t *identity, uint8_t *stage, void *stream)
+{
+	return v6_host(c, t, nullptr, nullptr, n, verdict, identity, stage, stream, 0);
+}
+
+CGPU_EXPORT int cgpu_classify_v6_lb_host(cgpu_ctx *c, const cgpu_tuples_v6 *t, const uint16_t *sport,
+					 const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+					 uint8_t *stage, void *stream)
+{
+	return v6_host(c, t, sport, hash, n, verdict, identity, stage, stream, 1);
+}
+
+
 static int frames_check(cgpu_ctx *c, const cgpu_frames *f, size_t n)
 {
 	if (!f || (n && (!f->data || !f->len || !f->flags || !f->ep)))
@@ -4982,6 +5101,63 @@ CGPU_EXPORT int cgpu_prefilter_v6(cgpu_ctx *c, const uint8_t *saddr, const uint8
 	HIP_OR_EIO(hipSetDevice(c->device));
 	HIP_OR_EIO(launch_prefilter_v6(s, a, (hipStream_t)stream));
 	return 0;
+}
+
+/* the prefilters over host-resident columns (addresses, flags in; one
+ * verdict byte out) */
+static int prefilter_host(cgpu_ctx *c, const void *saddr, const void *daddr, const uint8_t *flags, size_t n,
+			  uint8_t *verdict, void *stream, int v6)
+{
+	if (!c)
+		return fail(-EINVAL, "null context");
+	if (n && (!saddr || !daddr || !flags || !verdict))
+		return fail(-EINVAL, "null column");
+	if (c->device < 0)
+		return fail(-ENODEV, "context has no device (host-only); no CPU path");
+	if (!n)
+		return 0;
+	std::lock_guard<std::mutex> g(c->host_mu);
+	Pinned P;
+	if (int r = pin(c, stream, P))
+		return r;
+	const cgpu_snapshot &s = P.snap();
+	const hipStream_t cs = (hipStream_t)stream;
+	const size_t ael = v6 ? 16 : 4;
+	hs_cols C;
+	C.nin = 3;
+	C.in[0] = static_cast<const uint8_t *>(saddr);
+	C.in[1] = static_cast<const uint8_t *>(daddr);
+	C.in[2] = flags;
+	C.in_el[0] = C.in_el[1] = ael;
+	C.in_el[2] = 1;
+	C.nout = 1;
+	C.out[0] = verdict;
+	C.out_el[0] = 1;
+	return host_pipeline(c, n, C, cs, [&](size_t m, uint8_t *const *di, uint8_t *const *dout) -> int {
+		prefilter_args a{nullptr, nullptr, nullptr, nullptr, di[2], dout[0], (uint64_t)m};
+		if (v6) {
+			a.saddr16 = di[0];
+			a.daddr16 = di[1];
+			HIP_OR_EIO(launch_prefilter_v6(s, a, cs));
+		} else {
+			a.saddr4 = reinterpret_cast<const uint32_t *>(di[0]);
+			a.daddr4 = reinterpret_cast<const uint32_t *>(di[1]);
+			HIP_OR_EIO(launch_prefilter_v4(s, a, cs));
+		}
+		return 0;
+	});
+}
+
+CGPU_EXPORT int cgpu_prefilter_v4_host(cgpu_ctx *c, const uint32_t *saddr, const uint32_t *daddr,
+				       const uint8_t *flags, size_t n, uint8_t *verdict, void *stream)
+{
+	return prefilter_host(c, saddr, daddr, flags, n, verdict, stream, 0);
+}
+
+CGPU_EXPORT int cgpu_prefilter_v6_host(cgpu_ctx *c, const uint8_t *saddr, const uint8_t *daddr,
+				       const uint8_t *flags, size_t n, uint8_t *verdict, void *stream)
+{
+	return prefilter_host(c, saddr, daddr, flags, n, verdict, stream, 1);
 }
 
 /* ======================================================================= */

@@ -436,28 +436,61 @@ class Engine:
                                       _stream(stream)), "cgpu_classify_v4")
         return out
 
-    def classify_v4_host(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
-        """cgpu_classify_v4_host: t holds HOST arrays (numpy, or CPU tensors
-        -- page-locked ones overlap the copies with the classify) with the
-        dtypes of classify_v4; outputs are host numpy arrays, complete when
-        `stream` is (the call synchronizes it before returning unless
-        out is given)."""
-        import numpy as np
-        n = len(t["saddr"])
+    @staticmethod
+    def _hptr(x):
+        if x is None:
+            return None
+        return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else x.ctypes.data)
 
-        def ptr(x):
-            if x is None:
-                return None
-            return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else x.ctypes.data)
+    def _host_call(self, fn, tv_cls, t, n, out, stage, stream, lb):
+        """The host-resident classify entry points: t holds HOST arrays
+        (numpy, or CPU tensors -- page-locked ones overlap the copies with
+        the classify) with the dtypes of the device call; outputs are host
+        numpy arrays, complete when `stream` is (the call synchronizes it
+        before returning unless out is given)."""
+        p = self._hptr
         given = out is not None
         if out is None:
             out = {"verdict": np.empty(n, np.int32), "identity": np.empty(n, np.uint32),
                    "stage": np.empty(n, np.uint8) if stage else None}
-        cols = [t[k] for k in ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")]
-        tv = TuplesV4(*[ptr(x).value for x in cols])
-        check(self.L.cgpu_classify_v4_host(self.h, C.byref(tv), n, ptr(out["verdict"]),
-                                           ptr(out["identity"]), ptr(out.get("stage")),
-                                           _stream(stream)), "cgpu_classify_v4_host")
+        tv = tv_cls(*[p(t[k]).value for k in ("saddr", "daddr", "dport", "proto", "flags", "len", "ep")])
+        lbargs = (p(t.get("sport")), p(t.get("hash"))) if lb else ()
+        check(getattr(self.L, fn)(self.h, C.byref(tv), *lbargs, n, p(out["verdict"]),
+                                  p(out["identity"]), p(out.get("stage")), _stream(stream)), fn)
+        if not given:
+            import torch
+            (stream or torch.cuda.current_stream()).synchronize()
+        return out
+
+    def classify_v4_host(self, t: dict, out: dict | None = None, stage: bool = True, stream=None):
+        """cgpu_classify_v4_host: classify_v4 over host arrays (_host_call)."""
+        return self._host_call("cgpu_classify_v4_host", TuplesV4, t, len(t["saddr"]), out, stage,
+                               stream, False)
+
+    def classify_v4_lb_host(self, t: dict, out: dict | None = None, stage: bool = True, stream=None,
+                            xdp: bool = False):
+        """cgpu_classify_v4_lb_host / cgpu_classify_v4_cascade_host (xdp):
+        classify_v4_lb over host arrays; t holds "hash" or "sport" too."""
+        fn = "cgpu_classify_v4_cascade_host" if xdp else "cgpu_classify_v4_lb_host"
+        return self._host_call(fn, TuplesV4, t, len(t["saddr"]), out, stage, stream, True)
+
+    def classify_v6_host(self, t: dict, out: dict | None = None, stage: bool = True, stream=None,
+                         lb: bool = False):
+        """cgpu_classify_v6_host / cgpu_classify_v6_lb_host (lb): classify_v6
+        over host arrays (saddr / daddr (n, 16) uint8, any alignment)."""
+        fn = "cgpu_classify_v6_lb_host" if lb else "cgpu_classify_v6_host"
+        return self._host_call(fn, TuplesV6, t, len(t["flags"]), out, stage, stream, lb)
+
+    def prefilter_host(self, saddr, daddr, flags, v6: bool = False, out=None, stream=None):
+        """cgpu_prefilter_v4_host / _v6_host over host arrays; returns the
+        verdict bytes (synchronizes `stream` unless out is given)."""
+        p = self._hptr
+        given = out is not None
+        if out is None:
+            out = np.empty(len(flags), np.uint8)
+        fn = "cgpu_prefilter_v6_host" if v6 else "cgpu_prefilter_v4_host"
+        check(getattr(self.L, fn)(self.h, p(saddr), p(daddr), p(flags), len(flags), p(out),
+                                  _stream(stream)), fn)
         if not given:
             import torch
             (stream or torch.cuda.current_stream()).synchronize()

@@ -558,6 +558,28 @@ int cgpu_classify_v6_lb(cgpu_ctx *ctx, const cgpu_tuples_v6 *t, const uint16_t *
 			const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
 			uint8_t *stage, void *stream);
 
+/*
+ * The HOST-resident forms of the service, cascade and IPv6 paths: the same
+ * arguments, results, counters and metrics as the device call of the same
+ * name without _host, with every column and output a host pointer, streamed
+ * through the staging of cgpu_classify_v4_host (same snapshot pinning, same
+ * error drain, same completion on `stream`).  The service forms upload the
+ * hash column when one is given (it wins over sport, as on the device), else
+ * sport.  The v6 address columns need no alignment here (the staging is
+ * aligned).  -ENODEV on a host-only context.
+ */
+int cgpu_classify_v4_lb_host(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, const uint16_t *sport,
+			     const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+			     uint8_t *stage, void *stream);
+int cgpu_classify_v4_cascade_host(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, const uint16_t *sport,
+				  const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+				  uint8_t *stage, void *stream);
+int cgpu_classify_v6_host(cgpu_ctx *ctx, const cgpu_tuples_v6 *t, size_t n, int32_t *verdict,
+			  uint32_t *identity, uint8_t *stage, void *stream);
+int cgpu_classify_v6_lb_host(cgpu_ctx *ctx, const cgpu_tuples_v6 *t, const uint16_t *sport,
+			     const uint32_t *hash, size_t n, int32_t *verdict, uint32_t *identity,
+			     uint8_t *stage, void *stream);
+
 /* Service translation alone (device pointers). */
 #define CGPU_LB_NETDEV 0 /* bpf_lb.c handle_ipv4 (bpf_lb.c:118-170) */
 #define CGPU_LB_LXC 1    /* lb4_local on the endpoint egress path (bpf_lxc.c:444-460) */
@@ -597,6 +619,11 @@ int cgpu_prefilter_v4(cgpu_ctx *ctx, const uint32_t *saddr, const uint32_t *dadd
 /* saddr/daddr: 16 bytes per packet, contiguous */
 int cgpu_prefilter_v6(cgpu_ctx *ctx, const uint8_t *saddr, const uint8_t *daddr,
 		      const uint8_t *flags, size_t n, uint8_t *verdict, void *stream);
+/* the prefilters over host-resident columns (as cgpu_classify_v4_host) */
+int cgpu_prefilter_v4_host(cgpu_ctx *ctx, const uint32_t *saddr, const uint32_t *daddr,
+			   const uint8_t *flags, size_t n, uint8_t *verdict, void *stream);
+int cgpu_prefilter_v6_host(cgpu_ctx *ctx, const uint8_t *saddr, const uint8_t *daddr,
+			   const uint8_t *flags, size_t n, uint8_t *verdict, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* raw Ethernet frames                               */

@@ -450,6 +450,32 @@ def test_host_batch_entry_errors():
                                     None) == -errno.EINVAL
     assert L_.cgpu_classify_v4_host(None, C.byref(tv), n, v.ctypes.data, i.ctypes.data, None,
                                     None) == -errno.EINVAL
+    # the service / cascade / v6 / prefilter host forms
+    sp = np.zeros(n, np.uint16)
+    a16 = np.zeros((n, 16), np.uint8)
+    from cilium_amd._abi import TuplesV6
+    tv6 = TuplesV6(*([a16.ctypes.data] * 2 + [c.ctypes.data for c in cols[2:]]))
+    for fn in ("cgpu_classify_v4_lb_host", "cgpu_classify_v4_cascade_host"):
+        f = getattr(L_, fn)
+        assert f(e.h, C.byref(tv), sp.ctypes.data, None, n, v.ctypes.data, i.ctypes.data, None,
+                 None) == -errno.ENODEV
+        assert f(e.h, C.byref(tv), None, None, n, v.ctypes.data, i.ctypes.data, None,
+                 None) == -errno.EINVAL
+    assert L_.cgpu_classify_v6_lb_host(e.h, C.byref(tv6), None, None, n, v.ctypes.data,
+                                       i.ctypes.data, None, None) == -errno.EINVAL
+    assert L_.cgpu_classify_v6_lb_host(e.h, C.byref(tv6), sp.ctypes.data, None, n, v.ctypes.data,
+                                       i.ctypes.data, None, None) == -errno.ENODEV
+    assert L_.cgpu_classify_v6_host(e.h, C.byref(tv6), n, v.ctypes.data, i.ctypes.data, None,
+                                    None) == -errno.ENODEV
+    assert L_.cgpu_classify_v6_host(e.h, C.byref(tv6), n, None, i.ctypes.data, None,
+                                    None) == -errno.EINVAL
+    pv = np.zeros(n, np.uint8)
+    assert L_.cgpu_prefilter_v4_host(e.h, cols[0].ctypes.data, cols[1].ctypes.data, cols[4].ctypes.data,
+                                     n, pv.ctypes.data, None) == -errno.ENODEV
+    assert L_.cgpu_prefilter_v6_host(e.h, a16.ctypes.data, a16.ctypes.data, None, n, pv.ctypes.data,
+                                     None) == -errno.EINVAL
+    assert L_.cgpu_prefilter_v6_host(e.h, a16.ctypes.data, a16.ctypes.data, None, 0, pv.ctypes.data,
+                                     None) == -errno.ENODEV
     e.close()
 
 
