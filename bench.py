@@ -359,8 +359,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    if args.host_tuples and args.config not in ("gpu", "frames"):
-        raise SystemExit("--host-tuples measures config 2 (--config gpu) and its raw frames (--config frames)")
+    if args.host_tuples and args.config not in ("gpu", "frames", "cascade", "v6", "pf6"):
+        raise SystemExit("--host-tuples measures the stateless paths: --config gpu, frames, cascade, v6, pf6")
     pf6 = args.config == "pf6"
     cascade = args.config == "cascade"
     frames = args.config == "frames"
@@ -453,7 +453,10 @@ def main():
     t0 = time.time()
     e.commit()
     log(f"[rank {rank}] commit {time.time() - t0:.2f}s, checksum {e.checksum():#x}")
-    if pf6:
+    if pf6 and args.host_tuples:
+        d = {k: torch.from_numpy(np.ascontiguousarray(v, np.uint8)).pin_memory() for k, v in tup.items()}
+        out = {"verdict": torch.empty(n, dtype=torch.uint8).pin_memory()}
+    elif pf6:
         d = synth.packets6_to_device(tup, dev)
         out = {"verdict": torch.empty(n, dtype=torch.uint8, device=dev)}
     elif frames and args.host_tuples:
@@ -474,10 +477,11 @@ def main():
     elif args.host_tuples:
         # the batch in page-locked HOST memory, outputs back into it: every
         # step uploads the columns and downloads the verdicts through
-        # cgpu_classify_v4_host (PCIe-inclusive)
-        view = {np.uint32: np.int32, np.uint16: np.int16, np.uint8: np.uint8}
-        d = {k: torch.from_numpy(np.ascontiguousarray(tup[k], dt).view(view[dt])).pin_memory()
-             for k, dt in synth.TUPLE_DTYPES.items() if k in tup}
+        # cgpu_classify_v4_host / _v4_cascade_host / _v6_host (PCIe-inclusive;
+        # DESIGN §6)
+        view = {np.uint32: np.int32, np.uint16: np.int16, np.uint8: np.uint8, np.int32: np.int32}
+        d = {k: torch.from_numpy(np.ascontiguousarray(v).view(view[v.dtype.type])).pin_memory()
+             for k, v in tup.items()}
         out = {"verdict": torch.empty(n, dtype=torch.int32).pin_memory(),
                "identity": torch.empty(n, dtype=torch.int32).pin_memory(), "stage": None}
     else:
@@ -530,10 +534,16 @@ def main():
             e.classify_v4_ctlb(d, now, out=out, stream=stream)
         elif ct:
             e.classify_v4_ct(d, now, out=out, stream=stream)
+        elif pf6 and args.host_tuples:
+            e.prefilter_host(d["saddr"], d["daddr"], d["flags"], v6=True, out=out["verdict"], stream=stream)
         elif pf6:
             e.prefilter_v6(d["saddr"], d["daddr"], d["flags"], out=out["verdict"], stream=stream)
+        elif cascade and args.host_tuples:
+            e.classify_v4_lb_host(d, out=out, stream=stream, xdp=True)
         elif cascade:
             e.classify_v4_cascade(d, out=out, stream=stream)
+        elif v6 and args.host_tuples:
+            e.classify_v6_host(d, out=out, stream=stream)
         elif v6:
             e.classify_v6(d, out=out, stream=stream)
         elif frames and args.host_tuples:
@@ -902,19 +912,19 @@ def main():
         if args.host_tuples:
             bw = link_rates(torch, dev)
             # bytes up / down per tuple (frames: the 64-byte slot + len, flags, ep)
-            per_in, per_out = (B_IN_FRAMES if frames else B_IN), B_OUT
+            per_in, per_out = b_in, b_out
             conf.update(host_tuples=True,
                         pcie_measured_gbs=bw,
                         numa={"gpu": gpu_numa_node(torch, dev),
                               "inputs": numa_nodes(d["data" if frames else "saddr"]),
                               "verdict": numa_nodes(out["verdict"]),
-                              "identity": numa_nodes(out["identity"])},
+                              "identity": numa_nodes(out["identity"]) if "identity" in out else None},
                         ingest_bound_mpps=round(min(bw["h2d"] * 1e3 / per_in, bw["d2h"] * 1e3 / per_out), 1),
                         hbm_resident_roofline=roof,
-                        note=(f"PCIe-inclusive: the {'frames (64-B slots + len, flags, ep: 71 B' if frames else 'columns (18 B'}"
-                              "/tuple) go up and the verdict + identity (8 B) come down every step through "
-                              "the device staging chunks; ingest_bound_mpps = the measured link rate over "
-                              "those bytes. The HBM-resident rate is the default line (no --host-tuples)"))
+                        note=(f"PCIe-inclusive: the {'frames (64-B slots + len, flags, ep' if frames else 'columns ('}"
+                              f"{per_in} B/tuple) go up and the outputs ({per_out} B/tuple) come down every "
+                              "step through the device staging chunks; ingest_bound_mpps = the measured link "
+                              "rate over those bytes. The HBM-resident rate is the default line (no --host-tuples)"))
             # the host line is bound by the link, both directions at once: the
             # floor is the slower direction's bytes at its measured rate
             t_s = ms_per_step * 1e-3
