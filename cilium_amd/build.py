@@ -108,7 +108,9 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str = LIB
         return LIB
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + (".o" if out == LIB else ".diag.o"))
+        # (diagnostic objects named after their library: parallel tool builds)
+        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] +
+                           (".o" if out == LIB else f".diag.{os.path.basename(out)}.o"))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
                *[f"-D{d}" for d in defines],

@@ -74,7 +74,11 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "v6_pre_q3": ("CGPU_DIAG_IPC6_PRE_Q=3",), "v6_pre_q4b": ("CGPU_DIAG_IPC6_PRE_Q=4",),
             # LB frontend slots per frontend (hopscotch, round 6): 2 = 32 MiB at config 5
             "lb_fe4": ("CGPU_LB_SLOTS_PER_FE=4",), "lb_fe8": ("CGPU_LB_SLOTS_PER_FE=8",),
-            "lb_fe16": ("CGPU_LB_SLOTS_PER_FE=16",)}
+            "lb_fe16": ("CGPU_LB_SLOTS_PER_FE=16",),
+            # conntrack walker: records in flight ahead (product 2; the
+            # generic ring measured 11.44-11.51 ms against 11.09, r6_k; the
+            # macro left the tree with the result)
+            }
 
 
 def build(names):
