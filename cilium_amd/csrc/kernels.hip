@@ -258,62 +258,6 @@ __device__ __forceinline__ bool xdp_pass4(const cgpu_snapshot &s, uint32_t sa, u
 	return set4_has(s.ep4, da);
 }
 
-/* xdp_pass4 for Q packets of one lane, stage by stage: the Q deny-set
- * gathers (the /16's pf4x half-nodes) together, then, for the packets the
- * deny set passed, the Q endpoint buckets' first 16 bytes (slots 0 and 1)
- * together; a /16 of more than 15 boundaries and a bucket the first two
- * slots do not decide take the per-packet path.  act false: pass[u] = true. */
-template <int Q>
-__device__ __forceinline__ void xdp4_q(const cgpu_snapshot &s, const bool (&act)[Q], const uint32_t (&sa)[Q],
-				       const uint32_t (&da)[Q], bool (&pass)[Q])
-{
-	const bool pf = s.pf4_enabled && s.pf4x;
-	bool chk[Q];
-	{
-		/* the /16's first half-node for every packet, then the second half
-		 * for the /16s of 8..15 boundaries (the same line) */
-		uint4 q[Q];
-		uint32_t c[Q];
-#pragma unroll
-		for (int u = 0; u < Q; u++)
-			q[u] = (act[u] && pf) ? s.pf4x[2u * (bswap32(sa[u]) >> 16)] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-		for (int u = 0; u < Q; u++)
-			c[u] = pf4x_below(q[u], bswap32(sa[u]) & 0xFFFFu, true) + (q[u].x & 1u);
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			const uint4 q2 = (q[u].x & PF4X_TWO) ? s.pf4x[2u * (bswap32(sa[u]) >> 16) + 1u] : make_uint4(0, 0, 0, 0);
-			if (q[u].x & PF4X_TWO)
-				c[u] += pf4x_below(q2, bswap32(sa[u]) & 0xFFFFu, false);
-		}
-#pragma unroll
-		for (int u = 0; u < Q; u++) {
-			bool deny = false;
-			if (act[u] && pf)
-				deny = (q[u].x & PF4X_OVF) ? lpmc_lookup(s.pf4c, s.pf4c.dict, sa[u]) != 0u : (c[u] & 1u) != 0u;
-			pass[u] = !deny;
-			chk[u] = act[u] && !deny;
-		}
-	}
-	uint4 b[Q];
-#pragma unroll
-	for (int u = 0; u < Q; u++)
-		b[u] = chk[u] ? reinterpret_cast<const uint4 *>(s.ep4.slots)[(size_t)(mix32(da[u], 0x5e7) & s.ep4.bucket_mask) * 4u]
-			      : make_uint4(0, 0, 0, 0);
-#pragma unroll
-	for (int u = 0; u < Q; u++) {
-		if (!chk[u])
-			continue;
-		/* slots 0 / 1 of the home bucket decide unless both are used and
-		 * neither holds da */
-		const uint4 w = b[u];
-		if (!w.y || w.x == da[u] || !w.w || w.z == da[u])
-			pass[u] = w.y && (w.x == da[u] || (w.w && w.z == da[u]));
-		else
-			pass[u] = set4_has(s.ep4, da[u]);
-	}
-}
-
 /* Resolve a 16-byte-key probe whose first bucket is loaded: returns the
  * slot's entry word (pad[0], nonzero for prefix sets) or 0 on a miss. */
 __device__ __forceinline__ uint32_t set16_resolve(const addr_set16 &t, uint4 k0, uint4 m0, uint4 k1, uint4 m1,
@@ -780,14 +724,22 @@ __device__ __forceinline__ lb_res lb4_one(const cgpu_snapshot &s, uint32_t sa, u
  * needs it leaves for lb4_one itself, so every decision is lb4_one's.  Only
  * what the classify cascade reads comes back: *drop (DROP_NO_SERVICE), the
  * translated tuple.daddr and dport.
+ * XDP (cgpu_classify_v4_cascade): the ingress tuples (xin, disjoint from act)
+ * take check_v4 in the same stages, so the prefilter adds no dependent round
+ * trip: their /16 deny node rides with the egress tuples' vip-bitmap words,
+ * their endpoint bucket (and a /16's second half-node) with the frontend
+ * slots; xpass[u] = XDP_PASS (true where !xin[u]).  Same decisions as
+ * xdp_pass4.
  */
-template <int Q>
+template <int Q, bool XDP = false>
 __device__ __forceinline__ void lb4_lxc_q(const cgpu_snapshot &s, const uint32_t *sa, uint32_t *da, uint32_t *dp,
-					  const uint32_t *proto, const uint32_t *h, const bool *act, bool *drop)
+					  const uint32_t *proto, const uint32_t *h, const bool *act, bool *drop,
+					  const bool *xin = nullptr, bool *xpass = nullptr)
 {
 	constexpr uint32_t NONE = 0, L4K = 1, L3K = 2, RETRY = 3, FOUND = 4, SLOW = 5;
 	const lb_table &t = s.lb;
 	const bool l4 = s.lb_flags & CGPU_LB_L4, l3 = s.lb_flags & CGPU_LB_L3;
+	const bool pf = XDP && s.pf4_enabled && s.pf4x;
 	uint32_t st[Q], kd[Q], home[Q];
 	uint4 f[Q];
 #pragma unroll
@@ -813,20 +765,86 @@ __device__ __forceinline__ void lb4_lxc_q(const cgpu_snapshot &s, const uint32_t
 		home[u] = lb_vip_bit(da[u]) & t.vip_mask;
 	}
 	/* no frontend has this address (tables.h lb_table.vip): every key of
-	 * lb4_lookup_service misses, the tuple is not load-balanced */
+	 * lb4_lookup_service misses, the tuple is not load-balanced.  XDP: the
+	 * ingress tuples' /16 deny nodes in the same stage (into f) */
 	uint32_t vw[Q];
 #pragma unroll
-	for (int u = 0; u < Q; u++)
+	for (int u = 0; u < Q; u++) {
 		vw[u] = st[u] != NONE ? t.vip[home[u] >> 5] : 0u;
+		if (XDP)
+			f[u] = (xin[u] && pf) ? s.pf4x[2u * (bswap32(sa[u]) >> 16)] : make_uint4(0, 0, 0, 0);
+	}
+	/* XDP: the first half-node's count (bit 0: parity) and what the rest of
+	 * the decision needs: XN_TWO the second half-node, XN_OVF the pf4c
+	 * lookup, XN_EP the endpoint bucket (the deny set passed, or may) */
+	constexpr uint32_t XN_TWO = 2u, XN_OVF = 4u, XN_EP = 8u;
+	uint32_t xc[Q];
+#pragma unroll
+	for (int u = 0; u < Q; u++) {
+		xc[u] = 0;
+		if (!XDP || !xin[u])
+			continue;
+		if (!pf) {
+			xc[u] = XN_EP;
+			continue;
+		}
+		const uint4 q = f[u];
+		if (q.x & PF4X_OVF) {
+			xc[u] = XN_OVF | XN_EP;
+			continue;
+		}
+		xc[u] = (pf4x_below(q, bswap32(sa[u]) & 0xFFFFu, true) + (q.x & 1u)) & 1u;
+		if (q.x & PF4X_TWO)
+			xc[u] |= XN_TWO | XN_EP;
+		else if (!(xc[u] & 1u))
+			xc[u] |= XN_EP;
+	}
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		if (!((vw[u] >> (home[u] & 31u)) & 1u))
 			st[u] = NONE;
 		home[u] = lb_hash(da[u], kd[u]) & t.fe_mask;
 	}
+	/* the frontend home slots; XDP: the ingress tuples' endpoint buckets
+	 * (first 16 B: slots 0 and 1) into f, their second half-nodes into x2 */
+	uint4 x2[XDP ? Q : 1];
 #pragma unroll
-	for (int u = 0; u < Q; u++)
+	for (int u = 0; u < Q; u++) {
+		if (XDP && xin[u]) {
+			f[u] = (xc[u] & XN_EP)
+				       ? reinterpret_cast<const uint4 *>(s.ep4.slots)[(size_t)(mix32(da[u], 0x5e7) & s.ep4.bucket_mask) * 4u]
+				       : make_uint4(0, 0, 0, 0);
+			x2[XDP ? u : 0] = (xc[u] & XN_TWO) ? s.pf4x[2u * (bswap32(sa[u]) >> 16) + 1u] : make_uint4(0, 0, 0, 0);
+			continue;
+		}
 		f[u] = st[u] != NONE ? t.fe[home[u]] : make_uint4(0, 0, 0, 0);
+	}
+	if constexpr (XDP) {
+#pragma unroll
+		for (int u = 0; u < Q; u++) {
+			xpass[u] = true;
+			if (!xin[u])
+				continue;
+			bool deny;
+			if (xc[u] & XN_OVF)
+				deny = lpmc_lookup(s.pf4c, s.pf4c.dict, sa[u]) != 0u;
+			else if (xc[u] & XN_TWO)
+				deny = ((xc[u] + pf4x_below(x2[u], bswap32(sa[u]) & 0xFFFFu, false)) & 1u) != 0u;
+			else
+				deny = (xc[u] & 1u) != 0u;
+			if (deny) {
+				xpass[u] = false;
+				continue;
+			}
+			/* check_v4_endpoint: slots 0 / 1 of the home bucket decide
+			 * unless both are used and neither holds da */
+			const uint4 w = f[u];
+			if (!w.y || w.x == da[u] || !w.w || w.z == da[u])
+				xpass[u] = w.y && (w.x == da[u] || (w.w && w.z == da[u]));
+			else
+				xpass[u] = set4_has(s.ep4, da[u]);
+		}
+	}
 #pragma unroll
 	for (int u = 0; u < Q; u++) {
 		if (st[u] == NONE)
@@ -2107,25 +2125,20 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 					if (!a.hash)
 						hh[u] = flow_hash(sa[u], da[u], sp[u], dport[u], proto[u]);
 				}
-				lb4_lxc_q<Q>(s, sa, da, dport, proto, hh, act, drop);
+				/* XDP (config 5 whole): the netdev's XDP prefilter (bpf_xdp.c
+				 * check_v4) before an ingress tuple reaches from_netdev
+				 * (bpf_netdev.c:470), in the service step's stages */
+				bool in[Q], pass[Q];
 #pragma unroll
 				for (int u = 0; u < Q; u++)
+					in[u] = XDP && !(fl[u] & 1u) && i0 + u < a.n;
+				lb4_lxc_q<Q, XDP>(s, sa, da, dport, proto, hh, act, drop, in, pass);
+#pragma unroll
+				for (int u = 0; u < Q; u++) {
 					if (drop[u])
 						lbf[u] = F_LBDROP;
-				if constexpr (XDP) {
-					/* config 5 whole: the netdev's XDP prefilter (bpf_xdp.c
-					 * check_v4) before an ingress tuple reaches from_netdev
-					 * (bpf_netdev.c:470); the egress tuples took the service
-					 * step above */
-					bool in[QA], pass[QA];
-#pragma unroll
-					for (int u = 0; u < QA; u++)
-						in[u] = u < Q && !(fl[u] & 1u) && i0 + u < a.n;
-					xdp4_q<QA>(s, in, sa, da, pass);
-#pragma unroll
-					for (int u = 0; u < Q; u++)
-						if (!pass[u])
-							lbf[u] = F_LBDROP | F_XDP;
+					if (XDP && !pass[u])
+						lbf[u] = F_LBDROP | F_XDP;
 				}
 			}
 #pragma unroll
@@ -3475,6 +3488,13 @@ static hipError_t launch_ipc6_pre(const cgpu_snapshot &s, const cls_args &a, hip
 	return hipGetLastError();
 }
 
+/* tuples per lane of the config-5 cascade kernel: 2 (its service step and
+ * prefilter share stages; at 4 the kernel spilled 19 VGPRs with the stages
+ * apart and 101 with them shared): 3.18 -> 3.02 ms per 64M tuples, of which
+ * sharing the stages 0.015 (profiles/r6_l/) */
+#ifndef CGPU_XDP_Q
+#define CGPU_XDP_Q 2
+#endif
 template <bool LB, bool V6, int FR = 0, bool IPCE = false, bool XDP = false>
 static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStream_t st,
 			    const frames_x4 &fx = frames_x4{})
@@ -3508,7 +3528,7 @@ static hipError_t launch_x4(const cgpu_snapshot &s0, const cls_args &a, hipStrea
 #ifdef CGPU_DIAG_V6_Q /* timing-only tool build (tools/diag_ab.py): v6 tuples per lane */
 	constexpr int Q = V6 && !IPCE ? CGPU_DIAG_V6_Q : 4;
 #else
-	constexpr int Q = V6 && !IPCE ? 2 : 4; /* in-kernel v6 lookups: the trie's line registers */
+	constexpr int Q = V6 && !IPCE ? 2 : XDP ? CGPU_XDP_Q : 4; /* in-kernel v6 lookups: the trie's line registers */
 #endif
 	const void *kern = (const void *)k_classify_x4<NT, true, Q, 1, LB, V6, FR, IPCE, XDP>;
 	static_assert(!FF || Q == 4, "fused frames: Q = 4");

@@ -75,6 +75,9 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             # LB frontend slots per frontend (hopscotch, round 6): 2 = 32 MiB at config 5
             "lb_fe4": ("CGPU_LB_SLOTS_PER_FE=4",), "lb_fe8": ("CGPU_LB_SLOTS_PER_FE=8",),
             "lb_fe16": ("CGPU_LB_SLOTS_PER_FE=16",),
+            # the cascade kernel's tuples per lane (product 2, r6_l; sep_q2 was
+            # the same define on the stages-apart source)
+            "xdp_q4": ("CGPU_XDP_Q=4",),
             # conntrack walker: records in flight ahead (product 2; the
             # generic ring measured 11.44-11.51 ms against 11.09, r6_k; the
             # macro left the tree with the result)
