@@ -198,6 +198,9 @@ def pmc_traffic(args):
     from cilium_amd.build import lib_identity
     if getattr(args, "host_tuples", False):
         return None, "not profiled: the host-resident line is bound by the host link", None
+    if getattr(args, "ct_persist", 0):
+        return None, ("not profiled: profiles/traffic_<config>.json measures the empty-map workload, "
+                      "not the steady state"), None
     tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if not os.path.exists(tj):
         return None, f"no PMC profile ({os.path.relpath(tj, ROOT)} absent)", None

@@ -27,4 +27,7 @@ case $1 in
     one ctlb6 600 --config ctlb6 --steps 20 --warmup 3;;
   host)
     for C in gpu frames cascade v6 pf6; do one ${C}hosttuples 400 --config $C --host-tuples --steps 5 --warmup 2 --no-cpu-baseline; done;;
+  persist)
+    one ct_persist4 600 --config ct --steps 20 --warmup 3 --ct-persist 4
+    one ct6_persist4 600 --config ct6 --steps 20 --warmup 3 --ct-persist 4;;
 esac
