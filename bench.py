@@ -144,8 +144,10 @@ WORKLOADS = {
 
 
 def link_rates(torch, dev, nbytes=1 << 30):
-    """Host <-> device copy rates over page-locked memory (GB/s), each
-    direction alone, best of 3: the link the host-resident line rides on."""
+    """Host <-> device copy rates over page-locked memory (GB/s), best of 3:
+    each direction alone, and "both": the two directions at once (equal
+    bytes on two streams, total bytes over the time) -- the link the
+    host-resident line rides on moves columns up and results down together."""
     h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     g = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     out = {}
@@ -158,7 +160,21 @@ def link_rates(torch, dev, nbytes=1 << 30):
             torch.cuda.synchronize()
             best = max(best, nbytes / (time.perf_counter() - t0) / 1e9)
         out[name] = round(best, 2)
-    del h, g
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    g2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s_up, s_down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    best = 0.0
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_up):
+            g.copy_(h, non_blocking=True)
+        with torch.cuda.stream(s_down):
+            h2.copy_(g2, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, 2 * nbytes / (time.perf_counter() - t0) / 1e9)
+    out["both"] = round(best, 2)
+    del h, g, h2, g2
     return out
 
 
@@ -922,21 +938,28 @@ def main():
                               "inputs": numa_nodes(d["data" if frames else "saddr"]),
                               "verdict": numa_nodes(out["verdict"]),
                               "identity": numa_nodes(out["identity"]) if "identity" in out else None},
-                        ingest_bound_mpps=round(min(bw["h2d"] * 1e3 / per_in, bw["d2h"] * 1e3 / per_out), 1),
+                        ingest_bound_mpps=round(min(bw["h2d"] * 1e3 / per_in, bw["d2h"] * 1e3 / per_out,
+                                                    bw["both"] * 1e3 / (per_in + per_out)), 1),
                         hbm_resident_roofline=roof,
                         note=(f"PCIe-inclusive: the {'frames (64-B slots + len, flags, ep' if frames else 'columns ('}"
                               f"{per_in} B/tuple) go up and the outputs ({per_out} B/tuple) come down every "
                               "step through the device staging chunks; ingest_bound_mpps = the measured link "
-                              "rate over those bytes. The HBM-resident rate is the default line (no --host-tuples)"))
-            # the host line is bound by the link, both directions at once: the
-            # floor is the slower direction's bytes at its measured rate
+                              "rates over those bytes (each direction alone, and both directions at once "
+                              "over their sum). The HBM-resident rate is the default line (no --host-tuples)"))
+            # the host line is bound by the link: each direction's bytes at
+            # its rate alone, and the bytes of both at the measured rate of
+            # the two directions at once; the largest floor binds
             t_s = ms_per_step * 1e-3
             t_up, t_down = n * per_in / (bw["h2d"] * 1e9), n * per_out / (bw["d2h"] * 1e9)
+            t_both = n * (per_in + per_out) / (bw["both"] * 1e9)
+            t_floor = max(t_up, t_down, t_both)
             roof = {"bound": "link", "achieved": round(n * (per_in + per_out) / t_s / 1e9, 2),
-                    "peak": round(n * (per_in + per_out) / max(t_up, t_down) / 1e9, 2), "unit": "GB/s",
-                    "frac": round(max(t_up, t_down) / t_s, 4),
+                    "peak": round(n * (per_in + per_out) / t_floor / 1e9, 2), "unit": "GB/s",
+                    "frac": round(t_floor / t_s, 4),
+                    "frac_one_direction": round(max(t_up, t_down) / t_s, 4),
                     "components": {"h2d": {"gbs": bw["h2d"], "frac": round(t_up / t_s, 4)},
-                                   "d2h": {"gbs": bw["d2h"], "frac": round(t_down / t_s, 4)}}}
+                                   "d2h": {"gbs": bw["d2h"], "frac": round(t_down / t_s, 4)},
+                                   "both": {"gbs": bw["both"], "frac": round(t_both / t_s, 4)}}}
         if pf6:
             conf.update(dyn6_prefixes=len(P.dyn6), fix6_prefixes=len(P.fix6),
                         endpoints=len(P.ep6))

@@ -4390,6 +4390,13 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
  * 256-aligned columns; a wider tuple (frames) takes fewer per chunk */
 #define HS_IN_BYTES ((size_t)HS_CHUNK * 18 + 8 * 256)
 #define HS_OUT_BYTES ((size_t)HS_CHUNK * 9 + 4 * 256)
+/* uploads of a batch whose columns are all narrower than this many bytes
+ * per tuple go by the runtime's DMA copies, the others (64-byte frame
+ * slots) by the CUs: tuples 2.15 -> 2.37 Gpps, v6 1.00 -> 1.08, pf6 1.56 ->
+ * 1.64, frames 0.68 -> 0.59 with DMA uploads (profiles/r6_m/) */
+#ifndef CGPU_HS_UP_DMA_BELOW
+#define CGPU_HS_UP_DMA_BELOW 64
+#endif
 #ifndef CGPU_HS_STORE
 #define CGPU_HS_STORE 1
 #endif
@@ -4497,11 +4504,12 @@ static void *host_mapped(const void *p, size_t bytes)
 }
 
 /* The pipeline of a host batch.  classify(m, din, dout) enqueues one chunk's
- * work on cs over device columns.  Page-locked, mapped columns are read and
- * written by the CUs, all columns of a chunk in one launch (a DMA copy's wait
- * on another stream's event, and in this runtime the copy itself, held the
- * issuing thread; a DMA download ran at a quarter of the link rate beside the
- * uploads, profiles/r4_ah); other columns are copied by the runtime.
+ * work on cs over device columns.  Page-locked, mapped output columns are
+ * written by the CUs, all columns of a chunk in one launch (a DMA download
+ * ran at a quarter of the link rate beside the uploads, profiles/r4_ah);
+ * mapped input columns are read by the CUs too when one of them is a 64-byte
+ * frame slot, else uploaded by the runtime's DMA copies (CGPU_HS_UP_DMA_BELOW);
+ * columns that are not page-locked are copied by the runtime.
  * Called with host_mu held. */
 template <typename F>
 static int host_pipeline(cgpu_ctx *c, size_t n, const hs_cols &C, hipStream_t cs, F &&classify)
@@ -4534,6 +4542,10 @@ static int host_pipeline(cgpu_ctx *c, size_t n, const hs_cols &C, hipStream_t cs
 	for (int k = 0; k < C.nout; k++)
 		dst_dev[k] = C.out[k] ? static_cast<uint8_t *>(host_mapped(C.out[k], n * C.out_el[k])) : nullptr;
 	auto aligned = [](const void *p) { return !(reinterpret_cast<uintptr_t>(p) & 15u); };
+	size_t widest = 0;
+	for (int k = 0; k < C.nin; k++)
+		widest = std::max(widest, C.in_el[k]);
+	const bool dma_up = widest < CGPU_HS_UP_DMA_BELOW;
 	/* one launch for the mapped columns; the others (and, should the launch
 	 * fail, those too) by the runtime's copy on the same stream */
 	auto move = [&](hipStream_t st, hipMemcpyKind kind, int ncol, void *const *dst, const void *const *src,
@@ -4545,7 +4557,8 @@ static int host_pipeline(cgpu_ctx *c, size_t n, const hs_cols &C, hipStream_t cs
 				continue;
 			void *dd = dst_mapped ? dst_mapped[col] : dst[col];
 			const void *ss = src_mapped ? src_mapped[col] : src[col];
-			if (CGPU_HS_STORE && dd && ss && aligned(dd) && aligned(ss)) {
+			const bool by_cu = kind == hipMemcpyDeviceToHost || !dma_up;
+			if (CGPU_HS_STORE && by_cu && dd && ss && aligned(dd) && aligned(ss)) {
 				which[d.n] = col;
 				d.seg[d.n++] = copy_seg{dd, ss, bytes[col]};
 				continue;

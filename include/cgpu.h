@@ -468,8 +468,9 @@ int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *
  * streams through device staging (up to 16 chunks of 4M tuples): uploads,
  * the classify of each chunk on `stream` and the stores of its outputs
  * overlap on queues of their own.  Returns once enqueued; the outputs are
- * complete when `stream` is (page-locked buffers are read and written by
- * the CUs; pageable ones are copied by the runtime and serialise).  Same results, counters
+ * complete when `stream` is (page-locked outputs are written by the CUs,
+ * page-locked inputs uploaded by DMA, or read by the CUs for 64-byte frame
+ * slots; pageable buffers are copied by the runtime and serialise).  Same results, counters
  * and metrics as cgpu_classify_v4 of the same tuples.  -ENODEV on a
  * host-only context, -EINVAL for a null column or output.
  */

@@ -78,6 +78,9 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             # the cascade kernel's tuples per lane (product 2, r6_l; sep_q2 was
             # the same define on the stages-apart source)
             "xdp_q4": ("CGPU_XDP_Q=4",),
+            # host staging uploads by the CUs for every batch (product: DMA
+            # below 64-B columns; r6_m measured DMA both ways as hs_up_dma)
+            "hs_up_cu": ("CGPU_HS_UP_DMA_BELOW=0",),
             # conntrack walker: records in flight ahead (product 2; the
             # generic ring measured 11.44-11.51 ms against 11.09, r6_k; the
             # macro left the tree with the result)
