@@ -4381,8 +4381,10 @@ CGPU_EXPORT int cgpu_classify_v4(cgpu_ctx *c, const cgpu_tuples_v4 *t, size_t n,
  * chunk k's columns go up on the h2d stream, its classify runs on the
  * caller's stream, its outputs come back on the d2h stream, so chunk k + 1's
  * upload and chunk k - 1's download overlap chunk k's classify. */
-#ifndef CGPU_HS_CHUNK_LOG2 /* tuples per staging chunk (timing-only A/B builds vary it) */
-#define CGPU_HS_CHUNK_LOG2 22
+/* tuples per staging chunk: 8M (4M: tuples 2.45 -> 2.52 Gpps, frames 0.68 ->
+ * 0.71, v6 1.10 -> 1.20; 16M 2.49, profiles/r6_m/host_ab_chunk*.log) */
+#ifndef CGPU_HS_CHUNK_LOG2
+#define CGPU_HS_CHUNK_LOG2 23
 #endif
 #define HS_CHUNK (1u << CGPU_HS_CHUNK_LOG2)
 #define HS_NBUF 16

@@ -465,7 +465,7 @@ int cgpu_classify_v4(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int32_t *
  * classifies each packet as the NIC hands it over, bpf_xdp.c:181-184 /
  * bpf_netdev.c:470; the engine takes batches that arrive in host memory
  * too): every column of t and the outputs are host pointers.  The batch
- * streams through device staging (up to 16 chunks of 4M tuples): uploads,
+ * streams through device staging (up to 16 chunks of 8M tuples): uploads,
  * the classify of each chunk on `stream` and the stores of its outputs
  * overlap on queues of their own.  Returns once enqueued; the outputs are
  * complete when `stream` is (page-locked outputs are written by the CUs,
@@ -481,7 +481,7 @@ int cgpu_classify_v4_host(cgpu_ctx *ctx, const cgpu_tuples_v4 *t, size_t n, int3
  * another thread while the chunks are queued does not split the batch.  On
  * an error after the first chunk was queued, the call waits for every copy
  * it queued (they read and write the caller's buffers) before returning.
- * The staging (up to 16 x ~109 MB of device memory) stays allocated for the
+ * The staging (up to 16 x ~227 MB of device memory) stays allocated for the
  * next host call: cgpu_host_stage_bytes reports it, cgpu_host_stage_release
  * waits for the host calls queued on it and frees it (cgpu_ctx_destroy does
  * too).

@@ -1,6 +1,6 @@
 """Host-resident batches (cgpu_classify_v4_host): the same tuples
 classified from host memory (pageable numpy arrays and page-locked tensors,
-several 4M-tuple chunks with a ragged last one; outputs into pageable arrays,
+several 8M-tuple chunks with a ragged last one; outputs into pageable arrays,
 downloaded, or page-locked ones, which the CUs store into except where a
 chunk's column is not 16-byte aligned) give exactly the verdicts,
 identities, stages, per-entry counters and metrics of cgpu_classify_v4 over
@@ -71,10 +71,10 @@ def test_host_batch_equals_device_batch(setup, pinned):
 
 
 def test_host_batch_past_staging(setup):
-    """A batch longer than the device staging (16 chunks of 4M tuples):
+    """A batch longer than the device staging (16 chunks of 8M tuples):
     chunk k + 16 reuses chunk k's buffers once its classify is queued."""
     torch, T, _ = setup
-    n = 16 * (1 << 22) + 4097
+    n = 16 * (1 << 23) + 4097
     t = synth.make_tuples(T, n)
     ed, eh = _engine(T), _engine(T)
     out = ed.classify_v4(synth.to_device(t), stage=False)
@@ -117,7 +117,7 @@ def _pin(torch, cols):
 
 
 def test_host_batch_vs_restatement_config2(config2):
-    """Config-2 tables, 9M + 4097 tuples from page-locked memory (three
+    """Config-2 tables, 9M + 4097 tuples from page-locked memory (two
     chunks, a ragged last one): verdicts, identities, stages and metrics
     equal the CPU restatement's (oracle/cgpu_oracle.c, pinned to the
     reference's golden vectors); the staging is reported and released."""
@@ -160,7 +160,7 @@ def test_frames_host_vs_device_and_restatement(config2, stride, pinned):
     from cilium_amd.engine import Engine
     rng = np.random.Generator(np.random.PCG64(0x40F7 + stride))
     pool = T.pfx_addr.astype(np.uint32).byteswap()
-    n = 2 * (1 << 20) + 333 if stride == 64 else (1 << 20) + 77
+    n = 4 * (1 << 20) + 333 if stride == 64 else 2 * (1 << 20) + 77  # two chunks each
     f = synth.make_frames(rng, n, width=stride, n_ep=T.n_endpoints, addr4=pool)
     info = L.lxc_info(synth.LXC_MAC, synth.LXC_IPV4_RAW, synth.LXC_IP6, 7)
 

@@ -69,7 +69,7 @@ def _same(got, dev, ref=None):
 @pytest.fixture(scope="module")
 def cfg_cascade():
     """Config-1 tables, 50k services, the config-5 deny set; 7M + 333 tuples
-    (three staging chunks with the hash column, 22 B per tuple)."""
+    (two staging chunks with the hash column, 22 B per tuple)."""
     from oracle import Oracle
     T = synth.make_tables(**synth.CONFIGS["cpu"])
     T.n_endpoints = 1
@@ -133,7 +133,7 @@ def test_prefilter_v4_host(torch_cuda, cfg_cascade):
 
 @pytest.fixture(scope="module")
 def cfg_v6():
-    """20k IPv6 prefixes, 20k v6 services; 4M + 5 tuples (three staging
+    """20k IPv6 prefixes, 20k v6 services; 4M + 5 tuples (two staging
     chunks at 42-46 B per tuple)."""
     from oracle import Oracle
     T = synth.make_tables6(n_prefixes=20_000, n_identities=500, n_endpoints=3, keys_per_ep=6000)
@@ -179,14 +179,14 @@ def test_v6_host(torch_cuda, cfg_v6, lb, layout):
 
 
 def test_prefilter_v6_host(torch_cuda):
-    """200k-prefix v6 deny set, 3M + 11 packets (two chunks at 33 B each),
+    """200k-prefix v6 deny set, 6M + 11 packets (two chunks at 33 B each),
     address rows at an odd offset."""
     from oracle import Oracle
 
     from cilium_amd.engine import Engine
     torch = torch_cuda
     P = synth.make_prefilter6(n_prefixes=200_000, n_roots=64, n_endpoints=512)
-    p = synth.make_packets6(P, 3 * (1 << 20) + 11)
+    p = synth.make_packets6(P, 6 * (1 << 20) + 11)
     o = Oracle(**P.oracle_config())
     synth.load_prefilter6(o, P)
     ref, _ = o.prefilter_v6(p["saddr"], p["daddr"], p["flags"], nthreads=16)

@@ -50,7 +50,7 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "v6_full_line": ("CGPU_V6T_FULL_LINE=1",),
             "hs_g256": ("CGPU_HS_COPY_G=256",), "hs_g512": ("CGPU_HS_COPY_G=512",),
             "hs_g64": ("CGPU_HS_COPY_G=64",), "hs_chunk23": ("CGPU_HS_CHUNK_LOG2=23",),
-            "hs_chunk21": ("CGPU_HS_CHUNK_LOG2=21",),
+            "hs_chunk21": ("CGPU_HS_CHUNK_LOG2=21",), "hs_chunk24": ("CGPU_HS_CHUNK_LOG2=24",),
             "ct_noret": ("CGPU_DIAG_NO_RET",), "ret_default": ("CGPU_DIAG_RET_DEFAULT",),
             "ct_ret_small": ("CGPU_DIAG_RET_SMALL",), "ct_ret_nt": ("CGPU_DIAG_RET_NT",),
             "walk_grid1024": ("CT_WALK_GRID=1024",), "walk_grid2048": ("CT_WALK_GRID=2048",), "walk_grid4096": ("CT_WALK_GRID=4096",),
