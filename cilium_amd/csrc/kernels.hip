@@ -1723,6 +1723,12 @@ struct ftuple {
  * SMAC / DMAC / SIP checks then read LDS, not a global load that would wait
  * behind the frame loads */
 #define FR_LXC_LDS 256u
+/* the x4 schedule's cold-slot atomics of a full quad go out behind the next
+ * quad's column loads: config 2 1.612 -> 1.592 ms, v6 2.688 -> 2.661
+ * (deferring the output stores as well: 2.08 ms, spills; profiles/r6_n/) */
+#ifndef CGPU_X4_DEFER_COLD
+#define CGPU_X4_DEFER_COLD 1
+#endif
 #ifndef CGPU_FF_H
 #define CGPU_FF_H 2 /* fused frames: slots loaded together (1, 2, 4) */
 #endif
@@ -1840,15 +1846,37 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 	__syncthreads();
 
 	const uint32_t lane = threadIdx.x & 63u;
+	/* CGPU_X4_DEFER_COLD: a quad's cold-slot atomics (into pk) are issued
+	 * after the next quad's column loads, so the wait for those loads does
+	 * not wait for them too (vmcnt retires in issue order) */
+	constexpr bool DEFER = CGPU_X4_DEFER_COLD && !FF && Q == 4;
+	uint32_t dcs[DEFER ? Q : 1], dln[DEFER ? Q : 1];
+#pragma unroll
+	for (int u = 0; u < (DEFER ? Q : 1); u++)
+		dcs[u] = 0xFFFFFFFFu, dln[u] = 0u;
+	auto defer_flush = [&]() {
+		if constexpr (DEFER) {
+#pragma unroll
+			for (int u = 0; u < Q; u++)
+				if (dcs[u] != 0xFFFFFFFFu) {
+					atomicAdd((unsigned long long *)&pk[dcs[u]], (1ull << PKC_SHIFT) | (unsigned long long)dln[u]);
+					dcs[u] = 0xFFFFFFFFu;
+				}
+		}
+	};
 	for (uint64_t g = t0;; g += T) {
 		/* FF: i0 = the wave's first frame, frame u of the lane at iu(u) */
 		const uint64_t i0 = FF ? wave_uniform64((g - lane) * Q) : g * Q;
 		/* FF: wave-uniform, every lane of the wave stages its part of the
 		 * tile; a lane past the batch carries no tuple (F_OK clear) */
 		const bool live = i0 < a.n;
-		if (!live)
+		if (!live) {
+			defer_flush();
 			break;
+		}
 		const bool full = FF ? false : i0 + Q <= a.n;
+		if (!full || Q != 4)
+			defer_flush(); /* (a full quad's go out behind its column loads) */
 		/* FF: a scalar base (i0 + 64 u) plus the lane */
 		auto iu = [&](int u) -> uint64_t { return FF ? (i0 + 64u * (uint32_t)u) + lane : i0 + (uint64_t)u; };
 		/* decode: hi4 = the policy key's upper word {dport, proto, egress}
@@ -2007,6 +2035,7 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 						    : ld_x4<NTL>(static_cast<const uint32_t *>(a.saddr) + i0);
 				const uint4 a4 = V6 ? make_uint4(0, 0, 0, 0)
 						    : ld_x4<NTL>(static_cast<const uint32_t *>(a.daddr) + i0);
+				defer_flush(); /* behind the loads just issued */
 				const uint32_t dd[4] = {d4.x & 0xFFFFu, d4.x >> 16, d4.y & 0xFFFFu, d4.y >> 16};
 				const uint32_t ee[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
 				const uint32_t ll[4] = {l4.x, l4.y, l4.z, l4.w};
@@ -2426,9 +2455,15 @@ __global__ __launch_bounds__(NT, MINW) void k_classify_x4(cgpu_snapshot s, cls_a
 							}
 						}
 					}
-					if (!done)
-						atomicAdd((unsigned long long *)&pk[c],
-							  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
+					if (!done) {
+						if constexpr (DEFER) {
+							dcs[u] = c;
+							dln[u] = len[u];
+						} else {
+							atomicAdd((unsigned long long *)&pk[c],
+								  (1ull << PKC_SHIFT) | (unsigned long long)len[u]);
+						}
+					}
 #endif
 				}
 				v[u] = st[u] == 2 ? 0 : (int32_t)(z[u] >> 16);

@@ -77,7 +77,7 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "lb_fe16": ("CGPU_LB_SLOTS_PER_FE=16",),
             # the cascade kernel's tuples per lane (product 2, r6_l; sep_q2 was
             # the same define on the stages-apart source)
-            "xdp_q4": ("CGPU_XDP_Q=4",),
+            "xdp_q4": ("CGPU_XDP_Q=4",), "no_defer_cold": ("CGPU_X4_DEFER_COLD=0",),
             # host staging uploads by the CUs for every batch (product: DMA
             # below 64-B columns; r6_m measured DMA both ways as hs_up_dma)
             "hs_up_cu": ("CGPU_HS_UP_DMA_BELOW=0",),
