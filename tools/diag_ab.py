@@ -78,6 +78,9 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             # the cascade kernel's tuples per lane (product 2, r6_l; sep_q2 was
             # the same define on the stages-apart source)
             "xdp_q4": ("CGPU_XDP_Q=4",), "no_defer_cold": ("CGPU_X4_DEFER_COLD=0",),
+            # (round 6 also measured the deferral on the two-tuples-per-lane
+            # cascade kernel, 2.931 -> 2.921 ms, and on the fused frames
+            # kernel, 2.46 -> 2.72 ms with spills: r6_n; neither kept)
             # host staging uploads by the CUs for every batch (product: DMA
             # below 64-B columns; r6_m measured DMA both ways as hs_up_dma)
             "hs_up_cu": ("CGPU_HS_UP_DMA_BELOW=0",),
