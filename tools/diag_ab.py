@@ -78,6 +78,8 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             # the cascade kernel's tuples per lane (product 2, r6_l; sep_q2 was
             # the same define on the stages-apart source)
             "xdp_q4": ("CGPU_XDP_Q=4",), "no_defer_cold": ("CGPU_X4_DEFER_COLD=0",),
+            # (the v6 pre-pass's entry stores deferred the same way measured
+            # 2.659 -> 2.650 ms, r6_o: not kept)
             # (round 6 also measured the deferral on the two-tuples-per-lane
             # cascade kernel, 2.931 -> 2.921 ms, and on the fused frames
             # kernel, 2.46 -> 2.72 ms with spills: r6_n; neither kept)
