@@ -224,3 +224,46 @@ def test_host_paths_errors(torch_cuda):
     assert e.L.cgpu_prefilter_v4_host(e.h, None, out, out, 4, out, None) == -errno.EINVAL
     assert e.L.cgpu_prefilter_v6_host(e.h, out, out, out, 0, out, None) == 0
     e.close()
+
+
+@pytest.mark.parametrize("n", [1, 63, 4097])
+def test_host_paths_small_batches(torch_cuda, cfg_cascade, cfg_v6, n):
+    """Batches smaller than a vector quad, a wave and a staging alignment
+    unit, through each host form (stage output omitted on one of them):
+    equal to the device calls over the same tuples."""
+    torch = torch_cuda
+    T, S, P, t, _ = cfg_cascade
+    t = {k: v[:n] for k, v in t.items()}
+    ed, eh = _engine4(T, S, P), _engine4(T, S, P)
+    dev = ed.classify_v4_lb(synth.to_device(t), xdp=True)
+    torch.cuda.synchronize()
+    got = eh.classify_v4_lb_host(_hostcols(torch, t, False), xdp=True)
+    _same(got, dev)
+    np.testing.assert_array_equal(eh.metrics(), ed.metrics())
+    sa, da, fl = (np.ascontiguousarray(t[k]) for k in ("saddr", "daddr", "flags"))
+    pv = eh.prefilter_host(sa, da, fl)
+    dv = ed.prefilter_v4(*(torch.from_numpy(x.view(VIEW[x.dtype.type])).cuda() for x in (sa, da, fl)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(pv, dv.cpu().numpy())
+    ed.close()
+    eh.close()
+    from cilium_amd.engine import Engine
+    T6, S6, t6, _ = cfg_v6
+    t6 = {k: v[:n] for k, v in t6.items()}
+
+    def engine():
+        e = Engine(device=0, **T6.engine_config(), lb_max_entries=len(S6.keys))
+        synth.load_engine(e, T6)
+        synth.load_services6(e, S6)
+        e.commit()
+        return e
+    ed, eh = engine(), engine()
+    dev = ed.classify_v6(synth.to_device(t6), stage=False)
+    torch.cuda.synchronize()
+    got = eh.classify_v6_host(_hostcols(torch, t6, True), stage=False)
+    np.testing.assert_array_equal(got["verdict"], dev["verdict"].cpu().numpy())
+    np.testing.assert_array_equal(got["identity"], dev["identity"].cpu().numpy().view(np.uint32))
+    assert got["stage"] is None
+    np.testing.assert_array_equal(eh.metrics(), ed.metrics())
+    ed.close()
+    eh.close()
