@@ -78,6 +78,10 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             # the cascade kernel's tuples per lane (product 2, r6_l; sep_q2 was
             # the same define on the stages-apart source)
             "xdp_q4": ("CGPU_XDP_Q=4",), "no_defer_cold": ("CGPU_X4_DEFER_COLD=0",),
+            # (group-default conntrack results, the walker storing only the
+            # results that differ from its group's orientation default and the
+            # finish resolving the rest from a 2-MiB bitmap: ct 10.95 -> 10.73
+            # ms, r6_p; the source change is r6_p/ct_dflt_experiment.patch)
             # (the v6 pre-pass's entry stores deferred the same way measured
             # 2.659 -> 2.650 ms, r6_o: not kept)
             # (round 6 also measured the deferral on the two-tuples-per-lane
