@@ -433,3 +433,55 @@ def test_ct_lru_evicts_instead_of_failing(torch_cuda, cfg_ct, v6):
             # batch runs, so evictions start a little before the map is full)
             assert len(gone) > 300
     e.close()
+
+
+def test_ct_lru_many_batches_gc_compaction(torch_cuda, cfg_ct):
+    """LRU mode over eight batches of fresh connections into a CT_MAP_SIZE-
+    4096 map, a device GC between some of them: evictions and GC deletes
+    leave tombstones until a batch compacts the map on the device
+    (cgpu_ct_stats); every batch still gets exactly the restatement's
+    results from the map it found, never DROP_CT_CREATE_FAILED, and only
+    untouched entries disappear."""
+    from oracle import Oracle
+    T, _, _, _ = cfg_ct
+    ct_max = 1 << 12
+    streams = [synth.make_ct_workload(T, 1_200, seed=60 + b, mean_pkts=5.0, span=0.9) for b in range(8)]
+    seclabels = streams[0][2]
+    e = _engine(**T.engine_config(), ct_max=ct_max, ct_lru=1)
+    synth.load_engine(e, T)
+    for _, _, sl in streams:
+        synth.load_lxc(e, sl)
+    e.commit()
+    for bi, (tt, _, sl) in enumerate(streams):
+        now = 1000 + 20 * bi
+        if bi == 3:
+            e.ct4_gc(now)  # RemoveExpired: the expired entries of early batches
+        if bi == 5:
+            e.ct4_gc(now + 100_000)  # everything: tombstones past a quarter of the slots
+        pre_k, pre_v = e.ct4_dump()
+        o = Oracle(**T.oracle_config())
+        synth.load_oracle(o, T)
+        for _, _, sl2 in streams:
+            synth.load_lxc(o, sl2)
+        o.ct_set_max(1 << 20)
+        for k, v in zip(pre_k, pre_v):
+            assert o.ct4_update(k, v) == 0
+        out = e.classify_v4_ct(synth.to_device(tt), now)
+        torch_cuda.cuda.synchronize()
+        v0, cr0, i0, _, _ = o.classify_v4_ct(tt, now)
+        v = out["verdict"].cpu().numpy()
+        assert not (v == L.DROP_CT_CREATE_FAILED).any(), f"batch {bi}"
+        np.testing.assert_array_equal(v, v0, err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(out["ct_ret"].cpu().numpy(), cr0, err_msg=f"batch {bi}")
+        np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
+        assert e.ct4_count() <= ct_max
+        gk, gv = e.ct4_dump()
+        ok_, ov = o.ct4_dump()
+        gb = {a.tobytes(): b.tobytes() for a, b in zip(gk, gv)}
+        ob = {a.tobytes(): b.tobytes() for a, b in zip(ok_, ov)}
+        pre = {a.tobytes(): b.tobytes() for a, b in zip(pre_k, pre_v)}
+        for kk, vv in gb.items():
+            assert ob.get(kk) == vv
+        assert all(kk in pre and ob[kk] == pre[kk] for kk in set(ob) - set(gb))
+    assert e.ct_stats(False)["compactions"] >= 1
+    e.close()
