@@ -189,6 +189,42 @@ def test_classify_v4_cascade_scale_vs_oracle(torch_cuda, variant, monkeypatch):
     e.close()
 
 
+@pytest.mark.parametrize("fix_on", [1, 0])
+def test_classify_v4_cascade_filter_maps_off(torch_cuda, fix_on):
+    """The cascade with the dyn4 LPM map disabled (cgpu_config.prefilter_dyn4
+    = 0, the agent's PreFilter without the dyn map) and, second, the fix4
+    map too: the XDP stage then checks only what remains (bpf_xdp.c:97-121
+    under CIDR4_LPM_PREFILTER / CIDR4_FILTER), against the restatement
+    configured the same way; schedule x4, 256k tuples."""
+    from oracle import Oracle
+    torch = torch_cuda
+    T = synth.make_tables(**synth.CONFIGS["cpu"])
+    T.n_endpoints = 1
+    S = synth.make_services(T, 20_000)
+    P = synth.make_prefilter4(T)
+    t = synth.add_prefilter_traffic(synth.add_service_traffic(synth.make_tuples(T, (1 << 18) + 7), S), P,
+                                    deny_frac=0.2)
+    o = Oracle(**T.oracle_config(), dyn4=0, fix4=fix_on)
+    synth.load_oracle(o, T)
+    synth.load_services(o, S)
+    synth.load_prefilter4(o, P)
+    v0, i0, s0, _ = o.classify_v4_cascade(t, nthreads=8)
+    e = _engine(**T.engine_config(), lb_max_entries=len(S.keys), prefilter_dyn4=0, prefilter_fix4=fix_on)
+    synth.load_engine(e, T)
+    synth.load_services(e, S)
+    synth.load_prefilter4(e, P)
+    e.commit()
+    out = e.classify_v4_cascade(synth.to_device(t))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["verdict"].cpu().numpy(), v0)
+    np.testing.assert_array_equal(out["identity"].cpu().numpy().view(np.uint32), i0)
+    np.testing.assert_array_equal(out["stage"].cpu().numpy(), s0)
+    np.testing.assert_array_equal(e.metrics(), o.metrics())
+    # the stray destinations still drop at check_v4_endpoint
+    assert (v0 == L.VERDICT_XDP_DROP).sum() > 500
+    e.close()
+
+
 @pytest.fixture(scope="module")
 def cfg_lb():
     T = synth.make_tables(**synth.CONFIGS["cpu"])
