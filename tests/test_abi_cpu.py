@@ -261,8 +261,14 @@ def test_ct_map_semantics():
     keys, vals = e.ct4_dump()
     assert len(keys) == 8 and sorted(keys["daddr"].tolist()) == sorted(
         [0x0A000001 + i for i in (0, 1, 3, 4, 5, 6, 7, 8)])
+    assert e.ct_stats(False)["live"] == 8
     assert e.ct4_gc(104) == 3  # lifetimes 100, 101, 103
     assert e.ct4_count() == 5
+    # cgpu_ct_stats: the live count; the host GC rebuilt the table (no
+    # tombstones left), and compaction counts only device compactions
+    st = e.ct_stats(False)
+    assert st["live"] == 5 and st["tombstones"] == 0 and st["compactions"] == 0
+    assert e.ct_stats(True) == {"live": 0, "tombstones": 0, "compactions": 0}
     assert sorted(e.ct4_dump()[1]["lifetime"].tolist()) == [104, 105, 106, 107, 107]
     e.ct4_flush()
     assert e.ct4_count() == 0 and len(e.ct4_dump()[0]) == 0
