@@ -4242,6 +4242,25 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_RELX 1024u    /* grouped by connection in phase 1: the ICMP entry a create
 			   * writes is reserved and owed to phase 2 */
 #define CT_RELP 0x20u     /* walker -> phase 2: the ICMP entry of this create is owed */
+/* Group-default results (CGPU_CT_DFLT, the plain IPv4 path): the prep marks
+ * every packet's result CT_DFLT; the phase-1 walker stores only the results
+ * that differ from their group's default -- ESTABLISHED for a packet of the
+ * orientation the group's first decided packet created or found its entry in,
+ * REPLY for the other -- and sets the group's bit in dmap for orientation 1;
+ * the finish resolves CT_DFLT from the record's key and dmap.  Exact for any
+ * mix of connections in a group: a packet whose result is not the default is
+ * stored.  Saves most of the walker's scattered result stores (A/B on
+ * --config ct: 10.95 -> 10.73 ms, profiles/r6_p/). */
+#define CT_DFLT 0x10u
+#ifndef CGPU_CT_DFLT
+#define CGPU_CT_DFLT 1
+#endif
+/* a packet's orientation (any fixed function of its key) and its group key,
+ * as k_ct_prep_q computed it (ct_conn_group over the record's tuple) */
+__device__ __forceinline__ uint32_t ct4_orient(const uint4 &k)
+{
+	return (k.y < k.x || (k.y == k.x && (k.z & 0xFFFFu) < (k.z >> 16))) ? 1u : 0u;
+}
 #define CTB_LB_LOOPBACK 8u /* struct ct_entry lb_loopback (common.h:389) */
 #define TUPLE_F_SERVICE 4u /* conntrack.h:66 */
 /* rec word 2 .w of the service path: lb_loopback | address-entry mode << 1 */
@@ -4763,6 +4782,10 @@ struct ct_args {
 	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
 	uint8_t *pcls;               /* [n] service path: phase-2 class, PCL_* (k_ct_prep) */
 	uint64_t *pk;                /* packed per-slot counters (k_ct_finish, k_unpack) */
+	/* CGPU_CT_DFLT (plain IPv4 path): per connection group, its default
+	 * result orientation, a bitmap indexed by the group key & gmask */
+	uint32_t *dmap;
+	uint32_t gmask;
 };
 
 /* One packet's record, written by k_ct_prep{,6} and read by the walker and
@@ -5224,6 +5247,8 @@ __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 				}
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
+			if (CGPU_CT_DFLT && a.dmap)
+				a.ct_ret[i] = CT_DFLT; /* the walker stores only non-default results */
 			a.identity[i] = id;
 			uint4 *r = a.rec + 2u * i;
 			r[0] = uint4{da[u], sa[u], z[u], pr[u] | (tfl[u] << 8) | (m << 16)};
@@ -6602,6 +6627,7 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 #endif
 	using R = std::conditional_t<MODE == WALK_SVC, std::conditional_t<K::V6 != 0, ct_srec6, ct_srec>,
 				     ct_rec<K>>;
+	constexpr bool DFLT = CGPU_CT_DFLT && MODE == WALK_PKT && std::is_same<K, CtK4>::value;
 	__shared__ int s_acct[3];
 	/* each lane's last CT_RETB results (packet index, ct result), stored
 	 * together: a scattered 1-byte store is a memory-side write whose
@@ -6653,6 +6679,9 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {
 		const uint64_t p0 = a.gpos[h];
 		const uint64_t p1 = p0 + a.glen[h];
+		/* CGPU_CT_DFLT: the group's default orientation (-1: not yet) */
+		int gb = -1;
+		uint32_t gkk = 0u;
 		/* packets in batch order through the sort permutation, software-
 		 * pipelined: the record of p + 1 and the index of p + 2 are in
 		 * flight while packet p runs */
@@ -6722,6 +6751,18 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 				if (ret == ((meta & CTM_EGRESS) ? CT_ESTABLISHED : CT_REPLY))
 					continue;
 #endif
+				if constexpr (DFLT) {
+					if (a.dmap) {
+						const uint4 kk = r.key();
+						const uint32_t o = ct4_orient(kk);
+						if (gb < 0 && ret <= CT_REPLY) {
+							gb = (int)(ret == CT_REPLY ? o ^ 1u : o);
+							gkk = ct_conn_group(ct_group(kk.y, kk.x), kk.z, kk.w & 0xFFu) & a.gmask;
+						}
+						if (gb >= 0 && ret == (o == (uint32_t)gb ? CT_ESTABLISHED : CT_REPLY))
+							continue; /* the group default: nothing stored */
+					}
+				}
 				s_ri[nret][threadIdx.x] = i;
 				s_rr[nret][threadIdx.x] = (uint8_t)ret;
 				if (++nret == CT_RETB)
@@ -6729,6 +6770,8 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 			}
 		}
 		ctc_flush(T, c);
+		if (DFLT && gb == 1 && a.dmap)
+			atomicOr(&a.dmap[gkk >> 5], 1u << (gkk & 31u));
 	}
 	ret_flush();
 #ifdef CGPU_DIAG_WALK_CLOCK
@@ -6799,8 +6842,17 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 			act[u] = i < hi;
 			const uint64_t j = act[u] ? i : 0u;
 			/* batch order: records and the walker's results stream in */
-			q[u] = ct_rec<K>::load(a.rec, (uint32_t)j, true).pkt();
+			const ct_rec<K> rr = ct_rec<K>::load(a.rec, (uint32_t)j, true);
+			q[u] = rr.pkt();
 			c[u] = ntl(a.ct_ret + j) & ~(CT_ADDRP | CT_RELP);
+			if constexpr (CGPU_CT_DFLT && std::is_same<K, CtK4>::value) {
+				if (c[u] == CT_DFLT) { /* the group default (the walker stored nothing) */
+					const uint4 kk = rr.key();
+					const uint32_t g = ct_conn_group(ct_group(kk.y, kk.x), kk.z, kk.w & 0xFFu) & a.gmask;
+					const uint32_t b = (a.dmap[g >> 5] >> (g & 31u)) & 1u;
+					c[u] = ct4_orient(kk) == b ? CT_ESTABLISHED : CT_REPLY;
+				}
+			}
 			ep[u] = ntl(a.ep + j);
 			eg[u] = q[u].meta & CTM_EGRESS;
 			frag[u] = q[u].meta & CTM_FRAG;
@@ -7151,6 +7203,7 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.f2 = L.flags2;
 	a.pcls = L.pcls;
 	a.pk = L.pk;
+	a.dmap = L.dmap;
 	return a;
 }
 
@@ -7386,6 +7439,14 @@ template <class K>
 static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
 {
 	ct_args a = ct_args_of(L);
+	/* the group-default results (CT_DFLT): the plain IPv4 path, group keys
+	 * of at most 24 bits (a 2-MiB bitmap); otherwise every result stored */
+	{
+		const int bits = ct_sort_bits(s);
+		a.gmask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+		if (!CGPU_CT_DFLT || K::V6 || bits > 24)
+			a.dmap = nullptr;
+	}
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	if (K::V6) {
 		/* the ipcache lookups through the trie pre-pass (its entries into
@@ -7421,6 +7482,8 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	uint32_t nh;
 	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st, K::V6 != 0);
 	if (e != hipSuccess)
+		return e;
+	if (a.dmap && (e = hipMemsetAsync(a.dmap, 0, ((size_t)a.gmask + 32u) / 32u * 4u, st)) != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<K>(s, T, L, a, st)) != hipSuccess)

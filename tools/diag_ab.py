@@ -77,7 +77,7 @@ VARIANTS = {"product": (), "no_cold_atomics": ("CGPU_DIAG_NO_COLD",),
             "lb_fe16": ("CGPU_LB_SLOTS_PER_FE=16",),
             # the cascade kernel's tuples per lane (product 2, r6_l; sep_q2 was
             # the same define on the stages-apart source)
-            "xdp_q4": ("CGPU_XDP_Q=4",), "no_defer_cold": ("CGPU_X4_DEFER_COLD=0",),
+            "xdp_q4": ("CGPU_XDP_Q=4",), "no_defer_cold": ("CGPU_X4_DEFER_COLD=0",), "no_ct_dflt": ("CGPU_CT_DFLT=0",),
             # (group-default conntrack results, the walker storing only the
             # results that differ from its group's orientation default and the
             # finish resolving the rest from a 2-MiB bitmap: ct 10.95 -> 10.73
