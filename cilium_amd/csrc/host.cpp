@@ -1974,7 +1974,6 @@ struct cgpu_ctx {
 	CtMap ct4, ct6;
 	void *d_ct_scratch = nullptr;
 	uint64_t *d_ct_pk = nullptr; /* the conntrack finish's packed counters (k_unpack re-zeroes) */
-	uint32_t *d_ct_dmap = nullptr; /* the plain IPv4 walk's group-default bitmap (2^24 bits) */
 	/* host-resident batches (cgpu_classify_v4_host / _frames_host): device
 	 * staging for up to HS_NBUF chunks (grown to the largest batch seen,
 	 * freed by cgpu_host_stage_release), one stream per direction */
@@ -2282,7 +2281,6 @@ CGPU_EXPORT void cgpu_ctx_destroy(cgpu_ctx *c)
 		}
 		(void)hipFree(c->d_ct_scratch);
 		(void)hipFree(c->d_ct_pk);
-		(void)hipFree(c->d_ct_dmap);
 		host_stage_free(c);
 		(void)hipEventDestroy(c->ct_done);
 		(void)hipStreamDestroy(c->ct_stream);
@@ -6049,12 +6047,7 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.temp_bytes = L.temp_bytes;
 	a.flags2 = b + L.flags2;
 	a.pk = c->d_ct_pk;
-	a.dmap = nullptr;
-	if (!svc && !m.v6) {
-		if (!c->d_ct_dmap)
-			HIP_OR_EIO(hipMalloc((void **)&c->d_ct_dmap, (size_t)1u << 21));
-		a.dmap = c->d_ct_dmap;
-	}
+	a.dflt = !svc && !m.v6; /* group-default results (kernels.hip CT_DFLT) */
 	hipError_t le;
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);

@@ -4243,14 +4243,18 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 			   * writes is reserved and owed to phase 2 */
 #define CT_RELP 0x20u     /* walker -> phase 2: the ICMP entry of this create is owed */
 /* Group-default results (CGPU_CT_DFLT, the plain IPv4 path): the prep marks
- * every packet's result CT_DFLT; the phase-1 walker stores only the results
- * that differ from their group's default -- ESTABLISHED for a packet of the
- * orientation the group's first decided packet created or found its entry in,
- * REPLY for the other -- and sets the group's bit in dmap for orientation 1;
- * the finish resolves CT_DFLT from the record's key and dmap.  Exact for any
- * mix of connections in a group: a packet whose result is not the default is
- * stored.  Saves most of the walker's scattered result stores (A/B on
- * --config ct: 10.95 -> 10.73 ms, profiles/r6_p/). */
+ * every packet's result CT_DFLT.  A packet's orientation is a fixed function
+ * of its tuple that flips for the reversed tuple and is 0 for the usual
+ * initiator (ephemeral source port above the service port; an ICMP echo
+ * request).  When the group's first decided packet created or found its
+ * entry in orientation 0 (ESTABLISHED / NEW for orientation 0, REPLY for 1),
+ * the phase-1 walker stores none of the group's results that equal the
+ * orientation default -- ESTABLISHED for orientation 0, REPLY for 1 -- and
+ * the finish resolves CT_DFLT from the record's tuple alone.  Groups of the
+ * other orientation store every result.  Exact for any mix of connections
+ * in a group: a packet whose result is not the default is stored.  Saves
+ * most of the walker's scattered result stores with no lookup in the
+ * finish (a group bitmap read there cost 0.27 ms: profiles/r6_p/, r7_a/). */
 #define CT_DFLT 0x10u
 #ifndef CGPU_CT_DFLT
 #define CGPU_CT_DFLT 1
@@ -4259,7 +4263,18 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
  * as k_ct_prep_q computed it (ct_conn_group over the record's tuple) */
 __device__ __forceinline__ uint32_t ct4_orient(const uint4 &k)
 {
-	return (k.y < k.x || (k.y == k.x && (k.z & 0xFFFFu) < (k.z >> 16))) ? 1u : 0u;
+	/* k = {daddr, saddr, sport | dport << 16, proto | ...}: TCP / UDP ports
+	 * in network order, the ICMP id / type word as ct_lookup4 builds it */
+	uint32_t sp = k.z & 0xFFFFu, dp = k.z >> 16;
+	if ((k.w & 0xFFu) != 1u) {
+		sp = __builtin_bswap16((uint16_t)sp);
+		dp = __builtin_bswap16((uint16_t)dp);
+		if (sp != dp)
+			return sp < dp ? 1u : 0u; /* the initiator's source port is the higher */
+	} else if (sp != dp) {
+		return sp > dp ? 1u : 0u; /* an echo request carries its type as dport */
+	}
+	return k.y < k.x ? 1u : 0u;
 }
 #define CTB_LB_LOOPBACK 8u /* struct ct_entry lb_loopback (common.h:389) */
 #define TUPLE_F_SERVICE 4u /* conntrack.h:66 */
@@ -4782,10 +4797,7 @@ struct ct_args {
 	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
 	uint8_t *pcls;               /* [n] service path: phase-2 class, PCL_* (k_ct_prep) */
 	uint64_t *pk;                /* packed per-slot counters (k_ct_finish, k_unpack) */
-	/* CGPU_CT_DFLT (plain IPv4 path): per connection group, its default
-	 * result orientation, a bitmap indexed by the group key & gmask */
-	uint32_t *dmap;
-	uint32_t gmask;
+	uint32_t dflt; /* nonzero: group-default results (CGPU_CT_DFLT, plain IPv4 path) */
 };
 
 /* One packet's record, written by k_ct_prep{,6} and read by the walker and
@@ -5247,7 +5259,7 @@ __global__ __launch_bounds__(256) void k_ct_prep_q(cgpu_snapshot s, ct_args a)
 				}
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
-			if (CGPU_CT_DFLT && a.dmap)
+			if (CGPU_CT_DFLT && a.dflt)
 				a.ct_ret[i] = CT_DFLT; /* the walker stores only non-default results */
 			a.identity[i] = id;
 			uint4 *r = a.rec + 2u * i;
@@ -6679,9 +6691,8 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 	for (uint32_t h = blockIdx.x * 256u + threadIdx.x; h < nh; h += stride) {
 		const uint64_t p0 = a.gpos[h];
 		const uint64_t p1 = p0 + a.glen[h];
-		/* CGPU_CT_DFLT: the group's default orientation (-1: not yet) */
+		/* CGPU_CT_DFLT: the group's orientation (-1: not yet decided) */
 		int gb = -1;
-		uint32_t gkk = 0u;
 		/* packets in batch order through the sort permutation, software-
 		 * pipelined: the record of p + 1 and the index of p + 2 are in
 		 * flight while packet p runs */
@@ -6752,15 +6763,12 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 					continue;
 #endif
 				if constexpr (DFLT) {
-					if (a.dmap) {
-						const uint4 kk = r.key();
-						const uint32_t o = ct4_orient(kk);
-						if (gb < 0 && ret <= CT_REPLY) {
+					if (a.dflt) {
+						const uint32_t o = ct4_orient(r.key());
+						if (gb < 0 && ret <= CT_REPLY)
 							gb = (int)(ret == CT_REPLY ? o ^ 1u : o);
-							gkk = ct_conn_group(ct_group(kk.y, kk.x), kk.z, kk.w & 0xFFu) & a.gmask;
-						}
-						if (gb >= 0 && ret == (o == (uint32_t)gb ? CT_ESTABLISHED : CT_REPLY))
-							continue; /* the group default: nothing stored */
+						if (gb == 0 && ret == (o ? CT_REPLY : CT_ESTABLISHED))
+							continue; /* the orientation default: nothing stored */
 					}
 				}
 				s_ri[nret][threadIdx.x] = i;
@@ -6770,8 +6778,6 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 			}
 		}
 		ctc_flush(T, c);
-		if (DFLT && gb == 1 && a.dmap)
-			atomicOr(&a.dmap[gkk >> 5], 1u << (gkk & 31u));
 	}
 	ret_flush();
 #ifdef CGPU_DIAG_WALK_CLOCK
@@ -6846,12 +6852,8 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 			q[u] = rr.pkt();
 			c[u] = ntl(a.ct_ret + j) & ~(CT_ADDRP | CT_RELP);
 			if constexpr (CGPU_CT_DFLT && std::is_same<K, CtK4>::value) {
-				if (c[u] == CT_DFLT) { /* the group default (the walker stored nothing) */
-					const uint4 kk = rr.key();
-					const uint32_t g = ct_conn_group(ct_group(kk.y, kk.x), kk.z, kk.w & 0xFFu) & a.gmask;
-					const uint32_t b = (a.dmap[g >> 5] >> (g & 31u)) & 1u;
-					c[u] = ct4_orient(kk) == b ? CT_ESTABLISHED : CT_REPLY;
-				}
+				if (c[u] == CT_DFLT && a.dflt) /* the orientation default (the walker stored nothing) */
+					c[u] = ct4_orient(rr.key()) ? CT_REPLY : CT_ESTABLISHED;
 			}
 			ep[u] = ntl(a.ep + j);
 			eg[u] = q[u].meta & CTM_EGRESS;
@@ -7203,7 +7205,7 @@ static ct_args ct_args_of(const ct_launch &L)
 	a.f2 = L.flags2;
 	a.pcls = L.pcls;
 	a.pk = L.pk;
-	a.dmap = L.dmap;
+	a.dflt = L.dflt;
 	return a;
 }
 
@@ -7439,14 +7441,9 @@ template <class K>
 static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
 {
 	ct_args a = ct_args_of(L);
-	/* the group-default results (CT_DFLT): the plain IPv4 path, group keys
-	 * of at most 24 bits (a 2-MiB bitmap); otherwise every result stored */
-	{
-		const int bits = ct_sort_bits(s);
-		a.gmask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
-		if (!CGPU_CT_DFLT || K::V6 || bits > 24)
-			a.dmap = nullptr;
-	}
+	/* the group-default results (CT_DFLT): the plain IPv4 path */
+	if (!CGPU_CT_DFLT || K::V6)
+		a.dflt = 0u;
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	if (K::V6) {
 		/* the ipcache lookups through the trie pre-pass (its entries into
@@ -7482,8 +7479,6 @@ static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_
 	uint32_t nh;
 	hipError_t e = ct_group_sort(s, L, a, L.n, &nh, st, K::V6 != 0);
 	if (e != hipSuccess)
-		return e;
-	if (a.dmap && (e = hipMemsetAsync(a.dmap, 0, ((size_t)a.gmask + 32u) / 32u * 4u, st)) != hipSuccess)
 		return e;
 	hipLaunchKernelGGL((k_ct_walk<K, WALK_PKT>), dim3(CT_WALK_GRID), dim3(256), 0, st, s, T, a);
 	if ((e = ct_phase2<K>(s, T, L, a, st)) != hipSuccess)
