@@ -6047,7 +6047,7 @@ static int ct_classify(cgpu_ctx *c, const cgpu_snapshot &s, uint64_t *delta, CtM
 	a.temp_bytes = L.temp_bytes;
 	a.flags2 = b + L.flags2;
 	a.pk = c->d_ct_pk;
-	a.dflt = !svc && !m.v6; /* group-default results (kernels.hip CT_DFLT) */
+	a.dflt = 1u; /* group-default results (kernels.hip CT_DFLT; the launchers clear it where a prep stores every result) */
 	hipError_t le;
 	if (svc) {
 		a.svc_out = reinterpret_cast<uint4 *>(b + L.svc_out);

@@ -4242,7 +4242,7 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #define CTM_RELX 1024u    /* grouped by connection in phase 1: the ICMP entry a create
 			   * writes is reserved and owed to phase 2 */
 #define CT_RELP 0x20u     /* walker -> phase 2: the ICMP entry of this create is owed */
-/* Group-default results (CGPU_CT_DFLT, the plain IPv4 path): the prep marks
+/* Group-default results (CGPU_CT_DFLT, every conntrack path): the prep marks
  * every packet's result CT_DFLT.  A packet's orientation is a fixed function
  * of its tuple that flips for the reversed tuple and is 0 for the usual
  * initiator (ephemeral source port above the service port; an ICMP echo
@@ -4261,12 +4261,13 @@ hipError_t launch_slot_init(uint64_t *totals, uint64_t *delta, const uint32_t *s
 #endif
 /* a packet's orientation (any fixed function of its key) and its group key,
  * as k_ct_prep_q computed it (ct_conn_group over the record's tuple) */
-__device__ __forceinline__ uint32_t ct4_orient(const uint4 &k)
+/* z = sport | dport << 16 (TCP / UDP ports in network order, the ICMP /
+ * ICMPv6 type word as ct_lookup4 / ct_lookup6 build it), `tie` = saddr <
+ * daddr for the reversed-invariant tie */
+__device__ __forceinline__ uint32_t ct_orient(uint32_t z, uint32_t proto, bool tie)
 {
-	/* k = {daddr, saddr, sport | dport << 16, proto | ...}: TCP / UDP ports
-	 * in network order, the ICMP id / type word as ct_lookup4 builds it */
-	uint32_t sp = k.z & 0xFFFFu, dp = k.z >> 16;
-	if ((k.w & 0xFFu) != 1u) {
+	uint32_t sp = z & 0xFFFFu, dp = z >> 16;
+	if (proto != 1u && proto != 58u) {
 		sp = __builtin_bswap16((uint16_t)sp);
 		dp = __builtin_bswap16((uint16_t)dp);
 		if (sp != dp)
@@ -4274,7 +4275,7 @@ __device__ __forceinline__ uint32_t ct4_orient(const uint4 &k)
 	} else if (sp != dp) {
 		return sp > dp ? 1u : 0u; /* an echo request carries its type as dport */
 	}
-	return k.y < k.x ? 1u : 0u;
+	return tie ? 1u : 0u;
 }
 #define CTB_LB_LOOPBACK 8u /* struct ct_entry lb_loopback (common.h:389) */
 #define TUPLE_F_SERVICE 4u /* conntrack.h:66 */
@@ -4797,7 +4798,7 @@ struct ct_args {
 	uint8_t *f2;                 /* [2n] phase-2 candidate flags (plain path) */
 	uint8_t *pcls;               /* [n] service path: phase-2 class, PCL_* (k_ct_prep) */
 	uint64_t *pk;                /* packed per-slot counters (k_ct_finish, k_unpack) */
-	uint32_t dflt; /* nonzero: group-default results (CGPU_CT_DFLT, plain IPv4 path) */
+	uint32_t dflt; /* nonzero: group-default results (CGPU_CT_DFLT) */
 };
 
 /* One packet's record, written by k_ct_prep{,6} and read by the walker and
@@ -4905,6 +4906,28 @@ template <> struct ct_rec<CtK6S> {
 	{
 		return ct_pkt{r2.y >> 16, r2.z & 0xFFFFu, r2.w, r3.x, r3.z, r2.z >> 16, r3.y, r2.x & 0xFFFFu,
 			      r2.y & 0xFFu, 0u, 0u, r1, r0, r3.w & 0xFFFFu, r3.w >> 16, 0u, 0u};
+	}
+};
+
+/* CGPU_CT_DFLT: a walked packet's orientation from its record (ct_orient) */
+__device__ __forceinline__ bool ct6_lt(const uint4 &a, const uint4 &b)
+{
+	if (a.x != b.x)
+		return a.x < b.x;
+	if (a.y != b.y)
+		return a.y < b.y;
+	if (a.z != b.z)
+		return a.z < b.z;
+	return a.w < b.w;
+}
+template <class K> struct ct_dflt {
+	static constexpr bool ON = CGPU_CT_DFLT != 0;
+	__device__ static uint32_t orient(const ct_rec<K> &r)
+	{
+		if constexpr (K::V6 != 0) /* {daddr, saddr, {z, proto | ...}} */
+			return ct_orient(r.r2.x, r.r2.y & 0xFFu, ct6_lt(r.r1, r.r0));
+		else /* {daddr, saddr, z, proto | ...} */
+			return ct_orient(r.r0.z, r.r0.w & 0xFFu, r.r0.y < r.r0.x);
 	}
 };
 
@@ -5107,6 +5130,8 @@ __device__ __forceinline__ void prep4_post(const cgpu_snapshot &s, const ct_args
 		}
 	}
 	a.identity[i] = id;
+	if (!SERIAL && CGPU_CT_DFLT && a.dflt)
+		a.ct_ret[i] = CT_DFLT; /* as k_ct_prep_q */
 	uint4 *r = a.rec + RW * i;
 	r[0] = uint4{da, sa, z, pr | (tfl << 8) | (meta << 16)};
 	r[1] = uint4{w | (port << 16), len, sec, cst};
@@ -5409,6 +5434,8 @@ __global__ __launch_bounds__(256) void k_ct_prep6_q(cgpu_snapshot s, ct_args a, 
 				}
 			}
 			reinterpret_cast<uint16_t *>(a.f2)[i] = p2 ? 1u : 0u;
+			if (CGPU_CT_DFLT && a.dflt)
+				a.ct_ret[i] = CT_DFLT; /* as k_ct_prep_q */
 			a.identity[i] = id;
 			uint4 *r = a.rec + 4u * i;
 			r[0] = da;
@@ -6639,7 +6666,7 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 #endif
 	using R = std::conditional_t<MODE == WALK_SVC, std::conditional_t<K::V6 != 0, ct_srec6, ct_srec>,
 				     ct_rec<K>>;
-	constexpr bool DFLT = CGPU_CT_DFLT && MODE == WALK_PKT && std::is_same<K, CtK4>::value;
+	constexpr bool DFLT = MODE == WALK_PKT && ct_dflt<K>::ON;
 	__shared__ int s_acct[3];
 	/* each lane's last CT_RETB results (packet index, ct result), stored
 	 * together: a scattered 1-byte store is a memory-side write whose
@@ -6764,7 +6791,7 @@ __global__ __launch_bounds__(256, K::ADDR ? CGPU_WALK_MINB_SVC : CGPU_WALK_W) vo
 #endif
 				if constexpr (DFLT) {
 					if (a.dflt) {
-						const uint32_t o = ct4_orient(r.key());
+						const uint32_t o = ct_dflt<K>::orient(r);
 						if (gb < 0 && ret <= CT_REPLY)
 							gb = (int)(ret == CT_REPLY ? o ^ 1u : o);
 						if (gb == 0 && ret == (o ? CT_REPLY : CT_ESTABLISHED))
@@ -6851,9 +6878,9 @@ __global__ __launch_bounds__(NT) void k_ct_finish(cgpu_snapshot s, ct_args a, ui
 			const ct_rec<K> rr = ct_rec<K>::load(a.rec, (uint32_t)j, true);
 			q[u] = rr.pkt();
 			c[u] = ntl(a.ct_ret + j) & ~(CT_ADDRP | CT_RELP);
-			if constexpr (CGPU_CT_DFLT && std::is_same<K, CtK4>::value) {
+			if constexpr (ct_dflt<K>::ON) {
 				if (c[u] == CT_DFLT && a.dflt) /* the orientation default (the walker stored nothing) */
-					c[u] = ct4_orient(rr.key()) ? CT_REPLY : CT_ESTABLISHED;
+					c[u] = ct_dflt<K>::orient(rr) ? CT_REPLY : CT_ESTABLISHED;
 			}
 			ep[u] = ntl(a.ep + j);
 			eg[u] = q[u].meta & CTM_EGRESS;
@@ -7441,15 +7468,15 @@ template <class K>
 static hipError_t launch_ct(const cgpu_snapshot &s, const ct_table &T, const ct_launch &L, hipStream_t st)
 {
 	ct_args a = ct_args_of(L);
-	/* the group-default results (CT_DFLT): the plain IPv4 path */
-	if (!CGPU_CT_DFLT || K::V6)
+	/* the IPv6 preps: the trie pre-pass (its entries into idx_sorted, free
+	 * until the group sort) when it can fold the egress fallback identity */
+	const bool pre6 = s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK;
+	/* the orientation-default results (CT_DFLT) with the Q preps */
+	if (!CGPU_CT_DFLT || (K::V6 && !pre6))
 		a.dflt = 0u;
 	const unsigned g = (unsigned)std::min<uint64_t>((L.n + 255) / 256, 8192);
 	if (K::V6) {
-		/* the ipcache lookups through the trie pre-pass (its entries into
-		 * idx_sorted, free until the group sort) when it can fold the
-		 * egress fallback identity */
-		if (s.cluster_id && s.cluster_id <= DIR_PAYLOAD_MASK) {
+		if (pre6) {
 			constexpr int NT = 1024, QP = CGPU_DIAG_IPC6_PRE_Q, Q = 4;
 			const size_t lds = (size_t)(v6t_lds_words(s.ipc6) + v6t_lds_bloom(s.ipc6)) * 4u;
 			const unsigned res = resident_blocks((const void *)k_ipc6_pre<QP, NT>, NT, lds);
@@ -7552,6 +7579,7 @@ hipError_t launch_classify_v6_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 		const unsigned gq = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((L.n + 256 * Q - 1) / (256 * Q), 8192));
 		hipLaunchKernelGGL((k_ct_prep6_q<Q, true>), dim3(gq), dim3(256), 0, st, s, a, L.idx_sorted);
 	} else {
+		a.dflt = 0u; /* k_ct_prep6 stores every result */
 		hipLaunchKernelGGL(k_ct_prep6<true>, dim3(g), dim3(256), 0, st, s, a);
 		launch_ct_decq<CtK6S>(s, a, st);
 	}
@@ -7609,8 +7637,10 @@ hipError_t launch_classify_v4_ctlb(const cgpu_snapshot &s, const ct_table &T, co
 	if (e != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess)
 		return e;
 	const bool serial = ctl[0] != 0;
-	if (serial)
+	if (serial) {
+		a.dflt = 0u; /* one group: every result stored */
 		hipLaunchKernelGGL((k_ct_prep<true, true>), dim3(g), dim3(256), 0, st, s, a);
+	}
 	launch_ct_decq<CtK4S>(s, a, st);
 	e = ct_group_sort(s, L, a, L.n, &nh, st);
 	if (e != hipSuccess)

@@ -161,7 +161,7 @@ struct ct_launch {
 	uint64_t *pk;         /* [n_ctr_slots] packed counters, zero between calls */
 	void *xdaddr;         /* [n] optional (IPv6: 16 bytes each) */
 	uint16_t *xdport;     /* [n] optional */
-	uint32_t dflt;        /* nonzero: group-default results (CGPU_CT_DFLT, plain IPv4 path) */
+	uint32_t dflt;        /* nonzero: group-default results (CGPU_CT_DFLT) */
 };
 
 size_t ct_temp_bytes(uint64_t n);
