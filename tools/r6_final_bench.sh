@@ -1,6 +1,6 @@
 # round-6 final bench lines (run on the GPU box from the repo root):
 #   bash tools/r6_final_bench.sh <group>   -> gpurun_out/r6_final/bench_<name>.json
-# groups: stateless, ct, ctlb, host.  Each line under its own time limit; a
+# groups: stateless, default, ct, ctlb, host, persist.  Each line under its own time limit; a
 # failure ends the script.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -27,6 +27,8 @@ case $1 in
     one ctlb6 600 --config ctlb6 --steps 20 --warmup 3;;
   host)
     for C in gpu frames cascade v6 pf6; do one ${C}hosttuples 400 --config $C --host-tuples --steps 5 --warmup 2 --no-cpu-baseline; done;;
+  default)
+    one default 400;;
   persist)
     one ct_persist4 600 --config ct --steps 20 --warmup 3 --ct-persist 4
     one ct6_persist4 600 --config ct6 --steps 20 --warmup 3 --ct-persist 4;;
