@@ -101,14 +101,14 @@ def test_ct_golden_small_map(torch_cuda, golden):
 
 
 def _pair(torch, T, t, locals_be, seclabels, batches, nows, ct_max=1 << 18, pre=None,
-          deletes=None):
+          deletes=None, schedule=0):
     """Engine and restatement side by side over consecutive batches."""
     from oracle import Oracle
     o = Oracle(**T.oracle_config())
     synth.load_oracle(o, T)
     synth.load_lxc(o, seclabels)
     o.ct_set_max(ct_max)
-    e = _engine(**T.engine_config(), ct_max=ct_max)
+    e = _engine(**T.engine_config(), ct_max=ct_max, schedule=schedule)
     synth.load_engine(e, T)
     synth.load_lxc(e, seclabels)
     e.commit()
@@ -256,6 +256,50 @@ def test_ct_many_connections_per_pair(torch_cuda, cfg_ct):
     _assert_same_map(e, o)
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     e.close()
+
+
+def test_ct_orientation_defaults_edges(torch_cuda, cfg_ct):
+    """The walker leaves a result unstored when it equals its orientation's
+    default (kernels.hip CT_DFLT / ct_orient) and the finish rebuilds it
+    from the tuple alone.  Exact for any mix of connections in a group, so
+    here the group keys are cut to 8 bits (CGPU_SCHED_CT_SORT_BITS: 256
+    groups, every one mixing connections of both orientations) over tuples
+    that stress the orientation: initiators with the LOWER source port
+    (groups of orientation 1), equal ports (ties broken by address), equal
+    ports AND addresses (a tuple equal to its reverse), ICMP echo both ways
+    and ICMP timestamps (a zero type word), and connections whose first
+    packet in a batch is a reply (their entries from the batch before).
+    Three batches, the 24-bit default beside it; verdicts, ct results, map
+    and metrics bit-exact against the restatement."""
+    T, _, _, _ = cfg_ct
+    t, locals_be, seclabels = synth.make_ct_workload(T, 6_000, seed=123, mean_pkts=12.0, span=0.7)
+    tcpudp = np.isin(t["proto"], [6, 17])
+    sw = lambda x: x.astype(np.uint16).byteswap()  # noqa: E731
+    lo, hi = np.minimum(sw(t["sport"]), sw(t["dport"])), np.maximum(sw(t["sport"]), sw(t["dport"]))
+    # direction-free connection and address-pair hashes (both directions of
+    # a connection take the same changes)
+    pk = (np.minimum(t["saddr"], t["daddr"]).astype(np.uint64) * np.uint64(2654435761)
+          ^ np.maximum(t["saddr"], t["daddr"]).astype(np.uint64)) % np.uint64(97)
+    ck = (pk * np.uint64(40503) + lo.astype(np.uint64) * np.uint64(65537) + hi.astype(np.uint64)) % np.uint64(3)
+    # a third of the TCP / UDP connections: the local port below the remote
+    # one in host order, so those the endpoint initiates start in
+    # orientation 1 (their groups store every result)
+    eg = (t["flags"] & 1) == 1  # egress: sport is the local port
+    flip = tcpudp & (ck == 0)
+    t["sport"] = np.where(flip, sw(np.where(eg, lo, hi)), t["sport"]).astype(np.uint16)
+    t["dport"] = np.where(flip, sw(np.where(eg, hi, lo)), t["dport"]).astype(np.uint16)
+    # equal ports on some connections, equal addresses on a few of those
+    tie = tcpudp & (pk < 9)
+    t["sport"] = np.where(tie, t["dport"], t["sport"]).astype(np.uint16)
+    same = tie & (pk < 2)
+    t["daddr"] = np.where(same, t["saddr"], t["daddr"]).astype(np.uint32)
+    ic = t["proto"] == 1
+    assert flip.sum() > 1000 and tie.sum() > 100 and same.sum() > 10 and ic.sum() > 100
+    for sched in (8 << 8, 0):  # CGPU_SCHED_CT_SORT_BITS(8), then the default 24 bits
+        e, o = _pair(torch_cuda, T, t, locals_be, seclabels, 3, [4000, 4003, 4009], schedule=sched)
+        _assert_same_map(e, o)
+        np.testing.assert_array_equal(e.metrics(), o.metrics())
+        e.close()
 
 
 def test_ct_jumbo_counters_one_slot(torch_cuda, cfg_ct):

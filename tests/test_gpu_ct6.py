@@ -104,10 +104,13 @@ def cfg_ct6():
     return T, t, loc, seclabels
 
 
-def test_ct6_stream_vs_restatement(torch_cuda, cfg_ct6):
+@pytest.mark.parametrize("sched", [0, 8 << 8])
+def test_ct6_stream_vs_restatement(torch_cuda, cfg_ct6, sched):
     """~400k IPv6 packets of 40k connections in 3 batches, 1500 policy keys
     deleted before the middle batch, then ctmap GC and one more batch:
-    everything bit-exact, map, counters and metrics included."""
+    everything bit-exact, map, counters and metrics included.  Also with the
+    group keys cut to 8 bits (CGPU_SCHED_CT_SORT_BITS(8)): every walker group
+    mixes connections of both orientations (kernels.hip CT_DFLT)."""
     from oracle import Oracle
     torch = torch_cuda
     T, t, loc, seclabels = cfg_ct6
@@ -118,7 +121,7 @@ def test_ct6_stream_vs_restatement(torch_cuda, cfg_ct6):
         assert o.policy_update(int(ep), k, en) == 0
     synth.load_lxc(o, seclabels)
     o.ct6_set_max(1 << 18)
-    e = _engine(**T.engine_config(), ct_max=1 << 18)
+    e = _engine(**T.engine_config(), ct_max=1 << 18, schedule=sched)
     synth.load_engine(e, T)
     synth.load_lxc(e, seclabels)
     e.commit()

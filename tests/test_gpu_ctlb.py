@@ -122,7 +122,7 @@ def test_ctlb_golden_small_map(torch_cuda, golden):
     e.close()
 
 
-def _pair(torch, T, svcs, t, seclabels, batches, nows, ct_max=1 << 20, churn=None):
+def _pair(torch, T, svcs, t, seclabels, batches, nows, ct_max=1 << 20, churn=None, schedule=0):
     """Engine and restatement side by side over consecutive batches;
     churn(bi) -> [(op, key, val)] service map changes before batch bi."""
     from oracle import Oracle
@@ -131,7 +131,7 @@ def _pair(torch, T, svcs, t, seclabels, batches, nows, ct_max=1 << 20, churn=Non
     synth.load_services(o, svcs)
     synth.load_lxc(o, seclabels)
     o.ct_set_max(ct_max)
-    e = _engine(**T.engine_config(), ct_max=ct_max)
+    e = _engine(**T.engine_config(), ct_max=ct_max, schedule=schedule)
     synth.load_engine(e, T)
     synth.load_services(e, svcs)
     synth.load_lxc(e, seclabels)
@@ -170,11 +170,14 @@ def cfg_ctlb():
     return T, svcs, t, seclabels
 
 
-def test_ctlb_stream_vs_restatement(torch_cuda, cfg_ctlb):
+@pytest.mark.parametrize("sched", [0, 8 << 8])
+def test_ctlb_stream_vs_restatement(torch_cuda, cfg_ctlb, sched):
     """~600k packets of 60k connections (40 % to 4000 services, loopback
     backends) in 3 batches, 10 % of the backends deleted before batch 1 and
     half of them back with new targets before batch 2: everything
-    bit-exact, counters and metrics included."""
+    bit-exact, counters and metrics included.  Also with the group keys cut
+    to 8 bits (CGPU_SCHED_CT_SORT_BITS(8)): every walker group mixes
+    connections of both orientations (kernels.hip CT_DFLT)."""
     T, svcs, t, seclabels = cfg_ctlb
     rng = np.random.Generator(np.random.PCG64(12))
     ns = len(svcs.vip)
@@ -189,7 +192,7 @@ def test_ctlb_stream_vs_restatement(torch_cuda, cfg_ctlb):
         if bi == 2:
             return [("put", svcs.keys[d], v) for d, v in zip(back, nv)]
         return []
-    e, o = _pair(torch_cuda, T, svcs, t, seclabels, 3, [1000, 1004, 1100], churn=churn)
+    e, o = _pair(torch_cuda, T, svcs, t, seclabels, 3, [1000, 1004, 1100], churn=churn, schedule=sched)
     _assert_same_map(e, o)
     np.testing.assert_array_equal(e.metrics(), o.metrics())
     for k, ep in zip(T.pol_keys[:6000], T.pol_ep[:6000]):
